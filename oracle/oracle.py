@@ -1,0 +1,149 @@
+"""sfmx ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes wrapper over liboracle.so (oracle/match_oracle.cpp, oracle/ba_oracle.cpp):
+the CPU restatement of the reference's matching / bundle-adjustment semantics.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, and only as the checker / CPU baseline — never as the
+thing measured or shipped.  Parity status: unpinned against the reference
+itself (it cannot be built here and ships no fixtures).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = C.CDLL(LIB_PATH)
+    vp, i32p, i64p = C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int64)
+    f32p = C.POINTER(C.c_float)
+    lib.orc_knn2_l2.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, i32p, f32p]
+    lib.orc_knn2_hamming.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, i32p, f32p]
+    lib.orc_match_pair.restype = C.c_int64
+    lib.orc_match_pair.argtypes = [C.c_int, vp, C.c_int, vp, C.c_int, C.c_int, C.c_double, vp]
+    lib.orc_match_pairs.argtypes = [C.c_int, C.POINTER(vp), i32p, C.c_int, i32p, C.c_int, C.c_double, vp, i64p,
+                                    i64p, C.c_int]
+    for n in ("orc_pairs_unordered",):
+        getattr(lib, n).restype = C.c_int64
+        getattr(lib, n).argtypes = [C.c_int, i32p]
+    lib.orc_pairs_video.restype = C.c_int64
+    lib.orc_pairs_video.argtypes = [C.c_int, C.c_int, i32p]
+    lib.orc_pairs_grid.restype = C.c_int64
+    lib.orc_pairs_grid.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, i32p]
+    lib.orc_filter_matches.argtypes = [vp, i64p, i64p, C.c_int, C.c_int, C.c_int, i32p]
+    lib.orc_first_sqrt_collision.restype = C.c_int64
+    lib.orc_first_sqrt_collision.argtypes = [C.c_int64]
+    return lib
+
+
+lib = _load()
+
+
+def _ptr(a, t=C.c_int32):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def knn2(q: np.ndarray, t: np.ndarray):
+    """cv::BFMatcher knnMatch(q, t, k=2) restated: -> (idx[nq,2], dist[nq,2], n_neighbours)."""
+    l2 = q.dtype == np.float32
+    q = np.ascontiguousarray(q)
+    t = np.ascontiguousarray(t)
+    nq, nt = q.shape[0], t.shape[0]
+    dim = q.shape[1] if q.ndim == 2 else t.shape[1]
+    idx = np.empty((nq, 2), np.int32)
+    dist = np.empty((nq, 2), np.float32)
+    fn = lib.orc_knn2_l2 if l2 else lib.orc_knn2_hamming
+    nn = fn(q.ctypes.data, nq, t.ctypes.data, nt, dim, _ptr(idx), _ptr(dist, C.c_float))
+    return idx, dist, nn
+
+
+def match_pair(q: np.ndarray, t: np.ndarray, ratio: float = 0.7) -> np.ndarray:
+    l2 = q.dtype == np.float32
+    q = np.ascontiguousarray(q)
+    t = np.ascontiguousarray(t)
+    dim = q.shape[1] if q.ndim == 2 and q.shape[0] else t.shape[1]
+    out = np.zeros(max(q.shape[0], 1), DMATCH_DTYPE)
+    n = lib.orc_match_pair(0 if l2 else 1, q.ctypes.data, q.shape[0], t.ctypes.data, t.shape[0], dim, ratio,
+                           out.ctypes.data)
+    return out[:n].copy()
+
+
+def match_pairs(imgs, pairs: np.ndarray, ratio: float = 0.7, nthreads: int = 0):
+    """Pair-parallel exact BF (OpenMP over pairs, as the reference) ->
+    (matches, pair_offsets[n+1]) packed like sfmx_matcher_fetch."""
+    l2 = imgs[0].dtype == np.float32
+    imgs = [np.ascontiguousarray(m) for m in imgs]
+    dim = imgs[0].shape[1]
+    pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+    rows = np.array([m.shape[0] for m in imgs], np.int32)
+    ptrs = (C.c_void_p * len(imgs))(*[m.ctypes.data for m in imgs])
+    base = np.zeros(len(pairs), np.int64)
+    if len(pairs):
+        base[1:] = np.cumsum(rows[pairs[:-1, 0]])
+    cap = int(rows[pairs[:, 0]].sum()) if len(pairs) else 0
+    tmp = np.zeros(max(cap, 1), DMATCH_DTYPE)
+    counts = np.zeros(max(len(pairs), 1), np.int64)
+    lib.orc_match_pairs(0 if l2 else 1, ptrs, _ptr(rows), dim, _ptr(pairs), len(pairs), ratio, tmp.ctypes.data,
+                        _ptr(base, C.c_int64), _ptr(counts, C.c_int64), nthreads)
+    off = np.zeros(len(pairs) + 1, np.int64)
+    off[1:] = np.cumsum(counts[: len(pairs)])
+    out = np.concatenate([tmp[base[p]: base[p] + counts[p]] for p in range(len(pairs))]) if len(pairs) else tmp[:0]
+    return out, off
+
+
+def filter_matches(matches: np.ndarray, offsets: np.ndarray, distinct: bool, min_count: int):
+    """SfM.cpp:547-570 restated -> (matches, offsets, keep) with the same packing."""
+    n = len(offsets) - 1
+    m = matches.copy()
+    base = offsets[:-1].astype(np.int64).copy()
+    counts = np.diff(offsets).astype(np.int64)
+    keep = np.zeros(max(n, 1), np.int32)
+    lib.orc_filter_matches(m.ctypes.data, _ptr(base, C.c_int64), _ptr(counts, C.c_int64), n, int(distinct),
+                           int(min_count), _ptr(keep))
+    out = np.concatenate([m[base[p]: base[p] + counts[p]] for p in range(n)]) if n else m[:0]
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum(counts[:n])
+    return out, off, keep[:n]
+
+
+def pairs_unordered(n):
+    k = lib.orc_pairs_unordered(n, None)
+    out = np.empty((k, 2), np.int32)
+    lib.orc_pairs_unordered(n, _ptr(out))
+    return out
+
+
+def pairs_video(n, seq):
+    k = lib.orc_pairs_video(n, seq, None)
+    if k < 0:
+        raise ValueError("sequence length < 2")
+    out = np.empty((k, 2), np.int32)
+    lib.orc_pairs_video(n, seq, _ptr(out))
+    return out
+
+
+def pairs_grid(n, seq, row_len, mode=1):
+    k = lib.orc_pairs_grid(n, seq, row_len, mode, None)
+    if k < 0:
+        raise ValueError("bad grid parameters")
+    out = np.empty((k, 2), np.int32)
+    lib.orc_pairs_grid(n, seq, row_len, mode, _ptr(out))
+    return out
+
+
+def first_sqrt_collision(limit: int = 1 << 24) -> int:
+    return int(lib.orc_first_sqrt_collision(limit))

@@ -1,0 +1,47 @@
+// SPDX-License-Identifier: MIT
+// sfmx matcher — device data layout shared by the host driver and the kernels.
+//
+// HBM layout (one matcher context, one device):
+//   SIFT (NORM_L2):  desc8[row][128]  int8   a' = a - 128   (exact: SIFT values are integers 0..255)
+//                    norm [row]       int32  ||a'||^2        (<= 2^21)
+//                    keyc [row]       int32  -(||a'||^2 << 8) + 255 - (row & 255)   (see match_kernels.hip)
+//                    f32  [row][128]  float  only when an image is not integer-valued (fp32 fallback)
+//   ORB (NORM_HAMMING): desc8[row][32] uint8 (rows padded with zeros)
+// Images are concatenated; each starts at a row offset that is a multiple of
+// ROW_ALIGN and is padded to a multiple of ROW_ALIGN rows with zero rows
+// (int8 0 == descriptor value 128: contributes 0 to every dot product).
+#pragma once
+#include <cstdint>
+
+namespace sfmx {
+
+constexpr int ROW_ALIGN = 512;       // = query rows per work item = 2 x key chunk (256)
+constexpr int SIFT_DIM = 128;
+constexpr int ORB_BYTES = 32;
+// Queries whose best-2 squared distance reaches this value take the exact
+// float-sqrt slow path: below it sqrtf is injective on integers (first
+// collision is at s = 4,197,201), so ranking on the integer
+// s equals ranking on sqrtf(s) bits.
+constexpr int64_t SQRT_SAFE = 1 << 22;
+
+struct ImgDev {
+    int32_t rows;       // real descriptor rows (Nq or Nt)
+    int32_t rows_pad;   // multiple of ROW_ALIGN
+    int64_t row0;       // first row in the pool
+    int32_t integral;   // SIFT: 1 if all values are integers in [0,255]
+    int32_t _pad;
+};
+
+struct PairDev {
+    int32_t left, right;   // image indices: left = query, right = train
+    int64_t dense_base;    // offset of this pair's per-query results (sum of previous Nq)
+};
+
+struct WorkItem {          // one 512-query block of one pair
+    int32_t pair;
+    int32_t q0;
+};
+
+struct DMatchDev { int32_t queryIdx, trainIdx, imgIdx; float distance; };
+
+}  // namespace sfmx

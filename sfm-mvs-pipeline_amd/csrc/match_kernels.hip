@@ -1,0 +1,605 @@
+// SPDX-License-Identifier: MIT
+// sfmx matcher kernels for gfx950 (MI355X / CDNA4).
+//
+// Replaces, per image pair, cv::BFMatcher(NORM_L2|NORM_HAMMING)::knnMatch(L, R, m, 2)
+// + Lowe's ratio test as called at
+//   src/photogrammetrie/sfm/UnorderedFeatureMatchingStrategy.cpp:50-64
+//   (same code: VideoFeatureMatchingStrategy.cpp:61-75, GridFeatureMatchingStrategy.cpp:104-118)
+// and the match-graph filters of SfM::calculateShotMatches (sfm/SfM.cpp:547-570).
+//
+// Semantics reproduced bit for bit (see oracle/match_oracle.cpp):
+//   L2:      d = sqrtf(sum (a-b)^2), top-2 ranked on (float bits of d, train index)
+//   Hamming: d = popcount(a xor b),  top-2 ranked on (d, train index)
+//   ratio:   accept m0 iff (double)d0 < (double)d1 * ratio; a single neighbour is accepted.
+//
+// SIFT kernel design (sift_knn2_kernel):
+//   * descriptors are integer 0..255, stored as int8 a' = a - 128, so the
+//     distance contraction is an exact int8 MFMA: v_mfma_i32_32x32x32_i8,
+//     K = 128 = 4 MFMAs per 32x32 tile.
+//   * D = A * B with A = 32 train rows (from LDS), B = 32 queries (registers):
+//     each lane's accumulator column is ONE query, its 16 registers are 16
+//     train rows, so the 2-NN reduction is lane-local (no shuffles per tile).
+//   * ranking key per element, one VALU op (v_lshl_add_u32):
+//         key = (dot << 9) + keyc[j],  keyc[j] = -(nb_j << 8) + 255 - (j & 255)
+//             = 256 * (2 dot - nb_j) + (255 - (j & 255))
+//     Larger key <=> smaller s = na + nb - 2 dot, ties -> smaller j (within a
+//     256-row chunk); fits int32 because s < 2^23.  Top-2 by max: two VALU ops
+//     (v_med3_i32, v_max_i32).  Every 256 rows the chunk's top-2 is merged with
+//     the partner half-wave and folded into the running (t, j) top-2; later
+//     chunks only win on strictly smaller t (OpenCV's strict '<' insertion).
+//   * integer s ranks like sqrtf(s) bits while s < SQRT_SAFE; a query whose
+//     2nd-best s reaches it is handed to sift_slow_kernel (exact float sqrt
+//     ranking, 64-bit keys).  Real SIFT distances never get there.
+//   * train rows stream through a double-buffered LDS stage (64 rows, 8 KiB)
+//     filled by global_load_lds_dwordx4 with an XOR-swizzled source address
+//     (conflict-free ds_read_b128 fragment reads).
+//   * one work item = 512 queries of one pair (8 waves x 2 query tiles x 32);
+//     work items are sorted by train image and mapped XCD-contiguously so the
+//     blocks streaming one train image share an XCD's L2.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <climits>
+#include "match_common.hpp"
+
+namespace sfmx {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+#define GLOBAL_AS __attribute__((address_space(1)))
+#define LDS_AS __attribute__((address_space(3)))
+
+__device__ __forceinline__ int med3i(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
+__device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned c) { return max(min(a, b), min(max(a, b), c)); }
+
+// Correctly rounded sqrtf of an exact integer < 2^24: the double sqrt is
+// correctly rounded and 53 >= 2*24+2, so rounding it to float is the
+// correctly rounded float sqrt (no double-rounding error).  Exhaustively
+// checked against host sqrtf by tests/test_gpu_match.py.
+__device__ __forceinline__ float sqrt_rn_int(int64_t s) { return (float)__builtin_sqrt((double)s); }
+
+// Bijective XCD-contiguous remap: blocks b, b+8, ... share an XCD (observed
+// round-robin dispatch; speed only, never correctness).
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, x = b & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+// ---------------------------------------------------------------------------
+// prep: float SIFT rows -> int8 a' = a - 128, ||a'||^2, chunk keys, integrality.
+// 32 threads per row (float4 each); pad rows are written as zeros.
+__global__ void prep_l2_kernel(const float* __restrict__ src, int rows, int cols, int rows_pad,
+                               int8_t* __restrict__ dst, int32_t* __restrict__ norm,
+                               int32_t* __restrict__ keyc, int32_t* __restrict__ nonintegral) {
+    const int r = blockIdx.x * (blockDim.x >> 5) + (threadIdx.x >> 5);
+    const int c4 = threadIdx.x & 31;   // 4 columns each
+    if (r >= rows_pad) return;
+    int v[4] = {0, 0, 0, 0};
+    bool bad = false;
+    if (r < rows) {
+        for (int e = 0; e < 4; ++e) {
+            const int c = c4 * 4 + e;
+            if (c < cols) {
+                const float f = src[(int64_t)r * cols + c];
+                const bool ok = (f >= 0.f) && (f <= 255.f) && (f == __builtin_floorf(f));
+                bad |= !ok;
+                v[e] = ok ? (int)f - 128 : 0;
+            }
+        }
+    }
+    const unsigned packed = (unsigned)(v[0] & 255) | ((unsigned)(v[1] & 255) << 8) |
+                            ((unsigned)(v[2] & 255) << 16) | ((unsigned)(v[3] & 255) << 24);
+    reinterpret_cast<unsigned*>(dst + (int64_t)r * SIFT_DIM)[c4] = packed;
+    int n2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    for (int o = 16; o > 0; o >>= 1) n2 += __shfl_xor(n2, o, 32);
+    if (__any(bad) && c4 == 0) atomicOr(nonintegral, 1);
+    if (c4 == 0) {
+        norm[r] = n2;
+        keyc[r] = (r < rows) ? (-(n2 << 8) + 255 - (r & 255)) : INT_MIN;
+    }
+}
+
+// Copy of the raw float rows for the fp32 fallback (non-integer SIFT values).
+__global__ void prep_f32_kernel(const float* __restrict__ src, int rows, int cols, int rows_pad,
+                                float* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)rows_pad * SIFT_DIM;
+    if (i >= total) return;
+    const int r = (int)(i / SIFT_DIM), c = (int)(i % SIFT_DIM);
+    dst[i] = (r < rows && c < cols) ? src[(int64_t)r * cols + c] : 0.f;
+}
+
+// ORB rows (cols <= 32 bytes) -> zero-padded 32-byte rows.
+__global__ void prep_hamming_kernel(const uint8_t* __restrict__ src, int rows, int cols, int rows_pad,
+                                    uint8_t* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)rows_pad * ORB_BYTES;
+    if (i >= total) return;
+    const int r = (int)(i / ORB_BYTES), c = (int)(i % ORB_BYTES);
+    dst[i] = (r < rows && c < cols) ? src[(int64_t)r * cols + c] : 0;
+}
+
+// ---------------------------------------------------------------------------
+// SIFT 2-NN, int8 MFMA.
+template <int QT, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 2)
+void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
+                      const ImgDev* __restrict__ imgs, const int8_t* __restrict__ desc8,
+                      const int32_t* __restrict__ norm, const int32_t* __restrict__ keyc,
+                      int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
+                      int2* __restrict__ slow_list, int32_t* __restrict__ slow_count, double ratio) {
+    static_assert(WAVES * 64 * 16 == 64 * SIFT_DIM, "one 16-B glds per thread fills a 64-row stage");
+    constexpr int STAGE = 64;
+    constexpr int DESC_BYTES = STAGE * SIFT_DIM;           // 8 KiB
+    constexpr int BUF_BYTES = DESC_BYTES + STAGE * 4;      // + keys
+    __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
+
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const WorkItem w = work[xcd_remap(blockIdx.x, gridDim.x)];
+    const PairDev P = pairs[w.pair];
+    const ImgDev L = imgs[P.left], R = imgs[P.right];
+    const int nq = L.rows, nt = R.rows;
+    const int qbase = w.q0 + wid * (QT * 32);
+
+    // Query fragments (B operand): lane holds 16 bytes of k-block (2m + h).
+    i32x4 bq[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const i32x4* src = reinterpret_cast<const i32x4*>(desc8 + (L.row0 + qbase + qt * 32 + l32) * SIFT_DIM);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) bq[qt][m] = src[2 * m + h];
+    }
+
+    int T1[QT], J1[QT], T2[QT], J2[QT], c1[QT], c2[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        T1[qt] = T2[qt] = INT_MAX; J1[qt] = J2[qt] = -1; c1[qt] = c2[qt] = INT_MIN;
+    }
+
+    const int nstages = (nt + STAGE - 1) / STAGE;
+    const int8_t* tbase = desc8 + R.row0 * SIFT_DIM;
+    const int32_t* kbase = keyc + R.row0;
+
+    auto stage = [&](int s, int buf) {
+        char* base = lds + buf * BUF_BYTES;
+        const int p = threadIdx.x;                   // 16-byte unit index in the stage
+        const int rr = p >> 3, slot = p & 7, c = slot ^ ((rr >> 1) & 7);
+        const int8_t* g = tbase + (int64_t)(s * STAGE + rr) * SIFT_DIM + 16 * c;
+        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)g, (LDS_AS void*)(base + wid * 1024), 16, 0, 0);
+        if (wid == 0)
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(kbase + s * STAGE + lane),
+                                             (LDS_AS void*)(base + DESC_BYTES), 4, 0, 0);
+    };
+
+    if (nstages > 0) stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    for (int s = 0; s < nstages; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nstages) stage(s + 1, buf ^ 1);
+        const char* base = lds + buf * BUF_BYTES;
+#pragma unroll
+        for (int t = 0; t < STAGE / 32; ++t) {
+            const int row = t * 32 + l32;
+            i32x4 a[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int slot = (2 * m + h) ^ ((row >> 1) & 7);
+                a[m] = *reinterpret_cast<const i32x4*>(base + row * SIFT_DIM + 16 * slot);
+            }
+            i32x4 kv[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                kv[g] = *reinterpret_cast<const i32x4*>(base + DESC_BYTES + 4 * (t * 32 + 8 * g + 4 * h));
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                i32x16 acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bq[qt][m], acc, 0, 0, 0);
+                int b1 = c1[qt], b2 = c2[qt];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = (int)(((unsigned)acc[r] << 9) + (unsigned)kv[r >> 2][r & 3]);
+                    b2 = med3i(b1, b2, key);
+                    b1 = max(b1, key);
+                }
+                c1[qt] = b1; c2[qt] = b2;
+            }
+        }
+        if ((s & 3) == 3 || s + 1 == nstages) {      // end of a 256-row chunk
+            const int cb = (s >> 2) * 256;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const int p1 = __shfl_xor(c1[qt], 32), p2 = __shfl_xor(c2[qt], 32);
+                const int m1 = max(c1[qt], p1), m2 = max(min(c1[qt], p1), max(c2[qt], p2));
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int key = e == 0 ? m1 : m2;
+                    if (key != INT_MIN) {
+                        const int t_ = -(key >> 8), j_ = cb + 255 - (key & 255);
+                        if (t_ < T2[qt]) {
+                            if (t_ < T1[qt]) { T2[qt] = T1[qt]; J2[qt] = J1[qt]; T1[qt] = t_; J1[qt] = j_; }
+                            else { T2[qt] = t_; J2[qt] = j_; }
+                        }
+                    }
+                }
+                c1[qt] = c2[qt] = INT_MIN;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    // Epilogue: lanes of half 0 own query column l32 of each tile.
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int qi = qbase + qt * 32 + l32;
+        if (h != 0 || qi >= nq) continue;
+        const int64_t o = P.dense_base + qi;
+        if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }
+        const int64_t na = norm[L.row0 + qi];
+        const int64_t s1 = (int64_t)T1[qt] + na, s2 = (int64_t)T2[qt] + na;
+        if (nt >= 2 && s2 >= SQRT_SAFE) {
+            const int slot = atomicAdd(slow_count, 1);
+            slow_list[slot] = make_int2(w.pair, qi);
+            out_idx[o] = -2;
+            continue;
+        }
+        const float d1 = sqrt_rn_int(s1);
+        bool acc = true;
+        if (nt >= 2) acc = (double)d1 < (double)sqrt_rn_int(s2) * ratio;
+        out_idx[o] = acc ? J1[qt] : -1;
+        out_dist[o] = d1;
+    }
+}
+
+// Exact path for queries whose best-2 falls in the float-sqrt collision range:
+// one wave per query, s exact via v_dot4_i32_i8, ranked on (sqrtf bits, j).
+__device__ __forceinline__ void top2_u64(unsigned long long k, unsigned long long& b1, unsigned long long& b2) {
+    if (k < b2) { if (k < b1) { b2 = b1; b1 = k; } else b2 = k; }
+}
+
+__global__ __launch_bounds__(256)
+void sift_slow_kernel(const int2* __restrict__ slow_list, const int32_t* __restrict__ slow_count,
+                      const PairDev* __restrict__ pairs, const ImgDev* __restrict__ imgs,
+                      const int8_t* __restrict__ desc8, const int32_t* __restrict__ norm,
+                      int32_t* __restrict__ out_idx, float* __restrict__ out_dist, double ratio) {
+    const int lane = threadIdx.x & 63;
+    const int nwave = gridDim.x * (blockDim.x >> 6);
+    const int n = *slow_count;
+    for (int e = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); e < n; e += nwave) {
+        const int2 it = slow_list[e];
+        const PairDev P = pairs[it.x];
+        const ImgDev L = imgs[P.left], R = imgs[P.right];
+        const int* q = reinterpret_cast<const int*>(desc8 + (L.row0 + it.y) * SIFT_DIM);
+        int qw[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) qw[k] = q[k];
+        const int na = norm[L.row0 + it.y];
+        unsigned long long b1 = ~0ull, b2 = ~0ull;
+        for (int j = lane; j < R.rows; j += 64) {
+            const int* t = reinterpret_cast<const int*>(desc8 + (R.row0 + j) * SIFT_DIM);
+            int dot = 0;
+#pragma unroll
+            for (int k = 0; k < 32; ++k) dot = __builtin_amdgcn_sdot4(qw[k], t[k], dot, false);
+            const int64_t s = (int64_t)na + norm[R.row0 + j] - 2 * (int64_t)dot;
+            const float d = sqrt_rn_int(s);
+            top2_u64(((unsigned long long)__float_as_uint(d) << 32) | (unsigned)j, b1, b2);
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long p1 = __shfl_xor(b1, o), p2 = __shfl_xor(b2, o);
+            top2_u64(p1, b1, b2);
+            top2_u64(p2, b1, b2);
+        }
+        if (lane == 0) {
+            const float d1 = __uint_as_float((unsigned)(b1 >> 32)), d2 = __uint_as_float((unsigned)(b2 >> 32));
+            const bool acc = (double)d1 < (double)d2 * ratio;     // slow path implies nt >= 2
+            const int64_t o = P.dense_base + it.y;
+            out_idx[o] = acc ? (int)(b1 & 0xffffffffu) : -1;
+            out_dist[o] = d1;
+        }
+    }
+}
+
+// fp32 fallback (non-integer SIFT rows): one thread per query, the oracle's
+// 8-partial-sum order, train rows staged through LDS.  Not MFMA: this path
+// exists for correctness on out-of-contract input only.
+__global__ __launch_bounds__(512)
+void sift_f32_kernel(const WorkItem* __restrict__ work, const int32_t* __restrict__ pair_sel,
+                     const PairDev* __restrict__ pairs, const ImgDev* __restrict__ imgs,
+                     const float* __restrict__ f32, int32_t* __restrict__ out_idx,
+                     float* __restrict__ out_dist, double ratio) {
+    constexpr int STAGE = 32;
+    __shared__ float tl[STAGE * SIFT_DIM];
+    const WorkItem w = work[blockIdx.x];
+    (void)pair_sel;
+    const PairDev P = pairs[w.pair];
+    const ImgDev L = imgs[P.left], R = imgs[P.right];
+    const int qi = w.q0 + threadIdx.x;
+    const float* qrow = f32 + (L.row0 + (qi < L.rows_pad ? qi : 0)) * SIFT_DIM;
+    unsigned b1 = 0x7f7fffffu, b2 = 0x7f7fffffu;
+    int j1 = -1, j2 = -1;
+    for (int s0 = 0; s0 < R.rows; s0 += STAGE) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < STAGE * SIFT_DIM; i += blockDim.x)
+            tl[i] = f32[(R.row0 + s0) * SIFT_DIM + i];
+        __syncthreads();
+        const int lim = min(STAGE, R.rows - s0);
+        for (int jj = 0; jj < lim; ++jj) {
+            float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int k = 0; k < SIFT_DIM; k += 8)
+#pragma unroll
+                for (int l = 0; l < 8; ++l) {
+                    const float d = __fsub_rn(qrow[k + l], tl[jj * SIFT_DIM + k + l]);
+                    acc[l] = __fadd_rn(acc[l], __fmul_rn(d, d));   // no FMA contraction (oracle: -ffp-contract=off)
+                }
+            float ssum = acc[0];
+#pragma unroll
+            for (int l = 1; l < 8; ++l) ssum += acc[l];
+            const unsigned key = __float_as_uint(__builtin_sqrtf(ssum));
+            const int j = s0 + jj;
+            if (key < b2) { if (b1 > key) { b2 = b1; j2 = j1; b1 = key; j1 = j; } else { b2 = key; j2 = j; } }
+        }
+    }
+    (void)j2;
+    if (qi >= L.rows) return;
+    const int64_t o = P.dense_base + qi;
+    if (R.rows == 0) { out_idx[o] = -1; out_dist[o] = 0.f; return; }
+    const float d1 = __uint_as_float(b1), d2 = __uint_as_float(b2);
+    const bool acc = R.rows >= 2 ? ((double)d1 < (double)d2 * ratio) : true;
+    out_idx[o] = acc ? j1 : -1;
+    out_dist[o] = d1;
+}
+
+// ---------------------------------------------------------------------------
+// ORB Hamming 2-NN on the VALU (8 x v_xor + 8 x v_bcnt per pair, no MFMA).
+// 4 waves x 2 queries per lane = 512 queries per block; train rows stream
+// through LDS (256 rows = 8 KiB per stage, broadcast ds_read_b128).
+// key = (d << 23) | j (unsigned), top-2 by min: v_med3_u32 + v_min_u32.
+template <int QPL>
+__global__ __launch_bounds__(256, 2)
+void orb_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
+                     const ImgDev* __restrict__ imgs, const uint8_t* __restrict__ desc8,
+                     int32_t* __restrict__ out_idx, float* __restrict__ out_dist, double ratio) {
+    constexpr int STAGE = 256;
+    constexpr int BUF = STAGE * ORB_BYTES;   // 8 KiB
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * BUF];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const WorkItem w = work[xcd_remap(blockIdx.x, gridDim.x)];
+    const PairDev P = pairs[w.pair];
+    const ImgDev L = imgs[P.left], R = imgs[P.right];
+    const int nq = L.rows, nt = R.rows;
+
+    u32x4 q[QPL][2];
+#pragma unroll
+    for (int e = 0; e < QPL; ++e) {
+        const int qi = w.q0 + e * 256 + threadIdx.x;
+        const u32x4* src = reinterpret_cast<const u32x4*>(desc8 + (L.row0 + qi) * ORB_BYTES);
+        q[e][0] = src[0]; q[e][1] = src[1];
+    }
+    unsigned b1[QPL], b2[QPL];
+#pragma unroll
+    for (int e = 0; e < QPL; ++e) b1[e] = b2[e] = 0xffffffffu;
+
+    const uint8_t* tbase = desc8 + R.row0 * ORB_BYTES;
+    const int nstages = (nt + STAGE - 1) / STAGE;
+    auto stage = [&](int s, int buf) {
+        uint8_t* base = lds + buf * BUF;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {   // 2 x (256 threads x 16 B) = 8 KiB
+            const uint8_t* g = tbase + (int64_t)s * BUF + i * 4096 + threadIdx.x * 16;
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)g, (LDS_AS void*)(base + i * 4096 + wid * 1024), 16, 0, 0);
+        }
+    };
+    if (nstages > 0) stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < nstages; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nstages) stage(s + 1, buf ^ 1);
+        const u32x4* tl = reinterpret_cast<const u32x4*>(lds + buf * BUF);
+        const int lim = min(STAGE, nt - s * STAGE);
+        const unsigned j0 = (unsigned)(s * STAGE);
+        for (int jj = 0; jj < lim; ++jj) {
+            const u32x4 t0 = tl[2 * jj], t1 = tl[2 * jj + 1];
+#pragma unroll
+            for (int e = 0; e < QPL; ++e) {
+                unsigned d = __builtin_popcount(q[e][0].x ^ t0.x);
+                d += __builtin_popcount(q[e][0].y ^ t0.y);
+                d += __builtin_popcount(q[e][0].z ^ t0.z);
+                d += __builtin_popcount(q[e][0].w ^ t0.w);
+                d += __builtin_popcount(q[e][1].x ^ t1.x);
+                d += __builtin_popcount(q[e][1].y ^ t1.y);
+                d += __builtin_popcount(q[e][1].z ^ t1.z);
+                d += __builtin_popcount(q[e][1].w ^ t1.w);
+                const unsigned key = (d << 23) | (j0 + jj);
+                b2[e] = med3u(b1[e], b2[e], key);
+                b1[e] = min(b1[e], key);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+#pragma unroll
+    for (int e = 0; e < QPL; ++e) {
+        const int qi = w.q0 + e * 256 + threadIdx.x;
+        if (qi >= nq) continue;
+        const int64_t o = P.dense_base + qi;
+        if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }
+        const float d1 = (float)(b1[e] >> 23), d2 = (float)(b2[e] >> 23);
+        const bool acc = nt >= 2 ? ((double)d1 < (double)d2 * ratio) : true;
+        out_idx[o] = acc ? (int)(b1[e] & 0x7fffffu) : -1;
+        out_dist[o] = d1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Match-graph assembly: per pair (one 1024-thread block), optional distinct
+// filter (trainIdx seen/dup bitsets in LDS, SfM.cpp:547-564), count, min_count
+// keep flag (SfM.cpp:566-570), then a second launch writes packed DMatch in
+// query order at the scanned pair offset.
+__device__ __forceinline__ int block_exclusive_scan(int v, int* sh, int& total) {
+    // 1024 threads = 16 waves
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(x, o); if (lane >= o) x += y; }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        int s = lane < 16 ? sh[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) { const int y = __shfl_up(s, o); if (lane >= o) s += y; }
+        if (lane < 16) sh[16 + lane] = s;
+    }
+    __syncthreads();
+    const int wbase = wid ? sh[16 + wid - 1] : 0;
+    total = sh[31];
+    __syncthreads();
+    return wbase + x - v;
+}
+
+// mode 0: count -> counts[p], keep[p];  mode 1: write packed matches.
+template <int MODE>
+__global__ __launch_bounds__(1024)
+void assemble_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restrict__ imgs,
+                     const int32_t* __restrict__ out_idx, const float* __restrict__ out_dist,
+                     int distinct, int min_count, int64_t* __restrict__ counts, int32_t* __restrict__ keep,
+                     const int64_t* __restrict__ offsets, DMatchDev* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned bits[];   // seen | dup bitsets (distinct only)
+    __shared__ int sh[32];
+    const int p = blockIdx.x;
+    const PairDev P = pairs[p];
+    const int nq = imgs[P.left].rows, nt = imgs[P.right].rows;
+    const int words = (nt + 31) >> 5;
+    const int32_t* ix = out_idx + P.dense_base;
+    const float* dx = out_dist + P.dense_base;
+    if (distinct) {
+        for (int i = threadIdx.x; i < 2 * words; i += blockDim.x) bits[i] = 0;
+        __syncthreads();
+        for (int q = threadIdx.x; q < nq; q += blockDim.x) {
+            const int j = ix[q];
+            if (j >= 0) {
+                const unsigned bit = 1u << (j & 31);
+                const unsigned old = atomicOr(&bits[j >> 5], bit);
+                if (old & bit) atomicOr(&bits[words + (j >> 5)], bit);
+            }
+        }
+        __syncthreads();
+    }
+    int64_t run = 0;
+    const int64_t base = MODE == 1 ? offsets[p] : 0;
+    for (int q0 = 0; q0 < nq; q0 += blockDim.x) {
+        const int q = q0 + threadIdx.x;
+        int j = q < nq ? ix[q] : -1;
+        if (j >= 0 && distinct && (bits[words + (j >> 5)] >> (j & 31)) & 1u) j = -1;
+        int total;
+        const int rank = block_exclusive_scan(j >= 0 ? 1 : 0, sh, total);
+        if (MODE == 1 && j >= 0) out[base + run + rank] = DMatchDev{q, j, 0, dx[q]};
+        run += total;
+    }
+    if (MODE == 0 && threadIdx.x == 0) { counts[p] = run; keep[p] = run < min_count ? 0 : 1; }
+}
+
+// offsets[0..n] = exclusive scan of counts (single block, 1024 threads).
+__global__ __launch_bounds__(1024)
+void scan_offsets_kernel(const int64_t* __restrict__ counts, int n, int64_t* __restrict__ offsets) {
+    __shared__ long long sh[1024];
+    long long run = 0;
+    for (int c0 = 0; c0 < n; c0 += 1024) {
+        const int i = c0 + threadIdx.x;
+        const long long v = i < n ? counts[i] : 0;
+        sh[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const long long y = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
+            __syncthreads();
+            sh[threadIdx.x] += y;
+            __syncthreads();
+        }
+        if (i < n) offsets[i] = run + sh[threadIdx.x] - v;
+        run += sh[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) offsets[n] = run;
+}
+
+__global__ void selftest_sqrt_kernel(int64_t n, uint32_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = __float_as_uint(sqrt_rn_int(i));
+}
+
+// ---------------------------------------------------------------------------
+// Launch wrappers (host side, called by matcher.cpp).
+hipError_t launch_selftest_sqrt(int64_t n, uint32_t* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    selftest_sqrt_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, out);
+    return hipGetLastError();
+}
+hipError_t launch_prep_l2(const float* src, int rows, int cols, int rows_pad, int8_t* dst, int32_t* norm,
+                          int32_t* keyc, int32_t* nonintegral, hipStream_t st) {
+    if (rows_pad == 0) return hipSuccess;
+    const int rows_per_block = 8;   // 256 threads
+    prep_l2_kernel<<<(rows_pad + rows_per_block - 1) / rows_per_block, 256, 0, st>>>(src, rows, cols, rows_pad, dst, norm, keyc, nonintegral);
+    return hipGetLastError();
+}
+hipError_t launch_prep_f32(const float* src, int rows, int cols, int rows_pad, float* dst, hipStream_t st) {
+    const int64_t total = (int64_t)rows_pad * SIFT_DIM;
+    if (total == 0) return hipSuccess;
+    prep_f32_kernel<<<(unsigned)((total + 255) / 256), 256, 0, st>>>(src, rows, cols, rows_pad, dst);
+    return hipGetLastError();
+}
+hipError_t launch_prep_hamming(const uint8_t* src, int rows, int cols, int rows_pad, uint8_t* dst, hipStream_t st) {
+    const int64_t total = (int64_t)rows_pad * ORB_BYTES;
+    if (total == 0) return hipSuccess;
+    prep_hamming_kernel<<<(unsigned)((total + 255) / 256), 256, 0, st>>>(src, rows, cols, rows_pad, dst);
+    return hipGetLastError();
+}
+
+constexpr int SIFT_QT = 2, SIFT_WAVES = 8;
+static_assert(SIFT_QT * SIFT_WAVES * 32 == ROW_ALIGN, "work item = ROW_ALIGN queries");
+
+hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
+                            const int8_t* desc8, const int32_t* norm, const int32_t* keyc, int32_t* out_idx,
+                            float* out_dist, int2* slow_list, int32_t* slow_count, double ratio, hipStream_t st) {
+    if (n_work == 0) return hipSuccess;
+    sift_knn2_kernel<SIFT_QT, SIFT_WAVES><<<n_work, SIFT_WAVES * 64, 0, st>>>(
+        work, pairs, imgs, desc8, norm, keyc, out_idx, out_dist, slow_list, slow_count, ratio);
+    return hipGetLastError();
+}
+hipError_t launch_sift_slow(const int2* slow_list, const int32_t* slow_count, const PairDev* pairs,
+                            const ImgDev* imgs, const int8_t* desc8, const int32_t* norm, int32_t* out_idx,
+                            float* out_dist, double ratio, hipStream_t st) {
+    sift_slow_kernel<<<256, 256, 0, st>>>(slow_list, slow_count, pairs, imgs, desc8, norm, out_idx, out_dist, ratio);
+    return hipGetLastError();
+}
+hipError_t launch_sift_f32(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
+                           const float* f32, int32_t* out_idx, float* out_dist, double ratio, hipStream_t st) {
+    if (n_work == 0) return hipSuccess;
+    sift_f32_kernel<<<n_work, 512, 0, st>>>(work, nullptr, pairs, imgs, f32, out_idx, out_dist, ratio);
+    return hipGetLastError();
+}
+hipError_t launch_orb_knn2(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
+                           const uint8_t* desc8, int32_t* out_idx, float* out_dist, double ratio, hipStream_t st) {
+    if (n_work == 0) return hipSuccess;
+    orb_knn2_kernel<2><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc8, out_idx, out_dist, ratio);
+    return hipGetLastError();
+}
+hipError_t launch_assemble(const PairDev* pairs, int n_pairs, const ImgDev* imgs, const int32_t* out_idx,
+                           const float* out_dist, int distinct, int min_count, int max_nt, int64_t* counts,
+                           int32_t* keep, int64_t* offsets, DMatchDev* out, hipStream_t st) {
+    if (n_pairs == 0) {
+        hipMemsetAsync(offsets, 0, sizeof(int64_t), st);
+        return hipGetLastError();
+    }
+    const size_t shmem = distinct ? (size_t)2 * ((max_nt + 31) / 32) * 4 : 0;
+    if (shmem > 150 * 1024) return hipErrorInvalidValue;
+    assemble_kernel<0><<<n_pairs, 1024, shmem, st>>>(pairs, imgs, out_idx, out_dist, distinct, min_count, counts, keep, nullptr, nullptr);
+    scan_offsets_kernel<<<1, 1024, 0, st>>>(counts, n_pairs, offsets);
+    assemble_kernel<1><<<n_pairs, 1024, shmem, st>>>(pairs, imgs, out_idx, out_dist, distinct, min_count, counts, keep, offsets, out);
+    return hipGetLastError();
+}
+
+}  // namespace sfmx

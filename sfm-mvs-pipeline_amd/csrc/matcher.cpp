@@ -1,0 +1,505 @@
+// SPDX-License-Identifier: MIT
+// sfmx matcher — host driver behind the C ABI (include/sfmx.h).
+//
+// Mirrors the reference's strategy call
+//   IFeatureMatchingStrategy::calculateShotMatches(scene, matcher, out)
+//   (src/photogrammetrie/sfm/IFeatureMatchingStrategy.h:45-46, e.g.
+//    UnorderedFeatureMatchingStrategy.cpp:27-90)
+// followed by SfM::calculateShotMatches' filters (sfm/SfM.cpp:542-575):
+//   set_images  = the descriptor matrices the Scene's shots own (CameraShot.h:39-42),
+//                 uploaded once into an HBM pool and prepared (int8 + norms)
+//   run         = the OpenMP pair loop (:40-88) as one batched launch sequence
+//   fetch       = the vector<ShotMatches> hand-back, as packed DMatch lists
+// No CPU fallback: every numeric step runs in the HIP kernels of
+// match_kernels.hip; a missing/unsupported device returns SFMX_EDEVICE.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/sfmx.h"
+#include "match_common.hpp"
+
+namespace sfmx {
+hipError_t launch_prep_l2(const float*, int, int, int, int8_t*, int32_t*, int32_t*, int32_t*, hipStream_t);
+hipError_t launch_prep_f32(const float*, int, int, int, float*, hipStream_t);
+hipError_t launch_prep_hamming(const uint8_t*, int, int, int, uint8_t*, hipStream_t);
+hipError_t launch_sift_knn2(const WorkItem*, int, const PairDev*, const ImgDev*, const int8_t*, const int32_t*,
+                            const int32_t*, int32_t*, float*, int2*, int32_t*, double, hipStream_t);
+hipError_t launch_sift_slow(const int2*, const int32_t*, const PairDev*, const ImgDev*, const int8_t*,
+                            const int32_t*, int32_t*, float*, double, hipStream_t);
+hipError_t launch_sift_f32(const WorkItem*, int, const PairDev*, const ImgDev*, const float*, int32_t*, float*,
+                           double, hipStream_t);
+hipError_t launch_orb_knn2(const WorkItem*, int, const PairDev*, const ImgDev*, const uint8_t*, int32_t*, float*,
+                           double, hipStream_t);
+hipError_t launch_selftest_sqrt(int64_t, uint32_t*, hipStream_t);
+hipError_t launch_assemble(const PairDev*, int, const ImgDev*, const int32_t*, const float*, int, int, int,
+                           int64_t*, int32_t*, int64_t*, DMatchDev*, hipStream_t);
+}  // namespace sfmx
+
+using namespace sfmx;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(e_ == hipErrorOutOfMemory ? SFMX_ENOMEM : SFMX_EDEVICE,               \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                   \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return SFMX_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr; cap = 0;
+        const size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) { p = nullptr; return fail(SFMX_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)); }
+        cap = want;
+        return SFMX_OK;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+// Device guard: set the matcher's device for the duration of a call.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) { (void)hipGetDevice(&prev); (void)hipSetDevice(dev); }
+    ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+}  // namespace
+
+struct sfmx_matcher {
+    int device = 0;
+    int norm = 0;
+    int n_imgs = 0;
+    std::vector<ImgDev> imgs;
+    int64_t total_rows = 0;
+    int max_rows = 0;
+    bool any_nonintegral = false;
+    DevBuf raw, desc8, normv, keyc, f32, flags, imgs_d;
+    // run state
+    int n_pairs = 0;
+    int64_t dense_total = 0;
+    int64_t fp32_pairs = 0;
+    DevBuf pairs_d, work_d, work32_d, dense_idx, dense_dist, slow_list, slow_count, counts, keep, offsets, out;
+    bool has_run = false;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};   // run start, main kernel end, run end
+    bool ev_recorded = false;
+};
+
+namespace {
+
+int check_device(int dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(SFMX_EDEVICE, "no HIP device visible");
+    if (dev < 0 || dev >= n) return fail(SFMX_EINVAL, "device index out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(SFMX_EDEVICE, "hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SFMX_EDEVICE, std::string("sfmx kernels are built for gfx950 only, device is ") + prop.gcnArchName);
+    return SFMX_OK;
+}
+
+int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hipStream_t st, bool device_src) {
+    if (!m || (n > 0 && !imgs) || n < 0) return fail(SFMX_EINVAL, "null matcher/images");
+    if (norm != SFMX_NORM_L2 && norm != SFMX_NORM_HAMMING) return fail(SFMX_EINVAL, "norm must be SFMX_NORM_L2 or SFMX_NORM_HAMMING");
+    const int want_type = norm == SFMX_NORM_L2 ? SFMX_32F : SFMX_8U;
+    const int max_cols = norm == SFMX_NORM_L2 ? SIFT_DIM : ORB_BYTES;
+    for (int i = 0; i < n; ++i) {
+        if (imgs[i].rows < 0 || imgs[i].cols < 0) return fail(SFMX_EINVAL, "negative descriptor shape");
+        if (imgs[i].rows > 0 && imgs[i].type != want_type)
+            return fail(SFMX_EINVAL, "descriptor type does not match norm (L2 needs CV_32F, HAMMING needs CV_8U)");
+        if (imgs[i].rows > 0 && (imgs[i].cols < 1 || imgs[i].cols > max_cols))
+            return fail(SFMX_EINVAL, "descriptor width unsupported (SIFT <= 128 floats, ORB <= 32 bytes)");
+        if (imgs[i].rows >= (1 << 18))   // cv::BFMatcher asserts train rows < IMGIDX_ONE = 2^18 [ext]
+            return fail(SFMX_EINVAL, "more than 2^18 - 1 descriptors in one image");
+        if (imgs[i].rows > 0 && !imgs[i].data) return fail(SFMX_EINVAL, "null descriptor data");
+    }
+    DeviceGuard g(m->device);
+    m->norm = norm;
+    m->n_imgs = n;
+    m->imgs.assign(n, ImgDev{});
+    m->has_run = false;
+    int64_t row = 0, raw_bytes = 0;
+    std::vector<int64_t> raw_off(n);
+    m->max_rows = 0;
+    for (int i = 0; i < n; ++i) {
+        ImgDev& d = m->imgs[i];
+        d.rows = imgs[i].rows;
+        d.rows_pad = (int32_t)align_up(d.rows, ROW_ALIGN);
+        d.row0 = row;
+        d.integral = 1;
+        row += d.rows_pad;
+        m->max_rows = std::max(m->max_rows, d.rows);
+        const int64_t esz = norm == SFMX_NORM_L2 ? 4 : 1;
+        raw_off[i] = raw_bytes;
+        raw_bytes += align_up((int64_t)imgs[i].rows * imgs[i].cols * esz, 256);
+    }
+    m->total_rows = row;
+    const int row_bytes = norm == SFMX_NORM_L2 ? SIFT_DIM : ORB_BYTES;
+    int rc;
+    if ((rc = m->desc8.ensure((size_t)row * row_bytes))) return rc;
+    if ((rc = m->flags.ensure(sizeof(int32_t) * std::max(n, 1)))) return rc;
+    if ((rc = m->imgs_d.ensure(sizeof(ImgDev) * std::max(n, 1)))) return rc;
+    if (norm == SFMX_NORM_L2) {
+        if ((rc = m->normv.ensure((size_t)row * 4))) return rc;
+        if ((rc = m->keyc.ensure((size_t)row * 4))) return rc;
+    }
+    if (!device_src && (rc = m->raw.ensure((size_t)raw_bytes))) return rc;
+    HIPCHK(hipMemsetAsync(m->flags.p, 0, sizeof(int32_t) * std::max(n, 1), st));
+    std::vector<const void*> src(n);
+    for (int i = 0; i < n; ++i) {
+        const int64_t esz = norm == SFMX_NORM_L2 ? 4 : 1;
+        const size_t bytes = (size_t)imgs[i].rows * imgs[i].cols * esz;
+        if (device_src) src[i] = imgs[i].data;
+        else {
+            src[i] = m->raw.as<char>() + raw_off[i];
+            if (bytes) HIPCHK(hipMemcpyAsync((void*)src[i], imgs[i].data, bytes, hipMemcpyHostToDevice, st));
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        const ImgDev& d = m->imgs[i];
+        if (norm == SFMX_NORM_L2)
+            HIPCHK(launch_prep_l2((const float*)src[i], d.rows, imgs[i].cols, d.rows_pad,
+                                  m->desc8.as<int8_t>() + d.row0 * SIFT_DIM, m->normv.as<int32_t>() + d.row0,
+                                  m->keyc.as<int32_t>() + d.row0, m->flags.as<int32_t>() + i, st));
+        else
+            HIPCHK(launch_prep_hamming((const uint8_t*)src[i], d.rows, imgs[i].cols, d.rows_pad,
+                                       m->desc8.as<uint8_t>() + d.row0 * ORB_BYTES, st));
+    }
+    m->any_nonintegral = false;
+    if (norm == SFMX_NORM_L2 && n > 0) {
+        std::vector<int32_t> fl(n);
+        HIPCHK(hipMemcpyAsync(fl.data(), m->flags.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (int i = 0; i < n; ++i) {
+            m->imgs[i].integral = fl[i] ? 0 : 1;
+            m->any_nonintegral |= fl[i] != 0;
+        }
+        if (m->any_nonintegral) {
+            if ((rc = m->f32.ensure((size_t)row * SIFT_DIM * 4))) return rc;
+            for (int i = 0; i < n; ++i) {
+                const ImgDev& d = m->imgs[i];
+                if (!d.integral)
+                    HIPCHK(launch_prep_f32((const float*)src[i], d.rows, imgs[i].cols, d.rows_pad,
+                                           m->f32.as<float>() + d.row0 * SIFT_DIM, st));
+            }
+        }
+    }
+    if (n > 0) HIPCHK(hipMemcpyAsync(m->imgs_d.p, m->imgs.data(), sizeof(ImgDev) * n, hipMemcpyHostToDevice, st));
+    if (!device_src) HIPCHK(hipStreamSynchronize(st));   // host buffers may be released by the caller
+    return SFMX_OK;
+}
+
+int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, int distinct, int min_count,
+             hipStream_t st) {
+    if (!m) return fail(SFMX_EINVAL, "null matcher");
+    if (m->norm == 0) return fail(SFMX_ESTATE, "run before set_images");
+    if (n_pairs < 0 || (n_pairs > 0 && !pairs)) return fail(SFMX_EINVAL, "bad pair list");
+    if (!(ratio == ratio)) return fail(SFMX_EINVAL, "ratio is NaN");
+    DeviceGuard g(m->device);
+    std::vector<PairDev> pd(n_pairs);
+    int64_t dense = 0;
+    for (int p = 0; p < n_pairs; ++p) {
+        const int L = pairs[2 * p], R = pairs[2 * p + 1];
+        if (L < 0 || L >= m->n_imgs || R < 0 || R >= m->n_imgs) return fail(SFMX_EINVAL, "pair image index out of range");
+        pd[p] = PairDev{L, R, dense};
+        dense += m->imgs[L].rows;
+    }
+    // Work items: 512-query blocks, sorted by train image so XCD-contiguous
+    // blocks stream the same train rows (L2 reuse); fp32 pairs separately.
+    std::vector<WorkItem> work, work32;
+    std::vector<int> order(n_pairs);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pd[a].right < pd[b].right; });
+    m->fp32_pairs = 0;
+    for (int p : order) {
+        const ImgDev& L = m->imgs[pd[p].left];
+        const ImgDev& R = m->imgs[pd[p].right];
+        const bool f32path = m->norm == SFMX_NORM_L2 && !(L.integral && R.integral);
+        m->fp32_pairs += f32path;
+        for (int q0 = 0; q0 < L.rows; q0 += ROW_ALIGN) (f32path ? work32 : work).push_back(WorkItem{p, q0});
+    }
+    int rc;
+    if ((rc = m->pairs_d.ensure(sizeof(PairDev) * std::max(n_pairs, 1)))) return rc;
+    if ((rc = m->work_d.ensure(sizeof(WorkItem) * std::max<size_t>(work.size(), 1)))) return rc;
+    if ((rc = m->work32_d.ensure(sizeof(WorkItem) * std::max<size_t>(work32.size(), 1)))) return rc;
+    if ((rc = m->dense_idx.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
+    if ((rc = m->dense_dist.ensure(sizeof(float) * std::max<int64_t>(dense, 1)))) return rc;
+    if ((rc = m->slow_list.ensure(sizeof(int2) * std::max<int64_t>(dense, 1)))) return rc;
+    if ((rc = m->slow_count.ensure(sizeof(int32_t)))) return rc;
+    if ((rc = m->counts.ensure(sizeof(int64_t) * std::max(n_pairs, 1)))) return rc;
+    if ((rc = m->keep.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
+    if ((rc = m->offsets.ensure(sizeof(int64_t) * (n_pairs + 1)))) return rc;
+    if ((rc = m->out.ensure(sizeof(DMatchDev) * std::max<int64_t>(dense, 1)))) return rc;
+    if (n_pairs) HIPCHK(hipMemcpyAsync(m->pairs_d.p, pd.data(), sizeof(PairDev) * n_pairs, hipMemcpyHostToDevice, st));
+    if (!work.empty()) HIPCHK(hipMemcpyAsync(m->work_d.p, work.data(), sizeof(WorkItem) * work.size(), hipMemcpyHostToDevice, st));
+    if (!work32.empty()) HIPCHK(hipMemcpyAsync(m->work32_d.p, work32.data(), sizeof(WorkItem) * work32.size(), hipMemcpyHostToDevice, st));
+    if (!m->ev[0])
+        for (auto& e : m->ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipMemsetAsync(m->slow_count.p, 0, sizeof(int32_t), st));
+    HIPCHK(hipEventRecord(m->ev[0], st));
+    // Pairs with an empty left image have no work item; pairs with an empty
+    // right image are handled in-kernel (every query: no neighbour).
+    const PairDev* P = m->pairs_d.as<PairDev>();
+    const ImgDev* I = m->imgs_d.as<ImgDev>();
+    if (m->norm == SFMX_NORM_L2) {
+        HIPCHK(launch_sift_knn2(m->work_d.as<WorkItem>(), (int)work.size(), P, I, m->desc8.as<int8_t>(),
+                                m->normv.as<int32_t>(), m->keyc.as<int32_t>(), m->dense_idx.as<int32_t>(),
+                                m->dense_dist.as<float>(), m->slow_list.as<int2>(), m->slow_count.as<int32_t>(), ratio, st));
+        HIPCHK(hipEventRecord(m->ev[1], st));
+        HIPCHK(launch_sift_slow(m->slow_list.as<int2>(), m->slow_count.as<int32_t>(), P, I, m->desc8.as<int8_t>(),
+                                m->normv.as<int32_t>(), m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
+        if (!work32.empty())
+            HIPCHK(launch_sift_f32(m->work32_d.as<WorkItem>(), (int)work32.size(), P, I, m->f32.as<float>(),
+                                   m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
+    } else {
+        HIPCHK(launch_orb_knn2(m->work_d.as<WorkItem>(), (int)work.size(), P, I, m->desc8.as<uint8_t>(),
+                               m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
+        HIPCHK(hipEventRecord(m->ev[1], st));
+    }
+    int max_nt = 0;
+    for (int p = 0; p < n_pairs; ++p) max_nt = std::max(max_nt, m->imgs[pd[p].right].rows);
+    HIPCHK(launch_assemble(P, n_pairs, I, m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), distinct ? 1 : 0,
+                           min_count, max_nt, m->counts.as<int64_t>(), m->keep.as<int32_t>(),
+                           m->offsets.as<int64_t>(), m->out.as<DMatchDev>(), st));
+    HIPCHK(hipEventRecord(m->ev[2], st));
+    m->ev_recorded = true;
+    m->n_pairs = n_pairs;
+    m->dense_total = dense;
+    m->has_run = true;
+    return SFMX_OK;
+}
+
+int fetch_impl(sfmx_matcher* m, sfmx_dmatch* out, int64_t cap, int64_t* required, int64_t* pair_offsets,
+               int32_t* keep, hipStream_t st) {
+    if (!m) return fail(SFMX_EINVAL, "null matcher");
+    if (!m->has_run) return fail(SFMX_ESTATE, "fetch before run");
+    DeviceGuard g(m->device);
+    std::vector<int64_t> off(m->n_pairs + 1);
+    HIPCHK(hipMemcpyAsync(off.data(), m->offsets.p, sizeof(int64_t) * (m->n_pairs + 1), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const int64_t total = off[m->n_pairs];
+    if (required) *required = total;
+    if (pair_offsets) std::memcpy(pair_offsets, off.data(), sizeof(int64_t) * (m->n_pairs + 1));
+    if (keep && m->n_pairs) HIPCHK(hipMemcpyAsync(keep, m->keep.p, sizeof(int32_t) * m->n_pairs, hipMemcpyDeviceToHost, st));
+    if (out) {
+        if (cap < total) { HIPCHK(hipStreamSynchronize(st)); return fail(SFMX_ECAPACITY, "output capacity too small"); }
+        if (total) HIPCHK(hipMemcpyAsync(out, m->out.p, sizeof(sfmx_dmatch) * total, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    return SFMX_OK;
+}
+
+}  // namespace
+
+static_assert(sizeof(sfmx_dmatch) == 16 && sizeof(DMatchDev) == 16, "DMatch layout");
+
+extern "C" {
+
+const char* sfmx_version(void) { return "sfmx 0.1 (gfx950)"; }
+const char* sfmx_last_error(void) { return g_last_error.c_str(); }
+
+int sfmx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return fail(SFMX_EDEVICE, "hipGetDeviceCount failed");
+    int good = 0;
+    for (int d = 0; d < n; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) ++good;
+    }
+    return good;
+}
+
+int sfmx_selftest_sqrt(int32_t device, int64_t n, uint32_t* out_bits) {
+    if (n < 0 || n > (int64_t)1 << 24 || (n > 0 && !out_bits)) return fail(SFMX_EINVAL, "n must be in [0, 2^24]");
+    int rc = check_device(device);
+    if (rc) return rc;
+    DeviceGuard g(device);
+    DevBuf b;
+    if ((rc = b.ensure(sizeof(uint32_t) * std::max<int64_t>(n, 1)))) return rc;
+    hipError_t e = launch_selftest_sqrt(n, b.as<uint32_t>(), nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out_bits, b.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost);
+    b.release();
+    if (e != hipSuccess) return fail(SFMX_EDEVICE, hipGetErrorString(e));
+    return SFMX_OK;
+}
+
+int sfmx_matcher_create(int32_t device, sfmx_matcher** out) {
+    if (!out) return fail(SFMX_EINVAL, "null out");
+    *out = nullptr;
+    int rc = check_device(device);
+    if (rc) return rc;
+    auto* m = new (std::nothrow) sfmx_matcher();
+    if (!m) return fail(SFMX_ENOMEM, "host allocation");
+    m->device = device;
+    *out = m;
+    return SFMX_OK;
+}
+
+int sfmx_matcher_destroy(sfmx_matcher* m) {
+    if (!m) return SFMX_OK;
+    {
+        DeviceGuard g(m->device);
+        DevBuf* bufs[] = {&m->raw, &m->desc8, &m->normv, &m->keyc, &m->f32, &m->flags, &m->imgs_d, &m->pairs_d,
+                          &m->work_d, &m->work32_d, &m->dense_idx, &m->dense_dist, &m->slow_list, &m->slow_count,
+                          &m->counts, &m->keep, &m->offsets, &m->out};
+        for (DevBuf* b : bufs) b->release();
+        for (auto& e : m->ev) if (e) (void)hipEventDestroy(e);
+    }
+    delete m;
+    return SFMX_OK;
+}
+
+int sfmx_matcher_set_images(sfmx_matcher* m, const sfmx_desc* imgs, int32_t n, int32_t norm, void* stream) {
+    return set_images_impl(m, imgs, n, norm, (hipStream_t)stream, false);
+}
+
+int sfmx_matcher_set_images_device(sfmx_matcher* m, const sfmx_desc* imgs, int32_t n, int32_t norm, void* stream) {
+    return set_images_impl(m, imgs, n, norm, (hipStream_t)stream, true);
+}
+
+int sfmx_matcher_run(sfmx_matcher* m, const int32_t* pairs, int32_t n_pairs, double ratio, int32_t distinct,
+                     int32_t min_count, void* stream) {
+    return run_impl(m, pairs, n_pairs, ratio, distinct, min_count, (hipStream_t)stream);
+}
+
+int sfmx_matcher_fetch(sfmx_matcher* m, sfmx_dmatch* out, int64_t cap, int64_t* required, int64_t* pair_offsets,
+                       int32_t* keep, void* stream) {
+    return fetch_impl(m, out, cap, required, pair_offsets, keep, (hipStream_t)stream);
+}
+
+int sfmx_matcher_device_results(sfmx_matcher* m, const sfmx_dmatch** matches, const int64_t** pair_offsets,
+                                const int32_t** keep) {
+    if (!m) return fail(SFMX_EINVAL, "null matcher");
+    if (!m->has_run) return fail(SFMX_ESTATE, "no results before run");
+    if (matches) *matches = m->out.as<const sfmx_dmatch>();
+    if (pair_offsets) *pair_offsets = m->offsets.as<const int64_t>();
+    if (keep) *keep = m->keep.as<const int32_t>();
+    return SFMX_OK;
+}
+
+int sfmx_matcher_stats(sfmx_matcher* m, int64_t* slow_queries, int64_t* fp32_pairs, void* stream) {
+    if (!m) return fail(SFMX_EINVAL, "null matcher");
+    if (!m->has_run) return fail(SFMX_ESTATE, "no stats before run");
+    DeviceGuard g(m->device);
+    int32_t sc = 0;
+    HIPCHK(hipMemcpyAsync(&sc, m->slow_count.p, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    if (slow_queries) *slow_queries = sc;
+    if (fp32_pairs) *fp32_pairs = m->fp32_pairs;
+    return SFMX_OK;
+}
+
+int sfmx_matcher_timing(sfmx_matcher* m, float* main_kernel_ms, float* total_ms) {
+    if (!m) return fail(SFMX_EINVAL, "null matcher");
+    if (!m->ev_recorded) return fail(SFMX_ESTATE, "no timing before run");
+    DeviceGuard g(m->device);
+    HIPCHK(hipEventSynchronize(m->ev[2]));
+    float a = 0.f, b = 0.f;
+    HIPCHK(hipEventElapsedTime(&a, m->ev[0], m->ev[1]));
+    HIPCHK(hipEventElapsedTime(&b, m->ev[0], m->ev[2]));
+    if (main_kernel_ms) *main_kernel_ms = a;
+    if (total_ms) *total_ms = b;
+    return SFMX_OK;
+}
+
+int sfmx_match_pairs(const sfmx_desc* imgs, int32_t n_imgs, const int32_t* pairs, int32_t n_pairs, int32_t norm,
+                     double ratio, int32_t distinct, int32_t min_count, int32_t n_gpus, sfmx_dmatch* out,
+                     int64_t cap, int64_t* required, int64_t* pair_offsets, int32_t* keep) {
+    if (n_pairs < 0 || (n_pairs > 0 && !pairs)) return fail(SFMX_EINVAL, "bad pair list");
+    int ndev = sfmx_device_count();
+    if (ndev <= 0) return fail(SFMX_EDEVICE, "no gfx950 device");
+    const int G = std::max(1, std::min<int>(n_gpus <= 0 ? ndev : n_gpus, ndev));
+    // Split the pair list into G contiguous slices balanced by sum Nq*Nt.
+    std::vector<double> cost(n_pairs);
+    double tot = 0;
+    for (int p = 0; p < n_pairs; ++p) {
+        const int L = pairs[2 * p], R = pairs[2 * p + 1];
+        if (L < 0 || L >= n_imgs || R < 0 || R >= n_imgs) return fail(SFMX_EINVAL, "pair image index out of range");
+        cost[p] = (double)imgs[L].rows * imgs[R].rows + 1.0;
+        tot += cost[p];
+    }
+    std::vector<int> cut(G + 1, n_pairs);
+    cut[0] = 0;
+    {
+        double acc = 0; int g = 1;
+        for (int p = 0; p < n_pairs && g < G; ++p) {
+            acc += cost[p];
+            if (acc >= tot * g / G) cut[g++] = p + 1;
+        }
+    }
+    struct Slice { std::vector<sfmx_dmatch> m; std::vector<int64_t> off; std::vector<int32_t> keep; int rc = 0; std::string err; };
+    std::vector<Slice> sl(G);
+    auto work = [&](int g) {
+        Slice& s = sl[g];
+        const int np = cut[g + 1] - cut[g];
+        sfmx_matcher* m = nullptr;
+        if ((s.rc = sfmx_matcher_create(g, &m))) { s.err = g_last_error; return; }
+        hipStream_t st = nullptr;
+        {
+            DeviceGuard dg(g);
+            if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { s.rc = SFMX_EDEVICE; s.err = "stream"; sfmx_matcher_destroy(m); return; }
+        }
+        s.off.assign(np + 1, 0); s.keep.assign(np, 0);
+        int64_t req = 0;
+        if (!(s.rc = sfmx_matcher_set_images(m, imgs, n_imgs, norm, st)) &&
+            !(s.rc = sfmx_matcher_run(m, pairs + 2 * cut[g], np, ratio, distinct, min_count, st)) &&
+            !(s.rc = sfmx_matcher_fetch(m, nullptr, 0, &req, s.off.data(), s.keep.data(), st))) {
+            s.m.resize(req);
+            s.rc = sfmx_matcher_fetch(m, s.m.data(), req, &req, nullptr, nullptr, st);
+        }
+        if (s.rc) s.err = g_last_error;
+        { DeviceGuard dg(g); (void)hipStreamDestroy(st); }
+        sfmx_matcher_destroy(m);
+    };
+    if (G == 1) work(0);
+    else {
+        std::vector<std::thread> th;
+        for (int g = 0; g < G; ++g) th.emplace_back(work, g);
+        for (auto& t : th) t.join();
+    }
+    int64_t total = 0;
+    for (int g = 0; g < G; ++g) {
+        if (sl[g].rc) return fail(sl[g].rc, sl[g].err);
+        total += (int64_t)sl[g].m.size();
+    }
+    if (required) *required = total;
+    if (out && cap < total) return fail(SFMX_ECAPACITY, "output capacity too small");
+    int64_t base = 0;
+    for (int g = 0; g < G; ++g) {
+        const int np = cut[g + 1] - cut[g];
+        for (int p = 0; p < np; ++p) {
+            if (pair_offsets) pair_offsets[cut[g] + p] = base + sl[g].off[p];
+            if (keep) keep[cut[g] + p] = sl[g].keep[p];
+        }
+        if (out && !sl[g].m.empty()) std::memcpy(out + base, sl[g].m.data(), sizeof(sfmx_dmatch) * sl[g].m.size());
+        base += (int64_t)sl[g].m.size();
+    }
+    if (pair_offsets) pair_offsets[n_pairs] = base;
+    return SFMX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,94 @@
+"""ctypes binding of libsfmx.so (the C ABI declared in include/sfmx.h).
+
+The shared library is built in-tree by ``make -C sfm-mvs-pipeline_amd`` (or
+``__graft_entry__.build()``).  There is no Python or CPU fallback for any
+numeric step: if the library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libsfmx.so")
+
+SFMX_OK, SFMX_EINVAL, SFMX_ENOMEM, SFMX_EDEVICE, SFMX_ECAPACITY, SFMX_ESTATE = 0, -1, -2, -3, -4, -5
+SFMX_NORM_L2, SFMX_NORM_HAMMING = 4, 6
+SFMX_8U, SFMX_32F = 0, 5
+
+ERROR_NAMES = {
+    SFMX_EINVAL: "SFMX_EINVAL",
+    SFMX_ENOMEM: "SFMX_ENOMEM",
+    SFMX_EDEVICE: "SFMX_EDEVICE",
+    SFMX_ECAPACITY: "SFMX_ECAPACITY",
+    SFMX_ESTATE: "SFMX_ESTATE",
+}
+
+
+class sfmx_desc(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("rows", C.c_int32), ("cols", C.c_int32),
+                ("type", C.c_int32), ("_pad", C.c_int32)]
+
+
+class sfmx_dmatch(C.Structure):
+    _fields_ = [("queryIdx", C.c_int32), ("trainIdx", C.c_int32), ("imgIdx", C.c_int32),
+                ("distance", C.c_float)]
+
+
+# Every symbol include/sfmx.h (and include/sfmx_ba.h) declares, with its ctypes prototype.
+_P = C.POINTER
+_i32p, _i64p, _vp = _P(C.c_int32), _P(C.c_int64), C.c_void_p
+PROTOTYPES = {
+    "sfmx_pairs_unordered": (C.c_int64, [C.c_int32, _i32p, C.c_int64]),
+    "sfmx_pairs_video": (C.c_int64, [C.c_int32, C.c_int32, _i32p, C.c_int64]),
+    "sfmx_pairs_grid": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, _i32p, C.c_int64]),
+    "sfmx_matcher_create": (C.c_int, [C.c_int32, _P(_vp)]),
+    "sfmx_matcher_destroy": (C.c_int, [_vp]),
+    "sfmx_matcher_set_images": (C.c_int, [_vp, _P(sfmx_desc), C.c_int32, C.c_int32, _vp]),
+    "sfmx_matcher_set_images_device": (C.c_int, [_vp, _P(sfmx_desc), C.c_int32, C.c_int32, _vp]),
+    "sfmx_matcher_run": (C.c_int, [_vp, _i32p, C.c_int32, C.c_double, C.c_int32, C.c_int32, _vp]),
+    "sfmx_matcher_fetch": (C.c_int, [_vp, _vp, C.c_int64, _i64p, _i64p, _i32p, _vp]),
+    "sfmx_matcher_device_results": (C.c_int, [_vp, _P(_vp), _P(_vp), _P(_vp)]),
+    "sfmx_matcher_stats": (C.c_int, [_vp, _i64p, _i64p, _vp]),
+    "sfmx_matcher_timing": (C.c_int, [_vp, _P(C.c_float), _P(C.c_float)]),
+    "sfmx_match_pairs": (C.c_int, [_P(sfmx_desc), C.c_int32, _i32p, C.c_int32, C.c_int32, C.c_double,
+                                   C.c_int32, C.c_int32, C.c_int32, _vp, C.c_int64, _i64p, _i64p, _i32p]),
+    "sfmx_device_count": (C.c_int, []),
+    "sfmx_version": (C.c_char_p, []),
+    "sfmx_last_error": (C.c_char_p, []),
+    "sfmx_selftest_sqrt": (C.c_int, [C.c_int32, C.c_int64, _P(C.c_uint32)]),
+}
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"sfmx native library not found at {LIB_PATH}; build it with "
+            "`make -C sfm-mvs-pipeline_amd` (hipcc, gfx950). There is no CPU fallback.")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in PROTOTYPES.items():
+        if not hasattr(lib, name):
+            continue
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class SfmxError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        msg = (lib.sfmx_last_error() or b"").decode(errors="replace")
+        super().__init__(f"{where}: {ERROR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def check(code: int, where: str) -> int:
+    if code < 0:
+        if code == SFMX_EINVAL:
+            err = SfmxError(code, where)
+            raise ValueError(str(err))   # reference: std::invalid_argument
+        raise SfmxError(code, where)
+    return code

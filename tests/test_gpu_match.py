@@ -1,0 +1,161 @@
+"""GPU parity: the HIP matcher (through the C ABI) against the golden fixtures
+and the oracle, bit-exact (queryIdx, trainIdx, imgIdx, distance bits, order)."""
+import numpy as np
+import pytest
+
+import sfmx
+from sfmx import _lib, synth
+import fixtures
+
+pytestmark = pytest.mark.gpu
+
+
+def run(imgs, pairs, ratio=0.7, distinct=False, min_count=0, norm=None):
+    norm = norm or (sfmx.NORM_L2 if imgs[0].dtype == np.float32 else sfmx.NORM_HAMMING)
+    m = sfmx.BFMatcher(norm)
+    try:
+        m.set_images(imgs)
+        m.run(pairs, ratio, distinct, min_count)
+        out = m.fetch()
+        stats = m.stats()
+    finally:
+        m.close()
+    return out + (stats,)
+
+
+def assert_same(got, off, exp, exp_off):
+    assert np.array_equal(off, exp_off), (off, exp_off)
+    if got.tobytes() != exp.tobytes():
+        bad = np.nonzero(got != exp)[0][:5] if len(got) == len(exp) else []
+        raise AssertionError(f"mismatch at {bad}: got {got[bad] if len(bad) else got[:5]} exp {exp[bad] if len(bad) else exp[:5]}")
+
+
+def test_device_visible():
+    assert _lib.lib.sfmx_device_count() >= 1
+
+
+def test_sqrt_exhaustive():
+    n = 1 << 23                       # covers every SIFT squared distance (< 8,323,201)
+    out = np.zeros(n, np.uint32)
+    _lib.check(_lib.lib.sfmx_selftest_sqrt(0, n, out.ctypes.data_as(_lib.C.POINTER(_lib.C.c_uint32))), "sqrt")
+    ref = np.sqrt(np.arange(n, dtype=np.float32)).view(np.uint32)
+    assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("name", fixtures.desc_sets())
+def test_golden(name):
+    d = fixtures.load(name)
+    m, off, keep, stats = run(d["imgs"], d["pairs"], d["ratio"])
+    assert_same(m, off, d["matches"], d["offsets"])
+    if name.startswith("sift_extreme"):
+        assert stats[0] == 200 + 300          # every query took the exact slow path
+
+
+@pytest.mark.parametrize("distinct", [0, 1])
+def test_filters_golden(distinct):
+    d = fixtures.load("sift_small")
+    f = fixtures.load(f"sift_small_filter_d{distinct}")
+    m, off, keep, _ = run(d["imgs"], d["pairs"], 0.7, distinct, 20)
+    assert_same(m, off, f["matches"], f["offsets"])
+    assert np.array_equal(keep, f["keep"])
+
+
+def test_ragged_sizes_vs_oracle():
+    from oracle import oracle
+    sizes = [1, 31, 33, 64, 255, 257, 511, 513, 1000, 1300]
+    base = synth.sift_images(len(sizes), 1300, seed=21)
+    imgs = [b[:n] for b, n in zip(base, sizes)]
+    pairs = sfmx.pairs_unordered(len(imgs))
+    m, off, _, stats = run(imgs, pairs)
+    em, eoff = oracle.match_pairs(imgs, pairs)
+    assert_same(m, off, em, eoff)
+    assert stats == (0, 0)
+
+
+def test_non_integral_fp32_fallback():
+    from oracle import oracle
+    rng = np.random.default_rng(9)
+    imgs = [rng.random((300, 128), dtype=np.float32) * 50, rng.random((250, 128), dtype=np.float32) * 50,
+            synth.sift_images(1, 200, seed=3)[0]]
+    pairs = sfmx.pairs_unordered(3)
+    m, off, _, stats = run(imgs, pairs)
+    em, eoff = oracle.match_pairs(imgs, pairs)
+    assert_same(m, off, em, eoff)
+    assert stats[1] == 3                      # every pair touches a non-integral image
+
+
+def test_orb_ragged_vs_oracle():
+    from oracle import oracle
+    base = synth.orb_images(5, 1500, seed=31)
+    imgs = [b[:n] for b, n in zip(base, [1500, 1, 700, 513, 256])]
+    pairs = sfmx.pairs_grid(5, 3, 2)
+    m, off, _, _ = run(imgs, pairs)
+    em, eoff = oracle.match_pairs(imgs, pairs)
+    assert_same(m, off, em, eoff)
+
+
+def test_full_size_sift_spot_check_and_determinism():
+    """C2 shape subset: 8 images x 8192 (all 28 pairs on the GPU), 3 pairs re-derived by the
+    oracle; two GPU runs bit-identical; no slow-path / fp32 traffic on SIFT-like data."""
+    from oracle import oracle
+    imgs = synth.sift_images(8, 8192)
+    pairs = sfmx.pairs_unordered(8)
+    m1, off1, _, stats = run(imgs, pairs)
+    m2, off2, _, _ = run(imgs, pairs)
+    assert m1.tobytes() == m2.tobytes() and np.array_equal(off1, off2)
+    assert stats == (0, 0)
+    for p in (0, 13, 27):
+        l, r = pairs[p]
+        exp = oracle.match_pair(imgs[l], imgs[r])
+        assert m1[off1[p]:off1[p + 1]].tobytes() == exp.tobytes()
+    assert off1[-1] > 1000                    # the ratio test accepts planted neighbours
+
+
+def test_full_size_orb_spot_check():
+    from oracle import oracle
+    imgs = synth.orb_images(3, 16384)
+    pairs = np.array([[0, 1], [1, 2]], np.int32)
+    m, off, _, _ = run(imgs, pairs)
+    exp = oracle.match_pair(imgs[0], imgs[1])
+    assert m[off[0]:off[1]].tobytes() == exp.tobytes()
+
+
+def test_match_pairs_oneshot_and_strategy():
+    d = fixtures.load("sift_small")
+    m, off, keep = sfmx.match_pairs(d["imgs"], d["pairs"], n_gpus=1)
+    assert_same(m, off, d["matches"], d["offsets"])
+    scene = sfmx.Scene([sfmx.Shot(f"img{i}", x) for i, x in enumerate(d["imgs"])])
+    matcher = sfmx.BFMatcher(sfmx.NORM_L2)
+    sm = sfmx.UnorderedFeatureMatchingStrategy().calculateShotMatches(scene, matcher)
+    assert [(s.left, s.right) for s in sm] == [tuple(p) for p in d["pairs"]]
+    for p, s in enumerate(sm):
+        assert s.getMatches().tobytes() == d["matches"][d["offsets"][p]:d["offsets"][p + 1]].tobytes()
+        assert s.homographyInlierRatio == -1.0
+    f = fixtures.load("sift_small_filter_d1")
+    kept = sfmx.calculate_shot_matches(scene, sfmx.UnorderedFeatureMatchingStrategy(), matcher, True, 20)
+    assert len(kept) == int(f["keep"].sum())
+
+
+def test_device_resident_inputs():
+    torch = pytest.importorskip("torch")
+    d = fixtures.load("sift_small")
+    ts = [torch.from_numpy(x).cuda() for x in d["imgs"]]
+    m = sfmx.BFMatcher(sfmx.NORM_L2)
+    s = torch.cuda.current_stream().cuda_stream
+    m.set_images_device(ts, stream=s)
+    m.run(d["pairs"], stream=s)
+    got, off, _ = m.fetch(stream=s)
+    m.close()
+    assert_same(got, off, d["matches"], d["offsets"])
+
+
+def test_errors():
+    m = sfmx.BFMatcher(sfmx.NORM_L2)
+    with pytest.raises(ValueError):
+        m.set_images([np.zeros((3, 129), np.float32)])
+    with pytest.raises(_lib.SfmxError):
+        m.run(np.array([[0, 1]]))             # run before set_images -> SFMX_ESTATE
+    m.set_images([np.zeros((3, 128), np.float32)] * 2)
+    with pytest.raises(ValueError):
+        m.run(np.array([[0, 5]]))
+    m.close()

@@ -1,0 +1,100 @@
+"""CPU: the oracle against the golden fixtures, the independent numpy
+restatement and hand-derived known answers (pins the checker itself)."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+import refnp
+import kat
+import fixtures
+from sfmx import synth
+
+
+@pytest.mark.parametrize("name", fixtures.desc_sets())
+def test_oracle_reproduces_golden(name):
+    d = fixtures.load(name)
+    m, off = oracle.match_pairs(d["imgs"], d["pairs"], d["ratio"])
+    assert np.array_equal(off, d["offsets"])
+    assert m.tobytes() == d["matches"].tobytes()
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_oracle_vs_numpy_sift(seed):
+    imgs = synth.sift_images(3, 257 + 31 * seed, seed=100 + seed)
+    for l, r in oracle.pairs_unordered(3):
+        a = oracle.match_pair(imgs[l], imgs[r])
+        b = refnp.match_pair(imgs[l], imgs[r])
+        assert a.tobytes() == b.tobytes()
+
+
+def test_oracle_vs_numpy_orb():
+    imgs = synth.orb_images(3, 300, seed=7)
+    for l, r in oracle.pairs_unordered(3):
+        assert oracle.match_pair(imgs[l], imgs[r]).tobytes() == refnp.match_pair(imgs[l], imgs[r]).tobytes()
+
+
+def test_knn2_tie_break_lowest_index():
+    q, t = kat.sift_ties()
+    idx, dist, nn = oracle.knn2(q, t)
+    assert nn == 2
+    assert idx[0].tolist() == [3, 7]          # duplicate rows 3, 7, 20: lowest two, in order
+    assert dist[0].tolist() == [0.0, 0.0]
+
+
+def test_knn2_ranks_on_float_sqrt_bits():
+    q, t = kat.sift_sqrt_collision()
+    idx, dist, _ = oracle.knn2(q, t)
+    # rows 1 (s=4197201) and 2 (s=4197200) have equal sqrtf: lower index first
+    assert idx[0].tolist() == [1, 2]
+    assert dist[0, 0] == dist[0, 1]
+
+
+def test_first_sqrt_collision():
+    assert oracle.first_sqrt_collision(1 << 23) == 4197201
+
+
+def test_ratio_boundary_double_compare():
+    for q, t in kat.sift_ratio_boundary():
+        m = oracle.match_pair(q, t)
+        idx, dist, _ = oracle.knn2(q, t)
+        expect = float(dist[0, 0]) < float(dist[0, 1]) * 0.7
+        assert (len(m) == 1) == expect
+
+
+def test_single_and_empty_train():
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 256, (9, 128)).astype(np.float32)
+    m1 = oracle.match_pair(a, a[:1])
+    assert len(m1) == 9 and (m1["trainIdx"] == 0).all()          # <2 neighbours: accepted
+    assert len(oracle.match_pair(a, a[:0])) == 0                  # empty train: nothing
+    assert len(oracle.match_pair(a[:0], a)) == 0
+
+
+def test_filters_golden():
+    d = fixtures.load("sift_small")
+    for distinct in (0, 1):
+        f = fixtures.load(f"sift_small_filter_d{distinct}")
+        m, off, keep = oracle.filter_matches(d["matches"], d["offsets"], distinct, 20)
+        assert m.tobytes() == f["matches"].tobytes() and np.array_equal(off, f["offsets"])
+        assert np.array_equal(keep, f["keep"])
+
+
+def test_distinct_filter_semantics():
+    dt = oracle.DMATCH_DTYPE
+    m = np.array([(0, 5, 0, 1.0), (1, 5, 0, 2.0), (2, 6, 0, 3.0), (3, 7, 0, 4.0), (4, 7, 0, 1.0)], dt)
+    fm, off, keep = oracle.filter_matches(m, np.array([0, 5]), True, 1)
+    assert fm["queryIdx"].tolist() == [2] and keep.tolist() == [1]
+    fm, off, keep = oracle.filter_matches(m, np.array([0, 5]), False, 6)
+    assert keep.tolist() == [0]                                   # 5 < 6 -> dropped (strict '<')
+
+
+def test_pairs_golden_and_doc():
+    p = fixtures.load("pairs")
+    assert np.array_equal(oracle.pairs_unordered(7), p["unordered7"])
+    assert np.array_equal(oracle.pairs_video(10, 3), p["video10_3"])
+    assert np.array_equal(oracle.pairs_grid(200, 3, 20), p["grid200_3_20"])
+    assert len(p["grid200_3_20"]) == 881
+    g = oracle.pairs_grid(20, 3, 5)
+    # GridFeatureMatchingStrategy.h:31-37 example (image 01 = index 0), in loop order
+    assert [tuple(x) for x in g if x[0] == 0] == [(0, 1), (0, 2), (0, 5), (0, 6), (0, 10)]
+    assert len(oracle.pairs_grid(23, 3, 5, 0)) == len(oracle.pairs_grid(20, 3, 5, 1))
