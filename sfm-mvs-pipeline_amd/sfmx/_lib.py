@@ -60,7 +60,22 @@ PROTOTYPES = {
 }
 
 
+def _bind_runtime_like_torch() -> None:
+    """PyTorch-ROCm bundles its own libamdhip64 (SONAME libamdhip64.so.7).  If
+    libsfmx is loaded first, the system ROCm runtime is mapped and torch later
+    maps a second copy (and sees no GPU).  Importing torch first makes
+    libsfmx's DT_NEEDED resolve to torch's already-loaded runtime, so device
+    pointers and streams can be shared.  Set SFMX_NO_TORCH=1 to skip."""
+    if os.environ.get("SFMX_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def _load() -> C.CDLL:
+    _bind_runtime_like_torch()
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"sfmx native library not found at {LIB_PATH}; build it with "
