@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <climits>
+#include <cstdlib>
 #include "match_common.hpp"
 
 namespace sfmx {
@@ -51,6 +52,18 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #define LDS_AS __attribute__((address_space(3)))
 
 __device__ __forceinline__ int med3i(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
+// Explicit v_med3_i32 / v_max3_i32: hipcc only pattern-matches med3 from some
+// min/max shapes; in the pairwise top-2 update it otherwise emits 4 ops.
+__device__ __forceinline__ int v_med3(int a, int b, int c) {
+    int d;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ int v_max3(int a, int b, int c) {
+    int d;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
 __device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned c) { return max(min(a, b), min(max(a, b), c)); }
 
 // Correctly rounded sqrtf of an exact integer < 2^24: the double sqrt is
@@ -122,17 +135,19 @@ __global__ void prep_hamming_kernel(const uint8_t* __restrict__ src, int rows, i
 
 // ---------------------------------------------------------------------------
 // SIFT 2-NN, int8 MFMA.
-template <int QT, int WAVES>
-__global__ __launch_bounds__(WAVES * 64, 2)
+template <int QT, int WAVES, int MINW, int STAGE, bool MFMA_FIRST>
+__global__ __launch_bounds__(WAVES * 64, MINW)
 void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
                       const ImgDev* __restrict__ imgs, const int8_t* __restrict__ desc8,
                       const int32_t* __restrict__ norm, const int32_t* __restrict__ keyc,
                       int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
                       int2* __restrict__ slow_list, int32_t* __restrict__ slow_count, double ratio) {
-    static_assert(WAVES * 64 * 16 == 64 * SIFT_DIM, "one 16-B glds per thread fills a 64-row stage");
-    constexpr int STAGE = 64;
-    constexpr int DESC_BYTES = STAGE * SIFT_DIM;           // 8 KiB
+    constexpr int GLDS = STAGE * SIFT_DIM / (WAVES * 64 * 16);   // 16-B LDS-DMA pieces per thread per stage
+    static_assert(GLDS * WAVES * 64 * 16 == STAGE * SIFT_DIM, "stage must split into whole 16-B pieces");
+    static_assert(256 % STAGE == 0, "stages tile the 256-row key chunk");
+    constexpr int DESC_BYTES = STAGE * SIFT_DIM;
     constexpr int BUF_BYTES = DESC_BYTES + STAGE * 4;      // + keys
+    constexpr int SPC = 256 / STAGE;                       // stages per key chunk
     __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
 
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
@@ -163,13 +178,29 @@ void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restri
 
     auto stage = [&](int s, int buf) {
         char* base = lds + buf * BUF_BYTES;
-        const int p = threadIdx.x;                   // 16-byte unit index in the stage
-        const int rr = p >> 3, slot = p & 7, c = slot ^ ((rr >> 1) & 7);
-        const int8_t* g = tbase + (int64_t)(s * STAGE + rr) * SIFT_DIM + 16 * c;
-        __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)g, (LDS_AS void*)(base + wid * 1024), 16, 0, 0);
-        if (wid == 0)
-            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(kbase + s * STAGE + lane),
-                                             (LDS_AS void*)(base + DESC_BYTES), 4, 0, 0);
+#pragma unroll
+        for (int i = 0; i < GLDS; ++i) {
+            const int p = i * WAVES * 64 + threadIdx.x;  // 16-byte unit index in the stage
+            const int rr = p >> 3, slot = p & 7, c = slot ^ ((rr >> 1) & 7);
+            const int8_t* g = tbase + (int64_t)(s * STAGE + rr) * SIFT_DIM + 16 * c;
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)g,
+                                             (LDS_AS void*)(base + (i * WAVES + wid) * 1024), 16, 0, 0);
+        }
+        if (wid < STAGE / 64)
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(kbase + s * STAGE + wid * 64 + lane),
+                                             (LDS_AS void*)(base + DESC_BYTES + wid * 256), 4, 0, 0);
+    };
+
+    // Top-2 by max over packed keys, two new keys per step:
+    //   b2' = max(med3(b1, ka, kb), b2),  b1' = max3(b1, ka, kb)   (1.5 VALU per element)
+    auto select = [&](const i32x16& acc, const i32x4 (&kv)[4], int& b1, int& b2) {
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+            const int ka = (int)(((unsigned)acc[r] << 9) + (unsigned)kv[r >> 2][r & 3]);
+            const int kb = (int)(((unsigned)acc[r + 1] << 9) + (unsigned)kv[r >> 2][(r + 1) & 3]);
+            b2 = max(v_med3(b1, ka, kb), b2);
+            b1 = v_max3(b1, ka, kb);
+        }
     };
 
     if (nstages > 0) stage(0, 0);
@@ -193,23 +224,28 @@ void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restri
 #pragma unroll
             for (int g = 0; g < 4; ++g)
                 kv[g] = *reinterpret_cast<const i32x4*>(base + DESC_BYTES + 4 * (t * 32 + 8 * g + 4 * h));
+            if constexpr (MFMA_FIRST) {
+                i32x16 acc[QT];
 #pragma unroll
-            for (int qt = 0; qt < QT; ++qt) {
-                i32x16 acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+                for (int qt = 0; qt < QT; ++qt) {
+                    acc[qt] = i32x16{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-                for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bq[qt][m], acc, 0, 0, 0);
-                int b1 = c1[qt], b2 = c2[qt];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int key = (int)(((unsigned)acc[r] << 9) + (unsigned)kv[r >> 2][r & 3]);
-                    b2 = med3i(b1, b2, key);
-                    b1 = max(b1, key);
+                    for (int m = 0; m < 4; ++m) acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bq[qt][m], acc[qt], 0, 0, 0);
                 }
-                c1[qt] = b1; c2[qt] = b2;
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) select(acc[qt], kv, c1[qt], c2[qt]);
+            } else {
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+                    i32x16 acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bq[qt][m], acc, 0, 0, 0);
+                    select(acc, kv, c1[qt], c2[qt]);
+                }
             }
         }
-        if ((s & 3) == 3 || s + 1 == nstages) {      // end of a 256-row chunk
-            const int cb = (s >> 2) * 256;
+        if ((s % SPC) == SPC - 1 || s + 1 == nstages) {      // end of a 256-row chunk
+            const int cb = (s / SPC) * 256;
 #pragma unroll
             for (int qt = 0; qt < QT; ++qt) {
                 const int p1 = __shfl_xor(c1[qt], 32), p2 = __shfl_xor(c2[qt], 32);
@@ -558,15 +594,32 @@ hipError_t launch_prep_hamming(const uint8_t* src, int rows, int cols, int rows_
     return hipGetLastError();
 }
 
-constexpr int SIFT_QT = 2, SIFT_WAVES = 8;
-static_assert(SIFT_QT * SIFT_WAVES * 32 == ROW_ALIGN, "work item = ROW_ALIGN queries");
+// Kernel variants (queries per block = QT * WAVES * 32, must divide ROW_ALIGN).
+// Selected by sift_variant(); SFMX_SIFT_VARIANT overrides (tuning only).
+int sift_variant() {
+    static int v = [] {
+        const char* e = getenv("SFMX_SIFT_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+int sift_block_queries(int v) { return v == 2 || v == 4 ? 256 : 512; }
+
+#define SIFT_LAUNCH(QT, W, MINW, ST, MF)                                                                  \
+    sift_knn2_kernel<QT, W, MINW, ST, MF><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc,   \
+                                                                     out_idx, out_dist, slow_list, slow_count, ratio)
 
 hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
                             const int8_t* desc8, const int32_t* norm, const int32_t* keyc, int32_t* out_idx,
                             float* out_dist, int2* slow_list, int32_t* slow_count, double ratio, hipStream_t st) {
     if (n_work == 0) return hipSuccess;
-    sift_knn2_kernel<SIFT_QT, SIFT_WAVES><<<n_work, SIFT_WAVES * 64, 0, st>>>(
-        work, pairs, imgs, desc8, norm, keyc, out_idx, out_dist, slow_list, slow_count, ratio);
+    switch (sift_variant()) {
+    case 1: SIFT_LAUNCH(2, 8, 2, 128, false); break;
+    case 2: SIFT_LAUNCH(2, 4, 3, 64, true); break;
+    case 3: SIFT_LAUNCH(2, 8, 2, 64, false); break;
+    case 4: SIFT_LAUNCH(2, 4, 4, 128, false); break;
+    default: SIFT_LAUNCH(2, 8, 2, 64, true);   // measured best (r01 tuning, profiles/r01_*)
+    }
     return hipGetLastError();
 }
 hipError_t launch_sift_slow(const int2* slow_list, const int32_t* slow_count, const PairDev* pairs,

@@ -39,6 +39,8 @@ hipError_t launch_sift_f32(const WorkItem*, int, const PairDev*, const ImgDev*, 
 hipError_t launch_orb_knn2(const WorkItem*, int, const PairDev*, const ImgDev*, const uint8_t*, int32_t*, float*,
                            double, hipStream_t);
 hipError_t launch_selftest_sqrt(int64_t, uint32_t*, hipStream_t);
+int sift_variant();
+int sift_block_queries(int variant);
 hipError_t launch_assemble(const PairDev*, int, const ImgDev*, const int32_t*, const float*, int, int, int,
                            int64_t*, int32_t*, int64_t*, DMatchDev*, hipStream_t);
 }  // namespace sfmx
@@ -240,7 +242,8 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
         const ImgDev& R = m->imgs[pd[p].right];
         const bool f32path = m->norm == SFMX_NORM_L2 && !(L.integral && R.integral);
         m->fp32_pairs += f32path;
-        for (int q0 = 0; q0 < L.rows; q0 += ROW_ALIGN) (f32path ? work32 : work).push_back(WorkItem{p, q0});
+        const int bq = f32path ? 512 : (m->norm == SFMX_NORM_L2 ? sift_block_queries(sift_variant()) : 512);
+        for (int q0 = 0; q0 < L.rows; q0 += bq) (f32path ? work32 : work).push_back(WorkItem{p, q0});
     }
     int rc;
     if ((rc = m->pairs_d.ensure(sizeof(PairDev) * std::max(n_pairs, 1)))) return rc;
