@@ -1,0 +1,129 @@
+/* SPDX-License-Identifier: MIT
+ *
+ * sfmx bundle adjustment — C ABI.
+ *
+ * Replaces, for the reference (brunothg/sfm-mvs-pipeline, paths under src/photogrammetrie):
+ *   - BundleAdjustment::doBundleAdjustment(Scene&)                 common/BundleAdjustment.h:97
+ *     (problem build :29-91, write-back :97-138)
+ *   - CeresUtils::solve(ceres::Problem&, ceres::Solver::Summary&)  util/CeresUtils.h:69, .cpp:38-56
+ *     with DENSE_SCHUR, max_num_iterations = 5000 and Ceres 1.14 defaults otherwise
+ *   - the three AutoDiff reprojection functors                      common/SimpleRadialCamera.cpp:69-124,
+ *                                                                   common/SimpleCamera.cpp:63-112,
+ *                                                                   common/DistortionCamera.cpp:62-117
+ * The parameter-block layout is the reference's Ceres problem layout:
+ *   point double[3] (CeresPCE::coordinates, BundleAdjustment.h:28-45),
+ *   pose  double[6] = angle-axis + translation (CeresCameraShot::pose, :47-64),
+ *   ONE intrinsics block double[k] shared by all shots (ICamera::ceresCameraParameters, ICamera.h:171):
+ *     SIMPLE k=1 [f], SIMPLE_RADIAL k=3 [f,k1,k2], DISTORTION k=7 [f,cx,cy,k1,k2,p1,p2].
+ * One residual block (2 residuals) per observation, squared loss, no
+ * constant blocks (BundleAdjustment.cpp:83-89).
+ */
+#ifndef SFMX_BA_H
+#define SFMX_BA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { SFMX_CAM_SIMPLE = 1, SFMX_CAM_SIMPLE_RADIAL = 3, SFMX_CAM_DISTORTION = 7 };   /* value = k */
+/* ceres::TerminationType subset */
+enum { SFMX_BA_CONVERGENCE = 0, SFMX_BA_NO_CONVERGENCE = 1, SFMX_BA_FAILURE = 2 };
+
+typedef struct sfmx_ba_problem {
+    int32_t n_points, n_cams, n_obs, cam_model;   /* cam_model = SFMX_CAM_* */
+    double* points;                 /* 3*n_points, in/out                                      */
+    double* poses;                  /* 6*n_cams (angle-axis rx,ry,rz, tx,ty,tz), in/out        */
+    double* intr;                   /* k, in/out (shared intrinsics block)                     */
+    const int32_t* obs_point;       /* n_obs                                                   */
+    const int32_t* obs_cam;         /* n_obs                                                   */
+    const double* obs_xy;           /* 2*n_obs observed pixel (cv::Point2f promoted to double) */
+    double cx, cy;                  /* principal point, SIMPLE / SIMPLE_RADIAL only
+                                       (per-residual constant, SimpleRadialCamera.cpp:118-124) */
+} sfmx_ba_problem;
+
+typedef struct sfmx_ba_options {     /* defaults = CeresUtils::defaultOptions + Ceres 1.14 */
+    int32_t max_num_iterations;              /* 5000 (CeresUtils.cpp:45)  */
+    int32_t max_num_consecutive_invalid_steps;/* 5                        */
+    int32_t jacobi_scaling;                  /* 1                         */
+    int32_t device;                          /* HIP device index          */
+    double function_tolerance;               /* 1e-6  */
+    double gradient_tolerance;               /* 1e-10 */
+    double parameter_tolerance;              /* 1e-8  */
+    double initial_trust_region_radius;      /* 1e4   */
+    double max_trust_region_radius;          /* 1e16  */
+    double min_trust_region_radius;          /* 1e-32 */
+    double min_lm_diagonal;                  /* 1e-6  */
+    double max_lm_diagonal;                  /* 1e32  */
+    double min_relative_decrease;            /* 1e-3  */
+} sfmx_ba_options;
+
+typedef struct sfmx_ba_summary {
+    double initial_cost, final_cost;         /* 1/2 sum ||r||^2 (Ceres convention) */
+    int32_t num_successful_steps;            /* Ceres counting: iteration 0 counts as successful */
+    int32_t num_unsuccessful_steps;
+    int32_t num_invalid_steps;
+    int32_t termination_type;                /* SFMX_BA_* */
+    double total_ms;                         /* minimizer wall time */
+    double ms_per_iteration;                 /* total_ms / (successful + unsuccessful) */
+    double final_gradient_max_norm;
+    double final_radius;
+} sfmx_ba_summary;
+
+int sfmx_ba_default_options(sfmx_ba_options* opt);
+
+/* Solve in place (the reference's doBundleAdjustment + write-back).  trace
+ * (optional) receives 3 doubles per iteration: cost, trust-region radius,
+ * step accepted (1/0); returns the number of trace rows written (>= 0) or a
+ * negative SFMX_E* code. */
+int sfmx_ba_solve(sfmx_ba_problem* problem, const sfmx_ba_options* opt, sfmx_ba_summary* summary,
+                  double* trace, int32_t trace_cap);
+
+/* ---- context API (bench / multi-GPU) --------------------------------------
+ * A context keeps the problem resident in HBM.  For point-sharded multi-GPU
+ * BA every rank creates a context over ITS points' observations (all cameras
+ * and the intrinsics replicated) and installs an all-reduce callback; the
+ * solver calls it once per linear solve on the reduced camera system and
+ * gradient (device buffer of `count` doubles, sum across ranks), on the
+ * camera/intrinsics column norms once per linearization, and on a few scalars
+ * per iteration.  Residual costs and the point part of every norm are summed
+ * over ranks; camera and intrinsics parameters are replicated.  Without a callback the context is single-GPU. */
+typedef struct sfmx_ba_ctx sfmx_ba_ctx;
+/* op: SFMX_REDUCE_SUM or SFMX_REDUCE_MAX; in place on a device buffer of this
+ * context's device, ordered on `stream`; returns 0 on success. */
+enum { SFMX_REDUCE_SUM = 0, SFMX_REDUCE_MAX = 1 };
+typedef int (*sfmx_allreduce_fn)(double* device_buf, int64_t count, int32_t op, void* user, void* stream);
+
+int sfmx_ba_create(const sfmx_ba_problem* problem, const sfmx_ba_options* opt, sfmx_ba_ctx** out);
+int sfmx_ba_set_allreduce(sfmx_ba_ctx* ctx, sfmx_allreduce_fn fn, void* user);
+/* Run the LM minimizer from the context's current parameters for at most
+ * max_iterations iterations (<= 0: options.max_num_iterations). */
+int sfmx_ba_run(sfmx_ba_ctx* ctx, int32_t max_iterations, sfmx_ba_summary* summary,
+                double* trace, int32_t trace_cap);
+/* Copy the current parameters back into problem->points/poses/intr. */
+int sfmx_ba_get(sfmx_ba_ctx* ctx, sfmx_ba_problem* problem);
+/* Reset the parameters from problem->points/poses/intr (same topology). */
+int sfmx_ba_set(sfmx_ba_ctx* ctx, const sfmx_ba_problem* problem);
+/* Per-phase device time of the last run (ms, summed over its iterations):
+ * [0] linearize (residuals + Jacobians), [1] Schur assembly, [2] Cholesky + solves,
+ * [3] step / candidate cost.  n = number of entries written. */
+int sfmx_ba_phase_ms(sfmx_ba_ctx* ctx, double* ms, int32_t n);
+int sfmx_ba_destroy(sfmx_ba_ctx* ctx);
+
+/* Residuals and Jacobian blocks (device-computed) of every observation at the
+ * problem's current parameters: r[2*O], Je[6*O] (d r / d point, row-major 2x3),
+ * Jc[12*O] (2x6 pose), Ji[2*k*O] (2xk intrinsics).  For the autodiff tests. */
+int sfmx_ba_jacobian(const sfmx_ba_problem* problem, int32_t device, double* r, double* Je, double* Jc,
+                     double* Ji);
+
+/* Pose conversions of CeresUtils (util/CeresUtils.h:90-148): 3x4 [R|t]
+ * row-major <-> Ceres pose {angle-axis, t}, via ceres::RotationMatrixToAngleAxis /
+ * AngleAxisToRotationMatrix semantics.  Host-side. */
+int sfmx_pose_to_ceres(const double* Rt12, double* pose6);
+int sfmx_pose_from_ceres(const double* pose6, double* Rt12);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SFMX_BA_H */

@@ -97,8 +97,8 @@ void angle_axis_rotate_point(const T aa[3], const T pt[3], T result[3]) {
 enum { CAM_SIMPLE = 1, CAM_SIMPLE_RADIAL = 3, CAM_DISTORTION = 7 };
 
 // The reference functors (operator() bodies restated, same operation order).
-template <typename T>
-void residual(int model, const T* X, const T* pose, const T* intr, double ox, double oy, double cx, double cy, T* res) {
+template <int K, typename T>
+void residual(const T* X, const T* pose, const T* intr, double ox, double oy, double cx, double cy, T* res) {
     T p[3];
     angle_axis_rotate_point(pose, X, p);
     p[0] = p[0] + pose[3]; p[1] = p[1] + pose[4]; p[2] = p[2] + pose[5];
@@ -107,10 +107,10 @@ void residual(int model, const T* X, const T* pose, const T* intr, double ox, do
     const T& focal = intr[0];
     const T xd = focal * xp;
     const T yd = focal * yp;
-    if (model == CAM_SIMPLE) {
+    if constexpr (K == CAM_SIMPLE) {
         res[0] = xd - T(ox - cx);
         res[1] = yd - T(oy - cy);
-    } else if (model == CAM_SIMPLE_RADIAL) {
+    } else if constexpr (K == CAM_SIMPLE_RADIAL) {
         const T& k1 = intr[1]; const T& k2 = intr[2];
         const T r2 = (xp * xp) + (yp * yp);
         const T r4 = r2 * r2;
@@ -130,14 +130,14 @@ void residual(int model, const T* X, const T* pose, const T* intr, double ox, do
 }
 
 template <int K>
-void eval_jet(int model, const double* X, const double* pose, const double* intr, double ox, double oy, double cx,
+void eval_jet(const double* X, const double* pose, const double* intr, double ox, double oy, double cx,
               double cy, double* r, double* Je, double* Jc, double* Ji) {
     constexpr int N = 9 + K;
     Jet<N> x[3], ps[6], in[K], res[2];
     for (int i = 0; i < 3; ++i) x[i] = Jet<N>(X[i], i);
     for (int i = 0; i < 6; ++i) ps[i] = Jet<N>(pose[i], 3 + i);
     for (int i = 0; i < K; ++i) in[i] = Jet<N>(intr[i], 9 + i);
-    residual(model, x, ps, in, ox, oy, cx, cy, res);
+    residual<K>(x, ps, in, ox, oy, cx, cy, res);
     for (int j = 0; j < 2; ++j) {
         r[j] = res[j].a;
         for (int i = 0; i < 3; ++i) Je[j * 3 + i] = res[j].v[i];
@@ -166,8 +166,12 @@ double eval_cost(const Problem& pb, const double* x) {
     #pragma omp parallel for reduction(+ : cost) schedule(static)
     for (int o = 0; o < pb.O; ++o) {
         double res[2];
-        residual<double>(pb.model, pts + 3 * (size_t)pb.obs_point[o], poses + 6 * (size_t)pb.obs_cam[o], intr,
-                         pb.obs_xy[2 * o], pb.obs_xy[2 * o + 1], pb.cx, pb.cy, res);
+        const double* X = pts + 3 * (size_t)pb.obs_point[o];
+        const double* ps = poses + 6 * (size_t)pb.obs_cam[o];
+        const double ox = pb.obs_xy[2 * o], oy = pb.obs_xy[2 * o + 1];
+        if (pb.k == 1) residual<1>(X, ps, intr, ox, oy, pb.cx, pb.cy, res);
+        else if (pb.k == 3) residual<3>(X, ps, intr, ox, oy, pb.cx, pb.cy, res);
+        else residual<7>(X, ps, intr, ox, oy, pb.cx, pb.cy, res);
         cost += res[0] * res[0] + res[1] * res[1];
     }
     return 0.5 * cost;
@@ -189,9 +193,9 @@ double linearize(const Problem& pb, const double* x, Lin& L) {
         double* Jc = &L.Jc[12 * (size_t)o];
         double* Ji = &L.Ji[2 * (size_t)k * o];
         const double ox = pb.obs_xy[2 * o], oy = pb.obs_xy[2 * o + 1];
-        if (k == 1) eval_jet<1>(pb.model, X, ps, intr, ox, oy, pb.cx, pb.cy, r, Je, Jc, Ji);
-        else if (k == 3) eval_jet<3>(pb.model, X, ps, intr, ox, oy, pb.cx, pb.cy, r, Je, Jc, Ji);
-        else eval_jet<7>(pb.model, X, ps, intr, ox, oy, pb.cx, pb.cy, r, Je, Jc, Ji);
+        if (k == 1) eval_jet<1>(X, ps, intr, ox, oy, pb.cx, pb.cy, r, Je, Jc, Ji);
+        else if (k == 3) eval_jet<3>(X, ps, intr, ox, oy, pb.cx, pb.cy, r, Je, Jc, Ji);
+        else eval_jet<7>(X, ps, intr, ox, oy, pb.cx, pb.cy, r, Je, Jc, Ji);
         cost += r[0] * r[0] + r[1] * r[1];
     }
     return 0.5 * cost;

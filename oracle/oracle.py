@@ -147,3 +147,87 @@ def pairs_grid(n, seq, row_len, mode=1):
 
 def first_sqrt_collision(limit: int = 1 << 24) -> int:
     return int(lib.orc_first_sqrt_collision(limit))
+
+
+# ---- bundle adjustment (oracle/ba_oracle.cpp) --------------------------------
+
+class _BAProblem(C.Structure):
+    _fields_ = [("n_points", C.c_int32), ("n_cams", C.c_int32), ("n_obs", C.c_int32), ("cam_model", C.c_int32),
+                ("points", C.c_void_p), ("poses", C.c_void_p), ("intr", C.c_void_p),
+                ("obs_point", C.c_void_p), ("obs_cam", C.c_void_p), ("obs_xy", C.c_void_p),
+                ("cx", C.c_double), ("cy", C.c_double)]
+
+
+class _BAOptions(C.Structure):
+    _fields_ = [("max_num_iterations", C.c_int32), ("max_num_consecutive_invalid_steps", C.c_int32),
+                ("jacobi_scaling", C.c_int32), ("device", C.c_int32),
+                ("function_tolerance", C.c_double), ("gradient_tolerance", C.c_double),
+                ("parameter_tolerance", C.c_double), ("initial_trust_region_radius", C.c_double),
+                ("max_trust_region_radius", C.c_double), ("min_trust_region_radius", C.c_double),
+                ("min_lm_diagonal", C.c_double), ("max_lm_diagonal", C.c_double),
+                ("min_relative_decrease", C.c_double)]
+
+
+class _BASummary(C.Structure):
+    _fields_ = [("initial_cost", C.c_double), ("final_cost", C.c_double),
+                ("num_successful_steps", C.c_int32), ("num_unsuccessful_steps", C.c_int32),
+                ("num_invalid_steps", C.c_int32), ("termination_type", C.c_int32),
+                ("total_ms", C.c_double), ("ms_per_iteration", C.c_double),
+                ("final_gradient_max_norm", C.c_double), ("final_radius", C.c_double)]
+
+
+CERES_DEFAULTS = dict(max_num_iterations=5000, max_num_consecutive_invalid_steps=5, jacobi_scaling=1, device=0,
+                      function_tolerance=1e-6, gradient_tolerance=1e-10, parameter_tolerance=1e-8,
+                      initial_trust_region_radius=1e4, max_trust_region_radius=1e16, min_trust_region_radius=1e-32,
+                      min_lm_diagonal=1e-6, max_lm_diagonal=1e32, min_relative_decrease=1e-3)
+
+lib.orc_ba_solve.argtypes = [C.POINTER(_BAProblem), C.POINTER(_BAOptions), C.POINTER(_BASummary), C.c_void_p,
+                             C.c_int, C.c_int]
+lib.orc_ba_cost.restype = C.c_double
+lib.orc_ba_cost.argtypes = [C.POINTER(_BAProblem)]
+lib.orc_ba_jacobian.argtypes = [C.POINTER(_BAProblem), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+
+
+def _ba_struct(p: dict):
+    keep = {
+        "points": np.ascontiguousarray(p["points"], np.float64).reshape(-1, 3),
+        "poses": np.ascontiguousarray(p["poses"], np.float64).reshape(-1, 6),
+        "intr": np.ascontiguousarray(p["intr"], np.float64).reshape(-1),
+        "obs_point": np.ascontiguousarray(p["obs_point"], np.int32).reshape(-1),
+        "obs_cam": np.ascontiguousarray(p["obs_cam"], np.int32).reshape(-1),
+        "obs_xy": np.ascontiguousarray(p["obs_xy"], np.float64).reshape(-1, 2),
+    }
+    s = _BAProblem(len(keep["points"]), len(keep["poses"]), len(keep["obs_point"]), int(p["cam_model"]),
+                   keep["points"].ctypes.data, keep["poses"].ctypes.data, keep["intr"].ctypes.data,
+                   keep["obs_point"].ctypes.data, keep["obs_cam"].ctypes.data, keep["obs_xy"].ctypes.data,
+                   float(p.get("cx", 0.0)), float(p.get("cy", 0.0)))
+    return s, keep
+
+
+def ba_cost(p: dict) -> float:
+    s, keep = _ba_struct(p)
+    return float(lib.orc_ba_cost(C.byref(s)))
+
+
+def ba_jacobian(p: dict):
+    s, keep = _ba_struct(p)
+    O, k = len(keep["obs_point"]), int(p["cam_model"])
+    r = np.zeros((O, 2)); Je = np.zeros((O, 2, 3)); Jc = np.zeros((O, 2, 6)); Ji = np.zeros((O, 2, k))
+    lib.orc_ba_jacobian(C.byref(s), r.ctypes.data, Je.ctypes.data, Jc.ctypes.data, Ji.ctypes.data)
+    return r, Je, Jc, Ji
+
+
+def ba_solve(p: dict, nthreads: int = 0, trace_cap: int = 0, **options):
+    """LM + DENSE_SCHUR restatement of Ceres 1.14 -> (solution dict, summary dict, trace[n,3])."""
+    s, keep = _ba_struct(p)
+    o = dict(CERES_DEFAULTS)
+    o.update(options)
+    opt = _BAOptions(**o)
+    sm = _BASummary()
+    tr = np.zeros((max(trace_cap, 1), 3))
+    n = lib.orc_ba_solve(C.byref(s), C.byref(opt), C.byref(sm), tr.ctypes.data if trace_cap else None, trace_cap,
+                         nthreads)
+    summary = {f: getattr(sm, f) for f, _ in sm._fields_}
+    sol = dict(p)
+    sol.update(points=keep["points"], poses=keep["poses"], intr=keep["intr"])
+    return sol, summary, tr[:max(n, 0)]

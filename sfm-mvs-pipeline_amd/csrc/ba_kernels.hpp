@@ -1,0 +1,909 @@
+// SPDX-License-Identifier: MIT
+// sfmx bundle adjustment kernels for gfx950 (MI355X / CDNA4), fp64.
+//
+// One Levenberg-Marquardt iteration of the reference's Ceres problem
+// (BundleAdjustment.cpp:29-91 solved by CeresUtils::solve, DENSE_SCHUR):
+//   ba_linearize      residual + Jacobian of every observation by forward-mode
+//                     dual numbers (what ceres::AutoDiffCostFunction does for the
+//                     reference functors SimpleRadialCamera.cpp:79-115,
+//                     SimpleCamera.cpp:73-103, DistortionCamera.cpp:72-110)
+//   column kernels    J^T r and squared column norms (Jacobi scaling, LM diagonal)
+//   ba_point_blocks   per 3-dof point block: E = Je^T Je + D_e^2, E^-1, and the
+//                     per-observation factors the Schur complement needs
+//   ba_cam_blocks     per camera: pose-pose diagonal, pose-intrinsics coupling, rhs
+//   ba_pair_blocks    per co-visible camera pair: -sum W_a^T E^-1 W_b, one
+//                     workgroup per 6x6 block, fixed-order tree sums (deterministic)
+//   ba_assemble       dense reduced camera system S ((6C+k) padded to 64)
+//   chol_*            blocked right-looking Cholesky (64x64 tiles) + triangular solves
+//   ba_backsub / ba_step / ba_model / ba_cost
+// Layout in HBM: parameters x = [points 3P | poses 6C | intrinsics k]; the
+// Jacobian is stored field-major J[f][o] (f = r0,r1, Je 2x3, Jc 2x6, Ji 2xk) so
+// observation-parallel kernels read and write coalesced.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cfloat>
+
+namespace sfmx {
+namespace ba {
+
+constexpr int NB = 64;   // Cholesky tile
+
+// ---- dual numbers --------------------------------------------------------
+template <int N>
+struct DJet {
+    double a;
+    double v[N];
+};
+template <int N> __device__ __forceinline__ DJet<N> jconst(double x) { DJet<N> r; r.a = x;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = 0.0; return r; }
+template <int N> __device__ __forceinline__ DJet<N> jvar(double x, int k) { DJet<N> r = jconst<N>(x);
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = (i == k) ? 1.0 : 0.0; return r; }
+template <int N> __device__ __forceinline__ DJet<N> operator+(const DJet<N>& f, const DJet<N>& g) { DJet<N> r; r.a = f.a + g.a;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = f.v[i] + g.v[i]; return r; }
+template <int N> __device__ __forceinline__ DJet<N> operator-(const DJet<N>& f, const DJet<N>& g) { DJet<N> r; r.a = f.a - g.a;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = f.v[i] - g.v[i]; return r; }
+template <int N> __device__ __forceinline__ DJet<N> operator*(const DJet<N>& f, const DJet<N>& g) { DJet<N> r; r.a = f.a * g.a;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = f.a * g.v[i] + f.v[i] * g.a; return r; }
+template <int N> __device__ __forceinline__ DJet<N> operator*(double s, const DJet<N>& f) { DJet<N> r; r.a = s * f.a;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = s * f.v[i]; return r; }
+template <int N> __device__ __forceinline__ DJet<N> operator/(const DJet<N>& f, const DJet<N>& g) {
+    const double gi = 1.0 / g.a, fg = f.a * gi;
+    DJet<N> r; r.a = f.a * gi;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = (f.v[i] - fg * g.v[i]) * gi;
+    return r;
+}
+template <int N> __device__ __forceinline__ DJet<N> jsqrt(const DJet<N>& f) {
+    const double s = sqrt(f.a), t = 1.0 / (2.0 * s);
+    DJet<N> r; r.a = s;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = t * f.v[i]; return r;
+}
+template <int N> __device__ __forceinline__ void jsincos(const DJet<N>& f, DJet<N>& sn, DJet<N>& cs) {
+    double s, c;
+    sincos(f.a, &s, &c);
+    sn.a = s; cs.a = c;
+#pragma unroll
+    for (int i = 0; i < N; ++i) { sn.v[i] = c * f.v[i]; cs.v[i] = -s * f.v[i]; }
+}
+
+// ceres::AngleAxisRotatePoint (Ceres 1.14 rotation.h) on dual numbers.
+template <int N>
+__device__ __forceinline__ void rotate(const DJet<N> aa[3], const DJet<N> pt[3], DJet<N> res[3]) {
+    const DJet<N> theta2 = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
+    if (theta2.a > DBL_EPSILON) {
+        const DJet<N> theta = jsqrt(theta2);
+        DJet<N> st, ct;
+        jsincos(theta, st, ct);
+        const DJet<N> ti = jconst<N>(1.0) / theta;
+        const DJet<N> w[3] = {aa[0] * ti, aa[1] * ti, aa[2] * ti};
+        const DJet<N> wx[3] = {w[1] * pt[2] - w[2] * pt[1], w[2] * pt[0] - w[0] * pt[2], w[0] * pt[1] - w[1] * pt[0]};
+        const DJet<N> tmp = (w[0] * pt[0] + w[1] * pt[1] + w[2] * pt[2]) * (jconst<N>(1.0) - ct);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) res[i] = pt[i] * ct + wx[i] * st + w[i] * tmp;
+    } else {
+        const DJet<N> wx[3] = {aa[1] * pt[2] - aa[2] * pt[1], aa[2] * pt[0] - aa[0] * pt[2], aa[0] * pt[1] - aa[1] * pt[0]};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) res[i] = pt[i] + wx[i];
+    }
+}
+
+// The reference functors' arithmetic (same operation order).
+template <int K, int N>
+__device__ __forceinline__ void project(const DJet<N> X[3], const DJet<N> ps[6], const DJet<N> in[K], double ox, double oy,
+                                        double cx, double cy, DJet<N> res[2]) {
+    DJet<N> p[3];
+    rotate(ps, X, p);
+    p[0] = p[0] + ps[3]; p[1] = p[1] + ps[4]; p[2] = p[2] + ps[5];
+    const DJet<N> xp = p[0] / p[2];
+    const DJet<N> yp = p[1] / p[2];
+    const DJet<N> xd = in[0] * xp;
+    const DJet<N> yd = in[0] * yp;
+    if constexpr (K == 1) {
+        res[0] = xd - jconst<N>(ox - cx);
+        res[1] = yd - jconst<N>(oy - cy);
+    } else if constexpr (K == 3) {
+        const DJet<N> r2 = (xp * xp) + (yp * yp);
+        const DJet<N> r4 = r2 * r2;
+        const DJet<N> rad = in[1] * r2 + in[2] * r4;
+        res[0] = (xd + xd * rad) - (jconst<N>(ox) - jconst<N>(cx));
+        res[1] = (yd + yd * rad) - (jconst<N>(oy) - jconst<N>(cy));
+    } else {
+        const DJet<N> r2 = (xp * xp) + (yp * yp);
+        const DJet<N> r4 = r2 * r2;
+        const DJet<N> rad = in[3] * r2 + in[4] * r4;
+        const DJet<N> xu = xd + xd * rad + (in[5] * (r2 + 2.0 * (xd * xd)) + 2.0 * in[6] * xd * yd);
+        const DJet<N> yu = yd + yd * rad + (2.0 * in[5] * xd * yd + in[6] * (r2 + 2.0 * (yd * yd)));
+        res[0] = xu - (jconst<N>(ox) - in[1]);
+        res[1] = yu - (jconst<N>(oy) - in[2]);
+    }
+}
+
+// ---- block reduction helper (256 threads, fixed order) -------------------
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) sh[wid] = v;
+    __syncthreads();
+    double s = 0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += sh[w];
+    return s;   // valid in thread 0
+}
+
+// ---- linearization --------------------------------------------------------
+// Fields of the field-major Jacobian store: 0,1 r; 2..7 Je (row-major 2x3);
+// 8..19 Jc (2x6); 20..20+2K Ji (2xK).
+template <int K, bool JAC>
+__global__ __launch_bounds__(256)
+void ba_linearize(int O, const int* __restrict__ obs_point, const int* __restrict__ obs_cam,
+                  const double* __restrict__ obs_xy, double cx, double cy, const double* __restrict__ pts,
+                  const double* __restrict__ poses, const double* __restrict__ intr, double* __restrict__ J,
+                  double* __restrict__ partial) {
+    __shared__ double sh[8];
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    double c2 = 0.0;
+    if (o < O) {
+        const int p = obs_point[o], c = obs_cam[o];
+        const double ox = obs_xy[2 * (size_t)o], oy = obs_xy[2 * (size_t)o + 1];
+        if constexpr (JAC) {
+            constexpr int N = 9 + K;
+            DJet<N> X[3], ps[6], in[K], res[2];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) X[i] = jvar<N>(pts[3 * (size_t)p + i], i);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) ps[i] = jvar<N>(poses[6 * (size_t)c + i], 3 + i);
+#pragma unroll
+            for (int i = 0; i < K; ++i) in[i] = jvar<N>(intr[i], 9 + i);
+            project<K, N>(X, ps, in, ox, oy, cx, cy, res);
+            const size_t S = (size_t)O;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                J[j * S + o] = res[j].a;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) J[(2 + 3 * j + i) * S + o] = res[j].v[i];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) J[(8 + 6 * j + i) * S + o] = res[j].v[3 + i];
+#pragma unroll
+                for (int i = 0; i < K; ++i) J[(20 + K * j + i) * S + o] = res[j].v[9 + i];
+            }
+            c2 = res[0].a * res[0].a + res[1].a * res[1].a;
+        } else {
+            DJet<0> X[3], ps[6], in[K], res[2];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) X[i].a = pts[3 * (size_t)p + i];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) ps[i].a = poses[6 * (size_t)c + i];
+#pragma unroll
+            for (int i = 0; i < K; ++i) in[i].a = intr[i];
+            project<K, 0>(X, ps, in, ox, oy, cx, cy, res);
+            c2 = res[0].a * res[0].a + res[1].a * res[1].a;
+        }
+    }
+    const double s = block_sum(c2, sh);
+    if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+// Deterministic final sum of `n` partials (one block); out[0] = scale * sum.
+__global__ __launch_bounds__(256)
+void ba_sum(const double* __restrict__ partial, int n, double scale, double* __restrict__ out) {
+    __shared__ double sh[8];
+    double v = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) v += partial[i];
+    const double s = block_sum(v, sh);
+    if (threadIdx.x == 0) out[0] = scale * s;
+}
+
+// Squared column norms (unscaled) and gradient J^T r.
+// Points: one thread per point over its observations (CSR).
+template <int K>
+__global__ __launch_bounds__(256)
+void ba_point_cols(int P, int O, const int* __restrict__ pt_start, const int* __restrict__ pt_obs,
+                   const double* __restrict__ J, double* __restrict__ colsq, double* __restrict__ grad) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const size_t S = (size_t)O;
+    double cs[3] = {0, 0, 0}, g[3] = {0, 0, 0};
+    for (int a = pt_start[p]; a < pt_start[p + 1]; ++a) {
+        const int o = pt_obs[a];
+        const double r0 = J[o], r1 = J[S + o];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const double j0 = J[(2 + i) * S + o], j1 = J[(5 + i) * S + o];
+            cs[i] += j0 * j0 + j1 * j1;
+            g[i] += j0 * r0 + j1 * r1;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { colsq[3 * (size_t)p + i] = cs[i]; grad[3 * (size_t)p + i] = g[i]; }
+}
+
+// Cameras: one block per camera over its observations; intrinsics: per-block
+// partials over observation ranges (cam-major), summed by ba_intr_cols_final.
+template <int K>
+__global__ __launch_bounds__(256)
+void ba_cam_cols(int O, const int* __restrict__ cam_start, const int* __restrict__ cam_obs, const double* __restrict__ J,
+                 double* __restrict__ colsq, double* __restrict__ grad, double* __restrict__ ipart) {
+    __shared__ double sh[8];
+    const int c = blockIdx.x;
+    const size_t S = (size_t)O;
+    double v[12 + 2 * K];
+#pragma unroll
+    for (int i = 0; i < 12 + 2 * K; ++i) v[i] = 0.0;
+    for (int a = cam_start[c] + threadIdx.x; a < cam_start[c + 1]; a += blockDim.x) {
+        const int o = cam_obs[a];
+        const double r0 = J[o], r1 = J[S + o];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double j0 = J[(8 + i) * S + o], j1 = J[(14 + i) * S + o];
+            v[i] += j0 * j0 + j1 * j1;
+            v[6 + i] += j0 * r0 + j1 * r1;
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const double j0 = J[(20 + i) * S + o], j1 = J[(20 + K + i) * S + o];
+            v[12 + i] += j0 * j0 + j1 * j1;
+            v[12 + K + i] += j0 * r0 + j1 * r1;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 12 + 2 * K; ++i) {
+        const double s = block_sum(v[i], sh);
+        if (threadIdx.x == 0) {
+            if (i < 6) colsq[6 * (size_t)c + i] = s;
+            else if (i < 12) grad[6 * (size_t)c + i - 6] = s;
+            else ipart[(size_t)c * 2 * K + (i - 12)] = s;
+        }
+    }
+}
+
+template <int K>
+__global__ void ba_intr_cols_final(int C, const double* __restrict__ ipart, double* __restrict__ colsq,
+                                   double* __restrict__ grad) {
+    const int i = threadIdx.x;
+    if (i >= 2 * K) return;
+    double s = 0;
+    for (int c = 0; c < C; ++c) s += ipart[(size_t)c * 2 * K + i];
+    if (i < K) colsq[i] = s; else grad[i - K] = s;
+}
+
+// scale = 1 / (1 + sqrt(colsq)) (iteration 0 only, Ceres jacobi_scaling)
+__global__ void ba_scale(int n, const double* __restrict__ colsq, double* __restrict__ scale) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) scale[i] = 1.0 / (1.0 + sqrt(colsq[i]));
+}
+// LM diagonal from the scaled Jacobian: clamp(colsq * scale^2, min, max);
+// also max |grad| partials for the gradient tolerance.
+__global__ __launch_bounds__(256)
+void ba_diag(int n, const double* __restrict__ colsq, const double* __restrict__ scale, double dmin, double dmax,
+             double* __restrict__ diag, const double* __restrict__ grad, double* __restrict__ gpart) {
+    __shared__ double sh[8];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    double g = 0.0;
+    if (i < n) {
+        const double s = scale[i];
+        diag[i] = fmin(fmax(colsq[i] * s * s, dmin), dmax);
+        g = fabs(grad[i]);
+    }
+    for (int o = 32; o > 0; o >>= 1) g = fmax(g, __shfl_xor(g, o));
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) sh[wid] = g;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double m = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m = fmax(m, sh[w]);
+        gpart[blockIdx.x] = m;
+    }
+}
+__global__ __launch_bounds__(256)
+void ba_max(const double* __restrict__ part, int n, double* __restrict__ out) {
+    __shared__ double sh[8];
+    double g = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) g = fmax(g, part[i]);
+    for (int o = 32; o > 0; o >>= 1) g = fmax(g, __shfl_xor(g, o));
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = g;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double m = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m = fmax(m, sh[w]);
+        out[0] = m;
+    }
+}
+
+// ---- Schur complement -------------------------------------------------------
+// D = sqrt(diag / radius) (LevenbergMarquardtStrategy::ComputeStep [ext]).
+__global__ void ba_lm_d(int n, const double* __restrict__ diag, double radius, double* __restrict__ D) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) D[i] = sqrt(diag[i] / radius);
+}
+
+__device__ __forceinline__ bool inv3_spd(const double* A, double* Ai) {
+    double l00 = A[0];
+    if (!(l00 > 0)) return false;
+    l00 = sqrt(l00);
+    const double l10 = A[3] / l00, l20 = A[6] / l00;
+    double l11 = A[4] - l10 * l10;
+    if (!(l11 > 0)) return false;
+    l11 = sqrt(l11);
+    const double l21 = (A[7] - l20 * l10) / l11;
+    double l22 = A[8] - l20 * l20 - l21 * l21;
+    if (!(l22 > 0)) return false;
+    l22 = sqrt(l22);
+    const double i00 = 1 / l00, i11 = 1 / l11, i22 = 1 / l22;
+    const double i10 = -l10 * i00 * i11;
+    const double i21 = -l21 * i11 * i22;
+    const double i20 = -(l20 * i00 + l21 * i10) * i22;
+    const double Li[9] = {i00, 0, 0, i10, i11, 0, i20, i21, i22};
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            double s = 0;
+#pragma unroll
+            for (int m = 0; m < 3; ++m) s += Li[m * 3 + a] * Li[m * 3 + b];
+            Ai[a * 3 + b] = s;
+        }
+    return true;
+}
+
+// Per point: E = sum Je_s^T Je_s + D_e^2, g_e = sum Je_s^T r, Einv, EinvG = Einv g_e,
+// V = sum Je_s^T Ji_s (3xK), Z = Einv V; per obs U = Einv Je_s^T (3x2), q = Je_s EinvG.
+// Also per-block partials of sum_p V^T Z (KxK) for the intrinsics block.
+template <int K>
+__global__ __launch_bounds__(256)
+void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, const int* __restrict__ pt_obs,
+                     const double* __restrict__ J, const double* __restrict__ scale, const double* __restrict__ D,
+                     double* __restrict__ Einv, double* __restrict__ EinvG, double* __restrict__ Zp,
+                     double* __restrict__ U, double* __restrict__ q, double* __restrict__ vzpart, int* __restrict__ fail) {
+    __shared__ double sh[8];
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t S = (size_t)O;
+    const size_t ni = 3 * (size_t)P + 6 * (size_t)C;   // first intrinsics column
+    double VZ[K * K];
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) VZ[i] = 0.0;
+    if (p < P) {
+        const double s0 = scale[3 * (size_t)p], s1 = scale[3 * (size_t)p + 1], s2 = scale[3 * (size_t)p + 2];
+        double si[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) si[i] = scale[ni + i];
+        double E[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0}, V[3 * K];
+#pragma unroll
+        for (int i = 0; i < 3 * K; ++i) V[i] = 0.0;
+        const int a0 = pt_start[p], a1 = pt_start[p + 1];
+        for (int a = a0; a < a1; ++a) {
+            const int o = pt_obs[a];
+            const double r[2] = {J[o], J[S + o]};
+            double je[2][3];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                je[j][0] = J[(2 + 3 * j) * S + o] * s0;
+                je[j][1] = J[(3 + 3 * j) * S + o] * s1;
+                je[j][2] = J[(4 + 3 * j) * S + o] * s2;
+            }
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+#pragma unroll
+                for (int v = 0; v < 3; ++v) E[u * 3 + v] += je[0][u] * je[0][v] + je[1][u] * je[1][v];
+                g[u] += je[0][u] * r[0] + je[1][u] * r[1];
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+                    V[u * K + i] += je[0][u] * J[(20 + i) * S + o] * si[i] + je[1][u] * J[(20 + K + i) * S + o] * si[i];
+            }
+        }
+        const double d0 = D[3 * (size_t)p], d1 = D[3 * (size_t)p + 1], d2 = D[3 * (size_t)p + 2];
+        E[0] += d0 * d0; E[4] += d1 * d1; E[8] += d2 * d2;
+        double Ei[9];
+        if (!inv3_spd(E, Ei)) {
+            atomicOr(fail, 1);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) Ei[i] = 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Einv[9 * (size_t)p + i] = Ei[i];
+        double eg[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            eg[u] = Ei[u * 3] * g[0] + Ei[u * 3 + 1] * g[1] + Ei[u * 3 + 2] * g[2];
+            EinvG[3 * (size_t)p + u] = eg[u];
+        }
+        double Z[3 * K];
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                Z[u * K + i] = Ei[u * 3] * V[i] + Ei[u * 3 + 1] * V[K + i] + Ei[u * 3 + 2] * V[2 * K + i];
+                Zp[(size_t)p * 3 * K + u * K + i] = Z[u * K + i];
+            }
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int l = 0; l < K; ++l) VZ[i * K + l] = V[i] * Z[l] + V[K + i] * Z[K + l] + V[2 * K + i] * Z[2 * K + l];
+        for (int a = a0; a < a1; ++a) {
+            const int o = pt_obs[a];
+            double je[2][3];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                je[j][0] = J[(2 + 3 * j) * S + o] * s0;
+                je[j][1] = J[(3 + 3 * j) * S + o] * s1;
+                je[j][2] = J[(4 + 3 * j) * S + o] * s2;
+            }
+            // U = Einv Je^T (3x2), row-major; q = Je EinvG (2)
+#pragma unroll
+            for (int u = 0; u < 3; ++u)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    U[(size_t)(u * 2 + j) * S + o] = Ei[u * 3] * je[j][0] + Ei[u * 3 + 1] * je[j][1] + Ei[u * 3 + 2] * je[j][2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) q[j * S + o] = je[j][0] * eg[0] + je[j][1] * eg[1] + je[j][2] * eg[2];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) {
+        const double s = block_sum(VZ[i], sh);
+        if (threadIdx.x == 0) vzpart[(size_t)blockIdx.x * K * K + i] = s;
+    }
+}
+
+// Per camera c (one block): Scc = sum Jc_s^T Jc_s (6x6), Spi = sum Jc_s^T Ji_s - Jc_s^T Je_s Z_p (6xK),
+// rc = sum Jc_s^T (r - q); and per-camera partials of the intrinsics parts:
+// sum Ji_s^T Ji_s (KxK) and sum Ji_s^T (r - q) (K).
+template <int K>
+__global__ __launch_bounds__(256)
+void ba_cam_blocks(int P, int O, int C, const int* __restrict__ cam_start, const int* __restrict__ cam_obs,
+                   const int* __restrict__ obs_point, const double* __restrict__ J, const double* __restrict__ scale,
+                   const double* __restrict__ Zp, const double* __restrict__ q, double* __restrict__ Scc,
+                   double* __restrict__ Spi, double* __restrict__ rc, double* __restrict__ ipart) {
+    __shared__ double sh[8];
+    constexpr int NV = 21 + 6 * K + 6 + (K * (K + 1)) / 2 + K;   // upper 6x6, 6xK, 6, upper KxK, K
+    const int c = blockIdx.x;
+    const size_t S = (size_t)O;
+    const size_t nc = 3 * (size_t)P + 6 * (size_t)c, ni = 3 * (size_t)P + 6 * (size_t)C;
+    double sc[6], si[K];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) sc[i] = scale[nc + i];
+#pragma unroll
+    for (int i = 0; i < K; ++i) si[i] = scale[ni + i];
+    double v[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = 0.0;
+    for (int a = cam_start[c] + threadIdx.x; a < cam_start[c + 1]; a += blockDim.x) {
+        const int o = cam_obs[a];
+        const int p = obs_point[o];
+        const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
+        double jc[2][6], ji[2][K], je[2][3], rq[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) jc[j][i] = J[(8 + 6 * j + i) * S + o] * sc[i];
+#pragma unroll
+            for (int i = 0; i < K; ++i) ji[j][i] = J[(20 + K * j + i) * S + o] * si[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) je[j][i] = J[(2 + 3 * j + i) * S + o] * sp[i];
+            rq[j] = J[j * S + o] - q[j * S + o];
+        }
+        // T = Je Z (2xK)
+        double T[2][K];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                T[j][i] = je[j][0] * Zp[(size_t)p * 3 * K + i] + je[j][1] * Zp[(size_t)p * 3 * K + K + i] +
+                          je[j][2] * Zp[(size_t)p * 3 * K + 2 * K + i];
+        int e = 0;
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+#pragma unroll
+            for (int w = u; w < 6; ++w) v[e++] += jc[0][u] * jc[0][w] + jc[1][u] * jc[1][w];
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+#pragma unroll
+            for (int i = 0; i < K; ++i) v[e++] += jc[0][u] * (ji[0][i] - T[0][i]) + jc[1][u] * (ji[1][i] - T[1][i]);
+#pragma unroll
+        for (int u = 0; u < 6; ++u) v[e++] += jc[0][u] * rq[0] + jc[1][u] * rq[1];
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int l = i; l < K; ++l) v[e++] += ji[0][i] * ji[0][l] + ji[1][i] * ji[1][l];
+#pragma unroll
+        for (int i = 0; i < K; ++i) v[e++] += ji[0][i] * rq[0] + ji[1][i] * rq[1];
+    }
+    constexpr int NI = (K * (K + 1)) / 2 + K;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const double s = block_sum(v[i], sh);
+        if (threadIdx.x == 0) {
+            if (i < 21) {
+                int u = 0, w = 0, e = i;
+                while (e >= 6 - u) { e -= 6 - u; ++u; }
+                w = u + e;
+                Scc[36 * (size_t)c + u * 6 + w] = s;
+                Scc[36 * (size_t)c + w * 6 + u] = s;
+            } else if (i < 21 + 6 * K) {
+                Spi[(size_t)c * 6 * K + (i - 21)] = s;
+            } else if (i < 27 + 6 * K) {
+                rc[6 * (size_t)c + (i - 21 - 6 * K)] = s;
+            } else {
+                ipart[(size_t)c * NI + (i - 27 - 6 * K)] = s;
+            }
+        }
+    }
+}
+
+// Intrinsics block: Sii = sum_c ipart_JiJi - sum_blocks VZ, ri = sum_c ipart_Jir (fixed order).
+template <int K>
+__global__ void ba_intr_final(int C, int nvz, const double* __restrict__ ipart, const double* __restrict__ vzpart,
+                              double* __restrict__ Sii, double* __restrict__ ri) {
+    constexpr int NI = (K * (K + 1)) / 2 + K;
+    const int t = threadIdx.x;
+    if (t < K * K) {
+        const int i = t / K, l = t % K;
+        const int a = i < l ? i : l, b = i < l ? l : i;
+        int e = 0;
+        for (int u = 0; u < a; ++u) e += K - u;
+        e += b - a;
+        double s = 0;
+        for (int c = 0; c < C; ++c) s += ipart[(size_t)c * NI + e];
+        double z = 0;
+        for (int bk = 0; bk < nvz; ++bk) z += vzpart[(size_t)bk * K * K + i * K + l];
+        // symmetrise V^T Z (exactly symmetric in exact arithmetic)
+        double z2 = 0;
+        for (int bk = 0; bk < nvz; ++bk) z2 += vzpart[(size_t)bk * K * K + l * K + i];
+        Sii[t] = s - 0.5 * (z + z2);
+    } else if (t < K * K + K) {
+        const int i = t - K * K;
+        double s = 0;
+        for (int c = 0; c < C; ++c) s += ipart[(size_t)c * NI + (K * (K + 1)) / 2 + i];
+        ri[i] = s;
+    }
+}
+
+// Off-diagonal / same-camera pose blocks: for block b = (c1 <= c2) with its
+// segment of ordered observation pairs (o1 in c1, o2 in c2, same point):
+//   Spp_b = - sum Jc_s(o1)^T [Je_s(o1) U(o2)] Jc_s(o2)     (U = Einv Je_s^T)
+// one workgroup per block, fixed-order tree sum (deterministic).
+__global__ __launch_bounds__(256)
+void ba_pair_blocks(int P, int O, const int* __restrict__ blk_cam, const int* __restrict__ blk_start,
+                    const int2* __restrict__ trip, const int* __restrict__ obs_point, const double* __restrict__ J,
+                    const double* __restrict__ scale, const double* __restrict__ U, double* __restrict__ Spp) {
+    __shared__ double sh[8];
+    const int b = blockIdx.x;
+    const int c1 = blk_cam[2 * b], c2 = blk_cam[2 * b + 1];
+    const size_t S = (size_t)O;
+    double s1[6], s2[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) { s1[i] = scale[3 * (size_t)P + 6 * (size_t)c1 + i]; s2[i] = scale[3 * (size_t)P + 6 * (size_t)c2 + i]; }
+    double acc[36];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) acc[i] = 0.0;
+    for (int t = blk_start[b] + threadIdx.x; t < blk_start[b + 1]; t += blockDim.x) {
+        const int2 tr = trip[t];
+        const int o1 = tr.x, o2 = tr.y;
+        const int p = obs_point[o1];
+        const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
+        double M[2][2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int l = 0; l < 2; ++l) {
+                double m = 0;
+#pragma unroll
+                for (int u = 0; u < 3; ++u) m += J[(2 + 3 * j + u) * S + o1] * sp[u] * U[(size_t)(u * 2 + l) * S + o2];
+                M[j][l] = m;
+            }
+        double a1[2][6], a2[2][6];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                a1[j][i] = J[(8 + 6 * j + i) * S + o1] * s1[i];
+                a2[j][i] = J[(8 + 6 * j + i) * S + o2] * s2[i];
+            }
+        // T = M a2 (2x6); acc += a1^T T
+        double T[2][6];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) T[j][i] = M[j][0] * a2[0][i] + M[j][1] * a2[1][i];
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+#pragma unroll
+            for (int w = 0; w < 6; ++w) acc[u * 6 + w] += a1[0][u] * T[0][w] + a1[1][u] * T[1][w];
+    }
+#pragma unroll
+    for (int i = 0; i < 36; ++i) {
+        const double s = block_sum(acc[i], sh);
+        if (threadIdx.x == 0) Spp[36 * (size_t)b + i] = -s;
+    }
+}
+
+// Dense reduced camera system, row-major npad x npad (npad multiple of NB),
+// assembled by three ordered launches over a zeroed S (no two workgroups of one
+// launch touch the same element):
+//   ba_assemble_pairs  Spp(c1,c2) into the (c1,c2) block and its transpose
+//   ba_assemble_diag   += Scc on each pose diagonal block
+//   ba_assemble_rest   pose-intrinsics Spi, intrinsics Sii, + D^2 on the
+//                      diagonal (added once, after any cross-rank all-reduce),
+//                      identity on the padding, rhs = [rc ; ri].
+__global__ void ba_assemble_pairs(int npad, const int* __restrict__ blk_cam, const double* __restrict__ Spp,
+                                  double* __restrict__ S) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    if (t >= 36) return;
+    const int u = t / 6, w = t % 6;
+    const int c1 = blk_cam[2 * b], c2 = blk_cam[2 * b + 1];
+    const double v = Spp[36 * (size_t)b + t];
+    S[(size_t)(6 * c1 + u) * npad + 6 * c2 + w] = v;
+    if (c1 != c2) S[(size_t)(6 * c2 + w) * npad + 6 * c1 + u] = v;
+}
+
+__global__ void ba_assemble_diag(int npad, const double* __restrict__ Scc, double* __restrict__ S) {
+    const int c = blockIdx.x, t = threadIdx.x;
+    if (t >= 36) return;
+    const int u = t / 6, w = t % 6;
+    S[(size_t)(6 * c + u) * npad + 6 * c + w] += Scc[36 * (size_t)c + t];
+}
+
+__global__ void ba_assemble_rest(int C, int K, int nf, int npad, const double* __restrict__ Spi,
+                                 const double* __restrict__ Sii, const double* __restrict__ rc,
+                                 const double* __restrict__ ri, double* __restrict__ S, double* __restrict__ rhs) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npad) return;
+    if (i < 6 * C) {
+        const int c = i / 6, u = i % 6;
+        for (int l = 0; l < K; ++l) {
+            const double v = Spi[(size_t)c * 6 * K + u * K + l];
+            S[(size_t)i * npad + 6 * C + l] = v;
+            S[(size_t)(6 * C + l) * npad + i] = v;
+        }
+        rhs[i] = rc[i];
+    } else if (i < nf) {
+        const int l = i - 6 * C;
+        for (int m = 0; m < K; ++m) S[(size_t)i * npad + 6 * C + m] = Sii[l * K + m];
+        rhs[i] = ri[l];
+    } else {
+        S[(size_t)i * npad + i] = 1.0;
+        rhs[i] = 0.0;
+    }
+}
+
+// + D_f^2 on the reduced system's diagonal (after the cross-rank all-reduce).
+__global__ void ba_add_damping(int P, int nf, int npad, const double* __restrict__ D, double* __restrict__ S) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nf) return;
+    const double d = D[3 * (size_t)P + i];
+    S[(size_t)i * npad + i] += d * d;
+}
+
+// ---- dense Cholesky (lower, row-major, in place), NB x NB tiles ------------
+// potrf of diagonal tile k (one 256-thread block, tile in LDS).
+__global__ __launch_bounds__(256)
+void chol_potrf(double* __restrict__ A, int npad, int k, int* __restrict__ fail) {
+    __shared__ double T[NB][NB + 1];
+    const int k0 = k * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) T[e / NB][e % NB] = A[(size_t)(k0 + e / NB) * npad + k0 + e % NB];
+    __syncthreads();
+    for (int j = 0; j < NB; ++j) {
+        if (threadIdx.x == 0) {
+            const double d = T[j][j];
+            if (!(d > 0.0) || !isfinite(d)) { atomicOr(fail, 1); T[j][j] = 1.0; }
+            else T[j][j] = sqrt(d);
+        }
+        __syncthreads();
+        const double djj = T[j][j];
+        for (int i = j + 1 + threadIdx.x; i < NB; i += blockDim.x) T[i][j] /= djj;
+        __syncthreads();
+        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+            const int i = e / NB, l = e % NB;
+            if (i > j && l > j && l <= i) T[i][l] -= T[i][j] * T[l][j];
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+        const int i = e / NB, l = e % NB;
+        A[(size_t)(k0 + i) * npad + k0 + l] = l <= i ? T[i][l] : 0.0;
+    }
+}
+
+// trsm: tiles (i, k) for i > k: L_ik = A_ik L_kk^-T.  One block per tile row i.
+__global__ __launch_bounds__(256)
+void chol_trsm(double* __restrict__ A, int npad, int k) {
+    __shared__ double L[NB][NB + 1];
+    __shared__ double X[NB][NB + 1];
+    const int k0 = k * NB, i0 = (k + 1 + blockIdx.x) * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+        L[e / NB][e % NB] = A[(size_t)(k0 + e / NB) * npad + k0 + e % NB];
+        X[e / NB][e % NB] = A[(size_t)(i0 + e / NB) * npad + k0 + e % NB];
+    }
+    __syncthreads();
+    // rows of X are independent: x_j = (a_j - sum_{l<j} x_l L[j][l]) / L[j][j]
+    if (threadIdx.x < NB) {
+        const int r = threadIdx.x;
+        for (int j = 0; j < NB; ++j) {
+            double s = X[r][j];
+            for (int l = 0; l < j; ++l) s -= X[r][l] * L[j][l];
+            X[r][j] = s / L[j][j];
+        }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) A[(size_t)(i0 + e / NB) * npad + k0 + e % NB] = X[e / NB][e % NB];
+}
+
+// Trailing update A_ij -= L_ik L_jk^T for k < j <= i (lower tiles).  Block per tile.
+__global__ __launch_bounds__(256)
+void chol_update(double* __restrict__ A, int npad, int k, int T) {
+    __shared__ double Li[NB][NB + 1];
+    __shared__ double Lj[NB][NB + 1];
+    // decode linear tile index -> (i, j), j <= i, both in (k, T)
+    int rem = blockIdx.x, i = k + 1, j;
+    for (;; ++i) {
+        const int cnt = i - k;   // tiles j = k+1..i
+        if (rem < cnt) { j = k + 1 + rem; break; }
+        rem -= cnt;
+    }
+    const int i0 = i * NB, j0 = j * NB, k0 = k * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+        Li[e / NB][e % NB] = A[(size_t)(i0 + e / NB) * npad + k0 + e % NB];
+        Lj[e / NB][e % NB] = A[(size_t)(j0 + e / NB) * npad + k0 + e % NB];
+    }
+    __syncthreads();
+    // each thread: 4x4 outputs (rows ty*4.., cols tx*4..), 16x16 threads
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    double acc[4][4] = {};
+    for (int l = 0; l < NB; ++l) {
+        double a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { a[u] = Li[ty * 4 + u][l]; b[u] = Lj[tx * 4 + u][l]; }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) acc[u][w] += a[u] * b[w];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) A[(size_t)(i0 + ty * 4 + u) * npad + j0 + tx * 4 + w] -= acc[u][w];
+}
+
+// Solve L L^T x = b in place (one 1024-thread block; NB-row blocks, wave 0
+// does the diagonal solves with shuffles, all threads do the updates).
+__global__ __launch_bounds__(1024)
+void chol_solve(const double* __restrict__ L, int npad, double* __restrict__ b) {
+    __shared__ double y[NB];
+    const int T = npad / NB;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int k = 0; k < T; ++k) {                 // forward L y = b
+        const int k0 = k * NB;
+        if (wid == 0) {
+            double v = b[k0 + lane];
+            for (int j = 0; j < NB; ++j) {
+                const double yj = __shfl(v, j) / L[(size_t)(k0 + j) * npad + k0 + j];
+                if (lane == j) v = yj;
+                if (lane > j) v -= L[(size_t)(k0 + lane) * npad + k0 + j] * yj;
+            }
+            b[k0 + lane] = v;
+            y[lane] = v;
+        }
+        __syncthreads();
+        for (int r = k0 + NB + threadIdx.x; r < npad; r += blockDim.x) {
+            double s = 0;
+            const double* row = L + (size_t)r * npad + k0;
+            for (int l = 0; l < NB; ++l) s += row[l] * y[l];
+            b[r] -= s;
+        }
+        __syncthreads();
+    }
+    for (int k = T - 1; k >= 0; --k) {            // backward L^T x = y
+        const int k0 = k * NB;
+        if (wid == 0) {
+            double v = b[k0 + lane];
+            for (int j = NB - 1; j >= 0; --j) {
+                const double xj = __shfl(v, j) / L[(size_t)(k0 + j) * npad + k0 + j];
+                if (lane == j) v = xj;
+                if (lane < j) v -= L[(size_t)(k0 + j) * npad + k0 + lane] * xj;
+            }
+            b[k0 + lane] = v;
+            y[lane] = v;
+        }
+        __syncthreads();
+        for (int r = threadIdx.x; r < k0; r += blockDim.x) {
+            double s = 0;
+            for (int l = 0; l < NB; ++l) s += L[(size_t)(k0 + l) * npad + r] * y[l];
+            b[r] -= s;
+        }
+        __syncthreads();
+    }
+}
+
+// x_e = EinvG - sum_o U_o (F_o x_f), F_o = [Jc_s | Ji_s]
+template <int K>
+__global__ __launch_bounds__(256)
+void ba_backsub(int P, int O, int C, const int* __restrict__ pt_start, const int* __restrict__ pt_obs,
+                const int* __restrict__ obs_cam, const double* __restrict__ J, const double* __restrict__ scale,
+                const double* __restrict__ U, const double* __restrict__ EinvG, const double* __restrict__ xf,
+                double* __restrict__ xe) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const size_t S = (size_t)O, ne = 3 * (size_t)P;
+    double v[3] = {EinvG[3 * (size_t)p], EinvG[3 * (size_t)p + 1], EinvG[3 * (size_t)p + 2]};
+    for (int a = pt_start[p]; a < pt_start[p + 1]; ++a) {
+        const int o = pt_obs[a], c = obs_cam[o];
+        double f[2] = {0, 0};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) f[j] += J[(8 + 6 * j + i) * S + o] * scale[ne + 6 * (size_t)c + i] * xf[6 * c + i];
+#pragma unroll
+            for (int i = 0; i < K; ++i) f[j] += J[(20 + K * j + i) * S + o] * scale[ne + 6 * (size_t)C + i] * xf[6 * C + i];
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u) v[u] -= U[(size_t)(u * 2) * S + o] * f[0] + U[(size_t)(u * 2 + 1) * S + o] * f[1];
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u) xe[3 * (size_t)p + u] = v[u];
+}
+
+// step_s = -sol; delta = step_s * scale; cand = x + delta; partials of ||delta||^2 and finiteness.
+__global__ __launch_bounds__(256)
+void ba_step(int n, const double* __restrict__ sol, const double* __restrict__ scale, const double* __restrict__ x,
+             double* __restrict__ step, double* __restrict__ cand, double* __restrict__ part) {
+    __shared__ double sh[8];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    double d2 = 0.0;
+    if (i < n) {
+        const double st = -sol[i];
+        step[i] = st;
+        const double d = st * scale[i];
+        cand[i] = x[i] + d;
+        d2 = isfinite(d) ? (x[i] - cand[i]) * (x[i] - cand[i]) : INFINITY;
+    }
+    const double s = block_sum(d2, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// model cost change partials: sum_o m . (r + m/2), m = J_s step
+template <int K>
+__global__ __launch_bounds__(256)
+void ba_model(int P, int O, int C, const int* __restrict__ obs_point, const int* __restrict__ obs_cam,
+              const double* __restrict__ J, const double* __restrict__ scale, const double* __restrict__ step,
+              double* __restrict__ part) {
+    __shared__ double sh[8];
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t S = (size_t)O, ne = 3 * (size_t)P;
+    double acc = 0.0;
+    if (o < O) {
+        const int p = obs_point[o], c = obs_cam[o];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            double m = 0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) m += J[(2 + 3 * j + i) * S + o] * scale[3 * (size_t)p + i] * step[3 * (size_t)p + i];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) m += J[(8 + 6 * j + i) * S + o] * scale[ne + 6 * (size_t)c + i] * step[ne + 6 * (size_t)c + i];
+#pragma unroll
+            for (int i = 0; i < K; ++i) m += J[(20 + K * j + i) * S + o] * scale[ne + 6 * (size_t)C + i] * step[ne + 6 * (size_t)C + i];
+            acc += m * (J[j * S + o] + m / 2.0);
+        }
+    }
+    const double s = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256)
+void ba_sumsq(int n, const double* __restrict__ x, double* __restrict__ part) {
+    __shared__ double sh[8];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const double v = i < n ? x[i] * x[i] : 0.0;
+    const double s = block_sum(v, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+}  // namespace ba
+}  // namespace sfmx

@@ -12,6 +12,7 @@
 // (int8 0 == descriptor value 128: contributes 0 to every dot product).
 #pragma once
 #include <cstdint>
+#include <string>
 
 namespace sfmx {
 
@@ -43,5 +44,8 @@ struct WorkItem {          // one 512-query block of one pair
 };
 
 struct DMatchDev { int32_t queryIdx, trainIdx, imgIdx; float distance; };
+
+// Thread-local last-error text shared by every C-ABI entry point (sfmx_last_error).
+void set_last_error(const char* msg);
 
 }  // namespace sfmx

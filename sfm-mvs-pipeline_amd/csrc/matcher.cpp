@@ -50,6 +50,9 @@ using namespace sfmx;
 namespace {
 
 thread_local std::string g_last_error;
+}  // namespace
+void sfmx::set_last_error(const char* msg) { g_last_error = msg ? msg : ""; }
+namespace {
 
 int fail(int code, const std::string& msg) {
     g_last_error = msg;

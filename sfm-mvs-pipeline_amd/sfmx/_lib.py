@@ -35,6 +35,33 @@ class sfmx_dmatch(C.Structure):
                 ("distance", C.c_float)]
 
 
+class sfmx_ba_problem(C.Structure):
+    _fields_ = [("n_points", C.c_int32), ("n_cams", C.c_int32), ("n_obs", C.c_int32), ("cam_model", C.c_int32),
+                ("points", C.c_void_p), ("poses", C.c_void_p), ("intr", C.c_void_p),
+                ("obs_point", C.c_void_p), ("obs_cam", C.c_void_p), ("obs_xy", C.c_void_p),
+                ("cx", C.c_double), ("cy", C.c_double)]
+
+
+class sfmx_ba_options(C.Structure):
+    _fields_ = [("max_num_iterations", C.c_int32), ("max_num_consecutive_invalid_steps", C.c_int32),
+                ("jacobi_scaling", C.c_int32), ("device", C.c_int32),
+                ("function_tolerance", C.c_double), ("gradient_tolerance", C.c_double),
+                ("parameter_tolerance", C.c_double), ("initial_trust_region_radius", C.c_double),
+                ("max_trust_region_radius", C.c_double), ("min_trust_region_radius", C.c_double),
+                ("min_lm_diagonal", C.c_double), ("max_lm_diagonal", C.c_double),
+                ("min_relative_decrease", C.c_double)]
+
+
+class sfmx_ba_summary(C.Structure):
+    _fields_ = [("initial_cost", C.c_double), ("final_cost", C.c_double),
+                ("num_successful_steps", C.c_int32), ("num_unsuccessful_steps", C.c_int32),
+                ("num_invalid_steps", C.c_int32), ("termination_type", C.c_int32),
+                ("total_ms", C.c_double), ("ms_per_iteration", C.c_double),
+                ("final_gradient_max_norm", C.c_double), ("final_radius", C.c_double)]
+
+
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p)
+
 # Every symbol include/sfmx.h (and include/sfmx_ba.h) declares, with its ctypes prototype.
 _P = C.POINTER
 _i32p, _i64p, _vp = _P(C.c_int32), _P(C.c_int64), C.c_void_p
@@ -57,6 +84,18 @@ PROTOTYPES = {
     "sfmx_version": (C.c_char_p, []),
     "sfmx_last_error": (C.c_char_p, []),
     "sfmx_selftest_sqrt": (C.c_int, [C.c_int32, C.c_int64, _P(C.c_uint32)]),
+    "sfmx_ba_default_options": (C.c_int, [_P(sfmx_ba_options)]),
+    "sfmx_ba_solve": (C.c_int, [_P(sfmx_ba_problem), _P(sfmx_ba_options), _P(sfmx_ba_summary), _vp, C.c_int32]),
+    "sfmx_ba_create": (C.c_int, [_P(sfmx_ba_problem), _P(sfmx_ba_options), _P(_vp)]),
+    "sfmx_ba_set_allreduce": (C.c_int, [_vp, ALLREDUCE_FN, _vp]),
+    "sfmx_ba_run": (C.c_int, [_vp, C.c_int32, _P(sfmx_ba_summary), _vp, C.c_int32]),
+    "sfmx_ba_get": (C.c_int, [_vp, _P(sfmx_ba_problem)]),
+    "sfmx_ba_set": (C.c_int, [_vp, _P(sfmx_ba_problem)]),
+    "sfmx_ba_phase_ms": (C.c_int, [_vp, _P(C.c_double), C.c_int32]),
+    "sfmx_ba_destroy": (C.c_int, [_vp]),
+    "sfmx_ba_jacobian": (C.c_int, [_P(sfmx_ba_problem), C.c_int32, _vp, _vp, _vp, _vp]),
+    "sfmx_pose_to_ceres": (C.c_int, [_P(C.c_double), _P(C.c_double)]),
+    "sfmx_pose_from_ceres": (C.c_int, [_P(C.c_double), _P(C.c_double)]),
 }
 
 

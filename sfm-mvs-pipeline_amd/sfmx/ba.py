@@ -1,0 +1,186 @@
+"""Bundle adjustment: Python mirror of the reference's BA interface over the C ABI
+(include/sfmx_ba.h, libsfmx.so).
+
+Reference (brunothg/sfm-mvs-pipeline/src/photogrammetrie):
+  * ``BundleAdjustment::doBundleAdjustment(Scene&) -> bool``  common/BundleAdjustment.h:97,
+    returns ``termination_type == CONVERGENCE`` (BundleAdjustment.cpp:140)
+  * ``CeresUtils::solve`` with ``defaultOptions`` (DENSE_SCHUR, 5000 iterations)   util/CeresUtils.cpp:38-56
+  * ``CeresUtils::toCeresPose / toOpenCvPose``                                   util/CeresUtils.h:90-148
+  * camera models and their intrinsics block layout                               common/*Camera.cpp
+
+``BAProblem`` holds exactly the Ceres-problem data layout the reference builds
+(point[3], angle-axis pose[6], ONE shared intrinsics block[k], one residual per
+observation); all arithmetic runs in the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+from ._lib import (lib, check, sfmx_ba_problem, sfmx_ba_options, sfmx_ba_summary, ALLREDUCE_FN)
+
+CAM_SIMPLE, CAM_SIMPLE_RADIAL, CAM_DISTORTION = 1, 3, 7      # value = intrinsics size k
+CAMERA_MODELS = {"Simple": CAM_SIMPLE, "SimpleRadial": CAM_SIMPLE_RADIAL, "Distortion": CAM_DISTORTION}
+CONVERGENCE, NO_CONVERGENCE, FAILURE = 0, 1, 2
+TERMINATION_NAMES = {CONVERGENCE: "CONVERGENCE", NO_CONVERGENCE: "NO_CONVERGENCE", FAILURE: "FAILURE"}
+REDUCE_SUM, REDUCE_MAX = 0, 1
+
+
+@dataclass
+class BAProblem:
+    cam_model: int
+    points: np.ndarray          # (P, 3) float64
+    poses: np.ndarray           # (C, 6) float64 angle-axis | t
+    intr: np.ndarray            # (k,)  float64
+    obs_point: np.ndarray       # (O,)  int32
+    obs_cam: np.ndarray         # (O,)  int32
+    obs_xy: np.ndarray          # (O, 2) float64
+    cx: float = 0.0
+    cy: float = 0.0
+
+    def __post_init__(self):
+        self.points = np.ascontiguousarray(self.points, np.float64).reshape(-1, 3)
+        self.poses = np.ascontiguousarray(self.poses, np.float64).reshape(-1, 6)
+        self.intr = np.ascontiguousarray(self.intr, np.float64).reshape(-1)
+        self.obs_point = np.ascontiguousarray(self.obs_point, np.int32).reshape(-1)
+        self.obs_cam = np.ascontiguousarray(self.obs_cam, np.int32).reshape(-1)
+        self.obs_xy = np.ascontiguousarray(self.obs_xy, np.float64).reshape(-1, 2)
+        if self.cam_model not in (CAM_SIMPLE, CAM_SIMPLE_RADIAL, CAM_DISTORTION):
+            raise ValueError("cam_model must be CAM_SIMPLE, CAM_SIMPLE_RADIAL or CAM_DISTORTION")
+        if len(self.intr) != self.cam_model:
+            raise ValueError(f"intrinsics block must have {self.cam_model} entries")
+
+    def copy(self) -> "BAProblem":
+        return BAProblem(self.cam_model, self.points.copy(), self.poses.copy(), self.intr.copy(), self.obs_point,
+                         self.obs_cam, self.obs_xy, self.cx, self.cy)
+
+    def struct(self) -> sfmx_ba_problem:
+        return sfmx_ba_problem(len(self.points), len(self.poses), len(self.obs_point), self.cam_model,
+                               self.points.ctypes.data, self.poses.ctypes.data, self.intr.ctypes.data,
+                               self.obs_point.ctypes.data, self.obs_cam.ctypes.data, self.obs_xy.ctypes.data,
+                               float(self.cx), float(self.cy))
+
+
+def default_options(**kw) -> sfmx_ba_options:
+    o = sfmx_ba_options()
+    check(lib.sfmx_ba_default_options(C.byref(o)), "sfmx_ba_default_options")
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise ValueError(f"unknown option {k}")
+        setattr(o, k, v)
+    return o
+
+
+def summary_dict(s: sfmx_ba_summary) -> dict:
+    return {f: getattr(s, f) for f, _ in s._fields_}
+
+
+def solve(problem: BAProblem, options: Optional[sfmx_ba_options] = None, trace_cap: int = 0):
+    """In-place solve (problem.points/poses/intr updated) -> (summary dict, trace[n,3])."""
+    opt = options or default_options()
+    st = problem.struct()
+    sm = sfmx_ba_summary()
+    tr = np.zeros((max(trace_cap, 1), 3), np.float64)
+    n = check(lib.sfmx_ba_solve(C.byref(st), C.byref(opt), C.byref(sm), tr.ctypes.data if trace_cap else None,
+                                trace_cap), "sfmx_ba_solve")
+    return summary_dict(sm), tr[:n]
+
+
+def jacobian(problem: BAProblem, device: int = 0):
+    """Device residuals + Jacobian blocks -> (r[O,2], Je[O,2,3], Jc[O,2,6], Ji[O,2,k])."""
+    O, k = len(problem.obs_point), problem.cam_model
+    r = np.zeros((O, 2)); Je = np.zeros((O, 2, 3)); Jc = np.zeros((O, 2, 6)); Ji = np.zeros((O, 2, k))
+    st = problem.struct()
+    check(lib.sfmx_ba_jacobian(C.byref(st), device, r.ctypes.data, Je.ctypes.data, Jc.ctypes.data, Ji.ctypes.data),
+          "sfmx_ba_jacobian")
+    return r, Je, Jc, Ji
+
+
+class BAContext:
+    """HBM-resident problem (bench / multi-GPU).  ``allreduce(buf_ptr, count, op, stream)``
+    (optional) sums the reduced camera system across point-sharded ranks."""
+
+    def __init__(self, problem: BAProblem, options: Optional[sfmx_ba_options] = None, allreduce=None):
+        self.problem = problem
+        self.opt = options or default_options()
+        h = C.c_void_p()
+        st = problem.struct()
+        check(lib.sfmx_ba_create(C.byref(st), C.byref(self.opt), C.byref(h)), "sfmx_ba_create")
+        self._h = h
+        self._cb = None
+        if allreduce is not None:
+            def _cb(buf, count, op, user, stream):
+                try:
+                    allreduce(int(buf), int(count), int(op), int(stream or 0))
+                    return 0
+                except Exception:   # pragma: no cover - surfaced as SFMX_EDEVICE
+                    import traceback
+                    traceback.print_exc()
+                    return 1
+            self._cb = ALLREDUCE_FN(_cb)
+            check(lib.sfmx_ba_set_allreduce(self._h, self._cb, None), "sfmx_ba_set_allreduce")
+
+    def run(self, max_iterations: int = 0, trace_cap: int = 0):
+        sm = sfmx_ba_summary()
+        tr = np.zeros((max(trace_cap, 1), 3), np.float64)
+        n = check(lib.sfmx_ba_run(self._h, max_iterations, C.byref(sm), tr.ctypes.data if trace_cap else None,
+                                  trace_cap), "sfmx_ba_run")
+        return summary_dict(sm), tr[:n]
+
+    def reset(self, problem: Optional[BAProblem] = None):
+        st = (problem or self.problem).struct()
+        check(lib.sfmx_ba_set(self._h, C.byref(st)), "sfmx_ba_set")
+
+    def get(self, problem: Optional[BAProblem] = None) -> BAProblem:
+        p = problem or self.problem.copy()
+        st = p.struct()
+        check(lib.sfmx_ba_get(self._h, C.byref(st)), "sfmx_ba_get")
+        return p
+
+    def phase_ms(self):
+        v = (C.c_double * 4)()
+        n = check(lib.sfmx_ba_phase_ms(self._h, v, 4), "sfmx_ba_phase_ms")
+        return {k: v[i] for i, k in enumerate(["linearize", "schur", "cholesky_solve", "step_cost"][:n])}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.sfmx_ba_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def pose_to_ceres(Rt: np.ndarray) -> np.ndarray:
+    """CeresUtils::toCeresPose: 3x4 [R|t] -> {angle-axis, t}."""
+    Rt = np.ascontiguousarray(Rt, np.float64).reshape(3, 4)
+    out = np.zeros(6)
+    check(lib.sfmx_pose_to_ceres(Rt.ctypes.data_as(C.POINTER(C.c_double)), out.ctypes.data_as(C.POINTER(C.c_double))),
+          "sfmx_pose_to_ceres")
+    return out
+
+
+def pose_from_ceres(pose: np.ndarray) -> np.ndarray:
+    """CeresUtils::toOpenCvPose: {angle-axis, t} -> 3x4 [R|t]."""
+    pose = np.ascontiguousarray(pose, np.float64).reshape(6)
+    out = np.zeros((3, 4))
+    check(lib.sfmx_pose_from_ceres(pose.ctypes.data_as(C.POINTER(C.c_double)), out.ctypes.data_as(C.POINTER(C.c_double))),
+          "sfmx_pose_from_ceres")
+    return out
+
+
+class BundleAdjustment:
+    """``BundleAdjustment::doBundleAdjustment(scene)``: solve the scene's problem in
+    place and return ``termination_type == CONVERGENCE``."""
+
+    @staticmethod
+    def doBundleAdjustment(problem: BAProblem, options: Optional[sfmx_ba_options] = None) -> bool:
+        summary, _ = solve(problem, options)
+        BundleAdjustment.last_summary = summary
+        return summary["termination_type"] == CONVERGENCE

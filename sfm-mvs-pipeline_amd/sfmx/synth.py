@@ -68,3 +68,75 @@ def orb_images(n_images: int, n_desc: int, seed: int = ORB_SEED, shared: float =
         img = np.concatenate([obs, fresh], axis=0)
         out.append(np.ascontiguousarray(img[rng.permutation(n_desc)]))
     return out
+
+
+BA_SEED = 0xBA200
+
+
+def _aa_from_R(R):
+    """angle-axis of a rotation matrix (numpy, for synthetic truth only)."""
+    c = np.clip((np.trace(R) - 1) / 2, -1, 1)
+    th = np.arccos(c)
+    if th < 1e-12:
+        return np.zeros(3)
+    v = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    return v / (2 * np.sin(th)) * th
+
+
+def _R_from_aa(aa):
+    th = np.linalg.norm(aa)
+    if th < 1e-12:
+        return np.eye(3)
+    k = aa / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+
+
+def ba_problem(n_cams: int = 200, n_points: int = 200_000, obs_per_point: int = 6, noise_px: float = 0.5,
+               seed: int = BA_SEED, cam_model: int = 3, width: int = 720, height: int = 405, perturb: bool = True,
+               truth: bool = False):
+    """BASELINE config 5 shape: cameras on a ring looking at the centre (insel
+    720x405, f = 1.2 * 720 = 864 as PhotogrammetrieCli.cpp:312-314 sets it),
+    every point seen by exactly `obs_per_point` consecutive cameras, pixel noise
+    `noise_px`, initial perturbation 1e-2 rad / 1% translation / 1% f / 1e-2
+    point noise.  Observations point-major, as the reference
+    adds residual blocks (BundleAdjustment.cpp:50-90).  -> (BAProblem kwargs dict, truth dict)."""
+    rng = np.random.default_rng(seed)
+    f = 1.2 * max(width, height)
+    cx, cy = width / 2.0, height / 2.0
+    radius = 10.0
+    poses = np.zeros((n_cams, 6))
+    for c in range(n_cams):
+        ang = 2 * np.pi * c / n_cams
+        Cw = np.array([radius * np.cos(ang), radius * np.sin(ang), 0.3 * np.sin(3 * ang)])
+        z = -Cw / np.linalg.norm(Cw)
+        up = np.array([0.0, 0.0, 1.0])
+        x = np.cross(up, z); x /= np.linalg.norm(x)
+        y = np.cross(z, x)
+        R = np.stack([x, y, z])            # world -> camera rows
+        poses[c, :3] = _aa_from_R(R)
+        poses[c, 3:] = -R @ Cw
+    pts = np.concatenate([rng.uniform(-2.5, 2.5, (n_points, 2)), rng.uniform(-1.5, 1.5, (n_points, 1))], axis=1)
+    k = cam_model
+    intr = np.zeros(k)
+    intr[0] = f
+    if k == 7:
+        intr[1], intr[2] = cx, cy
+    start = rng.integers(0, n_cams, n_points)
+    obs_point = np.repeat(np.arange(n_points, dtype=np.int32), obs_per_point)
+    obs_cam = ((start[:, None] + np.arange(obs_per_point)[None, :]) % n_cams).astype(np.int32).reshape(-1)
+    Rs = np.stack([_R_from_aa(p[:3]) for p in poses])
+    Xc = np.einsum("oij,oj->oi", Rs[obs_cam], pts[obs_point]) + poses[obs_cam, 3:]
+    xy = f * Xc[:, :2] / Xc[:, 2:3]
+    xy = xy + np.array([cx, cy]) + rng.normal(0.0, noise_px, xy.shape)
+    tr = {"points": pts.copy(), "poses": poses.copy(), "intr": intr.copy()}
+    if perturb:
+        poses = poses.copy()
+        poses[:, :3] += rng.normal(0, 1e-2, (n_cams, 3))
+        poses[:, 3:] *= 1.0 + rng.normal(0, 1e-2, (n_cams, 3))
+        intr = intr.copy()
+        intr[0] *= 1.0 + 0.01 * rng.standard_normal()
+        pts = pts + rng.normal(0, 1e-2, pts.shape)
+    prob = dict(cam_model=k, points=pts, poses=poses, intr=intr, obs_point=obs_point, obs_cam=obs_cam,
+                obs_xy=xy, cx=cx, cy=cy)
+    return (prob, tr) if truth else prob
