@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--workload", choices=["sift", "orb"], default="sift")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
+    ap.add_argument("--no-ba", action="store_true", help="skip the bundle-adjustment leg")
+    ap.add_argument("--ba-cams", type=int, default=200)
+    ap.add_argument("--ba-points", type=int, default=200_000)
+    ap.add_argument("--ba-cpu-iters", type=int, default=2, help="LM iterations of the CPU BA baseline sample")
     return ap.parse_args()
 
 
@@ -124,6 +128,7 @@ def main():
     value = logical_total * args.steps / elapsed
     kern_ms = float(np.mean(main_ms))
     achieved = logical_mine * flop_per_pair / (kern_ms * 1e-3) / 1e12
+    ba_res = None if args.no_ba else bench_ba(args, rank, world, local)
     line = None
     if rank == 0:
         cpu = None
@@ -154,12 +159,63 @@ def main():
             "matches": n_matches,
             "slow_path_queries": slow,
             "fp32_fallback_pairs": f32p,
+            "ba": ba_res,
         }
         print(json.dumps(line), flush=True)
     matcher.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def bench_ba(args, rank, world, local):
+    """ms per LM iteration (BASELINE config 5): 200 cams / 200k points / 1.2M obs,
+    SimpleRadial, Ceres-1.14 LM + DENSE_SCHUR semantics.  Points sharded across
+    ranks (strong scaling), reduced camera system all-reduced over RCCL."""
+    import torch
+    import torch.distributed as dist
+    from sfmx import ba, synth
+    from sfmx.dist import shard_ba_problem, torch_allreduce
+    prob = synth.ba_problem(args.ba_cams, args.ba_points)
+    local_prob = shard_ba_problem(prob, rank, world) if world > 1 else dict(prob, point_range=(0, args.ba_points))
+    local_prob.pop("point_range")
+    opts = ba.default_options(device=local)
+    ctx = ba.BAContext(ba.BAProblem(**local_prob), opts, allreduce=torch_allreduce() if world > 1 else None)
+    ctx.run(max_iterations=1)                 # warm-up (code objects, allocations)
+    ctx.reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    sm, tr = ctx.run(trace_cap=1024)
+    phases = ctx.phase_ms()
+    ctx.close()
+    iters = sm["num_successful_steps"] + sm["num_unsuccessful_steps"]
+    ms = torch.tensor([sm["total_ms"]], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:
+        dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+    total_ms = float(ms.item())
+    res = {"metric": "ms per LM iteration", "value": total_ms / max(iters, 1), "unit": "ms", "higher_is_better": False,
+           "scaling": "strong", "n_gpus": world, "dtype": "f64",
+           "config": {"workload": f"BA {args.ba_cams} cams / {args.ba_points} points / {len(prob['obs_point'])} obs, "
+                                  "SimpleRadial, LM + DENSE_SCHUR (Ceres 1.14 defaults)", "parallelism": f"point-sharded x{world}"},
+           "iterations": iters, "successful": sm["num_successful_steps"], "initial_cost": sm["initial_cost"],
+           "final_cost": sm["final_cost"], "termination": ba.TERMINATION_NAMES[sm["termination_type"]],
+           "total_ms": total_ms, "phase_ms_rank0": phases}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            from oracle import oracle
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+            _, osm, _ = oracle.ba_solve(prob, nthreads=threads, max_num_iterations=args.ba_cpu_iters)
+            oit = osm["num_successful_steps"] + osm["num_unsuccessful_steps"]
+            res["cpu_baseline"] = {"value": osm["total_ms"] / max(oit, 1), "unit": "ms per LM iteration",
+                                   "cores": threads, "kind": "port",
+                                   "sample": f"first {oit} LM iterations (incl. iteration 0) of the same problem, "
+                                             "oracle/ba_oracle.cpp (LM + DENSE_SCHUR, OpenMP)",
+                                   "initial_cost": osm["initial_cost"]}
+            res["speedup_vs_cpu"] = res["cpu_baseline"]["value"] / res["value"]
+        except Exception as e:   # pragma: no cover
+            res["cpu_baseline"] = {"error": str(e)}
+    return res
 
 
 def cpu_baseline(imgs, pairs, target_s):

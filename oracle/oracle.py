@@ -189,10 +189,10 @@ lib.orc_ba_jacobian.argtypes = [C.POINTER(_BAProblem), C.c_void_p, C.c_void_p, C
 
 
 def _ba_struct(p: dict):
-    keep = {
-        "points": np.ascontiguousarray(p["points"], np.float64).reshape(-1, 3),
-        "poses": np.ascontiguousarray(p["poses"], np.float64).reshape(-1, 6),
-        "intr": np.ascontiguousarray(p["intr"], np.float64).reshape(-1),
+    keep = {   # parameter blocks are copied: the solver writes its result into them
+        "points": np.array(p["points"], np.float64, copy=True).reshape(-1, 3),
+        "poses": np.array(p["poses"], np.float64, copy=True).reshape(-1, 6),
+        "intr": np.array(p["intr"], np.float64, copy=True).reshape(-1),
         "obs_point": np.ascontiguousarray(p["obs_point"], np.int32).reshape(-1),
         "obs_cam": np.ascontiguousarray(p["obs_cam"], np.int32).reshape(-1),
         "obs_xy": np.ascontiguousarray(p["obs_xy"], np.float64).reshape(-1, 2),

@@ -42,9 +42,10 @@ class BAProblem:
     cy: float = 0.0
 
     def __post_init__(self):
-        self.points = np.ascontiguousarray(self.points, np.float64).reshape(-1, 3)
-        self.poses = np.ascontiguousarray(self.poses, np.float64).reshape(-1, 6)
-        self.intr = np.ascontiguousarray(self.intr, np.float64).reshape(-1)
+        # parameter blocks are owned (copied): solve() writes the result into them
+        self.points = np.array(self.points, np.float64, copy=True).reshape(-1, 3)
+        self.poses = np.array(self.poses, np.float64, copy=True).reshape(-1, 6)
+        self.intr = np.array(self.intr, np.float64, copy=True).reshape(-1)
         self.obs_point = np.ascontiguousarray(self.obs_point, np.int32).reshape(-1)
         self.obs_cam = np.ascontiguousarray(self.obs_cam, np.int32).reshape(-1)
         self.obs_xy = np.ascontiguousarray(self.obs_xy, np.float64).reshape(-1, 2)

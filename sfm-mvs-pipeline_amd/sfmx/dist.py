@@ -1,0 +1,62 @@
+"""Multi-GPU plumbing: one process per GPU, torch.distributed (RCCL over xGMI on
+MI355X, gloo on CPU for tests).
+
+* Matching shards image pairs (sfmx.shard): no collective on the data path.
+* Bundle adjustment shards POINTS (with their observations); cameras and the
+  shared intrinsics are replicated.  libsfmx calls the all-reduce hook on the
+  reduced camera system S + rhs once per LM step, on the camera/intrinsics
+  column norms once per linearisation, and on a few scalars (include/sfmx_ba.h).
+  The reference has no distributed path at all (OpenMP only).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+REDUCE_SUM, REDUCE_MAX = 0, 1
+
+
+def shard_ba_problem(prob: dict, rank: int, world: int) -> dict:
+    """Contiguous point range [P*r/W, P*(r+1)/W) with its observations; cameras and
+    intrinsics replicated.  Observation order (point-major) is preserved."""
+    P = len(prob["points"])
+    lo, hi = P * rank // world, P * (rank + 1) // world
+    op = np.asarray(prob["obs_point"])
+    sel = (op >= lo) & (op < hi)
+    out = dict(prob)
+    out["points"] = np.asarray(prob["points"])[lo:hi]
+    out["obs_point"] = (op[sel] - lo).astype(np.int32)
+    out["obs_cam"] = np.asarray(prob["obs_cam"])[sel]
+    out["obs_xy"] = np.asarray(prob["obs_xy"])[sel]
+    out["point_range"] = (lo, hi)
+    return out
+
+
+class _DevView:
+    """Zero-copy view of a raw device buffer (doubles) for torch.as_tensor."""
+
+    def __init__(self, ptr: int, count: int):
+        self.__cuda_array_interface__ = {"shape": (count,), "typestr": "<f8", "data": (ptr, False), "version": 3}
+
+
+def torch_allreduce(group=None, cpu_staging: bool = False):
+    """-> callable(ptr, count, op, stream) for sfmx.ba.BAContext(allreduce=...).
+    The collective is ordered on the solver's HIP stream (ExternalStream); with
+    cpu_staging the buffer goes through host memory (gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(ptr: int, count: int, op: int, stream: int):
+        rop = dist.ReduceOp.SUM if op == REDUCE_SUM else dist.ReduceOp.MAX
+        t = torch.as_tensor(_DevView(ptr, count), device="cuda")
+        if cpu_staging:
+            torch.cuda.synchronize()
+            h = t.cpu()
+            dist.all_reduce(h, op=rop, group=group)
+            t.copy_(h)
+            torch.cuda.synchronize()
+            return
+        s = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()
+        with torch.cuda.stream(s):
+            dist.all_reduce(t, op=rop, group=group)
+
+    return fn

@@ -81,3 +81,23 @@ def test_do_bundle_adjustment_mirror():
     before = P.points.copy()
     assert ba.BundleAdjustment.doBundleAdjustment(P) is True     # CONVERGENCE
     assert not np.array_equal(before, P.points)                  # written back in place
+
+
+def test_point_sharded_two_ranks_match_single():
+    """Point-sharded BA over 2 ranks (both on this GPU, gloo all-reduce of the
+    reduced camera system) reaches the 1-rank final cost within 1e-5."""
+    import json, os, subprocess, sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    args = ["10", "1200", "27"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                          "--master-addr=127.0.0.1", "--master-port=29531", os.path.join(here, "mp_ba_worker.py"), *args],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["cameras_identical"]
+    p = synth.ba_problem(int(args[0]), int(args[1]), seed=int(args[2]))
+    P, sm, _ = gpu_solve(p)
+    assert abs(r["initial_cost"] - sm["initial_cost"]) <= 1e-12 * sm["initial_cost"]
+    assert abs(r["final_cost"] - sm["final_cost"]) <= COST_RTOL * sm["final_cost"]
