@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-ba", action="store_true", help="skip the bundle-adjustment leg")
+    ap.add_argument("--only-ba", action="store_true", help="run only the bundle-adjustment leg (tuning)")
     ap.add_argument("--ba-cams", type=int, default=200)
     ap.add_argument("--ba-points", type=int, default=200_000)
     ap.add_argument("--ba-cpu-iters", type=int, default=2, help="LM iterations of the CPU BA baseline sample")
@@ -62,6 +63,14 @@ def main():
 
     import sfmx
     from sfmx import synth, shard
+
+    if args.only_ba:
+        res = bench_ba(args, rank, world, local)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     if args.workload == "sift":
         n_img = shard.images_for_weak_scaling(world)

@@ -354,24 +354,32 @@ __device__ __forceinline__ bool inv3_spd(const double* A, double* Ai) {
     return true;
 }
 
+// Per-observation records written by ba_point_blocks (AoS, so the gathers of
+// the Schur kernels touch whole cache lines instead of one line per field):
+//   R1[o]          (point-major, stride r1s(K) = 24 + 2K): Je_s 2x3 | U = Einv Je_s^T 3x2 | Jc_s 2x6 | Ji_s 2xK
+//   R2[campos(o)]  (camera-major, stride r2s(K) = 14 + 4K): Jc_s 2x6 | Ji_s 2xK | T = Je_s Einv V 2xK | r - q 2
+__host__ __device__ constexpr int r1s(int K) { return 24 + 2 * K; }
+__host__ __device__ constexpr int r2s(int K) { return 14 + 4 * K; }
+
 // Per point: E = sum Je_s^T Je_s + D_e^2, g_e = sum Je_s^T r, Einv, EinvG = Einv g_e,
-// V = sum Je_s^T Ji_s (3xK), Z = Einv V; per obs U = Einv Je_s^T (3x2), q = Je_s EinvG.
-// Also per-block partials of sum_p V^T Z (KxK) for the intrinsics block.
+// V = sum Je_s^T Ji_s (3xK); per observation the R1/R2 records (q = Je_s EinvG);
+// per-block partials of sum_p V^T Einv V (KxK) for the intrinsics block.
 template <int K>
 __global__ __launch_bounds__(256)
 void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, const int* __restrict__ pt_obs,
-                     const double* __restrict__ J, const double* __restrict__ scale, const double* __restrict__ D,
-                     double* __restrict__ Einv, double* __restrict__ EinvG, double* __restrict__ Zp,
-                     double* __restrict__ U, double* __restrict__ q, double* __restrict__ vzpart, int* __restrict__ fail) {
+                     const int* __restrict__ obs_cam, const int* __restrict__ campos, const double* __restrict__ J,
+                     const double* __restrict__ scale, const double* __restrict__ D, double* __restrict__ Einv,
+                     double* __restrict__ EinvG, double* __restrict__ R1, double* __restrict__ R2,
+                     double* __restrict__ vzpart, int* __restrict__ fail) {
     __shared__ double sh[8];
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     const size_t S = (size_t)O;
-    const size_t ni = 3 * (size_t)P + 6 * (size_t)C;   // first intrinsics column
+    const size_t ne = 3 * (size_t)P, ni = ne + 6 * (size_t)C;   // first camera / intrinsics column
     double VZ[K * K];
 #pragma unroll
     for (int i = 0; i < K * K; ++i) VZ[i] = 0.0;
     if (p < P) {
-        const double s0 = scale[3 * (size_t)p], s1 = scale[3 * (size_t)p + 1], s2 = scale[3 * (size_t)p + 2];
+        const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
         double si[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) si[i] = scale[ni + i];
@@ -382,12 +390,13 @@ void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, cons
         for (int a = a0; a < a1; ++a) {
             const int o = pt_obs[a];
             const double r[2] = {J[o], J[S + o]};
-            double je[2][3];
+            double je[2][3], ji[2][K];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                je[j][0] = J[(2 + 3 * j) * S + o] * s0;
-                je[j][1] = J[(3 + 3 * j) * S + o] * s1;
-                je[j][2] = J[(4 + 3 * j) * S + o] * s2;
+#pragma unroll
+                for (int u = 0; u < 3; ++u) je[j][u] = J[(2 + 3 * j + u) * S + o] * sp[u];
+#pragma unroll
+                for (int i = 0; i < K; ++i) ji[j][i] = J[(20 + K * j + i) * S + o] * si[i];
             }
 #pragma unroll
             for (int u = 0; u < 3; ++u) {
@@ -395,8 +404,7 @@ void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, cons
                 for (int v = 0; v < 3; ++v) E[u * 3 + v] += je[0][u] * je[0][v] + je[1][u] * je[1][v];
                 g[u] += je[0][u] * r[0] + je[1][u] * r[1];
 #pragma unroll
-                for (int i = 0; i < K; ++i)
-                    V[u * K + i] += je[0][u] * J[(20 + i) * S + o] * si[i] + je[1][u] * J[(20 + K + i) * S + o] * si[i];
+                for (int i = 0; i < K; ++i) V[u * K + i] += je[0][u] * ji[0][i] + je[1][u] * ji[1][i];
             }
         }
         const double d0 = D[3 * (size_t)p], d1 = D[3 * (size_t)p + 1], d2 = D[3 * (size_t)p + 2];
@@ -415,35 +423,49 @@ void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, cons
             eg[u] = Ei[u * 3] * g[0] + Ei[u * 3 + 1] * g[1] + Ei[u * 3 + 2] * g[2];
             EinvG[3 * (size_t)p + u] = eg[u];
         }
-        double Z[3 * K];
+        double Z[3 * K];   // Einv V
 #pragma unroll
         for (int u = 0; u < 3; ++u)
 #pragma unroll
-            for (int i = 0; i < K; ++i) {
-                Z[u * K + i] = Ei[u * 3] * V[i] + Ei[u * 3 + 1] * V[K + i] + Ei[u * 3 + 2] * V[2 * K + i];
-                Zp[(size_t)p * 3 * K + u * K + i] = Z[u * K + i];
-            }
+            for (int i = 0; i < K; ++i) Z[u * K + i] = Ei[u * 3] * V[i] + Ei[u * 3 + 1] * V[K + i] + Ei[u * 3 + 2] * V[2 * K + i];
 #pragma unroll
         for (int i = 0; i < K; ++i)
 #pragma unroll
             for (int l = 0; l < K; ++l) VZ[i * K + l] = V[i] * Z[l] + V[K + i] * Z[K + l] + V[2 * K + i] * Z[2 * K + l];
         for (int a = a0; a < a1; ++a) {
             const int o = pt_obs[a];
+            const size_t nc = ne + 6 * (size_t)obs_cam[o];
+            double* r1 = R1 + (size_t)o * r1s(K);
+            double* r2 = R2 + (size_t)campos[o] * r2s(K);
             double je[2][3];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                je[j][0] = J[(2 + 3 * j) * S + o] * s0;
-                je[j][1] = J[(3 + 3 * j) * S + o] * s1;
-                je[j][2] = J[(4 + 3 * j) * S + o] * s2;
+#pragma unroll
+                for (int u = 0; u < 3; ++u) { je[j][u] = J[(2 + 3 * j + u) * S + o] * sp[u]; r1[3 * j + u] = je[j][u]; }
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    const double v = J[(8 + 6 * j + i) * S + o] * scale[nc + i];
+                    r1[12 + 6 * j + i] = v;
+                    r2[6 * j + i] = v;
+                }
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    const double v = J[(20 + K * j + i) * S + o] * si[i];
+                    r1[24 + K * j + i] = v;
+                    r2[12 + K * j + i] = v;
+                }
             }
-            // U = Einv Je^T (3x2), row-major; q = Je EinvG (2)
 #pragma unroll
             for (int u = 0; u < 3; ++u)
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    U[(size_t)(u * 2 + j) * S + o] = Ei[u * 3] * je[j][0] + Ei[u * 3 + 1] * je[j][1] + Ei[u * 3 + 2] * je[j][2];
+                for (int j = 0; j < 2; ++j) r1[6 + u * 2 + j] = Ei[u * 3] * je[j][0] + Ei[u * 3 + 1] * je[j][1] + Ei[u * 3 + 2] * je[j][2];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) q[j * S + o] = je[j][0] * eg[0] + je[j][1] * eg[1] + je[j][2] * eg[2];
+            for (int j = 0; j < 2; ++j) {
+#pragma unroll
+                for (int i = 0; i < K; ++i) r2[12 + 2 * K + K * j + i] = je[j][0] * Z[i] + je[j][1] * Z[K + i] + je[j][2] * Z[2 * K + i];
+                const double qj = je[j][0] * eg[0] + je[j][1] * eg[1] + je[j][2] * eg[2];
+                r2[12 + 4 * K + j] = J[j * S + o] - qj;
+            }
         }
     }
 #pragma unroll
@@ -453,51 +475,31 @@ void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, cons
     }
 }
 
-// Per camera c (one block): Scc = sum Jc_s^T Jc_s (6x6), Spi = sum Jc_s^T Ji_s - Jc_s^T Je_s Z_p (6xK),
-// rc = sum Jc_s^T (r - q); and per-camera partials of the intrinsics parts:
-// sum Ji_s^T Ji_s (KxK) and sum Ji_s^T (r - q) (K).
+// Per camera c (one block) over its contiguous R2 records:
+// Scc = sum Jc^T Jc (6x6), Spi = sum Jc^T (Ji - T) (6xK), rc = sum Jc^T (r - q);
+// per-camera partials of sum Ji^T Ji (upper KxK) and sum Ji^T (r - q) (K).
 template <int K>
 __global__ __launch_bounds__(256)
-void ba_cam_blocks(int P, int O, int C, const int* __restrict__ cam_start, const int* __restrict__ cam_obs,
-                   const int* __restrict__ obs_point, const double* __restrict__ J, const double* __restrict__ scale,
-                   const double* __restrict__ Zp, const double* __restrict__ q, double* __restrict__ Scc,
+void ba_cam_blocks(int C, const int* __restrict__ cam_start, const double* __restrict__ R2, double* __restrict__ Scc,
                    double* __restrict__ Spi, double* __restrict__ rc, double* __restrict__ ipart) {
     __shared__ double sh[8];
     constexpr int NV = 21 + 6 * K + 6 + (K * (K + 1)) / 2 + K;   // upper 6x6, 6xK, 6, upper KxK, K
+    constexpr int NI = (K * (K + 1)) / 2 + K;
     const int c = blockIdx.x;
-    const size_t S = (size_t)O;
-    const size_t nc = 3 * (size_t)P + 6 * (size_t)c, ni = 3 * (size_t)P + 6 * (size_t)C;
-    double sc[6], si[K];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) sc[i] = scale[nc + i];
-#pragma unroll
-    for (int i = 0; i < K; ++i) si[i] = scale[ni + i];
     double v[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = 0.0;
     for (int a = cam_start[c] + threadIdx.x; a < cam_start[c + 1]; a += blockDim.x) {
-        const int o = cam_obs[a];
-        const int p = obs_point[o];
-        const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
-        double jc[2][6], ji[2][K], je[2][3], rq[2];
+        const double* r2 = R2 + (size_t)a * r2s(K);
+        double jc[2][6], ji[2][K], T[2][K], rq[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) jc[j][i] = J[(8 + 6 * j + i) * S + o] * sc[i];
+            for (int i = 0; i < 6; ++i) jc[j][i] = r2[6 * j + i];
 #pragma unroll
-            for (int i = 0; i < K; ++i) ji[j][i] = J[(20 + K * j + i) * S + o] * si[i];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) je[j][i] = J[(2 + 3 * j + i) * S + o] * sp[i];
-            rq[j] = J[j * S + o] - q[j * S + o];
+            for (int i = 0; i < K; ++i) { ji[j][i] = r2[12 + K * j + i]; T[j][i] = r2[12 + 2 * K + K * j + i]; }
+            rq[j] = r2[12 + 4 * K + j];
         }
-        // T = Je Z (2xK)
-        double T[2][K];
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-                T[j][i] = je[j][0] * Zp[(size_t)p * 3 * K + i] + je[j][1] * Zp[(size_t)p * 3 * K + K + i] +
-                          je[j][2] * Zp[(size_t)p * 3 * K + 2 * K + i];
         int e = 0;
 #pragma unroll
         for (int u = 0; u < 6; ++u)
@@ -516,15 +518,14 @@ void ba_cam_blocks(int P, int O, int C, const int* __restrict__ cam_start, const
 #pragma unroll
         for (int i = 0; i < K; ++i) v[e++] += ji[0][i] * rq[0] + ji[1][i] * rq[1];
     }
-    constexpr int NI = (K * (K + 1)) / 2 + K;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
         const double s = block_sum(v[i], sh);
         if (threadIdx.x == 0) {
             if (i < 21) {
-                int u = 0, w = 0, e = i;
+                int u = 0, e = i;
                 while (e >= 6 - u) { e -= 6 - u; ++u; }
-                w = u + e;
+                const int w = u + e;
                 Scc[36 * (size_t)c + u * 6 + w] = s;
                 Scc[36 * (size_t)c + w * 6 + u] = s;
             } else if (i < 21 + 6 * K) {
@@ -538,85 +539,72 @@ void ba_cam_blocks(int P, int O, int C, const int* __restrict__ cam_start, const
     }
 }
 
-// Intrinsics block: Sii = sum_c ipart_JiJi - sum_blocks VZ, ri = sum_c ipart_Jir (fixed order).
+// Intrinsics block, one 256-thread block per output (fixed-order tree sums):
+// outputs 0..K*K-1: Sii = sum_c JiJi - sym(sum_blocks V^T Einv V); K*K..K*K+K-1: ri.
 template <int K>
-__global__ void ba_intr_final(int C, int nvz, const double* __restrict__ ipart, const double* __restrict__ vzpart,
-                              double* __restrict__ Sii, double* __restrict__ ri) {
+__global__ __launch_bounds__(256)
+void ba_intr_final(int C, int nvz, const double* __restrict__ ipart, const double* __restrict__ vzpart,
+                   double* __restrict__ Sii, double* __restrict__ ri) {
+    __shared__ double sh[8];
     constexpr int NI = (K * (K + 1)) / 2 + K;
-    const int t = threadIdx.x;
+    const int t = blockIdx.x;
     if (t < K * K) {
         const int i = t / K, l = t % K;
         const int a = i < l ? i : l, b = i < l ? l : i;
         int e = 0;
         for (int u = 0; u < a; ++u) e += K - u;
         e += b - a;
-        double s = 0;
-        for (int c = 0; c < C; ++c) s += ipart[(size_t)c * NI + e];
-        double z = 0;
-        for (int bk = 0; bk < nvz; ++bk) z += vzpart[(size_t)bk * K * K + i * K + l];
-        // symmetrise V^T Z (exactly symmetric in exact arithmetic)
-        double z2 = 0;
-        for (int bk = 0; bk < nvz; ++bk) z2 += vzpart[(size_t)bk * K * K + l * K + i];
-        Sii[t] = s - 0.5 * (z + z2);
-    } else if (t < K * K + K) {
+        double s = 0.0, z = 0.0;
+        for (int c = threadIdx.x; c < C; c += blockDim.x) s += ipart[(size_t)c * NI + e];
+        for (int bk = threadIdx.x; bk < nvz; bk += blockDim.x)
+            z += 0.5 * (vzpart[(size_t)bk * K * K + i * K + l] + vzpart[(size_t)bk * K * K + l * K + i]);
+        const double tot = block_sum(s - z, sh);
+        if (threadIdx.x == 0) Sii[t] = tot;
+    } else {
         const int i = t - K * K;
-        double s = 0;
-        for (int c = 0; c < C; ++c) s += ipart[(size_t)c * NI + (K * (K + 1)) / 2 + i];
-        ri[i] = s;
+        double s = 0.0;
+        for (int c = threadIdx.x; c < C; c += blockDim.x) s += ipart[(size_t)c * NI + (K * (K + 1)) / 2 + i];
+        const double tot = block_sum(s, sh);
+        if (threadIdx.x == 0) ri[i] = tot;
     }
 }
 
-// Off-diagonal / same-camera pose blocks: for block b = (c1 <= c2) with its
-// segment of ordered observation pairs (o1 in c1, o2 in c2, same point):
+// Pose blocks: for block b = (c1 <= c2) with its segment of ordered observation
+// pairs (o1 in c1, o2 in c2, same point):
 //   Spp_b = - sum Jc_s(o1)^T [Je_s(o1) U(o2)] Jc_s(o2)     (U = Einv Je_s^T)
-// one workgroup per block, fixed-order tree sum (deterministic).
+// one workgroup per block, fixed-order tree sum (deterministic); R1 gathers.
+template <int K>
 __global__ __launch_bounds__(256)
-void ba_pair_blocks(int P, int O, const int* __restrict__ blk_cam, const int* __restrict__ blk_start,
-                    const int2* __restrict__ trip, const int* __restrict__ obs_point, const double* __restrict__ J,
-                    const double* __restrict__ scale, const double* __restrict__ U, double* __restrict__ Spp) {
+void ba_pair_blocks(const int* __restrict__ blk_start, const int2* __restrict__ trip, const double* __restrict__ R1,
+                    double* __restrict__ Spp) {
     __shared__ double sh[8];
     const int b = blockIdx.x;
-    const int c1 = blk_cam[2 * b], c2 = blk_cam[2 * b + 1];
-    const size_t S = (size_t)O;
-    double s1[6], s2[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) { s1[i] = scale[3 * (size_t)P + 6 * (size_t)c1 + i]; s2[i] = scale[3 * (size_t)P + 6 * (size_t)c2 + i]; }
     double acc[36];
 #pragma unroll
     for (int i = 0; i < 36; ++i) acc[i] = 0.0;
     for (int t = blk_start[b] + threadIdx.x; t < blk_start[b + 1]; t += blockDim.x) {
         const int2 tr = trip[t];
-        const int o1 = tr.x, o2 = tr.y;
-        const int p = obs_point[o1];
-        const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
+        const double* x1 = R1 + (size_t)tr.x * r1s(K);
+        const double* x2 = R1 + (size_t)tr.y * r1s(K);
+        double je1[6], u2[6], a1[12], a2[12];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { je1[i] = x1[i]; u2[i] = x2[6 + i]; }
+#pragma unroll
+        for (int i = 0; i < 12; ++i) { a1[i] = x1[12 + i]; a2[i] = x2[12 + i]; }
         double M[2][2];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int l = 0; l < 2; ++l) {
-                double m = 0;
-#pragma unroll
-                for (int u = 0; u < 3; ++u) m += J[(2 + 3 * j + u) * S + o1] * sp[u] * U[(size_t)(u * 2 + l) * S + o2];
-                M[j][l] = m;
-            }
-        double a1[2][6], a2[2][6];
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                a1[j][i] = J[(8 + 6 * j + i) * S + o1] * s1[i];
-                a2[j][i] = J[(8 + 6 * j + i) * S + o2] * s2[i];
-            }
-        // T = M a2 (2x6); acc += a1^T T
+            for (int l = 0; l < 2; ++l) M[j][l] = je1[3 * j] * u2[l] + je1[3 * j + 1] * u2[2 + l] + je1[3 * j + 2] * u2[4 + l];
         double T[2][6];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int i = 0; i < 6; ++i) T[j][i] = M[j][0] * a2[0][i] + M[j][1] * a2[1][i];
+            for (int i = 0; i < 6; ++i) T[j][i] = M[j][0] * a2[i] + M[j][1] * a2[6 + i];
 #pragma unroll
         for (int u = 0; u < 6; ++u)
 #pragma unroll
-            for (int w = 0; w < 6; ++w) acc[u * 6 + w] += a1[0][u] * T[0][w] + a1[1][u] * T[1][w];
+            for (int w = 0; w < 6; ++w) acc[u * 6 + w] += a1[u] * T[0][w] + a1[6 + u] * T[1][w];
     }
 #pragma unroll
     for (int i = 0; i < 36; ++i) {
@@ -683,57 +671,89 @@ __global__ void ba_add_damping(int P, int nf, int npad, const double* __restrict
 }
 
 // ---- dense Cholesky (lower, row-major, in place), NB x NB tiles ------------
-// potrf of diagonal tile k (one 256-thread block, tile in LDS).
+// potrf of diagonal tile k (one 256-thread block, tile in LDS): right-looking
+// LDL^T-form update with deferred column scaling (one barrier per column), then
+// L = L~ sqrt(D); also writes Linv_k = L_kk^-1 (lower) for the GEMM-form trsm
+// and the triangular solves.
 __global__ __launch_bounds__(256)
-void chol_potrf(double* __restrict__ A, int npad, int k, int* __restrict__ fail) {
+void chol_potrf(double* __restrict__ A, int npad, int k, double* __restrict__ Linv, int* __restrict__ fail) {
     __shared__ double T[NB][NB + 1];
+    __shared__ double dg[NB];
     const int k0 = k * NB;
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) T[e / NB][e % NB] = A[(size_t)(k0 + e / NB) * npad + k0 + e % NB];
     __syncthreads();
     for (int j = 0; j < NB; ++j) {
-        if (threadIdx.x == 0) {
-            const double d = T[j][j];
-            if (!(d > 0.0) || !isfinite(d)) { atomicOr(fail, 1); T[j][j] = 1.0; }
-            else T[j][j] = sqrt(d);
+        double d = T[j][j];
+        if (!(d > 0.0) || !isfinite(d)) {
+            if (threadIdx.x == 0) atomicOr(fail, 1);
+            d = 1.0;
         }
-        __syncthreads();
-        const double djj = T[j][j];
-        for (int i = j + 1 + threadIdx.x; i < NB; i += blockDim.x) T[i][j] /= djj;
-        __syncthreads();
-        for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-            const int i = e / NB, l = e % NB;
-            if (i > j && l > j && l <= i) T[i][l] -= T[i][j] * T[l][j];
+        if (threadIdx.x == 0) dg[j] = d;
+        const double inv = 1.0 / d;
+        const int m = NB - 1 - j;   // trailing size
+        for (int e = threadIdx.x; e < m * m; e += blockDim.x) {
+            const int i = j + 1 + e / m, l = j + 1 + e % m;
+            if (l <= i) T[i][l] -= T[i][j] * T[l][j] * inv;
         }
         __syncthreads();
     }
+    // L, back to A (upper part zeroed)
     for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
         const int i = e / NB, l = e % NB;
-        A[(size_t)(k0 + i) * npad + k0 + l] = l <= i ? T[i][l] : 0.0;
-    }
-}
-
-// trsm: tiles (i, k) for i > k: L_ik = A_ik L_kk^-T.  One block per tile row i.
-__global__ __launch_bounds__(256)
-void chol_trsm(double* __restrict__ A, int npad, int k) {
-    __shared__ double L[NB][NB + 1];
-    __shared__ double X[NB][NB + 1];
-    const int k0 = k * NB, i0 = (k + 1 + blockIdx.x) * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-        L[e / NB][e % NB] = A[(size_t)(k0 + e / NB) * npad + k0 + e % NB];
-        X[e / NB][e % NB] = A[(size_t)(i0 + e / NB) * npad + k0 + e % NB];
+        double v = 0.0;
+        if (l == i) v = sqrt(dg[i]);
+        else if (l < i) v = T[i][l] / sqrt(dg[l]);
+        A[(size_t)(k0 + i) * npad + k0 + l] = v;
     }
     __syncthreads();
-    // rows of X are independent: x_j = (a_j - sum_{l<j} x_l L[j][l]) / L[j][j]
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+        const int i = e / NB, l = e % NB;
+        T[i][l] = A[(size_t)(k0 + i) * npad + k0 + l];
+    }
+    __syncthreads();
+    // Linv: column c solves L x = e_c by forward substitution (independent per c)
+    __shared__ double X[NB][NB + 1];
     if (threadIdx.x < NB) {
-        const int r = threadIdx.x;
-        for (int j = 0; j < NB; ++j) {
-            double s = X[r][j];
-            for (int l = 0; l < j; ++l) s -= X[r][l] * L[j][l];
-            X[r][j] = s / L[j][j];
+        const int c = threadIdx.x;
+        for (int i = 0; i < NB; ++i) {
+            if (i < c) { X[i][c] = 0.0; continue; }
+            double s = (i == c) ? 1.0 : 0.0;
+            for (int l = c; l < i; ++l) s -= T[i][l] * X[l][c];
+            X[i][c] = s / T[i][i];
         }
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) A[(size_t)(i0 + e / NB) * npad + k0 + e % NB] = X[e / NB][e % NB];
+    double* Lk = Linv + (size_t)k * NB * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) Lk[e] = X[e / NB][e % NB];
+}
+
+// trsm as GEMM: tiles (i, k), i > k: L_ik = A_ik Linv_k^T.  One block per tile row i.
+__global__ __launch_bounds__(256)
+void chol_trsm(double* __restrict__ A, int npad, int k, const double* __restrict__ Linv) {
+    __shared__ double Li[NB][NB + 1];
+    __shared__ double Xa[NB][NB + 1];
+    const int k0 = k * NB, i0 = (k + 1 + blockIdx.x) * NB;
+    const double* Lk = Linv + (size_t)k * NB * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+        Li[e / NB][e % NB] = Lk[e];
+        Xa[e / NB][e % NB] = A[(size_t)(i0 + e / NB) * npad + k0 + e % NB];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    double acc[4][4] = {};
+    for (int l = 0; l < NB; ++l) {
+        double a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { a[u] = Xa[ty * 4 + u][l]; b[u] = Li[tx * 4 + u][l]; }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) acc[u][w] += a[u] * b[w];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) A[(size_t)(i0 + ty * 4 + u) * npad + k0 + tx * 4 + w] = acc[u][w];
 }
 
 // Trailing update A_ij -= L_ik L_jk^T for k < j <= i (lower tiles).  Block per tile.
@@ -741,10 +761,9 @@ __global__ __launch_bounds__(256)
 void chol_update(double* __restrict__ A, int npad, int k, int T) {
     __shared__ double Li[NB][NB + 1];
     __shared__ double Lj[NB][NB + 1];
-    // decode linear tile index -> (i, j), j <= i, both in (k, T)
     int rem = blockIdx.x, i = k + 1, j;
     for (;; ++i) {
-        const int cnt = i - k;   // tiles j = k+1..i
+        const int cnt = i - k;
         if (rem < cnt) { j = k + 1 + rem; break; }
         rem -= cnt;
     }
@@ -754,7 +773,6 @@ void chol_update(double* __restrict__ A, int npad, int k, int T) {
         Lj[e / NB][e % NB] = A[(size_t)(j0 + e / NB) * npad + k0 + e % NB];
     }
     __syncthreads();
-    // each thread: 4x4 outputs (rows ty*4.., cols tx*4..), 16x16 threads
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     double acc[4][4] = {};
     for (int l = 0; l < NB; ++l) {
@@ -772,45 +790,44 @@ void chol_update(double* __restrict__ A, int npad, int k, int T) {
         for (int w = 0; w < 4; ++w) A[(size_t)(i0 + ty * 4 + u) * npad + j0 + tx * 4 + w] -= acc[u][w];
 }
 
-// Solve L L^T x = b in place (one 1024-thread block; NB-row blocks, wave 0
-// does the diagonal solves with shuffles, all threads do the updates).
+// Solve L L^T x = b in place (one 1024-thread block) with the diagonal-tile
+// inverses: forward y_k = Linv_k (b_k - sum_{l<k} L_kl y_l), backward
+// x_k = Linv_k^T (y_k - sum_{l>k} L_lk^T x_l); every step is a GEMV.
 __global__ __launch_bounds__(1024)
-void chol_solve(const double* __restrict__ L, int npad, double* __restrict__ b) {
+void chol_solve(const double* __restrict__ L, const double* __restrict__ Linv, int npad, double* __restrict__ b) {
     __shared__ double y[NB];
+    __shared__ double bk[NB];
     const int T = npad / NB;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int k = 0; k < T; ++k) {                 // forward L y = b
+    for (int k = 0; k < T; ++k) {
         const int k0 = k * NB;
-        if (wid == 0) {
-            double v = b[k0 + lane];
-            for (int j = 0; j < NB; ++j) {
-                const double yj = __shfl(v, j) / L[(size_t)(k0 + j) * npad + k0 + j];
-                if (lane == j) v = yj;
-                if (lane > j) v -= L[(size_t)(k0 + lane) * npad + k0 + j] * yj;
-            }
-            b[k0 + lane] = v;
-            y[lane] = v;
+        if (threadIdx.x < NB) bk[threadIdx.x] = b[k0 + threadIdx.x];
+        __syncthreads();
+        if (threadIdx.x < NB) {
+            const double* Lk = Linv + (size_t)k * NB * NB + (size_t)threadIdx.x * NB;
+            double s = 0;
+            for (int l = 0; l <= (int)threadIdx.x; ++l) s += Lk[l] * bk[l];
+            y[threadIdx.x] = s;
+            b[k0 + threadIdx.x] = s;
         }
         __syncthreads();
         for (int r = k0 + NB + threadIdx.x; r < npad; r += blockDim.x) {
-            double s = 0;
             const double* row = L + (size_t)r * npad + k0;
+            double s = 0;
             for (int l = 0; l < NB; ++l) s += row[l] * y[l];
             b[r] -= s;
         }
         __syncthreads();
     }
-    for (int k = T - 1; k >= 0; --k) {            // backward L^T x = y
+    for (int k = T - 1; k >= 0; --k) {
         const int k0 = k * NB;
-        if (wid == 0) {
-            double v = b[k0 + lane];
-            for (int j = NB - 1; j >= 0; --j) {
-                const double xj = __shfl(v, j) / L[(size_t)(k0 + j) * npad + k0 + j];
-                if (lane == j) v = xj;
-                if (lane < j) v -= L[(size_t)(k0 + j) * npad + k0 + lane] * xj;
-            }
-            b[k0 + lane] = v;
-            y[lane] = v;
+        if (threadIdx.x < NB) bk[threadIdx.x] = b[k0 + threadIdx.x];
+        __syncthreads();
+        if (threadIdx.x < NB) {
+            const double* Lk = Linv + (size_t)k * NB * NB;
+            double s = 0;
+            for (int l = threadIdx.x; l < NB; ++l) s += Lk[(size_t)l * NB + threadIdx.x] * bk[l];
+            y[threadIdx.x] = s;
+            b[k0 + threadIdx.x] = s;
         }
         __syncthreads();
         for (int r = threadIdx.x; r < k0; r += blockDim.x) {
@@ -822,29 +839,31 @@ void chol_solve(const double* __restrict__ L, int npad, double* __restrict__ b) 
     }
 }
 
-// x_e = EinvG - sum_o U_o (F_o x_f), F_o = [Jc_s | Ji_s]
+// x_e = EinvG - sum_o U_o (F_o x_f), F_o = [Jc_s | Ji_s]   (R1 records)
 template <int K>
 __global__ __launch_bounds__(256)
-void ba_backsub(int P, int O, int C, const int* __restrict__ pt_start, const int* __restrict__ pt_obs,
-                const int* __restrict__ obs_cam, const double* __restrict__ J, const double* __restrict__ scale,
-                const double* __restrict__ U, const double* __restrict__ EinvG, const double* __restrict__ xf,
-                double* __restrict__ xe) {
+void ba_backsub(int P, int C, const int* __restrict__ pt_start, const int* __restrict__ pt_obs,
+                const int* __restrict__ obs_cam, const double* __restrict__ R1, const double* __restrict__ EinvG,
+                const double* __restrict__ xf, double* __restrict__ xe) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
-    const size_t S = (size_t)O, ne = 3 * (size_t)P;
+    double xi[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) xi[i] = xf[6 * C + i];
     double v[3] = {EinvG[3 * (size_t)p], EinvG[3 * (size_t)p + 1], EinvG[3 * (size_t)p + 2]};
     for (int a = pt_start[p]; a < pt_start[p + 1]; ++a) {
         const int o = pt_obs[a], c = obs_cam[o];
+        const double* r1 = R1 + (size_t)o * r1s(K);
         double f[2] = {0, 0};
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) f[j] += J[(8 + 6 * j + i) * S + o] * scale[ne + 6 * (size_t)c + i] * xf[6 * c + i];
+            for (int i = 0; i < 6; ++i) f[j] += r1[12 + 6 * j + i] * xf[6 * c + i];
 #pragma unroll
-            for (int i = 0; i < K; ++i) f[j] += J[(20 + K * j + i) * S + o] * scale[ne + 6 * (size_t)C + i] * xf[6 * C + i];
+            for (int i = 0; i < K; ++i) f[j] += r1[24 + K * j + i] * xi[i];
         }
 #pragma unroll
-        for (int u = 0; u < 3; ++u) v[u] -= U[(size_t)(u * 2) * S + o] * f[0] + U[(size_t)(u * 2 + 1) * S + o] * f[1];
+        for (int u = 0; u < 3; ++u) v[u] -= r1[6 + u * 2] * f[0] + r1[6 + u * 2 + 1] * f[1];
     }
 #pragma unroll
     for (int u = 0; u < 3; ++u) xe[3 * (size_t)p + u] = v[u];

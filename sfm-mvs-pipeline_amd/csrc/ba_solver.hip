@@ -68,17 +68,18 @@ struct sfmx_ba_ctx {
     sfmx_allreduce_fn ar = nullptr;
     void* ar_user = nullptr;
     // topology
-    Buf obs_point, obs_cam, obs_xy, pt_start, pt_obs, cam_start, cam_obs, blk_cam, blk_start, trip;
+    Buf obs_point, obs_cam, obs_xy, pt_start, pt_obs, cam_start, cam_obs, campos, blk_cam, blk_start, trip;
     // state
     Buf x, cand, scale, colsq, grad, diag, D, J, partA, partB, scal, ipart;
-    Buf Einv, EinvG, Zp, U, q, vzpart, Scc, Spi, Sii, rc, ri, Spp, SR, sol, step, failf;
+    Buf Einv, EinvG, R1, R2, vzpart, Scc, Spi, Sii, rc, ri, Spp, SR, Linv, sol, step, failf;
     bool scaled = false;
     double phase_ms[4] = {0, 0, 0, 0};
     hipEvent_t ev[6] = {};
     ~sfmx_ba_ctx() {
-        Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &pt_obs, &cam_start, &cam_obs, &blk_cam, &blk_start,
-                      &trip, &x, &cand, &scale, &colsq, &grad, &diag, &D, &J, &partA, &partB, &scal, &ipart,
-                      &Einv, &EinvG, &Zp, &U, &q, &vzpart, &Scc, &Spi, &Sii, &rc, &ri, &Spp, &SR, &sol, &step, &failf};
+        Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &pt_obs, &cam_start, &cam_obs, &campos, &blk_cam,
+                      &blk_start, &trip, &x, &cand, &scale, &colsq, &grad, &diag, &D, &J, &partA, &partB, &scal,
+                      &ipart, &Einv, &EinvG, &R1, &R2, &vzpart, &Scc, &Spi, &Sii, &rc, &ri, &Spp, &SR, &Linv, &sol,
+                      &step, &failf};
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
@@ -190,24 +191,22 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     hipLaunchKernelGGL(ba_lm_d, dim3(nblk(c->n)), dim3(256), 0, c->st, (int)c->n, c->diag.as<double>(), radius,
                        c->D.as<double>());
     HIPCHK(hipMemsetAsync(fl, 0, sizeof(int), c->st));
-#define SCHUR(KK)                                                                                                            \
-    hipLaunchKernelGGL(ba_point_blocks<KK>, dim3(c->nvz), dim3(256), 0, c->st, P, O, C, c->pt_start.as<int>(),               \
-                       c->pt_obs.as<int>(), c->J.as<double>(), c->scale.as<double>(), c->D.as<double>(),                     \
-                       c->Einv.as<double>(), c->EinvG.as<double>(), c->Zp.as<double>(), c->U.as<double>(), c->q.as<double>(), \
-                       c->vzpart.as<double>(), fl);                                                                          \
-    if (C > 0)                                                                                                               \
-        hipLaunchKernelGGL(ba_cam_blocks<KK>, dim3(C), dim3(256), 0, c->st, P, O, C, c->cam_start.as<int>(),                 \
-                           c->cam_obs.as<int>(), c->obs_point.as<int>(), c->J.as<double>(), c->scale.as<double>(),           \
-                           c->Zp.as<double>(), c->q.as<double>(), c->Scc.as<double>(), c->Spi.as<double>(),                  \
-                           c->rc.as<double>(), c->ipart.as<double>());                                                       \
-    hipLaunchKernelGGL(ba_intr_final<KK>, dim3(1), dim3(64), 0, c->st, C, c->nvz, c->ipart.as<double>(),                     \
-                       c->vzpart.as<double>(), c->Sii.as<double>(), c->ri.as<double>())
+#define SCHUR(KK)                                                                                                      \
+    hipLaunchKernelGGL(ba_point_blocks<KK>, dim3(c->nvz), dim3(256), 0, c->st, P, O, C, c->pt_start.as<int>(),         \
+                       c->pt_obs.as<int>(), c->obs_cam.as<int>(), c->campos.as<int>(), c->J.as<double>(),              \
+                       c->scale.as<double>(), c->D.as<double>(), c->Einv.as<double>(), c->EinvG.as<double>(),          \
+                       c->R1.as<double>(), c->R2.as<double>(), c->vzpart.as<double>(), fl);                            \
+    if (C > 0)                                                                                                         \
+        hipLaunchKernelGGL(ba_cam_blocks<KK>, dim3(C), dim3(256), 0, c->st, C, c->cam_start.as<int>(),                 \
+                           c->R2.as<double>(), c->Scc.as<double>(), c->Spi.as<double>(), c->rc.as<double>(),           \
+                           c->ipart.as<double>());                                                                     \
+    hipLaunchKernelGGL(ba_intr_final<KK>, dim3(KK * KK + KK), dim3(256), 0, c->st, C, c->nvz, c->ipart.as<double>(),   \
+                       c->vzpart.as<double>(), c->Sii.as<double>(), c->ri.as<double>());                               \
+    if (c->nblocks > 0)                                                                                                \
+        hipLaunchKernelGGL(ba_pair_blocks<KK>, dim3(c->nblocks), dim3(256), 0, c->st, c->blk_start.as<int>(),          \
+                           c->trip.as<int2>(), c->R1.as<double>(), c->Spp.as<double>())
     if (K == 1) { SCHUR(1); } else if (K == 3) { SCHUR(3); } else { SCHUR(7); }
 #undef SCHUR
-    if (c->nblocks > 0)
-        hipLaunchKernelGGL(ba_pair_blocks, dim3(c->nblocks), dim3(256), 0, c->st, P, O, c->blk_cam.as<int>(),
-                           c->blk_start.as<int>(), c->trip.as<int2>(), c->obs_point.as<int>(), c->J.as<double>(),
-                           c->scale.as<double>(), c->U.as<double>(), c->Spp.as<double>());
     HIPCHK(hipMemsetAsync(S, 0, sizeof(double) * ((size_t)npad * npad + npad), c->st));
     if (c->nblocks > 0)
         hipLaunchKernelGGL(ba_assemble_pairs, dim3(c->nblocks), dim3(64), 0, c->st, npad, c->blk_cam.as<int>(),
@@ -221,19 +220,18 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     RC(allreduce(c, S, (int64_t)npad * npad + npad, SFMX_REDUCE_SUM));
     hipLaunchKernelGGL(ba_add_damping, dim3(nblk(c->nf)), dim3(256), 0, c->st, P, c->nf, npad, c->D.as<double>(), S);
     for (int k = 0; k < T; ++k) {
-        hipLaunchKernelGGL(chol_potrf, dim3(1), dim3(256), 0, c->st, S, npad, k, fl);
+        hipLaunchKernelGGL(chol_potrf, dim3(1), dim3(256), 0, c->st, S, npad, k, c->Linv.as<double>(), fl);
         if (k + 1 < T) {
-            hipLaunchKernelGGL(chol_trsm, dim3(T - k - 1), dim3(256), 0, c->st, S, npad, k);
+            hipLaunchKernelGGL(chol_trsm, dim3(T - k - 1), dim3(256), 0, c->st, S, npad, k, c->Linv.as<double>());
             hipLaunchKernelGGL(chol_update, dim3((T - k - 1) * (T - k) / 2), dim3(256), 0, c->st, S, npad, k, T);
         }
     }
-    hipLaunchKernelGGL(chol_solve, dim3(1), dim3(1024), 0, c->st, S, npad, rhs);
+    hipLaunchKernelGGL(chol_solve, dim3(1), dim3(1024), 0, c->st, S, c->Linv.as<double>(), npad, rhs);
     double* sol = c->sol.as<double>();
     HIPCHK(hipMemcpyAsync(sol + c->ne, rhs, sizeof(double) * c->nf, hipMemcpyDeviceToDevice, c->st));
 #define BACK(KK)                                                                                                    \
-    hipLaunchKernelGGL(ba_backsub<KK>, dim3(nblk(P)), dim3(256), 0, c->st, P, O, C, c->pt_start.as<int>(),          \
-                       c->pt_obs.as<int>(), c->obs_cam.as<int>(), c->J.as<double>(), c->scale.as<double>(),         \
-                       c->U.as<double>(), c->EinvG.as<double>(), rhs, sol)
+    hipLaunchKernelGGL(ba_backsub<KK>, dim3(nblk(P)), dim3(256), 0, c->st, P, C, c->pt_start.as<int>(),              \
+                       c->pt_obs.as<int>(), c->obs_cam.as<int>(), c->R1.as<double>(), c->EinvG.as<double>(), rhs, sol)
     if (K == 1) { BACK(1); } else if (K == 3) { BACK(3); } else { BACK(7); }
 #undef BACK
     HIPCHK(hipGetLastError());
@@ -437,6 +435,8 @@ int create(const sfmx_ba_problem* pb, const sfmx_ba_options* opt, sfmx_ba_ctx** 
         std::vector<int> fp(pt_start.begin(), pt_start.end() - 1), fc(cam_start.begin(), cam_start.end() - 1);
         for (int i = 0; i < O; ++i) { pt_obs[fp[pb->obs_point[i]]++] = i; cam_obs[fc[pb->obs_cam[i]]++] = i; }
     }
+    std::vector<int> campos(O);   // position of each observation in the camera-major order
+    for (int a = 0; a < O; ++a) campos[cam_obs[a]] = a;
     // camera-pair blocks of the reduced system: ordered observation pairs of
     // each point with cam(a) <= cam(b), bucketed by (cam(a), cam(b)) (point order inside a bucket)
     std::unordered_map<int64_t, int> bid;
@@ -477,6 +477,7 @@ int create(const sfmx_ba_problem* pb, const sfmx_ba_options* opt, sfmx_ba_ctx** 
     if ((rc = upload(c->obs_point, op, st)) || (rc = upload(c->obs_cam, oc, st)) || (rc = upload(c->obs_xy, oxy, st)) ||
         (rc = upload(c->pt_start, pt_start, st)) || (rc = upload(c->pt_obs, pt_obs, st)) ||
         (rc = upload(c->cam_start, cam_start, st)) || (rc = upload(c->cam_obs, cam_obs, st)) ||
+        (rc = upload(c->campos, campos, st)) ||
         (rc = upload(c->blk_cam, blk_cam, st)) || (rc = upload(c->blk_start, blk_start, st)) ||
         (rc = upload(c->trip, trip, st)))
         return bail(rc);
@@ -488,8 +489,8 @@ int create(const sfmx_ba_problem* pb, const sfmx_ba_options* opt, sfmx_ba_ctx** 
         {&c->J, 8 * so * (20 + 2 * K)}, {&c->partA, 8 * (size_t)nblk(std::max<int64_t>(O, n))},
         {&c->partB, 8 * (size_t)nblk(std::max<int64_t>(O, n))}, {&c->scal, 8 * 16},
         {&c->ipart, 8 * (size_t)std::max(C, 1) * NI}, {&c->Einv, 72 * (size_t)std::max(P, 1)},
-        {&c->EinvG, 24 * (size_t)std::max(P, 1)}, {&c->Zp, 24 * (size_t)K * std::max(P, 1)},
-        {&c->U, 48 * so}, {&c->q, 16 * so}, {&c->vzpart, 8 * (size_t)c->nvz * K * K},
+        {&c->EinvG, 24 * (size_t)std::max(P, 1)}, {&c->R1, 8 * so * r1s(K)}, {&c->R2, 8 * so * r2s(K)},
+        {&c->vzpart, 8 * (size_t)c->nvz * K * K}, {&c->Linv, 8 * (size_t)c->T * NB * NB},
         {&c->Scc, 288 * (size_t)std::max(C, 1)}, {&c->Spi, 48 * (size_t)K * std::max(C, 1)}, {&c->Sii, 8 * (size_t)K * K},
         {&c->rc, 48 * (size_t)std::max(C, 1)}, {&c->ri, 8 * (size_t)K}, {&c->Spp, 288 * (size_t)std::max(NBLK, 1)},
         {&c->SR, 8 * ((size_t)c->npad * c->npad + c->npad)}, {&c->failf, 64}};
