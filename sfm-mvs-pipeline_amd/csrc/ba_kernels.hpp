@@ -671,60 +671,63 @@ __global__ void ba_add_damping(int P, int nf, int npad, const double* __restrict
 }
 
 // ---- dense Cholesky (lower, row-major, in place), NB x NB tiles ------------
-// potrf of diagonal tile k (one 256-thread block, tile in LDS): right-looking
-// LDL^T-form update with deferred column scaling (one barrier per column), then
-// L = L~ sqrt(D); also writes Linv_k = L_kk^-1 (lower) for the GEMM-form trsm
-// and the triangular solves.
-__global__ __launch_bounds__(256)
-void chol_potrf(double* __restrict__ A, int npad, int k, double* __restrict__ Linv, int* __restrict__ fail) {
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffff), l);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// potrf of diagonal tile k by ONE wave, tile in LDS, lane i owns row i:
+// LDL^T form (M[i][l] -= M[i][j] M[l][j] / d_j; column j read by broadcast),
+// then L = L~ sqrt(D).  A single wave needs no barriers (LDS is in order per wave).
+__global__ __launch_bounds__(64)
+void chol_potrf(double* __restrict__ A, int npad, int k, int* __restrict__ fail) {
     __shared__ double T[NB][NB + 1];
     __shared__ double dg[NB];
-    const int k0 = k * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) T[e / NB][e % NB] = A[(size_t)(k0 + e / NB) * npad + k0 + e % NB];
+    const int i = threadIdx.x, k0 = k * NB;
+    const double* arow = A + (size_t)(k0 + i) * npad + k0;
+    for (int l = 0; l < NB; ++l) T[i][l] = arow[l];
     __syncthreads();
+    bool bad = false;
     for (int j = 0; j < NB; ++j) {
         double d = T[j][j];
-        if (!(d > 0.0) || !isfinite(d)) {
-            if (threadIdx.x == 0) atomicOr(fail, 1);
-            d = 1.0;
-        }
-        if (threadIdx.x == 0) dg[j] = d;
-        const double inv = 1.0 / d;
-        const int m = NB - 1 - j;   // trailing size
-        for (int e = threadIdx.x; e < m * m; e += blockDim.x) {
-            const int i = j + 1 + e / m, l = j + 1 + e % m;
-            if (l <= i) T[i][l] -= T[i][j] * T[l][j] * inv;
-        }
-        __syncthreads();
+        if (!(d > 0.0) || !isfinite(d)) { bad = true; d = 1.0; }
+        if (i == 0) dg[j] = d;
+        const double a = T[i][j] / d;
+#pragma unroll 8
+        for (int l = j + 1; l < NB; ++l) T[i][l] -= a * T[l][j];
+        __builtin_amdgcn_wave_barrier();
     }
-    // L, back to A (upper part zeroed)
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-        const int i = e / NB, l = e % NB;
+    if (bad && i == 0) atomicOr(fail, 1);
+    __syncthreads();
+    double* wrow = A + (size_t)(k0 + i) * npad + k0;
+    for (int l = 0; l < NB; ++l) {
         double v = 0.0;
         if (l == i) v = sqrt(dg[i]);
         else if (l < i) v = T[i][l] / sqrt(dg[l]);
-        A[(size_t)(k0 + i) * npad + k0 + l] = v;
+        wrow[l] = v;
     }
-    __syncthreads();
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-        const int i = e / NB, l = e % NB;
-        T[i][l] = A[(size_t)(k0 + i) * npad + k0 + l];
-    }
-    __syncthreads();
-    // Linv: column c solves L x = e_c by forward substitution (independent per c)
-    __shared__ double X[NB][NB + 1];
-    if (threadIdx.x < NB) {
-        const int c = threadIdx.x;
-        for (int i = 0; i < NB; ++i) {
-            if (i < c) { X[i][c] = 0.0; continue; }
-            double s = (i == c) ? 1.0 : 0.0;
-            for (int l = c; l < i; ++l) s -= T[i][l] * X[l][c];
-            X[i][c] = s / T[i][i];
-        }
-    }
+}
+
+// Linv_k = L_kk^-1 (lower), one wave: lane c solves L x = e_c by forward
+// substitution, the tile's rows broadcast from LDS.
+__global__ __launch_bounds__(64)
+void chol_trinv(const double* __restrict__ A, int npad, int k, double* __restrict__ Linv) {
+    __shared__ double Ls[NB][NB + 1];
+    const int c = threadIdx.x, k0 = k * NB;
+    for (int l = 0; l < NB; ++l) Ls[l][c] = A[(size_t)(k0 + l) * npad + k0 + c];
     __syncthreads();
     double* Lk = Linv + (size_t)k * NB * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) Lk[e] = X[e / NB][e % NB];
+    double x[NB];
+#pragma unroll
+    for (int ii = 0; ii < NB; ++ii) {
+        double s = (ii == c) ? 1.0 : 0.0;
+#pragma unroll
+        for (int l = 0; l < ii; ++l) s -= Ls[ii][l] * x[l];
+        x[ii] = (ii >= c) ? s / Ls[ii][ii] : 0.0;
+        Lk[(size_t)ii * NB + c] = x[ii];
+    }
 }
 
 // trsm as GEMM: tiles (i, k), i > k: L_ik = A_ik Linv_k^T.  One block per tile row i.
@@ -792,29 +795,31 @@ void chol_update(double* __restrict__ A, int npad, int k, int T) {
 
 // Solve L L^T x = b in place (one 1024-thread block) with the diagonal-tile
 // inverses: forward y_k = Linv_k (b_k - sum_{l<k} L_kl y_l), backward
-// x_k = Linv_k^T (y_k - sum_{l>k} L_lk^T x_l); every step is a GEMV.
+// x_k = Linv_k^T (y_k - sum_{l>k} L_lk^T x_l); every step is a GEMV.  Forward
+// row updates: one wave per row (coalesced 512-B row segment + wave reduce).
 __global__ __launch_bounds__(1024)
 void chol_solve(const double* __restrict__ L, const double* __restrict__ Linv, int npad, double* __restrict__ b) {
     __shared__ double y[NB];
     __shared__ double bk[NB];
     const int T = npad / NB;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
     for (int k = 0; k < T; ++k) {
         const int k0 = k * NB;
         if (threadIdx.x < NB) bk[threadIdx.x] = b[k0 + threadIdx.x];
         __syncthreads();
-        if (threadIdx.x < NB) {
-            const double* Lk = Linv + (size_t)k * NB * NB + (size_t)threadIdx.x * NB;
+        if (wid == 0) {   // y = Linv_k bk : lane t row t (lower)
+            const double* Lk = Linv + (size_t)k * NB * NB + (size_t)lane * NB;
             double s = 0;
-            for (int l = 0; l <= (int)threadIdx.x; ++l) s += Lk[l] * bk[l];
-            y[threadIdx.x] = s;
-            b[k0 + threadIdx.x] = s;
+            for (int l = 0; l <= lane; ++l) s += Lk[l] * bk[l];
+            y[lane] = s;
+            b[k0 + lane] = s;
         }
         __syncthreads();
-        for (int r = k0 + NB + threadIdx.x; r < npad; r += blockDim.x) {
-            const double* row = L + (size_t)r * npad + k0;
-            double s = 0;
-            for (int l = 0; l < NB; ++l) s += row[l] * y[l];
-            b[r] -= s;
+        const double yl = y[lane];
+        for (int r = k0 + NB + wid; r < npad; r += nw) {
+            double s = L[(size_t)r * npad + k0 + lane] * yl;
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+            if (lane == 0) b[r] -= s;
         }
         __syncthreads();
     }
@@ -822,16 +827,17 @@ void chol_solve(const double* __restrict__ L, const double* __restrict__ Linv, i
         const int k0 = k * NB;
         if (threadIdx.x < NB) bk[threadIdx.x] = b[k0 + threadIdx.x];
         __syncthreads();
-        if (threadIdx.x < NB) {
+        if (wid == 0) {   // x = Linv_k^T bk : lane t column t (upper of the transpose)
             const double* Lk = Linv + (size_t)k * NB * NB;
             double s = 0;
-            for (int l = threadIdx.x; l < NB; ++l) s += Lk[(size_t)l * NB + threadIdx.x] * bk[l];
-            y[threadIdx.x] = s;
-            b[k0 + threadIdx.x] = s;
+            for (int l = lane; l < NB; ++l) s += Lk[(size_t)l * NB + lane] * bk[l];
+            y[lane] = s;
+            b[k0 + lane] = s;
         }
         __syncthreads();
         for (int r = threadIdx.x; r < k0; r += blockDim.x) {
             double s = 0;
+#pragma unroll 8
             for (int l = 0; l < NB; ++l) s += L[(size_t)(k0 + l) * npad + r] * y[l];
             b[r] -= s;
         }

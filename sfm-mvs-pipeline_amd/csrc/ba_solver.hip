@@ -220,7 +220,8 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     RC(allreduce(c, S, (int64_t)npad * npad + npad, SFMX_REDUCE_SUM));
     hipLaunchKernelGGL(ba_add_damping, dim3(nblk(c->nf)), dim3(256), 0, c->st, P, c->nf, npad, c->D.as<double>(), S);
     for (int k = 0; k < T; ++k) {
-        hipLaunchKernelGGL(chol_potrf, dim3(1), dim3(256), 0, c->st, S, npad, k, c->Linv.as<double>(), fl);
+        hipLaunchKernelGGL(chol_potrf, dim3(1), dim3(64), 0, c->st, S, npad, k, fl);
+        hipLaunchKernelGGL(chol_trinv, dim3(1), dim3(64), 0, c->st, S, npad, k, c->Linv.as<double>());
         if (k + 1 < T) {
             hipLaunchKernelGGL(chol_trsm, dim3(T - k - 1), dim3(256), 0, c->st, S, npad, k, c->Linv.as<double>());
             hipLaunchKernelGGL(chol_update, dim3((T - k - 1) * (T - k) / 2), dim3(256), 0, c->st, S, npad, k, T);
