@@ -14,11 +14,11 @@
 //   ba_pair_blocks    per co-visible camera pair: -sum W_a^T E^-1 W_b, one
 //                     workgroup per 6x6 block, fixed-order tree sums (deterministic)
 //   ba_assemble       dense reduced camera system S ((6C+k) padded to 64)
-//   chol_*            blocked right-looking Cholesky (64x64 tiles) + triangular solves
+//   chol_*            block LDL^T of S (64x64 tiles, one launch per panel) + solves
 //   ba_backsub / ba_step / ba_model / ba_cost
 // Layout in HBM: parameters x = [points 3P | poses 6C | intrinsics k]; the
-// Jacobian is stored field-major J[f][o] (f = r0,r1, Je 2x3, Jc 2x6, Ji 2xk) so
-// observation-parallel kernels read and write coalesced.
+// Jacobian is stored per observation, J[o][f] (f = r0,r1, Je 2x3, Jc 2x6, Ji 2xk,
+// stride jst(K) = 20 + 2k): every gather (by point, by camera) reads whole records.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -28,6 +28,7 @@ namespace sfmx {
 namespace ba {
 
 constexpr int NB = 64;   // Cholesky tile
+__host__ __device__ constexpr int jst(int K) { return 20 + 2 * K; }   // Jacobian record stride
 
 // ---- dual numbers --------------------------------------------------------
 template <int N>
@@ -164,16 +165,15 @@ void ba_linearize(int O, const int* __restrict__ obs_point, const int* __restric
 #pragma unroll
             for (int i = 0; i < K; ++i) in[i] = jvar<N>(intr[i], 9 + i);
             project<K, N>(X, ps, in, ox, oy, cx, cy, res);
-            const size_t S = (size_t)O;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                J[j * S + o] = res[j].a;
+                J[(size_t)o * jst(K) + j] = res[j].a;
 #pragma unroll
-                for (int i = 0; i < 3; ++i) J[(2 + 3 * j + i) * S + o] = res[j].v[i];
+                for (int i = 0; i < 3; ++i) J[(size_t)o * jst(K) + (2 + 3 * j + i)] = res[j].v[i];
 #pragma unroll
-                for (int i = 0; i < 6; ++i) J[(8 + 6 * j + i) * S + o] = res[j].v[3 + i];
+                for (int i = 0; i < 6; ++i) J[(size_t)o * jst(K) + (8 + 6 * j + i)] = res[j].v[3 + i];
 #pragma unroll
-                for (int i = 0; i < K; ++i) J[(20 + K * j + i) * S + o] = res[j].v[9 + i];
+                for (int i = 0; i < K; ++i) J[(size_t)o * jst(K) + (20 + K * j + i)] = res[j].v[9 + i];
             }
             c2 = res[0].a * res[0].a + res[1].a * res[1].a;
         } else {
@@ -210,14 +210,13 @@ void ba_point_cols(int P, int O, const int* __restrict__ pt_start, const int* __
                    const double* __restrict__ J, double* __restrict__ colsq, double* __restrict__ grad) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
-    const size_t S = (size_t)O;
     double cs[3] = {0, 0, 0}, g[3] = {0, 0, 0};
     for (int a = pt_start[p]; a < pt_start[p + 1]; ++a) {
         const int o = pt_obs[a];
-        const double r0 = J[o], r1 = J[S + o];
+        const double r0 = J[(size_t)o * jst(K)], r1 = J[(size_t)o * jst(K) + 1];
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const double j0 = J[(2 + i) * S + o], j1 = J[(5 + i) * S + o];
+            const double j0 = J[(size_t)o * jst(K) + (2 + i)], j1 = J[(size_t)o * jst(K) + (5 + i)];
             cs[i] += j0 * j0 + j1 * j1;
             g[i] += j0 * r0 + j1 * r1;
         }
@@ -234,22 +233,21 @@ void ba_cam_cols(int O, const int* __restrict__ cam_start, const int* __restrict
                  double* __restrict__ colsq, double* __restrict__ grad, double* __restrict__ ipart) {
     __shared__ double sh[8];
     const int c = blockIdx.x;
-    const size_t S = (size_t)O;
     double v[12 + 2 * K];
 #pragma unroll
     for (int i = 0; i < 12 + 2 * K; ++i) v[i] = 0.0;
     for (int a = cam_start[c] + threadIdx.x; a < cam_start[c + 1]; a += blockDim.x) {
         const int o = cam_obs[a];
-        const double r0 = J[o], r1 = J[S + o];
+        const double r0 = J[(size_t)o * jst(K)], r1 = J[(size_t)o * jst(K) + 1];
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            const double j0 = J[(8 + i) * S + o], j1 = J[(14 + i) * S + o];
+            const double j0 = J[(size_t)o * jst(K) + (8 + i)], j1 = J[(size_t)o * jst(K) + (14 + i)];
             v[i] += j0 * j0 + j1 * j1;
             v[6 + i] += j0 * r0 + j1 * r1;
         }
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            const double j0 = J[(20 + i) * S + o], j1 = J[(20 + K + i) * S + o];
+            const double j0 = J[(size_t)o * jst(K) + (20 + i)], j1 = J[(size_t)o * jst(K) + (20 + K + i)];
             v[12 + i] += j0 * j0 + j1 * j1;
             v[12 + K + i] += j0 * r0 + j1 * r1;
         }
@@ -373,7 +371,6 @@ void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, cons
                      double* __restrict__ vzpart, int* __restrict__ fail) {
     __shared__ double sh[8];
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t S = (size_t)O;
     const size_t ne = 3 * (size_t)P, ni = ne + 6 * (size_t)C;   // first camera / intrinsics column
     double VZ[K * K];
 #pragma unroll
@@ -389,14 +386,14 @@ void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, cons
         const int a0 = pt_start[p], a1 = pt_start[p + 1];
         for (int a = a0; a < a1; ++a) {
             const int o = pt_obs[a];
-            const double r[2] = {J[o], J[S + o]};
+            const double r[2] = {J[(size_t)o * jst(K)], J[(size_t)o * jst(K) + 1]};
             double je[2][3], ji[2][K];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
 #pragma unroll
-                for (int u = 0; u < 3; ++u) je[j][u] = J[(2 + 3 * j + u) * S + o] * sp[u];
+                for (int u = 0; u < 3; ++u) je[j][u] = J[(size_t)o * jst(K) + (2 + 3 * j + u)] * sp[u];
 #pragma unroll
-                for (int i = 0; i < K; ++i) ji[j][i] = J[(20 + K * j + i) * S + o] * si[i];
+                for (int i = 0; i < K; ++i) ji[j][i] = J[(size_t)o * jst(K) + (20 + K * j + i)] * si[i];
             }
 #pragma unroll
             for (int u = 0; u < 3; ++u) {
@@ -441,16 +438,16 @@ void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, cons
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
 #pragma unroll
-                for (int u = 0; u < 3; ++u) { je[j][u] = J[(2 + 3 * j + u) * S + o] * sp[u]; r1[3 * j + u] = je[j][u]; }
+                for (int u = 0; u < 3; ++u) { je[j][u] = J[(size_t)o * jst(K) + (2 + 3 * j + u)] * sp[u]; r1[3 * j + u] = je[j][u]; }
 #pragma unroll
                 for (int i = 0; i < 6; ++i) {
-                    const double v = J[(8 + 6 * j + i) * S + o] * scale[nc + i];
+                    const double v = J[(size_t)o * jst(K) + (8 + 6 * j + i)] * scale[nc + i];
                     r1[12 + 6 * j + i] = v;
                     r2[6 * j + i] = v;
                 }
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
-                    const double v = J[(20 + K * j + i) * S + o] * si[i];
+                    const double v = J[(size_t)o * jst(K) + (20 + K * j + i)] * si[i];
                     r1[24 + K * j + i] = v;
                     r2[12 + K * j + i] = v;
                 }
@@ -464,7 +461,7 @@ void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, cons
 #pragma unroll
                 for (int i = 0; i < K; ++i) r2[12 + 2 * K + K * j + i] = je[j][0] * Z[i] + je[j][1] * Z[K + i] + je[j][2] * Z[2 * K + i];
                 const double qj = je[j][0] * eg[0] + je[j][1] * eg[1] + je[j][2] * eg[2];
-                r2[12 + 4 * K + j] = J[j * S + o] - qj;
+                r2[12 + 4 * K + j] = J[(size_t)o * jst(K) + j] - qj;
             }
         }
     }
@@ -670,179 +667,211 @@ __global__ void ba_add_damping(int P, int nf, int npad, const double* __restrict
     S[(size_t)i * npad + i] += d * d;
 }
 
-// ---- dense Cholesky (lower, row-major, in place), NB x NB tiles ------------
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const long long u = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffff), l);
-    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+// ---- dense factorisation of the reduced camera system, NB x NB tiles -----
+// Block LDL^T, right-looking, one launch per panel: A = L~ D~ L~^T with
+// D~_k the (updated) diagonal tile and L~_ak = A_ak W_k, W_k = D~_k^-1.  A
+// pivot of D~_k is a pivot of the scalar Cholesky, so "not positive definite"
+// is detected exactly where LLT (Ceres DENSE_SCHUR) fails.  Storage in S
+// (row-major, npad x npad):
+//   lower tiles (a, b), a > b : A, updated in place until consumed
+//   upper tile (k, a), a > k  : L~_ak^T (for the back solve)
+// W_k lives in a ping-pong buffer; rhs is overwritten with w = D~^-1 L~^-1 b
+// during the factorisation, then with x by the back solve.
+constexpr int LDT = NB + 2;   // LDS row stride (doubles): 16-B aligned rows
+
+__device__ __forceinline__ void tile_load(double (*dst)[LDT], const double* __restrict__ src, int ld, bool transpose) {
+    double v[NB * NB / 256];
+#pragma unroll
+    for (int q = 0; q < NB * NB / 256; ++q) {
+        const int e = q * 256 + threadIdx.x;
+        v[q] = src[(size_t)(e / NB) * ld + e % NB];
+    }
+#pragma unroll
+    for (int q = 0; q < NB * NB / 256; ++q) {
+        const int e = q * 256 + threadIdx.x;
+        if (transpose) dst[e % NB][e / NB] = v[q];
+        else dst[e / NB][e % NB] = v[q];
+    }
 }
 
-// potrf of diagonal tile k by ONE wave, tile in LDS, lane i owns row i:
-// LDL^T form (M[i][l] -= M[i][j] M[l][j] / d_j; column j read by broadcast),
-// then L = L~ sqrt(D).  A single wave needs no barriers (LDS is in order per wave).
-__global__ __launch_bounds__(64)
-void chol_potrf(double* __restrict__ A, int npad, int k, int* __restrict__ fail) {
-    __shared__ double T[NB][NB + 1];
-    __shared__ double dg[NB];
-    const int i = threadIdx.x, k0 = k * NB;
-    const double* arow = A + (size_t)(k0 + i) * npad + k0;
-    for (int l = 0; l < NB; ++l) T[i][l] = arow[l];
-    __syncthreads();
+// acc[u][w] = sum_l At[l][4ty+u] * Bt[l][4tx+w]   (= (A B^T) for At = A^T, Bt = B^T)
+__device__ __forceinline__ void tile_gemm(const double (*At)[LDT], const double (*Bt)[LDT], double acc[4][4]) {
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) acc[u][w] = 0.0;
+#pragma unroll 4
+    for (int l = 0; l < NB; ++l) {
+        const double2 a01 = *reinterpret_cast<const double2*>(&At[l][4 * ty]);
+        const double2 a23 = *reinterpret_cast<const double2*>(&At[l][4 * ty + 2]);
+        const double2 b01 = *reinterpret_cast<const double2*>(&Bt[l][4 * tx]);
+        const double2 b23 = *reinterpret_cast<const double2*>(&Bt[l][4 * tx + 2]);
+        const double a[4] = {a01.x, a01.y, a23.x, a23.y}, b[4] = {b01.x, b01.y, b23.x, b23.y};
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) acc[u][w] = fma(a[u], b[w], acc[u][w]);
+    }
+}
+
+// 1/d: hardware estimate + two Newton steps (within an ulp or so of the divide).
+__device__ __forceinline__ double rcp_nr(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+
+// W_k = D~_k^-1 by symmetric sweeps (256 threads, thread (ty, tx) holds the
+// 4x4 block at rows 4ty.., cols 4tx..; one barrier per pivot).  Sweeping
+// pivot j: a_il -= a_ij a_jl / d (i, l != j), a_jl = a_jl / d, a_jj = -1/d;
+// after all pivots the tile holds -A^-1.  Then rhs_k <- W_k rhs_k.
+__device__ __forceinline__ void chol_diag_tile(double* __restrict__ S, int npad, int k, double* __restrict__ Wout,
+                                               double* __restrict__ rhs, int* __restrict__ fail, double (*buf)[LDT],
+                                               double (*colT)[NB]) {
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4, k0 = k * NB;
+    double t[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const double* row = S + (size_t)(k0 + 4 * ty + u) * npad + k0 + 4 * tx;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) t[u][w] = row[w];
+    }
     bool bad = false;
-    for (int j = 0; j < NB; ++j) {
-        double d = T[j][j];
-        if (!(d > 0.0) || !isfinite(d)) { bad = true; d = 1.0; }
-        if (i == 0) dg[j] = d;
-        const double a = T[i][j] / d;
-#pragma unroll 8
-        for (int l = j + 1; l < NB; ++l) T[i][l] -= a * T[l][j];
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (bad && i == 0) atomicOr(fail, 1);
-    __syncthreads();
-    double* wrow = A + (size_t)(k0 + i) * npad + k0;
-    for (int l = 0; l < NB; ++l) {
-        double v = 0.0;
-        if (l == i) v = sqrt(dg[i]);
-        else if (l < i) v = T[i][l] / sqrt(dg[l]);
-        wrow[l] = v;
-    }
-}
-
-// Linv_k = L_kk^-1 (lower), one wave: lane c solves L x = e_c by forward
-// substitution, the tile's rows broadcast from LDS.
-__global__ __launch_bounds__(64)
-void chol_trinv(const double* __restrict__ A, int npad, int k, double* __restrict__ Linv) {
-    __shared__ double Ls[NB][NB + 1];
-    const int c = threadIdx.x, k0 = k * NB;
-    for (int l = 0; l < NB; ++l) Ls[l][c] = A[(size_t)(k0 + l) * npad + k0 + c];
-    __syncthreads();
-    double* Lk = Linv + (size_t)k * NB * NB;
-    double x[NB];
+    for (int jb = 0; jb < NB / 4; ++jb) {
 #pragma unroll
-    for (int ii = 0; ii < NB; ++ii) {
-        double s = (ii == c) ? 1.0 : 0.0;
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * jb + jj, p = jj & 1;
+            if (tx == jb) {
 #pragma unroll
-        for (int l = 0; l < ii; ++l) s -= Ls[ii][l] * x[l];
-        x[ii] = (ii >= c) ? s / Ls[ii][ii] : 0.0;
-        Lk[(size_t)ii * NB + c] = x[ii];
+                for (int u = 0; u < 4; ++u) { colT[p][4 * ty + u] = t[u][jj]; t[u][jj] = 0.0; }
+            }
+            if (ty == jb) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) t[jj][w] = 0.0;
+            }
+            __syncthreads();
+            double d = colT[p][j];
+            if (!(d > 0.0) || !isfinite(d)) { bad = true; d = 1.0; }
+            const double r = rcp_nr(d);
+            double m[4], cl[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) m[u] = (4 * ty + u == j) ? -r : colT[p][4 * ty + u] * r;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) cl[w] = (4 * tx + w == j) ? -1.0 : colT[p][4 * tx + w];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int w = 0; w < 4; ++w) t[u][w] = fma(-m[u], cl[w], t[u][w]);
+        }
     }
-}
-
-// trsm as GEMM: tiles (i, k), i > k: L_ik = A_ik Linv_k^T.  One block per tile row i.
-__global__ __launch_bounds__(256)
-void chol_trsm(double* __restrict__ A, int npad, int k, const double* __restrict__ Linv) {
-    __shared__ double Li[NB][NB + 1];
-    __shared__ double Xa[NB][NB + 1];
-    const int k0 = k * NB, i0 = (k + 1 + blockIdx.x) * NB;
-    const double* Lk = Linv + (size_t)k * NB * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-        Li[e / NB][e % NB] = Lk[e];
-        Xa[e / NB][e % NB] = A[(size_t)(i0 + e / NB) * npad + k0 + e % NB];
-    }
-    __syncthreads();
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    double acc[4][4] = {};
-    for (int l = 0; l < NB; ++l) {
-        double a[4], b[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) { a[u] = Xa[ty * 4 + u][l]; b[u] = Li[tx * 4 + u][l]; }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int w = 0; w < 4; ++w) acc[u][w] += a[u] * b[w];
-    }
+    if (bad && tid == 0) atomicOr(fail, 1);
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int w = 0; w < 4; ++w) A[(size_t)(i0 + ty * 4 + u) * npad + k0 + tx * 4 + w] = acc[u][w];
-}
-
-// Trailing update A_ij -= L_ik L_jk^T for k < j <= i (lower tiles).  Block per tile.
-__global__ __launch_bounds__(256)
-void chol_update(double* __restrict__ A, int npad, int k, int T) {
-    __shared__ double Li[NB][NB + 1];
-    __shared__ double Lj[NB][NB + 1];
-    int rem = blockIdx.x, i = k + 1, j;
-    for (;; ++i) {
-        const int cnt = i - k;
-        if (rem < cnt) { j = k + 1 + rem; break; }
-        rem -= cnt;
-    }
-    const int i0 = i * NB, j0 = j * NB, k0 = k * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-        Li[e / NB][e % NB] = A[(size_t)(i0 + e / NB) * npad + k0 + e % NB];
-        Lj[e / NB][e % NB] = A[(size_t)(j0 + e / NB) * npad + k0 + e % NB];
+        for (int w = 0; w < 4; ++w) {
+            buf[4 * ty + u][4 * tx + w] = -t[u][w];
+            Wout[(4 * ty + u) * NB + 4 * tx + w] = -t[u][w];
+        }
+    __syncthreads();
+    if (tid < NB) {
+        double s = 0.0;
+        for (int c = 0; c < NB; ++c) s = fma(buf[tid][c], rhs[k0 + c], s);
+        colT[0][tid] = s;
     }
     __syncthreads();
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    double acc[4][4] = {};
-    for (int l = 0; l < NB; ++l) {
-        double a[4], b[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) { a[u] = Li[ty * 4 + u][l]; b[u] = Lj[tx * 4 + u][l]; }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int w = 0; w < 4; ++w) acc[u][w] += a[u] * b[w];
+    if (tid < NB) rhs[k0 + tid] = colT[0][tid];
+}
+
+struct alignas(16) CholLds {
+    double a[NB][LDT], m[NB][LDT], n[NB][LDT];
+    double colT[2][NB];
+};
+
+__global__ __launch_bounds__(256)
+void chol_first(double* __restrict__ S, int npad, double* __restrict__ W, double* __restrict__ rhs,
+                int* __restrict__ fail) {
+    __shared__ CholLds sm;
+    chol_diag_tile(S, npad, 0, W, rhs, fail, sm.a, sm.colT);
+}
+
+// Panel k: one block per trailing lower tile (a, b), k < b <= a.  Block 0 is
+// (k+1, k+1); after its update it inverts that tile for panel k+1.
+//   G = A_ak W_k
+//   b <  a : A_ab -= G A_bk^T
+//   b == a : A_aa -= G A_ak^T;  G^T -> upper tile (k, a);  rhs_a -= A_ak w_k (= G z_k)
+__global__ __launch_bounds__(256)
+void chol_step(double* __restrict__ S, int npad, int k, double* __restrict__ W, double* __restrict__ rhs,
+               int* __restrict__ fail) {
+    __shared__ CholLds sm;
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    int a = k + 1, b = k + 1;
+    if (blockIdx.x > 0) {   // tile rows a >= k + 2 hold a - k tiles (b = k+1 .. a)
+        int rem = blockIdx.x - 1;
+        for (a = k + 2; rem >= a - k; ++a) rem -= a - k;
+        b = k + 1 + rem;
     }
+    const int k0 = k * NB, a0 = a * NB, b0 = b * NB;
+    const bool diagblk = (a == b);
+    tile_load(sm.a, S + (size_t)a0 * npad + k0, npad, true);                   // A_ak^T
+    tile_load(sm.m, W + (size_t)(k & 1) * NB * NB, NB, false);                 // W_k
+    if (!diagblk) tile_load(sm.n, S + (size_t)b0 * npad + k0, npad, true);     // A_bk^T
+    __syncthreads();
+    double g[4][4];
+    tile_gemm(sm.a, sm.m, g);   // G[i][j] = sum_l A_ak[i][l] W[l][j]
+    __syncthreads();
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int w = 0; w < 4; ++w) A[(size_t)(i0 + ty * 4 + u) * npad + j0 + tx * 4 + w] -= acc[u][w];
+        for (int w = 0; w < 4; ++w) sm.m[4 * tx + w][4 * ty + u] = g[u][w];   // G^T
+    __syncthreads();
+    double upd[4][4];
+    tile_gemm(sm.m, diagblk ? sm.a : sm.n, upd);
+    double* dst = S + (size_t)a0 * npad + b0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) dst[(size_t)(4 * ty + u) * npad + 4 * tx + w] -= upd[u][w];
+    if (diagblk) {
+        // upper tile (k, a): row k0 + j, column a0 + i holds G[i][j] = G^T[j][i]
+        for (int e = tid; e < NB * NB; e += 256) S[(size_t)(k0 + e / NB) * npad + a0 + e % NB] = sm.m[e / NB][e % NB];
+        if (tid < NB) {
+            double s = 0.0;
+            for (int j = 0; j < NB; ++j) s = fma(sm.a[j][tid], rhs[k0 + j], s);   // G z_k = A_ak w_k
+            rhs[a0 + tid] -= s;
+        }
+    }
+    if (blockIdx.x == 0) {
+        __syncthreads();
+        chol_diag_tile(S, npad, k + 1, W + (size_t)((k + 1) & 1) * NB * NB, rhs, fail, sm.n, sm.colT);
+    }
 }
 
-// Solve L L^T x = b in place (one 1024-thread block) with the diagonal-tile
-// inverses: forward y_k = Linv_k (b_k - sum_{l<k} L_kl y_l), backward
-// x_k = Linv_k^T (y_k - sum_{l>k} L_lk^T x_l); every step is a GEMV.  Forward
-// row updates: one wave per row (coalesced 512-B row segment + wave reduce).
-__global__ __launch_bounds__(1024)
-void chol_solve(const double* __restrict__ L, const double* __restrict__ Linv, int npad, double* __restrict__ b) {
-    __shared__ double y[NB];
-    __shared__ double bk[NB];
-    const int T = npad / NB;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int k = 0; k < T; ++k) {
-        const int k0 = k * NB;
-        if (threadIdx.x < NB) bk[threadIdx.x] = b[k0 + threadIdx.x];
-        __syncthreads();
-        if (wid == 0) {   // y = Linv_k bk : lane t row t (lower)
-            const double* Lk = Linv + (size_t)k * NB * NB + (size_t)lane * NB;
-            double s = 0;
-            for (int l = 0; l <= lane; ++l) s += Lk[l] * bk[l];
-            y[lane] = s;
-            b[k0 + lane] = s;
-        }
-        __syncthreads();
-        const double yl = y[lane];
-        for (int r = k0 + NB + wid; r < npad; r += nw) {
-            double s = L[(size_t)r * npad + k0 + lane] * yl;
-            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-            if (lane == 0) b[r] -= s;
-        }
-        __syncthreads();
+// Back substitution L~^T x = w, panel k (descending): x_k = rhs_k is final;
+// block 0 stores it (rows < nf) into xout, every block i < k does
+// rhs_i -= L~_ki^T x_k (upper tile (i, k)).
+__global__ __launch_bounds__(256)
+void chol_back(const double* __restrict__ S, int npad, int nf, int k, double* __restrict__ rhs,
+               double* __restrict__ xout) {
+    __shared__ double xk[NB];
+    const int tid = threadIdx.x, k0 = k * NB;
+    if (tid < NB) {
+        const double v = rhs[k0 + tid];
+        xk[tid] = v;
+        if (blockIdx.x == 0 && k0 + tid < nf) xout[k0 + tid] = v;
     }
-    for (int k = T - 1; k >= 0; --k) {
-        const int k0 = k * NB;
-        if (threadIdx.x < NB) bk[threadIdx.x] = b[k0 + threadIdx.x];
-        __syncthreads();
-        if (wid == 0) {   // x = Linv_k^T bk : lane t column t (upper of the transpose)
-            const double* Lk = Linv + (size_t)k * NB * NB;
-            double s = 0;
-            for (int l = lane; l < NB; ++l) s += Lk[(size_t)l * NB + lane] * bk[l];
-            y[lane] = s;
-            b[k0 + lane] = s;
-        }
-        __syncthreads();
-        for (int r = threadIdx.x; r < k0; r += blockDim.x) {
-            double s = 0;
-#pragma unroll 8
-            for (int l = 0; l < NB; ++l) s += L[(size_t)(k0 + l) * npad + r] * y[l];
-            b[r] -= s;
-        }
-        __syncthreads();
-    }
+    __syncthreads();
+    if (blockIdx.x >= k) return;
+    const int i0 = blockIdx.x * NB, r = tid >> 2, qq = tid & 3;
+    const double* U = S + (size_t)(i0 + r) * npad + k0;
+    double t = 0.0;
+#pragma unroll 4
+    for (int m = 0; m < NB / 4; ++m) t = fma(U[4 * m + qq], xk[4 * m + qq], t);
+    t += __shfl_xor(t, 1);
+    t += __shfl_xor(t, 2);
+    if (qq == 0) rhs[i0 + r] -= t;
 }
 
 // x_e = EinvG - sum_o U_o (F_o x_f), F_o = [Jc_s | Ji_s]   (R1 records)
@@ -901,7 +930,7 @@ void ba_model(int P, int O, int C, const int* __restrict__ obs_point, const int*
               double* __restrict__ part) {
     __shared__ double sh[8];
     const int o = blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t S = (size_t)O, ne = 3 * (size_t)P;
+    const size_t ne = 3 * (size_t)P;
     double acc = 0.0;
     if (o < O) {
         const int p = obs_point[o], c = obs_cam[o];
@@ -909,12 +938,12 @@ void ba_model(int P, int O, int C, const int* __restrict__ obs_point, const int*
         for (int j = 0; j < 2; ++j) {
             double m = 0;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) m += J[(2 + 3 * j + i) * S + o] * scale[3 * (size_t)p + i] * step[3 * (size_t)p + i];
+            for (int i = 0; i < 3; ++i) m += J[(size_t)o * jst(K) + (2 + 3 * j + i)] * scale[3 * (size_t)p + i] * step[3 * (size_t)p + i];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) m += J[(8 + 6 * j + i) * S + o] * scale[ne + 6 * (size_t)c + i] * step[ne + 6 * (size_t)c + i];
+            for (int i = 0; i < 6; ++i) m += J[(size_t)o * jst(K) + (8 + 6 * j + i)] * scale[ne + 6 * (size_t)c + i] * step[ne + 6 * (size_t)c + i];
 #pragma unroll
-            for (int i = 0; i < K; ++i) m += J[(20 + K * j + i) * S + o] * scale[ne + 6 * (size_t)C + i] * step[ne + 6 * (size_t)C + i];
-            acc += m * (J[j * S + o] + m / 2.0);
+            for (int i = 0; i < K; ++i) m += J[(size_t)o * jst(K) + (20 + K * j + i)] * scale[ne + 6 * (size_t)C + i] * step[ne + 6 * (size_t)C + i];
+            acc += m * (J[(size_t)o * jst(K) + j] + m / 2.0);
         }
     }
     const double s = block_sum(acc, sh);

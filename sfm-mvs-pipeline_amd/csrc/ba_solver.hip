@@ -219,20 +219,18 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     // point-sharded ranks: the reduced camera system and its rhs are sums over ranks
     RC(allreduce(c, S, (int64_t)npad * npad + npad, SFMX_REDUCE_SUM));
     hipLaunchKernelGGL(ba_add_damping, dim3(nblk(c->nf)), dim3(256), 0, c->st, P, c->nf, npad, c->D.as<double>(), S);
-    for (int k = 0; k < T; ++k) {
-        hipLaunchKernelGGL(chol_potrf, dim3(1), dim3(64), 0, c->st, S, npad, k, fl);
-        hipLaunchKernelGGL(chol_trinv, dim3(1), dim3(64), 0, c->st, S, npad, k, c->Linv.as<double>());
-        if (k + 1 < T) {
-            hipLaunchKernelGGL(chol_trsm, dim3(T - k - 1), dim3(256), 0, c->st, S, npad, k, c->Linv.as<double>());
-            hipLaunchKernelGGL(chol_update, dim3((T - k - 1) * (T - k) / 2), dim3(256), 0, c->st, S, npad, k, T);
-        }
-    }
-    hipLaunchKernelGGL(chol_solve, dim3(1), dim3(1024), 0, c->st, S, c->Linv.as<double>(), npad, rhs);
+    double* W = c->Linv.as<double>();
     double* sol = c->sol.as<double>();
-    HIPCHK(hipMemcpyAsync(sol + c->ne, rhs, sizeof(double) * c->nf, hipMemcpyDeviceToDevice, c->st));
+    hipLaunchKernelGGL(chol_first, dim3(1), dim3(256), 0, c->st, S, npad, W, rhs, fl);
+    for (int k = 0; k + 1 < T; ++k) {
+        const int m = T - k - 1;
+        hipLaunchKernelGGL(chol_step, dim3(m * (m + 1) / 2), dim3(256), 0, c->st, S, npad, k, W, rhs, fl);
+    }
+    for (int k = T - 1; k >= 0; --k)
+        hipLaunchKernelGGL(chol_back, dim3(std::max(k, 1)), dim3(256), 0, c->st, S, npad, c->nf, k, rhs, sol + c->ne);
 #define BACK(KK)                                                                                                    \
     hipLaunchKernelGGL(ba_backsub<KK>, dim3(nblk(P)), dim3(256), 0, c->st, P, C, c->pt_start.as<int>(),              \
-                       c->pt_obs.as<int>(), c->obs_cam.as<int>(), c->R1.as<double>(), c->EinvG.as<double>(), rhs, sol)
+                       c->pt_obs.as<int>(), c->obs_cam.as<int>(), c->R1.as<double>(), c->EinvG.as<double>(), sol + c->ne, sol)
     if (K == 1) { BACK(1); } else if (K == 3) { BACK(3); } else { BACK(7); }
 #undef BACK
     HIPCHK(hipGetLastError());
@@ -491,7 +489,7 @@ int create(const sfmx_ba_problem* pb, const sfmx_ba_options* opt, sfmx_ba_ctx** 
         {&c->partB, 8 * (size_t)nblk(std::max<int64_t>(O, n))}, {&c->scal, 8 * 16},
         {&c->ipart, 8 * (size_t)std::max(C, 1) * NI}, {&c->Einv, 72 * (size_t)std::max(P, 1)},
         {&c->EinvG, 24 * (size_t)std::max(P, 1)}, {&c->R1, 8 * so * r1s(K)}, {&c->R2, 8 * so * r2s(K)},
-        {&c->vzpart, 8 * (size_t)c->nvz * K * K}, {&c->Linv, 8 * (size_t)c->T * NB * NB},
+        {&c->vzpart, 8 * (size_t)c->nvz * K * K}, {&c->Linv, 8 * (size_t)2 * NB * NB},
         {&c->Scc, 288 * (size_t)std::max(C, 1)}, {&c->Spi, 48 * (size_t)K * std::max(C, 1)}, {&c->Sii, 8 * (size_t)K * K},
         {&c->rc, 48 * (size_t)std::max(C, 1)}, {&c->ri, 8 * (size_t)K}, {&c->Spp, 288 * (size_t)std::max(NBLK, 1)},
         {&c->SR, 8 * ((size_t)c->npad * c->npad + c->npad)}, {&c->failf, 64}};
@@ -667,10 +665,10 @@ int sfmx_ba_jacobian(const sfmx_ba_problem* pb, int32_t device, double* r, doubl
                 rc = fail(SFMX_EDEVICE, "D2H");
             for (int o = 0; o < O && !rc; ++o) {
                 for (int j = 0; j < 2; ++j) {
-                    if (r) r[2 * (size_t)o + j] = h[(size_t)j * O + o];
-                    for (int i = 0; i < 3; ++i) if (Je) Je[6 * (size_t)o + 3 * j + i] = h[(size_t)(2 + 3 * j + i) * O + o];
-                    for (int i = 0; i < 6; ++i) if (Jc) Jc[12 * (size_t)o + 6 * j + i] = h[(size_t)(8 + 6 * j + i) * O + o];
-                    for (int i = 0; i < K; ++i) if (Ji) Ji[2 * (size_t)K * o + K * j + i] = h[(size_t)(20 + K * j + i) * O + o];
+                    if (r) r[2 * (size_t)o + j] = h[(size_t)o * F + j];
+                    for (int i = 0; i < 3; ++i) if (Je) Je[6 * (size_t)o + 3 * j + i] = h[(size_t)o * F + (2 + 3 * j + i)];
+                    for (int i = 0; i < 6; ++i) if (Jc) Jc[12 * (size_t)o + 6 * j + i] = h[(size_t)o * F + (8 + 6 * j + i)];
+                    for (int i = 0; i < K; ++i) if (Ji) Ji[2 * (size_t)K * o + K * j + i] = h[(size_t)o * F + (20 + K * j + i)];
                 }
             }
         }
