@@ -28,6 +28,12 @@ namespace sfmx {
 namespace ba {
 
 constexpr int NB = 64;   // Cholesky tile
+// Bijective XCD-contiguous block remap (blocks b, b+8, ... land on one XCD;
+// speed only, never correctness).
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, x = b & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
 __host__ __device__ constexpr int jst(int K) { return 20 + 2 * K; }   // Jacobian record stride
 
 // ---- dual numbers --------------------------------------------------------
@@ -575,7 +581,7 @@ __global__ __launch_bounds__(256)
 void ba_pair_blocks(const int* __restrict__ blk_start, const int2* __restrict__ trip, const double* __restrict__ R1,
                     double* __restrict__ Spp) {
     __shared__ double sh[8];
-    const int b = blockIdx.x;
+    const int b = xcd_remap(blockIdx.x, gridDim.x);
     double acc[36];
 #pragma unroll
     for (int i = 0; i < 36; ++i) acc[i] = 0.0;
@@ -724,13 +730,15 @@ __device__ __forceinline__ double rcp_nr(double d) {
     return fma(r, e, r);
 }
 
-// W_k = D~_k^-1 by symmetric sweeps (256 threads, thread (ty, tx) holds the
-// 4x4 block at rows 4ty.., cols 4tx..; one barrier per pivot).  Sweeping
-// pivot j: a_il -= a_ij a_jl / d (i, l != j), a_jl = a_jl / d, a_jj = -1/d;
-// after all pivots the tile holds -A^-1.  Then rhs_k <- W_k rhs_k.
+// W_k = D~_k^-1 by symmetric block sweeps (256 threads; thread (ty, tx) holds
+// the 4x4 block at rows 4ty.., cols 4tx..).  Sweeping the 4x4 pivot block B
+// with Q = A_BB^-1:  a_il -= A_iB Q A_Bl (i, l not in B), A_iB <- A_iB Q,
+// A_Bl <- Q A_Bl, A_BB <- -Q; after all 16 blocks the tile holds -A^-1.  Q
+// itself comes from 4 scalar sweeps whose pivots are the scalar Cholesky
+// pivots (failure detection).  One barrier per 4 pivots.  Then rhs_k <- W_k rhs_k.
 __device__ __forceinline__ void chol_diag_tile(double* __restrict__ S, int npad, int k, double* __restrict__ Wout,
                                                double* __restrict__ rhs, int* __restrict__ fail, double (*buf)[LDT],
-                                               double (*colT)[NB]) {
+                                               double (*colP)[NB][4]) {
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4, k0 = k * NB;
     double t[4][4];
 #pragma unroll
@@ -741,30 +749,70 @@ __device__ __forceinline__ void chol_diag_tile(double* __restrict__ S, int npad,
     }
     bool bad = false;
     for (int jb = 0; jb < NB / 4; ++jb) {
+        double (*P)[4] = colP[jb & 1];
+        if (tx == jb) {
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const int j = 4 * jb + jj, p = jj & 1;
-            if (tx == jb) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) { colT[p][4 * ty + u] = t[u][jj]; t[u][jj] = 0.0; }
+            for (int u = 0; u < 4; ++u) {
+                *reinterpret_cast<double2*>(&P[4 * ty + u][0]) = make_double2(t[u][0], t[u][1]);
+                *reinterpret_cast<double2*>(&P[4 * ty + u][2]) = make_double2(t[u][2], t[u][3]);
             }
-            if (ty == jb) {
+        }
+        const bool rowB = (ty == jb), colB = (tx == jb);
 #pragma unroll
-                for (int w = 0; w < 4; ++w) t[jj][w] = 0.0;
-            }
-            __syncthreads();
-            double d = colT[p][j];
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) t[u][w] = (rowB || colB) ? 0.0 : t[u][w];
+        __syncthreads();
+        // q = -P^-1 by scalar sweeps of the 4x4 pivot block (same values in every lane)
+        double q[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) q[i][l] = P[4 * jb + i][l];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            double d = q[j][j];
             if (!(d > 0.0) || !isfinite(d)) { bad = true; d = 1.0; }
             const double r = rcp_nr(d);
-            double m[4], cl[4];
+            double c[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) m[u] = (4 * ty + u == j) ? -r : colT[p][4 * ty + u] * r;
+            for (int i = 0; i < 4; ++i) c[i] = q[i][j];
 #pragma unroll
-            for (int w = 0; w < 4; ++w) cl[w] = (4 * tx + w == j) ? -1.0 : colT[p][4 * tx + w];
+            for (int i = 0; i < 4; ++i) {
+                const double m = (i == j) ? -r : c[i] * r;
+#pragma unroll
+                for (int l = 0; l < 4; ++l) {
+                    const double cl = (l == j) ? -1.0 : c[l];
+                    const double base = (i == j || l == j) ? 0.0 : q[i][l];
+                    q[i][l] = fma(-m, cl, base);
+                }
+            }
+        }
+        // row multipliers m[u] = A_iB Q (i not in B) or -Q = q (i in B)
+        double m[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double2 a01 = *reinterpret_cast<const double2*>(&P[4 * ty + u][0]);
+            const double2 a23 = *reinterpret_cast<const double2*>(&P[4 * ty + u][2]);
+            const double av[4] = {a01.x, a01.y, a23.x, a23.y};
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const double v = -(av[0] * q[0][b] + av[1] * q[1][b] + av[2] * q[2][b] + av[3] * q[3][b]);
+                m[u][b] = rowB ? q[u][b] : v;
+            }
+        }
+        // column factors cl[w] = A_Bl (l not in B) or -e_l (l in B)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const double2 c01 = *reinterpret_cast<const double2*>(&P[4 * tx + w][0]);
+            const double2 c23 = *reinterpret_cast<const double2*>(&P[4 * tx + w][2]);
+            const double cv[4] = {c01.x, c01.y, c23.x, c23.y};
+            double cl[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) cl[b] = colB ? (b == w ? -1.0 : 0.0) : cv[b];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int w = 0; w < 4; ++w) t[u][w] = fma(-m[u], cl[w], t[u][w]);
+                t[u][w] = fma(-m[u][0], cl[0], fma(-m[u][1], cl[1], fma(-m[u][2], cl[2], fma(-m[u][3], cl[3], t[u][w]))));
         }
     }
     if (bad && tid == 0) atomicOr(fail, 1);
@@ -776,25 +824,26 @@ __device__ __forceinline__ void chol_diag_tile(double* __restrict__ S, int npad,
             Wout[(4 * ty + u) * NB + 4 * tx + w] = -t[u][w];
         }
     __syncthreads();
+    double* yk = &colP[0][0][0];
     if (tid < NB) {
         double s = 0.0;
         for (int c = 0; c < NB; ++c) s = fma(buf[tid][c], rhs[k0 + c], s);
-        colT[0][tid] = s;
+        yk[tid] = s;
     }
     __syncthreads();
-    if (tid < NB) rhs[k0 + tid] = colT[0][tid];
+    if (tid < NB) rhs[k0 + tid] = yk[tid];
 }
 
 struct alignas(16) CholLds {
     double a[NB][LDT], m[NB][LDT], n[NB][LDT];
-    double colT[2][NB];
+    double colP[2][NB][4];
 };
 
 __global__ __launch_bounds__(256)
 void chol_first(double* __restrict__ S, int npad, double* __restrict__ W, double* __restrict__ rhs,
                 int* __restrict__ fail) {
     __shared__ CholLds sm;
-    chol_diag_tile(S, npad, 0, W, rhs, fail, sm.a, sm.colT);
+    chol_diag_tile(S, npad, 0, W, rhs, fail, sm.a, sm.colP);
 }
 
 // Panel k: one block per trailing lower tile (a, b), k < b <= a.  Block 0 is
@@ -845,7 +894,7 @@ void chol_step(double* __restrict__ S, int npad, int k, double* __restrict__ W, 
     }
     if (blockIdx.x == 0) {
         __syncthreads();
-        chol_diag_tile(S, npad, k + 1, W + (size_t)((k + 1) & 1) * NB * NB, rhs, fail, sm.n, sm.colT);
+        chol_diag_tile(S, npad, k + 1, W + (size_t)((k + 1) & 1) * NB * NB, rhs, fail, sm.n, sm.colP);
     }
 }
 

@@ -73,6 +73,9 @@ struct sfmx_ba_ctx {
     Buf x, cand, scale, colsq, grad, diag, D, J, partA, partB, scal, ipart;
     Buf Einv, EinvG, R1, R2, vzpart, Scc, Spi, Sii, rc, ri, Spp, SR, Linv, sol, step, failf;
     bool scaled = false;
+    // locality order: internal point p' is caller point pperm[p']; internal
+    // observation o' is caller observation operm[o'] (point-major)
+    std::vector<int> pperm, operm;
     double phase_ms[4] = {0, 0, 0, 0};
     hipEvent_t ev[6] = {};
     ~sfmx_ba_ctx() {
@@ -392,15 +395,65 @@ int upload(Buf& b, const std::vector<T>& v, hipStream_t st) {
 int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
     DeviceGuard dg(c->device);
     double* x = c->x.as<double>();
-    if (c->P) HIPCHK(hipMemcpyAsync(x, pb->points, sizeof(double) * 3 * c->P, hipMemcpyHostToDevice, c->st));
+    std::vector<double> pts(3 * (size_t)c->P);
+    for (int q = 0; q < c->P; ++q)
+        for (int i = 0; i < 3; ++i) pts[3 * (size_t)q + i] = pb->points[3 * (size_t)c->pperm[q] + i];
+    if (c->P) HIPCHK(hipMemcpyAsync(x, pts.data(), sizeof(double) * 3 * c->P, hipMemcpyHostToDevice, c->st));
     if (c->C) HIPCHK(hipMemcpyAsync(x + c->ne, pb->poses, sizeof(double) * 6 * c->C, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipMemcpyAsync(x + c->ne + 6 * (size_t)c->C, pb->intr, sizeof(double) * c->K, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     return SFMX_OK;
 }
 
-int create(const sfmx_ba_problem* pb, const sfmx_ba_options* opt, sfmx_ba_ctx** out) {
-    RC(validate(pb));
+// Locality order (internal only; results are reported in the caller's order):
+// points sorted by their sorted camera lists (points seen by the same cameras
+// become neighbours, so the per-camera and per-camera-pair gathers of the Schur
+// kernels hit contiguous records), observations point-major in that order.
+void locality_order(const sfmx_ba_problem* pb, std::vector<int>& pperm, std::vector<int>& operm) {
+    const int P = pb->n_points, O = pb->n_obs;
+    std::vector<int> start(P + 1, 0), obs(O);
+    for (int i = 0; i < O; ++i) start[pb->obs_point[i] + 1]++;
+    for (int p = 0; p < P; ++p) start[p + 1] += start[p];
+    {
+        std::vector<int> f(start.begin(), start.end() - 1);
+        for (int i = 0; i < O; ++i) obs[f[pb->obs_point[i]]++] = i;
+    }
+    std::vector<int> cams(O);   // per point: its cameras, sorted
+    for (int p = 0; p < P; ++p) {
+        for (int a = start[p]; a < start[p + 1]; ++a) cams[a] = pb->obs_cam[obs[a]];
+        std::sort(cams.begin() + start[p], cams.begin() + start[p + 1]);
+    }
+    pperm.resize(P);
+    for (int p = 0; p < P; ++p) pperm[p] = p;
+    std::stable_sort(pperm.begin(), pperm.end(), [&](int a, int b) {
+        return std::lexicographical_compare(cams.begin() + start[a], cams.begin() + start[a + 1],
+                                            cams.begin() + start[b], cams.begin() + start[b + 1]);
+    });
+    operm.clear();
+    operm.reserve(O);
+    for (int q = 0; q < P; ++q)
+        for (int a = start[pperm[q]]; a < start[pperm[q] + 1]; ++a) operm.push_back(obs[a]);
+}
+
+int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ctx** out) {
+    RC(validate(caller));
+    std::vector<int> pperm, operm, ipperm(caller->n_points), rop(caller->n_obs), roc(caller->n_obs);
+    std::vector<double> rxy(2 * (size_t)caller->n_obs);
+    locality_order(caller, pperm, operm);
+    for (int q = 0; q < caller->n_points; ++q) ipperm[pperm[q]] = q;
+    for (int q = 0; q < caller->n_obs; ++q) {
+        const int o = operm[q];
+        rop[q] = ipperm[caller->obs_point[o]];
+        roc[q] = caller->obs_cam[o];
+        rxy[2 * (size_t)q] = caller->obs_xy[2 * (size_t)o];
+        rxy[2 * (size_t)q + 1] = caller->obs_xy[2 * (size_t)o + 1];
+    }
+    sfmx_ba_problem internal = *caller;
+    internal.points = nullptr;   // parameters are uploaded from the caller's arrays by set_params
+    internal.obs_point = rop.data();
+    internal.obs_cam = roc.data();
+    internal.obs_xy = rxy.data();
+    const sfmx_ba_problem* pb = &internal;
     sfmx_ba_options o;
     sfmx_ba_default_options(&o);
     if (opt) o = *opt;
@@ -414,6 +467,8 @@ int create(const sfmx_ba_problem* pb, const sfmx_ba_options* opt, sfmx_ba_ctx** 
     if (!c) return fail(SFMX_ENOMEM, "host allocation");
     c->device = o.device;
     c->opt = o;
+    c->pperm.swap(pperm);
+    c->operm.swap(operm);
     DeviceGuard dg(c->device);
     auto bail = [&](int rc) { delete c; return rc; };
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) return bail(fail(SFMX_EDEVICE, "stream"));
@@ -453,6 +508,23 @@ int create(const sfmx_ba_problem* pb, const sfmx_ba_options* opt, sfmx_ba_ctx** 
                 cnt[id]++;
             }
     const int NBLK = (int)cnt.size();
+    {   // number blocks in (cam(a), cam(b)) order: neighbouring blocks share points, and
+        // ba_pair_blocks maps contiguous block ranges to one XCD (L2 reuse of the R1 records)
+        std::vector<std::pair<int64_t, int>> keys;
+        keys.reserve(NBLK);
+        for (auto& kv : bid) keys.emplace_back(kv.first, kv.second);
+        std::sort(keys.begin(), keys.end());
+        std::vector<int> cnt2(NBLK), cam2(2 * (size_t)NBLK);
+        for (int nb = 0; nb < NBLK; ++nb) {
+            const int ob = keys[nb].second;
+            cnt2[nb] = cnt[ob];
+            cam2[2 * nb] = blk_cam[2 * ob];
+            cam2[2 * nb + 1] = blk_cam[2 * ob + 1];
+            bid[keys[nb].first] = nb;
+        }
+        cnt.swap(cnt2);
+        blk_cam.swap(cam2);
+    }
     std::vector<int> blk_start(NBLK + 1, 0);
     for (int b = 0; b < NBLK; ++b) blk_start[b + 1] = blk_start[b] + cnt[b];
     std::vector<int2> trip(blk_start[NBLK]);
@@ -501,7 +573,7 @@ int create(const sfmx_ba_problem* pb, const sfmx_ba_options* opt, sfmx_ba_ctx** 
             hipStreamSynchronize(st) != hipSuccess)
             return bail(fail(SFMX_EDEVICE, "upload"));
     }
-    if ((rc = set_params(c, pb))) return bail(rc);
+    if ((rc = set_params(c, caller))) return bail(rc);
     *out = c;
     return SFMX_OK;
 }
@@ -610,10 +682,13 @@ int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
     if (!c || !pb) return fail(SFMX_EINVAL, "null context/problem");
     DeviceGuard dg(c->device);
     const double* x = c->x.as<double>();
-    if (c->P) HIPCHK(hipMemcpyAsync(pb->points, x, sizeof(double) * 3 * c->P, hipMemcpyDeviceToHost, c->st));
+    std::vector<double> pts(3 * (size_t)c->P);
+    if (c->P) HIPCHK(hipMemcpyAsync(pts.data(), x, sizeof(double) * 3 * c->P, hipMemcpyDeviceToHost, c->st));
     if (c->C) HIPCHK(hipMemcpyAsync(pb->poses, x + c->ne, sizeof(double) * 6 * c->C, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipMemcpyAsync(pb->intr, x + c->ne + 6 * (size_t)c->C, sizeof(double) * c->K, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    for (int q = 0; q < c->P; ++q)
+        for (int i = 0; i < 3; ++i) pb->points[3 * (size_t)c->pperm[q] + i] = pts[3 * (size_t)q + i];
     return SFMX_OK;
 }
 
@@ -663,12 +738,13 @@ int sfmx_ba_jacobian(const sfmx_ba_problem* pb, int32_t device, double* r, doubl
             std::vector<double> h((size_t)F * O);
             if (O && (hipMemcpy(h.data(), c->J.p, sizeof(double) * h.size(), hipMemcpyDeviceToHost) != hipSuccess))
                 rc = fail(SFMX_EDEVICE, "D2H");
-            for (int o = 0; o < O && !rc; ++o) {
+            for (int q = 0; q < O && !rc; ++q) {
+                const size_t o = (size_t)c->operm[q];   // caller's observation index
                 for (int j = 0; j < 2; ++j) {
-                    if (r) r[2 * (size_t)o + j] = h[(size_t)o * F + j];
-                    for (int i = 0; i < 3; ++i) if (Je) Je[6 * (size_t)o + 3 * j + i] = h[(size_t)o * F + (2 + 3 * j + i)];
-                    for (int i = 0; i < 6; ++i) if (Jc) Jc[12 * (size_t)o + 6 * j + i] = h[(size_t)o * F + (8 + 6 * j + i)];
-                    for (int i = 0; i < K; ++i) if (Ji) Ji[2 * (size_t)K * o + K * j + i] = h[(size_t)o * F + (20 + K * j + i)];
+                    if (r) r[2 * o + j] = h[(size_t)q * F + j];
+                    for (int i = 0; i < 3; ++i) if (Je) Je[6 * o + 3 * j + i] = h[(size_t)q * F + (2 + 3 * j + i)];
+                    for (int i = 0; i < 6; ++i) if (Jc) Jc[12 * o + 6 * j + i] = h[(size_t)q * F + (8 + 6 * j + i)];
+                    for (int i = 0; i < K; ++i) if (Ji) Ji[2 * (size_t)K * o + K * j + i] = h[(size_t)q * F + (20 + K * j + i)];
                 }
             }
         }
