@@ -174,7 +174,8 @@ def main():
                        "logical_descriptor_pairs": logical_total, "parallelism": f"pair-sharded x{world}",
                        "ratio": sfmx.LOWE_RATIO},
             "roofline": {"bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
-                         "frac": achieved / peak, "traffic": None,
+                         "frac": achieved / peak, "traffic": pmc_traffic(norm, n_img),
+                         "traffic_unit": "bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/r01_pmc_sift_v0.json)",
                          "kernel": "sift_knn2_kernel" if norm == sfmx.NORM_L2 else "orb_knn2_kernel",
                          "kernel_ms_per_launch": kern_ms, "run_ms_per_step": float(np.mean(run_ms)),
                          "algorithmic": f"{flop_per_pair:g} ops per descriptor pair x {logical_mine:.4g} pairs per launch"},
@@ -191,6 +192,23 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def pmc_traffic(norm, n_img):
+    """HBM bytes per launch of the 2-NN kernel from the committed PMC passes of this
+    workload (tools/pmc_sift.sh -> profiles/r01_pmc_sift_v0.json): 2 x FETCH_SIZE
+    (gfx950 counts half of a wide streaming read) + WRITE_SIZE, both in KiB.
+    None when no pass of this exact workload/kernel is on file."""
+    import sfmx
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_pmc_sift_v0.json")
+    if norm != sfmx.NORM_L2 or n_img != 50 or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    for k, v in d.items():
+        if "sift_knn2_kernel" in k and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            return (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0
+    return None
 
 
 def bench_ba(args, rank, world, local):
