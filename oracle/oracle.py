@@ -1,6 +1,6 @@
 """sfmx ORACLE — TEST INFRASTRUCTURE ONLY.
 
-ctypes wrapper over liboracle.so (oracle/match_oracle.cpp, oracle/ba_oracle.cpp):
+ctypes wrapper over liboracle.so (oracle/match_oracle.cpp, flann_oracle.cpp, ba_oracle.cpp):
 the CPU restatement of the reference's matching / bundle-adjustment semantics.
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
 import this module, and only as the checker / CPU baseline — never as the
@@ -45,6 +45,8 @@ def _load():
     lib.orc_pairs_grid.restype = C.c_int64
     lib.orc_pairs_grid.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, i32p]
     lib.orc_filter_matches.argtypes = [vp, i64p, i64p, C.c_int, C.c_int, C.c_int, i32p]
+    lib.orc_flann_match_pairs.argtypes = [C.c_int, C.POINTER(vp), i32p, C.c_int, i32p, C.c_int, C.c_double, vp,
+                                          i64p, i64p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]
     lib.orc_first_sqrt_collision.restype = C.c_int64
     lib.orc_first_sqrt_collision.argtypes = [C.c_int64]
     return lib
@@ -82,9 +84,10 @@ def match_pair(q: np.ndarray, t: np.ndarray, ratio: float = 0.7) -> np.ndarray:
     return out[:n].copy()
 
 
-def match_pairs(imgs, pairs: np.ndarray, ratio: float = 0.7, nthreads: int = 0):
-    """Pair-parallel exact BF (OpenMP over pairs, as the reference) ->
-    (matches, pair_offsets[n+1]) packed like sfmx_matcher_fetch."""
+def _pair_batch(imgs, pairs, call):
+    """Shared packing of the pair-parallel batch entry points: per-pair output
+    slots at the cumulative left-image row counts, then compacted in pair order
+    -> (matches, pair_offsets[n+1]) packed like sfmx_matcher_fetch."""
     l2 = imgs[0].dtype == np.float32
     imgs = [np.ascontiguousarray(m) for m in imgs]
     dim = imgs[0].shape[1]
@@ -97,12 +100,41 @@ def match_pairs(imgs, pairs: np.ndarray, ratio: float = 0.7, nthreads: int = 0):
     cap = int(rows[pairs[:, 0]].sum()) if len(pairs) else 0
     tmp = np.zeros(max(cap, 1), DMATCH_DTYPE)
     counts = np.zeros(max(len(pairs), 1), np.int64)
-    lib.orc_match_pairs(0 if l2 else 1, ptrs, _ptr(rows), dim, _ptr(pairs), len(pairs), ratio, tmp.ctypes.data,
-                        _ptr(base, C.c_int64), _ptr(counts, C.c_int64), nthreads)
+    call(0 if l2 else 1, ptrs, _ptr(rows), dim, _ptr(pairs), len(pairs), tmp.ctypes.data,
+         _ptr(base, C.c_int64), _ptr(counts, C.c_int64))
     off = np.zeros(len(pairs) + 1, np.int64)
     off[1:] = np.cumsum(counts[: len(pairs)])
     out = np.concatenate([tmp[base[p]: base[p] + counts[p]] for p in range(len(pairs))]) if len(pairs) else tmp[:0]
     return out, off
+
+
+def match_pairs(imgs, pairs: np.ndarray, ratio: float = 0.7, nthreads: int = 0):
+    """Pair-parallel exact BF (OpenMP over pairs, as the reference) ->
+    (matches, pair_offsets[n+1]) packed like sfmx_matcher_fetch."""
+    return _pair_batch(imgs, pairs, lambda t, ptrs, rows, dim, pr, n, out, base, counts: lib.orc_match_pairs(
+        t, ptrs, rows, dim, pr, n, ratio, out, base, counts, nthreads))
+
+
+def flann_match_pairs(imgs, pairs: np.ndarray, ratio: float = 0.7, nthreads: int = 0, trees: int = 5,
+                      checks: int = 100, tables: int = 6, key_size: int = 12, seed: int = 0x5F3D):
+    """FLANN-style approximate matcher (oracle/flann_oracle.cpp): per-pair
+    KDTreeIndex(trees) + SearchParams(checks) for f32 rows, LshIndex(tables,
+    key_size, 1) for u8 rows, index rebuilt per pair as the reference's
+    2-argument knnMatch does (PhotogrammetrieCli.cpp:371-384).  CPU baseline +
+    recall reference only; not a parity oracle (FLANN is RNG-driven)."""
+    return _pair_batch(imgs, pairs, lambda t, ptrs, rows, dim, pr, n, out, base, counts: lib.orc_flann_match_pairs(
+        t, ptrs, rows, dim, pr, n, ratio, out, base, counts, nthreads, trees, checks, tables, key_size, seed))
+
+
+def recall(exact: np.ndarray, exact_off: np.ndarray, approx: np.ndarray, approx_off: np.ndarray):
+    """(recall, precision) of an approximate match list against the exact one:
+    a match is the (pair, queryIdx, trainIdx) triple."""
+    def keys(m, off):
+        p = np.repeat(np.arange(len(off) - 1, dtype=np.int64), np.diff(off))
+        return (p << 40) | (m["queryIdx"].astype(np.int64) << 20) | m["trainIdx"].astype(np.int64)
+    a, b = keys(exact, exact_off), keys(approx, approx_off)
+    hit = np.intersect1d(a, b).size
+    return hit / max(a.size, 1), hit / max(b.size, 1)
 
 
 def filter_matches(matches: np.ndarray, offsets: np.ndarray, distinct: bool, min_count: int):

@@ -47,6 +47,9 @@ namespace sfmx {
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define GLOBAL_AS __attribute__((address_space(1)))
 #define LDS_AS __attribute__((address_space(3)))
@@ -131,6 +134,30 @@ __global__ void prep_hamming_kernel(const uint8_t* __restrict__ src, int rows, i
     if (i >= total) return;
     const int r = (int)(i / ORB_BYTES), c = (int)(i % ORB_BYTES);
     dst[i] = (r < rows && c < cols) ? src[(int64_t)r * cols + c] : 0;
+}
+
+// ORB rows -> +-1 FP4 (e2m1) rows for the MFMA Hamming path: bit 1 -> +1.0
+// (0x2), bit 0 -> -1.0 (0xA), so for two 256-bit rows dot = 256 - 2 * popcount(a ^ b).
+// Missing bytes (cols < 32) encode as zero bytes, as the VALU path pads them.
+// Pad rows are all +0.0 nibbles (contribute 0).  keyc[r] = float bits of the
+// row's MFMA C-operand: 767 + (16383 - (r & 16383)) / 16384 (exact in f32),
+// pad rows 0.0 (see orb_mfma_kernel).  32 threads per row, one u32 each.
+__global__ void prep_hamming_fp4_kernel(const uint8_t* __restrict__ src, int rows, int cols, int rows_pad,
+                                        uint32_t* __restrict__ dst, int32_t* __restrict__ keyc) {
+    const int r = blockIdx.x * (blockDim.x >> 5) + (threadIdx.x >> 5);
+    const int c = threadIdx.x & 31;
+    if (r >= rows_pad) return;
+    uint32_t w = 0;
+    if (r < rows) {
+        const unsigned byte = c < cols ? src[(int64_t)r * cols + c] : 0u;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) w |= (((byte >> b) & 1u) ? 0x2u : 0xAu) << (4 * b);
+    }
+    dst[(int64_t)r * 32 + c] = w;
+    if (c == 0) {
+        const int jj = 16383 - (r & 16383);
+        keyc[r] = r < rows ? __float_as_int((float)(767 * 16384 + jj) * (1.0f / 16384.0f)) : 0;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -390,6 +417,165 @@ void sift_f32_kernel(const WorkItem* __restrict__ work, const int32_t* __restric
 }
 
 // ---------------------------------------------------------------------------
+// ORB Hamming 2-NN on the matrix cores (FP4 e2m1, +-1 encoding).
+//
+//   With bits mapped to +-1, dot(a, b) = 256 - 2 * hamming(a, b): an exact
+//   contraction of 256 products of +-1, i.e. 4 x v_mfma_scale_f32_32x32x64_f8f6f4
+//   (FP4 operands, unit E8M0 scales) per 32x32 tile — the same 128-byte rows
+//   and LDS stage as the SIFT kernel, at the FP4 rate (2x int8 per clock).
+//   The key needs no VALU: the MFMA's C operand is a per-train-row constant
+//       C_j = 767 + (16383 - (j & 16383)) / 16384
+//   so acc = C_j + dot lies in [511, 1024) where the f32 ulp is <= 2^-14: the
+//   sum is exact, its integer part is 767 + dot and its fraction carries the
+//   row's tie-break index, so the top-2 runs on the raw accumulators with
+//   v_med3_f32 / v_max3_f32 (larger key = smaller hamming, then lower index:
+//   OpenCV's order).  Every
+//   16384 rows the chunk's top-2 is decoded and folded into the running
+//   (hamming, j) top-2 with strict '<' (earlier chunks keep ties).
+//   Pad rows have C = 0 and all-zero nibbles: key 0.0 never wins.
+template <int QT, int WAVES, int MINW, int STAGE>
+__global__ __launch_bounds__(WAVES * 64, MINW)
+void orb_mfma_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
+                     const ImgDev* __restrict__ imgs, const uint8_t* __restrict__ desc4,
+                     const int32_t* __restrict__ keyc, int32_t* __restrict__ out_idx,
+                     float* __restrict__ out_dist, double ratio) {
+    constexpr int ROWB = 128;                               // 256 fp4 nibbles per row
+    constexpr int GLDS = STAGE * ROWB / (WAVES * 64 * 16);
+    static_assert(GLDS * WAVES * 64 * 16 == STAGE * ROWB, "stage must split into whole 16-B pieces");
+    constexpr int CHUNK = 16384;                            // rows per key chunk (14 index bits)
+    static_assert(CHUNK % STAGE == 0, "stages tile the key chunk");
+    constexpr int DESC_BYTES = STAGE * ROWB;
+    constexpr int BUF_BYTES = DESC_BYTES + STAGE * 4;
+    constexpr int SPC = CHUNK / STAGE;
+    constexpr float KEY_FLOOR = 256.f;                      // real keys are >= 511, pad rows 0
+    __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
+
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const WorkItem w = work[xcd_remap(blockIdx.x, gridDim.x)];
+    const PairDev P = pairs[w.pair];
+    const ImgDev L = imgs[P.left], R = imgs[P.right];
+    const int nq = L.rows, nt = R.rows;
+    const int qbase = w.q0 + wid * (QT * 32);
+
+    i32x4 bq[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const i32x4* src = reinterpret_cast<const i32x4*>(desc4 + (L.row0 + qbase + qt * 32 + l32) * ROWB);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) bq[qt][m] = src[2 * m + h];
+    }
+    int T1[QT], J1[QT], T2[QT], J2[QT];
+    float c1[QT], c2[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        T1[qt] = T2[qt] = INT_MAX; J1[qt] = J2[qt] = -1; c1[qt] = c2[qt] = 0.f;
+    }
+    const int nstages = (nt + STAGE - 1) / STAGE;
+    const uint8_t* tbase = desc4 + R.row0 * ROWB;
+    const int32_t* kbase = keyc + R.row0;
+
+    auto stage = [&](int s, int buf) {
+        char* base = lds + buf * BUF_BYTES;
+#pragma unroll
+        for (int i = 0; i < GLDS; ++i) {
+            const int p = i * WAVES * 64 + threadIdx.x;
+            const int rr = p >> 3, slot = p & 7, c = slot ^ ((rr >> 1) & 7);
+            const uint8_t* g = tbase + (int64_t)(s * STAGE + rr) * ROWB + 16 * c;
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)g,
+                                             (LDS_AS void*)(base + (i * WAVES + wid) * 1024), 16, 0, 0);
+        }
+        if (wid < STAGE / 64)
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(kbase + s * STAGE + wid * 64 + lane),
+                                             (LDS_AS void*)(base + DESC_BYTES + wid * 256), 4, 0, 0);
+    };
+    // Top-2 by max on the f32 accumulators (v_med3_f32 / v_max3_f32; compiler
+    // builtins, not inline asm, so the MFMA->VALU read hazards are resolved).
+    auto select = [&](const f32x16& acc, float& b1, float& b2) {
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+            const float ka = acc[r], kb = acc[r + 1];
+            b2 = fmaxf(__builtin_amdgcn_fmed3f(b1, ka, kb), b2);
+            b1 = fmaxf(b1, fmaxf(ka, kb));
+        }
+    };
+    auto i8of = [](const i32x4& v) { return i32x8{v.x, v.y, v.z, v.w, 0, 0, 0, 0}; };
+
+    if (nstages > 0) stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    for (int s = 0; s < nstages; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nstages) stage(s + 1, buf ^ 1);
+        const char* base = lds + buf * BUF_BYTES;
+#pragma unroll
+        for (int t = 0; t < STAGE / 32; ++t) {
+            const int row = t * 32 + l32;
+            i32x4 a[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int slot = (2 * m + h) ^ ((row >> 1) & 7);
+                a[m] = *reinterpret_cast<const i32x4*>(base + row * ROWB + 16 * slot);
+            }
+            f32x16 cinit;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 kv = *reinterpret_cast<const f32x4*>(base + DESC_BYTES + 4 * (t * 32 + 8 * g + 4 * h));
+                cinit[4 * g + 0] = kv.x; cinit[4 * g + 1] = kv.y; cinit[4 * g + 2] = kv.z; cinit[4 * g + 3] = kv.w;
+            }
+            f32x16 acc[QT];
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                acc[qt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(i8of(a[0]), i8of(bq[qt][0]), cinit, 4, 4, 0,
+                                                                          0x7f7f7f7f, 0, 0x7f7f7f7f);
+#pragma unroll
+                for (int m = 1; m < 4; ++m)
+                    acc[qt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(i8of(a[m]), i8of(bq[qt][m]), acc[qt], 4, 4,
+                                                                              0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+            }
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) select(acc[qt], c1[qt], c2[qt]);
+        }
+        if ((s % SPC) == SPC - 1 || s + 1 == nstages) {      // end of a key chunk
+            const int cb = (s / SPC) * CHUNK;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const float p1 = __shfl_xor(c1[qt], 32), p2 = __shfl_xor(c2[qt], 32);
+                const float m1 = fmaxf(c1[qt], p1), m2 = fmaxf(fminf(c1[qt], p1), fmaxf(c2[qt], p2));
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const float v = e == 0 ? m1 : m2;
+                    if (v >= KEY_FLOOR) {
+                        const float ip = __builtin_floorf(v);
+                        const int dot = (int)ip - 767;
+                        const int t_ = (256 - dot) >> 1;                       // hamming distance
+                        const int j_ = cb + 16383 - (int)((v - ip) * 16384.0f);
+                        if (t_ < T2[qt]) {
+                            if (t_ < T1[qt]) { T2[qt] = T1[qt]; J2[qt] = J1[qt]; T1[qt] = t_; J1[qt] = j_; }
+                            else { T2[qt] = t_; J2[qt] = j_; }
+                        }
+                    }
+                }
+                c1[qt] = c2[qt] = 0.f;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int qi = qbase + qt * 32 + l32;
+        if (h != 0 || qi >= nq) continue;
+        const int64_t o = P.dense_base + qi;
+        if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }
+        const float d1 = (float)T1[qt], d2 = (float)T2[qt];
+        const bool acc = nt >= 2 ? ((double)d1 < (double)d2 * ratio) : true;
+        out_idx[o] = acc ? J1[qt] : -1;
+        out_dist[o] = d1;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // ORB Hamming 2-NN on the VALU (8 x v_xor + 8 x v_bcnt per pair, no MFMA).
 // 4 waves x 2 queries per lane = 512 queries per block; train rows stream
 // through LDS (256 rows = 8 KiB per stage, broadcast ds_read_b128).
@@ -640,11 +826,34 @@ hipError_t launch_orb_knn2(const WorkItem* work, int n_work, const PairDev* pair
     orb_knn2_kernel<2><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc8, out_idx, out_dist, ratio);
     return hipGetLastError();
 }
+// ORB kernel selection: 0 (default) = FP4 MFMA path on 128-byte +-1 rows,
+// 1 = VALU xor/popcount path on 32-byte rows.  SFMX_ORB_VARIANT overrides.
+int orb_variant() {
+    static int v = [] {
+        const char* e = getenv("SFMX_ORB_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+hipError_t launch_prep_hamming_fp4(const uint8_t* src, int rows, int cols, int rows_pad, uint8_t* dst, int32_t* keyc,
+                                   hipStream_t st) {
+    if (rows_pad == 0) return hipSuccess;
+    prep_hamming_fp4_kernel<<<(rows_pad + 7) / 8, 256, 0, st>>>(src, rows, cols, rows_pad,
+                                                               reinterpret_cast<uint32_t*>(dst), keyc);
+    return hipGetLastError();
+}
+hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
+                           const uint8_t* desc4, const int32_t* keyc, int32_t* out_idx, float* out_dist, double ratio,
+                           hipStream_t st) {
+    if (n_work == 0) return hipSuccess;
+    orb_mfma_kernel<2, 8, 2, 64><<<n_work, 512, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx, out_dist, ratio);
+    return hipGetLastError();
+}
 hipError_t launch_assemble(const PairDev* pairs, int n_pairs, const ImgDev* imgs, const int32_t* out_idx,
                            const float* out_dist, int distinct, int min_count, int max_nt, int64_t* counts,
                            int32_t* keep, int64_t* offsets, DMatchDev* out, hipStream_t st) {
     if (n_pairs == 0) {
-        hipMemsetAsync(offsets, 0, sizeof(int64_t), st);
+        (void)hipMemsetAsync(offsets, 0, sizeof(int64_t), st);
         return hipGetLastError();
     }
     const size_t shmem = distinct ? (size_t)2 * ((max_nt + 31) / 32) * 4 : 0;

@@ -38,6 +38,10 @@ hipError_t launch_sift_f32(const WorkItem*, int, const PairDev*, const ImgDev*, 
                            double, hipStream_t);
 hipError_t launch_orb_knn2(const WorkItem*, int, const PairDev*, const ImgDev*, const uint8_t*, int32_t*, float*,
                            double, hipStream_t);
+hipError_t launch_prep_hamming_fp4(const uint8_t*, int, int, int, uint8_t*, int32_t*, hipStream_t);
+hipError_t launch_orb_mfma(const WorkItem*, int, const PairDev*, const ImgDev*, const uint8_t*, const int32_t*,
+                           int32_t*, float*, double, hipStream_t);
+int orb_variant();
 hipError_t launch_selftest_sqrt(int64_t, uint32_t*, hipStream_t);
 int sift_variant();
 int sift_block_queries(int variant);
@@ -98,6 +102,7 @@ struct DeviceGuard {
 struct sfmx_matcher {
     int device = 0;
     int norm = 0;
+    bool orb_fp4 = false;   // ORB rows expanded to +-1 FP4 (MFMA path), else 32-byte rows (VALU path)
     int n_imgs = 0;
     std::vector<ImgDev> imgs;
     int64_t total_rows = 0;
@@ -144,6 +149,7 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
     }
     DeviceGuard g(m->device);
     m->norm = norm;
+    m->orb_fp4 = norm == SFMX_NORM_HAMMING && orb_variant() == 0;
     m->n_imgs = n;
     m->imgs.assign(n, ImgDev{});
     m->has_run = false;
@@ -163,15 +169,13 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
         raw_bytes += align_up((int64_t)imgs[i].rows * imgs[i].cols * esz, 256);
     }
     m->total_rows = row;
-    const int row_bytes = norm == SFMX_NORM_L2 ? SIFT_DIM : ORB_BYTES;
+    const int row_bytes = (norm == SFMX_NORM_L2 || m->orb_fp4) ? SIFT_DIM : ORB_BYTES;
     int rc;
     if ((rc = m->desc8.ensure((size_t)row * row_bytes))) return rc;
     if ((rc = m->flags.ensure(sizeof(int32_t) * std::max(n, 1)))) return rc;
     if ((rc = m->imgs_d.ensure(sizeof(ImgDev) * std::max(n, 1)))) return rc;
-    if (norm == SFMX_NORM_L2) {
-        if ((rc = m->normv.ensure((size_t)row * 4))) return rc;
-        if ((rc = m->keyc.ensure((size_t)row * 4))) return rc;
-    }
+    if (norm == SFMX_NORM_L2 && (rc = m->normv.ensure((size_t)row * 4))) return rc;
+    if ((norm == SFMX_NORM_L2 || m->orb_fp4) && (rc = m->keyc.ensure((size_t)row * 4))) return rc;
     if (!device_src && (rc = m->raw.ensure((size_t)raw_bytes))) return rc;
     HIPCHK(hipMemsetAsync(m->flags.p, 0, sizeof(int32_t) * std::max(n, 1), st));
     std::vector<const void*> src(n);
@@ -190,6 +194,9 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
             HIPCHK(launch_prep_l2((const float*)src[i], d.rows, imgs[i].cols, d.rows_pad,
                                   m->desc8.as<int8_t>() + d.row0 * SIFT_DIM, m->normv.as<int32_t>() + d.row0,
                                   m->keyc.as<int32_t>() + d.row0, m->flags.as<int32_t>() + i, st));
+        else if (m->orb_fp4)
+            HIPCHK(launch_prep_hamming_fp4((const uint8_t*)src[i], d.rows, imgs[i].cols, d.rows_pad,
+                                           m->desc8.as<uint8_t>() + d.row0 * SIFT_DIM, m->keyc.as<int32_t>() + d.row0, st));
         else
             HIPCHK(launch_prep_hamming((const uint8_t*)src[i], d.rows, imgs[i].cols, d.rows_pad,
                                        m->desc8.as<uint8_t>() + d.row0 * ORB_BYTES, st));
@@ -281,6 +288,10 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
         if (!work32.empty())
             HIPCHK(launch_sift_f32(m->work32_d.as<WorkItem>(), (int)work32.size(), P, I, m->f32.as<float>(),
                                    m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
+    } else if (m->orb_fp4) {
+        HIPCHK(launch_orb_mfma(m->work_d.as<WorkItem>(), (int)work.size(), P, I, m->desc8.as<uint8_t>(),
+                               m->keyc.as<int32_t>(), m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
+        HIPCHK(hipEventRecord(m->ev[1], st));
     } else {
         HIPCHK(launch_orb_knn2(m->work_d.as<WorkItem>(), (int)work.size(), P, I, m->desc8.as<uint8_t>(),
                                m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));

@@ -62,8 +62,10 @@ def orb_images(n_images: int, n_desc: int, seed: int = ORB_SEED, shared: float =
         obs = pool[sel].copy()
         bits = np.unpackbits(obs, axis=1)
         nflip = rng.integers(0, max_flips + 1, size=n_sh)
-        for r in range(n_sh):
-            bits[r, rng.choice(256, size=nflip[r], replace=False)] ^= 1
+        if max_flips > 0 and n_sh > 0:   # nflip[r] distinct random bits per planted row
+            pos = np.argsort(rng.random((n_sh, 256)), axis=1)[:, :max_flips]
+            valid = np.arange(max_flips)[None, :] < nflip[:, None]
+            bits[np.nonzero(valid)[0], pos[valid]] ^= 1
         obs = np.packbits(bits, axis=1)
         img = np.concatenate([obs, fresh], axis=0)
         out.append(np.ascontiguousarray(img[rng.permutation(n_desc)]))

@@ -120,6 +120,35 @@ def test_full_size_orb_spot_check():
     assert m[off[0]:off[1]].tobytes() == exp.tobytes()
 
 
+def test_orb_multichunk_ties_and_narrow_rows():
+    """ORB FP4-MFMA path beyond one 16384-row key chunk: train images of 40000
+    rows (3 chunks folded with strict '<'), planted duplicate rows in different
+    chunks (a query one bit away from both copies must report the LOWER train
+    index), ratio 1.5 so ties are accepted; plus narrow rows (cols = 17 < 32)."""
+    from oracle import oracle
+    rng = np.random.default_rng(5)
+    t = rng.integers(0, 256, size=(40000, 32), dtype=np.uint8)
+    t[35000:35100] = t[100:200]                      # duplicates: chunk 0 and chunk 2
+    t[20000:20050] = t[16000:16050]                  # duplicates: both in chunk 1
+    dup = np.concatenate([t[100:200], t[16000:16050]]).copy()
+    dup[:, 3] ^= 0x10                                # one flipped bit -> hamming 1 to both copies
+    q = np.concatenate([t[rng.choice(40000, 1400, replace=False)], dup, rng.integers(0, 256, (300, 32), dtype=np.uint8)])
+    imgs = [q, t, t[:16385].copy()]
+    pairs = np.array([[0, 1], [0, 2], [2, 0]], np.int32)
+    for ratio in (0.7, 1.5):
+        m, off, _, _ = run(imgs, pairs, ratio)
+        em, eoff = oracle.match_pairs(imgs, pairs, ratio)
+        assert_same(m, off, em, eoff)
+    got = m[off[0]:off[1]]
+    sel = got[(got["queryIdx"] >= 1400) & (got["queryIdx"] < 1550)]
+    assert len(sel) == 150 and np.all(sel["trainIdx"] == np.r_[100:200, 16000:16050]) and np.all(sel["distance"] == 1.0)
+    narrow = [x[:, :17].copy() for x in synth.orb_images(3, 900, seed=41)]
+    pairs = sfmx.pairs_unordered(3)
+    m, off, _, _ = run(narrow, pairs)
+    em, eoff = oracle.match_pairs(narrow, pairs)
+    assert_same(m, off, em, eoff)
+
+
 def test_match_pairs_oneshot_and_strategy():
     d = fixtures.load("sift_small")
     m, off, keep = sfmx.match_pairs(d["imgs"], d["pairs"], n_gpus=1)

@@ -98,3 +98,35 @@ def test_pairs_golden_and_doc():
     # GridFeatureMatchingStrategy.h:31-37 example (image 01 = index 0), in loop order
     assert [tuple(x) for x in g if x[0] == 0] == [(0, 1), (0, 2), (0, 5), (0, 6), (0, 10)]
     assert len(oracle.pairs_grid(23, 3, 5, 0)) == len(oracle.pairs_grid(20, 3, 5, 1))
+
+
+def test_flann_restatement_recall_and_determinism():
+    """FLANN-style CPU baseline (oracle/flann_oracle.cpp): not a parity oracle
+    (the reference's FLANN is RNG-driven) — check it is
+    deterministic for a seed, never reports a match the exact path could not
+    (precision 1: every accepted FLANN neighbour is a true candidate whose
+    distance equals the exact distance to that row), and recalls the planted
+    neighbours; for both the kd-forest (SIFT) and LSH (ORB) indexes."""
+    for imgs in (synth.sift_images(3, 1200, seed=9), synth.orb_images(3, 1500, seed=9)):
+        pairs = oracle.pairs_unordered(3)
+        e, eo = oracle.match_pairs(imgs, pairs)
+        a1, ao1 = oracle.flann_match_pairs(imgs, pairs, nthreads=2)
+        a2, ao2 = oracle.flann_match_pairs(imgs, pairs, nthreads=3)
+        assert a1.tobytes() == a2.tobytes() and np.array_equal(ao1, ao2)
+        rec, prec = oracle.recall(e, eo, a1, ao1)
+        assert rec > 0.9 and prec > 0.95, (rec, prec)
+        for p, (l, r) in enumerate(pairs):
+            for m in a1[ao1[p]:ao1[p + 1]]:
+                q, t = imgs[l][m["queryIdx"]], imgs[r][m["trainIdx"]]
+                if imgs[0].dtype == np.float32:
+                    d = np.float32(np.sqrt(np.float32(((q - t) ** 2).sum())))
+                else:
+                    d = np.float32(np.unpackbits(q ^ t).sum())
+                assert m["distance"] == d
+
+
+def test_flann_restatement_edge_sizes():
+    base = synth.sift_images(3, 300, seed=4)
+    imgs = [base[0], base[1][:1], base[2][:0].reshape(0, 128)]
+    m, off = oracle.flann_match_pairs(imgs, np.array([[0, 1], [0, 2], [2, 0]], np.int32))
+    assert off[1] - off[0] == 300 and off[2] == off[1] and off[3] == off[2]   # Nt=1: all accepted; Nt=0: none
