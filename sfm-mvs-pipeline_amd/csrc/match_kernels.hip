@@ -827,7 +827,8 @@ hipError_t launch_orb_knn2(const WorkItem* work, int n_work, const PairDev* pair
     return hipGetLastError();
 }
 // ORB kernel selection: 0 (default) = FP4 MFMA path on 128-byte +-1 rows,
-// 1 = VALU xor/popcount path on 32-byte rows.  SFMX_ORB_VARIANT overrides.
+// 1 = VALU xor/popcount path on 32-byte rows, 2.. = FP4 MFMA tiling variants
+// (tuning only).  SFMX_ORB_VARIANT overrides.
 int orb_variant() {
     static int v = [] {
         const char* e = getenv("SFMX_ORB_VARIANT");
@@ -846,7 +847,15 @@ hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pair
                            const uint8_t* desc4, const int32_t* keyc, int32_t* out_idx, float* out_dist, double ratio,
                            hipStream_t st) {
     if (n_work == 0) return hipSuccess;
-    orb_mfma_kernel<2, 8, 2, 64><<<n_work, 512, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx, out_dist, ratio);
+#define ORB_LAUNCH(QT, W, MINW, ST) \
+    orb_mfma_kernel<QT, W, MINW, ST><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx, out_dist, ratio)
+    switch (orb_variant()) {      // every variant: QT * W * 32 = 512 queries per work item
+    case 2: ORB_LAUNCH(2, 8, 2, 64); break;
+    case 3: ORB_LAUNCH(2, 8, 2, 128); break;
+    case 4: ORB_LAUNCH(1, 16, 1, 128); break;
+    default: ORB_LAUNCH(4, 4, 2, 64);   // measured best (r01: 20.7 ms on config 4 vs 21.3-24.3)
+    }
+#undef ORB_LAUNCH
     return hipGetLastError();
 }
 hipError_t launch_assemble(const PairDev* pairs, int n_pairs, const ImgDev* imgs, const int32_t* out_idx,

@@ -149,7 +149,7 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
     }
     DeviceGuard g(m->device);
     m->norm = norm;
-    m->orb_fp4 = norm == SFMX_NORM_HAMMING && orb_variant() == 0;
+    m->orb_fp4 = norm == SFMX_NORM_HAMMING && orb_variant() != 1;
     m->n_imgs = n;
     m->imgs.assign(n, ImgDev{});
     m->has_run = false;
