@@ -374,9 +374,10 @@ void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, cons
                      const int* __restrict__ obs_cam, const int* __restrict__ campos, const double* __restrict__ J,
                      const double* __restrict__ scale, const double* __restrict__ D, double* __restrict__ Einv,
                      double* __restrict__ EinvG, double* __restrict__ R1, double* __restrict__ R2,
-                     double* __restrict__ vzpart, int* __restrict__ fail) {
+                     double* __restrict__ vzpart, int* __restrict__ fail, const int* __restrict__ plist, int nlist) {
     __shared__ double sh[8];
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int gi = blockIdx.x * blockDim.x + threadIdx.x;
+    const int p = plist ? (gi < nlist ? plist[gi] : P) : gi;   // plist: only these points (see ba_point_blocks_lds)
     const size_t ne = 3 * (size_t)P, ni = ne + 6 * (size_t)C;   // first camera / intrinsics column
     double VZ[K * K];
 #pragma unroll
@@ -469,6 +470,181 @@ void ba_point_blocks(int P, int O, int C, const int* __restrict__ pt_start, cons
                 const double qj = je[j][0] * eg[0] + je[j][1] * eg[1] + je[j][2] * eg[2];
                 r2[12 + 4 * K + j] = J[(size_t)o * jst(K) + j] - qj;
             }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) {
+        const double s = block_sum(VZ[i], sh);
+        if (threadIdx.x == 0) vzpart[(size_t)blockIdx.x * K * K + i] = s;
+    }
+}
+
+// Same outputs as ba_point_blocks, LDS-staged so that every HBM access is a
+// coalesced stream: one workgroup per host-built point group (points bp[2b] ..
+// bp[2b+1]: at most PB_MAXP points whose observations, contiguous in the
+// point-major internal order, number at most PB_CAPO).
+//   1. the group's Jacobian records J[o0 .. o1) are copied into LDS (16-B loads)
+//   2. one thread per point: E, g, V from LDS; Einv, Einv g, Z = Einv V -> LDS
+//   3. one thread per observation: its R1 and R2 records in registers
+//   4. R1[o0 .. o1) staged in LDS and stored contiguously; then the R2 records
+//      staged and stored record by record at their camera-major slots.
+// Points with more than CAPO observations go to ba_point_blocks (point list).
+constexpr int PB_CAPO = 256;   // observations per group (= threads: one per observation)
+constexpr int PB_MAXP = 64;    // points per group
+template <int K>
+__global__ __launch_bounds__(256)
+void ba_point_blocks_lds(const int* __restrict__ bp, int P, int C, const int* __restrict__ pt_start,
+                         const int* __restrict__ obs_cam, const int* __restrict__ campos, const double* __restrict__ J,
+                         const double* __restrict__ scale, const double* __restrict__ D, double* __restrict__ Einv,
+                         double* __restrict__ EinvG, double* __restrict__ R1, double* __restrict__ R2,
+                         double* __restrict__ vzpart, int* __restrict__ fail) {
+    constexpr int JS = jst(K), RS1 = r1s(K), RS2 = r2s(K);
+    constexpr int BUF = PB_CAPO * (RS1 > JS ? RS1 : JS);
+    constexpr int PD = 12 + 3 * K;                       // per point: Ei (9) | Einv g (3) | Z = Einv V (3K)
+    static_assert(JS % 2 == 0 && RS1 % 2 == 0 && RS2 % 2 == 0, "records must be whole 16-B pieces");
+    __shared__ __attribute__((aligned(16))) double buf[BUF];
+    __shared__ double pd[PB_MAXP * PD];
+    __shared__ int opt[PB_CAPO];                         // observation -> point slot in the group
+    __shared__ double sh[8];
+    const int tid = threadIdx.x, b = blockIdx.x;
+    const int p0 = bp[2 * b], np = bp[2 * b + 1] - p0;
+    const int o0 = pt_start[p0], no = pt_start[p0 + np] - o0;
+    const size_t ne = 3 * (size_t)P, ni = ne + 6 * (size_t)C;   // first camera / intrinsics column
+    {   // 1. J records of the group -> LDS
+        const double2* src = reinterpret_cast<const double2*>(J + (size_t)o0 * JS);
+        double2* dst = reinterpret_cast<double2*>(buf);
+        for (int i = tid; i < no * (JS / 2); i += 256) dst[i] = src[i];
+    }
+    double si[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) si[i] = scale[ni + i];
+    __syncthreads();
+    // 2. one thread per point
+    double VZ[K * K];
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) VZ[i] = 0.0;
+    if (tid < np) {
+        const int p = p0 + tid;
+        const int a0 = pt_start[p] - o0, a1 = pt_start[p + 1] - o0;
+        const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
+        double E[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0}, V[3 * K];
+#pragma unroll
+        for (int i = 0; i < 3 * K; ++i) V[i] = 0.0;
+        for (int a = a0; a < a1; ++a) {
+            opt[a] = tid;
+            const double* jr = buf + a * JS;
+            const double r[2] = {jr[0], jr[1]};
+            double je[2][3], ji[2][K];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+#pragma unroll
+                for (int u = 0; u < 3; ++u) je[j][u] = jr[2 + 3 * j + u] * sp[u];
+#pragma unroll
+                for (int i = 0; i < K; ++i) ji[j][i] = jr[20 + K * j + i] * si[i];
+            }
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+#pragma unroll
+                for (int v = 0; v < 3; ++v) E[u * 3 + v] += je[0][u] * je[0][v] + je[1][u] * je[1][v];
+                g[u] += je[0][u] * r[0] + je[1][u] * r[1];
+#pragma unroll
+                for (int i = 0; i < K; ++i) V[u * K + i] += je[0][u] * ji[0][i] + je[1][u] * ji[1][i];
+            }
+        }
+        const double d0 = D[3 * (size_t)p], d1 = D[3 * (size_t)p + 1], d2 = D[3 * (size_t)p + 2];
+        E[0] += d0 * d0; E[4] += d1 * d1; E[8] += d2 * d2;
+        double Ei[9];
+        if (!inv3_spd(E, Ei)) {
+            atomicOr(fail, 1);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) Ei[i] = 0.0;
+        }
+        double* q = pd + tid * PD;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) { Einv[9 * (size_t)p + i] = Ei[i]; q[i] = Ei[i]; }
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const double eg = Ei[u * 3] * g[0] + Ei[u * 3 + 1] * g[1] + Ei[u * 3 + 2] * g[2];
+            EinvG[3 * (size_t)p + u] = eg;
+            q[9 + u] = eg;
+        }
+        double Z[3 * K];
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                Z[u * K + i] = Ei[u * 3] * V[i] + Ei[u * 3 + 1] * V[K + i] + Ei[u * 3 + 2] * V[2 * K + i];
+                q[12 + u * K + i] = Z[u * K + i];
+            }
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+#pragma unroll
+            for (int l = 0; l < K; ++l) VZ[i * K + l] = V[i] * Z[l] + V[K + i] * Z[K + l] + V[2 * K + i] * Z[2 * K + l];
+    }
+    __syncthreads();
+    // 3. one thread per observation: R1 / R2 records in registers
+    double r1[RS1], r2[RS2];
+    const int a = tid;
+    if (a < no) {
+        const int o = o0 + a, lp = opt[a], p = p0 + lp;
+        const double* jr = buf + a * JS;
+        const double* q = pd + lp * PD;
+        const size_t nc = ne + 6 * (size_t)obs_cam[o];
+        const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
+        double je[2][3];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int u = 0; u < 3; ++u) { je[j][u] = jr[2 + 3 * j + u] * sp[u]; r1[3 * j + u] = je[j][u]; }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double v = jr[8 + 6 * j + i] * scale[nc + i];
+                r1[12 + 6 * j + i] = v;
+                r2[6 * j + i] = v;
+            }
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const double v = jr[20 + K * j + i] * si[i];
+                r1[24 + K * j + i] = v;
+                r2[12 + K * j + i] = v;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) r1[6 + u * 2 + j] = q[u * 3] * je[j][0] + q[u * 3 + 1] * je[j][1] + q[u * 3 + 2] * je[j][2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                r2[12 + 2 * K + K * j + i] = je[j][0] * q[12 + i] + je[j][1] * q[12 + K + i] + je[j][2] * q[12 + 2 * K + i];
+            const double qj = je[j][0] * q[9] + je[j][1] * q[10] + je[j][2] * q[11];
+            r2[12 + 4 * K + j] = jr[j] - qj;
+        }
+    }
+    __syncthreads();   // every J read is done: buf is free
+    // 4. R1 (point-major, contiguous for the group) through LDS
+    if (a < no) {
+#pragma unroll
+        for (int i = 0; i < RS1; ++i) buf[a * RS1 + i] = r1[i];
+    }
+    __syncthreads();
+    {
+        const double2* src = reinterpret_cast<const double2*>(buf);
+        double2* dst = reinterpret_cast<double2*>(R1 + (size_t)o0 * RS1);
+        for (int i = tid; i < no * (RS1 / 2); i += 256) dst[i] = src[i];
+    }
+    __syncthreads();
+    if (a < no) {
+#pragma unroll
+        for (int i = 0; i < RS2; ++i) buf[a * RS2 + i] = r2[i];
+    }
+    __syncthreads();
+    {   // R2 records at their camera-major slots, RS2/2 lanes per record
+        const double2* src = reinterpret_cast<const double2*>(buf);
+        for (int i = tid; i < no * (RS2 / 2); i += 256) {
+            const int rec = i / (RS2 / 2), e = i - rec * (RS2 / 2);
+            reinterpret_cast<double2*>(R2 + (size_t)campos[o0 + rec] * RS2)[e] = src[i];
         }
     }
 #pragma unroll

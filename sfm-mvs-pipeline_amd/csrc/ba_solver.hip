@@ -17,6 +17,7 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <cstdlib>
 #include <unordered_map>
 #include <vector>
 
@@ -69,6 +70,8 @@ struct sfmx_ba_ctx {
     void* ar_user = nullptr;
     // topology
     Buf obs_point, obs_cam, obs_xy, pt_start, pt_obs, cam_start, cam_obs, campos, blk_cam, blk_start, trip;
+    Buf pgrp, pbig;   // ba_point_blocks_lds point groups (bounds) / points with more than PB_CAPO observations
+    int ngrp = 0, nbig = 0;
     // state
     Buf x, cand, scale, colsq, grad, diag, D, J, partA, partB, scal, ipart;
     Buf Einv, EinvG, R1, R2, vzpart, Scc, Spi, Sii, rc, ri, Spp, SR, Linv, sol, step, failf;
@@ -79,7 +82,7 @@ struct sfmx_ba_ctx {
     double phase_ms[4] = {0, 0, 0, 0};
     hipEvent_t ev[6] = {};
     ~sfmx_ba_ctx() {
-        Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &pt_obs, &cam_start, &cam_obs, &campos, &blk_cam,
+        Buf* all[] = {&pgrp, &pbig, &obs_point, &obs_cam, &obs_xy, &pt_start, &pt_obs, &cam_start, &cam_obs, &campos, &blk_cam,
                       &blk_start, &trip, &x, &cand, &scale, &colsq, &grad, &diag, &D, &J, &partA, &partB, &scal,
                       &ipart, &Einv, &EinvG, &R1, &R2, &vzpart, &Scc, &Spi, &Sii, &rc, &ri, &Spp, &SR, &Linv, &sol,
                       &step, &failf};
@@ -195,10 +198,17 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
                        c->D.as<double>());
     HIPCHK(hipMemsetAsync(fl, 0, sizeof(int), c->st));
 #define SCHUR(KK)                                                                                                      \
-    hipLaunchKernelGGL(ba_point_blocks<KK>, dim3(c->nvz), dim3(256), 0, c->st, P, O, C, c->pt_start.as<int>(),         \
-                       c->pt_obs.as<int>(), c->obs_cam.as<int>(), c->campos.as<int>(), c->J.as<double>(),              \
-                       c->scale.as<double>(), c->D.as<double>(), c->Einv.as<double>(), c->EinvG.as<double>(),          \
-                       c->R1.as<double>(), c->R2.as<double>(), c->vzpart.as<double>(), fl);                            \
+    if (c->ngrp > 0)                                                                                                   \
+        hipLaunchKernelGGL(ba_point_blocks_lds<KK>, dim3(c->ngrp), dim3(256), 0, c->st, c->pgrp.as<int>(), P, C,       \
+                           c->pt_start.as<int>(), c->obs_cam.as<int>(), c->campos.as<int>(), c->J.as<double>(),        \
+                           c->scale.as<double>(), c->D.as<double>(), c->Einv.as<double>(), c->EinvG.as<double>(),      \
+                           c->R1.as<double>(), c->R2.as<double>(), c->vzpart.as<double>(), fl);                        \
+    if (c->nbig > 0)                                                                                                   \
+        hipLaunchKernelGGL(ba_point_blocks<KK>, dim3(nblk(c->nbig)), dim3(256), 0, c->st, P, O, C, c->pt_start.as<int>(), \
+                           c->pt_obs.as<int>(), c->obs_cam.as<int>(), c->campos.as<int>(), c->J.as<double>(),          \
+                           c->scale.as<double>(), c->D.as<double>(), c->Einv.as<double>(), c->EinvG.as<double>(),      \
+                           c->R1.as<double>(), c->R2.as<double>(), c->vzpart.as<double>() + (size_t)c->ngrp * KK * KK, \
+                           fl, c->pbig.as<int>(), c->nbig);                                                            \
     if (C > 0)                                                                                                         \
         hipLaunchKernelGGL(ba_cam_blocks<KK>, dim3(C), dim3(256), 0, c->st, C, c->cam_start.as<int>(),                 \
                            c->R2.as<double>(), c->Scc.as<double>(), c->Spi.as<double>(), c->rc.as<double>(),           \
@@ -540,7 +550,27 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
                 }
     }
     c->nblocks = NBLK;
-    c->nvz = (int)nblk(P);
+    // point groups for ba_point_blocks_lds: consecutive points, <= PB_MAXP points and
+    // <= PB_CAPO observations per group; a point with more observations goes to the
+    // point-list fallback (ba_point_blocks)
+    std::vector<int> pgrp, pbig;
+    const char* pbenv = std::getenv("SFMX_BA_POINT_KERNEL");   // "list": every point via ba_point_blocks (A/B tuning)
+    if (pbenv && std::strcmp(pbenv, "list") == 0)
+        for (int p = 0; p < P; ++p) pbig.push_back(p);
+    for (int p = pbig.empty() ? 0 : P; p < P;) {
+        const int cnt = pt_start[p + 1] - pt_start[p];
+        if (cnt > PB_CAPO) { pbig.push_back(p); ++p; continue; }
+        pgrp.push_back(p);   // group = [pgrp[2g], pgrp[2g+1])
+        int np = 0, no = 0;
+        while (p < P && np < PB_MAXP && pt_start[p + 1] - pt_start[p] <= PB_CAPO && no + (pt_start[p + 1] - pt_start[p]) <= PB_CAPO) {
+            no += pt_start[p + 1] - pt_start[p];
+            ++np; ++p;
+        }
+        pgrp.push_back(p);
+    }
+    c->ngrp = (int)pgrp.size() / 2;
+    c->nbig = (int)pbig.size();
+    c->nvz = c->ngrp + (c->nbig ? (int)nblk(c->nbig) : 0);
     std::vector<int> op(pb->obs_point, pb->obs_point + O), oc(pb->obs_cam, pb->obs_cam + O);
     std::vector<double> oxy(pb->obs_xy, pb->obs_xy + 2 * (size_t)O);
     hipStream_t st = c->st;
@@ -550,7 +580,7 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
         (rc = upload(c->cam_start, cam_start, st)) || (rc = upload(c->cam_obs, cam_obs, st)) ||
         (rc = upload(c->campos, campos, st)) ||
         (rc = upload(c->blk_cam, blk_cam, st)) || (rc = upload(c->blk_start, blk_start, st)) ||
-        (rc = upload(c->trip, trip, st)))
+        (rc = upload(c->trip, trip, st)) || (rc = upload(c->pgrp, pgrp, st)) || (rc = upload(c->pbig, pbig, st)))
         return bail(rc);
     const size_t n = c->n, so = std::max(O, 1);
     const int NI = std::max(2 * K, K * (K + 1) / 2 + K);
@@ -561,7 +591,7 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
         {&c->partB, 8 * (size_t)nblk(std::max<int64_t>(O, n))}, {&c->scal, 8 * 16},
         {&c->ipart, 8 * (size_t)std::max(C, 1) * NI}, {&c->Einv, 72 * (size_t)std::max(P, 1)},
         {&c->EinvG, 24 * (size_t)std::max(P, 1)}, {&c->R1, 8 * so * r1s(K)}, {&c->R2, 8 * so * r2s(K)},
-        {&c->vzpart, 8 * (size_t)c->nvz * K * K}, {&c->Linv, 8 * (size_t)2 * NB * NB},
+        {&c->vzpart, 8 * (size_t)std::max(c->nvz, 1) * K * K}, {&c->Linv, 8 * (size_t)2 * NB * NB},
         {&c->Scc, 288 * (size_t)std::max(C, 1)}, {&c->Spi, 48 * (size_t)K * std::max(C, 1)}, {&c->Sii, 8 * (size_t)K * K},
         {&c->rc, 48 * (size_t)std::max(C, 1)}, {&c->ri, 8 * (size_t)K}, {&c->Spp, 288 * (size_t)std::max(NBLK, 1)},
         {&c->SR, 8 * ((size_t)c->npad * c->npad + c->npad)}, {&c->failf, 64}};

@@ -101,3 +101,25 @@ def test_point_sharded_two_ranks_match_single():
     P, sm, _ = gpu_solve(p)
     assert abs(r["initial_cost"] - sm["initial_cost"]) <= 1e-12 * sm["initial_cost"]
     assert abs(r["final_cost"] - sm["final_cost"]) <= COST_RTOL * sm["final_cost"]
+
+
+def test_mixed_track_lengths_matches_oracle():
+    """Points with more observations than one LDS point group holds (PB_CAPO =
+    256) take the point-list fallback of the Schur point kernel; short tracks
+    share the problem (LDS point groups)."""
+    from oracle import oracle
+    long_tracks = synth.ba_problem(300, 40, seed=27, obs_per_point=280)
+    short = synth.ba_problem(300, 3000, seed=28, obs_per_point=4)
+    P0 = len(long_tracks["points"])
+    p = dict(short)
+    p["points"] = np.concatenate([long_tracks["points"], short["points"]])
+    p["obs_point"] = np.concatenate([long_tracks["obs_point"], short["obs_point"] + P0]).astype(np.int32)
+    p["obs_cam"] = np.concatenate([long_tracks["obs_cam"], short["obs_cam"]]).astype(np.int32)
+    p["obs_xy"] = np.concatenate([long_tracks["obs_xy"], short["obs_xy"]])
+    p["poses"] = short["poses"]
+    _, osm, otr = oracle.ba_solve(p, trace_cap=512, max_num_iterations=8)
+    P, sm, tr = gpu_solve(p, max_num_iterations=8)
+    assert sm["termination_type"] == osm["termination_type"]
+    assert abs(sm["final_cost"] - osm["final_cost"]) <= COST_RTOL * osm["final_cost"]
+    n = min(len(tr), len(otr))
+    assert np.array_equal(tr[:n, 2], otr[:n, 2])
