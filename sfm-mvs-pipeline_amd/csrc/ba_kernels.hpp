@@ -860,40 +860,46 @@ __global__ void ba_add_damping(int P, int nf, int npad, const double* __restrict
 // W_k lives in a ping-pong buffer; rhs is overwritten with w = D~^-1 L~^-1 b
 // during the factorisation, then with x by the back solve.
 constexpr int LDT = NB + 2;   // LDS row stride (doubles): 16-B aligned rows
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void tile_load(double (*dst)[LDT], const double* __restrict__ src, int ld, bool transpose) {
-    double v[NB * NB / 256];
+// 64x64 fp64 tiles on the matrix cores: v_mfma_f64_16x16x4f64 (operands: lane
+// m + 16k holds A[m][k] and B[k][n = m]; result register r of lane l is
+// D[l/16 + 4r][l%16], checked by tools/micro/mfma_f64_layout.hip).  Wave w of
+// the 256-thread block owns the row strip 16w..16w+15 and four 16x16 column
+// tiles: acc[c][r] = out[16w + l/16 + 4r][16c + l%16].
+__device__ __forceinline__ int trow(int r) { return ((threadIdx.x & 63) >> 4) + 4 * r; }   // row in the strip
+__device__ __forceinline__ int tcol() { return threadIdx.x & 15; }
+
+__device__ __forceinline__ void tile_load(double (*dst)[LDT], const double* __restrict__ src, int ld) {
 #pragma unroll
-    for (int q = 0; q < NB * NB / 256; ++q) {
-        const int e = q * 256 + threadIdx.x;
-        v[q] = src[(size_t)(e / NB) * ld + e % NB];
-    }
-#pragma unroll
-    for (int q = 0; q < NB * NB / 256; ++q) {
-        const int e = q * 256 + threadIdx.x;
-        if (transpose) dst[e % NB][e / NB] = v[q];
-        else dst[e / NB][e % NB] = v[q];
+    for (int q = 0; q < NB * NB / 512; ++q) {
+        const int e = q * 512 + 2 * threadIdx.x;
+        *reinterpret_cast<double2*>(&dst[e / NB][e % NB]) = *reinterpret_cast<const double2*>(src + (size_t)(e / NB) * ld + e % NB);
     }
 }
 
-// acc[u][w] = sum_l At[l][4ty+u] * Bt[l][4tx+w]   (= (A B^T) for At = A^T, Bt = B^T)
-__device__ __forceinline__ void tile_gemm(const double (*At)[LDT], const double (*Bt)[LDT], double acc[4][4]) {
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+// acc[c] = A[strip] * B          (A, B row-major 64x64 in LDS)
+__device__ __forceinline__ void mfma_nn(const double (*A)[LDT], const double (*B)[LDT], f64x4 acc[4]) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, m = l & 15, kq = l >> 4;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) acc[u][w] = 0.0;
+    for (int c = 0; c < 4; ++c) acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
-    for (int l = 0; l < NB; ++l) {
-        const double2 a01 = *reinterpret_cast<const double2*>(&At[l][4 * ty]);
-        const double2 a23 = *reinterpret_cast<const double2*>(&At[l][4 * ty + 2]);
-        const double2 b01 = *reinterpret_cast<const double2*>(&Bt[l][4 * tx]);
-        const double2 b23 = *reinterpret_cast<const double2*>(&Bt[l][4 * tx + 2]);
-        const double a[4] = {a01.x, a01.y, a23.x, a23.y}, b[4] = {b01.x, b01.y, b23.x, b23.y};
+    for (int st = 0; st < NB / 4; ++st) {
+        const double av = A[16 * w + m][4 * st + kq];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, B[4 * st + kq][16 * c + m], acc[c], 0, 0, 0);
+    }
+}
+// acc[c] = A[strip] * X^T        (A, X row-major 64x64 in LDS)
+__device__ __forceinline__ void mfma_nt(const double (*A)[LDT], const double (*X)[LDT], f64x4 acc[4]) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, m = l & 15, kq = l >> 4;
 #pragma unroll
-            for (int w = 0; w < 4; ++w) acc[u][w] = fma(a[u], b[w], acc[u][w]);
+    for (int c = 0; c < 4; ++c) acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int st = 0; st < NB / 4; ++st) {
+        const double av = A[16 * w + m][4 * st + kq];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, X[16 * c + m][4 * st + kq], acc[c], 0, 0, 0);
     }
 }
 
@@ -906,132 +912,189 @@ __device__ __forceinline__ double rcp_nr(double d) {
     return fma(r, e, r);
 }
 
-// W_k = D~_k^-1 by symmetric block sweeps (256 threads; thread (ty, tx) holds
-// the 4x4 block at rows 4ty.., cols 4tx..).  Sweeping the 4x4 pivot block B
-// with Q = A_BB^-1:  a_il -= A_iB Q A_Bl (i, l not in B), A_iB <- A_iB Q,
-// A_Bl <- Q A_Bl, A_BB <- -Q; after all 16 blocks the tile holds -A^-1.  Q
-// itself comes from 4 scalar sweeps whose pivots are the scalar Cholesky
-// pivots (failure detection).  One barrier per 4 pivots.  Then rhs_k <- W_k rhs_k.
-__device__ __forceinline__ void chol_diag_tile(double* __restrict__ S, int npad, int k, double* __restrict__ Wout,
-                                               double* __restrict__ rhs, int* __restrict__ fail, double (*buf)[LDT],
-                                               double (*colP)[NB][4]) {
-    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4, k0 = k * NB;
-    double t[4][4];
+// W_k = D~_k^-1 by symmetric block sweeps.  Sweeping the pivot block B with
+// Q = A_BB^-1:  a_il -= A_iB Q A_Bl (i, l not in B), A_iB <- A_iB Q,
+// A_Bl <- Q A_Bl, A_BB <- -Q; after all blocks the tile holds -A^-1.
+// Two levels (256 threads, the tile in registers in the MFMA layout above):
+//   outer: 4 sweeps of 16-wide pivot blocks — the column panel A_:B goes
+//          through LDS; M = A_:B Q (per wave, its own strip) and the rank-16
+//          update of the other column tiles run on the fp64 matrix cores;
+//   inner: Qn = -A_BB^-1 (16x16) by wave 0 alone (no barriers): 8 sweeps of
+//          2x2 pivot blocks, each lane holding a 2x2 block; the 2x2 pivot
+//          inverse is closed-form and its two scalar pivots (a, det/a) are the
+//          scalar Cholesky pivots, i.e. exactly where LLT would fail.
+// Then rhs_k <- W_k rhs_k.
+constexpr int LDP = 18;   // LDS row stride of the 16-wide panels (16-B aligned rows)
+#ifdef SFMX_CHOL_STAMPS   // tools/micro/chol_tile.hip: phase timestamps of block 0 (never in the product build)
+__device__ long long g_chol_stamps[64];
+#define CHOL_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_chol_stamps[i] = wall_clock64(); } while (0)
+#else
+#define CHOL_STAMP(i) do { } while (0)
+#endif
+
+__device__ __forceinline__ void inner_inverse16(const double* __restrict__ Pc, int s, double* __restrict__ Qn,
+                                                double* __restrict__ ipan, bool& bad) {
+    // wave 0 only: Qn = -(Pc[16s + i][j])^-1, i, j < 16
+    const int lane = threadIdx.x & 63, r = lane >> 3, c = lane & 7;
+    double p[2][2];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const double* row = S + (size_t)(k0 + 4 * ty + u) * npad + k0 + 4 * tx;
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int w = 0; w < 4; ++w) t[u][w] = row[w];
+        for (int w = 0; w < 2; ++w) p[u][w] = Pc[(16 * s + 2 * r + u) * LDP + 2 * c + w];
+    for (int j = 0; j < 8; ++j) {
+        if (c == j) {   // column panel of the pivot block: rows 2r.., cols 2j..
+            *reinterpret_cast<double2*>(&ipan[(2 * r) * 2]) = make_double2(p[0][0], p[0][1]);
+            *reinterpret_cast<double2*>(&ipan[(2 * r + 1) * 2]) = make_double2(p[1][0], p[1][1]);
+        }
+        __builtin_amdgcn_wave_barrier();
+        const double2 b0 = *reinterpret_cast<const double2*>(&ipan[(2 * j) * 2]);
+        const double2 b1 = *reinterpret_cast<const double2*>(&ipan[(2 * j + 1) * 2]);
+        const double2 i0 = *reinterpret_cast<const double2*>(&ipan[(2 * r) * 2]);
+        const double2 i1 = *reinterpret_cast<const double2*>(&ipan[(2 * r + 1) * 2]);
+        const double2 l0 = *reinterpret_cast<const double2*>(&ipan[(2 * c) * 2]);
+        const double2 l1 = *reinterpret_cast<const double2*>(&ipan[(2 * c + 1) * 2]);
+        __builtin_amdgcn_wave_barrier();
+        // q = -[a b; b d]^-1
+        const double a = b0.x, bb = b0.y, d = b1.y;
+        double det = fma(a, d, -bb * bb);
+        if (!(a > 0.0) || !isfinite(a) || !(det > 0.0) || !isfinite(det)) { bad = true; det = 1.0; }
+        const double rd = rcp_nr(det);
+        const double q00 = -d * rd, q01 = bb * rd, q11 = -a * rd;   // q10 = q01
+        const bool rowB = (r == j), colB = (c == j);
+        double m[2][2];
+        {
+            const double ai[2][2] = {{i0.x, i0.y}, {i1.x, i1.y}};
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const double v0 = -(ai[u][0] * q00 + ai[u][1] * q01), v1 = -(ai[u][0] * q01 + ai[u][1] * q11);
+                m[u][0] = rowB ? (u == 0 ? q00 : q01) : v0;
+                m[u][1] = rowB ? (u == 0 ? q01 : q11) : v1;
+            }
+        }
+        const double al[2][2] = {{l0.x, l0.y}, {l1.x, l1.y}};   // al[w][b] = A_(2c+w),(2j+b) = A_Bl[b][w]
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                if (colB) p[u][w] = m[u][w];
+                else p[u][w] = (rowB ? 0.0 : p[u][w]) - (m[u][0] * al[w][0] + m[u][1] * al[w][1]);
+            }
     }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int w = 0; w < 2; ++w) Qn[(2 * r + u) * LDP + 2 * c + w] = p[u][w];
+}
+
+// t: the (updated) diagonal tile k in registers (MFMA layout); rk: rhs_k in LDS.
+// workspace: >= 2624 doubles of LDS (buf = 64 x LDT)
+__device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __restrict__ Wout,
+                                               double* __restrict__ rhs, const double* __restrict__ rk,
+                                               int* __restrict__ fail, double (*buf)[LDT]) {
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, m = l & 15, kq = l >> 4, k0 = k * NB;
+    double* ws = &buf[0][0];
+    double* Pc = ws;                       // [64][LDP]  column panel A_:B
+    double* Qn = ws + NB * LDP;            // [16][LDP]  -A_BB^-1
+    double* ipan = Qn + 16 * LDP;          // [16][2]    inner column panel
+    double* Mw = ipan + 32 + 16 * LDP * w; // [16][LDP]  this wave's -M strip
+    CHOL_STAMP(0);
     bool bad = false;
-    for (int jb = 0; jb < NB / 4; ++jb) {
-        double (*P)[4] = colP[jb & 1];
-        if (tx == jb) {
+    CHOL_STAMP(1);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                *reinterpret_cast<double2*>(&P[4 * ty + u][0]) = make_double2(t[u][0], t[u][1]);
-                *reinterpret_cast<double2*>(&P[4 * ty + u][2]) = make_double2(t[u][2], t[u][3]);
-            }
-        }
-        const bool rowB = (ty == jb), colB = (tx == jb);
+    for (int s = 0; s < NB / 16; ++s) {
+        const bool rowB = (w == s);
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int w = 0; w < 4; ++w) t[u][w] = (rowB || colB) ? 0.0 : t[u][w];
+        for (int r = 0; r < 4; ++r) Pc[(16 * w + trow(r)) * LDP + tcol()] = t[s][r];
         __syncthreads();
-        // q = -P^-1 by scalar sweeps of the 4x4 pivot block (same values in every lane)
-        double q[4][4];
+        CHOL_STAMP(2 + 4 * s);
+        if (tid < 64) inner_inverse16(Pc, s, Qn, ipan, bad);
+        __syncthreads();
+        CHOL_STAMP(3 + 4 * s);
+        // M = A_(strip),B Q on the matrix cores; rows in B take Q itself (-Qn)
+        f64x4 mm = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int st = 0; st < 4; ++st)
+            mm = __builtin_amdgcn_mfma_f64_16x16x4f64(Pc[(16 * w + m) * LDP + 4 * st + kq], Qn[(4 * st + kq) * LDP + m], mm, 0, 0, 0);
+        f64x4 mv;
 #pragma unroll
-            for (int l = 0; l < 4; ++l) q[i][l] = P[4 * jb + i][l];
+        for (int r = 0; r < 4; ++r) mv[r] = rowB ? Qn[trow(r) * LDP + tcol()] : -mm[r];   // M (Qn = -Q)
+        t[s] = mv;                                                         // A_iB <- A_iB Q, A_BB <- -Q
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            double d = q[j][j];
-            if (!(d > 0.0) || !isfinite(d)) { bad = true; d = 1.0; }
-            const double r = rcp_nr(d);
-            double c[4];
+        for (int r = 0; r < 4; ++r) Mw[trow(r) * LDP + tcol()] = -mv[r];   // -M as the A operand
+        __builtin_amdgcn_wave_barrier();
+        CHOL_STAMP(4 + 4 * s);
+        // a_il -= M[i][:] A_l,B for the other column tiles (rows in B start from 0)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) c[i] = q[i][j];
+        for (int c = 0; c < 4; ++c) {
+            if (c == s) continue;
+            f64x4 acc = rowB ? f64x4{0.0, 0.0, 0.0, 0.0} : t[c];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const double m = (i == j) ? -r : c[i] * r;
-#pragma unroll
-                for (int l = 0; l < 4; ++l) {
-                    const double cl = (l == j) ? -1.0 : c[l];
-                    const double base = (i == j || l == j) ? 0.0 : q[i][l];
-                    q[i][l] = fma(-m, cl, base);
-                }
-            }
+            for (int st = 0; st < 4; ++st)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Mw[m * LDP + 4 * st + kq], Pc[(16 * c + m) * LDP + 4 * st + kq], acc, 0, 0, 0);
+            t[c] = acc;
         }
-        // row multipliers m[u] = A_iB Q (i not in B) or -Q = q (i in B)
-        double m[4][4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const double2 a01 = *reinterpret_cast<const double2*>(&P[4 * ty + u][0]);
-            const double2 a23 = *reinterpret_cast<const double2*>(&P[4 * ty + u][2]);
-            const double av[4] = {a01.x, a01.y, a23.x, a23.y};
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const double v = -(av[0] * q[0][b] + av[1] * q[1][b] + av[2] * q[2][b] + av[3] * q[3][b]);
-                m[u][b] = rowB ? q[u][b] : v;
-            }
-        }
-        // column factors cl[w] = A_Bl (l not in B) or -e_l (l in B)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const double2 c01 = *reinterpret_cast<const double2*>(&P[4 * tx + w][0]);
-            const double2 c23 = *reinterpret_cast<const double2*>(&P[4 * tx + w][2]);
-            const double cv[4] = {c01.x, c01.y, c23.x, c23.y};
-            double cl[4];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) cl[b] = colB ? (b == w ? -1.0 : 0.0) : cv[b];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                t[u][w] = fma(-m[u][0], cl[0], fma(-m[u][1], cl[1], fma(-m[u][2], cl[2], fma(-m[u][3], cl[3], t[u][w]))));
-        }
+        __syncthreads();   // Pc is rewritten by the next sweep
+        CHOL_STAMP(5 + 4 * s);
     }
-    if (bad && tid == 0) atomicOr(fail, 1);
+    if (bad) atomicOr(fail, 1);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            buf[4 * ty + u][4 * tx + w] = -t[u][w];
-            Wout[(4 * ty + u) * NB + 4 * tx + w] = -t[u][w];
+        for (int r = 0; r < 4; ++r) {
+            const int i = 16 * w + trow(r), j = 16 * c + tcol();
+            buf[i][j] = -t[c][r];
+            Wout[i * NB + j] = -t[c][r];
         }
     __syncthreads();
-    double* yk = &colP[0][0][0];
-    if (tid < NB) {
-        double s = 0.0;
-        for (int c = 0; c < NB; ++c) s = fma(buf[tid][c], rhs[k0 + c], s);
-        yk[tid] = s;
+    CHOL_STAMP(20);
+    {   // rhs_k <- W_k rhs_k: 4 threads per row, 16 terms each
+        const int i = tid >> 2, q = tid & 3;
+        double sum = 0.0;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) sum = fma(buf[i][4 * c + q], rk[4 * c + q], sum);
+        sum += __shfl_xor(sum, 1);
+        sum += __shfl_xor(sum, 2);
+        if (q == 0) rhs[k0 + i] = sum;
     }
-    __syncthreads();
-    if (tid < NB) rhs[k0 + tid] = yk[tid];
+    CHOL_STAMP(21);
 }
 
 struct alignas(16) CholLds {
     double a[NB][LDT], m[NB][LDT], n[NB][LDT];
-    double colP[2][NB][4];
+    double rk[NB], ra[NB];   // rhs_k (= w_k after panel k's inverse), rhs_a
 };
+
+__device__ __forceinline__ void tile_regs(f64x4 (&t)[4], const double* __restrict__ src, int ld) {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[c][r] = src[(size_t)(16 * w + trow(r)) * ld + 16 * c + tcol()];
+}
 
 __global__ __launch_bounds__(256)
 void chol_first(double* __restrict__ S, int npad, double* __restrict__ W, double* __restrict__ rhs,
                 int* __restrict__ fail) {
     __shared__ CholLds sm;
-    chol_diag_tile(S, npad, 0, W, rhs, fail, sm.a, sm.colP);
+    f64x4 t[4];
+    tile_regs(t, S, npad);
+    if (threadIdx.x < NB) sm.rk[threadIdx.x] = rhs[threadIdx.x];
+    __syncthreads();
+    chol_diag_tile(t, 0, W, rhs, sm.rk, fail, sm.a);
 }
 
 // Panel k: one block per trailing lower tile (a, b), k < b <= a.  Block 0 is
-// (k+1, k+1); after its update it inverts that tile for panel k+1.
+// (k+1, k+1); after its update it inverts that tile for panel k+1 (its updated
+// value never goes back to S: only W_{k+1} is needed later).
 //   G = A_ak W_k
 //   b <  a : A_ab -= G A_bk^T
-//   b == a : A_aa -= G A_ak^T;  G^T -> upper tile (k, a);  rhs_a -= A_ak w_k (= G z_k)
+//   b == a : A_aa -= G A_ak^T;  G^T -> upper tile (k, a);  rhs_a -= A_ak w_k
+// The destination tile is prefetched into registers before the GEMMs.
 __global__ __launch_bounds__(256)
 void chol_step(double* __restrict__ S, int npad, int k, double* __restrict__ W, double* __restrict__ rhs,
                int* __restrict__ fail) {
     __shared__ CholLds sm;
-    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int tid = threadIdx.x, w = tid >> 6;
     int a = k + 1, b = k + 1;
     if (blockIdx.x > 0) {   // tile rows a >= k + 2 hold a - k tiles (b = k+1 .. a)
         int rem = blockIdx.x - 1;
@@ -1040,38 +1103,61 @@ void chol_step(double* __restrict__ S, int npad, int k, double* __restrict__ W, 
     }
     const int k0 = k * NB, a0 = a * NB, b0 = b * NB;
     const bool diagblk = (a == b);
-    tile_load(sm.a, S + (size_t)a0 * npad + k0, npad, true);                   // A_ak^T
-    tile_load(sm.m, W + (size_t)(k & 1) * NB * NB, NB, false);                 // W_k
-    if (!diagblk) tile_load(sm.n, S + (size_t)b0 * npad + k0, npad, true);     // A_bk^T
-    __syncthreads();
-    double g[4][4];
-    tile_gemm(sm.a, sm.m, g);   // G[i][j] = sum_l A_ak[i][l] W[l][j]
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) sm.m[4 * tx + w][4 * ty + u] = g[u][w];   // G^T
-    __syncthreads();
-    double upd[4][4];
-    tile_gemm(sm.m, diagblk ? sm.a : sm.n, upd);
+    CHOL_STAMP(30);
+    f64x4 t[4];
     double* dst = S + (size_t)a0 * npad + b0;
+    tile_regs(t, dst, npad);                                             // A_ab (prefetch)
+    tile_load(sm.a, S + (size_t)a0 * npad + k0, npad);                   // A_ak
+    tile_load(sm.m, W + (size_t)(k & 1) * NB * NB, NB);                  // W_k
+    if (!diagblk) tile_load(sm.n, S + (size_t)b0 * npad + k0, npad);     // A_bk
+    else if (tid < NB) { sm.rk[tid] = rhs[k0 + tid]; sm.ra[tid] = rhs[a0 + tid]; }
+    __syncthreads();
+    CHOL_STAMP(31);
+    f64x4 g[4];
+    mfma_nn(sm.a, sm.m, g);   // G = A_ak W_k
+    __syncthreads();
+    CHOL_STAMP(32);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-        for (int w = 0; w < 4; ++w) dst[(size_t)(4 * ty + u) * npad + 4 * tx + w] -= upd[u][w];
+        for (int r = 0; r < 4; ++r) sm.m[16 * w + trow(r)][16 * c + tcol()] = g[c][r];
+    __syncthreads();
+    f64x4 upd[4];
+    mfma_nt(sm.m, diagblk ? sm.a : sm.n, upd);   // G X^T
+#pragma unroll
+    for (int c = 0; c < 4; ++c) t[c] -= upd[c];
+    CHOL_STAMP(33);
     if (diagblk) {
-        // upper tile (k, a): row k0 + j, column a0 + i holds G[i][j] = G^T[j][i]
-        for (int e = tid; e < NB * NB; e += 256) S[(size_t)(k0 + e / NB) * npad + a0 + e % NB] = sm.m[e / NB][e % NB];
-        if (tid < NB) {
-            double s = 0.0;
-            for (int j = 0; j < NB; ++j) s = fma(sm.a[j][tid], rhs[k0 + j], s);   // G z_k = A_ak w_k
-            rhs[a0 + tid] -= s;
+        {   // rhs_a -= A_ak w_k: 4 threads per row
+            const int i = tid >> 2, q = tid & 3;
+            double sum = 0.0;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) sum = fma(sm.a[i][4 * c + q], sm.rk[4 * c + q], sum);
+            sum += __shfl_xor(sum, 1);
+            sum += __shfl_xor(sum, 2);
+            if (q == 0) sm.ra[i] -= sum;
         }
-    }
-    if (blockIdx.x == 0) {
         __syncthreads();
-        chol_diag_tile(S, npad, k + 1, W + (size_t)((k + 1) & 1) * NB * NB, rhs, fail, sm.n, sm.colP);
+        if (blockIdx.x == 0) chol_diag_tile(t, k + 1, W + (size_t)((k + 1) & 1) * NB * NB, rhs, sm.ra, fail, sm.n);
+        else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dst[(size_t)(16 * w + trow(r)) * npad + 16 * c + tcol()] = t[c][r];
+            if (tid < NB) rhs[a0 + tid] = sm.ra[tid];
+        }
+        // upper tile (k, a): row k0 + j, column a0 + i holds G[i][j]
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) S[(size_t)(k0 + 16 * c + tcol()) * npad + a0 + 16 * w + trow(r)] = g[c][r];
+    } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dst[(size_t)(16 * w + trow(r)) * npad + 16 * c + tcol()] = t[c][r];
     }
+    CHOL_STAMP(34);
 }
 
 // Back substitution L~^T x = w, panel k (descending): x_k = rhs_k is final;

@@ -219,15 +219,20 @@ void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restri
     };
 
     // Top-2 by max over packed keys, two new keys per step:
-    //   b2' = max(med3(b1, ka, kb), b2),  b1' = max3(b1, ka, kb)   (1.5 VALU per element)
+    //   m_i = med3(b1, ka, kb),  b1' = max3(b1, ka, kb)
+    // and b2' = max(b2, m_1 .. m_8) as a max3 tree once per 16 keys, since
+    // max(med3(b1, ka, kb), b2) chained over the steps equals that maximum
+    // (1.25 VALU per element for the selection, + 1 for the key).
     auto select = [&](const i32x16& acc, const i32x4 (&kv)[4], int& b1, int& b2) {
+        int m[8];
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
             const int ka = (int)(((unsigned)acc[r] << 9) + (unsigned)kv[r >> 2][r & 3]);
             const int kb = (int)(((unsigned)acc[r + 1] << 9) + (unsigned)kv[r >> 2][(r + 1) & 3]);
-            b2 = max(v_med3(b1, ka, kb), b2);
+            m[r >> 1] = v_med3(b1, ka, kb);
             b1 = v_max3(b1, ka, kb);
         }
+        b2 = v_max3(v_max3(m[0], m[1], m[2]), v_max3(m[3], m[4], m[5]), v_max3(m[6], m[7], b2));
     };
 
     if (nstages > 0) stage(0, 0);
