@@ -2,7 +2,9 @@
 """sfmx bench — descriptor-pairs/s matched + ms per LM iteration (BASELINE.json metric).
 
 One JSON line.  Top level: the SIFT leg on BASELINE config 2; nested "orb": the
-ORB leg on config 4; nested "ba": the bundle-adjustment leg on config 5.
+ORB leg on config 4; nested "c3": 200 x 8192 SIFT unordered (config 3, 19900
+pairs sharded over the N ranks); nested "ba": the bundle-adjustment leg on
+config 5.
 
 Matching step = one pass of the hot path over the whole synthetic job with the
 descriptors already resident in HBM: prepare every image (f32 -> int8 + norms,
@@ -19,6 +21,7 @@ Multi-GPU, one process per GPU:
         (n(N)(n(N)-1)/2 ~= 1225 N pairs: 50 / 71 / 99 / 141 images), pairs
         sharded across ranks by sum Nq*Nt, no collective on the data path.
   ORB:  strong scaling (the fixed 881-pair grid job sharded across ranks).
+  C3:   strong scaling (the fixed 19900-pair 200-image job sharded across ranks).
   BA:   strong scaling (points sharded, S + rhs all-reduced over RCCL).
 Timing: barrier + synchronize on both sides, max over ranks.
 CPU baselines (rank 0, N=1 only): exact BF and FLANN-style restatements from
@@ -57,6 +60,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target length of each CPU-baseline sample")
     ap.add_argument("--no-ba", action="store_true", help="skip the bundle-adjustment leg")
     ap.add_argument("--no-orb", action="store_true", help="skip the ORB (config 4) leg")
+    ap.add_argument("--no-c3", action="store_true", help="skip the 200-image SIFT (config 3) leg")
     ap.add_argument("--only-ba", action="store_true", help="run only the bundle-adjustment leg (tuning)")
     ap.add_argument("--ba-cams", type=int, default=200)
     ap.add_argument("--ba-points", type=int, default=200_000)
@@ -87,14 +91,18 @@ def main():
         return
 
     primary = bench_match(args.workload, args, rank, world, local)
-    orb = None
+    orb = c3 = None
     if args.workload == "sift" and not args.no_orb:
         orb = bench_match("orb", args, rank, world, local)
+    if args.workload == "sift" and not args.no_c3:
+        c3 = bench_match("c3", args, rank, world, local)
     ba_res = None if args.no_ba else bench_ba(args, rank, world, local)
     if rank == 0:
         line = {k: v for k, v in primary.items() if not k.startswith("_")}
         if orb is not None:
             line["orb"] = {k: v for k, v in orb.items() if not k.startswith("_")}
+        if c3 is not None:
+            line["c3"] = {k: v for k, v in c3.items() if not k.startswith("_")}
         line["ba"] = ba_res
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -111,15 +119,15 @@ def bench_match(kind, args, rank, world, local):
     import torch.distributed as dist
     import sfmx
     from sfmx import synth, shard
-    if kind == "sift":
-        n_img = shard.images_for_weak_scaling(world)
+    if kind in ("sift", "c3"):
+        n_img = shard.images_for_weak_scaling(world) if kind == "sift" else 200
         imgs = synth.sift_images(n_img, N_DESC)
         pairs_all = sfmx.pairs_unordered(n_img)
         norm = sfmx.NORM_L2
         op_per_pair, bound, peak, unit = 256.0, "mfma", INT8_MFMA_PEAK_TOPS, "TFLOP/s"
         workload = f"{n_img} images x {N_DESC} SIFT-128 f32, unordered all-pairs ({len(pairs_all)} pairs)"
         dtype = "int8->int32 (exact; f32 in/out)"
-        scaling = "weak"
+        scaling = "weak" if kind == "sift" else "strong"
         data = "synthetic (seeded SIFT-like descriptors, 25% planted re-observations; no dataset)"
         kernel = "sift_knn2_kernel"
         algo = "256 ops (128 int8 MAC) per descriptor pair"
@@ -158,7 +166,7 @@ def bench_match(kind, args, rank, world, local):
             dist.barrier()
         torch.cuda.synchronize()
 
-    steps = args.steps if kind == args.workload else max(2, args.steps // 3)
+    steps = args.steps if kind == args.workload else max(2, args.steps // 5)
     for _ in range(args.warmup):
         step()
     barrier()
@@ -231,12 +239,15 @@ def bench_match(kind, args, rank, world, local):
         "slow_path_queries": slow,
         "fp32_fallback_pairs": f32p,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and kind != "c3":
         res.update(cpu_baselines(kind, imgs, pairs_all, got, off, args.cpu_seconds))
+    del dev_imgs
+    torch.cuda.empty_cache()
     return res
 
 
-PMC_FILES = {"sift": ("r01_pmc_sift_v0.json", "sift_knn2_kernel", 50), "orb": ("r01_pmc_orb.json", "orb_mfma_kernel", 200)}
+PMC_FILES = {"sift": ("r01_pmc_sift_v0.json", "sift_knn2_kernel", 50), "orb": ("r01_pmc_orb.json", "orb_mfma_kernel", 200),
+             "c3": ("r01_pmc_sift_c3.json", "sift_knn2_kernel", 200)}
 
 
 def pmc_traffic(kind, n_img):
