@@ -47,6 +47,8 @@ def _load():
     lib.orc_filter_matches.argtypes = [vp, i64p, i64p, C.c_int, C.c_int, C.c_int, i32p]
     lib.orc_flann_match_pairs.argtypes = [C.c_int, C.POINTER(vp), i32p, C.c_int, i32p, C.c_int, C.c_double, vp,
                                           i64p, i64p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]
+    lib.orc_homography_ratios.argtypes = [C.POINTER(vp), i32p, i32p, C.c_int, vp, i64p, C.c_double, C.c_int,
+                                          C.c_double, C.POINTER(C.c_double), C.c_int]
     lib.orc_first_sqrt_collision.restype = C.c_int64
     lib.orc_first_sqrt_collision.argtypes = [C.c_int64]
     return lib
@@ -135,6 +137,23 @@ def recall(exact: np.ndarray, exact_off: np.ndarray, approx: np.ndarray, approx_
     a, b = keys(exact, exact_off), keys(approx, approx_off)
     hit = np.intersect1d(a, b).size
     return hit / max(a.size, 1), hit / max(b.size, 1)
+
+
+def homography_ratios(keypoints, image_sizes, pairs, matches, offsets, threshold=-3.0, max_iters=2000,
+                      confidence=0.995, nthreads: int = 0):
+    """SfM::calculateHomography (SfM.cpp:599-637) restated with OpenCV 4.5.1's
+    findHomography RANSAC (oracle/homography_oracle.cpp) -> ratio per pair."""
+    kps = [np.ascontiguousarray(k, np.float32).reshape(-1, 2) for k in keypoints]
+    ptrs = (C.c_void_p * max(len(kps), 1))(*[k.ctypes.data for k in kps])
+    sizes = np.ascontiguousarray(np.asarray(image_sizes).reshape(-1, 2), np.int32)
+    pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+    m = np.ascontiguousarray(matches, DMATCH_DTYPE)
+    off = np.ascontiguousarray(offsets, np.int64)
+    out = np.zeros(len(pairs))
+    lib.orc_homography_ratios(ptrs, _ptr(sizes), _ptr(pairs), len(pairs), m.ctypes.data if len(m) else None,
+                              _ptr(off, C.c_int64), threshold, max_iters, confidence,
+                              out.ctypes.data_as(C.POINTER(C.c_double)), nthreads)
+    return out
 
 
 def filter_matches(matches: np.ndarray, offsets: np.ndarray, distinct: bool, min_count: int):

@@ -593,7 +593,7 @@ void orb_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restric
     constexpr int STAGE = 256;
     constexpr int BUF = STAGE * ORB_BYTES;   // 8 KiB
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * BUF];
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
     const WorkItem w = work[xcd_remap(blockIdx.x, gridDim.x)];
     const PairDev P = pairs[w.pair];
     const ImgDev L = imgs[P.left], R = imgs[P.right];

@@ -62,7 +62,7 @@ class sfmx_ba_summary(C.Structure):
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p)
 
-# Every symbol include/sfmx.h (and include/sfmx_ba.h) declares, with its ctypes prototype.
+# Every symbol include/sfmx.h (and include/sfmx_ba.h, include/sfmx_homography.h) declares, with its ctypes prototype.
 _P = C.POINTER
 _i32p, _i64p, _vp = _P(C.c_int32), _P(C.c_int64), C.c_void_p
 PROTOTYPES = {
@@ -96,6 +96,9 @@ PROTOTYPES = {
     "sfmx_ba_jacobian": (C.c_int, [_P(sfmx_ba_problem), C.c_int32, _vp, _vp, _vp, _vp]),
     "sfmx_pose_to_ceres": (C.c_int, [_P(C.c_double), _P(C.c_double)]),
     "sfmx_pose_from_ceres": (C.c_int, [_P(C.c_double), _P(C.c_double)]),
+    "sfmx_homography_ratios": (C.c_int, [_P(_vp), _i32p, C.c_int32, _i32p, _i32p, C.c_int32, _vp, _vp, C.c_double,
+                                         C.c_int32, C.c_double, C.c_int32, C.c_int32, _vp, _P(C.c_double)]),
+    "sfmx_homography_last_kernel_ms": (C.c_float, []),
 }
 
 

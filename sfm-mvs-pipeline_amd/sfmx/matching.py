@@ -184,9 +184,16 @@ def match_pairs(mats: Sequence[np.ndarray], pairs: np.ndarray, norm: int = NORM_
 
 @dataclass
 class Shot:
-    """Minimal CameraShot: its image path and the descriptor matrix of its Features."""
+    """Minimal CameraShot: its image path, the descriptor matrix of its Features
+    and (for the homography step) their keypoint positions (n x 2 float32,
+    cv::KeyPoint::pt) and the image size (width, height) (CameraShot.h:39-54, :174)."""
     path: str
     descriptors: np.ndarray
+    keypoints: Optional[np.ndarray] = None
+    image_size: tuple = (0, 0)
+
+    def getImageSize(self):
+        return self.image_size
 
 
 @dataclass
@@ -207,6 +214,12 @@ class ShotMatches:
 
     def getMatches(self):
         return self.matches
+
+    def getHomographyInlierRatio(self):
+        return self.homographyInlierRatio
+
+    def setHomographyInlierRatio(self, r: float):
+        self.homographyInlierRatio = r
 
 
 class IFeatureMatchingStrategy:

@@ -22,28 +22,61 @@ def _sift_quantise(x: np.ndarray) -> np.ndarray:
 
 
 def sift_images(n_images: int, n_desc: int, seed: int = SIFT_SEED, shared: float = 0.25,
-                noise: float = 8.0, uniform: bool = False) -> list:
+                noise: float = 8.0, uniform: bool = False, with_pool: bool = False):
     """n_images x (n_desc x 128) float32 integer-valued SIFT-like descriptors.
 
     Images sit on a ring; image i re-observes (perturbed, sigma=noise,
     re-quantised) ``shared`` of its rows from a landmark pool it shares with
     its neighbours, so the ratio test accepts a realistic fraction of queries.
     ``uniform=True`` draws raw uniform 0..255 values instead (exercises the
-    float-sqrt collision range)."""
+    float-sqrt collision range).  ``with_pool=True`` also returns, per image,
+    the landmark-pool index of every row (-1 for fresh rows) and the pool size."""
     rng = np.random.default_rng(seed)
     if uniform:
         return [rng.integers(0, 256, size=(n_desc, 128)).astype(np.float32) for _ in range(n_images)]
     n_sh = int(n_desc * shared)
     pool_n = max(n_sh * 4, 1)
     pool = _sift_quantise(np.abs(rng.standard_normal((pool_n, 128), dtype=np.float32)))
-    out = []
+    out, src = [], []
     for i in range(n_images):
         fresh = _sift_quantise(np.abs(rng.standard_normal((n_desc - n_sh, 128), dtype=np.float32)))
         start = (i * n_sh) % pool_n
         sel = (start + rng.permutation(n_sh * 2)[:n_sh]) % pool_n
         obs = np.clip(np.rint(pool[sel] + rng.normal(0, noise, size=(n_sh, 128))), 0, 255).astype(np.float32)
         img = np.concatenate([obs, fresh], axis=0)
-        out.append(np.ascontiguousarray(img[rng.permutation(n_desc)]))
+        perm = rng.permutation(n_desc)
+        out.append(np.ascontiguousarray(img[perm]))
+        src.append(np.concatenate([sel, np.full(n_desc - n_sh, -1)]).astype(np.int64)[perm])
+    return (out, src, pool_n) if with_pool else out
+
+
+def scene_keypoints(src: list, pool_n: int, width: int = 720, height: int = 405, seed: int = 0x4B50,
+                    noise_px: float = 0.7, plane_frac: float = 0.85) -> list:
+    """Keypoints (n x 2 float32, cv::KeyPoint::pt) for the rows of sift_images(...,
+    with_pool=True): a landmark on the dominant scene plane (``plane_frac`` of the
+    pool) is seen by image i through a per-image homography H_i of the plane (a
+    camera sliding along the insel-like sequence), + Gaussian pixel noise; other
+    landmarks and fresh rows land uniformly in the image.  Pairs therefore carry
+    a strong homography (the quantity SfM::calculateHomography measures,
+    SfM.cpp:599-637) plus outliers."""
+    rng = np.random.default_rng(seed)
+    plane = rng.uniform(0, 1, (pool_n, 2))
+    on_plane = rng.uniform(0, 1, pool_n) < plane_frac
+    off_xy = np.stack([rng.uniform(0, width, pool_n), rng.uniform(0, height, pool_n)], axis=1)
+    out = []
+    for i, sidx in enumerate(src):
+        a = 0.02 * i
+        H = np.array([[0.8 * width * np.cos(a), -0.15 * height * np.sin(a), 0.1 * width + 3.0 * i],
+                      [0.15 * width * np.sin(a), 0.8 * height * np.cos(a), 0.1 * height + 1.0 * i],
+                      [0.05 * np.sin(0.3 * i), 0.04 * np.cos(0.2 * i), 1.0]])
+        n = len(sidx)
+        xy = np.stack([rng.uniform(0, width, n), rng.uniform(0, height, n)], axis=1)
+        m = sidx >= 0
+        p = sidx[m]
+        ph = np.concatenate([plane[p], np.ones((len(p), 1))], axis=1) @ H.T
+        proj = ph[:, :2] / ph[:, 2:3] + rng.normal(0, noise_px, (len(p), 2))
+        xy[m] = np.where(on_plane[p][:, None], proj, off_xy[p] + rng.normal(0, noise_px, (len(p), 2)))
+        out.append(np.ascontiguousarray(xy.astype(np.float32)))
     return out
 
 

@@ -1,0 +1,54 @@
+"""GPU parity for the homography step: the HIP RANSAC
+kernel (through the C ABI) against oracle/homography_oracle.cpp, bit-exact:
+both restate OpenCV 4.5.1's deterministic findHomography RANSAC with the same
+operation order and no FMA contraction."""
+import numpy as np
+import pytest
+import torch
+
+import sfmx
+from sfmx import homography
+import homog_cases
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed", [3, 8])
+def test_scene_graph_bit_exact(seed):
+    from oracle import oracle
+    kps, sizes, pairs, m, off = homog_cases.scene_case(7, 2500, seed=seed)
+    exp = oracle.homography_ratios(kps, sizes, pairs, m, off)
+    got = homography.homography_ratios(kps, sizes, pairs, m, off)
+    assert np.array_equal(got, exp), (got, exp)
+
+
+def test_edge_cases_bit_exact():
+    from oracle import oracle
+    kps, sizes, pairs, m, off = homog_cases.edge_case()
+    for thr, iters, conf in ((-3.0, 2000, 0.995), (-1.0, 50, 0.9), (0.004, 2000, 0.999)):
+        exp = oracle.homography_ratios(kps, sizes, pairs, m, off, thr, iters, conf)
+        got = homography.homography_ratios(kps, sizes, pairs, m, off, thr, iters, conf)
+        assert np.array_equal(got, exp), (thr, got, exp)
+
+
+def test_device_inputs_and_strategy_mirror():
+    kps, sizes, pairs, m, off = homog_cases.scene_case(5, 1500, seed=6)
+    host = homography.homography_ratios(kps, sizes, pairs, m, off)
+    dk = [torch.from_numpy(k).cuda() for k in kps]
+    dm = torch.from_numpy(m.view(np.uint8)).cuda()
+    do = torch.from_numpy(off).cuda()
+    dev = homography.homography_ratios_device([t.data_ptr() for t in dk], [len(k) for k in kps], sizes, pairs,
+                                              dm.data_ptr(), do.data_ptr())
+    assert np.array_equal(host, dev)
+    scene = sfmx.Scene([sfmx.Shot(f"img{i}", None, k, s) for i, (k, s) in enumerate(zip(kps, sizes))])
+    sms = [sfmx.ShotMatches(int(l), int(r), m[off[p]:off[p + 1]]) for p, (l, r) in enumerate(pairs)]
+    homography.calculateHomography(scene, sms)
+    assert np.array_equal([s.getHomographyInlierRatio() for s in sms], host)
+
+
+def test_invalid_index_rejected():
+    kps, sizes, pairs, m, off = homog_cases.edge_case()
+    m = m.copy()
+    m["trainIdx"][5] = 10 ** 6
+    with pytest.raises(ValueError):
+        homography.homography_ratios(kps, sizes, pairs, m, off)
