@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--no-ba", action="store_true", help="skip the bundle-adjustment leg")
     ap.add_argument("--no-orb", action="store_true", help="skip the ORB (config 4) leg")
     ap.add_argument("--no-c3", action="store_true", help="skip the 200-image SIFT (config 3) leg")
+    ap.add_argument("--no-homography", action="store_true", help="skip the homography RANSAC leg (SURVEY §8 f1)")
     ap.add_argument("--only-ba", action="store_true", help="run only the bundle-adjustment leg (tuning)")
     ap.add_argument("--ba-cams", type=int, default=200)
     ap.add_argument("--ba-points", type=int, default=200_000)
@@ -186,6 +187,9 @@ def bench_match(kind, args, rank, world, local):
 
     # sanity outside the timed region
     got, off, _ = matcher.fetch(stream=stream)
+    homog = None
+    if kind == "sift" and not args.no_homography:
+        homog = bench_homography(args, matcher, imgs, my_pairs, got, off, rank, world, local, stream)
     slow, f32p = matcher.stats(stream=stream)
     n_matches = int(off[-1])
     if world > 1:
@@ -239,10 +243,69 @@ def bench_match(kind, args, rank, world, local):
         "slow_path_queries": slow,
         "fp32_fallback_pairs": f32p,
     }
+    if homog is not None:
+        res["homography"] = homog
     if rank == 0 and world == 1 and not args.no_cpu_baseline and kind != "c3":
         res.update(cpu_baselines(kind, imgs, pairs_all, got, off, args.cpu_seconds))
     del dev_imgs
     torch.cuda.empty_cache()
+    return res
+
+
+def bench_homography(args, matcher, imgs, my_pairs, got, off, rank, world, local, stream):
+    """SURVEY §8 row f1 on the config-2 match graph: SfM::calculateHomography
+    (SfM.cpp:599-637) = cv::findHomography(RANSAC, 3 px) per image pair, inlier
+    ratio.  Inputs resident in HBM: the matcher's packed DMatch lists (left by
+    the SIFT leg's last run) and per-image keypoints (synthetic planted-plane
+    scene, synth.scene_keypoints).  Unit: image pairs per second (whole graph
+    per step).  CPU baseline: the oracle's restatement, OpenMP over pairs."""
+    import torch
+    import torch.distributed as dist
+    from sfmx import synth, homography
+    _, src, pool_n = synth.sift_images(len(imgs), N_DESC, with_pool=True)
+    kps = synth.scene_keypoints(src, pool_n)
+    sizes = [(720, 405)] * len(imgs)
+    dk = [torch.from_numpy(k).to(f"cuda:{local}") for k in kps]
+    mp, op, _ = matcher.device_results()
+    nkp = [len(k) for k in kps]
+
+    def step():
+        return homography.homography_ratios_device([t.data_ptr() for t in dk], nkp, sizes, my_pairs, mp, op,
+                                                   device=local, stream=stream)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    steps = max(2, args.steps // 2)
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = step()
+        kms.append(homography.last_kernel_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    n_all = len(my_pairs) * world    # pairs are sharded evenly enough; value = all ranks' pairs / max time
+    res = {"metric": "image pairs/s (homography RANSAC, SfM::calculateHomography)", "value": n_all * steps / el,
+           "unit": "image pairs/s", "ms_per_step": el / steps * 1e3, "kernel_ms": float(np.mean(kms)),
+           "pairs": int(len(my_pairs)), "matches": int(off[-1]),
+           "mean_inlier_ratio": float(np.mean(r[r >= 0])) if np.any(r >= 0) else None,
+           "config": "config-2 match graph, findHomography(RANSAC, 3 px, 2000 iters, 0.995), planted-plane keypoints"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+        t = time.perf_counter()
+        e = oracle.homography_ratios(kps, sizes, my_pairs, got, off, nthreads=threads)
+        dt = time.perf_counter() - t
+        res["cpu_baseline"] = {"value": len(my_pairs) / dt, "unit": "image pairs/s", "cores": threads, "kind": "port",
+                               "sample": f"all {len(my_pairs)} pairs, oracle/homography_oracle.cpp (OpenMP over pairs), {dt:.2f} s"}
+        res["bit_exact_vs_oracle"] = bool(np.array_equal(e, r))
     return res
 
 

@@ -24,18 +24,23 @@
 //     last point vs. the pairs before it, in both sets, FLT_EPSILON test; the
 //     orientation test on the 4 triangles {0,1,2},{1,2,3},{0,2,3},{1,3,0}:
 //     det(A)*det(B) < 0 must hold for none or all), up to 10000 attempts.
-//   * runKernel: normalised DLT — centroids, mean absolute deviations, the 9x9
-//     LtL of the normalised correspondences, cv::eigen (Jacobi with pivot
-//     search, eigenvalues sorted descending) -> eigenvector of the smallest
-//     eigenvalue, denormalised invHnorm * H0 * Hnorm2, scaled by 1/H(2,2).
+//   * runKernel: normalised DLT — centroids, mean absolute deviations, the
+//     normalised correspondences' equations, H0 = their null vector,
+//     denormalised invHnorm * H0 * Hnorm2, scaled by 1/H(2,2).  OpenCV takes
+//     H0 as the eigenvector of the smallest eigenvalue of the 9x9 LtL
+//     (cv::eigen, Jacobi).  RANSAC only ever fits minimal samples (4 points,
+//     8 equations of rank 8), whose null vector is unique up to scale, so
+//     this restatement solves the 8x8 system with h8 = 1 instead (solve8):
+//     the same H up to rounding, after the final 1/H(2,2) scaling.
 //   * computeError in float: ww = 1/(h6 x + h7 y + 1), err = dx^2 + dy^2;
 //     inlier iff err <= (float)(thr^2); a model replaces the best iff its
 //     count > max(best, 3); niters = RANSACUpdateNumIters(0.995, outlier
 //     fraction, 4, niters) after each improvement.
 // The LM refinement that follows in findHomography changes H, not the mask,
 // so it does not affect the ratio and is not restated.
-// Deviations (documented in DESIGN.md): hypot(a, b) is sqrt(a*a + b*b) (the
-// normalised LtL entries are O(1)); 3x3 products sum in k order.  The GPU
+// Deviations (documented in DESIGN.md): the minimal-sample null vector by an
+// 8x8 solve instead of a 9x9 Jacobi eigen-decomposition (same H up to
+// rounding); (1-ep)^4 as two squarings; 3x3 products sum in k order.  The GPU
 // kernel (csrc/homography.hip) follows the same operation order with FMA
 // contraction off, so the two agree bit for bit; parity against OpenCV itself
 // is unpinned (no OpenCV here).
@@ -59,94 +64,28 @@ struct Rng {
     int uniform(int a, int b) { return a == b ? a : (int)(next() % (uint32_t)(b - a) + (uint32_t)a); }
 };
 
-inline double rhypot(double a, double b) { return std::sqrt(a * a + b * b); }
-
-// cv::eigen for a symmetric 9x9 (hal::Jacobi), eigenvectors as rows of V,
-// eigenvalues descending.
-void jacobi9(double A[9][9], double W[9], double V[9][9]) {
-    const int n = 9;
-    const double eps = DBL_EPSILON;
-    for (int i = 0; i < n; ++i) {
-        for (int j = 0; j < n; ++j) V[i][j] = 0.0;
-        V[i][i] = 1.0;
-    }
-    int indR[9], indC[9];
-    int k, m, i;
-    double mv;
-    for (k = 0; k < n; ++k) {
-        W[k] = A[k][k];
-        if (k < n - 1) {
-            for (m = k + 1, mv = std::fabs(A[k][m]), i = k + 2; i < n; ++i) {
-                const double v = std::fabs(A[k][i]);
-                if (mv < v) mv = v, m = i;
-            }
-            indR[k] = m;
-        }
-        if (k > 0) {
-            for (m = 0, mv = std::fabs(A[0][k]), i = 1; i < k; ++i) {
-                const double v = std::fabs(A[i][k]);
-                if (mv < v) mv = v, m = i;
-            }
-            indC[k] = m;
+// Minimal-sample solve: the 8 equations [Lx; Ly] h = 0 of 4 normalised
+// correspondences with h8 = 1 (augmented 8x9, right-hand side -L[:, 8]),
+// Gaussian elimination with a compare-and-swap pivot sweep (for r > c: swap
+// rows r and c when |a[r][c]| > |a[c][c]|), then back substitution.
+bool solve8(double a[8][9], double h[9]) {
+    for (int c = 0; c < 8; ++c) {
+        for (int r = c + 1; r < 8; ++r)
+            if (std::fabs(a[r][c]) > std::fabs(a[c][c]))
+                for (int j = 0; j < 9; ++j) std::swap(a[r][j], a[c][j]);
+        if (a[c][c] == 0.0) return false;
+        for (int r = c + 1; r < 8; ++r) {
+            const double f = a[r][c] / a[c][c];
+            for (int j = c + 1; j < 9; ++j) a[r][j] -= f * a[c][j];
         }
     }
-    const int maxIters = n * n * 30;
-    for (int iters = 0; iters < maxIters; ++iters) {
-        for (k = 0, mv = std::fabs(A[0][indR[0]]), i = 1; i < n - 1; ++i) {
-            const double v = std::fabs(A[i][indR[i]]);
-            if (mv < v) mv = v, k = i;
-        }
-        int l = indR[k];
-        for (i = 1; i < n; ++i) {
-            const double v = std::fabs(A[indC[i]][i]);
-            if (mv < v) mv = v, k = indC[i], l = i;
-        }
-        const double p = A[k][l];
-        if (std::fabs(p) <= eps) break;
-        const double y = (W[l] - W[k]) * 0.5;
-        double t = std::fabs(y) + rhypot(p, y);
-        double s = rhypot(p, t);
-        const double c = t / s;
-        s = p / s;
-        t = (p / t) * p;
-        if (y < 0) s = -s, t = -t;
-        A[k][l] = 0;
-        W[k] -= t;
-        W[l] += t;
-        double a0, b0;
-#define ROT(v0, v1) a0 = v0, b0 = v1, v0 = a0 * c - b0 * s, v1 = a0 * s + b0 * c
-        for (i = 0; i < k; ++i) ROT(A[i][k], A[i][l]);
-        for (i = k + 1; i < l; ++i) ROT(A[k][i], A[i][l]);
-        for (i = l + 1; i < n; ++i) ROT(A[k][i], A[l][i]);
-        for (i = 0; i < n; ++i) ROT(V[k][i], V[l][i]);
-#undef ROT
-        for (int j = 0; j < 2; ++j) {
-            const int idx = j == 0 ? k : l;
-            if (idx < n - 1) {
-                for (m = idx + 1, mv = std::fabs(A[idx][m]), i = idx + 2; i < n; ++i) {
-                    const double v = std::fabs(A[idx][i]);
-                    if (mv < v) mv = v, m = i;
-                }
-                indR[idx] = m;
-            }
-            if (idx > 0) {
-                for (m = 0, mv = std::fabs(A[0][idx]), i = 1; i < idx; ++i) {
-                    const double v = std::fabs(A[i][idx]);
-                    if (mv < v) mv = v, m = i;
-                }
-                indC[idx] = m;
-            }
-        }
+    for (int r = 7; r >= 0; --r) {
+        double t = a[r][8];
+        for (int j = r + 1; j < 8; ++j) t -= a[r][j] * h[j];
+        h[r] = t / a[r][r];
     }
-    for (k = 0; k < n - 1; ++k) {
-        m = k;
-        for (i = k + 1; i < n; ++i)
-            if (W[m] < W[i]) m = i;
-        if (k != m) {
-            std::swap(W[m], W[k]);
-            for (i = 0; i < n; ++i) std::swap(V[m][i], V[k][i]);
-        }
-    }
+    h[8] = 1.0;
+    return true;
 }
 
 // HomographyEstimatorCallback::runKernel on `count` correspondences
@@ -168,21 +107,18 @@ bool dlt(const float* M, const float* m, int count, double H[9]) {
     smx = count / smx; smy = count / smy; sMx = count / sMx; sMy = count / sMy;
     const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
-    double LtL[9][9];
-    std::memset(LtL, 0, sizeof LtL);
-    for (int i = 0; i < count; ++i) {
+    double a[8][9];
+    for (int i = 0; i < count; ++i) {   // count == 4: the minimal sample
         const double x = (m[2 * i] - cmx) * smx, y = (m[2 * i + 1] - cmy) * smy;
         const double X = (M[2 * i] - cMx) * sMx, Y = (M[2 * i + 1] - cMy) * sMy;
         const double Lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
         const double Ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
-        for (int j = 0; j < 9; ++j)
-            for (int k = j; k < 9; ++k) LtL[j][k] += Lx[j] * Lx[k] + Ly[j] * Ly[k];
+        for (int j = 0; j < 8; ++j) { a[2 * i][j] = Lx[j]; a[2 * i + 1][j] = Ly[j]; }
+        a[2 * i][8] = -Lx[8];
+        a[2 * i + 1][8] = -Ly[8];
     }
-    for (int j = 0; j < 9; ++j)
-        for (int k = 0; k < j; ++k) LtL[j][k] = LtL[k][j];
-    double W[9], V[9][9];
-    jacobi9(LtL, W, V);
-    const double* H0 = V[8];
+    double H0[9];
+    if (!solve8(a, H0)) return false;
     double Ht[9], H1[9];
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) {

@@ -10,11 +10,11 @@
 // is compiled with -ffp-contract=off): the ratios agree bit for bit.
 //
 // One 256-thread workgroup per pair.  RANSAC iterations are processed in
-// batches of B = 64 in iteration order:
+// batches of B = 64 (16 in the first round) in iteration order:
 //   1. lane 0 draws the next B minimal subsets (the RNG stream and the
 //      checkSubset rejections are sequential by definition);
-//   2. lanes 0..B-1 fit one homography each (normalised DLT: 9x9 LtL, Jacobi
-//      eigen-decomposition with OpenCV's pivot search, fp64);
+//   2. lanes 0..B-1 fit one homography each (normalised DLT of the minimal
+//      sample: its 8x8 system solved in registers, fp64);
 //   3. all 256 threads count the inliers of every hypothesis over the pair's
 //      correspondences (fp32 reprojection error, ballot + popcount);
 //   4. lane 0 replays the batch in order: best-so-far (strict >, at least 4
@@ -39,159 +39,118 @@ struct PairH {
     double thr;
 };
 
-__device__ __forceinline__ double rhypot(double a, double b) { return sqrt(a * a + b * b); }
-
 // cv::RNG::next / uniform(0, count)
 __device__ __forceinline__ uint32_t rng_next(unsigned long long& st) {
     st = (unsigned long long)(uint32_t)st * 4164903690ull + (uint32_t)(st >> 32);
     return (uint32_t)st;
 }
 
-// hal::Jacobi on a symmetric 9x9 (eigenvectors as rows of V, eigenvalues descending).
-__device__ void jacobi9(double (&A)[9][9], double (&W)[9], double (&V)[9][9]) {
-    const int n = 9;
-    for (int i = 0; i < n; ++i) {
-        for (int j = 0; j < n; ++j) V[i][j] = 0.0;
-        V[i][i] = 1.0;
-    }
-    int indR[9], indC[9];
-    int k, m, i;
-    double mv;
-    for (k = 0; k < n; ++k) {
-        W[k] = A[k][k];
-        if (k < n - 1) {
-            for (m = k + 1, mv = fabs(A[k][m]), i = k + 2; i < n; ++i) {
-                const double v = fabs(A[k][i]);
-                if (mv < v) mv = v, m = i;
-            }
-            indR[k] = m;
-        }
-        if (k > 0) {
-            for (m = 0, mv = fabs(A[0][k]), i = 1; i < k; ++i) {
-                const double v = fabs(A[i][k]);
-                if (mv < v) mv = v, m = i;
-            }
-            indC[k] = m;
-        }
-    }
-    const int maxIters = n * n * 30;
-    for (int iters = 0; iters < maxIters; ++iters) {
-        for (k = 0, mv = fabs(A[0][indR[0]]), i = 1; i < n - 1; ++i) {
-            const double v = fabs(A[i][indR[i]]);
-            if (mv < v) mv = v, k = i;
-        }
-        int l = indR[k];
-        for (i = 1; i < n; ++i) {
-            const double v = fabs(A[indC[i]][i]);
-            if (mv < v) mv = v, k = indC[i], l = i;
-        }
-        const double p = A[k][l];
-        if (fabs(p) <= DBL_EPSILON) break;
-        const double y = (W[l] - W[k]) * 0.5;
-        double t = fabs(y) + rhypot(p, y);
-        double s = rhypot(p, t);
-        const double c = t / s;
-        s = p / s;
-        t = (p / t) * p;
-        if (y < 0) s = -s, t = -t;
-        A[k][l] = 0;
-        W[k] -= t;
-        W[l] += t;
-        double a0, b0;
-#define ROT(v0, v1) a0 = v0, b0 = v1, v0 = a0 * c - b0 * s, v1 = a0 * s + b0 * c
-        for (i = 0; i < k; ++i) ROT(A[i][k], A[i][l]);
-        for (i = k + 1; i < l; ++i) ROT(A[k][i], A[i][l]);
-        for (i = l + 1; i < n; ++i) ROT(A[k][i], A[l][i]);
-        for (i = 0; i < n; ++i) ROT(V[k][i], V[l][i]);
-#undef ROT
-        for (int j = 0; j < 2; ++j) {
-            const int idx = j == 0 ? k : l;
-            if (idx < n - 1) {
-                for (m = idx + 1, mv = fabs(A[idx][m]), i = idx + 2; i < n; ++i) {
-                    const double v = fabs(A[idx][i]);
-                    if (mv < v) mv = v, m = i;
-                }
-                indR[idx] = m;
-            }
-            if (idx > 0) {
-                for (m = 0, mv = fabs(A[0][idx]), i = 1; i < idx; ++i) {
-                    const double v = fabs(A[i][idx]);
-                    if (mv < v) mv = v, m = i;
-                }
-                indC[idx] = m;
+// Minimal-sample solve (the oracle's solve8): [Lx; Ly] h = 0 of 4 normalised
+// correspondences with h8 = 1, Gaussian elimination with the compare-and-swap
+// pivot sweep, back substitution.  Fully unrolled: every index is static, so
+// the 8x9 system lives in registers.
+__device__ __forceinline__ bool solve8(double (&a)[8][9], double (&h)[9]) {
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+#pragma unroll
+        for (int r = c + 1; r < 8; ++r) {
+            const bool sw = fabs(a[r][c]) > fabs(a[c][c]);
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                const double u = a[r][j], v = a[c][j];
+                a[r][j] = sw ? v : u;
+                a[c][j] = sw ? u : v;
             }
         }
-    }
-    for (k = 0; k < n - 1; ++k) {
-        m = k;
-        for (i = k + 1; i < n; ++i)
-            if (W[m] < W[i]) m = i;
-        if (k != m) {
-            const double tw = W[m]; W[m] = W[k]; W[k] = tw;
-            for (i = 0; i < n; ++i) { const double tv = V[m][i]; V[m][i] = V[k][i]; V[k][i] = tv; }
+        ok = ok && a[c][c] != 0.0;
+        const double piv = a[c][c] != 0.0 ? a[c][c] : 1.0;
+#pragma unroll
+        for (int r = c + 1; r < 8; ++r) {
+            const double f = a[r][c] / piv;
+#pragma unroll
+            for (int j = c + 1; j < 9; ++j) a[r][j] -= f * a[c][j];
         }
     }
+#pragma unroll
+    for (int r = 7; r >= 0; --r) {
+        double t = a[r][8];
+#pragma unroll
+        for (int j = r + 1; j < 8; ++j) t -= a[r][j] * h[j];
+        h[r] = t / (a[r][r] != 0.0 ? a[r][r] : 1.0);
+    }
+    h[8] = 1.0;
+    return ok;
 }
 
-// HomographyEstimatorCallback::runKernel on `count` correspondences
-// c[i] = (src.x, src.y, dst.x, dst.y) -> H (row-major, H[8] = 1); false if degenerate.
-__device__ bool dlt(const float4* c, int count, double (&H)[9]) {
+// HomographyEstimatorCallback::runKernel on the 4 correspondences of a minimal
+// sample, c[i] = (src.x, src.y, dst.x, dst.y) -> H (row-major, H[8] = 1);
+// false if degenerate.
+__device__ bool dlt4(const float4 (&c)[4], double (&H)[9]) {
+    const int count = 4;
     double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
+#pragma unroll
     for (int i = 0; i < count; ++i) {
-        const float4 q = c[i];
-        cmx += q.z; cmy += q.w;
-        cMx += q.x; cMy += q.y;
+        cmx += c[i].z; cmy += c[i].w;
+        cMx += c[i].x; cMy += c[i].y;
     }
     cmx /= count; cmy /= count; cMx /= count; cMy /= count;
+#pragma unroll
     for (int i = 0; i < count; ++i) {
-        const float4 q = c[i];
-        smx += fabs(q.z - cmx); smy += fabs(q.w - cmy);
-        sMx += fabs(q.x - cMx); sMy += fabs(q.y - cMy);
+        smx += fabs(c[i].z - cmx); smy += fabs(c[i].w - cmy);
+        sMx += fabs(c[i].x - cMx); sMy += fabs(c[i].y - cMy);
     }
     if (fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON || fabs(sMy) < DBL_EPSILON)
         return false;
     smx = count / smx; smy = count / smy; sMx = count / sMx; sMy = count / sMy;
     const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
-    double LtL[9][9];
-    for (int j = 0; j < 9; ++j)
-        for (int k = 0; k < 9; ++k) LtL[j][k] = 0.0;
+    double a[8][9];
+#pragma unroll
     for (int i = 0; i < count; ++i) {
-        const float4 q = c[i];
-        const double x = (q.z - cmx) * smx, y = (q.w - cmy) * smy;
-        const double X = (q.x - cMx) * sMx, Y = (q.y - cMy) * sMy;
+        const double x = (c[i].z - cmx) * smx, y = (c[i].w - cmy) * smy;
+        const double X = (c[i].x - cMx) * sMx, Y = (c[i].y - cMy) * sMy;
         const double Lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
         const double Ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
-        for (int j = 0; j < 9; ++j)
-            for (int k = j; k < 9; ++k) LtL[j][k] += Lx[j] * Lx[k] + Ly[j] * Ly[k];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a[2 * i][j] = Lx[j]; a[2 * i + 1][j] = Ly[j]; }
+        a[2 * i][8] = -Lx[8];
+        a[2 * i + 1][8] = -Ly[8];
     }
-    for (int j = 0; j < 9; ++j)
-        for (int k = 0; k < j; ++k) LtL[j][k] = LtL[k][j];
-    double W[9], V[9][9];
-    jacobi9(LtL, W, V);
+    double H0[9];
+    if (!solve8(a, H0)) return false;
     double Ht[9], H1[9];
+#pragma unroll
     for (int r = 0; r < 3; ++r)
+#pragma unroll
         for (int cc = 0; cc < 3; ++cc) {
             double s = 0;
-            for (int k = 0; k < 3; ++k) s += invHnorm[3 * r + k] * V[8][3 * k + cc];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s += invHnorm[3 * r + k] * H0[3 * k + cc];
             Ht[3 * r + cc] = s;
         }
+#pragma unroll
     for (int r = 0; r < 3; ++r)
+#pragma unroll
         for (int cc = 0; cc < 3; ++cc) {
             double s = 0;
+#pragma unroll
             for (int k = 0; k < 3; ++k) s += Ht[3 * r + k] * Hnorm2[3 * k + cc];
             H1[3 * r + cc] = s;
         }
     const double sc = 1. / H1[8];
+#pragma unroll
     for (int i = 0; i < 9; ++i) H[i] = H1[i] * sc;
     return true;
 }
 
 // haveCollinearPoints(m, 4) on one side of the subset (x at stride 4, from offset o)
-__device__ bool collinear4(const float (&q)[4][4], int o) {
+__device__ __forceinline__ bool collinear4(const float (&q)[4][4], int o) {
     const int i = 3;
+#pragma unroll
     for (int j = 0; j < i; ++j) {
         const double dx1 = (double)q[j][o] - q[i][o], dy1 = (double)q[j][o + 1] - q[i][o + 1];
+#pragma unroll
         for (int k = 0; k < j; ++k) {
             const double dx2 = (double)q[k][o] - q[i][o], dy2 = (double)q[k][o + 1] - q[i][o + 1];
             if (fabs(dx2 * dy1 - dy2 * dx1) <= FLT_EPSILON * (fabs(dx1) + fabs(dy1) + fabs(dx2) + fabs(dy2)))
@@ -205,10 +164,11 @@ __device__ __forceinline__ double det3(double a0, double a1, double b0, double b
     return a0 * (b1 - c1) - a1 * (b0 - c0) + (b0 * c1 - b1 * c0);
 }
 
-__device__ bool check_subset(const float (&q)[4][4]) {
+__device__ __forceinline__ bool check_subset(const float (&q)[4][4]) {
     if (collinear4(q, 0) || collinear4(q, 2)) return false;
     const int tt[4][3] = {{0, 1, 2}, {1, 2, 3}, {0, 2, 3}, {1, 3, 0}};
     int negative = 0;
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int* t = tt[i];
         const double dA = det3(q[t[0]][0], q[t[0]][1], q[t[1]][0], q[t[1]][1], q[t[2]][0], q[t[2]][1]);
@@ -230,8 +190,16 @@ __device__ int update_num_iters(double p, double ep, int max_iters) {
     return denom >= 0 || -num >= max_iters * (-denom) ? max_iters : (int)rint(num / denom);
 }
 
+#ifdef SFMX_HOMOG_STAMPS   // tools/micro/homog_stamps.hip: phase timestamps of workgroup 0 (never in the product build)
+__device__ long long g_h_stamps[256];
+__device__ int g_h_nst;
+#define H_STAMP(tag) do { if (threadIdx.x == 0 && blockIdx.x == 0 && g_h_nst < 254) { g_h_stamps[g_h_nst++] = (wall_clock64() << 8) | (tag); } } while (0)
+#else
+#define H_STAMP(tag) do { } while (0)
+#endif
+
 constexpr int CAP = 2048;   // correspondences kept in LDS (larger pairs read the global scratch copy)
-constexpr int BATCH = 64;   // hypotheses per round
+constexpr int BATCH = 64;   // hypotheses per round (the first round draws 16)
 
 __global__ __launch_bounds__(256)
 void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_t* __restrict__ nkp,
@@ -271,10 +239,12 @@ void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_
         return;
     }
     const float4* C = n <= CAP ? pts : scratch + o0;
+    H_STAMP(1);
     if (n == 4) {   // findHomography: 4 points -> the kernel directly, mask all ones
         if (tid == 0) {
+            const float4 c4[4] = {C[0], C[1], C[2], C[3]};
             double H[9];
-            out[p] = dlt(C, 4, H) ? 1.0 : 0.0;
+            out[p] = dlt4(c4, H) ? 1.0 : 0.0;
         }
         return;
     }
@@ -286,24 +256,29 @@ void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_
         if (tid == 0) {   // 1. the next minimal subsets, in iteration order
             int b = 0;
             s_fail_at = -1;
-            for (; b < BATCH && s_it + b < s_niters; ++b) {
+            const int want = s_it == 0 ? BATCH / 2 : BATCH;
+            for (; b < want && s_it + b < s_niters; ++b) {
                 float q[4][4];
                 int att = 0;
                 for (; att < 10000; ++att) {
                     int idx[4];
-                    for (int i = 0; i < 4; ++i) {
-                        int idx_i, j;
-                        for (;;) {
-                            idx_i = idx[i] = (int)(rng_next(rng) % (uint32_t)n);
-                            for (j = 0; j < i; ++j)
-                                if (idx_i == idx[j]) break;
-                            if (j == i) break;
-                        }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {   // static i: idx / q stay in registers
+                        int idx_i;
+                        bool dup;
+                        do {
+                            idx_i = (int)(rng_next(rng) % (uint32_t)n);
+                            dup = false;
+#pragma unroll
+                            for (int j = 0; j < i; ++j) dup = dup || idx_i == idx[j];
+                        } while (dup);
+                        idx[i] = idx_i;
                         const float4 v = C[idx_i];
                         q[i][0] = v.x; q[i][1] = v.y; q[i][2] = v.z; q[i][3] = v.w;
-                        sub[b][i] = idx_i;
                     }
                     if (!check_subset(q)) continue;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) sub[b][i] = idx[i];
                     break;
                 }
                 if (att >= 10000) { s_fail_at = s_it + b; break; }
@@ -311,17 +286,18 @@ void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_
             s_nb = b;
         }
         __syncthreads();
+        H_STAMP(2);
         const int nb = s_nb;
         if (tid < nb) {   // 2. one hypothesis per lane
-            float4 c4[4];
-            for (int i = 0; i < 4; ++i) c4[i] = C[sub[tid][i]];
+            const float4 c4[4] = {C[sub[tid][0]], C[sub[tid][1]], C[sub[tid][2]], C[sub[tid][3]]};
             double H[9];
-            const bool ok = dlt(c4, 4, H);
+            const bool ok = dlt4(c4, H);
             okb[tid] = ok;
             good[tid] = 0;
             for (int i = 0; i < 8; ++i) hf[tid][i] = (float)H[i];
         }
         __syncthreads();
+        H_STAMP(3);
         for (int b = 0; b < nb; ++b) {   // 3. inlier counts (computeError + findInliers)
             if (!okb[b]) continue;
             const float h0 = hf[b][0], h1 = hf[b][1], h2 = hf[b][2], h3 = hf[b][3], h4 = hf[b][4], h5 = hf[b][5],
@@ -338,6 +314,7 @@ void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_
             if ((tid & 63) == 0 && cnt) atomicAdd(&good[b], cnt);
         }
         __syncthreads();
+        H_STAMP(4);
         if (tid == 0) {   // 4. replay in iteration order
             for (int b = 0; b < nb; ++b) {
                 if (s_it + b >= s_niters) { s_done = 1; break; }

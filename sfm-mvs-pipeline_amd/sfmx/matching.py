@@ -130,6 +130,14 @@ class BFMatcher:
                                    int(min_count), C.c_void_p(stream)), "sfmx_matcher_run")
         self._n_pairs = len(pairs)
 
+    def device_results(self):
+        """-> (matches_ptr, pair_offsets_ptr, keep_ptr): the packed results left in
+        HBM by the last run (sfmx_matcher_device_results), valid until the next run."""
+        mp, op, kp = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        check(lib.sfmx_matcher_device_results(self._h, C.byref(mp), C.byref(op), C.byref(kp)),
+              "sfmx_matcher_device_results")
+        return mp.value, op.value, kp.value
+
     def fetch(self, stream: int = 0):
         """-> (matches[DMATCH_DTYPE], pair_offsets[int64, n_pairs+1], keep[int32, n_pairs])"""
         req = np.zeros(1, np.int64)
