@@ -309,7 +309,7 @@ def bench_homography(args, matcher, imgs, my_pairs, got, off, rank, world, local
     return res
 
 
-PMC_FILES = {"sift": ("r01_pmc_sift_v0.json", "sift_knn2_kernel", 50), "orb": ("r01_pmc_orb.json", "orb_mfma_kernel", 200),
+PMC_FILES = {"sift": ("r01_pmc_sift_qt4.json", "sift_knn2_kernel", 50), "orb": ("r01_pmc_orb.json", "orb_mfma_kernel", 200),
              "c3": ("r01_pmc_sift_c3.json", "sift_knn2_kernel", 200)}
 
 

@@ -162,7 +162,7 @@ __global__ void prep_hamming_fp4_kernel(const uint8_t* __restrict__ src, int row
 
 // ---------------------------------------------------------------------------
 // SIFT 2-NN, int8 MFMA.
-template <int QT, int WAVES, int MINW, int STAGE, bool MFMA_FIRST>
+template <int QT, int WAVES, int MINW, int STAGE, bool MFMA_FIRST, int PROBE = 0>
 __global__ __launch_bounds__(WAVES * 64, MINW)
 void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
                       const ImgDev* __restrict__ imgs, const int8_t* __restrict__ desc8,
@@ -264,8 +264,13 @@ void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restri
 #pragma unroll
                     for (int m = 0; m < 4; ++m) acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bq[qt][m], acc[qt], 0, 0, 0);
                 }
+                if constexpr (PROBE == 1) {   // timing probe only: MFMA + staging skeleton, no selection
 #pragma unroll
-                for (int qt = 0; qt < QT; ++qt) select(acc[qt], kv, c1[qt], c2[qt]);
+                    for (int qt = 0; qt < QT; ++qt) c1[qt] = v_max3(c1[qt], acc[qt][0], acc[qt][15]);
+                } else {
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt) select(acc[qt], kv, c1[qt], c2[qt]);
+                }
             } else {
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt) {
@@ -796,8 +801,8 @@ int sift_variant() {
 }
 int sift_block_queries(int v) { return v == 2 || v == 4 ? 256 : 512; }
 
-#define SIFT_LAUNCH(QT, W, MINW, ST, MF)                                                                  \
-    sift_knn2_kernel<QT, W, MINW, ST, MF><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc,   \
+#define SIFT_LAUNCH(QT, W, MINW, ST, MF, ...)                                                             \
+    sift_knn2_kernel<QT, W, MINW, ST, MF, ##__VA_ARGS__><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc, \
                                                                      out_idx, out_dist, slow_list, slow_count, ratio)
 
 hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
@@ -809,7 +814,13 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
     case 2: SIFT_LAUNCH(2, 4, 3, 64, true); break;
     case 3: SIFT_LAUNCH(2, 8, 2, 64, false); break;
     case 4: SIFT_LAUNCH(2, 4, 4, 128, false); break;
-    default: SIFT_LAUNCH(2, 8, 2, 64, true);   // measured best (r01 tuning, profiles/r01_*)
+    case 5: SIFT_LAUNCH(4, 4, 2, 64, true); break;
+    case 6: SIFT_LAUNCH(4, 4, 2, 128, true); break;
+    case 7: SIFT_LAUNCH(4, 4, 2, 256, true); break;
+    case 11: SIFT_LAUNCH(2, 8, 2, 64, true); break;    // r01 default
+    case 90: SIFT_LAUNCH(2, 8, 2, 64, true, 1); break;   // timing probe (wrong results): no selection
+    case 95: SIFT_LAUNCH(4, 4, 2, 64, true, 1); break;   // timing probe (wrong results): no selection
+    default: SIFT_LAUNCH(4, 4, 2, 128, false);   // measured best (r01 A/B: 9.57-9.67 ms vs 9.96-10.01 for QT=2 x 8 waves)
     }
     return hipGetLastError();
 }
