@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--no-orb", action="store_true", help="skip the ORB (config 4) leg")
     ap.add_argument("--no-c3", action="store_true", help="skip the 200-image SIFT (config 3) leg")
     ap.add_argument("--no-homography", action="store_true", help="skip the homography RANSAC leg (SURVEY §8 f1)")
+    ap.add_argument("--no-f4", action="store_true", help="skip the 3D-2D correspondence leg (SURVEY §8 f4)")
     ap.add_argument("--only-ba", action="store_true", help="run only the bundle-adjustment leg (tuning)")
     ap.add_argument("--ba-cams", type=int, default=200)
     ap.add_argument("--ba-points", type=int, default=200_000)
@@ -187,9 +188,11 @@ def bench_match(kind, args, rank, world, local):
 
     # sanity outside the timed region
     got, off, _ = matcher.fetch(stream=stream)
-    homog = None
+    homog = f4 = None
     if kind == "sift" and not args.no_homography:
         homog = bench_homography(args, matcher, imgs, my_pairs, got, off, rank, world, local, stream)
+    if kind == "sift" and not args.no_f4:
+        f4 = bench_3d2d(args, imgs, my_pairs, got, off, rank, world, local, stream)
     slow, f32p = matcher.stats(stream=stream)
     n_matches = int(off[-1])
     if world > 1:
@@ -245,6 +248,8 @@ def bench_match(kind, args, rank, world, local):
     }
     if homog is not None:
         res["homography"] = homog
+    if f4 is not None:
+        res["find_3d2d"] = f4
     if rank == 0 and world == 1 and not args.no_cpu_baseline and kind != "c3":
         res.update(cpu_baselines(kind, imgs, pairs_all, got, off, args.cpu_seconds))
     del dev_imgs
@@ -306,6 +311,75 @@ def bench_homography(args, matcher, imgs, my_pairs, got, off, rank, world, local
         res["cpu_baseline"] = {"value": len(my_pairs) / dt, "unit": "image pairs/s", "cores": threads, "kind": "port",
                                "sample": f"all {len(my_pairs)} pairs, oracle/homography_oracle.cpp (OpenMP over pairs), {dt:.2f} s"}
         res["bit_exact_vs_oracle"] = bool(np.array_equal(e, r))
+    return res
+
+
+def bench_3d2d(args, imgs, my_pairs, got, off, rank, world, local, stream):
+    """SURVEY §8 row f4 on the config-2 scene: Scene::find3d2dMatches
+    (Scene.cpp:369-424) for every shot in turn (the SfM loop registers them one
+    by one), over the point cloud of the planted landmarks (each seen by >= 2
+    images) and this rank's match graph, all resident in HBM.  Unit: origin
+    records searched per second.  CPU baseline: the reference's literal loops
+    (oracle/scene_oracle.cpp, OpenMP over points as Scene.cpp:375), a bounded
+    subset of shots."""
+    import torch
+    import torch.distributed as dist
+    from sfmx import synth, scene
+    _, src, pool_n = synth.sift_images(len(imgs), N_DESC, with_pool=True)
+    kps = synth.scene_keypoints(src, pool_n)
+    oo, osh, oxy = synth.point_cloud_origins(src, kps)
+    dev = f"cuda:{local}"
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    dk = [d(k) for k in kps]
+    dm, doff, doo, dsh, dxy = d(got.view(np.uint8)), d(off), d(oo), d(osh), d(oxy)
+    n = len(osh)
+    ok = torch.zeros(n, dtype=torch.int32, device=dev)
+    op = torch.zeros(n, dtype=torch.int32, device=dev)
+    shots = list(range(len(imgs)))
+    nkp = [len(k) for k in kps]
+
+    def one(s):
+        scene.find_3d2d_matches_device([t.data_ptr() for t in dk], nkp, my_pairs, dm.data_ptr(), doff.data_ptr(),
+                                       doo.data_ptr(), len(oo) - 1, dsh.data_ptr(), dxy.data_ptr(), s, ok.data_ptr(),
+                                       op.data_ptr(), 0, device=local, stream=stream)
+    one(0)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    kms = []
+    t0 = time.perf_counter()
+    for s in shots:
+        one(s)
+        kms.append(scene.last_kernel_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    res = {"metric": "origin records searched/s (Scene::find3d2dMatches)", "value": n * len(shots) * world / el,
+           "unit": "origin records/s", "ms_per_shot": el / len(shots) * 1e3, "kernel_ms_per_shot": float(np.mean(kms)),
+           "points": int(len(oo) - 1), "origin_records": int(n), "shots": len(shots),
+           "config": "config-2 scene: landmark point cloud (>= 2 views), this rank's match graph, every shot in turn"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+        sample = shots
+        t = time.perf_counter()
+        exact = True
+        for s in sample:
+            ek, ep = oracle.find_3d2d_matches(kps, my_pairs, got, off, oo, osh, oxy, s, nthreads=threads)
+            if s == sample[-1]:
+                one(s)
+                torch.cuda.synchronize()
+                exact = bool(np.array_equal(ok.cpu().numpy(), ek) and np.array_equal(op.cpu().numpy(), ep))
+        dt = time.perf_counter() - t
+        res["cpu_baseline"] = {"value": n * len(sample) / dt, "unit": "origin records/s", "cores": threads,
+                               "kind": "port", "sample": f"all {len(sample)} shots, the reference's nested find_if loops "
+                                                         f"(oracle/scene_oracle.cpp, OpenMP over points), {dt:.2f} s"}
+        res["exact_vs_oracle"] = exact
     return res
 
 

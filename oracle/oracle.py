@@ -49,6 +49,10 @@ def _load():
                                           i64p, i64p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]
     lib.orc_homography_ratios.argtypes = [C.POINTER(vp), i32p, i32p, C.c_int, vp, i64p, C.c_double, C.c_int,
                                           C.c_double, C.POINTER(C.c_double), C.c_int]
+    lib.orc_find_3d2d_matches.argtypes = [C.POINTER(vp), i32p, C.c_int, vp, i64p, i64p, C.c_int, i32p,
+                                          C.POINTER(C.c_double), C.c_int, i32p, i32p, C.c_int]
+    lib.orc_ba_observations.argtypes = [i64p, C.c_int, i32p, C.POINTER(C.c_double), C.c_int, i32p, i32p,
+                                        C.POINTER(C.c_double), i32p]
     lib.orc_first_sqrt_collision.restype = C.c_int64
     lib.orc_first_sqrt_collision.argtypes = [C.c_int64]
     return lib
@@ -154,6 +158,41 @@ def homography_ratios(keypoints, image_sizes, pairs, matches, offsets, threshold
                               _ptr(off, C.c_int64), threshold, max_iters, confidence,
                               out.ctypes.data_as(C.POINTER(C.c_double)), nthreads)
     return out
+
+
+def find_3d2d_matches(keypoints, pairs, matches, offsets, origin_offsets, origin_shot, origin_xy, shot, nthreads=0):
+    """Scene::find3d2dMatches (Scene.cpp:369-424) as the reference's literal loops
+    -> (keypoint index in `shot` per origin record or -1, pair index or -1)."""
+    kps = [np.ascontiguousarray(k, np.float32).reshape(-1, 2) for k in keypoints]
+    ptrs = (C.c_void_p * max(len(kps), 1))(*[k.ctypes.data for k in kps])
+    pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+    m = np.ascontiguousarray(matches, DMATCH_DTYPE)
+    off = np.ascontiguousarray(offsets, np.int64)
+    oo = np.ascontiguousarray(origin_offsets, np.int64)
+    os_ = np.ascontiguousarray(origin_shot, np.int32)
+    oxy = np.ascontiguousarray(origin_xy, np.float64)
+    n = int(oo[-1])
+    kp_out = np.zeros(max(n, 1), np.int32)
+    pr_out = np.zeros(max(n, 1), np.int32)
+    lib.orc_find_3d2d_matches(ptrs, _ptr(pairs), len(pairs), m.ctypes.data if len(m) else None, _ptr(off, C.c_int64),
+                              _ptr(oo, C.c_int64), len(oo) - 1, _ptr(os_), oxy.ctypes.data_as(C.POINTER(C.c_double)),
+                              int(shot), _ptr(kp_out), _ptr(pr_out), nthreads)
+    return kp_out[:n], pr_out[:n]
+
+
+def ba_observations(origin_offsets, origin_shot, origin_xy, n_shots):
+    """BundleAdjustment.cpp:50-91 problem assembly -> (obs_point, obs_cam, obs_xy, shot_of_pose)."""
+    oo = np.ascontiguousarray(origin_offsets, np.int64)
+    os_ = np.ascontiguousarray(origin_shot, np.int32)
+    oxy = np.ascontiguousarray(origin_xy, np.float64)
+    n = int(oo[-1])
+    op = np.zeros(max(n, 1), np.int32)
+    oc = np.zeros(max(n, 1), np.int32)
+    ox = np.zeros(max(2 * n, 1))
+    sp = np.zeros(max(n_shots, 1), np.int32)
+    npose = lib.orc_ba_observations(_ptr(oo, C.c_int64), len(oo) - 1, _ptr(os_), oxy.ctypes.data_as(C.POINTER(C.c_double)),
+                                    n_shots, _ptr(op), _ptr(oc), ox.ctypes.data_as(C.POINTER(C.c_double)), _ptr(sp))
+    return op[:n], oc[:n], ox[:2 * n].reshape(-1, 2), sp[:npose]
 
 
 def filter_matches(matches: np.ndarray, offsets: np.ndarray, distinct: bool, min_count: int):

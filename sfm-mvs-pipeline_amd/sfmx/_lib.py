@@ -62,7 +62,7 @@ class sfmx_ba_summary(C.Structure):
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p)
 
-# Every symbol include/sfmx.h (and include/sfmx_ba.h, include/sfmx_homography.h) declares, with its ctypes prototype.
+# Every symbol include/sfmx.h (and include/sfmx_ba.h, sfmx_homography.h, sfmx_scene.h) declares, with its ctypes prototype.
 _P = C.POINTER
 _i32p, _i64p, _vp = _P(C.c_int32), _P(C.c_int64), C.c_void_p
 PROTOTYPES = {
@@ -99,6 +99,11 @@ PROTOTYPES = {
     "sfmx_homography_ratios": (C.c_int, [_P(_vp), _i32p, C.c_int32, _i32p, _i32p, C.c_int32, _vp, _vp, C.c_double,
                                          C.c_int32, C.c_double, C.c_int32, C.c_int32, _vp, _P(C.c_double)]),
     "sfmx_homography_last_kernel_ms": (C.c_float, []),
+    "sfmx_find_3d2d_matches": (C.c_int, [_P(_vp), _i32p, C.c_int32, _i32p, C.c_int32, _vp, _vp, _vp, C.c_int32,
+                                         _vp, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp, _vp, _vp]),
+    "sfmx_find_3d2d_last_kernel_ms": (C.c_float, []),
+    "sfmx_ba_observations_from_origins": (C.c_int, [_i64p, C.c_int32, _i32p, _P(C.c_double), C.c_int32, _i32p, _i32p,
+                                                    _P(C.c_double), _i32p, _i32p, _i32p]),
 }
 
 

@@ -175,3 +175,27 @@ def ba_problem(n_cams: int = 200, n_points: int = 200_000, obs_per_point: int = 
     prob = dict(cam_model=k, points=pts, poses=poses, intr=intr, obs_point=obs_point, obs_cam=obs_cam,
                 obs_xy=xy, cx=cx, cy=cy)
     return (prob, tr) if truth else prob
+
+
+def point_cloud_origins(src: list, kps: list, min_views: int = 2):
+    """Point-cloud origin records (include/sfmx_scene.h layout) for a synthetic
+    scene: every landmark of the pool seen by >= min_views images is a 3-D
+    point; its origins are (image, keypoint position) of the rows carrying it,
+    in image order — what PointcloudElement::getOriginPoints lists after
+    triangulating the landmark from its matches (Scene.cpp:162-185).
+    -> (origin_offsets[int64], origin_shot[int32], origin_xy[n x 2 float64])."""
+    rows = []
+    for i, s in enumerate(src):
+        r = np.nonzero(s >= 0)[0]
+        rows.append(np.stack([s[r], np.full(len(r), i), r], axis=1))
+    allr = np.concatenate(rows) if rows else np.zeros((0, 3), np.int64)
+    order = np.lexsort((allr[:, 2], allr[:, 1], allr[:, 0]))   # landmark, image, row
+    allr = allr[order]
+    lm, start, cnt = np.unique(allr[:, 0], return_index=True, return_counts=True)
+    keep = cnt >= min_views
+    sel = np.concatenate([np.arange(s, s + c) for s, c in zip(start[keep], cnt[keep])]) if keep.any() else np.zeros(0, int)
+    recs = allr[sel]
+    off = np.zeros(int(keep.sum()) + 1, np.int64)
+    off[1:] = np.cumsum(cnt[keep])
+    xy = np.array([kps[int(i)][int(r)] for _, i, r in recs], np.float64).reshape(-1, 2)
+    return off, recs[:, 1].astype(np.int32), xy
