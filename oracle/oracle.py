@@ -53,6 +53,9 @@ def _load():
                                           C.POINTER(C.c_double), C.c_int, i32p, i32p, C.c_int]
     lib.orc_ba_observations.argtypes = [i64p, C.c_int, i32p, C.POINTER(C.c_double), C.c_int, i32p, i32p,
                                         C.POINTER(C.c_double), i32p]
+    lib.orc_undistort.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    lib.orc_undistort_batch.argtypes = [C.POINTER(vp), C.POINTER(vp), i32p, i32p, i32p, C.POINTER(C.c_double),
+                                        C.POINTER(C.c_double), C.c_int, C.c_int]
     lib.orc_first_sqrt_collision.restype = C.c_int64
     lib.orc_first_sqrt_collision.argtypes = [C.c_int64]
     return lib
@@ -193,6 +196,178 @@ def ba_observations(origin_offsets, origin_shot, origin_xy, n_shots):
     npose = lib.orc_ba_observations(_ptr(oo, C.c_int64), len(oo) - 1, _ptr(os_), oxy.ctypes.data_as(C.POINTER(C.c_double)),
                                     n_shots, _ptr(op), _ptr(oc), ox.ctypes.data_as(C.POINTER(C.c_double)), _ptr(sp))
     return op[:n], oc[:n], ox[:2 * n].reshape(-1, 2), sp[:npose]
+
+
+def _dist5(dist):
+    d = np.zeros(5)
+    d[:len(dist)] = np.asarray(dist, np.float64).ravel()[:5]
+    return d
+
+
+def undistort(img: np.ndarray, K, dist) -> np.ndarray:
+    """cv::undistort(img, out, K, dist) (ICamera.cpp:72-80; OpenCV 4.5.1 restated in
+    oracle/mvs_oracle.cpp) for an H x W [x C] uint8 image."""
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape[:2]
+    cn = 1 if img.ndim == 2 else img.shape[2]
+    out = np.empty_like(img)
+    Kd = np.ascontiguousarray(K, np.float64).reshape(9)
+    d = _dist5(dist)
+    lib.orc_undistort(img.ctypes.data, out.ctypes.data, W, H, cn, Kd.ctypes.data_as(C.POINTER(C.c_double)),
+                      d.ctypes.data_as(C.POINTER(C.c_double)))
+    return out
+
+
+def undistort_batch(imgs, Ks, dists, outs, nthreads=0):
+    """undistort() over a list of images into preallocated outs (OpenMP over images,
+    as the reference's omp loop, OpenMvsUtils.cpp:141)."""
+    n = len(imgs)
+    sp = (C.c_void_p * n)(*[a.ctypes.data for a in imgs])
+    dp = (C.c_void_p * n)(*[a.ctypes.data for a in outs])
+    W = np.array([a.shape[1] for a in imgs], np.int32)
+    H = np.array([a.shape[0] for a in imgs], np.int32)
+    cn = np.array([1 if a.ndim == 2 else a.shape[2] for a in imgs], np.int32)
+    Kd = np.ascontiguousarray(np.stack([np.asarray(k, np.float64).reshape(9) for k in Ks]))
+    dd = np.ascontiguousarray(np.stack([_dist5(d) for d in dists]))
+    lib.orc_undistort_batch(sp, dp, _ptr(W), _ptr(H), _ptr(cn), Kd.ctypes.data_as(C.POINTER(C.c_double)),
+                            dd.ctypes.data_as(C.POINTER(C.c_double)), n, nthreads or os.cpu_count())
+
+
+def openmvs_interface(cameras, shots, points, origin_offsets, origin_shot):
+    """OpenMvsUtils::toOpenMVS's Interface assembly (OpenMvsUtils.cpp:44-133), restated
+    in plain Python.  cameras: [(width, height, K 3x3)]; shots: [(camera index or -1,
+    recovered, pose 3x4, image name)]; origins: CSR of origin shot indices per point.
+    Returns a dict mirroring openMVS::Interface."""
+    platforms = [{"name": "", "cameras": [{"name": "", "width": int(w), "height": int(h),
+                                           "K": np.asarray(K, np.float64).reshape(3, 3),
+                                           "R": np.eye(3), "C": np.zeros(3)}], "poses": []}
+                 for (w, h, K) in cameras]
+    images, shot_to_id = [], {}
+    for s, (cam, rec, pose, name) in enumerate(shots):
+        if not rec or cam < 0 or cam >= len(cameras):                       # :76-78
+            continue
+        P = np.asarray(pose, np.float64).reshape(3, 4)
+        R, t = P[:, :3], P[:, 3]
+        C_ = np.array([-sum(R[k, i] * t[k] for k in range(3)) for i in range(3)])   # -R^T t
+        images.append({"name": name, "platformID": cam, "cameraID": 0,
+                       "poseID": len(platforms[cam]["poses"])})
+        platforms[cam]["poses"].append({"R": R.copy(), "C": C_})
+        shot_to_id[s] = len(images) - 1
+    vertices = []
+    pts = np.asarray(points, np.float64).reshape(-1, 3)
+    for p in range(len(pts)):
+        shots_p = set(int(x) for x in origin_shot[origin_offsets[p]:origin_offsets[p + 1]])   # getOriginShots
+        views = sorted(shot_to_id[s] for s in shots_p if s in shot_to_id)
+        if len(views) < 2:                                                   # :122-124
+            continue
+        vertices.append({"X": pts[p].astype(np.float32), "views": [(v, 0.0) for v in views]})
+    return {"platforms": platforms, "images": images, "vertices": vertices}
+
+
+def openmvs_serialize(iface, version=1) -> bytes:
+    """openMVS ARCHIVE::SerializeSave of an Interface dict (openMVS v1.1.1 stream:
+    'MVSI', uint32 version, uint32 0; uint64 counts; raw Matx / Point3; serialize()
+    field order with its version gates)."""
+    import struct
+    out = [b"MVSI", struct.pack("<II", version, 0)]
+    cnt = lambda n: out.append(struct.pack("<Q", n))
+
+    def st(s):
+        b = s.encode()
+        cnt(len(b))
+        out.append(b)
+    cnt(len(iface["platforms"]))
+    for pf in iface["platforms"]:
+        st(pf["name"])
+        cnt(len(pf["cameras"]))
+        for c in pf["cameras"]:
+            st(c["name"])
+            if version > 0:
+                out.append(struct.pack("<II", c["width"], c["height"]))
+            out.append(np.asarray(c["K"], "<f8").tobytes() + np.asarray(c["R"], "<f8").tobytes()
+                       + np.asarray(c["C"], "<f8").tobytes())
+        cnt(len(pf["poses"]))
+        for q in pf["poses"]:
+            out.append(np.asarray(q["R"], "<f8").tobytes() + np.asarray(q["C"], "<f8").tobytes())
+    cnt(len(iface["images"]))
+    for im in iface["images"]:
+        st(im["name"])
+        out.append(struct.pack("<III", im["platformID"], im["cameraID"], im["poseID"]))
+        if version > 2:
+            out.append(struct.pack("<I", 0xFFFFFFFF))
+    cnt(len(iface["vertices"]))
+    for v in iface["vertices"]:
+        out.append(np.asarray(v["X"], "<f4").tobytes())
+        cnt(len(v["views"]))
+        for (i, c) in v["views"]:
+            out.append(struct.pack("<If", i, c))
+    cnt(0)
+    cnt(0)
+    if version > 0:
+        cnt(0)
+        cnt(0)
+        cnt(0)
+        if version > 1:
+            out.append(np.eye(4, dtype="<f8").tobytes())
+    return b"".join(out)
+
+
+def openmvs_parse(buf: bytes) -> dict:
+    """Inverse of openmvs_serialize (what openMVS's SerializeLoad reads)."""
+    import struct
+    pos = 0
+
+    def take(fmt):
+        nonlocal pos
+        v = struct.unpack_from(fmt, buf, pos)
+        pos += struct.calcsize(fmt)
+        return v
+
+    def arr(n, dt):
+        nonlocal pos
+        a = np.frombuffer(buf, dt, n, pos).copy()
+        pos += n * np.dtype(dt).itemsize
+        return a
+
+    def st():
+        nonlocal pos
+        (n,) = take("<Q")
+        s = buf[pos:pos + n].decode()
+        pos += n
+        return s
+    assert buf[:4] == b"MVSI"
+    pos = 4
+    version, _ = take("<II")
+    pfs = []
+    for _ in range(take("<Q")[0]):
+        pf = {"name": st(), "cameras": [], "poses": []}
+        for _ in range(take("<Q")[0]):
+            c = {"name": st()}
+            if version > 0:
+                c["width"], c["height"] = take("<II")
+            c["K"], c["R"], c["C"] = arr(9, "<f8").reshape(3, 3), arr(9, "<f8").reshape(3, 3), arr(3, "<f8")
+            pf["cameras"].append(c)
+        for _ in range(take("<Q")[0]):
+            pf["poses"].append({"R": arr(9, "<f8").reshape(3, 3), "C": arr(3, "<f8")})
+        pfs.append(pf)
+    imgs = []
+    for _ in range(take("<Q")[0]):
+        im = {"name": st()}
+        im["platformID"], im["cameraID"], im["poseID"] = take("<III")
+        if version > 2:
+            im["ID"] = take("<I")[0]
+        imgs.append(im)
+    verts = []
+    for _ in range(take("<Q")[0]):
+        X = arr(3, "<f4")
+        verts.append({"X": X, "views": [take("<If") for _ in range(take("<Q")[0])]})
+    rest = {"verticesNormal": take("<Q")[0], "verticesColor": take("<Q")[0]}
+    if version > 0:
+        rest.update(lines=take("<Q")[0], linesNormal=take("<Q")[0], linesColor=take("<Q")[0])
+        if version > 1:
+            rest["transform"] = arr(16, "<f8").reshape(4, 4)
+    assert pos == len(buf), "trailing bytes"
+    return {"version": version, "platforms": pfs, "images": imgs, "vertices": verts, **rest}
 
 
 def filter_matches(matches: np.ndarray, offsets: np.ndarray, distinct: bool, min_count: int):

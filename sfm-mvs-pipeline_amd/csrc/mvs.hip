@@ -1,0 +1,395 @@
+// SPDX-License-Identifier: MIT
+// sfmx undistortion for the openMVS export, gfx950.
+//
+//   sfmx_undistort_images   cv::undistort(in, out, K, dist) of every recovered
+//                           shot (OpenMvsUtils.cpp:142-150 -> ICamera::undistort,
+//                           common/ICamera.cpp:72-80), OpenCV 4.5.1 semantics.
+//
+// cv::undistort works in horizontal stripes of max(1, 4096 / cols) rows.  For
+// each stripe starting at row y it sets the new camera matrix's (1,2) entry to
+// v0 - y, inverts it (cv::invert's 3x3 adjugate / det formula), builds the
+// inverse map with initUndistortRectifyMap into CV_16SC2 + CV_16UC1 (positions
+// in 1/32 px, round-half-even) and resamples with cv::remap INTER_LINEAR,
+// BORDER_CONSTANT 0 (15-bit fixed-point bilinear weights).
+//
+// For the camera matrices the reference produces (zero skew, K[3] = K[6] =
+// K[7] = 0, K[8] = 1) the inverse has ir[1] = ir[3] = ir[6] = ir[7] = 0 and
+// ir[0], ir[2], ir[8] do not depend on the stripe, so the running sum
+// `_x += ir[0]` of initUndistortRectifyMap's inner loop is the same sequence
+// for every row: it is summed once per image on the host (in the same order)
+// and read as a column table.  Everything per row (ir[5], 1/_w, y) and per
+// pixel (the distortion polynomial, the fixed-point map, the bilinear sum) is
+// recomputed here in the reference's operation order; the file is built with
+// -ffp-contract=off so no a*b+c is fused.  Result: bit-identical to the
+// restatement in oracle/mvs_oracle.cpp.
+//
+// Byte work: HBM-bound.  Algorithmic bytes per output pixel = 2 * channels
+// (the source read once, the destination written once).
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/sfmx_mvs.h"
+#include "match_common.hpp"
+
+namespace sfmx {
+namespace mvs {
+
+constexpr int PX_PER_THREAD = 4;
+
+// global (not flat) address space: the image pointers come out of a descriptor in
+// memory, so the compiler cannot infer it and would emit flat_load/flat_store
+#define GPTR(T) __attribute__((address_space(1))) T*
+#define CGPTR(T) const __attribute__((address_space(1))) T*
+constexpr int THREADS = 256;
+constexpr int PX_PER_BLOCK = PX_PER_THREAD * THREADS;
+
+struct UndImg {
+    const uint8_t* src;
+    uint8_t* dst;
+    int64_t src_pitch, dst_pitch;
+    const double2* xcol;     // per column: x = _x * (1/_w) and x*x (_x: initUndistortRectifyMap's running sum)
+    int64_t blk0;            // first block of this image in the launch
+    int32_t W, H, C, stripe0;
+    int32_t bpr;             // blocks per row
+    int32_t dst_words;       // 1: dst rows and base are 4-byte aligned (dword stores)
+    int32_t src_words;       // 1: src rows and base are 4-byte aligned and W >= 2 (dword tap loads)
+    int32_t radial;          // 1: p1 = p2 = k3 = 0 (SimpleRadialCamera): the zero terms drop out exactly
+    double K0, K5, d, t4, t8;
+    double fx, fy, u0, v0, k1, k2, p1, p2, k3;
+};
+
+// cvRound of a double on x86 (cvtsd2si): round half to even, and the
+// "integer indefinite" INT_MIN for NaN / out of range.
+__device__ __forceinline__ int cv_round(double v) {
+    const double r = rint(v);
+    if (!(r >= -2147483648.0 && r <= 2147483647.0)) return INT_MIN;
+    return (int)r;
+}
+
+// The two horizontal taps (bx, bx + 1) of one source row, as two packed C-byte
+// values.  Fast path: one aligned 2- or 3-dword load covering both pixels and a
+// byte funnel shift (v_alignbyte); the last source row and unaligned images use
+// byte loads so nothing is read past the end of the buffer.
+template <int C>
+__device__ __forceinline__ void fetch_taps(CGPTR(uint8_t) row, int bx, bool words, bool two,
+                                           uint32_t& t0, uint32_t& t1) {
+    const int o = bx * C;
+    if (words) {
+        const int oa = o & ~3, sh = o & 3;
+        CGPTR(uint32_t) p = reinterpret_cast<CGPTR(uint32_t)>(row + oa);
+        if constexpr (C == 3) {
+            const uint32_t a = p[0], b = p[1], c = p[2];
+            const uint32_t lo = __builtin_amdgcn_alignbyte(b, a, sh), hi = __builtin_amdgcn_alignbyte(c, b, sh);
+            t0 = lo & 0xFFFFFFu;
+            t1 = (lo >> 24) | ((hi & 0xFFFFu) << 8);
+        } else {
+            const uint32_t a = p[0], b = p[1];
+            if constexpr (C == 4) {
+                t0 = a;
+                t1 = b;
+            } else {
+                const uint32_t lo = __builtin_amdgcn_alignbyte(b, a, sh);
+                t0 = lo & ((1u << (8 * C)) - 1);
+                t1 = (lo >> (8 * C)) & ((1u << (8 * C)) - 1);
+            }
+        }
+    } else {
+        t0 = t1 = 0;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            t0 |= (uint32_t)row[o + c] << (8 * c);
+            if (two) t1 |= (uint32_t)row[o + C + c] << (8 * c);
+        }
+    }
+}
+
+template <int C>
+__global__ __launch_bounds__(THREADS)
+void undistort_kernel(const UndImg* __restrict__ imgs, int n_imgs, int64_t n_blocks) {
+    // XCD-aware order: hardware dispatches block b to XCD b % 8; give every XCD a
+    // contiguous run of logical blocks so adjacent rows share its L2.
+    const int64_t b = blockIdx.x;
+    const int64_t q = n_blocks / 8, r = n_blocks % 8;
+    const int64_t xcd = b % 8, idx = b / 8;
+    const int64_t lb = xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+    int lo = 0, hi = n_imgs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (imgs[mid].blk0 <= lb) lo = mid; else hi = mid - 1;
+    }
+    const UndImg& im = imgs[lo];
+    const int64_t rb = lb - im.blk0;
+    const int Y = (int)(rb / im.bpr);
+    const int x0 = (int)(rb % im.bpr) * PX_PER_BLOCK + (int)threadIdx.x * PX_PER_THREAD;
+    if (Y >= im.H || x0 >= im.W) return;
+
+    // per row: the stripe's inverse (cv::invert adjugate; see header comment)
+    const int ys = (Y / im.stripe0) * im.stripe0;
+    const int i = Y - ys;
+    const double m12 = im.K5 - (double)ys;                 // Ar(1,2) = v0 - y
+    const double t5 = (0.0 - im.K0 * m12) * im.d;           // (a02*a10 - a00*a12) * d
+    const double yr = ((double)i * im.t4 + t5);             // _y = i*ir[4] + ir[5]
+    const double w = 1. / im.t8;                            // _w = i*ir[7] + ir[8]
+    const double y = yr * w;
+    const double y2 = y * y;
+
+    const int W = im.W, H = im.H;
+    CGPTR(uint8_t) S = (CGPTR(uint8_t))im.src;
+    const int64_t sp = im.src_pitch;
+    const int npx = min(PX_PER_THREAD, W - x0);
+    double xv[PX_PER_THREAD], x2v[PX_PER_THREAD];
+    CGPTR(double) xc = (CGPTR(double))im.xcol;
+#pragma unroll
+    for (int p = 0; p < PX_PER_THREAD; ++p) {
+        const int j = min(x0 + p, W - 1);
+        xv[p] = xc[2 * j];
+        x2v[p] = xc[2 * j + 1];
+    }
+    uint32_t out[C];                                        // 4 px x C bytes, packed
+#pragma unroll
+    for (int k = 0; k < C; ++k) out[k] = 0;
+    const bool radial = im.radial;
+#pragma unroll
+    for (int p = 0; p < PX_PER_THREAD; ++p) {
+        const double x = xv[p], x2 = x2v[p];
+        const double r2 = x2 + y2;
+        double u, v;
+        if (radial) {
+            // k3 = 0: (0*r2 + k2) == k2; p1 = p2 = 0: the tangential terms are +-0 and
+            // x*kr + +-0 can only differ from x*kr in the sign of a zero, which
+            // fx*xd + u0 and the rounding below cannot see
+            const double kr = 1 + (im.k2 * r2 + im.k1) * r2;
+            u = im.fx * (x * kr) + im.u0;
+            v = im.fy * (y * kr) + im.v0;
+        } else {
+            const double _2xy = 2 * x * y;
+            const double kr = 1 + ((im.k3 * r2 + im.k2) * r2 + im.k1) * r2;   // / (1 + 0) == exact
+            const double xd = x * kr + im.p1 * _2xy + im.p2 * (r2 + 2 * x2);
+            const double yd = y * kr + im.p1 * (r2 + 2 * y2) + im.p2 * _2xy;
+            u = im.fx * xd + im.u0;
+            v = im.fy * yd + im.v0;
+        }
+        const int iu = cv_round(u * 32), iv = cv_round(v * 32);
+        const int sx = (int)(short)(iu >> 5), sy = (int)(short)(iv >> 5);
+        const int a = iu & 31, bb = iv & 31;
+        // weights of the taps that lie inside the image (BORDER_CONSTANT 0 elsewhere)
+        const bool x0in = (unsigned)sx < (unsigned)W, x1in = (unsigned)(sx + 1) < (unsigned)W;
+        const bool y0in = (unsigned)sy < (unsigned)H, y1in = (unsigned)(sy + 1) < (unsigned)H;
+        int w0 = (32 - bb) * (32 - a) * 32;
+        if (w0 == 32768) w0 = 32767;                        // saturate_cast<short> of the table entry
+        w0 = (y0in && x0in) ? w0 : 0;
+        const int w1 = (y0in && x1in) ? (32 - bb) * a * 32 : 0;
+        const int w2 = (y1in && x0in) ? bb * (32 - a) * 32 : 0;
+        const int w3 = (y1in && x1in) ? bb * a * 32 : 0;
+        // Both taps of a row come from the pixel pair (bx, bx + 1), bx clamped into
+        // [0, W - 2]; at the borders the in-image tap is the pair's first (sx = -1)
+        // or second (sx = W - 1) pixel, the other tap weighs 0.  (W == 1 images
+        // take the byte path with bx = 0 and a duplicated pixel.)
+        const int bx = W >= 2 ? min(max(sx, 0), W - 2) : 0;
+        const bool first_is_t1 = sx < 0, second_is_t0 = sx >= W - 1;
+        const int cy0 = min(max(sy, 0), H - 1), cy1 = min(max(sy + 1, 0), H - 1);
+        uint32_t a0, a1, b0, b1;
+        // row offsets: cy < 2^15 and pitch < 2^24 (checked on the host) -> 24-bit multiplies
+        fetch_taps<C>(S + __umul24((unsigned)cy0, (unsigned)sp), bx, im.src_words && cy0 < H - 1, W >= 2, a0, a1);
+        fetch_taps<C>(S + __umul24((unsigned)cy1, (unsigned)sp), bx, im.src_words && cy1 < H - 1, W >= 2, b0, b1);
+        if (W == 1) { a1 = a0; b1 = b0; }
+        const uint32_t p00 = second_is_t0 ? a1 : a0, p01 = first_is_t1 ? a0 : a1;
+        const uint32_t p10 = second_is_t0 ? b1 : b0, p11 = first_is_t1 ? b0 : b1;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int s = (int)((p00 >> (8 * c)) & 255) * w0 + (int)((p01 >> (8 * c)) & 255) * w1 +
+                          (int)((p10 >> (8 * c)) & 255) * w2 + (int)((p11 >> (8 * c)) & 255) * w3;
+            const uint32_t o = (uint32_t)((s + 16384) >> 15);   // 0 <= s <= 255 * 32768: no saturation needed
+            const int byte = p * C + c;                     // compile-time after unrolling
+            out[byte >> 2] |= o << (8 * (byte & 3));
+        }
+    }
+    GPTR(uint8_t) D = (GPTR(uint8_t))im.dst + (int64_t)Y * im.dst_pitch + (int64_t)x0 * C;
+    if (im.dst_words && npx == PX_PER_THREAD) {             // 4 px * C bytes = C dwords, 4-aligned
+        GPTR(uint32_t) Dw = reinterpret_cast<GPTR(uint32_t)>(D);
+#pragma unroll
+        for (int k = 0; k < C; ++k) Dw[k] = out[k];
+    } else {
+        for (int k = 0; k < npx * C; ++k) D[k] = (uint8_t)(out[k >> 2] >> (8 * (k & 3)));
+    }
+}
+
+thread_local float g_last_ms = -1.f;
+
+struct Bufs {
+    std::vector<void*> ptrs;
+    ~Bufs() { for (void* q : ptrs) (void)hipFree(q); }
+    void* alloc(size_t bytes) {
+        void* q = nullptr;
+        if (hipMalloc(&q, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
+        ptrs.push_back(q);
+        return q;
+    }
+};
+
+}  // namespace mvs
+}  // namespace sfmx
+
+using namespace sfmx;
+using namespace sfmx::mvs;
+
+#define UCHK(expr) do { if ((expr) != hipSuccess) { rc = SFMX_EDEVICE; set_last_error("HIP error in " #expr); goto done; } } while (0)
+
+extern "C" {
+
+float sfmx_undistort_last_kernel_ms(void) { return g_last_ms; }
+
+int sfmx_undistort_images(const sfmx_undistort_image* images, int32_t n_images, int32_t inputs_on_device,
+                          int32_t device, void* stream) {
+    if (n_images < 0 || (n_images && !images)) { set_last_error("bad image list"); return SFMX_EINVAL; }
+    for (int n = 0; n < n_images; ++n) {
+        const sfmx_undistort_image& g = images[n];
+        if (!g.src || !g.dst || g.src == g.dst) { set_last_error("null or aliased image buffer"); return SFMX_EINVAL; }
+        if (g.width <= 0 || g.height <= 0 || g.width >= 32767 || g.height >= 32767) {
+            set_last_error("image size outside (0, 32767)");
+            return SFMX_EINVAL;
+        }
+        if (g.channels < 1 || g.channels > 4) { set_last_error("channels must be 1..4"); return SFMX_EINVAL; }
+        if (g.src_pitch < (int64_t)g.width * g.channels || g.dst_pitch < (int64_t)g.width * g.channels) {
+            set_last_error("pitch smaller than a row");
+            return SFMX_EINVAL;
+        }
+        if (g.src_pitch >= (1 << 24)) { set_last_error("source pitch must be < 16 MiB"); return SFMX_EINVAL; }
+        if (g.K[1] != 0 || g.K[3] != 0 || g.K[6] != 0 || g.K[7] != 0 || g.K[8] != 1) {
+            set_last_error("camera matrix must be [fx 0 cx; 0 fy cy; 0 0 1] (ICamera::getK)");
+            return SFMX_EINVAL;
+        }
+        if (!(g.K[0] * g.K[4] != 0) || !std::isfinite(g.K[0] * g.K[4])) {
+            set_last_error("singular camera matrix");
+            return SFMX_EINVAL;
+        }
+    }
+    if (n_images == 0) return SFMX_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { set_last_error("no HIP device visible"); return SFMX_EDEVICE; }
+    if (device < 0 || device >= ndev) { set_last_error("device index out of range"); return SFMX_EINVAL; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_last_error("sfmx kernels are built for gfx950 only");
+        return SFMX_EDEVICE;
+    }
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device);
+    const hipStream_t st = (hipStream_t)stream;
+    int rc = SFMX_OK;
+    {
+        Bufs b;
+        std::vector<UndImg> h(n_images);
+        int64_t ncol = 0;
+        int cnt_c[5] = {0, 0, 0, 0, 0}, first_c[5] = {0, 0, 0, 0, 0};
+        int64_t blk_c[5] = {0, 0, 0, 0, 0};
+        std::vector<uint8_t*> staged_dst(n_images);
+        for (int n = 0; n < n_images; ++n) ncol += images[n].width;
+        std::vector<double2> xcol(ncol);
+        auto* dcol = static_cast<double2*>(b.alloc(sizeof(double2) * ncol));
+        auto* dimg = static_cast<UndImg*>(b.alloc(sizeof(UndImg) * n_images));
+        if (!dcol || !dimg) { rc = SFMX_ENOMEM; goto done; }
+        {
+            int64_t co = 0;
+            for (int n = 0; n < n_images; ++n) {
+                const sfmx_undistort_image& g = images[n];
+                UndImg& u = h[n];
+                u.W = g.width; u.H = g.height; u.C = g.channels;
+                u.stripe0 = std::min(std::max(1, (1 << 12) / std::max(g.width, 1)), g.height);
+                u.bpr = (g.width + PX_PER_BLOCK - 1) / PX_PER_BLOCK;
+                // cv::invert (3x3, DECOMP_LU) of the stripe's new camera matrix: det3 and
+                // the adjugate rows that do not depend on the stripe (header comment)
+                const double K0 = g.K[0], K2 = g.K[2], K4 = g.K[4];
+                const double det = K0 * K4;
+                const double d = 1. / det;
+                const double t0 = K4 * d, t2 = (0.0 - K2 * K4) * d;
+                u.K0 = K0; u.K5 = g.K[5]; u.d = d;
+                u.t4 = K0 * d; u.t8 = det * d;
+                u.fx = K0; u.fy = K4; u.u0 = K2; u.v0 = g.K[5];
+                u.k1 = g.dist[0]; u.k2 = g.dist[1]; u.p1 = g.dist[2]; u.p2 = g.dist[3]; u.k3 = g.dist[4];
+                const double w = 1. / u.t8;                            // 1/_w, the same for every row
+                double xs = 0.0 + t2;                                  // _x = i*ir[1] + ir[2]
+                for (int j = 0; j < g.width; ++j, xs += t0) {          // _x += ir[0]
+                    const double x = xs * w;
+                    xcol[co + j] = double2(x, x * x);
+                }
+                u.radial = (g.dist[2] == 0 && g.dist[3] == 0 && g.dist[4] == 0) ? 1 : 0;
+                u.xcol = dcol + co;
+                co += g.width;
+                u.src_pitch = g.src_pitch; u.dst_pitch = g.dst_pitch;
+                u.src = g.src; u.dst = g.dst;
+            }
+        }
+        if (!inputs_on_device) {   // stage every image on the device, packed rows
+            for (int n = 0; n < n_images; ++n) {
+                const sfmx_undistort_image& g = images[n];
+                const int64_t row = (int64_t)g.width * g.channels;
+                auto* s = static_cast<uint8_t*>(b.alloc(row * g.height));
+                auto* o = static_cast<uint8_t*>(b.alloc(row * g.height));
+                if (!s || !o) { rc = SFMX_ENOMEM; goto done; }
+                UCHK(hipMemcpy2DAsync(s, row, g.src, g.src_pitch, row, g.height, hipMemcpyHostToDevice, st));
+                h[n].src = s; h[n].dst = o;
+                h[n].src_pitch = h[n].dst_pitch = row;
+            }
+        }
+        for (UndImg& u : h)
+            u.dst_words = ((uintptr_t)u.dst % 4 == 0 && u.dst_pitch % 4 == 0) ? 1 : 0;
+        for (UndImg& u : h)
+            u.src_words = ((uintptr_t)u.src % 4 == 0 && u.src_pitch % 4 == 0 && u.W >= 2) ? 1 : 0;
+        for (int n = 0; n < n_images; ++n) staged_dst[n] = h[n].dst;
+        // one launch per channel count (the kernel is specialised on it): images grouped by C
+        std::stable_sort(h.begin(), h.end(), [](const UndImg& p, const UndImg& q) { return p.C < q.C; });
+        for (const UndImg& u : h) {
+            if (cnt_c[u.C] == 0) first_c[u.C] = (int)(&u - h.data());
+            cnt_c[u.C]++;
+        }
+        for (UndImg& u : h) {
+            u.blk0 = blk_c[u.C];
+            blk_c[u.C] += (int64_t)u.bpr * u.H;
+        }
+        UCHK(hipMemcpyAsync(dcol, xcol.data(), sizeof(double2) * ncol, hipMemcpyHostToDevice, st));
+        UCHK(hipMemcpyAsync(dimg, h.data(), sizeof(UndImg) * n_images, hipMemcpyHostToDevice, st));
+        {
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            UCHK(hipEventCreate(&e0));
+            UCHK(hipEventCreate(&e1));
+            UCHK(hipEventRecord(e0, st));
+            for (int c = 1; c <= 4; ++c) {
+                if (cnt_c[c] == 0) continue;
+                const int64_t nb = blk_c[c];
+                if (nb >= (int64_t)INT32_MAX) { set_last_error("images too large for one launch"); rc = SFMX_EINVAL; goto done; }
+                const UndImg* di = dimg + first_c[c];
+                if (c == 1) undistort_kernel<1><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], nb);
+                if (c == 2) undistort_kernel<2><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], nb);
+                if (c == 3) undistort_kernel<3><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], nb);
+                if (c == 4) undistort_kernel<4><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], nb);
+                UCHK(hipGetLastError());
+            }
+            UCHK(hipEventRecord(e1, st));
+            if (!inputs_on_device)
+                for (int n = 0; n < n_images; ++n) {
+                    const sfmx_undistort_image& g = images[n];
+                    const int64_t row = (int64_t)g.width * g.channels;
+                    UCHK(hipMemcpy2DAsync(g.dst, g.dst_pitch, staged_dst[n], row, row, g.height, hipMemcpyDeviceToHost, st));
+                }
+            UCHK(hipStreamSynchronize(st));
+            float ms = -1.f;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            g_last_ms = ms;
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+        }
+    done:;
+    }
+    if (rc == SFMX_ENOMEM) set_last_error("device allocation failed");
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return rc;
+}
+
+}  // extern "C"
