@@ -461,6 +461,20 @@ def bench_ba(args, rank, world, local):
 MVS_SHOTS, MVS_H, MVS_W, MVS_C = 50, 3000, 4000, 3
 
 
+def _mvs_traffic(px_mine):
+    """HBM bytes per undistortion launch from the committed PMC pass (tools/pmc_mvs.sh,
+    the full 50-shot job on one GPU); None for other shard sizes."""
+    path = os.path.join(REPO, "profiles", "r01_pmc_mvs.json")
+    if px_mine != MVS_SHOTS * MVS_H * MVS_W or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    for k, v in d.items():
+        if "undistort_kernel" in k:
+            return (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0
+    return None
+
+
 def bench_mvs(args, rank, world, local):
     """SURVEY §8 row f2, OpenMvsUtils::toOpenMVS (OpenMvsUtils.cpp:31-154) on the
     config-2 scene: cv::undistort of every recovered shot (50 x 12 MP RGB photos,
@@ -512,7 +526,9 @@ def bench_mvs(args, rank, world, local):
            "config": {"workload": f"{MVS_SHOTS} shots x {MVS_W}x{MVS_H} RGB u8, SimpleRadial cv::undistort "
                                   "(INTER_LINEAR, BORDER_CONSTANT)", "parallelism": f"shot-sharded x{world}"},
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "undistort_kernel",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": _mvs_traffic(px_mine),
+                        "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/r01_pmc_mvs.json)",
+                        "kernel": "undistort_kernel",
                         "kernel_ms_per_launch": kern_ms,
                         "algorithmic": f"2 x {MVS_C} B/pixel x {px_mine:.4g} pixels per launch"}}
     # native Interface serialisation (host), config-5-sized scene

@@ -27,6 +27,7 @@
 // (the source read once, the destination written once).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -59,6 +60,8 @@ struct UndImg {
     int32_t dst_words;       // 1: dst rows and base are 4-byte aligned (dword stores)
     int32_t src_words;       // 1: src rows and base are 4-byte aligned and W >= 2 (dword tap loads)
     int32_t radial;          // 1: p1 = p2 = k3 = 0 (SimpleRadialCamera): the zero terms drop out exactly
+    double w;                // 1/_w = 1/ir[8]
+    double t0, t2;           // ir[0], ir[2]
     double K0, K5, d, t4, t8;
     double fx, fy, u0, v0, k1, k2, p1, p2, k3;
 };
@@ -72,14 +75,13 @@ __device__ __forceinline__ int cv_round(double v) {
 }
 
 // The two horizontal taps (bx, bx + 1) of one source row, as two packed C-byte
-// values.  Fast path: one aligned 2- or 3-dword load covering both pixels and a
-// byte funnel shift (v_alignbyte); the last source row and unaligned images use
-// byte loads so nothing is read past the end of the buffer.
-template <int C>
-__device__ __forceinline__ void fetch_taps(CGPTR(uint8_t) row, int bx, bool words, bool two,
-                                           uint32_t& t0, uint32_t& t1) {
+// values.  WORDS: one aligned 2- or 3-dword load covering both pixels and a byte
+// funnel shift (v_alignbyte); it may read up to 8 bytes past the last row, which
+// the host checks against the allocation (else the image takes the byte path).
+template <int C, bool WORDS>
+__device__ __forceinline__ void fetch_taps(CGPTR(uint8_t) row, int bx, bool two, uint32_t& t0, uint32_t& t1) {
     const int o = bx * C;
-    if (words) {
+    if constexpr (WORDS) {
         const int oa = o & ~3, sh = o & 3;
         CGPTR(uint32_t) p = reinterpret_cast<CGPTR(uint32_t)>(row + oa);
         if constexpr (C == 3) {
@@ -108,55 +110,32 @@ __device__ __forceinline__ void fetch_taps(CGPTR(uint8_t) row, int bx, bool word
     }
 }
 
-template <int C>
-__global__ __launch_bounds__(THREADS)
-void undistort_kernel(const UndImg* __restrict__ imgs, int n_imgs, int64_t n_blocks) {
-    // XCD-aware order: hardware dispatches block b to XCD b % 8; give every XCD a
-    // contiguous run of logical blocks so adjacent rows share its L2.
-    const int64_t b = blockIdx.x;
-    const int64_t q = n_blocks / 8, r = n_blocks % 8;
-    const int64_t xcd = b % 8, idx = b / 8;
-    const int64_t lb = xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
-    int lo = 0, hi = n_imgs - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (imgs[mid].blk0 <= lb) lo = mid; else hi = mid - 1;
-    }
-    const UndImg& im = imgs[lo];
-    const int64_t rb = lb - im.blk0;
-    const int Y = (int)(rb / im.bpr);
-    const int x0 = (int)(rb % im.bpr) * PX_PER_BLOCK + (int)threadIdx.x * PX_PER_THREAD;
-    if (Y >= im.H || x0 >= im.W) return;
-
+// One thread: PX_PER_THREAD consecutive pixels of row Y.  Three phases so the
+// tap loads of all pixels are in flight together: (1) the inverse map of every
+// pixel in fp64, (2) the 2 x PX tap-pair loads, (3) the fixed-point blends.
+template <int C, bool WORDS>
+__device__ __forceinline__ void undistort_px(const UndImg& im, int Y, int x0) {
     // per row: the stripe's inverse (cv::invert adjugate; see header comment)
     const int ys = (Y / im.stripe0) * im.stripe0;
     const int i = Y - ys;
     const double m12 = im.K5 - (double)ys;                 // Ar(1,2) = v0 - y
     const double t5 = (0.0 - im.K0 * m12) * im.d;           // (a02*a10 - a00*a12) * d
     const double yr = ((double)i * im.t4 + t5);             // _y = i*ir[4] + ir[5]
-    const double w = 1. / im.t8;                            // _w = i*ir[7] + ir[8]
-    const double y = yr * w;
+    const double y = yr * im.w;                             // w = 1/_w, _w = i*ir[7] + ir[8] = ir[8]
     const double y2 = y * y;
 
     const int W = im.W, H = im.H;
     CGPTR(uint8_t) S = (CGPTR(uint8_t))im.src;
-    const int64_t sp = im.src_pitch;
-    const int npx = min(PX_PER_THREAD, W - x0);
-    double xv[PX_PER_THREAD], x2v[PX_PER_THREAD];
+    const unsigned sp = (unsigned)im.src_pitch;
     CGPTR(double) xc = (CGPTR(double))im.xcol;
+    const bool radial = im.radial;
+
+    // (1) map: source position in 1/32 px
+    int iu[PX_PER_THREAD], iv[PX_PER_THREAD];
 #pragma unroll
     for (int p = 0; p < PX_PER_THREAD; ++p) {
         const int j = min(x0 + p, W - 1);
-        xv[p] = xc[2 * j];
-        x2v[p] = xc[2 * j + 1];
-    }
-    uint32_t out[C];                                        // 4 px x C bytes, packed
-#pragma unroll
-    for (int k = 0; k < C; ++k) out[k] = 0;
-    const bool radial = im.radial;
-#pragma unroll
-    for (int p = 0; p < PX_PER_THREAD; ++p) {
-        const double x = xv[p], x2 = x2v[p];
+        const double x = xc[2 * j], x2 = xc[2 * j + 1];
         const double r2 = x2 + y2;
         double u, v;
         if (radial) {
@@ -174,10 +153,30 @@ void undistort_kernel(const UndImg* __restrict__ imgs, int n_imgs, int64_t n_blo
             u = im.fx * xd + im.u0;
             v = im.fy * yd + im.v0;
         }
-        const int iu = cv_round(u * 32), iv = cv_round(v * 32);
-        const int sx = (int)(short)(iu >> 5), sy = (int)(short)(iv >> 5);
-        const int a = iu & 31, bb = iv & 31;
-        // weights of the taps that lie inside the image (BORDER_CONSTANT 0 elsewhere)
+        iu[p] = cv_round(u * 32);
+        iv[p] = cv_round(v * 32);
+    }
+    // (2) taps.  Both taps of a row come from the pixel pair (bx, bx + 1), bx
+    // clamped into [0, W - 2]; at the borders the in-image tap is the pair's
+    // first (sx = -1) or second (sx = W - 1) pixel, the other tap weighs 0.
+    uint32_t ta0[PX_PER_THREAD], ta1[PX_PER_THREAD], tb0[PX_PER_THREAD], tb1[PX_PER_THREAD];
+#pragma unroll
+    for (int p = 0; p < PX_PER_THREAD; ++p) {
+        const int sx = (int)(short)(iu[p] >> 5), sy = (int)(short)(iv[p] >> 5);
+        const int bx = W >= 2 ? min(max(sx, 0), W - 2) : 0;
+        const unsigned cy0 = (unsigned)min(max(sy, 0), H - 1), cy1 = (unsigned)min(max(sy + 1, 0), H - 1);
+        // row offsets: cy < 2^15 and pitch < 2^24 (checked on the host) -> 24-bit multiplies
+        fetch_taps<C, WORDS>(S + __umul24(cy0, sp), bx, W >= 2, ta0[p], ta1[p]);
+        fetch_taps<C, WORDS>(S + __umul24(cy1, sp), bx, W >= 2, tb0[p], tb1[p]);
+    }
+    // (3) blend: cv::remap INTER_LINEAR, 15-bit weights, BORDER_CONSTANT 0
+    uint32_t out[C];                                        // 4 px x C bytes, packed
+#pragma unroll
+    for (int k = 0; k < C; ++k) out[k] = 0;
+#pragma unroll
+    for (int p = 0; p < PX_PER_THREAD; ++p) {
+        const int sx = (int)(short)(iu[p] >> 5), sy = (int)(short)(iv[p] >> 5);
+        const int a = iu[p] & 31, bb = iv[p] & 31;
         const bool x0in = (unsigned)sx < (unsigned)W, x1in = (unsigned)(sx + 1) < (unsigned)W;
         const bool y0in = (unsigned)sy < (unsigned)H, y1in = (unsigned)(sy + 1) < (unsigned)H;
         int w0 = (32 - bb) * (32 - a) * 32;
@@ -186,18 +185,9 @@ void undistort_kernel(const UndImg* __restrict__ imgs, int n_imgs, int64_t n_blo
         const int w1 = (y0in && x1in) ? (32 - bb) * a * 32 : 0;
         const int w2 = (y1in && x0in) ? bb * (32 - a) * 32 : 0;
         const int w3 = (y1in && x1in) ? bb * a * 32 : 0;
-        // Both taps of a row come from the pixel pair (bx, bx + 1), bx clamped into
-        // [0, W - 2]; at the borders the in-image tap is the pair's first (sx = -1)
-        // or second (sx = W - 1) pixel, the other tap weighs 0.  (W == 1 images
-        // take the byte path with bx = 0 and a duplicated pixel.)
-        const int bx = W >= 2 ? min(max(sx, 0), W - 2) : 0;
-        const bool first_is_t1 = sx < 0, second_is_t0 = sx >= W - 1;
-        const int cy0 = min(max(sy, 0), H - 1), cy1 = min(max(sy + 1, 0), H - 1);
-        uint32_t a0, a1, b0, b1;
-        // row offsets: cy < 2^15 and pitch < 2^24 (checked on the host) -> 24-bit multiplies
-        fetch_taps<C>(S + __umul24((unsigned)cy0, (unsigned)sp), bx, im.src_words && cy0 < H - 1, W >= 2, a0, a1);
-        fetch_taps<C>(S + __umul24((unsigned)cy1, (unsigned)sp), bx, im.src_words && cy1 < H - 1, W >= 2, b0, b1);
+        uint32_t a0 = ta0[p], a1 = ta1[p], b0 = tb0[p], b1 = tb1[p];
         if (W == 1) { a1 = a0; b1 = b0; }
+        const bool first_is_t1 = sx < 0, second_is_t0 = sx >= W - 1;
         const uint32_t p00 = second_is_t0 ? a1 : a0, p01 = first_is_t1 ? a0 : a1;
         const uint32_t p10 = second_is_t0 ? b1 : b0, p11 = first_is_t1 ? b0 : b1;
 #pragma unroll
@@ -209,6 +199,7 @@ void undistort_kernel(const UndImg* __restrict__ imgs, int n_imgs, int64_t n_blo
             out[byte >> 2] |= o << (8 * (byte & 3));
         }
     }
+    const int npx = min(PX_PER_THREAD, W - x0);
     GPTR(uint8_t) D = (GPTR(uint8_t))im.dst + (int64_t)Y * im.dst_pitch + (int64_t)x0 * C;
     if (im.dst_words && npx == PX_PER_THREAD) {             // 4 px * C bytes = C dwords, 4-aligned
         GPTR(uint32_t) Dw = reinterpret_cast<GPTR(uint32_t)>(D);
@@ -219,7 +210,80 @@ void undistort_kernel(const UndImg* __restrict__ imgs, int n_imgs, int64_t n_blo
     }
 }
 
+template <int C>
+__global__ __launch_bounds__(THREADS)
+void undistort_kernel(const UndImg* __restrict__ imgs, int n_imgs, int n_blocks) {
+    // XCD-aware order: hardware dispatches block b to XCD b % 8; give every XCD a
+    // contiguous run of logical blocks so adjacent rows share its L2.
+    const int b = blockIdx.x;
+    const int q = n_blocks / 8, r = n_blocks % 8;
+    const int xcd = b % 8, idx = b / 8;
+    const int lb = xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+    int lo = 0, hi = n_imgs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (imgs[mid].blk0 <= lb) lo = mid; else hi = mid - 1;
+    }
+    const UndImg& im = imgs[lo];
+    const int rb = lb - (int)im.blk0;
+    const int Y = rb / im.bpr;
+    const int x0 = (rb - Y * im.bpr) * PX_PER_BLOCK + (int)threadIdx.x * PX_PER_THREAD;
+    if (Y >= im.H || x0 >= im.W) return;
+    if (im.src_words) undistort_px<C, true>(im, Y, x0);
+    else undistort_px<C, false>(im, Y, x0);
+}
+
+// initUndistortRectifyMap's running sum _x += ir[0] (from _x = ir[2]) and the
+// row-invariant x = _x * (1/_w), x*x: one thread per image, sequential as in the
+// reference loop (a few microseconds per image).
+__global__ void xcol_kernel(const UndImg* __restrict__ imgs, int n) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n) return;
+    const UndImg& im = imgs[g];
+    double* __restrict__ xc = const_cast<double*>(reinterpret_cast<const double*>(im.xcol));
+    double xs = 0.0 + im.t2;
+    for (int j = 0; j < im.W; ++j, xs += im.t0) {
+        const double x = xs * im.w;
+        xc[2 * j] = x;
+        xc[2 * j + 1] = x * x;
+    }
+}
+
 thread_local float g_last_ms = -1.f;
+
+// per-thread device scratch (descriptors + column tables) and timing events,
+// grown on demand and kept across calls
+struct Scratch {
+    int dev = -1;
+    void* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    void* get(int device, size_t bytes) {
+        if (dev != device) { p = nullptr; cap = 0; e0 = e1 = nullptr; dev = device; }   // other device: leak-free enough
+        if (bytes > cap) {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+            if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+            cap = bytes;
+        }
+        if (!e0 && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) return nullptr;
+        return p;
+    }
+};
+thread_local Scratch g_scratch;
+
+bool is_gfx950(int device) {
+    static std::atomic<int> state[64];   // 0 unknown, 1 yes, 2 no
+    if (device < 0 || device >= 64) return false;
+    int v = state[device].load();
+    if (v == 0) {
+        hipDeviceProp_t prop;
+        v = (hipGetDeviceProperties(&prop, device) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) ? 1 : 2;
+        state[device].store(v);
+    }
+    return v == 1;
+}
 
 struct Bufs {
     std::vector<void*> ptrs;
@@ -273,28 +337,25 @@ int sfmx_undistort_images(const sfmx_undistort_image* images, int32_t n_images, 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { set_last_error("no HIP device visible"); return SFMX_EDEVICE; }
     if (device < 0 || device >= ndev) { set_last_error("device index out of range"); return SFMX_EINVAL; }
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-        set_last_error("sfmx kernels are built for gfx950 only");
-        return SFMX_EDEVICE;
-    }
+    if (!is_gfx950(device)) { set_last_error("sfmx kernels are built for gfx950 only"); return SFMX_EDEVICE; }
     int prev = -1;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(device);
     const hipStream_t st = (hipStream_t)stream;
     int rc = SFMX_OK;
     {
-        Bufs b;
+        Bufs b;   // host-mode staging only
         std::vector<UndImg> h(n_images);
         int64_t ncol = 0;
         int cnt_c[5] = {0, 0, 0, 0, 0}, first_c[5] = {0, 0, 0, 0, 0};
         int64_t blk_c[5] = {0, 0, 0, 0, 0};
         std::vector<uint8_t*> staged_dst(n_images);
         for (int n = 0; n < n_images; ++n) ncol += images[n].width;
-        std::vector<double2> xcol(ncol);
-        auto* dcol = static_cast<double2*>(b.alloc(sizeof(double2) * ncol));
-        auto* dimg = static_cast<UndImg*>(b.alloc(sizeof(UndImg) * n_images));
-        if (!dcol || !dimg) { rc = SFMX_ENOMEM; goto done; }
+        const size_t img_bytes = (sizeof(UndImg) * n_images + 255) & ~(size_t)255;
+        auto* scratch = static_cast<uint8_t*>(g_scratch.get(device, img_bytes + sizeof(double2) * ncol));
+        auto* dimg = reinterpret_cast<UndImg*>(scratch);
+        auto* dcol = reinterpret_cast<double2*>(scratch + img_bytes);
+        if (!scratch) { rc = SFMX_ENOMEM; goto done; }
         {
             int64_t co = 0;
             for (int n = 0; n < n_images; ++n) {
@@ -313,12 +374,8 @@ int sfmx_undistort_images(const sfmx_undistort_image* images, int32_t n_images, 
                 u.t4 = K0 * d; u.t8 = det * d;
                 u.fx = K0; u.fy = K4; u.u0 = K2; u.v0 = g.K[5];
                 u.k1 = g.dist[0]; u.k2 = g.dist[1]; u.p1 = g.dist[2]; u.p2 = g.dist[3]; u.k3 = g.dist[4];
-                const double w = 1. / u.t8;                            // 1/_w, the same for every row
-                double xs = 0.0 + t2;                                  // _x = i*ir[1] + ir[2]
-                for (int j = 0; j < g.width; ++j, xs += t0) {          // _x += ir[0]
-                    const double x = xs * w;
-                    xcol[co + j] = double2(x, x * x);
-                }
+                u.w = 1. / u.t8;                                       // 1/_w, the same for every row
+                u.t0 = t0; u.t2 = t2;                                  // column table: xcol_kernel
                 u.radial = (g.dist[2] == 0 && g.dist[3] == 0 && g.dist[4] == 0) ? 1 : 0;
                 u.xcol = dcol + co;
                 co += g.width;
@@ -330,7 +387,7 @@ int sfmx_undistort_images(const sfmx_undistort_image* images, int32_t n_images, 
             for (int n = 0; n < n_images; ++n) {
                 const sfmx_undistort_image& g = images[n];
                 const int64_t row = (int64_t)g.width * g.channels;
-                auto* s = static_cast<uint8_t*>(b.alloc(row * g.height));
+                auto* s = static_cast<uint8_t*>(b.alloc(row * g.height + 16));   // + overread pad
                 auto* o = static_cast<uint8_t*>(b.alloc(row * g.height));
                 if (!s || !o) { rc = SFMX_ENOMEM; goto done; }
                 UCHK(hipMemcpy2DAsync(s, row, g.src, g.src_pitch, row, g.height, hipMemcpyHostToDevice, st));
@@ -340,8 +397,19 @@ int sfmx_undistort_images(const sfmx_undistort_image* images, int32_t n_images, 
         }
         for (UndImg& u : h)
             u.dst_words = ((uintptr_t)u.dst % 4 == 0 && u.dst_pitch % 4 == 0) ? 1 : 0;
-        for (UndImg& u : h)
-            u.src_words = ((uintptr_t)u.src % 4 == 0 && u.src_pitch % 4 == 0 && u.W >= 2) ? 1 : 0;
+        for (UndImg& u : h) {
+            // dword tap loads read up to 8 bytes past the last row: allowed only when the
+            // allocation holding the image extends that far (host-staged copies are padded)
+            bool safe = false;
+            hipDeviceptr_t base = nullptr;
+            size_t range = 0;
+            if (hipMemGetAddressRange(&base, &range, (hipDeviceptr_t)u.src) == hipSuccess && base) {
+                const uintptr_t end = (uintptr_t)u.src + (uintptr_t)(u.H - 1) * u.src_pitch + (uintptr_t)u.W * u.C + 8;
+                safe = end <= (uintptr_t)base + range;
+            }
+            (void)hipGetLastError();
+            u.src_words = (safe && (uintptr_t)u.src % 4 == 0 && u.src_pitch % 4 == 0 && u.W >= 2) ? 1 : 0;
+        }
         for (int n = 0; n < n_images; ++n) staged_dst[n] = h[n].dst;
         // one launch per channel count (the kernel is specialised on it): images grouped by C
         std::stable_sort(h.begin(), h.end(), [](const UndImg& p, const UndImg& q) { return p.C < q.C; });
@@ -353,22 +421,20 @@ int sfmx_undistort_images(const sfmx_undistort_image* images, int32_t n_images, 
             u.blk0 = blk_c[u.C];
             blk_c[u.C] += (int64_t)u.bpr * u.H;
         }
-        UCHK(hipMemcpyAsync(dcol, xcol.data(), sizeof(double2) * ncol, hipMemcpyHostToDevice, st));
         UCHK(hipMemcpyAsync(dimg, h.data(), sizeof(UndImg) * n_images, hipMemcpyHostToDevice, st));
         {
-            hipEvent_t e0 = nullptr, e1 = nullptr;
-            UCHK(hipEventCreate(&e0));
-            UCHK(hipEventCreate(&e1));
+            hipEvent_t e0 = g_scratch.e0, e1 = g_scratch.e1;
             UCHK(hipEventRecord(e0, st));
+            xcol_kernel<<<(n_images + 63) / 64, 64, 0, st>>>(dimg, n_images);
             for (int c = 1; c <= 4; ++c) {
                 if (cnt_c[c] == 0) continue;
                 const int64_t nb = blk_c[c];
                 if (nb >= (int64_t)INT32_MAX) { set_last_error("images too large for one launch"); rc = SFMX_EINVAL; goto done; }
                 const UndImg* di = dimg + first_c[c];
-                if (c == 1) undistort_kernel<1><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], nb);
-                if (c == 2) undistort_kernel<2><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], nb);
-                if (c == 3) undistort_kernel<3><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], nb);
-                if (c == 4) undistort_kernel<4><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], nb);
+                if (c == 1) undistort_kernel<1><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], (int)nb);
+                if (c == 2) undistort_kernel<2><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], (int)nb);
+                if (c == 3) undistort_kernel<3><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], (int)nb);
+                if (c == 4) undistort_kernel<4><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], (int)nb);
                 UCHK(hipGetLastError());
             }
             UCHK(hipEventRecord(e1, st));
@@ -382,8 +448,6 @@ int sfmx_undistort_images(const sfmx_undistort_image* images, int32_t n_images, 
             float ms = -1.f;
             (void)hipEventElapsedTime(&ms, e0, e1);
             g_last_ms = ms;
-            (void)hipEventDestroy(e0);
-            (void)hipEventDestroy(e1);
         }
     done:;
     }
