@@ -162,7 +162,7 @@ __global__ void prep_hamming_fp4_kernel(const uint8_t* __restrict__ src, int row
 
 // ---------------------------------------------------------------------------
 // SIFT 2-NN, int8 MFMA.
-template <int QT, int WAVES, int MINW, int STAGE, bool MFMA_FIRST, int PROBE = 0>
+template <int QT, int WAVES, int MINW, int STAGE, bool MFMA_FIRST, int PROBE = 0, int PIPE = 0>
 __global__ __launch_bounds__(WAVES * 64, MINW)
 void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
                       const ImgDev* __restrict__ imgs, const int8_t* __restrict__ desc8,
@@ -243,6 +243,46 @@ void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restri
         const int buf = s & 1;
         if (s + 1 < nstages) stage(s + 1, buf ^ 1);
         const char* base = lds + buf * BUF_BYTES;
+        if constexpr (PIPE > 0) {
+            // Software pipeline over the stage's (tile, query-tile) steps: the MFMA chain
+            // of step k is issued first, the selection of step k-1 (independent of it)
+            // runs under it; sched_group_barrier interleaves 1 MFMA with PIPE VALU ops.
+            i32x16 prev = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+            i32x4 kvp[4];
+#pragma unroll
+            for (int t = 0; t < STAGE / 32; ++t) {
+                const int row = t * 32 + l32;
+                i32x4 a[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int slot = (2 * m + h) ^ ((row >> 1) & 7);
+                    a[m] = *reinterpret_cast<const i32x4*>(base + row * SIFT_DIM + 16 * slot);
+                }
+                i32x4 kv[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    kv[g] = *reinterpret_cast<const i32x4*>(base + DESC_BYTES + 4 * (t * 32 + 8 * g + 4 * h));
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+                    i32x16 acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bq[qt][m], acc, 0, 0, 0);
+                    if (t > 0 || qt > 0) {
+                        const int pq = qt > 0 ? qt - 1 : QT - 1;
+                        select(prev, qt > 0 ? kv : kvp, c1[pq], c2[pq]);
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);      // 1 MFMA
+                            __builtin_amdgcn_sched_group_barrier(0x002, PIPE, 0);   // PIPE VALU
+                        }
+                    }
+                    prev = acc;
+                }
+#pragma unroll
+                for (int g = 0; g < 4; ++g) kvp[g] = kv[g];
+            }
+            select(prev, kvp, c1[QT - 1], c2[QT - 1]);
+        } else
 #pragma unroll
         for (int t = 0; t < STAGE / 32; ++t) {
             const int row = t * 32 + l32;
@@ -799,10 +839,10 @@ int sift_variant() {
     }();
     return v;
 }
-int sift_block_queries(int v) { return v == 2 || v == 4 ? 256 : 512; }
+int sift_block_queries(int v) { return v == 2 || v == 4 || v == 23 ? 256 : 512; }
 
 #define SIFT_LAUNCH(QT, W, MINW, ST, MF, ...)                                                             \
-    sift_knn2_kernel<QT, W, MINW, ST, MF, ##__VA_ARGS__><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc, \
+    sift_knn2_kernel<QT, W, MINW, ST, MF __VA_OPT__(,) __VA_ARGS__><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc, \
                                                                      out_idx, out_dist, slow_list, slow_count, ratio)
 
 hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
@@ -820,6 +860,10 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
     case 11: SIFT_LAUNCH(2, 8, 2, 64, true); break;    // r01 default
     case 90: SIFT_LAUNCH(2, 8, 2, 64, true, 1); break;   // timing probe (wrong results): no selection
     case 95: SIFT_LAUNCH(4, 4, 2, 64, true, 1); break;   // timing probe (wrong results): no selection
+    case 20: SIFT_LAUNCH(4, 4, 2, 128, false, 0, 9); break;   // software-pipelined selection
+    case 21: SIFT_LAUNCH(2, 8, 2, 128, false, 0, 9); break;
+    case 22: SIFT_LAUNCH(4, 4, 2, 128, false, 0, 8); break;
+    case 23: SIFT_LAUNCH(2, 4, 4, 128, false, 0, 9); break;
     default: SIFT_LAUNCH(4, 4, 2, 128, false);   // measured best (r01 A/B: 9.57-9.67 ms vs 9.96-10.01 for QT=2 x 8 waves)
     }
     return hipGetLastError();

@@ -239,11 +239,14 @@ void undistort_kernel(const UndImg* __restrict__ imgs, int n_imgs, int n_blocks)
 __global__ void xcol_kernel(const UndImg* __restrict__ imgs, int n) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n) return;
-    const UndImg& im = imgs[g];
-    double* __restrict__ xc = const_cast<double*>(reinterpret_cast<const double*>(im.xcol));
-    double xs = 0.0 + im.t2;
-    for (int j = 0; j < im.W; ++j, xs += im.t0) {
-        const double x = xs * im.w;
+    // fields to registers first: the table aliases the descriptor buffer, so the
+    // compiler would otherwise reload them after every store
+    const int W = imgs[g].W;
+    const double t0 = imgs[g].t0, t2 = imgs[g].t2, w = imgs[g].w;
+    double* __restrict__ xc = const_cast<double*>(reinterpret_cast<const double*>(imgs[g].xcol));
+    double xs = 0.0 + t2;
+    for (int j = 0; j < W; ++j, xs += t0) {
+        const double x = xs * w;
         xc[2 * j] = x;
         xc[2 * j + 1] = x * x;
     }
