@@ -1,0 +1,62 @@
+/* SPDX-License-Identifier: MIT
+ *
+ * sfmx — feature extraction: the per-shot
+ *     featureDetector->detect(image, keypoints);
+ *     descriptorExtractor->compute(image, keypoints, descriptors);
+ * of SfM::extractFeatures (sfm/SfM.cpp:577-597) for the reference's SIFT
+ * setting cv::SIFT::create(featureLimit, 3, 0.09) (cli/PhotogrammetrieCli.cpp:354),
+ * i.e. OpenCV 4.5.1's SIFT::detectAndCompute on an 8-bit grayscale image
+ * (CameraShot::loadImage defaults to IMREAD_GRAYSCALE, CameraShot.h:149).
+ *
+ * The output feeds sfmx_matcher_set_images directly: descriptors are n x 128
+ * float rows with integer values 0..255 (OpenCV's saturate_cast<uchar>).
+ * Status codes and threading as in sfmx.h.
+ */
+#ifndef SFMX_FEATURES_H
+#define SFMX_FEATURES_H
+
+#include <stdint.h>
+#include "sfmx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* cv::KeyPoint, same layout (pt.x, pt.y, size, angle, response, octave, class_id). */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} sfmx_keypoint;
+
+/* cv::SIFT::create(nfeatures, nOctaveLayers, contrastThreshold, edgeThreshold, sigma). */
+typedef struct {
+    int32_t nfeatures;            /* featureLimit; 0 = keep all                      */
+    int32_t n_octave_layers;      /* 3                                               */
+    double contrast_threshold;    /* 0.09 in the reference (OpenCV default 0.04)     */
+    double edge_threshold;        /* 10                                              */
+    double sigma;                 /* 1.6                                             */
+} sfmx_sift_params;
+
+/* Fills OpenCV's defaults, with the reference's contrast threshold 0.09 and
+ * nfeatures = 0. */
+void sfmx_sift_default_params(sfmx_sift_params* p);
+
+/* SIFT detect + compute on one width x height 8-bit grayscale image (rows
+ * `pitch` bytes apart).  Writes min(n, capacity) keypoints and descriptor rows
+ * (128 floats each) and sets *n_keypoints = n; SFMX_ECAPACITY if n > capacity.
+ * inputs_on_device = 1: image, keypoints and descriptors are device pointers
+ * on `device` (the descriptors can go straight to the matcher); 0: host. */
+int sfmx_sift_detect_compute(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
+                             const sfmx_sift_params* params, int32_t inputs_on_device, int32_t device, void* stream,
+                             sfmx_keypoint* keypoints, float* descriptors, int32_t capacity, int32_t* n_keypoints);
+
+/* Device time (ms) of the last sfmx_sift_detect_compute call on this thread
+ * (all kernels, HIP events on its stream, host keypoint filtering excluded);
+ * -1 before any call. */
+float sfmx_sift_last_kernel_ms(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SFMX_FEATURES_H */

@@ -56,6 +56,8 @@ def _load():
     lib.orc_undistort.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     lib.orc_undistort_batch.argtypes = [C.POINTER(vp), C.POINTER(vp), i32p, i32p, i32p, C.POINTER(C.c_double),
                                         C.POINTER(C.c_double), C.c_int, C.c_int]
+    lib.orc_sift.argtypes = [vp, C.c_int, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
+                             vp, vp, C.c_int]
     lib.orc_first_sqrt_collision.restype = C.c_int64
     lib.orc_first_sqrt_collision.argtypes = [C.c_int64]
     return lib
@@ -196,6 +198,27 @@ def ba_observations(origin_offsets, origin_shot, origin_xy, n_shots):
     npose = lib.orc_ba_observations(_ptr(oo, C.c_int64), len(oo) - 1, _ptr(os_), oxy.ctypes.data_as(C.POINTER(C.c_double)),
                                     n_shots, _ptr(op), _ptr(oc), ox.ctypes.data_as(C.POINTER(C.c_double)), _ptr(sp))
     return op[:n], oc[:n], ox[:2 * n].reshape(-1, 2), sp[:npose]
+
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+                           ("octave", "<i4"), ("class_id", "<i4")])
+
+
+def sift(image: np.ndarray, nfeatures: int = 0, n_octave_layers: int = 3, contrast_threshold: float = 0.09,
+         edge_threshold: float = 10.0, sigma: float = 1.6, descriptors: bool = True):
+    """SIFT::detectAndCompute restated (oracle/sift_oracle.cpp) on an H x W uint8
+    grayscale image -> (keypoints (KEYPOINT_DTYPE), n x 128 float32 descriptors)."""
+    img = np.ascontiguousarray(image, np.uint8)
+    H, W = img.shape
+    cap = 4096
+    while True:
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 128), np.float32) if descriptors else None
+        n = lib.orc_sift(img.ctypes.data, W, H, W, nfeatures, n_octave_layers, contrast_threshold, edge_threshold, sigma,
+                         kps.ctypes.data, desc.ctypes.data if descriptors else None, cap)
+        if n <= cap:
+            return kps[:n], (desc[:n] if descriptors else None)
+        cap = n
 
 
 def _dist5(dist):

@@ -1,0 +1,739 @@
+// SPDX-License-Identifier: MIT
+// sfmx SIFT feature extraction for gfx950.
+//
+//   sfmx_sift_detect_compute   featureDetector->detect + descriptorExtractor->compute
+//                              of SfM::extractFeatures (sfm/SfM.cpp:577-597) with
+//                              cv::SIFT::create(featureLimit, 3, 0.09)
+//                              (cli/PhotogrammetrieCli.cpp:354): OpenCV 4.5.1's
+//                              SIFT::detectAndCompute, restated.
+//
+// Pipeline (one image, all on the device except the keypoint filter):
+//   up2_kernel          u8 -> float, 2x INTER_LINEAR (horizontal then vertical taps)
+//   blur_row/col        GaussianBlur: getGaussianKernel taps (host, double), row
+//                       filter in tap order then the symmetric column filter,
+//                       BORDER_REFLECT_101 -- base image and 5 layers per octave
+//   half_nn_kernel      INTER_NEAREST half of layer 3 -> next octave
+//   dog_kernel          DoG layers
+//   extrema_kernel      26-neighbour extrema above floor(0.5 c / 3 * 255)
+//   refine_kernel       adjustLocalExtrema (Cramer solve, <= 5 steps, contrast + edge)
+//   orient_kernel       one wave per refined point: 36-bin orientation histogram,
+//                       smoothing, 80 % peaks -> keypoints
+//   host                removeDuplicatedSorted order, retainBest(nfeatures), 2x rescale
+//   descriptor_kernel   one block per keypoint: 4x4x8 trilinear histogram,
+//                       0.2 clamp, 512 / norm, saturate_cast<uchar>
+// Float expressions follow oracle/sift_oracle.cpp operation for operation; the
+// file is built with -ffp-contract=off.  exp / sin / cos are the fixed float
+// formulas both sides share (sx_expf, sx_sincosf); histogram bins accumulate in
+// 2^-30 fixed point with 64-bit LDS atomics, which makes the sums independent
+// of the order the lanes add them.  Result: keypoints and descriptors
+// bit-identical to the oracle.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <atomic>
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/sfmx_features.h"
+#include "match_common.hpp"
+
+namespace sfmx {
+namespace sift {
+
+constexpr int IMG_BORDER = 5, MAX_INTERP = 5, ORI_BINS = 36, DD = 4, NB = 8;
+constexpr int HIST_LEN = (DD + 2) * (DD + 2) * (NB + 2);
+constexpr float ORI_SIG = 1.5f, ORI_RADIUS = 3 * ORI_SIG, ORI_PEAK = 0.8f, DESCR_SCL = 3.f, DESCR_MAG_THR = 0.2f,
+                INT_DESCR = 512.f, INIT_SIGMA = 0.5f;
+constexpr double FIX = 1073741824.0;   // 2^30
+
+struct Layer { float* p; int w, h; };
+struct Cand { int o, layer, r, c; };
+struct Refined { int o, layer, r, c; float x, y, size, response; int octave, _pad; };
+struct Kp { float x, y, size, angle, response; int32_t octave, class_id; };
+static_assert(sizeof(Kp) == sizeof(sfmx_keypoint), "cv::KeyPoint layout");
+
+__host__ __device__ inline int reflect101(int p, int n) {
+    if (n == 1) return 0;
+    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+    return p;
+}
+
+__device__ __forceinline__ int round_f(float v) { return (int)rintf(v); }
+__device__ __forceinline__ int round_d(double v) { return (int)rint(v); }
+
+__device__ float sx_expf(float x) {
+    if (!(x > -80.f)) return 0.f;
+    if (x > 88.f) x = 88.f;
+    const float k = rintf(x * 1.44269504088896341f);
+    const float r = (x - k * 0.693145751953125f) - k * 1.42860682030941723e-6f;
+    float p = 1.38888889e-3f;
+    p = p * r + 8.33333333e-3f;
+    p = p * r + 4.16666667e-2f;
+    p = p * r + 1.66666667e-1f;
+    p = p * r + 0.5f;
+    p = p * r + 1.0f;
+    p = p * r + 1.0f;
+    return ldexpf(p, (int)k);
+}
+
+__device__ void sx_sincosf(float a, float* s, float* c) {
+    const float q = rintf(a * 0.636619772367581343f);
+    const float r = (a - q * 1.5703125f) - q * 4.83826794897e-4f;
+    const float r2 = r * r;
+    float sp = -1.9515295891e-4f;
+    sp = sp * r2 + 8.3321608736e-3f;
+    sp = sp * r2 - 1.6666654611e-1f;
+    const float sr = r + r * (r2 * sp);
+    float cp = 2.443315711809948e-5f;
+    cp = cp * r2 - 1.388731625493765e-3f;
+    cp = cp * r2 + 4.166664568298827e-2f;
+    const float cr = (1.f - 0.5f * r2) + (r2 * r2) * cp;
+    switch (((int)q) & 3) {
+    case 0: *s = sr; *c = cr; break;
+    case 1: *s = cr; *c = -sr; break;
+    case 2: *s = -sr; *c = -cr; break;
+    default: *s = -cr; *c = sr; break;
+    }
+}
+
+__device__ float atan2_deg(float y, float x) {   // cv::fastAtan2
+    constexpr float R2D = (float)(180 / 3.14159265358979323846);
+    constexpr float P1 = 0.9997878412794807f * R2D, P3 = -0.3258083974640975f * R2D, P5 = 0.1555786518463281f * R2D,
+                    P7 = -0.04432655554792128f * R2D;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((P7 * c2 + P5) * c2 + P3) * c2 + P1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((P7 * c2 + P5) * c2 + P3) * c2 + P1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+__device__ __forceinline__ long long fixp(float v) { return (long long)(v * 1073741824.f); }
+
+// ------------------------------------------------------------------ pyramid
+__device__ __forceinline__ void lin_coef(int d, int ssize, int& s, float& f0, float& f1) {
+    float fx = (float)((d + 0.5) * 0.5 - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    if (sx >= ssize - 1) { fx = 0; sx = ssize - 1; }
+    s = sx;
+    f0 = 1.f - fx;
+    f1 = fx;
+}
+
+__global__ void up2_kernel(const uint8_t* __restrict__ img, int W, int H, int64_t pitch, float* __restrict__ dst) {
+    const int X = blockIdx.x * blockDim.x + threadIdx.x, Y = blockIdx.y;
+    if (X >= 2 * W) return;
+    int sy, sx;
+    float b0, b1, a0, a1;
+    lin_coef(Y, H, sy, b0, b1);
+    lin_coef(X, W, sx, a0, a1);
+    const int sy1 = min(sy + 1, H - 1), sx1 = min(sx + 1, W - 1);
+    const float h0 = (float)img[sy * pitch + sx] * a0 + (float)img[sy * pitch + sx1] * a1;
+    const float h1 = (float)img[sy1 * pitch + sx] * a0 + (float)img[sy1 * pitch + sx1] * a1;
+    dst[(int64_t)Y * (2 * W) + X] = h0 * b0 + h1 * b1;
+}
+
+__global__ void blur_row_kernel(const float* __restrict__ src, float* __restrict__ dst, int w, int h,
+                                const float* __restrict__ f, int n) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= w) return;
+    const int r = n / 2;
+    const float* row = src + (int64_t)y * w;
+    float s = f[0] * row[reflect101(x - r, w)];
+    for (int k = 1; k < n; ++k) s += f[k] * row[reflect101(x - r + k, w)];
+    dst[(int64_t)y * w + x] = s;
+}
+
+__global__ void blur_col_kernel(const float* __restrict__ src, float* __restrict__ dst, int w, int h,
+                                const float* __restrict__ f, int n) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= w) return;
+    const int r = n / 2;
+    float s = f[r] * src[(int64_t)y * w + x];
+    for (int k = 1; k <= r; ++k)
+        s += f[r + k] * (src[(int64_t)reflect101(y + k, h) * w + x] + src[(int64_t)reflect101(y - k, h) * w + x]);
+    dst[(int64_t)y * w + x] = s;
+}
+
+__global__ void half_nn_kernel(const float* __restrict__ src, int sw, int sh, float* __restrict__ dst, int dw, int dh,
+                               double ifx, double ify) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= dw) return;
+    const int sy = min((int)floor(y * ify), sh - 1), sx = min((int)floor(x * ifx), sw - 1);
+    dst[(int64_t)y * dw + x] = src[(int64_t)sy * sw + sx];
+}
+
+__global__ void dog_kernel(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ d, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) d[i] = b[i] - a[i];
+}
+
+// ------------------------------------------------------------------ detection
+__global__ void extrema_kernel(const float* __restrict__ prev, const float* __restrict__ img,
+                               const float* __restrict__ next, int w, int h, int threshold, int o, int layer,
+                               Cand* __restrict__ out, int* __restrict__ count, int cap) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x + IMG_BORDER, r = blockIdx.y + IMG_BORDER;
+    if (c >= w - IMG_BORDER || r >= h - IMG_BORDER) return;
+    const float val = img[(int64_t)r * w + c];
+    if (!(fabsf(val) > threshold)) return;
+    bool mx = val > 0, mn = val < 0;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+            const int64_t q = (int64_t)(r + dy) * w + c + dx;
+            const float a = img[q], b = prev[q], e = next[q];
+            mx = mx && val >= a && val >= b && val >= e;
+            mn = mn && val <= a && val <= b && val <= e;
+        }
+    if (!mx && !mn) return;
+    const int slot = atomicAdd(count, 1);
+    if (slot < cap) out[slot] = Cand{o, layer, r, c};
+}
+
+__device__ __forceinline__ float at(const Layer& L, int r, int c) { return L.p[(int64_t)r * L.w + c]; }
+
+// adjustLocalExtrema; dog[o * (L + 2) + i]
+__global__ void refine_kernel(const Cand* __restrict__ cands, const int* __restrict__ ncand_p, int cap,
+                              const Layer* __restrict__ dog, int L, float contrastThreshold, float edgeThreshold,
+                              float sigma, Refined* __restrict__ out, int* __restrict__ count, int out_cap) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= min(*ncand_p, cap)) return;
+    const Cand cd = cands[t];
+    const int octv = cd.o;
+    int layer = cd.layer, r = cd.r, c = cd.c;
+    const float img_scale = 1.f / 255, deriv_scale = img_scale * 0.5f, second_deriv_scale = img_scale,
+                cross_deriv_scale = img_scale * 0.25f;
+    float xi = 0, xr = 0, xc = 0, contr = 0;
+    int i = 0;
+    for (; i < MAX_INTERP; i++) {
+        const int idx = octv * (L + 2) + layer;
+        const Layer img = dog[idx], prev = dog[idx - 1], next = dog[idx + 1];
+        const float d0 = (at(img, r, c + 1) - at(img, r, c - 1)) * deriv_scale;
+        const float d1 = (at(img, r + 1, c) - at(img, r - 1, c)) * deriv_scale;
+        const float d2 = (at(next, r, c) - at(prev, r, c)) * deriv_scale;
+        const float v2 = at(img, r, c) * 2;
+        const float dxx = (at(img, r, c + 1) + at(img, r, c - 1) - v2) * second_deriv_scale;
+        const float dyy = (at(img, r + 1, c) + at(img, r - 1, c) - v2) * second_deriv_scale;
+        const float dss = (at(next, r, c) + at(prev, r, c) - v2) * second_deriv_scale;
+        const float dxy = (at(img, r + 1, c + 1) - at(img, r + 1, c - 1) - at(img, r - 1, c + 1) + at(img, r - 1, c - 1)) *
+                          cross_deriv_scale;
+        const float dxs = (at(next, r, c + 1) - at(next, r, c - 1) - at(prev, r, c + 1) + at(prev, r, c - 1)) *
+                          cross_deriv_scale;
+        const float dys = (at(next, r + 1, c) - at(next, r - 1, c) - at(prev, r + 1, c) + at(prev, r - 1, c)) *
+                          cross_deriv_scale;
+        const float a00 = dxx, a01 = dxy, a02 = dxs, a10 = dxy, a11 = dyy, a12 = dys, a20 = dxs, a21 = dys, a22 = dss;
+        float x0 = 0, x1 = 0, x2 = 0;
+        float det = a00 * (a11 * a22 - a21 * a12) - a01 * (a10 * a22 - a20 * a12) + a02 * (a10 * a21 - a20 * a11);
+        if (det != 0) {
+            det = 1 / det;
+            x0 = det * (d0 * (a11 * a22 - a12 * a21) - a01 * (d1 * a22 - a12 * d2) + a02 * (d1 * a21 - a11 * d2));
+            x1 = det * (a00 * (d1 * a22 - a12 * d2) - d0 * (a10 * a22 - a12 * a20) + a02 * (a10 * d2 - d1 * a20));
+            x2 = det * (a00 * (a11 * d2 - d1 * a21) - a01 * (a10 * d2 - d1 * a20) + d0 * (a10 * a21 - a11 * a20));
+        }
+        xi = -x2; xr = -x1; xc = -x0;
+        if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+        if (fabsf(xi) > (float)(INT_MAX / 3) || fabsf(xr) > (float)(INT_MAX / 3) || fabsf(xc) > (float)(INT_MAX / 3)) return;
+        c += round_f(xc);
+        r += round_f(xr);
+        layer += round_f(xi);
+        if (layer < 1 || layer > L || c < IMG_BORDER || c >= img.w - IMG_BORDER || r < IMG_BORDER || r >= img.h - IMG_BORDER)
+            return;
+    }
+    if (i >= MAX_INTERP) return;
+    const int idx = octv * (L + 2) + layer;
+    const Layer img = dog[idx], prev = dog[idx - 1], next = dog[idx + 1];
+    {
+        const float d0 = (at(img, r, c + 1) - at(img, r, c - 1)) * deriv_scale;
+        const float d1 = (at(img, r + 1, c) - at(img, r - 1, c)) * deriv_scale;
+        const float d2 = (at(next, r, c) - at(prev, r, c)) * deriv_scale;
+        float tt = 0;
+        tt += d0 * xc;
+        tt += d1 * xr;
+        tt += d2 * xi;
+        contr = at(img, r, c) * img_scale + tt * 0.5f;
+        if (fabsf(contr) * L < contrastThreshold) return;
+        const float v2 = at(img, r, c) * 2.f;
+        const float dxx = (at(img, r, c + 1) + at(img, r, c - 1) - v2) * second_deriv_scale;
+        const float dyy = (at(img, r + 1, c) + at(img, r - 1, c) - v2) * second_deriv_scale;
+        const float dxy = (at(img, r + 1, c + 1) - at(img, r + 1, c - 1) - at(img, r - 1, c + 1) + at(img, r - 1, c - 1)) *
+                          cross_deriv_scale;
+        const float tr = dxx + dyy;
+        const float det = dxx * dyy - dxy * dxy;
+        if (det <= 0 || tr * tr * edgeThreshold >= (edgeThreshold + 1) * (edgeThreshold + 1) * det) return;
+    }
+    Refined R;
+    R.o = octv; R.layer = layer; R.r = r; R.c = c;
+    R.x = (c + xc) * (1 << octv);
+    R.y = (r + xr) * (1 << octv);
+    R.octave = octv + (layer << 8) + (round_d((xi + 0.5) * 255) << 16);
+    R.size = sigma * sx_expf(((layer + xi) / L) * 0.693147180559945309f) * (1 << octv) * 2;
+    R.response = fabsf(contr);
+    R._pad = 0;
+    const int slot = atomicAdd(count, 1);
+    if (slot < out_cap) out[slot] = R;
+}
+
+// calcOrientationHist + peak emission; one wave per refined point
+__global__ __launch_bounds__(64)
+void orient_kernel(const Refined* __restrict__ refs, const int* __restrict__ nref_p, int cap,
+                   const Layer* __restrict__ gp, int L, Kp* __restrict__ out, int* __restrict__ count, int out_cap) {
+    __shared__ unsigned long long acc[ORI_BINS];
+    const int t = blockIdx.x;
+    if (t >= min(*nref_p, cap)) return;
+    const Refined R = refs[t];
+    const Layer img = gp[R.o * (L + 3) + R.layer];
+    const float scl_octv = R.size * 0.5f / (1 << R.o);
+    const int radius = round_f(ORI_RADIUS * scl_octv);
+    const float sigma = ORI_SIG * scl_octv;
+    const float expf_scale = -1.f / (2.f * sigma * sigma);
+    const int n = ORI_BINS;
+    for (int b = threadIdx.x; b < n; b += 64) acc[b] = 0;
+    __syncthreads();
+    const int side = 2 * radius + 1;
+    for (int q = threadIdx.x; q < side * side; q += 64) {
+        const int i = q / side - radius, j = q % side - radius;
+        const int y = R.r + i, x = R.c + j;
+        if (y <= 0 || y >= img.h - 1 || x <= 0 || x >= img.w - 1) continue;
+        const float dx = at(img, y, x + 1) - at(img, y, x - 1);
+        const float dy = at(img, y - 1, x) - at(img, y + 1, x);
+        const float w = sx_expf((i * i + j * j) * expf_scale);
+        const float ori = atan2_deg(dy, dx);
+        const float mag = sqrtf(dx * dx + dy * dy);
+        int bin = round_f((n / 360.f) * ori);
+        if (bin >= n) bin -= n;
+        if (bin < 0) bin += n;
+        atomicAdd(&acc[bin], (unsigned long long)fixp(w * mag));
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    float t_[ORI_BINS + 4];
+    float* temphist = t_ + 2;
+    float hist[ORI_BINS];
+    for (int b = 0; b < n; ++b) temphist[b] = (float)((double)(long long)acc[b] * (1.0 / FIX));
+    temphist[-1] = temphist[n - 1];
+    temphist[-2] = temphist[n - 2];
+    temphist[n] = temphist[0];
+    temphist[n + 1] = temphist[1];
+    for (int b = 0; b < n; b++)
+        hist[b] = (temphist[b - 2] + temphist[b + 2]) * (1.f / 16.f) + (temphist[b - 1] + temphist[b + 1]) * (4.f / 16.f) +
+                  temphist[b] * (6.f / 16.f);
+    float omax = hist[0];
+    for (int b = 1; b < n; b++) omax = fmaxf(omax, hist[b]);
+    const float mag_thr = omax * ORI_PEAK;
+    for (int j = 0; j < n; j++) {
+        const int l = j > 0 ? j - 1 : n - 1, r2 = j < n - 1 ? j + 1 : 0;
+        if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
+            float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
+            bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
+            Kp k;
+            k.x = R.x; k.y = R.y; k.size = R.size; k.response = R.response; k.octave = R.octave; k.class_id = -1;
+            k.angle = 360.f - (float)((360.f / n) * bin);
+            if (fabsf(k.angle - 360.f) < FLT_EPSILON) k.angle = 0.f;
+            const int slot = atomicAdd(count, 1);
+            if (slot < out_cap) out[slot] = k;
+        }
+    }
+}
+
+// calcSIFTDescriptor; one block per (final, rescaled) keypoint
+constexpr int DESC_THREADS = 256;
+__global__ __launch_bounds__(DESC_THREADS)
+void descriptor_kernel(const Kp* __restrict__ kps, int nkp, const Layer* __restrict__ gp, int L, int firstOctave,
+                       float* __restrict__ desc) {
+    __shared__ unsigned long long hist[HIST_LEN];
+    __shared__ float dst[DD * DD * NB];
+    const int q = blockIdx.x;
+    if (q >= nkp) return;
+    const Kp kp = kps[q];
+    int octave = kp.octave & 255;
+    const int layer = (kp.octave >> 8) & 255;
+    octave = octave < 128 ? octave : (-128 | octave);
+    const float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
+    const float size = kp.size * scale;
+    const float ptx = kp.x * scale, pty = kp.y * scale;
+    const Layer img = gp[(octave - firstOctave) * (L + 3) + layer];
+    float ori = 360.f - kp.angle;
+    if (fabsf(ori - 360.f) < FLT_EPSILON) ori = 0.f;
+    const float scl = size * 0.5f;
+    const int d = DD, n = NB;
+    const int ptX = round_f(ptx), ptY = round_f(pty);
+    float sin_t, cos_t;
+    sx_sincosf(ori * (float)(3.14159265358979323846 / 180), &sin_t, &cos_t);
+    const float bins_per_rad = n / 360.f;
+    const float exp_scale = -1.f / (d * d * 0.5f);
+    const float hist_width = DESCR_SCL * scl;
+    int radius = round_f(hist_width * 1.4142135623730951f * (d + 1) * 0.5f);
+    radius = min(radius, (int)sqrt(((double)img.w) * img.w + ((double)img.h) * img.h));
+    cos_t /= hist_width;
+    sin_t /= hist_width;
+    for (int b = threadIdx.x; b < HIST_LEN; b += DESC_THREADS) hist[b] = 0;
+    __syncthreads();
+    const int side = 2 * radius + 1;
+    for (int k = threadIdx.x; k < side * side; k += DESC_THREADS) {
+        const int i = k / side - radius, j = k % side - radius;
+        const float c_rot = j * cos_t - i * sin_t;
+        const float r_rot = j * sin_t + i * cos_t;
+        float rbin = r_rot + d / 2 - 0.5f;
+        float cbin = c_rot + d / 2 - 0.5f;
+        const int r = ptY + i, c = ptX + j;
+        if (!(rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < img.h - 1 && c > 0 && c < img.w - 1)) continue;
+        const float dx = at(img, r, c + 1) - at(img, r, c - 1);
+        const float dy = at(img, r - 1, c) - at(img, r + 1, c);
+        const float w = sx_expf((c_rot * c_rot + r_rot * r_rot) * exp_scale);
+        const float o = atan2_deg(dy, dx);
+        const float m = sqrtf(dx * dx + dy * dy);
+        float obin = (o - ori) * bins_per_rad;
+        const float mag = m * w;
+        const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
+        int o0 = (int)floorf(obin);
+        rbin -= r0;
+        cbin -= c0;
+        obin -= o0;
+        if (o0 < 0) o0 += n;
+        if (o0 >= n) o0 -= n;
+        const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+        const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+        const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+        const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+        const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+        const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+        const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+        const int idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
+        atomicAdd(&hist[idx], (unsigned long long)fixp(v_rco000));
+        atomicAdd(&hist[idx + 1], (unsigned long long)fixp(v_rco001));
+        atomicAdd(&hist[idx + (n + 2)], (unsigned long long)fixp(v_rco010));
+        atomicAdd(&hist[idx + (n + 3)], (unsigned long long)fixp(v_rco011));
+        atomicAdd(&hist[idx + (d + 2) * (n + 2)], (unsigned long long)fixp(v_rco100));
+        atomicAdd(&hist[idx + (d + 2) * (n + 2) + 1], (unsigned long long)fixp(v_rco101));
+        atomicAdd(&hist[idx + (d + 3) * (n + 2)], (unsigned long long)fixp(v_rco110));
+        atomicAdd(&hist[idx + (d + 3) * (n + 2) + 1], (unsigned long long)fixp(v_rco111));
+    }
+    __syncthreads();
+    if (threadIdx.x < d * d) {   // circular fold of each cell's orientation bins
+        const int i = threadIdx.x / d, j = threadIdx.x % d;
+        const int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
+        const long long h0 = (long long)hist[idx] + (long long)hist[idx + n];
+        const long long h1 = (long long)hist[idx + 1] + (long long)hist[idx + n + 1];
+        for (int k = 0; k < n; k++) {
+            const long long v = k == 0 ? h0 : (k == 1 ? h1 : (long long)hist[idx + k]);
+            dst[(i * d + j) * n + k] = (float)((double)v * (1.0 / FIX));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const int len = d * d * n;
+    float nrm2 = 0;
+    for (int k = 0; k < len; k++) nrm2 += dst[k] * dst[k];
+    const float thr = sqrtf(nrm2) * DESCR_MAG_THR;
+    nrm2 = 0;
+    for (int k = 0; k < len; k++) {
+        const float val = fminf(dst[k], thr);
+        dst[k] = val;
+        nrm2 += val * val;
+    }
+    nrm2 = INT_DESCR / fmaxf(sqrtf(nrm2), FLT_EPSILON);
+    float* out = desc + (int64_t)q * 128;
+    for (int k = 0; k < len; k++) out[k] = (float)min(max(round_f(dst[k] * nrm2), 0), 255);
+}
+
+// ------------------------------------------------------------------ host
+static int host_round(double v) { return (int)std::nearbyint(v); }
+
+std::vector<float> gauss_kernel(double sigma) {   // getGaussianKernel(cvRound(8 sigma + 1) | 1, sigma, CV_32F)
+    const int n = host_round(sigma * 4 * 2 + 1) | 1;
+    std::vector<float> cf(n);
+    const double scale2X = -0.5 / (sigma * sigma);
+    double sum = 0;
+    for (int i = 0; i < n; i++) {
+        const double x = i - (n - 1) * 0.5;
+        const double t = std::exp(scale2X * x * x);
+        cf[i] = (float)t;
+        sum += cf[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < n; i++) cf[i] = (float)(cf[i] * sum);
+    return cf;
+}
+
+static bool kp_less(const Kp& a, const Kp& b) {   // KeyPointsFilter::removeDuplicatedSorted's order
+    if (a.x != b.x) return a.x < b.x;
+    if (a.y != b.y) return a.y < b.y;
+    if (a.size != b.size) return a.size > b.size;
+    if (a.angle != b.angle) return a.angle < b.angle;
+    if (a.response != b.response) return a.response > b.response;
+    if (a.octave != b.octave) return a.octave > b.octave;
+    return a.class_id > b.class_id;
+}
+
+// removeDuplicatedSorted + retainBest + firstOctave = -1 rescale
+static void filter_keypoints(std::vector<Kp>& kps, int nfeatures) {
+    std::sort(kps.begin(), kps.end(), kp_less);
+    if (kps.size() > 1) {
+        size_t w = 0;
+        for (size_t j = 1; j < kps.size(); ++j) {
+            const Kp &a = kps[w], &b = kps[j];
+            if (a.x != b.x || a.y != b.y || a.size != b.size || a.angle != b.angle) kps[++w] = kps[j];
+        }
+        kps.resize(w + 1);
+    }
+    if (nfeatures > 0 && (int)kps.size() > nfeatures) {
+        std::vector<float> resp(kps.size());
+        for (size_t j = 0; j < kps.size(); ++j) resp[j] = kps[j].response;
+        std::nth_element(resp.begin(), resp.begin() + nfeatures - 1, resp.end(), std::greater<float>());
+        const float amb = resp[nfeatures - 1];
+        size_t w = 0;
+        for (size_t j = 0; j < kps.size(); ++j)
+            if (kps[j].response >= amb) kps[w++] = kps[j];
+        kps.resize(w);
+    }
+    for (Kp& q : kps) {
+        q.octave = (q.octave & ~255) | ((q.octave - 1) & 255);
+        q.x *= 0.5f;
+        q.y *= 0.5f;
+        q.size *= 0.5f;
+    }
+}
+
+thread_local float g_last_ms = -1.f;
+
+struct Arena {                 // per-thread device scratch, grown on demand
+    int dev = -1;
+    char* p = nullptr;
+    size_t cap = 0, used = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    bool reserve(int device, size_t bytes) {
+        if (dev != device) { p = nullptr; cap = 0; e0 = e1 = nullptr; dev = device; }
+        used = 0;
+        if (bytes > cap) {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+            if (hipMalloc(&p, bytes) != hipSuccess) return false;
+            cap = bytes;
+        }
+        if (!e0 && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) return false;
+        return true;
+    }
+    template <class T> T* take(size_t n) {
+        T* r = reinterpret_cast<T*>(p + used);
+        used += (sizeof(T) * n + 255) & ~(size_t)255;
+        return r;
+    }
+};
+thread_local Arena g_arena;
+
+bool is_gfx950(int device) {
+    static std::atomic<int> state[64];
+    if (device < 0 || device >= 64) return false;
+    int v = state[device].load();
+    if (v == 0) {
+        hipDeviceProp_t prop;
+        v = (hipGetDeviceProperties(&prop, device) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) ? 1 : 2;
+        state[device].store(v);
+    }
+    return v == 1;
+}
+
+}  // namespace sift
+}  // namespace sfmx
+
+using namespace sfmx;
+using namespace sfmx::sift;
+
+#define FCHK(expr) do { if ((expr) != hipSuccess) { rc = SFMX_EDEVICE; set_last_error("HIP error in " #expr); goto done; } } while (0)
+
+extern "C" {
+
+void sfmx_sift_default_params(sfmx_sift_params* p) {
+    if (!p) return;
+    p->nfeatures = 0;
+    p->n_octave_layers = 3;
+    p->contrast_threshold = 0.09;
+    p->edge_threshold = 10;
+    p->sigma = 1.6;
+}
+
+float sfmx_sift_last_kernel_ms(void) { return g_last_ms; }
+
+int sfmx_sift_detect_compute(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
+                             const sfmx_sift_params* params, int32_t inputs_on_device, int32_t device, void* stream,
+                             sfmx_keypoint* keypoints, float* descriptors, int32_t capacity, int32_t* n_keypoints) {
+    if (!image || !params || !n_keypoints || capacity < 0 || (capacity > 0 && !keypoints)) {
+        set_last_error("null argument");
+        return SFMX_EINVAL;
+    }
+    if (width < 1 || height < 1 || pitch < width || width > 16384 || height > 16384) {
+        set_last_error("image size must be 1..16384 with pitch >= width");
+        return SFMX_EINVAL;
+    }
+    const int L = params->n_octave_layers;
+    if (L < 1 || L > 16 || params->nfeatures < 0 || !(params->sigma > 0) || !(params->contrast_threshold >= 0) ||
+        !(params->edge_threshold > 0)) {
+        set_last_error("bad SIFT parameters");
+        return SFMX_EINVAL;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { set_last_error("no HIP device visible"); return SFMX_EDEVICE; }
+    if (device < 0 || device >= ndev) { set_last_error("device index out of range"); return SFMX_EINVAL; }
+    if (!is_gfx950(device)) { set_last_error("sfmx kernels are built for gfx950 only"); return SFMX_EDEVICE; }
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device);
+    const hipStream_t st = (hipStream_t)stream;
+    int rc = SFMX_OK;
+    {
+        const float sigma = (float)params->sigma;
+        const int BW = 2 * width, BH = 2 * height;
+        const int nOct = host_round(std::log((double)std::min(BW, BH)) / std::log(2.) - 2) + 1;
+        std::vector<double> sig(L + 3);
+        sig[0] = sigma;
+        const double k = std::pow(2., 1. / L);
+        for (int i = 1; i < L + 3; i++) {
+            const double sig_prev = std::pow(k, (double)(i - 1)) * sigma;
+            const double sig_total = sig_prev * k;
+            sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
+        }
+        const float sig_diff = std::sqrt(std::max(sigma * sigma - INIT_SIGMA * INIT_SIGMA * 4, 0.01f));
+        std::vector<std::vector<float>> kern(L + 3);
+        kern[0] = gauss_kernel(sig_diff);
+        for (int i = 1; i < L + 3; i++) kern[i] = gauss_kernel(sig[i]);
+        std::vector<int> ow(std::max(nOct, 1)), oh(std::max(nOct, 1));
+        size_t px = 0;
+        for (int o = 0; o < nOct; ++o) {
+            ow[o] = o == 0 ? BW : ow[o - 1] / 2;
+            oh[o] = o == 0 ? BH : oh[o - 1] / 2;
+            px += (size_t)ow[o] * oh[o];
+        }
+        const int CAND_CAP = 1 << 20, REF_CAP = 1 << 19, KP_CAP = 1 << 20;
+        size_t kbytes = 0;
+        for (auto& kk : kern) kbytes += (kk.size() * 4 + 255) & ~(size_t)255;
+        const size_t need = px * 4 * (size_t)(2 * L + 5) + (size_t)BW * BH * 4 + ((size_t)width * height + 256) +
+                            kbytes + sizeof(Cand) * CAND_CAP + sizeof(Refined) * REF_CAP + sizeof(Kp) * KP_CAP * 2 +
+                            (size_t)KP_CAP * 128 * 4 + 64 * 1024 + (size_t)nOct * (2 * L + 5) * sizeof(Layer) + 8192;
+        if (!g_arena.reserve(device, need)) { rc = SFMX_ENOMEM; set_last_error("device allocation failed"); goto done; }
+        {
+            Arena& A = g_arena;
+            std::vector<Layer> hgp((size_t)nOct * (L + 3)), hdog((size_t)nOct * (L + 2));
+            for (int o = 0; o < nOct; ++o) {
+                for (int i = 0; i < L + 3; ++i) hgp[o * (L + 3) + i] = Layer{A.take<float>((size_t)ow[o] * oh[o]), ow[o], oh[o]};
+                for (int i = 0; i < L + 2; ++i) hdog[o * (L + 2) + i] = Layer{A.take<float>((size_t)ow[o] * oh[o]), ow[o], oh[o]};
+            }
+            float* tmp = A.take<float>((size_t)BW * BH);
+            float* up = A.take<float>((size_t)BW * BH);
+            std::vector<float*> dk(L + 3);
+            for (int i = 0; i < L + 3; ++i) dk[i] = A.take<float>(kern[i].size());
+            Layer* dgp = A.take<Layer>(hgp.size());
+            Layer* ddog = A.take<Layer>(hdog.size());
+            Cand* cands = A.take<Cand>(CAND_CAP);
+            Refined* refs = A.take<Refined>(REF_CAP);
+            Kp* raw = A.take<Kp>(KP_CAP);
+            Kp* fin = A.take<Kp>(KP_CAP);
+            int* counters = A.take<int>(4);
+            const uint8_t* dimg = image;
+            int64_t dpitch = pitch;
+            if (!inputs_on_device) {
+                uint8_t* t = A.take<uint8_t>((size_t)width * height);
+                FCHK(hipMemcpy2DAsync(t, width, image, pitch, width, height, hipMemcpyHostToDevice, st));
+                dimg = t;
+                dpitch = width;
+            }
+            for (int i = 0; i < L + 3; ++i)
+                FCHK(hipMemcpyAsync(dk[i], kern[i].data(), kern[i].size() * 4, hipMemcpyHostToDevice, st));
+            FCHK(hipMemcpyAsync(dgp, hgp.data(), sizeof(Layer) * hgp.size(), hipMemcpyHostToDevice, st));
+            FCHK(hipMemcpyAsync(ddog, hdog.data(), sizeof(Layer) * hdog.size(), hipMemcpyHostToDevice, st));
+            FCHK(hipMemsetAsync(counters, 0, 16, st));
+            FCHK(hipEventRecord(A.e0, st));
+            auto blur = [&](const float* src, float* dst, int w, int h, int ki) {
+                const dim3 g((w + 255) / 256, h);
+                blur_row_kernel<<<g, 256, 0, st>>>(src, tmp, w, h, dk[ki], (int)kern[ki].size());
+                blur_col_kernel<<<g, 256, 0, st>>>(tmp, dst, w, h, dk[ki], (int)kern[ki].size());
+            };
+            up2_kernel<<<dim3((BW + 255) / 256, BH), 256, 0, st>>>(dimg, width, height, dpitch, up);
+            blur(up, hgp[0].p, BW, BH, 0);
+            for (int o = 0; o < nOct; ++o)
+                for (int i = 0; i < L + 3; ++i) {
+                    if (o == 0 && i == 0) continue;
+                    Layer& dst = hgp[o * (L + 3) + i];
+                    if (i == 0) {
+                        const Layer& src = hgp[(o - 1) * (L + 3) + L];
+                        half_nn_kernel<<<dim3((dst.w + 255) / 256, dst.h), 256, 0, st>>>(
+                            src.p, src.w, src.h, dst.p, dst.w, dst.h, 1. / ((double)dst.w / src.w), 1. / ((double)dst.h / src.h));
+                    } else {
+                        blur(hgp[o * (L + 3) + i - 1].p, dst.p, dst.w, dst.h, i);
+                    }
+                }
+            for (int o = 0; o < nOct; ++o)
+                for (int i = 0; i < L + 2; ++i) {
+                    const int64_t n = (int64_t)ow[o] * oh[o];
+                    dog_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(hgp[o * (L + 3) + i].p, hgp[o * (L + 3) + i + 1].p,
+                                                                           hdog[o * (L + 2) + i].p, n);
+                }
+            const int threshold = (int)std::floor(0.5 * params->contrast_threshold / L * 255);
+            for (int o = 0; o < nOct; ++o)
+                for (int i = 1; i <= L; ++i) {
+                    const int w = ow[o], h = oh[o];
+                    if (w <= 2 * IMG_BORDER || h <= 2 * IMG_BORDER) continue;
+                    extrema_kernel<<<dim3((w - 2 * IMG_BORDER + 255) / 256, h - 2 * IMG_BORDER), 256, 0, st>>>(
+                        hdog[o * (L + 2) + i - 1].p, hdog[o * (L + 2) + i].p, hdog[o * (L + 2) + i + 1].p, w, h, threshold, o,
+                        i, cands, counters + 0, CAND_CAP);
+                }
+            refine_kernel<<<CAND_CAP / 256, 256, 0, st>>>(cands, counters + 0, CAND_CAP, ddog, L,
+                                                          (float)params->contrast_threshold, (float)params->edge_threshold,
+                                                          sigma, refs, counters + 1, REF_CAP);
+            FCHK(hipGetLastError());
+            int hc[4] = {0, 0, 0, 0};
+            FCHK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
+            FCHK(hipStreamSynchronize(st));
+            if (hc[0] > CAND_CAP || hc[1] > REF_CAP) { set_last_error("too many extrema for the candidate buffers"); rc = SFMX_ECAPACITY; goto done; }
+            if (hc[1] > 0) orient_kernel<<<hc[1], 64, 0, st>>>(refs, counters + 1, REF_CAP, dgp, L, raw, counters + 2, KP_CAP);
+            FCHK(hipGetLastError());
+            FCHK(hipMemcpyAsync(hc, counters, 16, hipMemcpyDeviceToHost, st));
+            FCHK(hipStreamSynchronize(st));
+            if (hc[2] > KP_CAP) { set_last_error("too many keypoints for the buffer"); rc = SFMX_ECAPACITY; goto done; }
+            std::vector<Kp> kps(hc[2]);
+            if (hc[2]) FCHK(hipMemcpyAsync(kps.data(), raw, sizeof(Kp) * hc[2], hipMemcpyDeviceToHost, st));
+            FCHK(hipStreamSynchronize(st));
+            filter_keypoints(kps, params->nfeatures);
+            const int n = (int)kps.size();
+            *n_keypoints = n;
+            const int m = std::min(n, (int)capacity);
+            if (m > 0) {
+                FCHK(hipMemcpyAsync(fin, kps.data(), sizeof(Kp) * m, hipMemcpyHostToDevice, st));
+                if (descriptors) {
+                    float* dd = inputs_on_device ? descriptors : A.take<float>((size_t)m * 128);
+                    descriptor_kernel<<<m, DESC_THREADS, 0, st>>>(fin, m, dgp, L, -1, dd);
+                    FCHK(hipGetLastError());
+                    if (!inputs_on_device)
+                        FCHK(hipMemcpyAsync(descriptors, dd, sizeof(float) * 128 * m, hipMemcpyDeviceToHost, st));
+                }
+                if (inputs_on_device) FCHK(hipMemcpyAsync(keypoints, fin, sizeof(Kp) * m, hipMemcpyDeviceToDevice, st));
+                else std::memcpy(keypoints, kps.data(), sizeof(Kp) * m);
+            }
+            FCHK(hipEventRecord(A.e1, st));
+            FCHK(hipStreamSynchronize(st));
+            float ms = -1.f;
+            (void)hipEventElapsedTime(&ms, A.e0, A.e1);
+            g_last_ms = ms;
+            if (n > capacity) { set_last_error("keypoint capacity too small"); rc = SFMX_ECAPACITY; }
+        }
+    done:;
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return rc;
+}
+
+}  // extern "C"

@@ -11,6 +11,6 @@ from .matching import (  # noqa: F401
     GridFeatureMatchingStrategy, calculate_shot_matches, match_pairs, pairs_unordered, pairs_video, pairs_grid,
 )
 
-from . import homography, scene, mvs  # noqa: F401,E402
+from . import homography, scene, mvs, features  # noqa: F401,E402
 
 __version__ = "0.1.0"

@@ -1,0 +1,81 @@
+"""Feature extraction — host mirror over
+include/sfmx_features.h of the reference's
+
+    featureDetector = cv::SIFT::create(featureLimit, 3, 0.09)   (cli/PhotogrammetrieCli.cpp:354)
+    featureDetector->detect(image, keypoints); descriptorExtractor->compute(...)
+                                                                (sfm/SfM.cpp:577-597)
+
+``SIFT.create(...).detectAndCompute(image)`` runs csrc/sift_features.hip on the
+GPU (OpenCV 4.5.1 SIFT semantics restated; see DESIGN.md for the documented
+deviations).  Descriptors are n x 128 float32 with integer values, ready for
+``sfmx.BFMatcher``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import lib, check
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+                           ("octave", "<i4"), ("class_id", "<i4")])   # cv::KeyPoint
+
+
+class sfmx_sift_params(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("n_octave_layers", C.c_int32), ("contrast_threshold", C.c_double),
+                ("edge_threshold", C.c_double), ("sigma", C.c_double)]
+
+
+class SIFT:
+    """cv::SIFT::create(nfeatures, nOctaveLayers, contrastThreshold, edgeThreshold, sigma);
+    the reference passes (featureLimit, 3, 0.09)."""
+
+    def __init__(self, nfeatures: int = 0, nOctaveLayers: int = 3, contrastThreshold: float = 0.09,
+                 edgeThreshold: float = 10.0, sigma: float = 1.6, device: int = 0):
+        self.params = sfmx_sift_params(int(nfeatures), int(nOctaveLayers), float(contrastThreshold),
+                                       float(edgeThreshold), float(sigma))
+        self.device = device
+
+    @classmethod
+    def create(cls, nfeatures: int = 0, nOctaveLayers: int = 3, contrastThreshold: float = 0.09,
+               edgeThreshold: float = 10.0, sigma: float = 1.6, device: int = 0) -> "SIFT":
+        return cls(nfeatures, nOctaveLayers, contrastThreshold, edgeThreshold, sigma, device)
+
+    def detectAndCompute(self, image: np.ndarray, capacity: int = 1 << 16, stream: int = 0):
+        """H x W uint8 grayscale -> (keypoints (KEYPOINT_DTYPE), n x 128 float32 descriptors)."""
+        img = np.ascontiguousarray(image, np.uint8)
+        if img.ndim != 2:
+            raise ValueError("grayscale H x W uint8 image expected (CameraShot::loadImage default)")
+        n = C.c_int32(0)
+        while True:
+            kps = np.zeros(capacity, KEYPOINT_DTYPE)
+            desc = np.zeros((capacity, 128), np.float32)
+            rc = lib.sfmx_sift_detect_compute(img.ctypes.data, img.shape[1], img.shape[0], img.strides[0],
+                                              C.byref(self.params), 0, self.device, stream or None, kps.ctypes.data,
+                                              desc.ctypes.data, capacity, C.byref(n))
+            if rc == -4 and n.value > capacity:
+                capacity = n.value
+                continue
+            check(rc, "sfmx_sift_detect_compute")
+            return kps[:n.value], desc[:n.value]
+
+    def detect(self, image):
+        return self.detectAndCompute(image)[0]
+
+    def detectAndCompute_device(self, image_t, keypoints_t, descriptors_t, stream: int = 0) -> int:
+        """Resident torch tensors: image (H x W uint8), keypoints (cap x 7 int32 view of
+        KEYPOINT_DTYPE rows), descriptors (cap x 128 float32) -> keypoint count."""
+        n = C.c_int32(0)
+        cap = int(keypoints_t.shape[0])
+        check(lib.sfmx_sift_detect_compute(image_t.data_ptr(), image_t.shape[1], image_t.shape[0], image_t.stride(0),
+                                           C.byref(self.params), 1, self.device, stream or None, keypoints_t.data_ptr(),
+                                           descriptors_t.data_ptr(), cap, C.byref(n)), "sfmx_sift_detect_compute")
+        return n.value
+
+
+def last_kernel_ms() -> float:
+    return float(lib.sfmx_sift_last_kernel_ms())
+
+
+__all__ = ["SIFT", "KEYPOINT_DTYPE", "last_kernel_ms"]

@@ -1,0 +1,60 @@
+"""SIFT extraction on the GPU: sfmx_sift_detect_compute
+(csrc/sift_features.hip) bit-identical to the restatement in
+oracle/sift_oracle.cpp -- keypoints (all seven cv::KeyPoint fields) and
+descriptors -- through the C ABI, host and device modes."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+import sift_cases
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(img, **kw):
+    import sfmx
+    k, d = sfmx.features.SIFT.create(**kw).detectAndCompute(img)
+    ok = {"nfeatures": kw.get("nfeatures", 0), "contrast_threshold": kw.get("contrastThreshold", 0.09)}
+    ek, ed = oracle.sift(img, **ok)
+    assert len(k) == len(ek), (len(k), len(ek))
+    assert k.tobytes() == ek.tobytes()
+    assert np.array_equal(d, ed)
+    return k
+
+
+@pytest.mark.parametrize("shape,seed", [((120, 160), 1), ((97, 131), 2), ((64, 300), 3), ((240, 320), 4)])
+def test_bit_exact_reference_setting(shape, seed):
+    _check(sift_cases.blob_image(*shape, n_blobs=80, seed=seed))
+
+
+def test_bit_exact_many_points_and_limit():
+    img = sift_cases.blob_image(300, 400, n_blobs=300, seed=7)
+    k = _check(img, contrastThreshold=0.04)
+    assert len(k) > 50
+    _check(img, contrastThreshold=0.04, nfeatures=len(k) // 3)
+
+
+def test_tiny_and_flat_images():
+    import sfmx
+    for img in [np.full((40, 40), 128, np.uint8), np.zeros((8, 9), np.uint8), sift_cases.blob_image(23, 17, seed=1)]:
+        k, d = sfmx.features.SIFT.create().detectAndCompute(img)
+        ek, ed = oracle.sift(img)
+        assert k.tobytes() == ek.tobytes() and np.array_equal(d, ed)
+
+
+def test_device_mode_feeds_the_matcher():
+    import torch
+    import sfmx
+    img = sift_cases.blob_image(200, 260, n_blobs=150, seed=9)
+    dev = torch.device("cuda:0")
+    ti = torch.from_numpy(img).to(dev)
+    kt = torch.zeros((4096, 7), dtype=torch.int32, device=dev)
+    dt = torch.zeros((4096, 128), dtype=torch.float32, device=dev)
+    s = sfmx.features.SIFT.create(contrastThreshold=0.04)
+    n = s.detectAndCompute_device(ti, kt, dt)
+    torch.cuda.synchronize()
+    ek, ed = oracle.sift(img, contrast_threshold=0.04)
+    assert n == len(ek)
+    assert kt[:n].cpu().numpy().tobytes() == ek.tobytes()
+    assert np.array_equal(dt[:n].cpu().numpy(), ed)
+    assert sfmx.features.last_kernel_ms() > 0
