@@ -64,6 +64,7 @@ def parse():
     ap.add_argument("--no-homography", action="store_true", help="skip the homography RANSAC leg (SURVEY §8 f1)")
     ap.add_argument("--no-f4", action="store_true", help="skip the 3D-2D correspondence leg (SURVEY §8 f4)")
     ap.add_argument("--no-mvs", action="store_true", help="skip the openMVS export leg (SURVEY §8 f2)")
+    ap.add_argument("--no-features", action="store_true", help="skip the SIFT extraction leg (SURVEY §8 f3)")
     ap.add_argument("--only-ba", action="store_true", help="run only the bundle-adjustment leg (tuning)")
     ap.add_argument("--ba-cams", type=int, default=200)
     ap.add_argument("--ba-points", type=int, default=200_000)
@@ -101,6 +102,7 @@ def main():
         c3 = bench_match("c3", args, rank, world, local)
     ba_res = None if args.no_ba else bench_ba(args, rank, world, local)
     mvs_res = None if args.no_mvs else bench_mvs(args, rank, world, local)
+    feat_res = None if args.no_features else bench_features(args, rank, world, local)
     if rank == 0:
         line = {k: v for k, v in primary.items() if not k.startswith("_")}
         if orb is not None:
@@ -110,6 +112,8 @@ def main():
         line["ba"] = ba_res
         if mvs_res is not None:
             line["mvs"] = mvs_res
+        if feat_res is not None:
+            line["features"] = feat_res
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
@@ -556,6 +560,95 @@ def bench_mvs(args, rank, world, local):
                                "kind": "port", "sample": f"{n_s} of the shots, oracle/mvs_oracle.cpp (cv::undistort "
                                                         f"restated, OpenMP over images), {dt:.2f} s"}
         res["bit_exact_vs_oracle"] = bool(all(np.array_equal(dsts[i].cpu().numpy(), ho[i]) for i in range(n_s)))
+    return res
+
+
+FEAT_SHOTS, FEAT_H, FEAT_W, FEAT_LIMIT = 50, 1080, 1920, 8192
+
+
+def _sift_pyramid_bytes(h, w, layers=3):
+    """Algorithmic HBM bytes of one image's scale space (the dominant traffic):
+    u8 -> float 2x (4 B/px written), base blur (8 B/px), per octave `layers + 2`
+    blurred layers each reading its source and writing layer + DoG (12 B/px),
+    the extrema scan reading each DoG layer once (4 B/px x (layers + 2)), and the
+    nearest-neighbour halving (8 B/px of the next octave)."""
+    bw, bh = 2 * w, 2 * h
+    n_oct = int(round(np.log(min(bw, bh)) / np.log(2) - 2)) + 1
+    total, ow, oh = 12.0 * bw * bh, bw, bh
+    for o in range(n_oct):
+        px = ow * oh
+        total += px * (12.0 * (layers + 2) + 4.0 * (layers + 2)) + (8.0 * px if o > 0 else 0.0)
+        ow, oh = ow // 2, oh // 2
+    return total
+
+
+def bench_features(args, rank, world, local):
+    """SURVEY §8 row f3, SfM::extractFeatures (SfM.cpp:577-597) with the reference's
+    cv::SIFT::create(featureLimit, 3, 0.09) (PhotogrammetrieCli.cpp:354), featureLimit
+    8192 as config 2: 50 synthetic 1920x1080 grayscale photos resident in HBM,
+    shots sharded across ranks (strong scaling), keypoints + descriptors left in
+    HBM for the matcher.  Unit: images/s.  Roofline: the scale-space pipeline is
+    HBM-bound; achieved = algorithmic pyramid bytes / device time."""
+    import torch
+    import torch.distributed as dist
+    from sfmx import features, synth
+    dev = f"cuda:{local}"
+    mine = list(range(rank, FEAT_SHOTS, world))
+    host = {i: synth.gray_photo(FEAT_H, FEAT_W, seed=1000 + i) for i in mine[:2]}
+    base = [host.get(i) for i in mine[:2]]
+    imgs = []
+    for j, i in enumerate(mine):   # two distinct photos, shifted copies for the rest (same statistics)
+        b = base[j % len(base)]
+        imgs.append(torch.from_numpy(np.ascontiguousarray(np.roll(b, 37 * j, axis=1))).to(dev))
+    sift = features.SIFT.create(FEAT_LIMIT, 3, 0.09, device=local)
+    kt = torch.zeros((1 << 15, 7), dtype=torch.int32, device=dev)
+    dt = torch.zeros((1 << 15, 128), dtype=torch.float32, device=dev)
+    counts = [sift.detectAndCompute_device(t, kt, dt) for t in imgs[:2]]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    steps = max(args.steps // 5, 2)
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        for t in imgs:
+            counts.append(sift.detectAndCompute_device(t, kt, dt))
+            kms.append(features.last_kernel_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    k_ms = float(np.mean(kms))
+    pyr = _sift_pyramid_bytes(FEAT_H, FEAT_W)
+    achieved = pyr / (k_ms * 1e-3) / 1e9
+    res = {"metric": "images/s featurised (SIFT detect + compute, SfM::extractFeatures)",
+           "value": FEAT_SHOTS * steps / el, "unit": "images/s", "ms_per_image": el / (steps * len(imgs)) * 1e3,
+           "kernel_ms_per_image": k_ms, "keypoints_per_image": float(np.mean(counts)), "scaling": "strong",
+           "n_gpus": world, "dtype": "f32",
+           "config": {"workload": f"{FEAT_SHOTS} x {FEAT_W}x{FEAT_H} u8 grayscale, cv::SIFT::create({FEAT_LIMIT}, 3, 0.09)",
+                      "parallelism": f"shot-sharded x{world}"},
+           "data": "synthetic photos (sfmx.synth.gray_photo: shaded background + Gaussian blobs + noise)",
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "SIFT pipeline (blur_tile_n_kernel dominant)",
+                        "algorithmic": f"{pyr / 1e6:.0f} MB scale-space traffic per image (bench._sift_pyramid_bytes)"}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+        sample = [imgs[j % len(imgs)].cpu().numpy() for j in range(min(threads, 16))]
+        t = time.perf_counter()
+        cnt, ok, od = oracle.sift_batch(sample, nfeatures=FEAT_LIMIT, nthreads=threads)
+        dt_cpu = time.perf_counter() - t
+        res["cpu_baseline"] = {"value": len(sample) / dt_cpu, "unit": "images/s", "cores": threads, "kind": "port",
+                               "sample": f"{len(sample)} of the photos, oracle/sift_oracle.cpp (SIFT restated, OpenMP "
+                                         f"over images as SfM.cpp:582), {dt_cpu:.1f} s"}
+        n0 = sift.detectAndCompute_device(imgs[0], kt, dt)
+        torch.cuda.synchronize()
+        res["bit_exact_vs_oracle"] = bool(n0 == cnt[0] and kt[:n0].cpu().numpy().tobytes() == ok[0, :n0].tobytes()
+                                          and np.array_equal(dt[:n0].cpu().numpy(), od[0, :n0]))
     return res
 
 

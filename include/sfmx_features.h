@@ -51,7 +51,8 @@ int sfmx_sift_detect_compute(const uint8_t* image, int32_t width, int32_t height
                              sfmx_keypoint* keypoints, float* descriptors, int32_t capacity, int32_t* n_keypoints);
 
 /* Device time (ms) of the last sfmx_sift_detect_compute call on this thread
- * (all kernels, HIP events on its stream, host keypoint filtering excluded);
+ * (HIP events on its stream around all kernels; includes the host keypoint
+ * filter between the detection and descriptor kernels);
  * -1 before any call. */
 float sfmx_sift_last_kernel_ms(void);
 

@@ -58,6 +58,8 @@ def _load():
                                         C.POINTER(C.c_double), C.c_int, C.c_int]
     lib.orc_sift.argtypes = [vp, C.c_int, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
                              vp, vp, C.c_int]
+    lib.orc_sift_batch.argtypes = [C.POINTER(vp), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
+                                   C.c_double, vp, vp, C.c_int, i32p, C.c_int]
     lib.orc_first_sqrt_collision.restype = C.c_int64
     lib.orc_first_sqrt_collision.argtypes = [C.c_int64]
     return lib
@@ -219,6 +221,21 @@ def sift(image: np.ndarray, nfeatures: int = 0, n_octave_layers: int = 3, contra
         if n <= cap:
             return kps[:n], (desc[:n] if descriptors else None)
         cap = n
+
+
+def sift_batch(images, nfeatures=0, contrast_threshold=0.09, cap=16384, nthreads=0):
+    """sift() over equally sized images, OpenMP over images -> (counts, keypoints
+    (n_images x cap), descriptors (n_images x cap x 128))."""
+    n = len(images)
+    H, W = images[0].shape
+    imgs = [np.ascontiguousarray(a, np.uint8) for a in images]
+    ptrs = (C.c_void_p * n)(*[a.ctypes.data for a in imgs])
+    kps = np.zeros((n, cap), KEYPOINT_DTYPE)
+    desc = np.zeros((n, cap, 128), np.float32)
+    cnt = np.zeros(n, np.int32)
+    lib.orc_sift_batch(ptrs, n, W, H, nfeatures, 3, contrast_threshold, 10.0, 1.6, kps.ctypes.data, desc.ctypes.data,
+                       cap, _ptr(cnt), nthreads or os.cpu_count())
+    return cnt, kps, desc
 
 
 def _dist5(dist):

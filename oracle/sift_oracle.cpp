@@ -509,3 +509,18 @@ int orc_sift(const uint8_t* image, int W, int H, int64_t pitch, int nfeatures, i
 }
 
 }  // extern "C"
+
+extern "C" {
+// orc_sift over a batch of equally sized images, OpenMP over images (as the
+// reference's omp loop over shots, SfM.cpp:582); `cap` keypoint / descriptor
+// rows per image, counts in n_out.
+void orc_sift_batch(const uint8_t* const* images, int n_images, int W, int H, int nfeatures, int L,
+                    double contrastThreshold, double edgeThreshold, double sigma, void* kps_out, float* desc_out,
+                    int cap, int* n_out, int nthreads) {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int i = 0; i < n_images; ++i)
+        n_out[i] = orc_sift(images[i], W, H, W, nfeatures, L, contrastThreshold, edgeThreshold, sigma,
+                            static_cast<char*>(kps_out) + (size_t)i * cap * 28,
+                            desc_out ? desc_out + (size_t)i * cap * 128 : nullptr, cap);
+}
+}  // extern "C"

@@ -168,6 +168,108 @@ __global__ void blur_col_kernel(const float* __restrict__ src, float* __restrict
     dst[(int64_t)y * w + x] = s;
 }
 
+// Fused separable blur on a TX x TY output tile: the reflected source halo is
+// staged in LDS once, the row filter runs into LDS (taps in order, as
+// blur_row_kernel), then the symmetric column filter (as blur_col_kernel) --
+// the same operations on the same values, so the result equals the two-pass
+// kernels bit for bit.  With `dog` set it also writes the DoG layer
+// dst - src at each pixel (src is the previous pyramid layer).
+constexpr int TX = 64, TY = 32, RMAX = 16;
+__global__ __launch_bounds__(256)
+void blur_tile_kernel(const float* __restrict__ src, float* __restrict__ dst, float* __restrict__ dog, int w, int h,
+                      const float* __restrict__ fk, int n) {
+    __shared__ float in[(TY + 2 * RMAX) * (TX + 2 * RMAX)];
+    __shared__ float rowf[(TY + 2 * RMAX) * TX];
+    __shared__ float f[2 * RMAX + 1];
+    const int r = n / 2;
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    const int IW = TX + 2 * r, IH = TY + 2 * r;
+    if (threadIdx.x < n) f[threadIdx.x] = fk[threadIdx.x];
+    for (int q = threadIdx.x; q < IW * IH; q += 256) {
+        const int iy = q / IW, ix = q % IW;
+        const int sy = reflect101(y0 - r + iy, h), sx = reflect101(x0 - r + ix, w);
+        in[iy * IW + ix] = src[(int64_t)sy * w + sx];
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < IH * TX; q += 256) {
+        const int iy = q / TX, x = q % TX;
+        const float* row = in + iy * IW + x;
+        float s = f[0] * row[0];
+        for (int k = 1; k < n; ++k) s += f[k] * row[k];
+        rowf[iy * TX + x] = s;
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < TY * TX; q += 256) {
+        const int ty = q / TX, x = q % TX;
+        const int gx = x0 + x, gy = y0 + ty;
+        if (gx >= w || gy >= h) continue;
+        const float* col = rowf + (ty + r) * TX + x;
+        float s = f[r] * col[0];
+        for (int k = 1; k <= r; ++k) s += f[r + k] * (col[k * TX] + col[-k * TX]);
+        dst[(int64_t)gy * w + gx] = s;
+        if (dog) dog[(int64_t)gy * w + gx] = s - in[(ty + r) * IW + x + r];
+    }
+}
+
+// blur_tile_kernel specialised on the tap count N (the reference setting uses
+// N = 11, 13, 17, 21, 27) with 4 outputs per thread in both passes: the row
+// pass slides an (N + 3)-value window through registers, the column pass a
+// (2r + 4)-value one, giving 4 independent chains per thread.  Every output is
+// still the same sequence of float operations as blur_row/col_kernel.
+template <int N>
+__global__ __launch_bounds__(256)
+void blur_tile_n_kernel(const float* __restrict__ src, float* __restrict__ dst, float* __restrict__ dog, int w, int h,
+                        const float* __restrict__ fk) {
+    constexpr int R = N / 2, IW = TX + 2 * R, IH = TY + 2 * R;
+    __shared__ float in[IH * IW];
+    __shared__ float rowf[IH * TX];
+    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    float f[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) f[k] = fk[k];
+    for (int q = threadIdx.x; q < IW * IH; q += 256) {
+        const int iy = q / IW, ix = q % IW;
+        const int sy = reflect101(y0 - R + iy, h), sx = reflect101(x0 - R + ix, w);
+        in[iy * IW + ix] = src[(int64_t)sy * w + sx];
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < IH * (TX / 4); q += 256) {   // row pass: 4 consecutive x per thread
+        const int iy = q / (TX / 4), x = (q % (TX / 4)) * 4;
+        const float* row = in + iy * IW + x;
+        float v[N + 3];
+#pragma unroll
+        for (int t = 0; t < N + 3; ++t) v[t] = row[t];
+        float s[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[j] = f[0] * v[j];
+#pragma unroll
+        for (int k = 1; k < N; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[j] += f[k] * v[j + k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rowf[iy * TX + x + j] = s[j];
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < (TY / 4) * TX; q += 256) {   // column pass: 4 consecutive y per thread
+        const int ty = (q / TX) * 4, x = q % TX;
+        const float* col = rowf + ty * TX + x;                  // rowf row ty holds source row ty - R
+        float c[2 * R + 4];
+#pragma unroll
+        for (int t = 0; t < 2 * R + 4; ++t) c[t] = col[t * TX];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int gx = x0 + x, gy = y0 + ty + j;
+            float a = f[R] * c[j + R];
+#pragma unroll
+            for (int k = 1; k <= R; ++k) a += f[R + k] * (c[j + R + k] + c[j + R - k]);
+            if (gx < w && gy < h) {
+                dst[(int64_t)gy * w + gx] = a;
+                if (dog) dog[(int64_t)gy * w + gx] = a - in[(ty + j + R) * IW + x + R];
+            }
+        }
+    }
+}
+
 __global__ void half_nn_kernel(const float* __restrict__ src, int sw, int sh, float* __restrict__ dst, int dw, int dh,
                                double ifx, double ify) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
@@ -611,7 +713,12 @@ int sfmx_sift_detect_compute(const uint8_t* image, int32_t width, int32_t height
         std::vector<std::vector<float>> kern(L + 3);
         kern[0] = gauss_kernel(sig_diff);
         for (int i = 1; i < L + 3; i++) kern[i] = gauss_kernel(sig[i]);
-        std::vector<int> ow(std::max(nOct, 1)), oh(std::max(nOct, 1));
+        if (nOct < 1) {   // 1-pixel-high or -wide image: no octave, no keypoints (as OpenCV)
+            *n_keypoints = 0;
+            if (prev >= 0) (void)hipSetDevice(prev);
+            return SFMX_OK;
+        }
+        std::vector<int> ow(nOct), oh(nOct);
         size_t px = 0;
         for (int o = 0; o < nOct; ++o) {
             ow[o] = o == 0 ? BW : ow[o - 1] / 2;
@@ -657,13 +764,29 @@ int sfmx_sift_detect_compute(const uint8_t* image, int32_t width, int32_t height
             FCHK(hipMemcpyAsync(ddog, hdog.data(), sizeof(Layer) * hdog.size(), hipMemcpyHostToDevice, st));
             FCHK(hipMemsetAsync(counters, 0, 16, st));
             FCHK(hipEventRecord(A.e0, st));
-            auto blur = [&](const float* src, float* dst, int w, int h, int ki) {
-                const dim3 g((w + 255) / 256, h);
-                blur_row_kernel<<<g, 256, 0, st>>>(src, tmp, w, h, dk[ki], (int)kern[ki].size());
-                blur_col_kernel<<<g, 256, 0, st>>>(tmp, dst, w, h, dk[ki], (int)kern[ki].size());
+            // blur (+ the DoG of the new layer against its source layer when `dg` is set)
+            auto blur = [&](const float* src, float* dst, float* dg, int w, int h, int ki) {
+                const int n = (int)kern[ki].size();
+                const dim3 tg((w + TX - 1) / TX, (h + TY - 1) / TY);
+                if (n == 11) blur_tile_n_kernel<11><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki]);
+                else if (n == 13) blur_tile_n_kernel<13><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki]);
+                else if (n == 17) blur_tile_n_kernel<17><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki]);
+                else if (n == 21) blur_tile_n_kernel<21><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki]);
+                else if (n == 27) blur_tile_n_kernel<27><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki]);
+                else if (n / 2 <= RMAX) {
+                    blur_tile_kernel<<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki], n);
+                } else {
+                    const dim3 g((w + 255) / 256, h);
+                    blur_row_kernel<<<g, 256, 0, st>>>(src, tmp, w, h, dk[ki], n);
+                    blur_col_kernel<<<g, 256, 0, st>>>(tmp, dst, w, h, dk[ki], n);
+                    if (dg) {
+                        const int64_t m = (int64_t)w * h;
+                        dog_kernel<<<(unsigned)((m + 255) / 256), 256, 0, st>>>(src, dst, dg, m);
+                    }
+                }
             };
             up2_kernel<<<dim3((BW + 255) / 256, BH), 256, 0, st>>>(dimg, width, height, dpitch, up);
-            blur(up, hgp[0].p, BW, BH, 0);
+            blur(up, hgp[0].p, nullptr, BW, BH, 0);
             for (int o = 0; o < nOct; ++o)
                 for (int i = 0; i < L + 3; ++i) {
                     if (o == 0 && i == 0) continue;
@@ -673,14 +796,8 @@ int sfmx_sift_detect_compute(const uint8_t* image, int32_t width, int32_t height
                         half_nn_kernel<<<dim3((dst.w + 255) / 256, dst.h), 256, 0, st>>>(
                             src.p, src.w, src.h, dst.p, dst.w, dst.h, 1. / ((double)dst.w / src.w), 1. / ((double)dst.h / src.h));
                     } else {
-                        blur(hgp[o * (L + 3) + i - 1].p, dst.p, dst.w, dst.h, i);
+                        blur(hgp[o * (L + 3) + i - 1].p, dst.p, hdog[o * (L + 2) + i - 1].p, dst.w, dst.h, i);
                     }
-                }
-            for (int o = 0; o < nOct; ++o)
-                for (int i = 0; i < L + 2; ++i) {
-                    const int64_t n = (int64_t)ow[o] * oh[o];
-                    dog_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(hgp[o * (L + 3) + i].p, hgp[o * (L + 3) + i + 1].p,
-                                                                           hdog[o * (L + 2) + i].p, n);
                 }
             const int threshold = (int)std::floor(0.5 * params->contrast_threshold / L * 255);
             for (int o = 0; o < nOct; ++o)

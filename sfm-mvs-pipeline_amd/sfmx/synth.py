@@ -199,3 +199,25 @@ def point_cloud_origins(src: list, kps: list, min_views: int = 2):
     off[1:] = np.cumsum(cnt[keep])
     xy = np.array([kps[int(i)][int(r)] for _, i, r in recs], np.float64).reshape(-1, 2)
     return off, recs[:, 1].astype(np.int32), xy
+
+
+def gray_photo(height: int, width: int, seed: int = 0, density: float = 1 / 400) -> np.ndarray:
+    """Synthetic 8-bit grayscale "photo" for the SIFT extraction row (SURVEY.md
+    §8 f3): a smooth shaded background plus many small Gaussian blobs of random
+    scale (1.2-6 px) and contrast, plus sensor noise -- enough structure for the
+    reference's contrast threshold 0.09 to keep thousands of keypoints."""
+    r = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:height, 0:width].astype(np.float32)
+    img = 110 + 40 * np.sin(xx / 23.0 + r.uniform(0, 6)) * np.cos(yy / 17.0)
+    n = int(height * width * density)
+    cy, cx = r.uniform(0, height, n), r.uniform(0, width, n)
+    s = r.uniform(1.2, 6.0, n)
+    a = r.uniform(-90, 90, n)
+    for i in range(n):
+        y0, y1 = int(max(cy[i] - 3 * s[i], 0)), int(min(cy[i] + 3 * s[i] + 1, height))
+        x0, x1 = int(max(cx[i] - 3 * s[i], 0)), int(min(cx[i] + 3 * s[i] + 1, width))
+        if y1 <= y0 or x1 <= x0:
+            continue
+        img[y0:y1, x0:x1] += a[i] * np.exp(-((xx[y0:y1, x0:x1] - cx[i]) ** 2 + (yy[y0:y1, x0:x1] - cy[i]) ** 2)
+                                           / (2 * s[i] ** 2))
+    return np.clip(np.rint(img + r.normal(0, 3, img.shape)), 0, 255).astype(np.uint8)

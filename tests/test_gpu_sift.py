@@ -34,9 +34,20 @@ def test_bit_exact_many_points_and_limit():
     _check(img, contrastThreshold=0.04, nfeatures=len(k) // 3)
 
 
+def test_large_sigma_uses_the_two_pass_blur():
+    """sigma 3.2: the top layers' kernels exceed the fused tile's radius (16) and
+    take the row/column/DoG kernels; both paths must agree with the oracle."""
+    import sfmx
+    img = sift_cases.blob_image(180, 220, n_blobs=120, seed=12)
+    k, d = sfmx.features.SIFT.create(contrastThreshold=0.04, sigma=3.2).detectAndCompute(img)
+    ek, ed = oracle.sift(img, contrast_threshold=0.04, sigma=3.2)
+    assert len(ek) > 0 and k.tobytes() == ek.tobytes() and np.array_equal(d, ed)
+
+
 def test_tiny_and_flat_images():
     import sfmx
-    for img in [np.full((40, 40), 128, np.uint8), np.zeros((8, 9), np.uint8), sift_cases.blob_image(23, 17, seed=1)]:
+    for img in [np.full((40, 40), 128, np.uint8), np.zeros((8, 9), np.uint8), sift_cases.blob_image(23, 17, seed=1),
+                np.full((1, 50), 9, np.uint8), np.full((30, 1), 9, np.uint8)]:
         k, d = sfmx.features.SIFT.create().detectAndCompute(img)
         ek, ed = oracle.sift(img)
         assert k.tobytes() == ek.tobytes() and np.array_equal(d, ed)
