@@ -77,11 +77,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the N-rank path on a one-GPU box (tests only, never a bench
+    # result): every rank on cuda:0, collectives over gloo instead of RCCL.
+    rehearse = os.environ.get("SFMX_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group(backend="gloo")
+        else:
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
 
     import sfmx
     from sfmx import synth, shard
@@ -424,7 +432,8 @@ def bench_ba(args, rank, world, local):
     local_prob = shard_ba_problem(prob, rank, world) if world > 1 else dict(prob, point_range=(0, args.ba_points))
     local_prob.pop("point_range")
     opts = ba.default_options(device=local)
-    ctx = ba.BAContext(ba.BAProblem(**local_prob), opts, allreduce=torch_allreduce() if world > 1 else None)
+    ctx = ba.BAContext(ba.BAProblem(**local_prob), opts, allreduce=torch_allreduce(cpu_staging=os.environ.get("SFMX_BENCH_REHEARSE") == "1")
+                         if world > 1 else None)
     ctx.run(max_iterations=1)                 # warm-up (code objects, allocations)
     ctx.reset()
     if world > 1:
