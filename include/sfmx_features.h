@@ -50,7 +50,30 @@ int sfmx_sift_detect_compute(const uint8_t* image, int32_t width, int32_t height
                              const sfmx_sift_params* params, int32_t inputs_on_device, int32_t device, void* stream,
                              sfmx_keypoint* keypoints, float* descriptors, int32_t capacity, int32_t* n_keypoints);
 
+/* One 8-bit grayscale image (rows `pitch` bytes apart). */
+typedef struct {
+    const uint8_t* data;
+    int32_t width, height;
+    int64_t pitch;
+} sfmx_gray_image;
+
+/* SfM::extractFeatures over all shots (sfm/SfM.cpp:577-597, an OpenMP loop
+ * over shots in the reference): sfmx_sift_detect_compute on each image, with
+ * n_streams host workers (1..16), each on its own non-blocking HIP stream with
+ * its own scratch, so that the images' small-octave launches and host steps
+ * overlap on the GPU.  Per image i: keypoints[i], descriptors[i] (may be NULL
+ * as a whole: detect only), capacities[i], n_keypoints[i], status[i] (may be
+ * NULL) as for the single-image call.  Results are identical to calling
+ * sfmx_sift_detect_compute image by image.  Returns SFMX_OK or the code of the
+ * first failing image (sfmx_last_error names it).  One batch call at a time
+ * per process. */
+int sfmx_sift_detect_compute_batch(const sfmx_gray_image* images, int32_t n_images, const sfmx_sift_params* params,
+                                   int32_t inputs_on_device, int32_t device, int32_t n_streams,
+                                   sfmx_keypoint* const* keypoints, float* const* descriptors,
+                                   const int32_t* capacities, int32_t* n_keypoints, int32_t* status);
+
 /* Device time (ms) of the last sfmx_sift_detect_compute call on this thread
+ * (after a batch call: the mean per image of the workers' device times)
  * (HIP events on its stream around all kernels; includes the host keypoint
  * filter between the detection and descriptor kernels);
  * -1 before any call. */

@@ -35,6 +35,10 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sfmx_features.h"
@@ -671,9 +675,16 @@ void sfmx_sift_default_params(sfmx_sift_params* p) {
 
 float sfmx_sift_last_kernel_ms(void) { return g_last_ms; }
 
-int sfmx_sift_detect_compute(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
-                             const sfmx_sift_params* params, int32_t inputs_on_device, int32_t device, void* stream,
-                             sfmx_keypoint* keypoints, float* descriptors, int32_t capacity, int32_t* n_keypoints) {
+}  // extern "C"
+
+namespace {
+
+// One image through the whole pipeline on `stream`, scratch from `arena`;
+// *last_ms = device time of the kernels (HIP events on the stream).
+int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
+                        const sfmx_sift_params* params, int32_t inputs_on_device, int32_t device, void* stream,
+                        sfmx_keypoint* keypoints, float* descriptors, int32_t capacity, int32_t* n_keypoints,
+                        Arena& arena, float* last_ms) {
     if (!image || !params || !n_keypoints || capacity < 0 || (capacity > 0 && !keypoints)) {
         set_last_error("null argument");
         return SFMX_EINVAL;
@@ -731,9 +742,9 @@ int sfmx_sift_detect_compute(const uint8_t* image, int32_t width, int32_t height
         const size_t need = px * 4 * (size_t)(2 * L + 5) + (size_t)BW * BH * 4 + ((size_t)width * height + 256) +
                             kbytes + sizeof(Cand) * CAND_CAP + sizeof(Refined) * REF_CAP + sizeof(Kp) * KP_CAP * 2 +
                             (size_t)KP_CAP * 128 * 4 + 64 * 1024 + (size_t)nOct * (2 * L + 5) * sizeof(Layer) + 8192;
-        if (!g_arena.reserve(device, need)) { rc = SFMX_ENOMEM; set_last_error("device allocation failed"); goto done; }
+        if (!arena.reserve(device, need)) { rc = SFMX_ENOMEM; set_last_error("device allocation failed"); goto done; }
         {
-            Arena& A = g_arena;
+            Arena& A = arena;
             std::vector<Layer> hgp((size_t)nOct * (L + 3)), hdog((size_t)nOct * (L + 2));
             for (int o = 0; o < nOct; ++o) {
                 for (int i = 0; i < L + 3; ++i) hgp[o * (L + 3) + i] = Layer{A.take<float>((size_t)ow[o] * oh[o]), ow[o], oh[o]};
@@ -844,12 +855,101 @@ int sfmx_sift_detect_compute(const uint8_t* image, int32_t width, int32_t height
             FCHK(hipStreamSynchronize(st));
             float ms = -1.f;
             (void)hipEventElapsedTime(&ms, A.e0, A.e1);
-            g_last_ms = ms;
+            *last_ms = ms;
             if (n > capacity) { set_last_error("keypoint capacity too small"); rc = SFMX_ECAPACITY; }
         }
     done:;
     }
     if (prev >= 0) (void)hipSetDevice(prev);
+    return rc;
+}
+
+// Batch workers: one host thread and one non-blocking HIP stream per slot,
+// each with its own scratch arena, kept for the life of the process.
+struct BatchSlot {
+    Arena arena;
+    hipStream_t stream = nullptr;
+    int device = -1;
+};
+std::mutex g_batch_mu;
+std::vector<std::unique_ptr<BatchSlot>> g_slots;
+
+}  // namespace
+
+extern "C" {
+
+int sfmx_sift_detect_compute(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
+                             const sfmx_sift_params* params, int32_t inputs_on_device, int32_t device, void* stream,
+                             sfmx_keypoint* keypoints, float* descriptors, int32_t capacity, int32_t* n_keypoints) {
+    return detect_compute_impl(image, width, height, pitch, params, inputs_on_device, device, stream, keypoints,
+                               descriptors, capacity, n_keypoints, g_arena, &g_last_ms);
+}
+
+int sfmx_sift_detect_compute_batch(const sfmx_gray_image* images, int32_t n_images, const sfmx_sift_params* params,
+                                   int32_t inputs_on_device, int32_t device, int32_t n_streams,
+                                   sfmx_keypoint* const* keypoints, float* const* descriptors,
+                                   const int32_t* capacities, int32_t* n_keypoints, int32_t* status) {
+    if (n_images < 0 || (n_images > 0 && (!images || !keypoints || !capacities || !n_keypoints)) || !params) {
+        set_last_error("null argument");
+        return SFMX_EINVAL;
+    }
+    if (n_streams < 1 || n_streams > 16) { set_last_error("n_streams must be 1..16"); return SFMX_EINVAL; }
+    if (n_images == 0) { g_last_ms = 0.f; return SFMX_OK; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { set_last_error("no HIP device visible"); return SFMX_EDEVICE; }
+    if (device < 0 || device >= ndev) { set_last_error("device index out of range"); return SFMX_EINVAL; }
+    std::lock_guard<std::mutex> lock(g_batch_mu);
+    const int ns = std::min<int>(n_streams, n_images);
+    while ((int)g_slots.size() < ns) g_slots.emplace_back(new BatchSlot());
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device);
+    for (int i = 0; i < ns; ++i) {
+        BatchSlot& sl = *g_slots[i];
+        if (sl.device != device) {
+            if (sl.stream) (void)hipStreamDestroy(sl.stream);
+            sl.stream = nullptr;
+            if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) {
+                if (prev >= 0) (void)hipSetDevice(prev);
+                set_last_error("hipStreamCreate failed");
+                return SFMX_EDEVICE;
+            }
+            sl.device = device;
+        }
+    }
+    std::atomic<int> next{0};
+    std::vector<int> rcs(n_images, SFMX_OK);
+    std::vector<float> kms(ns, 0.f);
+    std::vector<std::string> errs(n_images);
+    auto work = [&](int slot) {
+        (void)hipSetDevice(device);
+        BatchSlot& sl = *g_slots[slot];
+        for (int i; (i = next.fetch_add(1)) < n_images;) {
+            float ms = 0.f;
+            const sfmx_gray_image& im = images[i];
+            rcs[i] = detect_compute_impl(im.data, im.width, im.height, im.pitch, params, inputs_on_device, device,
+                                         sl.stream, keypoints[i], descriptors ? descriptors[i] : nullptr,
+                                         capacities[i], &n_keypoints[i], sl.arena, &ms);
+            if (rcs[i] != SFMX_OK) errs[i] = sfmx_last_error();
+            kms[slot] += ms;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < ns; ++i) th.emplace_back(work, i);
+    work(0);
+    for (auto& t : th) t.join();
+    if (prev >= 0) (void)hipSetDevice(prev);
+    float total = 0.f;
+    for (float k : kms) total += k;
+    g_last_ms = total / n_images;
+    int rc = SFMX_OK;
+    for (int i = 0; i < n_images; ++i) {
+        if (status) status[i] = rcs[i];
+        if (rcs[i] != SFMX_OK && rc == SFMX_OK) {   // first failing image decides the return code
+            rc = rcs[i];
+            set_last_error(("image " + std::to_string(i) + ": " + errs[i]).c_str());
+        }
+    }
     return rc;
 }
 

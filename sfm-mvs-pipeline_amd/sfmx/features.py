@@ -73,6 +73,34 @@ class SIFT:
                                            descriptors_t.data_ptr(), cap, C.byref(n)), "sfmx_sift_detect_compute")
         return n.value
 
+    def detectAndCompute_batch_device(self, images, keypoints, descriptors, n_streams: int = 4):
+        """SfM::extractFeatures over shots (SfM.cpp:577-597): lists of resident torch
+        tensors as for detectAndCompute_device, run by n_streams workers with one HIP
+        stream each (sfmx_sift_detect_compute_batch) -> list of keypoint counts.
+        Results equal the one-image call's."""
+        n = len(images)
+        if not (len(keypoints) == len(descriptors) == n):
+            raise ValueError("images, keypoints and descriptors must have the same length")
+        imgs = (sfmx_gray_image * max(n, 1))()
+        for i, t in enumerate(images):
+            if t.dim() != 2:
+                raise ValueError("grayscale H x W uint8 image expected (CameraShot::loadImage default)")
+            imgs[i] = sfmx_gray_image(t.data_ptr(), t.shape[1], t.shape[0], t.stride(0))
+        kp = (C.c_void_p * max(n, 1))(*[k.data_ptr() for k in keypoints])
+        dd = (C.c_void_p * max(n, 1))(*[d.data_ptr() for d in descriptors])
+        caps = np.array([k.shape[0] for k in keypoints] or [0], np.int32)
+        cnt = np.zeros(max(n, 1), np.int32)
+        st = np.zeros(max(n, 1), np.int32)
+        i32p = C.POINTER(C.c_int32)
+        check(lib.sfmx_sift_detect_compute_batch(imgs, n, C.byref(self.params), 1, self.device, int(n_streams), kp, dd,
+                                                 caps.ctypes.data_as(i32p), cnt.ctypes.data_as(i32p),
+                                                 st.ctypes.data_as(i32p)), "sfmx_sift_detect_compute_batch")
+        return [int(c) for c in cnt[:n]]
+
+
+class sfmx_gray_image(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("width", C.c_int32), ("height", C.c_int32), ("pitch", C.c_int64)]
+
 
 def last_kernel_ms() -> float:
     return float(lib.sfmx_sift_last_kernel_ms())

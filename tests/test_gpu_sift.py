@@ -69,3 +69,28 @@ def test_device_mode_feeds_the_matcher():
     assert kt[:n].cpu().numpy().tobytes() == ek.tobytes()
     assert np.array_equal(dt[:n].cpu().numpy(), ed)
     assert sfmx.features.last_kernel_ms() > 0
+
+
+def test_batch_streams_equal_oracle():
+    """sfmx_sift_detect_compute_batch (SfM::extractFeatures' loop over shots) with
+    3 worker streams over images of different sizes: every image bit-identical to
+    the oracle, twice (the workers' arenas are reused)."""
+    import torch
+    import sfmx
+    imgs = [sift_cases.blob_image(120 + 17 * i, 160 + 29 * i, n_blobs=60 + 20 * i, seed=20 + i) for i in range(7)]
+    imgs.append(np.full((40, 40), 128, np.uint8))
+    dev = torch.device("cuda:0")
+    ts = [torch.from_numpy(i).to(dev) for i in imgs]
+    kts = [torch.zeros((4096, 7), dtype=torch.int32, device=dev) for _ in imgs]
+    dts = [torch.zeros((4096, 128), dtype=torch.float32, device=dev) for _ in imgs]
+    s = sfmx.features.SIFT.create(contrastThreshold=0.04)
+    expect = [oracle.sift(i, contrast_threshold=0.04) for i in imgs]
+    for _ in range(2):
+        counts = s.detectAndCompute_batch_device(ts, kts, dts, n_streams=3)
+        torch.cuda.synchronize()
+        for n, kt, dt, (ek, ed) in zip(counts, kts, dts, expect):
+            assert n == len(ek)
+            assert kt[:n].cpu().numpy().tobytes() == ek.tobytes()
+            assert np.array_equal(dt[:n].cpu().numpy(), ed)
+    with pytest.raises(sfmx._lib.SfmxError):   # capacity too small for one image: its status decides the return code
+        s.detectAndCompute_batch_device(ts[:2], [kts[0], kts[1][:3]], [dts[0], dts[1][:3]], n_streams=2)
