@@ -147,7 +147,7 @@ def bench_match(kind, args, rank, world, local):
         dtype = "int8->int32 (exact; f32 in/out)"
         scaling = "weak" if kind == "sift" else "strong"
         data = "synthetic (seeded SIFT-like descriptors, 25% planted re-observations; no dataset)"
-        kernel = "sift_knn2_kernel"
+        kernel = "sift_screen_kernel + sift_knn2_kernel<GATHER> (two-pass ratio test, both passes)"
         algo = "256 ops (128 int8 MAC) per descriptor pair"
     else:
         n_desc, n_img = 16384, 200
@@ -399,25 +399,29 @@ def bench_3d2d(args, imgs, my_pairs, got, off, rank, world, local, stream):
     return res
 
 
-PMC_FILES = {"sift": ("r01_pmc_sift_qt4.json", "sift_knn2_kernel", 50), "orb": ("r01_pmc_orb.json", "orb_mfma_kernel", 200),
-             "c3": ("r01_pmc_sift_c3.json", "sift_knn2_kernel", 200)}
+PMC_FILES = {"sift": ("r01f_pmc_sift_2p.json", ("sift_screen_kernel", "sift_knn2_kernel"), 50),
+             "orb": ("r01_pmc_orb.json", ("orb_mfma_kernel",), 200),
+             "c3": ("r01_pmc_sift_c3.json", ("sift_screen_kernel", "sift_knn2_kernel"), 200)}
 
 
 def pmc_traffic(kind, n_img):
-    """HBM bytes per launch of the 2-NN kernel from the committed PMC pass of this
-    exact workload (tools/pmc_sift.sh -> profiles/): 2 x FETCH_SIZE (gfx950
-    counts half of a wide streaming read) + WRITE_SIZE, both in KiB.  None when
-    no pass of this workload/kernel is on file."""
-    fname, kname, n_ref = PMC_FILES[kind]
+    """HBM bytes per launch of the 2-NN kernels (SIFT: screen + pass 2, summed)
+    from the committed PMC pass of this exact workload (tools/pmc_sift.sh ->
+    profiles/): 2 x FETCH_SIZE (gfx950 counts half of a wide streaming read) +
+    WRITE_SIZE, both in KiB.  None when no pass of this workload is on file."""
+    fname, knames, n_ref = PMC_FILES[kind]
     path = os.path.join(REPO, "profiles", fname)
     if n_img != n_ref or not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
+    total, found = 0.0, set()
     for k, v in d.items():
-        if kname in k and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-            return (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0
-    return None
+        for kn in knames:
+            if kn in k and "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+                total += (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024.0
+                found.add(kn)
+    return total if found == set(knames) else None
 
 
 def bench_ba(args, rank, world, local):

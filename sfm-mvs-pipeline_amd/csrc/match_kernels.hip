@@ -75,6 +75,12 @@ __device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned c) { 
 // checked against host sqrtf by tests/test_gpu_match.py.
 __device__ __forceinline__ float sqrt_rn_int(int64_t s) { return (float)__builtin_sqrt((double)s); }
 
+// Pad-row key of the screening pass (C2 operand): 0xC0C0C0C0 + dot never reaches
+// KEY_VALID, real keys are >= -(2^21 + 2^20).
+constexpr int PAD_KEY = (int)0xC0C0C0C0;
+constexpr int KEY_VALID = -(1 << 29);
+static_assert(PAD_KEY < KEY_VALID - (1 << 22), "pad keys must never look valid");
+
 // Bijective XCD-contiguous remap: blocks b, b+8, ... share an XCD (observed
 // round-robin dispatch; speed only, never correctness).
 __device__ __forceinline__ int xcd_remap(int b, int nwg) {
@@ -87,7 +93,8 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // 32 threads per row (float4 each); pad rows are written as zeros.
 __global__ void prep_l2_kernel(const float* __restrict__ src, int rows, int cols, int rows_pad,
                                int8_t* __restrict__ dst, int32_t* __restrict__ norm,
-                               int32_t* __restrict__ keyc, int32_t* __restrict__ nonintegral) {
+                               int32_t* __restrict__ keyc, int32_t* __restrict__ keyc2,
+                               int32_t* __restrict__ nonintegral) {
     const int r = blockIdx.x * (blockDim.x >> 5) + (threadIdx.x >> 5);
     const int c4 = threadIdx.x & 31;   // 4 columns each
     if (r >= rows_pad) return;
@@ -113,6 +120,7 @@ __global__ void prep_l2_kernel(const float* __restrict__ src, int rows, int cols
     if (c4 == 0) {
         norm[r] = n2;
         keyc[r] = (r < rows) ? (-(n2 << 8) + 255 - (r & 255)) : INT_MIN;
+        keyc2[r] = (r < rows) ? -((n2 + 1) >> 1) : PAD_KEY;     // screening pass: -ceil(nb / 2)
     }
 }
 
@@ -162,13 +170,19 @@ __global__ void prep_hamming_fp4_kernel(const uint8_t* __restrict__ src, int row
 
 // ---------------------------------------------------------------------------
 // SIFT 2-NN, int8 MFMA.
-template <int QT, int WAVES, int MINW, int STAGE, bool MFMA_FIRST, int PROBE = 0, int PIPE = 0>
+// GATHER (pass 2 of the two-pass path): `work` is the compacted list of
+// *work2_n items built by compact_work_kernel; an item's queries are entries
+// [q0, q0 + 512) of its pair's list of unresolved queries (qlist at the pair's
+// dense_base, qcount[pair] entries) written by sift_screen_kernel.
+template <int QT, int WAVES, int MINW, int STAGE, bool MFMA_FIRST, int PROBE = 0, int PIPE = 0, bool GATHER = false>
 __global__ __launch_bounds__(WAVES * 64, MINW)
 void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
                       const ImgDev* __restrict__ imgs, const int8_t* __restrict__ desc8,
                       const int32_t* __restrict__ norm, const int32_t* __restrict__ keyc,
                       int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
-                      int2* __restrict__ slow_list, int32_t* __restrict__ slow_count, double ratio) {
+                      int2* __restrict__ slow_list, int32_t* __restrict__ slow_count, double ratio,
+                      const int32_t* __restrict__ qlist = nullptr, const int32_t* __restrict__ qcount = nullptr,
+                      const int32_t* __restrict__ work2_n = nullptr) {
     constexpr int GLDS = STAGE * SIFT_DIM / (WAVES * 64 * 16);   // 16-B LDS-DMA pieces per thread per stage
     static_assert(GLDS * WAVES * 64 * 16 == STAGE * SIFT_DIM, "stage must split into whole 16-B pieces");
     static_assert(256 % STAGE == 0, "stages tile the 256-row key chunk");
@@ -178,17 +192,38 @@ void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restri
     __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
 
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
-    const WorkItem w = work[xcd_remap(blockIdx.x, gridDim.x)];
+    int nwork = gridDim.x;
+    if constexpr (GATHER) {           // compacted list of n2 work items; the grid is an upper bound
+        nwork = *work2_n;
+        if ((int)blockIdx.x >= nwork) return;
+    }
+    const WorkItem w = work[xcd_remap(blockIdx.x, nwork)];
     const PairDev P = pairs[w.pair];
     const ImgDev L = imgs[P.left], R = imgs[P.right];
     const int nq = L.rows, nt = R.rows;
     const int qbase = w.q0 + wid * (QT * 32);
+    int qrow[QT];                     // query row of this lane's column in each query tile (-1: none)
+    if constexpr (GATHER) {
+        const int cnt = qcount[w.pair];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const int e = qbase + qt * 32 + l32;
+            qrow[qt] = e < cnt ? qlist[P.dense_base + e] : -1;
+        }
+    } else {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            const int qi = qbase + qt * 32 + l32;
+            qrow[qt] = qi < nq ? qi : -1;
+        }
+    }
 
     // Query fragments (B operand): lane holds 16 bytes of k-block (2m + h).
     i32x4 bq[QT][4];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
-        const i32x4* src = reinterpret_cast<const i32x4*>(desc8 + (L.row0 + qbase + qt * 32 + l32) * SIFT_DIM);
+        const int lr = GATHER ? (qrow[qt] < 0 ? 0 : qrow[qt]) : qbase + qt * 32 + l32;   // rows < rows_pad
+        const i32x4* src = reinterpret_cast<const i32x4*>(desc8 + (L.row0 + lr) * SIFT_DIM);
 #pragma unroll
         for (int m = 0; m < 4; ++m) bq[qt][m] = src[2 * m + h];
     }
@@ -348,8 +383,8 @@ void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restri
     // Epilogue: lanes of half 0 own query column l32 of each tile.
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
-        const int qi = qbase + qt * 32 + l32;
-        if (h != 0 || qi >= nq) continue;
+        const int qi = qrow[qt];
+        if (h != 0 || qi < 0) continue;
         const int64_t o = P.dense_base + qi;
         if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }
         const int64_t na = norm[L.row0 + qi];
@@ -366,6 +401,173 @@ void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restri
         out_idx[o] = acc ? J1[qt] : -1;
         out_dist[o] = d1;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Two-pass ratio test, pass 1 (default SIFT path): sift_screen_kernel settles
+// every query whose ratio test certainly fails, with 0.5 VALU per element.
+//
+//   The C operand of train row j is  C2_j = -ceil(nb_j / 2),  so the MFMA leaves
+//       K = dot + C2_j = floor(X / 2),   X = 2 dot - nb_j,   s = na - X,
+//   i.e. s in [na - 2K - 1, na - 2K].  Each lane keeps, per query tile, the max of
+//   K over 8 disjoint row subsets (chain c takes accumulator rows 2c and 2c+1 of
+//   every tile: one v_max3 per two elements); with the partner half-wave that is
+//   16 subsets per query.  The best elements of two different subsets are two
+//   different rows, so with K1 >= K2 the two largest subset maxima,
+//       s1 >= na - 2 K1 - 1   and   s2 <= na - 2 K2.
+//   Lowe's test (double)sqrtf(s1) < (double)sqrtf(s2) * ratio is monotone
+//   (non-increasing in s1, non-decreasing in s2 for ratio >= 0; never true for
+//   ratio <= 0), so if it fails at (s1_lb, s2_ub) it fails for the true (s1, s2):
+//   the query is rejected, exactly as the exact path would reject it.  Every
+//   other query (accepted or undecided, fewer than 2 train rows, fewer than 2
+//   non-empty subsets) goes to its pair's list for pass 2, the exact kernel in
+//   GATHER mode.  Only accepted matches leave the matcher (sfmx_matcher_run /
+//   device_results), so a rejected query's distance is never observed.
+template <int QT, int WAVES, int MINW, int STAGE>
+__global__ __launch_bounds__(WAVES * 64, MINW)
+void sift_screen_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
+                        const ImgDev* __restrict__ imgs, const int8_t* __restrict__ desc8,
+                        const int32_t* __restrict__ norm, const int32_t* __restrict__ keyc2,
+                        int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
+                        int32_t* __restrict__ qlist, int32_t* __restrict__ qcount, double ratio) {
+    constexpr int GLDS = STAGE * SIFT_DIM / (WAVES * 64 * 16);
+    static_assert(GLDS * WAVES * 64 * 16 == STAGE * SIFT_DIM, "stage must split into whole 16-B pieces");
+    constexpr int DESC_BYTES = STAGE * SIFT_DIM;
+    constexpr int BUF_BYTES = DESC_BYTES + STAGE * 4;
+    __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
+
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
+    const WorkItem w = work[xcd_remap(blockIdx.x, gridDim.x)];
+    const PairDev P = pairs[w.pair];
+    const ImgDev L = imgs[P.left], R = imgs[P.right];
+    const int nq = L.rows, nt = R.rows;
+    const int qbase = w.q0 + wid * (QT * 32);
+
+    i32x4 bq[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const i32x4* src = reinterpret_cast<const i32x4*>(desc8 + (L.row0 + qbase + qt * 32 + l32) * SIFT_DIM);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) bq[qt][m] = src[2 * m + h];
+    }
+    int ch[QT][8];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) ch[qt][c] = INT_MIN;
+
+    const int nstages = (nt + STAGE - 1) / STAGE;
+    const int8_t* tbase = desc8 + R.row0 * SIFT_DIM;
+    const int32_t* kbase = keyc2 + R.row0;
+    auto stage = [&](int s, int buf) {
+        char* base = lds + buf * BUF_BYTES;
+#pragma unroll
+        for (int i = 0; i < GLDS; ++i) {
+            const int p = i * WAVES * 64 + threadIdx.x;
+            const int rr = p >> 3, slot = p & 7, c = slot ^ ((rr >> 1) & 7);
+            const int8_t* g = tbase + (int64_t)(s * STAGE + rr) * SIFT_DIM + 16 * c;
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)g,
+                                             (LDS_AS void*)(base + (i * WAVES + wid) * 1024), 16, 0, 0);
+        }
+        if (wid < STAGE / 64)
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(kbase + s * STAGE + wid * 64 + lane),
+                                             (LDS_AS void*)(base + DESC_BYTES + wid * 256), 4, 0, 0);
+    };
+
+    if (nstages > 0) stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < nstages; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nstages) stage(s + 1, buf ^ 1);
+        const char* base = lds + buf * BUF_BYTES;
+#pragma unroll
+        for (int t = 0; t < STAGE / 32; ++t) {
+            const int row = t * 32 + l32;
+            i32x4 a[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int slot = (2 * m + h) ^ ((row >> 1) & 7);
+                a[m] = *reinterpret_cast<const i32x4*>(base + row * SIFT_DIM + 16 * slot);
+            }
+            // C operand: keys of rows t*32 + 8g + 4h + (0..3) = accumulator rows 4g..4g+3.
+            i32x16 cv;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const i32x4 k4 = *reinterpret_cast<const i32x4*>(base + DESC_BYTES + 4 * (t * 32 + 8 * g + 4 * h));
+                cv[4 * g + 0] = k4[0]; cv[4 * g + 1] = k4[1]; cv[4 * g + 2] = k4[2]; cv[4 * g + 3] = k4[3];
+            }
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                i32x16 acc = cv;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bq[qt][m], acc, 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) ch[qt][c] = max(max(ch[qt][c], acc[2 * c]), acc[2 * c + 1]);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    // Per query: the two largest of the 16 subset maxima (8 per half-wave).
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        int k1 = INT_MIN, k2 = INT_MIN;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int v = ch[qt][c];
+            k2 = max(k2, min(k1, v));
+            k1 = max(k1, v);
+        }
+        const int p1 = __shfl_xor(k1, 32), p2 = __shfl_xor(k2, 32);
+        const int K2 = max(min(k1, p1), max(k2, p2)), K1 = max(k1, p1);
+        const int qi = qbase + qt * 32 + l32;
+        if (h != 0 || qi >= nq) continue;
+        const int64_t o = P.dense_base + qi;
+        if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }
+        bool reject = false;
+        if (nt >= 2 && K2 >= KEY_VALID) {
+            const int64_t na = norm[L.row0 + qi];
+            const int64_t s1 = max<int64_t>(na - 2 * (int64_t)K1 - 1, 0), s2 = na - 2 * (int64_t)K2;
+            reject = !((double)sqrt_rn_int(s1) < (double)sqrt_rn_int(s2) * ratio);
+        }
+        if (reject) {
+            out_idx[o] = -1;
+            out_dist[o] = 0.f;
+        } else {
+            const int slot = atomicAdd(&qcount[w.pair], 1);
+            qlist[P.dense_base + slot] = qi;
+        }
+    }
+}
+
+// Pass-2 work list: ceil(qcount[p] / 512) items per pair, pairs in the host's
+// order (sorted by train image, so XCD-contiguous items share train rows).
+// One 1024-thread block; each thread owns a contiguous run of pairs.
+__global__ __launch_bounds__(1024)
+void compact_work_kernel(const int32_t* __restrict__ porder, int n_pairs, const int32_t* __restrict__ qcount,
+                         WorkItem* __restrict__ work2, int32_t* __restrict__ work2_n) {
+    __shared__ int wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int per = (n_pairs + 1023) / 1024, p0 = min(tid * per, n_pairs), p1 = min(p0 + per, n_pairs);
+    int mine = 0;
+    for (int i = p0; i < p1; ++i) mine += (qcount[porder[i]] + 511) >> 9;
+    int incl = mine;                                  // inclusive scan: wave, then across waves
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int base = 0;
+    for (int i = 0; i < wv; ++i) base += wsum[i];
+    int at = base + incl - mine;
+    for (int i = p0; i < p1; ++i) {
+        const int p = porder[i], n = (qcount[p] + 511) >> 9;
+        for (int k = 0; k < n; ++k) work2[at++] = WorkItem{p, k * 512};
+    }
+    if (tid == 1023) *work2_n = base + incl;
 }
 
 // Exact path for queries whose best-2 falls in the float-sqrt collision range:
@@ -811,10 +1013,11 @@ hipError_t launch_selftest_sqrt(int64_t n, uint32_t* out, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_prep_l2(const float* src, int rows, int cols, int rows_pad, int8_t* dst, int32_t* norm,
-                          int32_t* keyc, int32_t* nonintegral, hipStream_t st) {
+                          int32_t* keyc, int32_t* keyc2, int32_t* nonintegral, hipStream_t st) {
     if (rows_pad == 0) return hipSuccess;
     const int rows_per_block = 8;   // 256 threads
-    prep_l2_kernel<<<(rows_pad + rows_per_block - 1) / rows_per_block, 256, 0, st>>>(src, rows, cols, rows_pad, dst, norm, keyc, nonintegral);
+    prep_l2_kernel<<<(rows_pad + rows_per_block - 1) / rows_per_block, 256, 0, st>>>(src, rows, cols, rows_pad, dst, norm,
+                                                                                      keyc, keyc2, nonintegral);
     return hipGetLastError();
 }
 hipError_t launch_prep_f32(const float* src, int rows, int cols, int rows_pad, float* dst, hipStream_t st) {
@@ -832,12 +1035,9 @@ hipError_t launch_prep_hamming(const uint8_t* src, int rows, int cols, int rows_
 
 // Kernel variants (queries per block = QT * WAVES * 32, must divide ROW_ALIGN).
 // Selected by sift_variant(); SFMX_SIFT_VARIANT overrides (tuning only).
-int sift_variant() {
-    static int v = [] {
-        const char* e = getenv("SFMX_SIFT_VARIANT");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
+int sift_variant() {   // read per run: tests switch paths within one process
+    const char* e = getenv("SFMX_SIFT_VARIANT");
+    return e ? atoi(e) : 0;
 }
 int sift_block_queries(int v) { return v == 2 || v == 4 || v == 23 ? 256 : 512; }
 
@@ -846,10 +1046,35 @@ int sift_block_queries(int v) { return v == 2 || v == 4 || v == 23 ? 256 : 512; 
                                                                      out_idx, out_dist, slow_list, slow_count, ratio)
 
 hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
-                            const int8_t* desc8, const int32_t* norm, const int32_t* keyc, int32_t* out_idx,
+                            const int8_t* desc8, const int32_t* norm, const int32_t* keyc, const int32_t* keyc2,
+                            int32_t* qlist, int32_t* qcount, int n_pairs, const int32_t* porder, WorkItem* work2,
+                            int32_t* work2_n, int32_t* out_idx,
                             float* out_dist, int2* slow_list, int32_t* slow_count, double ratio, hipStream_t st) {
     if (n_work == 0) return hipSuccess;
-    switch (sift_variant()) {
+    const int v = sift_variant();
+    if (v == 0 || v >= 101) {   // two-pass ratio test: screen every query, exact kernel on the rest
+        hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * n_pairs, st);
+        if (e != hipSuccess) return e;
+#define SCREEN_LAUNCH(QT, W, MINW, ST) \
+    sift_screen_kernel<QT, W, MINW, ST><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc2, out_idx, \
+                                                                   out_dist, qlist, qcount, ratio)
+        switch (v) {
+        // every variant: 512 queries per work item (pass 2's).  r01f A/B on config 2 (kernel ms, both
+        // passes): 64-row stages 8.31-8.41, 128-row 8.50-8.57, MINW 3 8.37-8.41, 2 x 8 waves 9.60-9.66
+        case 101: SCREEN_LAUNCH(4, 4, 2, 128); break;
+        case 102: SCREEN_LAUNCH(2, 8, 2, 128); break;
+        case 104: SCREEN_LAUNCH(2, 8, 2, 64); break;
+        case 105: SCREEN_LAUNCH(4, 4, 3, 64); break;
+        default: SCREEN_LAUNCH(4, 4, 2, 64);
+        }
+#undef SCREEN_LAUNCH
+        compact_work_kernel<<<1, 1024, 0, st>>>(porder, n_pairs, qcount, work2, work2_n);
+        sift_knn2_kernel<4, 4, 2, 128, false, 0, 0, true><<<n_work, 256, 0, st>>>(
+            work2, pairs, imgs, desc8, norm, keyc, out_idx, out_dist, slow_list, slow_count, ratio, qlist, qcount,
+            work2_n);
+        return hipGetLastError();
+    }
+    switch (v) {    // single pass (tuning / A-B only)
     case 1: SIFT_LAUNCH(2, 8, 2, 128, false); break;
     case 2: SIFT_LAUNCH(2, 4, 3, 64, true); break;
     case 3: SIFT_LAUNCH(2, 8, 2, 64, false); break;
@@ -864,7 +1089,7 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
     case 21: SIFT_LAUNCH(2, 8, 2, 128, false, 0, 9); break;
     case 22: SIFT_LAUNCH(4, 4, 2, 128, false, 0, 8); break;
     case 23: SIFT_LAUNCH(2, 4, 4, 128, false, 0, 9); break;
-    default: SIFT_LAUNCH(4, 4, 2, 128, false);   // measured best (r01 A/B: 9.57-9.67 ms vs 9.96-10.01 for QT=2 x 8 waves)
+    default: SIFT_LAUNCH(4, 4, 2, 128, false);   // 100: the r01d single-pass default (9.57-9.67 ms on config 2)
     }
     return hipGetLastError();
 }

@@ -27,11 +27,12 @@
 #include "match_common.hpp"
 
 namespace sfmx {
-hipError_t launch_prep_l2(const float*, int, int, int, int8_t*, int32_t*, int32_t*, int32_t*, hipStream_t);
+hipError_t launch_prep_l2(const float*, int, int, int, int8_t*, int32_t*, int32_t*, int32_t*, int32_t*, hipStream_t);
 hipError_t launch_prep_f32(const float*, int, int, int, float*, hipStream_t);
 hipError_t launch_prep_hamming(const uint8_t*, int, int, int, uint8_t*, hipStream_t);
 hipError_t launch_sift_knn2(const WorkItem*, int, const PairDev*, const ImgDev*, const int8_t*, const int32_t*,
-                            const int32_t*, int32_t*, float*, int2*, int32_t*, double, hipStream_t);
+                            const int32_t*, const int32_t*, int32_t*, int32_t*, int, const int32_t*, WorkItem*,
+                            int32_t*, int32_t*, float*, int2*, int32_t*, double, hipStream_t);
 hipError_t launch_sift_slow(const int2*, const int32_t*, const PairDev*, const ImgDev*, const int8_t*,
                             const int32_t*, int32_t*, float*, double, hipStream_t);
 hipError_t launch_sift_f32(const WorkItem*, int, const PairDev*, const ImgDev*, const float*, int32_t*, float*,
@@ -108,12 +109,14 @@ struct sfmx_matcher {
     int64_t total_rows = 0;
     int max_rows = 0;
     bool any_nonintegral = false;
-    DevBuf raw, desc8, normv, keyc, f32, flags, imgs_d;
+    DevBuf raw, desc8, normv, keyc, keyc2, f32, flags, imgs_d;
     // run state
     int n_pairs = 0;
     int64_t dense_total = 0;
     int64_t fp32_pairs = 0;
     DevBuf pairs_d, work_d, work32_d, dense_idx, dense_dist, slow_list, slow_count, counts, keep, offsets, out;
+    DevBuf qlist, qcount;   // two-pass SIFT path: per pair, the queries the screening pass could not settle
+    DevBuf porder, work2, work2_n;   // pair order (by train image) and the compacted pass-2 work list
     bool has_run = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};   // run start, main kernel end, run end
     bool ev_recorded = false;
@@ -176,6 +179,7 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
     if ((rc = m->imgs_d.ensure(sizeof(ImgDev) * std::max(n, 1)))) return rc;
     if (norm == SFMX_NORM_L2 && (rc = m->normv.ensure((size_t)row * 4))) return rc;
     if ((norm == SFMX_NORM_L2 || m->orb_fp4) && (rc = m->keyc.ensure((size_t)row * 4))) return rc;
+    if (norm == SFMX_NORM_L2 && (rc = m->keyc2.ensure((size_t)row * 4))) return rc;
     if (!device_src && (rc = m->raw.ensure((size_t)raw_bytes))) return rc;
     HIPCHK(hipMemsetAsync(m->flags.p, 0, sizeof(int32_t) * std::max(n, 1), st));
     std::vector<const void*> src(n);
@@ -193,7 +197,8 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
         if (norm == SFMX_NORM_L2)
             HIPCHK(launch_prep_l2((const float*)src[i], d.rows, imgs[i].cols, d.rows_pad,
                                   m->desc8.as<int8_t>() + d.row0 * SIFT_DIM, m->normv.as<int32_t>() + d.row0,
-                                  m->keyc.as<int32_t>() + d.row0, m->flags.as<int32_t>() + i, st));
+                                  m->keyc.as<int32_t>() + d.row0, m->keyc2.as<int32_t>() + d.row0,
+                                  m->flags.as<int32_t>() + i, st));
         else if (m->orb_fp4)
             HIPCHK(launch_prep_hamming_fp4((const uint8_t*)src[i], d.rows, imgs[i].cols, d.rows_pad,
                                            m->desc8.as<uint8_t>() + d.row0 * SIFT_DIM, m->keyc.as<int32_t>() + d.row0, st));
@@ -263,11 +268,17 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     if ((rc = m->dense_dist.ensure(sizeof(float) * std::max<int64_t>(dense, 1)))) return rc;
     if ((rc = m->slow_list.ensure(sizeof(int2) * std::max<int64_t>(dense, 1)))) return rc;
     if ((rc = m->slow_count.ensure(sizeof(int32_t)))) return rc;
+    if ((rc = m->qlist.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
+    if ((rc = m->qcount.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
+    if ((rc = m->porder.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
+    if ((rc = m->work2.ensure(sizeof(WorkItem) * std::max<size_t>(work.size(), 1)))) return rc;
+    if ((rc = m->work2_n.ensure(sizeof(int32_t)))) return rc;
     if ((rc = m->counts.ensure(sizeof(int64_t) * std::max(n_pairs, 1)))) return rc;
     if ((rc = m->keep.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
     if ((rc = m->offsets.ensure(sizeof(int64_t) * (n_pairs + 1)))) return rc;
     if ((rc = m->out.ensure(sizeof(DMatchDev) * std::max<int64_t>(dense, 1)))) return rc;
     if (n_pairs) HIPCHK(hipMemcpyAsync(m->pairs_d.p, pd.data(), sizeof(PairDev) * n_pairs, hipMemcpyHostToDevice, st));
+    if (n_pairs) HIPCHK(hipMemcpyAsync(m->porder.p, order.data(), sizeof(int32_t) * n_pairs, hipMemcpyHostToDevice, st));
     if (!work.empty()) HIPCHK(hipMemcpyAsync(m->work_d.p, work.data(), sizeof(WorkItem) * work.size(), hipMemcpyHostToDevice, st));
     if (!work32.empty()) HIPCHK(hipMemcpyAsync(m->work32_d.p, work32.data(), sizeof(WorkItem) * work32.size(), hipMemcpyHostToDevice, st));
     if (!m->ev[0])
@@ -280,7 +291,9 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     const ImgDev* I = m->imgs_d.as<ImgDev>();
     if (m->norm == SFMX_NORM_L2) {
         HIPCHK(launch_sift_knn2(m->work_d.as<WorkItem>(), (int)work.size(), P, I, m->desc8.as<int8_t>(),
-                                m->normv.as<int32_t>(), m->keyc.as<int32_t>(), m->dense_idx.as<int32_t>(),
+                                m->normv.as<int32_t>(), m->keyc.as<int32_t>(), m->keyc2.as<int32_t>(),
+                                m->qlist.as<int32_t>(), m->qcount.as<int32_t>(), n_pairs, m->porder.as<int32_t>(),
+                                m->work2.as<WorkItem>(), m->work2_n.as<int32_t>(), m->dense_idx.as<int32_t>(),
                                 m->dense_dist.as<float>(), m->slow_list.as<int2>(), m->slow_count.as<int32_t>(), ratio, st));
         HIPCHK(hipEventRecord(m->ev[1], st));
         HIPCHK(launch_sift_slow(m->slow_list.as<int2>(), m->slow_count.as<int32_t>(), P, I, m->desc8.as<int8_t>(),
@@ -380,7 +393,7 @@ int sfmx_matcher_destroy(sfmx_matcher* m) {
     if (!m) return SFMX_OK;
     {
         DeviceGuard g(m->device);
-        DevBuf* bufs[] = {&m->raw, &m->desc8, &m->normv, &m->keyc, &m->f32, &m->flags, &m->imgs_d, &m->pairs_d,
+        DevBuf* bufs[] = {&m->raw, &m->desc8, &m->normv, &m->keyc, &m->keyc2, &m->qlist, &m->qcount, &m->porder, &m->work2, &m->work2_n, &m->f32, &m->flags, &m->imgs_d, &m->pairs_d,
                           &m->work_d, &m->work32_d, &m->dense_idx, &m->dense_dist, &m->slow_list, &m->slow_count,
                           &m->counts, &m->keep, &m->offsets, &m->out};
         for (DevBuf* b : bufs) b->release();
