@@ -147,7 +147,7 @@ def bench_match(kind, args, rank, world, local):
         dtype = "int8->int32 (exact; f32 in/out)"
         scaling = "weak" if kind == "sift" else "strong"
         data = "synthetic (seeded SIFT-like descriptors, 25% planted re-observations; no dataset)"
-        kernel = "sift_screen_kernel + sift_knn2_kernel<GATHER> (two-pass ratio test, both passes)"
+        kernel = "sift_screen16_kernel + sift_knn2_kernel<GATHER> (two-pass ratio test, both passes)"
         algo = "256 ops (128 int8 MAC) per descriptor pair"
     else:
         n_desc, n_img = 16384, 200
@@ -399,9 +399,9 @@ def bench_3d2d(args, imgs, my_pairs, got, off, rank, world, local, stream):
     return res
 
 
-PMC_FILES = {"sift": ("r01f_pmc_sift_2p.json", ("sift_screen_kernel", "sift_knn2_kernel"), 50),
+PMC_FILES = {"sift": ("r01g_pmc_sift_2p.json", ("sift_screen16_kernel", "sift_knn2_kernel"), 50),
              "orb": ("r01_pmc_orb.json", ("orb_mfma_kernel",), 200),
-             "c3": ("r01_pmc_sift_c3.json", ("sift_screen_kernel", "sift_knn2_kernel"), 200)}
+             "c3": ("r01_pmc_sift_c3.json", ("sift_screen16_kernel", "sift_knn2_kernel"), 200)}
 
 
 def pmc_traffic(kind, n_img):

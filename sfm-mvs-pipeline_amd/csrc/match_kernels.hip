@@ -542,9 +542,155 @@ void sift_screen_kernel(const WorkItem* __restrict__ work, const PairDev* __rest
     }
 }
 
+// Screening pass on v_mfma_i32_16x16x64_i8 (same bounds, same outputs as
+// sift_screen_kernel; a second MFMA shape for the clock the chip holds under it).
+//   D = A * B, A = 16 train rows (LDS), B = 16 queries (registers), K = 128 = 2 MFMAs.
+//   Lane l: A row / B column l & 15, 16 operand bytes of chunk 4m + (l >> 4) (any
+//   chunk order is a dot product as long as A and B agree); accumulator rows
+//   4 (l >> 4) + i, i = 0..3, of column l & 15.  Two row blocks per step feed one
+//   v_max3 per accumulator row i: 4 chains per lane x 4 lanes = 16 disjoint row
+//   subsets per query, the same bound as the 32x32 form.
+template <int QT, int WAVES, int MINW, int STAGE>
+__global__ __launch_bounds__(WAVES * 64, MINW)
+void sift_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
+                          const ImgDev* __restrict__ imgs, const int8_t* __restrict__ desc8,
+                          const int32_t* __restrict__ norm, const int32_t* __restrict__ keyc2,
+                          int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
+                          int32_t* __restrict__ qlist, int32_t* __restrict__ qcount, double ratio) {
+    constexpr int GLDS = STAGE * SIFT_DIM / (WAVES * 64 * 16);
+    static_assert(GLDS * WAVES * 64 * 16 == STAGE * SIFT_DIM, "stage must split into whole 16-B pieces");
+    static_assert(QT * WAVES * 16 == 512, "work items are 512 queries");
+    constexpr int DESC_BYTES = STAGE * SIFT_DIM;
+    constexpr int BUF_BYTES = DESC_BYTES + STAGE * 4;
+    __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
+
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+    const WorkItem w = work[xcd_remap(blockIdx.x, gridDim.x)];
+    const PairDev P = pairs[w.pair];
+    const ImgDev L = imgs[P.left], R = imgs[P.right];
+    const int nq = L.rows, nt = R.rows;
+    const int qbase = w.q0 + wid * (QT * 16);
+
+    i32x4 bq[QT][2];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const i32x4* src = reinterpret_cast<const i32x4*>(desc8 + (L.row0 + qbase + qt * 16 + l16) * SIFT_DIM);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) bq[qt][m] = src[4 * m + g];
+    }
+    int ch[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ch[qt][i] = INT_MIN;
+
+    const int nstages = (nt + STAGE - 1) / STAGE;
+    const int8_t* tbase = desc8 + R.row0 * SIFT_DIM;
+    const int32_t* kbase = keyc2 + R.row0;
+    auto stage = [&](int s, int buf) {
+        char* base = lds + buf * BUF_BYTES;
+#pragma unroll
+        for (int i = 0; i < GLDS; ++i) {
+            const int p = i * WAVES * 64 + threadIdx.x;
+            const int rr = p >> 3, slot = p & 7, c = slot ^ ((rr >> 1) & 7);
+            const int8_t* gp = tbase + (int64_t)(s * STAGE + rr) * SIFT_DIM + 16 * c;
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)gp,
+                                             (LDS_AS void*)(base + (i * WAVES + wid) * 1024), 16, 0, 0);
+        }
+        if (wid < STAGE / 64)
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(kbase + s * STAGE + wid * 64 + lane),
+                                             (LDS_AS void*)(base + DESC_BYTES + wid * 256), 4, 0, 0);
+    };
+
+    if (nstages > 0) stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < nstages; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nstages) stage(s + 1, buf ^ 1);
+        const char* base = lds + buf * BUF_BYTES;
+#pragma unroll
+        for (int t = 0; t < STAGE / 32; ++t) {
+            i32x4 a[2][2], cv[2];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int row = t * 32 + b * 16 + l16;
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const int slot = (4 * m + g) ^ ((row >> 1) & 7);
+                    a[b][m] = *reinterpret_cast<const i32x4*>(base + row * SIFT_DIM + 16 * slot);
+                }
+                cv[b] = *reinterpret_cast<const i32x4*>(base + DESC_BYTES + 4 * (t * 32 + b * 16 + 4 * g));
+            }
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                i32x4 acc0 = cv[0], acc1 = cv[1];
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[0][m], bq[qt][m], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[1][m], bq[qt][m], acc1, 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) ch[qt][i] = max(max(ch[qt][i], acc0[i]), acc1[i]);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        int k1 = INT_MIN, k2 = INT_MIN;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int v = ch[qt][i];
+            k2 = max(k2, min(k1, v));
+            k1 = max(k1, v);
+        }
+#pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) {
+            const int p1 = __shfl_xor(k1, o), p2 = __shfl_xor(k2, o);
+            k2 = max(min(k1, p1), max(k2, p2));
+            k1 = max(k1, p1);
+        }
+        const int qi = qbase + qt * 16 + l16;
+        if (g != 0 || qi >= nq) continue;
+        const int64_t o = P.dense_base + qi;
+        if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }
+        bool reject = false;
+        if (nt >= 2 && k2 >= KEY_VALID) {
+            const int64_t na = norm[L.row0 + qi];
+            const int64_t s1 = max<int64_t>(na - 2 * (int64_t)k1 - 1, 0), s2 = na - 2 * (int64_t)k2;
+            reject = !((double)sqrt_rn_int(s1) < (double)sqrt_rn_int(s2) * ratio);
+        }
+        if (reject) {
+            out_idx[o] = -1;
+            out_dist[o] = 0.f;
+        } else {
+            const int slot = atomicAdd(&qcount[w.pair], 1);
+            qlist[P.dense_base + slot] = qi;
+        }
+    }
+}
+
+// Timing probe only (wrong results): flips the sign bit of every int8 operand
+// byte, i.e. the unshifted byte a instead of a - 128, to measure how operand
+// bit patterns move the clock the chip holds under the screening MFMAs.
+__global__ void probe_xor80_kernel(uint32_t* __restrict__ p, int64_t n_words) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_words) p[i] ^= 0x80808080u;
+}
+hipError_t launch_probe_xor80(int8_t* p, int64_t bytes, hipStream_t st) {
+    const int64_t n = bytes / 4;
+    if (n == 0) return hipSuccess;
+    probe_xor80_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(reinterpret_cast<uint32_t*>(p), n);
+    return hipGetLastError();
+}
+
 // Pass-2 work list: ceil(qcount[p] / 512) items per pair, pairs in the host's
 // order (sorted by train image, so XCD-contiguous items share train rows).
 // One 1024-thread block; each thread owns a contiguous run of pairs.
+template <int ISH>   // queries per pass-2 item = 1 << ISH
 __global__ __launch_bounds__(1024)
 void compact_work_kernel(const int32_t* __restrict__ porder, int n_pairs, const int32_t* __restrict__ qcount,
                          WorkItem* __restrict__ work2, int32_t* __restrict__ work2_n) {
@@ -552,7 +698,7 @@ void compact_work_kernel(const int32_t* __restrict__ porder, int n_pairs, const 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int per = (n_pairs + 1023) / 1024, p0 = min(tid * per, n_pairs), p1 = min(p0 + per, n_pairs);
     int mine = 0;
-    for (int i = p0; i < p1; ++i) mine += (qcount[porder[i]] + 511) >> 9;
+    for (int i = p0; i < p1; ++i) mine += (qcount[porder[i]] + (1 << ISH) - 1) >> ISH;
     int incl = mine;                                  // inclusive scan: wave, then across waves
     for (int o = 1; o < 64; o <<= 1) {
         const int v = __shfl_up(incl, o);
@@ -564,8 +710,8 @@ void compact_work_kernel(const int32_t* __restrict__ porder, int n_pairs, const 
     for (int i = 0; i < wv; ++i) base += wsum[i];
     int at = base + incl - mine;
     for (int i = p0; i < p1; ++i) {
-        const int p = porder[i], n = (qcount[p] + 511) >> 9;
-        for (int k = 0; k < n; ++k) work2[at++] = WorkItem{p, k * 512};
+        const int p = porder[i], n = (qcount[p] + (1 << ISH) - 1) >> ISH;
+        for (int k = 0; k < n; ++k) work2[at++] = WorkItem{p, k << ISH};
     }
     if (tid == 1023) *work2_n = base + incl;
 }
@@ -1039,6 +1185,10 @@ int sift_variant() {   // read per run: tests switch paths within one process
     const char* e = getenv("SFMX_SIFT_VARIANT");
     return e ? atoi(e) : 0;
 }
+int pass2_variant() {   // tuning only: SFMX_SIFT_P2 selects the pass-2 item size / shape
+    const char* e = getenv("SFMX_SIFT_P2");
+    return e ? atoi(e) : 0;
+}
 int sift_block_queries(int v) { return v == 2 || v == 4 || v == 23 ? 256 : 512; }
 
 #define SIFT_LAUNCH(QT, W, MINW, ST, MF, ...)                                                             \
@@ -1058,6 +1208,9 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
 #define SCREEN_LAUNCH(QT, W, MINW, ST) \
     sift_screen_kernel<QT, W, MINW, ST><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc2, out_idx, \
                                                                    out_dist, qlist, qcount, ratio)
+#define SCREEN16_LAUNCH(QT, W, MINW, ST) \
+    sift_screen16_kernel<QT, W, MINW, ST><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc2, out_idx, \
+                                                                     out_dist, qlist, qcount, ratio)
         switch (v) {
         // every variant: 512 queries per work item (pass 2's).  r01f A/B on config 2 (kernel ms, both
         // passes): 64-row stages 8.31-8.41, 128-row 8.50-8.57, MINW 3 8.37-8.41, 2 x 8 waves 9.60-9.66
@@ -1065,13 +1218,31 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
         case 102: SCREEN_LAUNCH(2, 8, 2, 128); break;
         case 104: SCREEN_LAUNCH(2, 8, 2, 64); break;
         case 105: SCREEN_LAUNCH(4, 4, 3, 64); break;
-        default: SCREEN_LAUNCH(4, 4, 2, 64);
+        case 103: SCREEN_LAUNCH(4, 4, 2, 64); break;       // r01f default (32x32x32 screen)
+        // r01g A/B on config 2 (kernel ms, both passes, 2 runs): 103 8.24-8.27, 106 7.43-7.50,
+        // 107 7.43-7.44, 108 8.60-8.61
+        case 107: SCREEN16_LAUNCH(8, 4, 2, 128); break;
+        case 108: SCREEN16_LAUNCH(4, 8, 2, 64); break;
+        default: SCREEN16_LAUNCH(8, 4, 2, 64);             // 0 / 106
         }
 #undef SCREEN_LAUNCH
-        compact_work_kernel<<<1, 1024, 0, st>>>(porder, n_pairs, qcount, work2, work2_n);
-        sift_knn2_kernel<4, 4, 2, 128, false, 0, 0, true><<<n_work, 256, 0, st>>>(
-            work2, pairs, imgs, desc8, norm, keyc, out_idx, out_dist, slow_list, slow_count, ratio, qlist, qcount,
-            work2_n);
+#undef SCREEN16_LAUNCH
+#define PASS2_LAUNCH(ISH, QT, W, MINW, ST)                                                                   \
+    compact_work_kernel<ISH><<<1, 1024, 0, st>>>(porder, n_pairs, qcount, work2, work2_n);                  \
+    sift_knn2_kernel<QT, W, MINW, ST, false, 0, 0, true><<<n_work << (9 - ISH), W * 64, 0, st>>>(             \
+        work2, pairs, imgs, desc8, norm, keyc, out_idx, out_dist, slow_list, slow_count, ratio, qlist, qcount, \
+        work2_n)
+        // pass-2 item size (queries); the work2 list holds up to n_work << 2 items (host sizes it)
+        switch (pass2_variant()) {
+        // r01g A/B on config 2 (kernel ms, both passes, 2 runs): 512-query items (r01f) 7.40-7.43,
+        // 256 (QT 2 x 4 waves) 7.19-7.22, 256 (QT 4 x 2 waves) 7.24-7.28, 128 (QT 1 x 4 waves) 7.16-7.21:
+        // a config-2 pair leaves ~500 queries for pass 2, so smaller items fill the chip's last round
+        case 1: PASS2_LAUNCH(8, 2, 4, 2, 128); break;
+        case 3: PASS2_LAUNCH(8, 4, 2, 2, 128); break;
+        case 4: PASS2_LAUNCH(9, 4, 4, 2, 128); break;   // r01f
+        default: PASS2_LAUNCH(7, 1, 4, 2, 128);         // 0 / 2
+        }
+#undef PASS2_LAUNCH
         return hipGetLastError();
     }
     switch (v) {    // single pass (tuning / A-B only)

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -28,6 +29,7 @@
 
 namespace sfmx {
 hipError_t launch_prep_l2(const float*, int, int, int, int8_t*, int32_t*, int32_t*, int32_t*, int32_t*, hipStream_t);
+hipError_t launch_probe_xor80(int8_t*, int64_t, hipStream_t);
 hipError_t launch_prep_f32(const float*, int, int, int, float*, hipStream_t);
 hipError_t launch_prep_hamming(const uint8_t*, int, int, int, uint8_t*, hipStream_t);
 hipError_t launch_sift_knn2(const WorkItem*, int, const PairDev*, const ImgDev*, const int8_t*, const int32_t*,
@@ -225,6 +227,8 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
             }
         }
     }
+    if (norm == SFMX_NORM_L2 && getenv("SFMX_PROBE_XOR80"))   // timing probe only (wrong results)
+        HIPCHK(launch_probe_xor80(m->desc8.as<int8_t>(), (int64_t)row * SIFT_DIM, st));
     if (n > 0) HIPCHK(hipMemcpyAsync(m->imgs_d.p, m->imgs.data(), sizeof(ImgDev) * n, hipMemcpyHostToDevice, st));
     if (!device_src) HIPCHK(hipStreamSynchronize(st));   // host buffers may be released by the caller
     return SFMX_OK;
@@ -271,7 +275,7 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     if ((rc = m->qlist.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
     if ((rc = m->qcount.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
     if ((rc = m->porder.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
-    if ((rc = m->work2.ensure(sizeof(WorkItem) * std::max<size_t>(work.size(), 1)))) return rc;
+    if ((rc = m->work2.ensure(sizeof(WorkItem) * std::max<size_t>(4 * work.size(), 1)))) return rc;   // pass-2 items >= 128 queries
     if ((rc = m->work2_n.ensure(sizeof(int32_t)))) return rc;
     if ((rc = m->counts.ensure(sizeof(int64_t) * std::max(n_pairs, 1)))) return rc;
     if ((rc = m->keep.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;

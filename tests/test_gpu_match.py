@@ -83,6 +83,32 @@ def test_ragged_sizes_vs_oracle():
     assert stats == (0, 0)
 
 
+# Screening-pass shapes (103: 32x32x32 MFMA, 106-108: 16x16x64) and pass-2 item
+# sizes (SFMX_SIFT_P2: 1/3 = 256 queries, 4 = 512, 0 = 128): every shipped or
+# tuned kernel form must give the oracle's matches.  The uniform set has many
+# queries whose best two share a screening subset, so pass 2 sees both accepted
+# and undecided queries; 1100-query images split a pair's list over several items.
+@pytest.mark.parametrize("variant,p2", [("103", "0"), ("106", "4"), ("107", "1"), ("108", "3"), ("0", "0")])
+def test_two_pass_variants_vs_oracle(variant, p2):
+    from oracle import oracle
+    sizes = [1, 33, 257, 513, 1100, 1100]
+    base = synth.sift_images(len(sizes), 1100, seed=57)
+    imgs = [b[:n] for b, n in zip(base, sizes)]
+    rng = np.random.default_rng(58)
+    imgs.append(rng.integers(0, 256, (900, 128)).astype(np.float32))
+    pairs = sfmx.pairs_unordered(len(imgs))
+    os.environ["SFMX_SIFT_VARIANT"], os.environ["SFMX_SIFT_P2"] = variant, p2
+    try:
+        m, off, _, stats = run(imgs, pairs)
+        m2, off2, _, _ = run(imgs, pairs, ratio=0.95)
+    finally:
+        del os.environ["SFMX_SIFT_VARIANT"], os.environ["SFMX_SIFT_P2"]
+    em, eoff = oracle.match_pairs(imgs, pairs)
+    assert_same(m, off, em, eoff)
+    em2, eoff2 = oracle.match_pairs(imgs, pairs, 0.95)
+    assert_same(m2, off2, em2, eoff2)
+
+
 def test_non_integral_fp32_fallback():
     from oracle import oracle
     rng = np.random.default_rng(9)
