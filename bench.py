@@ -159,7 +159,7 @@ def bench_match(kind, args, rank, world, local):
         dtype = "fp4 e2m1 (+-1 bits) -> f32, exact"
         scaling = "strong"
         data = "synthetic (seeded uniform 256-bit ORB descriptors, 25% planted with 0-24 flipped bits; no dataset)"
-        kernel = "orb_mfma_kernel"
+        kernel = "orb_screen16_kernel + orb_mfma16_kernel<GATHER> (two-pass ratio test, both passes)"
         algo = "512 ops (256 +-1 MAC: dot = 256 - 2 hamming) per descriptor pair"
         if os.environ.get("SFMX_ORB_VARIANT", "0") == "1":   # VALU xor/popcount kernel (comparison only)
             op_per_pair, bound, peak, unit = ORB_OPS_PER_PAIR, "valu", VALU_PEAK_TOPS, "TOP/s"
@@ -400,7 +400,7 @@ def bench_3d2d(args, imgs, my_pairs, got, off, rank, world, local, stream):
 
 
 PMC_FILES = {"sift": ("r01g_pmc_sift_2p.json", ("sift_screen16_kernel", "sift_knn2_kernel"), 50),
-             "orb": ("r01_pmc_orb.json", ("orb_mfma_kernel",), 200),
+             "orb": ("r01h_pmc_orb.json", ("orb_screen16_kernel", "orb_mfma16_kernel"), 200),
              "c3": ("r01_pmc_sift_c3.json", ("sift_screen16_kernel", "sift_knn2_kernel"), 200)}
 
 

@@ -973,6 +973,310 @@ void orb_mfma_kernel(const WorkItem* __restrict__ work, const PairDev* __restric
     }
 }
 
+// ORB FP4 2-NN on v_mfma_scale_f32_16x16x128_f8f6f4: the same +-1 encoding,
+// C-operand keys and chunked top-2 as orb_mfma_kernel, in the 16x16 shape (the
+// shape the SIFT screening pass holds a higher clock on).  K = 256 = 2 MFMAs per
+// 16x16 tile; lane l: A row / B column l & 15, operand chunk 4m + (l >> 4)
+// (A and B agree, so the chunk order is irrelevant to the dot product);
+// accumulator rows 4 (l >> 4) + i of column l & 15.  Each query's 16 rows of a
+// block are spread over 4 lanes, merged (shfl 16, 32) at each key chunk's end.
+//   GATHER (pass 2 of the two-pass ORB path): as sift_knn2_kernel<GATHER>, the
+//   item's queries are entries [q0, q0 + QT * WAVES * 16) of its pair's qlist.
+template <int QT, int WAVES, int MINW, int STAGE, bool GATHER = false>
+__global__ __launch_bounds__(WAVES * 64, MINW)
+void orb_mfma16_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
+                       const ImgDev* __restrict__ imgs, const uint8_t* __restrict__ desc4,
+                       const int32_t* __restrict__ keyc, int32_t* __restrict__ out_idx,
+                       float* __restrict__ out_dist, double ratio,
+                       const int32_t* __restrict__ qlist = nullptr, const int32_t* __restrict__ qcount = nullptr,
+                       const int32_t* __restrict__ work2_n = nullptr) {
+    constexpr int ROWB = 128;
+    constexpr int GLDS = STAGE * ROWB / (WAVES * 64 * 16);
+    static_assert(GLDS * WAVES * 64 * 16 == STAGE * ROWB, "stage must split into whole 16-B pieces");
+    static_assert(GATHER || QT * WAVES * 16 == 512, "pass-1 work items are 512 queries");
+    constexpr int CHUNK = 16384;
+    static_assert(CHUNK % STAGE == 0, "stages tile the key chunk");
+    constexpr int DESC_BYTES = STAGE * ROWB;
+    constexpr int BUF_BYTES = DESC_BYTES + STAGE * 4;
+    constexpr int SPC = CHUNK / STAGE;
+    constexpr float KEY_FLOOR = 256.f;
+    __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
+
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+    int nwork = gridDim.x;
+    if constexpr (GATHER) {           // compacted list; the grid is an upper bound
+        nwork = *work2_n;
+        if ((int)blockIdx.x >= nwork) return;
+    }
+    const WorkItem w = work[xcd_remap(blockIdx.x, nwork)];
+    const PairDev P = pairs[w.pair];
+    const ImgDev L = imgs[P.left], R = imgs[P.right];
+    const int nq = L.rows, nt = R.rows;
+    const int qbase = w.q0 + wid * (QT * 16);
+    int qrow[QT];                     // query row of this lane's column in each tile (-1: none)
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int e = qbase + qt * 16 + l16;
+        if constexpr (GATHER) qrow[qt] = e < qcount[w.pair] ? qlist[P.dense_base + e] : -1;
+        else qrow[qt] = e < nq ? e : -1;
+    }
+
+    i32x4 bq[QT][2];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int lr = GATHER ? (qrow[qt] < 0 ? 0 : qrow[qt]) : qbase + qt * 16 + l16;   // rows < rows_pad
+        const i32x4* src = reinterpret_cast<const i32x4*>(desc4 + (L.row0 + lr) * ROWB);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) bq[qt][m] = src[4 * m + g];
+    }
+    int T1[QT], J1[QT], T2[QT], J2[QT];
+    float c1[QT], c2[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        T1[qt] = T2[qt] = INT_MAX; J1[qt] = J2[qt] = -1; c1[qt] = c2[qt] = 0.f;
+    }
+    const int nstages = (nt + STAGE - 1) / STAGE;
+    const uint8_t* tbase = desc4 + R.row0 * ROWB;
+    const int32_t* kbase = keyc + R.row0;
+    auto stage = [&](int s, int buf) {
+        char* base = lds + buf * BUF_BYTES;
+#pragma unroll
+        for (int i = 0; i < GLDS; ++i) {
+            const int p = i * WAVES * 64 + threadIdx.x;
+            const int rr = p >> 3, slot = p & 7, c = slot ^ ((rr >> 1) & 7);
+            const uint8_t* gp = tbase + (int64_t)(s * STAGE + rr) * ROWB + 16 * c;
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)gp,
+                                             (LDS_AS void*)(base + (i * WAVES + wid) * 1024), 16, 0, 0);
+        }
+        if (wid < STAGE / 64)
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(kbase + s * STAGE + wid * 64 + lane),
+                                             (LDS_AS void*)(base + DESC_BYTES + wid * 256), 4, 0, 0);
+    };
+    auto i8of = [](const i32x4& v) { return i32x8{v.x, v.y, v.z, v.w, 0, 0, 0, 0}; };
+
+    if (nstages > 0) stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < nstages; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nstages) stage(s + 1, buf ^ 1);
+        const char* base = lds + buf * BUF_BYTES;
+#pragma unroll
+        for (int t = 0; t < STAGE / 32; ++t) {
+            i32x4 a[2][2];
+            f32x4 cinit[2];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int row = t * 32 + b * 16 + l16;
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const int slot = (4 * m + g) ^ ((row >> 1) & 7);
+                    a[b][m] = *reinterpret_cast<const i32x4*>(base + row * ROWB + 16 * slot);
+                }
+                cinit[b] = *reinterpret_cast<const f32x4*>(base + DESC_BYTES + 4 * (t * 32 + b * 16 + 4 * g));
+            }
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                f32x4 acc[2];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    acc[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(i8of(a[b][0]), i8of(bq[qt][0]), cinit[b], 4, 4,
+                                                                              0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+                    acc[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(i8of(a[b][1]), i8of(bq[qt][1]), acc[b], 4, 4,
+                                                                              0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+                }
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int r = 0; r < 4; r += 2) {
+                        const float ka = acc[b][r], kb = acc[b][r + 1];
+                        c2[qt] = fmaxf(__builtin_amdgcn_fmed3f(c1[qt], ka, kb), c2[qt]);
+                        c1[qt] = fmaxf(c1[qt], fmaxf(ka, kb));
+                    }
+            }
+        }
+        if ((s % SPC) == SPC - 1 || s + 1 == nstages) {      // end of a key chunk
+            const int cb = (s / SPC) * CHUNK;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                float m1 = c1[qt], m2 = c2[qt];
+#pragma unroll
+                for (int o = 16; o <= 32; o <<= 1) {
+                    const float p1 = __shfl_xor(m1, o), p2 = __shfl_xor(m2, o);
+                    m2 = fmaxf(fminf(m1, p1), fmaxf(m2, p2));
+                    m1 = fmaxf(m1, p1);
+                }
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const float v = e == 0 ? m1 : m2;
+                    if (v >= KEY_FLOOR) {
+                        const float ip = __builtin_floorf(v);
+                        const int dot = (int)ip - 767;
+                        const int t_ = (256 - dot) >> 1;
+                        const int j_ = cb + 16383 - (int)((v - ip) * 16384.0f);
+                        if (t_ < T2[qt]) {
+                            if (t_ < T1[qt]) { T2[qt] = T1[qt]; J2[qt] = J1[qt]; T1[qt] = t_; J1[qt] = j_; }
+                            else { T2[qt] = t_; J2[qt] = j_; }
+                        }
+                    }
+                }
+                c1[qt] = c2[qt] = 0.f;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int qi = qrow[qt];
+        if (g != 0 || qi < 0) continue;
+        const int64_t o = P.dense_base + qi;
+        if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }
+        const float d1 = (float)T1[qt], d2 = (float)T2[qt];
+        const bool acc = nt >= 2 ? ((double)d1 < (double)d2 * ratio) : true;
+        out_idx[o] = acc ? J1[qt] : -1;
+        out_dist[o] = d1;
+    }
+}
+
+// Two-pass ORB ratio test, pass 1: the SIFT screening argument on the FP4 path.
+// The accumulator acc = keyc_j + dot (orb_mfma_kernel) is exact, floor(acc) - 767
+// = dot = 256 - 2 hamming; each lane keeps the max over 4 disjoint row subsets
+// per query tile (one v_max3_f32 per two elements), 16 subsets per query with the
+// other 3 lanes of its column.  The best two subset maxima K1 >= K2 are two
+// different rows, so hamming d1 (of K1) is the true best and d2' (of K2) >= the
+// true second best; Lowe's test is non-decreasing in d2, so when it fails at
+// (d1, d2') it fails for the true pair and the query is rejected exactly.  Every
+// other query goes to its pair's qlist for orb_mfma16_kernel<GATHER>.
+template <int QT, int WAVES, int MINW, int STAGE>
+__global__ __launch_bounds__(WAVES * 64, MINW)
+void orb_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
+                         const ImgDev* __restrict__ imgs, const uint8_t* __restrict__ desc4,
+                         const int32_t* __restrict__ keyc, int32_t* __restrict__ out_idx,
+                         float* __restrict__ out_dist, int32_t* __restrict__ qlist, int32_t* __restrict__ qcount,
+                         double ratio) {
+    constexpr int ROWB = 128;
+    constexpr int GLDS = STAGE * ROWB / (WAVES * 64 * 16);
+    static_assert(GLDS * WAVES * 64 * 16 == STAGE * ROWB, "stage must split into whole 16-B pieces");
+    static_assert(QT * WAVES * 16 == 512, "work items are 512 queries");
+    constexpr int DESC_BYTES = STAGE * ROWB;
+    constexpr int BUF_BYTES = DESC_BYTES + STAGE * 4;
+    constexpr float KEY_FLOOR = 256.f;                      // real keys >= 511, pad rows 0
+    __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
+
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+    const WorkItem w = work[xcd_remap(blockIdx.x, gridDim.x)];
+    const PairDev P = pairs[w.pair];
+    const ImgDev L = imgs[P.left], R = imgs[P.right];
+    const int nq = L.rows, nt = R.rows;
+    const int qbase = w.q0 + wid * (QT * 16);
+
+    i32x4 bq[QT][2];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const i32x4* src = reinterpret_cast<const i32x4*>(desc4 + (L.row0 + qbase + qt * 16 + l16) * ROWB);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) bq[qt][m] = src[4 * m + g];
+    }
+    float ch[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ch[qt][i] = 0.f;
+
+    const int nstages = (nt + STAGE - 1) / STAGE;
+    const uint8_t* tbase = desc4 + R.row0 * ROWB;
+    const int32_t* kbase = keyc + R.row0;
+    auto stage = [&](int s, int buf) {
+        char* base = lds + buf * BUF_BYTES;
+#pragma unroll
+        for (int i = 0; i < GLDS; ++i) {
+            const int p = i * WAVES * 64 + threadIdx.x;
+            const int rr = p >> 3, slot = p & 7, c = slot ^ ((rr >> 1) & 7);
+            const uint8_t* gp = tbase + (int64_t)(s * STAGE + rr) * ROWB + 16 * c;
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)gp,
+                                             (LDS_AS void*)(base + (i * WAVES + wid) * 1024), 16, 0, 0);
+        }
+        if (wid < STAGE / 64)
+            __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)(kbase + s * STAGE + wid * 64 + lane),
+                                             (LDS_AS void*)(base + DESC_BYTES + wid * 256), 4, 0, 0);
+    };
+    auto i8of = [](const i32x4& v) { return i32x8{v.x, v.y, v.z, v.w, 0, 0, 0, 0}; };
+
+    if (nstages > 0) stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < nstages; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < nstages) stage(s + 1, buf ^ 1);
+        const char* base = lds + buf * BUF_BYTES;
+#pragma unroll
+        for (int t = 0; t < STAGE / 32; ++t) {
+            i32x4 a[2][2];
+            f32x4 cinit[2];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int row = t * 32 + b * 16 + l16;
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const int slot = (4 * m + g) ^ ((row >> 1) & 7);
+                    a[b][m] = *reinterpret_cast<const i32x4*>(base + row * ROWB + 16 * slot);
+                }
+                cinit[b] = *reinterpret_cast<const f32x4*>(base + DESC_BYTES + 4 * (t * 32 + b * 16 + 4 * g));
+            }
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                f32x4 acc[2];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    acc[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(i8of(a[b][0]), i8of(bq[qt][0]), cinit[b], 4, 4,
+                                                                              0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+                    acc[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(i8of(a[b][1]), i8of(bq[qt][1]), acc[b], 4, 4,
+                                                                              0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) ch[qt][i] = fmaxf(fmaxf(ch[qt][i], acc[0][i]), acc[1][i]);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        float k1 = 0.f, k2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float v = ch[qt][i];
+            k2 = fmaxf(k2, fminf(k1, v));
+            k1 = fmaxf(k1, v);
+        }
+#pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) {
+            const float p1 = __shfl_xor(k1, o), p2 = __shfl_xor(k2, o);
+            k2 = fmaxf(fminf(k1, p1), fmaxf(k2, p2));
+            k1 = fmaxf(k1, p1);
+        }
+        const int qi = qbase + qt * 16 + l16;
+        if (g != 0 || qi >= nq) continue;
+        const int64_t o = P.dense_base + qi;
+        if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }
+        bool reject = false;
+        if (nt >= 2 && k2 >= KEY_FLOOR) {
+            const int d1 = (256 - ((int)__builtin_floorf(k1) - 767)) >> 1;
+            const int d2 = (256 - ((int)__builtin_floorf(k2) - 767)) >> 1;
+            reject = !((double)(float)d1 < (double)(float)d2 * ratio);
+        }
+        if (reject) {
+            out_idx[o] = -1;
+            out_dist[o] = 0.f;
+        } else {
+            const int slot = atomicAdd(&qcount[w.pair], 1);
+            qlist[P.dense_base + slot] = qi;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // ORB Hamming 2-NN on the VALU (8 x v_xor + 8 x v_bcnt per pair, no MFMA).
 // 4 waves x 2 queries per lane = 512 queries per block; train rows stream
@@ -1300,18 +1604,49 @@ hipError_t launch_prep_hamming_fp4(const uint8_t* src, int rows, int cols, int r
     return hipGetLastError();
 }
 hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
-                           const uint8_t* desc4, const int32_t* keyc, int32_t* out_idx, float* out_dist, double ratio,
-                           hipStream_t st) {
+                           const uint8_t* desc4, const int32_t* keyc, int32_t* qlist, int32_t* qcount, int n_pairs,
+                           const int32_t* porder, WorkItem* work2, int32_t* work2_n, int32_t* out_idx, float* out_dist,
+                           double ratio, hipStream_t st) {
     if (n_work == 0) return hipSuccess;
+    if (orb_variant() == 0 || orb_variant() >= 10) {   // two-pass ratio test (default)
+        hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * n_pairs, st);
+        if (e != hipSuccess) return e;
+        orb_screen16_kernel<8, 4, 2, 64><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx, out_dist,
+                                                                  qlist, qcount, ratio);
+#define ORB_PASS2(ISH, QT, W)                                                                                   \
+    compact_work_kernel<ISH><<<1, 1024, 0, st>>>(porder, n_pairs, qcount, work2, work2_n);                      \
+    orb_mfma16_kernel<QT, W, 2, 64, true><<<n_work << (9 - ISH), W * 64, 0, st>>>(work2, pairs, imgs, desc4, keyc, \
+                                                                                  out_idx, out_dist, ratio, qlist, \
+                                                                                  qcount, work2_n)
+        switch (orb_variant()) {
+        // Pass-2 builds with 2 or 4 query tiles per wave (128- / 256-query items) lost about half
+        // the accepted matches in the GPU parity tests, also with 16 extra wait states after each
+        // tile's MFMAs and with the key added on the VALU instead of the C operand; the 8-tile build
+        // is exact on every test.  Not understood; only the 8-tile form is built.
+        // r01g config 4: 18.68-18.73 ms (two-pass) vs 20.19-20.24 (single pass, variant 5).
+        default: ORB_PASS2(9, 8, 4);       // 0 / 12: 512-query items
+        }
+#undef ORB_PASS2
+        return hipGetLastError();
+    }
 #define ORB_LAUNCH(QT, W, MINW, ST) \
     orb_mfma_kernel<QT, W, MINW, ST><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx, out_dist, ratio)
-    switch (orb_variant()) {      // every variant: QT * W * 32 = 512 queries per work item
+#define ORB16_LAUNCH(QT, W, MINW, ST) \
+    orb_mfma16_kernel<QT, W, MINW, ST><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx, out_dist, ratio)
+    switch (orb_variant()) {      // every variant: 512 queries per work item
+    // r01g A/B on config 4 (kernel ms, 2 runs): 32x32x64 4 x 4 waves (r01 default, now 8) 21.1-21.5,
+    // 16x16x128 8 x 4 waves / 64-row stages 20.16-20.21, 128-row stages 20.78-20.85.  A 16x16x128
+    // build with 4 tiles x 8 waves failed kat_orb_ties (one accepted match lost) and is not kept;
+    // like the MINW = 1 builds the cause is not understood.
+    case 6: ORB16_LAUNCH(8, 4, 2, 128); break;
+    case 8: ORB_LAUNCH(4, 4, 2, 64); break;
     case 2: ORB_LAUNCH(2, 8, 2, 64); break;
     case 3: ORB_LAUNCH(2, 8, 2, 128); break;
     case 4: ORB_LAUNCH(1, 16, 1, 128); break;
-    default: ORB_LAUNCH(4, 4, 2, 64);   // measured best (r01: 20.7 ms on config 4 vs 21.3-24.3)
+    default: ORB16_LAUNCH(8, 4, 2, 64);   // 5: single pass, 16x16x128
     }
 #undef ORB_LAUNCH
+#undef ORB16_LAUNCH
     return hipGetLastError();
 }
 hipError_t launch_assemble(const PairDev* pairs, int n_pairs, const ImgDev* imgs, const int32_t* out_idx,

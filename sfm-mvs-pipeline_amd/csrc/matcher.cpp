@@ -43,7 +43,8 @@ hipError_t launch_orb_knn2(const WorkItem*, int, const PairDev*, const ImgDev*, 
                            double, hipStream_t);
 hipError_t launch_prep_hamming_fp4(const uint8_t*, int, int, int, uint8_t*, int32_t*, hipStream_t);
 hipError_t launch_orb_mfma(const WorkItem*, int, const PairDev*, const ImgDev*, const uint8_t*, const int32_t*,
-                           int32_t*, float*, double, hipStream_t);
+                           int32_t*, int32_t*, int, const int32_t*, WorkItem*, int32_t*, int32_t*, float*, double,
+                           hipStream_t);
 int orb_variant();
 hipError_t launch_selftest_sqrt(int64_t, uint32_t*, hipStream_t);
 int sift_variant();
@@ -307,7 +308,9 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
                                    m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
     } else if (m->orb_fp4) {
         HIPCHK(launch_orb_mfma(m->work_d.as<WorkItem>(), (int)work.size(), P, I, m->desc8.as<uint8_t>(),
-                               m->keyc.as<int32_t>(), m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
+                               m->keyc.as<int32_t>(), m->qlist.as<int32_t>(), m->qcount.as<int32_t>(), n_pairs,
+                               m->porder.as<int32_t>(), m->work2.as<WorkItem>(), m->work2_n.as<int32_t>(),
+                               m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
         HIPCHK(hipEventRecord(m->ev[1], st));
     } else {
         HIPCHK(launch_orb_knn2(m->work_d.as<WorkItem>(), (int)work.size(), P, I, m->desc8.as<uint8_t>(),

@@ -131,6 +131,22 @@ def test_orb_ragged_vs_oracle():
     assert_same(m, off, em, eoff)
 
 
+@pytest.mark.parametrize("ratio", [0.0, 0.7, 0.95, 1.0, 1.5])
+def test_orb_two_pass_ratios_vs_oracle(ratio):
+    """The ORB screening pass settles rejections from subset-maxima bounds; every
+    ratio (none accepted at 0, ties accepted only above 1) must give the oracle's
+    list.  Planted rows with few flipped bits plus exact duplicates (ties)."""
+    from oracle import oracle
+    base = synth.orb_images(4, 1200, seed=61)
+    base[1][:40] = base[0][:40]
+    base[2][100:140] = base[2][:40]
+    imgs = [base[0], base[1][:900], base[2], base[3][:2]]
+    pairs = sfmx.pairs_unordered(4)
+    m, off, _, _ = run(imgs, pairs, ratio=ratio)
+    em, eoff = oracle.match_pairs(imgs, pairs, ratio)
+    assert_same(m, off, em, eoff)
+
+
 def test_full_size_sift_spot_check_and_determinism():
     """C2 shape subset: 8 images x 8192 (all 28 pairs on the GPU), 3 pairs re-derived by the
     oracle; two GPU runs bit-identical; no slow-path / fp32 traffic on SIFT-like data."""

@@ -11,7 +11,7 @@ for r in rows:
     name = r["Kernel_Name"]
     dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     grid = int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
-    for key in ("sift_screen", "sift_knn2_kernel", "orb_mfma_kernel", "homography_ransac_kernel", "chol_step",
+    for key in ("sift_screen", "sift_knn2_kernel", "orb_screen", "orb_mfma", "homography_ransac_kernel", "chol_step",
                 "ba_point_blocks_lds", "ba_pair_blocks", "undistort_kernel", "blur_tile_n_kernel"):
         if key in name:
             if key in ("sift_screen", "sift_knn2_kernel"):
