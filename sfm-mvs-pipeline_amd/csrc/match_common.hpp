@@ -45,6 +45,12 @@ struct WorkItem {          // one 512-query block of one pair
 
 struct DMatchDev { int32_t queryIdx, trainIdx, imgIdx; float distance; };
 
+struct PrepImg {           // one image of a batched prep launch
+    const float* src;
+    int32_t rows, cols, rows_pad, _pad;
+    int64_t row0;
+};
+
 // Thread-local last-error text shared by every C-ABI entry point (sfmx_last_error).
 void set_last_error(const char* msg);
 

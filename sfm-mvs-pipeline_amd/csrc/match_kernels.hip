@@ -91,13 +91,33 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // ---------------------------------------------------------------------------
 // prep: float SIFT rows -> int8 a' = a - 128, ||a'||^2, chunk keys, integrality.
 // 32 threads per row (float4 each); pad rows are written as zeros.
+__device__ __forceinline__ void prep_l2_row(const float* __restrict__ src, int r, int rows, int cols,
+                                            int8_t* __restrict__ dst, int32_t* __restrict__ norm,
+                                            int32_t* __restrict__ keyc, int32_t* __restrict__ keyc2,
+                                            int32_t* __restrict__ nonintegral);
 __global__ void prep_l2_kernel(const float* __restrict__ src, int rows, int cols, int rows_pad,
                                int8_t* __restrict__ dst, int32_t* __restrict__ norm,
                                int32_t* __restrict__ keyc, int32_t* __restrict__ keyc2,
                                int32_t* __restrict__ nonintegral) {
     const int r = blockIdx.x * (blockDim.x >> 5) + (threadIdx.x >> 5);
-    const int c4 = threadIdx.x & 31;   // 4 columns each
     if (r >= rows_pad) return;
+    prep_l2_row(src, r, rows, cols, dst, norm, keyc, keyc2, nonintegral);
+}
+// All images of a set_images call in one launch: blockIdx.y = image (table in HBM).
+__global__ void prep_l2_batch_kernel(const PrepImg* __restrict__ tab, int8_t* __restrict__ desc8,
+                                     int32_t* __restrict__ norm, int32_t* __restrict__ keyc,
+                                     int32_t* __restrict__ keyc2, int32_t* __restrict__ flags) {
+    const PrepImg t = tab[blockIdx.y];
+    const int r = blockIdx.x * (blockDim.x >> 5) + (threadIdx.x >> 5);
+    if (r >= t.rows_pad) return;
+    prep_l2_row(t.src, r, t.rows, t.cols, desc8 + t.row0 * SIFT_DIM, norm + t.row0, keyc + t.row0, keyc2 + t.row0,
+                flags + blockIdx.y);
+}
+__device__ __forceinline__ void prep_l2_row(const float* __restrict__ src, int r, int rows, int cols,
+                                            int8_t* __restrict__ dst, int32_t* __restrict__ norm,
+                                            int32_t* __restrict__ keyc, int32_t* __restrict__ keyc2,
+                                            int32_t* __restrict__ nonintegral) {
+    const int c4 = threadIdx.x & 31;   // 4 columns each
     int v[4] = {0, 0, 0, 0};
     bool bad = false;
     if (r < rows) {
@@ -679,6 +699,13 @@ void sift_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __re
 __global__ void probe_xor80_kernel(uint32_t* __restrict__ p, int64_t n_words) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n_words) p[i] ^= 0x80808080u;
+}
+hipError_t launch_prep_l2_batch(const PrepImg* tab, int n, int max_rows_pad, int8_t* desc8, int32_t* norm,
+                                int32_t* keyc, int32_t* keyc2, int32_t* flags, hipStream_t st) {
+    if (n == 0 || max_rows_pad == 0) return hipSuccess;
+    prep_l2_batch_kernel<<<dim3((unsigned)((max_rows_pad + 7) / 8), (unsigned)n), 256, 0, st>>>(tab, desc8, norm, keyc,
+                                                                                              keyc2, flags);
+    return hipGetLastError();
 }
 hipError_t launch_probe_xor80(int8_t* p, int64_t bytes, hipStream_t st) {
     const int64_t n = bytes / 4;

@@ -30,6 +30,7 @@
 namespace sfmx {
 hipError_t launch_prep_l2(const float*, int, int, int, int8_t*, int32_t*, int32_t*, int32_t*, int32_t*, hipStream_t);
 hipError_t launch_probe_xor80(int8_t*, int64_t, hipStream_t);
+hipError_t launch_prep_l2_batch(const PrepImg*, int, int, int8_t*, int32_t*, int32_t*, int32_t*, int32_t*, hipStream_t);
 hipError_t launch_prep_f32(const float*, int, int, int, float*, hipStream_t);
 hipError_t launch_prep_hamming(const uint8_t*, int, int, int, uint8_t*, hipStream_t);
 hipError_t launch_sift_knn2(const WorkItem*, int, const PairDev*, const ImgDev*, const int8_t*, const int32_t*,
@@ -92,6 +93,40 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// Pinned host staging for small H2D uploads (prep table, pair/work lists): truly
+// asynchronous copies.  `busy` is recorded after the copies that read the buffer;
+// a writer waits for it first, so a copy still in flight is never overwritten.
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t busy = nullptr;
+    bool pending = false;
+    int ensure(size_t bytes) {
+        if (pending) { (void)hipEventSynchronize(busy); pending = false; }
+        if (bytes <= cap) return SFMX_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr; cap = 0;
+        const size_t want = std::max<size_t>(bytes, 4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) { p = nullptr; return fail(SFMX_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e)); }
+        cap = want;
+        return SFMX_OK;
+    }
+    int copied(hipStream_t st) {     // call after enqueueing the copies that read the buffer
+        if (!busy && hipEventCreateWithFlags(&busy, hipEventDisableTiming) != hipSuccess) return fail(SFMX_EDEVICE, "hipEventCreate");
+        if (hipEventRecord(busy, st) != hipSuccess) return fail(SFMX_EDEVICE, "hipEventRecord");
+        pending = true;
+        return SFMX_OK;
+    }
+    void release() {
+        if (pending) (void)hipEventSynchronize(busy);
+        if (busy) (void)hipEventDestroy(busy);
+        if (p) (void)hipHostFree(p);
+        p = nullptr; cap = 0; busy = nullptr; pending = false;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
 int64_t align_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 
 // Device guard: set the matcher's device for the duration of a call.
@@ -120,6 +155,17 @@ struct sfmx_matcher {
     DevBuf pairs_d, work_d, work32_d, dense_idx, dense_dist, slow_list, slow_count, counts, keep, offsets, out;
     DevBuf qlist, qcount;   // two-pass SIFT path: per pair, the queries the screening pass could not settle
     DevBuf porder, work2, work2_n;   // pair order (by train image) and the compacted pass-2 work list
+    DevBuf prep_tab;                 // batched SIFT prep: one PrepImg per image
+    PinnedBuf stage_prep, stage_run; // pinned staging of the H2D uploads
+    // Run plan cache: the device pair/work lists of the last run stay valid while the
+    // pair list, the images' row counts and integrality and the kernel variant are unchanged.
+    std::vector<int32_t> plan_pairs;
+    std::vector<int64_t> plan_imgs;
+    int plan_variant = -1;
+    bool plan_valid = false;
+    int64_t plan_dense = 0;
+    size_t plan_nwork = 0, plan_nwork32 = 0;
+    int plan_max_nt = 0;
     bool has_run = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};   // run start, main kernel end, run end
     bool ev_recorded = false;
@@ -195,14 +241,24 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
             if (bytes) HIPCHK(hipMemcpyAsync((void*)src[i], imgs[i].data, bytes, hipMemcpyHostToDevice, st));
         }
     }
-    for (int i = 0; i < n; ++i) {
+    if (norm == SFMX_NORM_L2 && n > 0) {      // one launch for every image
+        if ((rc = m->stage_prep.ensure(sizeof(PrepImg) * n))) return rc;
+        if ((rc = m->prep_tab.ensure(sizeof(PrepImg) * n))) return rc;
+        PrepImg* tab = m->stage_prep.as<PrepImg>();
+        int max_pad = 0;
+        for (int i = 0; i < n; ++i) {
+            const ImgDev& d = m->imgs[i];
+            tab[i] = PrepImg{(const float*)src[i], d.rows, imgs[i].cols, d.rows_pad, 0, d.row0};
+            max_pad = std::max(max_pad, d.rows_pad);
+        }
+        HIPCHK(hipMemcpyAsync(m->prep_tab.p, tab, sizeof(PrepImg) * n, hipMemcpyHostToDevice, st));
+        if ((rc = m->stage_prep.copied(st))) return rc;
+        HIPCHK(launch_prep_l2_batch(m->prep_tab.as<PrepImg>(), n, max_pad, m->desc8.as<int8_t>(), m->normv.as<int32_t>(),
+                                    m->keyc.as<int32_t>(), m->keyc2.as<int32_t>(), m->flags.as<int32_t>(), st));
+    }
+    for (int i = 0; i < n && norm != SFMX_NORM_L2; ++i) {
         const ImgDev& d = m->imgs[i];
-        if (norm == SFMX_NORM_L2)
-            HIPCHK(launch_prep_l2((const float*)src[i], d.rows, imgs[i].cols, d.rows_pad,
-                                  m->desc8.as<int8_t>() + d.row0 * SIFT_DIM, m->normv.as<int32_t>() + d.row0,
-                                  m->keyc.as<int32_t>() + d.row0, m->keyc2.as<int32_t>() + d.row0,
-                                  m->flags.as<int32_t>() + i, st));
-        else if (m->orb_fp4)
+        if (m->orb_fp4)
             HIPCHK(launch_prep_hamming_fp4((const uint8_t*)src[i], d.rows, imgs[i].cols, d.rows_pad,
                                            m->desc8.as<uint8_t>() + d.row0 * SIFT_DIM, m->keyc.as<int32_t>() + d.row0, st));
         else
@@ -242,50 +298,84 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     if (n_pairs < 0 || (n_pairs > 0 && !pairs)) return fail(SFMX_EINVAL, "bad pair list");
     if (!(ratio == ratio)) return fail(SFMX_EINVAL, "ratio is NaN");
     DeviceGuard g(m->device);
-    std::vector<PairDev> pd(n_pairs);
-    int64_t dense = 0;
-    for (int p = 0; p < n_pairs; ++p) {
-        const int L = pairs[2 * p], R = pairs[2 * p + 1];
-        if (L < 0 || L >= m->n_imgs || R < 0 || R >= m->n_imgs) return fail(SFMX_EINVAL, "pair image index out of range");
-        pd[p] = PairDev{L, R, dense};
-        dense += m->imgs[L].rows;
-    }
-    // Work items: 512-query blocks, sorted by train image so XCD-contiguous
-    // blocks stream the same train rows (L2 reuse); fp32 pairs separately.
-    std::vector<WorkItem> work, work32;
-    std::vector<int> order(n_pairs);
-    std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pd[a].right < pd[b].right; });
-    m->fp32_pairs = 0;
-    for (int p : order) {
-        const ImgDev& L = m->imgs[pd[p].left];
-        const ImgDev& R = m->imgs[pd[p].right];
-        const bool f32path = m->norm == SFMX_NORM_L2 && !(L.integral && R.integral);
-        m->fp32_pairs += f32path;
-        const int bq = f32path ? 512 : (m->norm == SFMX_NORM_L2 ? sift_block_queries(sift_variant()) : 512);
-        for (int q0 = 0; q0 < L.rows; q0 += bq) (f32path ? work32 : work).push_back(WorkItem{p, q0});
-    }
+    // Run plan: per-pair dense offsets, the pair order by train image and the work
+    // items.  Reused (no host work, no uploads) while the pair list, the images'
+    // row counts / integrality and the kernel variant are those of the last run.
+    const int variant_key = m->norm == SFMX_NORM_L2 ? sift_variant() : 0;
+    std::vector<int64_t> img_key(2 * (size_t)m->n_imgs);
+    for (int i = 0; i < m->n_imgs; ++i) { img_key[2 * i] = m->imgs[i].rows; img_key[2 * i + 1] = m->imgs[i].integral; }
+    const bool reuse = m->plan_valid && m->plan_variant == variant_key && m->plan_imgs == img_key &&
+                       m->plan_pairs.size() == 2 * (size_t)n_pairs &&
+                       (n_pairs == 0 || std::memcmp(m->plan_pairs.data(), pairs, sizeof(int32_t) * 2 * n_pairs) == 0);
     int rc;
-    if ((rc = m->pairs_d.ensure(sizeof(PairDev) * std::max(n_pairs, 1)))) return rc;
-    if ((rc = m->work_d.ensure(sizeof(WorkItem) * std::max<size_t>(work.size(), 1)))) return rc;
-    if ((rc = m->work32_d.ensure(sizeof(WorkItem) * std::max<size_t>(work32.size(), 1)))) return rc;
-    if ((rc = m->dense_idx.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
-    if ((rc = m->dense_dist.ensure(sizeof(float) * std::max<int64_t>(dense, 1)))) return rc;
-    if ((rc = m->slow_list.ensure(sizeof(int2) * std::max<int64_t>(dense, 1)))) return rc;
-    if ((rc = m->slow_count.ensure(sizeof(int32_t)))) return rc;
-    if ((rc = m->qlist.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
-    if ((rc = m->qcount.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
-    if ((rc = m->porder.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
-    if ((rc = m->work2.ensure(sizeof(WorkItem) * std::max<size_t>(4 * work.size(), 1)))) return rc;   // pass-2 items >= 128 queries
-    if ((rc = m->work2_n.ensure(sizeof(int32_t)))) return rc;
-    if ((rc = m->counts.ensure(sizeof(int64_t) * std::max(n_pairs, 1)))) return rc;
-    if ((rc = m->keep.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
-    if ((rc = m->offsets.ensure(sizeof(int64_t) * (n_pairs + 1)))) return rc;
-    if ((rc = m->out.ensure(sizeof(DMatchDev) * std::max<int64_t>(dense, 1)))) return rc;
-    if (n_pairs) HIPCHK(hipMemcpyAsync(m->pairs_d.p, pd.data(), sizeof(PairDev) * n_pairs, hipMemcpyHostToDevice, st));
-    if (n_pairs) HIPCHK(hipMemcpyAsync(m->porder.p, order.data(), sizeof(int32_t) * n_pairs, hipMemcpyHostToDevice, st));
-    if (!work.empty()) HIPCHK(hipMemcpyAsync(m->work_d.p, work.data(), sizeof(WorkItem) * work.size(), hipMemcpyHostToDevice, st));
-    if (!work32.empty()) HIPCHK(hipMemcpyAsync(m->work32_d.p, work32.data(), sizeof(WorkItem) * work32.size(), hipMemcpyHostToDevice, st));
+    if (!reuse) {
+        m->plan_valid = false;
+        std::vector<PairDev> pd(n_pairs);
+        int64_t dense = 0;
+        for (int p = 0; p < n_pairs; ++p) {
+            const int L = pairs[2 * p], R = pairs[2 * p + 1];
+            if (L < 0 || L >= m->n_imgs || R < 0 || R >= m->n_imgs) return fail(SFMX_EINVAL, "pair image index out of range");
+            pd[p] = PairDev{L, R, dense};
+            dense += m->imgs[L].rows;
+        }
+        // Work items: 512-query blocks, sorted by train image so XCD-contiguous
+        // blocks stream the same train rows (L2 reuse); fp32 pairs separately.
+        std::vector<WorkItem> work, work32;
+        std::vector<int> order(n_pairs);
+        std::iota(order.begin(), order.end(), 0);
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pd[a].right < pd[b].right; });
+        m->fp32_pairs = 0;
+        int max_nt = 0;
+        for (int p : order) {
+            const ImgDev& L = m->imgs[pd[p].left];
+            const ImgDev& R = m->imgs[pd[p].right];
+            max_nt = std::max(max_nt, R.rows);
+            const bool f32path = m->norm == SFMX_NORM_L2 && !(L.integral && R.integral);
+            m->fp32_pairs += f32path;
+            const int bq = f32path ? 512 : (m->norm == SFMX_NORM_L2 ? sift_block_queries(sift_variant()) : 512);
+            for (int q0 = 0; q0 < L.rows; q0 += bq) (f32path ? work32 : work).push_back(WorkItem{p, q0});
+        }
+        if ((rc = m->pairs_d.ensure(sizeof(PairDev) * std::max(n_pairs, 1)))) return rc;
+        if ((rc = m->work_d.ensure(sizeof(WorkItem) * std::max<size_t>(work.size(), 1)))) return rc;
+        if ((rc = m->work32_d.ensure(sizeof(WorkItem) * std::max<size_t>(work32.size(), 1)))) return rc;
+        if ((rc = m->dense_idx.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
+        if ((rc = m->dense_dist.ensure(sizeof(float) * std::max<int64_t>(dense, 1)))) return rc;
+        if ((rc = m->slow_list.ensure(sizeof(int2) * std::max<int64_t>(dense, 1)))) return rc;
+        if ((rc = m->slow_count.ensure(sizeof(int32_t)))) return rc;
+        if ((rc = m->qlist.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
+        if ((rc = m->qcount.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
+        if ((rc = m->porder.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
+        if ((rc = m->work2.ensure(sizeof(WorkItem) * std::max<size_t>(4 * work.size(), 1)))) return rc;   // pass-2 items >= 128 queries
+        if ((rc = m->work2_n.ensure(sizeof(int32_t)))) return rc;
+        if ((rc = m->counts.ensure(sizeof(int64_t) * std::max(n_pairs, 1)))) return rc;
+        if ((rc = m->keep.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
+        if ((rc = m->offsets.ensure(sizeof(int64_t) * (n_pairs + 1)))) return rc;
+        if ((rc = m->out.ensure(sizeof(DMatchDev) * std::max<int64_t>(dense, 1)))) return rc;
+        // uploads from pinned staging: [pairs | order | work | work32], 256-B aligned parts
+        const size_t b_pd = align_up(sizeof(PairDev) * n_pairs, 256), b_or = align_up(sizeof(int32_t) * n_pairs, 256),
+                     b_w = align_up(sizeof(WorkItem) * work.size(), 256), b_w32 = sizeof(WorkItem) * work32.size();
+        if ((rc = m->stage_run.ensure(b_pd + b_or + b_w + b_w32))) return rc;
+        char* hs = m->stage_run.as<char>();
+        std::memcpy(hs, pd.data(), sizeof(PairDev) * n_pairs);
+        std::memcpy(hs + b_pd, order.data(), sizeof(int32_t) * n_pairs);
+        std::memcpy(hs + b_pd + b_or, work.data(), sizeof(WorkItem) * work.size());
+        std::memcpy(hs + b_pd + b_or + b_w, work32.data(), b_w32);
+        if (n_pairs) HIPCHK(hipMemcpyAsync(m->pairs_d.p, hs, sizeof(PairDev) * n_pairs, hipMemcpyHostToDevice, st));
+        if (n_pairs) HIPCHK(hipMemcpyAsync(m->porder.p, hs + b_pd, sizeof(int32_t) * n_pairs, hipMemcpyHostToDevice, st));
+        if (!work.empty()) HIPCHK(hipMemcpyAsync(m->work_d.p, hs + b_pd + b_or, sizeof(WorkItem) * work.size(), hipMemcpyHostToDevice, st));
+        if (!work32.empty()) HIPCHK(hipMemcpyAsync(m->work32_d.p, hs + b_pd + b_or + b_w, b_w32, hipMemcpyHostToDevice, st));
+        if ((rc = m->stage_run.copied(st))) return rc;
+        m->plan_pairs.assign(pairs, pairs + 2 * (size_t)n_pairs);
+        m->plan_imgs = img_key;
+        m->plan_variant = variant_key;
+        m->plan_dense = dense;
+        m->plan_nwork = work.size();
+        m->plan_nwork32 = work32.size();
+        m->plan_max_nt = max_nt;
+        m->plan_valid = true;
+    }
+    const int64_t dense = m->plan_dense;
+    const size_t n_work = m->plan_nwork, n_work32 = m->plan_nwork32;
     if (!m->ev[0])
         for (auto& e : m->ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipMemsetAsync(m->slow_count.p, 0, sizeof(int32_t), st));
@@ -295,7 +385,7 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     const PairDev* P = m->pairs_d.as<PairDev>();
     const ImgDev* I = m->imgs_d.as<ImgDev>();
     if (m->norm == SFMX_NORM_L2) {
-        HIPCHK(launch_sift_knn2(m->work_d.as<WorkItem>(), (int)work.size(), P, I, m->desc8.as<int8_t>(),
+        HIPCHK(launch_sift_knn2(m->work_d.as<WorkItem>(), (int)n_work, P, I, m->desc8.as<int8_t>(),
                                 m->normv.as<int32_t>(), m->keyc.as<int32_t>(), m->keyc2.as<int32_t>(),
                                 m->qlist.as<int32_t>(), m->qcount.as<int32_t>(), n_pairs, m->porder.as<int32_t>(),
                                 m->work2.as<WorkItem>(), m->work2_n.as<int32_t>(), m->dense_idx.as<int32_t>(),
@@ -303,22 +393,21 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
         HIPCHK(hipEventRecord(m->ev[1], st));
         HIPCHK(launch_sift_slow(m->slow_list.as<int2>(), m->slow_count.as<int32_t>(), P, I, m->desc8.as<int8_t>(),
                                 m->normv.as<int32_t>(), m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
-        if (!work32.empty())
-            HIPCHK(launch_sift_f32(m->work32_d.as<WorkItem>(), (int)work32.size(), P, I, m->f32.as<float>(),
+        if (n_work32)
+            HIPCHK(launch_sift_f32(m->work32_d.as<WorkItem>(), (int)n_work32, P, I, m->f32.as<float>(),
                                    m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
     } else if (m->orb_fp4) {
-        HIPCHK(launch_orb_mfma(m->work_d.as<WorkItem>(), (int)work.size(), P, I, m->desc8.as<uint8_t>(),
+        HIPCHK(launch_orb_mfma(m->work_d.as<WorkItem>(), (int)n_work, P, I, m->desc8.as<uint8_t>(),
                                m->keyc.as<int32_t>(), m->qlist.as<int32_t>(), m->qcount.as<int32_t>(), n_pairs,
                                m->porder.as<int32_t>(), m->work2.as<WorkItem>(), m->work2_n.as<int32_t>(),
                                m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
         HIPCHK(hipEventRecord(m->ev[1], st));
     } else {
-        HIPCHK(launch_orb_knn2(m->work_d.as<WorkItem>(), (int)work.size(), P, I, m->desc8.as<uint8_t>(),
+        HIPCHK(launch_orb_knn2(m->work_d.as<WorkItem>(), (int)n_work, P, I, m->desc8.as<uint8_t>(),
                                m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
         HIPCHK(hipEventRecord(m->ev[1], st));
     }
-    int max_nt = 0;
-    for (int p = 0; p < n_pairs; ++p) max_nt = std::max(max_nt, m->imgs[pd[p].right].rows);
+    const int max_nt = m->plan_max_nt;
     HIPCHK(launch_assemble(P, n_pairs, I, m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), distinct ? 1 : 0,
                            min_count, max_nt, m->counts.as<int64_t>(), m->keep.as<int32_t>(),
                            m->offsets.as<int64_t>(), m->out.as<DMatchDev>(), st));
@@ -400,7 +489,9 @@ int sfmx_matcher_destroy(sfmx_matcher* m) {
     if (!m) return SFMX_OK;
     {
         DeviceGuard g(m->device);
-        DevBuf* bufs[] = {&m->raw, &m->desc8, &m->normv, &m->keyc, &m->keyc2, &m->qlist, &m->qcount, &m->porder, &m->work2, &m->work2_n, &m->f32, &m->flags, &m->imgs_d, &m->pairs_d,
+        m->stage_prep.release();
+        m->stage_run.release();
+        DevBuf* bufs[] = {&m->raw, &m->desc8, &m->normv, &m->keyc, &m->keyc2, &m->qlist, &m->qcount, &m->porder, &m->work2, &m->work2_n, &m->f32, &m->flags, &m->imgs_d, &m->pairs_d, &m->prep_tab,
                           &m->work_d, &m->work32_d, &m->dense_idx, &m->dense_dist, &m->slow_list, &m->slow_count,
                           &m->counts, &m->keep, &m->offsets, &m->out};
         for (DevBuf* b : bufs) b->release();
