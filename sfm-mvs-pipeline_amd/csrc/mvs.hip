@@ -27,6 +27,7 @@
 // (the source read once, the destination written once).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <climits>
 #include <cmath>
@@ -47,6 +48,7 @@ constexpr int PX_PER_THREAD = 4;
 #define GPTR(T) __attribute__((address_space(1))) T*
 #define CGPTR(T) const __attribute__((address_space(1))) T*
 constexpr int THREADS = 256;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr int PX_PER_BLOCK = PX_PER_THREAD * THREADS;
 
 struct UndImg {
@@ -60,10 +62,21 @@ struct UndImg {
     int32_t dst_words;       // 1: dst rows and base are 4-byte aligned (dword stores)
     int32_t src_words;       // 1: src rows and base are 4-byte aligned and W >= 2 (dword tap loads)
     int32_t radial;          // 1: p1 = p2 = k3 = 0 (SimpleRadialCamera): the zero terms drop out exactly
+    int32_t mpitch;          // map row pitch in pixels (bpr * PX_PER_BLOCK) when `map` is set
+    const int2* map;         // shared inverse map (iu, iv) of this image's unit, or null: computed per pixel
     double w;                // 1/_w = 1/ir[8]
     double t0, t2;           // ir[0], ir[2]
     double K0, K5, d, t4, t8;
     double fx, fy, u0, v0, k1, k2, p1, p2, k3;
+};
+
+// A run of launch blocks: g images whose blocks are interleaved image-fastest
+// (block rb -> image first + rb % g, row block rb / g), so images that share one
+// inverse map (same size, K and distortion -- the reference's toOpenMVS export:
+// one camera for every shot) read each map tile g times while it sits in L2.
+struct UndUnit {
+    int64_t blk0;            // first block of the unit in the launch
+    int32_t first, g;        // image range [first, first + g) of the launch's image array
 };
 
 // cvRound of a double on x86 (cvtsd2si): round half to even, and the
@@ -110,11 +123,9 @@ __device__ __forceinline__ void fetch_taps(CGPTR(uint8_t) row, int bx, bool two,
     }
 }
 
-// One thread: PX_PER_THREAD consecutive pixels of row Y.  Three phases so the
-// tap loads of all pixels are in flight together: (1) the inverse map of every
-// pixel in fp64, (2) the 2 x PX tap-pair loads, (3) the fixed-point blends.
-template <int C, bool WORDS>
-__device__ __forceinline__ void undistort_px(const UndImg& im, int Y, int x0) {
+// initUndistortRectifyMap for PX_PER_THREAD consecutive pixels of row Y (columns
+// past the last one repeat it): source position in 1/32 px, as cvRound gives it.
+__device__ __forceinline__ void map4(const UndImg& im, int Y, int x0, int (&iu)[PX_PER_THREAD], int (&iv)[PX_PER_THREAD]) {
     // per row: the stripe's inverse (cv::invert adjugate; see header comment)
     const int ys = (Y / im.stripe0) * im.stripe0;
     const int i = Y - ys;
@@ -124,14 +135,9 @@ __device__ __forceinline__ void undistort_px(const UndImg& im, int Y, int x0) {
     const double y = yr * im.w;                             // w = 1/_w, _w = i*ir[7] + ir[8] = ir[8]
     const double y2 = y * y;
 
-    const int W = im.W, H = im.H;
-    CGPTR(uint8_t) S = (CGPTR(uint8_t))im.src;
-    const unsigned sp = (unsigned)im.src_pitch;
+    const int W = im.W;
     CGPTR(double) xc = (CGPTR(double))im.xcol;
     const bool radial = im.radial;
-
-    // (1) map: source position in 1/32 px
-    int iu[PX_PER_THREAD], iv[PX_PER_THREAD];
 #pragma unroll
     for (int p = 0; p < PX_PER_THREAD; ++p) {
         const int j = min(x0 + p, W - 1);
@@ -155,6 +161,28 @@ __device__ __forceinline__ void undistort_px(const UndImg& im, int Y, int x0) {
         }
         iu[p] = cv_round(u * 32);
         iv[p] = cv_round(v * 32);
+    }
+}
+
+// One thread: PX_PER_THREAD consecutive pixels of row Y.  Three phases so the
+// tap loads of all pixels are in flight together: (1) the inverse map of every
+// pixel in fp64, (2) the 2 x PX tap-pair loads, (3) the fixed-point blends.
+template <int C, bool WORDS, bool MAPPED>
+__device__ __forceinline__ void undistort_px(const UndImg& im, int Y, int x0) {
+    const int W = im.W, H = im.H;
+    CGPTR(uint8_t) S = (CGPTR(uint8_t))im.src;
+    const unsigned sp = (unsigned)im.src_pitch;
+
+    // (1) map: source position in 1/32 px -- from the unit's shared map, or computed here
+    int iu[PX_PER_THREAD], iv[PX_PER_THREAD];
+    if constexpr (MAPPED) {
+        CGPTR(i32x4) m = (CGPTR(i32x4))(im.map + (int64_t)Y * im.mpitch + x0);
+        static_assert(PX_PER_THREAD == 4, "two 16-byte map loads per thread");
+        const i32x4 m0 = m[0], m1 = m[1];
+        iu[0] = m0.x; iv[0] = m0.y; iu[1] = m0.z; iv[1] = m0.w;
+        iu[2] = m1.x; iv[2] = m1.y; iu[3] = m1.z; iv[3] = m1.w;
+    } else {
+        map4(im, Y, x0, iu, iv);
     }
     // (2) taps.  Both taps of a row come from the pixel pair (bx, bx + 1), bx
     // clamped into [0, W - 2]; at the borders the in-image tap is the pair's
@@ -210,45 +238,73 @@ __device__ __forceinline__ void undistort_px(const UndImg& im, int Y, int x0) {
     }
 }
 
-template <int C>
-__global__ __launch_bounds__(THREADS)
-void undistort_kernel(const UndImg* __restrict__ imgs, int n_imgs, int n_blocks) {
-    // XCD-aware order: hardware dispatches block b to XCD b % 8; give every XCD a
-    // contiguous run of logical blocks so adjacent rows share its L2.
+// Logical block of a launch: hardware dispatches block b to XCD b % 8; give every
+// XCD a contiguous run of logical blocks so neighbouring blocks share its L2.
+__device__ __forceinline__ int xcd_block(int n_blocks) {
     const int b = blockIdx.x;
     const int q = n_blocks / 8, r = n_blocks % 8;
     const int xcd = b % 8, idx = b / 8;
-    const int lb = xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
-    int lo = 0, hi = n_imgs - 1;
+    return xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+}
+
+__device__ __forceinline__ int find_unit(const UndUnit* __restrict__ units, int n_units, int lb) {
+    int lo = 0, hi = n_units - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (imgs[mid].blk0 <= lb) lo = mid; else hi = mid - 1;
+        if (units[mid].blk0 <= lb) lo = mid; else hi = mid - 1;
     }
-    const UndImg& im = imgs[lo];
-    const int rb = lb - (int)im.blk0;
+    return lo;
+}
+
+template <int C>
+__global__ __launch_bounds__(THREADS)
+void undistort_kernel(const UndUnit* __restrict__ units, int n_units, const UndImg* __restrict__ imgs, int n_blocks) {
+    const int lb = xcd_block(n_blocks);
+    const UndUnit& u = units[find_unit(units, n_units, lb)];
+    const int rb = lb - (int)u.blk0;
+    const int rest = rb / u.g;
+    const UndImg& im = imgs[u.first + (rb - rest * u.g)];
+    const int Y = rest / im.bpr;
+    const int x0 = (rest - Y * im.bpr) * PX_PER_BLOCK + (int)threadIdx.x * PX_PER_THREAD;
+    if (Y >= im.H || x0 >= im.W) return;
+    if (im.map) {
+        if (im.src_words) undistort_px<C, true, true>(im, Y, x0);
+        else undistort_px<C, false, true>(im, Y, x0);
+    } else {
+        if (im.src_words) undistort_px<C, true, false>(im, Y, x0);
+        else undistort_px<C, false, false>(im, Y, x0);
+    }
+}
+
+// The shared inverse map of every unit with g >= 2, from its first image: (iu, iv)
+// per pixel, rows padded to mpitch with the last column repeated (map4 clamps).
+// units[k].first = that image; g = 1.
+__global__ __launch_bounds__(THREADS)
+void map_kernel(const UndUnit* __restrict__ units, int n_units, const UndImg* __restrict__ imgs, int n_blocks) {
+    const int lb = xcd_block(n_blocks);
+    const UndUnit& u = units[find_unit(units, n_units, lb)];
+    const UndImg& im = imgs[u.first];
+    const int rb = lb - (int)u.blk0;
     const int Y = rb / im.bpr;
     const int x0 = (rb - Y * im.bpr) * PX_PER_BLOCK + (int)threadIdx.x * PX_PER_THREAD;
-    if (Y >= im.H || x0 >= im.W) return;
-    if (im.src_words) undistort_px<C, true>(im, Y, x0);
-    else undistort_px<C, false>(im, Y, x0);
+    if (Y >= im.H) return;
+    int iu[PX_PER_THREAD], iv[PX_PER_THREAD];
+    map4(im, Y, x0, iu, iv);
+    GPTR(i32x4) m = (GPTR(i32x4))(const_cast<int2*>(im.map) + (int64_t)Y * im.mpitch + x0);
+    m[0] = i32x4{iu[0], iv[0], iu[1], iv[1]};
+    m[1] = i32x4{iu[2], iv[2], iu[3], iv[3]};
 }
 
 // initUndistortRectifyMap's running sum _x += ir[0] (from _x = ir[2]) and the
-// row-invariant x = _x * (1/_w), x*x: one thread per image, sequential as in the
-// reference loop (a few microseconds per image).
-__global__ void xcol_kernel(const UndImg* __restrict__ imgs, int n) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n) return;
-    // fields to registers first: the table aliases the descriptor buffer, so the
-    // compiler would otherwise reload them after every store
-    const int W = imgs[g].W;
-    const double t0 = imgs[g].t0, t2 = imgs[g].t2, w = imgs[g].w;
-    double* __restrict__ xc = const_cast<double*>(reinterpret_cast<const double*>(imgs[g].xcol));
-    double xs = 0.0 + t2;
-    for (int j = 0; j < W; ++j, xs += t0) {
-        const double x = xs * w;
-        xc[2 * j] = x;
-        xc[2 * j + 1] = x * x;
+// row-invariant x = _x * (1/_w), x*x, for one image: sequential as in the
+// reference loop.  Host code: one dependent fp64 add per column is a few
+// microseconds on a CPU core (and ~25 ns per column as a single GPU lane); IEEE
+// binary64 add/mul round identically on both, and no a*b+c here can fuse.
+static void xcol_table(const UndImg& u, double2* xc) {
+    double xs = 0.0 + u.t2;
+    for (int j = 0; j < u.W; ++j, xs += u.t0) {
+        const double x = xs * u.w;
+        xc[j] = make_double2(x, x * x);
     }
 }
 
@@ -349,42 +405,32 @@ int sfmx_undistort_images(const sfmx_undistort_image* images, int32_t n_images, 
     {
         Bufs b;   // host-mode staging only
         std::vector<UndImg> h(n_images);
-        int64_t ncol = 0;
-        int cnt_c[5] = {0, 0, 0, 0, 0}, first_c[5] = {0, 0, 0, 0, 0};
-        int64_t blk_c[5] = {0, 0, 0, 0, 0};
         std::vector<uint8_t*> staged_dst(n_images);
-        for (int n = 0; n < n_images; ++n) ncol += images[n].width;
-        const size_t img_bytes = (sizeof(UndImg) * n_images + 255) & ~(size_t)255;
-        auto* scratch = static_cast<uint8_t*>(g_scratch.get(device, img_bytes + sizeof(double2) * ncol));
-        auto* dimg = reinterpret_cast<UndImg*>(scratch);
-        auto* dcol = reinterpret_cast<double2*>(scratch + img_bytes);
-        if (!scratch) { rc = SFMX_ENOMEM; goto done; }
-        {
-            int64_t co = 0;
-            for (int n = 0; n < n_images; ++n) {
-                const sfmx_undistort_image& g = images[n];
-                UndImg& u = h[n];
-                u.W = g.width; u.H = g.height; u.C = g.channels;
-                u.stripe0 = std::min(std::max(1, (1 << 12) / std::max(g.width, 1)), g.height);
-                u.bpr = (g.width + PX_PER_BLOCK - 1) / PX_PER_BLOCK;
-                // cv::invert (3x3, DECOMP_LU) of the stripe's new camera matrix: det3 and
-                // the adjugate rows that do not depend on the stripe (header comment)
-                const double K0 = g.K[0], K2 = g.K[2], K4 = g.K[4];
-                const double det = K0 * K4;
-                const double d = 1. / det;
-                const double t0 = K4 * d, t2 = (0.0 - K2 * K4) * d;
-                u.K0 = K0; u.K5 = g.K[5]; u.d = d;
-                u.t4 = K0 * d; u.t8 = det * d;
-                u.fx = K0; u.fy = K4; u.u0 = K2; u.v0 = g.K[5];
-                u.k1 = g.dist[0]; u.k2 = g.dist[1]; u.p1 = g.dist[2]; u.p2 = g.dist[3]; u.k3 = g.dist[4];
-                u.w = 1. / u.t8;                                       // 1/_w, the same for every row
-                u.t0 = t0; u.t2 = t2;                                  // column table: xcol_kernel
-                u.radial = (g.dist[2] == 0 && g.dist[3] == 0 && g.dist[4] == 0) ? 1 : 0;
-                u.xcol = dcol + co;
-                co += g.width;
-                u.src_pitch = g.src_pitch; u.dst_pitch = g.dst_pitch;
-                u.src = g.src; u.dst = g.dst;
-            }
+        for (int n = 0; n < n_images; ++n) {
+            const sfmx_undistort_image& g = images[n];
+            UndImg& u = h[n];
+            u.W = g.width; u.H = g.height; u.C = g.channels;
+            u.stripe0 = std::min(std::max(1, (1 << 12) / std::max(g.width, 1)), g.height);
+            u.bpr = (g.width + PX_PER_BLOCK - 1) / PX_PER_BLOCK;
+            // cv::invert (3x3, DECOMP_LU) of the stripe's new camera matrix: det3 and
+            // the adjugate rows that do not depend on the stripe (header comment)
+            const double K0 = g.K[0], K2 = g.K[2], K4 = g.K[4];
+            const double det = K0 * K4;
+            const double d = 1. / det;
+            const double t0 = K4 * d, t2 = (0.0 - K2 * K4) * d;
+            u.K0 = K0; u.K5 = g.K[5]; u.d = d;
+            u.t4 = K0 * d; u.t8 = det * d;
+            u.fx = K0; u.fy = K4; u.u0 = K2; u.v0 = g.K[5];
+            u.k1 = g.dist[0]; u.k2 = g.dist[1]; u.p1 = g.dist[2]; u.p2 = g.dist[3]; u.k3 = g.dist[4];
+            u.w = 1. / u.t8;                                       // 1/_w, the same for every row
+            u.t0 = t0; u.t2 = t2;                                  // column table: xcol_table
+            u.radial = (g.dist[2] == 0 && g.dist[3] == 0 && g.dist[4] == 0) ? 1 : 0;
+            u.mpitch = u.bpr * PX_PER_BLOCK;
+            u.map = nullptr;
+            u.xcol = nullptr;
+            u.blk0 = 0;                                            // unused by the kernels (units carry it)
+            u.src_pitch = g.src_pitch; u.dst_pitch = g.dst_pitch;
+            u.src = g.src; u.dst = g.dst;
         }
         if (!inputs_on_device) {   // stage every image on the device, packed rows
             for (int n = 0; n < n_images; ++n) {
@@ -414,30 +460,91 @@ int sfmx_undistort_images(const sfmx_undistort_image* images, int32_t n_images, 
             u.src_words = (safe && (uintptr_t)u.src % 4 == 0 && u.src_pitch % 4 == 0 && u.W >= 2) ? 1 : 0;
         }
         for (int n = 0; n < n_images; ++n) staged_dst[n] = h[n].dst;
-        // one launch per channel count (the kernel is specialised on it): images grouped by C
-        std::stable_sort(h.begin(), h.end(), [](const UndImg& p, const UndImg& q) { return p.C < q.C; });
-        for (const UndImg& u : h) {
-            if (cnt_c[u.C] == 0) first_c[u.C] = (int)(&u - h.data());
-            cnt_c[u.C]++;
-        }
-        for (UndImg& u : h) {
-            u.blk0 = blk_c[u.C];
-            blk_c[u.C] += (int64_t)u.bpr * u.H;
-        }
-        UCHK(hipMemcpyAsync(dimg, h.data(), sizeof(UndImg) * n_images, hipMemcpyHostToDevice, st));
         {
+            // Launch order: by channel count (one launch each, the kernel is specialised
+            // on it), then by the inputs of the inverse map (size, K, distortion), so
+            // images sharing a map are adjacent and form one unit.
+            // bitwise key: a total order, and equal keys = identical maps
+            auto key = [](const UndImg& u) {
+                std::array<uint64_t, 12> k{(uint64_t)u.C, (uint64_t)u.W, (uint64_t)u.H};
+                const double v[9] = {u.fx, u.fy, u.u0, u.v0, u.k1, u.k2, u.p1, u.p2, u.k3};
+                std::memcpy(k.data() + 3, v, sizeof v);
+                return k;
+            };
+            auto same_map = [&](const UndImg& p, const UndImg& q) { return key(p) == key(q); };
+            std::stable_sort(h.begin(), h.end(), [&](const UndImg& p, const UndImg& q) { return key(p) < key(q); });
+            std::vector<UndUnit> units, maps;                     // units: per C contiguous; maps: g >= 2 units
+            int ufirst_c[5] = {0, 0, 0, 0, 0}, ucnt_c[5] = {0, 0, 0, 0, 0};
+            int64_t blk_c[5] = {0, 0, 0, 0, 0}, map_blocks = 0, map_bytes = 0;
+            std::vector<int64_t> map_off;                         // per maps entry: byte offset in the map area
+            for (int n = 0; n < n_images;) {
+                int e = n + 1;
+                while (e < n_images && same_map(h[n], h[e])) ++e;
+                const int c = h[n].C;
+                if (ucnt_c[c] == 0) ufirst_c[c] = (int)units.size();
+                ucnt_c[c]++;
+                const int64_t blocks = (int64_t)h[n].bpr * h[n].H;
+                units.push_back(UndUnit{blk_c[c], n, e - n});
+                blk_c[c] += blocks * (e - n);
+                if (e - n >= 2) {
+                    maps.push_back(UndUnit{map_blocks, n, 1});
+                    map_off.push_back(map_bytes);
+                    map_blocks += blocks;
+                    map_bytes += ((int64_t)h[n].mpitch * h[n].H * (int64_t)sizeof(int2) + 255) & ~(int64_t)255;
+                }
+                n = e;
+            }
+            for (int c = 1; c <= 4; ++c)
+                if (blk_c[c] >= (int64_t)INT32_MAX) { set_last_error("images too large for one launch"); rc = SFMX_EINVAL; goto done; }
+            if (map_blocks >= (int64_t)INT32_MAX) { set_last_error("images too large for one launch"); rc = SFMX_EINVAL; goto done; }
+            // device scratch: descriptors | units | map jobs | column tables | maps
+            auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+            const size_t o_units = al(sizeof(UndImg) * n_images);
+            const size_t o_maps = o_units + al(sizeof(UndUnit) * units.size());
+            std::vector<int> need;                                // images whose map is computed from xcol
+            for (const UndUnit& q : units) need.push_back(q.first);   // singleton, or the map's source
+            const size_t o_col = o_maps + al(sizeof(UndUnit) * std::max<size_t>(maps.size(), 1));
+            int64_t ncol_need = 0;
+            for (int i : need) ncol_need += h[i].W;
+            const size_t o_map = o_col + al(sizeof(double2) * ncol_need);
+            auto* scratch = static_cast<uint8_t*>(g_scratch.get(device, o_map + (size_t)map_bytes));
+            if (!scratch) { rc = SFMX_ENOMEM; goto done; }
+            auto* dimg = reinterpret_cast<UndImg*>(scratch);
+            auto* dunits = reinterpret_cast<UndUnit*>(scratch + o_units);
+            auto* dmaps = reinterpret_cast<UndUnit*>(scratch + o_maps);
+            auto* dcol = reinterpret_cast<double2*>(scratch + o_col);
+            std::vector<uint8_t> blob(o_map);
+            {
+                int64_t co = 0;
+                for (int i : need) {
+                    h[i].xcol = dcol + co;                     // the unit's other images never read it
+                    xcol_table(h[i], reinterpret_cast<double2*>(blob.data() + o_col) + co);
+                    co += h[i].W;
+                }
+            }
+            for (size_t k = 0; k < maps.size(); ++k) {
+                const UndUnit& m = maps[k];
+                const UndUnit* un = nullptr;
+                for (const UndUnit& q : units) if (q.first == m.first) { un = &q; break; }
+                auto* mp = reinterpret_cast<int2*>(scratch + o_map + map_off[k]);
+                for (int i = un->first; i < un->first + un->g; ++i) h[i].map = mp;
+            }
+            std::memcpy(blob.data(), h.data(), sizeof(UndImg) * n_images);
+            std::memcpy(blob.data() + o_units, units.data(), sizeof(UndUnit) * units.size());
+            if (!maps.empty()) std::memcpy(blob.data() + o_maps, maps.data(), sizeof(UndUnit) * maps.size());
+            UCHK(hipMemcpyAsync(scratch, blob.data(), o_map, hipMemcpyHostToDevice, st));
             hipEvent_t e0 = g_scratch.e0, e1 = g_scratch.e1;
             UCHK(hipEventRecord(e0, st));
-            xcol_kernel<<<(n_images + 63) / 64, 64, 0, st>>>(dimg, n_images);
+            if (map_blocks)
+                map_kernel<<<(unsigned)map_blocks, THREADS, 0, st>>>(dmaps, (int)maps.size(), dimg, (int)map_blocks);
             for (int c = 1; c <= 4; ++c) {
-                if (cnt_c[c] == 0) continue;
-                const int64_t nb = blk_c[c];
-                if (nb >= (int64_t)INT32_MAX) { set_last_error("images too large for one launch"); rc = SFMX_EINVAL; goto done; }
-                const UndImg* di = dimg + first_c[c];
-                if (c == 1) undistort_kernel<1><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], (int)nb);
-                if (c == 2) undistort_kernel<2><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], (int)nb);
-                if (c == 3) undistort_kernel<3><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], (int)nb);
-                if (c == 4) undistort_kernel<4><<<(unsigned)nb, THREADS, 0, st>>>(di, cnt_c[c], (int)nb);
+                if (ucnt_c[c] == 0) continue;
+                const int nb = (int)blk_c[c];
+                const UndUnit* du = dunits + ufirst_c[c];
+                if (c == 1) undistort_kernel<1><<<(unsigned)nb, THREADS, 0, st>>>(du, ucnt_c[c], dimg, nb);
+                if (c == 2) undistort_kernel<2><<<(unsigned)nb, THREADS, 0, st>>>(du, ucnt_c[c], dimg, nb);
+                if (c == 3) undistort_kernel<3><<<(unsigned)nb, THREADS, 0, st>>>(du, ucnt_c[c], dimg, nb);
+                if (c == 4) undistort_kernel<4><<<(unsigned)nb, THREADS, 0, st>>>(du, ucnt_c[c], dimg, nb);
                 UCHK(hipGetLastError());
             }
             UCHK(hipEventRecord(e1, st));

@@ -75,3 +75,43 @@ def test_to_openmvs_end_to_end(tmp_path):
             np.testing.assert_array_equal(und[name], oracle.undistort(images[s], small[c][2], dists[c]))
         else:
             assert name not in und
+
+
+def test_shared_map_units_bit_exact():
+    """Images with identical size, K and distortion (the reference's toOpenMVS: one
+    camera for every shot) form one unit that reads a shared inverse map
+    (map_kernel); mixed here with singleton images, other channel counts, a
+    second shared camera, a -0.0 distortion term (bitwise-different key: its own
+    unit) and, in device mode, padded rows and unaligned destinations inside a unit."""
+    import torch
+    import sfmx
+    rng = np.random.default_rng(21)
+    KA, dA = mvs_cases.camera(rng, 61, 203)
+    dA[2:] = 0
+    KB, dB = mvs_cases.camera(rng, 40, 1030, strength=2.0)
+    dAz = dA.copy()
+    dAz[4] = -0.0
+    spec = [(61, 203, 3, KA, dA), (40, 1030, 1, KB, dB), (61, 203, 3, KA, dA), (61, 203, 1, KA, dA),
+            (61, 203, 3, KA, dAz), (40, 1030, 1, KB, dB), (61, 203, 3, KA, dA), (61, 203, 1, KA, dA),
+            (40, 1030, 1, KB, dB), (33, 47, 3, KA, dA)]
+    imgs = [mvs_cases.image(rng, h, w, cn) for (h, w, cn, _, _) in spec]
+    want = [oracle.undistort(i, K, d) for i, (_, _, _, K, d) in zip(imgs, spec)]
+    got = sfmx.mvs.undistort(imgs, [s[3] for s in spec], [s[4] for s in spec])
+    for g, w_, s in zip(got, want, spec):
+        np.testing.assert_array_equal(g, w_, err_msg=f"host mode {s[:3]}")
+    dev = torch.device("cuda:0")
+    srcs, dsts, parents = [], [], []
+    for k, (img, (h, w, cn, _, _)) in enumerate(zip(imgs, spec)):
+        tail = (cn,) if cn > 1 else ()
+        pad = 3 if k % 2 else 0
+        big = torch.zeros((h, w + pad) + tail, dtype=torch.uint8, device=dev)
+        big[:, :w] = torch.from_numpy(img).to(dev)
+        srcs.append(big[:, :w])
+        off = k % 3
+        out = torch.full((h, w + 2) + tail, 9, dtype=torch.uint8, device=dev)
+        dsts.append(out[:, off:off + w])
+        parents.append(out)
+    sfmx.mvs.undistort_device(srcs, dsts, [s[3] for s in spec], [s[4] for s in spec])
+    torch.cuda.synchronize()
+    for d, w_, s in zip(dsts, want, spec):
+        np.testing.assert_array_equal(d.cpu().numpy(), w_, err_msg=f"device mode {s[:3]}")

@@ -15,6 +15,8 @@ dsts = [torch.empty_like(t) for t in srcs]
 rng = np.random.default_rng(1)
 Ks = [np.array([[4000.0, 0, 2000.3], [0, 4000.0, 1500.2], [0, 0, 1]]) for _ in range(N)]
 ds = [np.array([rng.normal(0, 0.1), rng.normal(0, 0.03), 0, 0, 0]) for _ in range(N)]
+if os.environ.get("MVS_DISTINCT", "0") != "1":   # the reference's export: one camera for every shot
+    ds = [ds[0]] * N
 for _ in range(int(os.environ.get("MVS_REPS", "5"))):
     mvs.undistort_device(srcs, dsts, Ks, ds)
     print(f"kernel_ms {mvs.last_kernel_ms():.3f}", flush=True)
