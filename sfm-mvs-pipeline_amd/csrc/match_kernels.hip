@@ -121,10 +121,17 @@ __device__ __forceinline__ void prep_l2_row(const float* __restrict__ src, int r
     int v[4] = {0, 0, 0, 0};
     bool bad = false;
     if (r < rows) {
+        float f4[4] = {0.f, 0.f, 0.f, 0.f};
+        if (cols == SIFT_DIM && ((uintptr_t)src & 15) == 0) {   // full 512-B rows: one 16-B load per lane
+            const float4 q = reinterpret_cast<const float4*>(src + (int64_t)r * SIFT_DIM)[c4];
+            f4[0] = q.x; f4[1] = q.y; f4[2] = q.z; f4[3] = q.w;
+        } else {
+            for (int e = 0; e < 4; ++e)
+                if (c4 * 4 + e < cols) f4[e] = src[(int64_t)r * cols + c4 * 4 + e];
+        }
         for (int e = 0; e < 4; ++e) {
-            const int c = c4 * 4 + e;
-            if (c < cols) {
-                const float f = src[(int64_t)r * cols + c];
+            if (c4 * 4 + e < cols) {
+                const float f = f4[e];
                 const bool ok = (f >= 0.f) && (f <= 255.f) && (f == __builtin_floorf(f));
                 bad |= !ok;
                 v[e] = ok ? (int)f - 128 : 0;

@@ -156,7 +156,7 @@ struct sfmx_matcher {
     DevBuf qlist, qcount;   // two-pass SIFT path: per pair, the queries the screening pass could not settle
     DevBuf porder, work2, work2_n;   // pair order (by train image) and the compacted pass-2 work list
     DevBuf prep_tab;                 // batched SIFT prep: one PrepImg per image
-    PinnedBuf stage_prep, stage_run; // pinned staging of the H2D uploads
+    PinnedBuf stage_prep, stage_run, stage_imgs, stage_flags; // pinned staging of the small uploads / flag readback
     // Run plan cache: the device pair/work lists of the last run stay valid while the
     // pair list, the images' row counts and integrality and the kernel variant are unchanged.
     std::vector<int32_t> plan_pairs;
@@ -267,8 +267,9 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
     }
     m->any_nonintegral = false;
     if (norm == SFMX_NORM_L2 && n > 0) {
-        std::vector<int32_t> fl(n);
-        HIPCHK(hipMemcpyAsync(fl.data(), m->flags.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+        if ((rc = m->stage_flags.ensure(sizeof(int32_t) * n))) return rc;
+        const int32_t* fl = m->stage_flags.as<int32_t>();
+        HIPCHK(hipMemcpyAsync(m->stage_flags.p, m->flags.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         for (int i = 0; i < n; ++i) {
             m->imgs[i].integral = fl[i] ? 0 : 1;
@@ -286,7 +287,12 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
     }
     if (norm == SFMX_NORM_L2 && getenv("SFMX_PROBE_XOR80"))   // timing probe only (wrong results)
         HIPCHK(launch_probe_xor80(m->desc8.as<int8_t>(), (int64_t)row * SIFT_DIM, st));
-    if (n > 0) HIPCHK(hipMemcpyAsync(m->imgs_d.p, m->imgs.data(), sizeof(ImgDev) * n, hipMemcpyHostToDevice, st));
+    if (n > 0) {
+        if ((rc = m->stage_imgs.ensure(sizeof(ImgDev) * n))) return rc;
+        std::memcpy(m->stage_imgs.p, m->imgs.data(), sizeof(ImgDev) * n);
+        HIPCHK(hipMemcpyAsync(m->imgs_d.p, m->stage_imgs.p, sizeof(ImgDev) * n, hipMemcpyHostToDevice, st));
+        if ((rc = m->stage_imgs.copied(st))) return rc;
+    }
     if (!device_src) HIPCHK(hipStreamSynchronize(st));   // host buffers may be released by the caller
     return SFMX_OK;
 }
@@ -491,6 +497,8 @@ int sfmx_matcher_destroy(sfmx_matcher* m) {
         DeviceGuard g(m->device);
         m->stage_prep.release();
         m->stage_run.release();
+        m->stage_imgs.release();
+        m->stage_flags.release();
         DevBuf* bufs[] = {&m->raw, &m->desc8, &m->normv, &m->keyc, &m->keyc2, &m->qlist, &m->qcount, &m->porder, &m->work2, &m->work2_n, &m->f32, &m->flags, &m->imgs_d, &m->pairs_d, &m->prep_tab,
                           &m->work_d, &m->work32_d, &m->dense_idx, &m->dense_dist, &m->slow_list, &m->slow_count,
                           &m->counts, &m->keep, &m->offsets, &m->out};

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libsfmx.so")
+# SFMX_LIB_NAME: another in-tree build under lib/ (A/B timing of two builds in one run, tools/ab_build.sh)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", os.path.basename(os.environ.get("SFMX_LIB_NAME", "libsfmx.so")))
 
 SFMX_OK, SFMX_EINVAL, SFMX_ENOMEM, SFMX_EDEVICE, SFMX_ECAPACITY, SFMX_ESTATE = 0, -1, -2, -3, -4, -5
 SFMX_NORM_L2, SFMX_NORM_HAMMING = 4, 6
