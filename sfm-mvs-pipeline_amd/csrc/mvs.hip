@@ -184,47 +184,84 @@ __device__ __forceinline__ void undistort_px(const UndImg& im, int Y, int x0) {
     } else {
         map4(im, Y, x0, iu, iv);
     }
-    // (2) taps.  Both taps of a row come from the pixel pair (bx, bx + 1), bx
-    // clamped into [0, W - 2]; at the borders the in-image tap is the pair's
-    // first (sx = -1) or second (sx = W - 1) pixel, the other tap weighs 0.
-    uint32_t ta0[PX_PER_THREAD], ta1[PX_PER_THREAD], tb0[PX_PER_THREAD], tb1[PX_PER_THREAD];
+    // Interior threads (every pixel's four taps inside the image -- all but the
+    // border bands of a photo) skip the clamps, the tap-validity weights and the
+    // border tap selection; the general path below handles the rest.  In the
+    // interior the two paths compute the same sums term for term, except that
+    // the saturated w0 (a = bb = 0) is left at 32768: its taps' other weights are
+    // 0, so s = p*32768 vs p*32767 and (s + 16384) >> 15 = p either way (p <= 255).
+    bool interior = W >= 2 && H >= 2;
 #pragma unroll
     for (int p = 0; p < PX_PER_THREAD; ++p) {
         const int sx = (int)(short)(iu[p] >> 5), sy = (int)(short)(iv[p] >> 5);
-        const int bx = W >= 2 ? min(max(sx, 0), W - 2) : 0;
-        const unsigned cy0 = (unsigned)min(max(sy, 0), H - 1), cy1 = (unsigned)min(max(sy + 1, 0), H - 1);
-        // row offsets: cy < 2^15 and pitch < 2^24 (checked on the host) -> 24-bit multiplies
-        fetch_taps<C, WORDS>(S + __umul24(cy0, sp), bx, W >= 2, ta0[p], ta1[p]);
-        fetch_taps<C, WORDS>(S + __umul24(cy1, sp), bx, W >= 2, tb0[p], tb1[p]);
+        interior = interior && (unsigned)sx <= (unsigned)(W - 2) && (unsigned)sy <= (unsigned)(H - 2);
     }
-    // (3) blend: cv::remap INTER_LINEAR, 15-bit weights, BORDER_CONSTANT 0
     uint32_t out[C];                                        // 4 px x C bytes, packed
 #pragma unroll
     for (int k = 0; k < C; ++k) out[k] = 0;
+    if (interior) {
+        uint32_t ta0[PX_PER_THREAD], ta1[PX_PER_THREAD], tb0[PX_PER_THREAD], tb1[PX_PER_THREAD];
 #pragma unroll
-    for (int p = 0; p < PX_PER_THREAD; ++p) {
-        const int sx = (int)(short)(iu[p] >> 5), sy = (int)(short)(iv[p] >> 5);
-        const int a = iu[p] & 31, bb = iv[p] & 31;
-        const bool x0in = (unsigned)sx < (unsigned)W, x1in = (unsigned)(sx + 1) < (unsigned)W;
-        const bool y0in = (unsigned)sy < (unsigned)H, y1in = (unsigned)(sy + 1) < (unsigned)H;
-        int w0 = (32 - bb) * (32 - a) * 32;
-        if (w0 == 32768) w0 = 32767;                        // saturate_cast<short> of the table entry
-        w0 = (y0in && x0in) ? w0 : 0;
-        const int w1 = (y0in && x1in) ? (32 - bb) * a * 32 : 0;
-        const int w2 = (y1in && x0in) ? bb * (32 - a) * 32 : 0;
-        const int w3 = (y1in && x1in) ? bb * a * 32 : 0;
-        uint32_t a0 = ta0[p], a1 = ta1[p], b0 = tb0[p], b1 = tb1[p];
-        if (W == 1) { a1 = a0; b1 = b0; }
-        const bool first_is_t1 = sx < 0, second_is_t0 = sx >= W - 1;
-        const uint32_t p00 = second_is_t0 ? a1 : a0, p01 = first_is_t1 ? a0 : a1;
-        const uint32_t p10 = second_is_t0 ? b1 : b0, p11 = first_is_t1 ? b0 : b1;
+        for (int p = 0; p < PX_PER_THREAD; ++p) {
+            const int sx = (int)(short)(iu[p] >> 5), sy = (int)(short)(iv[p] >> 5);
+            CGPTR(uint8_t) r0 = S + __umul24((unsigned)sy, sp);
+            fetch_taps<C, WORDS>(r0, sx, true, ta0[p], ta1[p]);
+            fetch_taps<C, WORDS>(r0 + sp, sx, true, tb0[p], tb1[p]);
+        }
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const int s = (int)((p00 >> (8 * c)) & 255) * w0 + (int)((p01 >> (8 * c)) & 255) * w1 +
-                          (int)((p10 >> (8 * c)) & 255) * w2 + (int)((p11 >> (8 * c)) & 255) * w3;
-            const uint32_t o = (uint32_t)((s + 16384) >> 15);   // 0 <= s <= 255 * 32768: no saturation needed
-            const int byte = p * C + c;                     // compile-time after unrolling
-            out[byte >> 2] |= o << (8 * (byte & 3));
+        for (int p = 0; p < PX_PER_THREAD; ++p) {
+            const int a = iu[p] & 31, bb = iv[p] & 31;
+            const int w0 = (32 - bb) * (32 - a) * 32, w1 = (32 - bb) * a * 32;
+            const int w2 = bb * (32 - a) * 32, w3 = bb * a * 32;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int s = (int)((ta0[p] >> (8 * c)) & 255) * w0 + (int)((ta1[p] >> (8 * c)) & 255) * w1 +
+                              (int)((tb0[p] >> (8 * c)) & 255) * w2 + (int)((tb1[p] >> (8 * c)) & 255) * w3;
+                const uint32_t o = (uint32_t)((s + 16384) >> 15);
+                const int byte = p * C + c;
+                out[byte >> 2] |= o << (8 * (byte & 3));
+            }
+        }
+    } else {
+        // (2) taps.  Both taps of a row come from the pixel pair (bx, bx + 1), bx
+        // clamped into [0, W - 2]; at the borders the in-image tap is the pair's
+        // first (sx = -1) or second (sx = W - 1) pixel, the other tap weighs 0.
+        uint32_t ta0[PX_PER_THREAD], ta1[PX_PER_THREAD], tb0[PX_PER_THREAD], tb1[PX_PER_THREAD];
+#pragma unroll
+        for (int p = 0; p < PX_PER_THREAD; ++p) {
+            const int sx = (int)(short)(iu[p] >> 5), sy = (int)(short)(iv[p] >> 5);
+            const int bx = W >= 2 ? min(max(sx, 0), W - 2) : 0;
+            const unsigned cy0 = (unsigned)min(max(sy, 0), H - 1), cy1 = (unsigned)min(max(sy + 1, 0), H - 1);
+            // row offsets: cy < 2^15 and pitch < 2^24 (checked on the host) -> 24-bit multiplies
+            fetch_taps<C, WORDS>(S + __umul24(cy0, sp), bx, W >= 2, ta0[p], ta1[p]);
+            fetch_taps<C, WORDS>(S + __umul24(cy1, sp), bx, W >= 2, tb0[p], tb1[p]);
+        }
+        // (3) blend: cv::remap INTER_LINEAR, 15-bit weights, BORDER_CONSTANT 0
+#pragma unroll
+        for (int p = 0; p < PX_PER_THREAD; ++p) {
+            const int sx = (int)(short)(iu[p] >> 5), sy = (int)(short)(iv[p] >> 5);
+            const int a = iu[p] & 31, bb = iv[p] & 31;
+            const bool x0in = (unsigned)sx < (unsigned)W, x1in = (unsigned)(sx + 1) < (unsigned)W;
+            const bool y0in = (unsigned)sy < (unsigned)H, y1in = (unsigned)(sy + 1) < (unsigned)H;
+            int w0 = (32 - bb) * (32 - a) * 32;
+            if (w0 == 32768) w0 = 32767;                        // saturate_cast<short> of the table entry
+            w0 = (y0in && x0in) ? w0 : 0;
+            const int w1 = (y0in && x1in) ? (32 - bb) * a * 32 : 0;
+            const int w2 = (y1in && x0in) ? bb * (32 - a) * 32 : 0;
+            const int w3 = (y1in && x1in) ? bb * a * 32 : 0;
+            uint32_t a0 = ta0[p], a1 = ta1[p], b0 = tb0[p], b1 = tb1[p];
+            if (W == 1) { a1 = a0; b1 = b0; }
+            const bool first_is_t1 = sx < 0, second_is_t0 = sx >= W - 1;
+            const uint32_t p00 = second_is_t0 ? a1 : a0, p01 = first_is_t1 ? a0 : a1;
+            const uint32_t p10 = second_is_t0 ? b1 : b0, p11 = first_is_t1 ? b0 : b1;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int s = (int)((p00 >> (8 * c)) & 255) * w0 + (int)((p01 >> (8 * c)) & 255) * w1 +
+                              (int)((p10 >> (8 * c)) & 255) * w2 + (int)((p11 >> (8 * c)) & 255) * w3;
+                const uint32_t o = (uint32_t)((s + 16384) >> 15);   // 0 <= s <= 255 * 32768: no saturation needed
+                const int byte = p * C + c;                     // compile-time after unrolling
+                out[byte >> 2] |= o << (8 * (byte & 3));
+            }
         }
     }
     const int npx = min(PX_PER_THREAD, W - x0);
@@ -257,7 +294,7 @@ __device__ __forceinline__ int find_unit(const UndUnit* __restrict__ units, int 
 }
 
 template <int C>
-__global__ __launch_bounds__(THREADS)
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(C == 1 ? 1 : 8)))  // C >= 2: <= 64 VGPRs, 8 waves/SIMD
 void undistort_kernel(const UndUnit* __restrict__ units, int n_units, const UndImg* __restrict__ imgs, int n_blocks) {
     const int lb = xcd_block(n_blocks);
     const UndUnit& u = units[find_unit(units, n_units, lb)];
