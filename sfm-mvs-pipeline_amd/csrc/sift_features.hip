@@ -288,11 +288,17 @@ __global__ void dog_kernel(const float* __restrict__ a, const float* __restrict_
 }
 
 // ------------------------------------------------------------------ detection
-__global__ void extrema_kernel(const float* __restrict__ prev, const float* __restrict__ img,
-                               const float* __restrict__ next, int w, int h, int threshold, int o, int layer,
+// One launch per octave: blockIdx.z picks the inner DoG layer 1 + z of dog[o * (L + 2) ..],
+// so a small octave's three scans fill the chip together.  Candidate slots come from
+// one atomic counter in any order; the host filter sorts them (as before).
+__global__ void extrema_kernel(const Layer* __restrict__ dog, int L, int w, int h, int threshold, int o,
                                Cand* __restrict__ out, int* __restrict__ count, int cap) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x + IMG_BORDER, r = blockIdx.y + IMG_BORDER;
     if (c >= w - IMG_BORDER || r >= h - IMG_BORDER) return;
+    const int layer = 1 + (int)blockIdx.z;
+    const float* __restrict__ prev = dog[o * (L + 2) + layer - 1].p;
+    const float* __restrict__ img = dog[o * (L + 2) + layer].p;
+    const float* __restrict__ next = dog[o * (L + 2) + layer + 1].p;
     const float val = img[(int64_t)r * w + c];
     if (!(fabsf(val) > threshold)) return;
     bool mx = val > 0, mn = val < 0;
@@ -811,14 +817,12 @@ int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int
                     }
                 }
             const int threshold = (int)std::floor(0.5 * params->contrast_threshold / L * 255);
-            for (int o = 0; o < nOct; ++o)
-                for (int i = 1; i <= L; ++i) {
-                    const int w = ow[o], h = oh[o];
-                    if (w <= 2 * IMG_BORDER || h <= 2 * IMG_BORDER) continue;
-                    extrema_kernel<<<dim3((w - 2 * IMG_BORDER + 255) / 256, h - 2 * IMG_BORDER), 256, 0, st>>>(
-                        hdog[o * (L + 2) + i - 1].p, hdog[o * (L + 2) + i].p, hdog[o * (L + 2) + i + 1].p, w, h, threshold, o,
-                        i, cands, counters + 0, CAND_CAP);
-                }
+            for (int o = 0; o < nOct; ++o) {
+                const int w = ow[o], h = oh[o];
+                if (w <= 2 * IMG_BORDER || h <= 2 * IMG_BORDER || L < 1) continue;
+                extrema_kernel<<<dim3((w - 2 * IMG_BORDER + 255) / 256, h - 2 * IMG_BORDER, L), 256, 0, st>>>(
+                    ddog, L, w, h, threshold, o, cands, counters + 0, CAND_CAP);
+            }
             refine_kernel<<<CAND_CAP / 256, 256, 0, st>>>(cands, counters + 0, CAND_CAP, ddog, L,
                                                           (float)params->contrast_threshold, (float)params->edge_threshold,
                                                           sigma, refs, counters + 1, REF_CAP);
