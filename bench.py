@@ -266,8 +266,9 @@ def bench_match(kind, args, rank, world, local):
         res["homography"] = homog
     if f4 is not None:
         res["find_3d2d"] = f4
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and kind != "c3":
-        res.update(cpu_baselines(kind, imgs, pairs_all, got, off, args.cpu_seconds))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res.update(cpu_baselines("sift" if kind == "c3" else kind, imgs, pairs_all, got, off,
+                                 args.cpu_seconds if kind != "c3" else min(args.cpu_seconds, 6.0)))
     del dev_imgs
     torch.cuda.empty_cache()
     return res
@@ -718,10 +719,18 @@ def cpu_baselines(kind, imgs, pairs, gpu_matches, gpu_off, target_s):
         return {"cpu_baseline": {"error": f"oracle unavailable: {e}"}}
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     legs = {}
-    nb, tb, wb, _ = _timed_sample(lambda im, pr: oracle.match_pairs(im, pr, 0.7, threads), imgs, pairs, threads, target_s)
+    nb, tb, wb, (bm, boff) = _timed_sample(lambda im, pr: oracle.match_pairs(im, pr, 0.7, threads), imgs, pairs,
+                                            threads, target_s)
     legs["bf"] = {"value": wb / tb, "unit": "descriptor-pairs/s", "cores": threads, "kind": "port",
                   "sample": f"first {nb} of {len(pairs)} pairs ({wb:.3g} descriptor pairs), exact BF restatement "
                             f"(oracle/match_oracle.cpp, -O3 AVX2, OpenMP over pairs), {tb:.1f} s"}
+    # the exact BF sample doubles as a parity check of the GPU's lists on the same pairs (byte-equal DMatch
+    # lists and offsets: queryIdx, trainIdx, imgIdx, distance bits, order)
+    g_off = np.asarray(gpu_off[: nb + 1], np.int64) - int(gpu_off[0])
+    exact = bool(np.array_equal(g_off, np.asarray(boff, np.int64)) and
+                 gpu_matches[int(gpu_off[0]): int(gpu_off[nb])].tobytes() == bm.tobytes())
+    parity = {"bit_exact_vs_oracle": exact, "bit_exact_pairs": int(nb), "bit_exact_matches": int(len(bm)),
+              "what": "GPU DMatch lists byte-equal to the oracle BF restatement on the CPU-baseline sample"}
     index = "KDTreeIndex(5 trees), SearchParams(checks=100)" if kind == "sift" else "LshIndex(6 tables, 12-bit keys, multi-probe 1)"
     nf, tf, wf, (fm, foff) = _timed_sample(lambda im, pr: oracle.flann_match_pairs(im, pr, 0.7, threads), imgs, pairs,
                                             threads, target_s)
@@ -733,7 +742,7 @@ def cpu_baselines(kind, imgs, pairs, gpu_matches, gpu_off, target_s):
     best = max(legs, key=lambda k: legs[k]["value"])
     out = dict(legs[best])
     out["which"] = best
-    return {"cpu_baseline": out, "cpu_baselines": legs,
+    return {"cpu_baseline": out, "cpu_baselines": legs, "parity": parity,
             "flann_vs_exact": {"recall": rec, "precision": prec, "pairs": nf,
                                "what": "FLANN-restatement accepted matches vs the GPU exact path, same pairs"}}
 

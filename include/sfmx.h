@@ -35,7 +35,8 @@ enum {
     SFMX_ENOMEM = -2,        /* device or host allocation failed                          */
     SFMX_EDEVICE = -3,       /* HIP runtime error / no usable gfx950 device               */
     SFMX_ECAPACITY = -4,     /* caller's output buffer too small; required size returned  */
-    SFMX_ESTATE = -5         /* call out of order (e.g. run before set_images)            */
+    SFMX_ESTATE = -5,        /* call out of order (e.g. run before set_images)            */
+    SFMX_EINTERNAL = -6      /* a device-side self check failed (a bug: please report)     */
 };
 
 /* Norm types: numerically equal to cv::NORM_L2 / cv::NORM_HAMMING so a caller
@@ -133,8 +134,12 @@ int sfmx_matcher_stats(sfmx_matcher* m, int64_t* slow_queries, int64_t* fp32_pai
  * total_ms = first to last kernel of the run.  Synchronises the run's end event. */
 int sfmx_matcher_timing(sfmx_matcher* m, float* main_kernel_ms, float* total_ms);
 
-/* One-shot convenience wrapper = the whole strategy call: uses n_gpus devices
- * (pairs split by Σ Nq·Nt, one host thread per device) and host buffers. */
+/* One-shot convenience wrapper = the whole strategy call
+ * (IFeatureMatchingStrategy::calculateShotMatches, IFeatureMatchingStrategy.h:45-46, as SfM.cpp:545
+ * calls it): uses n_gpus devices (pairs split by Σ Nq·Nt, one host thread per device; each device
+ * uploads only the images its slice references) and host buffers.  Each query yields at most one
+ * match, so cap = Σ over pairs of rows(left) always suffices and ONE call does the whole job; with a
+ * smaller cap the call still matches once, sets *required and returns SFMX_ECAPACITY. */
 int sfmx_match_pairs(const sfmx_desc* imgs, int32_t n_imgs, const int32_t* pairs, int32_t n_pairs,
                      int32_t norm, double ratio, int32_t distinct, int32_t min_count, int32_t n_gpus,
                      sfmx_dmatch* out, int64_t cap, int64_t* required,

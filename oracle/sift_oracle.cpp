@@ -475,15 +475,15 @@ int orc_sift(const uint8_t* image, int W, int H, int64_t pitch, int nfeatures, i
         }
         kps.resize(w + 1);
     }
+    // KeyPointsFilter::retainBest (OpenCV 4.5.1): nth_element on the keypoint vector itself with
+    // KeypointResponseGreater, then std::partition of the tail by response >= the boundary response.
+    // Both reorder the kept keypoints in place; the descriptor rows follow that order.
     if (nfeatures > 0 && (int)kps.size() > nfeatures) {
-        std::vector<float> resp(kps.size());
-        for (size_t j = 0; j < kps.size(); ++j) resp[j] = kps[j].response;
-        std::nth_element(resp.begin(), resp.begin() + nfeatures - 1, resp.end(), std::greater<float>());
-        const float amb = resp[nfeatures - 1];
-        std::vector<Kp> keep;
-        for (const Kp& q : kps)
-            if (q.response >= amb) keep.push_back(q);
-        kps.swap(keep);
+        std::nth_element(kps.begin(), kps.begin() + nfeatures - 1, kps.end(),
+                         [](const Kp& a, const Kp& b) { return a.response > b.response; });
+        const float amb = kps[nfeatures - 1].response;
+        auto new_end = std::partition(kps.begin() + nfeatures, kps.end(), [amb](const Kp& q) { return q.response >= amb; });
+        kps.resize(new_end - kps.begin());
     }
     for (Kp& q : kps) {
         q.octave = (q.octave & ~255) | ((q.octave + firstOctave) & 255);
@@ -491,6 +491,31 @@ int orc_sift(const uint8_t* image, int W, int H, int64_t pitch, int nfeatures, i
         q.y *= 0.5f;
         q.size *= 0.5f;
     }
+    // SfM.cpp:586-587 calls detect() and compute() separately. compute() (useProvidedKeypoints) rebuilds the
+    // pyramid from firstOctave = min(0, min keypoint octave) with maxOctave - firstOctave + 1 octaves, so when
+    // no kept keypoint comes from the upsampled octave the descriptors are taken from an un-doubled pyramid.
+    int cFirst = 0, cMaxOct = INT_MIN;
+    for (const Kp& q : kps) {
+        int o = q.octave & 255;
+        o = o < 128 ? o : (-128 | o);
+        cFirst = std::min(cFirst, o);
+        cMaxOct = std::max(cMaxOct, o);
+    }
+    std::vector<Img> gp0;
+    if (!kps.empty() && cFirst == 0 && desc_out) {
+        const float sd0 = std::sqrt(std::max(sigma * sigma - INIT_SIGMA * INIT_SIGMA, 0.01f));
+        const int nOc = cMaxOct + 1;
+        gp0.resize((size_t)nOc * (L + 3));
+        for (int o = 0; o < nOc; o++)
+            for (int i = 0; i < L + 3; i++) {
+                Img& dst = gp0[o * (L + 3) + i];
+                if (o == 0 && i == 0) dst = blur(gray, sd0);
+                else if (i == 0) dst = half_nn(gp0[(o - 1) * (L + 3) + L]);
+                else dst = blur(gp0[o * (L + 3) + i - 1], sig[i]);
+            }
+    }
+    const std::vector<Img>& dgp = gp0.empty() ? gp : gp0;
+    const int dFirst = gp0.empty() ? firstOctave : 0;
     const int n = (int)kps.size();
     Kp* out = static_cast<Kp*>(kps_out);
     for (int q = 0; q < n && q < cap; ++q) {
@@ -500,7 +525,7 @@ int orc_sift(const uint8_t* image, int W, int H, int64_t pitch, int nfeatures, i
         octave = octave < 128 ? octave : (-128 | octave);
         const float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
         const float size = kps[q].size * scale;
-        const Img& img = gp[(octave - firstOctave) * (L + 3) + layer];
+        const Img& img = dgp[(octave - dFirst) * (L + 3) + layer];
         float angle = 360.f - kps[q].angle;
         if (std::fabs(angle - 360.f) < FLT_EPSILON) angle = 0.f;
         descriptor(img, kps[q].x * scale, kps[q].y * scale, angle, size * 0.5f, desc_out + (size_t)q * 128);

@@ -79,6 +79,9 @@ __device__ __forceinline__ float sqrt_rn_int(int64_t s) { return (float)__builti
 // KEY_VALID, real keys are >= -(2^21 + 2^20).
 constexpr int PAD_KEY = (int)0xC0C0C0C0;
 constexpr int KEY_VALID = -(1 << 29);
+// dense_idx of a query pass 1 forwarded to pass 2; assemble_kernel counts any left over
+// (a pass-2 grid that did not cover its item's queries) and the run fails loudly.
+constexpr int UNSETTLED = -3;
 static_assert(PAD_KEY < KEY_VALID - (1 << 22), "pad keys must never look valid");
 
 // Bijective XCD-contiguous remap: blocks b, b+8, ... share an XCD (observed
@@ -565,6 +568,7 @@ void sift_screen_kernel(const WorkItem* __restrict__ work, const PairDev* __rest
         } else {
             const int slot = atomicAdd(&qcount[w.pair], 1);
             qlist[P.dense_base + slot] = qi;
+            out_idx[o] = UNSETTLED;   // pass 2 must overwrite it (assemble counts survivors)
         }
     }
 }
@@ -696,6 +700,7 @@ void sift_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __re
         } else {
             const int slot = atomicAdd(&qcount[w.pair], 1);
             qlist[P.dense_base + slot] = qi;
+            out_idx[o] = UNSETTLED;   // pass 2 must overwrite it (assemble counts survivors)
         }
     }
 }
@@ -1307,6 +1312,7 @@ void orb_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __res
         } else {
             const int slot = atomicAdd(&qcount[w.pair], 1);
             qlist[P.dense_base + slot] = qi;
+            out_idx[o] = UNSETTLED;   // pass 2 must overwrite it (assemble counts survivors)
         }
     }
 }
@@ -1425,7 +1431,7 @@ __global__ __launch_bounds__(1024)
 void assemble_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restrict__ imgs,
                      const int32_t* __restrict__ out_idx, const float* __restrict__ out_dist,
                      int distinct, int min_count, int64_t* __restrict__ counts, int32_t* __restrict__ keep,
-                     const int64_t* __restrict__ offsets, DMatchDev* __restrict__ out) {
+                     const int64_t* __restrict__ offsets, DMatchDev* __restrict__ out, int32_t* __restrict__ unsettled) {
     extern __shared__ __attribute__((aligned(16))) unsigned bits[];   // seen | dup bitsets (distinct only)
     __shared__ int sh[32];
     const int p = blockIdx.x;
@@ -1446,6 +1452,11 @@ void assemble_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restrict
             }
         }
         __syncthreads();
+    }
+    if (MODE == 0) {
+        int bad = 0;
+        for (int q = threadIdx.x; q < nq; q += blockDim.x) bad += ix[q] == UNSETTLED;
+        if (bad) atomicAdd(unsettled, bad);
     }
     int64_t run = 0;
     const int64_t base = MODE == 1 ? offsets[p] : 0;
@@ -1566,6 +1577,8 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
 #undef SCREEN_LAUNCH
 #undef SCREEN16_LAUNCH
 #define PASS2_LAUNCH(ISH, QT, W, MINW, ST)                                                                   \
+    static_assert((1 << (ISH)) == (QT) * (W) * 32, "pass-2 item size must equal the queries one block covers"); \
+    static_assert((ISH) >= 7 && (ISH) <= 9, "work2 holds n_work << 2 items: items of 128..512 queries");       \
     compact_work_kernel<ISH><<<1, 1024, 0, st>>>(porder, n_pairs, qcount, work2, work2_n);                  \
     sift_knn2_kernel<QT, W, MINW, ST, false, 0, 0, true><<<n_work << (9 - ISH), W * 64, 0, st>>>(             \
         work2, pairs, imgs, desc8, norm, keyc, out_idx, out_dist, slow_list, slow_count, ratio, qlist, qcount, \
@@ -1598,6 +1611,8 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
     case 21: SIFT_LAUNCH(2, 8, 2, 128, false, 0, 9); break;
     case 22: SIFT_LAUNCH(4, 4, 2, 128, false, 0, 8); break;
     case 23: SIFT_LAUNCH(2, 4, 4, 128, false, 0, 9); break;
+    case 30: SIFT_LAUNCH(4, 4, 1, 128, false); break;   // MINW = 1 (r01: failed kat_sift_nt1_nt0)
+    case 31: SIFT_LAUNCH(2, 8, 1, 64, true); break;     // MINW = 1, the r01 default's tiling
     default: SIFT_LAUNCH(4, 4, 2, 128, false);   // 100: the r01d single-pass default (9.57-9.67 ms on config 2)
     }
     return hipGetLastError();
@@ -1623,12 +1638,9 @@ hipError_t launch_orb_knn2(const WorkItem* work, int n_work, const PairDev* pair
 // ORB kernel selection: 0 (default) = FP4 MFMA path on 128-byte +-1 rows,
 // 1 = VALU xor/popcount path on 32-byte rows, 2.. = FP4 MFMA tiling variants
 // (tuning only).  SFMX_ORB_VARIANT overrides.
-int orb_variant() {
-    static int v = [] {
-        const char* e = getenv("SFMX_ORB_VARIANT");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
+int orb_variant() {   // read per run, as sift_variant(): tests switch variants within one process
+    const char* e = getenv("SFMX_ORB_VARIANT");
+    return e ? atoi(e) : 0;
 }
 hipError_t launch_prep_hamming_fp4(const uint8_t* src, int rows, int cols, int rows_pad, uint8_t* dst, int32_t* keyc,
                                    hipStream_t st) {
@@ -1648,6 +1660,8 @@ hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pair
         orb_screen16_kernel<8, 4, 2, 64><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx, out_dist,
                                                                   qlist, qcount, ratio);
 #define ORB_PASS2(ISH, QT, W)                                                                                   \
+    static_assert((1 << (ISH)) == (QT) * (W) * 16, "pass-2 item size must equal the queries one block covers"); \
+    static_assert((ISH) >= 7 && (ISH) <= 9, "work2 holds n_work << 2 items: items of 128..512 queries");       \
     compact_work_kernel<ISH><<<1, 1024, 0, st>>>(porder, n_pairs, qcount, work2, work2_n);                      \
     orb_mfma16_kernel<QT, W, 2, 64, true><<<n_work << (9 - ISH), W * 64, 0, st>>>(work2, pairs, imgs, desc4, keyc, \
                                                                                   out_idx, out_dist, ratio, qlist, \
@@ -1658,6 +1672,8 @@ hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pair
         // tile's MFMAs and with the key added on the VALU instead of the C operand; the 8-tile build
         // is exact on every test.  Not understood; only the 8-tile form is built.
         // r01g config 4: 18.68-18.73 ms (two-pass) vs 20.19-20.24 (single pass, variant 5).
+        case 13: ORB_PASS2(7, 2, 4); break;   // 128-query items (2 tiles per wave)
+        case 14: ORB_PASS2(8, 4, 4); break;   // 256-query items (4 tiles per wave)
         default: ORB_PASS2(9, 8, 4);       // 0 / 12: 512-query items
         }
 #undef ORB_PASS2
@@ -1673,6 +1689,8 @@ hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pair
     // build with 4 tiles x 8 waves failed kat_orb_ties (one accepted match lost) and is not kept;
     // like the MINW = 1 builds the cause is not understood.
     case 6: ORB16_LAUNCH(8, 4, 2, 128); break;
+    case 7: ORB16_LAUNCH(4, 8, 2, 64); break;    // 4 tiles x 8 waves (r01g: lost a kat_orb_ties match)
+    case 9: ORB_LAUNCH(4, 4, 1, 64); break;      // 32x32x64 with MINW = 1
     case 8: ORB_LAUNCH(4, 4, 2, 64); break;
     case 2: ORB_LAUNCH(2, 8, 2, 64); break;
     case 3: ORB_LAUNCH(2, 8, 2, 128); break;
@@ -1685,16 +1703,18 @@ hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pair
 }
 hipError_t launch_assemble(const PairDev* pairs, int n_pairs, const ImgDev* imgs, const int32_t* out_idx,
                            const float* out_dist, int distinct, int min_count, int max_nt, int64_t* counts,
-                           int32_t* keep, int64_t* offsets, DMatchDev* out, hipStream_t st) {
+                           int32_t* keep, int64_t* offsets, DMatchDev* out, int32_t* unsettled, hipStream_t st) {
     if (n_pairs == 0) {
         (void)hipMemsetAsync(offsets, 0, sizeof(int64_t), st);
         return hipGetLastError();
     }
     const size_t shmem = distinct ? (size_t)2 * ((max_nt + 31) / 32) * 4 : 0;
     if (shmem > 150 * 1024) return hipErrorInvalidValue;
-    assemble_kernel<0><<<n_pairs, 1024, shmem, st>>>(pairs, imgs, out_idx, out_dist, distinct, min_count, counts, keep, nullptr, nullptr);
+    assemble_kernel<0><<<n_pairs, 1024, shmem, st>>>(pairs, imgs, out_idx, out_dist, distinct, min_count, counts, keep, nullptr,
+                                                     nullptr, unsettled);
     scan_offsets_kernel<<<1, 1024, 0, st>>>(counts, n_pairs, offsets);
-    assemble_kernel<1><<<n_pairs, 1024, shmem, st>>>(pairs, imgs, out_idx, out_dist, distinct, min_count, counts, keep, offsets, out);
+    assemble_kernel<1><<<n_pairs, 1024, shmem, st>>>(pairs, imgs, out_idx, out_dist, distinct, min_count, counts, keep, offsets,
+                                                     out, unsettled);
     return hipGetLastError();
 }
 

@@ -51,7 +51,7 @@ hipError_t launch_selftest_sqrt(int64_t, uint32_t*, hipStream_t);
 int sift_variant();
 int sift_block_queries(int variant);
 hipError_t launch_assemble(const PairDev*, int, const ImgDev*, const int32_t*, const float*, int, int, int,
-                           int64_t*, int32_t*, int64_t*, DMatchDev*, hipStream_t);
+                           int64_t*, int32_t*, int64_t*, DMatchDev*, int32_t*, hipStream_t);
 }  // namespace sfmx
 
 using namespace sfmx;
@@ -155,6 +155,7 @@ struct sfmx_matcher {
     DevBuf pairs_d, work_d, work32_d, dense_idx, dense_dist, slow_list, slow_count, counts, keep, offsets, out;
     DevBuf qlist, qcount;   // two-pass SIFT path: per pair, the queries the screening pass could not settle
     DevBuf porder, work2, work2_n;   // pair order (by train image) and the compacted pass-2 work list
+    DevBuf unsettled;                // int32: pass-1 forwarded queries pass 2 never wrote (must stay 0)
     DevBuf prep_tab;                 // batched SIFT prep: one PrepImg per image
     PinnedBuf stage_prep, stage_run, stage_imgs, stage_flags; // pinned staging of the small uploads / flag readback
     // Run plan cache: the device pair/work lists of the last run stay valid while the
@@ -353,6 +354,7 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
         if ((rc = m->porder.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
         if ((rc = m->work2.ensure(sizeof(WorkItem) * std::max<size_t>(4 * work.size(), 1)))) return rc;   // pass-2 items >= 128 queries
         if ((rc = m->work2_n.ensure(sizeof(int32_t)))) return rc;
+        if ((rc = m->unsettled.ensure(sizeof(int32_t)))) return rc;
         if ((rc = m->counts.ensure(sizeof(int64_t) * std::max(n_pairs, 1)))) return rc;
         if ((rc = m->keep.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
         if ((rc = m->offsets.ensure(sizeof(int64_t) * (n_pairs + 1)))) return rc;
@@ -385,6 +387,7 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     if (!m->ev[0])
         for (auto& e : m->ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipMemsetAsync(m->slow_count.p, 0, sizeof(int32_t), st));
+    HIPCHK(hipMemsetAsync(m->unsettled.p, 0, sizeof(int32_t), st));
     HIPCHK(hipEventRecord(m->ev[0], st));
     // Pairs with an empty left image have no work item; pairs with an empty
     // right image are handled in-kernel (every query: no neighbour).
@@ -416,7 +419,7 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     const int max_nt = m->plan_max_nt;
     HIPCHK(launch_assemble(P, n_pairs, I, m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), distinct ? 1 : 0,
                            min_count, max_nt, m->counts.as<int64_t>(), m->keep.as<int32_t>(),
-                           m->offsets.as<int64_t>(), m->out.as<DMatchDev>(), st));
+                           m->offsets.as<int64_t>(), m->out.as<DMatchDev>(), m->unsettled.as<int32_t>(), st));
     HIPCHK(hipEventRecord(m->ev[2], st));
     m->ev_recorded = true;
     m->n_pairs = n_pairs;
@@ -431,8 +434,11 @@ int fetch_impl(sfmx_matcher* m, sfmx_dmatch* out, int64_t cap, int64_t* required
     if (!m->has_run) return fail(SFMX_ESTATE, "fetch before run");
     DeviceGuard g(m->device);
     std::vector<int64_t> off(m->n_pairs + 1);
+    int32_t unsettled = 0;
     HIPCHK(hipMemcpyAsync(off.data(), m->offsets.p, sizeof(int64_t) * (m->n_pairs + 1), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&unsettled, m->unsettled.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (unsettled) return fail(SFMX_EINTERNAL, std::to_string(unsettled) + " forwarded queries were not settled by pass 2");
     const int64_t total = off[m->n_pairs];
     if (required) *required = total;
     if (pair_offsets) std::memcpy(pair_offsets, off.data(), sizeof(int64_t) * (m->n_pairs + 1));
@@ -501,7 +507,7 @@ int sfmx_matcher_destroy(sfmx_matcher* m) {
         m->stage_flags.release();
         DevBuf* bufs[] = {&m->raw, &m->desc8, &m->normv, &m->keyc, &m->keyc2, &m->qlist, &m->qcount, &m->porder, &m->work2, &m->work2_n, &m->f32, &m->flags, &m->imgs_d, &m->pairs_d, &m->prep_tab,
                           &m->work_d, &m->work32_d, &m->dense_idx, &m->dense_dist, &m->slow_list, &m->slow_count,
-                          &m->counts, &m->keep, &m->offsets, &m->out};
+                          &m->unsettled, &m->counts, &m->keep, &m->offsets, &m->out};
         for (DevBuf* b : bufs) b->release();
         for (auto& e : m->ev) if (e) (void)hipEventDestroy(e);
     }
@@ -541,9 +547,11 @@ int sfmx_matcher_stats(sfmx_matcher* m, int64_t* slow_queries, int64_t* fp32_pai
     if (!m) return fail(SFMX_EINVAL, "null matcher");
     if (!m->has_run) return fail(SFMX_ESTATE, "no stats before run");
     DeviceGuard g(m->device);
-    int32_t sc = 0;
+    int32_t sc = 0, unsettled = 0;
     HIPCHK(hipMemcpyAsync(&sc, m->slow_count.p, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIPCHK(hipMemcpyAsync(&unsettled, m->unsettled.p, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
     HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    if (unsettled) return fail(SFMX_EINTERNAL, std::to_string(unsettled) + " forwarded queries were not settled by pass 2");
     if (slow_queries) *slow_queries = sc;
     if (fp32_pairs) *fp32_pairs = m->fp32_pairs;
     return SFMX_OK;
@@ -600,9 +608,17 @@ int sfmx_match_pairs(const sfmx_desc* imgs, int32_t n_imgs, const int32_t* pairs
             if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { s.rc = SFMX_EDEVICE; s.err = "stream"; sfmx_matcher_destroy(m); return; }
         }
         s.off.assign(np + 1, 0); s.keep.assign(np, 0);
+        // upload only the images this GPU's slice references (remapped to a dense local table)
+        std::vector<int32_t> local_of(n_imgs, -1), lpairs(2 * (size_t)np);
+        std::vector<sfmx_desc> limgs;
+        for (int q = 0; q < 2 * np; ++q) {
+            const int im = pairs[2 * cut[g] + q];
+            if (local_of[im] < 0) { local_of[im] = (int32_t)limgs.size(); limgs.push_back(imgs[im]); }
+            lpairs[q] = local_of[im];
+        }
         int64_t req = 0;
-        if (!(s.rc = sfmx_matcher_set_images(m, imgs, n_imgs, norm, st)) &&
-            !(s.rc = sfmx_matcher_run(m, pairs + 2 * cut[g], np, ratio, distinct, min_count, st)) &&
+        if (!(s.rc = sfmx_matcher_set_images(m, limgs.data(), (int32_t)limgs.size(), norm, st)) &&
+            !(s.rc = sfmx_matcher_run(m, lpairs.data(), np, ratio, distinct, min_count, st)) &&
             !(s.rc = sfmx_matcher_fetch(m, nullptr, 0, &req, s.off.data(), s.keep.data(), st))) {
             s.m.resize(req);
             s.rc = sfmx_matcher_fetch(m, s.m.data(), req, &req, nullptr, nullptr, st);

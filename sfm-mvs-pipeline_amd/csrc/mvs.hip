@@ -355,7 +355,18 @@ struct Scratch {
     size_t cap = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     void* get(int device, size_t bytes) {
-        if (dev != device) { p = nullptr; cap = 0; e0 = e1 = nullptr; dev = device; }   // other device: leak-free enough
+        if (dev != device) {   // free the old device's buffer and events on that device first
+            if (dev >= 0) {
+                int prev = -1;
+                (void)hipGetDevice(&prev);
+                (void)hipSetDevice(dev);
+                if (p) (void)hipFree(p);
+                if (e0) (void)hipEventDestroy(e0);
+                if (e1) (void)hipEventDestroy(e1);
+                if (prev >= 0) (void)hipSetDevice(prev);
+            }
+            p = nullptr; cap = 0; e0 = e1 = nullptr; dev = device;
+        }
         if (bytes > cap) {
             if (p) (void)hipFree(p);
             p = nullptr;

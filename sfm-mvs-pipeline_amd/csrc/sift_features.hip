@@ -150,6 +150,13 @@ __global__ void up2_kernel(const uint8_t* __restrict__ img, int W, int H, int64_
     dst[(int64_t)Y * (2 * W) + X] = h0 * b0 + h1 * b1;
 }
 
+// img.convertTo(CV_32F) of createInitialImage's un-doubled branch (compute() with firstOctave = 0)
+__global__ void to_float_kernel(const uint8_t* __restrict__ img, int W, int H, int64_t pitch, float* __restrict__ dst) {
+    const int X = blockIdx.x * blockDim.x + threadIdx.x, Y = blockIdx.y;
+    if (X >= W) return;
+    dst[(int64_t)Y * W + X] = (float)img[Y * pitch + X];
+}
+
 __global__ void blur_row_kernel(const float* __restrict__ src, float* __restrict__ dst, int w, int h,
                                 const float* __restrict__ f, int n) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
@@ -602,15 +609,15 @@ static void filter_keypoints(std::vector<Kp>& kps, int nfeatures) {
         }
         kps.resize(w + 1);
     }
+    // KeyPointsFilter::retainBest (OpenCV 4.5.1): nth_element on the keypoint vector itself with
+    // KeypointResponseGreater, then std::partition of the tail by response >= the boundary response. Both
+    // reorder the kept keypoints in place (libstdc++ algorithms, as OpenCV's build), and descriptor rows follow.
     if (nfeatures > 0 && (int)kps.size() > nfeatures) {
-        std::vector<float> resp(kps.size());
-        for (size_t j = 0; j < kps.size(); ++j) resp[j] = kps[j].response;
-        std::nth_element(resp.begin(), resp.begin() + nfeatures - 1, resp.end(), std::greater<float>());
-        const float amb = resp[nfeatures - 1];
-        size_t w = 0;
-        for (size_t j = 0; j < kps.size(); ++j)
-            if (kps[j].response >= amb) kps[w++] = kps[j];
-        kps.resize(w);
+        std::nth_element(kps.begin(), kps.begin() + nfeatures - 1, kps.end(),
+                         [](const Kp& a, const Kp& b) { return a.response > b.response; });
+        const float amb = kps[nfeatures - 1].response;
+        auto new_end = std::partition(kps.begin() + nfeatures, kps.end(), [amb](const Kp& q) { return q.response >= amb; });
+        kps.resize(new_end - kps.begin());
     }
     for (Kp& q : kps) {
         q.octave = (q.octave & ~255) | ((q.octave - 1) & 255);
@@ -626,10 +633,27 @@ struct Arena {                 // per-thread device scratch, grown on demand
     int dev = -1;
     char* p = nullptr;
     size_t cap = 0, used = 0;
+    bool overflow = false;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    void release() {   // frees on the device the arena was made for
+        if (dev < 0) return;
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(dev);
+        if (p) (void)hipFree(p);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        if (prev >= 0) (void)hipSetDevice(prev);
+        p = nullptr; cap = 0; e0 = e1 = nullptr; dev = -1;
+    }
     bool reserve(int device, size_t bytes) {
-        if (dev != device) { p = nullptr; cap = 0; e0 = e1 = nullptr; dev = device; }
+        if (dev != device) {
+            release();
+            (void)hipSetDevice(device);
+            dev = device;
+        }
         used = 0;
+        overflow = false;
         if (bytes > cap) {
             if (p) (void)hipFree(p);
             p = nullptr;
@@ -640,9 +664,10 @@ struct Arena {                 // per-thread device scratch, grown on demand
         if (!e0 && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) return false;
         return true;
     }
-    template <class T> T* take(size_t n) {
+    template <class T> T* take(size_t n) {   // callers check `overflow` before the first launch
         T* r = reinterpret_cast<T*>(p + used);
         used += (sizeof(T) * n + 255) & ~(size_t)255;
+        if (used > cap) overflow = true;
         return r;
     }
 };
@@ -727,9 +752,12 @@ int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int
             sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
         }
         const float sig_diff = std::sqrt(std::max(sigma * sigma - INIT_SIGMA * INIT_SIGMA * 4, 0.01f));
-        std::vector<std::vector<float>> kern(L + 3);
+        // kern[L + 3]: createInitialImage's blur without doubling (compute() with firstOctave = 0)
+        const float sig_diff0 = std::sqrt(std::max(sigma * sigma - INIT_SIGMA * INIT_SIGMA, 0.01f));
+        std::vector<std::vector<float>> kern(L + 4);
         kern[0] = gauss_kernel(sig_diff);
         for (int i = 1; i < L + 3; i++) kern[i] = gauss_kernel(sig[i]);
+        kern[L + 3] = gauss_kernel(sig_diff0);
         if (nOct < 1) {   // 1-pixel-high or -wide image: no octave, no keypoints (as OpenCV)
             *n_keypoints = 0;
             if (prev >= 0) (void)hipSetDevice(prev);
@@ -745,9 +773,13 @@ int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int
         const int CAND_CAP = 1 << 20, REF_CAP = 1 << 19, KP_CAP = 1 << 20;
         size_t kbytes = 0;
         for (auto& kk : kern) kbytes += (kk.size() * 4 + 255) & ~(size_t)255;
-        const size_t need = px * 4 * (size_t)(2 * L + 5) + (size_t)BW * BH * 4 + ((size_t)width * height + 256) +
+        // the take() sequence below, each take rounded up to 256 B: the 2L + 5 layers per octave, tmp and up
+        // (two BW x BH float buffers), the kernels, the layer tables, the candidate / keypoint buffers, the
+        // staged host image and the staged descriptors
+        const size_t ntakes = (size_t)nOct * (2 * L + 5) + (L + 4) + 12;
+        const size_t need = px * 4 * (size_t)(2 * L + 5) + 2 * ((size_t)BW * BH * 4) + (size_t)width * height +
                             kbytes + sizeof(Cand) * CAND_CAP + sizeof(Refined) * REF_CAP + sizeof(Kp) * KP_CAP * 2 +
-                            (size_t)KP_CAP * 128 * 4 + 64 * 1024 + (size_t)nOct * (2 * L + 5) * sizeof(Layer) + 8192;
+                            (size_t)KP_CAP * 128 * 4 + 16 + (size_t)nOct * (2 * L + 5) * sizeof(Layer) + 256 * ntakes;
         if (!arena.reserve(device, need)) { rc = SFMX_ENOMEM; set_last_error("device allocation failed"); goto done; }
         {
             Arena& A = arena;
@@ -758,8 +790,8 @@ int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int
             }
             float* tmp = A.take<float>((size_t)BW * BH);
             float* up = A.take<float>((size_t)BW * BH);
-            std::vector<float*> dk(L + 3);
-            for (int i = 0; i < L + 3; ++i) dk[i] = A.take<float>(kern[i].size());
+            std::vector<float*> dk(L + 4);
+            for (int i = 0; i < L + 4; ++i) dk[i] = A.take<float>(kern[i].size());
             Layer* dgp = A.take<Layer>(hgp.size());
             Layer* ddog = A.take<Layer>(hdog.size());
             Cand* cands = A.take<Cand>(CAND_CAP);
@@ -769,13 +801,15 @@ int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int
             int* counters = A.take<int>(4);
             const uint8_t* dimg = image;
             int64_t dpitch = pitch;
+            uint8_t* t = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)width * height);
+            float* dd_stage = inputs_on_device || !descriptors ? nullptr : A.take<float>((size_t)KP_CAP * 128);
+            if (A.overflow) { set_last_error("internal: SIFT scratch arena too small"); rc = SFMX_ECAPACITY; goto done; }
             if (!inputs_on_device) {
-                uint8_t* t = A.take<uint8_t>((size_t)width * height);
                 FCHK(hipMemcpy2DAsync(t, width, image, pitch, width, height, hipMemcpyHostToDevice, st));
                 dimg = t;
                 dpitch = width;
             }
-            for (int i = 0; i < L + 3; ++i)
+            for (int i = 0; i < L + 4; ++i)
                 FCHK(hipMemcpyAsync(dk[i], kern[i].data(), kern[i].size() * 4, hipMemcpyHostToDevice, st));
             FCHK(hipMemcpyAsync(dgp, hgp.data(), sizeof(Layer) * hgp.size(), hipMemcpyHostToDevice, st));
             FCHK(hipMemcpyAsync(ddog, hdog.data(), sizeof(Layer) * hdog.size(), hipMemcpyHostToDevice, st));
@@ -846,8 +880,39 @@ int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int
             if (m > 0) {
                 FCHK(hipMemcpyAsync(fin, kps.data(), sizeof(Kp) * m, hipMemcpyHostToDevice, st));
                 if (descriptors) {
-                    float* dd = inputs_on_device ? descriptors : A.take<float>((size_t)m * 128);
-                    descriptor_kernel<<<m, DESC_THREADS, 0, st>>>(fin, m, dgp, L, -1, dd);
+                    // compute() after detect() (SfM.cpp:586-587): firstOctave = min(0, min kept octave). When no kept
+                    // keypoint is from the doubled octave the pyramid is rebuilt un-doubled for the descriptors; its
+                    // octave o has exactly the size of the doubled pyramid's octave o + 1, so it reuses those slots.
+                    int cFirst = 0, cMaxOct = INT_MIN;
+                    for (int q = 0; q < n; ++q) {
+                        int o = kps[q].octave & 255;
+                        o = o < 128 ? o : (-128 | o);
+                        cFirst = std::min(cFirst, o);
+                        cMaxOct = std::max(cMaxOct, o);
+                    }
+                    const Layer* dgp_desc = dgp;
+                    int first_desc = -1;
+                    if (cFirst == 0) {
+                        const int nOc = cMaxOct + 1;   // <= nOct - 1: detection octaves are < nOct in doubled numbering
+                        to_float_kernel<<<dim3((width + 255) / 256, height), 256, 0, st>>>(dimg, width, height, dpitch, up);
+                        blur(up, hgp[L + 3].p, nullptr, width, height, L + 3);
+                        for (int o = 0; o < nOc; ++o)
+                            for (int i = 0; i < L + 3; ++i) {
+                                if (o == 0 && i == 0) continue;
+                                Layer& dst = hgp[(o + 1) * (L + 3) + i];
+                                if (i == 0) {
+                                    const Layer& src = hgp[o * (L + 3) + L];   // rebuilt octave o - 1, layer L
+                                    half_nn_kernel<<<dim3((dst.w + 255) / 256, dst.h), 256, 0, st>>>(
+                                        src.p, src.w, src.h, dst.p, dst.w, dst.h, 1. / ((double)dst.w / src.w), 1. / ((double)dst.h / src.h));
+                                } else {
+                                    blur(hgp[(o + 1) * (L + 3) + i - 1].p, dst.p, nullptr, dst.w, dst.h, i);
+                                }
+                            }
+                        dgp_desc = dgp + (L + 3);
+                        first_desc = 0;
+                    }
+                    float* dd = inputs_on_device ? descriptors : dd_stage;
+                    descriptor_kernel<<<m, DESC_THREADS, 0, st>>>(fin, m, dgp_desc, L, first_desc, dd);
                     FCHK(hipGetLastError());
                     if (!inputs_on_device)
                         FCHK(hipMemcpyAsync(descriptors, dd, sizeof(float) * 128 * m, hipMemcpyDeviceToHost, st));

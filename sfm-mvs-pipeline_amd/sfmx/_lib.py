@@ -13,7 +13,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # SFMX_LIB_NAME: another in-tree build under lib/ (A/B timing of two builds in one run, tools/ab_build.sh)
 LIB_PATH = os.path.join(PKG_ROOT, "lib", os.path.basename(os.environ.get("SFMX_LIB_NAME", "libsfmx.so")))
 
-SFMX_OK, SFMX_EINVAL, SFMX_ENOMEM, SFMX_EDEVICE, SFMX_ECAPACITY, SFMX_ESTATE = 0, -1, -2, -3, -4, -5
+SFMX_OK, SFMX_EINVAL, SFMX_ENOMEM, SFMX_EDEVICE, SFMX_ECAPACITY, SFMX_ESTATE, SFMX_EINTERNAL = 0, -1, -2, -3, -4, -5, -6
 SFMX_NORM_L2, SFMX_NORM_HAMMING = 4, 6
 SFMX_8U, SFMX_32F = 0, 5
 
@@ -23,6 +23,7 @@ ERROR_NAMES = {
     SFMX_EDEVICE: "SFMX_EDEVICE",
     SFMX_ECAPACITY: "SFMX_ECAPACITY",
     SFMX_ESTATE: "SFMX_ESTATE",
+    SFMX_EINTERNAL: "SFMX_EINTERNAL",
 }
 
 

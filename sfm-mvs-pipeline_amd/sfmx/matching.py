@@ -181,11 +181,12 @@ def match_pairs(mats: Sequence[np.ndarray], pairs: np.ndarray, norm: int = NORM_
     keep = np.zeros(max(len(pairs), 1), np.int32)
     args = (arr, len(mats), _i32p(pairs), len(pairs), norm, float(ratio), int(bool(distinct)), int(min_count),
             int(n_gpus))
-    check(lib.sfmx_match_pairs(*args, None, 0, _i64p(req), None, None), "sfmx_match_pairs")
-    out = np.zeros(int(req[0]), DMATCH_DTYPE)
-    check(lib.sfmx_match_pairs(*args, C.c_void_p(out.ctypes.data) if len(out) else None, len(out), _i64p(req),
-                               _i64p(off), _i32p(keep)), "sfmx_match_pairs")
-    return out, off, keep[: len(pairs)]
+    # one call: each query yields at most one match, so sum(rows(left)) always suffices
+    cap = int(sum(len(mats[l]) for l in pairs[:, 0])) if len(pairs) else 0
+    out = np.zeros(max(cap, 1), DMATCH_DTYPE)
+    check(lib.sfmx_match_pairs(*args, C.c_void_p(out.ctypes.data), cap, _i64p(req), _i64p(off), _i32p(keep)),
+          "sfmx_match_pairs")
+    return out[: int(req[0])], off, keep[: len(pairs)]
 
 
 # ---- reference plugin interface -------------------------------------------

@@ -1,0 +1,68 @@
+"""Worker for test_gpu_fullsize::test_pair_sharded_two_ranks_equal_one_rank:
+pair-sharded matching across ranks (torchrun, every rank on this one GPU, gloo),
+as bench.py / SURVEY §8e shard it: each rank matches its contiguous slice of the
+pair list (sfmx.shard.shard_pairs), no collective on the data path.  Rank 0
+gathers the per-rank DMatch lists (outside the data path), runs the same job on
+one rank and prints one JSON line saying whether the merged lists are byte-equal."""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "sfm-mvs-pipeline_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def match(imgs, pairs, norm):
+    import sfmx
+    m = sfmx.BFMatcher(norm, device=0)
+    try:
+        m.set_images(imgs)
+        m.run(pairs, sfmx.LOWE_RATIO)
+        got, off, _ = m.fetch()
+    finally:
+        m.close()
+    return got, off
+
+
+def main():
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    import sfmx
+    from sfmx import shard, synth
+    kind, n_img = sys.argv[1], int(sys.argv[2])
+    if kind == "sift":
+        imgs = synth.sift_images(n_img, 8192)
+        pairs = sfmx.pairs_unordered(n_img)
+        norm = sfmx.NORM_L2
+    else:
+        imgs = synth.orb_images(n_img, 16384)
+        pairs = sfmx.pairs_grid(n_img, 3, 20)
+        norm = sfmx.NORM_HAMMING
+    rows = np.array([len(x) for x in imgs], np.int64)
+    mine, (lo, hi) = shard.shard_pairs(pairs, rows, rank, world)
+    got, off = match(imgs, mine, norm)
+    parts = [None] * world
+    dist.all_gather_object(parts, (lo, hi, got.tobytes(), off.tolist()))
+    if rank == 0:
+        parts.sort(key=lambda t: t[0])
+        covered = all(parts[i][1] == parts[i + 1][0] for i in range(world - 1)) and parts[0][0] == 0 and \
+            parts[-1][1] == len(pairs)
+        merged = b"".join(p[2] for p in parts)
+        moff = [0]
+        for p in parts:
+            moff += [moff[-1] + x for x in p[3][1:]]
+        one, ooff = match(imgs, pairs, norm)
+        print(json.dumps({"covered": bool(covered), "equal": merged == one.tobytes() and moff == ooff.tolist(),
+                          "matches": int(ooff[-1]), "pairs": int(len(pairs)),
+                          "per_rank_pairs": [p[1] - p[0] for p in parts]}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

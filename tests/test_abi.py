@@ -75,3 +75,81 @@ def test_no_gpu_fails_loudly():
         pytest.skip("a gfx950 device is visible")
     with pytest.raises(_lib.SfmxError):
         sfmx.BFMatcher(sfmx.NORM_L2)
+
+
+# ---- header <-> binding agreement --------------------------------
+
+_SCALARS = {"int32_t": "c_int32", "int64_t": "c_int64", "uint32_t": "c_uint32", "double": "c_double",
+            "float": "c_float", "int": "c_int", "char": "c_char"}
+
+
+def _declarations():
+    """(name, return type, [param types]) of every function the headers declare."""
+    out = []
+    for h in sorted(glob.glob(os.path.join(REPO, "include", "*.h"))):
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        src = re.sub(r"//[^\n]*", "", src)
+        src = re.sub(r"typedef[^;]*;", "", src)
+        src = re.sub(r"^\s*#[^\n]*", "", src, flags=re.M)
+        src = src.replace('extern "C" {', "")
+        for m in re.finditer(r"([A-Za-z_][\w\s\*]*?)\b(sfmx_\w+)\s*\(([^()]*)\)\s*;", src):
+            ret, name, params = " ".join(m.group(1).split()), m.group(2), " ".join(m.group(3).split())
+            ps = [] if params in ("", "void") else [re.sub(r"\s*\b\w+$", "", p.strip()) for p in params.split(",")]
+            out.append((name, ret, ps))
+    return out
+
+
+def _ctype_ok(ctype_decl, ct):
+    import ctypes as C
+    t = ctype_decl.replace("const", "").strip()
+    if t == "void":
+        return ct is None
+    if t == "sfmx_allreduce_fn":
+        return ct is _lib.ALLREDUCE_FN
+    if "*" in t:
+        base = t.replace("*", "").strip()
+        if base == "char" and t.count("*") == 1:
+            return ct in (C.c_char_p, C.c_void_p)
+        return ct is C.c_void_p or (isinstance(ct, type) and issubclass(ct, C._Pointer))
+    return ct is getattr(C, _SCALARS[t])
+
+
+@pytest.mark.parametrize("name,ret,params", _declarations(), ids=[d[0] for d in _declarations()])
+def test_ctypes_prototype_matches_header(name, ret, params):
+    assert name in _lib.PROTOTYPES, name
+    res, args = _lib.PROTOTYPES[name]
+    assert len(args) == len(params), f"{name}: header has {len(params)} params, binding {len(args)}"
+    assert _ctype_ok(ret, res), f"{name}: return {ret} vs {res}"
+    for i, (p, a) in enumerate(zip(params, args)):
+        assert _ctype_ok(p, a), f"{name}: param {i} {p} vs {a}"
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """sizeof/offsetof of the ABI structs from a C compile of the headers == the ctypes mirrors."""
+    import ctypes as C
+    import subprocess
+    structs = {"sfmx_dmatch": _lib.sfmx_dmatch, "sfmx_desc": _lib.sfmx_desc, "sfmx_ba_problem": _lib.sfmx_ba_problem,
+               "sfmx_ba_options": _lib.sfmx_ba_options, "sfmx_ba_summary": _lib.sfmx_ba_summary}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sfmx.h"', '#include "sfmx_ba.h"', 'int main(void){']
+    for s, cls in structs.items():
+        lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{s}.{f} %zu\\n", offsetof({s}, {f}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n") if l)
+    for s, cls in structs.items():
+        assert int(got[s]) == C.sizeof(cls), s
+        for f, _ in cls._fields_:
+            assert int(got[f"{s}.{f}"]) == getattr(cls, f).offset, f"{s}.{f}"
+
+
+def test_integration_adapter_is_the_compiled_one():
+    """INTEGRATION.md §2 shows exactly the adapter body tests/cpp compiles and the GPU suite runs."""
+    body = open(os.path.join(REPO, "tests", "cpp", "GpuFeatureMatchingStrategy.h")).read()
+    adapter = body[body.index("// --- adapter begin ---\n") + 24: body.index("// --- adapter end ---")]
+    assert adapter in open(os.path.join(REPO, "INTEGRATION.md")).read()
+    assert os.path.exists(os.path.join(REPO, "tests", "cpp", "adapter_test")), "build() compiles tests/cpp/adapter_test"

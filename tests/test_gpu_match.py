@@ -241,3 +241,43 @@ def test_errors():
     with pytest.raises(ValueError):
         m.run(np.array([[0, 5]]))
     m.close()
+
+
+# Kernel builds that gave wrong results in r01, selectable again:
+#   ORB pass 2 with 2 / 4 query tiles per wave (128- / 256-query items, variants 13 / 14): the r01
+#   builds kept compact_work_kernel's item size at 512 queries while a block covered 128 / 256,
+#   so pass 2 skipped the rest of each item (now a static_assert, and assemble_kernel counts any
+#   forwarded query pass 2 left unwritten: the run fails with SFMX_EINTERNAL);
+#   ORB16 single pass 4 tiles x 8 waves (7), 32x32 ORB with MINW = 1 (9, 4), SIFT single pass with
+#   MINW = 1 (30, 31).
+ORB_KATS = ["kat_orb_ties", "kat_orb_ties_r15", "orb_small"]
+SIFT_KATS = ["kat_sift_nt1_nt0", "kat_sift_ties", "kat_sift_ties_r15", "sift_small"]
+
+
+@pytest.mark.parametrize("env,variant", [("SFMX_ORB_VARIANT", "13"), ("SFMX_ORB_VARIANT", "14"),
+                                         ("SFMX_ORB_VARIANT", "7"), ("SFMX_ORB_VARIANT", "9"),
+                                         ("SFMX_ORB_VARIANT", "4"), ("SFMX_SIFT_VARIANT", "30"),
+                                         ("SFMX_SIFT_VARIANT", "31")])
+def test_previously_failing_variants(env, variant):
+    from oracle import oracle
+    names = ORB_KATS if env == "SFMX_ORB_VARIANT" else SIFT_KATS
+    os.environ[env] = variant
+    try:
+        for name in names:
+            d = fixtures.load(name)
+            m, off, _, _ = run(d["imgs"], d["pairs"], d["ratio"])
+            assert_same(m, off, d["matches"], d["offsets"])
+        if env == "SFMX_ORB_VARIANT":
+            base = synth.orb_images(4, 1200, seed=61)
+            base[1][:40] = base[0][:40]
+            imgs = [base[0], base[1][:900], base[2], base[3][:2]]
+        else:
+            base = synth.sift_images(5, 1100, seed=57)
+            imgs = [b[:n] for b, n in zip(base, [1, 33, 513, 1100, 1100])]
+        pairs = sfmx.pairs_unordered(len(imgs))
+        for ratio in (0.7, 1.5):
+            m, off, _, _ = run(imgs, pairs, ratio)
+            em, eoff = oracle.match_pairs(imgs, pairs, ratio)
+            assert_same(m, off, em, eoff)
+    finally:
+        del os.environ[env]

@@ -34,6 +34,39 @@ def test_bit_exact_many_points_and_limit():
     _check(img, contrastThreshold=0.04, nfeatures=len(k) // 3)
 
 
+@pytest.mark.parametrize("seed,nf", [(0, 0), (2, 0), (3, 1), (4, 2), (5, 0)])
+def test_compute_from_undoubled_pyramid(seed, nf):
+    """No kept keypoint from the doubled octave -> compute() rebuilds the pyramid from
+    firstOctave = 0 (OpenCV 4.5.1 SIFT_Impl::detectAndCompute with useProvidedKeypoints)."""
+    img = sift_cases.big_blob_image(160, 200, seed=seed)
+    k = _check(img, nfeatures=nf)
+    assert len(k) > 0 and np.all((k["octave"] & 255).astype(np.int8) >= 0)
+
+
+def test_nfeatures_reorders_like_retain_best():
+    """retainBest's nth_element + partition reorder the kept keypoints; descriptor rows follow."""
+    img = sift_cases.blob_image(260, 300, n_blobs=260, seed=17)
+    ek, _ = oracle.sift(img, contrast_threshold=0.04)
+    for nf in (len(ek) // 2, len(ek) // 5, 7):
+        _check(img, contrastThreshold=0.04, nfeatures=nf)
+
+
+def test_37mp_image_fits_the_arena():
+    """A 6144 x 6144 photo (37.7 MP), host input: the scratch arena must hold both doubled-size
+    float buffers, the staged image and the staged descriptors. Expected output is the oracle's,
+    committed (tests/golden/sift_37mp.npz, tests/golden/make_sift_big.py: ~2 min of oracle time)."""
+    import hashlib
+    import os
+    import sfmx
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "sift_37mp.npz"))
+    img = sift_cases.big_photo_37mp()
+    assert hashlib.sha256(img.tobytes()).digest() == g["sha256"].tobytes(), "fixture image changed"
+    k, d = sfmx.features.SIFT.create(nfeatures=3000).detectAndCompute(img)
+    assert len(k) == len(g["keypoints"]) > 100
+    assert k.tobytes() == g["keypoints"].tobytes()
+    assert np.array_equal(d, g["descriptors"].astype(np.float32))
+
+
 def test_large_sigma_uses_the_two_pass_blur():
     """sigma 3.2: the top layers' kernels exceed the fused tile's radius (16) and
     take the row/column/DoG kernels; both paths must agree with the oracle."""
