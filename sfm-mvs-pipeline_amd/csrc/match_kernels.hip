@@ -84,6 +84,17 @@ constexpr int KEY_VALID = -(1 << 29);
 constexpr int UNSETTLED = -3;
 static_assert(PAD_KEY < KEY_VALID - (1 << 22), "pad keys must never look valid");
 
+// Lowe's acceptance applied to the best index as an all-ones mask, with no bool PHI.
+// ROCm 7.2 (clang 22) miscompiled `acc = nt >= 2 ? (d1 < d2 * ratio) : true; out = acc ? J1 : -1`
+// in some register allocations (MINW = 1 / other tilings): the divergent select became an
+// exec-masked PHI whose -1 default was written with the full exec mask into the VGPR that also
+// held J1, which the same block had already reused as a temporary, so every query of a pair with
+// nt >= 2 came out rejected.  Integer arithmetic keeps it a straight-line select.
+__device__ __forceinline__ int lowe_select(int j1, float d1, float d2, int nt, double ratio) {
+    const int rej = (int)(nt >= 2) & (int)!((double)d1 < (double)d2 * ratio);
+    return j1 | -rej;
+}
+
 // Bijective XCD-contiguous remap: blocks b, b+8, ... share an XCD (observed
 // round-robin dispatch; speed only, never correctness).
 __device__ __forceinline__ int xcd_remap(int b, int nwg) {
@@ -426,9 +437,7 @@ void sift_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restri
             continue;
         }
         const float d1 = sqrt_rn_int(s1);
-        bool acc = true;
-        if (nt >= 2) acc = (double)d1 < (double)sqrt_rn_int(s2) * ratio;
-        out_idx[o] = acc ? J1[qt] : -1;
+        out_idx[o] = lowe_select(J1[qt], d1, nt >= 2 ? sqrt_rn_int(s2) : 0.f, nt, ratio);
         out_dist[o] = d1;
     }
 }
@@ -795,9 +804,8 @@ void sift_slow_kernel(const int2* __restrict__ slow_list, const int32_t* __restr
         }
         if (lane == 0) {
             const float d1 = __uint_as_float((unsigned)(b1 >> 32)), d2 = __uint_as_float((unsigned)(b2 >> 32));
-            const bool acc = (double)d1 < (double)d2 * ratio;     // slow path implies nt >= 2
             const int64_t o = P.dense_base + it.y;
-            out_idx[o] = acc ? (int)(b1 & 0xffffffffu) : -1;
+            out_idx[o] = lowe_select((int)(b1 & 0xffffffffu), d1, d2, 2, ratio);   // slow path implies nt >= 2
             out_dist[o] = d1;
         }
     }
@@ -848,8 +856,7 @@ void sift_f32_kernel(const WorkItem* __restrict__ work, const int32_t* __restric
     const int64_t o = P.dense_base + qi;
     if (R.rows == 0) { out_idx[o] = -1; out_dist[o] = 0.f; return; }
     const float d1 = __uint_as_float(b1), d2 = __uint_as_float(b2);
-    const bool acc = R.rows >= 2 ? ((double)d1 < (double)d2 * ratio) : true;
-    out_idx[o] = acc ? j1 : -1;
+    out_idx[o] = lowe_select(j1, d1, d2, R.rows, ratio);
     out_dist[o] = d1;
 }
 
@@ -1006,8 +1013,7 @@ void orb_mfma_kernel(const WorkItem* __restrict__ work, const PairDev* __restric
         const int64_t o = P.dense_base + qi;
         if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }
         const float d1 = (float)T1[qt], d2 = (float)T2[qt];
-        const bool acc = nt >= 2 ? ((double)d1 < (double)d2 * ratio) : true;
-        out_idx[o] = acc ? J1[qt] : -1;
+        out_idx[o] = lowe_select(J1[qt], d1, d2, nt, ratio);
         out_dist[o] = d1;
     }
 }
@@ -1172,8 +1178,7 @@ void orb_mfma16_kernel(const WorkItem* __restrict__ work, const PairDev* __restr
         const int64_t o = P.dense_base + qi;
         if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }
         const float d1 = (float)T1[qt], d2 = (float)T2[qt];
-        const bool acc = nt >= 2 ? ((double)d1 < (double)d2 * ratio) : true;
-        out_idx[o] = acc ? J1[qt] : -1;
+        out_idx[o] = lowe_select(J1[qt], d1, d2, nt, ratio);
         out_dist[o] = d1;
     }
 }
@@ -1393,8 +1398,7 @@ void orb_knn2_kernel(const WorkItem* __restrict__ work, const PairDev* __restric
         const int64_t o = P.dense_base + qi;
         if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }
         const float d1 = (float)(b1[e] >> 23), d2 = (float)(b2[e] >> 23);
-        const bool acc = nt >= 2 ? ((double)d1 < (double)d2 * ratio) : true;
-        out_idx[o] = acc ? (int)(b1[e] & 0x7fffffu) : -1;
+        out_idx[o] = lowe_select((int)(b1[e] & 0x7fffffu), d1, d2, nt, ratio);
         out_dist[o] = d1;
     }
 }
