@@ -3,19 +3,26 @@
 //
 // Replaces BundleAdjustment::doBundleAdjustment (src/photogrammetrie/common/
 // BundleAdjustment.cpp:29-141) + CeresUtils::solve (util/CeresUtils.cpp:38-56):
-//   * problem assembly as flat CSR arrays in O(observations), instead of one
+//   * problem assembly as flat arrays in O(observations), instead of one
 //     OpenMpUtils::find_if parallel region per observation (BundleAdjustment.cpp:66-69);
 //   * the Ceres 1.14 trust-region / Levenberg-Marquardt loop with DENSE_SCHUR on the
-//     host, every numeric step in the HIP kernels of ba_kernels.hpp; only a handful of
-//     scalars cross PCIe per iteration.
+//     host, every numeric step in the HIP kernels of ba_group.hpp / ba_kernels.hpp; one
+//     host round trip (8 scalars) per LM step.
 // The controller mirrors oracle/ba_oracle.cpp (the CPU restatement) step for step.
-#include "ba_kernels.hpp"
+//
+// Per LM step (try_step), in stream order:
+//   ba_gschur -> memset S -> ba_assemble -> [all-reduce S, rhs] -> ba_add_cam -> chol_first,
+//   chol_step x (T-1), chol_back_all -> ba_gupdate, ba_fstep -> ba_glin (the candidate,
+//   speculatively: its Jacobian is the next linearization if the step is accepted) -> ba_camred
+//   -> [all-reduce] -> ba_finalize -> [all-reduce scalars] -> one D2H of the scalars.
+#include "ba_group.hpp"
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstring>
 #include <limits>
+#include <map>
 #include <string>
 #include <cstdlib>
 #include <unordered_map>
@@ -65,16 +72,16 @@ struct sfmx_ba_ctx {
     int P = 0, C = 0, O = 0, K = 0;
     double cx = 0, cy = 0;
     int64_t n = 0, ne = 0;
-    int nf = 0, npad = 0, T = 0, nblocks = 0, nvz = 0;
+    int nf = 0, npad = 0, T = 0;
     sfmx_allreduce_fn ar = nullptr;
     void* ar_user = nullptr;
-    // topology
-    Buf obs_point, obs_cam, obs_xy, pt_start, pt_obs, cam_start, cam_obs, campos, blk_cam, blk_start, trip;
-    Buf pgrp, pbig;   // ba_point_blocks_lds point groups (bounds) / points with more than PB_CAPO observations
-    int ngrp = 0, nbig = 0;
-    // state
-    Buf x, cand, scale, colsq, grad, diag, D, J, partA, partB, scal, ipart;
-    Buf Einv, EinvG, R1, R2, vzpart, Scc, Spi, Sii, rc, ri, Spp, SR, Linv, sol, step, failf;
+    // topology: groups, chunks, group cameras, local camera per observation, assembly tasks
+    int ngroups = 0, ntasks = 0, nslots = 0, stage_n = 0;
+    size_t lds_schur = 0, lds_lin = 0, lds_upd = 0;
+    Buf obs_point, obs_cam, obs_xy, pt_start, grp, chk, gcam, obs_lc, tasks, ents, cref_start, cref;
+    // state (the *2 buffers hold the candidate's linearization until the step is accepted)
+    Buf x, cand, scale, colsq, colsq2, grad, grad2, J, J2, camsum, camsum2, plt, sg, rg, hbig, gpart, gpl, scal,
+        SR, Linv, sol, failf, partA;
     bool scaled = false;
     // locality order: internal point p' is caller point pperm[p']; internal
     // observation o' is caller observation operm[o'] (point-major)
@@ -82,10 +89,9 @@ struct sfmx_ba_ctx {
     double phase_ms[4] = {0, 0, 0, 0};
     hipEvent_t ev[6] = {};
     ~sfmx_ba_ctx() {
-        Buf* all[] = {&pgrp, &pbig, &obs_point, &obs_cam, &obs_xy, &pt_start, &pt_obs, &cam_start, &cam_obs, &campos, &blk_cam,
-                      &blk_start, &trip, &x, &cand, &scale, &colsq, &grad, &diag, &D, &J, &partA, &partB, &scal,
-                      &ipart, &Einv, &EinvG, &R1, &R2, &vzpart, &Scc, &Spi, &Sii, &rc, &ri, &Spp, &SR, &Linv, &sol,
-                      &step, &failf};
+        Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &gcam, &obs_lc, &tasks, &ents, &cref_start,
+                      &cref, &x, &cand, &scale, &colsq, &colsq2, &grad, &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg,
+                      &rg, &hbig, &gpart, &gpl, &scal, &SR, &Linv, &sol, &failf, &partA};
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
@@ -105,7 +111,7 @@ struct DeviceGuard {
 };
 
 int allreduce(sfmx_ba_ctx* c, double* buf, int64_t count, int op) {
-    if (!c->ar) return SFMX_OK;
+    if (!c->ar || count <= 0) return SFMX_OK;
     if (c->ar(buf, count, op, c->ar_user, (void*)c->st) != 0) return fail(SFMX_EDEVICE, "all-reduce callback failed");
     return SFMX_OK;
 }
@@ -118,120 +124,76 @@ int fetch_scalars(sfmx_ba_ctx* c, int i0, int cnt, double* out) {
     return SFMX_OK;
 }
 
-// 1/2 sum ||r||^2 at parameters xp (all ranks); with JAC also r + Jacobian into c->J.
-template <bool JAC>
-int eval(sfmx_ba_ctx* c, const double* xp, double* cost_out) {
+// 1/2 sum ||r||^2 at parameters xp with the Jacobian into c->partA-sized J (sfmx_ba_jacobian only).
+int eval_jacobian(sfmx_ba_ctx* c, const double* xp, double* cost_out) {
     const unsigned g = nblk(c->O);
     const double* pts = xp;
     const double* poses = xp + c->ne;
     const double* intr = poses + 6 * (size_t)c->C;
-#define LIN(KK) hipLaunchKernelGGL((ba_linearize<KK, JAC>), dim3(g), dim3(256), 0, c->st, c->O, c->obs_point.as<int>(), \
+#define LIN(KK) hipLaunchKernelGGL((ba_linearize<KK, true>), dim3(g), dim3(256), 0, c->st, c->O, c->obs_point.as<int>(), \
                                    c->obs_cam.as<int>(), c->obs_xy.as<double>(), c->cx, c->cy, pts, poses, intr,         \
                                    c->J.as<double>(), c->partA.as<double>())
     if (c->K == 1) LIN(1); else if (c->K == 3) LIN(3); else LIN(7);
 #undef LIN
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(ba_sum, dim3(1), dim3(256), 0, c->st, c->partA.as<double>(), (int)g, 0.5, scal(c, 0));
-    RC(allreduce(c, scal(c, 0), 1, SFMX_REDUCE_SUM));
     RC(fetch_scalars(c, 0, 1, cost_out));
     return SFMX_OK;
 }
 
-// After a linearisation: unscaled column norms and gradient, the Jacobi scale
-// (iteration 0 only), the clamped LM diagonal of the scaled Jacobian, |g|_max.
-int columns(sfmx_ba_ctx* c, double* gmax) {
-    double* cs = c->colsq.as<double>();
-    double* gr = c->grad.as<double>();
-    double* fcs = cs + c->ne;
-    double* fgr = gr + c->ne;
-#define COLS(KK)                                                                                                        \
-    hipLaunchKernelGGL(ba_point_cols<KK>, dim3(nblk(c->P)), dim3(256), 0, c->st, c->P, c->O, c->pt_start.as<int>(),     \
-                       c->pt_obs.as<int>(), c->J.as<double>(), cs, gr);                                                 \
-    hipLaunchKernelGGL(ba_cam_cols<KK>, dim3(std::max(c->C, 1)), dim3(256), 0, c->st, c->O, c->cam_start.as<int>(),     \
-                       c->cam_obs.as<int>(), c->J.as<double>(), fcs, fgr, c->ipart.as<double>());                       \
-    hipLaunchKernelGGL(ba_intr_cols_final<KK>, dim3(1), dim3(64), 0, c->st, c->C, c->ipart.as<double>(),                \
-                       fcs + 6 * (size_t)c->C, fgr + 6 * (size_t)c->C)
-    if (c->K == 1) { COLS(1); } else if (c->K == 3) { COLS(3); } else { COLS(7); }
-#undef COLS
+// Linearization at xp (x or the candidate) into (Jo, colsq_o, grad_o, camsum_o) and the LM scalars
+// into scal (cand_mode: the step's model / step-norm partials are already in gpl): -> out[SC_N].
+template <int K>
+int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double* grad_o, double* camsum_o,
+           bool cand_mode, double* out) {
+    if (c->ngroups > 0)
+        hipLaunchKernelGGL(ba_glin<K>, dim3(c->ngroups), dim3(256), c->lds_lin, c->st, c->grp.as<Grp>(),
+                           c->chk.as<Chunk>(), c->obs_lc.as<short>(), c->obs_point.as<int>(), c->obs_cam.as<int>(),
+                           c->obs_xy.as<double>(), c->pt_start.as<int>(), c->cx, c->cy, c->P, c->C, xp, Jo, colsq_o,
+                           grad_o, c->gpart.as<double>(), c->gpl.as<double>());
+    hipLaunchKernelGGL(ba_camred<K>, dim3(c->C + 1), dim3(128), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
+                       c->cref.as<int>(), c->gpart.as<double>(), camsum_o);
     HIPCHK(hipGetLastError());
-    RC(allreduce(c, fcs, c->nf, SFMX_REDUCE_SUM));   // camera / intrinsics columns: sums over all ranks' observations
-    RC(allreduce(c, fgr, c->nf, SFMX_REDUCE_SUM));
-    if (!c->scaled) {
-        if (c->opt.jacobi_scaling)
-            hipLaunchKernelGGL(ba_scale, dim3(nblk(c->n)), dim3(256), 0, c->st, (int)c->n, cs, c->scale.as<double>());
-        c->scaled = true;
-    }
-    const unsigned g = nblk(c->n);
-    hipLaunchKernelGGL(ba_diag, dim3(g), dim3(256), 0, c->st, (int)c->n, cs, c->scale.as<double>(), c->opt.min_lm_diagonal,
-                       c->opt.max_lm_diagonal, c->diag.as<double>(), gr, c->partB.as<double>());
-    hipLaunchKernelGGL(ba_max, dim3(1), dim3(256), 0, c->st, c->partB.as<double>(), (int)g, scal(c, 1));
+    RC(allreduce(c, camsum_o, (int64_t)c->C * ncp(K) + K * (K + 1) / 2 + K, SFMX_REDUCE_SUM));
+    hipLaunchKernelGGL(ba_finalize<K>, dim3(1), dim3(256), 0, c->st, c->ngroups, c->P, c->C, camsum_o,
+                       c->gpl.as<double>(), xp + c->ne, c->x.as<double>() + c->ne, cand_mode ? 1 : 0, c->failf.as<int>(),
+                       colsq_o, grad_o, scal(c, 0));
     HIPCHK(hipGetLastError());
-    RC(allreduce(c, scal(c, 1), 1, SFMX_REDUCE_MAX));
-    RC(fetch_scalars(c, 1, 1, gmax));
+    RC(allreduce(c, scal(c, SC_COST), 4, SFMX_REDUCE_SUM));
+    RC(allreduce(c, scal(c, SC_GMAX), 2, SFMX_REDUCE_MAX));
+    RC(fetch_scalars(c, 0, SC_N, out));
     return SFMX_OK;
 }
 
-// sum of squares of v over [0, ne) (summed across ranks) + [ne, n) (replicated) -> sqrt
-int split_norm(sfmx_ba_ctx* c, const double* v, double* out) {
-    const unsigned ge = nblk(c->ne), gf = nblk(c->nf);
-    hipLaunchKernelGGL(ba_sumsq, dim3(ge), dim3(256), 0, c->st, (int)c->ne, v, c->partA.as<double>());
-    hipLaunchKernelGGL(ba_sum, dim3(1), dim3(256), 0, c->st, c->partA.as<double>(), (int)ge, 1.0, scal(c, 2));
-    hipLaunchKernelGGL(ba_sumsq, dim3(gf), dim3(256), 0, c->st, c->nf, v + c->ne, c->partB.as<double>());
-    hipLaunchKernelGGL(ba_sum, dim3(1), dim3(256), 0, c->st, c->partB.as<double>(), (int)gf, 1.0, scal(c, 3));
-    HIPCHK(hipGetLastError());
-    RC(allreduce(c, scal(c, 2), 1, SFMX_REDUCE_SUM));
-    double s[2];
-    RC(fetch_scalars(c, 2, 2, s));
-    *out = std::sqrt(s[0] + s[1]);
-    return SFMX_OK;
-}
-
-// Schur solve of (J_s^T J_s + D^2) sol = J_s^T r, step_s = -sol, candidate
-// = x + step_s * scale; model cost change, step norm, candidate cost.
-int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* step_norm, double* ccost) {
-    const int K = c->K, P = c->P, O = c->O, C = c->C, npad = c->npad, T = c->T;
+// One LM step at `radius`: Schur solve of (J_s^T J_s + D^2) sol = J_s^T r, step_s = -sol,
+// candidate = x + step_s * scale, its cost, Jacobian and scalars (speculative linearization).
+template <int K>
+int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* step_norm, double* ccost,
+             double* cgmax, double* cxnorm) {
+    const int C = c->C, npad = c->npad, T = c->T;
     double* S = c->SR.as<double>();
     double* rhs = S + (size_t)npad * npad;
     int* fl = c->failf.as<int>();
-    HIPCHK(hipEventRecord(c->ev[0], c->st));
-    hipLaunchKernelGGL(ba_lm_d, dim3(nblk(c->n)), dim3(256), 0, c->st, (int)c->n, c->diag.as<double>(), radius,
-                       c->D.as<double>());
+    const sfmx_ba_options& o = c->opt;
     HIPCHK(hipMemsetAsync(fl, 0, sizeof(int), c->st));
-#define SCHUR(KK)                                                                                                      \
-    if (c->ngrp > 0)                                                                                                   \
-        hipLaunchKernelGGL(ba_point_blocks_lds<KK>, dim3(c->ngrp), dim3(256), 0, c->st, c->pgrp.as<int>(), P, C,       \
-                           c->pt_start.as<int>(), c->obs_cam.as<int>(), c->campos.as<int>(), c->J.as<double>(),        \
-                           c->scale.as<double>(), c->D.as<double>(), c->Einv.as<double>(), c->EinvG.as<double>(),      \
-                           c->R1.as<double>(), c->R2.as<double>(), c->vzpart.as<double>(), fl);                        \
-    if (c->nbig > 0)                                                                                                   \
-        hipLaunchKernelGGL(ba_point_blocks<KK>, dim3(nblk(c->nbig)), dim3(256), 0, c->st, P, O, C, c->pt_start.as<int>(), \
-                           c->pt_obs.as<int>(), c->obs_cam.as<int>(), c->campos.as<int>(), c->J.as<double>(),          \
-                           c->scale.as<double>(), c->D.as<double>(), c->Einv.as<double>(), c->EinvG.as<double>(),      \
-                           c->R1.as<double>(), c->R2.as<double>(), c->vzpart.as<double>() + (size_t)c->ngrp * KK * KK, \
-                           fl, c->pbig.as<int>(), c->nbig);                                                            \
-    if (C > 0)                                                                                                         \
-        hipLaunchKernelGGL(ba_cam_blocks<KK>, dim3(C), dim3(256), 0, c->st, C, c->cam_start.as<int>(),                 \
-                           c->R2.as<double>(), c->Scc.as<double>(), c->Spi.as<double>(), c->rc.as<double>(),           \
-                           c->ipart.as<double>());                                                                     \
-    hipLaunchKernelGGL(ba_intr_final<KK>, dim3(KK * KK + KK), dim3(256), 0, c->st, C, c->nvz, c->ipart.as<double>(),   \
-                       c->vzpart.as<double>(), c->Sii.as<double>(), c->ri.as<double>());                               \
-    if (c->nblocks > 0)                                                                                                \
-        hipLaunchKernelGGL(ba_pair_blocks<KK>, dim3(c->nblocks), dim3(256), 0, c->st, c->blk_start.as<int>(),          \
-                           c->trip.as<int2>(), c->R1.as<double>(), c->Spp.as<double>())
-    if (K == 1) { SCHUR(1); } else if (K == 3) { SCHUR(3); } else { SCHUR(7); }
-#undef SCHUR
+    HIPCHK(hipEventRecord(c->ev[0], c->st));
+    if (c->ngroups > 0)
+        hipLaunchKernelGGL(ba_gschur<K>, dim3(c->ngroups), dim3(256), c->lds_schur, c->st, c->grp.as<Grp>(),
+                           c->chk.as<Chunk>(), c->gcam.as<int>(), c->obs_lc.as<short>(), c->obs_point.as<int>(),
+                           c->obs_cam.as<int>(), c->pt_start.as<int>(), c->J.as<double>(), c->scale.as<double>(),
+                           c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, c->P, C, c->stage_n,
+                           c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl);
     HIPCHK(hipMemsetAsync(S, 0, sizeof(double) * ((size_t)npad * npad + npad), c->st));
-    if (c->nblocks > 0)
-        hipLaunchKernelGGL(ba_assemble_pairs, dim3(c->nblocks), dim3(64), 0, c->st, npad, c->blk_cam.as<int>(),
-                           c->Spp.as<double>(), S);
-    if (C > 0) hipLaunchKernelGGL(ba_assemble_diag, dim3(C), dim3(64), 0, c->st, npad, c->Scc.as<double>(), S);
-    hipLaunchKernelGGL(ba_assemble_rest, dim3(nblk(npad)), dim3(256), 0, c->st, C, K, c->nf, npad, c->Spi.as<double>(),
-                       c->Sii.as<double>(), c->rc.as<double>(), c->ri.as<double>(), S, rhs);
+    hipLaunchKernelGGL(ba_assemble, dim3(c->ntasks), dim3(64), 0, c->st, c->tasks.as<ATask>(), c->ents.as<AEnt>(),
+                       c->grp.as<Grp>(), c->sg.as<double>(), c->hbig.as<double>(), c->rg.as<double>(), C, K, c->nf,
+                       npad, S, rhs);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->st));
-    // point-sharded ranks: the reduced camera system and its rhs are sums over ranks
+    // point-sharded ranks: the group part of the reduced camera system and its rhs are sums over ranks
     RC(allreduce(c, S, (int64_t)npad * npad + npad, SFMX_REDUCE_SUM));
-    hipLaunchKernelGGL(ba_add_damping, dim3(nblk(c->nf)), dim3(256), 0, c->st, P, c->nf, npad, c->D.as<double>(), S);
+    hipLaunchKernelGGL(ba_add_cam<K>, dim3(C + 1), dim3(64), 0, c->st, c->P, C, npad, c->camsum.as<double>(),
+                       c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, S,
+                       rhs);
     double* W = c->Linv.as<double>();
     double* sol = c->sol.as<double>();
     hipLaunchKernelGGL(chol_first, dim3(1), dim3(256), 0, c->st, S, npad, W, rhs, fl);
@@ -239,60 +201,30 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
         const int m = T - k - 1;
         hipLaunchKernelGGL(chol_step, dim3(m * (m + 1) / 2), dim3(256), 0, c->st, S, npad, k, W, rhs, fl);
     }
-    for (int k = T - 1; k >= 0; --k)
-        hipLaunchKernelGGL(chol_back, dim3(std::max(k, 1)), dim3(256), 0, c->st, S, npad, c->nf, k, rhs, sol + c->ne);
-#define BACK(KK)                                                                                                    \
-    hipLaunchKernelGGL(ba_backsub<KK>, dim3(nblk(P)), dim3(256), 0, c->st, P, C, c->pt_start.as<int>(),              \
-                       c->pt_obs.as<int>(), c->obs_cam.as<int>(), c->R1.as<double>(), c->EinvG.as<double>(), sol + c->ne, sol)
-    if (K == 1) { BACK(1); } else if (K == 3) { BACK(3); } else { BACK(7); }
-#undef BACK
+    hipLaunchKernelGGL(chol_back_all, dim3(1), dim3(256), 0, c->st, S, npad, c->nf, T, rhs, sol + c->ne);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[2], c->st));
-    // step, candidate, ||x - candidate||^2 split into the rank-local point part and the replicated rest
-    const unsigned ge = nblk(c->ne), gf = nblk(c->nf);
-    double* x = c->x.as<double>();
-    double* cand = c->cand.as<double>();
-    double* stp = c->step.as<double>();
-    hipLaunchKernelGGL(ba_step, dim3(ge), dim3(256), 0, c->st, (int)c->ne, sol, c->scale.as<double>(), x, stp, cand,
-                       c->partA.as<double>());
-    hipLaunchKernelGGL(ba_sum, dim3(1), dim3(256), 0, c->st, c->partA.as<double>(), (int)ge, 1.0, scal(c, 4));
-    hipLaunchKernelGGL(ba_step, dim3(gf), dim3(256), 0, c->st, c->nf, sol + c->ne, c->scale.as<double>() + c->ne,
-                       x + c->ne, stp + c->ne, cand + c->ne, c->partB.as<double>());
-    hipLaunchKernelGGL(ba_sum, dim3(1), dim3(256), 0, c->st, c->partB.as<double>(), (int)gf, 1.0, scal(c, 5));
-    const unsigned go = nblk(O);
-#define MODEL(KK)                                                                                                 \
-    hipLaunchKernelGGL(ba_model<KK>, dim3(go), dim3(256), 0, c->st, P, O, C, c->obs_point.as<int>(),              \
-                       c->obs_cam.as<int>(), c->J.as<double>(), c->scale.as<double>(), stp, c->partA.as<double>())
-    if (K == 1) { MODEL(1); } else if (K == 3) { MODEL(3); } else { MODEL(7); }
-#undef MODEL
-    hipLaunchKernelGGL(ba_sum, dim3(1), dim3(256), 0, c->st, c->partA.as<double>(), (int)go, 1.0, scal(c, 6));
+    if (c->ngroups > 0)
+        hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups), dim3(256), c->lds_upd, c->st, c->grp.as<Grp>(),
+                           c->chk.as<Chunk>(), c->obs_point.as<int>(), c->obs_cam.as<int>(), c->pt_start.as<int>(),
+                           c->J.as<double>(), c->scale.as<double>(), c->plt.as<double>(), sol + c->ne, c->P, C,
+                           c->x.as<double>(), c->cand.as<double>(), c->gpl.as<double>());
+    hipLaunchKernelGGL(ba_fstep, dim3(nblk(c->nf)), dim3(256), 0, c->st, c->nf, sol + c->ne, c->scale.as<double>() + c->ne,
+                       c->x.as<double>() + c->ne, c->cand.as<double>() + c->ne);
     HIPCHK(hipGetLastError());
-    // fail flag as a double for the cross-rank max
-    {
-        int h_fail = 0;
-        HIPCHK(hipMemcpyAsync(&h_fail, fl, sizeof(int), hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipStreamSynchronize(c->st));
-        double fd = h_fail ? 1.0 : 0.0;
-        HIPCHK(hipMemcpyAsync(scal(c, 7), &fd, sizeof(double), hipMemcpyHostToDevice, c->st));
-        HIPCHK(hipStreamSynchronize(c->st));
-    }
-    RC(allreduce(c, scal(c, 4), 1, SFMX_REDUCE_SUM));
-    RC(allreduce(c, scal(c, 6), 1, SFMX_REDUCE_SUM));
-    RC(allreduce(c, scal(c, 7), 1, SFMX_REDUCE_MAX));
-    double v[4];
-    RC(fetch_scalars(c, 4, 4, v));
-    const double sn2 = v[0] + v[1];
-    *mcc = -v[2];
-    *step_norm = std::sqrt(sn2);
-    *valid = v[3] == 0.0 && std::isfinite(sn2) && std::isfinite(v[2]) && *mcc > 0.0;
-    *ccost = std::numeric_limits<double>::max();
-    if (*valid) {
-        double cc;
-        RC(eval<false>(c, cand, &cc));
-        *ccost = std::isfinite(cc) ? cc : std::numeric_limits<double>::max();
-    }
+    double v[SC_N];
+    RC(lin_at<K>(c, c->cand.as<double>(), c->J2.as<double>(), c->colsq2.as<double>(), c->grad2.as<double>(),
+                 c->camsum2.as<double>(), true, v));
     HIPCHK(hipEventRecord(c->ev[3], c->st));
     HIPCHK(hipEventSynchronize(c->ev[3]));
+    const double sn2 = v[SC_STEPN] + v[SC_STEPN_F];
+    *mcc = -v[SC_MODEL];
+    *step_norm = std::sqrt(sn2);
+    *valid = v[SC_FAIL] == 0.0 && std::isfinite(sn2) && std::isfinite(v[SC_MODEL]) && *mcc > 0.0;
+    *ccost = std::numeric_limits<double>::max();
+    if (*valid) *ccost = std::isfinite(v[SC_COST]) ? v[SC_COST] : std::numeric_limits<double>::max();
+    *cgmax = v[SC_GMAX];
+    *cxnorm = std::sqrt(v[SC_XN] + v[SC_XN_F]);
     float a = 0, b = 0, d = 0;
     HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
     HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
@@ -303,28 +235,31 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     return SFMX_OK;
 }
 
-int relinearize(sfmx_ba_ctx* c, double* cost, double* gmax) {
-    HIPCHK(hipEventRecord(c->ev[4], c->st));
-    RC(eval<true>(c, c->x.as<double>(), cost));
-    RC(columns(c, gmax));
-    HIPCHK(hipEventRecord(c->ev[5], c->st));
-    HIPCHK(hipEventSynchronize(c->ev[5]));
-    float a = 0;
-    HIPCHK(hipEventElapsedTime(&a, c->ev[4], c->ev[5]));
-    c->phase_ms[0] += a;
-    return SFMX_OK;
-}
-
-int run_lm(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace, int trace_cap, int* ntrace_out) {
+template <int K>
+int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace, int trace_cap, int* ntrace_out) {
     DeviceGuard dg(c->device);
     const auto t0 = std::chrono::steady_clock::now();
     const sfmx_ba_options& o = c->opt;
     const int maxit = max_iters > 0 ? max_iters : o.max_num_iterations;
     for (double& v : c->phase_ms) v = 0;
     c->scaled = false;   // Ceres computes the Jacobi scale at iteration 0 of each Solve
-    double cost, gmax, x_norm;
-    RC(relinearize(c, &cost, &gmax));
-    RC(split_norm(c, c->x.as<double>(), &x_norm));
+    HIPCHK(hipEventRecord(c->ev[4], c->st));
+    HIPCHK(hipMemsetAsync(c->failf.p, 0, sizeof(int), c->st));
+    double v[SC_N];
+    RC(lin_at<K>(c, c->x.as<double>(), c->J.as<double>(), c->colsq.as<double>(), c->grad.as<double>(),
+                 c->camsum.as<double>(), false, v));
+    if (o.jacobi_scaling)
+        hipLaunchKernelGGL(ba_scale, dim3(nblk(c->n)), dim3(256), 0, c->st, (int)c->n, c->colsq.as<double>(),
+                           c->scale.as<double>());
+    c->scaled = true;
+    HIPCHK(hipEventRecord(c->ev[5], c->st));
+    HIPCHK(hipEventSynchronize(c->ev[5]));
+    {
+        float a = 0;
+        HIPCHK(hipEventElapsedTime(&a, c->ev[4], c->ev[5]));
+        c->phase_ms[0] += a;
+    }
+    double cost = v[SC_COST], gmax = v[SC_GMAX], x_norm = std::sqrt(v[SC_XN] + v[SC_XN_F]);
     sum->initial_cost = cost;
     double radius = o.initial_trust_region_radius, decrease = 2.0;
     bool successful = true;
@@ -341,8 +276,8 @@ int run_lm(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace, i
         if (successful && gmax <= o.gradient_tolerance) { term = SFMX_BA_CONVERGENCE; break; }
         if (radius <= o.min_trust_region_radius) { term = SFMX_BA_CONVERGENCE; break; }
         ++iteration;
-        bool valid; double mcc, sn, ccost;
-        RC(try_step(c, radius, &valid, &mcc, &sn, &ccost));
+        bool valid; double mcc, sn, ccost, cgmax, cxn;
+        RC(try_step<K>(c, radius, &valid, &mcc, &sn, &ccost, &cgmax, &cxn));
         if (!valid) {   // HandleInvalidStep
             ++invalid_total;
             if (++consec_invalid >= o.max_num_consecutive_invalid_steps) { term = SFMX_BA_FAILURE; break; }
@@ -354,10 +289,15 @@ int run_lm(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace, i
         if (sn <= o.parameter_tolerance * (x_norm + o.parameter_tolerance)) { term = SFMX_BA_CONVERGENCE; break; }
         if (std::fabs(cost - ccost) <= o.function_tolerance * cost) { term = SFMX_BA_CONVERGENCE; break; }
         const double rel = (cost - ccost) / mcc;
-        if (rel > o.min_relative_decrease) {   // HandleSuccessfulStep
+        if (rel > o.min_relative_decrease) {   // HandleSuccessfulStep: the candidate's linearization is current
             std::swap(c->x, c->cand);
-            RC(split_norm(c, c->x.as<double>(), &x_norm));
-            RC(relinearize(c, &cost, &gmax));
+            std::swap(c->J, c->J2);
+            std::swap(c->colsq, c->colsq2);
+            std::swap(c->grad, c->grad2);
+            std::swap(c->camsum, c->camsum2);
+            cost = ccost;
+            gmax = cgmax;
+            x_norm = cxn;
             radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3));
             radius = std::min(o.max_trust_region_radius, radius);
             decrease = 2.0;
@@ -379,6 +319,12 @@ int run_lm(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace, i
     sum->final_radius = radius;
     if (ntrace_out) *ntrace_out = ntrace;
     return SFMX_OK;
+}
+
+int run_lm(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace, int trace_cap, int* ntrace_out) {
+    if (c->K == 1) return run_lm_k<1>(c, max_iters, sum, trace, trace_cap, ntrace_out);
+    if (c->K == 3) return run_lm_k<3>(c, max_iters, sum, trace, trace_cap, ntrace_out);
+    return run_lm_k<7>(c, max_iters, sum, trace, trace_cap, ntrace_out);
 }
 
 int validate(const sfmx_ba_problem* pb) {
@@ -417,8 +363,8 @@ int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
 
 // Locality order (internal only; results are reported in the caller's order):
 // points sorted by their sorted camera lists (points seen by the same cameras
-// become neighbours, so the per-camera and per-camera-pair gathers of the Schur
-// kernels hit contiguous records), observations point-major in that order.
+// become neighbours, so a point group spans few cameras), observations
+// point-major in that order.
 void locality_order(const sfmx_ba_problem* pb, std::vector<int>& pperm, std::vector<int>& operm) {
     const int P = pb->n_points, O = pb->n_obs;
     std::vector<int> start(P + 1, 0), obs(O);
@@ -445,6 +391,127 @@ void locality_order(const sfmx_ba_problem* pb, std::vector<int>& pperm, std::vec
         for (int a = start[pperm[q]]; a < start[pperm[q] + 1]; ++a) operm.push_back(obs[a]);
 }
 
+// Point groups, chunks, local cameras, assembly task lists and camera slot lists (see ba_group.hpp).
+struct Topology {
+    std::vector<Grp> grp;
+    std::vector<Chunk> chk;
+    std::vector<int> gcam, cref_start, cref;
+    std::vector<short> obs_lc;
+    std::vector<ATask> tasks;
+    std::vector<AEnt> ents;
+    long long sg_total = 0, h_total = 0;
+    int rg_total = 0, dp_max = 16;
+};
+
+void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start, const int* obs_cam, Topology& tp) {
+    tp.obs_lc.assign(O, 0);
+    std::vector<int> cur;   // sorted union of the open group's cameras
+    int g_p0 = 0, g_obs = 0;
+    auto add_group = [&](int p0, int p1, const std::vector<int>& cams, bool big) {
+        Grp G{};
+        G.o0 = pt_start[p0]; G.o1 = pt_start[p1]; G.p0 = p0; G.p1 = p1;
+        G.u = (int)cams.size();
+        G.cam_off = (int)tp.gcam.size();
+        G.big = big ? 1 : 0;
+        const int dim = 6 * G.u + K;
+        G.rg_off = tp.rg_total;
+        tp.rg_total += dim;
+        G.ch0 = (int)tp.chk.size();
+        G.nch = 0;
+        if (big) {
+            G.h_off = tp.h_total;
+            tp.h_total += (long long)dim * 3;
+            G.sg_off = 0;
+        } else {
+            G.sg_off = tp.sg_total;
+            tp.sg_total += (long long)dim * dim;
+            G.h_off = 0;
+            tp.dp_max = std::max(tp.dp_max, (dim + 15) & ~15);
+            // chunks of whole points, <= GCH observations
+            int q = p0;
+            while (q < p1) {
+                Chunk ch{pt_start[q], pt_start[q], q - p0, q - p0};
+                while (q < p1 && pt_start[q + 1] - ch.o0 <= GCH) { ++q; }
+                ch.o1 = pt_start[q]; ch.q1 = q - p0;
+                tp.chk.push_back(ch);
+                ++G.nch;
+            }
+        }
+        for (int cm : cams) tp.gcam.push_back(cm);
+        for (int o = G.o0; o < G.o1; ++o)
+            tp.obs_lc[o] = (short)(std::lower_bound(cams.begin(), cams.end(), obs_cam[o]) - cams.begin());
+        tp.grp.push_back(G);
+    };
+    std::vector<int> pc, uni;
+    for (int p = 0; p < P; ++p) {
+        const int m = pt_start[p + 1] - pt_start[p];
+        pc.assign(obs_cam + pt_start[p], obs_cam + pt_start[p + 1]);
+        std::sort(pc.begin(), pc.end());
+        const bool dup = std::adjacent_find(pc.begin(), pc.end()) != pc.end();
+        pc.erase(std::unique(pc.begin(), pc.end()), pc.end());
+        const bool big = m > GCH || (int)pc.size() > UMAX || dup;
+        if (big) {
+            if (p > g_p0) add_group(g_p0, p, cur, false);
+            add_group(p, p + 1, pc, true);
+            g_p0 = p + 1; g_obs = 0; cur.clear();
+            continue;
+        }
+        uni.clear();
+        std::set_union(cur.begin(), cur.end(), pc.begin(), pc.end(), std::back_inserter(uni));
+        if (p > g_p0 && (g_obs + m > GOBS || p - g_p0 + 1 > GPTS || (int)uni.size() > UMAX)) {
+            add_group(g_p0, p, cur, false);
+            g_p0 = p; g_obs = 0; cur = pc;
+        } else {
+            cur.swap(uni);
+        }
+        g_obs += m;
+    }
+    if (P > g_p0) add_group(g_p0, P, cur, false);
+    // camera slots: per camera, its (group, local camera) slots in group order
+    tp.cref_start.assign(C + 1, 0);
+    for (const Grp& G : tp.grp)
+        for (int lc = 0; lc < G.u; ++lc) tp.cref_start[tp.gcam[G.cam_off + lc] + 1]++;
+    for (int c = 0; c < C; ++c) tp.cref_start[c + 1] += tp.cref_start[c];
+    tp.cref.assign(tp.cref_start[C], 0);
+    {
+        std::vector<int> f(tp.cref_start.begin(), tp.cref_start.end() - 1);
+        for (const Grp& G : tp.grp)
+            for (int lc = 0; lc < G.u; ++lc) tp.cref[f[tp.gcam[G.cam_off + lc]]++] = G.cam_off + lc;
+    }
+    // assembly tasks: pose blocks (a <= b) with their (group, la, lb) lists in group order, then
+    // pose-intrinsics blocks per camera, then the intrinsics block
+    std::map<std::pair<int, int>, std::vector<AEnt>> pairs;
+    for (int g = 0; g < (int)tp.grp.size(); ++g) {
+        const Grp& G = tp.grp[g];
+        for (int la = 0; la < G.u; ++la)
+            for (int lb = la; lb < G.u; ++lb)
+                pairs[{tp.gcam[G.cam_off + la], tp.gcam[G.cam_off + lb]}].push_back(AEnt{g, la, lb, 0});
+    }
+    for (auto& kv : pairs) {
+        ATask t{0, kv.first.first, kv.first.second, (int)tp.ents.size(), 0, 0, 0, 0};
+        tp.ents.insert(tp.ents.end(), kv.second.begin(), kv.second.end());
+        t.l1 = (int)tp.ents.size();
+        tp.tasks.push_back(t);
+    }
+    for (int cm = 0; cm < C; ++cm) {
+        ATask t{1, cm, 0, (int)tp.ents.size(), 0, 0, 0, 0};
+        for (int e = tp.cref_start[cm]; e < tp.cref_start[cm + 1]; ++e) {
+            const int slot = tp.cref[e];
+            const int g = (int)(std::upper_bound(tp.grp.begin(), tp.grp.end(), slot,
+                                                 [](int s, const Grp& G) { return s < G.cam_off; }) - tp.grp.begin()) - 1;
+            tp.ents.push_back(AEnt{g, slot - tp.grp[g].cam_off, 0, 0});
+        }
+        t.l1 = (int)tp.ents.size();
+        if (t.l1 > t.l0) tp.tasks.push_back(t);
+    }
+    {
+        ATask t{2, 0, 0, (int)tp.ents.size(), 0, 0, 0, 0};
+        for (int g = 0; g < (int)tp.grp.size(); ++g) tp.ents.push_back(AEnt{g, 0, 0, 0});
+        t.l1 = (int)tp.ents.size();
+        tp.tasks.push_back(t);
+    }
+}
+
 int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ctx** out) {
     RC(validate(caller));
     std::vector<int> pperm, operm, ipperm(caller->n_points), rop(caller->n_obs), roc(caller->n_obs);
@@ -458,12 +525,6 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
         rxy[2 * (size_t)q] = caller->obs_xy[2 * (size_t)o];
         rxy[2 * (size_t)q + 1] = caller->obs_xy[2 * (size_t)o + 1];
     }
-    sfmx_ba_problem internal = *caller;
-    internal.points = nullptr;   // parameters are uploaded from the caller's arrays by set_params
-    internal.obs_point = rop.data();
-    internal.obs_cam = roc.data();
-    internal.obs_xy = rxy.data();
-    const sfmx_ba_problem* pb = &internal;
     sfmx_ba_options o;
     sfmx_ba_default_options(&o);
     if (opt) o = *opt;
@@ -483,119 +544,59 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
     auto bail = [&](int rc) { delete c; return rc; };
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) return bail(fail(SFMX_EDEVICE, "stream"));
     for (auto& e : c->ev) if (hipEventCreate(&e) != hipSuccess) return bail(fail(SFMX_EDEVICE, "event"));
-    const int P = pb->n_points, C = pb->n_cams, O = pb->n_obs, K = pb->cam_model;
-    c->P = P; c->C = C; c->O = O; c->K = K; c->cx = pb->cx; c->cy = pb->cy;
+    const int P = caller->n_points, C = caller->n_cams, O = caller->n_obs, K = caller->cam_model;
+    c->P = P; c->C = C; c->O = O; c->K = K; c->cx = caller->cx; c->cy = caller->cy;
     c->ne = 3 * (int64_t)P;
     c->nf = 6 * C + K;
     c->n = c->ne + c->nf;
     c->npad = (c->nf + NB - 1) / NB * NB;
     c->T = c->npad / NB;
-    // CSR by point and by camera (stable: input order inside each list)
-    std::vector<int> pt_start(P + 1, 0), pt_obs(O), cam_start(C + 1, 0), cam_obs(O);
-    for (int i = 0; i < O; ++i) { pt_start[pb->obs_point[i] + 1]++; cam_start[pb->obs_cam[i] + 1]++; }
+    if (c->npad > 16 * 1024) return bail(fail(SFMX_EINVAL, "too many cameras for the dense reduced system (6C + k > 16384)"));
+    std::vector<int> pt_start(P + 1, 0);
+    for (int i = 0; i < O; ++i) pt_start[rop[i] + 1]++;
     for (int p = 0; p < P; ++p) pt_start[p + 1] += pt_start[p];
-    for (int k = 0; k < C; ++k) cam_start[k + 1] += cam_start[k];
+    Topology tp;
+    build_topology(P, C, O, K, pt_start, roc.data(), tp);
+    c->ngroups = (int)tp.grp.size();
+    c->ntasks = (int)tp.tasks.size();
+    c->nslots = (int)tp.gcam.size();
+    const int JS = jst(K);
+    c->stage_n = std::max(GCH * JS, tp.dp_max * ALD);
+    c->lds_schur = sizeof(double) * ((size_t)c->stage_n + (size_t)GPTS * (9 + 3 * K));
+    c->lds_lin = sizeof(double) * (size_t)GCH * JS + sizeof(short) * GCH;
+    c->lds_upd = sizeof(double) * ((size_t)GCH * JS + GCH * 3 + GPTS * 3);
     {
-        std::vector<int> fp(pt_start.begin(), pt_start.end() - 1), fc(cam_start.begin(), cam_start.end() - 1);
-        for (int i = 0; i < O; ++i) { pt_obs[fp[pb->obs_point[i]]++] = i; cam_obs[fc[pb->obs_cam[i]]++] = i; }
+        hipError_t e = hipSuccess;
+#define LDSATTR(KK)                                                                                                  \
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_gschur<KK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_schur); \
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_glin<KK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_lin);     \
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_gupdate<KK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_upd)
+        if (K == 1) { LDSATTR(1); } else if (K == 3) { LDSATTR(3); } else { LDSATTR(7); }
+#undef LDSATTR
+        if (e != hipSuccess) return bail(fail(SFMX_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(e)));
     }
-    std::vector<int> campos(O);   // position of each observation in the camera-major order
-    for (int a = 0; a < O; ++a) campos[cam_obs[a]] = a;
-    // camera-pair blocks of the reduced system: ordered observation pairs of
-    // each point with cam(a) <= cam(b), bucketed by (cam(a), cam(b)) (point order inside a bucket)
-    std::unordered_map<int64_t, int> bid;
-    std::vector<int> blk_cam, cnt;
-    for (int p = 0; p < P; ++p)
-        for (int a = pt_start[p]; a < pt_start[p + 1]; ++a)
-            for (int b = pt_start[p]; b < pt_start[p + 1]; ++b) {
-                const int ca = pb->obs_cam[pt_obs[a]], cb = pb->obs_cam[pt_obs[b]];
-                if (ca > cb) continue;
-                const int64_t key = (int64_t)ca * C + cb;
-                auto it = bid.find(key);
-                int id;
-                if (it == bid.end()) { id = (int)cnt.size(); bid.emplace(key, id); cnt.push_back(0); blk_cam.push_back(ca); blk_cam.push_back(cb); }
-                else id = it->second;
-                cnt[id]++;
-            }
-    const int NBLK = (int)cnt.size();
-    {   // number blocks in (cam(a), cam(b)) order: neighbouring blocks share points, and
-        // ba_pair_blocks maps contiguous block ranges to one XCD (L2 reuse of the R1 records)
-        std::vector<std::pair<int64_t, int>> keys;
-        keys.reserve(NBLK);
-        for (auto& kv : bid) keys.emplace_back(kv.first, kv.second);
-        std::sort(keys.begin(), keys.end());
-        std::vector<int> cnt2(NBLK), cam2(2 * (size_t)NBLK);
-        for (int nb = 0; nb < NBLK; ++nb) {
-            const int ob = keys[nb].second;
-            cnt2[nb] = cnt[ob];
-            cam2[2 * nb] = blk_cam[2 * ob];
-            cam2[2 * nb + 1] = blk_cam[2 * ob + 1];
-            bid[keys[nb].first] = nb;
-        }
-        cnt.swap(cnt2);
-        blk_cam.swap(cam2);
-    }
-    std::vector<int> blk_start(NBLK + 1, 0);
-    for (int b = 0; b < NBLK; ++b) blk_start[b + 1] = blk_start[b] + cnt[b];
-    std::vector<int2> trip(blk_start[NBLK]);
-    {
-        std::vector<int> fill(blk_start.begin(), blk_start.end() - 1);
-        for (int p = 0; p < P; ++p)
-            for (int a = pt_start[p]; a < pt_start[p + 1]; ++a)
-                for (int b = pt_start[p]; b < pt_start[p + 1]; ++b) {
-                    const int oa = pt_obs[a], ob = pt_obs[b];
-                    const int ca = pb->obs_cam[oa], cb = pb->obs_cam[ob];
-                    if (ca > cb) continue;
-                    trip[fill[bid[(int64_t)ca * C + cb]]++] = make_int2(oa, ob);
-                }
-    }
-    c->nblocks = NBLK;
-    // point groups for ba_point_blocks_lds: consecutive points, <= PB_MAXP points and
-    // <= PB_CAPO observations per group; a point with more observations goes to the
-    // point-list fallback (ba_point_blocks)
-    std::vector<int> pgrp, pbig;
-    const char* pbenv = std::getenv("SFMX_BA_POINT_KERNEL");   // "list": every point via ba_point_blocks (A/B tuning)
-    if (pbenv && std::strcmp(pbenv, "list") == 0)
-        for (int p = 0; p < P; ++p) pbig.push_back(p);
-    for (int p = pbig.empty() ? 0 : P; p < P;) {
-        const int cnt = pt_start[p + 1] - pt_start[p];
-        if (cnt > PB_CAPO) { pbig.push_back(p); ++p; continue; }
-        pgrp.push_back(p);   // group = [pgrp[2g], pgrp[2g+1])
-        int np = 0, no = 0;
-        while (p < P && np < PB_MAXP && pt_start[p + 1] - pt_start[p] <= PB_CAPO && no + (pt_start[p + 1] - pt_start[p]) <= PB_CAPO) {
-            no += pt_start[p + 1] - pt_start[p];
-            ++np; ++p;
-        }
-        pgrp.push_back(p);
-    }
-    c->ngrp = (int)pgrp.size() / 2;
-    c->nbig = (int)pbig.size();
-    c->nvz = c->ngrp + (c->nbig ? (int)nblk(c->nbig) : 0);
-    std::vector<int> op(pb->obs_point, pb->obs_point + O), oc(pb->obs_cam, pb->obs_cam + O);
-    std::vector<double> oxy(pb->obs_xy, pb->obs_xy + 2 * (size_t)O);
     hipStream_t st = c->st;
     int rc;
-    if ((rc = upload(c->obs_point, op, st)) || (rc = upload(c->obs_cam, oc, st)) || (rc = upload(c->obs_xy, oxy, st)) ||
-        (rc = upload(c->pt_start, pt_start, st)) || (rc = upload(c->pt_obs, pt_obs, st)) ||
-        (rc = upload(c->cam_start, cam_start, st)) || (rc = upload(c->cam_obs, cam_obs, st)) ||
-        (rc = upload(c->campos, campos, st)) ||
-        (rc = upload(c->blk_cam, blk_cam, st)) || (rc = upload(c->blk_start, blk_start, st)) ||
-        (rc = upload(c->trip, trip, st)) || (rc = upload(c->pgrp, pgrp, st)) || (rc = upload(c->pbig, pbig, st)))
+    if ((rc = upload(c->obs_point, rop, st)) || (rc = upload(c->obs_cam, roc, st)) || (rc = upload(c->obs_xy, rxy, st)) ||
+        (rc = upload(c->pt_start, pt_start, st)) || (rc = upload(c->grp, tp.grp, st)) || (rc = upload(c->chk, tp.chk, st)) ||
+        (rc = upload(c->gcam, tp.gcam, st)) || (rc = upload(c->obs_lc, tp.obs_lc, st)) ||
+        (rc = upload(c->tasks, tp.tasks, st)) || (rc = upload(c->ents, tp.ents, st)) ||
+        (rc = upload(c->cref_start, tp.cref_start, st)) || (rc = upload(c->cref, tp.cref, st)))
         return bail(rc);
     const size_t n = c->n, so = std::max(O, 1);
-    const int NI = std::max(2 * K, K * (K + 1) / 2 + K);
+    const size_t ncams = (size_t)C * ncp(K) + K * (K + 1) / 2 + K;
     struct { Buf* b; size_t bytes; } allocs[] = {
-        {&c->x, 8 * n}, {&c->cand, 8 * n}, {&c->scale, 8 * n}, {&c->colsq, 8 * n}, {&c->grad, 8 * n},
-        {&c->diag, 8 * n}, {&c->D, 8 * n}, {&c->sol, 8 * n}, {&c->step, 8 * n},
-        {&c->J, 8 * so * (20 + 2 * K)}, {&c->partA, 8 * (size_t)nblk(std::max<int64_t>(O, n))},
-        {&c->partB, 8 * (size_t)nblk(std::max<int64_t>(O, n))}, {&c->scal, 8 * 16},
-        {&c->ipart, 8 * (size_t)std::max(C, 1) * NI}, {&c->Einv, 72 * (size_t)std::max(P, 1)},
-        {&c->EinvG, 24 * (size_t)std::max(P, 1)}, {&c->R1, 8 * so * r1s(K)}, {&c->R2, 8 * so * r2s(K)},
-        {&c->vzpart, 8 * (size_t)std::max(c->nvz, 1) * K * K}, {&c->Linv, 8 * (size_t)2 * NB * NB},
-        {&c->Scc, 288 * (size_t)std::max(C, 1)}, {&c->Spi, 48 * (size_t)K * std::max(C, 1)}, {&c->Sii, 8 * (size_t)K * K},
-        {&c->rc, 48 * (size_t)std::max(C, 1)}, {&c->ri, 8 * (size_t)K}, {&c->Spp, 288 * (size_t)std::max(NBLK, 1)},
-        {&c->SR, 8 * ((size_t)c->npad * c->npad + c->npad)}, {&c->failf, 64}};
+        {&c->x, 8 * n}, {&c->cand, 8 * n}, {&c->scale, 8 * n}, {&c->colsq, 8 * n}, {&c->colsq2, 8 * n},
+        {&c->grad, 8 * n}, {&c->grad2, 8 * n}, {&c->sol, 8 * n},
+        {&c->J, 8 * so * jst(K)}, {&c->J2, 8 * so * jst(K)}, {&c->camsum, 8 * ncams}, {&c->camsum2, 8 * ncams},
+        {&c->plt, 72 * (size_t)std::max(P, 1)}, {&c->sg, 8 * (size_t)std::max<long long>(tp.sg_total, 1)},
+        {&c->rg, 8 * (size_t)std::max(tp.rg_total, 1)}, {&c->hbig, 8 * (size_t)std::max<long long>(tp.h_total, 1)},
+        {&c->gpart, 8 * (size_t)std::max(c->nslots, 1) * ncp(K)}, {&c->gpl, 8 * (size_t)std::max(c->ngroups, 1) * GP_N},
+        {&c->scal, 8 * SC_N}, {&c->Linv, 8 * (size_t)2 * NB * NB},
+        {&c->SR, 8 * ((size_t)c->npad * c->npad + c->npad)}, {&c->failf, 64},
+        {&c->partA, 8 * (size_t)nblk(std::max<int64_t>(O, n))}};
     for (auto& a : allocs) if ((rc = a.b->alloc(a.bytes))) return bail(rc);
+    HIPCHK(hipMemsetAsync(c->gpl.p, 0, c->gpl.bytes, st));
     // scale = 1 until (and unless) Jacobi scaling sets it
     {
         std::vector<double> ones(n, 1.0);
@@ -762,7 +763,7 @@ int sfmx_ba_jacobian(const sfmx_ba_problem* pb, int32_t device, double* r, doubl
     {
         DeviceGuard dg(c->device);
         double cost;
-        rc = eval<true>(c, c->x.as<double>(), &cost);
+        rc = eval_jacobian(c, c->x.as<double>(), &cost);
         if (!rc) {
             const int O = c->O, K = c->K, F = 20 + 2 * K;
             std::vector<double> h((size_t)F * O);
