@@ -70,9 +70,13 @@ struct Grp {
     long long h_off;         // H (dim x 3) in hbig (big groups)
     int rg_off, big;         // rhs block (dim) in rg; big-group flag
 };
-struct Chunk { int o0, o1, q0, q1; };   // observations [o0, o1), point slots [q0, q1) of the group
+// observations [o0, o1), point slots [q0, q1) of the group; the chunk's feature rows sorted by
+// local camera: camera lc owns rows lcrow[lc0 + lc] .. lcrow[lc0 + lc + 1) (a multiple of 4, zero-padded)
+struct Chunk { int o0, o1, q0, q1, lc0, nrows, pad0, pad1; };
 struct ATask { int type, a, b, l0, l1, pad0, pad1, pad2; };   // 0: pose (a <= b), 1: pose-intr a, 2: intr
-struct AEnt { int g, la, lb, pad; };
+// one contribution to an S block: normal group: b0 = sg offset of its (6la, 6lb) element (row
+// stride dim); big group: b0 / b1 = hbig offsets of the H rows 6la / 6lb (row stride 3)
+struct AEnt { long long b0, b1; int dim, big, rg, pad; };
 
 __device__ __forceinline__ int gdim(const Grp& G, int K) { return 6 * G.u + K; }
 
@@ -131,6 +135,21 @@ template <int K>
 __device__ __forceinline__ void load_jrec(const double* __restrict__ J, int o, const double* sp, const double* sc,
                                           const double* si, JRec<K>& R) {
     load_rec<K>(J + (size_t)o * jst(K), sp, sc, si, R);
+}
+
+// Copy n2 16-B pieces global -> LDS with every load issued before the first store (a plain
+// load / store loop waits for each load in turn).
+template <int PER>
+__device__ __forceinline__ void stage_copy(double2* __restrict__ dst, const double2* __restrict__ src, int n2) {
+    if (n2 <= 0) return;
+    double2 v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = src[min((int)threadIdx.x + 256 * i, n2 - 1)];   // clamped: always valid
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int e = threadIdx.x + 256 * i;
+        if (e < n2) dst[e] = v[i];
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -267,12 +286,8 @@ void ba_gschur(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const
     const int np = G.p1 - G.p0;
     for (int c = 0; c < G.nch; ++c) {
         const Chunk ch = chk[G.ch0 + c];
-        {   // the chunk's J records -> LDS (16-B coalesced loads)
-            const double2* src = reinterpret_cast<const double2*>(J + (size_t)ch.o0 * JS);
-            double2* dst = reinterpret_cast<double2*>(stg);
-            const int n2 = (ch.o1 - ch.o0) * (JS / 2);
-            for (int i = tid; i < n2; i += blockDim.x) dst[i] = src[i];
-        }
+        stage_copy<JS / 2>(reinterpret_cast<double2*>(stg), reinterpret_cast<const double2*>(J + (size_t)ch.o0 * JS),
+                           (ch.o1 - ch.o0) * (JS / 2));   // the chunk's J records -> LDS (coalesced)
         __syncthreads();
         const int a = tid, o = ch.o0 + a;
         const bool ov = o < ch.o1;
@@ -425,69 +440,68 @@ void ba_gschur(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const
 // ba_assemble: one 64-thread workgroup per block of S, summing the group contributions in group
 // order (normal groups: their dense block; big groups: -H_a H_b^T from the stored H); writes S and
 // its transpose, and the rhs rows (pose-intr task: camera rows; intr task: intrinsics rows and the
-// padding).  S is zeroed before; C, D^2 and g_f are added by ba_add_cam.
-__device__ __forceinline__ double gval(const Grp& G, const double* __restrict__ sg, const double* __restrict__ hbig,
-                                       int K, int r, int c) {
-    if (!G.big) return sg[G.sg_off + (size_t)r * gdim(G, K) + c];
-    const double* H = hbig + G.h_off;
-    return -(H[r * 3] * H[c * 3] + H[r * 3 + 1] * H[c * 3 + 1] + H[r * 3 + 2] * H[c * 3 + 2]);
+// padding).  S is zeroed before; C, D^2 and g_f are added by ba_add_cam.  Entries carry absolute
+// offsets (no dependent loads); the intrinsics block (every group) is a strided, fixed-order
+// wave reduction.
+__device__ __forceinline__ double aval(const AEnt& E, const double* __restrict__ sg, const double* __restrict__ hbig,
+                                       int r, int c) {
+    if (!E.big) return sg[E.b0 + (long long)r * E.dim + c];
+    const double* Ha = hbig + E.b0 + 3 * r;
+    const double* Hb = hbig + E.b1 + 3 * c;
+    return -(Ha[0] * Hb[0] + Ha[1] * Hb[1] + Ha[2] * Hb[2]);
+}
+__device__ __forceinline__ double wave_sum(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
 }
 __global__ __launch_bounds__(64)
-void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents, const Grp* __restrict__ grp,
-                 const double* __restrict__ sg, const double* __restrict__ hbig, const double* __restrict__ rg, int C,
-                 int K, int nf, int npad, double* __restrict__ S, double* __restrict__ rhs) {
+void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents, const double* __restrict__ sg,
+                 const double* __restrict__ hbig, const double* __restrict__ rg, int C, int K, int nf, int npad,
+                 double* __restrict__ S, double* __restrict__ rhs) {
     const ATask T = tasks[blockIdx.x];
     const int t = threadIdx.x;
     if (T.type == 0) {
         if (t >= 36) return;
         const int u = t / 6, w = t % 6;
         double v = 0.0;
-        for (int e = T.l0; e < T.l1; ++e) {
-            const AEnt E = ents[e];
-            v += gval(grp[E.g], sg, hbig, K, 6 * E.la + u, 6 * E.lb + w);
-        }
+#pragma unroll 4
+        for (int e = T.l0; e < T.l1; ++e) v += aval(ents[e], sg, hbig, u, w);
         S[(size_t)(6 * T.a + u) * npad + 6 * T.b + w] = v;
         if (T.a != T.b) S[(size_t)(6 * T.b + w) * npad + 6 * T.a + u] = v;
-    } else if (T.type == 1) {
+    } else if (T.type == 1) {   // entries: b0 / b1 at the camera rows / the intrinsics rows of the group
         if (t < 6 * K) {
             const int u = t / K, i = t % K;
             double v = 0.0;
-            for (int e = T.l0; e < T.l1; ++e) {
-                const AEnt E = ents[e];
-                const Grp G = grp[E.g];
-                v += gval(G, sg, hbig, K, 6 * E.la + u, 6 * G.u + i);
-            }
+#pragma unroll 4
+            for (int e = T.l0; e < T.l1; ++e) v += aval(ents[e], sg, hbig, u, i);
             S[(size_t)(6 * T.a + u) * npad + 6 * C + i] = v;
             S[(size_t)(6 * C + i) * npad + 6 * T.a + u] = v;
         } else if (t < 6 * K + 6) {
             const int d = t - 6 * K;
             double v = 0.0;
-            for (int e = T.l0; e < T.l1; ++e) {
-                const AEnt E = ents[e];
-                v += rg[grp[E.g].rg_off + 6 * E.la + d];
-            }
+#pragma unroll 4
+            for (int e = T.l0; e < T.l1; ++e) v += rg[ents[e].rg + d];
             rhs[6 * T.a + d] = v;
         }
-    } else {
-        for (int x = t; x < K * K + K; x += 64) {
-            double v = 0.0;
-            if (x < K * K) {
-                const int i = x / K, j = x % K;
-                for (int e = T.l0; e < T.l1; ++e) {
-                    const Grp G = grp[ents[e].g];
-                    v += gval(G, sg, hbig, K, 6 * G.u + i, 6 * G.u + j);
-                }
-                S[(size_t)(6 * C + i) * npad + 6 * C + j] = v;
-            } else {
-                const int i = x - K * K;
-                for (int e = T.l0; e < T.l1; ++e) {
-                    const Grp G = grp[ents[e].g];
-                    v += rg[G.rg_off + 6 * G.u + i];
-                }
-                rhs[6 * C + i] = v;
-            }
+    } else {                    // one intrinsics output x = T.b over every group; entries at the intrinsics rows
+        const int x = T.b;
+        double v0 = 0.0, v1 = 0.0;
+        int e = T.l0 + t;
+        if (x < K * K) {
+            const int i = x / K, j = x % K;
+            for (; e + 64 < T.l1; e += 128) { v0 += aval(ents[e], sg, hbig, i, j); v1 += aval(ents[e + 64], sg, hbig, i, j); }
+            if (e < T.l1) v0 += aval(ents[e], sg, hbig, i, j);
+        } else {
+            for (; e + 64 < T.l1; e += 128) { v0 += rg[ents[e].rg + (x - K * K)]; v1 += rg[ents[e + 64].rg + (x - K * K)]; }
+            if (e < T.l1) v0 += rg[ents[e].rg + (x - K * K)];
         }
-        for (int i = nf + t; i < npad; i += 64) { S[(size_t)i * npad + i] = 1.0; rhs[i] = 0.0; }
+        const double v = wave_sum(v0 + v1);
+        if (t == 0) {
+            if (x < K * K) S[(size_t)(6 * C + x / K) * npad + 6 * C + x % K] = v;
+            else rhs[6 * C + x - K * K] = v;
+        }
+        if (x == 0)
+            for (int i = nf + t; i < npad; i += 64) { S[(size_t)i * npad + i] = 1.0; rhs[i] = 0.0; }
     }
 }
 
@@ -501,12 +515,12 @@ void ba_add_cam(int P, int C, int npad, const double* __restrict__ camsum, const
                 double* __restrict__ rhs) {
     constexpr int NCP = ncp(K);
     const size_t ne = 3 * (size_t)P, nfc = 6 * (size_t)C;
-    const int t = threadIdx.x;
     const double* si = scale + ne + nfc;
     if ((int)blockIdx.x < C) {
         const int c = blockIdx.x;
         const double* cs = camsum + (size_t)c * NCP;
         const double* sc = scale + ne + 6 * (size_t)c;
+        for (int t = threadIdx.x; t < 42 + 6 * K; t += 64)
         if (t < 36) {
             const int u = t / 6, w = t % 6, a = u < w ? u : w, b = u < w ? w : u;
             int e = 0;
@@ -526,7 +540,7 @@ void ba_add_cam(int P, int C, int npad, const double* __restrict__ camsum, const
         }
     } else {
         const double* ii = camsum + (size_t)C * NCP;
-        for (int x = t; x < K * K + K; x += 64) {
+        for (int x = threadIdx.x; x < K * K + K; x += 64) {
             if (x < K * K) {
                 const int i = x / K, j = x % K, a = i < j ? i : j, b = i < j ? j : i;
                 int e = 0;
@@ -543,76 +557,68 @@ void ba_add_cam(int P, int C, int npad, const double* __restrict__ camsum, const
     }
 }
 
-// sum over the chunk's observations of camera lc (in order) of one field of the per-(group,
-// camera) partials (see ncp); records in LDS (jst(K) doubles each), olc = local camera per obs.
+// Feature rows of the per-(group, camera) partials: each observation gives two rows (residual
+// rows j = 0, 1) of NF(K) features [Jc (6) | Ji (K) | r], unscaled.  Their Gram matrix per camera
+// holds every partial field (see ncp): D[u][w] = Jc^T Jc, D[u][6 + i] = Jc^T Ji, D[u][6 + K] =
+// Jc^T r, D[6 + i][6 + l] = Ji^T Ji, D[6 + i][6 + K] = Ji^T r.
+__host__ __device__ constexpr int nfeat(int K) { return 7 + K; }
 template <int K>
-__device__ __forceinline__ double cam_field_sum(const double* __restrict__ jl, const short* __restrict__ olc, int no,
-                                                int lc, int f) {
-    constexpr int JS = jst(K);
-    // decode the field into two operand offsets within a record: v = x0[i] * y0[j] + x1[i] * y1[j]
-    int oa, ob;   // offsets of row 0 operands; row 1 operands are at oa + da, ob + db
-    int da, db;
-    if (f < 21) {
-        int u = 0, e = f;
-        while (e >= 6 - u) { e -= 6 - u; ++u; }
-        oa = 8 + u; ob = 8 + u + e; da = 6; db = 6;
-    } else if (f < cp_gc(K)) {
-        const int y = f - 21, u = y / K, ii = y % K;
-        oa = 8 + u; ob = 20 + ii; da = 6; db = K;
-    } else if (f < cp_ii(K)) {
-        oa = 8 + (f - cp_gc(K)); ob = 0; da = 6; db = 1;
-    } else if (f < cp_gi(K)) {
-        int ii = 0, e = f - cp_ii(K);
-        while (e >= K - ii) { e -= K - ii; ++ii; }
-        oa = 20 + ii; ob = 20 + ii + e; da = K; db = K;
-    } else {
-        oa = 20 + (f - cp_gi(K)); ob = 0; da = K; db = 1;
+__device__ __forceinline__ int field_of(int r, int c) {   // Gram entry (r <= c) -> partial field, -1: none
+    if (r < 6) {
+        if (c < 6) return 21 - (6 - r) * (7 - r) / 2 + (c - r);
+        if (c < 6 + K) return 21 + r * K + (c - 6);
+        return cp_gc(K) + r;
     }
-    double s = 0.0;
-    for (int b = 0; b < no; ++b) {
-        if (olc[b] != lc) continue;
-        const double* r = jl + b * JS;
-        s += r[oa] * r[ob] + r[oa + da] * r[ob + db];
+    if (r < 6 + K) {
+        const int i = r - 6;
+        if (c < 6 + K) return cp_ii(K) + (K * (K + 1) / 2 - (K - i) * (K - i + 1) / 2) + (c - 6 - i);
+        return cp_gi(K) + i;
     }
-    return s;
+    return -1;   // r^T r (not a partial field)
 }
 
-// ---------------------------------------------------------------------------------------------
 // ba_glin: residuals + Jacobian at xp (x or the candidate) for the group's observations.
-// Writes the J records, per point colsq / grad (unscaled), per (group, camera) partials (gpart),
-// and the group's cost, sum xp^2 (its points) and max |grad| partials.
-// Dynamic LDS: jl[GCH][jst(K)] | olc[GCH] (short).
+// Writes the J records, per point colsq / grad (unscaled), per (group, camera) partials (gpart:
+// the per-camera Gram matrices of the feature rows on the fp64 matrix cores, rows of one camera
+// contiguous and zero-padded by the host-built layout), and the group's cost, sum xp^2 (its
+// points) and max |grad| partials.  Big groups: feature rows in observation order and a scalar
+// per-(camera, field) loop.
+// Dynamic LDS: G[max rows][NF] | jer[GCH][8] (je | r) | olc[GCH] (short).
+constexpr int GROWS = 2 * GCH + 3 * UMAX;   // feature rows of a chunk incl. per-camera padding
 template <int K>
 __global__ __launch_bounds__(256)
-void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const short* __restrict__ obs_lc,
-             const int* __restrict__ obs_point, const int* __restrict__ obs_cam, const double* __restrict__ obs_xy,
-             const int* __restrict__ pt_start, double cx, double cy, int P, int C, const double* __restrict__ xp,
-             double* __restrict__ J, double* __restrict__ colsq, double* __restrict__ grad, double* __restrict__ gpart,
+void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const int* __restrict__ lcrow,
+             const short* __restrict__ obs_lc, const short* __restrict__ obs_row, const int* __restrict__ obs_point,
+             const int* __restrict__ obs_cam, const double* __restrict__ obs_xy, const int* __restrict__ pt_start,
+             double cx, double cy, int P, int C, const double* __restrict__ xp, double* __restrict__ J,
+             double* __restrict__ colsq, double* __restrict__ grad, double* __restrict__ gpart,
              double* __restrict__ gpl) {
     extern __shared__ __attribute__((aligned(16))) double gl[];
-    constexpr int JS = jst(K), NCP = ncp(K), N = 9 + K;
-    constexpr int NOWN = (UMAX * NCP + 255) / 256;   // (camera, field) pairs per thread, normal groups
+    constexpr int JS = jst(K), NCP = ncp(K), N = 9 + K, NF = nfeat(K);
     __shared__ double sh[8];
-    double* jl = gl;
-    short* olc = reinterpret_cast<short*>(jl + GCH * JS);
-    const Grp G = grp[blockIdx.x];
-    const int tid = threadIdx.x;
+    double* G = gl;                                    // [GROWS][NF]
+    double* jer = G + GROWS * NF;                      // [GCH][8]
+    short* olc = reinterpret_cast<short*>(jer + GCH * 8);
+    const Grp Gp = grp[blockIdx.x];
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, m16 = l & 15, kq = l >> 4;
     const double* pts = xp;
     const double* poses = xp + 3 * (size_t)P;
     const double* intr = poses + 6 * (size_t)C;
     double cost = 0.0, xn = 0.0, gmax = 0.0;
-    double own[NOWN];
+    f64x4 acc[UMAX / 4];
 #pragma unroll
-    for (int i = 0; i < NOWN; ++i) own[i] = 0.0;
-    const int npart = G.u * NCP;
+    for (int i = 0; i < UMAX / 4; ++i) acc[i] = f64x4{0.0, 0.0, 0.0, 0.0};
+    const int npart = Gp.u * NCP;
     double pcs[3] = {0, 0, 0}, pgr[3] = {0, 0, 0};   // big groups: the point's sums (thread 0)
-    if (G.big)
-        for (int i = tid; i < npart; i += blockDim.x) gpart[(size_t)G.cam_off * NCP + i] = 0.0;
-    const int nchunks = G.big ? (G.o1 - G.o0 + GCH - 1) / GCH : G.nch;
+    if (Gp.big)
+        for (int i = tid; i < npart; i += blockDim.x) gpart[(size_t)Gp.cam_off * NCP + i] = 0.0;
+    const int nchunks = Gp.big ? (Gp.o1 - Gp.o0 + GCH - 1) / GCH : Gp.nch;
     for (int c = 0; c < nchunks; ++c) {
         Chunk ch;
-        if (G.big) { ch.o0 = G.o0 + c * GCH; ch.o1 = min(G.o1, ch.o0 + GCH); ch.q0 = 0; ch.q1 = 0; }
-        else ch = chk[G.ch0 + c];
+        if (Gp.big) { ch.o0 = Gp.o0 + c * GCH; ch.o1 = min(Gp.o1, ch.o0 + GCH); ch.q0 = 0; ch.q1 = 0; ch.lc0 = 0; ch.nrows = 2 * (ch.o1 - ch.o0); }
+        else ch = chk[Gp.ch0 + c];
+        for (int e = tid; e < ch.nrows * NF; e += blockDim.x) G[e] = 0.0;   // padding rows stay zero
+        __syncthreads();
         const int a = tid, o = ch.o0 + a;
         if (o < ch.o1) {
             const int p = obs_point[o], cm = obs_cam[o];
@@ -636,31 +642,41 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const s
 #pragma unroll
                 for (int i = 0; i < K; ++i) rec[20 + K * j + i] = res[j].v[9 + i];
             }
+            double2* dst = reinterpret_cast<double2*>(J + (size_t)o * JS);
 #pragma unroll
-            for (int i = 0; i < JS; ++i) jl[a * JS + i] = rec[i];
+            for (int i = 0; i < JS / 2; ++i) dst[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) jer[a * 8 + i] = rec[2 + i];
+            jer[a * 8 + 6] = rec[0];
+            jer[a * 8 + 7] = rec[1];
+            const int row = Gp.big ? 2 * a : obs_row[o];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                double* gr = G + (row + j) * NF;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) gr[i] = rec[8 + 6 * j + i];
+#pragma unroll
+                for (int i = 0; i < K; ++i) gr[6 + i] = rec[20 + K * j + i];
+                gr[6 + K] = rec[j];
+            }
             olc[a] = obs_lc[o];
             cost += res[0].a * res[0].a + res[1].a * res[1].a;
         }
         __syncthreads();
         const int no = ch.o1 - ch.o0;
-        {   // J records of the chunk -> HBM (16-B coalesced stores)
-            const double2* src = reinterpret_cast<const double2*>(jl);
-            double2* dst = reinterpret_cast<double2*>(J + (size_t)ch.o0 * JS);
-            for (int i = tid; i < no * (JS / 2); i += blockDim.x) dst[i] = src[i];
-        }
         // per point: column norms and gradient of its 3 columns (whole points in a normal chunk)
-        if (!G.big) {
+        if (!Gp.big) {
             if (tid >= ch.q0 && tid < ch.q1) {
-                const int p = G.p0 + tid;
+                const int p = Gp.p0 + tid;
                 const int a0 = pt_start[p] - ch.o0, a1 = pt_start[p + 1] - ch.o0;
                 double cs[3] = {0, 0, 0}, gr[3] = {0, 0, 0};
                 for (int b = a0; b < a1; ++b) {
-                    const double* r = jl + b * JS;
+                    const double* r = jer + b * 8;
 #pragma unroll
                     for (int i = 0; i < 3; ++i) {
-                        const double j0 = r[2 + i], j1 = r[5 + i];
+                        const double j0 = r[i], j1 = r[3 + i];
                         cs[i] += j0 * j0 + j1 * j1;
-                        gr[i] += j0 * r[0] + j1 * r[1];
+                        gr[i] += j0 * r[6] + j1 * r[7];
                     }
                 }
 #pragma unroll
@@ -671,38 +687,61 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const s
                     xn += pts[3 * (size_t)p + i] * pts[3 * (size_t)p + i];
                 }
             }
-        } else if (tid == 0) {
-            for (int b = 0; b < no; ++b) {
-                const double* r = jl + b * JS;
+            // per camera: Gram of its feature rows, accumulated over the group's chunks
 #pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    const double j0 = r[2 + i], j1 = r[5 + i];
-                    pcs[i] += j0 * j0 + j1 * j1;
-                    pgr[i] += j0 * r[0] + j1 * r[1];
+            for (int i = 0; i < UMAX / 4; ++i) {
+                const int lc = w + 4 * i;
+                if (lc >= Gp.u) continue;
+                const int r0 = lcrow[ch.lc0 + lc], r1 = lcrow[ch.lc0 + lc + 1];
+                for (int row = r0; row < r1; row += 4) {
+                    const double v = m16 < NF ? G[(row + kq) * NF + m16] : 0.0;
+                    acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc[i], 0, 0, 0);
                 }
             }
-        }
-        // per (camera, field): sum over this chunk's observations of that camera, in order
-        if (!G.big) {
-#pragma unroll
-            for (int i = 0; i < NOWN; ++i) {
-                const int x = tid + 256 * i;
-                if (x < npart) own[i] += cam_field_sum<K>(jl, olc, no, x / NCP, x % NCP);
-            }
         } else {
-            for (int x = tid; x < npart; x += blockDim.x)
-                gpart[(size_t)G.cam_off * NCP + x] += cam_field_sum<K>(jl, olc, no, x / NCP, x % NCP);
+            if (tid == 0)
+                for (int b = 0; b < no; ++b) {
+                    const double* r = jer + b * 8;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        const double j0 = r[i], j1 = r[3 + i];
+                        pcs[i] += j0 * j0 + j1 * j1;
+                        pgr[i] += j0 * r[6] + j1 * r[7];
+                    }
+                }
+            for (int x = tid; x < npart; x += blockDim.x) {   // per (camera, field), in observation order
+                const int lc = x / NCP, f = x % NCP;
+                int fr = -1, fc = -1;
+                for (int rr = 0; rr < NF && fr < 0; ++rr)
+                    for (int cc = rr; cc < NF; ++cc)
+                        if (field_of<K>(rr, cc) == f) { fr = rr; fc = cc; break; }
+                double sum = 0.0;
+                for (int b = 0; b < no; ++b) {
+                    if (olc[b] != lc) continue;
+                    const double* g0 = G + (2 * b) * NF;
+                    sum += g0[fr] * g0[fc] + g0[NF + fr] * g0[NF + fc];
+                }
+                gpart[(size_t)Gp.cam_off * NCP + x] += sum;
+            }
         }
         __syncthreads();
     }
-    if (!G.big) {
+    if (!Gp.big) {
 #pragma unroll
-        for (int i = 0; i < NOWN; ++i) {
-            const int x = tid + 256 * i;
-            if (x < npart) gpart[(size_t)G.cam_off * NCP + x] = own[i];
+        for (int i = 0; i < UMAX / 4; ++i) {
+            const int lc = w + 4 * i;
+            if (lc >= Gp.u) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rr = trow(r), cc = tcol();
+                if (rr <= cc && cc < NF) {
+                    const int f = field_of<K>(rr, cc);
+                    if (f >= 0) gpart[(size_t)(Gp.cam_off + lc) * NCP + f] = acc[i][r];
+                }
+            }
         }
     } else if (tid == 0) {
-        const int p = G.p0;
+        const int p = Gp.p0;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             colsq[3 * (size_t)p + i] = pcs[i];
@@ -736,17 +775,32 @@ void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int*
     constexpr int NCP = ncp(K), NI = K * (K + 1) / 2 + K;
     const int t = threadIdx.x;
     if ((int)blockIdx.x < C) {
-        const int c = blockIdx.x;
+        const int c = blockIdx.x, e0 = cref_start[c], e1 = cref_start[c + 1];
         for (int f = t; f < cp_ii(K); f += blockDim.x) {
-            double s = 0.0;
-            for (int e = cref_start[c]; e < cref_start[c + 1]; ++e) s += gpart[(size_t)cref[e] * NCP + f];
-            camsum[(size_t)c * NCP + f] = s;
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;   // 4 interleaved chains, combined in fixed order
+            int e = e0;
+            for (; e + 3 < e1; e += 4) {
+                const int c0 = cref[e], c1 = cref[e + 1], c2 = cref[e + 2], c3 = cref[e + 3];
+                s0 += gpart[(size_t)c0 * NCP + f]; s1 += gpart[(size_t)c1 * NCP + f];
+                s2 += gpart[(size_t)c2 * NCP + f]; s3 += gpart[(size_t)c3 * NCP + f];
+            }
+            for (; e < e1; ++e) s0 += gpart[(size_t)cref[e] * NCP + f];
+            camsum[(size_t)c * NCP + f] = (s0 + s1) + (s2 + s3);
         }
-    } else {
-        for (int f = t; f < NI; f += blockDim.x) {
-            double s = 0.0;
-            for (int e = 0; e < nslots; ++e) s += gpart[(size_t)e * NCP + cp_ii(K) + f];
-            camsum[(size_t)C * NCP + f] = s;
+    } else {   // every slot: strided per thread (4 chains), then a fixed-order block reduction
+        __shared__ double sh[8];
+        for (int f = 0; f < NI; ++f) {
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+            int e = t;
+            for (; e + 3 * (int)blockDim.x < nslots; e += 4 * blockDim.x) {
+                s0 += gpart[(size_t)e * NCP + cp_ii(K) + f];
+                s1 += gpart[(size_t)(e + blockDim.x) * NCP + cp_ii(K) + f];
+                s2 += gpart[(size_t)(e + 2 * blockDim.x) * NCP + cp_ii(K) + f];
+                s3 += gpart[(size_t)(e + 3 * blockDim.x) * NCP + cp_ii(K) + f];
+            }
+            for (; e < nslots; e += blockDim.x) s0 += gpart[(size_t)e * NCP + cp_ii(K) + f];
+            const double tot = block_sum((s0 + s1) + (s2 + s3), sh);
+            if (t == 0) camsum[(size_t)C * NCP + f] = tot;
         }
     }
 }
@@ -853,11 +907,8 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
             Chunk ch;
             if (G.big) { ch.o0 = G.o0 + c * GCH; ch.o1 = min(G.o1, ch.o0 + GCH); ch.q0 = 0; ch.q1 = 1; }
             else ch = chk[G.ch0 + c];
-            {
-                const double2* src = reinterpret_cast<const double2*>(J + (size_t)ch.o0 * JS);
-                double2* dst = reinterpret_cast<double2*>(stg);
-                for (int i = tid; i < (ch.o1 - ch.o0) * (JS / 2); i += blockDim.x) dst[i] = src[i];
-            }
+            stage_copy<JS / 2>(reinterpret_cast<double2*>(stg), reinterpret_cast<const double2*>(J + (size_t)ch.o0 * JS),
+                               (ch.o1 - ch.o0) * (JS / 2));
             __syncthreads();
             const int a = tid, o = ch.o0 + a;
             const bool ov = o < ch.o1;

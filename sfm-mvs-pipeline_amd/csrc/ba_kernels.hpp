@@ -1092,11 +1092,14 @@ void chol_first(double* __restrict__ S, int npad, double* __restrict__ W, double
 // The destination tile is prefetched into registers before the GEMMs.
 __global__ __launch_bounds__(256)
 void chol_step(double* __restrict__ S, int npad, int k, double* __restrict__ W, double* __restrict__ rhs,
-               int* __restrict__ fail) {
+               int* __restrict__ fail, const int2* __restrict__ tl) {
     __shared__ CholLds sm;
     const int tid = threadIdx.x, w = tid >> 6;
     int a = k + 1, b = k + 1;
-    if (blockIdx.x > 0) {   // tile rows a >= k + 2 hold a - k tiles (b = k+1 .. a)
+    if (tl) {               // tile-sparse: this step's structurally nonzero updates, tl[0] = (k+1, k+1)
+        const int2 ab = tl[blockIdx.x];
+        a = ab.x; b = ab.y;
+    } else if (blockIdx.x > 0) {   // dense: tile rows a >= k + 2 hold a - k tiles (b = k+1 .. a)
         int rem = blockIdx.x - 1;
         for (a = k + 2; rem >= a - k; ++a) rem -= a - k;
         b = k + 1 + rem;
@@ -1183,6 +1186,36 @@ void chol_back(const double* __restrict__ S, int npad, int nf, int k, double* __
     t += __shfl_xor(t, 1);
     t += __shfl_xor(t, 2);
     if (qq == 0) rhs[i0 + r] -= t;
+}
+
+// Tile-sparse back substitution L~^T x = w in one workgroup: panels descending; for panel k only
+// the structurally nonzero upper tiles (i, k), i < k (list ut[ut_start[k] .. ut_start[k+1])) update
+// rhs_i -= U(i, k) x_k.  rhs lives in LDS (npad <= 16384).
+__global__ __launch_bounds__(256)
+void chol_back_sparse(const double* __restrict__ S, int npad, int nf, int T, const double* __restrict__ rhs_in,
+                      const int* __restrict__ ut_start, const int* __restrict__ ut, double* __restrict__ xout) {
+    extern __shared__ double r[];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < npad; i += 256) r[i] = rhs_in[i];
+    __syncthreads();
+    for (int k = T - 1; k >= 0; --k) {
+        const int k0 = k * NB;
+        for (int i = tid; i < NB; i += 256)
+            if (k0 + i < nf) xout[k0 + i] = r[k0 + i];
+        const int e0 = ut_start[k], e1 = ut_start[k + 1];
+        // 4 threads per row, 64 rows per pass over the listed tiles' rows
+        for (int e = e0; e < e1; ++e) {
+            const int i0 = ut[e] * NB, rr = tid >> 2, qq = tid & 3;
+            const double* U = S + (size_t)(i0 + rr) * npad + k0;
+            double t = 0.0;
+#pragma unroll
+            for (int m = 0; m < NB / 4; ++m) t = fma(U[4 * m + qq], r[k0 + 4 * m + qq], t);
+            t += __shfl_xor(t, 1);
+            t += __shfl_xor(t, 2);
+            if (qq == 0) r[i0 + rr] -= t;
+        }
+        __syncthreads();
+    }
 }
 
 // x_e = EinvG - sum_o U_o (F_o x_f), F_o = [Jc_s | Ji_s]   (R1 records)

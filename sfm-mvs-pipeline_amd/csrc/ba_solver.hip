@@ -78,7 +78,10 @@ struct sfmx_ba_ctx {
     // topology: groups, chunks, group cameras, local camera per observation, assembly tasks
     int ngroups = 0, ntasks = 0, nslots = 0, stage_n = 0;
     size_t lds_schur = 0, lds_lin = 0, lds_upd = 0;
-    Buf obs_point, obs_cam, obs_xy, pt_start, grp, chk, gcam, obs_lc, tasks, ents, cref_start, cref;
+    Buf obs_point, obs_cam, obs_xy, pt_start, grp, chk, gcam, obs_lc, obs_row, lcrow, tasks, ents, cref_start, cref,
+        tl, ut_start, ut;
+    std::vector<int> tl_start;   // host copy: per panel k, the launch's task range
+    bool sparse = true;          // tile-sparse factorization (SFMX_BA_DENSE=1: dense, for A/B)
     // state (the *2 buffers hold the candidate's linearization until the step is accepted)
     Buf x, cand, scale, colsq, colsq2, grad, grad2, J, J2, camsum, camsum2, plt, sg, rg, hbig, gpart, gpl, scal,
         SR, Linv, sol, failf, partA;
@@ -89,7 +92,7 @@ struct sfmx_ba_ctx {
     double phase_ms[4] = {0, 0, 0, 0};
     hipEvent_t ev[6] = {};
     ~sfmx_ba_ctx() {
-        Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &gcam, &obs_lc, &tasks, &ents, &cref_start,
+        Buf* all[] = {&tl, &ut_start, &ut, &obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &gcam, &obs_lc, &obs_row, &lcrow, &tasks, &ents, &cref_start,
                       &cref, &x, &cand, &scale, &colsq, &colsq2, &grad, &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg,
                       &rg, &hbig, &gpart, &gpl, &scal, &SR, &Linv, &sol, &failf, &partA};
         int prev = 0;
@@ -148,7 +151,8 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double
            bool cand_mode, double* out) {
     if (c->ngroups > 0)
         hipLaunchKernelGGL(ba_glin<K>, dim3(c->ngroups), dim3(256), c->lds_lin, c->st, c->grp.as<Grp>(),
-                           c->chk.as<Chunk>(), c->obs_lc.as<short>(), c->obs_point.as<int>(), c->obs_cam.as<int>(),
+                           c->chk.as<Chunk>(), c->lcrow.as<int>(), c->obs_lc.as<short>(), c->obs_row.as<short>(),
+                           c->obs_point.as<int>(), c->obs_cam.as<int>(),
                            c->obs_xy.as<double>(), c->pt_start.as<int>(), c->cx, c->cy, c->P, c->C, xp, Jo, colsq_o,
                            grad_o, c->gpart.as<double>(), c->gpl.as<double>());
     hipLaunchKernelGGL(ba_camred<K>, dim3(c->C + 1), dim3(128), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
@@ -185,8 +189,7 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
                            c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl);
     HIPCHK(hipMemsetAsync(S, 0, sizeof(double) * ((size_t)npad * npad + npad), c->st));
     hipLaunchKernelGGL(ba_assemble, dim3(c->ntasks), dim3(64), 0, c->st, c->tasks.as<ATask>(), c->ents.as<AEnt>(),
-                       c->grp.as<Grp>(), c->sg.as<double>(), c->hbig.as<double>(), c->rg.as<double>(), C, K, c->nf,
-                       npad, S, rhs);
+                       c->sg.as<double>(), c->hbig.as<double>(), c->rg.as<double>(), C, K, c->nf, npad, S, rhs);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->st));
     // point-sharded ranks: the group part of the reduced camera system and its rhs are sums over ranks
@@ -197,11 +200,21 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     double* W = c->Linv.as<double>();
     double* sol = c->sol.as<double>();
     hipLaunchKernelGGL(chol_first, dim3(1), dim3(256), 0, c->st, S, npad, W, rhs, fl);
-    for (int k = 0; k + 1 < T; ++k) {
-        const int m = T - k - 1;
-        hipLaunchKernelGGL(chol_step, dim3(m * (m + 1) / 2), dim3(256), 0, c->st, S, npad, k, W, rhs, fl);
+    if (c->sparse) {
+        for (int k = 0; k + 1 < T; ++k)
+            hipLaunchKernelGGL(chol_step, dim3(c->tl_start[k + 1] - c->tl_start[k]), dim3(256), 0, c->st, S, npad, k, W,
+                               rhs, fl, c->tl.as<int2>() + c->tl_start[k]);
+        hipLaunchKernelGGL(chol_back_sparse, dim3(1), dim3(256), sizeof(double) * npad, c->st, S, npad, c->nf, T, rhs,
+                           c->ut_start.as<int>(), c->ut.as<int>(), sol + c->ne);
+    } else {
+        for (int k = 0; k + 1 < T; ++k) {
+            const int m = T - k - 1;
+            hipLaunchKernelGGL(chol_step, dim3(m * (m + 1) / 2), dim3(256), 0, c->st, S, npad, k, W, rhs, fl,
+                               (const int2*)nullptr);
+        }
+        for (int k = T - 1; k >= 0; --k)
+            hipLaunchKernelGGL(chol_back, dim3(std::max(k, 1)), dim3(256), 0, c->st, S, npad, c->nf, k, rhs, sol + c->ne);
     }
-    hipLaunchKernelGGL(chol_back_all, dim3(1), dim3(256), 0, c->st, S, npad, c->nf, T, rhs, sol + c->ne);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[2], c->st));
     if (c->ngroups > 0)
@@ -395,16 +408,71 @@ void locality_order(const sfmx_ba_problem* pb, std::vector<int>& pperm, std::vec
 struct Topology {
     std::vector<Grp> grp;
     std::vector<Chunk> chk;
-    std::vector<int> gcam, cref_start, cref;
-    std::vector<short> obs_lc;
+    std::vector<int> gcam, cref_start, cref, lcrow;
+    std::vector<short> obs_lc, obs_row;
     std::vector<ATask> tasks;
     std::vector<AEnt> ents;
     long long sg_total = 0, h_total = 0;
     int rg_total = 0, dp_max = 16;
+    // tile-sparse factorization: per panel k the nonzero trailing updates (tl_start / tl, the
+    // (k+1, k+1) tile first) and the nonzero upper tiles for the back solve (ut_start / ut)
+    std::vector<int> tl_start, ut_start, ut;
+    std::vector<int2> tl;
+    int tiles_nz = 0;
 };
+
+// Tile pattern of S (lower) from the assembly blocks, then the symbolic fill of the block
+// factorization in natural order: a tile that starts and stays exactly zero is skipped, which
+// changes no computed value (updates from zero tiles are exact zeros).
+void tile_pattern(int C, int K, int nf, int T, const std::vector<ATask>& tasks, Topology& tp) {
+    std::vector<char> nz((size_t)T * T, 0);
+    auto mark = [&](int r0, int r1, int c0, int c1) {   // rows [r0, r1) x cols [c0, c1)
+        for (int I = r0 / NB; I <= (r1 - 1) / NB; ++I)
+            for (int Jj = c0 / NB; Jj <= (c1 - 1) / NB; ++Jj) {
+                const int a = std::max(I, Jj), b = std::min(I, Jj);
+                nz[(size_t)a * T + b] = 1;
+            }
+    };
+    for (int I = 0; I < T; ++I) nz[(size_t)I * T + I] = 1;
+    for (const ATask& t : tasks) {
+        if (t.type == 0) mark(6 * t.a, 6 * t.a + 6, 6 * t.b, 6 * t.b + 6);
+        else if (t.type == 1) mark(6 * t.a, 6 * t.a + 6, 6 * C, 6 * C + K);
+    }
+    mark(6 * C, nf, 6 * C, nf);
+    for (int c = 0; c < C; ++c) mark(6 * c, 6 * c + 6, 6 * C, 6 * C + K);   // C (camera-intrinsics coupling)
+    for (int k = 0; k < T; ++k)
+        for (int a = k + 1; a < T; ++a)
+            if (nz[(size_t)a * T + k])
+                for (int b = k + 1; b <= a; ++b)
+                    if (nz[(size_t)b * T + k]) nz[(size_t)a * T + b] = 1;
+    tp.tl_start.assign(T, 0);
+    tp.tl.clear();
+    for (int k = 0; k + 1 < T; ++k) {
+        tp.tl_start[k] = (int)tp.tl.size();
+        tp.tl.push_back(make_int2(k + 1, k + 1));
+        for (int a = k + 1; a < T; ++a)
+            for (int b = k + 1; b <= a; ++b) {
+                if (a == k + 1 && b == k + 1) continue;
+                if (nz[(size_t)a * T + k] && nz[(size_t)b * T + k]) tp.tl.push_back(make_int2(a, b));
+            }
+    }
+    tp.tl_start[T - 1] = (int)tp.tl.size();
+    tp.tl_start.push_back((int)tp.tl.size());
+    tp.ut_start.assign(T + 1, 0);
+    tp.ut.clear();
+    for (int k = 0; k < T; ++k) {
+        tp.ut_start[k] = (int)tp.ut.size();
+        for (int i = 0; i < k; ++i)
+            if (nz[(size_t)k * T + i]) tp.ut.push_back(i);
+    }
+    tp.ut_start[T] = (int)tp.ut.size();
+    tp.tiles_nz = 0;
+    for (char v : nz) tp.tiles_nz += v;
+}
 
 void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start, const int* obs_cam, Topology& tp) {
     tp.obs_lc.assign(O, 0);
+    tp.obs_row.assign(O, 0);
     std::vector<int> cur;   // sorted union of the open group's cameras
     int g_p0 = 0, g_obs = 0;
     auto add_group = [&](int p0, int p1, const std::vector<int>& cams, bool big) {
@@ -427,12 +495,30 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
             tp.sg_total += (long long)dim * dim;
             G.h_off = 0;
             tp.dp_max = std::max(tp.dp_max, (dim + 15) & ~15);
-            // chunks of whole points, <= GCH observations
+            // chunks of whole points, <= GCH observations; feature rows sorted by local camera
+            // (observation order inside a camera), each camera's rows zero-padded to a multiple of 4
             int q = p0;
             while (q < p1) {
-                Chunk ch{pt_start[q], pt_start[q], q - p0, q - p0};
+                Chunk ch{pt_start[q], pt_start[q], q - p0, q - p0, (int)tp.lcrow.size(), 0, 0, 0};
                 while (q < p1 && pt_start[q + 1] - ch.o0 <= GCH) { ++q; }
                 ch.o1 = pt_start[q]; ch.q1 = q - p0;
+                std::vector<int> cnt(cams.size(), 0);
+                for (int o = ch.o0; o < ch.o1; ++o)
+                    cnt[std::lower_bound(cams.begin(), cams.end(), obs_cam[o]) - cams.begin()]++;
+                std::vector<int> fill(cams.size());
+                int row = 0;
+                for (size_t lc = 0; lc < cams.size(); ++lc) {
+                    tp.lcrow.push_back(row);
+                    fill[lc] = row;
+                    row += (2 * cnt[lc] + 3) & ~3;
+                }
+                tp.lcrow.push_back(row);
+                ch.nrows = row;
+                for (int o = ch.o0; o < ch.o1; ++o) {
+                    const int lc = (int)(std::lower_bound(cams.begin(), cams.end(), obs_cam[o]) - cams.begin());
+                    tp.obs_row[o] = (short)fill[lc];
+                    fill[lc] += 2;
+                }
                 tp.chk.push_back(ch);
                 ++G.nch;
             }
@@ -480,12 +566,23 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
     }
     // assembly tasks: pose blocks (a <= b) with their (group, la, lb) lists in group order, then
     // pose-intrinsics blocks per camera, then the intrinsics block
+    auto ent = [&](int g, int la, int lb) {   // contribution of group g at local rows 6la / 6lb
+        const Grp& G = tp.grp[g];
+        const int dim = 6 * G.u + K;
+        AEnt e{};
+        e.dim = dim;
+        e.big = G.big;
+        e.rg = G.rg_off + 6 * la;
+        if (G.big) { e.b0 = G.h_off + 3LL * (6 * la); e.b1 = G.h_off + 3LL * (6 * lb); }
+        else { e.b0 = G.sg_off + (long long)(6 * la) * dim + 6 * lb; e.b1 = 0; }
+        return e;
+    };
     std::map<std::pair<int, int>, std::vector<AEnt>> pairs;
     for (int g = 0; g < (int)tp.grp.size(); ++g) {
         const Grp& G = tp.grp[g];
         for (int la = 0; la < G.u; ++la)
             for (int lb = la; lb < G.u; ++lb)
-                pairs[{tp.gcam[G.cam_off + la], tp.gcam[G.cam_off + lb]}].push_back(AEnt{g, la, lb, 0});
+                pairs[{tp.gcam[G.cam_off + la], tp.gcam[G.cam_off + lb]}].push_back(ent(g, la, lb));
     }
     for (auto& kv : pairs) {
         ATask t{0, kv.first.first, kv.first.second, (int)tp.ents.size(), 0, 0, 0, 0};
@@ -499,16 +596,15 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
             const int slot = tp.cref[e];
             const int g = (int)(std::upper_bound(tp.grp.begin(), tp.grp.end(), slot,
                                                  [](int s, const Grp& G) { return s < G.cam_off; }) - tp.grp.begin()) - 1;
-            tp.ents.push_back(AEnt{g, slot - tp.grp[g].cam_off, 0, 0});
+            tp.ents.push_back(ent(g, slot - tp.grp[g].cam_off, tp.grp[g].u));   // column block: the intrinsics rows
         }
         t.l1 = (int)tp.ents.size();
         if (t.l1 > t.l0) tp.tasks.push_back(t);
     }
-    {
-        ATask t{2, 0, 0, (int)tp.ents.size(), 0, 0, 0, 0};
-        for (int g = 0; g < (int)tp.grp.size(); ++g) tp.ents.push_back(AEnt{g, 0, 0, 0});
-        t.l1 = (int)tp.ents.size();
-        tp.tasks.push_back(t);
+    {   // the intrinsics block and rhs: one task per output, every group
+        const int l0 = (int)tp.ents.size();
+        for (int g = 0; g < (int)tp.grp.size(); ++g) tp.ents.push_back(ent(g, tp.grp[g].u, tp.grp[g].u));
+        for (int x = 0; x < K * K + K; ++x) tp.tasks.push_back(ATask{2, 0, x, l0, (int)tp.ents.size(), 0, 0, 0});
     }
 }
 
@@ -557,13 +653,19 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
     for (int p = 0; p < P; ++p) pt_start[p + 1] += pt_start[p];
     Topology tp;
     build_topology(P, C, O, K, pt_start, roc.data(), tp);
+    tile_pattern(C, K, c->nf, c->T, tp.tasks, tp);
+    {
+        const char* de = std::getenv("SFMX_BA_DENSE");
+        c->sparse = !(de && de[0] == '1');
+    }
+    c->tl_start = tp.tl_start;
     c->ngroups = (int)tp.grp.size();
     c->ntasks = (int)tp.tasks.size();
     c->nslots = (int)tp.gcam.size();
     const int JS = jst(K);
     c->stage_n = std::max(GCH * JS, tp.dp_max * ALD);
     c->lds_schur = sizeof(double) * ((size_t)c->stage_n + (size_t)GPTS * (9 + 3 * K));
-    c->lds_lin = sizeof(double) * (size_t)GCH * JS + sizeof(short) * GCH;
+    c->lds_lin = sizeof(double) * ((size_t)GROWS * nfeat(K) + GCH * 8) + sizeof(short) * GCH;
     c->lds_upd = sizeof(double) * ((size_t)GCH * JS + GCH * 3 + GPTS * 3);
     {
         hipError_t e = hipSuccess;
@@ -573,6 +675,8 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
         if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_gupdate<KK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_upd)
         if (K == 1) { LDSATTR(1); } else if (K == 3) { LDSATTR(3); } else { LDSATTR(7); }
 #undef LDSATTR
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)chol_back_sparse, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(sizeof(double) * c->npad));
         if (e != hipSuccess) return bail(fail(SFMX_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(e)));
     }
     hipStream_t st = c->st;
@@ -580,8 +684,10 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
     if ((rc = upload(c->obs_point, rop, st)) || (rc = upload(c->obs_cam, roc, st)) || (rc = upload(c->obs_xy, rxy, st)) ||
         (rc = upload(c->pt_start, pt_start, st)) || (rc = upload(c->grp, tp.grp, st)) || (rc = upload(c->chk, tp.chk, st)) ||
         (rc = upload(c->gcam, tp.gcam, st)) || (rc = upload(c->obs_lc, tp.obs_lc, st)) ||
+        (rc = upload(c->obs_row, tp.obs_row, st)) || (rc = upload(c->lcrow, tp.lcrow, st)) ||
         (rc = upload(c->tasks, tp.tasks, st)) || (rc = upload(c->ents, tp.ents, st)) ||
-        (rc = upload(c->cref_start, tp.cref_start, st)) || (rc = upload(c->cref, tp.cref, st)))
+        (rc = upload(c->cref_start, tp.cref_start, st)) || (rc = upload(c->cref, tp.cref, st)) ||
+        (rc = upload(c->tl, tp.tl, st)) || (rc = upload(c->ut_start, tp.ut_start, st)) || (rc = upload(c->ut, tp.ut, st)))
         return bail(rc);
     const size_t n = c->n, so = std::max(O, 1);
     const size_t ncams = (size_t)C * ncp(K) + K * (K + 1) / 2 + K;

@@ -42,7 +42,7 @@ int main() {
         printf(" | store %lld rhs %lld  (ticks of 100 MHz wall clock)\n", st[20] - st[17], st[21] - st[20]);
         hipEventRecord(e0);
         const int m = T - 1;
-        chol_step<<<m * (m + 1) / 2, 256>>>(S, npad, 0, W, rhs, fail);
+        chol_step<<<m * (m + 1) / 2, 256>>>(S, npad, 0, W, rhs, fail, nullptr);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         hipEventElapsedTime(&ms, e0, e1);
