@@ -45,7 +45,7 @@ constexpr int GCH = 256;      // observations per chunk = threads per group work
 constexpr int GOBS = 1024;    // observations per (normal) group
 constexpr int GPTS = 128;     // points per group (one thread per point)
 constexpr int UMAX = 16;      // cameras per group: S block <= (6*16 + K)^2
-constexpr int SBP = 16;       // points per SYRK sub-batch
+constexpr int SBP = 32;       // points per SYRK sub-batch
 constexpr int SBK = 3 * SBP;  // SYRK depth per sub-batch (3 per point)
 constexpr int ALD = SBK + 1;  // LDS row stride of the SYRK operand (doubles)
 constexpr int MAXT = 7;       // 16x16 upper tiles per wave: dp <= 112 -> 28 tiles / 4 waves
@@ -772,7 +772,7 @@ template <int K>
 __global__ __launch_bounds__(128)
 void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int* __restrict__ cref,
                const double* __restrict__ gpart, double* __restrict__ camsum) {
-    constexpr int NCP = ncp(K), NI = K * (K + 1) / 2 + K;
+    constexpr int NCP = ncp(K);
     const int t = threadIdx.x;
     if ((int)blockIdx.x < C) {
         const int c = blockIdx.x, e0 = cref_start[c], e1 = cref_start[c + 1];
@@ -787,9 +787,11 @@ void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int*
             for (; e < e1; ++e) s0 += gpart[(size_t)cref[e] * NCP + f];
             camsum[(size_t)c * NCP + f] = (s0 + s1) + (s2 + s3);
         }
-    } else {   // every slot: strided per thread (4 chains), then a fixed-order block reduction
+    } else {   // intrinsics field f = blockIdx.x - C over every slot: strided per thread (4 chains), then a
+               // fixed-order block reduction
         __shared__ double sh[8];
-        for (int f = 0; f < NI; ++f) {
+        {
+            const int f = blockIdx.x - C;
             double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
             int e = t;
             for (; e + 3 * (int)blockDim.x < nslots; e += 4 * blockDim.x) {

@@ -155,7 +155,7 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double
                            c->obs_point.as<int>(), c->obs_cam.as<int>(),
                            c->obs_xy.as<double>(), c->pt_start.as<int>(), c->cx, c->cy, c->P, c->C, xp, Jo, colsq_o,
                            grad_o, c->gpart.as<double>(), c->gpl.as<double>());
-    hipLaunchKernelGGL(ba_camred<K>, dim3(c->C + 1), dim3(128), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
+    hipLaunchKernelGGL(ba_camred<K>, dim3(c->C + K * (K + 1) / 2 + K), dim3(128), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
                        c->cref.as<int>(), c->gpart.as<double>(), camsum_o);
     HIPCHK(hipGetLastError());
     RC(allreduce(c, camsum_o, (int64_t)c->C * ncp(K) + K * (K + 1) / 2 + K, SFMX_REDUCE_SUM));
