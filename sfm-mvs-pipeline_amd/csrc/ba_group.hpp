@@ -45,7 +45,7 @@ constexpr int GCH = 256;      // observations per chunk = threads per group work
 constexpr int GOBS = 1024;    // observations per (normal) group
 constexpr int GPTS = 128;     // points per group (one thread per point)
 constexpr int UMAX = 16;      // cameras per group: S block <= (6*16 + K)^2
-constexpr int SBP = 32;       // points per SYRK sub-batch
+constexpr int SBP = 16;       // points per SYRK sub-batch
 constexpr int SBK = 3 * SBP;  // SYRK depth per sub-batch (3 per point)
 constexpr int ALD = SBK + 1;  // LDS row stride of the SYRK operand (doubles)
 constexpr int MAXT = 7;       // 16x16 upper tiles per wave: dp <= 112 -> 28 tiles / 4 waves

@@ -62,6 +62,24 @@ class sfmx_ba_summary(C.Structure):
                 ("final_gradient_max_norm", C.c_double), ("final_radius", C.c_double)]
 
 
+class sfmx_cli_config(C.Structure):
+    """include/sfmx_cli.h"""
+    _fields_ = [(n, C.c_int32) for n in ("run", "loglevel", "omp_cpu_threads", "force_colored_output", "help",
+                                         "n_images", "camera_model", "feature_detector", "feature_limit",
+                                         "sift_n_octave_layers")] + \
+               [("sift_contrast_threshold", C.c_double)] + \
+               [(n, C.c_int32) for n in ("feature_matcher", "norm", "strategy", "feature_sequence",
+                                         "feature_gridlength", "omp_feature_threads", "match_threshold",
+                                         "baseline_homography_threshold", "distinct_matches")] + \
+               [(n, C.c_double) for n in ("ransac_matching_threshold", "ransac_baseline_threshold",
+                                          "ransac_pose_threshold", "homography_inlier_ratio_threshold",
+                                          "pose_inlier_ratio_threshold", "reprojection_error_threshold",
+                                          "pointcloud_feature_merge_distance", "pointcloud_point_merge_distance")] + \
+               [(n, C.c_int32) for n in ("colored", "dense", "sgm", "mesh", "no_decimate", "refine_mesh", "stats",
+                                         "artifacts", "n_warnings")] + \
+               [("out", C.c_char * 1024)]
+
+
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p)
 
 # Every symbol include/sfmx.h (and include/sfmx_ba.h, sfmx_homography.h, sfmx_scene.h) declares, with its ctypes prototype.
@@ -118,6 +136,15 @@ PROTOTYPES = {
                                          _i64p, _i32p, _vp, C.c_int64, _i64p, _i32p, _i32p]),
     "sfmx_openmvs_write": (C.c_int, [C.c_char_p, C.c_uint32, _vp, C.c_int32, _vp, C.c_int32, _P(C.c_double),
                                      C.c_int32, _i64p, _i32p, _i32p, _i32p]),
+    "sfmx_args_parse": (C.c_int, [C.c_int32, _P(C.c_char_p), _P(_vp)]),
+    "sfmx_args_destroy": (C.c_int, [_vp]),
+    "sfmx_args_get": (C.c_int64, [_vp, C.c_char_p, C.c_char_p, _vp, C.c_int64]),
+    "sfmx_args_count": (C.c_int32, [_vp, C.c_char_p]),
+    "sfmx_args_get_at": (C.c_int64, [_vp, C.c_char_p, C.c_int32, _vp, C.c_int64]),
+    "sfmx_args_is_flag": (C.c_int32, [_vp, C.c_char_p]),
+    "sfmx_args_to_string": (C.c_int64, [_vp, _vp, C.c_int64]),
+    "sfmx_cli_configure": (C.c_int, [_vp, _P(sfmx_cli_config), _vp, C.c_int64, _i64p]),
+    "sfmx_cli_usage": (C.c_int64, [C.c_char_p, C.c_int32, _vp, C.c_int64]),
 }
 
 

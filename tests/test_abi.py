@@ -129,8 +129,10 @@ def test_struct_layouts_match_header(tmp_path):
     import ctypes as C
     import subprocess
     structs = {"sfmx_dmatch": _lib.sfmx_dmatch, "sfmx_desc": _lib.sfmx_desc, "sfmx_ba_problem": _lib.sfmx_ba_problem,
-               "sfmx_ba_options": _lib.sfmx_ba_options, "sfmx_ba_summary": _lib.sfmx_ba_summary}
-    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sfmx.h"', '#include "sfmx_ba.h"', 'int main(void){']
+               "sfmx_ba_options": _lib.sfmx_ba_options, "sfmx_ba_summary": _lib.sfmx_ba_summary,
+               "sfmx_cli_config": _lib.sfmx_cli_config}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sfmx.h"', '#include "sfmx_ba.h"', '#include "sfmx_cli.h"',
+             'int main(void){']
     for s, cls in structs.items():
         lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
         for f, _ in cls._fields_:
