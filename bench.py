@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-f4", action="store_true", help="skip the 3D-2D correspondence leg (SURVEY §8 f4)")
     ap.add_argument("--no-mvs", action="store_true", help="skip the openMVS export leg (SURVEY §8 f2)")
     ap.add_argument("--no-features", action="store_true", help="skip the SIFT extraction leg (SURVEY §8 f3)")
+    ap.add_argument("--no-orb-features", action="store_true", help="skip the ORB extraction leg (SURVEY §8 f3)")
+    ap.add_argument("--only-orb-features", action="store_true", help="run only the ORB extraction leg (tuning)")
     ap.add_argument("--only-ba", action="store_true", help="run only the bundle-adjustment leg (tuning)")
     ap.add_argument("--ba-cams", type=int, default=200)
     ap.add_argument("--ba-points", type=int, default=200_000)
@@ -102,6 +104,14 @@ def main():
             dist.destroy_process_group()
         return
 
+    if args.only_orb_features:
+        res = bench_features_orb(args, rank, world, local)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     primary = bench_match(args.workload, args, rank, world, local)
     orb = c3 = None
     if args.workload == "sift" and not args.no_orb:
@@ -111,6 +121,7 @@ def main():
     ba_res = None if args.no_ba else bench_ba(args, rank, world, local)
     mvs_res = None if args.no_mvs else bench_mvs(args, rank, world, local)
     feat_res = None if args.no_features else bench_features(args, rank, world, local)
+    orbf_res = None if args.no_orb_features else bench_features_orb(args, rank, world, local)
     if rank == 0:
         line = {k: v for k, v in primary.items() if not k.startswith("_")}
         if orb is not None:
@@ -122,6 +133,8 @@ def main():
             line["mvs"] = mvs_res
         if feat_res is not None:
             line["features"] = feat_res
+        if orbf_res is not None:
+            line["features_orb"] = orbf_res
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
@@ -682,6 +695,88 @@ def bench_features(args, rank, world, local):
         n0 = counts[-len(imgs)]                  # image 0 of the last timed batch
         res["bit_exact_vs_oracle"] = bool(n0 == cnt[0] and kts[0][:n0].cpu().numpy().tobytes() == ok[0, :n0].tobytes()
                                           and np.array_equal(dts[0][:n0].cpu().numpy(), od[0, :n0]))
+    return res
+
+
+ORB_SHOTS, ORB_LIMIT = 200, 30000   # config 4's 200 shots; cv::ORB::create(30000) as run-orb-*.sh
+
+
+def _orb_pyramid_bytes(h, w, nlevels=8, sf=1.2):
+    """Algorithmic HBM bytes of one image's ORB pass: per level of the 1.2 pyramid the
+    level written (1 B/px) and read by the next resize (1), the FAST pass (read 1 +
+    score written 1), the two NMS passes over the score map (2), and compute()'s blur
+    (read 1 + write 1) -- 8 B per level pixel; corner / keypoint records are noise."""
+    px = 0.0
+    for l in range(nlevels):
+        s = float(np.float32(float(np.float32(sf)) ** l))
+        px += round(w / s) * round(h / s)
+    return 8.0 * px
+
+
+def bench_features_orb(args, rank, world, local):
+    """SURVEY §8 row f3, the ORB half: SfM::extractFeatures (SfM.cpp:577-597) with the
+    run-orb-*.sh detector cv::ORB::create(30000) (PhotogrammetrieCli.cpp:347-348) on
+    200 synthetic 1920x1080 photos resident in HBM -- config 4's shot count; these
+    photos yield ~16.8k keypoints each, config 4's 16k-descriptor shape.  Shots
+    sharded across ranks (strong scaling); keypoints + 32-byte descriptors left in HBM
+    for the Hamming matcher.  Unit: images/s.  Roofline: HBM-bound byte work."""
+    import torch
+    import torch.distributed as dist
+    from sfmx import features, synth
+    dev = f"cuda:{local}"
+    mine = list(range(rank, ORB_SHOTS, world))
+    base = [synth.gray_photo(FEAT_H, FEAT_W, seed=2000 + i) for i in range(2)]
+    imgs = [torch.from_numpy(np.ascontiguousarray(np.roll(base[j % 2], 41 * j, axis=1))).to(dev)
+            for j in range(len(mine))]
+    orb = features.ORB.create(ORB_LIMIT, device=local)
+    kts = [torch.zeros((1 << 15, 7), dtype=torch.int32, device=dev) for _ in imgs]
+    dts = [torch.zeros((1 << 15, 32), dtype=torch.uint8, device=dev) for _ in imgs]
+    counts = orb.detectAndCompute_batch_device(imgs, kts, dts, n_streams=FEAT_STREAMS)   # warm-up
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    steps = max(args.steps // 5, 2)
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        counts = orb.detectAndCompute_batch_device(imgs, kts, dts, n_streams=FEAT_STREAMS)
+        kms.append(features.orb_last_kernel_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = el_rank = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    pyr = _orb_pyramid_bytes(FEAT_H, FEAT_W)
+    achieved = pyr * len(imgs) * steps / el_rank / 1e9
+    res = {"metric": "images/s featurised (ORB detect + compute, SfM::extractFeatures)",
+           "value": ORB_SHOTS * steps / el, "unit": "images/s", "ms_per_image": el_rank / (steps * len(imgs)) * 1e3,
+           "kernel_ms_per_image": float(np.mean(kms)), "streams": FEAT_STREAMS,
+           "keypoints_per_image": float(np.mean(counts)), "scaling": "strong", "n_gpus": world, "dtype": "u8",
+           "config": {"workload": f"{ORB_SHOTS} x {FEAT_W}x{FEAT_H} u8 grayscale, cv::ORB::create({ORB_LIMIT})",
+                      "parallelism": f"shot-sharded x{world}"},
+           "data": "synthetic photos (sfmx.synth.gray_photo), two distinct photos, shifted copies",
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                        "kernel": "ORB pipeline, wall time of the batch (host retainBest steps included)",
+                        "algorithmic": f"{pyr / 1e6:.1f} MB pyramid / FAST / NMS / blur traffic per image "
+                                       f"(bench._orb_pyramid_bytes)"}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+        sample = [imgs[j].cpu().numpy() for j in range(min(threads, 16, len(imgs)))]
+        t = time.perf_counter()
+        cnt, ok, od = oracle.orb_batch(sample, nfeatures=ORB_LIMIT, nthreads=threads)
+        dt_cpu = time.perf_counter() - t
+        res["cpu_baseline"] = {"value": len(sample) / dt_cpu, "unit": "images/s", "cores": threads, "kind": "port",
+                               "sample": f"{len(sample)} of the photos, oracle/orb_oracle.cpp (ORB restated, OpenMP "
+                                         f"over images as SfM.cpp:582), {dt_cpu:.1f} s"}
+        n0 = counts[0]
+        res["bit_exact_vs_oracle"] = bool(all(
+            counts[j] == cnt[j] and kts[j][:counts[j]].cpu().numpy().tobytes() == ok[j, :cnt[j]].tobytes()
+            and np.array_equal(dts[j][:counts[j]].cpu().numpy(), od[j, :cnt[j]]) for j in range(len(sample)))) and n0 > 0
     return res
 
 

@@ -79,6 +79,43 @@ int sfmx_sift_detect_compute_batch(const sfmx_gray_image* images, int32_t n_imag
  * -1 before any call. */
 float sfmx_sift_last_kernel_ms(void);
 
+/* ---- ORB ---------------------------------------------------------------------
+ * cv::ORB::create(nfeatures, scaleFactor, nlevels, edgeThreshold, firstLevel, WTA_K,
+ * scoreType, patchSize, fastThreshold); the reference passes only nfeatures =
+ * featureLimit (cli/PhotogrammetrieCli.cpp:347-348) and keeps OpenCV's defaults. */
+typedef struct {
+    int32_t nfeatures;            /* featureLimit (OpenCV default 500)               */
+    float scale_factor;           /* 1.2                                             */
+    int32_t n_levels;             /* 8 (1..16)                                       */
+    int32_t edge_threshold;       /* 31 (16..256)                                    */
+    int32_t first_level;          /* 0 (only 0)                                      */
+    int32_t wta_k;                /* 2 (only 2)                                      */
+    int32_t score_type;           /* 0 = HARRIS_SCORE (only)                         */
+    int32_t patch_size;           /* 31 (only)                                       */
+    int32_t fast_threshold;       /* 20                                              */
+} sfmx_orb_params;
+
+/* OpenCV's defaults (nfeatures = 500). */
+void sfmx_orb_default_params(sfmx_orb_params* p);
+
+/* ORB detect() then compute() on one width x height 8-bit grayscale image, as
+ * SfM::extractFeatures calls them (sfm/SfM.cpp:586-587).  Writes min(n, capacity)
+ * keypoints and n x 32 descriptor bytes (cv::Mat CV_8U rows, ready for the Hamming
+ * matcher) and sets *n_keypoints = n; SFMX_ECAPACITY if n > capacity.
+ * inputs_on_device as for sfmx_sift_detect_compute. */
+int sfmx_orb_detect_compute(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
+                            const sfmx_orb_params* params, int32_t inputs_on_device, int32_t device, void* stream,
+                            sfmx_keypoint* keypoints, uint8_t* descriptors, int32_t capacity, int32_t* n_keypoints);
+
+/* The batch form over all shots, as sfmx_sift_detect_compute_batch. */
+int sfmx_orb_detect_compute_batch(const sfmx_gray_image* images, int32_t n_images, const sfmx_orb_params* params,
+                                  int32_t inputs_on_device, int32_t device, int32_t n_streams,
+                                  sfmx_keypoint* const* keypoints, uint8_t* const* descriptors,
+                                  const int32_t* capacities, int32_t* n_keypoints, int32_t* status);
+
+/* Device time of the last call (batch: mean per image), HIP events on its stream. */
+float sfmx_orb_last_kernel_ms(void);
+
 #ifdef __cplusplus
 }
 #endif

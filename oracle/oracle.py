@@ -60,6 +60,13 @@ def _load():
                              vp, vp, C.c_int]
     lib.orc_sift_batch.argtypes = [C.POINTER(vp), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
                                    C.c_double, vp, vp, C.c_int, i32p, C.c_int]
+    lib.orc_orb.restype = C.c_int
+    lib.orc_orb.argtypes = [vp, C.c_int, C.c_int, C.c_int64, C.c_int, C.c_float, C.c_int, C.c_int, C.c_int, vp, vp,
+                            C.c_int]
+    lib.orc_orb_batch.restype = None
+    lib.orc_orb_batch.argtypes = [C.POINTER(vp), C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, i32p, C.c_int]
+    lib.orc_orb_stage.restype = C.c_int64
+    lib.orc_orb_stage.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_float, C.c_int, C.c_int, vp, i32p]
     lib.orc_first_sqrt_collision.restype = C.c_int64
     lib.orc_first_sqrt_collision.argtypes = [C.c_int64]
     return lib
@@ -236,6 +243,55 @@ def sift_batch(images, nfeatures=0, contrast_threshold=0.09, cap=16384, nthreads
     lib.orc_sift_batch(ptrs, n, W, H, nfeatures, 3, contrast_threshold, 10.0, 1.6, kps.ctypes.data, desc.ctypes.data,
                        cap, _ptr(cnt), nthreads or os.cpu_count())
     return cnt, kps, desc
+
+
+def orb(image: np.ndarray, nfeatures: int = 500, scale_factor: float = 1.2, nlevels: int = 8, edge_threshold: int = 31,
+        fast_threshold: int = 20):
+    """ORB detect() then compute() restated (oracle/orb_oracle.cpp) on an H x W uint8
+    image -> (keypoints (KEYPOINT_DTYPE), n x 32 uint8 descriptors)."""
+    img = np.ascontiguousarray(image, np.uint8)
+    H, W = img.shape
+    cap = 4096
+    while True:
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = lib.orc_orb(img.ctypes.data, W, H, W, nfeatures, scale_factor, nlevels, edge_threshold, fast_threshold,
+                        kps.ctypes.data, desc.ctypes.data, cap)
+        if n <= cap:
+            return kps[:n], desc[:n]
+        cap = n
+
+
+def orb_batch(images, nfeatures=30000, cap=32768, nthreads=0):
+    """orb() over equally sized images, OpenMP over images -> (counts, keypoints
+    (n_images x cap), descriptors (n_images x cap x 32))."""
+    n = len(images)
+    H, W = images[0].shape
+    imgs = [np.ascontiguousarray(a, np.uint8) for a in images]
+    ptrs = (C.c_void_p * n)(*[a.ctypes.data for a in imgs])
+    kps = np.zeros((n, cap), KEYPOINT_DTYPE)
+    desc = np.zeros((n, cap, 32), np.uint8)
+    cnt = np.zeros(n, np.int32)
+    lib.orc_orb_batch(ptrs, n, W, H, nfeatures, kps.ctypes.data, desc.ctypes.data, cap, _ptr(cnt),
+                      nthreads or os.cpu_count())
+    return cnt, kps, desc
+
+
+def orb_stage(image: np.ndarray, stage: int, nlevels: int = 8, scale_factor: float = 1.2, fast_threshold: int = 20):
+    """Per-level intermediate of the ORB restatement: stage 0 = pyramid, 1 = FAST score
+    maps, 2 = blurred levels -> list of H_l x W_l uint8 arrays."""
+    img = np.ascontiguousarray(image, np.uint8)
+    H, W = img.shape
+    sizes = np.zeros(2 * nlevels, np.int32)
+    n = lib.orc_orb_stage(img.ctypes.data, W, H, nlevels, scale_factor, fast_threshold, stage, None, _ptr(sizes))
+    out = np.zeros(n, np.uint8)
+    lib.orc_orb_stage(img.ctypes.data, W, H, nlevels, scale_factor, fast_threshold, stage, out.ctypes.data, _ptr(sizes))
+    res, off = [], 0
+    for l in range(nlevels):
+        w, h = int(sizes[2 * l]), int(sizes[2 * l + 1])
+        res.append(out[off:off + w * h].reshape(h, w))
+        off += w * h
+    return res
 
 
 def _dist5(dist):

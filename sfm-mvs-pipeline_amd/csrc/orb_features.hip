@@ -1,0 +1,928 @@
+// SPDX-License-Identifier: MIT
+// sfmx ORB extraction on gfx950: the
+// reference's cv::ORB::create(featureLimit) (cli/PhotogrammetrieCli.cpp:347-348)
+// as SfM::extractFeatures runs it, detect() then compute() (sfm/SfM.cpp:586-587),
+// i.e. OpenCV 4.5.1's ORB_Impl::detectAndCompute twice.  Bit-identical to the
+// restatement in oracle/orb_oracle.cpp (which lists the OpenCV pieces restated).
+//
+// Device pipeline per image (one HIP stream; every level of the pyramid lives in
+// one packed u8 slab in HBM, level l at lv[l].off, pitch = width):
+//   orb_resize_kernel     level l = INTER_LINEAR_EXACT resize of level l-1 (8.8 fixed
+//                         point; per-axis offset/coefficient tables from the host)
+//   orb_fast_kernel       FAST 9/16 score map of every level in one launch (64 x 16
+//                         tiles + 3-pixel halo staged in LDS)
+//   orb_nms_kernel        3x3 strict maximum + the 31-pixel border test, ordered
+//                         (raster) compaction per row, two passes around a row scan
+//   host                  retainBest(2 n_l) per level (std::nth_element + partition on
+//                         the FAST scores, exactly the reference's libstdc++ calls)
+//   orb_harris_kernel     Harris response (7x7 block, k = 0.04) per kept corner
+//   host                  retainBest(n_l) per level on the Harris responses
+//   orb_angle_kernel      intensity-centroid angle, one wavefront per keypoint
+//   host                  compute()'s runByImageBorder(31) at full resolution
+//   orb_blur_kernel       7x7 integer Gaussian of the levels the keypoints use (LDS tile)
+//   orb_brief_kernel      rBRIEF, 32 lanes per keypoint, one descriptor byte per lane
+// The host steps sort a few bytes per corner; everything that touches pixels runs
+// on the device.  Roofline: HBM-bound byte work.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/sfmx.h"
+#include "../../include/sfmx_features.h"
+#include "match_common.hpp"
+
+namespace sfmx {
+namespace orb {
+
+constexpr int PATCH = 31, HALF_PATCH = 15, HARRIS_BLOCK = 7, MAX_LEVELS = 16;
+constexpr float HARRIS_K = 0.04f;
+
+struct Lvl {              // one pyramid level in the packed slabs
+    int64_t off;          // byte offset of (0, 0) in pyr / score / blur slabs
+    int w, h;
+    int row0;             // first global row index of this level (NMS rows)
+    float scale, inv_scale;
+    int ax_off, ay_off;   // offsets of this level's axis tables in the coefficient buffer (level >= 1)
+    int xdmin, xdmax, ydmin, ydmax;
+};
+
+struct Kp { float x, y, size, angle, response; int32_t octave, class_id; };
+static_assert(sizeof(Kp) == sizeof(sfmx_keypoint), "cv::KeyPoint layout");
+
+struct AxisEnt { int32_t ofs; uint16_t m0, m1; };
+
+__constant__ int c_pattern[256 * 4] = {
+#include "orb_pattern.inc"
+};
+
+__device__ __forceinline__ int round_f(float v) { return __float2int_rn(v); }   // cvRound(float)
+
+// ------------------------------------------------------------------ pyramid
+// resize(prev, level, INTER_LINEAR_EXACT): horizontal 8.8 taps, then vertical taps,
+// (sum + 2^15) >> 16; rows/columns outside [dmin, dmax) replicate the edge source
+// row/column ((v + 2^7) >> 8 for the replicated rows).
+__device__ __forceinline__ uint32_t hval(const uint8_t* __restrict__ r, const AxisEnt* __restrict__ ax, int x,
+                                         int dmin, int dmax, int last_ofs) {
+    if (x < dmin) return (uint32_t)r[0] << 8;
+    if (x >= dmax) return (uint32_t)r[last_ofs] << 8;
+    const AxisEnt e = ax[x];
+    return min((uint32_t)e.m0 * r[e.ofs] + (uint32_t)e.m1 * r[e.ofs + 1], 0xFFFFu);
+}
+
+__global__ __launch_bounds__(256)
+void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int l,
+                       const AxisEnt* __restrict__ tables) {
+    const Lvl D = lv[l], S = lv[l - 1];
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= D.w || y >= D.h) return;
+    const AxisEnt* ax = tables + D.ax_off;
+    const AxisEnt* ay = tables + D.ay_off;
+    const uint8_t* src = pyr + S.off;
+    const int last_ofs = ax[D.w - 1].ofs;
+    uint32_t v;
+    if (y < D.ydmin || y >= D.ydmax) {
+        const int sy = y < D.ydmin ? 0 : S.h - 1;
+        v = (hval(src + (int64_t)sy * S.w, ax, x, D.xdmin, D.xdmax, last_ofs) + 128u) >> 8;
+    } else {
+        const AxisEnt e = ay[y];
+        const uint32_t h0 = hval(src + (int64_t)e.ofs * S.w, ax, x, D.xdmin, D.xdmax, last_ofs);
+        const uint32_t h1 = hval(src + (int64_t)(e.ofs + 1) * S.w, ax, x, D.xdmin, D.xdmax, last_ofs);
+        v = (h0 * e.m0 + h1 * e.m1 + 32768u) >> 16;
+    }
+    pyr[D.off + (int64_t)y * D.w + x] = (uint8_t)min(v, 255u);
+}
+
+__global__ void orb_copy_kernel(const uint8_t* __restrict__ img, int W, int H, int64_t pitch, uint8_t* __restrict__ dst) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x < W && y < H) dst[(int64_t)y * W + x] = img[(int64_t)y * pitch + x];
+}
+
+// ------------------------------------------------------------------ FAST 9/16
+constexpr int FT_X = 64, FT_Y = 16, FT_H = 3;
+__constant__ int8_t c_ring[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+                                     {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+__global__ __launch_bounds__(256)
+void orb_fast_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int threshold,
+                     uint8_t* __restrict__ score) {
+    const Lvl L = lv[blockIdx.z];
+    const int x0 = blockIdx.x * FT_X, y0 = blockIdx.y * FT_Y;
+    if (x0 >= L.w || y0 >= L.h) return;
+    __shared__ uint8_t t[FT_Y + 2 * FT_H][FT_X + 2 * FT_H + 2];
+    const uint8_t* src = pyr + L.off;
+    for (int i = threadIdx.x; i < (FT_Y + 2 * FT_H) * (FT_X + 2 * FT_H); i += 256) {
+        const int ty = i / (FT_X + 2 * FT_H), tx = i % (FT_X + 2 * FT_H);
+        const int gy = min(max(y0 + ty - FT_H, 0), L.h - 1), gx = min(max(x0 + tx - FT_H, 0), L.w - 1);
+        t[ty][tx] = src[(int64_t)gy * L.w + gx];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x % FT_X;
+    for (int ty = threadIdx.x / FT_X; ty < FT_Y; ty += 256 / FT_X) {
+        const int x = x0 + tx, y = y0 + ty;
+        if (x >= L.w || y >= L.h) continue;
+        int sc = 0;
+        if (x >= 3 && x < L.w - 3 && y >= 3 && y < L.h - 3) {
+            const int v = t[ty + FT_H][tx + FT_H];
+            int d[16];
+            uint32_t dark = 0, bright = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int p = t[ty + FT_H + c_ring[k][1]][tx + FT_H + c_ring[k][0]];
+                d[k] = v - p;
+                dark |= (uint32_t)(p < v - threshold) << k;
+                bright |= (uint32_t)(p > v + threshold) << k;
+            }
+            // a run of >= 9 consecutive ring pixels (cyclic): AND of 9 rotations
+            const uint32_t dd = dark | (dark << 16), bb = bright | (bright << 16);
+            uint32_t rd = dd, rb = bb;
+#pragma unroll
+            for (int s = 1; s < 9; s++) { rd &= dd >> s; rb &= bb >> s; }
+            if ((rd | rb) & 0xFFFFu) {
+                // cornerScore<16>
+                int a0 = threshold;
+#pragma unroll
+                for (int k = 0; k < 16; k += 2) {
+                    int a = min(min(d[(k + 1) & 15], d[(k + 2) & 15]), d[(k + 3) & 15]);
+                    a = min(a, d[(k + 4) & 15]);
+                    a = min(a, d[(k + 5) & 15]);
+                    a = min(a, d[(k + 6) & 15]);
+                    a = min(a, d[(k + 7) & 15]);
+                    a = min(a, d[(k + 8) & 15]);
+                    a0 = max(a0, min(a, d[k]));
+                    a0 = max(a0, min(a, d[(k + 9) & 15]));
+                }
+                int b0 = -a0;
+#pragma unroll
+                for (int k = 0; k < 16; k += 2) {
+                    int b = max(max(d[(k + 1) & 15], d[(k + 2) & 15]), d[(k + 3) & 15]);
+                    b = max(b, d[(k + 4) & 15]);
+                    b = max(b, d[(k + 5) & 15]);
+                    b = max(b, d[(k + 6) & 15]);
+                    b = max(b, d[(k + 7) & 15]);
+                    b = max(b, d[(k + 8) & 15]);
+                    b0 = min(b0, max(b, d[k]));
+                    b0 = min(b0, max(b, d[(k + 9) & 15]));
+                }
+                sc = (-b0 - 1) & 255;
+            }
+        }
+        score[L.off + (int64_t)y * L.w + x] = (uint8_t)sc;
+    }
+}
+
+// ------------------------------------------------------------------ NMS + ordered compaction
+// One workgroup per (level, row).  pass 0 writes the row's corner count, pass 1 the
+// corners (packed (y << 16) | x and the FAST score) at the scanned row offset.
+__device__ __forceinline__ int find_level(const Lvl* lv, int nl, int row) {
+    int l = 0;
+    while (l + 1 < nl && row >= lv[l + 1].row0) l++;
+    return l;
+}
+
+__global__ __launch_bounds__(256)
+void orb_nms_kernel(const uint8_t* __restrict__ score, const Lvl* __restrict__ lv, int nl, int border, int pass,
+                    int* __restrict__ row_count, const int* __restrict__ row_off, int32_t* __restrict__ cpos,
+                    uint8_t* __restrict__ cscore) {
+    __shared__ int wsum[4];
+    const int row = blockIdx.x;
+    const int l = find_level(lv, nl, row);
+    const Lvl L = lv[l];
+    const int y = row - L.row0;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int b = max(border, 3);                        // FAST_t's own 3-pixel frame
+    const bool row_ok = y >= b && y < L.h - b && L.w > 2 * b;
+    int base = pass ? row_off[row] : 0;
+    int total = 0;
+    const uint8_t* s = score + L.off;
+    for (int xc = 0; xc < L.w; xc += 256) {
+        const int x = xc + threadIdx.x;
+        bool keep = false;
+        uint8_t sc = 0;
+        if (row_ok && x >= b && x < L.w - b) {
+            const uint8_t* p = s + (int64_t)y * L.w + x;
+            sc = p[0];
+            if (sc) {
+                const int w = L.w;
+                keep = sc > p[-1] && sc > p[1] && sc > p[-w - 1] && sc > p[-w] && sc > p[-w + 1] && sc > p[w - 1] &&
+                       sc > p[w] && sc > p[w + 1];
+            }
+        }
+        const uint64_t m = __ballot(keep);
+        if (lane == 0) wsum[wid] = __popcll(m);
+        __syncthreads();
+        int before = 0, chunk = 0;
+        for (int w = 0; w < 4; w++) {
+            before += w < wid ? wsum[w] : 0;
+            chunk += wsum[w];
+        }
+        if (pass && keep) {
+            const int k = base + total + before + __popcll(m & ((1ull << lane) - 1));
+            cpos[k] = (y << 16) | x;
+            cscore[k] = sc;
+        }
+        total += chunk;
+        __syncthreads();
+    }
+    if (!pass && threadIdx.x == 0) row_count[row] = total;
+}
+
+// exclusive scan of n row counts into off[0..n] (one workgroup)
+__global__ __launch_bounds__(1024)
+void orb_scan_kernel(const int* __restrict__ cnt, int n, int* __restrict__ off) {
+    __shared__ int part[1024];
+    const int per = (n + 1023) / 1024;
+    const int b = threadIdx.x * per, e = min(b + per, n);
+    int s = 0;
+    for (int i = b; i < e; i++) s += cnt[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int v = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+    for (int i = b; i < e; i++) {
+        off[i] = run;
+        run += cnt[i];
+    }
+    if (threadIdx.x == 1023) off[n] = part[1023];
+}
+
+// ------------------------------------------------------------------ Harris / angle
+struct Kept { int32_t cand; int32_t level; };
+
+__global__ __launch_bounds__(256)
+void orb_harris_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const Kept* __restrict__ kept,
+                       int n, const int32_t* __restrict__ cpos, float* __restrict__ resp) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const Kept k = kept[i];
+    const Lvl L = lv[k.level];
+    const int pos = cpos[k.cand], x0 = pos & 0xFFFF, y0 = pos >> 16;
+    const uint8_t* img = pyr + L.off;
+    const int step = L.w, r = HARRIS_BLOCK / 2;
+    int a = 0, b = 0, c = 0;
+    for (int ii = 0; ii < HARRIS_BLOCK; ii++) {
+        const uint8_t* p = img + (int64_t)(y0 - r + ii) * step + (x0 - r);
+        for (int j = 0; j < HARRIS_BLOCK; j++) {
+            const uint8_t* q = p + j;
+            const int Ix = (q[1] - q[-1]) * 2 + (q[-step + 1] - q[-step - 1]) + (q[step + 1] - q[step - 1]);
+            const int Iy = (q[step] - q[-step]) * 2 + (q[step - 1] - q[-step - 1]) + (q[step + 1] - q[-step + 1]);
+            a += Ix * Ix;
+            b += Iy * Iy;
+            c += Ix * Iy;
+        }
+    }
+    const float scale = 1.f / ((1 << 2) * HARRIS_BLOCK * 255.f);
+    const float scale_sq_sq = scale * scale * scale * scale;
+    resp[i] = ((float)a * b - (float)c * c - HARRIS_K * ((float)a + b) * ((float)a + b)) * scale_sq_sq;
+}
+
+__device__ float fast_atan2(float y, float x) {   // cv::fastAtan2
+    constexpr float R2D = (float)(180 / 3.14159265358979323846);
+    constexpr float P1 = 0.9997878412794807f * R2D, P3 = -0.3258083974640975f * R2D, P5 = 0.1555786518463281f * R2D,
+                    P7 = -0.04432655554792128f * R2D;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((P7 * c2 + P5) * c2 + P3) * c2 + P1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((P7 * c2 + P5) * c2 + P3) * c2 + P1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+__device__ __forceinline__ int wave_isum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// final[j] -> cv::KeyPoint with ICAngles' angle; one wavefront per keypoint (the 31 patch
+// rows u = -15..15 across lanes; integer moments, so the lane order is irrelevant)
+__global__ __launch_bounds__(256)
+void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const Kept* __restrict__ kept,
+                      const float* __restrict__ resp, const int32_t* __restrict__ final_idx, int n,
+                      const int32_t* __restrict__ cpos, const int* __restrict__ umax, Kp* __restrict__ out) {
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j >= n) return;
+    const int ki = final_idx[j];
+    const Kept k = kept[ki];
+    const Lvl L = lv[k.level];
+    const int pos = cpos[k.cand], cx = pos & 0xFFFF, cy = pos >> 16;
+    const uint8_t* img = pyr + L.off;
+    const int step = L.w;
+    int m10 = 0, m01 = 0;
+    if (lane < 2 * HALF_PATCH + 1) {
+        const int u = lane - HALF_PATCH;
+        const uint8_t* col = img + (int64_t)cy * step + cx + u;
+        m10 = u * col[0];
+        const int au = u < 0 ? -u : u;
+        for (int v = 1; v <= HALF_PATCH; ++v) {
+            if (au > umax[v]) continue;
+            const int vp = col[v * step], vm = col[-v * step];
+            m10 += u * (vp + vm);
+            m01 += v * (vp - vm);
+        }
+    }
+    m10 = wave_isum(m10);
+    m01 = wave_isum(m01);
+    if (lane == 0) {
+        Kp q;
+        q.x = (float)cx * L.scale;
+        q.y = (float)cy * L.scale;
+        q.size = PATCH * L.scale;
+        q.angle = fast_atan2((float)m01, (float)m10);
+        q.response = resp[ki];
+        q.octave = k.level;
+        q.class_id = -1;
+        out[j] = q;
+    }
+}
+
+// ------------------------------------------------------------------ compute(): blur + rBRIEF
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on the 8U level through OpenCV's
+// integer separable path: taps x 2^8, (sum + 2^15) >> 16, saturated.
+constexpr int BT_X = 64, BT_Y = 16, BR = 3;
+__constant__ int c_taps[7];
+
+__device__ __forceinline__ int reflect101(int p, int n) {
+    if (n == 1) return 0;
+    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+    return p;
+}
+
+__global__ __launch_bounds__(256)
+void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, uint8_t* __restrict__ blur) {
+    const Lvl L = lv[blockIdx.z];
+    const int x0 = blockIdx.x * BT_X, y0 = blockIdx.y * BT_Y;
+    if (x0 >= L.w || y0 >= L.h) return;
+    __shared__ uint8_t t[BT_Y + 2 * BR][BT_X + 2 * BR + 2];
+    __shared__ int r[BT_Y + 2 * BR][BT_X + 1];
+    const uint8_t* src = pyr + L.off;
+    for (int i = threadIdx.x; i < (BT_Y + 2 * BR) * (BT_X + 2 * BR); i += 256) {
+        const int ty = i / (BT_X + 2 * BR), tx = i % (BT_X + 2 * BR);
+        const int gy = reflect101(y0 + ty - BR, L.h), gx = reflect101(x0 + tx - BR, L.w);
+        t[ty][tx] = src[(int64_t)gy * L.w + gx];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (BT_Y + 2 * BR) * BT_X; i += 256) {
+        const int ty = i / BT_X, tx = i % BT_X;
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 7; j++) s += c_taps[j] * t[ty][tx + j];
+        r[ty][tx] = s;
+    }
+    __syncthreads();
+    const int tx = threadIdx.x % BT_X;
+    for (int ty = threadIdx.x / BT_X; ty < BT_Y; ty += 256 / BT_X) {
+        const int x = x0 + tx, y = y0 + ty;
+        if (x >= L.w || y >= L.h) continue;
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 7; j++) s += c_taps[j] * r[ty + j][tx];
+        blur[L.off + (int64_t)y * L.w + x] = (uint8_t)min(max((s + (1 << 15)) >> 16, 0), 255);
+    }
+}
+
+// fdlibm-style double sin/cos for the descriptor angle (|x| < 8), the same operation
+// sequence as oracle/orb_oracle.cpp:orb_sincos (this file is built with -ffp-contract=off)
+__device__ void orb_sincos(double x, double* s, double* c) {
+    const double q = rint(x * 6.36619772367581382433e-01);
+    const double r = (x - q * 1.57079632673412561417e+00) - q * 6.07710050650619224932e-11;
+    const double z = r * r;
+    const double sr = r + (z * r) * (-1.66666666666666324348e-01 +
+                      z * (8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 +
+                      z * (2.75573137070700676789e-06 + z * (-2.50507602534068634195e-08 +
+                      z * 1.58969099521155010221e-10)))));
+    const double cz = z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 +
+                      z * (2.48015872894767294178e-05 + z * (-2.75573143513906633035e-07 +
+                      z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    const double cr = w + (((1.0 - w) - hz) + z * cz);
+    switch (((int)q) & 3) {
+    case 0: *s = sr; *c = cr; break;
+    case 1: *s = cr; *c = -sr; break;
+    case 2: *s = -sr; *c = -cr; break;
+    default: *s = -cr; *c = sr; break;
+    }
+}
+
+// computeOrbDescriptors (WTA_K 2): 32 lanes per keypoint, lane i builds byte i from
+// pattern pairs 8 i .. 8 i + 7
+__global__ __launch_bounds__(256)
+void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ lv, const Kp* __restrict__ kps, int n,
+                      uint8_t* __restrict__ desc) {
+    const int j = blockIdx.x * 8 + (threadIdx.x >> 5), i = threadIdx.x & 31;
+    if (j >= n) return;
+    const Kp k = kps[j];
+    const Lvl L = lv[k.octave];
+    float angle = k.angle;
+    angle *= (float)(3.14159265358979323846 / 180.f);
+    double sd, cd;
+    orb_sincos((double)angle, &sd, &cd);
+    const float a = (float)cd, b = (float)sd;
+    const int cy = round_f(k.y * L.inv_scale), cx = round_f(k.x * L.inv_scale);
+    const uint8_t* img = blur + L.off;
+    auto value = [&](int idx) -> int {
+        const int px = c_pattern[2 * idx], py = c_pattern[2 * idx + 1];
+        const float x = px * a - py * b, y = px * b + py * a;
+        const int yy = min(max(cy + round_f(y), 0), L.h - 1), xx = min(max(cx + round_f(x), 0), L.w - 1);
+        return img[(int64_t)yy * L.w + xx];
+    };
+    int val = 0;
+#pragma unroll
+    for (int bit = 0; bit < 8; bit++) {
+        const int base = 16 * i + 2 * bit;
+        val |= (value(base) < value(base + 1)) << bit;
+    }
+    desc[(int64_t)j * 32 + i] = (uint8_t)val;
+}
+
+// ------------------------------------------------------------------ host
+static int host_round_f(float v) { return (int)std::nearbyint(v); }
+static int host_round_d(double v) { return (int)std::nearbyint(v); }
+static float get_scale(int level, double sf) { return (float)std::pow(sf, (double)level); }
+
+struct Resp { float response; int32_t idx; };
+
+// KeyPointsFilter::retainBest on (response, index) records: the same comparisons and moves
+// as on the reference's KeyPoint vector, so the same permutation
+static void retain_best(std::vector<Resp>& k, int n) {
+    if (n >= 0 && k.size() > (size_t)n) {
+        if (n == 0) { k.clear(); return; }
+        std::nth_element(k.begin(), k.begin() + n - 1, k.end(),
+                         [](const Resp& a, const Resp& b) { return a.response > b.response; });
+        const float amb = k[n - 1].response;
+        auto end = std::partition(k.begin() + n, k.end(), [amb](const Resp& p) { return p.response >= amb; });
+        k.resize(end - k.begin());
+    }
+}
+
+static void linear_axis(int dsize, int ssize, std::vector<AxisEnt>& out, int& dmin, int& dmax) {
+    dmin = 0;
+    dmax = dsize;
+    const double inv = (double)dsize / ssize;
+    const double scale = 1.0 / inv;
+    for (int v = 0; v < dsize; v++) {
+        AxisEnt e{0, 0, 0};
+        const double fval = scale * ((double)v + 0.5) - 0.5;
+        const int ival = (int)std::floor(fval);
+        if (ival >= 0 && ssize > 1) {
+            if (ival < ssize - 1) {
+                e.ofs = ival;
+                e.m1 = (uint16_t)host_round_d((fval - (double)ival) * 256.0);
+                e.m0 = (uint16_t)(256 - e.m1);
+            } else {
+                e.ofs = ssize - 1;
+                dmax = std::min(dmax, v);
+            }
+        } else {
+            dmin = std::max(dmin, v + 1);
+        }
+        out.push_back(e);
+    }
+}
+
+static void blur_taps(int taps[7]) {   // getGaussianKernel(7, 2, CV_32F) x 2^8 (see the oracle)
+    const int n = 7;
+    const double sigma = 2.0, scale2X = -0.125 / (sigma * sigma);
+    double t[4], sum = 0;
+    for (int i = 0, x = 1 - n; i < n / 2; i++, x += 2) {
+        t[i] = std::exp((double)(x * x) * scale2X);
+        sum += t[i];
+    }
+    sum *= 2.0;
+    sum += 1.0;
+    t[n / 2] = 1.0;
+    for (int i = 0; i <= n / 2; i++) {
+        const float k = (float)(t[i] / sum);
+        taps[i] = taps[n - 1 - i] = host_round_d((double)k * 256.0);
+    }
+}
+
+static std::vector<int> circle_umax() {
+    std::vector<int> umax(HALF_PATCH + 2);
+    const int vmax = (int)std::floor(HALF_PATCH * std::sqrt(2.f) / 2 + 1);
+    const int vmin = (int)std::ceil(HALF_PATCH * std::sqrt(2.f) / 2);
+    for (int v = 0; v <= vmax; ++v) umax[v] = host_round_d(std::sqrt((double)HALF_PATCH * HALF_PATCH - v * v));
+    for (int v = HALF_PATCH, v0 = 0; v >= vmin; --v) {
+        while (umax[v0] == umax[v0 + 1]) ++v0;
+        umax[v] = v0;
+        ++v0;
+    }
+    return umax;
+}
+
+thread_local float g_last_ms = -1.f;
+std::once_flag g_const_once[64];
+
+struct Arena {                 // per-thread device scratch, grown on demand
+    int dev = -1;
+    char* p = nullptr;
+    size_t cap = 0, used = 0;
+    bool overflow = false;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    void release() {
+        if (dev < 0) return;
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(dev);
+        if (p) (void)hipFree(p);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        if (prev >= 0) (void)hipSetDevice(prev);
+        p = nullptr; cap = 0; e0 = e1 = nullptr; dev = -1;
+    }
+    bool reserve(int device, size_t bytes) {
+        if (dev != device) {
+            release();
+            (void)hipSetDevice(device);
+            dev = device;
+        }
+        used = 0;
+        overflow = false;
+        if (bytes > cap) {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+            if (hipMalloc(&p, bytes) != hipSuccess) return false;
+            cap = bytes;
+        }
+        if (!e0 && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) return false;
+        return true;
+    }
+    template <class T> T* take(size_t n) {
+        T* r = reinterpret_cast<T*>(p + used);
+        used += (sizeof(T) * n + 255) & ~(size_t)255;
+        if (used > cap) overflow = true;
+        return r;
+    }
+};
+
+bool is_gfx950(int device) {
+    static std::atomic<int> state[64];
+    if (device < 0 || device >= 64) return false;
+    int v = state[device].load();
+    if (v == 0) {
+        hipDeviceProp_t prop;
+        v = (hipGetDeviceProperties(&prop, device) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) ? 1 : 2;
+        state[device].store(v);
+    }
+    return v == 1;
+}
+
+}  // namespace orb
+}  // namespace sfmx
+
+using namespace sfmx;
+using namespace sfmx::orb;
+
+#define OCHK(expr) do { if ((expr) != hipSuccess) { rc = SFMX_EDEVICE; set_last_error("HIP error in " #expr); goto done; } } while (0)
+
+extern "C" {
+
+void sfmx_orb_default_params(sfmx_orb_params* p) {
+    if (!p) return;
+    p->nfeatures = 500;
+    p->scale_factor = 1.2f;
+    p->n_levels = 8;
+    p->edge_threshold = 31;
+    p->first_level = 0;
+    p->wta_k = 2;
+    p->score_type = 0;
+    p->patch_size = 31;
+    p->fast_threshold = 20;
+}
+
+float sfmx_orb_last_kernel_ms(void) { return g_last_ms; }
+
+}  // extern "C"
+
+namespace {
+
+struct Scratch {            // image-size buffers / corner-count buffers, grown on demand
+    Arena img, kp;
+};
+thread_local Scratch g_scratch;
+
+int orb_impl(const uint8_t* image, int32_t width, int32_t height, int64_t pitch, const sfmx_orb_params* P,
+             int32_t inputs_on_device, int32_t device, void* stream, sfmx_keypoint* keypoints, uint8_t* descriptors,
+             int32_t capacity, int32_t* n_keypoints, Scratch& scratch, float* last_ms) {
+    if (!image || !P || !n_keypoints || capacity < 0 || (capacity > 0 && !keypoints)) {
+        set_last_error("null argument");
+        return SFMX_EINVAL;
+    }
+    if (width < 1 || height < 1 || pitch < width || width > 16384 || height > 16384) {
+        set_last_error("image size must be 1..16384 with pitch >= width");
+        return SFMX_EINVAL;
+    }
+    if (P->nfeatures < 0 || !(P->scale_factor > 1.f) || P->n_levels < 1 || P->n_levels > MAX_LEVELS ||
+        P->edge_threshold < 16 || P->edge_threshold > 256 || P->first_level != 0 || P->wta_k != 2 ||
+        P->score_type != 0 || P->patch_size != 31 || P->fast_threshold < 0) {
+        set_last_error("unsupported ORB parameters (edgeThreshold 16..256, firstLevel 0, WTA_K 2, HARRIS_SCORE, patchSize 31)");
+        return SFMX_EINVAL;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { set_last_error("no HIP device visible"); return SFMX_EDEVICE; }
+    if (device < 0 || device >= ndev) { set_last_error("device index out of range"); return SFMX_EINVAL; }
+    if (!is_gfx950(device)) { set_last_error("sfmx kernels are built for gfx950 only"); return SFMX_EDEVICE; }
+    // levels, their packed layout and resize tables (host)
+    const double sf = (double)P->scale_factor;
+    const int nl = P->n_levels, border = P->edge_threshold;
+    const int thr = std::min(std::max(P->fast_threshold, 0), 255);
+    std::vector<Lvl> lv(nl);
+    std::vector<AxisEnt> tables;
+    int64_t px = 0;
+    int rows = 0, maxw = 0, maxh = 0;
+    for (int l = 0; l < nl; l++) {
+        Lvl& L = lv[l];
+        L = Lvl{};
+        L.scale = get_scale(l, sf);
+        L.inv_scale = 1.f / L.scale;
+        const float inv = 1.0f / L.scale;
+        L.w = host_round_f(width * inv);
+        L.h = host_round_f(height * inv);
+        if (L.w < 1 || L.h < 1) { set_last_error("pyramid level of zero size (image too small for n_levels)"); return SFMX_EINVAL; }
+        L.off = px;
+        L.row0 = rows;
+        px += ((int64_t)L.w * L.h + 255) & ~(int64_t)255;
+        rows += L.h;
+        maxw = std::max(maxw, L.w);
+        maxh = std::max(maxh, L.h);
+        if (l > 0) {
+            L.ax_off = (int)tables.size();
+            linear_axis(L.w, lv[l - 1].w, tables, L.xdmin, L.xdmax);
+            L.ay_off = (int)tables.size();
+            linear_axis(L.h, lv[l - 1].h, tables, L.ydmin, L.ydmax);
+        }
+    }
+    std::vector<int> per(nl);                  // computeKeyPoints' nfeaturesPerLevel
+    {
+        const float factor = (float)(1.0 / sf);
+        float nd = P->nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nl));
+        int sum = 0;
+        for (int l = 0; l < nl - 1; l++) {
+            per[l] = host_round_f(nd);
+            sum += per[l];
+            nd *= factor;
+        }
+        per[nl - 1] = std::max(P->nfeatures - sum, 0);
+    }
+    const std::vector<int> umax = circle_umax();
+    const int64_t CAND_CAP = px / 4 + 1024;    // strict 3x3 maxima: at most one per 2 x 2 cell
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device);
+    const hipStream_t st = (hipStream_t)stream;
+    int rc = SFMX_OK;
+    {
+        const size_t need = (size_t)px * 3 + (size_t)CAND_CAP * 5 + (size_t)(rows + 1) * 8 +
+                            tables.size() * sizeof(AxisEnt) + sizeof(Lvl) * nl + sizeof(int) * umax.size() +
+                            (size_t)width * height + 256 * 16;
+        if (!scratch.img.reserve(device, need)) { rc = SFMX_ENOMEM; set_last_error("device allocation failed"); goto done; }
+        std::call_once(g_const_once[device], [] {
+            int taps[7];
+            blur_taps(taps);
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(c_taps), taps, sizeof(taps));
+        });
+        {
+            Arena& A = scratch.img;
+            uint8_t* pyr = A.take<uint8_t>(px);
+            uint8_t* score = A.take<uint8_t>(px);
+            uint8_t* blur = A.take<uint8_t>(px);
+            int32_t* cpos = A.take<int32_t>(CAND_CAP);
+            uint8_t* cscore = A.take<uint8_t>(CAND_CAP);
+            int* row_cnt = A.take<int>(rows + 1);
+            int* row_off = A.take<int>(rows + 1);
+            AxisEnt* dtab = A.take<AxisEnt>(std::max<size_t>(tables.size(), 1));
+            Lvl* dlv = A.take<Lvl>(nl);
+            int* dumax = A.take<int>(umax.size());
+            uint8_t* t = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)width * height);
+            if (A.overflow) { set_last_error("internal: ORB scratch arena too small"); rc = SFMX_ECAPACITY; goto done; }
+            const uint8_t* dimg = image;
+            int64_t dpitch = pitch;
+            if (!inputs_on_device) {
+                OCHK(hipMemcpy2DAsync(t, width, image, pitch, width, height, hipMemcpyHostToDevice, st));
+                dimg = t;
+                dpitch = width;
+            }
+            if (!tables.empty())
+                OCHK(hipMemcpyAsync(dtab, tables.data(), tables.size() * sizeof(AxisEnt), hipMemcpyHostToDevice, st));
+            OCHK(hipMemcpyAsync(dlv, lv.data(), sizeof(Lvl) * nl, hipMemcpyHostToDevice, st));
+            OCHK(hipMemcpyAsync(dumax, umax.data(), sizeof(int) * umax.size(), hipMemcpyHostToDevice, st));
+            OCHK(hipEventRecord(A.e0, st));
+            // ---- detect(): pyramid, FAST, NMS
+            orb_copy_kernel<<<dim3((width + 255) / 256, height), 256, 0, st>>>(dimg, width, height, dpitch, pyr);
+            for (int l = 1; l < nl; l++)
+                orb_resize_kernel<<<dim3((lv[l].w + 255) / 256, lv[l].h), 256, 0, st>>>(pyr, dlv, l, dtab);
+            orb_fast_kernel<<<dim3((maxw + FT_X - 1) / FT_X, (maxh + FT_Y - 1) / FT_Y, nl), 256, 0, st>>>(pyr, dlv, thr,
+                                                                                                      score);
+            orb_nms_kernel<<<rows, 256, 0, st>>>(score, dlv, nl, border, 0, row_cnt, nullptr, nullptr, nullptr);
+            orb_scan_kernel<<<1, 1024, 0, st>>>(row_cnt, rows, row_off);
+            orb_nms_kernel<<<rows, 256, 0, st>>>(score, dlv, nl, border, 1, nullptr, row_off, cpos, cscore);
+            OCHK(hipGetLastError());
+            std::vector<int> hoff(rows + 1);
+            OCHK(hipMemcpyAsync(hoff.data(), row_off, sizeof(int) * (rows + 1), hipMemcpyDeviceToHost, st));
+            OCHK(hipStreamSynchronize(st));
+            const int ncand = hoff[rows];
+            if (ncand > CAND_CAP) { set_last_error("internal: corner buffer overflow"); rc = SFMX_EINTERNAL; goto done; }
+            std::vector<uint8_t> hsc(ncand);
+            if (ncand) OCHK(hipMemcpyAsync(hsc.data(), cscore, ncand, hipMemcpyDeviceToHost, st));
+            OCHK(hipStreamSynchronize(st));
+            // retainBest(2 n_l) per level on the FAST scores
+            std::vector<Kept> kept;
+            std::vector<int> kcount(nl);
+            for (int l = 0; l < nl; l++) {
+                const int c0 = hoff[lv[l].row0], c1 = hoff[lv[l].row0 + lv[l].h];
+                std::vector<Resp> r(c1 - c0);
+                for (int i = c0; i < c1; i++) r[i - c0] = Resp{(float)hsc[i], i};
+                retain_best(r, 2 * per[l]);
+                kcount[l] = (int)r.size();
+                for (const Resp& q : r) kept.push_back(Kept{q.idx, l});
+            }
+            const int nk = (int)kept.size();
+            // buffers sized by the kept-corner count (ties at the retainBest boundary can exceed 2 n)
+            const size_t kneed = (size_t)(nk + 1) * (sizeof(Kept) + 4 + 4 + 2 * sizeof(Kp) + 32) + 256 * 8;
+            if (!scratch.kp.reserve(device, kneed)) { rc = SFMX_ENOMEM; set_last_error("device allocation failed"); goto done; }
+            {
+                Arena& K = scratch.kp;
+                Kept* dkept = K.take<Kept>(nk + 1);
+                float* dresp = K.take<float>(nk + 1);
+                int32_t* dfinal = K.take<int32_t>(nk + 1);
+                Kp* dkp = K.take<Kp>(nk + 1);
+                Kp* dfin = K.take<Kp>(nk + 1);
+                uint8_t* ddesc = K.take<uint8_t>((size_t)(nk + 1) * 32);
+                if (K.overflow) { set_last_error("internal: ORB keypoint arena too small"); rc = SFMX_ECAPACITY; goto done; }
+                std::vector<float> hresp(nk);
+                if (nk) {
+                    OCHK(hipMemcpyAsync(dkept, kept.data(), sizeof(Kept) * nk, hipMemcpyHostToDevice, st));
+                    orb_harris_kernel<<<(nk + 255) / 256, 256, 0, st>>>(pyr, dlv, dkept, nk, cpos, dresp);
+                    OCHK(hipGetLastError());
+                    OCHK(hipMemcpyAsync(hresp.data(), dresp, sizeof(float) * nk, hipMemcpyDeviceToHost, st));
+                    OCHK(hipStreamSynchronize(st));
+                }
+                // retainBest(n_l) per level on the Harris responses
+                std::vector<int32_t> fin;
+                for (int l = 0, k0 = 0; l < nl; k0 += kcount[l], l++) {
+                    std::vector<Resp> r(kcount[l]);
+                    for (int i = 0; i < kcount[l]; i++) r[i] = Resp{hresp[k0 + i], k0 + i};
+                    retain_best(r, per[l]);
+                    for (const Resp& q : r) fin.push_back(q.idx);
+                }
+                const int nf = (int)fin.size();
+                std::vector<Kp> kps(nf);
+                if (nf) {
+                    OCHK(hipMemcpyAsync(dfinal, fin.data(), sizeof(int32_t) * nf, hipMemcpyHostToDevice, st));
+                    orb_angle_kernel<<<(nf + 3) / 4, 256, 0, st>>>(pyr, dlv, dkept, dresp, dfinal, nf, cpos, dumax, dkp);
+                    OCHK(hipGetLastError());
+                    OCHK(hipMemcpyAsync(kps.data(), dkp, sizeof(Kp) * nf, hipMemcpyDeviceToHost, st));
+                    OCHK(hipStreamSynchronize(st));
+                }
+                // ---- compute(): runByImageBorder at full resolution (Rect::contains(Point(pt)))
+                if (height <= 2 * border || width <= 2 * border) kps.clear();
+                else
+                    kps.erase(std::remove_if(kps.begin(), kps.end(), [&](const Kp& q) {
+                                  const int x = host_round_f(q.x), y = host_round_f(q.y);
+                                  return !(border <= x && x < width - border && border <= y && y < height - border);
+                              }), kps.end());
+                const int n = (int)kps.size();
+                *n_keypoints = n;
+                const int m = std::min(n, (int)capacity);
+                if (m > 0) {
+                    OCHK(hipMemcpyAsync(dfin, kps.data(), sizeof(Kp) * m, hipMemcpyHostToDevice, st));
+                    if (descriptors) {
+                        int nlev = 0;
+                        for (int q = 0; q < m; q++) nlev = std::max(nlev, kps[q].octave + 1);
+                        orb_blur_kernel<<<dim3((maxw + BT_X - 1) / BT_X, (maxh + BT_Y - 1) / BT_Y, nlev), 256, 0, st>>>(
+                            pyr, dlv, blur);
+                        uint8_t* dd = inputs_on_device ? descriptors : ddesc;
+                        orb_brief_kernel<<<(m + 7) / 8, 256, 0, st>>>(blur, dlv, dfin, m, dd);
+                        OCHK(hipGetLastError());
+                        if (!inputs_on_device)
+                            OCHK(hipMemcpyAsync(descriptors, dd, (size_t)m * 32, hipMemcpyDeviceToHost, st));
+                    }
+                    if (inputs_on_device) OCHK(hipMemcpyAsync(keypoints, dfin, sizeof(Kp) * m, hipMemcpyDeviceToDevice, st));
+                    else std::memcpy(keypoints, kps.data(), sizeof(Kp) * m);
+                }
+                OCHK(hipEventRecord(A.e1, st));
+                OCHK(hipStreamSynchronize(st));
+                float ms = -1.f;
+                (void)hipEventElapsedTime(&ms, A.e0, A.e1);
+                *last_ms = ms;
+                if (n > capacity) { set_last_error("keypoint capacity too small"); rc = SFMX_ECAPACITY; }
+            }
+        }
+    done:;
+    }
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return rc;
+}
+
+struct BatchSlot {
+    Scratch arena;
+    hipStream_t stream = nullptr;
+    int device = -1;
+};
+std::mutex g_batch_mu;
+std::vector<std::unique_ptr<BatchSlot>> g_slots;
+
+}  // namespace
+
+extern "C" {
+
+int sfmx_orb_detect_compute(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
+                            const sfmx_orb_params* params, int32_t inputs_on_device, int32_t device, void* stream,
+                            sfmx_keypoint* keypoints, uint8_t* descriptors, int32_t capacity, int32_t* n_keypoints) {
+    return orb_impl(image, width, height, pitch, params, inputs_on_device, device, stream, keypoints, descriptors,
+                    capacity, n_keypoints, g_scratch, &g_last_ms);
+}
+
+int sfmx_orb_detect_compute_batch(const sfmx_gray_image* images, int32_t n_images, const sfmx_orb_params* params,
+                                  int32_t inputs_on_device, int32_t device, int32_t n_streams,
+                                  sfmx_keypoint* const* keypoints, uint8_t* const* descriptors,
+                                  const int32_t* capacities, int32_t* n_keypoints, int32_t* status) {
+    if (n_images < 0 || (n_images > 0 && (!images || !keypoints || !capacities || !n_keypoints)) || !params) {
+        set_last_error("null argument");
+        return SFMX_EINVAL;
+    }
+    if (n_streams < 1 || n_streams > 16) { set_last_error("n_streams must be 1..16"); return SFMX_EINVAL; }
+    if (n_images == 0) { g_last_ms = 0.f; return SFMX_OK; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { set_last_error("no HIP device visible"); return SFMX_EDEVICE; }
+    if (device < 0 || device >= ndev) { set_last_error("device index out of range"); return SFMX_EINVAL; }
+    std::lock_guard<std::mutex> lock(g_batch_mu);
+    const int ns = std::min<int>(n_streams, n_images);
+    while ((int)g_slots.size() < ns) g_slots.emplace_back(new BatchSlot());
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device);
+    for (int i = 0; i < ns; ++i) {
+        BatchSlot& sl = *g_slots[i];
+        if (sl.device != device) {
+            if (sl.stream) (void)hipStreamDestroy(sl.stream);
+            sl.stream = nullptr;
+            if (hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) {
+                if (prev >= 0) (void)hipSetDevice(prev);
+                set_last_error("hipStreamCreate failed");
+                return SFMX_EDEVICE;
+            }
+            sl.device = device;
+        }
+    }
+    std::atomic<int> next{0};
+    std::vector<int> rcs(n_images, SFMX_OK);
+    std::vector<float> kms(ns, 0.f);
+    std::vector<std::string> errs(n_images);
+    auto work = [&](int slot) {
+        (void)hipSetDevice(device);
+        BatchSlot& sl = *g_slots[slot];
+        for (int i; (i = next.fetch_add(1)) < n_images;) {
+            float ms = 0.f;
+            const sfmx_gray_image& im = images[i];
+            rcs[i] = orb_impl(im.data, im.width, im.height, im.pitch, params, inputs_on_device, device, sl.stream,
+                              keypoints[i], descriptors ? descriptors[i] : nullptr, capacities[i], &n_keypoints[i],
+                              sl.arena, &ms);
+            if (rcs[i] != SFMX_OK) errs[i] = sfmx_last_error();
+            kms[slot] += ms;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < ns; ++i) th.emplace_back(work, i);
+    work(0);
+    for (auto& t : th) t.join();
+    if (prev >= 0) (void)hipSetDevice(prev);
+    float total = 0.f;
+    for (float k : kms) total += k;
+    g_last_ms = total / n_images;
+    int rc = SFMX_OK;
+    for (int i = 0; i < n_images; ++i) {
+        if (status) status[i] = rcs[i];
+        if (rcs[i] != SFMX_OK && rc == SFMX_OK) {
+            rc = rcs[i];
+            set_last_error(("image " + std::to_string(i) + ": " + errs[i]).c_str());
+        }
+    }
+    return rc;
+}
+
+}  // extern "C"

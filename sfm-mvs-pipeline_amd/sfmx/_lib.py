@@ -131,6 +131,12 @@ PROTOTYPES = {
     "sfmx_sift_detect_compute_batch": (C.c_int, [_vp, C.c_int32, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp,
                                                  _i32p, _i32p, _i32p]),
     "sfmx_sift_last_kernel_ms": (C.c_float, []),
+    "sfmx_orb_default_params": (None, [_vp]),
+    "sfmx_orb_detect_compute": (C.c_int, [_vp, C.c_int32, C.c_int32, C.c_int64, _vp, C.c_int32, C.c_int32, _vp, _vp,
+                                          _vp, C.c_int32, _i32p]),
+    "sfmx_orb_detect_compute_batch": (C.c_int, [_vp, C.c_int32, _vp, C.c_int32, C.c_int32, C.c_int32, _vp, _vp,
+                                                _i32p, _i32p, _i32p]),
+    "sfmx_orb_last_kernel_ms": (C.c_float, []),
     "sfmx_undistort_last_kernel_ms": (C.c_float, []),
     "sfmx_openmvs_serialize": (C.c_int, [C.c_uint32, _vp, C.c_int32, _vp, C.c_int32, _P(C.c_double), C.c_int32,
                                          _i64p, _i32p, _vp, C.c_int64, _i64p, _i32p, _i32p]),

@@ -3,7 +3,7 @@ driver (sfmx/cli.py -> csrc/cli.cpp flags -> SIFT / matching / filters / homogra
 kernels) on the reference's insel images (BASELINE config C1, tests/golden/insel/),
 and every artefact compared with the oracle chain on the same decoded pixels:
 
-    oracle.sift(limit, 3, 0.09)  ->  strategy pairs  ->  oracle.match_pairs (exact 2-NN,
+    oracle.sift(limit, 3, 0.09) | oracle.orb(limit)  ->  strategy pairs  ->  oracle.match_pairs (exact 2-NN,
     ratio 0.7)  ->  oracle.filter_matches(--distinct-matches, -Pmatch-threshold)  ->
     oracle.homography_ratios(-Pransac-matching-threshold) over the kept pairs.
 
@@ -32,6 +32,9 @@ CASES = [  # (script, $1, $2, extra flags)
     ("run-grid-featurelimit.sh", "2", "1", []),
     ("run-unordered-flann.sh", "", "", ["-Pmatch-threshold=4", "-Pransac-matching-threshold=0.01"]),
     ("run-grid-flann-distortion.sh", "3", "3", ["-Pfeature-limit=150"]),
+    ("run-orb-sequence-flann.sh", "2", "", []),              # ORB(30000) -> Hamming
+    ("run-orb-grid.sh", "2", "1", ["--distinct-matches"]),
+    ("run-orb-unordered.sh", "", "", ["-Pfeature-limit=400"]),
 ]
 
 
@@ -58,8 +61,11 @@ def test_run_script_replay_matches_oracle(script, a1, a2, extra, tmp_path):
 
     # oracle chain on the same pixels
     imgs = [cli.load_gray(p, summary["camera"]["resolution"]) for p in paths]
-    feats = [oracle.sift(im, nfeatures=cfg["feature_limit"], contrast_threshold=cfg["sift_contrast_threshold"])
-             for im in imgs]
+    if cfg["feature_detector"] == 1:
+        feats = [oracle.orb(im, nfeatures=cfg["feature_limit"]) for im in imgs]
+    else:
+        feats = [oracle.sift(im, nfeatures=cfg["feature_limit"], contrast_threshold=cfg["sift_contrast_threshold"])
+                 for im in imgs]
     for i, (k, d) in enumerate(feats):
         z = np.load(out / "features" / f"{i}{os.path.basename(paths[i])}.npz")
         assert z["keypoints"].tobytes() == k.tobytes(), i

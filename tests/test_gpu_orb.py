@@ -1,0 +1,92 @@
+"""ORB extraction on the GPU:
+sfmx_orb_detect_compute (csrc/orb_features.hip) bit-identical to the restatement in
+oracle/orb_oracle.cpp -- all seven cv::KeyPoint fields, keypoint order (retainBest's
+nth_element / partition order) and the 32-byte descriptors -- through the C ABI,
+host, device and batch modes.  Parity with OpenCV itself: unpinned (no OpenCV here)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+import sift_cases
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _insel(i):
+    from sfmx import cli
+    return cli.load_gray(os.path.join(REPO, "tests", "golden", "insel", f"{i}.jpg"))
+
+
+def _check(img, **kw):
+    import sfmx
+    k, d = sfmx.features.ORB.create(**kw).detectAndCompute(img)
+    ok = {"nfeatures": kw.get("nfeatures", 500), "scale_factor": kw.get("scaleFactor", 1.2),
+          "nlevels": kw.get("nlevels", 8), "edge_threshold": kw.get("edgeThreshold", 31),
+          "fast_threshold": kw.get("fastThreshold", 20)}
+    ek, ed = oracle.orb(img, **ok)
+    assert len(k) == len(ek), (len(k), len(ek))
+    assert k.tobytes() == ek.tobytes(), [(a, b) for a, b in zip(k, ek) if a.tobytes() != b.tobytes()][:3]
+    assert np.array_equal(d, ed), np.nonzero((d != ed).any(1))[0][:5]
+    return k, d
+
+
+@pytest.mark.parametrize("i", [1, 2, 3])
+@pytest.mark.parametrize("nf", [30000, 500, 7])
+def test_insel_bit_exact(i, nf):
+    k, _ = _check(_insel(i), nfeatures=nf)
+    assert len(k) >= min(nf, 7)
+
+
+@pytest.mark.parametrize("shape,seed", [((120, 160), 1), ((97, 131), 2), ((300, 400), 3), ((481, 641), 4)])
+def test_blob_images_bit_exact(shape, seed):
+    _check(sift_cases.blob_image(*shape, n_blobs=120, seed=seed, noise=6.0), nfeatures=2000)
+
+
+def test_ties_at_the_retain_best_boundary():
+    """A flat image with a sparse checkerboard of identical corners: FAST scores and Harris
+    responses tie massively, so retainBest's partition keeps > n and the order is
+    nth_element's."""
+    img = np.full((240, 320), 100, np.uint8)
+    img[40:200:8, 40:280:8] = 200
+    img[44:196:16, 44:276:16] = 10
+    k, _ = _check(img, nfeatures=50)
+    assert len(k) > 50
+
+
+def test_large_photo_and_parameters():
+    img = sift_cases.blob_image(1080, 1920, n_blobs=400, seed=11, noise=8.0)
+    k, _ = _check(img, nfeatures=30000)
+    assert len(k) > 1000
+    _check(img, nfeatures=3000, scaleFactor=1.5, nlevels=5, fastThreshold=12, edgeThreshold=40)
+
+
+def test_degenerate_inputs():
+    import sfmx
+    assert len(_check(np.zeros((40, 40), np.uint8))[0]) == 0         # below 2 x edgeThreshold
+    assert len(_check(sift_cases.blob_image(200, 200, seed=5), nfeatures=0)[0]) == 0   # retainBest(0) clears
+    assert len(_check(np.full((100, 100), 7, np.uint8))[0]) == 0     # no corners
+    with pytest.raises(ValueError):                                  # SFMX_EINVAL
+        sfmx.features.ORB.create(100, WTA_K=3).detectAndCompute(np.zeros((64, 64), np.uint8))
+
+
+def test_device_and_batch_modes_match():
+    import torch
+    import sfmx
+    imgs = [_insel(i) for i in (1, 2, 3)] + [sift_cases.blob_image(300, 500, n_blobs=150, seed=9, noise=5.0)]
+    orb = sfmx.features.ORB.create(30000)
+    ref = [orb.detectAndCompute(im) for im in imgs]
+    got = orb.detectAndCompute_batch(imgs, n_streams=3)
+    for (k0, d0), (k1, d1) in zip(ref, got):
+        assert k0.tobytes() == k1.tobytes() and np.array_equal(d0, d1)
+    t = torch.from_numpy(imgs[0]).cuda()
+    kt = torch.zeros((1 << 15, 7), dtype=torch.int32, device="cuda")
+    dt = torch.zeros((1 << 15, 32), dtype=torch.uint8, device="cuda")
+    n = orb.detectAndCompute_device(t, kt, dt)
+    torch.cuda.synchronize()
+    assert n == len(ref[0][0])
+    assert kt[:n].cpu().numpy().tobytes() == ref[0][0].tobytes()
+    assert np.array_equal(dt[:n].cpu().numpy(), ref[0][1])

@@ -1,0 +1,159 @@
+"""CPU: the ORB restatement (oracle/orb_oracle.cpp) cross-checked stage by stage
+against a second, independent numpy restatement of the same OpenCV 4.5.1 pieces
+(OpenCV itself is absent, so parity with it is unpinned -- see DESIGN.md):
+
+  pyramid   level sizes cvRound(cols * (1 / scale)) and resize(INTER_LINEAR_EXACT)
+            as the closed-form 8.8 fixed-point formula
+  FAST      score = max(threshold, best 9-arc min |difference|) - 1 for corners
+            (the quantity cornerScore<16> computes), 0 elsewhere
+  blur      7x7 integer Gaussian (getGaussianKernel(7, 2) x 256 taps), reflect-101
+and end-to-end invariants of orb(): border, counts, octave/size consistency,
+determinism, and the rBRIEF table's provenance."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+import sift_cases
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RING = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3),
+        (0, -3), (-1, -3), (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+
+
+def level_sizes(W, H, n=8, sf=1.2):
+    out = []
+    for l in range(n):
+        s = np.float32(np.float64(np.float32(sf)) ** l)
+        inv = np.float32(1.0) / s
+        out.append((int(np.rint(np.float32(W) * inv)), int(np.rint(np.float32(H) * inv))))
+    return out
+
+
+def axis(dsize, ssize):
+    scale = 1.0 / (dsize / ssize)
+    fval = scale * (np.arange(dsize) + 0.5) - 0.5
+    ival = np.floor(fval).astype(np.int64)
+    m1 = np.rint((fval - ival) * 256).astype(np.int64)
+    lo = ival < 0
+    hi = ival >= ssize - 1
+    ofs = np.clip(ival, 0, ssize - 2)
+    return ofs, 256 - m1, m1, lo, hi
+
+
+def resize_exact(src, dw, dh):
+    sh, sw = src.shape
+    s = src.astype(np.int64)
+    xo, xm0, xm1, xlo, xhi = axis(dw, sw)
+    h = xm0 * s[:, xo] + xm1 * s[:, xo + 1]
+    h[:, xlo] = s[:, :1] << 8
+    h[:, xhi] = s[:, -1:] << 8
+    yo, ym0, ym1, ylo, yhi = axis(dh, sh)
+    v = (h[yo] * ym0[:, None] + h[yo + 1] * ym1[:, None] + 32768) >> 16
+    v[ylo] = (h[0] + 128) >> 8
+    v[yhi] = (h[-1] + 128) >> 8
+    return np.clip(v, 0, 255).astype(np.uint8)
+
+
+def fast_scores(img, thr=20):
+    H, W = img.shape
+    v = img.astype(np.int64)
+    out = np.zeros((H, W), np.uint8)
+    if H < 7 or W < 7:
+        return out
+    c = v[3:H - 3, 3:W - 3]
+    ring = np.stack([v[3 + dy:H - 3 + dy, 3 + dx:W - 3 + dx] for dx, dy in RING])       # 16 x h x w
+    d = c[None] - ring                                                                # center - neighbour
+    best_dark = np.full(c.shape, -10 ** 9)
+    best_bright = np.full(c.shape, -10 ** 9)
+    for k in range(16):
+        arc = [(k + j) % 16 for j in range(9)]
+        best_dark = np.maximum(best_dark, d[arc].min(0))
+        best_bright = np.maximum(best_bright, (-d[arc]).min(0))
+    corner = (best_dark > thr) | (best_bright > thr)
+    score = np.maximum(thr, np.maximum(best_dark, best_bright)) - 1
+    out[3:H - 3, 3:W - 3] = np.where(corner, score, 0)
+    return out
+
+
+def blur7(img):
+    n, sigma = 7, 2.0
+    t = [math.exp((x * x) * (-0.125 / (sigma * sigma))) for x in range(1 - n, 0, 2)]
+    s = 2 * sum(t) + 1.0
+    k = [float(np.float32(v / s)) for v in t + [1.0]]
+    taps = [int(np.rint(v * 256)) for v in k]
+    taps = taps + taps[-2::-1]
+    p = np.pad(img.astype(np.int64), 3, mode="reflect")                               # numpy reflect = reflect-101
+    H, W = img.shape
+    r = sum(taps[j] * p[:, j:j + W] for j in range(7))
+    c = sum(taps[j] * r[j:j + H, :] for j in range(7))
+    return np.clip((c + (1 << 15)) >> 16, 0, 255).astype(np.uint8)
+
+
+IMGS = [sift_cases.blob_image(97, 131, n_blobs=60, seed=2, noise=6.0),
+        sift_cases.blob_image(160, 213, n_blobs=90, seed=3, noise=4.0),
+        np.tile(np.arange(256, dtype=np.uint8), (70, 1))[:, :203]]
+
+
+@pytest.mark.parametrize("img", IMGS, ids=["97x131", "160x213", "ramp"])
+def test_pyramid_matches_numpy(img):
+    lv = oracle.orb_stage(img, 0)
+    sizes = level_sizes(img.shape[1], img.shape[0])
+    assert [(l.shape[1], l.shape[0]) for l in lv] == sizes
+    assert np.array_equal(lv[0], img)
+    for l in range(1, 8):
+        assert np.array_equal(lv[l], resize_exact(lv[l - 1], *sizes[l])), l
+
+
+@pytest.mark.parametrize("img", IMGS, ids=["97x131", "160x213", "ramp"])
+def test_fast_scores_match_numpy(img):
+    lv = oracle.orb_stage(img, 0)
+    sc = oracle.orb_stage(img, 1)
+    for a, b in zip(lv, sc):
+        assert np.array_equal(b, fast_scores(a))
+
+
+@pytest.mark.parametrize("img", IMGS, ids=["97x131", "160x213", "ramp"])
+def test_blur_matches_numpy(img):
+    lv = oracle.orb_stage(img, 0)
+    bl = oracle.orb_stage(img, 2)
+    for a, b in zip(lv, bl):
+        assert np.array_equal(b, blur7(a))
+
+
+def test_blur_taps_sum_and_constant_image():
+    # the x256 taps (18, 34, 49, 55, 49, 34, 18) sum to 257: a flat level brightens by (257/256)^2
+    v = (100 * 257 * 257 + (1 << 15)) >> 16
+    assert v == 101
+    assert np.array_equal(blur7(np.full((9, 9), 100, np.uint8)), np.full((9, 9), v, np.uint8))
+    assert np.array_equal(oracle.orb_stage(np.full((80, 90), 100, np.uint8), 2)[0], np.full((80, 90), v, np.uint8))
+    b = oracle.orb_stage(np.full((80, 90), 255, np.uint8), 2)
+    assert all((x == 255).all() for x in b)                                           # saturate_cast at 255
+
+
+@pytest.mark.parametrize("nf", [500, 50, 3])
+def test_orb_invariants(nf):
+    img = sift_cases.blob_image(300, 400, n_blobs=200, seed=7, noise=6.0)
+    k, d = oracle.orb(img, nfeatures=nf)
+    assert len(k) >= min(nf, 1) and d.shape == (len(k), 32)
+    x, y = np.rint(k["x"]), np.rint(k["y"])
+    assert ((x >= 31) & (x < 400 - 31) & (y >= 31) & (y < 300 - 31)).all()
+    s = np.float32(1.2) ** k["octave"].astype(np.float64)
+    assert np.allclose(k["size"], 31 * s.astype(np.float32), rtol=1e-6)
+    assert (k["class_id"] == -1).all() and ((k["angle"] >= 0) & (k["angle"] <= 360)).all()
+    assert (np.diff(k["octave"]) >= 0).all()                                           # levels concatenated in order
+    k2, d2 = oracle.orb(img, nfeatures=nf)
+    assert k.tobytes() == k2.tobytes() and np.array_equal(d, d2)
+
+
+def test_pattern_table_provenance():
+    """csrc/orb_pattern.inc (tools/gen_orb_pattern.py) holds ORB's published 31x31 rBRIEF
+    table: 256 pairs inside the patch, starting with the well-known first rows."""
+    inc = "".join(l for l in open(os.path.join(REPO, "sfm-mvs-pipeline_amd", "csrc", "orb_pattern.inc"))
+                  if not l.lstrip().startswith("//"))
+    vals = [int(v) for v in inc.replace(",", " ").split() if v.lstrip("-").isdigit()]
+    assert len(vals) == 1024
+    assert vals[:8] == [8, -3, 9, 5, 4, 2, 7, -12]
+    assert max(abs(v) for v in vals) <= 13
