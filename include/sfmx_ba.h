@@ -117,6 +117,21 @@ int sfmx_ba_destroy(sfmx_ba_ctx* ctx);
 int sfmx_ba_jacobian(const sfmx_ba_problem* problem, int32_t device, double* r, double* Je, double* Jc,
                      double* Ji);
 
+/* The factorization plan of the reduced camera system (host only, no device work): for a
+ * camera co-visibility graph adj (n_cams x n_cams, row-major, nonzero = the two cameras share a
+ * point) the ordering and level schedule the solver uses (SFMX_BA_ORDER in the solver):
+ * order -1 automatic (latency model), 0 natural, 1 nested dissection, 2/3/4 nested dissection
+ * with leaves of 1/2/4 tiles.  Optional outputs: camrow[n_cams] (first row of each camera's 6
+ * in S_cc), leaves[info.leaves], tasks[6 * info.tasks] rows (level, a, b, invert, s0, s1: tile
+ * (a, b) updated from the panels src[s0 .. s1), then inverted if `invert`), src[info.src].
+ * Returns SFMX_ECAPACITY (info filled) when a capacity is short.  The tiles are 64 x 64. */
+typedef struct sfmx_ba_plan_info {
+    int32_t order, leaf_tiles, npad, tiles, tiles_nz, height, leaves, tasks, src;
+    double predicted_us;
+} sfmx_ba_plan_info;
+int sfmx_ba_plan(int32_t n_cams, const uint8_t* adj, int32_t order, sfmx_ba_plan_info* info, int32_t* camrow,
+                 int32_t* leaves, int32_t leaves_cap, int32_t* tasks, int32_t tasks_cap, int32_t* src, int32_t src_cap);
+
 /* Pose conversions of CeresUtils (util/CeresUtils.h:90-148): 3x4 [R|t]
  * row-major <-> Ceres pose {angle-axis, t}, via ceres::RotationMatrixToAngleAxis /
  * AngleAxisToRotationMatrix semantics.  Host-side. */

@@ -1,0 +1,441 @@
+// SPDX-License-Identifier: MIT
+// sfmx bundle adjustment — solve of the reduced camera system on gfx950 (fp64 matrix cores).
+//
+// Ceres DENSE_SCHUR (CeresUtils.cpp:43-50) solves  [S_cc B; B^T D] [x_c; x_i] = [r_c; r_i]  with
+// one dense LLT, the shared intrinsics block (k unknowns) last.  Here the same system is solved as
+// a bordered one, in the order the factorization plan (ba_plan.hpp) gives:
+//   * S_cc (6C camera rows, nested-dissection order, identity padding rows) by block LDL^T on 64x64
+//     tiles, S_cc = L~ D~ L~^T, L~_ak = A_ak W_k, W_k = D~_k^-1, level by level (one launch per
+//     level of the tile elimination tree, one workgroup per destination tile);
+//   * the forward solve rides along with k + 1 right-hand sides R = [B | r_c]: y_a = R_a - sum
+//     A_ak w_k, w_a = W_a y_a (RW = k + 1 columns);
+//   * the intrinsics Schur complement D' = D - B^T S_cc^-1 B = D - sum_a y_a(B)^T w_a(B) and
+//     r' = r_i - sum_a y_a(B)^T w_a(r_c) are summed per panel (fixed panel order), D' is factored
+//     (k x k Cholesky) and x_i = D'^-1 r';
+//   * back solve L~^T x_c = w(r_c) - w(B) x_i, level by level from the root.
+// A non-positive pivot of any D~_k (scalar Cholesky pivots of the symmetric sweeps) or of D' is
+// where Eigen's LLT on the whole matrix fails (in exact arithmetic the same condition: S is
+// positive definite iff S_cc and D' are); LM treats it as an invalid step.
+//
+// Storage (SR buffer, row-major): S_cc npad x npad | R npad x RW | D k x k | r_i k.
+//   lower tiles (a, b), a > b : A, updated in place until consumed
+//   upper tile (k, a), a > k  : L~_ak^T (for the back solve)
+//   W[k] (one 64x64 tile per panel), contrib[k] (k x RW per panel)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ba_kernels.hpp"
+
+namespace sfmx {
+namespace ba {
+
+constexpr int LDT = NB + 2;   // LDS row stride (doubles): 16-B aligned rows
+// 64x64 fp64 tiles on the matrix cores (layout: f64x4 / trow / tcol in ba_kernels.hpp).  Wave w of a
+// 256-thread block owns the row strip 16w..16w+15 and four 16x16 column tiles.
+
+__device__ __forceinline__ void tile_load(double (*dst)[LDT], const double* __restrict__ src, int ld) {
+#pragma unroll
+    for (int q = 0; q < NB * NB / 512; ++q) {
+        const int e = q * 512 + 2 * threadIdx.x;
+        *reinterpret_cast<double2*>(&dst[e / NB][e % NB]) = *reinterpret_cast<const double2*>(src + (size_t)(e / NB) * ld + e % NB);
+    }
+}
+__device__ __forceinline__ void tile_regs(f64x4 (&t)[4], const double* __restrict__ src, int ld) {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[c][r] = src[(size_t)(16 * w + trow(r)) * ld + 16 * c + tcol()];
+}
+__device__ __forceinline__ void tile_store(const f64x4 (&t)[4], double* __restrict__ dst, int ld) {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[(size_t)(16 * w + trow(r)) * ld + 16 * c + tcol()] = t[c][r];
+}
+
+// acc[c] = A[strip] * B          (A, B row-major 64x64 in LDS)
+__device__ __forceinline__ void mfma_nn(const double (*A)[LDT], const double (*B)[LDT], f64x4 acc[4]) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, m = l & 15, kq = l >> 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int st = 0; st < NB / 4; ++st) {
+        const double av = A[16 * w + m][4 * st + kq];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, B[4 * st + kq][16 * c + m], acc[c], 0, 0, 0);
+    }
+}
+// acc[c] = A[strip] * X^T        (A, X row-major 64x64 in LDS)
+__device__ __forceinline__ void mfma_nt(const double (*A)[LDT], const double (*X)[LDT], f64x4 acc[4]) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, m = l & 15, kq = l >> 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int st = 0; st < NB / 4; ++st) {
+        const double av = A[16 * w + m][4 * st + kq];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, X[16 * c + m][4 * st + kq], acc[c], 0, 0, 0);
+    }
+}
+
+// 1/d: hardware estimate + two Newton steps (within an ulp or so of the divide).
+__device__ __forceinline__ double rcp_nr(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+
+// W_k = D~_k^-1 by symmetric block sweeps.  Sweeping the pivot block B with
+// Q = A_BB^-1:  a_il -= A_iB Q A_Bl (i, l not in B), A_iB <- A_iB Q,
+// A_Bl <- Q A_Bl, A_BB <- -Q; after all blocks the tile holds -A^-1.
+// Two levels (256 threads, the tile in registers in the MFMA layout above):
+//   outer: 4 sweeps of 16-wide pivot blocks — the column panel A_:B goes
+//          through LDS; M = A_:B Q (per wave, its own strip) and the rank-16
+//          update of the other column tiles run on the fp64 matrix cores;
+//   inner: Qn = -A_BB^-1 (16x16) by wave 0 alone (no barriers): 8 sweeps of
+//          2x2 pivot blocks, each lane holding a 2x2 block; the 2x2 pivot
+//          inverse is closed-form and its two scalar pivots (a, det/a) are the
+//          scalar Cholesky pivots, i.e. exactly where LLT would fail.
+constexpr int LDP = 18;   // LDS row stride of the 16-wide panels (16-B aligned rows)
+#ifdef SFMX_CHOL_STAMPS   // tools/micro/chol_tile.hip: phase timestamps of block 0 (never in the product build)
+__device__ long long g_chol_stamps[64];
+#define CHOL_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_chol_stamps[i] = wall_clock64(); } while (0)
+#else
+#define CHOL_STAMP(i) do { } while (0)
+#endif
+
+__device__ __forceinline__ void inner_inverse16(const double* __restrict__ Pc, int s, double* __restrict__ Qn,
+                                                double* __restrict__ ipan, bool& bad) {
+    // wave 0 only: Qn = -(Pc[16s + i][j])^-1, i, j < 16
+    const int lane = threadIdx.x & 63, r = lane >> 3, c = lane & 7;
+    double p[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int w = 0; w < 2; ++w) p[u][w] = Pc[(16 * s + 2 * r + u) * LDP + 2 * c + w];
+    for (int j = 0; j < 8; ++j) {
+        if (c == j) {   // column panel of the pivot block: rows 2r.., cols 2j..
+            *reinterpret_cast<double2*>(&ipan[(2 * r) * 2]) = make_double2(p[0][0], p[0][1]);
+            *reinterpret_cast<double2*>(&ipan[(2 * r + 1) * 2]) = make_double2(p[1][0], p[1][1]);
+        }
+        __builtin_amdgcn_wave_barrier();
+        const double2 b0 = *reinterpret_cast<const double2*>(&ipan[(2 * j) * 2]);
+        const double2 b1 = *reinterpret_cast<const double2*>(&ipan[(2 * j + 1) * 2]);
+        const double2 i0 = *reinterpret_cast<const double2*>(&ipan[(2 * r) * 2]);
+        const double2 i1 = *reinterpret_cast<const double2*>(&ipan[(2 * r + 1) * 2]);
+        const double2 l0 = *reinterpret_cast<const double2*>(&ipan[(2 * c) * 2]);
+        const double2 l1 = *reinterpret_cast<const double2*>(&ipan[(2 * c + 1) * 2]);
+        __builtin_amdgcn_wave_barrier();
+        // q = -[a b; b d]^-1
+        const double a = b0.x, bb = b0.y, d = b1.y;
+        double det = fma(a, d, -bb * bb);
+        if (!(a > 0.0) || !isfinite(a) || !(det > 0.0) || !isfinite(det)) { bad = true; det = 1.0; }
+        const double rd = rcp_nr(det);
+        const double q00 = -d * rd, q01 = bb * rd, q11 = -a * rd;   // q10 = q01
+        const bool rowB = (r == j), colB = (c == j);
+        double m[2][2];
+        {
+            const double ai[2][2] = {{i0.x, i0.y}, {i1.x, i1.y}};
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const double v0 = -(ai[u][0] * q00 + ai[u][1] * q01), v1 = -(ai[u][0] * q01 + ai[u][1] * q11);
+                m[u][0] = rowB ? (u == 0 ? q00 : q01) : v0;
+                m[u][1] = rowB ? (u == 0 ? q01 : q11) : v1;
+            }
+        }
+        const double al[2][2] = {{l0.x, l0.y}, {l1.x, l1.y}};   // al[w][b] = A_(2c+w),(2j+b) = A_Bl[b][w]
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                if (colB) p[u][w] = m[u][w];
+                else p[u][w] = (rowB ? 0.0 : p[u][w]) - (m[u][0] * al[w][0] + m[u][1] * al[w][1]);
+            }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int w = 0; w < 2; ++w) Qn[(2 * r + u) * LDP + 2 * c + w] = p[u][w];
+}
+
+// The inverse of the (final) diagonal tile k held in registers t (MFMA layout) -> W_k (global)
+// and buf (LDS); then w_k = W_k y_k for the RW right-hand sides (y: LDS [NB][RW] -> R rows of
+// tile k) and the panel's intrinsics Schur terms contrib_k[i][j] = sum_r y[r][i] w[r][j] (i < RW-1).
+// buf: 64 x LDT doubles of LDS workspace; wv: NB x RW doubles of LDS.
+template <int RW>
+__device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __restrict__ Wk,
+                                               double* __restrict__ R, const double* __restrict__ y,
+                                               double* __restrict__ wv, double* __restrict__ contrib,
+                                               int* __restrict__ fail, double (*buf)[LDT]) {
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, m = l & 15, kq = l >> 4, k0 = k * NB;
+    double* ws = &buf[0][0];
+    double* Pc = ws;                       // [64][LDP]  column panel A_:B
+    double* Qn = ws + NB * LDP;            // [16][LDP]  -A_BB^-1
+    double* ipan = Qn + 16 * LDP;          // [16][2]    inner column panel
+    double* Mw = ipan + 32 + 16 * LDP * w; // [16][LDP]  this wave's -M strip
+    CHOL_STAMP(0);
+    bool bad = false;
+    CHOL_STAMP(1);
+#pragma unroll
+    for (int s = 0; s < NB / 16; ++s) {
+        const bool rowB = (w == s);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Pc[(16 * w + trow(r)) * LDP + tcol()] = t[s][r];
+        __syncthreads();
+        CHOL_STAMP(2 + 4 * s);
+        if (tid < 64) inner_inverse16(Pc, s, Qn, ipan, bad);
+        __syncthreads();
+        CHOL_STAMP(3 + 4 * s);
+        // M = A_(strip),B Q on the matrix cores; rows in B take Q itself (-Qn)
+        f64x4 mm = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+            mm = __builtin_amdgcn_mfma_f64_16x16x4f64(Pc[(16 * w + m) * LDP + 4 * st + kq], Qn[(4 * st + kq) * LDP + m], mm, 0, 0, 0);
+        f64x4 mv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mv[r] = rowB ? Qn[trow(r) * LDP + tcol()] : -mm[r];   // M (Qn = -Q)
+        t[s] = mv;                                                         // A_iB <- A_iB Q, A_BB <- -Q
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Mw[trow(r) * LDP + tcol()] = -mv[r];   // -M as the A operand
+        __builtin_amdgcn_wave_barrier();
+        CHOL_STAMP(4 + 4 * s);
+        // a_il -= M[i][:] A_l,B for the other column tiles (rows in B start from 0)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (c == s) continue;
+            f64x4 acc = rowB ? f64x4{0.0, 0.0, 0.0, 0.0} : t[c];
+#pragma unroll
+            for (int st = 0; st < 4; ++st)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Mw[m * LDP + 4 * st + kq], Pc[(16 * c + m) * LDP + 4 * st + kq], acc, 0, 0, 0);
+            t[c] = acc;
+        }
+        __syncthreads();   // Pc is rewritten by the next sweep
+        CHOL_STAMP(5 + 4 * s);
+    }
+    if (bad) atomicOr(fail, 1);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 16 * w + trow(r), j = 16 * c + tcol();
+            buf[i][j] = -t[c][r];
+            Wk[i * NB + j] = -t[c][r];
+        }
+    __syncthreads();
+    CHOL_STAMP(20);
+    {   // w = W y: NB x RW outputs, TPO threads per output (fixed-order shuffle combine)
+        constexpr int TPO = (256 / (NB * RW)) > 0 ? 256 / (NB * RW) : 1;
+        constexpr int OPT = (NB * RW) / (256 / TPO);
+        const int part = tid % TPO;
+#pragma unroll
+        for (int u = 0; u < OPT; ++u) {
+            const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+            double sum = 0.0;
+            for (int c = part; c < NB; c += TPO) sum = fma(buf[i][c], y[c * RW + q], sum);
+            if (TPO >= 2) sum += __shfl_xor(sum, 1);
+            if (TPO >= 4) sum += __shfl_xor(sum, 2);
+            if (part == 0) { wv[i * RW + q] = sum; R[(size_t)(k0 + i) * RW + q] = sum; }
+        }
+    }
+    __syncthreads();
+    if (tid < (RW - 1) * RW) {   // contrib_k[i][j] = sum_r y[r][i] w[r][j]
+        const int i = tid / RW, j = tid % RW;
+        double s = 0.0;
+        for (int r = 0; r < NB; ++r) s = fma(y[r * RW + i], wv[r * RW + j], s);
+        contrib[(size_t)k * (RW - 1) * RW + tid] = s;
+    }
+    CHOL_STAMP(21);
+}
+
+template <int RW>
+struct alignas(16) CholLds {
+    double a[NB][LDT], m[NB][LDT], n[NB][LDT];
+    double rk[NB * RW], ra[NB * RW], wv[NB * RW];   // w_k of a source panel; y_a; w_a
+};
+
+// launch 0: the diagonal tiles of the level-0 panels (untouched by any update) -> W_k, w_k, contrib_k
+template <int RW>
+__global__ __launch_bounds__(256)
+void chol_leaves(double* __restrict__ S, int npad, double* __restrict__ R, const int* __restrict__ leaves,
+                 double* __restrict__ W, double* __restrict__ contrib, int* __restrict__ fail) {
+    __shared__ CholLds<RW> sm;
+    const int k = leaves[blockIdx.x], k0 = k * NB;
+    f64x4 t[4];
+    tile_regs(t, S + (size_t)k0 * npad + k0, npad);
+    for (int e = threadIdx.x; e < NB * RW; e += 256) sm.ra[e] = R[(size_t)k0 * RW + e];
+    __syncthreads();
+    chol_diag_tile<RW>(t, k, W + (size_t)k * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a);
+}
+
+// launch l + 1: one workgroup per destination tile (a, b) of level l's updates, its source panels
+// k = src[s0 .. s1) in ascending order:
+//   G = A_ak W_k;  A_ab -= G A_bk^T  (b == a: A_aa -= G A_ak^T, G^T -> upper tile (k, a), y_a -= A_ak w_k)
+// The first ninv workgroups hold diagonal tiles whose last update this is: they invert it.
+template <int RW>
+__global__ __launch_bounds__(256)
+void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
+                const int* __restrict__ src, int ninv, double* __restrict__ W, double* __restrict__ contrib,
+                int* __restrict__ fail) {
+    __shared__ CholLds<RW> sm;
+    const int tid = threadIdx.x, w = tid >> 6;
+    const int4 task = tasks[blockIdx.x];
+    const int a = task.x, b = task.y, a0 = a * NB, b0 = b * NB;
+    const bool diag = (a == b);
+    CHOL_STAMP(30);
+    f64x4 t[4];
+    double* dst = S + (size_t)a0 * npad + b0;
+    tile_regs(t, dst, npad);                                                   // A_ab (prefetch)
+    if (diag)
+        for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = R[(size_t)a0 * RW + e];
+    for (int s = task.z; s < task.w; ++s) {
+        const int k = src[s], k0 = k * NB;
+        tile_load(sm.a, S + (size_t)a0 * npad + k0, npad);                     // A_ak
+        tile_load(sm.m, W + (size_t)k * NB * NB, NB);                          // W_k
+        if (!diag) tile_load(sm.n, S + (size_t)b0 * npad + k0, npad);          // A_bk
+        else
+            for (int e = tid; e < NB * RW; e += 256) sm.rk[e] = R[(size_t)k0 * RW + e];   // w_k
+        __syncthreads();
+        CHOL_STAMP(31);
+        f64x4 g[4];
+        mfma_nn(sm.a, sm.m, g);   // G = A_ak W_k
+        __syncthreads();
+        CHOL_STAMP(32);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sm.m[16 * w + trow(r)][16 * c + tcol()] = g[c][r];
+        __syncthreads();
+        f64x4 upd[4];
+        mfma_nt(sm.m, diag ? sm.a : sm.n, upd);   // G X^T
+#pragma unroll
+        for (int c = 0; c < 4; ++c) t[c] -= upd[c];
+        CHOL_STAMP(33);
+        if (diag) {
+            // y_a -= A_ak w_k: NB x RW outputs, 256 / RW ... threads; 4 lanes per output for RW <= 4
+            constexpr int TPO = (256 / (NB * RW)) > 0 ? 256 / (NB * RW) : 1;
+            constexpr int OPT = (NB * RW) / (256 / TPO);
+            const int part = tid % TPO;
+#pragma unroll
+            for (int u = 0; u < OPT; ++u) {
+                const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+                double sum = 0.0;
+                for (int c = part; c < NB; c += TPO) sum = fma(sm.a[i][c], sm.rk[c * RW + q], sum);
+                if (TPO >= 2) sum += __shfl_xor(sum, 1);
+                if (TPO >= 4) sum += __shfl_xor(sum, 2);
+                if (part == 0) sm.ra[i * RW + q] -= sum;
+            }
+            // upper tile (k, a): row k0 + j, column a0 + i holds G[i][j]
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) S[(size_t)(k0 + 16 * c + tcol()) * npad + a0 + 16 * w + trow(r)] = g[c][r];
+        }
+        __syncthreads();   // the next source panel overwrites sm
+    }
+    if (diag && (int)blockIdx.x < ninv) {
+        chol_diag_tile<RW>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n);
+    } else {
+        tile_store(t, dst, npad);
+        if (diag)
+            for (int e = tid; e < NB * RW; e += 256) R[(size_t)a0 * RW + e] = sm.ra[e];
+    }
+    CHOL_STAMP(34);
+}
+
+// The intrinsics (one workgroup of 64): D' = D - sum_k contrib_k[:, :K], r' = r_i - sum_k
+// contrib_k[:, K] (panel order), K x K Cholesky (non-positive pivot -> fail), x_i = D'^-1 r' ->
+// xi (device scalars for the back solve) and sol_i.
+template <int K>
+__global__ __launch_bounds__(64)
+void chol_intr(const double* __restrict__ Dm, const double* __restrict__ ri, const double* __restrict__ contrib,
+               int T, double* __restrict__ xi, double* __restrict__ sol_i, int* __restrict__ fail) {
+    constexpr int RW = K + 1;
+    __shared__ double Dp[K * RW];
+    const int t = threadIdx.x;
+    if (t < K * RW) {
+        const int i = t / RW, j = t % RW;
+        double s = j < K ? Dm[i * K + j] : ri[i];
+        for (int k = 0; k < T; ++k) s -= contrib[(size_t)k * K * RW + t];
+        Dp[t] = s;
+    }
+    __syncthreads();
+    if (t == 0) {
+        double L[K][K], v[K];
+        bool bad = false;
+        for (int j = 0; j < K; ++j) {   // lower Cholesky of D' (its lower triangle), Eigen LLT order
+            double d = Dp[j * RW + j];
+            for (int m = 0; m < j; ++m) d -= L[j][m] * L[j][m];
+            if (!(d > 0.0) || !isfinite(d)) { bad = true; d = 1.0; }
+            L[j][j] = sqrt(d);
+            for (int i = j + 1; i < K; ++i) {
+                double s = Dp[i * RW + j];
+                for (int m = 0; m < j; ++m) s -= L[i][m] * L[j][m];
+                L[i][j] = s / L[j][j];
+            }
+        }
+        for (int i = 0; i < K; ++i) {
+            double s = Dp[i * RW + K];
+            for (int m = 0; m < i; ++m) s -= L[i][m] * v[m];
+            v[i] = s / L[i][i];
+        }
+        for (int i = K - 1; i >= 0; --i) {
+            double s = v[i];
+            for (int m = i + 1; m < K; ++m) s -= L[m][i] * v[m];
+            v[i] = s / L[i][i];
+        }
+        if (bad) atomicOr(fail, 1);
+        for (int i = 0; i < K; ++i) { xi[i] = v[i]; sol_i[i] = v[i]; }
+    }
+}
+
+// Back solve in one workgroup of 1024: z = w(r_c) - w(B) x_i, then per level, from the root down,
+// z_i -= sum_k U(i, k) z_k over the ancestors k of panel i (upper tiles (i, k) = L~_ki^T); the
+// camera solution leaves through rowmap (natural order 6c + d).  z lives in LDS (npad <= 16384).
+template <int RW>
+__global__ __launch_bounds__(1024)
+void chol_back(const double* __restrict__ S, int npad, const double* __restrict__ R, const double* __restrict__ xi,
+               int height, const int* __restrict__ lvl_start, const int* __restrict__ lvl_panels,
+               const int* __restrict__ bs_start, const int* __restrict__ bs_k, const int* __restrict__ rowmap,
+               double* __restrict__ xout) {
+    extern __shared__ double z[];
+    const int tid = threadIdx.x;
+    double xv[RW - 1];
+#pragma unroll
+    for (int i = 0; i < RW - 1; ++i) xv[i] = xi[i];
+    for (int r = tid; r < npad; r += 1024) {
+        double s = R[(size_t)r * RW + RW - 1];
+#pragma unroll
+        for (int i = 0; i < RW - 1; ++i) s -= R[(size_t)r * RW + i] * xv[i];
+        z[r] = s;
+    }
+    __syncthreads();
+    for (int l = height - 1; l >= 0; --l) {
+        const int p0 = lvl_start[l], np = lvl_start[l + 1] - p0;
+        // items: (panel, row), 4 lanes per item, 256 items per pass
+        for (int it = tid >> 2; it < np * NB; it += 256) {
+            const int i = lvl_panels[p0 + it / NB], row = i * NB + it % NB, q = tid & 3;
+            double t = 0.0;
+            for (int e = bs_start[i]; e < bs_start[i + 1]; ++e) {
+                const int k0 = bs_k[e] * NB;
+                const double* U = S + (size_t)row * npad + k0;
+#pragma unroll
+                for (int m = 0; m < NB / 4; ++m) t = fma(U[4 * m + q], z[k0 + 4 * m + q], t);
+            }
+            t += __shfl_xor(t, 1);
+            t += __shfl_xor(t, 2);
+            if (q == 0) z[row] -= t;
+        }
+        __syncthreads();
+    }
+    for (int r = tid; r < npad; r += 1024) {
+        const int o = rowmap[r];
+        if (o >= 0) xout[o] = z[r];
+    }
+}
+
+}  // namespace ba
+}  // namespace sfmx

@@ -28,6 +28,7 @@
 //   ba_gschur    per-point E, M, t, H; the group's -sum H H^T block and -sum H t
 //   ba_assemble  one workgroup per block of S: sum over the groups that hold it, in group order
 //   ba_add_cam   + scaled C, D_f^2 and g_f (after any cross-rank all-reduce of S)
+//   (the solve of S itself: ba_chol.hpp, planned by ba_plan.hpp)
 //   ba_gupdate   back substitution, step, candidate points, model cost change, step norm
 //   ba_fstep     candidate cameras / intrinsics
 //   ba_finalize  the LM scalars of one step (one workgroup)
@@ -437,12 +438,13 @@ void ba_gschur(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const
 }
 
 // ---------------------------------------------------------------------------------------------
-// ba_assemble: one 64-thread workgroup per block of S, summing the group contributions in group
-// order (normal groups: their dense block; big groups: -H_a H_b^T from the stored H); writes S and
-// its transpose, and the rhs rows (pose-intr task: camera rows; intr task: intrinsics rows and the
-// padding).  S is zeroed before; C, D^2 and g_f are added by ba_add_cam.  Entries carry absolute
-// offsets (no dependent loads); the intrinsics block (every group) is a strided, fixed-order
-// wave reduction.
+// ba_assemble: one 64-thread workgroup per block of the reduced system, summing the group
+// contributions in group order (normal groups: their dense block; big groups: -H_a H_b^T from the
+// stored H).  Bordered layout (ba_chol.hpp): pose blocks into S_cc at the plan's camera rows (and
+// the transpose), pose-intrinsics blocks and the camera rhs into R = [B | r_c], the intrinsics
+// block and rhs into D / r_i.  Everything is zeroed before; C, D^2
+// and g_f are added by ba_add_cam (after any cross-rank all-reduce).  Entries carry absolute offsets (no dependent loads); the
+// intrinsics block (every group) is a strided, fixed-order wave reduction.
 __device__ __forceinline__ double aval(const AEnt& E, const double* __restrict__ sg, const double* __restrict__ hbig,
                                        int r, int c) {
     if (!E.big) return sg[E.b0 + (long long)r * E.dim + c];
@@ -456,32 +458,33 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 __global__ __launch_bounds__(64)
 void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents, const double* __restrict__ sg,
-                 const double* __restrict__ hbig, const double* __restrict__ rg, int C, int K, int nf, int npad,
-                 double* __restrict__ S, double* __restrict__ rhs) {
+                 const double* __restrict__ hbig, const double* __restrict__ rg, int K, const int* __restrict__ camrow,
+                 int npad, double* __restrict__ S, double* __restrict__ R, double* __restrict__ Dm,
+                 double* __restrict__ ri) {
     const ATask T = tasks[blockIdx.x];
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, RW = K + 1;
     if (T.type == 0) {
         if (t >= 36) return;
-        const int u = t / 6, w = t % 6;
+        const int u = t / 6, w = t % 6, ra = camrow[T.a], rb = camrow[T.b];
         double v = 0.0;
 #pragma unroll 4
         for (int e = T.l0; e < T.l1; ++e) v += aval(ents[e], sg, hbig, u, w);
-        S[(size_t)(6 * T.a + u) * npad + 6 * T.b + w] = v;
-        if (T.a != T.b) S[(size_t)(6 * T.b + w) * npad + 6 * T.a + u] = v;
+        S[(size_t)(ra + u) * npad + rb + w] = v;
+        if (T.a != T.b) S[(size_t)(rb + w) * npad + ra + u] = v;
     } else if (T.type == 1) {   // entries: b0 / b1 at the camera rows / the intrinsics rows of the group
-        if (t < 6 * K) {
+        const int ra = camrow[T.a];
+        if (t < 6 * K) {        // B (camera rows x intrinsics): the first K right-hand sides
             const int u = t / K, i = t % K;
             double v = 0.0;
 #pragma unroll 4
             for (int e = T.l0; e < T.l1; ++e) v += aval(ents[e], sg, hbig, u, i);
-            S[(size_t)(6 * T.a + u) * npad + 6 * C + i] = v;
-            S[(size_t)(6 * C + i) * npad + 6 * T.a + u] = v;
+            R[(size_t)(ra + u) * RW + i] = v;
         } else if (t < 6 * K + 6) {
             const int d = t - 6 * K;
             double v = 0.0;
 #pragma unroll 4
             for (int e = T.l0; e < T.l1; ++e) v += rg[ents[e].rg + d];
-            rhs[6 * T.a + d] = v;
+            R[(size_t)(ra + d) * RW + K] = v;
         }
     } else {                    // one intrinsics output x = T.b over every group; entries at the intrinsics rows
         const int x = T.b;
@@ -497,27 +500,27 @@ void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents,
         }
         const double v = wave_sum(v0 + v1);
         if (t == 0) {
-            if (x < K * K) S[(size_t)(6 * C + x / K) * npad + 6 * C + x % K] = v;
-            else rhs[6 * C + x - K * K] = v;
+            if (x < K * K) Dm[x] = v;
+            else ri[x - K * K] = v;
         }
-        if (x == 0)
-            for (int i = nf + t; i < npad; i += 64) { S[(size_t)i * npad + i] = 1.0; rhs[i] = 0.0; }
     }
 }
 
 // + the camera-camera part C of the scaled J^T J, D_f^2 and g_f: one workgroup per camera
-// (blockIdx.x < C) and one for the intrinsics.  camsum (per camera ncp(K) unscaled sums, then
-// the intrinsics K(K+1)/2 + K) is already summed over ranks.
+// (blockIdx.x < C) and one for the intrinsics and the identity padding rows of S_cc.  camsum (per
+// camera ncp(K) unscaled sums, then the intrinsics K(K+1)/2 + K) is already summed over ranks.
 template <int K>
 __global__ __launch_bounds__(64)
-void ba_add_cam(int P, int C, int npad, const double* __restrict__ camsum, const double* __restrict__ scale,
-                const double* __restrict__ colsq, double dmin, double dmax, double radius, double* __restrict__ S,
-                double* __restrict__ rhs) {
-    constexpr int NCP = ncp(K);
+void ba_add_cam(int P, int C, int npad, const int* __restrict__ camrow, const int* __restrict__ padrows,
+                int npadrows, const double* __restrict__ camsum,
+                const double* __restrict__ scale, const double* __restrict__ colsq, double dmin, double dmax,
+                double radius, double* __restrict__ S, double* __restrict__ R, double* __restrict__ Dm,
+                double* __restrict__ ri) {
+    constexpr int NCP = ncp(K), RW = K + 1;
     const size_t ne = 3 * (size_t)P, nfc = 6 * (size_t)C;
     const double* si = scale + ne + nfc;
     if ((int)blockIdx.x < C) {
-        const int c = blockIdx.x;
+        const int c = blockIdx.x, rc = camrow[c];
         const double* cs = camsum + (size_t)c * NCP;
         const double* sc = scale + ne + 6 * (size_t)c;
         for (int t = threadIdx.x; t < 42 + 6 * K; t += 64)
@@ -528,15 +531,13 @@ void ba_add_cam(int P, int C, int npad, const double* __restrict__ camsum, const
             e += b - a;
             double v = sc[u] * sc[w] * cs[e];
             if (u == w) v += dsq(colsq[ne + 6 * (size_t)c + u], sc[u], dmin, dmax, radius);
-            S[(6 * (size_t)c + u) * npad + 6 * c + w] += v;
+            S[(size_t)(rc + u) * npad + rc + w] += v;
         } else if (t < 36 + 6 * K) {
             const int x = t - 36, u = x / K, i = x % K;
-            const double v = sc[u] * si[i] * cs[cp_ci(K) + u * K + i];
-            S[(6 * (size_t)c + u) * npad + 6 * C + i] += v;
-            S[(nfc + i) * npad + 6 * c + u] += v;
+            R[(size_t)(rc + u) * RW + i] += sc[u] * si[i] * cs[cp_ci(K) + u * K + i];
         } else if (t < 42 + 6 * K) {
             const int u = t - 36 - 6 * K;
-            rhs[6 * c + u] += sc[u] * cs[cp_gc(K) + u];
+            R[(size_t)(rc + u) * RW + K] += sc[u] * cs[cp_gc(K) + u];
         }
     } else {
         const double* ii = camsum + (size_t)C * NCP;
@@ -548,12 +549,13 @@ void ba_add_cam(int P, int C, int npad, const double* __restrict__ camsum, const
                 e += b - a;
                 double v = si[i] * si[j] * ii[e];
                 if (i == j) v += dsq(colsq[ne + nfc + i], si[i], dmin, dmax, radius);
-                S[(nfc + i) * npad + nfc + j] += v;
+                Dm[x] += v;
             } else {
                 const int i = x - K * K;
-                rhs[nfc + i] += si[i] * ii[K * (K + 1) / 2 + i];
+                ri[i] += si[i] * ii[K * (K + 1) / 2 + i];
             }
         }
+        for (int i = threadIdx.x; i < npadrows; i += 64) S[(size_t)padrows[i] * npad + padrows[i]] = 1.0;
     }
 }
 
@@ -1024,34 +1026,6 @@ __global__ void ba_fstep(int nf, const double* __restrict__ sol_f, const double*
                          const double* __restrict__ x_f, double* __restrict__ cand_f) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nf) cand_f[i] = x_f[i] + (-sol_f[i]) * scale_f[i];
-}
-
-// Back substitution L~^T x = w over all panels in one workgroup (descending panels):
-// x_k = rhs_k is final; rows < k0 get rhs_i -= U(i, k) x_k (upper tiles hold L~^T).
-__global__ __launch_bounds__(256)
-void chol_back_all(const double* __restrict__ S, int npad, int nf, int T, const double* __restrict__ rhs_in,
-                   double* __restrict__ xout) {
-    __shared__ double r[16 * 1024];   // npad <= 16384 doubles (128 KB)
-    const int tid = threadIdx.x;
-    for (int i = tid; i < npad; i += 256) r[i] = rhs_in[i];
-    __syncthreads();
-    for (int k = T - 1; k >= 0; --k) {
-        const int k0 = k * NB;
-        for (int i = tid; i < NB; i += 256)
-            if (k0 + i < nf) xout[k0 + i] = r[k0 + i];
-        // rows [0, k0): 4 threads per row, 16 terms each
-        for (int rb = tid >> 2; rb < k0; rb += 64) {
-            const int qq = tid & 3;
-            const double* U = S + (size_t)rb * npad + k0;
-            double t = 0.0;
-#pragma unroll 4
-            for (int m = 0; m < NB / 4; ++m) t = fma(U[4 * m + qq], r[k0 + 4 * m + qq], t);
-            t += __shfl_xor(t, 1);
-            t += __shfl_xor(t, 2);
-            if (qq == 0) r[rb] -= t;
-        }
-        __syncthreads();
-    }
 }
 
 }  // namespace ba

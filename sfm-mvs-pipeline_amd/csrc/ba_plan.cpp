@@ -1,0 +1,330 @@
+// SPDX-License-Identifier: MIT
+// sfmx bundle adjustment — factorization plan (see ba_plan.hpp).
+#include "ba_plan.hpp"
+
+#include "../../include/sfmx.h"
+#include "../../include/sfmx_ba.h"
+#include "match_common.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <utility>
+
+namespace sfmx {
+namespace ba {
+namespace {
+
+constexpr int NBP = PLAN_NB;
+
+// ---- nested dissection of the camera graph ----------------------------------------------
+struct Nd {
+    const std::vector<std::vector<int>>& g;
+    int leaf;                       // cameras per leaf node
+    std::vector<int> in, seen, lvl, taken;
+    int epoch = 0, stamp = 0;
+    std::vector<std::vector<int>> nodes;   // children before their separator
+    Nd(const std::vector<std::vector<int>>& g_, int leaf_)
+        : g(g_), leaf(leaf_), in(g_.size(), 0), seen(g_.size(), 0), lvl(g_.size(), 0), taken(g_.size(), 0) {}
+
+    // BFS from root inside the current set (in == ep): level sets
+    void levels(int root, int ep, std::vector<std::vector<int>>& L) {
+        L.clear();
+        const int s = ++stamp;
+        seen[root] = s;
+        lvl[root] = 0;
+        L.push_back({root});
+        for (;;) {
+            std::vector<int> nx;
+            for (int v : L.back())
+                for (int w : g[v])
+                    if (in[w] == ep && seen[w] != s) { seen[w] = s; lvl[w] = (int)L.size(); nx.push_back(w); }
+            if (nx.empty()) break;
+            std::sort(nx.begin(), nx.end());
+            L.push_back(std::move(nx));
+        }
+    }
+    int degree(int v, int ep) const {
+        int d = 0;
+        for (int w : g[v]) d += in[w] == ep;
+        return d;
+    }
+    // lowest-index vertex of minimum degree in `vs`
+    int min_degree(const std::vector<int>& vs, int ep) const {
+        int best = vs[0], bd = degree(vs[0], ep);
+        for (int v : vs) { const int d = degree(v, ep); if (d < bd) { bd = d; best = v; } }
+        return best;
+    }
+
+    void rec(std::vector<int> verts) {
+        std::sort(verts.begin(), verts.end());
+        if ((int)verts.size() <= leaf) { nodes.push_back(verts); return; }
+        const int ep = ++epoch;
+        for (int v : verts) in[v] = ep;
+        {   // connected components (each dissected on its own, no separator between them)
+            std::vector<std::vector<int>> comps, L;
+            for (int v : verts) {
+                if (taken[v] == ep) continue;
+                levels(v, ep, L);
+                std::vector<int> comp;
+                for (const auto& l : L)
+                    for (int w : l) { taken[w] = ep; comp.push_back(w); }
+                comps.push_back(std::move(comp));
+            }
+            if (comps.size() > 1) {
+                for (auto& c : comps) rec(std::move(c));
+                return;
+            }
+        }
+        // pseudo-peripheral root: repeated BFS from the farthest minimum-degree vertex
+        std::vector<std::vector<int>> L;
+        int root = min_degree(verts, ep);
+        levels(root, ep, L);
+        for (int it = 0; it < 4; ++it) {
+            const int cand = min_degree(L.back(), ep);
+            std::vector<std::vector<int>> L2;
+            levels(cand, ep, L2);
+            if (L2.size() <= L.size()) break;
+            root = cand;
+            L.swap(L2);
+        }
+        levels(root, ep, L);   // leaves lvl[] of this BFS
+        const int h = (int)L.size(), n = (int)verts.size();
+        if (h < 3) { nodes.push_back(verts); return; }
+        // separator level: smallest level set among the balanced ones (each side >= n/4), ties to
+        // the most balanced; none balanced: the most balanced
+        int m = -1;
+        long best_sz = 0, best_im = 0;
+        int cum = 0;
+        std::vector<int> before(h, 0);
+        for (int i = 0; i < h; ++i) { before[i] = cum; cum += (int)L[i].size(); }
+        for (int i = 1; i + 1 < h; ++i) {
+            const int lo = before[i], hi = n - before[i] - (int)L[i].size();
+            if (4 * lo < n || 4 * hi < n) continue;
+            const long sz = (long)L[i].size(), im = std::labs((long)lo - hi);
+            if (m < 0 || sz < best_sz || (sz == best_sz && im < best_im)) { m = i; best_sz = sz; best_im = im; }
+        }
+        if (m < 0)
+            for (int i = 1; i + 1 < h; ++i) {
+                const long im = std::labs((long)before[i] - (n - before[i] - (long)L[i].size()));
+                if (m < 0 || im < best_im) { m = i; best_im = im; }
+            }
+        std::vector<int> left, right, sep;
+        for (int i = 0; i < m; ++i) left.insert(left.end(), L[i].begin(), L[i].end());
+        for (int i = m + 1; i < h; ++i) right.insert(right.end(), L[i].begin(), L[i].end());
+        for (int v : L[m]) {   // a separator vertex with no neighbour beyond it belongs to the near side
+            bool touches = false;
+            for (int w : g[v]) if (in[w] == ep && lvl[w] == m + 1) { touches = true; break; }
+            (touches ? sep : left).push_back(v);
+        }
+        rec(std::move(left));
+        rec(std::move(right));
+        std::sort(sep.begin(), sep.end());
+        if (!sep.empty()) nodes.push_back(std::move(sep));
+    }
+};
+
+// ---- layout, pattern, schedule ------------------------------------------------------------
+void layout(int C, const std::vector<std::vector<int>>& nodes, FactorPlan& P) {
+    P.camrow.assign(C, 0);
+    int row = 0;
+    const int nn = (int)nodes.size();
+    P.rowmap.clear();
+    P.padrows.clear();
+    for (int i = 0; i < nn; ++i) {
+        const int r0 = row;
+        const int used = 6 * (int)nodes[i].size();
+        for (size_t j = 0; j < nodes[i].size(); ++j) {
+            P.camrow[nodes[i][j]] = r0 + 6 * (int)j;
+            for (int d = 0; d < 6; ++d) P.rowmap.push_back(6 * nodes[i][j] + d);
+        }
+        const int span = std::max(1, (used + NBP - 1) / NBP) * NBP;
+        for (int r = used; r < span; ++r) { P.padrows.push_back(r0 + r); P.rowmap.push_back(-1); }
+        row = r0 + span;
+    }
+    if (nn == 0) {   // no cameras: one identity tile keeps the launch sequence well formed
+        for (int r = 0; r < NBP; ++r) { P.padrows.push_back(r); P.rowmap.push_back(-1); }
+        row = NBP;
+    }
+    P.npad = row;
+    P.T = row / NBP;
+}
+
+void pattern(const std::vector<char>& adj, FactorPlan& P) {
+    const int T = P.T, C = P.C;
+    std::vector<char>& nz = P.nz;
+    nz.assign((size_t)T * T, 0);
+    auto mark = [&](int r0, int r1, int c0, int c1) {   // rows [r0, r1) x cols [c0, c1), lower-normalised
+        for (int I = r0 / NBP; I <= (r1 - 1) / NBP; ++I)
+            for (int J = c0 / NBP; J <= (c1 - 1) / NBP; ++J) nz[(size_t)std::max(I, J) * T + std::min(I, J)] = 1;
+    };
+    for (int I = 0; I < T; ++I) nz[(size_t)I * T + I] = 1;
+    for (int a = 0; a < C; ++a) {
+        mark(P.camrow[a], P.camrow[a] + 6, P.camrow[a], P.camrow[a] + 6);
+        for (int b = a + 1; b < C; ++b)
+            if (adj[(size_t)a * C + b] || adj[(size_t)b * C + a]) mark(P.camrow[a], P.camrow[a] + 6, P.camrow[b], P.camrow[b] + 6);
+    }
+    // symbolic fill of the block factorization in tile order
+    for (int k = 0; k < T; ++k)
+        for (int a = k + 1; a < T; ++a)
+            if (nz[(size_t)a * T + k])
+                for (int b = k + 1; b <= a; ++b)
+                    if (nz[(size_t)b * T + k]) nz[(size_t)a * T + b] = 1;
+    P.tiles_nz = 0;
+    for (char v : nz) P.tiles_nz += v;
+}
+
+// latency model of one launch sequence (us): per launch its slowest task
+constexpr double LAT_LAUNCH = 6.0, LAT_LOAD = 2.5, LAT_UPD = 6.5, LAT_INV = 12.0;
+
+void schedule(FactorPlan& P) {
+    const int T = P.T;
+    const std::vector<char>& nz = P.nz;
+    P.parent.assign(T, -1);
+    P.level.assign(T, 0);
+    for (int k = 0; k < T; ++k) {
+        for (int a = k + 1; a < T; ++a)
+            if (nz[(size_t)a * T + k]) { P.parent[k] = a; break; }
+        if (P.parent[k] >= 0) P.level[P.parent[k]] = std::max(P.level[P.parent[k]], P.level[k] + 1);
+    }
+    P.height = 0;
+    for (int k = 0; k < T; ++k) P.height = std::max(P.height, P.level[k]);
+    P.leaves.clear();
+    for (int k = 0; k < T; ++k) if (P.level[k] == 0) P.leaves.push_back(k);
+    P.task_start.assign(1, 0);
+    P.ninv.clear();
+    P.tasks.clear();
+    P.src.clear();
+    P.predicted_us = LAT_LAUNCH + LAT_LOAD + LAT_INV;
+    for (int l = 0; l < P.height; ++l) {
+        std::map<std::pair<int, int>, std::vector<int>> dst;   // (a, b) -> source panels, ascending
+        for (int k = 0; k < T; ++k) {
+            if (P.level[k] != l) continue;
+            for (int a = k + 1; a < T; ++a) {
+                if (!nz[(size_t)a * T + k]) continue;
+                for (int b = k + 1; b <= a; ++b)
+                    if (nz[(size_t)b * T + k]) dst[{a, b}].push_back(k);
+            }
+        }
+        std::vector<PlanTask> inv, rest;
+        double worst = 0.0;
+        for (auto& kv : dst) {
+            const int a = kv.first.first, b = kv.first.second;
+            PlanTask t{a, b, (int)P.src.size(), 0};
+            P.src.insert(P.src.end(), kv.second.begin(), kv.second.end());
+            t.s1 = (int)P.src.size();
+            const bool iv = a == b && P.level[a] == l + 1;
+            (iv ? inv : rest).push_back(t);
+            worst = std::max(worst, LAT_LOAD + LAT_UPD * (double)kv.second.size() + (iv ? LAT_INV : 0.0));
+        }
+        P.ninv.push_back((int)inv.size());
+        P.tasks.insert(P.tasks.end(), inv.begin(), inv.end());
+        P.tasks.insert(P.tasks.end(), rest.begin(), rest.end());
+        P.task_start.push_back((int)P.tasks.size());
+        P.predicted_us += LAT_LAUNCH + worst;
+    }
+    // back solve: per panel i its ancestors' upper tiles (i, k), k > i with nz(k, i)
+    P.bs_start.assign(T + 1, 0);
+    P.bs_k.clear();
+    for (int i = 0; i < T; ++i) {
+        P.bs_start[i] = (int)P.bs_k.size();
+        for (int k = i + 1; k < T; ++k) if (nz[(size_t)k * T + i]) P.bs_k.push_back(k);
+    }
+    P.bs_start[T] = (int)P.bs_k.size();
+    P.lvl_start.assign(P.height + 2, 0);
+    P.lvl_panels.clear();
+    for (int l = 0; l <= P.height; ++l) {
+        P.lvl_start[l] = (int)P.lvl_panels.size();
+        for (int k = 0; k < T; ++k) if (P.level[k] == l) P.lvl_panels.push_back(k);
+    }
+    P.lvl_start[P.height + 1] = (int)P.lvl_panels.size();
+}
+
+void build(int C, const std::vector<char>& adj, const std::vector<std::vector<int>>& nodes, int order,
+           int leaf_tiles, FactorPlan& P) {
+    P = FactorPlan{};
+    P.C = C;
+    P.order = order;
+    P.leaf_tiles = leaf_tiles;
+    layout(C, nodes, P);
+    pattern(adj, P);
+    schedule(P);
+}
+
+}  // namespace
+
+void make_plan(int C, const std::vector<char>& adj, int order_mode, FactorPlan& out) {
+    std::vector<std::vector<int>> natural;
+    if (C > 0) {
+        natural.emplace_back(C);
+        for (int c = 0; c < C; ++c) natural[0][c] = c;
+    }
+    FactorPlan best;
+    build(C, adj, natural, 0, 0, best);
+    if (order_mode == 0 || C == 0) { out = std::move(best); return; }
+    std::vector<std::vector<int>> g(C);
+    for (int a = 0; a < C; ++a)
+        for (int b = 0; b < C; ++b)
+            if (a != b && (adj[(size_t)a * C + b] || adj[(size_t)b * C + a])) g[a].push_back(b);
+    const int leaves_all[3] = {1, 2, 4};
+    bool have_nd = false;
+    for (int li = 0; li < 3; ++li) {
+        const int lt = leaves_all[li];
+        if (order_mode >= 2 && order_mode - 1 != li + 1) continue;
+        Nd nd(g, std::max(1, lt * NBP / 6));
+        std::vector<int> all(C);
+        for (int c = 0; c < C; ++c) all[c] = c;
+        nd.rec(all);
+        FactorPlan p;
+        build(C, adj, nd.nodes, 1, lt, p);
+        const bool forced = order_mode >= 1;
+        if ((forced && !have_nd) || p.predicted_us < best.predicted_us ||
+            (p.predicted_us == best.predicted_us && p.T < best.T)) {
+            best = std::move(p);
+            have_nd = true;
+        }
+    }
+    out = std::move(best);
+}
+
+}  // namespace ba
+}  // namespace sfmx
+
+extern "C" int sfmx_ba_plan(int32_t n_cams, const uint8_t* adj, int32_t order, sfmx_ba_plan_info* info,
+                            int32_t* camrow, int32_t* leaves, int32_t leaves_cap, int32_t* tasks, int32_t tasks_cap,
+                            int32_t* src, int32_t src_cap) {
+    if (!info || n_cams < 0 || (n_cams > 0 && !adj) || order < -1 || order > 4) {
+        sfmx::set_last_error("sfmx_ba_plan: invalid arguments");
+        return SFMX_EINVAL;
+    }
+    const int C = n_cams;
+    std::vector<char> a((size_t)C * C);
+    for (size_t i = 0; i < a.size(); ++i) a[i] = adj[i] != 0;
+    sfmx::ba::FactorPlan p;
+    sfmx::ba::make_plan(C, a, order, p);
+    info->order = p.order;
+    info->leaf_tiles = p.leaf_tiles;
+    info->npad = p.npad;
+    info->tiles = p.T;
+    info->tiles_nz = p.tiles_nz;
+    info->height = p.height;
+    info->leaves = (int32_t)p.leaves.size();
+    info->tasks = (int32_t)p.tasks.size();
+    info->src = (int32_t)p.src.size();
+    info->predicted_us = p.predicted_us;
+    if (camrow) for (int c = 0; c < C; ++c) camrow[c] = p.camrow[c];
+    if ((leaves && leaves_cap < info->leaves) || (tasks && tasks_cap < info->tasks) || (src && src_cap < info->src)) {
+        sfmx::set_last_error("sfmx_ba_plan: output capacity too small");
+        return SFMX_ECAPACITY;
+    }
+    if (leaves) for (size_t i = 0; i < p.leaves.size(); ++i) leaves[i] = p.leaves[i];
+    if (src) for (size_t i = 0; i < p.src.size(); ++i) src[i] = p.src[i];
+    if (tasks)
+        for (int l = 0; l < p.height; ++l)
+            for (int t = p.task_start[l]; t < p.task_start[l + 1]; ++t) {
+                int32_t* r = tasks + 6 * (size_t)t;
+                r[0] = l; r[1] = p.tasks[t].a; r[2] = p.tasks[t].b; r[3] = t - p.task_start[l] < p.ninv[l];
+                r[4] = p.tasks[t].s0; r[5] = p.tasks[t].s1;
+            }
+    return SFMX_OK;
+}

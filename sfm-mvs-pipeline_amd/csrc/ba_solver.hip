@@ -11,11 +11,14 @@
 // The controller mirrors oracle/ba_oracle.cpp (the CPU restatement) step for step.
 //
 // Per LM step (try_step), in stream order:
-//   ba_gschur -> memset S -> ba_assemble -> [all-reduce S, rhs] -> ba_add_cam -> chol_first,
-//   chol_step x (T-1), chol_back_all -> ba_gupdate, ba_fstep -> ba_glin (the candidate,
-//   speculatively: its Jacobian is the next linearization if the step is accepted) -> ba_camred
-//   -> [all-reduce] -> ba_finalize -> [all-reduce scalars] -> one D2H of the scalars.
+//   ba_gschur -> memset S -> ba_assemble -> [all-reduce S, R, D, r_i] -> ba_add_cam -> chol_leaves,
+//   chol_level x height, chol_intr, chol_back (the plan's level schedule, ba_plan.hpp / ba_chol.hpp)
+//   -> ba_gupdate, ba_fstep -> ba_glin (the candidate, speculatively: its Jacobian is the next
+//   linearization if the step is accepted) -> ba_camred -> [all-reduce] -> ba_finalize ->
+//   [all-reduce scalars] -> one D2H of the scalars.
 #include "ba_group.hpp"
+#include "ba_chol.hpp"
+#include "ba_plan.hpp"
 
 #include <algorithm>
 #include <chrono>
@@ -62,6 +65,7 @@ struct Buf {
 };
 
 inline unsigned nblk(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
+constexpr int MAX_NPAD = 16 * 1024;   // rows of S_cc: the back solve keeps its vector in LDS
 
 }  // namespace
 
@@ -72,19 +76,23 @@ struct sfmx_ba_ctx {
     int P = 0, C = 0, O = 0, K = 0;
     double cx = 0, cy = 0;
     int64_t n = 0, ne = 0;
-    int nf = 0, npad = 0, T = 0;
+    int nf = 0, npad = 0, T = 0, RW = 0;
     sfmx_allreduce_fn ar = nullptr;
     void* ar_user = nullptr;
     // topology: groups, chunks, group cameras, local camera per observation, assembly tasks
     int ngroups = 0, ntasks = 0, nslots = 0, stage_n = 0;
     size_t lds_schur = 0, lds_lin = 0, lds_upd = 0;
-    Buf obs_point, obs_cam, obs_xy, pt_start, grp, chk, gcam, obs_lc, obs_row, lcrow, tasks, ents, cref_start, cref,
-        tl, ut_start, ut;
-    std::vector<int> tl_start;   // host copy: per panel k, the launch's task range
-    bool sparse = true;          // tile-sparse factorization (SFMX_BA_DENSE=1: dense, for A/B)
+    Buf obs_point, obs_cam, obs_xy, pt_start, grp, chk, gcam, obs_lc, obs_row, lcrow, tasks, ents, cref_start, cref;
+    // factorization plan of the reduced camera system (built at the first run, from the camera
+    // co-visibility of every rank: the layout of S must be the same on all of them)
+    std::vector<char> adj;       // local camera co-visibility, C x C
+    bool planned = false;
+    sfmx::ba::FactorPlan plan;
+    Buf camrow, padrows, rowmap, leaves, ptasks, psrc, lvl_start, lvl_panels, bs_start, bs_k, Wt, contrib, xi;
+    size_t sr_count = 0;         // doubles of SR = S_cc | R | D | r_i
     // state (the *2 buffers hold the candidate's linearization until the step is accepted)
     Buf x, cand, scale, colsq, colsq2, grad, grad2, J, J2, camsum, camsum2, plt, sg, rg, hbig, gpart, gpl, scal,
-        SR, Linv, sol, failf, partA;
+        SR, sol, failf, partA;
     bool scaled = false;
     // locality order: internal point p' is caller point pperm[p']; internal
     // observation o' is caller observation operm[o'] (point-major)
@@ -92,9 +100,11 @@ struct sfmx_ba_ctx {
     double phase_ms[4] = {0, 0, 0, 0};
     hipEvent_t ev[6] = {};
     ~sfmx_ba_ctx() {
-        Buf* all[] = {&tl, &ut_start, &ut, &obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &gcam, &obs_lc, &obs_row, &lcrow, &tasks, &ents, &cref_start,
-                      &cref, &x, &cand, &scale, &colsq, &colsq2, &grad, &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg,
-                      &rg, &hbig, &gpart, &gpl, &scal, &SR, &Linv, &sol, &failf, &partA};
+        Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
+                      &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
+                      &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &x, &cand, &scale, &colsq, &colsq2, &grad,
+                      &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
+                      &failf, &partA};
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
@@ -116,6 +126,13 @@ struct DeviceGuard {
 int allreduce(sfmx_ba_ctx* c, double* buf, int64_t count, int op) {
     if (!c->ar || count <= 0) return SFMX_OK;
     if (c->ar(buf, count, op, c->ar_user, (void*)c->st) != 0) return fail(SFMX_EDEVICE, "all-reduce callback failed");
+    return SFMX_OK;
+}
+
+template <class T>
+int upload(Buf& b, const std::vector<T>& v, hipStream_t st) {
+    RC(b.alloc(sizeof(T) * std::max<size_t>(v.size(), 1)));
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st));
     return SFMX_OK;
 }
 
@@ -171,12 +188,43 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double
 
 // One LM step at `radius`: Schur solve of (J_s^T J_s + D^2) sol = J_s^T r, step_s = -sol,
 // candidate = x + step_s * scale, its cost, Jacobian and scalars (speculative linearization).
+// The level-scheduled solve of the bordered reduced system (ba_chol.hpp) -> sol (natural order).
+template <int RW>
+int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
+    const sfmx::ba::FactorPlan& pl = c->plan;
+    const int npad = c->npad;
+    double* S = c->SR.as<double>();
+    double* R = S + (size_t)npad * npad;
+    double* Dm = R + (size_t)npad * RW;
+    double* ri = Dm + (RW - 1) * (RW - 1);
+    int* fl = c->failf.as<int>();
+    hipLaunchKernelGGL(chol_leaves<RW>, dim3((unsigned)pl.leaves.size()), dim3(256), 0, c->st, S, npad, R,
+                       c->leaves.as<int>(), c->Wt.as<double>(), c->contrib.as<double>(), fl);
+    for (int l = 0; l < pl.height; ++l) {
+        const int t0 = pl.task_start[l], nt = pl.task_start[l + 1] - t0;
+        hipLaunchKernelGGL(chol_level<RW>, dim3(nt), dim3(256), 0, c->st, S, npad, R, c->ptasks.as<int4>() + t0,
+                           c->psrc.as<int>(), pl.ninv[l], c->Wt.as<double>(), c->contrib.as<double>(), fl);
+    }
+    hipLaunchKernelGGL(chol_intr<RW - 1>, dim3(1), dim3(64), 0, c->st, Dm, ri, c->contrib.as<double>(), c->T,
+                       c->xi.as<double>(), sol_f + 6 * (size_t)c->C, fl);
+    hipLaunchKernelGGL(chol_back<RW>, dim3(1), dim3(1024), sizeof(double) * npad, c->st, S, npad, R,
+                       c->xi.as<double>(), pl.height, c->lvl_start.as<int>(), c->lvl_panels.as<int>(),
+                       c->bs_start.as<int>(), c->bs_k.as<int>(), c->rowmap.as<int>(), sol_f);
+    HIPCHK(hipGetLastError());
+    return SFMX_OK;
+}
+
+// One LM step at `radius`: Schur solve of (J_s^T J_s + D^2) sol = J_s^T r, step_s = -sol,
+// candidate = x + step_s * scale, its cost, Jacobian and scalars (speculative linearization).
 template <int K>
 int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* step_norm, double* ccost,
              double* cgmax, double* cxnorm) {
-    const int C = c->C, npad = c->npad, T = c->T;
+    constexpr int RW = K + 1;
+    const int C = c->C, npad = c->npad;
     double* S = c->SR.as<double>();
-    double* rhs = S + (size_t)npad * npad;
+    double* R = S + (size_t)npad * npad;
+    double* Dm = R + (size_t)npad * RW;
+    double* ri = Dm + K * K;
     int* fl = c->failf.as<int>();
     const sfmx_ba_options& o = c->opt;
     HIPCHK(hipMemsetAsync(fl, 0, sizeof(int), c->st));
@@ -187,35 +235,20 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
                            c->obs_cam.as<int>(), c->pt_start.as<int>(), c->J.as<double>(), c->scale.as<double>(),
                            c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, c->P, C, c->stage_n,
                            c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl);
-    HIPCHK(hipMemsetAsync(S, 0, sizeof(double) * ((size_t)npad * npad + npad), c->st));
+    HIPCHK(hipMemsetAsync(S, 0, sizeof(double) * c->sr_count, c->st));
     hipLaunchKernelGGL(ba_assemble, dim3(c->ntasks), dim3(64), 0, c->st, c->tasks.as<ATask>(), c->ents.as<AEnt>(),
-                       c->sg.as<double>(), c->hbig.as<double>(), c->rg.as<double>(), C, K, c->nf, npad, S, rhs);
+                       c->sg.as<double>(), c->hbig.as<double>(), c->rg.as<double>(), K, c->camrow.as<int>(), npad, S,
+                       R, Dm, ri);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->st));
     // point-sharded ranks: the group part of the reduced camera system and its rhs are sums over ranks
-    RC(allreduce(c, S, (int64_t)npad * npad + npad, SFMX_REDUCE_SUM));
-    hipLaunchKernelGGL(ba_add_cam<K>, dim3(C + 1), dim3(64), 0, c->st, c->P, C, npad, c->camsum.as<double>(),
+    RC(allreduce(c, S, (int64_t)c->sr_count, SFMX_REDUCE_SUM));
+    hipLaunchKernelGGL(ba_add_cam<K>, dim3(C + 1), dim3(64), 0, c->st, c->P, C, npad, c->camrow.as<int>(),
+                       c->padrows.as<int>(), (int)c->plan.padrows.size(), c->camsum.as<double>(),
                        c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, S,
-                       rhs);
-    double* W = c->Linv.as<double>();
+                       R, Dm, ri);
     double* sol = c->sol.as<double>();
-    hipLaunchKernelGGL(chol_first, dim3(1), dim3(256), 0, c->st, S, npad, W, rhs, fl);
-    if (c->sparse) {
-        for (int k = 0; k + 1 < T; ++k)
-            hipLaunchKernelGGL(chol_step, dim3(c->tl_start[k + 1] - c->tl_start[k]), dim3(256), 0, c->st, S, npad, k, W,
-                               rhs, fl, c->tl.as<int2>() + c->tl_start[k]);
-        hipLaunchKernelGGL(chol_back_sparse, dim3(1), dim3(256), sizeof(double) * npad, c->st, S, npad, c->nf, T, rhs,
-                           c->ut_start.as<int>(), c->ut.as<int>(), sol + c->ne);
-    } else {
-        for (int k = 0; k + 1 < T; ++k) {
-            const int m = T - k - 1;
-            hipLaunchKernelGGL(chol_step, dim3(m * (m + 1) / 2), dim3(256), 0, c->st, S, npad, k, W, rhs, fl,
-                               (const int2*)nullptr);
-        }
-        for (int k = T - 1; k >= 0; --k)
-            hipLaunchKernelGGL(chol_back, dim3(std::max(k, 1)), dim3(256), 0, c->st, S, npad, c->nf, k, rhs, sol + c->ne);
-    }
-    HIPCHK(hipGetLastError());
+    RC(solve_reduced<RW>(c, sol + c->ne));
     HIPCHK(hipEventRecord(c->ev[2], c->st));
     if (c->ngroups > 0)
         hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups), dim3(256), c->lds_upd, c->st, c->grp.as<Grp>(),
@@ -248,9 +281,68 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     return SFMX_OK;
 }
 
+// The factorization plan, once per context (at the first run, when the all-reduce callback is
+// known): the camera co-visibility summed over ranks (every rank builds the same plan), the
+// ordering and level schedule (SFMX_BA_ORDER: auto | natural | nd | nd1 | nd2 | nd4), the device
+// copies of the schedule, and S / W / the Schur terms sized by it.
+int ensure_plan(sfmx_ba_ctx* c) {
+    if (c->planned) return SFMX_OK;
+    const int C = c->C;
+    std::vector<char> adj = c->adj;
+    if (c->ar && C > 1) {   // global co-visibility: sum of the ranks' upper triangles
+        std::vector<double> h((size_t)C * (C - 1) / 2);
+        for (int a = 0, e = 0; a < C; ++a)
+            for (int b = a + 1; b < C; ++b, ++e) h[e] = adj[(size_t)a * C + b] ? 1.0 : 0.0;
+        Buf& d = c->SR;   // scratch until S is sized below
+        RC(d.alloc(sizeof(double) * h.size()));
+        HIPCHK(hipMemcpyAsync(d.p, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, c->st));
+        RC(allreduce(c, d.as<double>(), (int64_t)h.size(), SFMX_REDUCE_SUM));
+        HIPCHK(hipMemcpyAsync(h.data(), d.p, sizeof(double) * h.size(), hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        for (int a = 0, e = 0; a < C; ++a)
+            for (int b = a + 1; b < C; ++b, ++e) adj[(size_t)a * C + b] = adj[(size_t)b * C + a] = h[e] > 0.0;
+    }
+    int mode = -1;
+    if (const char* e = std::getenv("SFMX_BA_ORDER")) {
+        const std::string m(e);
+        mode = m == "natural" ? 0 : m == "nd" ? 1 : m == "nd1" ? 2 : m == "nd2" ? 3 : m == "nd4" ? 4 : -1;
+    }
+    sfmx::ba::FactorPlan& pl = c->plan;
+    sfmx::ba::make_plan(C, adj, mode, pl);
+    if (pl.npad > MAX_NPAD) sfmx::ba::make_plan(C, adj, 0, pl);   // padding past the back solve's LDS
+    c->npad = pl.npad;
+    c->T = pl.T;
+    const int RW = c->RW, K = c->K;
+    c->sr_count = (size_t)pl.npad * pl.npad + (size_t)pl.npad * RW + (size_t)K * K + K;
+    std::vector<int4> tk(pl.tasks.size());
+    for (size_t i = 0; i < tk.size(); ++i) tk[i] = make_int4(pl.tasks[i].a, pl.tasks[i].b, pl.tasks[i].s0, pl.tasks[i].s1);
+    hipStream_t st = c->st;
+    int rc;
+    if ((rc = upload(c->camrow, pl.camrow, st)) || (rc = upload(c->padrows, pl.padrows, st)) ||
+        (rc = upload(c->rowmap, pl.rowmap, st)) || (rc = upload(c->leaves, pl.leaves, st)) ||
+        (rc = upload(c->ptasks, tk, st)) || (rc = upload(c->psrc, pl.src, st)) ||
+        (rc = upload(c->lvl_start, pl.lvl_start, st)) || (rc = upload(c->lvl_panels, pl.lvl_panels, st)) ||
+        (rc = upload(c->bs_start, pl.bs_start, st)) || (rc = upload(c->bs_k, pl.bs_k, st)))
+        return rc;
+    RC(c->SR.alloc(sizeof(double) * c->sr_count));
+    RC(c->Wt.alloc(sizeof(double) * (size_t)pl.T * NB * NB));
+    RC(c->contrib.alloc(sizeof(double) * (size_t)pl.T * K * RW));
+    RC(c->xi.alloc(sizeof(double) * K));
+    hipError_t e = hipSuccess;
+#define BACKATTR(RWV) e = hipFuncSetAttribute((const void*)chol_back<RWV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                              (int)(sizeof(double) * pl.npad))
+    if (RW == 2) BACKATTR(2); else if (RW == 4) BACKATTR(4); else BACKATTR(8);
+#undef BACKATTR
+    if (e != hipSuccess) return fail(SFMX_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(e));
+    HIPCHK(hipStreamSynchronize(st));
+    c->planned = true;
+    return SFMX_OK;
+}
+
 template <int K>
 int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace, int trace_cap, int* ntrace_out) {
     DeviceGuard dg(c->device);
+    RC(ensure_plan(c));
     const auto t0 = std::chrono::steady_clock::now();
     const sfmx_ba_options& o = c->opt;
     const int maxit = max_iters > 0 ? max_iters : o.max_num_iterations;
@@ -354,13 +446,6 @@ int validate(const sfmx_ba_problem* pb) {
     return SFMX_OK;
 }
 
-template <class T>
-int upload(Buf& b, const std::vector<T>& v, hipStream_t st) {
-    RC(b.alloc(sizeof(T) * std::max<size_t>(v.size(), 1)));
-    if (!v.empty()) HIPCHK(hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st));
-    return SFMX_OK;
-}
-
 int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
     DeviceGuard dg(c->device);
     double* x = c->x.as<double>();
@@ -414,61 +499,7 @@ struct Topology {
     std::vector<AEnt> ents;
     long long sg_total = 0, h_total = 0;
     int rg_total = 0, dp_max = 16;
-    // tile-sparse factorization: per panel k the nonzero trailing updates (tl_start / tl, the
-    // (k+1, k+1) tile first) and the nonzero upper tiles for the back solve (ut_start / ut)
-    std::vector<int> tl_start, ut_start, ut;
-    std::vector<int2> tl;
-    int tiles_nz = 0;
 };
-
-// Tile pattern of S (lower) from the assembly blocks, then the symbolic fill of the block
-// factorization in natural order: a tile that starts and stays exactly zero is skipped, which
-// changes no computed value (updates from zero tiles are exact zeros).
-void tile_pattern(int C, int K, int nf, int T, const std::vector<ATask>& tasks, Topology& tp) {
-    std::vector<char> nz((size_t)T * T, 0);
-    auto mark = [&](int r0, int r1, int c0, int c1) {   // rows [r0, r1) x cols [c0, c1)
-        for (int I = r0 / NB; I <= (r1 - 1) / NB; ++I)
-            for (int Jj = c0 / NB; Jj <= (c1 - 1) / NB; ++Jj) {
-                const int a = std::max(I, Jj), b = std::min(I, Jj);
-                nz[(size_t)a * T + b] = 1;
-            }
-    };
-    for (int I = 0; I < T; ++I) nz[(size_t)I * T + I] = 1;
-    for (const ATask& t : tasks) {
-        if (t.type == 0) mark(6 * t.a, 6 * t.a + 6, 6 * t.b, 6 * t.b + 6);
-        else if (t.type == 1) mark(6 * t.a, 6 * t.a + 6, 6 * C, 6 * C + K);
-    }
-    mark(6 * C, nf, 6 * C, nf);
-    for (int c = 0; c < C; ++c) mark(6 * c, 6 * c + 6, 6 * C, 6 * C + K);   // C (camera-intrinsics coupling)
-    for (int k = 0; k < T; ++k)
-        for (int a = k + 1; a < T; ++a)
-            if (nz[(size_t)a * T + k])
-                for (int b = k + 1; b <= a; ++b)
-                    if (nz[(size_t)b * T + k]) nz[(size_t)a * T + b] = 1;
-    tp.tl_start.assign(T, 0);
-    tp.tl.clear();
-    for (int k = 0; k + 1 < T; ++k) {
-        tp.tl_start[k] = (int)tp.tl.size();
-        tp.tl.push_back(make_int2(k + 1, k + 1));
-        for (int a = k + 1; a < T; ++a)
-            for (int b = k + 1; b <= a; ++b) {
-                if (a == k + 1 && b == k + 1) continue;
-                if (nz[(size_t)a * T + k] && nz[(size_t)b * T + k]) tp.tl.push_back(make_int2(a, b));
-            }
-    }
-    tp.tl_start[T - 1] = (int)tp.tl.size();
-    tp.tl_start.push_back((int)tp.tl.size());
-    tp.ut_start.assign(T + 1, 0);
-    tp.ut.clear();
-    for (int k = 0; k < T; ++k) {
-        tp.ut_start[k] = (int)tp.ut.size();
-        for (int i = 0; i < k; ++i)
-            if (nz[(size_t)k * T + i]) tp.ut.push_back(i);
-    }
-    tp.ut_start[T] = (int)tp.ut.size();
-    tp.tiles_nz = 0;
-    for (char v : nz) tp.tiles_nz += v;
-}
 
 void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start, const int* obs_cam, Topology& tp) {
     tp.obs_lc.assign(O, 0);
@@ -645,20 +676,17 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
     c->ne = 3 * (int64_t)P;
     c->nf = 6 * C + K;
     c->n = c->ne + c->nf;
-    c->npad = (c->nf + NB - 1) / NB * NB;
-    c->T = c->npad / NB;
-    if (c->npad > 16 * 1024) return bail(fail(SFMX_EINVAL, "too many cameras for the dense reduced system (6C + k > 16384)"));
+    c->RW = K + 1;
+    if (6 * (int64_t)C > MAX_NPAD) return bail(fail(SFMX_EINVAL, "too many cameras for the reduced camera system (6C > 16384)"));
     std::vector<int> pt_start(P + 1, 0);
     for (int i = 0; i < O; ++i) pt_start[rop[i] + 1]++;
     for (int p = 0; p < P; ++p) pt_start[p + 1] += pt_start[p];
     Topology tp;
     build_topology(P, C, O, K, pt_start, roc.data(), tp);
-    tile_pattern(C, K, c->nf, c->T, tp.tasks, tp);
-    {
-        const char* de = std::getenv("SFMX_BA_DENSE");
-        c->sparse = !(de && de[0] == '1');
-    }
-    c->tl_start = tp.tl_start;
+    // local camera co-visibility (the pose blocks this rank's points create)
+    c->adj.assign((size_t)C * C, 0);
+    for (const ATask& t : tp.tasks)
+        if (t.type == 0 && t.a != t.b) c->adj[(size_t)t.a * C + t.b] = c->adj[(size_t)t.b * C + t.a] = 1;
     c->ngroups = (int)tp.grp.size();
     c->ntasks = (int)tp.tasks.size();
     c->nslots = (int)tp.gcam.size();
@@ -675,8 +703,6 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
         if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_gupdate<KK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_upd)
         if (K == 1) { LDSATTR(1); } else if (K == 3) { LDSATTR(3); } else { LDSATTR(7); }
 #undef LDSATTR
-        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)chol_back_sparse, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)(sizeof(double) * c->npad));
         if (e != hipSuccess) return bail(fail(SFMX_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(e)));
     }
     hipStream_t st = c->st;
@@ -686,8 +712,7 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
         (rc = upload(c->gcam, tp.gcam, st)) || (rc = upload(c->obs_lc, tp.obs_lc, st)) ||
         (rc = upload(c->obs_row, tp.obs_row, st)) || (rc = upload(c->lcrow, tp.lcrow, st)) ||
         (rc = upload(c->tasks, tp.tasks, st)) || (rc = upload(c->ents, tp.ents, st)) ||
-        (rc = upload(c->cref_start, tp.cref_start, st)) || (rc = upload(c->cref, tp.cref, st)) ||
-        (rc = upload(c->tl, tp.tl, st)) || (rc = upload(c->ut_start, tp.ut_start, st)) || (rc = upload(c->ut, tp.ut, st)))
+        (rc = upload(c->cref_start, tp.cref_start, st)) || (rc = upload(c->cref, tp.cref, st)))
         return bail(rc);
     const size_t n = c->n, so = std::max(O, 1);
     const size_t ncams = (size_t)C * ncp(K) + K * (K + 1) / 2 + K;
@@ -698,8 +723,7 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
         {&c->plt, 72 * (size_t)std::max(P, 1)}, {&c->sg, 8 * (size_t)std::max<long long>(tp.sg_total, 1)},
         {&c->rg, 8 * (size_t)std::max(tp.rg_total, 1)}, {&c->hbig, 8 * (size_t)std::max<long long>(tp.h_total, 1)},
         {&c->gpart, 8 * (size_t)std::max(c->nslots, 1) * ncp(K)}, {&c->gpl, 8 * (size_t)std::max(c->ngroups, 1) * GP_N},
-        {&c->scal, 8 * SC_N}, {&c->Linv, 8 * (size_t)2 * NB * NB},
-        {&c->SR, 8 * ((size_t)c->npad * c->npad + c->npad)}, {&c->failf, 64},
+        {&c->scal, 8 * SC_N}, {&c->failf, 64},
         {&c->partA, 8 * (size_t)nblk(std::max<int64_t>(O, n))}};
     for (auto& a : allocs) if ((rc = a.b->alloc(a.bytes))) return bail(rc);
     HIPCHK(hipMemsetAsync(c->gpl.p, 0, c->gpl.bytes, st));

@@ -54,6 +54,12 @@ class sfmx_ba_options(C.Structure):
                 ("min_relative_decrease", C.c_double)]
 
 
+class sfmx_ba_plan_info(C.Structure):
+    _fields_ = [("order", C.c_int32), ("leaf_tiles", C.c_int32), ("npad", C.c_int32), ("tiles", C.c_int32),
+                ("tiles_nz", C.c_int32), ("height", C.c_int32), ("leaves", C.c_int32), ("tasks", C.c_int32),
+                ("src", C.c_int32), ("predicted_us", C.c_double)]
+
+
 class sfmx_ba_summary(C.Structure):
     _fields_ = [("initial_cost", C.c_double), ("final_cost", C.c_double),
                 ("num_successful_steps", C.c_int32), ("num_unsuccessful_steps", C.c_int32),
@@ -114,6 +120,8 @@ PROTOTYPES = {
     "sfmx_ba_phase_ms": (C.c_int, [_vp, _P(C.c_double), C.c_int32]),
     "sfmx_ba_destroy": (C.c_int, [_vp]),
     "sfmx_ba_jacobian": (C.c_int, [_P(sfmx_ba_problem), C.c_int32, _vp, _vp, _vp, _vp]),
+    "sfmx_ba_plan": (C.c_int, [C.c_int32, _vp, C.c_int32, _P(sfmx_ba_plan_info), _i32p, _i32p, C.c_int32, _i32p,
+                               C.c_int32, _i32p, C.c_int32]),
     "sfmx_pose_to_ceres": (C.c_int, [_P(C.c_double), _P(C.c_double)]),
     "sfmx_pose_from_ceres": (C.c_int, [_P(C.c_double), _P(C.c_double)]),
     "sfmx_homography_ratios": (C.c_int, [_P(_vp), _i32p, C.c_int32, _i32p, _i32p, C.c_int32, _vp, _vp, C.c_double,

@@ -20,7 +20,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import (lib, check, sfmx_ba_problem, sfmx_ba_options, sfmx_ba_summary, ALLREDUCE_FN)
+from ._lib import (lib, check, sfmx_ba_problem, sfmx_ba_options, sfmx_ba_summary, sfmx_ba_plan_info, ALLREDUCE_FN)
 
 CAM_SIMPLE, CAM_SIMPLE_RADIAL, CAM_DISTORTION = 1, 3, 7      # value = intrinsics size k
 CAMERA_MODELS = {"Simple": CAM_SIMPLE, "SimpleRadial": CAM_SIMPLE_RADIAL, "Distortion": CAM_DISTORTION}
@@ -156,6 +156,29 @@ class BAContext:
             self.close()
         except Exception:
             pass
+
+
+ORDER_AUTO, ORDER_NATURAL, ORDER_ND = -1, 0, 1
+
+
+def factor_plan(adj: np.ndarray, order: int = ORDER_AUTO) -> dict:
+    """The solver's factorization plan for a camera co-visibility graph (host only): camera rows,
+    tile counts, elimination-tree height and the level schedule (include/sfmx_ba.h sfmx_ba_plan)."""
+    adj = np.ascontiguousarray(adj, np.uint8)
+    n = adj.shape[0]
+    info = sfmx_ba_plan_info()
+    camrow = np.zeros(max(n, 1), np.int32)
+    check(lib.sfmx_ba_plan(n, adj.ctypes.data, order, C.byref(info), camrow.ctypes.data_as(C.POINTER(C.c_int32)),
+                           None, 0, None, 0, None, 0), "sfmx_ba_plan")
+    leaves = np.zeros(max(info.leaves, 1), np.int32)
+    tasks = np.zeros((max(info.tasks, 1), 6), np.int32)
+    src = np.zeros(max(info.src, 1), np.int32)
+    i32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))   # noqa: E731
+    check(lib.sfmx_ba_plan(n, adj.ctypes.data, order, C.byref(info), i32(camrow), i32(leaves), len(leaves),
+                           i32(tasks), len(tasks), i32(src), len(src)), "sfmx_ba_plan")
+    out = {f: getattr(info, f) for f, _ in info._fields_}
+    out.update(camrow=camrow[:n], leaves=leaves[:info.leaves], tasks=tasks[:info.tasks], src=src[:info.src])
+    return out
 
 
 def pose_to_ceres(Rt: np.ndarray) -> np.ndarray:

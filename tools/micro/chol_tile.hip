@@ -1,14 +1,16 @@
-// Phase timing of the BA dense solve's diagonal-tile inverse (chol_first) and one
-// trailing step (chol_step) on a random SPD 1216x1216 system; wall_clock64 stamps.
+// Phase timing of the BA solve's diagonal-tile inverse (chol_leaves, one leaf) and one level of
+// trailing updates (chol_level: every tile below panel 0, natural order) on a random SPD 1216x1216
+// system with 4 right-hand sides; wall_clock64 stamps.
 #define SFMX_CHOL_STAMPS
-#include "../../sfm-mvs-pipeline_amd/csrc/ba_kernels.hpp"
+#include "../../sfm-mvs-pipeline_amd/csrc/ba_chol.hpp"
 #include <cstdio>
 #include <vector>
 #include <random>
 using namespace sfmx::ba;
 int main() {
     const int npad = 1216, T = npad / NB;
-    std::vector<double> h((size_t)npad * npad + npad);
+    constexpr int RW = 4;
+    std::vector<double> h((size_t)npad * npad + (size_t)npad * RW);
     std::mt19937 rng(3);
     std::normal_distribution<double> nd;
     std::vector<double> B((size_t)npad * 40);
@@ -19,35 +21,44 @@ int main() {
             for (int k = 0; k < 40; ++k) s += B[i * 40 + k] * B[j * 40 + k];
             h[(size_t)i * npad + j] = h[(size_t)j * npad + i] = s;
         }
-    for (int i = 0; i < npad; ++i) h[(size_t)npad * npad + i] = nd(rng);
-    double *S, *W, *S0; int* fail;
-    hipMalloc(&S, h.size() * 8); hipMalloc(&S0, h.size() * 8); hipMalloc(&W, 2 * NB * NB * 8); hipMalloc(&fail, 4);
+    for (int i = 0; i < npad * RW; ++i) h[(size_t)npad * npad + i] = nd(rng);
+    // level 0 of a natural-order plan: panel 0 updates every tile (a, b), 1 <= b <= a; (1, 1) inverts
+    std::vector<int4> tasks;
+    tasks.push_back(make_int4(1, 1, 0, 1));
+    for (int a = 1; a < T; ++a)
+        for (int b = 1; b <= a; ++b)
+            if (a != 1 || b != 1) tasks.push_back(make_int4(a, b, 0, 1));
+    int zero = 0;
+    double *S, *W, *S0, *contrib; int *fail, *src, *leaves; int4* dt;
+    hipMalloc(&S, h.size() * 8); hipMalloc(&S0, h.size() * 8); hipMalloc(&W, (size_t)T * NB * NB * 8); hipMalloc(&fail, 4);
+    hipMalloc(&contrib, (size_t)T * 3 * RW * 8); hipMalloc(&src, 4); hipMalloc(&leaves, 4); hipMalloc(&dt, tasks.size() * 16);
+    hipMemcpy(src, &zero, 4, hipMemcpyHostToDevice); hipMemcpy(leaves, &zero, 4, hipMemcpyHostToDevice);
+    hipMemcpy(dt, tasks.data(), tasks.size() * 16, hipMemcpyHostToDevice);
     hipMemcpy(S0, h.data(), h.size() * 8, hipMemcpyHostToDevice);
     hipMemset(fail, 0, 4);
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
     long long st[64];
     for (int rep = 0; rep < 3; ++rep) {
         hipMemcpy(S, S0, h.size() * 8, hipMemcpyDeviceToDevice);
-        double* rhs = S + (size_t)npad * npad;
+        double* R = S + (size_t)npad * npad;
         hipEventRecord(e0);
-        chol_first<<<1, 256>>>(S, npad, W, rhs, fail);
+        chol_leaves<RW><<<1, 256>>>(S, npad, R, leaves, W, contrib, fail);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms; hipEventElapsedTime(&ms, e0, e1);
         hipMemcpyFromSymbol(st, HIP_SYMBOL(g_chol_stamps), sizeof st);
-        printf("chol_first %.2f us | load %lld", ms * 1e3, st[1] - st[0]);
+        printf("chol_leaves %.2f us | load %lld", ms * 1e3, st[1] - st[0]);
         for (int s = 0; s < 4; ++s)
             printf(" | s%d panel->inner %lld inner %lld M %lld upd %lld", s, st[2 + 4 * s] - (s ? st[1 + 4 * s] : st[1]),
                    st[3 + 4 * s] - st[2 + 4 * s], st[4 + 4 * s] - st[3 + 4 * s], st[5 + 4 * s] - st[4 + 4 * s]);
         printf(" | store %lld rhs %lld  (ticks of 100 MHz wall clock)\n", st[20] - st[17], st[21] - st[20]);
         hipEventRecord(e0);
-        const int m = T - 1;
-        chol_step<<<m * (m + 1) / 2, 256>>>(S, npad, 0, W, rhs, fail, nullptr);
+        chol_level<RW><<<(unsigned)tasks.size(), 256>>>(S, npad, R, dt, src, 1, W, contrib, fail);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         hipEventElapsedTime(&ms, e0, e1);
         hipMemcpyFromSymbol(st, HIP_SYMBOL(g_chol_stamps), sizeof st);
-        printf("chol_step(0) %.2f us: load %lld gemm1 %lld store+gemm2 %lld -> inverse %lld | diag inverse %lld | GT %lld ticks\n", ms * 1e3,
+        printf("chol_level(0) %.2f us: load %lld gemm1 %lld store+gemm2 %lld -> inverse %lld | diag inverse %lld | GT %lld ticks\n", ms * 1e3,
                st[31] - st[30], st[32] - st[31], st[33] - st[32], st[0] - st[33], st[21] - st[0], st[34] - st[21]);
     }
     int hf; hipMemcpy(&hf, fail, 4, hipMemcpyDeviceToHost);
