@@ -48,6 +48,12 @@ FP4_MFMA_PEAK_TOPS = 4 * 256 * 4 * (32 * 32 * 16 * 2 / 32) * 2.4e9 / 1e12   # 10
 # VALU integer issue: 256 CU x 4 SIMD x 16 lanes/clk (a wave64 op issues in 4 cycles) x 2.4 GHz
 VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 ORB_OPS_PER_PAIR = 16.0   # 8 v_xor + 8 v_bcnt (popcount-accumulate) per 256-bit pair
+# fp64 (matrix and vector) dense peak: 256 CU x 128 flop/clk x 2.4 GHz
+FP64_PEAK_TFLOPS = 256 * 128 * 2.4e9 / 1e12
+# BA algorithmic work per LM iteration at C5: S assembly ~2-2.5 + J ~0.4 +
+# Cholesky ~0.58 GFLOP; bytes: obs read twice, points, S written and read
+BA_FLOP_PER_ITER_C5, BA_BYTES_PER_ITER_C5 = 3.0e9, 0.1e9
+BA_PMC_FILE = "r02_pmc_ba.json"
 
 
 def parse():
@@ -472,6 +478,7 @@ def bench_ba(args, rank, world, local):
            "iterations": iters, "successful": sm["num_successful_steps"], "initial_cost": sm["initial_cost"],
            "final_cost": sm["final_cost"], "termination": ba.TERMINATION_NAMES[sm["termination_type"]],
            "total_ms": total_ms, "phase_ms_rank0": phases}
+    res["roofline"] = ba_roofline(args, res["value"], world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             from oracle import oracle
@@ -487,6 +494,32 @@ def bench_ba(args, rank, world, local):
         except Exception as e:   # pragma: no cover
             res["cpu_baseline"] = {"error": str(e)}
     return res
+
+
+def ba_roofline(args, ms_per_iter, world):
+    """Roofline of one LM iteration at C5 (3.0 GFLOP fp64, 0.1 GB): the fp64 bound
+    (38 us at 78.6 TF/s) dominates the HBM bound (12.5 us).  `traffic` = HBM bytes per iteration
+    from the committed PMC passes of this leg (tools/pmc_ba.sh -> tools/pmc_ba_json.py), null for
+    other problem sizes or shards."""
+    c5 = args.ba_cams == 200 and args.ba_points == 200_000
+    flop = BA_FLOP_PER_ITER_C5 if c5 else None
+    out = {"bound": "mfma", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS, "achieved": None, "frac": None,
+           "traffic": None, "kernel": "one LM iteration: every BA kernel of the step (ba_gschur, ba_assemble, the "
+                                      "chol_* level schedule, ba_gupdate, ba_glin, ...) + host control",
+           "algorithmic": "3.0 GFLOP fp64 and 0.1 GB per LM iteration at C5 (SURVEY.md §8d)"}
+    if flop is None or not ms_per_iter:
+        return out
+    t = ms_per_iter * 1e-3
+    out["achieved"] = flop / t / 1e12   # one iteration of the whole job (all ranks) over its wall time
+    out["frac"] = out["achieved"] / FP64_PEAK_TFLOPS
+    out["hbm_frac"] = BA_BYTES_PER_ITER_C5 / t / (HBM_PEAK_GBS * 1e9)
+    out["roofline_ms"] = max(flop / (FP64_PEAK_TFLOPS * 1e12), BA_BYTES_PER_ITER_C5 / (HBM_PEAK_GBS * 1e9)) * 1e3
+    path = os.path.join(REPO, "profiles", BA_PMC_FILE)
+    if world == 1 and os.path.exists(path):
+        with open(path) as f:
+            out["traffic"] = json.load(f)["bytes_per_iteration"]
+        out["traffic_unit"] = f"HBM bytes per LM iteration (2 x FETCH_SIZE + WRITE_SIZE, profiles/{BA_PMC_FILE})"
+    return out
 
 
 MVS_SHOTS, MVS_H, MVS_W, MVS_C = 50, 3000, 4000, 3

@@ -42,14 +42,13 @@
 namespace sfmx {
 namespace ba {
 
-constexpr int GCH = 256;      // observations per chunk = threads per group workgroup
+constexpr int GCH = 256;      // observations per chunk = threads per group workgroup (ba_glin, ba_gupdate)
 constexpr int GOBS = 1024;    // observations per (normal) group
 constexpr int GPTS = 128;     // points per group (one thread per point)
-constexpr int UMAX = 16;      // cameras per group: S block <= (6*16 + K)^2
-constexpr int SBP = 16;       // points per SYRK sub-batch
-constexpr int SBK = 3 * SBP;  // SYRK depth per sub-batch (3 per point)
-constexpr int ALD = SBK + 1;  // LDS row stride of the SYRK operand (doubles)
-constexpr int MAXT = 7;       // 16x16 upper tiles per wave: dp <= 112 -> 28 tiles / 4 waves
+constexpr int UMAX = 16;      // cameras per group (ba_glin's per-camera Gram accumulators)
+constexpr int GDPMAX = 64;    // ba_gschur: dp = round16(6u + K) <= 64 (the host cuts groups there)
+constexpr int WB_OBS = 64;    // ba_gschur wave batch: observations (one lane each)
+constexpr int WB_PTS = 16;    // ba_gschur wave batch: whole points
 
 // per-(group, camera) partials of the unscaled camera columns:
 //   Jc^T Jc upper (21) | Jc^T Ji (6K) | Jc^T r (6) | Ji^T Ji upper (K(K+1)/2) | Ji^T r (K)
@@ -67,6 +66,7 @@ struct Grp {
     int o0, o1, p0, p1;      // observation / point range (internal order)
     int u, cam_off;          // cameras: gcam[cam_off .. cam_off + u), sorted; partial rows gpart[cam_off + lc]
     int ch0, nch;            // chunks chk[ch0 .. ch0 + nch)
+    int b0, nb;              // ba_gschur wave batches bat[b0 .. b0 + nb)
     long long sg_off;        // dense (6u+K)^2 block in sg (normal groups)
     long long h_off;         // H (dim x 3) in hbig (big groups)
     int rg_off, big;         // rhs block (dim) in rg; big-group flag
@@ -74,12 +74,37 @@ struct Grp {
 // observations [o0, o1), point slots [q0, q1) of the group; the chunk's feature rows sorted by
 // local camera: camera lc owns rows lcrow[lc0 + lc] .. lcrow[lc0 + lc + 1) (a multiple of 4, zero-padded)
 struct Chunk { int o0, o1, q0, q1, lc0, nrows, pad0, pad1; };
+// ba_gschur wave batch: whole points [p0, p1) with their observations [o0, o1) (<= WB_OBS, <= WB_PTS)
+struct Batch { int o0, o1, p0, p1; };
 struct ATask { int type, a, b, l0, l1, pad0, pad1, pad2; };   // 0: pose (a <= b), 1: pose-intr a, 2: intr
 // one contribution to an S block: normal group: b0 = sg offset of its (6la, 6lb) element (row
 // stride dim); big group: b0 / b1 = hbig offsets of the H rows 6la / 6lb (row stride 3)
 struct AEnt { long long b0, b1; int dim, big, rg, pad; };
 
 __device__ __forceinline__ int gdim(const Grp& G, int K) { return 6 * G.u + K; }
+
+// Diagnostic build only (make stamps -> lib/libsfmx_stamps.so, tools/ba_stamps.py): per-phase
+// s_memtime cycle totals of thread 0 of every workgroup.  Compiled out of the product library.
+#ifdef SFMX_BA_STAMPS
+__device__ unsigned long long g_ba_stamps[64];
+#define BA_T0() long long ba_t_ = __builtin_amdgcn_s_memtime(); long long ba_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define BA_STAMP(i)                                                                                \
+    do {                                                                                           \
+        const long long t_ = __builtin_amdgcn_s_memtime();                                         \
+        ba_acc_[i] += t_ - ba_t_;                                                                  \
+        ba_t_ = t_;                                                                                \
+    } while (0)
+#define BA_FLUSH(base)                                                                             \
+    do {                                                                                           \
+        if (threadIdx.x == 0)                                                                      \
+            for (int i_ = 0; i_ < 8; ++i_)                                                         \
+                if (ba_acc_[i_]) atomicAdd(&g_ba_stamps[(base) + i_], (unsigned long long)ba_acc_[i_]); \
+    } while (0)
+#else
+#define BA_T0() do { } while (0)
+#define BA_STAMP(i) do { } while (0)
+#define BA_FLUSH(base) do { } while (0)
+#endif
 
 // M = L^-1 of the Cholesky factor of the SPD 3x3 E (row-major full); false if not positive definite.
 // Packed lower: M[0] = m00, M[1] = m10, M[2] = m11, M[3] = m20, M[4] = m21, M[5] = m22
@@ -114,28 +139,39 @@ __device__ __forceinline__ double dsq(double colsq, double s, double dmin, doubl
     return d * d;
 }
 
+// J records are stored Jacobi-scaled (J_s = J diag(scale): ba_glin writes them scaled once the
+// scale of the solve is known; the first step's ba_gschur<SCALEJ> scales the iteration-0
+// linearization in place), so the step kernels read them without gathering the scales.
 template <int K>
 struct JRec {            // one observation's Jacobian record, scaled
     double r[2], je[2][3], jc[2][6], ji[2][K];
 };
 template <int K>
-__device__ __forceinline__ void load_rec(const double* __restrict__ jr, const double* sp, const double* sc,
-                                         const double* si, JRec<K>& R) {
+__device__ __forceinline__ void load_rec(const double* __restrict__ jr, JRec<K>& R) {
     R.r[0] = jr[0]; R.r[1] = jr[1];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) R.je[j][i] = jr[2 + 3 * j + i] * sp[i];
+        for (int i = 0; i < 3; ++i) R.je[j][i] = jr[2 + 3 * j + i];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) R.jc[j][i] = jr[8 + 6 * j + i] * sc[i];
+        for (int i = 0; i < 6; ++i) R.jc[j][i] = jr[8 + 6 * j + i];
 #pragma unroll
-        for (int i = 0; i < K; ++i) R.ji[j][i] = jr[20 + K * j + i] * si[i];
+        for (int i = 0; i < K; ++i) R.ji[j][i] = jr[20 + K * j + i];
     }
 }
 template <int K>
-__device__ __forceinline__ void load_jrec(const double* __restrict__ J, int o, const double* sp, const double* sc,
-                                          const double* si, JRec<K>& R) {
-    load_rec<K>(J + (size_t)o * jst(K), sp, sc, si, R);
+__device__ __forceinline__ void load_jrec(const double* __restrict__ J, int o, JRec<K>& R) {
+    load_rec<K>(J + (size_t)o * jst(K), R);
+}
+// the record as 13 (or 10 + K) independent 16-B loads
+template <int K>
+__device__ __forceinline__ void load_jrec_v(const double* __restrict__ J, int o, JRec<K>& R) {
+    constexpr int JS = jst(K);
+    const double2* s2 = reinterpret_cast<const double2*>(J + (size_t)o * JS);
+    double v[JS];
+#pragma unroll
+    for (int i = 0; i < JS / 2; ++i) { const double2 t = s2[i]; v[2 * i] = t.x; v[2 * i + 1] = t.y; }
+    load_rec<K>(v, R);
 }
 
 // Copy n2 16-B pieces global -> LDS with every load issued before the first store (a plain
@@ -156,44 +192,78 @@ __device__ __forceinline__ void stage_copy(double2* __restrict__ dst, const doub
 // ---------------------------------------------------------------------------------------------
 // ba_gschur: per group, its block -sum_p H_p H_p^T (dense dim x dim into sg) and -sum_p H_p t_p
 // (into rg); per point M_p and t_p (plt, 9 doubles) for the back substitution.
-// Dynamic LDS: stage[max(GCH * jst(K), dp_max * ALD)] (the chunk's J records, coalesced; later the
-// SYRK operand A[dp][ALD]) | pd[GPTS][9 + 3K].
-template <int K>
-__global__ __launch_bounds__(256, K == 7 ? 1 : 2)
-void ba_gschur(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const int* __restrict__ gcam,
+// Normal groups: no workgroup barrier until the end.  Each wave takes every 4th batch of the
+// group (<= 64 observations, <= 16 whole points, host-built) and keeps its own accumulators:
+//   lane = observation: its J record straight into registers (13 x 16-B loads), the scaled
+//     blocks, W_o = Je_s^T Jc_s (registers) and the point partials E (6), g (3), V (3K) -> wave LDS;
+//   lane = point: sums its observations' partials in observation order, + D_p^2, M = chol(E)^-1,
+//     t = M g, Hi = M V -> wave LDS + plt;
+//   rounds of 4 points: H_p columns (camera rows Z_o = (M W_o)^T, intrinsics rows Hi) -> a zeroed
+//     4 x dp x 3 wave buffer; the SYRK on v_mfma_f64_16x16x4f64 takes the 4 points as its k
+//     slots: lane m + 16kk holds H_{p_kk}[16I + m][c], so tile (I, J) += 3 MFMAs (c = 0..2), the
+//     same register both as the A operand (H[16I + m][kk]) and, for tile row J, the B operand;
+//   rhs: lane rows 16I + m accumulate H t of its point.
+// Then the 4 waves' tiles and rhs are summed in wave order (fixed, deterministic) through LDS.
+// Groups are cut on the host so that dp = round16(6u + K) <= GDPMAX; the launch is specialised on
+// NT = dp_max / 16 (NT (NT + 1) / 2 upper 16x16 tiles per wave).
+// Big groups (one point with > 64 observations, too many cameras or two observations in one
+// camera): the serial path, one thread per point / camera.
+// SCALEJ (the first step of a solve, J still unscaled from iteration 0): every record is scaled
+// by the solve's Jacobi scale as it is read, and written back scaled (J_s, load_rec).
+// Dynamic LDS: per wave max(64 x NPF partials, 4 x HS H columns) + WB_PTS x PD point data;
+// the final combine reuses it as [dp][dp + 1] + rhs.
+__host__ __device__ constexpr int gs_npf(int K) { return 9 + 3 * K; }                 // E 6 | g 3 | V 3K
+__host__ __device__ constexpr int gs_pd(int K) { return 9 + 3 * K; }                  // M 6 | t 3 | Hi 3K
+__host__ __device__ constexpr int gs_hs(int dp) { return 3 * dp + 2; }                // per-point H column block
+__host__ __device__ constexpr int gs_wreg(int K, int dp) {                            // doubles per wave
+    return (WB_OBS * gs_npf(K) > 4 * gs_hs(dp) ? WB_OBS * gs_npf(K) : 4 * gs_hs(dp)) + WB_PTS * gs_pd(K);
+}
+template <int K, int NT, bool SCALEJ>
+__global__ __launch_bounds__(256, 2)
+void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const int* __restrict__ gcam,
                const short* __restrict__ obs_lc, const int* __restrict__ obs_point, const int* __restrict__ obs_cam,
                const int* __restrict__ pt_start, const double* __restrict__ J, const double* __restrict__ scale,
-               const double* __restrict__ colsq, double dmin, double dmax, double radius, int P, int C, int stage_n,
+               const double* __restrict__ colsq, double dmin, double dmax, double radius, int P, int C,
                double* __restrict__ plt, double* __restrict__ sg, double* __restrict__ rg, double* __restrict__ hbig,
                int* __restrict__ fail) {
     extern __shared__ __attribute__((aligned(16))) double gl[];
-    constexpr int JS = jst(K);
-    constexpr int PD = 9 + 3 * K;           // LDS per point: M (6) | t (3) | Hi (K x 3)
-    double* stg = gl;                       // J records of the chunk, then the SYRK operand
-    double* A = gl;
-    double* pd = gl + stage_n;
+    constexpr int NPF = gs_npf(K), PD = gs_pd(K);
     const Grp G = grp[blockIdx.x];
-    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, m16 = l & 15, kq = l >> 4;
-    const size_t ne = 3 * (size_t)P, ni = ne + 6 * (size_t)C;
-    double si[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) si[i] = scale[ni + i];
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, m16 = l & 15, kk = l >> 4;
     const int dim = gdim(G, K);
+    double* pd = gl;   // big groups: the point's M, t
 
     if (G.big) {   // one point, any number of observations / cameras: serial per point, per camera
         const int p = G.p0;
+        if (SCALEJ) {   // scale the point's records in place first (one thread per observation)
+            constexpr int JS = jst(K);
+            const size_t ne = 3 * (size_t)P;
+            for (int o = G.o0 + tid; o < G.o1; o += blockDim.x) {
+                double* v = const_cast<double*>(J) + (size_t)o * JS;
+                const double* sp = scale + 3 * (size_t)p;
+                const double* sc = scale + ne + 6 * (size_t)obs_cam[o];
+                const double* si = scale + ne + 6 * (size_t)C;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) v[2 + 3 * j + i] *= sp[i];
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) v[8 + 6 * j + i] *= sc[i];
+#pragma unroll
+                    for (int i = 0; i < K; ++i) v[20 + K * j + i] *= si[i];
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
         if (tid == 0) {
             const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
             double E[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0}, Wi[3 * K];
 #pragma unroll
             for (int i = 0; i < 3 * K; ++i) Wi[i] = 0.0;
             for (int o = G.o0; o < G.o1; ++o) {
-                const int c = obs_cam[o];
-                double sc[6];
-#pragma unroll
-                for (int d = 0; d < 6; ++d) sc[d] = scale[ne + 6 * (size_t)c + d];
                 JRec<K> R;
-                load_jrec<K>(J, o, sp, sc, si, R);
+                load_jrec<K>(J, o, R);
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
 #pragma unroll
@@ -237,13 +307,8 @@ void ba_gschur(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const
         for (int i = 0; i < 6; ++i) M[i] = pd[i];
 #pragma unroll
         for (int k = 0; k < 3; ++k) t[k] = pd[6 + k];
-        const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
         double* H = hbig + G.h_off;
         for (int lc = tid; lc < G.u; lc += blockDim.x) {   // W of camera lc over the point's observations, in order
-            const int c = gcam[G.cam_off + lc];
-            double sc[6];
-#pragma unroll
-            for (int d = 0; d < 6; ++d) sc[d] = scale[ne + 6 * (size_t)c + d];
             double W[3][6];
 #pragma unroll
             for (int a = 0; a < 3; ++a)
@@ -252,7 +317,7 @@ void ba_gschur(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const
             for (int o = G.o0; o < G.o1; ++o) {
                 if (obs_lc[o] != lc) continue;
                 JRec<K> R;
-                load_jrec<K>(J, o, sp, sc, si, R);
+                load_jrec<K>(J, o, R);
 #pragma unroll
                 for (int a = 0; a < 3; ++a)
 #pragma unroll
@@ -273,168 +338,254 @@ void ba_gschur(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const
         return;
     }
 
-    const int dp = (dim + 15) & ~15, nt = dp >> 4, ntiles = nt * (nt + 1) / 2;
-    f64x4 acc[MAXT];
-    int ti[MAXT], tj[MAXT];
+    BA_T0();
+    const int dp = (dim + 15) & ~15, nt = dp >> 4, HS = gs_hs(dp);
+    const int wreg = gs_wreg(K, dp);
+    double* part = gl + (size_t)w * wreg;            // [64][NPF] partials, then the H columns [4][HS]
+    double* Hb = part;
+    double* pw = part + wreg - WB_PTS * PD;           // [WB_PTS][PD] point data
+    constexpr int NTT = NT * (NT + 1) / 2;            // upper tiles (NT = dp_max / 16 of the launch)
+    f64x4 acc[NTT];
 #pragma unroll
-    for (int i = 0; i < MAXT; ++i) {
-        acc[i] = f64x4{0.0, 0.0, 0.0, 0.0};
-        int tt = w + 4 * i, I = 0;
-        while (tt >= nt - I && I < nt) { tt -= nt - I; ++I; }
-        ti[i] = I; tj[i] = I + tt;                 // valid when w + 4i < ntiles
-    }
-    double racc = 0.0;                             // rhs row tid (< dim)
-    const int np = G.p1 - G.p0;
-    for (int c = 0; c < G.nch; ++c) {
-        const Chunk ch = chk[G.ch0 + c];
-        stage_copy<JS / 2>(reinterpret_cast<double2*>(stg), reinterpret_cast<const double2*>(J + (size_t)ch.o0 * JS),
-                           (ch.o1 - ch.o0) * (JS / 2));   // the chunk's J records -> LDS (coalesced)
-        __syncthreads();
-        const int a = tid, o = ch.o0 + a;
-        const bool ov = o < ch.o1;
-        // B2: one thread per point of the chunk: E, g, Wi; M, t, Hi
-        if (tid >= ch.q0 && tid < ch.q1) {
-            const int p = G.p0 + tid;
-            const int a0 = pt_start[p] - ch.o0, a1 = pt_start[p + 1] - ch.o0;
-            const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
-            double E[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0}, Wi[3 * K];
+    for (int t = 0; t < NTT; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+    double racc[NT] = {};
+    // The group's batch descriptors go to LDS once, so the batch loop issues no dependent loads.
+    // Software pipeline: every global load of batch bi + 4 (this lane's observation: its J record,
+    // point and camera slot; this lane's point: its observation range, colsq and scale) is issued
+    // right after batch bi has consumed its own, before the plt stores; the SYRK rounds in between
+    // touch only LDS and registers, so nothing waits for those loads until the next batch.
+    Batch* bl = reinterpret_cast<Batch*>(gl + 4 * (size_t)wreg);
+    for (int i = tid; i < G.nb; i += 256) bl[i] = bat[G.b0 + i];
+    __syncthreads();
+    constexpr int JS = jst(K);
+    double2 pre[JS / 2];
+    int pre_q = 0, pre_lc = 0, pre_a0 = 0, pre_a1 = 0, pre_p = 0, pre_c = 0;
+    double pre_cs[3] = {0, 0, 0}, pre_sp[3] = {0, 0, 0};
+    auto prefetch = [&](int bi) {
+        if (bi >= G.nb) return;
+        const Batch Bn = bl[bi];
+        const int on = Bn.o0 + l;
+        if (on < Bn.o1) {
+            pre_p = obs_point[on];
+            pre_q = pre_p - Bn.p0;
+            pre_lc = obs_lc[on];
+            if (SCALEJ) pre_c = obs_cam[on];
+            const double2* s2 = reinterpret_cast<const double2*>(J + (size_t)on * JS);
 #pragma unroll
-            for (int i = 0; i < 3 * K; ++i) Wi[i] = 0.0;
-            for (int b = a0; b < a1; ++b) {
-                const double* s_ = stg + b * JS;
-                double je[2][3], ji[2][K];
+            for (int i = 0; i < JS / 2; ++i) pre[i] = s2[i];
+        }
+        if (l < Bn.p1 - Bn.p0) {
+            const int p = Bn.p0 + l;
+            pre_a0 = pt_start[p] - Bn.o0;
+            pre_a1 = pt_start[p + 1] - Bn.o0;
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
+            for (int i = 0; i < 3; ++i) { pre_cs[i] = colsq[3 * (size_t)p + i]; pre_sp[i] = scale[3 * (size_t)p + i]; }
+        }
+    };
+    prefetch(w);
+    for (int bi = w; bi < G.nb; bi += 4) {
+        const Batch B = bl[bi];
+        const int o = B.o0 + l, np = B.p1 - B.p0;
+        const bool ov = o < B.o1;
+        double W[3][6];
+        const int lc = pre_lc, q = pre_q;
+        if (ov) {
+            JRec<K> R;
+            {
+                double v[JS];
 #pragma unroll
-                    for (int i = 0; i < 3; ++i) je[j][i] = s_[2 + 3 * j + i] * sp[i];
+                for (int i = 0; i < JS / 2; ++i) { v[2 * i] = pre[i].x; v[2 * i + 1] = pre[i].y; }
+                if (SCALEJ) {   // J_s = J diag(scale), stored back once
+                    const size_t ne = 3 * (size_t)P;
+                    const double* sp = scale + 3 * (size_t)pre_p;
+                    const double* sc = scale + ne + 6 * (size_t)pre_c;
+                    const double* si = scale + ne + 6 * (size_t)C;
 #pragma unroll
-                    for (int i = 0; i < K; ++i) ji[j][i] = s_[20 + K * j + i] * si[i];
+                    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) v[2 + 3 * j + i] *= sp[i];
+#pragma unroll
+                        for (int i = 0; i < 6; ++i) v[8 + 6 * j + i] *= sc[i];
+#pragma unroll
+                        for (int i = 0; i < K; ++i) v[20 + K * j + i] *= si[i];
+                    }
+                    double2* d2 = reinterpret_cast<double2*>(const_cast<double*>(J) + (size_t)o * JS);
+#pragma unroll
+                    for (int i = 0; i < JS / 2; ++i) d2[i] = make_double2(v[2 * i], v[2 * i + 1]);
                 }
-                const double r0 = s_[0], r1 = s_[1];
-#pragma unroll
-                for (int u = 0; u < 3; ++u) {
-#pragma unroll
-                    for (int v = 0; v < 3; ++v) E[u * 3 + v] += je[0][u] * je[0][v] + je[1][u] * je[1][v];
-                    g[u] += je[0][u] * r0 + je[1][u] * r1;
-#pragma unroll
-                    for (int i = 0; i < K; ++i) Wi[u * K + i] += je[0][u] * ji[0][i] + je[1][u] * ji[1][i];
-                }
+                load_rec<K>(v, R);
             }
+            double* pt = part + l * NPF;
+            int e = 0;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) E[4 * i] += dsq(colsq[3 * (size_t)p + i], sp[i], dmin, dmax, radius);
-            double M[6];
-            if (!chol3_inv(E, M)) {
+            for (int u = 0; u < 3; ++u)
+#pragma unroll
+                for (int v = u; v < 3; ++v) pt[e++] = R.je[0][u] * R.je[0][v] + R.je[1][u] * R.je[1][v];
+#pragma unroll
+            for (int u = 0; u < 3; ++u) pt[6 + u] = R.je[0][u] * R.r[0] + R.je[1][u] * R.r[1];
+#pragma unroll
+            for (int u = 0; u < 3; ++u)
+#pragma unroll
+                for (int i = 0; i < K; ++i) pt[9 + u * K + i] = R.je[0][u] * R.ji[0][i] + R.je[1][u] * R.ji[1][i];
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int d = 0; d < 6; ++d) W[a][d] = R.je[0][a] * R.jc[0][d] + R.je[1][a] * R.jc[1][d];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        BA_STAMP(3);
+        double Mq[6] = {0, 0, 0, 0, 0, 0}, tq[3] = {0, 0, 0};
+        if (l < np) {   // lane = point
+            const int a0 = pre_a0, a1 = pre_a1;
+            double E6[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0}, V[3 * K];
+#pragma unroll
+            for (int i = 0; i < 3 * K; ++i) V[i] = 0.0;
+            for (int b = a0; b < a1; ++b) {
+                const double* pt = part + b * NPF;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) E6[i] += pt[i];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) g[i] += pt[6 + i];
+#pragma unroll
+                for (int i = 0; i < 3 * K; ++i) V[i] += pt[9 + i];
+            }
+            double E[9] = {E6[0], E6[1], E6[2], E6[1], E6[3], E6[4], E6[2], E6[4], E6[5]};
+#pragma unroll
+            for (int i = 0; i < 3; ++i) E[4 * i] += dsq(pre_cs[i], pre_sp[i], dmin, dmax, radius);
+            if (!chol3_inv(E, Mq)) {
                 atomicOr(fail, 1);
 #pragma unroll
-                for (int i = 0; i < 6; ++i) M[i] = 0.0;
+                for (int i = 0; i < 6; ++i) Mq[i] = 0.0;
             }
-            double* q_ = pd + tid * PD;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) { q_[i] = M[i]; plt[9 * (size_t)p + i] = M[i]; }
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                double t = 0.0;
+                tq[k] = 0.0;
 #pragma unroll
-                for (int j = 0; j <= k; ++j) t += mlo(M, k, j) * g[j];
-                q_[6 + k] = t;
-                plt[9 * (size_t)p + 6 + k] = t;
+                for (int j = 0; j <= k; ++j) tq[k] += mlo(Mq, k, j) * g[j];
             }
+            double* pq = pw + l * PD;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) pq[i] = Mq[i];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) pq[6 + k] = tq[k];
 #pragma unroll
             for (int i = 0; i < K; ++i)
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     double h = 0.0;
 #pragma unroll
-                    for (int j = 0; j <= k; ++j) h += mlo(M, k, j) * Wi[j * K + i];
-                    q_[9 + 3 * i + k] = h;
+                    for (int j = 0; j <= k; ++j) h += mlo(Mq, k, j) * V[j * K + i];
+                    pq[9 + 3 * i + k] = h;
                 }
         }
-        __syncthreads();   // pd complete
-        // B3: one thread per observation: H_o = (M_p W_o)^T (6x3), W_o = Je_o^T Jc_o, from the staged record
-        double H[6][3];
-        int q = 0, lc = 0;
-        if (ov) {
-            const int p = obs_point[o], cm = obs_cam[o];
-            q = p - G.p0;
-            lc = obs_lc[o];
-            const double* rr = stg + (size_t)a * JS;
-            double je[2][3], jc[2][6];
+        prefetch(bi + 4);
+        if (l < np) {   // after the prefetch: a later wait for its loads does not wait for these stores
+            const int p = B.p0 + l;
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
+            for (int i = 0; i < 6; ++i) plt[9 * (size_t)p + i] = Mq[i];
 #pragma unroll
-                for (int i = 0; i < 3; ++i) je[j][i] = rr[2 + 3 * j + i] * scale[3 * (size_t)p + i];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) jc[j][i] = rr[8 + 6 * j + i] * scale[ne + 6 * (size_t)cm + i];
-            }
-            const double* M = pd + q * PD;
-#pragma unroll
-            for (int d = 0; d < 6; ++d) {
-                double Wd[3];
-#pragma unroll
-                for (int j = 0; j < 3; ++j) Wd[j] = je[0][j] * jc[0][d] + je[1][j] * jc[1][d];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    double h = 0.0;
-#pragma unroll
-                    for (int j = 0; j <= k; ++j) h += mlo(M, k, j) * Wd[j];
-                    H[d][k] = h;
-                }
-            }
+            for (int k = 0; k < 3; ++k) plt[9 * (size_t)p + 6 + k] = tq[k];
         }
-        __syncthreads();   // every staged record read: A reuses the buffer
-        // SYRK over sub-batches of SBP points: A[row][3s + k] = H_p[row][k]
-        for (int sb = ch.q0; sb < ch.q1; sb += SBP) {
-            for (int e = tid; e < dp * ALD; e += blockDim.x) A[e] = 0.0;
-            __syncthreads();
-            if (ov && q >= sb && q < sb + SBP) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        BA_STAMP(4);
+        for (int r0 = 0; r0 < np; r0 += 4) {
+            for (int e = l; e < 4 * HS; e += 64) Hb[e] = 0.0;   // partials are dead: overlay
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (ov && q >= r0 && q < r0 + 4) {   // Z_o = (M_q W_o)^T: the observation's 6 camera rows of H_q
+                const double* pq = pw + q * PD;
+                double* h = Hb + (q - r0) * HS + 3 * (6 * lc);
 #pragma unroll
                 for (int d = 0; d < 6; ++d)
 #pragma unroll
-                    for (int k = 0; k < 3; ++k) A[(6 * lc + d) * ALD + 3 * (q - sb) + k] = H[d][k];
+                    for (int k = 0; k < 3; ++k) {
+                        double z = 0.0;
+#pragma unroll
+                        for (int j = 0; j <= k; ++j) z += mlo(pq, k, j) * W[j][d];
+                        h[3 * d + k] = z;
+                    }
             }
-            if (tid >= sb && tid < min(sb + SBP, ch.q1)) {
-                const double* q_ = pd + tid * PD;
+            if (m16 < K && r0 + kk < np) {   // intrinsics rows of the round's points
+                const double* pq = pw + (r0 + kk) * PD;
 #pragma unroll
-                for (int i = 0; i < K; ++i)
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) A[(6 * G.u + i) * ALD + 3 * (tid - sb) + k] = q_[9 + 3 * i + k];
+                for (int k = 0; k < 3; ++k) Hb[kk * HS + 3 * (6 * G.u + m16) + k] = pq[9 + 3 * m16 + k];
             }
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < MAXT; ++i) {
-                if (w + 4 * i >= ntiles) continue;
-                const double* Ar = A + (16 * ti[i] + m16) * ALD;
-                const double* Br = A + (16 * tj[i] + m16) * ALD;
-#pragma unroll
-                for (int st = 0; st < SBK / 4; ++st)
-                    acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(Ar[4 * st + kq], Br[4 * st + kq], acc[i], 0, 0, 0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            BA_STAMP(5);
+            double hv[NT][3];
+            double tk[3] = {0, 0, 0};
+            if (r0 + kk < np) {
+                const double* pq = pw + (r0 + kk) * PD;
+                tk[0] = pq[6]; tk[1] = pq[7]; tk[2] = pq[8];
             }
-            if (tid < dim) {
-                const int sn = min(SBP, ch.q1 - sb);
-                for (int s = 0; s < sn; ++s) {
-                    const double* q_ = pd + (sb + s) * PD;
-                    racc += A[tid * ALD + 3 * s] * q_[6] + A[tid * ALD + 3 * s + 1] * q_[7] + A[tid * ALD + 3 * s + 2] * q_[8];
+#pragma unroll
+            for (int I = 0; I < NT; ++I)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) hv[I][c] = I < nt ? Hb[kk * HS + 3 * (16 * I + m16) + c] : 0.0;
+#pragma unroll
+            for (int I = 0, t = 0; I < NT; ++I)
+#pragma unroll
+                for (int Jt = I; Jt < NT; ++Jt, ++t) {
+                    if (Jt >= nt) continue;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(hv[I][c], hv[Jt][c], acc[t], 0, 0, 0);
                 }
-            }
-            __syncthreads();
+#pragma unroll
+            for (int I = 0; I < NT; ++I) racc[I] += hv[I][0] * tk[0] + hv[I][1] * tk[1] + hv[I][2] * tk[2];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
+        BA_STAMP(0);
     }
-    // -sum H H^T (full square) and -sum H t
+    // rhs: the 4 points of a round sit in the 4 lane groups: sum them (fixed order)
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+        const double a = racc[I] + __shfl_xor(racc[I], 16);   // lanes m, m+16 | m+32, m+48
+        racc[I] = a + __shfl_xor(a, 32);
+    }
+    // combine the 4 waves' tiles and rhs in wave order: [dp][dp + 1] | rhs[dp]
+    __syncthreads();
+    double* Sb = gl;
+    double* Rb = gl + dp * (dp + 1);
+    for (int ww = 0; ww < 4; ++ww) {
+        if (w == ww) {
+#pragma unroll
+            for (int I = 0, t = 0; I < NT; ++I)
+#pragma unroll
+                for (int Jt = I; Jt < NT; ++Jt, ++t) {
+                    if (Jt >= nt) continue;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = 16 * I + kk + 4 * r, col = 16 * Jt + m16;
+                        double* d = Sb + row * (dp + 1) + col;
+                        *d = ww == 0 ? acc[t][r] : *d + acc[t][r];
+                    }
+                }
+            if (l < 16)
+#pragma unroll
+                for (int I = 0; I < NT; ++I)
+                    if (I < nt) Rb[16 * I + l] = ww == 0 ? racc[I] : Rb[16 * I + l] + racc[I];
+        }
+        __syncthreads();
+    }
+    BA_STAMP(1);
+    // -sum H H^T (full square from the upper tiles) and -sum H t
     double* Sg = sg + G.sg_off;
-#pragma unroll
-    for (int i = 0; i < MAXT; ++i) {
-        if (w + 4 * i >= ntiles) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = 16 * ti[i] + trow(r), col = 16 * tj[i] + tcol();
-            if (row < dim && col < dim) {
-                Sg[(size_t)row * dim + col] = -acc[i][r];
-                Sg[(size_t)col * dim + row] = -acc[i][r];
-            }
-        }
+    for (int e = tid; e < dim * dim; e += 256) {
+        const int r = e / dim, c = e % dim;
+        Sg[e] = -(r <= c ? Sb[r * (dp + 1) + c] : Sb[c * (dp + 1) + r]);
     }
-    if (tid < dim) rg[G.rg_off + tid] = -racc;
-    (void)np;
+    if (tid < dim) rg[G.rg_off + tid] = -Rb[tid];
+    BA_STAMP(2);
+    BA_FLUSH(0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -580,7 +731,7 @@ __device__ __forceinline__ int field_of(int r, int c) {   // Gram entry (r <= c)
 }
 
 // ba_glin: residuals + Jacobian at xp (x or the candidate) for the group's observations.
-// Writes the J records, per point colsq / grad (unscaled), per (group, camera) partials (gpart:
+// Writes the J records (scaled by jscale when given: the solve's Jacobi scale), per point colsq / grad (unscaled), per (group, camera) partials (gpart:
 // the per-camera Gram matrices of the feature rows on the fp64 matrix cores, rows of one camera
 // contiguous and zero-padded by the host-built layout), and the group's cost, sum xp^2 (its
 // points) and max |grad| partials.  Big groups: feature rows in observation order and a scalar
@@ -592,9 +743,9 @@ __global__ __launch_bounds__(256)
 void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const int* __restrict__ lcrow,
              const short* __restrict__ obs_lc, const short* __restrict__ obs_row, const int* __restrict__ obs_point,
              const int* __restrict__ obs_cam, const double* __restrict__ obs_xy, const int* __restrict__ pt_start,
-             double cx, double cy, int P, int C, const double* __restrict__ xp, double* __restrict__ J,
-             double* __restrict__ colsq, double* __restrict__ grad, double* __restrict__ gpart,
-             double* __restrict__ gpl) {
+             double cx, double cy, int P, int C, const double* __restrict__ xp, const double* __restrict__ jscale,
+             double* __restrict__ J, double* __restrict__ colsq, double* __restrict__ grad,
+             double* __restrict__ gpart, double* __restrict__ gpl) {
     extern __shared__ __attribute__((aligned(16))) double gl[];
     constexpr int JS = jst(K), NCP = ncp(K), N = 9 + K, NF = nfeat(K);
     __shared__ double sh[8];
@@ -644,9 +795,28 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
 #pragma unroll
                 for (int i = 0; i < K; ++i) rec[20 + K * j + i] = res[j].v[9 + i];
             }
-            double2* dst = reinterpret_cast<double2*>(J + (size_t)o * JS);
+            {   // the stored record is Jacobi-scaled (load_rec); the partials below use the unscaled one
+                double sj[JS];
 #pragma unroll
-            for (int i = 0; i < JS / 2; ++i) dst[i] = make_double2(rec[2 * i], rec[2 * i + 1]);
+                for (int i = 0; i < JS; ++i) sj[i] = rec[i];
+                if (jscale) {
+                    const double* sp = jscale + 3 * (size_t)p;
+                    const double* sc = jscale + 3 * (size_t)P + 6 * (size_t)cm;
+                    const double* si = jscale + 3 * (size_t)P + 6 * (size_t)C;
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) sj[2 + 3 * j + i] *= sp[i];
+#pragma unroll
+                        for (int i = 0; i < 6; ++i) sj[8 + 6 * j + i] *= sc[i];
+#pragma unroll
+                        for (int i = 0; i < K; ++i) sj[20 + K * j + i] *= si[i];
+                    }
+                }
+                double2* dst = reinterpret_cast<double2*>(J + (size_t)o * JS);
+#pragma unroll
+                for (int i = 0; i < JS / 2; ++i) dst[i] = make_double2(sj[2 * i], sj[2 * i + 1]);
+            }
 #pragma unroll
             for (int i = 0; i < 6; ++i) jer[a * 8 + i] = rec[2 + i];
             jer[a * 8 + 6] = rec[0];
@@ -883,25 +1053,24 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
 // ba_gupdate: per group, from sol_f (scaled camera/intrinsics solution) and the stored M, t:
 // sol_e = M^T (t - M y), y = sum_o Je_o^T ([Jc_o | Ji_o] sol_f); step = -sol; candidate points
 // cand = x + step * scale; ||x - cand||^2 and the model cost change sum m (r + m / 2), m = J_s step_s.
-// Dynamic LDS: yv[GCH][3] | pst[GPTS][3].
+// One thread per observation of a chunk: its J record is loaded straight into registers (13
+// independent 16-B loads, kept across the two barriers of the chunk), so a chunk costs one memory
+// latency, not a staging round trip; LDS holds only the per-observation y terms and point steps.
+
 template <int K>
 __global__ __launch_bounds__(256)
 void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const int* __restrict__ obs_point,
                 const int* __restrict__ obs_cam, const int* __restrict__ pt_start, const double* __restrict__ J,
                 const double* __restrict__ scale, const double* __restrict__ plt, const double* __restrict__ sol_f,
                 int P, int C, const double* __restrict__ x, double* __restrict__ cand, double* __restrict__ gpl) {
-    extern __shared__ __attribute__((aligned(16))) double gl[];
+    __shared__ double yv[GCH * 3];
+    __shared__ double pst[GPTS * 3];
     __shared__ double sh[8];
-    constexpr int JS = jst(K);
-    double* stg = gl;                 // the chunk's J records
-    double* yv = stg + GCH * JS;
-    double* pst = yv + GCH * 3;
     const Grp G = grp[blockIdx.x];
     const int tid = threadIdx.x;
-    const size_t ne = 3 * (size_t)P, ni = ne + 6 * (size_t)C;
-    double si[K], soli[K];
+        double soli[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i) { si[i] = scale[ni + i]; soli[i] = sol_f[6 * (size_t)C + i]; }
+    for (int i = 0; i < K; ++i) soli[i] = sol_f[6 * (size_t)C + i];
     double model = 0.0, sn = 0.0;
     double ybig[3] = {0, 0, 0};
     const int nchunks = G.big ? (G.o1 - G.o0 + GCH - 1) / GCH : G.nch;
@@ -911,9 +1080,6 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
             Chunk ch;
             if (G.big) { ch.o0 = G.o0 + c * GCH; ch.o1 = min(G.o1, ch.o0 + GCH); ch.q0 = 0; ch.q1 = 1; }
             else ch = chk[G.ch0 + c];
-            stage_copy<JS / 2>(reinterpret_cast<double2*>(stg), reinterpret_cast<const double2*>(J + (size_t)ch.o0 * JS),
-                               (ch.o1 - ch.o0) * (JS / 2));
-            __syncthreads();
             const int a = tid, o = ch.o0 + a;
             const bool ov = o < ch.o1;
             JRec<K> R;
@@ -923,11 +1089,7 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
                 const int p = obs_point[o];
                 cm = obs_cam[o];
                 q = p - G.p0;
-                const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
-                double sc[6];
-#pragma unroll
-                for (int d = 0; d < 6; ++d) sc[d] = scale[ne + 6 * (size_t)cm + d];
-                load_rec<K>(stg + (size_t)a * JS, sp, sc, si, R);
+                load_jrec_v<K>(J, o, R);
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
 #pragma unroll
@@ -996,7 +1158,7 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
                     sn += isfinite(dd) ? dd * dd : INFINITY;
                 }
             }
-            __syncthreads();
+            __syncthreads();   // yv of the next chunk is written after this chunk's point phase
             if (pass == 1 && ov) {
                 const double* ps = pst + (G.big ? 0 : q) * 3;
 #pragma unroll
@@ -1009,7 +1171,7 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
                     model += mm * (R.r[j] + mm / 2.0);
                 }
             }
-            __syncthreads();
+            // no barrier: the next chunk's pst writes come after its first barrier
         }
     }
     const double sm = block_sum(model, sh);

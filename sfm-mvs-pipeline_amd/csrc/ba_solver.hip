@@ -80,9 +80,9 @@ struct sfmx_ba_ctx {
     sfmx_allreduce_fn ar = nullptr;
     void* ar_user = nullptr;
     // topology: groups, chunks, group cameras, local camera per observation, assembly tasks
-    int ngroups = 0, ntasks = 0, nslots = 0, stage_n = 0;
-    size_t lds_schur = 0, lds_lin = 0, lds_upd = 0;
-    Buf obs_point, obs_cam, obs_xy, pt_start, grp, chk, gcam, obs_lc, obs_row, lcrow, tasks, ents, cref_start, cref;
+    int ngroups = 0, ntasks = 0, nslots = 0, gs_nt = 4;   // gs_nt: ba_gschur specialisation, dp_max / 16
+    size_t lds_schur = 0, lds_lin = 0;
+    Buf obs_point, obs_cam, obs_xy, pt_start, grp, chk, bat, gcam, obs_lc, obs_row, lcrow, tasks, ents, cref_start, cref;
     // factorization plan of the reduced camera system (built at the first run, from the camera
     // co-visibility of every rank: the layout of S must be the same on all of them)
     std::vector<char> adj;       // local camera co-visibility, C x C
@@ -93,14 +93,14 @@ struct sfmx_ba_ctx {
     // state (the *2 buffers hold the candidate's linearization until the step is accepted)
     Buf x, cand, scale, colsq, colsq2, grad, grad2, J, J2, camsum, camsum2, plt, sg, rg, hbig, gpart, gpl, scal,
         SR, sol, failf, partA;
-    bool scaled = false;
+    bool scaled = false, j_scaled = false;   // j_scaled: the records in J are J_s (ba_gschur SCALEJ)
     // locality order: internal point p' is caller point pperm[p']; internal
     // observation o' is caller observation operm[o'] (point-major)
     std::vector<int> pperm, operm;
     double phase_ms[4] = {0, 0, 0, 0};
     hipEvent_t ev[6] = {};
     ~sfmx_ba_ctx() {
-        Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
+        Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
                       &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
@@ -170,8 +170,9 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double
         hipLaunchKernelGGL(ba_glin<K>, dim3(c->ngroups), dim3(256), c->lds_lin, c->st, c->grp.as<Grp>(),
                            c->chk.as<Chunk>(), c->lcrow.as<int>(), c->obs_lc.as<short>(), c->obs_row.as<short>(),
                            c->obs_point.as<int>(), c->obs_cam.as<int>(),
-                           c->obs_xy.as<double>(), c->pt_start.as<int>(), c->cx, c->cy, c->P, c->C, xp, Jo, colsq_o,
-                           grad_o, c->gpart.as<double>(), c->gpl.as<double>());
+                           c->obs_xy.as<double>(), c->pt_start.as<int>(), c->cx, c->cy, c->P, c->C, xp,
+                           c->scaled ? c->scale.as<double>() : nullptr, Jo, colsq_o, grad_o, c->gpart.as<double>(),
+                           c->gpl.as<double>());
     hipLaunchKernelGGL(ba_camred<K>, dim3(c->C + K * (K + 1) / 2 + K), dim3(128), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
                        c->cref.as<int>(), c->gpart.as<double>(), camsum_o);
     HIPCHK(hipGetLastError());
@@ -229,12 +230,19 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     const sfmx_ba_options& o = c->opt;
     HIPCHK(hipMemsetAsync(fl, 0, sizeof(int), c->st));
     HIPCHK(hipEventRecord(c->ev[0], c->st));
-    if (c->ngroups > 0)
-        hipLaunchKernelGGL(ba_gschur<K>, dim3(c->ngroups), dim3(256), c->lds_schur, c->st, c->grp.as<Grp>(),
-                           c->chk.as<Chunk>(), c->gcam.as<int>(), c->obs_lc.as<short>(), c->obs_point.as<int>(),
-                           c->obs_cam.as<int>(), c->pt_start.as<int>(), c->J.as<double>(), c->scale.as<double>(),
-                           c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, c->P, C, c->stage_n,
-                           c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl);
+    if (c->ngroups > 0) {
+#define GSCHUR(NTV) if (sj) GSCHUR2(NTV, true); else GSCHUR2(NTV, false)
+#define GSCHUR2(NTV, SJ) hipLaunchKernelGGL((ba_gschur<K, NTV, SJ>), dim3(c->ngroups), dim3(256), c->lds_schur, c->st,     \
+                           c->grp.as<Grp>(), c->bat.as<Batch>(), c->gcam.as<int>(), c->obs_lc.as<short>(),             \
+                           c->obs_point.as<int>(), c->obs_cam.as<int>(), c->pt_start.as<int>(), c->J.as<double>(),      \
+                           c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, \
+                           c->P, C, c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl)
+        const bool sj = !c->j_scaled;   // the first step of a solve scales J in place
+        switch (c->gs_nt) { case 1: GSCHUR(1); break; case 2: GSCHUR(2); break; case 3: GSCHUR(3); break; default: GSCHUR(4); }
+#undef GSCHUR2
+#undef GSCHUR
+        c->j_scaled = true;
+    }
     HIPCHK(hipMemsetAsync(S, 0, sizeof(double) * c->sr_count, c->st));
     hipLaunchKernelGGL(ba_assemble, dim3(c->ntasks), dim3(64), 0, c->st, c->tasks.as<ATask>(), c->ents.as<AEnt>(),
                        c->sg.as<double>(), c->hbig.as<double>(), c->rg.as<double>(), K, c->camrow.as<int>(), npad, S,
@@ -251,7 +259,7 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     RC(solve_reduced<RW>(c, sol + c->ne));
     HIPCHK(hipEventRecord(c->ev[2], c->st));
     if (c->ngroups > 0)
-        hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups), dim3(256), c->lds_upd, c->st, c->grp.as<Grp>(),
+        hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups), dim3(256), 0, c->st, c->grp.as<Grp>(),
                            c->chk.as<Chunk>(), c->obs_point.as<int>(), c->obs_cam.as<int>(), c->pt_start.as<int>(),
                            c->J.as<double>(), c->scale.as<double>(), c->plt.as<double>(), sol + c->ne, c->P, C,
                            c->x.as<double>(), c->cand.as<double>(), c->gpl.as<double>());
@@ -353,9 +361,12 @@ int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace,
     double v[SC_N];
     RC(lin_at<K>(c, c->x.as<double>(), c->J.as<double>(), c->colsq.as<double>(), c->grad.as<double>(),
                  c->camsum.as<double>(), false, v));
-    if (o.jacobi_scaling)
+    if (o.jacobi_scaling) {
         hipLaunchKernelGGL(ba_scale, dim3(nblk(c->n)), dim3(256), 0, c->st, (int)c->n, c->colsq.as<double>(),
                            c->scale.as<double>());
+    }
+    // the iteration-0 records were written unscaled: the first step's ba_gschur scales them in place
+    c->j_scaled = !o.jacobi_scaling;
     c->scaled = true;
     HIPCHK(hipEventRecord(c->ev[5], c->st));
     HIPCHK(hipEventSynchronize(c->ev[5]));
@@ -493,6 +504,7 @@ void locality_order(const sfmx_ba_problem* pb, std::vector<int>& pperm, std::vec
 struct Topology {
     std::vector<Grp> grp;
     std::vector<Chunk> chk;
+    std::vector<Batch> bat;
     std::vector<int> gcam, cref_start, cref, lcrow;
     std::vector<short> obs_lc, obs_row;
     std::vector<ATask> tasks;
@@ -517,6 +529,8 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
         tp.rg_total += dim;
         G.ch0 = (int)tp.chk.size();
         G.nch = 0;
+        G.b0 = (int)tp.bat.size();
+        G.nb = 0;
         if (big) {
             G.h_off = tp.h_total;
             tp.h_total += (long long)dim * 3;
@@ -526,6 +540,15 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
             tp.sg_total += (long long)dim * dim;
             G.h_off = 0;
             tp.dp_max = std::max(tp.dp_max, (dim + 15) & ~15);
+            // ba_gschur wave batches: whole points, <= WB_OBS observations, <= WB_PTS points
+            for (int q = p0; q < p1;) {
+                Batch b{pt_start[q], pt_start[q], q, q};
+                while (q < p1 && pt_start[q + 1] - b.o0 <= WB_OBS && q - b.p0 < WB_PTS) ++q;
+                b.o1 = pt_start[q];
+                b.p1 = q;
+                tp.bat.push_back(b);
+                ++G.nb;
+            }
             // chunks of whole points, <= GCH observations; feature rows sorted by local camera
             // (observation order inside a camera), each camera's rows zero-padded to a multiple of 4
             int q = p0;
@@ -566,7 +589,7 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
         std::sort(pc.begin(), pc.end());
         const bool dup = std::adjacent_find(pc.begin(), pc.end()) != pc.end();
         pc.erase(std::unique(pc.begin(), pc.end()), pc.end());
-        const bool big = m > GCH || (int)pc.size() > UMAX || dup;
+        const bool big = m > WB_OBS || 6 * (int)pc.size() + K > GDPMAX || dup;
         if (big) {
             if (p > g_p0) add_group(g_p0, p, cur, false);
             add_group(p, p + 1, pc, true);
@@ -575,7 +598,7 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
         }
         uni.clear();
         std::set_union(cur.begin(), cur.end(), pc.begin(), pc.end(), std::back_inserter(uni));
-        if (p > g_p0 && (g_obs + m > GOBS || p - g_p0 + 1 > GPTS || (int)uni.size() > UMAX)) {
+        if (p > g_p0 && (g_obs + m > GOBS || p - g_p0 + 1 > GPTS || 6 * (int)uni.size() + K > GDPMAX)) {
             add_group(g_p0, p, cur, false);
             g_p0 = p; g_obs = 0; cur = pc;
         } else {
@@ -690,17 +713,24 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
     c->ngroups = (int)tp.grp.size();
     c->ntasks = (int)tp.tasks.size();
     c->nslots = (int)tp.gcam.size();
-    const int JS = jst(K);
-    c->stage_n = std::max(GCH * JS, tp.dp_max * ALD);
-    c->lds_schur = sizeof(double) * ((size_t)c->stage_n + (size_t)GPTS * (9 + 3 * K));
+    {
+        const size_t wreg = K == 1 ? gs_wreg(1, tp.dp_max) : K == 3 ? gs_wreg(3, tp.dp_max) : gs_wreg(7, tp.dp_max);
+        size_t nb_max = 0;   // batch descriptors of one group in LDS (2 doubles each)
+        for (const Grp& G : tp.grp) nb_max = std::max<size_t>(nb_max, G.nb);
+        c->lds_schur = sizeof(double) *
+                       std::max<size_t>({4 * wreg + 2 * nb_max, (size_t)tp.dp_max * (tp.dp_max + 1) + tp.dp_max, 16});
+        c->gs_nt = std::min(4, std::max(1, tp.dp_max / 16));
+    }
     c->lds_lin = sizeof(double) * ((size_t)GROWS * nfeat(K) + GCH * 8) + sizeof(short) * GCH;
-    c->lds_upd = sizeof(double) * ((size_t)GCH * JS + GCH * 3 + GPTS * 3);
     {
         hipError_t e = hipSuccess;
 #define LDSATTR(KK)                                                                                                  \
-        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_gschur<KK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_schur); \
-        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_glin<KK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_lin);     \
-        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_gupdate<KK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_upd)
+        for (const void* f : {(const void*)ba_gschur<KK, 1, false>, (const void*)ba_gschur<KK, 2, false>,              \
+                              (const void*)ba_gschur<KK, 3, false>, (const void*)ba_gschur<KK, 4, false>,             \
+                              (const void*)ba_gschur<KK, 1, true>, (const void*)ba_gschur<KK, 2, true>,               \
+                              (const void*)ba_gschur<KK, 3, true>, (const void*)ba_gschur<KK, 4, true>})              \
+            if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_schur); \
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_glin<KK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_lin);    
         if (K == 1) { LDSATTR(1); } else if (K == 3) { LDSATTR(3); } else { LDSATTR(7); }
 #undef LDSATTR
         if (e != hipSuccess) return bail(fail(SFMX_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(e)));
@@ -708,7 +738,7 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
     hipStream_t st = c->st;
     int rc;
     if ((rc = upload(c->obs_point, rop, st)) || (rc = upload(c->obs_cam, roc, st)) || (rc = upload(c->obs_xy, rxy, st)) ||
-        (rc = upload(c->pt_start, pt_start, st)) || (rc = upload(c->grp, tp.grp, st)) || (rc = upload(c->chk, tp.chk, st)) ||
+        (rc = upload(c->pt_start, pt_start, st)) || (rc = upload(c->grp, tp.grp, st)) || (rc = upload(c->chk, tp.chk, st)) || (rc = upload(c->bat, tp.bat, st)) ||
         (rc = upload(c->gcam, tp.gcam, st)) || (rc = upload(c->obs_lc, tp.obs_lc, st)) ||
         (rc = upload(c->obs_row, tp.obs_row, st)) || (rc = upload(c->lcrow, tp.lcrow, st)) ||
         (rc = upload(c->tasks, tp.tasks, st)) || (rc = upload(c->ents, tp.ents, st)) ||
@@ -913,6 +943,17 @@ int sfmx_ba_jacobian(const sfmx_ba_problem* pb, int32_t device, double* r, doubl
     delete c;
     return rc;
 }
+
+#ifdef SFMX_BA_STAMPS
+// diagnostic build only: read and clear the phase cycle totals (ba_group.hpp BA_STAMP)
+int sfmx_ba_debug_stamps(unsigned long long* out, int32_t n) {
+    if (n > 64) n = 64;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sfmx::ba::g_ba_stamps), sizeof(unsigned long long) * n) != hipSuccess) return SFMX_EDEVICE;
+    std::vector<unsigned long long> z(64, 0);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(sfmx::ba::g_ba_stamps), z.data(), sizeof(unsigned long long) * 64) != hipSuccess) return SFMX_EDEVICE;
+    return n;
+}
+#endif
 
 int sfmx_pose_to_ceres(const double* Rt, double* pose) {
     if (!Rt || !pose) return fail(SFMX_EINVAL, "null");

@@ -1,0 +1,35 @@
+"""Phase cycle totals of the BA group kernels from the diagnostic stamp build
+(make -C sfm-mvs-pipeline_amd stamps -> lib/libsfmx_stamps.so; SFMX_BA_STAMPS, ba_group.hpp).
+Runs the C5 bench problem once and prints, per stamp slot, the s_memtime cycles of thread 0
+summed over workgroups and divided by the number of LM steps.  GPU box only (tooling)."""
+import ctypes as C
+import os
+import sys
+
+os.environ["SFMX_LIB_NAME"] = "libsfmx_stamps.so"
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "sfm-mvs-pipeline_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+from sfmx import ba, synth  # noqa: E402
+from sfmx._lib import lib  # noqa: E402
+
+NAMES = {0: "gschur round MFMA", 1: "gschur wave combine", 2: "gschur store", 3: "gschur obs phase",
+         4: "gschur point phase", 5: "gschur round H fill", 8: "glin lin+store",
+         9: "glin point+gram", 10: "glin epilogue",
+         16: "gupdate obs", 17: "gupdate point", 18: "gupdate model", 19: "gupdate epilogue"}
+prob = synth.ba_problem(200, 200_000)
+ctx = ba.BAContext(ba.BAProblem(**prob), ba.default_options())
+ctx.run(max_iterations=1)
+ctx.reset()
+f = lib.sfmx_ba_debug_stamps
+f.argtypes, f.restype = [C.POINTER(C.c_ulonglong), C.c_int32], C.c_int
+buf = (C.c_ulonglong * 64)()
+f(buf, 64)   # clear
+sm, _ = ctx.run()
+f(buf, 64)
+steps = sm["num_successful_steps"] + sm["num_unsuccessful_steps"] - 1
+print(f"LM steps {steps}; cycles per step (thread 0 of each workgroup, summed over workgroups):")
+for i, v in enumerate(buf):
+    if v:
+        print(f"  [{i:2d}] {NAMES.get(i, '?'):22s} {v / max(steps, 1) / 1e6:10.2f} Mcyc")

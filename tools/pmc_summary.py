@@ -1,16 +1,26 @@
 """Summarise tools/pmc_ba.sh / pmc_sift.sh passes: tools/pmc_summary.py DIR
 HBM bytes per launch = 2 x FETCH_SIZE (gfx950: FETCH_SIZE counts half of a wide streaming read,
-MI355X_MICROARCH.md HBM section) + WRITE_SIZE; FETCH/WRITE_SIZE are in KiB."""
+MI355X_MICROARCH.md HBM section) + WRITE_SIZE; FETCH/WRITE_SIZE are in KiB.  Wave-state fractions
+are of SQ_WAVE_CYCLES (WAIT_ANY: parked at s_waitcnt / barrier; WAIT_INST: issue stalls;
+ACTIVE: issuing); LDS conflict = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; MFMA busy =
+SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)."""
 import csv, collections, glob, sys
 D = sys.argv[1].rstrip("/") + "/"
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(D + "p*_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        agg[r["Kernel_Name"].split("(")[0][:48]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-print(f"{'kernel':48s} {'fetch2x MB':>10s} {'write MB':>9s} {'wait_any':>8s} {'active':>6s}")
+        agg[r["Kernel_Name"].split("(")[0][:40]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+print(f"{'kernel':40s} {'fetch2x MB':>10s} {'write MB':>9s} {'wait':>5s} {'winst':>5s} {'activ':>5s} "
+      f"{'valu/w':>7s} {'lds/w':>6s} {'vmem/w':>6s} {'ldsconf':>7s} {'mfma':>5s}")
 for k, v in agg.items():
     s = {c: sum(x) / len(x) for c, x in v.items()}
     fs = s.get("FETCH_SIZE", 0) * 2 * 1024 / 1e6
     ws = s.get("WRITE_SIZE", 0) * 1024 / 1e6
     wc = max(s.get("SQ_WAVE_CYCLES", 1), 1)
-    print(f"{k:48s} {fs:10.1f} {ws:9.1f} {s.get('SQ_WAIT_ANY', 0) / wc:8.2f} {s.get('SQ_ACTIVE_INST_ANY', 0) / wc:6.2f}")
+    nw = max(s.get("SQ_WAVES", 1), 1)
+    gui = s.get("GRBM_GUI_ACTIVE", 0)
+    mf = s.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (gui / 8 * 1024) if gui else 0
+    lc = s.get("SQ_LDS_BANK_CONFLICT", 0) / max(s.get("SQ_LDS_IDX_ACTIVE", 1), 1)
+    print(f"{k:40s} {fs:10.1f} {ws:9.1f} {s.get('SQ_WAIT_ANY', 0) / wc:5.2f} {s.get('SQ_WAIT_INST_ANY', 0) / wc:5.2f} "
+          f"{s.get('SQ_ACTIVE_INST_ANY', 0) / wc:5.2f} {s.get('SQ_INSTS_VALU', 0) / nw:7.0f} {s.get('SQ_INSTS_LDS', 0) / nw:6.0f} "
+          f"{s.get('SQ_INSTS_VMEM', 0) / nw:6.0f} {lc:7.2f} {mf:5.2f}")
