@@ -218,8 +218,11 @@ __host__ __device__ constexpr int gs_hs(int dp) { return 3 * dp + 2; }          
 __host__ __device__ constexpr int gs_wreg(int K, int dp) {                            // doubles per wave
     return (WB_OBS * gs_npf(K) > 4 * gs_hs(dp) ? WB_OBS * gs_npf(K) : 4 * gs_hs(dp)) + WB_PTS * gs_pd(K);
 }
+#ifndef GSCHUR_WAVES
+#define GSCHUR_WAVES 2   // waves per SIMD the register budget targets (A/B: -DGSCHUR_WAVES=3)
+#endif
 template <int K, int NT, bool SCALEJ>
-__global__ __launch_bounds__(256, 2)
+__global__ __launch_bounds__(256, GSCHUR_WAVES)
 void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const int* __restrict__ gcam,
                const short* __restrict__ obs_lc, const int* __restrict__ obs_point, const int* __restrict__ obs_cam,
                const int* __restrict__ pt_start, const double* __restrict__ J, const double* __restrict__ scale,
@@ -739,7 +742,7 @@ __device__ __forceinline__ int field_of(int r, int c) {   // Gram entry (r <= c)
 // Dynamic LDS: G[max rows][NF] | jer[GCH][8] (je | r) | olc[GCH] (short).
 constexpr int GROWS = 2 * GCH + 3 * UMAX;   // feature rows of a chunk incl. per-camera padding
 template <int K>
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(256, 2)
 void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const int* __restrict__ lcrow,
              const short* __restrict__ obs_lc, const short* __restrict__ obs_row, const int* __restrict__ obs_point,
              const int* __restrict__ obs_cam, const double* __restrict__ obs_xy, const int* __restrict__ pt_start,
@@ -766,13 +769,37 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
     if (Gp.big)
         for (int i = tid; i < npart; i += blockDim.x) gpart[(size_t)Gp.cam_off * NCP + i] = 0.0;
     const int nchunks = Gp.big ? (Gp.o1 - Gp.o0 + GCH - 1) / GCH : Gp.nch;
+    BA_T0();
     for (int c = 0; c < nchunks; ++c) {
         Chunk ch;
         if (Gp.big) { ch.o0 = Gp.o0 + c * GCH; ch.o1 = min(Gp.o1, ch.o0 + GCH); ch.q0 = 0; ch.q1 = 0; ch.lc0 = 0; ch.nrows = 2 * (ch.o1 - ch.o0); }
         else ch = chk[Gp.ch0 + c];
         for (int e = tid; e < ch.nrows * NF; e += blockDim.x) G[e] = 0.0;   // padding rows stay zero
-        __syncthreads();
+        // every global load of the chunk goes out before its J stores: a wait for a load issued
+        // after 13 stores per lane would wait for the stores too (vmcnt counts both, in order)
         const int a = tid, o = ch.o0 + a;
+        const bool ptl = !Gp.big && tid >= ch.q0 && tid < ch.q1;
+        int pa0 = 0, pa1 = 0, orow = 0, olcv = 0;
+        if (ptl) {
+            const int p = Gp.p0 + tid;
+            pa0 = pt_start[p] - ch.o0;
+            pa1 = pt_start[p + 1] - ch.o0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) xn += pts[3 * (size_t)p + i] * pts[3 * (size_t)p + i];
+        }
+        int cr0[UMAX / 4], cr1[UMAX / 4];
+#pragma unroll
+        for (int i = 0; i < UMAX / 4; ++i) {
+            const int lc = w + 4 * i;
+            cr0[i] = cr1[i] = 0;
+            if (!Gp.big && lc < Gp.u) { cr0[i] = lcrow[ch.lc0 + lc]; cr1[i] = lcrow[ch.lc0 + lc + 1]; }
+        }
+        if (o < ch.o1) {
+            orow = Gp.big ? 2 * a : obs_row[o];
+            olcv = obs_lc[o];
+        }
+        __syncthreads();
+        BA_STAMP(0);
         if (o < ch.o1) {
             const int p = obs_point[o], cm = obs_cam[o];
             const double ox = obs_xy[2 * (size_t)o], oy = obs_xy[2 * (size_t)o + 1];
@@ -821,7 +848,7 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
             for (int i = 0; i < 6; ++i) jer[a * 8 + i] = rec[2 + i];
             jer[a * 8 + 6] = rec[0];
             jer[a * 8 + 7] = rec[1];
-            const int row = Gp.big ? 2 * a : obs_row[o];
+            const int row = orow;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 double* gr = G + (row + j) * NF;
@@ -831,16 +858,18 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
                 for (int i = 0; i < K; ++i) gr[6 + i] = rec[20 + K * j + i];
                 gr[6 + K] = rec[j];
             }
-            olc[a] = obs_lc[o];
+            olc[a] = (short)olcv;
             cost += res[0].a * res[0].a + res[1].a * res[1].a;
         }
+        BA_STAMP(1);
         __syncthreads();
+        BA_STAMP(2);
         const int no = ch.o1 - ch.o0;
         // per point: column norms and gradient of its 3 columns (whole points in a normal chunk)
         if (!Gp.big) {
-            if (tid >= ch.q0 && tid < ch.q1) {
+            if (ptl) {
                 const int p = Gp.p0 + tid;
-                const int a0 = pt_start[p] - ch.o0, a1 = pt_start[p + 1] - ch.o0;
+                const int a0 = pa0, a1 = pa1;
                 double cs[3] = {0, 0, 0}, gr[3] = {0, 0, 0};
                 for (int b = a0; b < a1; ++b) {
                     const double* r = jer + b * 8;
@@ -856,18 +885,25 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
                     colsq[3 * (size_t)p + i] = cs[i];
                     grad[3 * (size_t)p + i] = gr[i];
                     gmax = fmax(gmax, fabs(gr[i]));
-                    xn += pts[3 * (size_t)p + i] * pts[3 * (size_t)p + i];
                 }
             }
-            // per camera: Gram of its feature rows, accumulated over the group's chunks
+            // per camera: Gram of its feature rows, accumulated over the group's chunks; the
+            // operand reads go out 8 MFMA steps at a time, ahead of their MFMAs
 #pragma unroll
             for (int i = 0; i < UMAX / 4; ++i) {
                 const int lc = w + 4 * i;
                 if (lc >= Gp.u) continue;
-                const int r0 = lcrow[ch.lc0 + lc], r1 = lcrow[ch.lc0 + lc + 1];
-                for (int row = r0; row < r1; row += 4) {
-                    const double v = m16 < NF ? G[(row + kq) * NF + m16] : 0.0;
-                    acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc[i], 0, 0, 0);
+                const int r0 = cr0[i], r1 = cr1[i];
+                for (int row = r0; row < r1; row += 32) {
+                    double v[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int rr = row + 4 * u;
+                        v[u] = (m16 < NF && rr < r1) ? G[(rr + kq) * NF + m16] : 0.0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (row + 4 * u < r1) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[u], v[u], acc[i], 0, 0, 0);
                 }
             }
         } else {
@@ -897,6 +933,7 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
             }
         }
         __syncthreads();
+        BA_STAMP(3);
     }
     if (!Gp.big) {
 #pragma unroll
@@ -936,6 +973,8 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
         q[GP_XN] = sx;
         q[GP_GMAX] = gm;
     }
+    BA_STAMP(4);
+    BA_FLUSH(8);
 }
 
 // ba_camred: per camera (one workgroup) the partials of its (group, camera) slots in group

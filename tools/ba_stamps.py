@@ -15,8 +15,9 @@ from sfmx import ba, synth  # noqa: E402
 from sfmx._lib import lib  # noqa: E402
 
 NAMES = {0: "gschur round MFMA", 1: "gschur wave combine", 2: "gschur store", 3: "gschur obs phase",
-         4: "gschur point phase", 5: "gschur round H fill", 8: "glin lin+store",
-         9: "glin point+gram", 10: "glin epilogue",
+         4: "gschur point phase", 5: "gschur round H fill", 8: "glin zero G + sync",
+         9: "glin dual numbers + stores", 10: "glin barrier wait", 11: "glin point sums + gram + sync",
+         12: "glin epilogue",
          16: "gupdate obs", 17: "gupdate point", 18: "gupdate model", 19: "gupdate epilogue"}
 prob = synth.ba_problem(200, 200_000)
 ctx = ba.BAContext(ba.BAProblem(**prob), ba.default_options())
