@@ -346,6 +346,29 @@ void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const 
     CHOL_STAMP(34);
 }
 
+// Cross-rank all-reduce of the reduced system, compacted: the structurally nonzero lower tiles of
+// S_cc (incl. the diagonal ones) + R | D | r_i, packed into one contiguous buffer and back.
+// One workgroup per tile; the tail block (blockIdx.x == ntiles) moves the rest.
+__global__ __launch_bounds__(256)
+void chol_pack(const double* __restrict__ S, int npad, const int2* __restrict__ tiles, int ntiles, int tail,
+               double* __restrict__ buf, int unpack_dir) {
+    if ((int)blockIdx.x < ntiles) {
+        const int2 t = tiles[blockIdx.x];
+        double* sp = const_cast<double*>(S) + (size_t)t.x * NB * npad + (size_t)t.y * NB;
+        double* bp = buf + (size_t)blockIdx.x * NB * NB;
+        for (int e = threadIdx.x; e < NB * NB; e += 256) {
+            double* g = sp + (size_t)(e / NB) * npad + e % NB;
+            if (unpack_dir) *g = bp[e]; else bp[e] = *g;
+        }
+    } else {
+        double* rest = const_cast<double*>(S) + (size_t)npad * npad;
+        double* bp = buf + (size_t)ntiles * NB * NB;
+        for (int e = threadIdx.x; e < tail; e += 256) {
+            if (unpack_dir) rest[e] = bp[e]; else bp[e] = rest[e];
+        }
+    }
+}
+
 // The intrinsics (one workgroup of 64): D' = D - sum_k contrib_k[:, :K], r' = r_i - sum_k
 // contrib_k[:, K] (panel order), K x K Cholesky (non-positive pivot -> fail), x_i = D'^-1 r' ->
 // xi (device scalars for the back solve) and sol_i.

@@ -88,7 +88,9 @@ struct sfmx_ba_ctx {
     std::vector<char> adj;       // local camera co-visibility, C x C
     bool planned = false;
     sfmx::ba::FactorPlan plan;
-    Buf camrow, padrows, rowmap, leaves, ptasks, psrc, lvl_start, lvl_panels, bs_start, bs_k, Wt, contrib, xi;
+    Buf camrow, padrows, rowmap, leaves, ptasks, psrc, lvl_start, lvl_panels, bs_start, bs_k, Wt, contrib, xi,
+        nztiles, packbuf;          // all-reduce of the nonzero lower tiles only (multi-rank)
+    int n_nztiles = 0;
     size_t sr_count = 0;         // doubles of SR = S_cc | R | D | r_i
     // state (the *2 buffers hold the candidate's linearization until the step is accepted)
     Buf x, cand, scale, colsq, colsq2, grad, grad2, J, J2, camsum, camsum2, plt, sg, rg, hbig, gpart, gpl, scal,
@@ -102,7 +104,7 @@ struct sfmx_ba_ctx {
     ~sfmx_ba_ctx() {
         Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
-                      &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &x, &cand, &scale, &colsq, &colsq2, &grad,
+                      &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
                       &failf, &partA};
         int prev = 0;
@@ -249,8 +251,16 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
                        R, Dm, ri);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], c->st));
-    // point-sharded ranks: the group part of the reduced camera system and its rhs are sums over ranks
-    RC(allreduce(c, S, (int64_t)c->sr_count, SFMX_REDUCE_SUM));
+    // point-sharded ranks: the group part of the reduced camera system and its rhs are sums over
+    // ranks; only the structurally nonzero lower tiles (+ R, D, r_i) travel
+    if (c->ar) {
+        const int tail = (int)(c->sr_count - (size_t)npad * npad);
+        hipLaunchKernelGGL(chol_pack, dim3(c->n_nztiles + 1), dim3(256), 0, c->st, S, npad, c->nztiles.as<int2>(),
+                           c->n_nztiles, tail, c->packbuf.as<double>(), 0);
+        RC(allreduce(c, c->packbuf.as<double>(), (int64_t)c->n_nztiles * NB * NB + tail, SFMX_REDUCE_SUM));
+        hipLaunchKernelGGL(chol_pack, dim3(c->n_nztiles + 1), dim3(256), 0, c->st, S, npad, c->nztiles.as<int2>(),
+                           c->n_nztiles, tail, c->packbuf.as<double>(), 1);
+    }
     hipLaunchKernelGGL(ba_add_cam<K>, dim3(C + 1), dim3(64), 0, c->st, c->P, C, npad, c->camrow.as<int>(),
                        c->padrows.as<int>(), (int)c->plan.padrows.size(), c->camsum.as<double>(),
                        c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, S,
@@ -333,6 +343,15 @@ int ensure_plan(sfmx_ba_ctx* c) {
         (rc = upload(c->bs_start, pl.bs_start, st)) || (rc = upload(c->bs_k, pl.bs_k, st)))
         return rc;
     RC(c->SR.alloc(sizeof(double) * c->sr_count));
+    {   // nonzero lower tiles (diagonal included): the compact all-reduce payload
+        std::vector<int2> nzt;
+        for (int a = 0; a < pl.T; ++a)
+            for (int b = 0; b <= a; ++b)
+                if (pl.nz[(size_t)a * pl.T + b]) nzt.push_back(make_int2(a, b));
+        c->n_nztiles = (int)nzt.size();
+        RC(upload(c->nztiles, nzt, st));
+        RC(c->packbuf.alloc(sizeof(double) * ((size_t)c->n_nztiles * NB * NB + (c->sr_count - (size_t)pl.npad * pl.npad))));
+    }
     RC(c->Wt.alloc(sizeof(double) * (size_t)pl.T * NB * NB));
     RC(c->contrib.alloc(sizeof(double) * (size_t)pl.T * K * RW));
     RC(c->xi.alloc(sizeof(double) * K));
