@@ -40,7 +40,10 @@
 // so it does not affect the ratio and is not restated.
 // Deviations (documented in DESIGN.md): the minimal-sample null vector by an
 // 8x8 solve instead of a 9x9 Jacobi eigen-decomposition (same H up to
-// rounding); (1-ep)^4 as two squarings; 3x3 products sum in k order.  The GPU
+// rounding; a RANSAC sample whose 8x8 system is exactly singular is skipped,
+// where OpenCV would score cv::eigen's vector); (1-ep)^4 as two squarings; 3x3
+// products sum in k order.  orc_homography_set_arith(1) switches the oracle to
+// the LtL + Jacobi null vector for measuring that gap (tools/arith_gap.py).  The GPU
 // kernel (csrc/homography.hip) follows the same operation order with FMA
 // contraction off, so the two agree bit for bit; parity against OpenCV itself
 // is unpinned (no OpenCV here).
@@ -88,9 +91,100 @@ bool solve8(double a[8][9], double h[9]) {
     return true;
 }
 
+// ---- OpenCV-arithmetic model (orc_homography_set_arith; measurement only) ----
+// 1: the minimal-sample null vector as OpenCV 4.5.1 computes it: LtL = sum Lx^T Lx + Ly^T Ly
+// (upper triangle, j <= k, then completeSymm), cv::eigen -> hal::Jacobi (cyclic-max pivot with the
+// indR / indC row and column maxima, hypot rotations, |p| <= DBL_EPSILON stop, n*n*30 rotations at
+// most, eigenvalues sorted descending with their rows of V), H0 = the last row of V.
+int g_harith = 0;
+
+void jacobi9(double A[9][9], double W[9], double V[9][9]) {
+    const int n = 9;
+    const double eps = DBL_EPSILON;
+    for (int i = 0; i < n; i++) {
+        for (int j = 0; j < n; j++) V[i][j] = 0;
+        V[i][i] = 1;
+    }
+    int indR[9] = {0}, indC[9] = {0};
+    auto row_max = [&](int k) {   // argmax_{i > k} |A[k][i]|
+        int m = k + 1;
+        double mv = std::fabs(A[k][m]);
+        for (int i = k + 2; i < n; i++) {
+            const double v = std::fabs(A[k][i]);
+            if (mv < v) mv = v, m = i;
+        }
+        indR[k] = m;
+    };
+    auto col_max = [&](int k) {   // argmax_{i < k} |A[i][k]|
+        int m = 0;
+        double mv = std::fabs(A[0][k]);
+        for (int i = 1; i < k; i++) {
+            const double v = std::fabs(A[i][k]);
+            if (mv < v) mv = v, m = i;
+        }
+        indC[k] = m;
+    };
+    for (int k = 0; k < n; k++) {
+        W[k] = A[k][k];
+        if (k < n - 1) row_max(k);
+        if (k > 0) col_max(k);
+    }
+    for (int iters = 0; iters < n * n * 30; iters++) {
+        int k = 0;
+        double mv = std::fabs(A[0][indR[0]]);
+        for (int i = 1; i < n - 1; i++) {
+            const double v = std::fabs(A[i][indR[i]]);
+            if (mv < v) mv = v, k = i;
+        }
+        int l = indR[k];
+        for (int i = 1; i < n; i++) {
+            const double v = std::fabs(A[indC[i]][i]);
+            if (mv < v) mv = v, k = indC[i], l = i;
+        }
+        const double p = A[k][l];
+        if (std::fabs(p) <= eps) break;
+        const double y = (W[l] - W[k]) * 0.5;
+        double t = std::fabs(y) + std::hypot(p, y);
+        double s = std::hypot(p, t);
+        const double c = t / s;
+        s = p / s;
+        t = (p / t) * p;
+        if (y < 0) s = -s, t = -t;
+        A[k][l] = 0;
+        W[k] -= t;
+        W[l] += t;
+        auto rot = [&](double& v0, double& v1) {
+            const double a0 = v0, b0 = v1;
+            v0 = a0 * c - b0 * s;
+            v1 = a0 * s + b0 * c;
+        };
+        for (int i = 0; i < k; i++) rot(A[i][k], A[i][l]);
+        for (int i = k + 1; i < l; i++) rot(A[k][i], A[i][l]);
+        for (int i = l + 1; i < n; i++) rot(A[k][i], A[l][i]);
+        for (int i = 0; i < n; i++) rot(V[k][i], V[l][i]);
+        for (int j = 0; j < 2; j++) {
+            const int idx = j == 0 ? k : l;
+            if (idx < n - 1) row_max(idx);
+            if (idx > 0) col_max(idx);
+        }
+    }
+    for (int k = 0; k < n - 1; k++) {
+        int m = k;
+        for (int i = k + 1; i < n; i++)
+            if (W[m] < W[i]) m = i;
+        if (k != m) {
+            std::swap(W[m], W[k]);
+            for (int i = 0; i < n; i++) std::swap(V[m][i], V[k][i]);
+        }
+    }
+}
+
 // HomographyEstimatorCallback::runKernel on `count` correspondences
-// (M = left/src, m = right/dst, float x,y interleaved) -> H (row-major, H[8] = 1).
-bool dlt(const float* M, const float* m, int count, double H[9]) {
+// (M = left/src, m = right/dst, float x,y interleaved) -> H (row-major, H[8] = 1).  runKernel
+// itself fails only on the zero-spread test (cv::eigen always returns a vector); solve8 also
+// reports a singular minimal system.  scales_only: stop after the spread test (findHomography's
+// 4-point path needs only runKernel's return value).
+bool dlt(const float* M, const float* m, int count, double H[9], bool scales_only = false) {
     double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
     for (int i = 0; i < count; ++i) {
         cmx += m[2 * i]; cmy += m[2 * i + 1];
@@ -104,21 +198,35 @@ bool dlt(const float* M, const float* m, int count, double H[9]) {
     if (std::fabs(smx) < DBL_EPSILON || std::fabs(smy) < DBL_EPSILON || std::fabs(sMx) < DBL_EPSILON ||
         std::fabs(sMy) < DBL_EPSILON)
         return false;
+    if (scales_only) return true;
     smx = count / smx; smy = count / smy; sMx = count / sMx; sMy = count / sMy;
     const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
-    double a[8][9];
+    double a[8][9], LtL[9][9] = {{0}};
     for (int i = 0; i < count; ++i) {   // count == 4: the minimal sample
         const double x = (m[2 * i] - cmx) * smx, y = (m[2 * i + 1] - cmy) * smy;
         const double X = (M[2 * i] - cMx) * sMx, Y = (M[2 * i + 1] - cMy) * sMy;
         const double Lx[9] = {X, Y, 1, 0, 0, 0, -x * X, -x * Y, -x};
         const double Ly[9] = {0, 0, 0, X, Y, 1, -y * X, -y * Y, -y};
+        if (g_harith & 1) {
+            for (int j = 0; j < 9; j++)
+                for (int k = j; k < 9; k++) LtL[j][k] += Lx[j] * Lx[k] + Ly[j] * Ly[k];
+            continue;
+        }
         for (int j = 0; j < 8; ++j) { a[2 * i][j] = Lx[j]; a[2 * i + 1][j] = Ly[j]; }
         a[2 * i][8] = -Lx[8];
         a[2 * i + 1][8] = -Ly[8];
     }
     double H0[9];
-    if (!solve8(a, H0)) return false;
+    if (g_harith & 1) {
+        for (int j = 0; j < 9; j++)
+            for (int k = 0; k < j; k++) LtL[j][k] = LtL[k][j];
+        double W[9], V[9][9];
+        jacobi9(LtL, W, V);
+        for (int i = 0; i < 9; ++i) H0[i] = V[8][i];
+    } else if (!solve8(a, H0)) {
+        return false;
+    }
     double Ht[9], H1[9];
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) {
@@ -199,7 +307,9 @@ int update_num_iters(double p, double ep, int model_points, int max_iters) {
 // correspondences; -1 if the homography comes back empty.
 int ransac_inliers(const float* M, const float* m, int count, double thr, int max_iters, double confidence) {
     double H[9];
-    if (count == 4) return dlt(M, m, 4, H) ? 4 : -1;
+    // findHomography with 4 points: result = runKernel > 0, mask all ones (fundam.cpp); runKernel
+    // fails only on zero spread, a degenerate (e.g. collinear) 4-point set still yields ratio 1
+    if (count == 4) return dlt(M, m, 4, H, true) ? 4 : -1;
     Rng rng((uint64_t)-1);
     const float thr2 = (float)(thr * thr);
     int niters = std::max(max_iters, 1), max_good = 0;
@@ -240,6 +350,14 @@ int ransac_inliers(const float* M, const float* m, int count, double thr, int ma
 }  // namespace
 
 extern "C" {
+
+// Selects the arithmetic model (1: cv::eigen minimal-sample null vector) for later calls; returns
+// the previous flags.  Not thread safe: set it before a call, not during one.
+int orc_homography_set_arith(int flags) {
+    const int old = g_harith;
+    g_harith = flags;
+    return old;
+}
 
 // Per pair p: matches m[off[p] .. off[p+1]) (sfmx_dmatch / cv::DMatch, 16 B),
 // left image pairs[2p], right pairs[2p+1]; kp[i] = image i's keypoints (x, y

@@ -60,6 +60,10 @@ def _load():
                              vp, vp, C.c_int]
     lib.orc_sift_batch.argtypes = [C.POINTER(vp), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double,
                                    C.c_double, vp, vp, C.c_int, i32p, C.c_int]
+    lib.orc_sift_set_arith.restype = C.c_int
+    lib.orc_sift_set_arith.argtypes = [C.c_int]
+    lib.orc_homography_set_arith.restype = C.c_int
+    lib.orc_homography_set_arith.argtypes = [C.c_int]
     lib.orc_orb.restype = C.c_int
     lib.orc_orb.argtypes = [vp, C.c_int, C.c_int, C.c_int64, C.c_int, C.c_float, C.c_int, C.c_int, C.c_int, vp, vp,
                             C.c_int]
@@ -228,6 +232,30 @@ def sift(image: np.ndarray, nfeatures: int = 0, n_octave_layers: int = 3, contra
         if n <= cap:
             return kps[:n], (desc[:n] if descriptors else None)
         cap = n
+
+
+# OpenCV-arithmetic model of the SIFT restatement (oracle/sift_oracle.cpp AR_* flags).  0 is the
+# arithmetic the GPU kernels share; SIFT_OPENCV_AVX2 models OpenCV 4.5.1 on an AVX2/FMA3 host.
+SIFT_EXP32F, SIFT_TRIG, SIFT_POWF, SIFT_FLOATHIST, SIFT_FMAVEC, SIFT_FMAFILT = 1, 2, 4, 8, 16, 32
+SIFT_OPENCV_SSE2 = SIFT_EXP32F | SIFT_TRIG | SIFT_POWF | SIFT_FLOATHIST
+SIFT_OPENCV_AVX2 = SIFT_OPENCV_SSE2 | SIFT_FMAVEC | SIFT_FMAFILT
+
+
+class arith:
+    """with oracle.arith(sift=flags, homography=flags): ... selects the oracle's arithmetic model
+    for the block (measurement of the deviations from OpenCV's own arithmetic; tests only)."""
+
+    def __init__(self, sift: int = 0, homography: int = 0):
+        self.flags = (sift, homography)
+
+    def __enter__(self):
+        self.old = (lib.orc_sift_set_arith(self.flags[0]), lib.orc_homography_set_arith(self.flags[1]))
+        return self
+
+    def __exit__(self, *exc):
+        lib.orc_sift_set_arith(self.old[0])
+        lib.orc_homography_set_arith(self.old[1])
+        return False
 
 
 def sift_batch(images, nfeatures=0, contrast_threshold=0.09, cap=16384, nthreads=0):

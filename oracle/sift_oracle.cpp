@@ -112,6 +112,81 @@ float atan2_deg(float y, float x) {
     return a;
 }
 
+// ---- OpenCV-arithmetic model (orc_sift_set_arith; measurement only, never the GPU-parity mode) ----
+// Bit flags; 0 (the default) is the arithmetic csrc/sift_features.hip shares.  The flags restate
+// what OpenCV 4.5.1 itself executes on an x86-64 host whose dispatcher picks the AVX2/FMA3 code
+// paths (core mathfuncs_core, imgproc filter, features2d sift are CPU-dispatched):
+enum {
+    AR_EXP32F = 1,      // cv::hal::exp32f (64-entry 2^(i/64) table x degree-4 polynomial) for the weights
+    AR_TRIG = 2,        // libm sinf / cosf (calcSIFTDescriptor calls them directly)
+    AR_POWF = 4,        // libm powf(2, (layer + xi) / L) for the keypoint size
+    AR_FLOATHIST = 8,   // histogram bins accumulate in float, in pixel order
+    AR_FMAVEC = 16,     // FMA3 in the vectorised exp32f / fastAtan2 / magnitude / smoothing / norm
+    AR_FMAFILT = 32,    // FMA3 in the separable Gaussian row / column filters
+};
+int g_arith = 0;
+
+constexpr double EXPPOLY_A0 = .9670371139572337719125840413672004409288e-2;
+
+struct ExpTab {
+    float t[64];
+    ExpTab() {
+        for (int i = 0; i < 64; ++i) t[i] = (float)(std::exp2(i / 64.0) * EXPPOLY_A0);
+    }
+};
+const ExpTab g_exptab;
+
+// cv::hal::exp32f, one element.  fused: the vector body (FMA3 polynomial); else the scalar loop.
+float cv_exp32f(float x, bool fused) {
+    const float A4 = (float)(1.000000000000002438532970795181890933776 / EXPPOLY_A0),
+                A3 = (float)(.6931471805521448196800669615864773144641 / EXPPOLY_A0),
+                A2 = (float)(.2402265109513301490103372422686535526573 / EXPPOLY_A0),
+                A1 = (float)(.5550339366753125211915322047004666939128e-1 / EXPPOLY_A0);
+    const double prescale = 1.4426950408889634073599246810019 * 64, maxv = 3000. * 64;
+    const float minval = (float)(-maxv / prescale), maxval = (float)(maxv / prescale);
+    float x0 = std::min(std::max(x, minval), maxval) * (float)prescale;
+    const int xi = (int)std::nearbyint(x0);
+    x0 = (x0 - (float)xi) * (float)(1. / 64);
+    int t = (xi >> 6) + 127;
+    t = !(t & ~255) ? t : t < 0 ? 0 : 255;
+    uint32_t bits = (uint32_t)t << 23;
+    float p2;
+    std::memcpy(&p2, &bits, 4);
+    float poly;
+    if (fused) poly = std::fma(std::fma(std::fma(x0 + A1, x0, A2), x0, A3), x0, A4);
+    else poly = (((x0 + A1) * x0 + A2) * x0 + A3) * x0 + A4;
+    return p2 * g_exptab.t[xi & 63] * poly;
+}
+
+// exp of element k of an in-place exp32f over len elements (the AVX2 body covers whole 16-element
+// blocks; an in-place call finishes the rest in the scalar loop)
+float weight_exp(float x, int k, int len) {
+    if (!(g_arith & AR_EXP32F)) return sx_expf(x);
+    return cv_exp32f(x, (g_arith & AR_FMAVEC) && k < (len / 16) * 16);
+}
+
+// fastAtan2 / magnitude32f of one element of a len-element (not in-place) call: len >= 16 runs the
+// vector body for every element (the last block overlaps), FMA3 polynomial / x*x + y*y
+float ori_deg(float y, float x, int len) {
+    if (!((g_arith & AR_FMAVEC) && len >= 16)) return atan2_deg(y, x);
+    constexpr float R2D = (float)(180 / 3.14159265358979323846);
+    constexpr float P1 = 0.9997878412794807f * R2D, P3 = -0.3258083974640975f * R2D, P5 = 0.1555786518463281f * R2D,
+                    P7 = -0.04432655554792128f * R2D;
+    const float ax = std::fabs(x), ay = std::fabs(y);
+    const float c = std::min(ax, ay) / (std::max(ax, ay) + (float)DBL_EPSILON);
+    const float cc = c * c;
+    float a = std::fma(std::fma(std::fma(cc, P7, P5), cc, P3), cc, P1) * c;
+    if (!(ax >= ay)) a = 90.f - a;
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+float magnitude(float dx, float dy, int len) {
+    if ((g_arith & AR_FMAVEC) && len >= 16) return std::sqrt(std::fma(dx, dx, dy * dy));
+    return std::sqrt(dx * dx + dy * dy);
+}
+
 int reflect101(int p, int n) {
     if (n == 1) return 0;
     while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
@@ -139,17 +214,23 @@ Img blur(const Img& src, double sigma) {
     const std::vector<float> f = gauss_kernel(sigma);
     const int n = (int)f.size(), r = n / 2;
     Img tmp(src.w, src.h), dst(src.w, src.h);
+    const bool fused = g_arith & AR_FMAFILT;
     for (int y = 0; y < src.h; ++y)
         for (int x = 0; x < src.w; ++x) {
             float s = f[0] * src.at(y, reflect101(x - r, src.w));
-            for (int k = 1; k < n; ++k) s += f[k] * src.at(y, reflect101(x - r + k, src.w));
+            for (int k = 1; k < n; ++k) {
+                const float v = src.at(y, reflect101(x - r + k, src.w));
+                s = fused ? std::fma(v, f[k], s) : s + f[k] * v;
+            }
             tmp.at(y, x) = s;
         }
     for (int y = 0; y < src.h; ++y)
         for (int x = 0; x < src.w; ++x) {
             float s = f[r] * tmp.at(y, x);
-            for (int k = 1; k <= r; ++k)
-                s += f[r + k] * (tmp.at(reflect101(y + k, src.h), x) + tmp.at(reflect101(y - k, src.h), x));
+            for (int k = 1; k <= r; ++k) {
+                const float v = tmp.at(reflect101(y + k, src.h), x) + tmp.at(reflect101(y - k, src.h), x);
+                s = fused ? std::fma(v, f[r + k], s) : s + f[r + k] * v;
+            }
             dst.at(y, x) = s;
         }
     return dst;
@@ -262,7 +343,9 @@ bool adjust(const std::vector<Img>& dog, int L, Kp& kpt, int octv, int& layer, i
     kpt.x = (c + xc) * (1 << octv);
     kpt.y = (r + xr) * (1 << octv);
     kpt.octave = octv + (layer << 8) + (round_d((xi + 0.5) * 255) << 16);
-    kpt.size = sigma * sx_expf(((layer + xi) / L) * 0.693147180559945309f) * (1 << octv) * 2;
+    kpt.size = sigma *
+               ((g_arith & AR_POWF) ? std::pow(2.f, (layer + xi) / L) : sx_expf(((layer + xi) / L) * 0.693147180559945309f)) *
+               (1 << octv) * 2;
     kpt.response = std::fabs(contr);
     kpt.angle = -1;
     kpt.class_id = -1;
@@ -272,34 +355,46 @@ bool adjust(const std::vector<Img>& dog, int L, Kp& kpt, int octv, int& layer, i
 float orientation_hist(const Img& img, int px, int py, int radius, float sigma, float* hist) {
     const int n = ORI_BINS;
     const float expf_scale = -1.f / (2.f * sigma * sigma);
-    int64_t acc[ORI_BINS] = {0};
+    // the window's samples in pixel order (calcOrientationHist's X / Y / W arrays)
+    struct S { float dx, dy, w; };
+    std::vector<S> smp;
+    smp.reserve((size_t)(2 * radius + 1) * (2 * radius + 1));
     for (int i = -radius; i <= radius; i++) {
         const int y = py + i;
         if (y <= 0 || y >= img.h - 1) continue;
         for (int j = -radius; j <= radius; j++) {
             const int x = px + j;
             if (x <= 0 || x >= img.w - 1) continue;
-            const float dx = img.at(y, x + 1) - img.at(y, x - 1);
-            const float dy = img.at(y - 1, x) - img.at(y + 1, x);
-            const float w = sx_expf((i * i + j * j) * expf_scale);
-            const float ori = atan2_deg(dy, dx);
-            const float mag = std::sqrt(dx * dx + dy * dy);
-            int bin = round_f((n / 360.f) * ori);
-            if (bin >= n) bin -= n;
-            if (bin < 0) bin += n;
-            acc[bin] += (int64_t)(w * mag * 1073741824.f);
+            smp.push_back({img.at(y, x + 1) - img.at(y, x - 1), img.at(y - 1, x) - img.at(y + 1, x), (i * i + j * j) * expf_scale});
         }
     }
-    float t[ORI_BINS + 4];
+    const int len = (int)smp.size();
+    int64_t acc[ORI_BINS] = {0};
+    float t[ORI_BINS + 4] = {0};
     float* temphist = t + 2;
-    for (int b = 0; b < n; ++b) temphist[b] = (float)((double)acc[b] * (1.0 / FIX));
+    for (int k = 0; k < len; ++k) {
+        const float w = weight_exp(smp[k].w, k, len);
+        const float ori = ori_deg(smp[k].dy, smp[k].dx, len);
+        const float mag = magnitude(smp[k].dx, smp[k].dy, len);
+        int bin = round_f((n / 360.f) * ori);
+        if (bin >= n) bin -= n;
+        if (bin < 0) bin += n;
+        if (g_arith & AR_FLOATHIST) temphist[bin] += w * mag;
+        else acc[bin] += (int64_t)(w * mag * 1073741824.f);
+    }
+    if (!(g_arith & AR_FLOATHIST))
+        for (int b = 0; b < n; ++b) temphist[b] = (float)((double)acc[b] * (1.0 / FIX));
     temphist[-1] = temphist[n - 1];
     temphist[-2] = temphist[n - 2];
     temphist[n] = temphist[0];
     temphist[n + 1] = temphist[1];
-    for (int b = 0; b < n; b++)
-        hist[b] = (temphist[b - 2] + temphist[b + 2]) * (1.f / 16.f) + (temphist[b - 1] + temphist[b + 1]) * (4.f / 16.f) +
-                  temphist[b] * (6.f / 16.f);
+    for (int b = 0; b < n; b++) {
+        const float tn2 = temphist[b - 2] + temphist[b + 2], tn1 = temphist[b - 1] + temphist[b + 1];
+        if ((g_arith & AR_FMAVEC) && b < (n / 8) * 8)   // the 8-lane body: fma(tn2, 1/16, fma(tn1, 4/16, t0 * 6/16))
+            hist[b] = std::fma(tn2, 1.f / 16.f, std::fma(tn1, 4.f / 16.f, temphist[b] * (6.f / 16.f)));
+        else
+            hist[b] = tn2 * (1.f / 16.f) + tn1 * (4.f / 16.f) + temphist[b] * (6.f / 16.f);
+    }
     float maxval = hist[0];
     for (int b = 1; b < n; b++) maxval = std::max(maxval, hist[b]);
     return maxval;
@@ -309,7 +404,12 @@ void descriptor(const Img& img, float ptx, float pty, float ori, float scl, floa
     const int d = D, n = NB;
     const int ptX = round_f(ptx), ptY = round_f(pty);
     float sin_t, cos_t;
-    sx_sincosf(ori * (float)(3.14159265358979323846 / 180), &sin_t, &cos_t);
+    if (g_arith & AR_TRIG) {
+        cos_t = std::cos(ori * (float)(3.14159265358979323846 / 180));
+        sin_t = std::sin(ori * (float)(3.14159265358979323846 / 180));
+    } else {
+        sx_sincosf(ori * (float)(3.14159265358979323846 / 180), &sin_t, &cos_t);
+    }
     const float bins_per_rad = n / 360.f;
     const float exp_scale = -1.f / (d * d * 0.5f);
     const float hist_width = DESCR_SCL * scl;
@@ -317,21 +417,33 @@ void descriptor(const Img& img, float ptx, float pty, float ori, float scl, floa
     radius = std::min(radius, (int)std::sqrt(((double)img.w) * img.w + ((double)img.h) * img.h));
     cos_t /= hist_width;
     sin_t /= hist_width;
-    int64_t hist[(D + 2) * (D + 2) * (NB + 2)] = {0};
+    // the window's samples in pixel order (calcSIFTDescriptor's X / Y / RBin / CBin / W arrays)
+    struct S { float dx, dy, rbin, cbin, w; };
+    std::vector<S> smp;
+    smp.reserve((size_t)(2 * radius + 1) * (2 * radius + 1));
     for (int i = -radius; i <= radius; i++)
         for (int j = -radius; j <= radius; j++) {
             const float c_rot = j * cos_t - i * sin_t;
             const float r_rot = j * sin_t + i * cos_t;
-            float rbin = r_rot + d / 2 - 0.5f;
-            float cbin = c_rot + d / 2 - 0.5f;
+            const float rbin = r_rot + d / 2 - 0.5f;
+            const float cbin = c_rot + d / 2 - 0.5f;
             const int r = ptY + i, c = ptX + j;
             if (!(rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < img.h - 1 && c > 0 && c < img.w - 1))
                 continue;
-            const float dx = img.at(r, c + 1) - img.at(r, c - 1);
-            const float dy = img.at(r - 1, c) - img.at(r + 1, c);
-            const float w = sx_expf((c_rot * c_rot + r_rot * r_rot) * exp_scale);
-            const float o = atan2_deg(dy, dx);
-            const float m = std::sqrt(dx * dx + dy * dy);
+            smp.push_back({img.at(r, c + 1) - img.at(r, c - 1), img.at(r - 1, c) - img.at(r + 1, c), rbin, cbin,
+                           (c_rot * c_rot + r_rot * r_rot) * exp_scale});
+        }
+    const int len_s = (int)smp.size();
+    const bool fhist = g_arith & AR_FLOATHIST;
+    int64_t hist[(D + 2) * (D + 2) * (NB + 2)] = {0};
+    float fh[(D + 2) * (D + 2) * (NB + 2)] = {0};
+    for (int k = 0; k < len_s; ++k) {
+        {
+            const float dx = smp[k].dx, dy = smp[k].dy;
+            float rbin = smp[k].rbin, cbin = smp[k].cbin;
+            const float w = weight_exp(smp[k].w, k, len_s);
+            const float o = ori_deg(dy, dx, len_s);
+            const float m = magnitude(dx, dy, len_s);
             float obin = (o - ori) * bins_per_rad;
             const float mag = m * w;
             const int r0 = (int)std::floor(rbin), c0 = (int)std::floor(cbin);
@@ -349,26 +461,38 @@ void descriptor(const Img& img, float ptx, float pty, float ori, float scl, floa
             const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
             const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
             const int idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
-            auto fx = [](float v) { return (int64_t)(v * 1073741824.f); };
-            hist[idx] += fx(v_rco000);
-            hist[idx + 1] += fx(v_rco001);
-            hist[idx + (n + 2)] += fx(v_rco010);
-            hist[idx + (n + 3)] += fx(v_rco011);
-            hist[idx + (d + 2) * (n + 2)] += fx(v_rco100);
-            hist[idx + (d + 2) * (n + 2) + 1] += fx(v_rco101);
-            hist[idx + (d + 3) * (n + 2)] += fx(v_rco110);
-            hist[idx + (d + 3) * (n + 2) + 1] += fx(v_rco111);
+            const int tgt[8] = {idx, idx + 1, idx + (n + 2), idx + (n + 3), idx + (d + 2) * (n + 2),
+                                idx + (d + 2) * (n + 2) + 1, idx + (d + 3) * (n + 2), idx + (d + 3) * (n + 2) + 1};
+            const float val[8] = {v_rco000, v_rco001, v_rco010, v_rco011, v_rco100, v_rco101, v_rco110, v_rco111};
+            for (int q = 0; q < 8; ++q) {
+                if (fhist) fh[tgt[q]] += val[q];
+                else hist[tgt[q]] += (int64_t)(val[q] * 1073741824.f);
+            }
         }
+    }
     for (int i = 0; i < d; i++)
         for (int j = 0; j < d; j++) {
             const int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
-            hist[idx] += hist[idx + n];
-            hist[idx + 1] += hist[idx + n + 1];
-            for (int k = 0; k < n; k++) dst[(i * d + j) * n + k] = (float)((double)hist[idx + k] * (1.0 / FIX));
+            if (fhist) {
+                fh[idx] += fh[idx + n];
+                fh[idx + 1] += fh[idx + n + 1];
+                for (int k = 0; k < n; k++) dst[(i * d + j) * n + k] = fh[idx + k];
+            } else {
+                hist[idx] += hist[idx + n];
+                hist[idx + 1] += hist[idx + n + 1];
+                for (int k = 0; k < n; k++) dst[(i * d + j) * n + k] = (float)((double)hist[idx + k] * (1.0 / FIX));
+            }
         }
     const int len = d * d * n;
     float nrm2 = 0;
-    for (int k = 0; k < len; k++) nrm2 += dst[k] * dst[k];
+    if (g_arith & AR_FMAVEC) {   // 8-lane fma accumulation, then v_reduce_sum ((l0+l4)+(l1+l5)) + ((l2+l6)+(l3+l7))
+        float lane[8] = {0};
+        for (int k = 0; k < len; k++) lane[k & 7] = std::fma(dst[k], dst[k], lane[k & 7]);
+        const float s0 = lane[0] + lane[4], s1 = lane[1] + lane[5], s2 = lane[2] + lane[6], s3 = lane[3] + lane[7];
+        nrm2 = (s0 + s1) + (s2 + s3);
+    } else {
+        for (int k = 0; k < len; k++) nrm2 += dst[k] * dst[k];
+    }
     const float thr = std::sqrt(nrm2) * DESCR_MAG_THR;
     nrm2 = 0;
     for (int k = 0; k < len; k++) {
@@ -393,6 +517,14 @@ bool kp_less(const Kp& a, const Kp& b) {   // KeyPointsFilter::removeDuplicatedS
 }  // namespace
 
 extern "C" {
+
+// Selects the arithmetic model (AR_* flags above) for later orc_sift / orc_sift_batch calls;
+// returns the previous flags.  Not thread safe: set it before a call, not during one.
+int orc_sift_set_arith(int flags) {
+    const int old = g_arith;
+    g_arith = flags;
+    return old;
+}
 
 // SIFT::detectAndCompute restated; returns the keypoint count n (writes min(n, cap)).
 int orc_sift(const uint8_t* image, int W, int H, int64_t pitch, int nfeatures, int L, double contrastThreshold,

@@ -85,8 +85,8 @@ __device__ __forceinline__ bool solve8(double (&a)[8][9], double (&h)[9]) {
 
 // HomographyEstimatorCallback::runKernel on the 4 correspondences of a minimal
 // sample, c[i] = (src.x, src.y, dst.x, dst.y) -> H (row-major, H[8] = 1);
-// false if degenerate.
-__device__ bool dlt4(const float4 (&c)[4], double (&H)[9]) {
+// false if degenerate.  scales_only: stop after runKernel's own failure test (zero spread).
+__device__ bool dlt4(const float4 (&c)[4], double (&H)[9], bool scales_only = false) {
     const int count = 4;
     double cMx = 0, cMy = 0, cmx = 0, cmy = 0, sMx = 0, sMy = 0, smx = 0, smy = 0;
 #pragma unroll
@@ -102,6 +102,7 @@ __device__ bool dlt4(const float4 (&c)[4], double (&H)[9]) {
     }
     if (fabs(smx) < DBL_EPSILON || fabs(smy) < DBL_EPSILON || fabs(sMx) < DBL_EPSILON || fabs(sMy) < DBL_EPSILON)
         return false;
+    if (scales_only) return true;
     smx = count / smx; smy = count / smy; sMx = count / sMx; sMy = count / sMy;
     const double invHnorm[9] = {1. / smx, 0, cmx, 0, 1. / smy, cmy, 0, 0, 1};
     const double Hnorm2[9] = {sMx, 0, -cMx * sMx, 0, sMy, -cMy * sMy, 0, 0, 1};
@@ -240,11 +241,11 @@ void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_
     }
     const float4* C = n <= CAP ? pts : scratch + o0;
     H_STAMP(1);
-    if (n == 4) {   // findHomography: 4 points -> the kernel directly, mask all ones
+    if (n == 4) {   // findHomography: 4 points -> result = runKernel > 0 (fails only on zero spread), mask all ones
         if (tid == 0) {
             const float4 c4[4] = {C[0], C[1], C[2], C[3]};
             double H[9];
-            out[p] = dlt4(c4, H) ? 1.0 : 0.0;
+            out[p] = dlt4(c4, H, true) ? 1.0 : 0.0;
         }
         return;
     }
