@@ -74,6 +74,7 @@ def parse():
     ap.add_argument("--no-orb-features", action="store_true", help="skip the ORB extraction leg (SURVEY §8 f3)")
     ap.add_argument("--only-orb-features", action="store_true", help="run only the ORB extraction leg (tuning)")
     ap.add_argument("--only-ba", action="store_true", help="run only the bundle-adjustment leg (tuning)")
+    ap.add_argument("--only-c3", action="store_true", help="run only the 200-image SIFT (config 3) leg (profiling)")
     ap.add_argument("--ba-cams", type=int, default=200)
     ap.add_argument("--ba-points", type=int, default=200_000)
     ap.add_argument("--ba-cpu-iters", type=int, default=2, help="LM iterations of the CPU BA baseline sample")
@@ -106,6 +107,14 @@ def main():
         res = bench_ba(args, rank, world, local)
         if rank == 0:
             print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    if args.only_c3:
+        res = bench_match("c3", args, rank, world, local)
+        if rank == 0:
+            print(json.dumps({k: v for k, v in res.items() if not k.startswith("_")}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -166,7 +175,8 @@ def bench_match(kind, args, rank, world, local):
         dtype = "int8->int32 (exact; f32 in/out)"
         scaling = "weak" if kind == "sift" else "strong"
         data = "synthetic (seeded SIFT-like descriptors, 25% planted re-observations; no dataset)"
-        kernel = "sift_screen16_kernel + sift_knn2_kernel<GATHER> (two-pass ratio test, both passes)"
+        kernel = ("sift_screen16_kernel + sift_subset_kernel + sift_settle_kernel (two-pass ratio test, both passes; "
+                  "pass 2 on the forwarded queries' row subsets)")
         algo = "256 ops (128 int8 MAC) per descriptor pair"
     else:
         n_desc, n_img = 16384, 200
@@ -207,13 +217,14 @@ def bench_match(kind, args, rank, world, local):
     for _ in range(args.warmup):
         step()
     barrier()
-    main_ms, run_ms = [], []
+    main_ms, run_ms, scr_ms = [], [], []
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
         a, b = matcher.timing()
         main_ms.append(a)
         run_ms.append(b)
+        scr_ms.append(matcher.pass_timing()[0])
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -253,6 +264,10 @@ def bench_match(kind, args, rank, world, local):
         pcie_s = float(t.item())
     matcher.close()
     achieved = logical_mine * op_per_pair / (kern_ms * 1e-3) / 1e12
+    screen_ms = float(np.mean(scr_ms))
+    screen = {"kernel_ms_per_launch": screen_ms, "achieved": logical_mine * op_per_pair / (screen_ms * 1e-3) / 1e12 if screen_ms > 0 else None,
+              "frac": logical_mine * op_per_pair / (screen_ms * 1e-3) / 1e12 / peak if screen_ms > 0 else None,
+              "what": "pass 1 alone (the screening kernel over every descriptor pair); frac is of the same nominal peak"}
     res = {
         "metric": "descriptor-pairs/s matched",
         "value": value,
@@ -273,6 +288,7 @@ def bench_match(kind, args, rank, world, local):
                      "frac": achieved / peak, "traffic": pmc_traffic(kind, n_img),
                      "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE from the committed PMC pass)",
                      "kernel": kernel, "kernel_ms_per_launch": kern_ms, "run_ms_per_step": float(np.mean(run_ms)),
+                     "screen_only": screen,
                      "algorithmic": f"{algo} x {logical_mine:.4g} pairs per launch"},
         "cpu_baseline": None,
         "pcie_inclusive": {"value": logical_total / pcie_s, "unit": "descriptor-pairs/s", "ms": pcie_s * 1e3,
@@ -419,9 +435,10 @@ def bench_3d2d(args, imgs, my_pairs, got, off, rank, world, local, stream):
     return res
 
 
-PMC_FILES = {"sift": ("r01g_pmc_sift_2p.json", ("sift_screen16_kernel", "sift_knn2_kernel"), 50),
+SIFT_KERNELS = ("sift_screen16_kernel", "sift_subset_kernel", "sift_settle_kernel")
+PMC_FILES = {"sift": ("r02_pmc_sift_c2.json", SIFT_KERNELS, 50),
              "orb": ("r01h_pmc_orb.json", ("orb_screen16_kernel", "orb_mfma16_kernel"), 200),
-             "c3": ("r01_pmc_sift_c3.json", ("sift_screen16_kernel", "sift_knn2_kernel"), 200)}
+             "c3": ("r02_pmc_sift_c3.json", SIFT_KERNELS, 200)}
 
 
 def pmc_traffic(kind, n_img):

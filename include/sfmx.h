@@ -134,6 +134,11 @@ int sfmx_matcher_stats(sfmx_matcher* m, int64_t* slow_queries, int64_t* fp32_pai
  * total_ms = first to last kernel of the run.  Synchronises the run's end event. */
 int sfmx_matcher_timing(sfmx_matcher* m, float* main_kernel_ms, float* total_ms);
 
+/* The two-pass split of main_kernel_ms (SIFT-L2 and ORB-FP4 paths): screen_ms = pass 1 (the
+ * screening kernel), pass2_ms = the rest of the 2-NN launch (work compaction + the exact kernel on
+ * the forwarded queries).  Single-pass variants report screen_ms = 0. */
+int sfmx_matcher_pass_timing(sfmx_matcher* m, float* screen_ms, float* pass2_ms);
+
 /* One-shot convenience wrapper = the whole strategy call
  * (IFeatureMatchingStrategy::calculateShotMatches, IFeatureMatchingStrategy.h:45-46, as SfM.cpp:545
  * calls it): uses n_gpus devices (pairs split by Σ Nq·Nt, one host thread per device; each device

@@ -590,13 +590,14 @@ void sift_screen_kernel(const WorkItem* __restrict__ work, const PairDev* __rest
 //   4 (l >> 4) + i, i = 0..3, of column l & 15.  Two row blocks per step feed one
 //   v_max3 per accumulator row i: 4 chains per lane x 4 lanes = 16 disjoint row
 //   subsets per query, the same bound as the 32x32 form.
-template <int QT, int WAVES, int MINW, int STAGE>
+template <int QT, int WAVES, int MINW, int STAGE, bool SUBSET = false>
 __global__ __launch_bounds__(WAVES * 64, MINW)
 void sift_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
                           const ImgDev* __restrict__ imgs, const int8_t* __restrict__ desc8,
                           const int32_t* __restrict__ norm, const int32_t* __restrict__ keyc2,
                           int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
-                          int32_t* __restrict__ qlist, int32_t* __restrict__ qcount, double ratio) {
+                          int32_t* __restrict__ qlist, int32_t* __restrict__ qcount, double ratio,
+                          int32_t* __restrict__ qmask = nullptr, unsigned long long* __restrict__ top2 = nullptr) {
     constexpr int GLDS = STAGE * SIFT_DIM / (WAVES * 64 * 16);
     static_assert(GLDS * WAVES * 64 * 16 == STAGE * SIFT_DIM, "stage must split into whole 16-B pieces");
     static_assert(QT * WAVES * 16 == 512, "work items are 512 queries");
@@ -693,6 +694,18 @@ void sift_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __re
             k2 = max(min(k1, p1), max(k2, p2));
             k1 = max(k1, p1);
         }
+        // SUBSET: the row subsets (j mod 16 = 4g + i) whose maximum reaches k2; only they can hold
+        // the first or second neighbour (a row of a subset with K <= k2 - 1 has s >= na - 2 k2 + 1 > s2)
+        int mask = 0xFFFF;
+        if constexpr (SUBSET) {
+            int nib = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) nib |= (ch[qt][i] >= k2 ? 1 : 0) << i;
+            int mk = nib << (4 * g);
+            mk |= __shfl_xor(mk, 16);
+            mk |= __shfl_xor(mk, 32);
+            if (nt >= 2 && k2 >= KEY_VALID) mask = mk;
+        }
         const int qi = qbase + qt * 16 + l16;
         if (g != 0 || qi >= nq) continue;
         const int64_t o = P.dense_base + qi;
@@ -709,8 +722,177 @@ void sift_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __re
         } else {
             const int slot = atomicAdd(&qcount[w.pair], 1);
             qlist[P.dense_base + slot] = qi;
+            if constexpr (SUBSET) {
+                qmask[P.dense_base + slot] = mask;
+                top2[2 * o] = ~0ull;
+                top2[2 * o + 1] = ~0ull;
+            }
             out_idx[o] = UNSETTLED;   // pass 2 must overwrite it (assemble counts survivors)
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 2, subset form (SFMX_SIFT_P2 = 10): one workgroup per (pair, row subset r), r = j mod 16.
+// The screen forwarded each unsettled query with the mask of the subsets whose maximum reaches
+// its second-largest subset maximum; only rows of those subsets can be the first or second
+// neighbour (sift_screen16_kernel), typically 2 of 16.  The workgroup gathers the pair's forwarded
+// queries with bit r, stages subset r's rows (j = r + 16 i, 256 per LDS chunk, the 8-bit local
+// index i & 255 in the packed key) and runs the exact top-2 of sift_knn2_kernel on them
+// (v_mfma_i32_32x32x32_i8, packed keys, 32 queries per wave).  Each (query, subset) top-2 is
+// merged into the query's global top-2 with two 64-bit atomicMin: key = (s << 32) | j, i.e.
+// (distance, train index) order; old = min(b0, k), then b1 = min(b1, max(old, k)) leaves b0 and
+// b1 the two smallest keys inserted, whatever the order (sift_settle_kernel reads them).
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 2)
+void sift_subset_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restrict__ imgs,
+                        const int8_t* __restrict__ desc8, const int32_t* __restrict__ norm,
+                        const int32_t* __restrict__ qlist, const int32_t* __restrict__ qmask,
+                        const int32_t* __restrict__ qcount, const int32_t* __restrict__ porder,
+                        unsigned long long* __restrict__ top2) {
+    constexpr int CH = 256;                   // rows per LDS chunk
+    constexpr int QC = WAVES * 32;            // queries per tile group (one 32-query tile per wave)
+    constexpr int WIN = 1024;                 // forwarded-query window scanned per round
+    constexpr int GLDS = CH * SIFT_DIM / (WAVES * 64 * 16);
+    static_assert(GLDS * WAVES * 64 * 16 == CH * SIFT_DIM, "chunk must split into whole 16-B pieces");
+    __shared__ __attribute__((aligned(16))) char rows_lds[CH * SIFT_DIM];
+    __shared__ int keys_lds[CH];
+    __shared__ int ql[WIN];
+    __shared__ int s_n;
+
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    const int pi = porder[item >> 4], r = item & 15;
+    const int cnt = qcount[pi];
+    const PairDev P = pairs[pi];
+    const ImgDev L = imgs[P.left], R = imgs[P.right];
+    const int nt = R.rows;
+    const int nr = R.rows_pad >> 4;           // rows j = r + 16 i < rows_pad (pad rows are zero)
+    if (cnt == 0 || r >= nt) return;
+    const int32_t* qls = qlist + P.dense_base;
+    const int32_t* qms = qmask + P.dense_base;
+
+    for (int e0 = 0; e0 < cnt; e0 += WIN) {
+        if (tid == 0) s_n = 0;
+        __syncthreads();
+        for (int e = e0 + tid; e < min(cnt, e0 + WIN); e += WAVES * 64)
+            if ((qms[e] >> r) & 1) ql[atomicAdd(&s_n, 1)] = qls[e];
+        __syncthreads();
+        const int n = s_n;
+        for (int g0 = 0; g0 < n; g0 += QC) {
+            const int qe = g0 + wid * 32 + l32;
+            const int qrow = qe < n ? ql[qe] : -1;
+            const bool active = g0 + wid * 32 < n;   // wave-uniform
+            i32x4 bq[4];
+            {
+                const i32x4* src = reinterpret_cast<const i32x4*>(desc8 + (L.row0 + (qrow < 0 ? 0 : qrow)) * SIFT_DIM);
+#pragma unroll
+                for (int m = 0; m < 4; ++m) bq[m] = src[2 * m + h];
+            }
+            int T1 = INT_MAX, J1 = -1, T2 = INT_MAX, J2 = -1;
+            for (int c0 = 0; c0 < nr; c0 += CH) {
+                const int rows = min(CH, nr - c0);   // a multiple of 32
+                __syncthreads();                     // the previous chunk's readers are done
+#pragma unroll
+                for (int u = 0; u < GLDS; ++u) {
+                    const int p = u * WAVES * 64 + tid;
+                    const int rr = p >> 3, slot = p & 7, c = slot ^ ((rr >> 1) & 7);
+                    const int j = r + 16 * (c0 + (rr < rows ? rr : 0));
+                    const int8_t* gp = desc8 + (R.row0 + j) * SIFT_DIM + 16 * c;
+                    __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)gp,
+                                                     (LDS_AS void*)(rows_lds + (u * WAVES + wid) * 1024), 16, 0, 0);
+                }
+                for (int i = tid; i < CH; i += WAVES * 64) {
+                    const int j = r + 16 * (c0 + i);
+                    keys_lds[i] = (i < rows && j < nt) ? (-(norm[R.row0 + j] << 8) + 255 - i) : INT_MIN;
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (active) {
+                    int c1 = INT_MIN, c2 = INT_MIN;
+                    for (int t = 0; t < rows / 32; ++t) {
+                        const int row = t * 32 + l32;
+                        i32x4 a[4];
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            const int slot = (2 * m + h) ^ ((row >> 1) & 7);
+                            a[m] = *reinterpret_cast<const i32x4*>(rows_lds + row * SIFT_DIM + 16 * slot);
+                        }
+                        i32x4 kv[4];
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) kv[g] = *reinterpret_cast<const i32x4*>(keys_lds + t * 32 + 8 * g + 4 * h);
+                        i32x16 acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], bq[m], acc, 0, 0, 0);
+                        int mm[8];
+#pragma unroll
+                        for (int q = 0; q < 16; q += 2) {
+                            const int ka = (int)(((unsigned)acc[q] << 9) + (unsigned)kv[q >> 2][q & 3]);
+                            const int kb = (int)(((unsigned)acc[q + 1] << 9) + (unsigned)kv[q >> 2][(q + 1) & 3]);
+                            mm[q >> 1] = v_med3(c1, ka, kb);
+                            c1 = v_max3(c1, ka, kb);
+                        }
+                        c2 = v_max3(v_max3(mm[0], mm[1], mm[2]), v_max3(mm[3], mm[4], mm[5]), v_max3(mm[6], mm[7], c2));
+                    }
+                    const int p1 = __shfl_xor(c1, 32), p2 = __shfl_xor(c2, 32);
+                    const int m1 = max(c1, p1), m2 = max(min(c1, p1), max(c2, p2));
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {   // chunk top-2 into the running top-2 (later chunks: strict <)
+                        const int key = e == 0 ? m1 : m2;
+                        if (key != INT_MIN) {
+                            const int t_ = -(key >> 8), i_ = c0 + 255 - (key & 255);
+                            if (t_ < T2) {
+                                if (t_ < T1) { T2 = T1; J2 = J1; T1 = t_; J1 = i_; }
+                                else { T2 = t_; J2 = i_; }
+                            }
+                        }
+                    }
+                }
+            }
+            if (active && h == 0 && qrow >= 0) {
+                const long long na = norm[L.row0 + qrow];
+                unsigned long long* b = top2 + 2 * (P.dense_base + qrow);
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int t_ = e == 0 ? T1 : T2, i_ = e == 0 ? J1 : J2;
+                    if (t_ == INT_MAX) continue;
+                    const unsigned long long k = ((unsigned long long)(na + t_) << 32) | (unsigned)(r + 16 * i_);
+                    const unsigned long long old = atomicMin(b, k);
+                    atomicMin(b + 1, old > k ? old : k);
+                }
+            }
+        }
+        __syncthreads();   // ql / s_n are rewritten by the next window
+    }
+}
+
+// Pass 2, subset form: the forwarded queries' merged top-2 -> dense results (one workgroup per pair).
+__global__ __launch_bounds__(256)
+void sift_settle_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restrict__ imgs,
+                        const int32_t* __restrict__ qlist, const int32_t* __restrict__ qcount,
+                        const unsigned long long* __restrict__ top2, int32_t* __restrict__ out_idx,
+                        float* __restrict__ out_dist, int2* __restrict__ slow_list, int32_t* __restrict__ slow_count,
+                        double ratio) {
+    const int pi = blockIdx.x;
+    const int cnt = qcount[pi];
+    if (cnt == 0) return;
+    const PairDev P = pairs[pi];
+    const int nt = imgs[P.right].rows;
+    for (int e = threadIdx.x; e < cnt; e += 256) {
+        const int qi = qlist[P.dense_base + e];
+        const int64_t o = P.dense_base + qi;
+        const unsigned long long b0 = top2[2 * o], b1 = top2[2 * o + 1];
+        if (b0 == ~0ull || (nt >= 2 && b1 == ~0ull)) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }   // not reached
+        const int64_t s1 = (int64_t)(b0 >> 32), s2 = (int64_t)(b1 >> 32);
+        if (nt >= 2 && s2 >= SQRT_SAFE) {
+            const int slot = atomicAdd(slow_count, 1);
+            slow_list[slot] = make_int2(pi, qi);
+            out_idx[o] = -2;
+            continue;
+        }
+        const float d1 = sqrt_rn_int(s1);
+        out_idx[o] = lowe_select((int)(b0 & 0xffffffffu), d1, nt >= 2 ? sqrt_rn_int(s2) : 0.f, nt, ratio);
+        out_dist[o] = d1;
     }
 }
 
@@ -1538,9 +1720,9 @@ int sift_variant() {   // read per run: tests switch paths within one process
     const char* e = getenv("SFMX_SIFT_VARIANT");
     return e ? atoi(e) : 0;
 }
-int pass2_variant() {   // tuning only: SFMX_SIFT_P2 selects the pass-2 item size / shape
-    const char* e = getenv("SFMX_SIFT_P2");
-    return e ? atoi(e) : 0;
+int pass2_variant() {   // SFMX_SIFT_P2 (tuning / tests only): 10 = subset pass 2 (default), else the full-row
+    const char* e = getenv("SFMX_SIFT_P2");   // GATHER pass 2 with that item size (0 / 2 = 128 queries)
+    return e ? atoi(e) : 10;
 }
 int sift_block_queries(int v) { return v == 2 || v == 4 || v == 23 ? 256 : 512; }
 
@@ -1552,17 +1734,30 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
                             const int8_t* desc8, const int32_t* norm, const int32_t* keyc, const int32_t* keyc2,
                             int32_t* qlist, int32_t* qcount, int n_pairs, const int32_t* porder, WorkItem* work2,
                             int32_t* work2_n, int32_t* out_idx,
-                            float* out_dist, int2* slow_list, int32_t* slow_count, double ratio, hipStream_t st) {
+                            float* out_dist, int2* slow_list, int32_t* slow_count, double ratio, hipStream_t st,
+                            hipEvent_t ev_screen, int32_t* qmask, unsigned long long* top2) {
     if (n_work == 0) return hipSuccess;
     const int v = sift_variant();
     if (v == 0 || v >= 101) {   // two-pass ratio test: screen every query, exact kernel on the rest
         hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * n_pairs, st);
         if (e != hipSuccess) return e;
+        if (pass2_variant() == 10 && qmask && top2) {   // subset-restricted pass 2
+            sift_screen16_kernel<8, 4, 2, 64, true><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc8, norm, keyc2, out_idx,
+                                                                           out_dist, qlist, qcount, ratio, qmask, top2);
+            if (ev_screen) {
+                e = hipEventRecord(ev_screen, st);
+                if (e != hipSuccess) return e;
+            }
+            sift_subset_kernel<4><<<n_pairs * 16, 256, 0, st>>>(pairs, imgs, desc8, norm, qlist, qmask, qcount, porder, top2);
+            sift_settle_kernel<<<n_pairs, 256, 0, st>>>(pairs, imgs, qlist, qcount, top2, out_idx, out_dist, slow_list,
+                                                        slow_count, ratio);
+            return hipGetLastError();
+        }
 #define SCREEN_LAUNCH(QT, W, MINW, ST) \
     sift_screen_kernel<QT, W, MINW, ST><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc2, out_idx, \
                                                                    out_dist, qlist, qcount, ratio)
-#define SCREEN16_LAUNCH(QT, W, MINW, ST) \
-    sift_screen16_kernel<QT, W, MINW, ST><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc2, out_idx, \
+#define SCREEN16_LAUNCH(QT, W, MINW, ST, ...) \
+    sift_screen16_kernel<QT, W, MINW, ST __VA_OPT__(,) __VA_ARGS__><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc2, out_idx, \
                                                                      out_dist, qlist, qcount, ratio)
         switch (v) {
         // every variant: 512 queries per work item (pass 2's).  r01f A/B on config 2 (kernel ms, both
@@ -1580,6 +1775,10 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
         }
 #undef SCREEN_LAUNCH
 #undef SCREEN16_LAUNCH
+        if (ev_screen) {   // pass-1 / pass-2 split of the launch (sfmx_matcher_pass_timing)
+            e = hipEventRecord(ev_screen, st);
+            if (e != hipSuccess) return e;
+        }
 #define PASS2_LAUNCH(ISH, QT, W, MINW, ST)                                                                   \
     static_assert((1 << (ISH)) == (QT) * (W) * 32, "pass-2 item size must equal the queries one block covers"); \
     static_assert((ISH) >= 7 && (ISH) <= 9, "work2 holds n_work << 2 items: items of 128..512 queries");       \
@@ -1656,13 +1855,17 @@ hipError_t launch_prep_hamming_fp4(const uint8_t* src, int rows, int cols, int r
 hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
                            const uint8_t* desc4, const int32_t* keyc, int32_t* qlist, int32_t* qcount, int n_pairs,
                            const int32_t* porder, WorkItem* work2, int32_t* work2_n, int32_t* out_idx, float* out_dist,
-                           double ratio, hipStream_t st) {
+                           double ratio, hipStream_t st, hipEvent_t ev_screen) {
     if (n_work == 0) return hipSuccess;
     if (orb_variant() == 0 || orb_variant() >= 10) {   // two-pass ratio test (default)
         hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * n_pairs, st);
         if (e != hipSuccess) return e;
         orb_screen16_kernel<8, 4, 2, 64><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx, out_dist,
                                                                   qlist, qcount, ratio);
+        if (ev_screen) {
+            e = hipEventRecord(ev_screen, st);
+            if (e != hipSuccess) return e;
+        }
 #define ORB_PASS2(ISH, QT, W)                                                                                   \
     static_assert((1 << (ISH)) == (QT) * (W) * 16, "pass-2 item size must equal the queries one block covers"); \
     static_assert((ISH) >= 7 && (ISH) <= 9, "work2 holds n_work << 2 items: items of 128..512 queries");       \

@@ -35,7 +35,8 @@ hipError_t launch_prep_f32(const float*, int, int, int, float*, hipStream_t);
 hipError_t launch_prep_hamming(const uint8_t*, int, int, int, uint8_t*, hipStream_t);
 hipError_t launch_sift_knn2(const WorkItem*, int, const PairDev*, const ImgDev*, const int8_t*, const int32_t*,
                             const int32_t*, const int32_t*, int32_t*, int32_t*, int, const int32_t*, WorkItem*,
-                            int32_t*, int32_t*, float*, int2*, int32_t*, double, hipStream_t);
+                            int32_t*, int32_t*, float*, int2*, int32_t*, double, hipStream_t, hipEvent_t, int32_t*,
+                            unsigned long long*);
 hipError_t launch_sift_slow(const int2*, const int32_t*, const PairDev*, const ImgDev*, const int8_t*,
                             const int32_t*, int32_t*, float*, double, hipStream_t);
 hipError_t launch_sift_f32(const WorkItem*, int, const PairDev*, const ImgDev*, const float*, int32_t*, float*,
@@ -45,7 +46,7 @@ hipError_t launch_orb_knn2(const WorkItem*, int, const PairDev*, const ImgDev*, 
 hipError_t launch_prep_hamming_fp4(const uint8_t*, int, int, int, uint8_t*, int32_t*, hipStream_t);
 hipError_t launch_orb_mfma(const WorkItem*, int, const PairDev*, const ImgDev*, const uint8_t*, const int32_t*,
                            int32_t*, int32_t*, int, const int32_t*, WorkItem*, int32_t*, int32_t*, float*, double,
-                           hipStream_t);
+                           hipStream_t, hipEvent_t);
 int orb_variant();
 hipError_t launch_selftest_sqrt(int64_t, uint32_t*, hipStream_t);
 int sift_variant();
@@ -154,6 +155,7 @@ struct sfmx_matcher {
     int64_t fp32_pairs = 0;
     DevBuf pairs_d, work_d, work32_d, dense_idx, dense_dist, slow_list, slow_count, counts, keep, offsets, out;
     DevBuf qlist, qcount;   // two-pass SIFT path: per pair, the queries the screening pass could not settle
+    DevBuf qmask, top2;     // subset pass 2: per forwarded query its row-subset mask; per query the merged top-2 keys
     DevBuf porder, work2, work2_n;   // pair order (by train image) and the compacted pass-2 work list
     DevBuf unsettled;                // int32: pass-1 forwarded queries pass 2 never wrote (must stay 0)
     DevBuf prep_tab;                 // batched SIFT prep: one PrepImg per image
@@ -168,7 +170,7 @@ struct sfmx_matcher {
     size_t plan_nwork = 0, plan_nwork32 = 0;
     int plan_max_nt = 0;
     bool has_run = false;
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};   // run start, main kernel end, run end
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // run start, main kernel end, run end, pass-1 end
     bool ev_recorded = false;
 };
 
@@ -350,6 +352,10 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
         if ((rc = m->slow_list.ensure(sizeof(int2) * std::max<int64_t>(dense, 1)))) return rc;
         if ((rc = m->slow_count.ensure(sizeof(int32_t)))) return rc;
         if ((rc = m->qlist.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
+        if (m->norm == SFMX_NORM_L2) {
+            if ((rc = m->qmask.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
+            if ((rc = m->top2.ensure(2 * sizeof(uint64_t) * std::max<int64_t>(dense, 1)))) return rc;
+        }
         if ((rc = m->qcount.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
         if ((rc = m->porder.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
         if ((rc = m->work2.ensure(sizeof(WorkItem) * std::max<size_t>(4 * work.size(), 1)))) return rc;   // pass-2 items >= 128 queries
@@ -389,6 +395,7 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     HIPCHK(hipMemsetAsync(m->slow_count.p, 0, sizeof(int32_t), st));
     HIPCHK(hipMemsetAsync(m->unsettled.p, 0, sizeof(int32_t), st));
     HIPCHK(hipEventRecord(m->ev[0], st));
+    HIPCHK(hipEventRecord(m->ev[3], st));   // re-recorded after pass 1 by the two-pass launchers
     // Pairs with an empty left image have no work item; pairs with an empty
     // right image are handled in-kernel (every query: no neighbour).
     const PairDev* P = m->pairs_d.as<PairDev>();
@@ -398,7 +405,8 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
                                 m->normv.as<int32_t>(), m->keyc.as<int32_t>(), m->keyc2.as<int32_t>(),
                                 m->qlist.as<int32_t>(), m->qcount.as<int32_t>(), n_pairs, m->porder.as<int32_t>(),
                                 m->work2.as<WorkItem>(), m->work2_n.as<int32_t>(), m->dense_idx.as<int32_t>(),
-                                m->dense_dist.as<float>(), m->slow_list.as<int2>(), m->slow_count.as<int32_t>(), ratio, st));
+                                m->dense_dist.as<float>(), m->slow_list.as<int2>(), m->slow_count.as<int32_t>(), ratio, st,
+                                m->ev[3], m->qmask.as<int32_t>(), m->top2.as<unsigned long long>()));
         HIPCHK(hipEventRecord(m->ev[1], st));
         HIPCHK(launch_sift_slow(m->slow_list.as<int2>(), m->slow_count.as<int32_t>(), P, I, m->desc8.as<int8_t>(),
                                 m->normv.as<int32_t>(), m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
@@ -409,7 +417,7 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
         HIPCHK(launch_orb_mfma(m->work_d.as<WorkItem>(), (int)n_work, P, I, m->desc8.as<uint8_t>(),
                                m->keyc.as<int32_t>(), m->qlist.as<int32_t>(), m->qcount.as<int32_t>(), n_pairs,
                                m->porder.as<int32_t>(), m->work2.as<WorkItem>(), m->work2_n.as<int32_t>(),
-                               m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
+                               m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st, m->ev[3]));
         HIPCHK(hipEventRecord(m->ev[1], st));
     } else {
         HIPCHK(launch_orb_knn2(m->work_d.as<WorkItem>(), (int)n_work, P, I, m->desc8.as<uint8_t>(),
@@ -567,6 +575,19 @@ int sfmx_matcher_timing(sfmx_matcher* m, float* main_kernel_ms, float* total_ms)
     HIPCHK(hipEventElapsedTime(&b, m->ev[0], m->ev[2]));
     if (main_kernel_ms) *main_kernel_ms = a;
     if (total_ms) *total_ms = b;
+    return SFMX_OK;
+}
+
+int sfmx_matcher_pass_timing(sfmx_matcher* m, float* screen_ms, float* pass2_ms) {
+    if (!m) return fail(SFMX_EINVAL, "null matcher");
+    if (!m->ev_recorded) return fail(SFMX_ESTATE, "no timing before run");
+    DeviceGuard g(m->device);
+    HIPCHK(hipEventSynchronize(m->ev[2]));
+    float a = 0.f, b = 0.f;
+    HIPCHK(hipEventElapsedTime(&a, m->ev[0], m->ev[3]));
+    HIPCHK(hipEventElapsedTime(&b, m->ev[3], m->ev[1]));
+    if (screen_ms) *screen_ms = a;
+    if (pass2_ms) *pass2_ms = b;
     return SFMX_OK;
 }
 

@@ -163,6 +163,12 @@ class BFMatcher:
         check(lib.sfmx_matcher_timing(self._h, C.byref(a), C.byref(b)), "sfmx_matcher_timing")
         return a.value, b.value
 
+    def pass_timing(self):
+        """-> (screen ms, pass-2 ms) of the last run's two-pass 2-NN launch (screen 0 when single pass)."""
+        a, b = C.c_float(), C.c_float()
+        check(lib.sfmx_matcher_pass_timing(self._h, C.byref(a), C.byref(b)), "sfmx_matcher_pass_timing")
+        return a.value, b.value
+
     def match_pairs(self, mats, pairs, ratio=LOWE_RATIO, distinct=False, min_count=0):
         self.set_images(mats)
         self.run(pairs, ratio, distinct, min_count)

@@ -83,12 +83,15 @@ def test_ragged_sizes_vs_oracle():
     assert stats == (0, 0)
 
 
-# Screening-pass shapes (103: 32x32x32 MFMA, 106-108: 16x16x64) and pass-2 item
-# sizes (SFMX_SIFT_P2: 1/3 = 256 queries, 4 = 512, 0 = 128): every shipped or
-# tuned kernel form must give the oracle's matches.  The uniform set has many
-# queries whose best two share a screening subset, so pass 2 sees both accepted
-# and undecided queries; 1100-query images split a pair's list over several items.
-@pytest.mark.parametrize("variant,p2", [("103", "0"), ("106", "4"), ("107", "1"), ("108", "3"), ("0", "0")])
+# Screening-pass shapes (103: 32x32x32 MFMA, 106-108: 16x16x64) and pass 2 forms
+# (SFMX_SIFT_P2: 10 = the subset pass 2, the default; full-row GATHER items of
+# 1/3 = 256 queries, 4 = 512, 0 = 128): every shipped or tuned kernel form must give
+# the oracle's matches.  The uniform set has many queries whose best two share a
+# screening subset, so pass 2 sees both accepted and undecided queries; 1100-query
+# images split a pair's list over several items; images of 1 and 33 rows leave
+# row subsets empty (r >= nt) or hold a single row.
+@pytest.mark.parametrize("variant,p2", [("103", "0"), ("106", "4"), ("107", "1"), ("108", "3"), ("0", "0"),
+                                        ("0", "10")])
 def test_two_pass_variants_vs_oracle(variant, p2):
     from oracle import oracle
     sizes = [1, 33, 257, 513, 1100, 1100]
