@@ -1374,13 +1374,14 @@ void orb_mfma16_kernel(const WorkItem* __restrict__ work, const PairDev* __restr
 // true second best; Lowe's test is non-decreasing in d2, so when it fails at
 // (d1, d2') it fails for the true pair and the query is rejected exactly.  Every
 // other query goes to its pair's qlist for orb_mfma16_kernel<GATHER>.
-template <int QT, int WAVES, int MINW, int STAGE>
+template <int QT, int WAVES, int MINW, int STAGE, bool SUBSET = false>
 __global__ __launch_bounds__(WAVES * 64, MINW)
 void orb_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
                          const ImgDev* __restrict__ imgs, const uint8_t* __restrict__ desc4,
                          const int32_t* __restrict__ keyc, int32_t* __restrict__ out_idx,
                          float* __restrict__ out_dist, int32_t* __restrict__ qlist, int32_t* __restrict__ qcount,
-                         double ratio) {
+                         double ratio, int32_t* __restrict__ qmask = nullptr,
+                         unsigned long long* __restrict__ top2 = nullptr) {
     constexpr int ROWB = 128;
     constexpr int GLDS = STAGE * ROWB / (WAVES * 64 * 16);
     static_assert(GLDS * WAVES * 64 * 16 == STAGE * ROWB, "stage must split into whole 16-B pieces");
@@ -1483,6 +1484,19 @@ void orb_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __res
             k2 = fmaxf(fminf(k1, p1), fmaxf(k2, p2));
             k1 = fmaxf(k1, p1);
         }
+        // SUBSET: subsets whose best Hamming distance is <= the second subset's (integer part of
+        // the key): a row of any other subset is strictly farther than two distinct rows
+        int mask = 0xFFFF;
+        if constexpr (SUBSET) {
+            const float f2 = __builtin_floorf(k2);
+            int nib = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) nib |= (__builtin_floorf(ch[qt][i]) >= f2 ? 1 : 0) << i;
+            int mk = nib << (4 * g);
+            mk |= __shfl_xor(mk, 16);
+            mk |= __shfl_xor(mk, 32);
+            if (nt >= 2 && k2 >= KEY_FLOOR) mask = mk;
+        }
         const int qi = qbase + qt * 16 + l16;
         if (g != 0 || qi >= nq) continue;
         const int64_t o = P.dense_base + qi;
@@ -1499,8 +1513,177 @@ void orb_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __res
         } else {
             const int slot = atomicAdd(&qcount[w.pair], 1);
             qlist[P.dense_base + slot] = qi;
+            if constexpr (SUBSET) {
+                qmask[P.dense_base + slot] = mask;
+                top2[2 * o] = ~0ull;
+                top2[2 * o + 1] = ~0ull;
+            }
             out_idx[o] = UNSETTLED;   // pass 2 must overwrite it (assemble counts survivors)
         }
+    }
+}
+
+// ORB pass 2, subset form (default): as sift_subset_kernel, on the FP4 +-1 rows with
+// v_mfma_scale_f32_16x16x128_f8f6f4.  Subset r's rows j = r + 16 i get the C-operand key
+// 767 + (16383 - i) / 16384 (the local index keeps j's order), so a lane's float top-2 (v_med3_f32 /
+// v_max_f32) ranks (Hamming distance, j) exactly; one 16-query tile per wave pair of blocks.  The
+// (query, subset) top-2 is merged into the query's pair of 64-bit keys (d << 32) | j with atomicMin
+// (sift_subset_kernel); orb_settle_kernel writes the results.
+template <int WAVES, int QT>
+__global__ __launch_bounds__(WAVES * 64, 2)
+void orb_subset_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restrict__ imgs,
+                       const uint8_t* __restrict__ desc4, const int32_t* __restrict__ qlist,
+                       const int32_t* __restrict__ qmask, const int32_t* __restrict__ qcount,
+                       const int32_t* __restrict__ porder, unsigned long long* __restrict__ top2) {
+    constexpr int ROWB = 128;
+    constexpr int CH = 256;                   // rows per LDS chunk
+    constexpr int QC = WAVES * QT * 16;       // queries per tile group
+    constexpr int WIN = 1024;
+    constexpr int GLDS = CH * ROWB / (WAVES * 64 * 16);
+    static_assert(GLDS * WAVES * 64 * 16 == CH * ROWB, "chunk must split into whole 16-B pieces");
+    constexpr float KEY_FLOOR = 256.f;
+    __shared__ __attribute__((aligned(16))) char rows_lds[CH * ROWB];
+    __shared__ float keys_lds[CH];
+    __shared__ int ql[WIN];
+    __shared__ int s_n;
+
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, g = lane >> 4, l16 = lane & 15;
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    const int pi = porder[item >> 4], r = item & 15;
+    const int cnt = qcount[pi];
+    const PairDev P = pairs[pi];
+    const ImgDev L = imgs[P.left], R = imgs[P.right];
+    const int nt = R.rows;
+    const int nr = R.rows_pad >> 4;
+    if (cnt == 0 || r >= nt) return;
+    const int32_t* qls = qlist + P.dense_base;
+    const int32_t* qms = qmask + P.dense_base;
+    auto i8of = [](const i32x4& v) { return i32x8{v.x, v.y, v.z, v.w, 0, 0, 0, 0}; };
+
+    for (int e0 = 0; e0 < cnt; e0 += WIN) {
+        if (tid == 0) s_n = 0;
+        __syncthreads();
+        for (int e = e0 + tid; e < min(cnt, e0 + WIN); e += WAVES * 64)
+            if ((qms[e] >> r) & 1) ql[atomicAdd(&s_n, 1)] = qls[e];
+        __syncthreads();
+        const int n = s_n;
+        for (int g0 = 0; g0 < n; g0 += QC) {
+            int qrow[QT];
+            i32x4 bq[QT][2];
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const int qe = g0 + (wid * QT + qt) * 16 + l16;
+                qrow[qt] = qe < n ? ql[qe] : -1;
+                const i32x4* src = reinterpret_cast<const i32x4*>(desc4 + (L.row0 + (qrow[qt] < 0 ? 0 : qrow[qt])) * ROWB);
+#pragma unroll
+                for (int m = 0; m < 2; ++m) bq[qt][m] = src[4 * m + g];
+            }
+            const bool active = g0 + wid * QT * 16 < n;   // wave-uniform
+            float c1[QT], c2[QT];
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) c1[qt] = c2[qt] = 0.f;
+            for (int c0 = 0; c0 < nr; c0 += CH) {
+                const int rows = min(CH, nr - c0);   // a multiple of 32
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < GLDS; ++u) {
+                    const int p = u * WAVES * 64 + tid;
+                    const int rr = p >> 3, slot = p & 7, c = slot ^ ((rr >> 1) & 7);
+                    const int j = r + 16 * (c0 + (rr < rows ? rr : 0));
+                    const uint8_t* gp = desc4 + (R.row0 + j) * ROWB + 16 * c;
+                    __builtin_amdgcn_global_load_lds((const GLOBAL_AS void*)gp,
+                                                     (LDS_AS void*)(rows_lds + (u * WAVES + wid) * 1024), 16, 0, 0);
+                }
+                for (int i = tid; i < CH; i += WAVES * 64) {
+                    const int li = c0 + i, j = r + 16 * li;
+                    keys_lds[i] = (i < rows && j < nt) ? (float)(767 * 16384 + 16383 - li) * (1.0f / 16384.0f) : 0.f;
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (active) {
+                    for (int t = 0; t < rows / 32; ++t) {
+                        i32x4 a[2][2];
+                        f32x4 cinit[2];
+#pragma unroll
+                        for (int b = 0; b < 2; ++b) {
+                            const int row = t * 32 + b * 16 + l16;
+#pragma unroll
+                            for (int m = 0; m < 2; ++m) {
+                                const int slot = (4 * m + g) ^ ((row >> 1) & 7);
+                                a[b][m] = *reinterpret_cast<const i32x4*>(rows_lds + row * ROWB + 16 * slot);
+                            }
+                            cinit[b] = *reinterpret_cast<const f32x4*>(keys_lds + t * 32 + b * 16 + 4 * g);
+                        }
+#pragma unroll
+                        for (int qt = 0; qt < QT; ++qt) {
+                            f32x4 acc[2];
+#pragma unroll
+                            for (int b = 0; b < 2; ++b) {
+                                acc[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(i8of(a[b][0]), i8of(bq[qt][0]), cinit[b],
+                                                                                          4, 4, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+                                acc[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(i8of(a[b][1]), i8of(bq[qt][1]), acc[b],
+                                                                                          4, 4, 0, 0x7f7f7f7f, 0, 0x7f7f7f7f);
+                            }
+#pragma unroll
+                            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                                for (int q = 0; q < 4; q += 2) {
+                                    const float ka = acc[b][q], kb = acc[b][q + 1];
+                                    c2[qt] = fmaxf(__builtin_amdgcn_fmed3f(c1[qt], ka, kb), c2[qt]);
+                                    c1[qt] = fmaxf(c1[qt], fmaxf(ka, kb));
+                                }
+                        }
+                    }
+                }
+            }
+            if (active) {
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) {
+                    float m1 = c1[qt], m2 = c2[qt];
+#pragma unroll
+                    for (int o = 16; o <= 32; o <<= 1) {
+                        const float p1 = __shfl_xor(m1, o), p2 = __shfl_xor(m2, o);
+                        m2 = fmaxf(fminf(m1, p1), fmaxf(m2, p2));
+                        m1 = fmaxf(m1, p1);
+                    }
+                    if (g != 0 || qrow[qt] < 0) continue;
+                    unsigned long long* bp = top2 + 2 * (P.dense_base + qrow[qt]);
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const float v = e == 0 ? m1 : m2;
+                        if (v < KEY_FLOOR) continue;
+                        const float ip = __builtin_floorf(v);
+                        const int d = (256 - ((int)ip - 767)) >> 1;
+                        const int li = 16383 - (int)((v - ip) * 16384.0f);
+                        const unsigned long long k = ((unsigned long long)d << 32) | (unsigned)(r + 16 * li);
+                        const unsigned long long old = atomicMin(bp, k);
+                        atomicMin(bp + 1, old > k ? old : k);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256)
+void orb_settle_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restrict__ imgs,
+                       const int32_t* __restrict__ qlist, const int32_t* __restrict__ qcount,
+                       const unsigned long long* __restrict__ top2, int32_t* __restrict__ out_idx,
+                       float* __restrict__ out_dist, double ratio) {
+    const int pi = blockIdx.x;
+    const int cnt = qcount[pi];
+    if (cnt == 0) return;
+    const PairDev P = pairs[pi];
+    const int nt = imgs[P.right].rows;
+    for (int e = threadIdx.x; e < cnt; e += 256) {
+        const int qi = qlist[P.dense_base + e];
+        const int64_t o = P.dense_base + qi;
+        const unsigned long long b0 = top2[2 * o], b1 = top2[2 * o + 1];
+        if (b0 == ~0ull || (nt >= 2 && b1 == ~0ull)) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }   // not reached
+        const float d1 = (float)(int)(b0 >> 32), d2 = nt >= 2 ? (float)(int)(b1 >> 32) : 0.f;
+        out_idx[o] = lowe_select((int)(b0 & 0xffffffffu), d1, d2, nt, ratio);
+        out_dist[o] = d1;
     }
 }
 
@@ -1855,11 +2038,23 @@ hipError_t launch_prep_hamming_fp4(const uint8_t* src, int rows, int cols, int r
 hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
                            const uint8_t* desc4, const int32_t* keyc, int32_t* qlist, int32_t* qcount, int n_pairs,
                            const int32_t* porder, WorkItem* work2, int32_t* work2_n, int32_t* out_idx, float* out_dist,
-                           double ratio, hipStream_t st, hipEvent_t ev_screen) {
+                           double ratio, hipStream_t st, hipEvent_t ev_screen, int32_t* qmask,
+                           unsigned long long* top2) {
     if (n_work == 0) return hipSuccess;
     if (orb_variant() == 0 || orb_variant() >= 10) {   // two-pass ratio test (default)
         hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * n_pairs, st);
         if (e != hipSuccess) return e;
+        if (orb_variant() == 0 && qmask && top2) {   // subset-restricted pass 2 (default)
+            orb_screen16_kernel<8, 4, 2, 64, true><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx,
+                                                                          out_dist, qlist, qcount, ratio, qmask, top2);
+            if (ev_screen) {
+                e = hipEventRecord(ev_screen, st);
+                if (e != hipSuccess) return e;
+            }
+            orb_subset_kernel<4, 2><<<n_pairs * 16, 256, 0, st>>>(pairs, imgs, desc4, qlist, qmask, qcount, porder, top2);
+            orb_settle_kernel<<<n_pairs, 256, 0, st>>>(pairs, imgs, qlist, qcount, top2, out_idx, out_dist, ratio);
+            return hipGetLastError();
+        }
         orb_screen16_kernel<8, 4, 2, 64><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx, out_dist,
                                                                   qlist, qcount, ratio);
         if (ev_screen) {
@@ -1881,7 +2076,7 @@ hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pair
         // r01g config 4: 18.68-18.73 ms (two-pass) vs 20.19-20.24 (single pass, variant 5).
         case 13: ORB_PASS2(7, 2, 4); break;   // 128-query items (2 tiles per wave)
         case 14: ORB_PASS2(8, 4, 4); break;   // 256-query items (4 tiles per wave)
-        default: ORB_PASS2(9, 8, 4);       // 0 / 12: 512-query items
+        default: ORB_PASS2(9, 8, 4);       // 12: 512-query items (the r01 pass 2)
         }
 #undef ORB_PASS2
         return hipGetLastError();

@@ -46,7 +46,7 @@ hipError_t launch_orb_knn2(const WorkItem*, int, const PairDev*, const ImgDev*, 
 hipError_t launch_prep_hamming_fp4(const uint8_t*, int, int, int, uint8_t*, int32_t*, hipStream_t);
 hipError_t launch_orb_mfma(const WorkItem*, int, const PairDev*, const ImgDev*, const uint8_t*, const int32_t*,
                            int32_t*, int32_t*, int, const int32_t*, WorkItem*, int32_t*, int32_t*, float*, double,
-                           hipStream_t, hipEvent_t);
+                           hipStream_t, hipEvent_t, int32_t*, unsigned long long*);
 int orb_variant();
 hipError_t launch_selftest_sqrt(int64_t, uint32_t*, hipStream_t);
 int sift_variant();
@@ -352,7 +352,7 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
         if ((rc = m->slow_list.ensure(sizeof(int2) * std::max<int64_t>(dense, 1)))) return rc;
         if ((rc = m->slow_count.ensure(sizeof(int32_t)))) return rc;
         if ((rc = m->qlist.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
-        if (m->norm == SFMX_NORM_L2) {
+        if (m->norm == SFMX_NORM_L2 || m->orb_fp4) {
             if ((rc = m->qmask.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
             if ((rc = m->top2.ensure(2 * sizeof(uint64_t) * std::max<int64_t>(dense, 1)))) return rc;
         }
@@ -417,7 +417,8 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
         HIPCHK(launch_orb_mfma(m->work_d.as<WorkItem>(), (int)n_work, P, I, m->desc8.as<uint8_t>(),
                                m->keyc.as<int32_t>(), m->qlist.as<int32_t>(), m->qcount.as<int32_t>(), n_pairs,
                                m->porder.as<int32_t>(), m->work2.as<WorkItem>(), m->work2_n.as<int32_t>(),
-                               m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st, m->ev[3]));
+                               m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st, m->ev[3],
+                               m->qmask.as<int32_t>(), m->top2.as<unsigned long long>()));
         HIPCHK(hipEventRecord(m->ev[1], st));
     } else {
         HIPCHK(launch_orb_knn2(m->work_d.as<WorkItem>(), (int)n_work, P, I, m->desc8.as<uint8_t>(),

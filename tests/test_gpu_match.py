@@ -134,18 +134,24 @@ def test_orb_ragged_vs_oracle():
     assert_same(m, off, em, eoff)
 
 
+@pytest.mark.parametrize("variant", ["0", "12"])
 @pytest.mark.parametrize("ratio", [0.0, 0.7, 0.95, 1.0, 1.5])
-def test_orb_two_pass_ratios_vs_oracle(ratio):
+def test_orb_two_pass_ratios_vs_oracle(ratio, variant):
     """The ORB screening pass settles rejections from subset-maxima bounds; every
     ratio (none accepted at 0, ties accepted only above 1) must give the oracle's
-    list.  Planted rows with few flipped bits plus exact duplicates (ties)."""
+    list, with the subset pass 2 (default, 0) and the r01 full-row pass 2 (12).
+    Planted rows with few flipped bits plus exact duplicates (ties)."""
     from oracle import oracle
     base = synth.orb_images(4, 1200, seed=61)
     base[1][:40] = base[0][:40]
     base[2][100:140] = base[2][:40]
     imgs = [base[0], base[1][:900], base[2], base[3][:2]]
     pairs = sfmx.pairs_unordered(4)
-    m, off, _, _ = run(imgs, pairs, ratio=ratio)
+    os.environ["SFMX_ORB_VARIANT"] = variant
+    try:
+        m, off, _, _ = run(imgs, pairs, ratio=ratio)
+    finally:
+        del os.environ["SFMX_ORB_VARIANT"]
     em, eoff = oracle.match_pairs(imgs, pairs, ratio)
     assert_same(m, off, em, eoff)
 
