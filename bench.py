@@ -188,7 +188,8 @@ def bench_match(kind, args, rank, world, local):
         dtype = "fp4 e2m1 (+-1 bits) -> f32, exact"
         scaling = "strong"
         data = "synthetic (seeded uniform 256-bit ORB descriptors, 25% planted with 0-24 flipped bits; no dataset)"
-        kernel = "orb_screen16_kernel + orb_mfma16_kernel<GATHER> (two-pass ratio test, both passes)"
+        kernel = ("orb_screen16_kernel + orb_subset_kernel + orb_settle_kernel (two-pass ratio test, both passes; "
+                  "pass 2 on the forwarded queries' row subsets)")
         algo = "512 ops (256 +-1 MAC: dot = 256 - 2 hamming) per descriptor pair"
         if os.environ.get("SFMX_ORB_VARIANT", "0") == "1":   # VALU xor/popcount kernel (comparison only)
             op_per_pair, bound, peak, unit = ORB_OPS_PER_PAIR, "valu", VALU_PEAK_TOPS, "TOP/s"
@@ -297,6 +298,15 @@ def bench_match(kind, args, rank, world, local):
         "slow_path_queries": slow,
         "fp32_fallback_pairs": f32p,
     }
+    if kind == "orb" and bound == "mfma":
+        # SURVEY.md §8d prices ORB at 16 VALU ops per pair (8 xor + 8 popcount): the same pairs/s on
+        # that scale, against the VALU issue peak (north_star reserves MFMA for SIFT; this path uses
+        # the FP4 MFMA on a +-1 encoding instead, so the VALU view can exceed 1)
+        pairs_per_s = logical_mine / (kern_ms * 1e-3)
+        res["roofline"]["survey_valu_view"] = {
+            "ops_per_pair": ORB_OPS_PER_PAIR, "achieved": pairs_per_s * ORB_OPS_PER_PAIR / 1e12,
+            "peak": VALU_PEAK_TOPS, "unit": "TOP/s", "frac": pairs_per_s * ORB_OPS_PER_PAIR / 1e12 / VALU_PEAK_TOPS,
+            "what": "pairs/s x 16 VALU ops vs the VALU peak: how far past the VALU xor/popcount ceiling the FP4 MFMA path runs"}
     if homog is not None:
         res["homography"] = homog
     if f4 is not None:
@@ -437,7 +447,7 @@ def bench_3d2d(args, imgs, my_pairs, got, off, rank, world, local, stream):
 
 SIFT_KERNELS = ("sift_screen16_kernel", "sift_subset_kernel", "sift_settle_kernel")
 PMC_FILES = {"sift": ("r02_pmc_sift_c2.json", SIFT_KERNELS, 50),
-             "orb": ("r01h_pmc_orb.json", ("orb_screen16_kernel", "orb_mfma16_kernel"), 200),
+             "orb": ("r02_pmc_orb_c4.json", ("orb_screen16_kernel", "orb_subset_kernel", "orb_settle_kernel"), 200),
              "c3": ("r02_pmc_sift_c3.json", SIFT_KERNELS, 200)}
 
 
@@ -481,6 +491,11 @@ def bench_ba(args, rank, world, local):
         dist.barrier()
     torch.cuda.synchronize()
     sm, tr = ctx.run(trace_cap=1024)
+    # per-phase breakdown from a second solve with phase events on (outside the timed run: each
+    # event costs GPU time)
+    ctx.reset()
+    ctx.set_phase_timing(True)
+    ctx.run(trace_cap=0)
     phases = ctx.phase_ms()
     ctx.close()
     iters = sm["num_successful_steps"] + sm["num_unsuccessful_steps"]

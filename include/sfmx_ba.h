@@ -107,8 +107,11 @@ int sfmx_ba_get(sfmx_ba_ctx* ctx, sfmx_ba_problem* problem);
 int sfmx_ba_set(sfmx_ba_ctx* ctx, const sfmx_ba_problem* problem);
 /* Per-phase device time of the last run (ms, summed over its iterations):
  * [0] linearize (residuals + Jacobians), [1] Schur assembly, [2] Cholesky + solves,
- * [3] step / candidate cost.  n = number of entries written. */
+ * [3] step / candidate cost.  n = number of entries written.  [1]..[3] are recorded only while
+ * phase timing is on (sfmx_ba_set_phase_timing; off by default: each event costs GPU time). */
 int sfmx_ba_phase_ms(sfmx_ba_ctx* ctx, double* ms, int32_t n);
+/* Diagnostics: record the per-phase events of sfmx_ba_phase_ms in later runs (on != 0). */
+int sfmx_ba_set_phase_timing(sfmx_ba_ctx* ctx, int32_t on);
 int sfmx_ba_destroy(sfmx_ba_ctx* ctx);
 
 /* Residuals and Jacobian blocks (device-computed) of every observation at the

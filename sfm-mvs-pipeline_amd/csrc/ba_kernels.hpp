@@ -203,6 +203,21 @@ void ba_sum(const double* __restrict__ partial, int n, double scale, double* __r
 }
 
 // scale = 1 / (1 + sqrt(colsq)) (iteration 0 only, Ceres jacobi_scaling)
+// The LM scalars into pinned, host-coherent memory, then the sequence number with system-scope
+// release: the host polls the sequence number instead of a D2H copy + stream synchronisation
+// (the interrupt-driven wake-up of hipStreamSynchronize costs ~50 us per LM step).
+// It also clears the step's failure flag (already folded into the scalars by ba_finalize), so the
+// next step starts without a separate memset.
+__global__ void ba_publish(const double* __restrict__ src, int n, double* __restrict__ dst, unsigned* __restrict__ seq,
+                           unsigned v, int* __restrict__ fail) {
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < n; ++i) dst[i] = src[i];
+        *fail = 0;
+        __threadfence_system();
+        __hip_atomic_store(seq, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __global__ void ba_scale(int n, const double* __restrict__ colsq, double* __restrict__ scale) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) scale[i] = 1.0 / (1.0 + sqrt(colsq[i]));

@@ -100,7 +100,10 @@ struct sfmx_ba_ctx {
     // observation o' is caller observation operm[o'] (point-major)
     std::vector<int> pperm, operm;
     double phase_ms[4] = {0, 0, 0, 0};
+    bool phases = false;         // per-phase events (sfmx_ba_set_phase_timing): ~6 us of GPU time each
     hipEvent_t ev[6] = {};
+    double* hs = nullptr;        // pinned host-coherent LM scalars [SC_N] + sequence word (ba_publish)
+    unsigned seq = 0;
     ~sfmx_ba_ctx() {
         Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
@@ -113,6 +116,7 @@ struct sfmx_ba_ctx {
         for (Buf* b : all) b->release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (st) (void)hipStreamDestroy(st);
+        if (hs) (void)hipHostFree(hs);
         (void)hipSetDevice(prev);
     }
 };
@@ -143,6 +147,30 @@ double* scal(sfmx_ba_ctx* c, int i) { return c->scal.as<double>() + i; }
 int fetch_scalars(sfmx_ba_ctx* c, int i0, int cnt, double* out) {
     HIPCHK(hipMemcpyAsync(out, scal(c, i0), sizeof(double) * cnt, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    return SFMX_OK;
+}
+
+// The LM step's scalars: ba_publish writes them to pinned memory behind everything queued so far
+// and the host spins on the sequence word (a stream error or a drained stream without the word
+// ends the wait).
+int poll_scalars(sfmx_ba_ctx* c, double* out, hipEvent_t mark) {
+    const unsigned want = ++c->seq;
+    if (mark) HIPCHK(hipEventRecord(mark, c->st));
+    unsigned* hseq = reinterpret_cast<unsigned*>(c->hs + SC_N);
+    hipLaunchKernelGGL(ba_publish, dim3(1), dim3(64), 0, c->st, scal(c, 0), (int)SC_N, c->hs, hseq, want,
+                       c->failf.as<int>());
+    HIPCHK(hipGetLastError());
+    for (unsigned spins = 1;; ++spins) {
+        if (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == want) break;
+        if ((spins & 255) == 0) {
+            const hipError_t e = hipStreamQuery(c->st);
+            if (e != hipSuccess && e != hipErrorNotReady) return fail(SFMX_EDEVICE, std::string("LM step: ") + hipGetErrorString(e));
+            if (e == hipSuccess && __atomic_load_n(hseq, __ATOMIC_ACQUIRE) != want)
+                return fail(SFMX_EINTERNAL, "LM step: stream drained without the scalar handoff");
+        }
+        __builtin_ia32_pause();
+    }
+    std::memcpy(out, c->hs, sizeof(double) * SC_N);
     return SFMX_OK;
 }
 
@@ -185,7 +213,7 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double
     HIPCHK(hipGetLastError());
     RC(allreduce(c, scal(c, SC_COST), 4, SFMX_REDUCE_SUM));
     RC(allreduce(c, scal(c, SC_GMAX), 2, SFMX_REDUCE_MAX));
-    RC(fetch_scalars(c, 0, SC_N, out));
+    RC(poll_scalars(c, out, c->phases && cand_mode ? c->ev[3] : nullptr));
     return SFMX_OK;
 }
 
@@ -230,8 +258,8 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     double* ri = Dm + K * K;
     int* fl = c->failf.as<int>();
     const sfmx_ba_options& o = c->opt;
-    HIPCHK(hipMemsetAsync(fl, 0, sizeof(int), c->st));
-    HIPCHK(hipEventRecord(c->ev[0], c->st));
+    // the failure flag is zero here: cleared by the run's start and by every scalar handoff (ba_publish)
+    if (c->phases) HIPCHK(hipEventRecord(c->ev[0], c->st));
     if (c->ngroups > 0) {
 #define GSCHUR(NTV) if (sj) GSCHUR2(NTV, true); else GSCHUR2(NTV, false)
 #define GSCHUR2(NTV, SJ) hipLaunchKernelGGL((ba_gschur<K, NTV, SJ>), dim3(c->ngroups), dim3(256), c->lds_schur, c->st,     \
@@ -250,7 +278,7 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
                        c->sg.as<double>(), c->hbig.as<double>(), c->rg.as<double>(), K, c->camrow.as<int>(), npad, S,
                        R, Dm, ri);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[1], c->st));
+    if (c->phases) HIPCHK(hipEventRecord(c->ev[1], c->st));
     // point-sharded ranks: the group part of the reduced camera system and its rhs are sums over
     // ranks; only the structurally nonzero lower tiles (+ R, D, r_i) travel
     if (c->ar) {
@@ -267,7 +295,7 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
                        R, Dm, ri);
     double* sol = c->sol.as<double>();
     RC(solve_reduced<RW>(c, sol + c->ne));
-    HIPCHK(hipEventRecord(c->ev[2], c->st));
+    if (c->phases) HIPCHK(hipEventRecord(c->ev[2], c->st));
     if (c->ngroups > 0)
         hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups), dim3(256), 0, c->st, c->grp.as<Grp>(),
                            c->chk.as<Chunk>(), c->obs_point.as<int>(), c->obs_cam.as<int>(), c->pt_start.as<int>(),
@@ -279,8 +307,6 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     double v[SC_N];
     RC(lin_at<K>(c, c->cand.as<double>(), c->J2.as<double>(), c->colsq2.as<double>(), c->grad2.as<double>(),
                  c->camsum2.as<double>(), true, v));
-    HIPCHK(hipEventRecord(c->ev[3], c->st));
-    HIPCHK(hipEventSynchronize(c->ev[3]));
     const double sn2 = v[SC_STEPN] + v[SC_STEPN_F];
     *mcc = -v[SC_MODEL];
     *step_norm = std::sqrt(sn2);
@@ -289,13 +315,16 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     if (*valid) *ccost = std::isfinite(v[SC_COST]) ? v[SC_COST] : std::numeric_limits<double>::max();
     *cgmax = v[SC_GMAX];
     *cxnorm = std::sqrt(v[SC_XN] + v[SC_XN_F]);
-    float a = 0, b = 0, d = 0;
-    HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
-    HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
-    HIPCHK(hipEventElapsedTime(&d, c->ev[2], c->ev[3]));
-    c->phase_ms[1] += a;
-    c->phase_ms[2] += b;
-    c->phase_ms[3] += d;
+    if (c->phases) {
+        float a = 0, b = 0, d = 0;
+        HIPCHK(hipEventSynchronize(c->ev[3]));
+        HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+        HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+        HIPCHK(hipEventElapsedTime(&d, c->ev[2], c->ev[3]));
+        c->phase_ms[1] += a;
+        c->phase_ms[2] += b;
+        c->phase_ms[3] += d;
+    }
     return SFMX_OK;
 }
 
@@ -713,6 +742,10 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
     auto bail = [&](int rc) { delete c; return rc; };
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) return bail(fail(SFMX_EDEVICE, "stream"));
     for (auto& e : c->ev) if (hipEventCreate(&e) != hipSuccess) return bail(fail(SFMX_EDEVICE, "event"));
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->hs), sizeof(double) * (SC_N + 1),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return bail(fail(SFMX_ENOMEM, "pinned scalar buffer"));
+    std::memset(c->hs, 0, sizeof(double) * (SC_N + 1));
     const int P = caller->n_points, C = caller->n_cams, O = caller->n_obs, K = caller->cam_model;
     c->P = P; c->C = C; c->O = O; c->K = K; c->cx = caller->cx; c->cy = caller->cy;
     c->ne = 3 * (int64_t)P;
@@ -906,6 +939,12 @@ int sfmx_ba_set(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
     if (!c || !pb) return fail(SFMX_EINVAL, "null context/problem");
     if (pb->n_points != c->P || pb->n_cams != c->C || pb->cam_model != c->K) return fail(SFMX_EINVAL, "topology mismatch");
     return set_params(c, pb);
+}
+
+int sfmx_ba_set_phase_timing(sfmx_ba_ctx* c, int32_t on) {
+    if (!c) return fail(SFMX_EINVAL, "null context");
+    c->phases = on != 0;
+    return SFMX_OK;
 }
 
 int sfmx_ba_phase_ms(sfmx_ba_ctx* c, double* ms, int32_t n) {

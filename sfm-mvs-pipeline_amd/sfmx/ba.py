@@ -141,6 +141,10 @@ class BAContext:
         check(lib.sfmx_ba_get(self._h, C.byref(st)), "sfmx_ba_get")
         return p
 
+    def set_phase_timing(self, on: bool = True):
+        """Record per-phase device events in later runs (diagnostics; each costs GPU time)."""
+        check(lib.sfmx_ba_set_phase_timing(self._h, 1 if on else 0), "sfmx_ba_set_phase_timing")
+
     def phase_ms(self):
         v = (C.c_double * 4)()
         n = check(lib.sfmx_ba_phase_ms(self._h, v, 4), "sfmx_ba_phase_ms")

@@ -64,9 +64,12 @@ def test_context_api_allreduce_identity_and_reset():
     calls = []
     ctx = ba.BAContext(ba.BAProblem(**p), allreduce=lambda ptr, n, op, st: calls.append((n, op)))
     s1, _ = ctx.run()
+    ph0 = ctx.phase_ms()
+    assert ph0["linearize"] > 0 and ph0["schur"] == ph0["cholesky_solve"] == ph0["step_cost"] == 0   # events off by default
     ctx.reset()
+    ctx.set_phase_timing(True)
     s2, _ = ctx.run()
-    assert s1["final_cost"] == s2["final_cost"]
+    assert s1["final_cost"] == s2["final_cost"]             # phase events do not change the numbers
     assert calls and any(n > 1000 for n, _ in calls)        # the reduced camera system went through the hook
     ph = ctx.phase_ms()
     assert set(ph) == {"linearize", "schur", "cholesky_solve", "step_cost"} and all(v > 0 for v in ph.values())
