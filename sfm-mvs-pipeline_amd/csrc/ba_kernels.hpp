@@ -202,7 +202,6 @@ void ba_sum(const double* __restrict__ partial, int n, double scale, double* __r
     if (threadIdx.x == 0) out[0] = scale * s;
 }
 
-// scale = 1 / (1 + sqrt(colsq)) (iteration 0 only, Ceres jacobi_scaling)
 // The LM scalars into pinned, host-coherent memory, then the sequence number with system-scope
 // release: the host polls the sequence number instead of a D2H copy + stream synchronisation
 // (the interrupt-driven wake-up of hipStreamSynchronize costs ~50 us per LM step).
@@ -218,6 +217,7 @@ __global__ void ba_publish(const double* __restrict__ src, int n, double* __rest
     }
 }
 
+// scale = 1 / (1 + sqrt(colsq)) (iteration 0 only, Ceres jacobi_scaling)
 __global__ void ba_scale(int n, const double* __restrict__ colsq, double* __restrict__ scale) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) scale[i] = 1.0 / (1.0 + sqrt(colsq[i]));
