@@ -369,26 +369,26 @@ void chol_pack(const double* __restrict__ S, int npad, const int2* __restrict__ 
     }
 }
 
-// The intrinsics (one workgroup of 64): D' = D - sum_k contrib_k[:, :K], r' = r_i - sum_k
-// contrib_k[:, K] (panel order), K x K Cholesky (non-positive pivot -> fail), x_i = D'^-1 r' ->
-// xi (device scalars for the back solve) and sol_i.
+// The intrinsics: D' = D - sum_k contrib_k[:, :K], r' = r_i - sum_k contrib_k[:, K] (panel order),
+// K x K Cholesky (non-positive pivot -> bad), x_i = D'^-1 r' -> v (thread 0).  Threads t < K (K + 1)
+// fill Dp; the caller's workgroup must reach the barrier inside.
 template <int K>
-__global__ __launch_bounds__(64)
-void chol_intr(const double* __restrict__ Dm, const double* __restrict__ ri, const double* __restrict__ contrib,
-               int T, double* __restrict__ xi, double* __restrict__ sol_i, int* __restrict__ fail) {
+__device__ __forceinline__ void intr_solve(const double* __restrict__ Dm, const double* __restrict__ ri,
+                                           const double* __restrict__ contrib, int T, double* __restrict__ Dp,
+                                           double (&v)[K], bool& bad) {
     constexpr int RW = K + 1;
-    __shared__ double Dp[K * RW];
     const int t = threadIdx.x;
     if (t < K * RW) {
         const int i = t / RW, j = t % RW;
         double s = j < K ? Dm[i * K + j] : ri[i];
-        for (int k = 0; k < T; ++k) s -= contrib[(size_t)k * K * RW + t];
+#pragma unroll 8
+        for (int k = 0; k < T; ++k) s -= contrib[(size_t)k * K * RW + t];   // loads issued 8 ahead, same order
         Dp[t] = s;
     }
     __syncthreads();
+    bad = false;
     if (t == 0) {
-        double L[K][K], v[K];
-        bool bad = false;
+        double L[K][K];
         for (int j = 0; j < K; ++j) {   // lower Cholesky of D' (its lower triangle), Eigen LLT order
             double d = Dp[j * RW + j];
             for (int m = 0; m < j; ++m) d -= L[j][m] * L[j][m];
@@ -410,11 +410,128 @@ void chol_intr(const double* __restrict__ Dm, const double* __restrict__ ri, con
             for (int m = i + 1; m < K; ++m) s -= L[m][i] * v[m];
             v[i] = s / L[i][i];
         }
+    }
+}
+
+// Back solve, one workgroup per panel in ONE launch (replaces chol_intr + chol_back, bit-identical
+// results).  A workgroup takes a ticket (atomic counter) and the panel border[ticket]; border lists
+// the panels root first (level descending), so every panel it waits for (its ancestors k, the
+// upper tiles (i, k)) holds an earlier ticket and is already running or done: no residency or
+// dispatch-order assumption.  Per workgroup:
+//   * prefetch its ancestor tiles U(i, k) (written by earlier launches) into LDS;
+//   * x_i = D'^-1 r' (intr_solve, every workgroup the same; ticket 0 also writes sol_i);
+//   * z_i = w_i(r_c) - w_i(B) x_i - sum_k U(i, k) z_k once every ancestor's z_k is published;
+//   * publish z_i: write-through (sc1) stores, every wave drains, then one lane's sc1 flag store;
+//     the consumer polls the flags with sc1 loads (one lane) and reads z only with sc1 loads
+//     behind the workgroup barrier, so no L1 line can be stale and no acquire fence is needed
+//     (MI355X_MICROARCH.md, inter-workgroup visibility: the valid sc1-load form, table row 1).
+// Spins are bounded (DAG_TIMEOUT of the 100 MHz wall clock): a timed-out wait sets fail bit 2 and
+// the solve reports an internal error.  ctr = [ticket, finished, zdone[T]] is zero at launch; the
+// last workgroup to finish zeroes it for the next launch (nobody polls by then).
+constexpr int BS_PF = 4;                   // ancestor tiles prefetched into LDS per workgroup
+constexpr long long DAG_TIMEOUT = 2000000; // 20 ms
+typedef __attribute__((address_space(1))) int g_i32;
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+__device__ __forceinline__ double ld_wt(const double* p) {   // sc1 load (bypasses this CU's L1)
+    return __longlong_as_double((long long)__hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <int RW>
+__global__ __launch_bounds__(256)
+void chol_backsolve(const double* __restrict__ S, int npad, const double* __restrict__ R,
+                    const double* __restrict__ Dm, const double* __restrict__ ri, const double* __restrict__ contrib,
+                    int T, const int* __restrict__ border, const int* __restrict__ bs_start,
+                    const int* __restrict__ bs_k, const int* __restrict__ rowmap, double* z,
+                    double* __restrict__ xout, double* __restrict__ sol_i, int* ctr, int* __restrict__ fail) {
+    constexpr int K = RW - 1;
+    __shared__ double Ut[BS_PF][NB / 4][256];   // thread-private: its 16 U values per prefetched tile
+    __shared__ double Dp[K * RW], xs[K];
+    __shared__ int sh[2];
+    const int tid = threadIdx.x;
+    if (tid == 0) sh[0] = __hip_atomic_fetch_add((g_i32*)ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int tk = sh[0], i = border[tk];
+    const int row = tid >> 2, q = tid & 3, r = i * NB + row;
+    const int e0 = bs_start[i], e1 = bs_start[i + 1];
+    for (int e = e0; e < e1 && e - e0 < BS_PF; ++e) {
+        const double* U = S + (size_t)r * npad + bs_k[e] * NB;
+#pragma unroll
+        for (int m = 0; m < NB / 4; ++m) Ut[e - e0][m][tid] = U[4 * m + q];
+    }
+    {
+        double v[K];
+        bool bad;
+        intr_solve<K>(Dm, ri, contrib, T, Dp, v, bad);
+        if (tid == 0) {
+            for (int a = 0; a < K; ++a) xs[a] = v[a];
+            if (tk == 0) {
+                if (bad) atomicOr(fail, 1);
+                for (int a = 0; a < K; ++a) sol_i[a] = v[a];
+            }
+        }
+    }
+    __syncthreads();
+    double s = R[(size_t)r * RW + RW - 1];
+#pragma unroll
+    for (int a = 0; a < K; ++a) s -= R[(size_t)r * RW + a] * xs[a];
+    if (tid == 0) {   // ONE lane polls (relaxed), then ONE agent acquire
+        bool ok = true;
+        const long long t0 = wall_clock64();
+        for (int e = e0; e < e1 && ok; ++e)
+            while (__hip_atomic_load((g_i32*)&ctr[2 + bs_k[e]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t0 > DAG_TIMEOUT) { atomicOr(fail, 2); ok = false; break; }
+            }
+        sh[1] = ok;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the z loads below
+    double t = 0.0;
+    if (sh[1]) {
+        for (int e = e0; e < e1; ++e) {
+            const int k0 = bs_k[e] * NB;
+            if (e - e0 < BS_PF) {
+#pragma unroll
+                for (int m = 0; m < NB / 4; ++m) t = fma(Ut[e - e0][m][tid], ld_wt(&z[k0 + 4 * m + q]), t);
+            } else {
+                const double* U = S + (size_t)r * npad + k0;
+#pragma unroll
+                for (int m = 0; m < NB / 4; ++m) t = fma(U[4 * m + q], ld_wt(&z[k0 + 4 * m + q]), t);
+            }
+        }
+    }
+    t += __shfl_xor(t, 1);
+    t += __shfl_xor(t, 2);
+    if (q == 0) {
+        s -= t;
+        __hip_atomic_store((g_u64*)&z[r], (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);   // write-through
+        const int o = rowmap[r];
+        if (o >= 0) xout[o] = s;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains before the flag
+    __syncthreads();
+    if (tid == 0) {
+        __hip_atomic_store((g_i32*)&ctr[2 + i], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_fetch_add((g_i32*)&ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == T - 1)
+            for (int w = 0; w < T + 2; ++w) __hip_atomic_store((g_i32*)&ctr[w], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// The intrinsics (one workgroup of 64): x_i -> xi (device scalars for chol_back) and sol_i.
+template <int K>
+__global__ __launch_bounds__(64)
+void chol_intr(const double* __restrict__ Dm, const double* __restrict__ ri, const double* __restrict__ contrib,
+               int T, double* __restrict__ xi, double* __restrict__ sol_i, int* __restrict__ fail) {
+    __shared__ double Dp[K * (K + 1)];
+    double v[K];
+    bool bad;
+    intr_solve<K>(Dm, ri, contrib, T, Dp, v, bad);
+    if (threadIdx.x == 0) {
         if (bad) atomicOr(fail, 1);
         for (int i = 0; i < K; ++i) { xi[i] = v[i]; sol_i[i] = v[i]; }
     }
 }
-
 // Back solve in one workgroup of 1024: z = w(r_c) - w(B) x_i, then per level, from the root down,
 // z_i -= sum_k U(i, k) z_k over the ancestors k of panel i (upper tiles (i, k) = L~_ki^T); the
 // camera solution leaves through rowmap (natural order 6c + d).  z lives in LDS (npad <= 16384).

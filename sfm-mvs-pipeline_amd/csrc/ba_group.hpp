@@ -1083,7 +1083,7 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
         scal[SC_STEPN] = s2;
         scal[SC_XN] = s3;
         scal[SC_GMAX] = m;
-        scal[SC_FAIL] = *fail ? 1.0 : 0.0;
+        scal[SC_FAIL] = (double)*fail;   // bit 0: non-positive pivot / invalid step, bit 1: solve wait timed out
         scal[SC_STEPN_F] = ssn;
         scal[SC_XN_F] = sxn;
     }

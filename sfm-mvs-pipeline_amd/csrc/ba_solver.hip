@@ -89,7 +89,9 @@ struct sfmx_ba_ctx {
     bool planned = false;
     sfmx::ba::FactorPlan plan;
     Buf camrow, padrows, rowmap, leaves, ptasks, psrc, lvl_start, lvl_panels, bs_start, bs_k, Wt, contrib, xi,
-        nztiles, packbuf;          // all-reduce of the nonzero lower tiles only (multi-rank)
+        nztiles, packbuf,          // all-reduce of the nonzero lower tiles only (multi-rank)
+        border, zbuf, dagctr;      // chol_backsolve: panels root first, z, [ticket, finished, zdone[T]]
+    bool back_dag = true;          // SFMX_BA_BACK=0: the r02 chol_intr + one-workgroup chol_back
     int n_nztiles = 0;
     size_t sr_count = 0;         // doubles of SR = S_cc | R | D | r_i
     // state (the *2 buffers hold the candidate's linearization until the step is accepted)
@@ -107,7 +109,7 @@ struct sfmx_ba_ctx {
     ~sfmx_ba_ctx() {
         Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
-                      &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &x, &cand, &scale, &colsq, &colsq2, &grad,
+                      &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
                       &failf, &partA};
         int prev = 0;
@@ -236,11 +238,18 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
         hipLaunchKernelGGL(chol_level<RW>, dim3(nt), dim3(256), 0, c->st, S, npad, R, c->ptasks.as<int4>() + t0,
                            c->psrc.as<int>(), pl.ninv[l], c->Wt.as<double>(), c->contrib.as<double>(), fl);
     }
-    hipLaunchKernelGGL(chol_intr<RW - 1>, dim3(1), dim3(64), 0, c->st, Dm, ri, c->contrib.as<double>(), c->T,
-                       c->xi.as<double>(), sol_f + 6 * (size_t)c->C, fl);
-    hipLaunchKernelGGL(chol_back<RW>, dim3(1), dim3(1024), sizeof(double) * npad, c->st, S, npad, R,
-                       c->xi.as<double>(), pl.height, c->lvl_start.as<int>(), c->lvl_panels.as<int>(),
-                       c->bs_start.as<int>(), c->bs_k.as<int>(), c->rowmap.as<int>(), sol_f);
+    if (c->back_dag) {
+        hipLaunchKernelGGL(chol_backsolve<RW>, dim3(c->T), dim3(256), 0, c->st, S, npad, R, Dm, ri,
+                           c->contrib.as<double>(), c->T, c->border.as<int>(), c->bs_start.as<int>(), c->bs_k.as<int>(),
+                           c->rowmap.as<int>(), c->zbuf.as<double>(), sol_f, sol_f + 6 * (size_t)c->C,
+                           c->dagctr.as<int>(), fl);
+    } else {
+        hipLaunchKernelGGL(chol_intr<RW - 1>, dim3(1), dim3(64), 0, c->st, Dm, ri, c->contrib.as<double>(), c->T,
+                           c->xi.as<double>(), sol_f + 6 * (size_t)c->C, fl);
+        hipLaunchKernelGGL(chol_back<RW>, dim3(1), dim3(1024), sizeof(double) * npad, c->st, S, npad, R,
+                           c->xi.as<double>(), pl.height, c->lvl_start.as<int>(), c->lvl_panels.as<int>(),
+                           c->bs_start.as<int>(), c->bs_k.as<int>(), c->rowmap.as<int>(), sol_f);
+    }
     HIPCHK(hipGetLastError());
     return SFMX_OK;
 }
@@ -307,6 +316,7 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     double v[SC_N];
     RC(lin_at<K>(c, c->cand.as<double>(), c->J2.as<double>(), c->colsq2.as<double>(), c->grad2.as<double>(),
                  c->camsum2.as<double>(), true, v));
+    if (v[SC_FAIL] >= 2.0) return fail(SFMX_EINTERNAL, "BA solve: a dependency wait of chol_backsolve timed out");
     const double sn2 = v[SC_STEPN] + v[SC_STEPN_F];
     *mcc = -v[SC_MODEL];
     *step_norm = std::sqrt(sn2);
@@ -384,6 +394,17 @@ int ensure_plan(sfmx_ba_ctx* c) {
     RC(c->Wt.alloc(sizeof(double) * (size_t)pl.T * NB * NB));
     RC(c->contrib.alloc(sizeof(double) * (size_t)pl.T * K * RW));
     RC(c->xi.alloc(sizeof(double) * K));
+    {   // chol_backsolve: panels root first (level descending), so a workgroup only waits on earlier tickets
+        std::vector<int> order;
+        for (int l = pl.height; l >= 0; --l)
+            for (int t = pl.lvl_start[l]; t < pl.lvl_start[l + 1]; ++t) order.push_back(pl.lvl_panels[t]);
+        RC(upload(c->border, order, st));
+        RC(c->zbuf.alloc(sizeof(double) * (size_t)pl.npad));
+        RC(c->dagctr.alloc(sizeof(int) * (size_t)((pl.T + 2 + 3) / 4 * 4)));
+        HIPCHK(hipMemsetAsync(c->dagctr.p, 0, c->dagctr.bytes, st));
+        const char* e = std::getenv("SFMX_BA_BACK");
+        c->back_dag = !(e && e[0] == '0');
+    }
     hipError_t e = hipSuccess;
 #define BACKATTR(RWV) e = hipFuncSetAttribute((const void*)chol_back<RWV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                               (int)(sizeof(double) * pl.npad))
