@@ -30,6 +30,12 @@ namespace sfmx {
 namespace ba {
 
 constexpr int LDT = NB + 2;   // LDS row stride (doubles): 16-B aligned rows
+// global-address-space words for in-launch hand-offs (agent-scope atomics / sc1 accesses)
+typedef __attribute__((address_space(1))) int g_i32;
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+__device__ __forceinline__ double ld_wt(const double* p) {   // sc1 load (bypasses this CU's L1)
+    return __longlong_as_double((long long)__hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
 // 64x64 fp64 tiles on the matrix cores (layout: f64x4 / trow / tcol in ba_kernels.hpp).  Wave w of a
 // 256-thread block owns the row strip 16w..16w+15 and four 16x16 column tiles.
 
@@ -346,6 +352,139 @@ void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const 
     CHOL_STAMP(34);
 }
 
+// chol_level with the sources of a destination tile split over workgroups (SFMX_BA_SPLIT, default
+// on): one workgroup per (task, source) "part".  A task with one source runs as in chol_level.  A
+// task with n > 1 sources: every part computes its product U_k = G A_bk^T (diag: also its y term
+// A_ak w_k and the upper tile G^T) from zero, exactly as chol_level's loop body does, writes U_k
+// (+ y term) write-through (sc1) into its slot of pbuf, drains, and adds to the task's arrival
+// counter; the part whose add returns n - 1 (the last) loads A_ab and subtracts the n products in
+// source order (its own from registers, the others by sc1 loads behind its add: no acquire needed,
+// MI355X_MICROARCH.md inter-workgroup visibility, valid sc1-load form row 1), then inverts or
+// stores as chol_level does.  Same operations in the same order as chol_level: bit-identical.
+// The critical path of a level falls from n source steps + inverse to one source step + the
+// hand-off + inverse.  part = {task (global index), source index, slot, n | inverting << 16};
+// ctr[task] is zero at launch and the last part zeroes it again.
+template <int RW>
+__device__ __forceinline__ void part_store(double* __restrict__ slot, const f64x4 (&u)[4], const double* ys, int nys) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            __hip_atomic_store((g_u64*)&slot[(4 * c + r) * 256 + tid], (unsigned long long)__double_as_longlong(u[c][r]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int u2 = 0; u2 < nys; ++u2)
+        __hip_atomic_store((g_u64*)&slot[(16 + u2) * 256 + tid], (unsigned long long)__double_as_longlong(ys[u2]),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int RW>
+__global__ __launch_bounds__(256)
+void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
+                      const int4* __restrict__ parts, const int* __restrict__ src, double* __restrict__ W,
+                      double* __restrict__ contrib, int* __restrict__ fail, double* pbuf, int* ctr) {
+    __shared__ CholLds<RW> sm;
+    __shared__ int last_sh;
+    constexpr int TPO = (256 / (NB * RW)) > 0 ? 256 / (NB * RW) : 1;
+    constexpr int OPT = (NB * RW) / (256 / TPO);
+    constexpr int SLOT = (16 + OPT) * 256;   // doubles per part slot
+    const int tid = threadIdx.x, w = tid >> 6;
+    const int4 part = parts[blockIdx.x];
+    const int4 task = tasks[part.x];
+    const int a = task.x, b = task.y, a0 = a * NB, b0 = b * NB, n = part.w & 0xffff, j = part.y - task.z;
+    const bool diag = (a == b), inv = (part.w >> 16) != 0;
+    const int k = src[part.y], k0 = k * NB;
+    double* dst = S + (size_t)a0 * npad + b0;
+    f64x4 t[4];
+    if (n == 1) {
+        tile_regs(t, dst, npad);                                                   // A_ab (prefetch)
+        if (diag)
+            for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = R[(size_t)a0 * RW + e];
+    }
+    tile_load(sm.a, S + (size_t)a0 * npad + k0, npad);                         // A_ak
+    tile_load(sm.m, W + (size_t)k * NB * NB, NB);                              // W_k
+    if (!diag) tile_load(sm.n, S + (size_t)b0 * npad + k0, npad);              // A_bk
+    else
+        for (int e = tid; e < NB * RW; e += 256) sm.rk[e] = R[(size_t)k0 * RW + e];   // w_k
+    __syncthreads();
+    f64x4 g[4];
+    mfma_nn(sm.a, sm.m, g);   // G = A_ak W_k
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm.m[16 * w + trow(r)][16 * c + tcol()] = g[c][r];
+    __syncthreads();
+    f64x4 upd[4];
+    mfma_nt(sm.m, diag ? sm.a : sm.n, upd);   // G X^T
+    double ys[OPT];
+    if (diag) {
+        const int pp = tid % TPO;
+#pragma unroll
+        for (int u = 0; u < OPT; ++u) {
+            const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+            double sum = 0.0;
+            for (int c = pp; c < NB; c += TPO) sum = fma(sm.a[i][c], sm.rk[c * RW + q], sum);
+            if (TPO >= 2) sum += __shfl_xor(sum, 1);
+            if (TPO >= 4) sum += __shfl_xor(sum, 2);
+            ys[u] = sum;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) S[(size_t)(k0 + 16 * c + tcol()) * npad + a0 + 16 * w + trow(r)] = g[c][r];
+    }
+    if (n > 1) {   // publish this part; the last arriver finishes the task
+        part_store<RW>(pbuf + (size_t)part.z * SLOT, upd, ys, diag ? OPT : 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+            last_sh = __hip_atomic_fetch_add((g_i32*)&ctr[part.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
+        __syncthreads();
+        if (!last_sh) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the slot loads below
+        if (tid == 0) ctr[part.x] = 0;                              // nobody else touches it in this launch
+        tile_regs(t, dst, npad);
+        if (diag)
+            for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = R[(size_t)a0 * RW + e];
+        __syncthreads();
+        const double* base = pbuf + (size_t)(part.z - j) * SLOT;   // slot of source 0 of this task
+        for (int jj = 0; jj < n; ++jj) {
+            const double* sl = base + (size_t)jj * SLOT;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) t[c][r] -= (jj == j) ? upd[c][r] : ld_wt(&sl[(4 * c + r) * 256 + tid]);
+            if (diag) {
+#pragma unroll
+                for (int u = 0; u < OPT; ++u) {
+                    const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+                    const double y = (jj == j) ? ys[u] : ld_wt(&sl[(16 + u) * 256 + tid]);
+                    if (tid % TPO == 0) sm.ra[i * RW + q] -= y;
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) t[c] -= upd[c];
+        if (diag) {
+#pragma unroll
+            for (int u = 0; u < OPT; ++u) {
+                const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+                if (tid % TPO == 0) sm.ra[i * RW + q] -= ys[u];
+            }
+        }
+    }
+    __syncthreads();
+    if (diag && inv) {
+        chol_diag_tile<RW>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n);
+    } else {
+        tile_store(t, dst, npad);
+        if (diag)
+            for (int e = tid; e < NB * RW; e += 256) R[(size_t)a0 * RW + e] = sm.ra[e];
+    }
+}
+
 // Cross-rank all-reduce of the reduced system, compacted: the structurally nonzero lower tiles of
 // S_cc (incl. the diagonal ones) + R | D | r_i, packed into one contiguous buffer and back.
 // One workgroup per tile; the tail block (blockIdx.x == ntiles) moves the rest.
@@ -430,11 +569,6 @@ __device__ __forceinline__ void intr_solve(const double* __restrict__ Dm, const 
 // last workgroup to finish zeroes it for the next launch (nobody polls by then).
 constexpr int BS_PF = 4;                   // ancestor tiles prefetched into LDS per workgroup
 constexpr long long DAG_TIMEOUT = 2000000; // 20 ms
-typedef __attribute__((address_space(1))) int g_i32;
-typedef __attribute__((address_space(1))) unsigned long long g_u64;
-__device__ __forceinline__ double ld_wt(const double* p) {   // sc1 load (bypasses this CU's L1)
-    return __longlong_as_double((long long)__hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
 
 template <int RW>
 __global__ __launch_bounds__(256)

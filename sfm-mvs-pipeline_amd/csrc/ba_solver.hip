@@ -90,8 +90,11 @@ struct sfmx_ba_ctx {
     sfmx::ba::FactorPlan plan;
     Buf camrow, padrows, rowmap, leaves, ptasks, psrc, lvl_start, lvl_panels, bs_start, bs_k, Wt, contrib, xi,
         nztiles, packbuf,          // all-reduce of the nonzero lower tiles only (multi-rank)
-        border, zbuf, dagctr;      // chol_backsolve: panels root first, z, [ticket, finished, zdone[T]]
+        border, zbuf, dagctr,      // chol_backsolve: panels root first, z, [ticket, finished, zdone[T]]
+        parts, pbuf, lctr;         // chol_level_split: (task, source) parts per level, product slots, arrivals
     bool back_dag = true;          // SFMX_BA_BACK=0: the r02 chol_intr + one-workgroup chol_back
+    bool split = true;             // SFMX_BA_SPLIT=0: chol_level (a task's sources in one workgroup)
+    std::vector<int> part_start;   // per level: parts[part_start[l] .. part_start[l + 1])
     int n_nztiles = 0;
     size_t sr_count = 0;         // doubles of SR = S_cc | R | D | r_i
     // state (the *2 buffers hold the candidate's linearization until the step is accepted)
@@ -109,7 +112,7 @@ struct sfmx_ba_ctx {
     ~sfmx_ba_ctx() {
         Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
-                      &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
+                      &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
                       &failf, &partA};
         int prev = 0;
@@ -235,8 +238,15 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
                        c->leaves.as<int>(), c->Wt.as<double>(), c->contrib.as<double>(), fl);
     for (int l = 0; l < pl.height; ++l) {
         const int t0 = pl.task_start[l], nt = pl.task_start[l + 1] - t0;
-        hipLaunchKernelGGL(chol_level<RW>, dim3(nt), dim3(256), 0, c->st, S, npad, R, c->ptasks.as<int4>() + t0,
-                           c->psrc.as<int>(), pl.ninv[l], c->Wt.as<double>(), c->contrib.as<double>(), fl);
+        if (c->split) {
+            const int p0 = c->part_start[l], np = c->part_start[l + 1] - p0;
+            hipLaunchKernelGGL(chol_level_split<RW>, dim3(np), dim3(256), 0, c->st, S, npad, R, c->ptasks.as<int4>(),
+                               c->parts.as<int4>() + p0, c->psrc.as<int>(), c->Wt.as<double>(), c->contrib.as<double>(),
+                               fl, c->pbuf.as<double>(), c->lctr.as<int>());
+        } else {
+            hipLaunchKernelGGL(chol_level<RW>, dim3(nt), dim3(256), 0, c->st, S, npad, R, c->ptasks.as<int4>() + t0,
+                               c->psrc.as<int>(), pl.ninv[l], c->Wt.as<double>(), c->contrib.as<double>(), fl);
+        }
     }
     if (c->back_dag) {
         hipLaunchKernelGGL(chol_backsolve<RW>, dim3(c->T), dim3(256), 0, c->st, S, npad, R, Dm, ri,
@@ -404,6 +414,29 @@ int ensure_plan(sfmx_ba_ctx* c) {
         HIPCHK(hipMemsetAsync(c->dagctr.p, 0, c->dagctr.bytes, st));
         const char* e = std::getenv("SFMX_BA_BACK");
         c->back_dag = !(e && e[0] == '0');
+    }
+    {   // chol_level_split: per level, the parts of the inverting tasks first (the plan's task order)
+        std::vector<int4> parts;
+        c->part_start.assign(1, 0);
+        int max_slots = 1;
+        for (int l = 0; l < pl.height; ++l) {
+            int slot = 0;
+            for (int t = pl.task_start[l]; t < pl.task_start[l + 1]; ++t) {
+                const int n = pl.tasks[t].s1 - pl.tasks[t].s0, inv = (t - pl.task_start[l]) < pl.ninv[l];
+                if (n == 1) { parts.push_back(make_int4(t, pl.tasks[t].s0, 0, 1 | inv << 16)); continue; }
+                for (int j = 0; j < n; ++j) parts.push_back(make_int4(t, pl.tasks[t].s0 + j, slot + j, n | inv << 16));
+                slot += n;
+            }
+            max_slots = std::max(max_slots, slot);
+            c->part_start.push_back((int)parts.size());
+        }
+        RC(upload(c->parts, parts, st));
+        const int tpo = std::max(1, 256 / (NB * RW)), opt = NB * RW / (256 / tpo);
+        RC(c->pbuf.alloc(sizeof(double) * (size_t)max_slots * (16 + opt) * 256));
+        RC(c->lctr.alloc(sizeof(int) * (size_t)((pl.tasks.size() + 4) / 4 * 4)));
+        HIPCHK(hipMemsetAsync(c->lctr.p, 0, c->lctr.bytes, st));
+        const char* e = std::getenv("SFMX_BA_SPLIT");
+        c->split = !(e && e[0] == '0');
     }
     hipError_t e = hipSuccess;
 #define BACKATTR(RWV) e = hipFuncSetAttribute((const void*)chol_back<RWV>, hipFuncAttributeMaxDynamicSharedMemorySize, \

@@ -129,7 +129,7 @@ def test_mixed_track_lengths_matches_oracle():
 
 
 @pytest.mark.parametrize("order", ["natural", "nd", "nd1", "nd4"])
-def test_backsolve_dag_bit_identical_to_one_workgroup_back_solve(order, monkeypatch):
+def test_split_level_and_backsolve_bit_identical_to_r02_forms(order, monkeypatch):
     """chol_backsolve (one workgroup per panel, ticket-ordered flag hand-offs in one launch) gives
     the same bits as the r02 chol_intr + one-workgroup chol_back, on several elimination trees
     (natural order = a chain of panels; nested dissection with leaves of 1 / 4 tiles); a ring of
@@ -137,10 +137,13 @@ def test_backsolve_dag_bit_identical_to_one_workgroup_back_solve(order, monkeypa
     p = synth.ba_problem(200, 6000, seed=29)
     monkeypatch.setenv("SFMX_BA_ORDER", order)
     res = {}
-    for back in ("0", "1"):
+    for back, split in (("0", "0"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("SFMX_BA_BACK", back)
+        monkeypatch.setenv("SFMX_BA_SPLIT", split)   # chol_level_split: a task's sources over workgroups
         P, sm, tr = gpu_solve(p, max_num_iterations=4)
-        res[back] = (P.points.copy(), P.poses.copy(), sm["final_cost"], tr.copy())
-    a, b = res["0"], res["1"]
-    assert a[2] == b[2]
-    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[3], b[3])
+        res[back + split] = (P.points.copy(), P.poses.copy(), sm["final_cost"], tr.copy())
+    a = res["00"]
+    for key in ("10", "11"):
+        b = res[key]
+        assert a[2] == b[2], key
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[3], b[3]), key
