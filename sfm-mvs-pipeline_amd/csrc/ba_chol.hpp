@@ -123,6 +123,7 @@ __device__ __forceinline__ void inner_inverse16(const double* __restrict__ Pc, i
     for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int w = 0; w < 2; ++w) p[u][w] = Pc[(16 * s + 2 * r + u) * LDP + 2 * c + w];
+#pragma unroll
     for (int j = 0; j < 8; ++j) {
         if (c == j) {   // column panel of the pivot block: rows 2r.., cols 2j..
             *reinterpret_cast<double2*>(&ipan[(2 * r) * 2]) = make_double2(p[0][0], p[0][1]);
@@ -136,30 +137,37 @@ __device__ __forceinline__ void inner_inverse16(const double* __restrict__ Pc, i
         const double2 l0 = *reinterpret_cast<const double2*>(&ipan[(2 * c) * 2]);
         const double2 l1 = *reinterpret_cast<const double2*>(&ipan[(2 * c + 1) * 2]);
         __builtin_amdgcn_wave_barrier();
-        // q = -[a b; b d]^-1
+        // q = -[a b; b d]^-1 = -adj / det.  The row panel's m = -A_iB q = (A_iB adj) / det: the
+        // adjugate products run beside the reciprocal, so only one multiply follows it.
         const double a = b0.x, bb = b0.y, d = b1.y;
         double det = fma(a, d, -bb * bb);
-        if (!(a > 0.0) || !isfinite(a) || !(det > 0.0) || !isfinite(det)) { bad = true; det = 1.0; }
+        const bool badj = !(a > 0.0) || !isfinite(a) || !(det > 0.0) || !isfinite(det);   // branch-free
+        bad |= badj;
+        det = badj ? 1.0 : det;
+        const double ai[2][2] = {{i0.x, i0.y}, {i1.x, i1.y}};
+        double pre[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            pre[u][0] = fma(ai[u][0], d, -ai[u][1] * bb);
+            pre[u][1] = fma(ai[u][1], a, -ai[u][0] * bb);
+        }
         const double rd = rcp_nr(det);
         const double q00 = -d * rd, q01 = bb * rd, q11 = -a * rd;   // q10 = q01
         const bool rowB = (r == j), colB = (c == j);
         double m[2][2];
-        {
-            const double ai[2][2] = {{i0.x, i0.y}, {i1.x, i1.y}};
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const double v0 = -(ai[u][0] * q00 + ai[u][1] * q01), v1 = -(ai[u][0] * q01 + ai[u][1] * q11);
-                m[u][0] = rowB ? (u == 0 ? q00 : q01) : v0;
-                m[u][1] = rowB ? (u == 0 ? q01 : q11) : v1;
-            }
+        for (int u = 0; u < 2; ++u) {
+            m[u][0] = rowB ? (u == 0 ? q00 : q01) : pre[u][0] * rd;
+            m[u][1] = rowB ? (u == 0 ? q01 : q11) : pre[u][1] * rd;
         }
         const double al[2][2] = {{l0.x, l0.y}, {l1.x, l1.y}};   // al[w][b] = A_(2c+w),(2j+b) = A_Bl[b][w]
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int w = 0; w < 2; ++w) {
-                if (colB) p[u][w] = m[u][w];
-                else p[u][w] = (rowB ? 0.0 : p[u][w]) - (m[u][0] * al[w][0] + m[u][1] * al[w][1]);
+                const double base = rowB ? 0.0 : p[u][w];
+                const double upd = fma(-m[u][1], al[w][1], fma(-m[u][0], al[w][0], base));
+                p[u][w] = colB ? m[u][w] : upd;
             }
     }
 #pragma unroll
@@ -233,26 +241,51 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __r
         }
     __syncthreads();
     CHOL_STAMP(20);
-    {   // w = W y: NB x RW outputs, TPO threads per output (fixed-order shuffle combine)
-        constexpr int TPO = (256 / (NB * RW)) > 0 ? 256 / (NB * RW) : 1;
-        constexpr int OPT = (NB * RW) / (256 / TPO);
-        const int part = tid % TPO;
+    {   // w = W y: 4 threads per row i, each over 16 columns c for all RW right-hand sides (16-B LDS
+        // reads), the 4 partial sums combined by two shuffles in a fixed order
+        static_assert(RW % 2 == 0, "RW is k + 1 with k odd");
+        const int i = tid >> 2, cp = tid & 3;
+        double acc[RW];
 #pragma unroll
-        for (int u = 0; u < OPT; ++u) {
-            const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
-            double sum = 0.0;
-            for (int c = part; c < NB; c += TPO) sum = fma(buf[i][c], y[c * RW + q], sum);
-            if (TPO >= 2) sum += __shfl_xor(sum, 1);
-            if (TPO >= 4) sum += __shfl_xor(sum, 2);
-            if (part == 0) { wv[i * RW + q] = sum; R[(size_t)(k0 + i) * RW + q] = sum; }
+        for (int q = 0; q < RW; ++q) acc[q] = 0.0;
+#pragma unroll
+        for (int cc = 0; cc < 16; cc += 2) {
+            const int c = cp * 16 + cc;
+            const double2 wi = *reinterpret_cast<const double2*>(&buf[i][c]);
+#pragma unroll
+            for (int q = 0; q < RW; q += 2) {
+                const double2 y0 = *reinterpret_cast<const double2*>(&y[c * RW + q]);
+                const double2 y1 = *reinterpret_cast<const double2*>(&y[(c + 1) * RW + q]);
+                acc[q] = fma(wi.x, y0.x, acc[q]);
+                acc[q + 1] = fma(wi.x, y0.y, acc[q + 1]);
+                acc[q] = fma(wi.y, y1.x, acc[q]);
+                acc[q + 1] = fma(wi.y, y1.y, acc[q + 1]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < RW; ++q) {
+            acc[q] += __shfl_xor(acc[q], 1);
+            acc[q] += __shfl_xor(acc[q], 2);
+        }
+        if (cp == 0) {
+#pragma unroll
+            for (int q = 0; q < RW; ++q) { wv[i * RW + q] = acc[q]; R[(size_t)(k0 + i) * RW + q] = acc[q]; }
         }
     }
+    CHOL_STAMP(22);
     __syncthreads();
-    if (tid < (RW - 1) * RW) {   // contrib_k[i][j] = sum_r y[r][i] w[r][j]
-        const int i = tid / RW, j = tid % RW;
-        double s = 0.0;
-        for (int r = 0; r < NB; ++r) s = fma(y[r * RW + i], wv[r * RW + j], s);
-        contrib[(size_t)k * (RW - 1) * RW + tid] = s;
+    CHOL_STAMP(23);
+    // contrib_k[i][j] = sum_r y[r][i] w[r][j]: 16 lanes per output, 4 rows each, then 4 shuffles
+    for (int o = tid >> 4; o < (RW - 1) * RW; o += 16) {
+        const int i = o / RW, j = o % RW, rp = tid & 15;
+        double sacc = 0.0;
+#pragma unroll
+        for (int h = 0; h < NB / 16; ++h) sacc = fma(y[(rp + 16 * h) * RW + i], wv[(rp + 16 * h) * RW + j], sacc);
+        sacc += __shfl_xor(sacc, 1);
+        sacc += __shfl_xor(sacc, 2);
+        sacc += __shfl_xor(sacc, 4);
+        sacc += __shfl_xor(sacc, 8);
+        if (rp == 0) contrib[(size_t)k * (RW - 1) * RW + o] = sacc;
     }
     CHOL_STAMP(21);
 }

@@ -51,7 +51,8 @@ int main() {
         for (int s = 0; s < 4; ++s)
             printf(" | s%d panel->inner %lld inner %lld M %lld upd %lld", s, st[2 + 4 * s] - (s ? st[1 + 4 * s] : st[1]),
                    st[3 + 4 * s] - st[2 + 4 * s], st[4 + 4 * s] - st[3 + 4 * s], st[5 + 4 * s] - st[4 + 4 * s]);
-        printf(" | store %lld rhs %lld  (ticks of 100 MHz wall clock)\n", st[20] - st[17], st[21] - st[20]);
+        printf(" | store %lld rhs %lld (w %lld sync %lld contrib %lld)  (ticks of 100 MHz wall clock)\n", st[20] - st[17], st[21] - st[20],
+               st[22] - st[20], st[23] - st[22], st[21] - st[23]);
         hipEventRecord(e0);
         chol_level<RW><<<(unsigned)tasks.size(), 256>>>(S, npad, R, dt, src, 1, W, contrib, fail);
         hipEventRecord(e1);
