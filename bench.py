@@ -99,6 +99,12 @@ def main():
             dist.init_process_group(backend="gloo")
         else:
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    elif os.environ.get("SFMX_BENCH_BA_AR1") == "1":
+        # tuning only: the BA leg's multi-rank path (all-reduce callbacks through torch / RCCL) on a
+        # world of one, to price the host side of that path on a one-GPU box
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        dist.init_process_group(backend="nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
 
     import sfmx
     from sfmx import synth, shard
@@ -483,8 +489,9 @@ def bench_ba(args, rank, world, local):
     local_prob = shard_ba_problem(prob, rank, world) if world > 1 else dict(prob, point_range=(0, args.ba_points))
     local_prob.pop("point_range")
     opts = ba.default_options(device=local)
+    use_ar = world > 1 or os.environ.get("SFMX_BENCH_BA_AR1") == "1"
     ctx = ba.BAContext(ba.BAProblem(**local_prob), opts, allreduce=torch_allreduce(cpu_staging=os.environ.get("SFMX_BENCH_REHEARSE") == "1")
-                         if world > 1 else None)
+                         if use_ar else None)
     ctx.run(max_iterations=1)                 # warm-up (code objects, allocations)
     ctx.reset()
     if world > 1:

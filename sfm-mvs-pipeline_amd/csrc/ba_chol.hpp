@@ -301,6 +301,7 @@ template <int RW>
 __global__ __launch_bounds__(256)
 void chol_leaves(double* __restrict__ S, int npad, double* __restrict__ R, const int* __restrict__ leaves,
                  double* __restrict__ W, double* __restrict__ contrib, int* __restrict__ fail) {
+    if (step_gated(fail + 1)) return;
     __shared__ CholLds<RW> sm;
     const int k = leaves[blockIdx.x], k0 = k * NB;
     f64x4 t[4];
@@ -319,6 +320,7 @@ __global__ __launch_bounds__(256)
 void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
                 const int* __restrict__ src, int ninv, double* __restrict__ W, double* __restrict__ contrib,
                 int* __restrict__ fail) {
+    if (step_gated(fail + 1)) return;
     __shared__ CholLds<RW> sm;
     const int tid = threadIdx.x, w = tid >> 6;
     const int4 task = tasks[blockIdx.x];
@@ -416,6 +418,7 @@ __global__ __launch_bounds__(256)
 void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
                       const int4* __restrict__ parts, const int* __restrict__ src, double* __restrict__ W,
                       double* __restrict__ contrib, int* __restrict__ fail, double* pbuf, int* ctr) {
+    if (step_gated(fail + 1)) return;
     __shared__ CholLds<RW> sm;
     __shared__ int last_sh;
     constexpr int TPO = (256 / (NB * RW)) > 0 ? 256 / (NB * RW) : 1;
@@ -523,7 +526,8 @@ void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, 
 // One workgroup per tile; the tail block (blockIdx.x == ntiles) moves the rest.
 __global__ __launch_bounds__(256)
 void chol_pack(const double* __restrict__ S, int npad, const int2* __restrict__ tiles, int ntiles, int tail,
-               double* __restrict__ buf, int unpack_dir) {
+               double* __restrict__ buf, int unpack_dir, const int* __restrict__ gate) {
+    if (step_gated(gate)) return;
     if ((int)blockIdx.x < ntiles) {
         const int2 t = tiles[blockIdx.x];
         double* sp = const_cast<double*>(S) + (size_t)t.x * NB * npad + (size_t)t.y * NB;
@@ -610,6 +614,7 @@ void chol_backsolve(const double* __restrict__ S, int npad, const double* __rest
                     int T, const int* __restrict__ border, const int* __restrict__ bs_start,
                     const int* __restrict__ bs_k, const int* __restrict__ rowmap, double* z,
                     double* __restrict__ xout, double* __restrict__ sol_i, int* ctr, int* __restrict__ fail) {
+    if (step_gated(fail + 1)) return;
     constexpr int K = RW - 1;
     __shared__ double Ut[BS_PF][NB / 4][256];   // thread-private: its 16 U values per prefetched tile
     __shared__ double Dp[K * RW], xs[K];
@@ -690,6 +695,7 @@ template <int K>
 __global__ __launch_bounds__(64)
 void chol_intr(const double* __restrict__ Dm, const double* __restrict__ ri, const double* __restrict__ contrib,
                int T, double* __restrict__ xi, double* __restrict__ sol_i, int* __restrict__ fail) {
+    if (step_gated(fail + 1)) return;
     __shared__ double Dp[K * (K + 1)];
     double v[K];
     bool bad;
@@ -707,7 +713,8 @@ __global__ __launch_bounds__(1024)
 void chol_back(const double* __restrict__ S, int npad, const double* __restrict__ R, const double* __restrict__ xi,
                int height, const int* __restrict__ lvl_start, const int* __restrict__ lvl_panels,
                const int* __restrict__ bs_start, const int* __restrict__ bs_k, const int* __restrict__ rowmap,
-               double* __restrict__ xout) {
+               double* __restrict__ xout, const int* __restrict__ gate) {
+    if (step_gated(gate)) return;
     extern __shared__ double z[];
     const int tid = threadIdx.x;
     double xv[RW - 1];

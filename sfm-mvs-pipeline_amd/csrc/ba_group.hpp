@@ -60,7 +60,6 @@ __host__ __device__ constexpr int cp_gi(int K) { return 27 + 6 * K + K * (K + 1)
 // per-group scalar partials
 enum { GP_COST = 0, GP_MODEL = 1, GP_STEPN = 2, GP_XN = 3, GP_GMAX = 4, GP_N = 8 };
 // LM scalars (scal[]): [0..3] rank-local sums, [4..5] maxima, [6..7] replicated camera parts
-enum { SC_COST = 0, SC_MODEL = 1, SC_STEPN = 2, SC_XN = 3, SC_GMAX = 4, SC_FAIL = 5, SC_STEPN_F = 6, SC_XN_F = 7, SC_N = 8 };
 
 struct Grp {
     int o0, o1, p0, p1;      // observation / point range (internal order)
@@ -228,7 +227,9 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
                const int* __restrict__ pt_start, const double* __restrict__ J, const double* __restrict__ scale,
                const double* __restrict__ colsq, double dmin, double dmax, double radius, int P, int C,
                double* __restrict__ plt, double* __restrict__ sg, double* __restrict__ rg, double* __restrict__ hbig,
-               int* __restrict__ fail) {
+               int* __restrict__ fail, const double* __restrict__ lm) {
+    if (step_gated(fail + 1)) return;
+    if (lm) radius = lm[LM_RADIUS];
     extern __shared__ __attribute__((aligned(16))) double gl[];
     constexpr int NPF = gs_npf(K), PD = gs_pd(K);
     const Grp G = grp[blockIdx.x];
@@ -614,7 +615,8 @@ __global__ __launch_bounds__(64)
 void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents, const double* __restrict__ sg,
                  const double* __restrict__ hbig, const double* __restrict__ rg, int K, const int* __restrict__ camrow,
                  int npad, double* __restrict__ S, double* __restrict__ R, double* __restrict__ Dm,
-                 double* __restrict__ ri) {
+                 double* __restrict__ ri, const int* __restrict__ gate) {
+    if (step_gated(gate)) return;
     const ATask T = tasks[blockIdx.x];
     const int t = threadIdx.x, RW = K + 1;
     if (T.type == 0) {
@@ -669,7 +671,9 @@ void ba_add_cam(int P, int C, int npad, const int* __restrict__ camrow, const in
                 int npadrows, const double* __restrict__ camsum,
                 const double* __restrict__ scale, const double* __restrict__ colsq, double dmin, double dmax,
                 double radius, double* __restrict__ S, double* __restrict__ R, double* __restrict__ Dm,
-                double* __restrict__ ri) {
+                double* __restrict__ ri, const int* __restrict__ gate, const double* __restrict__ lm) {
+    if (step_gated(gate)) return;
+    if (lm) radius = lm[LM_RADIUS];
     constexpr int NCP = ncp(K), RW = K + 1;
     const size_t ne = 3 * (size_t)P, nfc = 6 * (size_t)C;
     const double* si = scale + ne + nfc;
@@ -748,7 +752,8 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
              const int* __restrict__ obs_cam, const double* __restrict__ obs_xy, const int* __restrict__ pt_start,
              double cx, double cy, int P, int C, const double* __restrict__ xp, const double* __restrict__ jscale,
              double* __restrict__ J, double* __restrict__ colsq, double* __restrict__ grad,
-             double* __restrict__ gpart, double* __restrict__ gpl) {
+             double* __restrict__ gpart, double* __restrict__ gpl, const int* __restrict__ gate) {
+    if (step_gated(gate)) return;
     extern __shared__ __attribute__((aligned(16))) double gl[];
     constexpr int JS = jst(K), NCP = ncp(K), N = 9 + K, NF = nfeat(K);
     __shared__ double sh[8];
@@ -982,7 +987,8 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
 template <int K>
 __global__ __launch_bounds__(128)
 void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int* __restrict__ cref,
-               const double* __restrict__ gpart, double* __restrict__ camsum) {
+               const double* __restrict__ gpart, double* __restrict__ camsum, const int* __restrict__ gate) {
+    if (step_gated(gate)) return;
     constexpr int NCP = ncp(K);
     const int t = threadIdx.x;
     if ((int)blockIdx.x < C) {
@@ -1026,10 +1032,14 @@ __global__ __launch_bounds__(256)
 void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, const double* __restrict__ gpl,
                  const double* __restrict__ xf_new, const double* __restrict__ xf_old, int cand_mode,
                  const int* __restrict__ fail, double* __restrict__ colsq, double* __restrict__ grad,
-                 double* __restrict__ scal) {
+                 double* __restrict__ scal, double* __restrict__ camsum_out, int ncs) {
+    if (step_gated(fail + 1)) return;
     constexpr int NCP = ncp(K);
     __shared__ double sh[8];
     const int t = threadIdx.x;
+    // the camera sums were all-reduced in a scratch buffer (a skipped speculative step reduces only
+    // scratch): the linearization's own copy is written here, behind the gate
+    for (int i = t; i < ncs; i += blockDim.x) camsum_out[i] = camsum[i];
     const size_t ne = 3 * (size_t)P;
     const int nf = 6 * C + K;
     double gmax = 0.0, xn = 0.0, sn = 0.0;
@@ -1101,7 +1111,9 @@ __global__ __launch_bounds__(256)
 void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const int* __restrict__ obs_point,
                 const int* __restrict__ obs_cam, const int* __restrict__ pt_start, const double* __restrict__ J,
                 const double* __restrict__ scale, const double* __restrict__ plt, const double* __restrict__ sol_f,
-                int P, int C, const double* __restrict__ x, double* __restrict__ cand, double* __restrict__ gpl) {
+                int P, int C, const double* __restrict__ x, double* __restrict__ cand, double* __restrict__ gpl,
+                const int* __restrict__ gate) {
+    if (step_gated(gate)) return;
     __shared__ double yv[GCH * 3];
     __shared__ double pst[GPTS * 3];
     __shared__ double sh[8];
@@ -1224,7 +1236,8 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
 
 // candidate cameras / intrinsics: cand_f = x_f + (-sol_f) * scale_f (one or more workgroups)
 __global__ void ba_fstep(int nf, const double* __restrict__ sol_f, const double* __restrict__ scale_f,
-                         const double* __restrict__ x_f, double* __restrict__ cand_f) {
+                         const double* __restrict__ x_f, double* __restrict__ cand_f, const int* __restrict__ gate) {
+    if (step_gated(gate)) return;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nf) cand_f[i] = x_f[i] + (-sol_f[i]) * scale_f[i];
 }

@@ -19,6 +19,8 @@
 namespace sfmx {
 namespace ba {
 
+// LM scalars of one step (ba_finalize -> host / ba_decide)
+enum { SC_COST = 0, SC_MODEL = 1, SC_STEPN = 2, SC_XN = 3, SC_GMAX = 4, SC_FAIL = 5, SC_STEPN_F = 6, SC_XN_F = 7, SC_N = 8 };
 constexpr int NB = 64;   // tile of the reduced camera system (ba_chol.hpp, ba_plan.hpp PLAN_NB)
 __host__ __device__ constexpr int jst(int K) { return 20 + 2 * K; }   // Jacobian record stride
 
@@ -202,20 +204,110 @@ void ba_sum(const double* __restrict__ partial, int n, double scale, double* __r
     if (threadIdx.x == 0) out[0] = scale * s;
 }
 
+// The step gate (speculative LM, ba_solver.hip): every kernel of an LM step returns at once when
+// the gate word is 0.  ba_decide sets it to 1 only when the step it judged was accepted and the
+// minimisation continues, so the next step, enqueued by the host before it knows the outcome (with
+// the accepted step's buffers), runs exactly then; after a rejection the host re-opens the gate and
+// enqueues the step again on the unchanged buffers.  Outside the speculative mode it stays 1.
+__device__ __forceinline__ bool step_gated(const int* __restrict__ gate) { return gate && *gate == 0; }
+
+// LM controller state on the device (speculative mode), doubles so it publishes with the scalars.
+enum { LM_COST = 0, LM_GMAX, LM_XNORM, LM_RADIUS, LM_DECREASE, LM_ITER, LM_SUCC, LM_UNSUCC, LM_INVALID, LM_CONSEC,
+       LM_SUCCESSFUL, LM_TERM, LM_ACCEPTED, LM_TRACE, LM_ERROR, LM_N = 16 };
+constexpr double LM_RUNNING = -1.0;
+struct LmOpt {
+    double ptol, ftol, minrel, maxr, gtol, minr;
+    int maxit, maxinv, term_conv, term_noconv, term_fail;
+};
+// (2 rho - 1)^3 of the radius update (Ceres: std::pow(2 rho - 1, 3)): the cube with the errors of both
+// products carried (fma) and one final rounding, so the host and the device get the same bits.
+__host__ __device__ inline double lm_cube(double y) {
+#pragma clang fp contract(off)   // host and device must not fuse t + ... into an fma differently
+    const double p = y * y, pe = fma(y, y, -p);
+    const double t = p * y, te = fma(p, y, -t);
+    return t + fma(pe, y, te);
+}
+
 // The LM scalars into pinned, host-coherent memory, then the sequence number with system-scope
 // release: the host polls the sequence number instead of a D2H copy + stream synchronisation
 // (the interrupt-driven wake-up of hipStreamSynchronize costs ~50 us per LM step).
 // It also clears the step's failure flag (already folded into the scalars by ba_finalize), so the
 // next step starts without a separate memset.
+__device__ __forceinline__ void publish_body(const double* __restrict__ src, int n, const double* __restrict__ src2,
+                                             int n2, double* __restrict__ dst, unsigned* __restrict__ seq, unsigned v,
+                                             int* __restrict__ fail) {
+    for (int i = 0; i < n; ++i) dst[i] = src[i];
+    for (int i = 0; i < n2; ++i) dst[n + i] = src2[i];
+    *fail = 0;
+    __threadfence_system();
+    __hip_atomic_store(seq, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __global__ void ba_publish(const double* __restrict__ src, int n, double* __restrict__ dst, unsigned* __restrict__ seq,
                            unsigned v, int* __restrict__ fail) {
-    if (threadIdx.x == 0) {
-        for (int i = 0; i < n; ++i) dst[i] = src[i];
-        *fail = 0;
-        __threadfence_system();
-        __hip_atomic_store(seq, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (threadIdx.x == 0) publish_body(src, n, nullptr, 0, dst, seq, v, fail);
 }
+
+// Speculative mode, the step's last kernel: Ceres 1.14 TrustRegionMinimizer +
+// LevenbergMarquardtStrategy after one step (the host loop of run_lm_k, line for line): accept /
+// reject / invalid, the radius update, then the next iteration's
+// FinalizeIterationAndCheckIfMinimizerCanContinue; then the scalars + this state are published as
+// ba_publish does and the gate for the next step is set.  scal holds the step's (all-reduced) scalars.
+__global__ void ba_decide(const double* __restrict__ scal, double* __restrict__ lm, int* __restrict__ fail, LmOpt o,
+                          double* __restrict__ dst, unsigned* __restrict__ seq, unsigned v) {
+#pragma clang fp contract(off)   // the host loop's arithmetic, bit for bit
+    if (threadIdx.x != 0 || step_gated(fail + 1)) return;
+    double cost = lm[LM_COST], gmax = lm[LM_GMAX], xn = lm[LM_XNORM], radius = lm[LM_RADIUS], dec = lm[LM_DECREASE];
+    int consec = (int)lm[LM_CONSEC];
+    bool successful = lm[LM_SUCCESSFUL] != 0.0, accepted = false, trace = false;
+    double term = LM_RUNNING;
+    const double sn2 = scal[SC_STEPN] + scal[SC_STEPN_F], mcc = -scal[SC_MODEL], sn = sqrt(sn2);
+    const bool valid = scal[SC_FAIL] == 0.0 && isfinite(sn2) && isfinite(scal[SC_MODEL]) && mcc > 0.0;
+    if (scal[SC_FAIL] >= 2.0) {   // internal error (a dependency wait timed out)
+        lm[LM_ERROR] = 1.0;
+        term = o.term_fail;
+    } else if (!valid) {          // HandleInvalidStep
+        lm[LM_INVALID] += 1.0;
+        if (++consec >= o.maxinv) term = o.term_fail;
+        else { radius /= dec; dec *= 2.0; successful = false; }
+    } else {
+        consec = 0;
+        const double ccost = isfinite(scal[SC_COST]) ? scal[SC_COST] : DBL_MAX;
+        if (sn <= o.ptol * (xn + o.ptol)) term = o.term_conv;
+        else if (fabs(cost - ccost) <= o.ftol * cost) term = o.term_conv;
+        else {
+            const double rel = (cost - ccost) / mcc;
+            if (rel > o.minrel) {     // HandleSuccessfulStep
+                accepted = true;
+                cost = ccost;
+                gmax = scal[SC_GMAX];
+                xn = sqrt(scal[SC_XN] + scal[SC_XN_F]);
+                radius = radius / fmax(1.0 / 3.0, 1.0 - lm_cube(2.0 * rel - 1.0));
+                radius = fmin(o.maxr, radius);
+                dec = 2.0;
+                successful = true;
+            } else {                  // HandleUnsuccessfulStep
+                radius /= dec; dec *= 2.0;
+                successful = false;
+            }
+        }
+    }
+    if (term == LM_RUNNING) {         // the next iteration's FinalizeIteration...
+        lm[successful ? LM_SUCC : LM_UNSUCC] += 1.0;
+        trace = true;
+        if (lm[LM_ITER] >= o.maxit) term = o.term_noconv;
+        else if (successful && gmax <= o.gtol) term = o.term_conv;
+        else if (radius <= o.minr) term = o.term_conv;
+        else lm[LM_ITER] += 1.0;
+    }
+    lm[LM_COST] = cost; lm[LM_GMAX] = gmax; lm[LM_XNORM] = xn; lm[LM_RADIUS] = radius; lm[LM_DECREASE] = dec;
+    lm[LM_CONSEC] = consec; lm[LM_SUCCESSFUL] = successful ? 1.0 : 0.0; lm[LM_TERM] = term;
+    lm[LM_ACCEPTED] = accepted ? 1.0 : 0.0; lm[LM_TRACE] = trace ? 1.0 : 0.0;
+    fail[1] = (term == LM_RUNNING && accepted) ? 1 : 0;
+    publish_body(scal, SC_N, lm, LM_N, dst, seq, v, fail);
+}
+
+// Re-opens the step gate (after a rejected step, before the host enqueues the step again).
+__global__ void ba_open_gate(int* __restrict__ fail) { if (threadIdx.x == 0) fail[1] = 1; }
 
 // scale = 1 / (1 + sqrt(colsq)) (iteration 0 only, Ceres jacobi_scaling)
 __global__ void ba_scale(int n, const double* __restrict__ colsq, double* __restrict__ scale) {

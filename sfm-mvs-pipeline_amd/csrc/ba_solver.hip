@@ -100,6 +100,7 @@ struct sfmx_ba_ctx {
     // state (the *2 buffers hold the candidate's linearization until the step is accepted)
     Buf x, cand, scale, colsq, colsq2, grad, grad2, J, J2, camsum, camsum2, plt, sg, rg, hbig, gpart, gpl, scal,
         SR, sol, failf, partA;
+    static constexpr int HS_SLOT = SC_N + LM_N, HS_SEQ = 2 * HS_SLOT, HS_N = HS_SEQ + 3;
     bool scaled = false, j_scaled = false;   // j_scaled: the records in J are J_s (ba_gschur SCALEJ)
     // locality order: internal point p' is caller point pperm[p']; internal
     // observation o' is caller observation operm[o'] (point-major)
@@ -107,14 +108,20 @@ struct sfmx_ba_ctx {
     double phase_ms[4] = {0, 0, 0, 0};
     bool phases = false;         // per-phase events (sfmx_ba_set_phase_timing): ~6 us of GPU time each
     hipEvent_t ev[6] = {};
-    double* hs = nullptr;        // pinned host-coherent LM scalars [SC_N] + sequence word (ba_publish)
+    double* hs = nullptr;        // pinned host-coherent: 2 slots of [scalars SC_N | LM state LM_N], their
+                                 // sequence words (HS_SEQ + slot) and ba_publish's sequence word (HS_SEQ + 2)
+    Buf lmst;                    // device LM state (speculative mode, ba_decide)
+    Buf camscr;                  // camera sums of a linearization before the all-reduce (scratch)
+    bool spec = false;           // SFMX_BA_SPEC=1: device-judged steps, step s + 1 enqueued before s is judged
+    int spec_maxit = 0;
+    double lm_init[LM_N] = {};   // host source of the initial device LM state (outlives its async copy)
     unsigned seq = 0;
     ~sfmx_ba_ctx() {
         Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
                       &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
-                      &failf, &partA};
+                      &failf, &partA, &lmst, &camscr};
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
@@ -148,6 +155,7 @@ int upload(Buf& b, const std::vector<T>& v, hipStream_t st) {
 }
 
 double* scal(sfmx_ba_ctx* c, int i) { return c->scal.as<double>() + i; }
+int* gate(sfmx_ba_ctx* c) { return c->failf.as<int>() + 1; }   // the step gate word (ba_kernels.hpp step_gated)
 
 int fetch_scalars(sfmx_ba_ctx* c, int i0, int cnt, double* out) {
     HIPCHK(hipMemcpyAsync(out, scal(c, i0), sizeof(double) * cnt, hipMemcpyDeviceToHost, c->st));
@@ -161,7 +169,7 @@ int fetch_scalars(sfmx_ba_ctx* c, int i0, int cnt, double* out) {
 int poll_scalars(sfmx_ba_ctx* c, double* out, hipEvent_t mark) {
     const unsigned want = ++c->seq;
     if (mark) HIPCHK(hipEventRecord(mark, c->st));
-    unsigned* hseq = reinterpret_cast<unsigned*>(c->hs + SC_N);
+    unsigned* hseq = reinterpret_cast<unsigned*>(c->hs + sfmx_ba_ctx::HS_SEQ + 2);
     hipLaunchKernelGGL(ba_publish, dim3(1), dim3(64), 0, c->st, scal(c, 0), (int)SC_N, c->hs, hseq, want,
                        c->failf.as<int>());
     HIPCHK(hipGetLastError());
@@ -176,6 +184,23 @@ int poll_scalars(sfmx_ba_ctx* c, double* out, hipEvent_t mark) {
         __builtin_ia32_pause();
     }
     std::memcpy(out, c->hs, sizeof(double) * SC_N);
+    return SFMX_OK;
+}
+
+// Speculative mode: wait for ba_decide's publication with sequence number q (slot q & 1) -> out[HS_SLOT].
+int wait_slot(sfmx_ba_ctx* c, unsigned q, double* out) {
+    unsigned* hseq = reinterpret_cast<unsigned*>(c->hs + sfmx_ba_ctx::HS_SEQ + (q & 1));
+    for (unsigned spins = 1;; ++spins) {
+        if (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == q) break;
+        if ((spins & 255) == 0) {
+            const hipError_t e = hipStreamQuery(c->st);
+            if (e != hipSuccess && e != hipErrorNotReady) return fail(SFMX_EDEVICE, std::string("LM step: ") + hipGetErrorString(e));
+            if (e == hipSuccess && __atomic_load_n(hseq, __ATOMIC_ACQUIRE) != q)
+                return fail(SFMX_EINTERNAL, "LM step: stream drained without the step's publication");
+        }
+        __builtin_ia32_pause();
+    }
+    std::memcpy(out, c->hs + (q & 1) * sfmx_ba_ctx::HS_SLOT, sizeof(double) * sfmx_ba_ctx::HS_SLOT);
     return SFMX_OK;
 }
 
@@ -207,17 +232,22 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double
                            c->obs_point.as<int>(), c->obs_cam.as<int>(),
                            c->obs_xy.as<double>(), c->pt_start.as<int>(), c->cx, c->cy, c->P, c->C, xp,
                            c->scaled ? c->scale.as<double>() : nullptr, Jo, colsq_o, grad_o, c->gpart.as<double>(),
-                           c->gpl.as<double>());
+                           c->gpl.as<double>(), gate(c));
+    // multi-rank speculative steps all-reduce a scratch copy of the camera sums: a skipped step's
+    // all-reduce then touches no state (ba_finalize copies them behind the step gate)
+    const int ncs = c->C * ncp(K) + K * (K + 1) / 2 + K;
+    double* cs_red = (c->ar && c->spec) ? c->camscr.as<double>() : camsum_o;
     hipLaunchKernelGGL(ba_camred<K>, dim3(c->C + K * (K + 1) / 2 + K), dim3(128), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
-                       c->cref.as<int>(), c->gpart.as<double>(), camsum_o);
+                       c->cref.as<int>(), c->gpart.as<double>(), cs_red, gate(c));
     HIPCHK(hipGetLastError());
-    RC(allreduce(c, camsum_o, (int64_t)c->C * ncp(K) + K * (K + 1) / 2 + K, SFMX_REDUCE_SUM));
-    hipLaunchKernelGGL(ba_finalize<K>, dim3(1), dim3(256), 0, c->st, c->ngroups, c->P, c->C, camsum_o,
+    RC(allreduce(c, cs_red, ncs, SFMX_REDUCE_SUM));
+    hipLaunchKernelGGL(ba_finalize<K>, dim3(1), dim3(256), 0, c->st, c->ngroups, c->P, c->C, cs_red,
                        c->gpl.as<double>(), xp + c->ne, c->x.as<double>() + c->ne, cand_mode ? 1 : 0, c->failf.as<int>(),
-                       colsq_o, grad_o, scal(c, 0));
+                       colsq_o, grad_o, scal(c, 0), camsum_o, cs_red == camsum_o ? 0 : ncs);
     HIPCHK(hipGetLastError());
     RC(allreduce(c, scal(c, SC_COST), 4, SFMX_REDUCE_SUM));
     RC(allreduce(c, scal(c, SC_GMAX), 2, SFMX_REDUCE_MAX));
+    if (!out) return SFMX_OK;   // speculative step: ba_decide judges and publishes
     RC(poll_scalars(c, out, c->phases && cand_mode ? c->ev[3] : nullptr));
     return SFMX_OK;
 }
@@ -258,7 +288,7 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
                            c->xi.as<double>(), sol_f + 6 * (size_t)c->C, fl);
         hipLaunchKernelGGL(chol_back<RW>, dim3(1), dim3(1024), sizeof(double) * npad, c->st, S, npad, R,
                            c->xi.as<double>(), pl.height, c->lvl_start.as<int>(), c->lvl_panels.as<int>(),
-                           c->bs_start.as<int>(), c->bs_k.as<int>(), c->rowmap.as<int>(), sol_f);
+                           c->bs_start.as<int>(), c->bs_k.as<int>(), c->rowmap.as<int>(), sol_f, gate(c));
     }
     HIPCHK(hipGetLastError());
     return SFMX_OK;
@@ -266,10 +296,13 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
 
 // One LM step at `radius`: Schur solve of (J_s^T J_s + D^2) sol = J_s^T r, step_s = -sol,
 // candidate = x + step_s * scale, its cost, Jacobian and scalars (speculative linearization).
+// spec: speculative mode (the device LM state supplies the radius; ba_decide judges the step and
+// publishes with sequence number spec_seq); otherwise the host reads the scalars and judges.
 template <int K>
 int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* step_norm, double* ccost,
-             double* cgmax, double* cxnorm) {
+             double* cgmax, double* cxnorm, bool spec = false, unsigned spec_seq = 0) {
     constexpr int RW = K + 1;
+    const double* lmr = spec ? c->lmst.as<double>() : nullptr;
     const int C = c->C, npad = c->npad;
     double* S = c->SR.as<double>();
     double* R = S + (size_t)npad * npad;
@@ -285,7 +318,7 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
                            c->grp.as<Grp>(), c->bat.as<Batch>(), c->gcam.as<int>(), c->obs_lc.as<short>(),             \
                            c->obs_point.as<int>(), c->obs_cam.as<int>(), c->pt_start.as<int>(), c->J.as<double>(),      \
                            c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, \
-                           c->P, C, c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl)
+                           c->P, C, c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl, lmr)
         const bool sj = !c->j_scaled;   // the first step of a solve scales J in place
         switch (c->gs_nt) { case 1: GSCHUR(1); break; case 2: GSCHUR(2); break; case 3: GSCHUR(3); break; default: GSCHUR(4); }
 #undef GSCHUR2
@@ -295,7 +328,7 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     HIPCHK(hipMemsetAsync(S, 0, sizeof(double) * c->sr_count, c->st));
     hipLaunchKernelGGL(ba_assemble, dim3(c->ntasks), dim3(64), 0, c->st, c->tasks.as<ATask>(), c->ents.as<AEnt>(),
                        c->sg.as<double>(), c->hbig.as<double>(), c->rg.as<double>(), K, c->camrow.as<int>(), npad, S,
-                       R, Dm, ri);
+                       R, Dm, ri, gate(c));
     HIPCHK(hipGetLastError());
     if (c->phases) HIPCHK(hipEventRecord(c->ev[1], c->st));
     // point-sharded ranks: the group part of the reduced camera system and its rhs are sums over
@@ -303,15 +336,15 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     if (c->ar) {
         const int tail = (int)(c->sr_count - (size_t)npad * npad);
         hipLaunchKernelGGL(chol_pack, dim3(c->n_nztiles + 1), dim3(256), 0, c->st, S, npad, c->nztiles.as<int2>(),
-                           c->n_nztiles, tail, c->packbuf.as<double>(), 0);
+                           c->n_nztiles, tail, c->packbuf.as<double>(), 0, gate(c));
         RC(allreduce(c, c->packbuf.as<double>(), (int64_t)c->n_nztiles * NB * NB + tail, SFMX_REDUCE_SUM));
         hipLaunchKernelGGL(chol_pack, dim3(c->n_nztiles + 1), dim3(256), 0, c->st, S, npad, c->nztiles.as<int2>(),
-                           c->n_nztiles, tail, c->packbuf.as<double>(), 1);
+                           c->n_nztiles, tail, c->packbuf.as<double>(), 1, gate(c));
     }
     hipLaunchKernelGGL(ba_add_cam<K>, dim3(C + 1), dim3(64), 0, c->st, c->P, C, npad, c->camrow.as<int>(),
                        c->padrows.as<int>(), (int)c->plan.padrows.size(), c->camsum.as<double>(),
                        c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, S,
-                       R, Dm, ri);
+                       R, Dm, ri, gate(c), lmr);
     double* sol = c->sol.as<double>();
     RC(solve_reduced<RW>(c, sol + c->ne));
     if (c->phases) HIPCHK(hipEventRecord(c->ev[2], c->st));
@@ -319,13 +352,25 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
         hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups), dim3(256), 0, c->st, c->grp.as<Grp>(),
                            c->chk.as<Chunk>(), c->obs_point.as<int>(), c->obs_cam.as<int>(), c->pt_start.as<int>(),
                            c->J.as<double>(), c->scale.as<double>(), c->plt.as<double>(), sol + c->ne, c->P, C,
-                           c->x.as<double>(), c->cand.as<double>(), c->gpl.as<double>());
+                           c->x.as<double>(), c->cand.as<double>(), c->gpl.as<double>(), gate(c));
     hipLaunchKernelGGL(ba_fstep, dim3(nblk(c->nf)), dim3(256), 0, c->st, c->nf, sol + c->ne, c->scale.as<double>() + c->ne,
-                       c->x.as<double>() + c->ne, c->cand.as<double>() + c->ne);
+                       c->x.as<double>() + c->ne, c->cand.as<double>() + c->ne, gate(c));
     HIPCHK(hipGetLastError());
     double v[SC_N];
     RC(lin_at<K>(c, c->cand.as<double>(), c->J2.as<double>(), c->colsq2.as<double>(), c->grad2.as<double>(),
-                 c->camsum2.as<double>(), true, v));
+                 c->camsum2.as<double>(), true, spec ? nullptr : v));
+    if (spec) {
+        const sfmx_ba_options& op = c->opt;
+        LmOpt lo{op.parameter_tolerance, op.function_tolerance, op.min_relative_decrease, op.max_trust_region_radius,
+                 op.gradient_tolerance, op.min_trust_region_radius, c->spec_maxit, op.max_num_consecutive_invalid_steps,
+                 SFMX_BA_CONVERGENCE, SFMX_BA_NO_CONVERGENCE, SFMX_BA_FAILURE};
+        const int slot = spec_seq & 1;
+        unsigned* hseq = reinterpret_cast<unsigned*>(c->hs + sfmx_ba_ctx::HS_SEQ + slot);
+        hipLaunchKernelGGL(ba_decide, dim3(1), dim3(64), 0, c->st, scal(c, 0), c->lmst.as<double>(), c->failf.as<int>(),
+                           lo, c->hs + slot * sfmx_ba_ctx::HS_SLOT, hseq, spec_seq);
+        HIPCHK(hipGetLastError());
+        return SFMX_OK;
+    }
     if (v[SC_FAIL] >= 2.0) return fail(SFMX_EINTERNAL, "BA solve: a dependency wait of chol_backsolve timed out");
     const double sn2 = v[SC_STEPN] + v[SC_STEPN_F];
     *mcc = -v[SC_MODEL];
@@ -414,6 +459,8 @@ int ensure_plan(sfmx_ba_ctx* c) {
         HIPCHK(hipMemsetAsync(c->dagctr.p, 0, c->dagctr.bytes, st));
         const char* e = std::getenv("SFMX_BA_BACK");
         c->back_dag = !(e && e[0] == '0');
+        e = std::getenv("SFMX_BA_SPEC");   // opt-in: measured no faster (host turnaround)
+        c->spec = e && e[0] == '1';
     }
     {   // chol_level_split: per level, the parts of the inverting tasks first (the plan's task order)
         std::vector<int4> parts;
@@ -460,6 +507,7 @@ int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace,
     c->scaled = false;   // Ceres computes the Jacobi scale at iteration 0 of each Solve
     HIPCHK(hipEventRecord(c->ev[4], c->st));
     HIPCHK(hipMemsetAsync(c->failf.p, 0, sizeof(int), c->st));
+    hipLaunchKernelGGL(ba_open_gate, dim3(1), dim3(64), 0, c->st, c->failf.as<int>());
     double v[SC_N];
     RC(lin_at<K>(c, c->x.as<double>(), c->J.as<double>(), c->colsq.as<double>(), c->grad.as<double>(),
                  c->camsum.as<double>(), false, v));
@@ -483,6 +531,68 @@ int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace,
     bool successful = true;
     int iteration = 0, succ = 0, unsucc = 0, invalid_total = 0, consec_invalid = 0, ntrace = 0;
     int term = SFMX_BA_NO_CONVERGENCE;
+    if (c->spec && !c->phases) {
+        // Speculative LM: the device judges every step (ba_decide, the loop below restated) and the
+        // host enqueues step s + 1 on the accepted buffers before it reads step s's outcome, so the GPU
+        // never waits for the host; a rejected step's successor is skipped by the step gate and
+        // enqueued again on the unchanged buffers.  The first iteration's top is the host's.
+        ++succ;
+        if (trace && ntrace < trace_cap) { trace[0] = cost; trace[1] = radius; trace[2] = 1.0; ++ntrace; }
+        if (iteration >= maxit) term = SFMX_BA_NO_CONVERGENCE;
+        else if (gmax <= o.gradient_tolerance) term = SFMX_BA_CONVERGENCE;
+        else if (radius <= o.min_trust_region_radius) term = SFMX_BA_CONVERGENCE;
+        else {
+            ++iteration;
+            c->spec_maxit = maxit;
+            double* li = c->lm_init;
+            for (int i = 0; i < LM_N; ++i) li[i] = 0.0;
+            li[LM_COST] = cost; li[LM_GMAX] = gmax; li[LM_XNORM] = x_norm; li[LM_RADIUS] = radius; li[LM_DECREASE] = 2.0;
+            li[LM_ITER] = iteration; li[LM_SUCC] = succ; li[LM_SUCCESSFUL] = 1.0; li[LM_TERM] = LM_RUNNING;
+            HIPCHK(hipMemcpyAsync(c->lmst.p, li, sizeof(double) * LM_N, hipMemcpyHostToDevice, c->st));
+            auto swap_state = [c]() {
+                std::swap(c->x, c->cand);
+                std::swap(c->J, c->J2);
+                std::swap(c->colsq, c->colsq2);
+                std::swap(c->grad, c->grad2);
+                std::swap(c->camsum, c->camsum2);
+            };
+            bool vd; double d0, d1, d2, d3, d4;
+            unsigned q = ++c->seq;
+            RC(try_step<K>(c, radius, &vd, &d0, &d1, &d2, &d3, &d4, true, q));
+            double L[sfmx_ba_ctx::HS_SLOT];
+            for (;;) {
+                swap_state();   // provisional: the next step runs on the accepted step's buffers
+                unsigned q2 = ++c->seq;
+                RC(try_step<K>(c, radius, &vd, &d0, &d1, &d2, &d3, &d4, true, q2));
+                RC(wait_slot(c, q, L));
+                const double* lm = L + SC_N;
+                if (lm[LM_ERROR] != 0.0) {
+                    (void)hipStreamSynchronize(c->st);
+                    return fail(SFMX_EINTERNAL, "BA solve: a dependency wait of chol_backsolve timed out");
+                }
+                const bool acc = lm[LM_ACCEPTED] != 0.0;
+                if (!acc) swap_state();
+                if (lm[LM_TRACE] != 0.0 && trace && ntrace < trace_cap) {
+                    trace[3 * ntrace] = lm[LM_COST]; trace[3 * ntrace + 1] = lm[LM_RADIUS];
+                    trace[3 * ntrace + 2] = lm[LM_SUCCESSFUL]; ++ntrace;
+                }
+                if (lm[LM_TERM] != LM_RUNNING) {   // the successor is gated off
+                    term = (int)lm[LM_TERM];
+                    break;
+                }
+                if (!acc) {   // the successor was skipped: the same step again, on the unchanged buffers
+                    hipLaunchKernelGGL(ba_open_gate, dim3(1), dim3(64), 0, c->st, c->failf.as<int>());
+                    q2 = ++c->seq;
+                    RC(try_step<K>(c, radius, &vd, &d0, &d1, &d2, &d3, &d4, true, q2));
+                }
+                q = q2;
+            }
+            HIPCHK(hipStreamSynchronize(c->st));   // the skipped successor drains
+            const double* lm = L + SC_N;
+            cost = lm[LM_COST]; gmax = lm[LM_GMAX]; radius = lm[LM_RADIUS];
+            succ = (int)lm[LM_SUCC]; unsucc = (int)lm[LM_UNSUCC]; invalid_total = (int)lm[LM_INVALID];
+        }
+    } else
     for (;;) {
         // FinalizeIterationAndCheckIfMinimizerCanContinue (Ceres 1.14 trust_region_minimizer.cc [ext])
         if (successful) ++succ; else ++unsucc;
@@ -516,7 +626,7 @@ int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace,
             cost = ccost;
             gmax = cgmax;
             x_norm = cxn;
-            radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3));
+            radius = radius / std::max(1.0 / 3.0, 1.0 - lm_cube(2.0 * rel - 1.0));   // == ba_decide's bits
             radius = std::min(o.max_trust_region_radius, radius);
             decrease = 2.0;
             successful = true;
@@ -796,10 +906,10 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
     auto bail = [&](int rc) { delete c; return rc; };
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) return bail(fail(SFMX_EDEVICE, "stream"));
     for (auto& e : c->ev) if (hipEventCreate(&e) != hipSuccess) return bail(fail(SFMX_EDEVICE, "event"));
-    if (hipHostMalloc(reinterpret_cast<void**>(&c->hs), sizeof(double) * (SC_N + 1),
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->hs), sizeof(double) * sfmx_ba_ctx::HS_N,
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
         return bail(fail(SFMX_ENOMEM, "pinned scalar buffer"));
-    std::memset(c->hs, 0, sizeof(double) * (SC_N + 1));
+    std::memset(c->hs, 0, sizeof(double) * sfmx_ba_ctx::HS_N);
     const int P = caller->n_points, C = caller->n_cams, O = caller->n_obs, K = caller->cam_model;
     c->P = P; c->C = C; c->O = O; c->K = K; c->cx = caller->cx; c->cy = caller->cy;
     c->ne = 3 * (int64_t)P;
@@ -859,7 +969,7 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
         {&c->plt, 72 * (size_t)std::max(P, 1)}, {&c->sg, 8 * (size_t)std::max<long long>(tp.sg_total, 1)},
         {&c->rg, 8 * (size_t)std::max(tp.rg_total, 1)}, {&c->hbig, 8 * (size_t)std::max<long long>(tp.h_total, 1)},
         {&c->gpart, 8 * (size_t)std::max(c->nslots, 1) * ncp(K)}, {&c->gpl, 8 * (size_t)std::max(c->ngroups, 1) * GP_N},
-        {&c->scal, 8 * SC_N}, {&c->failf, 64},
+        {&c->scal, 8 * SC_N}, {&c->failf, 64}, {&c->lmst, 8 * LM_N}, {&c->camscr, 8 * ncams},
         {&c->partA, 8 * (size_t)nblk(std::max<int64_t>(O, n))}};
     for (auto& a : allocs) if ((rc = a.b->alloc(a.bytes))) return bail(rc);
     HIPCHK(hipMemsetAsync(c->gpl.p, 0, c->gpl.bytes, st));
