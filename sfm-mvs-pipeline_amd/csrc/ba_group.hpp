@@ -1032,7 +1032,8 @@ __global__ __launch_bounds__(256)
 void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, const double* __restrict__ gpl,
                  const double* __restrict__ xf_new, const double* __restrict__ xf_old, int cand_mode,
                  const int* __restrict__ fail, double* __restrict__ colsq, double* __restrict__ grad,
-                 double* __restrict__ scal, double* __restrict__ camsum_out, int ncs) {
+                 double* __restrict__ scal, double* __restrict__ camsum_out, int ncs,
+                 const double* __restrict__ pre) {
     if (step_gated(fail + 1)) return;
     constexpr int NCP = ncp(K);
     __shared__ double sh[8];
@@ -1069,15 +1070,21 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
         }
     }
     double g[5] = {0, 0, 0, 0, 0};
-    for (int b = t; b < ngroups; b += blockDim.x) {
-        const double* q = gpl + (size_t)b * GP_N;
-        g[0] += q[GP_COST]; g[1] += q[GP_MODEL]; g[2] += q[GP_STEPN]; g[3] += q[GP_XN];
-        g[4] = fmax(g[4], q[GP_GMAX]);
+    double s0, s1, s2, s3;
+    if (pre) {   // the group sums came through the camera-sum all-reduce (ba_group_sums), g[4] local
+        s0 = pre[0]; s1 = pre[1]; s2 = pre[2]; s3 = pre[3];
+        g[4] = pre[4];
+    } else {
+        for (int b = t; b < ngroups; b += blockDim.x) {
+            const double* q = gpl + (size_t)b * GP_N;
+            g[0] += q[GP_COST]; g[1] += q[GP_MODEL]; g[2] += q[GP_STEPN]; g[3] += q[GP_XN];
+            g[4] = fmax(g[4], q[GP_GMAX]);
+        }
+        s0 = block_sum(g[0], sh);
+        s1 = block_sum(g[1], sh);
+        s2 = block_sum(g[2], sh);
+        s3 = block_sum(g[3], sh);
     }
-    const double s0 = block_sum(g[0], sh);
-    const double s1 = block_sum(g[1], sh);
-    const double s2 = block_sum(g[2], sh);
-    const double s3 = block_sum(g[3], sh);
     const double sxn = block_sum(xn, sh);
     const double ssn = block_sum(sn, sh);
     double gm = fmax(gmax, g[4]);
@@ -1096,6 +1103,37 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
         scal[SC_FAIL] = (double)*fail;   // bit 0: non-positive pivot / invalid step, bit 1: solve wait timed out
         scal[SC_STEPN_F] = ssn;
         scal[SC_XN_F] = sxn;
+    }
+}
+
+// Point-sharded ranks: the rank's group sums (cost, model change, step and parameter norms: the
+// loop of ba_finalize) and its max |grad| of the points, written behind the camera sums so the
+// four sums travel in the camera-sum all-reduce (one collective per linearization fewer);
+// out[4] (the max) stays outside the reduced range.  One workgroup of 256.
+__global__ __launch_bounds__(256)
+void ba_group_sums(int ngroups, const double* __restrict__ gpl, double* __restrict__ out, const int* __restrict__ gate) {
+    if (step_gated(gate)) return;
+    __shared__ double sh[8];
+    const int t = threadIdx.x;
+    double g[5] = {0, 0, 0, 0, 0};
+    for (int b = t; b < ngroups; b += blockDim.x) {
+        const double* q = gpl + (size_t)b * GP_N;
+        g[0] += q[GP_COST]; g[1] += q[GP_MODEL]; g[2] += q[GP_STEPN]; g[3] += q[GP_XN];
+        g[4] = fmax(g[4], q[GP_GMAX]);
+    }
+    const double s0 = block_sum(g[0], sh);
+    const double s1 = block_sum(g[1], sh);
+    const double s2 = block_sum(g[2], sh);
+    const double s3 = block_sum(g[3], sh);
+    double gm = g[4];
+    for (int o = 32; o > 0; o >>= 1) gm = fmax(gm, __shfl_xor(gm, o));
+    __syncthreads();
+    if ((t & 63) == 0) sh[t >> 6] = gm;
+    __syncthreads();
+    if (t == 0) {
+        double m = 0.0;
+        for (int i = 0; i < 4; ++i) m = fmax(m, sh[i]);
+        out[0] = s0; out[1] = s1; out[2] = s2; out[3] = s3; out[4] = m;
     }
 }
 

@@ -240,12 +240,16 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double
     hipLaunchKernelGGL(ba_camred<K>, dim3(c->C + K * (K + 1) / 2 + K), dim3(128), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
                        c->cref.as<int>(), c->gpart.as<double>(), cs_red, gate(c));
     HIPCHK(hipGetLastError());
-    RC(allreduce(c, cs_red, ncs, SFMX_REDUCE_SUM));
+    // multi-rank: the group sums ride in the camera-sum all-reduce (cs_red[ncs .. ncs + 4), the
+    // rank's point max |grad| at cs_red[ncs + 4] outside it): 3 collectives per LM step, not 4
+    double* pre = c->ar ? cs_red + ncs : nullptr;
+    if (pre)
+        hipLaunchKernelGGL(ba_group_sums, dim3(1), dim3(256), 0, c->st, c->ngroups, c->gpl.as<double>(), pre, gate(c));
+    RC(allreduce(c, cs_red, ncs + (pre ? 4 : 0), SFMX_REDUCE_SUM));
     hipLaunchKernelGGL(ba_finalize<K>, dim3(1), dim3(256), 0, c->st, c->ngroups, c->P, c->C, cs_red,
                        c->gpl.as<double>(), xp + c->ne, c->x.as<double>() + c->ne, cand_mode ? 1 : 0, c->failf.as<int>(),
-                       colsq_o, grad_o, scal(c, 0), camsum_o, cs_red == camsum_o ? 0 : ncs);
+                       colsq_o, grad_o, scal(c, 0), camsum_o, cs_red == camsum_o ? 0 : ncs, pre);
     HIPCHK(hipGetLastError());
-    RC(allreduce(c, scal(c, SC_COST), 4, SFMX_REDUCE_SUM));
     RC(allreduce(c, scal(c, SC_GMAX), 2, SFMX_REDUCE_MAX));
     if (!out) return SFMX_OK;   // speculative step: ba_decide judges and publishes
     RC(poll_scalars(c, out, c->phases && cand_mode ? c->ev[3] : nullptr));
@@ -965,11 +969,11 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
     struct { Buf* b; size_t bytes; } allocs[] = {
         {&c->x, 8 * n}, {&c->cand, 8 * n}, {&c->scale, 8 * n}, {&c->colsq, 8 * n}, {&c->colsq2, 8 * n},
         {&c->grad, 8 * n}, {&c->grad2, 8 * n}, {&c->sol, 8 * n},
-        {&c->J, 8 * so * jst(K)}, {&c->J2, 8 * so * jst(K)}, {&c->camsum, 8 * ncams}, {&c->camsum2, 8 * ncams},
+        {&c->J, 8 * so * jst(K)}, {&c->J2, 8 * so * jst(K)}, {&c->camsum, 8 * (ncams + 5)}, {&c->camsum2, 8 * (ncams + 5)},
         {&c->plt, 72 * (size_t)std::max(P, 1)}, {&c->sg, 8 * (size_t)std::max<long long>(tp.sg_total, 1)},
         {&c->rg, 8 * (size_t)std::max(tp.rg_total, 1)}, {&c->hbig, 8 * (size_t)std::max<long long>(tp.h_total, 1)},
         {&c->gpart, 8 * (size_t)std::max(c->nslots, 1) * ncp(K)}, {&c->gpl, 8 * (size_t)std::max(c->ngroups, 1) * GP_N},
-        {&c->scal, 8 * SC_N}, {&c->failf, 64}, {&c->lmst, 8 * LM_N}, {&c->camscr, 8 * ncams},
+        {&c->scal, 8 * SC_N}, {&c->failf, 64}, {&c->lmst, 8 * LM_N}, {&c->camscr, 8 * (ncams + 5)},
         {&c->partA, 8 * (size_t)nblk(std::max<int64_t>(O, n))}};
     for (auto& a : allocs) if ((rc = a.b->alloc(a.bytes))) return bail(rc);
     HIPCHK(hipMemsetAsync(c->gpl.p, 0, c->gpl.bytes, st));
