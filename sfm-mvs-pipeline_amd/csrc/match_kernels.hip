@@ -910,6 +910,21 @@ hipError_t launch_prep_l2_batch(const PrepImg* tab, int n, int max_rows_pad, int
                                                                                               keyc2, flags);
     return hipGetLastError();
 }
+// The per-image integrality flags into pinned, host-coherent memory, then a sequence word with
+// system-scope release: set_images spins on the word instead of a D2H copy + hipStreamSynchronize
+// (whose interrupt-driven wake-up the host would pay once per matching call).
+__global__ __launch_bounds__(256)
+void publish_flags_kernel(const int32_t* __restrict__ flags, int n, int32_t* __restrict__ dst, unsigned* __restrict__ seq,
+                          unsigned v) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = flags[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(seq, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+hipError_t launch_publish_flags(const int32_t* flags, int n, int32_t* dst, unsigned* seq, unsigned v, hipStream_t st) {
+    publish_flags_kernel<<<1, 256, 0, st>>>(flags, n, dst, seq, v);
+    return hipGetLastError();
+}
 hipError_t launch_probe_xor80(int8_t* p, int64_t bytes, hipStream_t st) {
     const int64_t n = bytes / 4;
     if (n == 0) return hipSuccess;

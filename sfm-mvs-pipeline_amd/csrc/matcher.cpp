@@ -30,6 +30,7 @@
 namespace sfmx {
 hipError_t launch_prep_l2(const float*, int, int, int, int8_t*, int32_t*, int32_t*, int32_t*, int32_t*, hipStream_t);
 hipError_t launch_probe_xor80(int8_t*, int64_t, hipStream_t);
+hipError_t launch_publish_flags(const int32_t*, int, int32_t*, unsigned*, unsigned, hipStream_t);
 hipError_t launch_prep_l2_batch(const PrepImg*, int, int, int8_t*, int32_t*, int32_t*, int32_t*, int32_t*, hipStream_t);
 hipError_t launch_prep_f32(const float*, int, int, int, float*, hipStream_t);
 hipError_t launch_prep_hamming(const uint8_t*, int, int, int, uint8_t*, hipStream_t);
@@ -160,6 +161,9 @@ struct sfmx_matcher {
     DevBuf unsettled;                // int32: pass-1 forwarded queries pass 2 never wrote (must stay 0)
     DevBuf prep_tab;                 // batched SIFT prep: one PrepImg per image
     PinnedBuf stage_prep, stage_run, stage_imgs, stage_flags; // pinned staging of the small uploads / flag readback
+    int32_t* hflags = nullptr;   // host-coherent mapped: integrality flags [hflags_cap] + sequence word (publish_flags_kernel)
+    int hflags_cap = 0;
+    unsigned flag_seq = 0;
     // Run plan cache: the device pair/work lists of the last run stay valid while the
     // pair list, the images' row counts and integrality and the kernel variant are unchanged.
     std::vector<int32_t> plan_pairs;
@@ -270,10 +274,30 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
     }
     m->any_nonintegral = false;
     if (norm == SFMX_NORM_L2 && n > 0) {
-        if ((rc = m->stage_flags.ensure(sizeof(int32_t) * n))) return rc;
-        const int32_t* fl = m->stage_flags.as<int32_t>();
-        HIPCHK(hipMemcpyAsync(m->stage_flags.p, m->flags.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+        if (n > m->hflags_cap) {
+            if (m->hflags) (void)hipHostFree(m->hflags);
+            m->hflags = nullptr;
+            m->hflags_cap = 0;
+            if (hipHostMalloc(reinterpret_cast<void**>(&m->hflags), sizeof(int32_t) * (n + 4),
+                              hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+                return fail(SFMX_ENOMEM, "hipHostMalloc (integrality flags)");
+            m->hflags_cap = n;
+            m->hflags[n] = 0;
+        }
+        unsigned* hseq = reinterpret_cast<unsigned*>(m->hflags + m->hflags_cap);
+        const unsigned want = ++m->flag_seq;
+        HIPCHK(launch_publish_flags(m->flags.as<int32_t>(), n, m->hflags, hseq, want, st));
+        for (unsigned spins = 1;; ++spins) {   // the host needs the flags to plan the run
+            if (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == want) break;
+            if ((spins & 255) == 0) {
+                const hipError_t e = hipStreamQuery(st);
+                if (e != hipSuccess && e != hipErrorNotReady) return fail(SFMX_EDEVICE, std::string("set_images: ") + hipGetErrorString(e));
+                if (e == hipSuccess && __atomic_load_n(hseq, __ATOMIC_ACQUIRE) != want)
+                    return fail(SFMX_EINTERNAL, "set_images: stream drained without the flag handoff");
+            }
+            __builtin_ia32_pause();
+        }
+        const int32_t* fl = m->hflags;
         for (int i = 0; i < n; ++i) {
             m->imgs[i].integral = fl[i] ? 0 : 1;
             m->any_nonintegral |= fl[i] != 0;
@@ -514,6 +538,8 @@ int sfmx_matcher_destroy(sfmx_matcher* m) {
         m->stage_run.release();
         m->stage_imgs.release();
         m->stage_flags.release();
+        if (m->hflags) (void)hipHostFree(m->hflags);
+        m->hflags = nullptr;
         DevBuf* bufs[] = {&m->raw, &m->desc8, &m->normv, &m->keyc, &m->keyc2, &m->qlist, &m->qcount, &m->porder, &m->work2, &m->work2_n, &m->f32, &m->flags, &m->imgs_d, &m->pairs_d, &m->prep_tab,
                           &m->work_d, &m->work32_d, &m->dense_idx, &m->dense_dist, &m->slow_list, &m->slow_count,
                           &m->unsettled, &m->counts, &m->keep, &m->offsets, &m->out};
