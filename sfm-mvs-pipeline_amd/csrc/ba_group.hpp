@@ -1031,9 +1031,10 @@ template <int K>
 __global__ __launch_bounds__(256)
 void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, const double* __restrict__ gpl,
                  const double* __restrict__ xf_new, const double* __restrict__ xf_old, int cand_mode,
-                 const int* __restrict__ fail, double* __restrict__ colsq, double* __restrict__ grad,
+                 int* __restrict__ fail, double* __restrict__ colsq, double* __restrict__ grad,
                  double* __restrict__ scal, double* __restrict__ camsum_out, int ncs,
-                 const double* __restrict__ pre) {
+                 const double* __restrict__ pre, double* __restrict__ pub_dst, unsigned* __restrict__ pub_seq,
+                 unsigned pub_v) {
     if (step_gated(fail + 1)) return;
     constexpr int NCP = ncp(K);
     __shared__ double sh[8];
@@ -1103,6 +1104,8 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
         scal[SC_FAIL] = (double)*fail;   // bit 0: non-positive pivot / invalid step, bit 1: solve wait timed out
         scal[SC_STEPN_F] = ssn;
         scal[SC_XN_F] = sxn;
+        // one rank: nothing is reduced after this kernel, so it publishes the scalars itself (ba_publish)
+        if (pub_dst) publish_body(scal, SC_N, nullptr, 0, pub_dst, pub_seq, pub_v, fail);
     }
 }
 

@@ -166,13 +166,16 @@ int fetch_scalars(sfmx_ba_ctx* c, int i0, int cnt, double* out) {
 // The LM step's scalars: ba_publish writes them to pinned memory behind everything queued so far
 // and the host spins on the sequence word (a stream error or a drained stream without the word
 // ends the wait).
-int poll_scalars(sfmx_ba_ctx* c, double* out, hipEvent_t mark) {
-    const unsigned want = ++c->seq;
-    if (mark) HIPCHK(hipEventRecord(mark, c->st));
+// published: ba_finalize already published sequence number `published` (one rank, no phase mark)
+int poll_scalars(sfmx_ba_ctx* c, double* out, hipEvent_t mark, unsigned published = 0) {
+    const unsigned want = published ? published : ++c->seq;
     unsigned* hseq = reinterpret_cast<unsigned*>(c->hs + sfmx_ba_ctx::HS_SEQ + 2);
-    hipLaunchKernelGGL(ba_publish, dim3(1), dim3(64), 0, c->st, scal(c, 0), (int)SC_N, c->hs, hseq, want,
-                       c->failf.as<int>());
-    HIPCHK(hipGetLastError());
+    if (!published) {
+        if (mark) HIPCHK(hipEventRecord(mark, c->st));
+        hipLaunchKernelGGL(ba_publish, dim3(1), dim3(64), 0, c->st, scal(c, 0), (int)SC_N, c->hs, hseq, want,
+                           c->failf.as<int>());
+        HIPCHK(hipGetLastError());
+    }
     for (unsigned spins = 1;; ++spins) {
         if (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == want) break;
         if ((spins & 255) == 0) {
@@ -246,13 +249,17 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double
     if (pre)
         hipLaunchKernelGGL(ba_group_sums, dim3(1), dim3(256), 0, c->st, c->ngroups, c->gpl.as<double>(), pre, gate(c));
     RC(allreduce(c, cs_red, ncs + (pre ? 4 : 0), SFMX_REDUCE_SUM));
+    // one rank, host-judged, no phase mark: ba_finalize publishes the scalars itself (one launch fewer)
+    const bool fold = out && !c->ar && !(c->phases && cand_mode);
+    const unsigned fold_seq = fold ? ++c->seq : 0;
     hipLaunchKernelGGL(ba_finalize<K>, dim3(1), dim3(256), 0, c->st, c->ngroups, c->P, c->C, cs_red,
                        c->gpl.as<double>(), xp + c->ne, c->x.as<double>() + c->ne, cand_mode ? 1 : 0, c->failf.as<int>(),
-                       colsq_o, grad_o, scal(c, 0), camsum_o, cs_red == camsum_o ? 0 : ncs, pre);
+                       colsq_o, grad_o, scal(c, 0), camsum_o, cs_red == camsum_o ? 0 : ncs, pre,
+                       fold ? c->hs : nullptr, reinterpret_cast<unsigned*>(c->hs + sfmx_ba_ctx::HS_SEQ + 2), fold_seq);
     HIPCHK(hipGetLastError());
     RC(allreduce(c, scal(c, SC_GMAX), 2, SFMX_REDUCE_MAX));
     if (!out) return SFMX_OK;   // speculative step: ba_decide judges and publishes
-    RC(poll_scalars(c, out, c->phases && cand_mode ? c->ev[3] : nullptr));
+    RC(poll_scalars(c, out, c->phases && cand_mode ? c->ev[3] : nullptr, fold ? fold_seq : 0));
     return SFMX_OK;
 }
 
