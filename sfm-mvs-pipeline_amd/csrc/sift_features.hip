@@ -281,6 +281,95 @@ void blur_tile_n_kernel(const float* __restrict__ src, float* __restrict__ dst, 
     }
 }
 
+// The small octaves of one image in ONE workgroup (1024 threads): octaves o_s .. nOct - 1 (each of
+// at most SMALL_PX pixels), in order: INTER_NEAREST half of the previous octave's layer L, then per
+// layer the row filter (taps in order, as blur_row_kernel) into `rf`, the symmetric column filter
+// (as blur_col_kernel) into the layer and its DoG against the previous layer, then the octave's
+// 26-neighbour extrema (as extrema_kernel).  The same operations on the same values as the
+// per-octave launches (tile blur, half_nn_kernel, extrema_kernel), so every layer, DoG and candidate
+// is bit-identical; ~7 launches per small octave become one launch for all of them.  Everything goes
+// through global memory (L1/L2-resident at these sizes); __syncthreads orders the passes.
+constexpr int SMALL_PX = 2048, SMALL_MAXL = 8;   // r02q sweep: 512 / 2048 +3 %, 8192 -7 %, 32768 -40 %
+struct SmallTaps { const float* p[SMALL_MAXL]; int n[SMALL_MAXL]; };
+__global__ __launch_bounds__(1024)
+void small_octaves_kernel(const Layer* __restrict__ gp, const Layer* __restrict__ dog, int L, int o_s, int nOct,
+                          SmallTaps taps, float* __restrict__ rf, int threshold, Cand* __restrict__ out,
+                          int* __restrict__ count, int cap) {
+    const int tid = threadIdx.x;
+    for (int o = o_s; o < nOct; ++o) {
+        const Layer base = gp[o * (L + 3)];
+        const int w = base.w, h = base.h, npx = w * h;
+        {   // layer 0: INTER_NEAREST half of the previous octave's layer L
+            const Layer src = gp[(o - 1) * (L + 3) + L];
+            const double ifx = 1. / ((double)w / src.w), ify = 1. / ((double)h / src.h);
+            for (int e = tid; e < npx; e += 1024) {
+                const int y = e / w, x = e % w;
+                const int sy = min((int)floor(y * ify), src.h - 1), sx = min((int)floor(x * ifx), src.w - 1);
+                base.p[e] = src.p[(int64_t)sy * src.w + sx];
+            }
+        }
+        __syncthreads();
+        for (int i = 1; i < L + 3; ++i) {
+            const float* src = gp[o * (L + 3) + i - 1].p;
+            float* dst = gp[o * (L + 3) + i].p;
+            float* dg = dog[o * (L + 2) + i - 1].p;
+            const float* f = taps.p[i];
+            const int n = taps.n[i], r = n / 2;
+            for (int e = tid; e < npx; e += 1024) {   // row filter
+                const int y = e / w, x = e % w;
+                const float* row = src + (int64_t)y * w;
+                float sm = f[0] * row[reflect101(x - r, w)];
+                for (int k = 1; k < n; ++k) sm += f[k] * row[reflect101(x - r + k, w)];
+                rf[e] = sm;
+            }
+            __syncthreads();
+            for (int e = tid; e < npx; e += 1024) {   // column filter + DoG
+                const int y = e / w, x = e % w;
+                float sm = f[r] * rf[e];
+                for (int k = 1; k <= r; ++k)
+                    sm += f[r + k] * (rf[(int64_t)reflect101(y + k, h) * w + x] + rf[(int64_t)reflect101(y - k, h) * w + x]);
+                dst[e] = sm;
+                dg[e] = sm - src[e];
+            }
+            __syncthreads();
+        }
+        if (w > 2 * IMG_BORDER && h > 2 * IMG_BORDER) {   // extrema of layers 1 .. L
+            const int iw = w - 2 * IMG_BORDER, ih = h - 2 * IMG_BORDER, m = iw * ih;
+            for (int e = tid; e < L * m; e += 1024) {
+                const int layer = 1 + e / m, q0 = e % m, rr = q0 / iw + IMG_BORDER, c = q0 % iw + IMG_BORDER;
+                const float* prev = dog[o * (L + 2) + layer - 1].p;
+                const float* img = dog[o * (L + 2) + layer].p;
+                const float* next = dog[o * (L + 2) + layer + 1].p;
+                const float val = img[(int64_t)rr * w + c];
+                if (!(fabsf(val) > threshold)) continue;
+                bool mx = val > 0, mn = val < 0;
+#pragma unroll
+                for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; ++dx) {
+                        const int64_t q = (int64_t)(rr + dy) * w + c + dx;
+                        const float a = img[q], b = prev[q], ee = next[q];
+                        mx = mx && val >= a && val >= b && val >= ee;
+                        mn = mn && val <= a && val <= b && val <= ee;
+                    }
+                if (!mx && !mn) continue;
+                const int slot = atomicAdd(count, 1);
+                if (slot < cap) out[slot] = Cand{o, layer, rr, c};
+            }
+        }
+        __syncthreads();   // the next octave halves this octave's layer L
+    }
+}
+
+inline bool small_octaves_on() {   // SFMX_SIFT_SMALL=0: every octave as per-octave launches (A/B, tests)
+    const char* e = std::getenv("SFMX_SIFT_SMALL");
+    return !(e && e[0] == '0');
+}
+inline int small_px() {   // SFMX_SIFT_SMALL_PX: the largest octave (pixels) the fused launch takes (tuning)
+    const char* e = std::getenv("SFMX_SIFT_SMALL_PX");
+    return e ? std::atoi(e) : SMALL_PX;
+}
+
 __global__ void half_nn_kernel(const float* __restrict__ src, int sw, int sh, float* __restrict__ dst, int dw, int dh,
                                double ifx, double ify) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
@@ -838,7 +927,11 @@ int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int
             };
             up2_kernel<<<dim3((BW + 255) / 256, BH), 256, 0, st>>>(dimg, width, height, dpitch, up);
             blur(up, hgp[0].p, nullptr, BW, BH, 0);
-            for (int o = 0; o < nOct; ++o)
+            // the trailing octaves of at most SMALL_PX pixels run in one launch (small_octaves_kernel)
+            int o_small = nOct;
+            if (small_octaves_on() && L + 3 <= SMALL_MAXL)
+                while (o_small > 1 && (int64_t)ow[o_small - 1] * oh[o_small - 1] <= small_px()) --o_small;
+            for (int o = 0; o < o_small; ++o)
                 for (int i = 0; i < L + 3; ++i) {
                     if (o == 0 && i == 0) continue;
                     Layer& dst = hgp[o * (L + 3) + i];
@@ -851,7 +944,13 @@ int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int
                     }
                 }
             const int threshold = (int)std::floor(0.5 * params->contrast_threshold / L * 255);
-            for (int o = 0; o < nOct; ++o) {
+            if (o_small < nOct) {
+                SmallTaps tp{};
+                for (int i = 0; i < L + 3; ++i) { tp.p[i] = dk[i]; tp.n[i] = (int)kern[i].size(); }
+                small_octaves_kernel<<<1, 1024, 0, st>>>(dgp, ddog, L, o_small, nOct, tp, tmp, threshold, cands, counters + 0,
+                                                         CAND_CAP);
+            }
+            for (int o = 0; o < o_small; ++o) {
                 const int w = ow[o], h = oh[o];
                 if (w <= 2 * IMG_BORDER || h <= 2 * IMG_BORDER || L < 1) continue;
                 extrema_kernel<<<dim3((w - 2 * IMG_BORDER + 255) / 256, h - 2 * IMG_BORDER, L), 256, 0, st>>>(
