@@ -175,7 +175,9 @@ void pattern(const std::vector<char>& adj, FactorPlan& P) {
 }
 
 // latency model of one launch sequence (us): per launch its slowest task
-constexpr double LAT_LAUNCH = 6.0, LAT_LOAD = 2.5, LAT_UPD = 6.5, LAT_INV = 12.0;
+// latency model of one level launch (us, r02q kernels): a task's sources run in parallel parts
+// (chol_level_split), so a task costs one source update, plus the hand-off when it has several
+constexpr double LAT_LAUNCH = 6.0, LAT_LOAD = 2.5, LAT_UPD = 6.5, LAT_INV = 12.0, LAT_HANDOFF = 3.0;
 
 void schedule(FactorPlan& P) {
     const int T = P.T;
@@ -215,7 +217,7 @@ void schedule(FactorPlan& P) {
             t.s1 = (int)P.src.size();
             const bool iv = a == b && P.level[a] == l + 1;
             (iv ? inv : rest).push_back(t);
-            worst = std::max(worst, LAT_LOAD + LAT_UPD * (double)kv.second.size() + (iv ? LAT_INV : 0.0));
+            worst = std::max(worst, LAT_LOAD + LAT_UPD + (kv.second.size() > 1 ? LAT_HANDOFF : 0.0) + (iv ? LAT_INV : 0.0));
         }
         P.ninv.push_back((int)inv.size());
         P.tasks.insert(P.tasks.end(), inv.begin(), inv.end());
