@@ -378,12 +378,13 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
 #pragma unroll
             for (int i = 0; i < JS / 2; ++i) pre[i] = s2[i];
         }
-        if (l < Bn.p1 - Bn.p0) {
-            const int p = Bn.p0 + l;
+        if ((l >> 2) < Bn.p1 - Bn.p0) {   // 4 lanes per point (the point phase)
+            const int p = Bn.p0 + (l >> 2);
             pre_a0 = pt_start[p] - Bn.o0;
             pre_a1 = pt_start[p + 1] - Bn.o0;
+            if ((l & 3) == 0)
 #pragma unroll
-            for (int i = 0; i < 3; ++i) { pre_cs[i] = colsq[3 * (size_t)p + i]; pre_sp[i] = scale[3 * (size_t)p + i]; }
+                for (int i = 0; i < 3; ++i) { pre_cs[i] = colsq[3 * (size_t)p + i]; pre_sp[i] = scale[3 * (size_t)p + i]; }
         }
     };
     prefetch(w);
@@ -441,20 +442,38 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         BA_STAMP(3);
         double Mq[6] = {0, 0, 0, 0, 0, 0}, tq[3] = {0, 0, 0};
-        if (l < np) {   // lane = point
-            const int a0 = pre_a0, a1 = pre_a1;
-            double E6[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0}, V[3 * K];
+        // point phase, 4 lanes per point (lane = 4 q + k): lane k sums quantities [k QS, (k + 1) QS) of
+        // the point's observation partials (each sum in observation order, as one lane summed them all),
+        // into the point's pw slot; after a wave barrier lane k = 0 reads them back and does the rest
+        constexpr int NQ = 9 + 3 * K, QS = (NQ + 3) / 4;
+        const int qp = l >> 2, qk = l & 3;
+        if (qp < np) {
+            double sq[QS];
 #pragma unroll
-            for (int i = 0; i < 3 * K; ++i) V[i] = 0.0;
-            for (int b = a0; b < a1; ++b) {
-                const double* pt = part + b * NPF;
+            for (int j = 0; j < QS; ++j) sq[j] = 0.0;
+            for (int b = pre_a0; b < pre_a1; ++b) {
+                const double* pt = part + b * NPF + qk * QS;
 #pragma unroll
-                for (int i = 0; i < 6; ++i) E6[i] += pt[i];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) g[i] += pt[6 + i];
-#pragma unroll
-                for (int i = 0; i < 3 * K; ++i) V[i] += pt[9 + i];
+                for (int j = 0; j < QS; ++j)
+                    if (qk * QS + j < NQ) sq[j] += pt[j];
             }
+            double* ps = pw + qp * PD + qk * QS;
+#pragma unroll
+            for (int j = 0; j < QS; ++j)
+                if (qk * QS + j < NQ) ps[j] = sq[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (qp < np && qk == 0) {
+            double* pq = pw + qp * PD;
+            double E6[6], g[3], V[3 * K];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) E6[i] = pq[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) g[i] = pq[6 + i];
+#pragma unroll
+            for (int i = 0; i < 3 * K; ++i) V[i] = pq[9 + i];
             double E[9] = {E6[0], E6[1], E6[2], E6[1], E6[3], E6[4], E6[2], E6[4], E6[5]};
 #pragma unroll
             for (int i = 0; i < 3; ++i) E[4 * i] += dsq(pre_cs[i], pre_sp[i], dmin, dmax, radius);
@@ -469,7 +488,6 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
 #pragma unroll
                 for (int j = 0; j <= k; ++j) tq[k] += mlo(Mq, k, j) * g[j];
             }
-            double* pq = pw + l * PD;
 #pragma unroll
             for (int i = 0; i < 6; ++i) pq[i] = Mq[i];
 #pragma unroll
@@ -485,8 +503,8 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
                 }
         }
         prefetch(bi + 4);
-        if (l < np) {   // after the prefetch: a later wait for its loads does not wait for these stores
-            const int p = B.p0 + l;
+        if (qp < np && qk == 0) {   // after the prefetch: a later wait for its loads does not wait for these stores
+            const int p = B.p0 + qp;
 #pragma unroll
             for (int i = 0; i < 6; ++i) plt[9 * (size_t)p + i] = Mq[i];
 #pragma unroll
