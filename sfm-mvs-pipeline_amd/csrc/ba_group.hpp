@@ -521,6 +521,9 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (ov && q >= r0 && q < r0 + 4) {   // Z_o = (M_q W_o)^T: the observation's 6 camera rows of H_q
                 const double* pq = pw + q * PD;
+                double Mr[6];   // in registers: the h stores below may alias pw for the compiler
+#pragma unroll
+                for (int i = 0; i < 6; ++i) Mr[i] = pq[i];
                 double* h = Hb + (q - r0) * HS + 3 * (6 * lc);
 #pragma unroll
                 for (int d = 0; d < 6; ++d)
@@ -528,7 +531,7 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
                     for (int k = 0; k < 3; ++k) {
                         double z = 0.0;
 #pragma unroll
-                        for (int j = 0; j <= k; ++j) z += mlo(pq, k, j) * W[j][d];
+                        for (int j = 0; j <= k; ++j) z += mlo(Mr, k, j) * W[j][d];
                         h[3 * d + k] = z;
                     }
             }
@@ -579,6 +582,14 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
     double* Rb = gl + dp * (dp + 1);
     for (int ww = 0; ww < 4; ++ww) {
         if (w == ww) {
+            double prev[NTT][4];   // all reads first: the stores may alias them for the compiler
+#pragma unroll
+            for (int I = 0, t = 0; I < NT; ++I)
+#pragma unroll
+                for (int Jt = I; Jt < NT; ++Jt, ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        prev[t][r] = (ww == 0 || Jt >= nt) ? 0.0 : Sb[(16 * I + kk + 4 * r) * (dp + 1) + 16 * Jt + m16];
 #pragma unroll
             for (int I = 0, t = 0; I < NT; ++I)
 #pragma unroll
@@ -587,8 +598,7 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int row = 16 * I + kk + 4 * r, col = 16 * Jt + m16;
-                        double* d = Sb + row * (dp + 1) + col;
-                        *d = ww == 0 ? acc[t][r] : *d + acc[t][r];
+                        Sb[row * (dp + 1) + col] = ww == 0 ? acc[t][r] : prev[t][r] + acc[t][r];
                     }
                 }
             if (l < 16)
