@@ -30,11 +30,22 @@ namespace sfmx {
 namespace ba {
 
 constexpr int LDT = NB + 2;   // LDS row stride (doubles): 16-B aligned rows
+constexpr long long DAG_TIMEOUT = 2000000;   // bound of every in-launch wait: 20 ms of the 100 MHz wall clock
 // global-address-space words for in-launch hand-offs (agent-scope atomics / sc1 accesses)
 typedef __attribute__((address_space(1))) int g_i32;
 typedef __attribute__((address_space(1))) unsigned long long g_u64;
 __device__ __forceinline__ double ld_wt(const double* p) {   // sc1 load (bypasses this CU's L1)
     return __longlong_as_double((long long)__hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_wt(double* p, double v) {   // sc1 (write-through) store
+    __hip_atomic_store((g_u64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16-B sc1 loads through a buffer resource (aux 16 = sc1 on gfx950; word 3 as for every gfx9 raw buffer)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const double* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ double2 ld_wt2(__amdgpu_buffer_rsrc_t rs, size_t elem) {
+    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(elem * 8), 0, 16));
 }
 // 64x64 fp64 tiles on the matrix cores (layout: f64x4 / trow / tcol in ba_kernels.hpp).  Wave w of a
 // 256-thread block owns the row strip 16w..16w+15 and four 16x16 column tiles.
@@ -45,6 +56,28 @@ __device__ __forceinline__ void tile_load(double (*dst)[LDT], const double* __re
         const int e = q * 512 + 2 * threadIdx.x;
         *reinterpret_cast<double2*>(&dst[e / NB][e % NB]) = *reinterpret_cast<const double2*>(src + (size_t)(e / NB) * ld + e % NB);
     }
+}
+// the same from bytes another workgroup of this launch stored write-through (sc1 loads; elements of rs)
+__device__ __forceinline__ void tile_load_wt(double (*dst)[LDT], __amdgpu_buffer_rsrc_t rs, size_t src, int ld) {
+#pragma unroll
+    for (int q = 0; q < NB * NB / 512; ++q) {
+        const int e = q * 512 + 2 * threadIdx.x;
+        *reinterpret_cast<double2*>(&dst[e / NB][e % NB]) = ld_wt2(rs, src + (size_t)(e / NB) * ld + e % NB);
+    }
+}
+__device__ __forceinline__ void tile_regs_wt(f64x4 (&t)[4], const double* __restrict__ src, int ld) {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[c][r] = ld_wt(&src[(size_t)(16 * w + trow(r)) * ld + 16 * c + tcol()]);
+}
+__device__ __forceinline__ void tile_store_wt(const f64x4 (&t)[4], double* __restrict__ dst, int ld) {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st_wt(&dst[(size_t)(16 * w + trow(r)) * ld + 16 * c + tcol()], t[c][r]);
 }
 __device__ __forceinline__ void tile_regs(f64x4 (&t)[4], const double* __restrict__ src, int ld) {
     const int w = threadIdx.x >> 6;
@@ -179,8 +212,9 @@ __device__ __forceinline__ void inner_inverse16(const double* __restrict__ Pc, i
 // The inverse of the (final) diagonal tile k held in registers t (MFMA layout) -> W_k (global)
 // and buf (LDS); then w_k = W_k y_k for the RW right-hand sides (y: LDS [NB][RW] -> R rows of
 // tile k) and the panel's intrinsics Schur terms contrib_k[i][j] = sum_r y[r][i] w[r][j] (i < RW-1).
-// buf: 64 x LDT doubles of LDS workspace; wv: NB x RW doubles of LDS.
-template <int RW>
+// buf: 64 x LDT doubles of LDS workspace; wv: NB x RW doubles of LDS.  WT: W_k and the R rows are
+// stored write-through (sc1), for readers in the same launch (chol_factor).
+template <int RW, bool WT = false>
 __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __restrict__ Wk,
                                                double* __restrict__ R, const double* __restrict__ y,
                                                double* __restrict__ wv, double* __restrict__ contrib,
@@ -237,7 +271,8 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __r
         for (int r = 0; r < 4; ++r) {
             const int i = 16 * w + trow(r), j = 16 * c + tcol();
             buf[i][j] = -t[c][r];
-            Wk[i * NB + j] = -t[c][r];
+            if (WT) st_wt(&Wk[i * NB + j], -t[c][r]);
+            else Wk[i * NB + j] = -t[c][r];
         }
     __syncthreads();
     CHOL_STAMP(20);
@@ -269,7 +304,11 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __r
         }
         if (cp == 0) {
 #pragma unroll
-            for (int q = 0; q < RW; ++q) { wv[i * RW + q] = acc[q]; R[(size_t)(k0 + i) * RW + q] = acc[q]; }
+            for (int q = 0; q < RW; ++q) {
+                wv[i * RW + q] = acc[q];
+                if (WT) st_wt(&R[(size_t)(k0 + i) * RW + q], acc[q]);
+                else R[(size_t)(k0 + i) * RW + q] = acc[q];
+            }
         }
     }
     CHOL_STAMP(22);
@@ -521,6 +560,188 @@ void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, 
     }
 }
 
+// The whole factorization in ONE launch (SFMX_BA_DAG, default on): the leaves and every level's
+// parts of chol_level_split, with in-launch hand-offs instead of launch boundaries.  A workgroup
+// takes a ticket (atomic counter) and the item at that ticket; items are listed leaves first, then
+// level by level, so everything an item waits for holds an earlier ticket and is running or done
+// (no residency or dispatch-order assumption).  Every lower tile (a, b) has a version word
+// tver[a (a + 1) / 2 + b] = the number of its tasks (leaf inverse included) that have finished.
+// A part waits (one lane, sc1 polls, bounded) until A_ak, A_bk and the diagonal tile (k, k) (W_k,
+// the R rows of k) carry their final versions, and -- for a one-source task, or as the last arriver
+// -- until A_ab carries the version before this task; then it runs chol_level_split's body.  Every
+// byte another item reads in this launch (lower tiles, W_k, R rows) is stored write-through (sc1)
+// and loaded only with sc1 loads; the storing workgroup drains (vmcnt(0)), meets at a barrier and
+// one lane adds to the tile's version (MI355X_MICROARCH.md, inter-workgroup visibility, sc1 form
+// row 1).  The upper tiles (k, a) and contrib are read only by chol_backsolve (the next launch).
+// items[i] = {task | leaf panel, source index (-1: leaf), slot, n | inverting << 16};
+// need[i] = {version of A_ak, of A_bk, of (k, k), of A_ab before this task}.
+// ctr = [ticket, finished, tver[T (T + 1) / 2]], zero at launch; the last workgroup re-zeroes it.
+// Same operations in the same order as the level launches: bit-identical.
+__device__ __forceinline__ int tver_id(int a, int b) { return a * (a + 1) / 2 + b; }
+
+template <int RW>
+__global__ __launch_bounds__(256)
+void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
+                 const int4* __restrict__ items, const int4* __restrict__ need, const int* __restrict__ src,
+                 double* __restrict__ W, double* __restrict__ contrib, int* __restrict__ fail, double* pbuf,
+                 int* tctr, int* ctr, int nitems, int nver) {
+    if (step_gated(fail + 1)) return;
+    __shared__ CholLds<RW> sm;
+    __shared__ int sh[2];
+    constexpr int TPO = (256 / (NB * RW)) > 0 ? 256 / (NB * RW) : 1;
+    constexpr int OPT = (NB * RW) / (256 / TPO);
+    constexpr int SLOT = (16 + OPT) * 256;
+    const int tid = threadIdx.x, w = tid >> 6;
+    int* tver = ctr + 2;
+    if (tid == 0) sh[0] = __hip_atomic_fetch_add((g_i32*)ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int tk = sh[0];
+    const int4 it = items[tk], nd = need[tk];
+    // one lane waits until tile `id` carries version `v` (bounded: a timeout sets fail bit 2 and the
+    // item runs on, so every counter still advances and the launch drains)
+    auto wait_ver = [&](int id, int v, long long t0) {
+        while (__hip_atomic_load((g_i32*)&tver[id], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > DAG_TIMEOUT) { atomicOr(fail, 2); return; }
+        }
+    };
+    const __amdgpu_buffer_rsrc_t rS = wt_rsrc(S), rW = wt_rsrc(W);
+    int done_id = -1;   // the tile whose version this item advances (-1: none)
+    if (it.y < 0) {     // leaf: diagonal tile k, untouched by any update
+        const int k = it.x, k0 = k * NB;
+        f64x4 t[4];
+        tile_regs(t, S + (size_t)k0 * npad + k0, npad);
+        for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = R[(size_t)k0 * RW + e];
+        __syncthreads();
+        chol_diag_tile<RW, true>(t, k, W + (size_t)k * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a);
+        done_id = tver_id(k, k);
+    } else {
+        const int4 task = tasks[it.x];
+        const int a = task.x, b = task.y, a0 = a * NB, b0 = b * NB, n = it.w & 0xffff, j = it.y - task.z;
+        const bool diag = (a == b), inv = (it.w >> 16) != 0;
+        const int k = src[it.y], k0 = k * NB;
+        double* dst = S + (size_t)a0 * npad + b0;
+        // A_ak, A_bk (and A_ab of a one-source task) are final before W_k is (the inverse of (k, k) ends
+        // the previous level's chain): they load while that inverse still runs
+        long long t0 = 0;
+        if (tid == 0) {
+            t0 = wall_clock64();
+            wait_ver(tver_id(a, k), nd.x, t0);
+            if (!diag) wait_ver(tver_id(b, k), nd.y, t0);
+            if (n == 1) wait_ver(tver_id(a, b), nd.w, t0);
+        }
+        __syncthreads();
+        f64x4 t[4];
+        if (n == 1) {
+            tile_regs_wt(t, dst, npad);
+            if (diag)
+                for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = ld_wt(&R[(size_t)a0 * RW + e]);
+        }
+        tile_load_wt(sm.a, rS, (size_t)a0 * npad + k0, npad);                   // A_ak
+        if (!diag) tile_load_wt(sm.n, rS, (size_t)b0 * npad + k0, npad);        // A_bk
+        if (tid == 0) wait_ver(tver_id(k, k), nd.z, t0);
+        __syncthreads();
+        tile_load_wt(sm.m, rW, (size_t)k * NB * NB, NB);                        // W_k
+        if (diag)
+            for (int e = tid; e < NB * RW; e += 256) sm.rk[e] = ld_wt(&R[(size_t)k0 * RW + e]);   // w_k
+        __syncthreads();
+        f64x4 g[4];
+        mfma_nn(sm.a, sm.m, g);   // G = A_ak W_k
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sm.m[16 * w + trow(r)][16 * c + tcol()] = g[c][r];
+        __syncthreads();
+        f64x4 upd[4];
+        mfma_nt(sm.m, diag ? sm.a : sm.n, upd);   // G X^T
+        double ys[OPT];
+        if (diag) {
+            const int pp = tid % TPO;
+#pragma unroll
+            for (int u = 0; u < OPT; ++u) {
+                const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+                double sum = 0.0;
+                for (int c = pp; c < NB; c += TPO) sum = fma(sm.a[i][c], sm.rk[c * RW + q], sum);
+                if (TPO >= 2) sum += __shfl_xor(sum, 1);
+                if (TPO >= 4) sum += __shfl_xor(sum, 2);
+                ys[u] = sum;
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) S[(size_t)(k0 + 16 * c + tcol()) * npad + a0 + 16 * w + trow(r)] = g[c][r];
+        }
+        bool fin = true;
+        if (n > 1) {   // publish this part; the last arriver finishes the task
+            part_store<RW>(pbuf + (size_t)it.z * SLOT, upd, ys, diag ? OPT : 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                const bool last = __hip_atomic_fetch_add((g_i32*)&tctr[it.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
+                if (last) {
+                    tctr[it.x] = 0;   // nobody else touches it in this launch
+                    wait_ver(tver_id(a, b), nd.w, wall_clock64());
+                }
+                sh[1] = last;
+            }
+            __syncthreads();
+            fin = sh[1] != 0;
+            if (fin) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below
+                tile_regs_wt(t, dst, npad);
+                if (diag)
+                    for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = ld_wt(&R[(size_t)a0 * RW + e]);
+                __syncthreads();
+                const double* base = pbuf + (size_t)(it.z - j) * SLOT;   // slot of source 0 of this task
+                for (int jj = 0; jj < n; ++jj) {
+                    const double* sl = base + (size_t)jj * SLOT;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) t[c][r] -= (jj == j) ? upd[c][r] : ld_wt(&sl[(4 * c + r) * 256 + tid]);
+                    if (diag) {
+#pragma unroll
+                        for (int u = 0; u < OPT; ++u) {
+                            const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+                            const double y = (jj == j) ? ys[u] : ld_wt(&sl[(16 + u) * 256 + tid]);
+                            if (tid % TPO == 0) sm.ra[i * RW + q] -= y;
+                        }
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) t[c] -= upd[c];
+            if (diag) {
+#pragma unroll
+                for (int u = 0; u < OPT; ++u) {
+                    const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+                    if (tid % TPO == 0) sm.ra[i * RW + q] -= ys[u];
+                }
+            }
+        }
+        if (fin) {
+            __syncthreads();
+            if (diag && inv) {
+                chol_diag_tile<RW, true>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n);
+            } else {
+                tile_store_wt(t, dst, npad);
+                if (diag)
+                    for (int e = tid; e < NB * RW; e += 256) st_wt(&R[(size_t)a0 * RW + e], sm.ra[e]);
+            }
+            done_id = tver_id(a, b);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains before the version add
+    __syncthreads();
+    if (tid == 0) {
+        if (done_id >= 0) __hip_atomic_fetch_add((g_i32*)&tver[done_id], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_fetch_add((g_i32*)&ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nitems - 1)
+            for (int e = 0; e < nver + 2; ++e) __hip_atomic_store((g_i32*)&ctr[e], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // Cross-rank all-reduce of the reduced system, compacted: the structurally nonzero lower tiles of
 // S_cc (incl. the diagonal ones) + R | D | r_i, packed into one contiguous buffer and back.
 // One workgroup per tile; the tail block (blockIdx.x == ntiles) moves the rest.
@@ -605,7 +826,6 @@ __device__ __forceinline__ void intr_solve(const double* __restrict__ Dm, const 
 // the solve reports an internal error.  ctr = [ticket, finished, zdone[T]] is zero at launch; the
 // last workgroup to finish zeroes it for the next launch (nobody polls by then).
 constexpr int BS_PF = 4;                   // ancestor tiles prefetched into LDS per workgroup
-constexpr long long DAG_TIMEOUT = 2000000; // 20 ms
 
 template <int RW>
 __global__ __launch_bounds__(256)

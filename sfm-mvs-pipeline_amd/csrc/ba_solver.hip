@@ -91,10 +91,13 @@ struct sfmx_ba_ctx {
     Buf camrow, padrows, rowmap, leaves, ptasks, psrc, lvl_start, lvl_panels, bs_start, bs_k, Wt, contrib, xi,
         nztiles, packbuf,          // all-reduce of the nonzero lower tiles only (multi-rank)
         border, zbuf, dagctr,      // chol_backsolve: panels root first, z, [ticket, finished, zdone[T]]
-        parts, pbuf, lctr;         // chol_level_split: (task, source) parts per level, product slots, arrivals
+        parts, pbuf, lctr,         // chol_level_split: (task, source) parts per level, product slots, arrivals
+        ditems, dneed, dctr;       // chol_factor: leaves + every level's parts, their version needs, [ticket, finished, tver]
     bool back_dag = true;          // SFMX_BA_BACK=0: the r02 chol_intr + one-workgroup chol_back
     bool split = true;             // SFMX_BA_SPLIT=0: chol_level (a task's sources in one workgroup)
     std::vector<int> part_start;   // per level: parts[part_start[l] .. part_start[l + 1])
+    bool dag = true;               // SFMX_BA_DAG=0: one launch per level (chol_leaves + chol_level[_split])
+    int n_ditems = 0, n_ver = 0;
     int n_nztiles = 0;
     size_t sr_count = 0;         // doubles of SR = S_cc | R | D | r_i
     // state (the *2 buffers hold the candidate's linearization until the step is accepted)
@@ -119,7 +122,7 @@ struct sfmx_ba_ctx {
     ~sfmx_ba_ctx() {
         Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
-                      &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
+                      &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
                       &failf, &partA, &lmst, &camscr};
         int prev = 0;
@@ -275,6 +278,12 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
     double* Dm = R + (size_t)npad * RW;
     double* ri = Dm + (RW - 1) * (RW - 1);
     int* fl = c->failf.as<int>();
+    if (c->dag && c->split) {
+        hipLaunchKernelGGL(chol_factor<RW>, dim3((unsigned)c->n_ditems), dim3(256), 0, c->st, S, npad, R,
+                           c->ptasks.as<int4>(), c->ditems.as<int4>(), c->dneed.as<int4>(), c->psrc.as<int>(),
+                           c->Wt.as<double>(), c->contrib.as<double>(), fl, c->pbuf.as<double>(), c->lctr.as<int>(),
+                           c->dctr.as<int>(), c->n_ditems, c->n_ver);
+    } else {
     hipLaunchKernelGGL(chol_leaves<RW>, dim3((unsigned)pl.leaves.size()), dim3(256), 0, c->st, S, npad, R,
                        c->leaves.as<int>(), c->Wt.as<double>(), c->contrib.as<double>(), fl);
     for (int l = 0; l < pl.height; ++l) {
@@ -288,6 +297,7 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
             hipLaunchKernelGGL(chol_level<RW>, dim3(nt), dim3(256), 0, c->st, S, npad, R, c->ptasks.as<int4>() + t0,
                                c->psrc.as<int>(), pl.ninv[l], c->Wt.as<double>(), c->contrib.as<double>(), fl);
         }
+    }
     }
     if (c->back_dag) {
         hipLaunchKernelGGL(chol_backsolve<RW>, dim3(c->T), dim3(256), 0, c->st, S, npad, R, Dm, ri,
@@ -489,6 +499,48 @@ int ensure_plan(sfmx_ba_ctx* c) {
             c->part_start.push_back((int)parts.size());
         }
         RC(upload(c->parts, parts, st));
+        // chol_factor: the leaves, then every level's parts in the same order, product slots unique over
+        // the launch; need = the versions (finished tasks, leaf inverse included) of A_ak, A_bk, (k, k)
+        // and of A_ab before the task.  A plan whose source tile is not final at its use (never built
+        // by ba_plan) keeps the per-level launches.
+        const int T = pl.T, nver = T * (T + 1) / 2;
+        auto vid = [](int a, int b) { return a * (a + 1) / 2 + b; };
+        std::vector<int> vfin(nver, 0), vcnt(nver, 0);
+        for (int k : pl.leaves) vfin[vid(k, k)] += 1;
+        for (const auto& t : pl.tasks) vfin[vid(t.a, t.b)] += 1;
+        std::vector<int4> items, need;
+        for (int k : pl.leaves) {
+            items.push_back(make_int4(k, -1, 0, 0));
+            need.push_back(make_int4(0, 0, 0, 0));
+            vcnt[vid(k, k)] = 1;
+        }
+        int dslots = 0;
+        bool dag_ok = (size_t)c->sr_count * 8 < (1u << 31) && (size_t)T * NB * NB * 8 < (1u << 31);   // 32-bit buffer offsets
+        for (int l = 0; l < pl.height; ++l) {
+            for (int t = pl.task_start[l]; t < pl.task_start[l + 1]; ++t) {
+                const auto& tk = pl.tasks[t];
+                const int n = tk.s1 - tk.s0, inv = (t - pl.task_start[l]) < pl.ninv[l];
+                for (int j = 0; j < n; ++j) {
+                    const int k = pl.src[tk.s0 + j];
+                    dag_ok = dag_ok && k < tk.b && vcnt[vid(tk.a, k)] == vfin[vid(tk.a, k)] &&
+                             vcnt[vid(tk.b, k)] == vfin[vid(tk.b, k)] && vcnt[vid(k, k)] == vfin[vid(k, k)];
+                    items.push_back(make_int4(t, tk.s0 + j, n == 1 ? 0 : dslots + j, n | inv << 16));
+                    need.push_back(make_int4(vfin[vid(tk.a, k)], tk.a == tk.b ? 0 : vfin[vid(tk.b, k)], vfin[vid(k, k)],
+                                             vcnt[vid(tk.a, tk.b)]));
+                }
+                if (n > 1) dslots += n;
+            }
+            for (int t = pl.task_start[l]; t < pl.task_start[l + 1]; ++t) vcnt[vid(pl.tasks[t].a, pl.tasks[t].b)] += 1;
+        }
+        c->n_ditems = (int)items.size();
+        c->n_ver = nver;
+        RC(upload(c->ditems, items, st));
+        RC(upload(c->dneed, need, st));
+        RC(c->dctr.alloc(sizeof(int) * (size_t)((nver + 2 + 3) / 4 * 4)));
+        HIPCHK(hipMemsetAsync(c->dctr.p, 0, c->dctr.bytes, st));
+        const char* ed = std::getenv("SFMX_BA_DAG");
+        c->dag = dag_ok && !(ed && ed[0] == '0');
+        max_slots = std::max(max_slots, dslots);
         const int tpo = std::max(1, 256 / (NB * RW)), opt = NB * RW / (256 / tpo);
         RC(c->pbuf.alloc(sizeof(double) * (size_t)max_slots * (16 + opt) * 256));
         RC(c->lctr.alloc(sizeof(int) * (size_t)((pl.tasks.size() + 4) / 4 * 4)));

@@ -133,17 +133,20 @@ def test_split_level_and_backsolve_bit_identical_to_r02_forms(order, monkeypatch
     """chol_backsolve (one workgroup per panel, ticket-ordered flag hand-offs in one launch) gives
     the same bits as the r02 chol_intr + one-workgroup chol_back, on several elimination trees
     (natural order = a chain of panels; nested dissection with leaves of 1 / 4 tiles); a ring of
-    200 cameras gives a tree of height > 1 with multi-ancestor panels."""
+    200 cameras gives a tree of height > 1 with multi-ancestor panels.  The split per-level
+    launches and chol_factor (the whole factorization in one launch, version-counted tile
+    hand-offs) give the same bits as the per-level chol_level launches."""
     p = synth.ba_problem(200, 6000, seed=29)
     monkeypatch.setenv("SFMX_BA_ORDER", order)
     res = {}
-    for back, split in (("0", "0"), ("1", "0"), ("1", "1")):
+    for back, split, dag in (("0", "0", "0"), ("1", "0", "0"), ("1", "1", "0"), ("1", "1", "1")):
         monkeypatch.setenv("SFMX_BA_BACK", back)
         monkeypatch.setenv("SFMX_BA_SPLIT", split)   # chol_level_split: a task's sources over workgroups
+        monkeypatch.setenv("SFMX_BA_DAG", dag)       # chol_factor: leaves + every level in one launch
         P, sm, tr = gpu_solve(p, max_num_iterations=4)
-        res[back + split] = (P.points.copy(), P.poses.copy(), sm["final_cost"], tr.copy())
-    a = res["00"]
-    for key in ("10", "11"):
+        res[back + split + dag] = (P.points.copy(), P.poses.copy(), sm["final_cost"], tr.copy())
+    a = res["000"]
+    for key in ("100", "110", "111"):
         b = res[key]
         assert a[2] == b[2], key
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[3], b[3]), key
