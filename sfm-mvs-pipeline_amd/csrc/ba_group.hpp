@@ -789,7 +789,9 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
     double* jer = G + GROWS * NF;                      // [GCH][8]
     short* olc = reinterpret_cast<short*>(jer + GCH * 8);
     const Grp Gp = grp[blockIdx.x];
-    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, m16 = l & 15, kq = l >> 4;
+    // w through readfirstlane: the per-camera row ranges (lcrow of camera w + 4i) become scalar, so
+    // the Gram loop's bounds and its tail conditions are scalar branches, not exec-masked lanes
+    const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, m16 = l & 15, kq = l >> 4;
     const double* pts = xp;
     const double* poses = xp + 3 * (size_t)P;
     const double* intr = poses + 6 * (size_t)C;
