@@ -218,7 +218,7 @@ template <int RW, bool WT = false>
 __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __restrict__ Wk,
                                                double* __restrict__ R, const double* __restrict__ y,
                                                double* __restrict__ wv, double* __restrict__ contrib,
-                                               int* __restrict__ fail, double (*buf)[LDT]) {
+                                               int* __restrict__ fail, double (*buf)[LDT], int* wver = nullptr) {
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, m = l & 15, kq = l >> 4, k0 = k * NB;
     double* ws = &buf[0][0];
     double* Pc = ws;                       // [64][LDP]  column panel A_:B
@@ -274,7 +274,9 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __r
             if (WT) st_wt(&Wk[i * NB + j], -t[c][r]);
             else Wk[i * NB + j] = -t[c][r];
         }
+    if (WT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W_k drained before its version add
     __syncthreads();
+    if (wver && tid == 0) __hip_atomic_fetch_add((g_i32*)wver, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // W_k ready
     CHOL_STAMP(20);
     {   // w = W y: 4 threads per row i, each over 16 columns c for all RW right-hand sides (16-B LDS
         // reads), the 4 partial sums combined by two shuffles in a fixed order
@@ -566,15 +568,18 @@ void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, 
 // level by level, so everything an item waits for holds an earlier ticket and is running or done
 // (no residency or dispatch-order assumption).  Every lower tile (a, b) has a version word
 // tver[a (a + 1) / 2 + b] = the number of its tasks (leaf inverse included) that have finished.
-// A part waits (one lane, sc1 polls, bounded) until A_ak, A_bk and the diagonal tile (k, k) (W_k,
-// the R rows of k) carry their final versions, and -- for a one-source task, or as the last arriver
-// -- until A_ab carries the version before this task; then it runs chol_level_split's body.  Every
+// An inverse adds 2 to its diagonal tile's version: once W_k is stored, and at its end (the R rows
+// of k, contrib).  A part waits (one lane, sc1 polls, bounded) until A_ak and A_bk carry their final
+// versions (and, for a one-source task, A_ab the version before this task) and loads them, then
+// until W_k is stored, and -- a diagonal part, after its tile product -- until the R rows of k are;
+// the last arriver of a multi-source task waits for A_ab's version before this task.  The arithmetic
+// is chol_level_split's body.  Every
 // byte another item reads in this launch (lower tiles, W_k, R rows) is stored write-through (sc1)
 // and loaded only with sc1 loads; the storing workgroup drains (vmcnt(0)), meets at a barrier and
 // one lane adds to the tile's version (MI355X_MICROARCH.md, inter-workgroup visibility, sc1 form
 // row 1).  The upper tiles (k, a) and contrib are read only by chol_backsolve (the next launch).
 // items[i] = {task | leaf panel, source index (-1: leaf), slot, n | inverting << 16};
-// need[i] = {version of A_ak, of A_bk, of (k, k), of A_ab before this task}.
+// need[i] = {version of A_ak, of A_bk, of (k, k) (final; W_k stored at one less), of A_ab before this task}.
 // ctr = [ticket, finished, tver[T (T + 1) / 2]], zero at launch; the last workgroup re-zeroes it.
 // Same operations in the same order as the level launches: bit-identical.
 __device__ __forceinline__ int tver_id(int a, int b) { return a * (a + 1) / 2 + b; }
@@ -613,7 +618,7 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
         tile_regs(t, S + (size_t)k0 * npad + k0, npad);
         for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = R[(size_t)k0 * RW + e];
         __syncthreads();
-        chol_diag_tile<RW, true>(t, k, W + (size_t)k * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a);
+        chol_diag_tile<RW, true>(t, k, W + (size_t)k * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a, &tver[tver_id(k, k)]);
         done_id = tver_id(k, k);
     } else {
         const int4 task = tasks[it.x];
@@ -639,11 +644,9 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
         }
         tile_load_wt(sm.a, rS, (size_t)a0 * npad + k0, npad);                   // A_ak
         if (!diag) tile_load_wt(sm.n, rS, (size_t)b0 * npad + k0, npad);        // A_bk
-        if (tid == 0) wait_ver(tver_id(k, k), nd.z, t0);
+        if (tid == 0) wait_ver(tver_id(k, k), nd.z - 1, t0);   // W_k stored (its R rows may still be in flight)
         __syncthreads();
         tile_load_wt(sm.m, rW, (size_t)k * NB * NB, NB);                        // W_k
-        if (diag)
-            for (int e = tid; e < NB * RW; e += 256) sm.rk[e] = ld_wt(&R[(size_t)k0 * RW + e]);   // w_k
         __syncthreads();
         f64x4 g[4];
         mfma_nn(sm.a, sm.m, g);   // G = A_ak W_k
@@ -657,6 +660,10 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
         mfma_nt(sm.m, diag ? sm.a : sm.n, upd);   // G X^T
         double ys[OPT];
         if (diag) {
+            if (tid == 0) wait_ver(tver_id(k, k), nd.z, t0);   // w_k (the R rows of k) stored
+            __syncthreads();
+            for (int e = tid; e < NB * RW; e += 256) sm.rk[e] = ld_wt(&R[(size_t)k0 * RW + e]);   // w_k
+            __syncthreads();
             const int pp = tid % TPO;
 #pragma unroll
             for (int u = 0; u < OPT; ++u) {
@@ -724,7 +731,8 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
         if (fin) {
             __syncthreads();
             if (diag && inv) {
-                chol_diag_tile<RW, true>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n);
+                chol_diag_tile<RW, true>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n,
+                                         &tver[tver_id(a, a)]);
             } else {
                 tile_store_wt(t, dst, npad);
                 if (diag)

@@ -506,13 +506,16 @@ int ensure_plan(sfmx_ba_ctx* c) {
         const int T = pl.T, nver = T * (T + 1) / 2;
         auto vid = [](int a, int b) { return a * (a + 1) / 2 + b; };
         std::vector<int> vfin(nver, 0), vcnt(nver, 0);
-        for (int k : pl.leaves) vfin[vid(k, k)] += 1;
-        for (const auto& t : pl.tasks) vfin[vid(t.a, t.b)] += 1;
+        // an inverse (leaf or inverting task) adds 2: once when W_k is stored, once at its end (R rows)
+        for (int k : pl.leaves) vfin[vid(k, k)] += 2;
+        for (int l = 0; l < pl.height; ++l)
+            for (int t = pl.task_start[l]; t < pl.task_start[l + 1]; ++t)
+                vfin[vid(pl.tasks[t].a, pl.tasks[t].b)] += 1 + ((t - pl.task_start[l]) < pl.ninv[l] ? 1 : 0);
         std::vector<int4> items, need;
         for (int k : pl.leaves) {
             items.push_back(make_int4(k, -1, 0, 0));
             need.push_back(make_int4(0, 0, 0, 0));
-            vcnt[vid(k, k)] = 1;
+            vcnt[vid(k, k)] = 2;
         }
         int dslots = 0;
         bool dag_ok = (size_t)c->sr_count * 8 < (1u << 31) && (size_t)T * NB * NB * 8 < (1u << 31);   // 32-bit buffer offsets
@@ -530,7 +533,8 @@ int ensure_plan(sfmx_ba_ctx* c) {
                 }
                 if (n > 1) dslots += n;
             }
-            for (int t = pl.task_start[l]; t < pl.task_start[l + 1]; ++t) vcnt[vid(pl.tasks[t].a, pl.tasks[t].b)] += 1;
+            for (int t = pl.task_start[l]; t < pl.task_start[l + 1]; ++t)
+                vcnt[vid(pl.tasks[t].a, pl.tasks[t].b)] += 1 + ((t - pl.task_start[l]) < pl.ninv[l] ? 1 : 0);
         }
         c->n_ditems = (int)items.size();
         c->n_ver = nver;
