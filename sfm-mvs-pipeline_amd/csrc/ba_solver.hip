@@ -19,6 +19,7 @@
 #include "ba_group.hpp"
 #include "ba_chol.hpp"
 #include "ba_plan.hpp"
+#include "diag.hpp"
 
 #include <algorithm>
 #include <chrono>
@@ -436,7 +437,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
             for (int b = a + 1; b < C; ++b, ++e) adj[(size_t)a * C + b] = adj[(size_t)b * C + a] = h[e] > 0.0;
     }
     int mode = -1;
-    if (const char* e = std::getenv("SFMX_BA_ORDER")) {
+    if (const char* e = SFMX_DIAG_ENV("SFMX_BA_ORDER")) {
         const std::string m(e);
         mode = m == "natural" ? 0 : m == "nd" ? 1 : m == "nd1" ? 2 : m == "nd2" ? 3 : m == "nd4" ? 4 : -1;
     }
@@ -478,9 +479,9 @@ int ensure_plan(sfmx_ba_ctx* c) {
         RC(c->zbuf.alloc(sizeof(double) * (size_t)pl.npad));
         RC(c->dagctr.alloc(sizeof(int) * (size_t)((pl.T + 2 + 3) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->dagctr.p, 0, c->dagctr.bytes, st));
-        const char* e = std::getenv("SFMX_BA_BACK");
+        const char* e = SFMX_DIAG_ENV("SFMX_BA_BACK");
         c->back_dag = !(e && e[0] == '0');
-        e = std::getenv("SFMX_BA_SPEC");   // opt-in: measured no faster (host turnaround)
+        e = SFMX_DIAG_ENV("SFMX_BA_SPEC");   // opt-in: measured no faster (host turnaround)
         c->spec = e && e[0] == '1';
     }
     {   // chol_level_split: per level, the parts of the inverting tasks first (the plan's task order)
@@ -542,14 +543,14 @@ int ensure_plan(sfmx_ba_ctx* c) {
         RC(upload(c->dneed, need, st));
         RC(c->dctr.alloc(sizeof(int) * (size_t)((nver + 2 + 3) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->dctr.p, 0, c->dctr.bytes, st));
-        const char* ed = std::getenv("SFMX_BA_DAG");
+        const char* ed = SFMX_DIAG_ENV("SFMX_BA_DAG");
         c->dag = dag_ok && !(ed && ed[0] == '0');
         max_slots = std::max(max_slots, dslots);
         const int tpo = std::max(1, 256 / (NB * RW)), opt = NB * RW / (256 / tpo);
         RC(c->pbuf.alloc(sizeof(double) * (size_t)max_slots * (16 + opt) * 256));
         RC(c->lctr.alloc(sizeof(int) * (size_t)((pl.tasks.size() + 4) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->lctr.p, 0, c->lctr.bytes, st));
-        const char* e = std::getenv("SFMX_BA_SPLIT");
+        const char* e = SFMX_DIAG_ENV("SFMX_BA_SPLIT");
         c->split = !(e && e[0] == '0');
     }
     hipError_t e = hipSuccess;

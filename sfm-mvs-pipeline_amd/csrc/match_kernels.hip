@@ -41,6 +41,7 @@
 #include <climits>
 #include <cstdlib>
 #include "match_common.hpp"
+#include "diag.hpp"
 
 namespace sfmx {
 
@@ -896,13 +897,15 @@ void sift_settle_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restr
     }
 }
 
-// Timing probe only (wrong results): flips the sign bit of every int8 operand
-// byte, i.e. the unshifted byte a instead of a - 128, to measure how operand
+#ifdef SFMX_DIAG
+// Timing probe only (wrong results; diagnostic build only): flips the sign bit of every int8
+// operand byte, i.e. the unshifted byte a instead of a - 128, to measure how operand
 // bit patterns move the clock the chip holds under the screening MFMAs.
 __global__ void probe_xor80_kernel(uint32_t* __restrict__ p, int64_t n_words) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n_words) p[i] ^= 0x80808080u;
 }
+#endif
 hipError_t launch_prep_l2_batch(const PrepImg* tab, int n, int max_rows_pad, int8_t* desc8, int32_t* norm,
                                 int32_t* keyc, int32_t* keyc2, int32_t* flags, hipStream_t st) {
     if (n == 0 || max_rows_pad == 0) return hipSuccess;
@@ -925,12 +928,14 @@ hipError_t launch_publish_flags(const int32_t* flags, int n, int32_t* dst, unsig
     publish_flags_kernel<<<1, 256, 0, st>>>(flags, n, dst, seq, v);
     return hipGetLastError();
 }
+#ifdef SFMX_DIAG
 hipError_t launch_probe_xor80(int8_t* p, int64_t bytes, hipStream_t st) {
     const int64_t n = bytes / 4;
     if (n == 0) return hipSuccess;
     probe_xor80_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(reinterpret_cast<uint32_t*>(p), n);
     return hipGetLastError();
 }
+#endif
 
 // Pass-2 work list: ceil(qcount[p] / 512) items per pair, pairs in the host's
 // order (sorted by train image, so XCD-contiguous items share train rows).
@@ -1913,13 +1918,15 @@ hipError_t launch_prep_hamming(const uint8_t* src, int rows, int cols, int rows_
 }
 
 // Kernel variants (queries per block = QT * WAVES * 32, must divide ROW_ALIGN).
-// Selected by sift_variant(); SFMX_SIFT_VARIANT overrides (tuning only).
-int sift_variant() {   // read per run: tests switch paths within one process
-    const char* e = getenv("SFMX_SIFT_VARIANT");
+// The product library runs only the default two-pass forms (variant 0, subset pass 2);
+// the diagnostic build (diag.hpp) selects the others with SFMX_SIFT_VARIANT / SFMX_SIFT_P2,
+// read per run so tests switch paths within one process.
+int sift_variant() {
+    const char* e = SFMX_DIAG_ENV("SFMX_SIFT_VARIANT");
     return e ? atoi(e) : 0;
 }
-int pass2_variant() {   // SFMX_SIFT_P2 (tuning / tests only): 10 = subset pass 2 (default), else the full-row
-    const char* e = getenv("SFMX_SIFT_P2");   // GATHER pass 2 with that item size (0 / 2 = 128 queries)
+int pass2_variant() {   // 10 = subset pass 2 (default), else the full-row GATHER pass 2
+    const char* e = SFMX_DIAG_ENV("SFMX_SIFT_P2");   // with that item size (0 / 2 = 128 queries)
     return e ? atoi(e) : 10;
 }
 int sift_block_queries(int v) { return v == 2 || v == 4 || v == 23 ? 256 : 512; }
@@ -1951,6 +1958,11 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
                                                         slow_count, ratio);
             return hipGetLastError();
         }
+#ifndef SFMX_DIAG
+        return hipErrorInvalidValue;   // the product path always has the subset buffers
+    }
+    return hipErrorInvalidValue;
+#else
 #define SCREEN_LAUNCH(QT, W, MINW, ST) \
     sift_screen_kernel<QT, W, MINW, ST><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc2, out_idx, \
                                                                    out_dist, qlist, qcount, ratio)
@@ -2017,6 +2029,7 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
     default: SIFT_LAUNCH(4, 4, 2, 128, false);   // 100: the r01d single-pass default (9.57-9.67 ms on config 2)
     }
     return hipGetLastError();
+#endif   // SFMX_DIAG
 }
 hipError_t launch_sift_slow(const int2* slow_list, const int32_t* slow_count, const PairDev* pairs,
                             const ImgDev* imgs, const int8_t* desc8, const int32_t* norm, int32_t* out_idx,
@@ -2036,11 +2049,11 @@ hipError_t launch_orb_knn2(const WorkItem* work, int n_work, const PairDev* pair
     orb_knn2_kernel<2><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc8, out_idx, out_dist, ratio);
     return hipGetLastError();
 }
-// ORB kernel selection: 0 (default) = FP4 MFMA path on 128-byte +-1 rows,
-// 1 = VALU xor/popcount path on 32-byte rows, 2.. = FP4 MFMA tiling variants
-// (tuning only).  SFMX_ORB_VARIANT overrides.
+// ORB kernel selection: 0 (default, the only form in the product library) = FP4 MFMA path on
+// 128-byte +-1 rows; in the diagnostic build SFMX_ORB_VARIANT selects 1 = VALU xor/popcount path
+// on 32-byte rows, 2.. = FP4 MFMA tiling variants (tuning only).
 int orb_variant() {   // read per run, as sift_variant(): tests switch variants within one process
-    const char* e = getenv("SFMX_ORB_VARIANT");
+    const char* e = SFMX_DIAG_ENV("SFMX_ORB_VARIANT");
     return e ? atoi(e) : 0;
 }
 hipError_t launch_prep_hamming_fp4(const uint8_t* src, int rows, int cols, int rows_pad, uint8_t* dst, int32_t* keyc,
@@ -2070,6 +2083,11 @@ hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pair
             orb_settle_kernel<<<n_pairs, 256, 0, st>>>(pairs, imgs, qlist, qcount, top2, out_idx, out_dist, ratio);
             return hipGetLastError();
         }
+#ifndef SFMX_DIAG
+        return hipErrorInvalidValue;   // the product path always has the subset buffers
+    }
+    return hipErrorInvalidValue;
+#else
         orb_screen16_kernel<8, 4, 2, 64><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx, out_dist,
                                                                   qlist, qcount, ratio);
         if (ev_screen) {
@@ -2117,6 +2135,7 @@ hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pair
 #undef ORB_LAUNCH
 #undef ORB16_LAUNCH
     return hipGetLastError();
+#endif   // SFMX_DIAG
 }
 hipError_t launch_assemble(const PairDev* pairs, int n_pairs, const ImgDev* imgs, const int32_t* out_idx,
                            const float* out_dist, int distinct, int min_count, int max_nt, int64_t* counts,

@@ -13,6 +13,7 @@
 // No CPU fallback: every numeric step runs in the HIP kernels of
 // match_kernels.hip; a missing/unsupported device returns SFMX_EDEVICE.
 #include <hip/hip_runtime.h>
+#include "diag.hpp"
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
@@ -312,8 +313,10 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
             }
         }
     }
-    if (norm == SFMX_NORM_L2 && getenv("SFMX_PROBE_XOR80"))   // timing probe only (wrong results)
+#ifdef SFMX_DIAG
+    if (norm == SFMX_NORM_L2 && SFMX_DIAG_ENV("SFMX_PROBE_XOR80"))   // timing probe only (wrong results)
         HIPCHK(launch_probe_xor80(m->desc8.as<int8_t>(), (int64_t)row * SIFT_DIM, st));
+#endif
     if (n > 0) {
         if ((rc = m->stage_imgs.ensure(sizeof(ImgDev) * n))) return rc;
         std::memcpy(m->stage_imgs.p, m->imgs.data(), sizeof(ImgDev) * n);

@@ -28,6 +28,7 @@
 // of the order the lanes add them.  Result: keypoints and descriptors
 // bit-identical to the oracle.
 #include <hip/hip_runtime.h>
+#include "diag.hpp"
 #include <algorithm>
 #include <atomic>
 #include <cfloat>
@@ -362,11 +363,11 @@ void small_octaves_kernel(const Layer* __restrict__ gp, const Layer* __restrict_
 }
 
 inline bool small_octaves_on() {   // SFMX_SIFT_SMALL=0: every octave as per-octave launches (A/B, tests)
-    const char* e = std::getenv("SFMX_SIFT_SMALL");
+    const char* e = SFMX_DIAG_ENV("SFMX_SIFT_SMALL");
     return !(e && e[0] == '0');
 }
 inline int small_px() {   // SFMX_SIFT_SMALL_PX: the largest octave (pixels) the fused launch takes (tuning)
-    const char* e = std::getenv("SFMX_SIFT_SMALL_PX");
+    const char* e = SFMX_DIAG_ENV("SFMX_SIFT_SMALL_PX");
     return e ? std::atoi(e) : SMALL_PX;
 }
 

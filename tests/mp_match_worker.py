@@ -3,7 +3,10 @@ pair-sharded matching across ranks (torchrun, every rank on this one GPU, gloo),
 as bench.py / SURVEY §8e shard it: each rank matches its contiguous slice of the
 pair list (sfmx.shard.shard_pairs), no collective on the data path.  Rank 0
 gathers the per-rank DMatch lists (outside the data path), runs the same job on
-one rank and prints one JSON line saying whether the merged lists are byte-equal."""
+one rank and prints one JSON line saying whether the merged lists are byte-equal.
+An optional third argument S (> 0) also checks every S-th pair of the merged
+lists against oracle.match_pairs (test infrastructure: the CPU checker), so the
+high image indices and large row offsets of a full C3 job are oracle-pinned."""
 import json
 import os
 import sys
@@ -35,6 +38,7 @@ def main():
     import sfmx
     from sfmx import shard, synth
     kind, n_img = sys.argv[1], int(sys.argv[2])
+    stride = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     if kind == "sift":
         imgs = synth.sift_images(n_img, 8192)
         pairs = sfmx.pairs_unordered(n_img)
@@ -57,9 +61,19 @@ def main():
         for p in parts:
             moff += [moff[-1] + x for x in p[3][1:]]
         one, ooff = match(imgs, pairs, norm)
-        print(json.dumps({"covered": bool(covered), "equal": merged == one.tobytes() and moff == ooff.tolist(),
-                          "matches": int(ooff[-1]), "pairs": int(len(pairs)),
-                          "per_rank_pairs": [p[1] - p[0] for p in parts]}), flush=True)
+        res = {"covered": bool(covered), "equal": merged == one.tobytes() and moff == ooff.tolist(),
+               "matches": int(ooff[-1]), "pairs": int(len(pairs)), "per_rank_pairs": [p[1] - p[0] for p in parts]}
+        if stride > 0:
+            from oracle import oracle
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+            sel = np.arange(0, len(pairs), stride)
+            exp, eoff = oracle.match_pairs(imgs, pairs[sel], sfmx.LOWE_RATIO, threads)
+            mb = np.frombuffer(merged, np.uint8).reshape(-1, 16)
+            bad = [int(i) for k, i in enumerate(sel)
+                   if mb[moff[i]:moff[i + 1]].tobytes() != exp[eoff[k]:eoff[k + 1]].tobytes()]
+            res.update(oracle_pairs=int(len(sel)), oracle_matches=int(eoff[-1]), oracle_bad=bad[:20],
+                       max_pair_index=int(sel[-1]))
+        print(json.dumps(res), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 

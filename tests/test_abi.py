@@ -155,3 +155,24 @@ def test_integration_adapter_is_the_compiled_one():
     adapter = body[body.index("// --- adapter begin ---\n") + 24: body.index("// --- adapter end ---")]
     assert adapter in open(os.path.join(REPO, "INTEGRATION.md")).read()
     assert os.path.exists(os.path.join(REPO, "tests", "cpp", "adapter_test")), "build() compiles tests/cpp/adapter_test"
+
+
+def test_product_library_reads_no_tuning_variables():
+    """a drop-in library whose output changes with a stray environment
+    variable is a hazard.  The kernel variants, timing probes and alternative factorization
+    forms live only in lib/libsfmx_diag.so (csrc/diag.hpp); the product library carries no
+    SFMX_* variable name and no getenv of its own."""
+    blob = open(_lib.LIB_PATH, "rb").read()
+    for var in (b"SFMX_PROBE_XOR80", b"SFMX_SIFT_VARIANT", b"SFMX_SIFT_P2", b"SFMX_ORB_VARIANT", b"SFMX_BA_ORDER",
+                b"SFMX_BA_BACK", b"SFMX_BA_SPLIT", b"SFMX_BA_DAG", b"SFMX_BA_SPEC", b"SFMX_SIFT_SMALL"):
+        assert var not in blob, var
+    names = set(re.findall(rb"SFMX_[A-Z0-9_]+", blob))
+    assert names <= {b"SFMX_CAM_SIMPLE", b"SFMX_NORM_L2", b"SFMX_NORM_HAMMING"}, names
+
+
+def test_diagnostic_library_exports_the_same_entry_points():
+    import diag
+    dl = diag.diag_lib()
+    for name in declared_functions():
+        assert hasattr(dl, name), name
+    assert b"SFMX_SIFT_VARIANT" in open(diag.DIAG_PATH, "rb").read()

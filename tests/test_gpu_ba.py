@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 from sfmx import ba, synth
+from diag import diagnostic
 
 pytestmark = pytest.mark.gpu
 COST_RTOL = 1e-5
@@ -129,7 +130,7 @@ def test_mixed_track_lengths_matches_oracle():
 
 
 @pytest.mark.parametrize("order", ["natural", "nd", "nd1", "nd4"])
-def test_split_level_and_backsolve_bit_identical_to_r02_forms(order, monkeypatch):
+def test_split_level_and_backsolve_bit_identical_to_r02_forms(order):
     """chol_backsolve (one workgroup per panel, ticket-ordered flag hand-offs in one launch) gives
     the same bits as the r02 chol_intr + one-workgroup chol_back, on several elimination trees
     (natural order = a chain of panels; nested dissection with leaves of 1 / 4 tiles); a ring of
@@ -137,13 +138,12 @@ def test_split_level_and_backsolve_bit_identical_to_r02_forms(order, monkeypatch
     launches and chol_factor (the whole factorization in one launch, version-counted tile
     hand-offs) give the same bits as the per-level chol_level launches."""
     p = synth.ba_problem(200, 6000, seed=29)
-    monkeypatch.setenv("SFMX_BA_ORDER", order)
     res = {}
     for back, split, dag in (("0", "0", "0"), ("1", "0", "0"), ("1", "1", "0"), ("1", "1", "1")):
-        monkeypatch.setenv("SFMX_BA_BACK", back)
-        monkeypatch.setenv("SFMX_BA_SPLIT", split)   # chol_level_split: a task's sources over workgroups
-        monkeypatch.setenv("SFMX_BA_DAG", dag)       # chol_factor: leaves + every level in one launch
-        P, sm, tr = gpu_solve(p, max_num_iterations=4)
+        # diagnostic library: SFMX_BA_SPLIT = chol_level_split (a task's sources over workgroups),
+        # SFMX_BA_DAG = chol_factor (leaves + every level in one launch)
+        with diagnostic(SFMX_BA_ORDER=order, SFMX_BA_BACK=back, SFMX_BA_SPLIT=split, SFMX_BA_DAG=dag):
+            P, sm, tr = gpu_solve(p, max_num_iterations=4)
         res[back + split + dag] = (P.points.copy(), P.poses.copy(), sm["final_cost"], tr.copy())
     a = res["000"]
     for key in ("100", "110", "111"):
@@ -166,15 +166,15 @@ def _hard_problem(seed):
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_speculative_lm_bit_identical_to_host_judged_lm(seed, monkeypatch):
+def test_speculative_lm_bit_identical_to_host_judged_lm(seed):
     """The device-judged LM (ba_decide; step s + 1 enqueued before step s is judged, skipped by the
     step gate after a rejection and enqueued again) gives the same bits as the host-judged loop,
     including rejected steps, the iteration limit and the accept/reject trace."""
     p = _hard_problem(seed)
     res = {}
     for spec in ("0", "1"):
-        monkeypatch.setenv("SFMX_BA_SPEC", spec)
-        P, sm, tr = gpu_solve(p, max_num_iterations=40)
+        with diagnostic(SFMX_BA_SPEC=spec):
+            P, sm, tr = gpu_solve(p, max_num_iterations=40)
         res[spec] = (P.points.copy(), P.poses.copy(), P.intr.copy(), sm, tr.copy())
     a, b = res["0"], res["1"]
     assert (a[4][:, 2] == 0).any(), "the problem must exercise rejected steps"

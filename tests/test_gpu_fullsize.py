@@ -5,7 +5,9 @@ bench measures.  The oracle runs with OpenMP on the box's host cores (tens of se
 
   C2  50 x 8192 SIFT, all 1225 unordered pairs: DMatch lists byte-equal to the oracle.
   C4  200 x 16384 ORB-256, grid seq 3 / rowLen 20 (881 pairs): byte-equal to the oracle.
-  C3  pair-sharded matching: 2 ranks (gloo, both on this GPU) merged == 1 rank, byte-equal.
+  C3  pair-sharded matching: 2 ranks (gloo, both on this GPU) merged == 1 rank, byte-equal;
+      at its full size (200 x 8192 SIFT, all 19 900 unordered pairs) plus a stride sample of
+      1 048 pairs spread over the whole list byte-equal to the oracle.
   C5  200 cams / 200k points / 1.2M obs BA: final cost within 1e-5 relative of the oracle,
       same termination, same accept/reject sequence.
 """
@@ -70,6 +72,22 @@ def test_pair_sharded_two_ranks_equal_one_rank(kind, n_img):
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     assert r["covered"] and r["equal"], r
     assert min(r["per_rank_pairs"]) > 0 and r["matches"] > 0
+
+
+@pytest.mark.timeout(900)
+def test_c3_full_size_sharded_equal_one_rank_and_oracle_sample():
+    """BASELINE config 3 at its size (UnorderedFeatureMatchingStrategy.cpp:32-40): 200 x 8192
+    SIFT, 19 900 pairs, pair-sharded over 2 ranks; merged == 1 rank, and every 19th pair
+    (1 048 pairs, up to pair 19 893 = images (197, 199)) byte-equal to oracle.match_pairs."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                          "--master-addr=127.0.0.1", "--master-port=29534", os.path.join(HERE, "mp_match_worker.py"),
+                          "sift", "200", "19"], capture_output=True, text=True, timeout=900, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert r["pairs"] == 19_900 and r["covered"] and r["equal"], r
+    assert r["oracle_pairs"] == 1048 and r["max_pair_index"] > 19_800, r
+    assert r["oracle_bad"] == [] and r["oracle_matches"] > 400_000, r
 
 
 def test_c5_full_ba_matches_oracle():

@@ -1,5 +1,6 @@
 """GPU parity: the HIP matcher (through the C ABI) against the golden fixtures
 and the oracle, bit-exact (queryIdx, trainIdx, imgIdx, distance bits, order)."""
+import contextlib
 import os
 
 import numpy as np
@@ -8,6 +9,7 @@ import pytest
 import sfmx
 from sfmx import _lib, synth
 import fixtures
+from diag import diagnostic
 
 pytestmark = pytest.mark.gpu
 
@@ -53,11 +55,8 @@ def test_golden(name):
         # The two-pass path settles these far queries in the screening pass; the
         # single-pass kernel (variant 100) sends every query whose best-2 reach
         # s >= 2^22 to the exact float-sqrt slow path.  Same matches either way.
-        os.environ["SFMX_SIFT_VARIANT"] = "100"
-        try:
+        with diagnostic(SFMX_SIFT_VARIANT="100"):
             m1, off1, _, stats1 = run(d["imgs"], d["pairs"], d["ratio"])
-        finally:
-            del os.environ["SFMX_SIFT_VARIANT"]
         assert_same(m1, off1, d["matches"], d["offsets"])
         assert stats1[0] == 250
 
@@ -100,12 +99,10 @@ def test_two_pass_variants_vs_oracle(variant, p2):
     rng = np.random.default_rng(58)
     imgs.append(rng.integers(0, 256, (900, 128)).astype(np.float32))
     pairs = sfmx.pairs_unordered(len(imgs))
-    os.environ["SFMX_SIFT_VARIANT"], os.environ["SFMX_SIFT_P2"] = variant, p2
-    try:
+    default = (variant, p2) == ("0", "10")   # the product library's form
+    with contextlib.nullcontext() if default else diagnostic(SFMX_SIFT_VARIANT=variant, SFMX_SIFT_P2=p2):
         m, off, _, stats = run(imgs, pairs)
         m2, off2, _, _ = run(imgs, pairs, ratio=0.95)
-    finally:
-        del os.environ["SFMX_SIFT_VARIANT"], os.environ["SFMX_SIFT_P2"]
     em, eoff = oracle.match_pairs(imgs, pairs)
     assert_same(m, off, em, eoff)
     em2, eoff2 = oracle.match_pairs(imgs, pairs, 0.95)
@@ -147,11 +144,8 @@ def test_orb_two_pass_ratios_vs_oracle(ratio, variant):
     base[2][100:140] = base[2][:40]
     imgs = [base[0], base[1][:900], base[2], base[3][:2]]
     pairs = sfmx.pairs_unordered(4)
-    os.environ["SFMX_ORB_VARIANT"] = variant
-    try:
+    with contextlib.nullcontext() if variant == "0" else diagnostic(SFMX_ORB_VARIANT=variant):
         m, off, _, _ = run(imgs, pairs, ratio=ratio)
-    finally:
-        del os.environ["SFMX_ORB_VARIANT"]
     em, eoff = oracle.match_pairs(imgs, pairs, ratio)
     assert_same(m, off, em, eoff)
 
@@ -270,8 +264,7 @@ SIFT_KATS = ["kat_sift_nt1_nt0", "kat_sift_ties", "kat_sift_ties_r15", "sift_sma
 def test_previously_failing_variants(env, variant):
     from oracle import oracle
     names = ORB_KATS if env == "SFMX_ORB_VARIANT" else SIFT_KATS
-    os.environ[env] = variant
-    try:
+    with diagnostic(**{env: variant}):
         for name in names:
             d = fixtures.load(name)
             m, off, _, _ = run(d["imgs"], d["pairs"], d["ratio"])
@@ -288,5 +281,3 @@ def test_previously_failing_variants(env, variant):
             m, off, _, _ = run(imgs, pairs, ratio)
             em, eoff = oracle.match_pairs(imgs, pairs, ratio)
             assert_same(m, off, em, eoff)
-    finally:
-        del os.environ[env]
