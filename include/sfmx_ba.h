@@ -13,10 +13,14 @@
  * The parameter-block layout is the reference's Ceres problem layout:
  *   point double[3] (CeresPCE::coordinates, BundleAdjustment.h:28-45),
  *   pose  double[6] = angle-axis + translation (CeresCameraShot::pose, :47-64),
- *   ONE intrinsics block double[k] shared by all shots (ICamera::ceresCameraParameters, ICamera.h:171):
+ *   one intrinsics block double[k] per camera (ICamera::ceresCameraParameters, ICamera.h:171;
+ *   BundleAdjustment.cpp:45-48 registers every scene camera, :81-89 binds each residual to
+ *   shot->getCamera()'s block):
  *     SIMPLE k=1 [f], SIMPLE_RADIAL k=3 [f,k1,k2], DISTORTION k=7 [f,cx,cy,k1,k2,p1,p2].
  * One residual block (2 residuals) per observation, squared loss, no
- * constant blocks (BundleAdjustment.cpp:83-89).
+ * constant blocks (BundleAdjustment.cpp:83-89).  A camera no residual references is not a
+ * parameter of the problem (Ceres only knows blocks that AddResidualBlock named): its values
+ * are left as they are.
  */
 #ifndef SFMX_BA_H
 #define SFMX_BA_H
@@ -32,16 +36,30 @@ enum { SFMX_CAM_SIMPLE = 1, SFMX_CAM_SIMPLE_RADIAL = 3, SFMX_CAM_DISTORTION = 7 
 enum { SFMX_BA_CONVERGENCE = 0, SFMX_BA_NO_CONVERGENCE = 1, SFMX_BA_FAILURE = 2 };
 
 typedef struct sfmx_ba_problem {
-    int32_t n_points, n_cams, n_obs, cam_model;   /* cam_model = SFMX_CAM_* */
+    int32_t n_points, n_cams, n_obs, cam_model;   /* cam_model = SFMX_CAM_* (n_intr == 0)     */
     double* points;                 /* 3*n_points, in/out                                      */
     double* poses;                  /* 6*n_cams (angle-axis rx,ry,rz, tx,ty,tz), in/out        */
-    double* intr;                   /* k, in/out (shared intrinsics block)                     */
+    double* intr;                   /* in/out: n_intr == 0: the one block of k = cam_model;
+                                       else the n_intr blocks back to back (block m starts at
+                                       the sum of the k of blocks 0 .. m-1)                    */
     const int32_t* obs_point;       /* n_obs                                                   */
-    const int32_t* obs_cam;         /* n_obs                                                   */
+    const int32_t* obs_cam;         /* n_obs: the pose (shot) of the observation               */
     const double* obs_xy;           /* 2*n_obs observed pixel (cv::Point2f promoted to double) */
-    double cx, cy;                  /* principal point, SIMPLE / SIMPLE_RADIAL only
+    double cx, cy;                  /* principal point, SIMPLE / SIMPLE_RADIAL only, n_intr == 0
                                        (per-residual constant, SimpleRadialCamera.cpp:118-124) */
+    /* Several cameras (scene.getCameras(), BundleAdjustment.cpp:45-48).  n_intr = 0 (a
+     * zero-initialised struct): every pose uses the single block above.  n_intr >= 1: */
+    int32_t n_intr;                 /* number of intrinsics blocks (cameras)                   */
+    int32_t _reserved;
+    const int32_t* intr_model;      /* n_intr: SFMX_CAM_* of each block (models may be mixed)  */
+    const int32_t* pose_intr;       /* n_cams: the block of each pose (shot->getCamera())      */
+    const double* intr_center;      /* 2*n_intr: (cx, cy) of each block, read for SIMPLE /
+                                       SIMPLE_RADIAL (ICamera::getCenter, ICamera.h:90)        */
 } sfmx_ba_problem;
+/* Capacity: the referenced blocks hold at most SFMX_BA_MAX_INTR parameters in total (e.g. one
+ * DISTORTION camera, two SIMPLE_RADIAL cameras, or seven SIMPLE ones); a larger problem fails
+ * with SFMX_ECAPACITY. */
+enum { SFMX_BA_MAX_INTR = 7 };
 
 typedef struct sfmx_ba_options {     /* defaults = CeresUtils::defaultOptions + Ceres 1.14 */
     int32_t max_num_iterations;              /* 5000 (CeresUtils.cpp:45)  */
@@ -116,7 +134,9 @@ int sfmx_ba_destroy(sfmx_ba_ctx* ctx);
 
 /* Residuals and Jacobian blocks (device-computed) of every observation at the
  * problem's current parameters: r[2*O], Je[6*O] (d r / d point, row-major 2x3),
- * Jc[12*O] (2x6 pose), Ji[2*k*O] (2xk intrinsics).  For the autodiff tests. */
+ * Jc[12*O] (2x6 pose), Ji[2*k*O] (2xk intrinsics; with n_intr >= 1, k = the length of the
+ * whole intr array and an observation's columns outside its camera's block are 0).  For the
+ * autodiff tests. */
 int sfmx_ba_jacobian(const sfmx_ba_problem* problem, int32_t device, double* r, double* Je, double* Jc,
                      double* Ji);
 

@@ -146,17 +146,35 @@ void eval_jet(const double* X, const double* pose, const double* intr, double ox
     }
 }
 
+// The problem the reference builds (BundleAdjustment.cpp:45-91): every shot's residuals use
+// ITS camera's intrinsics block (shot->getCamera(), :81-89), so per pose c: the camera's
+// model k_c, the first column of its block among the intrinsics parameters of x, and the
+// principal point the SIMPLE / SIMPLE_RADIAL functors capture (getCenter, :83 ->
+// SimpleRadialCamera.cpp:118-124).  x = [points 3P | poses 6C | intrinsics kt]: the blocks some
+// residual references, in camera order (Ceres knows only blocks AddResidualBlock named).
 struct Problem {
-    int P, C, O, model, k;
+    int P, C, O, kt;
     const int32_t* obs_point;
     const int32_t* obs_cam;
     const double* obs_xy;
-    double cx, cy;
+    std::vector<int> cmodel, coff;      // per pose
+    std::vector<double> ccx, ccy;       // per pose
+    std::vector<int> isrc;              // intrinsics column j of x <- caller intr[isrc[j]]
 };
+
+constexpr int KMAX = 7;   // Ji rows are stored KMAX wide per observation, the first k_c used
 
 struct Lin {   // linearisation at x: residuals + Jacobian blocks per observation
     std::vector<double> r, Je, Jc, Ji;
 };
+
+void residual_of(const Problem& pb, int c, const double* X, const double* ps, const double* intr, double ox, double oy,
+                 double* res) {
+    const double* in = intr + pb.coff[c];
+    if (pb.cmodel[c] == 1) residual<1>(X, ps, in, ox, oy, pb.ccx[c], pb.ccy[c], res);
+    else if (pb.cmodel[c] == 3) residual<3>(X, ps, in, ox, oy, pb.ccx[c], pb.ccy[c], res);
+    else residual<7>(X, ps, in, ox, oy, pb.ccx[c], pb.ccy[c], res);
+}
 
 double eval_cost(const Problem& pb, const double* x) {
     const double* pts = x;
@@ -166,12 +184,10 @@ double eval_cost(const Problem& pb, const double* x) {
     #pragma omp parallel for reduction(+ : cost) schedule(static)
     for (int o = 0; o < pb.O; ++o) {
         double res[2];
+        const int c = pb.obs_cam[o];
         const double* X = pts + 3 * (size_t)pb.obs_point[o];
-        const double* ps = poses + 6 * (size_t)pb.obs_cam[o];
-        const double ox = pb.obs_xy[2 * o], oy = pb.obs_xy[2 * o + 1];
-        if (pb.k == 1) residual<1>(X, ps, intr, ox, oy, pb.cx, pb.cy, res);
-        else if (pb.k == 3) residual<3>(X, ps, intr, ox, oy, pb.cx, pb.cy, res);
-        else residual<7>(X, ps, intr, ox, oy, pb.cx, pb.cy, res);
+        const double* ps = poses + 6 * (size_t)c;
+        residual_of(pb, c, X, ps, intr, pb.obs_xy[2 * o], pb.obs_xy[2 * o + 1], res);
         cost += res[0] * res[0] + res[1] * res[1];
     }
     return 0.5 * cost;
@@ -181,35 +197,42 @@ double linearize(const Problem& pb, const double* x, Lin& L) {
     const double* pts = x;
     const double* poses = x + 3 * (size_t)pb.P;
     const double* intr = poses + 6 * (size_t)pb.C;
-    const int k = pb.k;
-    L.r.resize(2 * (size_t)pb.O); L.Je.resize(6 * (size_t)pb.O); L.Jc.resize(12 * (size_t)pb.O); L.Ji.resize(2 * (size_t)k * pb.O);
+    L.r.resize(2 * (size_t)pb.O); L.Je.resize(6 * (size_t)pb.O); L.Jc.resize(12 * (size_t)pb.O);
+    L.Ji.assign(2 * (size_t)KMAX * pb.O, 0.0);
     double cost = 0;
     #pragma omp parallel for reduction(+ : cost) schedule(static)
     for (int o = 0; o < pb.O; ++o) {
+        const int c = pb.obs_cam[o];
         const double* X = pts + 3 * (size_t)pb.obs_point[o];
-        const double* ps = poses + 6 * (size_t)pb.obs_cam[o];
+        const double* ps = poses + 6 * (size_t)c;
+        const double* in = intr + pb.coff[c];
         double* r = &L.r[2 * (size_t)o];
         double* Je = &L.Je[6 * (size_t)o];
         double* Jc = &L.Jc[12 * (size_t)o];
-        double* Ji = &L.Ji[2 * (size_t)k * o];
+        double Jk[2 * KMAX];
         const double ox = pb.obs_xy[2 * o], oy = pb.obs_xy[2 * o + 1];
-        if (k == 1) eval_jet<1>(X, ps, intr, ox, oy, pb.cx, pb.cy, r, Je, Jc, Ji);
-        else if (k == 3) eval_jet<3>(X, ps, intr, ox, oy, pb.cx, pb.cy, r, Je, Jc, Ji);
-        else eval_jet<7>(X, ps, intr, ox, oy, pb.cx, pb.cy, r, Je, Jc, Ji);
+        const int k = pb.cmodel[c];
+        if (k == 1) eval_jet<1>(X, ps, in, ox, oy, pb.ccx[c], pb.ccy[c], r, Je, Jc, Jk);
+        else if (k == 3) eval_jet<3>(X, ps, in, ox, oy, pb.ccx[c], pb.ccy[c], r, Je, Jc, Jk);
+        else eval_jet<7>(X, ps, in, ox, oy, pb.ccx[c], pb.ccy[c], r, Je, Jc, Jk);
+        for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < k; ++i) L.Ji[2 * (size_t)KMAX * o + KMAX * j + i] = Jk[j * k + i];
         cost += r[0] * r[0] + r[1] * r[1];
     }
     return 0.5 * cost;
 }
+// the observation's intrinsics entry i (< k_c) of row j, and its column among the frame parameters
+inline double ji(const Lin& L, int o, int j, int i) { return L.Ji[2 * (size_t)KMAX * o + KMAX * j + i]; }
 
 // Column functionals of J (squared column norms or J^T r), parameter order
 // [points 3P | poses 6C | intrinsics k].  Deterministic: per-thread partials
 // reduced in thread order.
 void column_reduce(const Problem& pb, const Lin& L, const double* scale, bool squares, std::vector<double>& out) {
-    const int k = pb.k;
-    const size_t n = 3 * (size_t)pb.P + 6 * (size_t)pb.C + k;
+    const int kt = pb.kt;
+    const size_t n = 3 * (size_t)pb.P + 6 * (size_t)pb.C + kt;
     out.assign(n, 0.0);
     const int T = omp_get_max_threads();
-    std::vector<std::vector<double>> part(T, std::vector<double>(6 * (size_t)pb.C + k, 0.0));
+    std::vector<std::vector<double>> part(T, std::vector<double>(6 * (size_t)pb.C + kt, 0.0));
     #pragma omp parallel
     {
         std::vector<double>& my = part[omp_get_thread_num()];
@@ -228,9 +251,10 @@ void column_reduce(const Problem& pb, const Lin& L, const double* scale, bool sq
                     const double v = L.Jc[12 * (size_t)o + 6 * j + i] * (scale ? scale[3 * (size_t)pb.P + 6 * (size_t)c + i] : 1.0);
                     my[6 * (size_t)c + i] += squares ? v * v : v * w;
                 }
-                for (int i = 0; i < k; ++i) {
-                    const double v = L.Ji[2 * (size_t)k * o + k * j + i] * (scale ? scale[n - k + i] : 1.0);
-                    my[6 * (size_t)pb.C + i] += squares ? v * v : v * w;
+                for (int i = 0; i < pb.cmodel[c]; ++i) {
+                    const size_t col = 6 * (size_t)pb.C + pb.coff[c] + i;
+                    const double v = ji(L, o, j, i) * (scale ? scale[3 * (size_t)pb.P + col] : 1.0);
+                    my[col] += squares ? v * v : v * w;
                 }
             }
         }
@@ -326,8 +350,9 @@ bool inv3_spd(const double* A, double* Ai) {   // via Cholesky of a 3x3 SPD matr
 // J is the (column-scaled) Jacobian held in L, scaled by `scale`.
 bool schur_solve(const Problem& pb, const Lin& L, const double* scale, const double* D, const std::vector<int>& pt_start,
                  const std::vector<int>& pt_obs, double* x) {
-    const int P = pb.P, C = pb.C, k = pb.k;
-    const int nf = 6 * C + k, fb = 6 + k;
+    const int P = pb.P, C = pb.C;
+    const int nf = 6 * C + pb.kt, fb = 6 + KMAX;   // F / W / Y rows are fb wide, 6 + k_c of them used
+    auto gcol = [&](int c, int u) { return u < 6 ? 6 * c + u : 6 * C + pb.coff[c] + (u - 6); };
     const size_t ne = 3 * (size_t)P;
     std::vector<double> S((size_t)nf * nf, 0.0), rhs(nf, 0.0);
     const int T = omp_get_max_threads();
@@ -356,19 +381,19 @@ bool schur_solve(const Problem& pb, const Lin& L, const double* scale, const dou
                 double* F = &Fo[(size_t)a * 2 * fb];
                 for (int j = 0; j < 2; ++j) {
                     for (int i = 0; i < 6; ++i) F[j * fb + i] = L.Jc[12 * (size_t)o + 6 * j + i] * scale[ne + 6 * (size_t)c + i];
-                    for (int i = 0; i < k; ++i) F[j * fb + 6 + i] = L.Ji[2 * (size_t)k * o + k * j + i] * scale[ne + 6 * (size_t)C + i];
+                    for (int i = 0; i < pb.cmodel[c]; ++i) F[j * fb + 6 + i] = ji(L, o, j, i) * scale[ne + gcol(c, 6 + i)];
                 }
                 for (int aa = 0; aa < 3; ++aa) {
                     for (int bb = 0; bb < 3; ++bb) E[aa * 3 + bb] += je[aa] * je[bb] + je[3 + aa] * je[3 + bb];
                     g[aa] += je[aa] * r[0] + je[3 + aa] * r[1];
                 }
                 // C block + rhs_f: F^T F, F^T r
-                const int base[2] = {6 * c, 6 * C};
-                for (int u = 0; u < fb; ++u) {
-                    const int gu = u < 6 ? base[0] + u : base[1] + (u - 6);
+                const int fo = 6 + pb.cmodel[c];
+                for (int u = 0; u < fo; ++u) {
+                    const int gu = gcol(c, u);
                     rl[gu] += F[u] * r[0] + F[fb + u] * r[1];
-                    for (int v = 0; v < fb; ++v) {
-                        const int gv = v < 6 ? base[0] + v : base[1] + (v - 6);
+                    for (int v = 0; v < fo; ++v) {
+                        const int gv = gcol(c, v);
                         Sl[(size_t)gu * nf + gv] += F[u] * F[v] + F[fb + u] * F[fb + v];
                     }
                 }
@@ -383,35 +408,36 @@ bool schur_solve(const Problem& pb, const Lin& L, const double* scale, const dou
             Y.assign((size_t)m * 3 * fb, 0.0);
             for (int a = 0; a < m; ++a) {
                 const int o = pt_obs[o0 + a];
+                const int fo = 6 + pb.cmodel[pb.obs_cam[o]];
                 double je[6];
                 for (int j = 0; j < 2; ++j)
                     for (int i = 0; i < 3; ++i) je[j * 3 + i] = L.Je[6 * (size_t)o + 3 * j + i] * scale[3 * (size_t)p + i];
                 const double* F = &Fo[(size_t)a * 2 * fb];
                 double* Wa = &W[(size_t)a * 3 * fb];
                 for (int i = 0; i < 3; ++i)
-                    for (int u = 0; u < fb; ++u) Wa[i * fb + u] = je[i] * F[u] + je[3 + i] * F[fb + u];
+                    for (int u = 0; u < fo; ++u) Wa[i * fb + u] = je[i] * F[u] + je[3 + i] * F[fb + u];
                 double* Ya = &Y[(size_t)a * 3 * fb];
                 for (int i = 0; i < 3; ++i)
-                    for (int u = 0; u < fb; ++u)
+                    for (int u = 0; u < fo; ++u)
                         Ya[i * fb + u] = Ei[i * 3] * Wa[u] + Ei[i * 3 + 1] * Wa[fb + u] + Ei[i * 3 + 2] * Wa[2 * fb + u];
             }
             // S -= W_a^T Y_b ; rhs_f -= W_a^T Einv g
             double Eg[3];
             for (int i = 0; i < 3; ++i) Eg[i] = Ei[i * 3] * g[0] + Ei[i * 3 + 1] * g[1] + Ei[i * 3 + 2] * g[2];
             for (int a = 0; a < m; ++a) {
-                const int ca = pb.obs_cam[pt_obs[o0 + a]];
+                const int ca = pb.obs_cam[pt_obs[o0 + a]], fa = 6 + pb.cmodel[ca];
                 const double* Wa = &W[(size_t)a * 3 * fb];
-                for (int u = 0; u < fb; ++u) {
-                    const int gu = u < 6 ? 6 * ca + u : 6 * C + (u - 6);
+                for (int u = 0; u < fa; ++u) {
+                    const int gu = gcol(ca, u);
                     rl[gu] -= Wa[u] * Eg[0] + Wa[fb + u] * Eg[1] + Wa[2 * fb + u] * Eg[2];
                 }
                 for (int b = 0; b < m; ++b) {
-                    const int cb = pb.obs_cam[pt_obs[o0 + b]];
+                    const int cb = pb.obs_cam[pt_obs[o0 + b]], fbb = 6 + pb.cmodel[cb];
                     const double* Yb = &Y[(size_t)b * 3 * fb];
-                    for (int u = 0; u < fb; ++u) {
-                        const int gu = u < 6 ? 6 * ca + u : 6 * C + (u - 6);
-                        for (int v = 0; v < fb; ++v) {
-                            const int gv = v < 6 ? 6 * cb + v : 6 * C + (v - 6);
+                    for (int u = 0; u < fa; ++u) {
+                        const int gu = gcol(ca, u);
+                        for (int v = 0; v < fbb; ++v) {
+                            const int gv = gcol(cb, v);
                             Sl[(size_t)gu * nf + gv] -= Wa[u] * Yb[v] + Wa[fb + u] * Yb[fb + v] + Wa[2 * fb + u] * Yb[2 * fb + v];
                         }
                     }
@@ -441,16 +467,17 @@ bool schur_solve(const Problem& pb, const Lin& L, const double* scale, const dou
         double q[3] = {ge[3 * (size_t)p], ge[3 * (size_t)p + 1], ge[3 * (size_t)p + 2]};
         for (int a = pt_start[p]; a < pt_start[p + 1]; ++a) {
             const int o = pt_obs[a], c = pb.obs_cam[o];
+            const int kc = pb.cmodel[c];
             double je[6], F[2][16];
             for (int j = 0; j < 2; ++j) {
                 for (int i = 0; i < 3; ++i) je[j * 3 + i] = L.Je[6 * (size_t)o + 3 * j + i] * scale[3 * (size_t)p + i];
                 for (int i = 0; i < 6; ++i) F[j][i] = L.Jc[12 * (size_t)o + 6 * j + i] * scale[ne + 6 * (size_t)c + i];
-                for (int i = 0; i < k; ++i) F[j][6 + i] = L.Ji[2 * (size_t)k * o + k * j + i] * scale[ne + 6 * (size_t)C + i];
+                for (int i = 0; i < kc; ++i) F[j][6 + i] = ji(L, o, j, i) * scale[ne + gcol(c, 6 + i)];
             }
             double Fx[2] = {0, 0};
             for (int j = 0; j < 2; ++j) {
                 for (int i = 0; i < 6; ++i) Fx[j] += F[j][i] * xf[6 * c + i];
-                for (int i = 0; i < k; ++i) Fx[j] += F[j][6 + i] * xf[6 * C + i];
+                for (int i = 0; i < kc; ++i) Fx[j] += F[j][6 + i] * xf[gcol(c, 6 + i)];
             }
             for (int i = 0; i < 3; ++i) q[i] -= je[i] * Fx[0] + je[3 + i] * Fx[1];
         }
@@ -472,6 +499,8 @@ struct orc_ba_problem {
     double* points; double* poses; double* intr;
     const int32_t* obs_point; const int32_t* obs_cam; const double* obs_xy;
     double cx, cy;
+    int32_t n_intr, reserved;
+    const int32_t* intr_model; const int32_t* pose_intr; const double* intr_center;
 };
 struct orc_ba_options {
     int32_t max_num_iterations, max_num_consecutive_invalid_steps, jacobi_scaling, device;
@@ -488,28 +517,77 @@ struct orc_ba_summary {
 
 enum { TERM_CONVERGENCE = 0, TERM_NO_CONVERGENCE = 1, TERM_FAILURE = 2 };
 
+// The Ceres problem of the caller's arrays (BundleAdjustment.cpp:45-91): n_intr == 0 is the one
+// camera (cam_model, cx, cy) every pose uses.  Returns the length of the caller's intr array, or -1.
+int make_problem(const orc_ba_problem* in, Problem& pb) {
+    pb.P = in->n_points; pb.C = in->n_cams; pb.O = in->n_obs;
+    pb.obs_point = in->obs_point; pb.obs_cam = in->obs_cam; pb.obs_xy = in->obs_xy;
+    const int M = in->n_intr > 0 ? in->n_intr : 1;
+    std::vector<int> model(M), start(M + 1, 0), used(M, 0), first(M, -1);
+    std::vector<double> mcx(M), mcy(M);
+    for (int m = 0; m < M; ++m) {
+        model[m] = in->n_intr > 0 ? in->intr_model[m] : in->cam_model;
+        if (model[m] != 1 && model[m] != 3 && model[m] != 7) return -1;
+        mcx[m] = in->n_intr > 0 ? in->intr_center[2 * m] : in->cx;
+        mcy[m] = in->n_intr > 0 ? in->intr_center[2 * m + 1] : in->cy;
+        start[m + 1] = start[m] + model[m];
+    }
+    auto cam_of = [&](int c) { return in->n_intr > 0 ? in->pose_intr[c] : 0; };
+    for (int o = 0; o < pb.O; ++o) used[cam_of(pb.obs_cam[o])] = 1;
+    pb.kt = 0;
+    pb.isrc.clear();
+    for (int m = 0; m < M; ++m)
+        if (used[m]) {
+            first[m] = pb.kt;
+            for (int i = 0; i < model[m]; ++i) pb.isrc.push_back(start[m] + i);
+            pb.kt += model[m];
+        }
+    pb.cmodel.assign(pb.C, 1); pb.coff.assign(pb.C, 0); pb.ccx.assign(pb.C, 0.0); pb.ccy.assign(pb.C, 0.0);
+    for (int c = 0; c < pb.C; ++c) {
+        const int m = cam_of(c);
+        if (first[m] < 0) continue;   // a pose without observations is never evaluated
+        pb.cmodel[c] = model[m]; pb.coff[c] = first[m]; pb.ccx[c] = mcx[m]; pb.ccy[c] = mcy[m];
+    }
+    return start[M];
+}
+
+void load_x(const orc_ba_problem* in, const Problem& pb, std::vector<double>& x) {
+    const size_t ne = 3 * (size_t)pb.P;
+    x.assign(ne + 6 * (size_t)pb.C + pb.kt, 0.0);
+    std::memcpy(x.data(), in->points, sizeof(double) * ne);
+    std::memcpy(x.data() + ne, in->poses, sizeof(double) * 6 * pb.C);
+    for (int j = 0; j < pb.kt; ++j) x[ne + 6 * (size_t)pb.C + j] = in->intr[pb.isrc[j]];
+}
+
 double orc_ba_cost(const orc_ba_problem* in) {
-    Problem pb{in->n_points, in->n_cams, in->n_obs, in->cam_model, in->cam_model, in->obs_point, in->obs_cam, in->obs_xy, in->cx, in->cy};
-    std::vector<double> x(3 * (size_t)pb.P + 6 * (size_t)pb.C + pb.k);
-    std::memcpy(x.data(), in->points, sizeof(double) * 3 * pb.P);
-    std::memcpy(x.data() + 3 * (size_t)pb.P, in->poses, sizeof(double) * 6 * pb.C);
-    std::memcpy(x.data() + 3 * (size_t)pb.P + 6 * (size_t)pb.C, in->intr, sizeof(double) * pb.k);
+    Problem pb;
+    if (make_problem(in, pb) < 0) return -1.0;
+    std::vector<double> x;
+    load_x(in, pb, x);
     return eval_cost(pb, x.data());
 }
 
-// Residuals + Jacobian blocks of every observation (for the autodiff tests).
+// Residuals + Jacobian blocks of every observation (for the autodiff tests).  Ji rows are the
+// caller's intr layout (its whole length), the observation's camera block filled, the rest 0.
 int orc_ba_jacobian(const orc_ba_problem* in, double* r, double* Je, double* Jc, double* Ji) {
-    Problem pb{in->n_points, in->n_cams, in->n_obs, in->cam_model, in->cam_model, in->obs_point, in->obs_cam, in->obs_xy, in->cx, in->cy};
-    std::vector<double> x(3 * (size_t)pb.P + 6 * (size_t)pb.C + pb.k);
-    std::memcpy(x.data(), in->points, sizeof(double) * 3 * pb.P);
-    std::memcpy(x.data() + 3 * (size_t)pb.P, in->poses, sizeof(double) * 6 * pb.C);
-    std::memcpy(x.data() + 3 * (size_t)pb.P + 6 * (size_t)pb.C, in->intr, sizeof(double) * pb.k);
+    Problem pb;
+    const int kl = make_problem(in, pb);
+    if (kl < 0) return -1;
+    std::vector<double> x;
+    load_x(in, pb, x);
     Lin L;
     linearize(pb, x.data(), L);
     std::memcpy(r, L.r.data(), sizeof(double) * L.r.size());
     std::memcpy(Je, L.Je.data(), sizeof(double) * L.Je.size());
     std::memcpy(Jc, L.Jc.data(), sizeof(double) * L.Jc.size());
-    std::memcpy(Ji, L.Ji.data(), sizeof(double) * L.Ji.size());
+    for (int o = 0; o < pb.O; ++o) {
+        const int c = pb.obs_cam[o];
+        for (int j = 0; j < 2; ++j) {
+            double* row = Ji + 2 * (size_t)kl * o + (size_t)kl * j;
+            for (int i = 0; i < kl; ++i) row[i] = 0.0;
+            for (int i = 0; i < pb.cmodel[c]; ++i) row[pb.isrc[pb.coff[c] + i]] = ji(L, o, j, i);
+        }
+    }
     return 0;
 }
 
@@ -521,13 +599,11 @@ int orc_ba_solve(orc_ba_problem* in, const orc_ba_options* opt, orc_ba_summary* 
                  int nthreads) {
     if (nthreads > 0) omp_set_num_threads(nthreads);
     const auto t0 = std::chrono::steady_clock::now();
-    Problem pb{in->n_points, in->n_cams, in->n_obs, in->cam_model, in->cam_model, in->obs_point, in->obs_cam, in->obs_xy, in->cx, in->cy};
-    if (pb.k != 1 && pb.k != 3 && pb.k != 7) return -1;
-    const size_t ne = 3 * (size_t)pb.P, n = ne + 6 * (size_t)pb.C + pb.k;
-    std::vector<double> x(n), cand(n), delta(n), scale(n, 1.0), D(n), diag(n), step(n), g;
-    std::memcpy(x.data(), in->points, sizeof(double) * ne);
-    std::memcpy(x.data() + ne, in->poses, sizeof(double) * 6 * pb.C);
-    std::memcpy(x.data() + ne + 6 * (size_t)pb.C, in->intr, sizeof(double) * pb.k);
+    Problem pb;
+    if (make_problem(in, pb) < 0) return -1;
+    const size_t ne = 3 * (size_t)pb.P, n = ne + 6 * (size_t)pb.C + pb.kt;
+    std::vector<double> x, cand(n), delta(n), scale(n, 1.0), D(n), diag(n), step(n), g;
+    load_x(in, pb, x);
     // point -> observation CSR (observations are point-major in the reference, but do not rely on it)
     std::vector<int> pt_start(pb.P + 1, 0), pt_obs(pb.O);
     for (int o = 0; o < pb.O; ++o) pt_start[pb.obs_point[o] + 1]++;
@@ -573,15 +649,15 @@ int orc_ba_solve(orc_ba_problem* in, const orc_ba_options* opt, orc_ba_summary* 
             for (size_t i = 0; i < n; ++i) step[i] = -step[i];
             // model residuals J_s step (per observation)
             double acc = 0;
-            const int k = pb.k;
             #pragma omp parallel for reduction(+ : acc) schedule(static)
             for (int o = 0; o < pb.O; ++o) {
                 const int p = pb.obs_point[o], c = pb.obs_cam[o];
+                const size_t i0 = ne + 6 * (size_t)pb.C + pb.coff[c];
                 for (int j = 0; j < 2; ++j) {
                     double m = 0;
                     for (int i = 0; i < 3; ++i) m += L.Je[6 * (size_t)o + 3 * j + i] * scale[3 * (size_t)p + i] * step[3 * (size_t)p + i];
                     for (int i = 0; i < 6; ++i) m += L.Jc[12 * (size_t)o + 6 * j + i] * scale[ne + 6 * (size_t)c + i] * step[ne + 6 * (size_t)c + i];
-                    for (int i = 0; i < k; ++i) m += L.Ji[2 * (size_t)k * o + k * j + i] * scale[n - k + i] * step[n - k + i];
+                    for (int i = 0; i < pb.cmodel[c]; ++i) m += ji(L, o, j, i) * scale[i0 + i] * step[i0 + i];
                     acc += m * (L.r[2 * (size_t)o + j] + m / 2.0);
                 }
             }
@@ -623,7 +699,7 @@ int orc_ba_solve(orc_ba_problem* in, const orc_ba_options* opt, orc_ba_summary* 
     }
     std::memcpy(in->points, x.data(), sizeof(double) * ne);
     std::memcpy(in->poses, x.data() + ne, sizeof(double) * 6 * pb.C);
-    std::memcpy(in->intr, x.data() + ne + 6 * (size_t)pb.C, sizeof(double) * pb.k);
+    for (int j = 0; j < pb.kt; ++j) in->intr[pb.isrc[j]] = x[ne + 6 * (size_t)pb.C + j];   // unreferenced cameras untouched
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     sum->final_cost = cost;
     sum->num_successful_steps = succ;

@@ -544,7 +544,9 @@ class _BAProblem(C.Structure):
     _fields_ = [("n_points", C.c_int32), ("n_cams", C.c_int32), ("n_obs", C.c_int32), ("cam_model", C.c_int32),
                 ("points", C.c_void_p), ("poses", C.c_void_p), ("intr", C.c_void_p),
                 ("obs_point", C.c_void_p), ("obs_cam", C.c_void_p), ("obs_xy", C.c_void_p),
-                ("cx", C.c_double), ("cy", C.c_double)]
+                ("cx", C.c_double), ("cy", C.c_double),
+                ("n_intr", C.c_int32), ("_reserved", C.c_int32), ("intr_model", C.c_void_p),
+                ("pose_intr", C.c_void_p), ("intr_center", C.c_void_p)]
 
 
 class _BAOptions(C.Structure):
@@ -590,6 +592,14 @@ def _ba_struct(p: dict):
                    keep["points"].ctypes.data, keep["poses"].ctypes.data, keep["intr"].ctypes.data,
                    keep["obs_point"].ctypes.data, keep["obs_cam"].ctypes.data, keep["obs_xy"].ctypes.data,
                    float(p.get("cx", 0.0)), float(p.get("cy", 0.0)))
+    if p.get("intr_models") is not None:   # several cameras (BundleAdjustment.cpp:45-48, 81-89)
+        keep["intr_models"] = np.ascontiguousarray(p["intr_models"], np.int32).reshape(-1)
+        keep["pose_intr"] = np.ascontiguousarray(p["pose_intr"], np.int32).reshape(-1)
+        keep["centers"] = np.ascontiguousarray(p["centers"], np.float64).reshape(-1, 2)
+        s.n_intr = len(keep["intr_models"])
+        s.intr_model = keep["intr_models"].ctypes.data
+        s.pose_intr = keep["pose_intr"].ctypes.data
+        s.intr_center = keep["centers"].ctypes.data
     return s, keep
 
 
@@ -600,7 +610,7 @@ def ba_cost(p: dict) -> float:
 
 def ba_jacobian(p: dict):
     s, keep = _ba_struct(p)
-    O, k = len(keep["obs_point"]), int(p["cam_model"])
+    O, k = len(keep["obs_point"]), len(keep["intr"])
     r = np.zeros((O, 2)); Je = np.zeros((O, 2, 3)); Jc = np.zeros((O, 2, 6)); Ji = np.zeros((O, 2, k))
     lib.orc_ba_jacobian(C.byref(s), r.ctypes.data, Je.ctypes.data, Jc.ctypes.data, Ji.ctypes.data)
     return r, Je, Jc, Ji

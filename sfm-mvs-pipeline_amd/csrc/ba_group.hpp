@@ -773,14 +773,16 @@ __device__ __forceinline__ int field_of(int r, int c) {   // Gram entry (r <= c)
 // per-(camera, field) loop.
 // Dynamic LDS: G[max rows][NF] | jer[GCH][8] (je | r) | olc[GCH] (short).
 constexpr int GROWS = 2 * GCH + 3 * UMAX;   // feature rows of a chunk incl. per-camera padding
-template <int K>
+// MULTI: several cameras, each pose's block and principal point from (pim, pcc) (project_blk).
+template <int K, bool MULTI = false>
 __global__ __launch_bounds__(256, 2)
 void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const int* __restrict__ lcrow,
              const short* __restrict__ obs_lc, const short* __restrict__ obs_row, const int* __restrict__ obs_point,
              const int* __restrict__ obs_cam, const double* __restrict__ obs_xy, const int* __restrict__ pt_start,
              double cx, double cy, int P, int C, const double* __restrict__ xp, const double* __restrict__ jscale,
              double* __restrict__ J, double* __restrict__ colsq, double* __restrict__ grad,
-             double* __restrict__ gpart, double* __restrict__ gpl, const int* __restrict__ gate) {
+             double* __restrict__ gpart, double* __restrict__ gpl, const int* __restrict__ gate,
+             const int* __restrict__ pim, const double2* __restrict__ pcc) {
     if (step_gated(gate)) return;
     extern __shared__ __attribute__((aligned(16))) double gl[];
     constexpr int JS = jst(K), NCP = ncp(K), N = 9 + K, NF = nfeat(K);
@@ -843,9 +845,13 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
             for (int i = 0; i < 3; ++i) X[i] = jvar<N>(pts[3 * (size_t)p + i], i);
 #pragma unroll
             for (int i = 0; i < 6; ++i) ps[i] = jvar<N>(poses[6 * (size_t)cm + i], 3 + i);
+            if constexpr (MULTI) {
+                project_blk<K, N>(X, ps, intr, pim[cm], pcc[cm], ox, oy, res);
+            } else {
 #pragma unroll
-            for (int i = 0; i < K; ++i) in[i] = jvar<N>(intr[i], 9 + i);
-            project<K, N>(X, ps, in, ox, oy, cx, cy, res);
+                for (int i = 0; i < K; ++i) in[i] = jvar<N>(intr[i], 9 + i);
+                project<K, N>(X, ps, in, ox, oy, cx, cy, res);
+            }
             double rec[JS];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {

@@ -129,6 +129,39 @@ __device__ __forceinline__ void project(const DJet<N> X[3], const DJet<N> ps[6],
     }
 }
 
+// Several cameras (BundleAdjustment.cpp:81-89: each residual takes its shot's camera block):
+// the intrinsics columns of x are the border [0, K) holding every referenced block back to
+// back.  Per pose, pim = model | (first border column << 4) and pcc = the block's (cx, cy).
+// The observation's own block enters the jets at derivative slots 9 + off ..; every other
+// border column gets a zero derivative, so the J record's Ji row is the observation's block
+// scattered into K columns.  Only models that fit the border are instantiated.
+template <int K, int N>
+__device__ __forceinline__ void project_blk(const DJet<N> X[3], const DJet<N> ps[6], const double* __restrict__ intr,
+                                            int pim, double2 pcc, double ox, double oy, DJet<N> res[2]) {
+    const int model = pim & 15, off = pim >> 4;
+    if constexpr (K >= 7) {
+        if (model == 7) {
+            DJet<N> in[7];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) in[i] = N ? jvar<N>(intr[off + i], 9 + off + i) : jconst<N>(intr[off + i]);
+            project<7, N>(X, ps, in, ox, oy, pcc.x, pcc.y, res);
+            return;
+        }
+    }
+    if constexpr (K >= 3) {
+        if (model == 3) {
+            DJet<N> in[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) in[i] = N ? jvar<N>(intr[off + i], 9 + off + i) : jconst<N>(intr[off + i]);
+            project<3, N>(X, ps, in, ox, oy, pcc.x, pcc.y, res);
+            return;
+        }
+    }
+    DJet<N> in[1];
+    in[0] = N ? jvar<N>(intr[off], 9 + off) : jconst<N>(intr[off]);
+    project<1, N>(X, ps, in, ox, oy, pcc.x, pcc.y, res);
+}
+
 // ---- block reduction helper (256 threads, fixed order) -------------------
 __device__ __forceinline__ double block_sum(double v, double* sh) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -150,7 +183,7 @@ __global__ __launch_bounds__(256)
 void ba_linearize(int O, const int* __restrict__ obs_point, const int* __restrict__ obs_cam,
                   const double* __restrict__ obs_xy, double cx, double cy, const double* __restrict__ pts,
                   const double* __restrict__ poses, const double* __restrict__ intr, double* __restrict__ J,
-                  double* __restrict__ partial) {
+                  double* __restrict__ partial, const int* __restrict__ pim, const double2* __restrict__ pcc) {
     __shared__ double sh[8];
     const int o = blockIdx.x * blockDim.x + threadIdx.x;
     double c2 = 0.0;
@@ -164,9 +197,13 @@ void ba_linearize(int O, const int* __restrict__ obs_point, const int* __restric
             for (int i = 0; i < 3; ++i) X[i] = jvar<N>(pts[3 * (size_t)p + i], i);
 #pragma unroll
             for (int i = 0; i < 6; ++i) ps[i] = jvar<N>(poses[6 * (size_t)c + i], 3 + i);
+            if (pim) {
+                project_blk<K, N>(X, ps, intr, pim[c], pcc[c], ox, oy, res);
+            } else {
 #pragma unroll
-            for (int i = 0; i < K; ++i) in[i] = jvar<N>(intr[i], 9 + i);
-            project<K, N>(X, ps, in, ox, oy, cx, cy, res);
+                for (int i = 0; i < K; ++i) in[i] = jvar<N>(intr[i], 9 + i);
+                project<K, N>(X, ps, in, ox, oy, cx, cy, res);
+            }
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 J[(size_t)o * jst(K) + j] = res[j].a;
@@ -184,9 +221,13 @@ void ba_linearize(int O, const int* __restrict__ obs_point, const int* __restric
             for (int i = 0; i < 3; ++i) X[i].a = pts[3 * (size_t)p + i];
 #pragma unroll
             for (int i = 0; i < 6; ++i) ps[i].a = poses[6 * (size_t)c + i];
+            if (pim) {
+                project_blk<K, 0>(X, ps, intr, pim[c], pcc[c], ox, oy, res);
+            } else {
 #pragma unroll
-            for (int i = 0; i < K; ++i) in[i].a = intr[i];
-            project<K, 0>(X, ps, in, ox, oy, cx, cy, res);
+                for (int i = 0; i < K; ++i) in[i].a = intr[i];
+                project<K, 0>(X, ps, in, ox, oy, cx, cy, res);
+            }
             c2 = res[0].a * res[0].a + res[1].a * res[1].a;
         }
     }

@@ -76,6 +76,13 @@ struct sfmx_ba_ctx {
     sfmx_ba_options opt{};
     int P = 0, C = 0, O = 0, K = 0;
     double cx = 0, cy = 0;
+    // several cameras (sfmx_ba_problem.n_intr >= 1): border column j of x's intrinsics part holds the
+    // caller's intr[isrc[j]] (the referenced blocks back to back, then zero padding up to K, -1);
+    // per pose its block (pim = model | first column << 4) and principal point (pcc)
+    bool multi = false;
+    int n_intr = 0, intr_len = 0;   // caller's blocks and the length of its intr array
+    std::vector<int> isrc;
+    Buf pim, pcc;
     int64_t n = 0, ne = 0;
     int nf = 0, npad = 0, T = 0, RW = 0;
     sfmx_allreduce_fn ar = nullptr;
@@ -125,7 +132,7 @@ struct sfmx_ba_ctx {
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
                       &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
-                      &failf, &partA, &lmst, &camscr};
+                      &failf, &partA, &lmst, &camscr, &pim, &pcc};
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
@@ -219,7 +226,8 @@ int eval_jacobian(sfmx_ba_ctx* c, const double* xp, double* cost_out) {
     const double* intr = poses + 6 * (size_t)c->C;
 #define LIN(KK) hipLaunchKernelGGL((ba_linearize<KK, true>), dim3(g), dim3(256), 0, c->st, c->O, c->obs_point.as<int>(), \
                                    c->obs_cam.as<int>(), c->obs_xy.as<double>(), c->cx, c->cy, pts, poses, intr,         \
-                                   c->J.as<double>(), c->partA.as<double>())
+                                   c->J.as<double>(), c->partA.as<double>(), c->multi ? c->pim.as<int>() : nullptr,      \
+                                   c->multi ? c->pcc.as<double2>() : nullptr)
     if (c->K == 1) LIN(1); else if (c->K == 3) LIN(3); else LIN(7);
 #undef LIN
     HIPCHK(hipGetLastError());
@@ -233,13 +241,16 @@ int eval_jacobian(sfmx_ba_ctx* c, const double* xp, double* cost_out) {
 template <int K>
 int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double* grad_o, double* camsum_o,
            bool cand_mode, double* out) {
-    if (c->ngroups > 0)
-        hipLaunchKernelGGL(ba_glin<K>, dim3(c->ngroups), dim3(256), c->lds_lin, c->st, c->grp.as<Grp>(),
-                           c->chk.as<Chunk>(), c->lcrow.as<int>(), c->obs_lc.as<short>(), c->obs_row.as<short>(),
-                           c->obs_point.as<int>(), c->obs_cam.as<int>(),
-                           c->obs_xy.as<double>(), c->pt_start.as<int>(), c->cx, c->cy, c->P, c->C, xp,
-                           c->scaled ? c->scale.as<double>() : nullptr, Jo, colsq_o, grad_o, c->gpart.as<double>(),
-                           c->gpl.as<double>(), gate(c));
+    if (c->ngroups > 0) {
+#define GLIN(MULTI) hipLaunchKernelGGL((ba_glin<K, MULTI>), dim3(c->ngroups), dim3(256), c->lds_lin, c->st, c->grp.as<Grp>(), \
+                           c->chk.as<Chunk>(), c->lcrow.as<int>(), c->obs_lc.as<short>(), c->obs_row.as<short>(),         \
+                           c->obs_point.as<int>(), c->obs_cam.as<int>(),                                                   \
+                           c->obs_xy.as<double>(), c->pt_start.as<int>(), c->cx, c->cy, c->P, c->C, xp,                    \
+                           c->scaled ? c->scale.as<double>() : nullptr, Jo, colsq_o, grad_o, c->gpart.as<double>(),        \
+                           c->gpl.as<double>(), gate(c), c->pim.as<int>(), c->pcc.as<double2>())
+        if (c->multi) GLIN(true); else GLIN(false);
+#undef GLIN
+    }
     // multi-rank speculative steps all-reduce a scratch copy of the camera sums: a skipped step's
     // all-reduce then touches no state (ba_finalize copies them behind the step gate)
     const int ncs = c->C * ncp(K) + K * (K + 1) / 2 + K;
@@ -723,11 +734,23 @@ int run_lm(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace, i
     return run_lm_k<7>(c, max_iters, sum, trace, trace_cap, ntrace_out);
 }
 
+bool valid_model(int m) { return m == SFMX_CAM_SIMPLE || m == SFMX_CAM_SIMPLE_RADIAL || m == SFMX_CAM_DISTORTION; }
+
 int validate(const sfmx_ba_problem* pb) {
     if (!pb) return fail(SFMX_EINVAL, "null problem");
-    if (pb->n_points < 0 || pb->n_cams < 0 || pb->n_obs < 0) return fail(SFMX_EINVAL, "negative sizes");
-    if (pb->cam_model != SFMX_CAM_SIMPLE && pb->cam_model != SFMX_CAM_SIMPLE_RADIAL && pb->cam_model != SFMX_CAM_DISTORTION)
+    if (pb->n_points < 0 || pb->n_cams < 0 || pb->n_obs < 0 || pb->n_intr < 0) return fail(SFMX_EINVAL, "negative sizes");
+    if (pb->n_intr == 0 && !valid_model(pb->cam_model))
         return fail(SFMX_EINVAL, "cam_model must be SFMX_CAM_SIMPLE, _SIMPLE_RADIAL or _DISTORTION");
+    if (pb->n_intr > 0) {
+        if (!pb->intr_model || (pb->n_cams && !pb->pose_intr) || !pb->intr_center)
+            return fail(SFMX_EINVAL, "n_intr > 0 needs intr_model, pose_intr and intr_center");
+        for (int m = 0; m < pb->n_intr; ++m)
+            if (!valid_model(pb->intr_model[m]))
+                return fail(SFMX_EINVAL, "intr_model entries must be SFMX_CAM_SIMPLE, _SIMPLE_RADIAL or _DISTORTION");
+        for (int c = 0; c < pb->n_cams; ++c)
+            if (pb->pose_intr[c] < 0 || pb->pose_intr[c] >= pb->n_intr)
+                return fail(SFMX_EINVAL, "pose_intr entry out of range");
+    }
     if ((pb->n_points && !pb->points) || (pb->n_cams && !pb->poses) || !pb->intr ||
         (pb->n_obs && (!pb->obs_point || !pb->obs_cam || !pb->obs_xy)))
         return fail(SFMX_EINVAL, "null problem array");
@@ -745,7 +768,9 @@ int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
         for (int i = 0; i < 3; ++i) pts[3 * (size_t)q + i] = pb->points[3 * (size_t)c->pperm[q] + i];
     if (c->P) HIPCHK(hipMemcpyAsync(x, pts.data(), sizeof(double) * 3 * c->P, hipMemcpyHostToDevice, c->st));
     if (c->C) HIPCHK(hipMemcpyAsync(x + c->ne, pb->poses, sizeof(double) * 6 * c->C, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipMemcpyAsync(x + c->ne + 6 * (size_t)c->C, pb->intr, sizeof(double) * c->K, hipMemcpyHostToDevice, c->st));
+    std::vector<double> iv(c->K, 0.0);   // the border: referenced blocks, zero padding
+    for (int j = 0; j < c->K; ++j) if (c->isrc[j] >= 0) iv[j] = pb->intr[c->isrc[j]];
+    HIPCHK(hipMemcpyAsync(x + c->ne + 6 * (size_t)c->C, iv.data(), sizeof(double) * c->K, hipMemcpyHostToDevice, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     return SFMX_OK;
 }
@@ -978,8 +1003,56 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
         return bail(fail(SFMX_ENOMEM, "pinned scalar buffer"));
     std::memset(c->hs, 0, sizeof(double) * sfmx_ba_ctx::HS_N);
-    const int P = caller->n_points, C = caller->n_cams, O = caller->n_obs, K = caller->cam_model;
-    c->P = P; c->C = C; c->O = O; c->K = K; c->cx = caller->cx; c->cy = caller->cy;
+    const int P = caller->n_points, C = caller->n_cams, O = caller->n_obs;
+    c->P = P; c->C = C; c->O = O; c->cx = caller->cx; c->cy = caller->cy;
+    std::vector<int> pim_h;
+    std::vector<double2> pcc_h;
+    if (caller->n_intr == 0) {
+        c->K = caller->cam_model;
+        c->intr_len = c->K;
+        for (int j = 0; j < c->K; ++j) c->isrc.push_back(j);
+    } else {
+        // several cameras: the blocks some residual references, in block order, back to back in
+        // the border (a camera no residual names is no parameter of the Ceres problem)
+        const int M = caller->n_intr;
+        c->n_intr = M;
+        std::vector<int> used(M, 0), first(M, -1), off(M + 1, 0), cam_used(C, 0);
+        for (int m = 0; m < M; ++m) off[m + 1] = off[m] + caller->intr_model[m];
+        c->intr_len = off[M];
+        for (int q = 0; q < O; ++q) cam_used[roc[q]] = 1;
+        for (int cm = 0; cm < C; ++cm) if (cam_used[cm]) used[caller->pose_intr[cm]] = 1;
+        int kb = 0, nused = 0;
+        for (int m = 0; m < M; ++m)
+            if (used[m]) {
+                ++nused;
+                first[m] = kb;
+                for (int i = 0; i < caller->intr_model[m]; ++i) c->isrc.push_back(off[m] + i);
+                kb += caller->intr_model[m];
+            }
+        if (nused <= 1) {   // one referenced camera: the single-block kernels with its block and centre
+            const int m = (int)(std::find(used.begin(), used.end(), 1) - used.begin());
+            c->K = m < M ? caller->intr_model[m] : caller->intr_model[0];
+            if (m == M) for (int i = 0; i < c->K; ++i) c->isrc.push_back(i);
+            c->cx = caller->intr_center[2 * (m < M ? m : 0)];
+            c->cy = caller->intr_center[2 * (m < M ? m : 0) + 1];
+        } else {
+            if (kb > SFMX_BA_MAX_INTR)
+                return bail(fail(SFMX_ECAPACITY, "the referenced cameras hold " + std::to_string(kb) +
+                                                     " intrinsics parameters; at most SFMX_BA_MAX_INTR = 7 are supported"));
+            c->multi = true;
+            c->K = kb <= 1 ? 1 : kb <= 3 ? 3 : 7;   // the kernels' border widths; padding columns stay 0
+            while ((int)c->isrc.size() < c->K) c->isrc.push_back(-1);
+            pim_h.assign(std::max(C, 1), 1);
+            pcc_h.assign(std::max(C, 1), double2{0.0, 0.0});
+            for (int cm = 0; cm < C; ++cm) {
+                const int m = caller->pose_intr[cm];
+                if (first[m] < 0) continue;   // a pose without observations: never evaluated
+                pim_h[cm] = caller->intr_model[m] | (first[m] << 4);
+                pcc_h[cm] = double2{caller->intr_center[2 * m], caller->intr_center[2 * m + 1]};
+            }
+        }
+    }
+    const int K = c->K;
     c->ne = 3 * (int64_t)P;
     c->nf = 6 * C + K;
     c->n = c->ne + c->nf;
@@ -1014,7 +1087,8 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
                               (const void*)ba_gschur<KK, 1, true>, (const void*)ba_gschur<KK, 2, true>,               \
                               (const void*)ba_gschur<KK, 3, true>, (const void*)ba_gschur<KK, 4, true>})              \
             if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_schur); \
-        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_glin<KK>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_lin);    
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_glin<KK, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_lin); \
+        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_glin<KK, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_lin);
         if (K == 1) { LDSATTR(1); } else if (K == 3) { LDSATTR(3); } else { LDSATTR(7); }
 #undef LDSATTR
         if (e != hipSuccess) return bail(fail(SFMX_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(e)));
@@ -1026,7 +1100,8 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
         (rc = upload(c->gcam, tp.gcam, st)) || (rc = upload(c->obs_lc, tp.obs_lc, st)) ||
         (rc = upload(c->obs_row, tp.obs_row, st)) || (rc = upload(c->lcrow, tp.lcrow, st)) ||
         (rc = upload(c->tasks, tp.tasks, st)) || (rc = upload(c->ents, tp.ents, st)) ||
-        (rc = upload(c->cref_start, tp.cref_start, st)) || (rc = upload(c->cref, tp.cref, st)))
+        (rc = upload(c->cref_start, tp.cref_start, st)) || (rc = upload(c->cref, tp.cref, st)) ||
+        (rc = upload(c->pim, pim_h, st)) || (rc = upload(c->pcc, pcc_h, st)))
         return bail(rc);
     const size_t n = c->n, so = std::max(O, 1);
     const size_t ncams = (size_t)C * ncp(K) + K * (K + 1) / 2 + K;
@@ -1160,8 +1235,10 @@ int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
     std::vector<double> pts(3 * (size_t)c->P);
     if (c->P) HIPCHK(hipMemcpyAsync(pts.data(), x, sizeof(double) * 3 * c->P, hipMemcpyDeviceToHost, c->st));
     if (c->C) HIPCHK(hipMemcpyAsync(pb->poses, x + c->ne, sizeof(double) * 6 * c->C, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipMemcpyAsync(pb->intr, x + c->ne + 6 * (size_t)c->C, sizeof(double) * c->K, hipMemcpyDeviceToHost, c->st));
+    std::vector<double> iv(c->K);
+    HIPCHK(hipMemcpyAsync(iv.data(), x + c->ne + 6 * (size_t)c->C, sizeof(double) * c->K, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    for (int j = 0; j < c->K; ++j) if (c->isrc[j] >= 0) pb->intr[c->isrc[j]] = iv[j];   // unreferenced cameras: untouched
     for (int q = 0; q < c->P; ++q)
         for (int i = 0; i < 3; ++i) pb->points[3 * (size_t)c->pperm[q] + i] = pts[3 * (size_t)q + i];
     return SFMX_OK;
@@ -1169,7 +1246,8 @@ int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
 
 int sfmx_ba_set(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
     if (!c || !pb) return fail(SFMX_EINVAL, "null context/problem");
-    if (pb->n_points != c->P || pb->n_cams != c->C || pb->cam_model != c->K) return fail(SFMX_EINVAL, "topology mismatch");
+    if (pb->n_points != c->P || pb->n_cams != c->C || pb->n_intr != c->n_intr || (!c->multi && pb->cam_model != c->K))
+        return fail(SFMX_EINVAL, "topology mismatch");
     return set_params(c, pb);
 }
 
@@ -1215,7 +1293,7 @@ int sfmx_ba_jacobian(const sfmx_ba_problem* pb, int32_t device, double* r, doubl
         double cost;
         rc = eval_jacobian(c, c->x.as<double>(), &cost);
         if (!rc) {
-            const int O = c->O, K = c->K, F = 20 + 2 * K;
+            const int O = c->O, K = c->K, F = 20 + 2 * K, KL = c->intr_len;
             std::vector<double> h((size_t)F * O);
             if (O && (hipMemcpy(h.data(), c->J.p, sizeof(double) * h.size(), hipMemcpyDeviceToHost) != hipSuccess))
                 rc = fail(SFMX_EDEVICE, "D2H");
@@ -1225,7 +1303,11 @@ int sfmx_ba_jacobian(const sfmx_ba_problem* pb, int32_t device, double* r, doubl
                     if (r) r[2 * o + j] = h[(size_t)q * F + j];
                     for (int i = 0; i < 3; ++i) if (Je) Je[6 * o + 3 * j + i] = h[(size_t)q * F + (2 + 3 * j + i)];
                     for (int i = 0; i < 6; ++i) if (Jc) Jc[12 * o + 6 * j + i] = h[(size_t)q * F + (8 + 6 * j + i)];
-                    for (int i = 0; i < K; ++i) if (Ji) Ji[2 * (size_t)K * o + K * j + i] = h[(size_t)q * F + (20 + K * j + i)];
+                    if (Ji) {   // the caller's intr layout; columns of other cameras 0
+                        for (int i = 0; i < KL; ++i) Ji[2 * (size_t)KL * o + KL * j + i] = 0.0;
+                        for (int i = 0; i < K; ++i)
+                            if (c->isrc[i] >= 0) Ji[2 * (size_t)KL * o + KL * j + c->isrc[i]] = h[(size_t)q * F + (20 + K * j + i)];
+                    }
                 }
             }
         }

@@ -41,7 +41,9 @@ class sfmx_ba_problem(C.Structure):
     _fields_ = [("n_points", C.c_int32), ("n_cams", C.c_int32), ("n_obs", C.c_int32), ("cam_model", C.c_int32),
                 ("points", C.c_void_p), ("poses", C.c_void_p), ("intr", C.c_void_p),
                 ("obs_point", C.c_void_p), ("obs_cam", C.c_void_p), ("obs_xy", C.c_void_p),
-                ("cx", C.c_double), ("cy", C.c_double)]
+                ("cx", C.c_double), ("cy", C.c_double),
+                ("n_intr", C.c_int32), ("_reserved", C.c_int32), ("intr_model", C.c_void_p),
+                ("pose_intr", C.c_void_p), ("intr_center", C.c_void_p)]
 
 
 class sfmx_ba_options(C.Structure):

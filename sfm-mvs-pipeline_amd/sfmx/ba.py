@@ -9,8 +9,11 @@ Reference (brunothg/sfm-mvs-pipeline/src/photogrammetrie):
   * camera models and their intrinsics block layout                               common/*Camera.cpp
 
 ``BAProblem`` holds exactly the Ceres-problem data layout the reference builds
-(point[3], angle-axis pose[6], ONE shared intrinsics block[k], one residual per
-observation); all arithmetic runs in the HIP kernels.
+(point[3], angle-axis pose[6], one intrinsics block[k] per camera, one residual per
+observation bound to its shot's camera, BundleAdjustment.cpp:45-48, 81-89); all
+arithmetic runs in the HIP kernels.  One camera: ``cam_model`` / ``intr`` / ``cx, cy``.
+Several cameras: ``intr_models`` (model per camera), ``pose_intr`` (camera of each
+pose), ``centers`` ((cx, cy) per camera) and ``intr`` = the blocks back to back.
 """
 from __future__ import annotations
 
@@ -40,6 +43,13 @@ class BAProblem:
     obs_xy: np.ndarray          # (O, 2) float64
     cx: float = 0.0
     cy: float = 0.0
+    intr_models: Optional[np.ndarray] = None   # (M,) int32: several cameras (None: the one block)
+    pose_intr: Optional[np.ndarray] = None     # (C,) int32: camera of each pose
+    centers: Optional[np.ndarray] = None       # (M, 2) float64: (cx, cy) per camera
+
+    @property
+    def multi(self) -> bool:
+        return self.intr_models is not None
 
     def __post_init__(self):
         # parameter blocks are owned (copied): solve() writes the result into them
@@ -49,20 +59,38 @@ class BAProblem:
         self.obs_point = np.ascontiguousarray(self.obs_point, np.int32).reshape(-1)
         self.obs_cam = np.ascontiguousarray(self.obs_cam, np.int32).reshape(-1)
         self.obs_xy = np.ascontiguousarray(self.obs_xy, np.float64).reshape(-1, 2)
-        if self.cam_model not in (CAM_SIMPLE, CAM_SIMPLE_RADIAL, CAM_DISTORTION):
+        models = (CAM_SIMPLE, CAM_SIMPLE_RADIAL, CAM_DISTORTION)
+        if self.multi:
+            self.intr_models = np.ascontiguousarray(self.intr_models, np.int32).reshape(-1)
+            self.pose_intr = np.ascontiguousarray(self.pose_intr, np.int32).reshape(-1)
+            self.centers = np.ascontiguousarray(self.centers if self.centers is not None
+                                                else np.zeros((len(self.intr_models), 2)), np.float64).reshape(-1, 2)
+            if not all(int(m) in models for m in self.intr_models):
+                raise ValueError("intr_models entries must be CAM_SIMPLE, CAM_SIMPLE_RADIAL or CAM_DISTORTION")
+            if len(self.intr) != int(self.intr_models.sum()) or len(self.pose_intr) != len(self.poses) or \
+                    len(self.centers) != len(self.intr_models):
+                raise ValueError("intr must hold every camera's block; pose_intr one entry per pose; centers one per camera")
+            return
+        if self.cam_model not in models:
             raise ValueError("cam_model must be CAM_SIMPLE, CAM_SIMPLE_RADIAL or CAM_DISTORTION")
         if len(self.intr) != self.cam_model:
             raise ValueError(f"intrinsics block must have {self.cam_model} entries")
 
     def copy(self) -> "BAProblem":
         return BAProblem(self.cam_model, self.points.copy(), self.poses.copy(), self.intr.copy(), self.obs_point,
-                         self.obs_cam, self.obs_xy, self.cx, self.cy)
+                         self.obs_cam, self.obs_xy, self.cx, self.cy, self.intr_models, self.pose_intr, self.centers)
 
     def struct(self) -> sfmx_ba_problem:
-        return sfmx_ba_problem(len(self.points), len(self.poses), len(self.obs_point), self.cam_model,
-                               self.points.ctypes.data, self.poses.ctypes.data, self.intr.ctypes.data,
-                               self.obs_point.ctypes.data, self.obs_cam.ctypes.data, self.obs_xy.ctypes.data,
-                               float(self.cx), float(self.cy))
+        s = sfmx_ba_problem(len(self.points), len(self.poses), len(self.obs_point), self.cam_model,
+                            self.points.ctypes.data, self.poses.ctypes.data, self.intr.ctypes.data,
+                            self.obs_point.ctypes.data, self.obs_cam.ctypes.data, self.obs_xy.ctypes.data,
+                            float(self.cx), float(self.cy))
+        if self.multi:
+            s.n_intr = len(self.intr_models)
+            s.intr_model = self.intr_models.ctypes.data
+            s.pose_intr = self.pose_intr.ctypes.data
+            s.intr_center = self.centers.ctypes.data
+        return s
 
 
 def default_options(**kw) -> sfmx_ba_options:
@@ -92,7 +120,7 @@ def solve(problem: BAProblem, options: Optional[sfmx_ba_options] = None, trace_c
 
 def jacobian(problem: BAProblem, device: int = 0):
     """Device residuals + Jacobian blocks -> (r[O,2], Je[O,2,3], Jc[O,2,6], Ji[O,2,k])."""
-    O, k = len(problem.obs_point), problem.cam_model
+    O, k = len(problem.obs_point), len(problem.intr)
     r = np.zeros((O, 2)); Je = np.zeros((O, 2, 3)); Jc = np.zeros((O, 2, 6)); Ji = np.zeros((O, 2, k))
     st = problem.struct()
     check(lib.sfmx_ba_jacobian(C.byref(st), device, r.ctypes.data, Je.ctypes.data, Jc.ctypes.data, Ji.ctypes.data),

@@ -177,6 +177,45 @@ def ba_problem(n_cams: int = 200, n_points: int = 200_000, obs_per_point: int = 
     return (prob, tr) if truth else prob
 
 
+def ba_problem_multi(n_cams: int = 24, n_points: int = 3000, cameras=((3, 1.0), (3, 1.1)), obs_per_point: int = 6,
+                     noise_px: float = 0.5, seed: int = BA_SEED + 7, width: int = 720, height: int = 405,
+                     perturb: bool = True, pose_intr=None):
+    """Several physical cameras (scene.getCameras(), BundleAdjustment.cpp:45-48): camera m is
+    (model k_m, focal scale s_m) with its own f = 1.2 * max(W, H) * s_m and principal point;
+    pose c uses camera pose_intr[c] (default c % M), each residual its shot's camera
+    (:81-89).  Ring geometry of ba_problem.  -> BAProblem kwargs dict (intr = the blocks back
+    to back; DISTORTION blocks carry cx, cy as parameters)."""
+    base, tr = ba_problem(n_cams, n_points, obs_per_point, 0.0, seed, 3, width, height, False, True)
+    rng = np.random.default_rng(seed + 1)
+    M = len(cameras)
+    models = np.array([k for k, _ in cameras], np.int32)
+    pim = np.asarray(pose_intr if pose_intr is not None else np.arange(n_cams) % M, np.int32)
+    f = np.array([1.2 * max(width, height) * sc for _, sc in cameras])
+    centers = np.stack([width / 2.0 + rng.uniform(-8, 8, M), height / 2.0 + rng.uniform(-8, 8, M)], 1)
+    poses, pts = tr["poses"], tr["points"]
+    obs_point, obs_cam = base["obs_point"], base["obs_cam"]
+    Rs = np.stack([_R_from_aa(p[:3]) for p in poses])
+    Xc = np.einsum("oij,oj->oi", Rs[obs_cam], pts[obs_point]) + poses[obs_cam, 3:]
+    m_o = pim[obs_cam]
+    xy = f[m_o, None] * Xc[:, :2] / Xc[:, 2:3] + centers[m_o] + rng.normal(0.0, noise_px, (len(obs_cam), 2))
+    blocks = []
+    for m, k in enumerate(models):
+        b = np.zeros(k)
+        b[0] = f[m]
+        if k == 7:
+            b[1], b[2] = centers[m]
+        blocks.append(b)
+    if perturb:
+        poses = poses.copy()
+        poses[:, :3] += rng.normal(0, 1e-2, (n_cams, 3))
+        poses[:, 3:] *= 1.0 + rng.normal(0, 1e-2, (n_cams, 3))
+        for b in blocks:
+            b[0] *= 1.0 + 0.01 * rng.standard_normal()
+        pts = pts + rng.normal(0, 1e-2, pts.shape)
+    return dict(cam_model=int(models[0]), points=pts, poses=poses, intr=np.concatenate(blocks), obs_point=obs_point,
+                obs_cam=obs_cam, obs_xy=xy, cx=0.0, cy=0.0, intr_models=models, pose_intr=pim, centers=centers)
+
+
 def point_cloud_origins(src: list, kps: list, min_views: int = 2):
     """Point-cloud origin records (include/sfmx_scene.h layout) for a synthetic
     scene: every landmark of the pool seen by >= min_views images is a 3-D

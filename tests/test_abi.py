@@ -167,7 +167,7 @@ def test_product_library_reads_no_tuning_variables():
                 b"SFMX_BA_BACK", b"SFMX_BA_SPLIT", b"SFMX_BA_DAG", b"SFMX_BA_SPEC", b"SFMX_SIFT_SMALL"):
         assert var not in blob, var
     names = set(re.findall(rb"SFMX_[A-Z0-9_]+", blob))
-    assert names <= {b"SFMX_CAM_SIMPLE", b"SFMX_NORM_L2", b"SFMX_NORM_HAMMING"}, names
+    assert names <= {b"SFMX_CAM_SIMPLE", b"SFMX_NORM_L2", b"SFMX_NORM_HAMMING", b"SFMX_BA_MAX_INTR"}, names   # messages
 
 
 def test_diagnostic_library_exports_the_same_entry_points():
@@ -176,3 +176,22 @@ def test_diagnostic_library_exports_the_same_entry_points():
     for name in declared_functions():
         assert hasattr(dl, name), name
     assert b"SFMX_SIFT_VARIANT" in open(diag.DIAG_PATH, "rb").read()
+
+
+def test_integration_ba_adapter_is_the_compiled_one():
+    """INTEGRATION.md §4 shows exactly the doBundleAdjustment adapter tests/cpp compiles and the GPU
+    suite runs (several cameras: one intrinsics block per ICamera, getCenter, dynamic_cast)."""
+    body = open(os.path.join(REPO, "tests", "cpp", "GpuBundleAdjustment.h")).read()
+    adapter = body[body.index("// --- adapter begin ---\n") + 24: body.index("// --- adapter end ---")]
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    assert adapter in text
+    assert "getCenter(cx, cy)" in adapter and "ceresParameterCount" not in text and "getCx" not in text
+    assert os.path.exists(os.path.join(REPO, "tests", "cpp", "ba_adapter_test")), "build() compiles tests/cpp/ba_adapter_test"
+
+
+def test_ba_problem_struct_layout():
+    """The ctypes mirror of sfmx_ba_problem has the header's field offsets (several-camera fields)."""
+    import ctypes as C
+    S = _lib.sfmx_ba_problem
+    assert S.n_intr.offset == 4 * 4 + 6 * 8 + 2 * 8 and S.intr_model.offset == S.n_intr.offset + 8
+    assert C.sizeof(S) == S.intr_center.offset + 8

@@ -182,3 +182,67 @@ def test_speculative_lm_bit_identical_to_host_judged_lm(seed):
         assert a[3][key] == b[3][key], key
     assert np.array_equal(a[4], b[4])
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+
+
+# ---- several cameras (BundleAdjustment.cpp:45-48, 81-89) ------------------------------------
+MULTI = [((3, 1.0), (3, 1.1)), ((1, 1.0), (3, 0.95)), ((1, 1.0), (1, 1.05)), ((1, 1.0), (3, 1.1), (1, 0.9)),
+         ((3, 1.0), (1, 1.02), (3, 0.97)), ((7, 1.0), (7, 1.1))]
+
+
+@pytest.mark.parametrize("cams", MULTI[:4])
+def test_multi_camera_jacobian_matches_oracle(cams):
+    from oracle import oracle
+    p = synth.ba_problem_multi(9, 300, cameras=cams, seed=41)
+    g = ba.jacobian(ba.BAProblem(**p))
+    o = oracle.ba_jacobian(p)
+    for a, b in zip(g, o):
+        np.testing.assert_allclose(a, b, rtol=1e-9, atol=1e-9 * np.abs(b).max())
+
+
+@pytest.mark.parametrize("cams", MULTI[:5])
+def test_multi_camera_solve_matches_oracle(cams):
+    """Every pose's residuals use its camera's block (mixed models, padded border): final cost
+    within 1e-5, same termination and accept/reject sequence as the oracle; every camera's
+    block written back in the caller's layout."""
+    from oracle import oracle
+    p = synth.ba_problem_multi(16, 1500, cameras=cams, seed=42)
+    sol, osm, otr = oracle.ba_solve(p, trace_cap=512)
+    P, sm, tr = gpu_solve(p)
+    assert sm["termination_type"] == osm["termination_type"]
+    assert abs(sm["initial_cost"] - osm["initial_cost"]) <= 1e-12 * osm["initial_cost"]
+    assert abs(sm["final_cost"] - osm["final_cost"]) <= COST_RTOL * osm["final_cost"]
+    n = min(len(tr), len(otr))
+    assert np.array_equal(tr[:n, 2], otr[:n, 2])
+    np.testing.assert_allclose(P.intr, sol["intr"], rtol=1e-4, atol=1e-6)
+
+
+def test_one_referenced_camera_block_is_the_single_form_bit_for_bit():
+    """n_intr >= 1 with one referenced camera runs the single-block kernels: the same bits as the
+    single-block fields; an unreferenced camera's block is left untouched."""
+    p = synth.ba_problem(12, 2000, seed=43)
+    q = dict(p, intr_models=np.array([7, 3]), pose_intr=np.ones(12, np.int32),
+             centers=np.array([[5.0, 6.0], [p["cx"], p["cy"]]]), intr=np.concatenate([np.arange(7.0), p["intr"]]))
+    P1, s1, t1 = gpu_solve(p)
+    P2, s2, t2 = gpu_solve(q)
+    assert s1["final_cost"] == s2["final_cost"] and np.array_equal(t1, t2)
+    assert np.array_equal(P1.points, P2.points) and np.array_equal(P1.poses, P2.poses)
+    assert np.array_equal(P2.intr[:7], np.arange(7.0)) and np.array_equal(P2.intr[7:], P1.intr)
+
+
+def test_multi_camera_capacity_is_reported():
+    """More than SFMX_BA_MAX_INTR = 7 referenced intrinsics parameters fail loudly (SFMX_ECAPACITY),
+    never with a silently wrong model."""
+    from sfmx import _lib
+    p = synth.ba_problem_multi(12, 300, cameras=((3, 1.0), (3, 1.1), (3, 0.9)), seed=44)
+    with pytest.raises(_lib.SfmxError) as e:
+        gpu_solve(p)
+    assert e.value.code == _lib.SFMX_ECAPACITY
+
+
+def test_multi_camera_distortion_pair_capacity():
+    """Two DISTORTION cameras = 14 parameters: over capacity as well."""
+    from sfmx import _lib
+    p = synth.ba_problem_multi(8, 200, cameras=MULTI[5], seed=45)
+    with pytest.raises(_lib.SfmxError) as e:
+        gpu_solve(p)
+    assert e.value.code == _lib.SFMX_ECAPACITY
