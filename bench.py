@@ -229,9 +229,17 @@ def bench_match(kind, args, rank, world, local):
         step()
     barrier()
     elapsed = time.perf_counter() - t0
-    # kernel durations: the HIP events the matcher recorded on its stream in the last timed step
+    # kernel durations: the HIP events the matcher records on its stream, read after each of a few
+    # extra untimed steps (reading them inside the timed loop would sync the host every step); the
+    # median of the timed loop's last step and these
     a, b = matcher.timing()
     main_ms, run_ms, scr_ms = [a], [b], [matcher.pass_timing()[0]]
+    for _ in range(int(os.environ.get("SFMX_BENCH_EVENT_STEPS", "4"))):
+        step()
+        a, b = matcher.timing()
+        main_ms.append(a)
+        run_ms.append(b)
+        scr_ms.append(matcher.pass_timing()[0])
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -252,7 +260,7 @@ def bench_match(kind, args, rank, world, local):
         n_matches = int(t.item())
 
     value = logical_total * steps / elapsed   # all ranks' pairs / max-over-ranks time
-    kern_ms = float(np.mean(main_ms))
+    kern_ms = float(np.median(main_ms))
 
     # PCIe-inclusive rate (outside the timed region; never `value`): host descriptor
     # buffers in, H2D + prepare + match + D2H of the DMatch lists, as the one-shot ABI sees it.
@@ -269,7 +277,7 @@ def bench_match(kind, args, rank, world, local):
         pcie_s = float(t.item())
     matcher.close()
     achieved = logical_mine * op_per_pair / (kern_ms * 1e-3) / 1e12
-    screen_ms = float(np.mean(scr_ms))
+    screen_ms = float(np.median(scr_ms))
     screen = {"kernel_ms_per_launch": screen_ms, "achieved": logical_mine * op_per_pair / (screen_ms * 1e-3) / 1e12 if screen_ms > 0 else None,
               "frac": logical_mine * op_per_pair / (screen_ms * 1e-3) / 1e12 / peak if screen_ms > 0 else None,
               "what": "pass 1 alone (the screening kernel over every descriptor pair); frac is of the same nominal peak"}
@@ -292,7 +300,8 @@ def bench_match(kind, args, rank, world, local):
         "roofline": {"bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
                      "frac": achieved / peak, "traffic": pmc_traffic(kind, n_img),
                      "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE from the committed PMC pass)",
-                     "kernel": kernel, "kernel_ms_per_launch": kern_ms, "run_ms_per_step": float(np.mean(run_ms)),
+                     "kernel": kernel, "kernel_ms_per_launch": kern_ms, "run_ms_per_step": float(np.median(run_ms)),
+                     "kernel_ms_samples": [float(x) for x in main_ms],
                      "screen_only": screen,
                      "algorithmic": f"{algo} x {logical_mine:.4g} pairs per launch"},
         "cpu_baseline": None,

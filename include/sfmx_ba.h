@@ -125,7 +125,9 @@ int sfmx_ba_get(sfmx_ba_ctx* ctx, sfmx_ba_problem* problem);
 int sfmx_ba_set(sfmx_ba_ctx* ctx, const sfmx_ba_problem* problem);
 /* Per-phase device time of the last run (ms, summed over its iterations):
  * [0] linearize (residuals + Jacobians), [1] Schur assembly, [2] Cholesky + solves,
- * [3] step / candidate cost.  n = number of entries written.  [1]..[3] are recorded only while
+ * [3] step / candidate cost; [4] (n >= 5) the number of steps this context re-ran with the
+ * per-level factorization launches because an in-launch dependency wait saw no progress for
+ * 20 ms (a preempted queue), after which the context stays on them.  n = entries written.  [1]..[3] are recorded only while
  * phase timing is on (sfmx_ba_set_phase_timing; off by default: each event costs GPU time). */
 int sfmx_ba_phase_ms(sfmx_ba_ctx* ctx, double* ms, int32_t n);
 /* Diagnostics: record the per-phase events of sfmx_ba_phase_ms in later runs (on != 0). */

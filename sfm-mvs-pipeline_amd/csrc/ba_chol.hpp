@@ -30,7 +30,13 @@ namespace sfmx {
 namespace ba {
 
 constexpr int LDT = NB + 2;   // LDS row stride (doubles): 16-B aligned rows
-constexpr long long DAG_TIMEOUT = 2000000;   // bound of every in-launch wait: 20 ms of the 100 MHz wall clock
+// Bound of every in-launch wait without progress: 20 ms of the 100 MHz wall clock (the kernels take
+// it as an argument; the diagnostic build can shorten it, SFMX_BA_DAG_TIMEOUT).  A wait that sees
+// the polled version / flag move restarts its clock, so a preempted queue (ranks sharing a GPU, a
+// profiler) only trips it when nothing at all advances.  Fail bits: 2 = chol_factor, 4 =
+// chol_backsolve; the host then re-runs the step with the per-level launches.
+constexpr long long DAG_TIMEOUT = 2000000;
+enum { FAIL_PIVOT = 1, FAIL_FACTOR_WAIT = 2, FAIL_BACK_WAIT = 4 };
 // global-address-space words for in-launch hand-offs (agent-scope atomics / sc1 accesses)
 typedef __attribute__((address_space(1))) int g_i32;
 typedef __attribute__((address_space(1))) unsigned long long g_u64;
@@ -589,7 +595,7 @@ __global__ __launch_bounds__(256)
 void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
                  const int4* __restrict__ items, const int4* __restrict__ need, const int* __restrict__ src,
                  double* __restrict__ W, double* __restrict__ contrib, int* __restrict__ fail, double* pbuf,
-                 int* tctr, int* ctr, int nitems, int nver) {
+                 int* tctr, int* ctr, int nitems, int nver, long long tmo) {
     if (step_gated(fail + 1)) return;
     __shared__ CholLds<RW> sm;
     __shared__ int sh[2];
@@ -602,12 +608,17 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
     __syncthreads();
     const int tk = sh[0];
     const int4 it = items[tk], nd = need[tk];
-    // one lane waits until tile `id` carries version `v` (bounded: a timeout sets fail bit 2 and the
-    // item runs on, so every counter still advances and the launch drains)
-    auto wait_ver = [&](int id, int v, long long t0) {
-        while (__hip_atomic_load((g_i32*)&tver[id], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
+    // one lane waits until tile `id` carries version `v` (bounded: `tmo` ticks without the version
+    // moving set fail bit 2 and the item runs on, so every counter still advances and the launch drains)
+    auto wait_ver = [&](int id, int v) {
+        long long t0 = wall_clock64();
+        int last = -1;
+        for (;;) {
+            const int cur = __hip_atomic_load((g_i32*)&tver[id], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur >= v) return;
+            if (cur != last) { last = cur; t0 = wall_clock64(); }   // progress restarts the clock
             __builtin_amdgcn_s_sleep(1);
-            if (wall_clock64() - t0 > DAG_TIMEOUT) { atomicOr(fail, 2); return; }
+            if (wall_clock64() - t0 > tmo) { atomicOr(fail, FAIL_FACTOR_WAIT); return; }
         }
     };
     const __amdgpu_buffer_rsrc_t rS = wt_rsrc(S), rW = wt_rsrc(W);
@@ -628,12 +639,10 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
         double* dst = S + (size_t)a0 * npad + b0;
         // A_ak, A_bk (and A_ab of a one-source task) are final before W_k is (the inverse of (k, k) ends
         // the previous level's chain): they load while that inverse still runs
-        long long t0 = 0;
         if (tid == 0) {
-            t0 = wall_clock64();
-            wait_ver(tver_id(a, k), nd.x, t0);
-            if (!diag) wait_ver(tver_id(b, k), nd.y, t0);
-            if (n == 1) wait_ver(tver_id(a, b), nd.w, t0);
+            wait_ver(tver_id(a, k), nd.x);
+            if (!diag) wait_ver(tver_id(b, k), nd.y);
+            if (n == 1) wait_ver(tver_id(a, b), nd.w);
         }
         __syncthreads();
         f64x4 t[4];
@@ -644,7 +653,7 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
         }
         tile_load_wt(sm.a, rS, (size_t)a0 * npad + k0, npad);                   // A_ak
         if (!diag) tile_load_wt(sm.n, rS, (size_t)b0 * npad + k0, npad);        // A_bk
-        if (tid == 0) wait_ver(tver_id(k, k), nd.z - 1, t0);   // W_k stored (its R rows may still be in flight)
+        if (tid == 0) wait_ver(tver_id(k, k), nd.z - 1);   // W_k stored (its R rows may still be in flight)
         __syncthreads();
         tile_load_wt(sm.m, rW, (size_t)k * NB * NB, NB);                        // W_k
         __syncthreads();
@@ -660,7 +669,7 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
         mfma_nt(sm.m, diag ? sm.a : sm.n, upd);   // G X^T
         double ys[OPT];
         if (diag) {
-            if (tid == 0) wait_ver(tver_id(k, k), nd.z, t0);   // w_k (the R rows of k) stored
+            if (tid == 0) wait_ver(tver_id(k, k), nd.z);   // w_k (the R rows of k) stored
             __syncthreads();
             for (int e = tid; e < NB * RW; e += 256) sm.rk[e] = ld_wt(&R[(size_t)k0 * RW + e]);   // w_k
             __syncthreads();
@@ -688,7 +697,7 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
                 const bool last = __hip_atomic_fetch_add((g_i32*)&tctr[it.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
                 if (last) {
                     tctr[it.x] = 0;   // nobody else touches it in this launch
-                    wait_ver(tver_id(a, b), nd.w, wall_clock64());
+                    wait_ver(tver_id(a, b), nd.w);
                 }
                 sh[1] = last;
             }
@@ -830,8 +839,8 @@ __device__ __forceinline__ void intr_solve(const double* __restrict__ Dm, const 
 //     the consumer polls the flags with sc1 loads (one lane) and reads z only with sc1 loads
 //     behind the workgroup barrier, so no L1 line can be stale and no acquire fence is needed
 //     (MI355X_MICROARCH.md, inter-workgroup visibility: the valid sc1-load form, table row 1).
-// Spins are bounded (DAG_TIMEOUT of the 100 MHz wall clock): a timed-out wait sets fail bit 2 and
-// the solve reports an internal error.  ctr = [ticket, finished, zdone[T]] is zero at launch; the
+// Spins are bounded (`tmo` ticks of the 100 MHz wall clock per ancestor): a timed-out wait sets fail
+// bit 4 and the host re-runs the step with the per-level launches.  ctr = [ticket, finished, zdone[T]] is zero at launch; the
 // last workgroup to finish zeroes it for the next launch (nobody polls by then).
 constexpr int BS_PF = 4;                   // ancestor tiles prefetched into LDS per workgroup
 
@@ -841,7 +850,8 @@ void chol_backsolve(const double* __restrict__ S, int npad, const double* __rest
                     const double* __restrict__ Dm, const double* __restrict__ ri, const double* __restrict__ contrib,
                     int T, const int* __restrict__ border, const int* __restrict__ bs_start,
                     const int* __restrict__ bs_k, const int* __restrict__ rowmap, double* z,
-                    double* __restrict__ xout, double* __restrict__ sol_i, int* ctr, int* __restrict__ fail) {
+                    double* __restrict__ xout, double* __restrict__ sol_i, int* ctr, int* __restrict__ fail,
+                    long long tmo) {
     if (step_gated(fail + 1)) return;
     constexpr int K = RW - 1;
     __shared__ double Ut[BS_PF][NB / 4][256];   // thread-private: its 16 U values per prefetched tile
@@ -876,12 +886,13 @@ void chol_backsolve(const double* __restrict__ S, int npad, const double* __rest
     for (int a = 0; a < K; ++a) s -= R[(size_t)r * RW + a] * xs[a];
     if (tid == 0) {   // ONE lane polls (relaxed), then ONE agent acquire
         bool ok = true;
-        const long long t0 = wall_clock64();
-        for (int e = e0; e < e1 && ok; ++e)
+        for (int e = e0; e < e1 && ok; ++e) {   // each ancestor's flag gets its own bound (progress restarts it)
+            const long long t0 = wall_clock64();
             while (__hip_atomic_load((g_i32*)&ctr[2 + bs_k[e]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
                 __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() - t0 > DAG_TIMEOUT) { atomicOr(fail, 2); ok = false; break; }
+                if (wall_clock64() - t0 > tmo) { atomicOr(fail, FAIL_BACK_WAIT); ok = false; break; }
             }
+        }
         sh[1] = ok;
     }
     __syncthreads();

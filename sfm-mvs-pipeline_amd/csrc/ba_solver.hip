@@ -106,6 +106,8 @@ struct sfmx_ba_ctx {
     std::vector<int> part_start;   // per level: parts[part_start[l] .. part_start[l + 1])
     bool dag = true;               // SFMX_BA_DAG=0: one launch per level (chol_leaves + chol_level[_split])
     int n_ditems = 0, n_ver = 0;
+    long long dag_timeout = DAG_TIMEOUT;   // in-launch wait bound (wall-clock ticks without progress)
+    int dag_fallbacks = 0;                 // steps re-run with the per-level launches after a wait timed out
     int n_nztiles = 0;
     size_t sr_count = 0;         // doubles of SR = S_cc | R | D | r_i
     // state (the *2 buffers hold the candidate's linearization until the step is accepted)
@@ -294,7 +296,7 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
         hipLaunchKernelGGL(chol_factor<RW>, dim3((unsigned)c->n_ditems), dim3(256), 0, c->st, S, npad, R,
                            c->ptasks.as<int4>(), c->ditems.as<int4>(), c->dneed.as<int4>(), c->psrc.as<int>(),
                            c->Wt.as<double>(), c->contrib.as<double>(), fl, c->pbuf.as<double>(), c->lctr.as<int>(),
-                           c->dctr.as<int>(), c->n_ditems, c->n_ver);
+                           c->dctr.as<int>(), c->n_ditems, c->n_ver, c->dag_timeout);
     } else {
     hipLaunchKernelGGL(chol_leaves<RW>, dim3((unsigned)pl.leaves.size()), dim3(256), 0, c->st, S, npad, R,
                        c->leaves.as<int>(), c->Wt.as<double>(), c->contrib.as<double>(), fl);
@@ -315,7 +317,7 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
         hipLaunchKernelGGL(chol_backsolve<RW>, dim3(c->T), dim3(256), 0, c->st, S, npad, R, Dm, ri,
                            c->contrib.as<double>(), c->T, c->border.as<int>(), c->bs_start.as<int>(), c->bs_k.as<int>(),
                            c->rowmap.as<int>(), c->zbuf.as<double>(), sol_f, sol_f + 6 * (size_t)c->C,
-                           c->dagctr.as<int>(), fl);
+                           c->dagctr.as<int>(), fl, c->dag_timeout);
     } else {
         hipLaunchKernelGGL(chol_intr<RW - 1>, dim3(1), dim3(64), 0, c->st, Dm, ri, c->contrib.as<double>(), c->T,
                            c->xi.as<double>(), sol_f + 6 * (size_t)c->C, fl);
@@ -404,7 +406,21 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
         HIPCHK(hipGetLastError());
         return SFMX_OK;
     }
-    if (v[SC_FAIL] >= 2.0) return fail(SFMX_EINTERNAL, "BA solve: a dependency wait of chol_backsolve timed out");
+    if (v[SC_FAIL] >= 2.0) {
+        // an in-launch dependency wait saw no progress for dag_timeout ticks (e.g. a preempted
+        // queue): the step's solve is void, nothing of the state was touched (the step writes only
+        // candidate buffers), so re-run it with the per-level launches, which have no waits
+        const int fb = (int)v[SC_FAIL];
+        if (c->dag || c->back_dag) {
+            c->dag = false;
+            c->back_dag = false;
+            ++c->dag_fallbacks;
+            return try_step<K>(c, radius, valid, mcc, step_norm, ccost, cgmax, cxnorm);
+        }
+        return fail(SFMX_EINTERNAL, std::string("BA solve: a dependency wait of the in-launch ") +
+                                        ((fb & FAIL_FACTOR_WAIT) ? "factorization (chol_factor)" : "back solve (chol_backsolve)") +
+                                        " timed out");
+    }
     const double sn2 = v[SC_STEPN] + v[SC_STEPN_F];
     *mcc = -v[SC_MODEL];
     *step_norm = std::sqrt(sn2);
@@ -556,6 +572,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
         HIPCHK(hipMemsetAsync(c->dctr.p, 0, c->dctr.bytes, st));
         const char* ed = SFMX_DIAG_ENV("SFMX_BA_DAG");
         c->dag = dag_ok && !(ed && ed[0] == '0');
+        if (const char* et = SFMX_DIAG_ENV("SFMX_BA_DAG_TIMEOUT")) c->dag_timeout = std::atoll(et);   // recovery test
         max_slots = std::max(max_slots, dslots);
         const int tpo = std::max(1, 256 / (NB * RW)), opt = NB * RW / (256 / tpo);
         RC(c->pbuf.alloc(sizeof(double) * (size_t)max_slots * (16 + opt) * 256));
@@ -647,7 +664,8 @@ int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace,
                 const double* lm = L + SC_N;
                 if (lm[LM_ERROR] != 0.0) {
                     (void)hipStreamSynchronize(c->st);
-                    return fail(SFMX_EINTERNAL, "BA solve: a dependency wait of chol_backsolve timed out");
+                    return fail(SFMX_EINTERNAL, "BA solve: a dependency wait of the in-launch factorization / back "
+                                                "solve timed out (speculative mode has no per-level fallback)");
                 }
                 const bool acc = lm[LM_ACCEPTED] != 0.0;
                 if (!acc) swap_state();
@@ -1259,8 +1277,9 @@ int sfmx_ba_set_phase_timing(sfmx_ba_ctx* c, int32_t on) {
 
 int sfmx_ba_phase_ms(sfmx_ba_ctx* c, double* ms, int32_t n) {
     if (!c || !ms) return fail(SFMX_EINVAL, "null");
-    const int m = std::min<int>(n, 4);
-    for (int i = 0; i < m; ++i) ms[i] = c->phase_ms[i];
+    const int m = std::min<int>(n, 5);
+    for (int i = 0; i < m && i < 4; ++i) ms[i] = c->phase_ms[i];
+    if (m > 4) ms[4] = c->dag_fallbacks;
     return m;
 }
 

@@ -883,7 +883,12 @@ void sift_settle_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restr
         const int qi = qlist[P.dense_base + e];
         const int64_t o = P.dense_base + qi;
         const unsigned long long b0 = top2[2 * o], b1 = top2[2 * o + 1];
-        if (b0 == ~0ull || (nt >= 2 && b1 == ~0ull)) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }   // not reached
+        if (b0 == ~0ull || (nt >= 2 && b1 == ~0ull)) {
+            if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; }   // an empty train image: no neighbour
+            // otherwise pass 2 left a flagged subset unscanned: the UNSETTLED stamp stays, so
+            // assemble_kernel counts the query and the run fails (SFMX_EINTERNAL), never a lost match
+            continue;
+        }
         const int64_t s1 = (int64_t)(b0 >> 32), s2 = (int64_t)(b1 >> 32);
         if (nt >= 2 && s2 >= SQRT_SAFE) {
             const int slot = atomicAdd(slow_count, 1);
@@ -1700,7 +1705,12 @@ void orb_settle_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restri
         const int qi = qlist[P.dense_base + e];
         const int64_t o = P.dense_base + qi;
         const unsigned long long b0 = top2[2 * o], b1 = top2[2 * o + 1];
-        if (b0 == ~0ull || (nt >= 2 && b1 == ~0ull)) { out_idx[o] = -1; out_dist[o] = 0.f; continue; }   // not reached
+        if (b0 == ~0ull || (nt >= 2 && b1 == ~0ull)) {
+            if (nt == 0) { out_idx[o] = -1; out_dist[o] = 0.f; }   // an empty train image: no neighbour
+            // otherwise pass 2 left a flagged subset unscanned: the UNSETTLED stamp stays, so
+            // assemble_kernel counts the query and the run fails (SFMX_EINTERNAL), never a lost match
+            continue;
+        }
         const float d1 = (float)(int)(b0 >> 32), d2 = nt >= 2 ? (float)(int)(b1 >> 32) : 0.f;
         out_idx[o] = lowe_select((int)(b0 & 0xffffffffu), d1, d2, nt, ratio);
         out_dist[o] = d1;

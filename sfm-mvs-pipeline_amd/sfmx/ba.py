@@ -174,9 +174,11 @@ class BAContext:
         check(lib.sfmx_ba_set_phase_timing(self._h, 1 if on else 0), "sfmx_ba_set_phase_timing")
 
     def phase_ms(self):
-        v = (C.c_double * 4)()
-        n = check(lib.sfmx_ba_phase_ms(self._h, v, 4), "sfmx_ba_phase_ms")
-        return {k: v[i] for i, k in enumerate(["linearize", "schur", "cholesky_solve", "step_cost"][:n])}
+        """Per-phase device ms of the last run, plus ``dag_fallbacks``: steps re-run with the
+        per-level factorization launches after an in-launch dependency wait timed out."""
+        v = (C.c_double * 5)()
+        n = check(lib.sfmx_ba_phase_ms(self._h, v, 5), "sfmx_ba_phase_ms")
+        return {k: v[i] for i, k in enumerate(["linearize", "schur", "cholesky_solve", "step_cost", "dag_fallbacks"][:n])}
 
     def close(self):
         if getattr(self, "_h", None):

@@ -44,6 +44,23 @@ STRATEGY_NAMES = {STRATEGY_UNORDERED: "Unordered", STRATEGY_VIDEO: "Video", STRA
 EXIT_USAGE = 255          # the reference's exit(-1)
 
 
+
+def prepare_working_dir(workdir: str, log) -> None:
+    """PhotogrammetrieCli::prepareWorkingDir (PhotogrammetrieCli.cpp:399-402): remove_all(-Pout),
+    then create it.  The reference's semantics are kept, but a -Pout that is the filesystem root,
+    the home directory, the current directory or one of its ancestors is refused (that would wipe
+    the caller's tree), and the path being cleared is logged."""
+    target = os.path.realpath(workdir)
+    cwd = os.path.realpath(os.getcwd())
+    home = os.path.realpath(os.path.expanduser("~"))
+    if target in (os.path.realpath(os.sep), home) or cwd == target or cwd.startswith(target.rstrip(os.sep) + os.sep):
+        raise ValueError(f"-Pout={workdir}: refusing to clear {target} (the filesystem root, the home directory, "
+                         "or the current directory or one of its ancestors)")
+    if os.path.exists(target):
+        log.info(f"clearing working directory {target}")
+    shutil.rmtree(target, ignore_errors=True)
+    os.makedirs(target, exist_ok=True)
+
 def _string(call, *args) -> str:
     n = call(*args, None, 0)
     if n < 0:
@@ -283,11 +300,10 @@ class PhotogrammetrieCli:
             sys.stdout.write(json.dumps(plan) + "\n")
             return 0
 
-        shutil.rmtree(workdir, ignore_errors=True)                 # prepareWorkingDir (:399-402)
-        os.makedirs(workdir, exist_ok=True)
+        prepare_working_dir(workdir, log)                          # prepareWorkingDir (:399-402)
         if cfg.feature_matcher == MATCHER_FLANN:
             log.info("-Pfeature-matcher=FLANN: matching runs as exact brute force on the GPU "
-                     "(a superset of FLANN's approximate neighbours)")
+                     "(exact 2-NN: FLANN's approximate search is randomised, so its lists are not reproducible)")
 
         from .matching import BFMatcher, LOWE_RATIO
         from .homography import homography_ratios

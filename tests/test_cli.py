@@ -338,3 +338,22 @@ def test_run_script_replay_plan(script, tmp_path):
     for f in ("colored", "dense", "mesh", "stats", "artifacts", "sgm"):
         assert c[f] == int(f"--{f}" in argv)
     assert c["loglevel"] == 2 and c["force_colored_output"] == 1 and c["n_warnings"] == 0
+
+
+def test_prepare_working_dir_refuses_dangerous_targets(tmp_path, monkeypatch):
+    """prepareWorkingDir (PhotogrammetrieCli.cpp:399-402) clears -Pout; the restatement keeps that
+    but refuses the filesystem root, the home directory and the current directory or its ancestors."""
+    import logging
+    from sfmx import cli
+    log = logging.getLogger("t")
+    monkeypatch.chdir(tmp_path)
+    (tmp_path / "keep.txt").write_text("x")
+    for bad in (os.sep, os.path.expanduser("~"), ".", str(tmp_path), str(tmp_path.parent)):
+        with pytest.raises(ValueError):
+            cli.prepare_working_dir(bad, log)
+    assert (tmp_path / "keep.txt").exists()
+    out = tmp_path / "out"
+    out.mkdir()
+    (out / "stale.txt").write_text("x")
+    cli.prepare_working_dir(str(out), log)
+    assert out.is_dir() and not (out / "stale.txt").exists()

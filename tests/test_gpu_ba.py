@@ -246,3 +246,23 @@ def test_multi_camera_distortion_pair_capacity():
     with pytest.raises(_lib.SfmxError) as e:
         gpu_solve(p)
     assert e.value.code == _lib.SFMX_ECAPACITY
+
+
+def test_dag_wait_timeout_falls_back_to_per_level_launches():
+    """a dependency wait of chol_factor / chol_backsolve that sees no progress for the
+    bound (here 0 ticks, diagnostic library) must not fail the solve: the step re-runs with the
+    per-level launches, bit-identical to the in-launch forms, and the context stays on them."""
+    p = synth.ba_problem(200, 6000, seed=29)
+    P0, s0, t0 = gpu_solve(p, max_num_iterations=4)
+    with diagnostic(SFMX_BA_DAG_TIMEOUT="0"):
+        P1 = ba.BAProblem(**p)
+        ctx = ba.BAContext(P1, ba.default_options(max_num_iterations=4))
+        try:
+            s1, t1 = ctx.run(trace_cap=512)
+            ph = ctx.phase_ms()
+            ctx.get(P1)
+        finally:
+            ctx.close()
+    assert ph["dag_fallbacks"] >= 1
+    assert s1["final_cost"] == s0["final_cost"] and np.array_equal(t1, t0)
+    assert np.array_equal(P1.points, P0.points) and np.array_equal(P1.poses, P0.poses)
