@@ -73,6 +73,7 @@ def test_context_api_allreduce_identity_and_reset():
     assert s1["final_cost"] == s2["final_cost"]             # phase events do not change the numbers
     assert calls and any(n > 1000 for n, _ in calls)        # the reduced camera system went through the hook
     ph = ctx.phase_ms()
+    assert ph.pop("dag_fallbacks") == 0                      # no in-launch wait ran out
     assert set(ph) == {"linearize", "schur", "cholesky_solve", "step_cost"} and all(v > 0 for v in ph.values())
     ctx.close()
     P, sm, _ = gpu_solve(p)
