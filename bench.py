@@ -75,6 +75,7 @@ def parse():
     ap.add_argument("--only-orb-features", action="store_true", help="run only the ORB extraction leg (tuning)")
     ap.add_argument("--only-ba", action="store_true", help="run only the bundle-adjustment leg (tuning)")
     ap.add_argument("--only-c3", action="store_true", help="run only the 200-image SIFT (config 3) leg (profiling)")
+    ap.add_argument("--no-ba-calls", action="store_true", help="skip the BA call-pattern replay (SfM.cpp:235/371)")
     ap.add_argument("--ba-cams", type=int, default=200)
     ap.add_argument("--ba-points", type=int, default=200_000)
     ap.add_argument("--ba-cpu-iters", type=int, default=2, help="LM iterations of the CPU BA baseline sample")
@@ -111,6 +112,8 @@ def main():
 
     if args.only_ba:
         res = bench_ba(args, rank, world, local)
+        if world == 1 and not args.no_ba_calls:
+            res["calls"] = bench_ba_calls(args)
         if rank == 0:
             print(json.dumps(res), flush=True)
         if world > 1:
@@ -140,6 +143,8 @@ def main():
     if args.workload == "sift" and not args.no_c3:
         c3 = bench_match("c3", args, rank, world, local)
     ba_res = None if args.no_ba else bench_ba(args, rank, world, local)
+    if ba_res is not None and world == 1 and not args.no_ba_calls:
+        ba_res["calls"] = bench_ba_calls(args)
     mvs_res = None if args.no_mvs else bench_mvs(args, rank, world, local)
     feat_res = None if args.no_features else bench_features(args, rank, world, local)
     orbf_res = None if args.no_orb_features else bench_features_orb(args, rank, world, local)
@@ -540,6 +545,55 @@ def bench_ba(args, rank, world, local):
         except Exception as e:   # pragma: no cover
             res["cpu_baseline"] = {"error": str(e)}
     return res
+
+
+def bench_ba_calls(args):
+    """The reference's BA call pattern (SfM.cpp:235 / :371): BundleAdjustment after every registered
+    camera, on a growing scene.  Replayed on the C5 ring (synth.ba_registered: the first n cameras,
+    points seen by >= 2 of them) for n = 20, 40, ..., 200 through one solver context, as
+    sfmx_ba_solve's per-device cache does; per call the end-to-end ms (host arrays in, results out)
+    split into the host setup (ordering + groups, device allocation, uploads, plan) and the LM
+    minimiser, plus a cold call (fresh context) at the C5 size.  Rank 0, one GPU."""
+    from sfmx import ba, synth
+    base = synth.ba_problem(args.ba_cams, args.ba_points)
+    calls, ctx = [], None
+    sizes = list(range(20, args.ba_cams + 1, 20))
+    if sizes[-1] != args.ba_cams:
+        sizes.append(args.ba_cams)
+    try:
+        for n in sizes:
+            P = ba.BAProblem(**synth.ba_registered(base, n))
+            t0 = time.perf_counter()
+            if ctx is None:
+                ctx = ba.BAContext(P)
+            else:
+                ctx.update(P)
+            sm, _ = ctx.run()
+            ctx.get(P)
+            wall = (time.perf_counter() - t0) * 1e3
+            su = ctx.setup_ms()
+            it = sm["num_successful_steps"] + sm["num_unsuccessful_steps"]
+            calls.append({"cams": n, "points": len(P.points), "obs": len(P.obs_point), "ms": wall, "lm_ms": sm["total_ms"],
+                          "setup_ms": su, "iterations": it, "setup_frac": (wall - sm["total_ms"]) / wall})
+    finally:
+        if ctx is not None:
+            ctx.close()
+    P = ba.BAProblem(**synth.ba_registered(base, args.ba_cams))
+    t0 = time.perf_counter()
+    cold = ba.BAContext(P)
+    try:
+        sm, _ = cold.run()
+        cold.get(P)
+        cold_ms = (time.perf_counter() - t0) * 1e3
+        cold_su = cold.setup_ms()
+    finally:
+        cold.close()
+    last = calls[-1]
+    return {"what": "BundleAdjustment after every registered camera (SfM.cpp:235 / :371), C5 ring grown 20 -> "
+                    f"{args.ba_cams} cameras; one context reused (sfmx_ba_update, = sfmx_ba_solve's cache)",
+            "calls": calls, "c5_call_ms": last["ms"], "c5_setup_frac": last["setup_frac"],
+            "c5_cold_call": {"ms": cold_ms, "lm_ms": sm["total_ms"], "setup_ms": cold_su,
+                             "setup_frac": (cold_ms - sm["total_ms"]) / cold_ms}}
 
 
 def ba_roofline(args, ms_per_iter, world):

@@ -94,9 +94,14 @@ int sfmx_ba_default_options(sfmx_ba_options* opt);
 /* Solve in place (the reference's doBundleAdjustment + write-back).  trace
  * (optional) receives 3 doubles per iteration: cost, trust-region radius,
  * step accepted (1/0); returns the number of trace rows written (>= 0) or a
- * negative SFMX_E* code. */
+ * negative SFMX_E* code.  The library keeps one solver context per device between
+ * calls (the reference adjusts a growing scene after every registered camera,
+ * SfM.cpp:235 / :371): its HIP stream, pinned memory and device buffers are reused
+ * and the factorization plan too while the camera co-visibility is unchanged.
+ * Calls are serialised by a lock; sfmx_ba_release_cache frees the contexts. */
 int sfmx_ba_solve(sfmx_ba_problem* problem, const sfmx_ba_options* opt, sfmx_ba_summary* summary,
                   double* trace, int32_t trace_cap);
+int sfmx_ba_release_cache(void);
 
 /* ---- context API (bench / multi-GPU) --------------------------------------
  * A context keeps the problem resident in HBM.  For point-sharded multi-GPU
@@ -119,6 +124,15 @@ int sfmx_ba_set_allreduce(sfmx_ba_ctx* ctx, sfmx_allreduce_fn fn, void* user);
  * max_iterations iterations (<= 0: options.max_num_iterations). */
 int sfmx_ba_run(sfmx_ba_ctx* ctx, int32_t max_iterations, sfmx_ba_summary* summary,
                 double* trace, int32_t trace_cap);
+/* Replace the context's problem by another one of any topology (a grown scene): the
+ * context's device buffers are reused when large enough and its factorization plan when
+ * the camera co-visibility is unchanged (single rank).  Options and the all-reduce
+ * callback stay.  Then sfmx_ba_run / sfmx_ba_get as after sfmx_ba_create. */
+int sfmx_ba_update(sfmx_ba_ctx* ctx, const sfmx_ba_problem* problem);
+/* Host-side setup time of the last create / update (ms): [0] point ordering + groups,
+ * [1] device allocation, [2] uploads (pinned staging, incl. the parameters), [3] the
+ * factorization plan (built at the next run; 0 when reused), [4] total.  n = entries. */
+int sfmx_ba_setup_ms(sfmx_ba_ctx* ctx, double* ms, int32_t n);
 /* Copy the current parameters back into problem->points/poses/intr. */
 int sfmx_ba_get(sfmx_ba_ctx* ctx, sfmx_ba_problem* problem);
 /* Reset the parameters from problem->points/poses/intr (same topology). */

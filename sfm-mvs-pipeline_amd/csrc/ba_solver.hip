@@ -20,6 +20,7 @@
 #include "ba_chol.hpp"
 #include "ba_plan.hpp"
 #include "diag.hpp"
+#include "host_par.hpp"
 
 #include <algorithm>
 #include <chrono>
@@ -27,6 +28,7 @@
 #include <cstring>
 #include <limits>
 #include <map>
+#include <mutex>
 #include <string>
 #include <cstdlib>
 #include <unordered_map>
@@ -51,20 +53,29 @@ int fail(int code, const std::string& m) { sfmx::set_last_error(m.c_str()); retu
     } while (0)
 #define RC(expr) do { int rc_ = (expr); if (rc_) return rc_; } while (0)
 
+// Device buffer that keeps its allocation across problems (sfmx_ba_update, the cached context of
+// sfmx_ba_solve): alloc(b) reuses the block when it holds b bytes, else reallocates with 25 %
+// headroom (a scene grows by a few cameras per BundleAdjustment call, SfM.cpp:235 / :371).
 struct Buf {
     void* p = nullptr;
-    size_t bytes = 0;
+    size_t bytes = 0, cap = 0;
     int alloc(size_t b) {
+        b = std::max<size_t>(b, 64);
+        if (p && b <= cap) { bytes = b; return SFMX_OK; }
+        const size_t want = p ? std::max(b, cap + cap / 4) : b;   // first allocation exact, regrowth with headroom
         if (p) { (void)hipFree(p); p = nullptr; }
-        bytes = std::max<size_t>(b, 64);
-        hipError_t e = hipMalloc(&p, bytes);
-        if (e != hipSuccess) { p = nullptr; return fail(SFMX_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)); }
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) { p = nullptr; cap = bytes = 0; return fail(SFMX_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)); }
+        cap = want;
+        bytes = b;
         return SFMX_OK;
     }
-    void release() { if (p) (void)hipFree(p); p = nullptr; }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = bytes = 0; }
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+struct HostScratch;                       // the host setup's vectors, kept between calls (below)
+void destroy_scratch(HostScratch* h);
 inline unsigned nblk(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
 constexpr int MAX_NPAD = 16 * 1024;   // rows of S_cc: the back solve keeps its vector in LDS
 
@@ -83,6 +94,7 @@ struct sfmx_ba_ctx {
     int n_intr = 0, intr_len = 0;   // caller's blocks and the length of its intr array
     std::vector<int> isrc;
     Buf pim, pcc;
+    Buf xyraw, operm_d;   // the caller's obs_xy and the internal -> caller observation map (setup)
     int64_t n = 0, ne = 0;
     int nf = 0, npad = 0, T = 0, RW = 0;
     sfmx_allreduce_fn ar = nullptr;
@@ -129,12 +141,22 @@ struct sfmx_ba_ctx {
     int spec_maxit = 0;
     double lm_init[LM_N] = {};   // host source of the initial device LM state (outlives its async copy)
     unsigned seq = 0;
+    // uploads go through a pinned staging arena (bump-allocated; the stream is synchronised before
+    // it is reused), not pageable memory
+    char* stage = nullptr;
+    size_t stage_cap = 0, stage_off = 0;
+    // host-side setup of the last create / update: [0] ordering + topology, [1] device allocation,
+    // [2] uploads, [3] factorization plan, [4] total (ms)
+    double setup_ms[5] = {0, 0, 0, 0, 0};
+    std::vector<char> plan_adj;   // the co-visibility the current plan was built from (reused if equal)
+    int plan_K = 0;
+    HostScratch* hscr = nullptr;
     ~sfmx_ba_ctx() {
         Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
                       &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
-                      &failf, &partA, &lmst, &camscr, &pim, &pcc};
+                      &failf, &partA, &lmst, &camscr, &pim, &pcc, &xyraw, &operm_d};
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
@@ -142,6 +164,8 @@ struct sfmx_ba_ctx {
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (st) (void)hipStreamDestroy(st);
         if (hs) (void)hipHostFree(hs);
+        if (stage) (void)hipHostFree(stage);
+        destroy_scratch(hscr);
         (void)hipSetDevice(prev);
     }
 };
@@ -160,10 +184,42 @@ int allreduce(sfmx_ba_ctx* c, double* buf, int64_t count, int op) {
     return SFMX_OK;
 }
 
+// bytes of pinned staging for one upload; the arena restarts (after a stream sync) when full
+void* stage_bytes(sfmx_ba_ctx* c, size_t n) {
+    n = (n + 255) & ~(size_t)255;
+    if (c->stage_off + n > c->stage_cap) {
+        if (hipStreamSynchronize(c->st) != hipSuccess) return nullptr;
+        c->stage_off = 0;
+        if (n > c->stage_cap) {
+            if (c->stage) (void)hipHostFree(c->stage);
+            c->stage = nullptr;
+            c->stage_cap = std::max(n, c->stage_cap * 2);
+            if (hipHostMalloc(reinterpret_cast<void**>(&c->stage), c->stage_cap, hipHostMallocDefault) != hipSuccess) {
+                c->stage_cap = 0;
+                return nullptr;
+            }
+        }
+    }
+    void* p = c->stage + c->stage_off;
+    c->stage_off += n;
+    return p;
+}
+
 template <class T>
-int upload(Buf& b, const std::vector<T>& v, hipStream_t st) {
+int upload(sfmx_ba_ctx* c, Buf& b, const std::vector<T>& v) {
     RC(b.alloc(sizeof(T) * std::max<size_t>(v.size(), 1)));
-    if (!v.empty()) HIPCHK(hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st));
+    if (v.empty()) return SFMX_OK;
+    void* h = stage_bytes(c, sizeof(T) * v.size());
+    if (!h) return fail(SFMX_ENOMEM, "pinned staging buffer");
+    const size_t nb = sizeof(T) * v.size();
+    if (nb < ((size_t)1 << 20)) {
+        std::memcpy(h, v.data(), nb);
+    } else {   // large arrays: the copy into pinned memory on several host threads
+        sfmx::parallel_ranges((int64_t)nb, 16, [&](int64_t b0, int64_t b1) {
+            std::memcpy(static_cast<char*>(h) + b0, reinterpret_cast<const char*>(v.data()) + b0, (size_t)(b1 - b0));
+        });
+    }
+    HIPCHK(hipMemcpyAsync(b.p, h, sizeof(T) * v.size(), hipMemcpyHostToDevice, c->st));
     return SFMX_OK;
 }
 
@@ -448,6 +504,7 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
 // copies of the schedule, and S / W / the Schur terms sized by it.
 int ensure_plan(sfmx_ba_ctx* c) {
     if (c->planned) return SFMX_OK;
+    const auto t_plan = std::chrono::steady_clock::now();
     const int C = c->C;
     std::vector<char> adj = c->adj;
     if (c->ar && C > 1) {   // global co-visibility: sum of the ranks' upper triangles
@@ -479,11 +536,11 @@ int ensure_plan(sfmx_ba_ctx* c) {
     for (size_t i = 0; i < tk.size(); ++i) tk[i] = make_int4(pl.tasks[i].a, pl.tasks[i].b, pl.tasks[i].s0, pl.tasks[i].s1);
     hipStream_t st = c->st;
     int rc;
-    if ((rc = upload(c->camrow, pl.camrow, st)) || (rc = upload(c->padrows, pl.padrows, st)) ||
-        (rc = upload(c->rowmap, pl.rowmap, st)) || (rc = upload(c->leaves, pl.leaves, st)) ||
-        (rc = upload(c->ptasks, tk, st)) || (rc = upload(c->psrc, pl.src, st)) ||
-        (rc = upload(c->lvl_start, pl.lvl_start, st)) || (rc = upload(c->lvl_panels, pl.lvl_panels, st)) ||
-        (rc = upload(c->bs_start, pl.bs_start, st)) || (rc = upload(c->bs_k, pl.bs_k, st)))
+    if ((rc = upload(c, c->camrow, pl.camrow)) || (rc = upload(c, c->padrows, pl.padrows)) ||
+        (rc = upload(c, c->rowmap, pl.rowmap)) || (rc = upload(c, c->leaves, pl.leaves)) ||
+        (rc = upload(c, c->ptasks, tk)) || (rc = upload(c, c->psrc, pl.src)) ||
+        (rc = upload(c, c->lvl_start, pl.lvl_start)) || (rc = upload(c, c->lvl_panels, pl.lvl_panels)) ||
+        (rc = upload(c, c->bs_start, pl.bs_start)) || (rc = upload(c, c->bs_k, pl.bs_k)))
         return rc;
     RC(c->SR.alloc(sizeof(double) * c->sr_count));
     {   // nonzero lower tiles (diagonal included): the compact all-reduce payload
@@ -492,7 +549,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
             for (int b = 0; b <= a; ++b)
                 if (pl.nz[(size_t)a * pl.T + b]) nzt.push_back(make_int2(a, b));
         c->n_nztiles = (int)nzt.size();
-        RC(upload(c->nztiles, nzt, st));
+        RC(upload(c, c->nztiles, nzt));
         RC(c->packbuf.alloc(sizeof(double) * ((size_t)c->n_nztiles * NB * NB + (c->sr_count - (size_t)pl.npad * pl.npad))));
     }
     RC(c->Wt.alloc(sizeof(double) * (size_t)pl.T * NB * NB));
@@ -502,7 +559,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
         std::vector<int> order;
         for (int l = pl.height; l >= 0; --l)
             for (int t = pl.lvl_start[l]; t < pl.lvl_start[l + 1]; ++t) order.push_back(pl.lvl_panels[t]);
-        RC(upload(c->border, order, st));
+        RC(upload(c, c->border, order));
         RC(c->zbuf.alloc(sizeof(double) * (size_t)pl.npad));
         RC(c->dagctr.alloc(sizeof(int) * (size_t)((pl.T + 2 + 3) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->dagctr.p, 0, c->dagctr.bytes, st));
@@ -526,7 +583,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
             max_slots = std::max(max_slots, slot);
             c->part_start.push_back((int)parts.size());
         }
-        RC(upload(c->parts, parts, st));
+        RC(upload(c, c->parts, parts));
         // chol_factor: the leaves, then every level's parts in the same order, product slots unique over
         // the launch; need = the versions (finished tasks, leaf inverse included) of A_ak, A_bk, (k, k)
         // and of A_ab before the task.  A plan whose source tile is not final at its use (never built
@@ -566,8 +623,8 @@ int ensure_plan(sfmx_ba_ctx* c) {
         }
         c->n_ditems = (int)items.size();
         c->n_ver = nver;
-        RC(upload(c->ditems, items, st));
-        RC(upload(c->dneed, need, st));
+        RC(upload(c, c->ditems, items));
+        RC(upload(c, c->dneed, need));
         RC(c->dctr.alloc(sizeof(int) * (size_t)((nver + 2 + 3) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->dctr.p, 0, c->dctr.bytes, st));
         const char* ed = SFMX_DIAG_ENV("SFMX_BA_DAG");
@@ -589,6 +646,11 @@ int ensure_plan(sfmx_ba_ctx* c) {
     if (e != hipSuccess) return fail(SFMX_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(e));
     HIPCHK(hipStreamSynchronize(st));
     c->planned = true;
+    c->plan_adj = c->adj;
+    c->plan_K = c->K;
+    const double pms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_plan).count();
+    c->setup_ms[3] = pms;
+    c->setup_ms[4] += pms;
     return SFMX_OK;
 }
 
@@ -781,10 +843,13 @@ int validate(const sfmx_ba_problem* pb) {
 int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
     DeviceGuard dg(c->device);
     double* x = c->x.as<double>();
-    std::vector<double> pts(3 * (size_t)c->P);
-    for (int q = 0; q < c->P; ++q)
-        for (int i = 0; i < 3; ++i) pts[3 * (size_t)q + i] = pb->points[3 * (size_t)c->pperm[q] + i];
-    if (c->P) HIPCHK(hipMemcpyAsync(x, pts.data(), sizeof(double) * 3 * c->P, hipMemcpyHostToDevice, c->st));
+    if (c->P) {
+        double* pts = static_cast<double*>(stage_bytes(c, sizeof(double) * 3 * (size_t)c->P));
+        if (!pts) return fail(SFMX_ENOMEM, "pinned staging buffer");
+        for (int q = 0; q < c->P; ++q)
+            for (int i = 0; i < 3; ++i) pts[3 * (size_t)q + i] = pb->points[3 * (size_t)c->pperm[q] + i];
+        HIPCHK(hipMemcpyAsync(x, pts, sizeof(double) * 3 * c->P, hipMemcpyHostToDevice, c->st));
+    }
     if (c->C) HIPCHK(hipMemcpyAsync(x + c->ne, pb->poses, sizeof(double) * 6 * c->C, hipMemcpyHostToDevice, c->st));
     std::vector<double> iv(c->K, 0.0);   // the border: referenced blocks, zero padding
     for (int j = 0; j < c->K; ++j) if (c->isrc[j] >= 0) iv[j] = pb->intr[c->isrc[j]];
@@ -793,38 +858,101 @@ int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
     return SFMX_OK;
 }
 
-// Locality order (internal only; results are reported in the caller's order):
-// points sorted by their sorted camera lists (points seen by the same cameras
-// become neighbours, so a point group spans few cameras), observations
-// point-major in that order.
-void locality_order(const sfmx_ba_problem* pb, std::vector<int>& pperm, std::vector<int>& operm) {
-    const int P = pb->n_points, O = pb->n_obs;
-    std::vector<int> start(P + 1, 0), obs(O);
+// Locality order (internal only; results are reported in the caller's order): points sorted by
+// their sorted camera lists (points seen by the same cameras become neighbours, so a point group
+// spans few cameras), observations point-major in that order.  The sort key is the list's first
+// cameras, as many as fit 64 bits at ceil(log2(C + 2)) bits each, at most 6 (lexicographic, a
+// shorter list first), ties keep the caller's order (an LSD radix sort is stable).  Fills pperm / operm (internal -> caller), rop /
+// roc (internal observations) and pt_start.
+struct Ordered {   // rxy is gathered on the device (ba_gather_xy) from the caller's obs_xy
+    std::vector<int> pperm, operm, rop, roc, pt_start;
+    std::vector<int> start, obs, tmp;          // scratch, kept with the context between calls
+    std::vector<uint64_t> key, ktmp;
+    std::vector<uint32_t> cnt;
+};
+
+void order_problem(const sfmx_ba_problem* pb, Ordered& od) {
+    const int P = pb->n_points, O = pb->n_obs, C = pb->n_cams;
+    constexpr int PIECES = 64;   // fixed ranges (host_par.hpp): the same result on every host
+    std::vector<int>& start = od.start;
+    std::vector<int>& obs = od.obs;
+    start.assign(P + 1, 0);
+    obs.resize(O);
     for (int i = 0; i < O; ++i) start[pb->obs_point[i] + 1]++;
     for (int p = 0; p < P; ++p) start[p + 1] += start[p];
-    {
+    bool point_major = true;   // the reference adds residuals point by point: obs[a] == a then
+    for (int i = 1; i < O && point_major; ++i) point_major = pb->obs_point[i] >= pb->obs_point[i - 1];
+    if (point_major) {
+        for (int i = 0; i < O; ++i) obs[i] = i;
+    } else {
         std::vector<int> f(start.begin(), start.end() - 1);
         for (int i = 0; i < O; ++i) obs[f[pb->obs_point[i]]++] = i;
     }
-    std::vector<int> cams(O);   // per point: its cameras, sorted
-    for (int p = 0; p < P; ++p) {
-        for (int a = start[p]; a < start[p + 1]; ++a) cams[a] = pb->obs_cam[obs[a]];
-        std::sort(cams.begin() + start[p], cams.begin() + start[p + 1]);
-    }
+    int kb = 1;   // bits per camera (c + 1, 0 = none) and cameras per 64-bit key
+    while ((1ll << kb) < (long long)C + 2) ++kb;
+    const int nk = std::min(6, 64 / kb);
+    std::vector<uint64_t>& key = od.key;
+    key.resize(P);
+    sfmx::parallel_ranges(P, PIECES, [&](int64_t p0, int64_t p1) {
+        for (int64_t p = p0; p < p1; ++p) {
+            uint32_t lo[6] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u};   // the nk smallest cameras, sorted
+            for (int a = start[p]; a < start[p + 1]; ++a) {
+                uint32_t v = (uint32_t)pb->obs_cam[obs[a]];
+                for (int j = 0; j < nk; ++j)
+                    if (v < lo[j]) std::swap(v, lo[j]);
+            }
+            uint64_t k = 0;
+            for (int j = 0; j < nk; ++j) k = (k << kb) | (lo[j] == ~0u ? 0u : lo[j] + 1);
+            key[p] = k;
+        }
+    });
+    // LSD radix sort of (key, p) pairs over the key's nk * kb bits, 16 per pass (stable), passes
+    // whose digit is constant skipped
+    std::vector<int>& pperm = od.pperm;
     pperm.resize(P);
     for (int p = 0; p < P; ++p) pperm[p] = p;
-    std::stable_sort(pperm.begin(), pperm.end(), [&](int a, int b) {
-        return std::lexicographical_compare(cams.begin() + start[a], cams.begin() + start[a + 1],
-                                            cams.begin() + start[b], cams.begin() + start[b + 1]);
+    {
+        std::vector<int>& tmp = od.tmp;
+        std::vector<uint64_t>& ktmp = od.ktmp;
+        std::vector<uint32_t>& cnt = od.cnt;
+        tmp.resize(P);
+        ktmp.resize(P);
+        cnt.resize(65536 + 1);
+        for (int sh = 0; sh < nk * kb; sh += 16) {
+            std::fill(cnt.begin(), cnt.end(), 0u);
+            for (int i = 0; i < P; ++i) cnt[((key[i] >> sh) & 0xffff) + 1]++;
+            bool one = false;
+            for (size_t d = 1; d < cnt.size(); ++d) one |= cnt[d] == (uint32_t)P;
+            if (one) continue;
+            for (size_t d = 1; d < cnt.size(); ++d) cnt[d] += cnt[d - 1];
+            for (int i = 0; i < P; ++i) {
+                const uint32_t j = cnt[(key[i] >> sh) & 0xffff]++;
+                tmp[j] = pperm[i];
+                ktmp[j] = key[i];
+            }
+            pperm.swap(tmp);
+            key.swap(ktmp);
+        }
+    }
+    od.pt_start.assign(P + 1, 0);
+    for (int q = 0; q < P; ++q) od.pt_start[q + 1] = od.pt_start[q] + start[pperm[q] + 1] - start[pperm[q]];
+    od.operm.resize(O); od.rop.resize(O); od.roc.resize(O);
+    sfmx::parallel_ranges(P, PIECES, [&](int64_t q0, int64_t q1) {
+        for (int64_t q = q0; q < q1; ++q) {
+            const int p = pperm[q];
+            for (int a = start[p], k = od.pt_start[q]; a < start[p + 1]; ++a, ++k) {
+                const int o = obs[a];
+                od.operm[k] = o;
+                od.rop[k] = (int)q;
+                od.roc[k] = pb->obs_cam[o];
+            }
+        }
     });
-    operm.clear();
-    operm.reserve(O);
-    for (int q = 0; q < P; ++q)
-        for (int a = start[pperm[q]]; a < start[pperm[q] + 1]; ++a) operm.push_back(obs[a]);
 }
 
 // Point groups, chunks, local cameras, assembly task lists and camera slot lists (see ba_group.hpp).
-struct Topology {
+struct TopoSeg;
+struct Topology {   // kept with the context: its vectors keep their capacity between calls
     std::vector<Grp> grp;
     std::vector<Chunk> chk;
     std::vector<Batch> bat;
@@ -834,13 +962,34 @@ struct Topology {
     std::vector<AEnt> ents;
     long long sg_total = 0, h_total = 0;
     int rg_total = 0, dp_max = 16;
+    std::vector<TopoSeg>* seg = nullptr;   // per-segment scratch (owned by the caller)
+    void clear() {
+        grp.clear(); chk.clear(); bat.clear(); gcam.clear(); cref_start.clear(); cref.clear(); lcrow.clear();
+        tasks.clear(); ents.clear();
+        sg_total = h_total = 0; rg_total = 0; dp_max = 16;
+    }
 };
 
-void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start, const int* obs_cam, Topology& tp) {
-    tp.obs_lc.assign(O, 0);
-    tp.obs_row.assign(O, 0);
-    std::vector<int> cur;   // sorted union of the open group's cameras
-    int g_p0 = 0, g_obs = 0;
+// One segment of the greedy point-group scan: points [s0, s1) (groups never span segments);
+// offsets in the group records are local to the segment until the merge.
+struct TopoSeg {
+    std::vector<Grp> grp;
+    std::vector<Chunk> chk;
+    std::vector<Batch> bat;
+    std::vector<int> gcam, lcrow;
+    long long sg_total = 0, h_total = 0;
+    int rg_total = 0, dp_max = 16;
+    void clear() { grp.clear(); chk.clear(); bat.clear(); gcam.clear(); lcrow.clear(); sg_total = h_total = 0; rg_total = 0; dp_max = 16; }
+};
+
+void topo_segment(int s0, int s1, int K, const std::vector<int>& pt_start, const int* obs_cam, short* obs_lc,
+                  short* obs_row, TopoSeg& tp) {
+    std::vector<int> cur, pc, uni, cnt, fill;
+    tp.clear();
+    int g_p0 = s0, g_obs = 0;
+    auto lc_of = [](const std::vector<int>& cams, int cm) {
+        return (int)(std::lower_bound(cams.begin(), cams.end(), cm) - cams.begin());
+    };
     auto add_group = [&](int p0, int p1, const std::vector<int>& cams, bool big) {
         Grp G{};
         G.o0 = pt_start[p0]; G.o1 = pt_start[p1]; G.p0 = p0; G.p1 = p1;
@@ -879,10 +1028,9 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
                 Chunk ch{pt_start[q], pt_start[q], q - p0, q - p0, (int)tp.lcrow.size(), 0, 0, 0};
                 while (q < p1 && pt_start[q + 1] - ch.o0 <= GCH) { ++q; }
                 ch.o1 = pt_start[q]; ch.q1 = q - p0;
-                std::vector<int> cnt(cams.size(), 0);
-                for (int o = ch.o0; o < ch.o1; ++o)
-                    cnt[std::lower_bound(cams.begin(), cams.end(), obs_cam[o]) - cams.begin()]++;
-                std::vector<int> fill(cams.size());
+                cnt.assign(cams.size(), 0);
+                for (int o = ch.o0; o < ch.o1; ++o) cnt[lc_of(cams, obs_cam[o])]++;
+                fill.resize(cams.size());
                 int row = 0;
                 for (size_t lc = 0; lc < cams.size(); ++lc) {
                     tp.lcrow.push_back(row);
@@ -892,8 +1040,8 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
                 tp.lcrow.push_back(row);
                 ch.nrows = row;
                 for (int o = ch.o0; o < ch.o1; ++o) {
-                    const int lc = (int)(std::lower_bound(cams.begin(), cams.end(), obs_cam[o]) - cams.begin());
-                    tp.obs_row[o] = (short)fill[lc];
+                    const int lc = lc_of(cams, obs_cam[o]);
+                    obs_row[o] = (short)fill[lc];
                     fill[lc] += 2;
                 }
                 tp.chk.push_back(ch);
@@ -901,12 +1049,10 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
             }
         }
         for (int cm : cams) tp.gcam.push_back(cm);
-        for (int o = G.o0; o < G.o1; ++o)
-            tp.obs_lc[o] = (short)(std::lower_bound(cams.begin(), cams.end(), obs_cam[o]) - cams.begin());
+        for (int o = G.o0; o < G.o1; ++o) obs_lc[o] = (short)lc_of(cams, obs_cam[o]);
         tp.grp.push_back(G);
     };
-    std::vector<int> pc, uni;
-    for (int p = 0; p < P; ++p) {
+    for (int p = s0; p < s1; ++p) {
         const int m = pt_start[p + 1] - pt_start[p];
         pc.assign(obs_cam + pt_start[p], obs_cam + pt_start[p + 1]);
         std::sort(pc.begin(), pc.end());
@@ -929,17 +1075,56 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
         }
         g_obs += m;
     }
-    if (P > g_p0) add_group(g_p0, P, cur, false);
+    if (s1 > g_p0) add_group(g_p0, s1, cur, false);
+}
+
+// Points in segments of SEG_PTS (a fixed size: the same groups on every host), scanned in
+// parallel (host_par.hpp), merged in segment order; then the camera slots and assembly tasks.
+constexpr int SEG_PTS = 8192;
+
+void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start, const int* obs_cam, Topology& tp) {
+    tp.clear();
+    tp.obs_lc.assign(O, 0);
+    tp.obs_row.assign(O, 0);
+    const int nseg = std::max(1, (P + SEG_PTS - 1) / SEG_PTS);
+    std::vector<TopoSeg> own;
+    std::vector<TopoSeg>& seg = tp.seg ? *tp.seg : own;
+    if ((int)seg.size() < nseg) seg.resize(nseg);
+    sfmx::parallel_items(nseg, [&](int i) {
+        topo_segment(i * SEG_PTS, std::min(P, (i + 1) * SEG_PTS), K, pt_start, obs_cam, tp.obs_lc.data(),
+                     tp.obs_row.data(), seg[i]);
+    });
+    {   // merge: shift every segment's local offsets
+        size_t ng = 0, nc = 0, nb = 0, ngc = 0, nl = 0;
+        for (int i = 0; i < nseg; ++i) { const TopoSeg& g = seg[i]; ng += g.grp.size(); nc += g.chk.size(); nb += g.bat.size(); ngc += g.gcam.size(); nl += g.lcrow.size(); }
+        tp.grp.reserve(ng); tp.chk.reserve(nc); tp.bat.reserve(nb); tp.gcam.reserve(ngc); tp.lcrow.reserve(nl);
+        for (int i = 0; i < nseg; ++i) {
+            TopoSeg& g = seg[i];
+            const int cam0 = (int)tp.gcam.size(), ch0 = (int)tp.chk.size(), b0 = (int)tp.bat.size(), l0 = (int)tp.lcrow.size();
+            for (Grp G : g.grp) {
+                G.cam_off += cam0; G.ch0 += ch0; G.b0 += b0; G.rg_off += tp.rg_total;
+                if (G.big) G.h_off += tp.h_total; else G.sg_off += tp.sg_total;
+                tp.grp.push_back(G);
+            }
+            for (Chunk ch : g.chk) { ch.lc0 += l0; tp.chk.push_back(ch); }
+            tp.bat.insert(tp.bat.end(), g.bat.begin(), g.bat.end());
+            tp.gcam.insert(tp.gcam.end(), g.gcam.begin(), g.gcam.end());
+            tp.lcrow.insert(tp.lcrow.end(), g.lcrow.begin(), g.lcrow.end());
+            tp.rg_total += g.rg_total; tp.sg_total += g.sg_total; tp.h_total += g.h_total;
+            tp.dp_max = std::max(tp.dp_max, g.dp_max);
+        }
+    }
     // camera slots: per camera, its (group, local camera) slots in group order
+    std::vector<int> slot_g(tp.gcam.size());
+    for (int g = 0; g < (int)tp.grp.size(); ++g)
+        for (int lc = 0; lc < tp.grp[g].u; ++lc) slot_g[tp.grp[g].cam_off + lc] = g;
     tp.cref_start.assign(C + 1, 0);
-    for (const Grp& G : tp.grp)
-        for (int lc = 0; lc < G.u; ++lc) tp.cref_start[tp.gcam[G.cam_off + lc] + 1]++;
+    for (int cm : tp.gcam) tp.cref_start[cm + 1]++;
     for (int c = 0; c < C; ++c) tp.cref_start[c + 1] += tp.cref_start[c];
     tp.cref.assign(tp.cref_start[C], 0);
     {
         std::vector<int> f(tp.cref_start.begin(), tp.cref_start.end() - 1);
-        for (const Grp& G : tp.grp)
-            for (int lc = 0; lc < G.u; ++lc) tp.cref[f[tp.gcam[G.cam_off + lc]]++] = G.cam_off + lc;
+        for (int sl = 0; sl < (int)tp.gcam.size(); ++sl) tp.cref[f[tp.gcam[sl]]++] = sl;
     }
     // assembly tasks: pose blocks (a <= b) with their (group, la, lb) lists in group order, then
     // pose-intrinsics blocks per camera, then the intrinsics block
@@ -954,26 +1139,35 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
         else { e.b0 = G.sg_off + (long long)(6 * la) * dim + 6 * lb; e.b1 = 0; }
         return e;
     };
-    std::map<std::pair<int, int>, std::vector<AEnt>> pairs;
-    for (int g = 0; g < (int)tp.grp.size(); ++g) {
-        const Grp& G = tp.grp[g];
-        for (int la = 0; la < G.u; ++la)
-            for (int lb = la; lb < G.u; ++lb)
-                pairs[{tp.gcam[G.cam_off + la], tp.gcam[G.cam_off + lb]}].push_back(ent(g, la, lb));
-    }
-    for (auto& kv : pairs) {
-        ATask t{0, kv.first.first, kv.first.second, (int)tp.ents.size(), 0, 0, 0, 0};
-        tp.ents.insert(tp.ents.end(), kv.second.begin(), kv.second.end());
-        t.l1 = (int)tp.ents.size();
-        tp.tasks.push_back(t);
+    {   // (camera a, camera b) keys in group order, stably sorted: tasks in key order, entries in group order
+        struct PairRef { uint64_t key; int g, la, lb; };
+        std::vector<PairRef> pr;
+        size_t npr = 0;
+        for (const Grp& G : tp.grp) npr += (size_t)G.u * (G.u + 1) / 2;
+        pr.reserve(npr);
+        for (int g = 0; g < (int)tp.grp.size(); ++g) {
+            const Grp& G = tp.grp[g];
+            for (int la = 0; la < G.u; ++la)
+                for (int lb = la; lb < G.u; ++lb)
+                    pr.push_back(PairRef{((uint64_t)(uint32_t)tp.gcam[G.cam_off + la] << 32) | (uint32_t)tp.gcam[G.cam_off + lb],
+                                         g, la, lb});
+        }
+        std::stable_sort(pr.begin(), pr.end(), [](const PairRef& x, const PairRef& y) { return x.key < y.key; });
+        tp.ents.reserve(pr.size() + tp.gcam.size() + tp.grp.size());
+        for (size_t i = 0; i < pr.size();) {
+            ATask t{0, (int)(pr[i].key >> 32), (int)(pr[i].key & 0xffffffffu), (int)tp.ents.size(), 0, 0, 0, 0};
+            size_t j = i;
+            for (; j < pr.size() && pr[j].key == pr[i].key; ++j) tp.ents.push_back(ent(pr[j].g, pr[j].la, pr[j].lb));
+            t.l1 = (int)tp.ents.size();
+            tp.tasks.push_back(t);
+            i = j;
+        }
     }
     for (int cm = 0; cm < C; ++cm) {
         ATask t{1, cm, 0, (int)tp.ents.size(), 0, 0, 0, 0};
         for (int e = tp.cref_start[cm]; e < tp.cref_start[cm + 1]; ++e) {
-            const int slot = tp.cref[e];
-            const int g = (int)(std::upper_bound(tp.grp.begin(), tp.grp.end(), slot,
-                                                 [](int s, const Grp& G) { return s < G.cam_off; }) - tp.grp.begin()) - 1;
-            tp.ents.push_back(ent(g, slot - tp.grp[g].cam_off, tp.grp[g].u));   // column block: the intrinsics rows
+            const int sl = tp.cref[e], g = slot_g[sl];
+            tp.ents.push_back(ent(g, sl - tp.grp[g].cam_off, tp.grp[g].u));   // column block: the intrinsics rows
         }
         t.l1 = (int)tp.ents.size();
         if (t.l1 > t.l0) tp.tasks.push_back(t);
@@ -985,42 +1179,38 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
     }
 }
 
-int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ctx** out) {
-    RC(validate(caller));
-    std::vector<int> pperm, operm, ipperm(caller->n_points), rop(caller->n_obs), roc(caller->n_obs);
-    std::vector<double> rxy(2 * (size_t)caller->n_obs);
-    locality_order(caller, pperm, operm);
-    for (int q = 0; q < caller->n_points; ++q) ipperm[pperm[q]] = q;
-    for (int q = 0; q < caller->n_obs; ++q) {
-        const int o = operm[q];
-        rop[q] = ipperm[caller->obs_point[o]];
-        roc[q] = caller->obs_cam[o];
-        rxy[2 * (size_t)q] = caller->obs_xy[2 * (size_t)o];
-        rxy[2 * (size_t)q + 1] = caller->obs_xy[2 * (size_t)o + 1];
-    }
-    sfmx_ba_options o;
-    sfmx_ba_default_options(&o);
-    if (opt) o = *opt;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(SFMX_EDEVICE, "no HIP device visible");
-    if (o.device < 0 || o.device >= ndev) return fail(SFMX_EINVAL, "device index out of range");
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, o.device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-        return fail(SFMX_EDEVICE, "sfmx BA kernels are built for gfx950 only");
-    auto* c = new (std::nothrow) sfmx_ba_ctx();
-    if (!c) return fail(SFMX_ENOMEM, "host allocation");
-    c->device = o.device;
-    c->opt = o;
-    c->pperm.swap(pperm);
-    c->operm.swap(operm);
+// Everything problem-dependent of a context: the locality order, the point groups, the device
+// copies of the topology and the state buffers (reused when they are large enough), the
+// parameters.  The factorization plan is kept when the camera co-visibility and the border are
+// unchanged (ensure_plan), else rebuilt at the next run.  Used by create and by sfmx_ba_update
+// (the reference's BundleAdjustment call after every registered camera, SfM.cpp:235 / :371).
+struct HostScratch {
+    Ordered od;
+    Topology tp;
+    std::vector<TopoSeg> seg;
+};
+void destroy_scratch(HostScratch* h) { delete h; }
+
+int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
+    using clk = std::chrono::steady_clock;
+    const auto t_start = clk::now();
+    auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
     DeviceGuard dg(c->device);
-    auto bail = [&](int rc) { delete c; return rc; };
-    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) return bail(fail(SFMX_EDEVICE, "stream"));
-    for (auto& e : c->ev) if (hipEventCreate(&e) != hipSuccess) return bail(fail(SFMX_EDEVICE, "event"));
-    if (hipHostMalloc(reinterpret_cast<void**>(&c->hs), sizeof(double) * sfmx_ba_ctx::HS_N,
-                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-        return bail(fail(SFMX_ENOMEM, "pinned scalar buffer"));
-    std::memset(c->hs, 0, sizeof(double) * sfmx_ba_ctx::HS_N);
+    if (!c->hscr) c->hscr = new (std::nothrow) HostScratch();
+    if (!c->hscr) return fail(SFMX_ENOMEM, "host allocation");
+    Ordered& od = c->hscr->od;
+    order_problem(caller, od);
+    std::vector<int>& rop = od.rop;
+    std::vector<int>& roc = od.roc;
+    c->pperm.swap(od.pperm);
+    c->operm.swap(od.operm);
+    auto bail = [](int rc) { return rc; };
+    // per-problem state starts over
+    c->isrc.clear();
+    c->multi = false;
+    c->n_intr = 0;
+    c->scaled = c->j_scaled = false;
+    c->stage_off = 0;
     const int P = caller->n_points, C = caller->n_cams, O = caller->n_obs;
     c->P = P; c->C = C; c->O = O; c->cx = caller->cx; c->cy = caller->cy;
     std::vector<int> pim_h;
@@ -1071,20 +1261,24 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
         }
     }
     const int K = c->K;
+    if (c->plan_K != K) c->planned = false;   // the border sizes S, W and the Schur terms
     c->ne = 3 * (int64_t)P;
     c->nf = 6 * C + K;
     c->n = c->ne + c->nf;
     c->RW = K + 1;
     if (6 * (int64_t)C > MAX_NPAD) return bail(fail(SFMX_EINVAL, "too many cameras for the reduced camera system (6C > 16384)"));
-    std::vector<int> pt_start(P + 1, 0);
-    for (int i = 0; i < O; ++i) pt_start[rop[i] + 1]++;
-    for (int p = 0; p < P; ++p) pt_start[p + 1] += pt_start[p];
-    Topology tp;
+    std::vector<int>& pt_start = od.pt_start;
+    Topology& tp = c->hscr->tp;
+    tp.seg = &c->hscr->seg;
     build_topology(P, C, O, K, pt_start, roc.data(), tp);
     // local camera co-visibility (the pose blocks this rank's points create)
     c->adj.assign((size_t)C * C, 0);
     for (const ATask& t : tp.tasks)
         if (t.type == 0 && t.a != t.b) c->adj[(size_t)t.a * C + t.b] = c->adj[(size_t)t.b * C + t.a] = 1;
+    // a plan is reused only when this graph is the one it was built from; ranks of a sharded solve
+    // rebuild on every update (the plan needs the co-visibility all-reduced over all of them)
+    if (c->adj != c->plan_adj || c->ar) c->planned = false;
+    c->setup_ms[0] = ms_since(t_start);
     c->ngroups = (int)tp.grp.size();
     c->ntasks = (int)tp.tasks.size();
     c->nslots = (int)tp.gcam.size();
@@ -1113,13 +1307,25 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
     }
     hipStream_t st = c->st;
     int rc;
-    if ((rc = upload(c->obs_point, rop, st)) || (rc = upload(c->obs_cam, roc, st)) || (rc = upload(c->obs_xy, rxy, st)) ||
-        (rc = upload(c->pt_start, pt_start, st)) || (rc = upload(c->grp, tp.grp, st)) || (rc = upload(c->chk, tp.chk, st)) || (rc = upload(c->bat, tp.bat, st)) ||
-        (rc = upload(c->gcam, tp.gcam, st)) || (rc = upload(c->obs_lc, tp.obs_lc, st)) ||
-        (rc = upload(c->obs_row, tp.obs_row, st)) || (rc = upload(c->lcrow, tp.lcrow, st)) ||
-        (rc = upload(c->tasks, tp.tasks, st)) || (rc = upload(c->ents, tp.ents, st)) ||
-        (rc = upload(c->cref_start, tp.cref_start, st)) || (rc = upload(c->cref, tp.cref, st)) ||
-        (rc = upload(c->pim, pim_h, st)) || (rc = upload(c->pcc, pcc_h, st)))
+    const auto t_up = clk::now();
+    // observed pixels: the caller's array as it is (no host shuffle), gathered into the internal
+    // order on the device
+    RC(c->xyraw.alloc(sizeof(double) * 2 * std::max<size_t>(O, 1)));
+    RC(c->obs_xy.alloc(sizeof(double) * 2 * std::max<size_t>(O, 1)));
+    if (O) HIPCHK(hipMemcpyAsync(c->xyraw.p, caller->obs_xy, sizeof(double) * 2 * (size_t)O, hipMemcpyHostToDevice, st));
+    RC(upload(c, c->operm_d, c->operm));
+    if (O) {
+        hipLaunchKernelGGL(ba_gather_xy, dim3(nblk(O)), dim3(256), 0, st, O, c->operm_d.as<int>(),
+                           c->xyraw.as<double2>(), c->obs_xy.as<double2>());
+        HIPCHK(hipGetLastError());
+    }
+    if ((rc = upload(c, c->obs_point, rop)) || (rc = upload(c, c->obs_cam, roc)) ||
+        (rc = upload(c, c->pt_start, pt_start)) || (rc = upload(c, c->grp, tp.grp)) || (rc = upload(c, c->chk, tp.chk)) || (rc = upload(c, c->bat, tp.bat)) ||
+        (rc = upload(c, c->gcam, tp.gcam)) || (rc = upload(c, c->obs_lc, tp.obs_lc)) ||
+        (rc = upload(c, c->obs_row, tp.obs_row)) || (rc = upload(c, c->lcrow, tp.lcrow)) ||
+        (rc = upload(c, c->tasks, tp.tasks)) || (rc = upload(c, c->ents, tp.ents)) ||
+        (rc = upload(c, c->cref_start, tp.cref_start)) || (rc = upload(c, c->cref, tp.cref)) ||
+        (rc = upload(c, c->pim, pim_h)) || (rc = upload(c, c->pcc, pcc_h)))
         return bail(rc);
     const size_t n = c->n, so = std::max(O, 1);
     const size_t ncams = (size_t)C * ncp(K) + K * (K + 1) / 2 + K;
@@ -1132,16 +1338,51 @@ int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ct
         {&c->gpart, 8 * (size_t)std::max(c->nslots, 1) * ncp(K)}, {&c->gpl, 8 * (size_t)std::max(c->ngroups, 1) * GP_N},
         {&c->scal, 8 * SC_N}, {&c->failf, 64}, {&c->lmst, 8 * LM_N}, {&c->camscr, 8 * (ncams + 5)},
         {&c->partA, 8 * (size_t)nblk(std::max<int64_t>(O, n))}};
+    const double up_ms = ms_since(t_up);
+    const auto t_al = clk::now();
     for (auto& a : allocs) if ((rc = a.b->alloc(a.bytes))) return bail(rc);
+    c->setup_ms[1] = ms_since(t_al);
+    const auto t_up2 = clk::now();
     HIPCHK(hipMemsetAsync(c->gpl.p, 0, c->gpl.bytes, st));
     // scale = 1 until (and unless) Jacobi scaling sets it
-    {
-        std::vector<double> ones(n, 1.0);
-        if (hipMemcpyAsync(c->scale.p, ones.data(), 8 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            return bail(fail(SFMX_EDEVICE, "upload"));
-    }
+    hipLaunchKernelGGL(ba_fill, dim3(nblk((int64_t)n)), dim3(256), 0, st, (int64_t)n, 1.0, c->scale.as<double>());
+    HIPCHK(hipGetLastError());
     if ((rc = set_params(c, caller))) return bail(rc);
+    c->setup_ms[2] = up_ms + ms_since(t_up2);
+    c->setup_ms[3] = 0.0;
+    c->setup_ms[4] = ms_since(t_start);
+    return SFMX_OK;
+}
+
+int init_ctx(sfmx_ba_ctx* c, const sfmx_ba_options* opt) {
+    sfmx_ba_options o;
+    sfmx_ba_default_options(&o);
+    if (opt) o = *opt;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(SFMX_EDEVICE, "no HIP device visible");
+    if (o.device < 0 || o.device >= ndev) return fail(SFMX_EINVAL, "device index out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, o.device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SFMX_EDEVICE, "sfmx BA kernels are built for gfx950 only");
+    c->device = o.device;
+    c->opt = o;
+    DeviceGuard dg(c->device);
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) return fail(SFMX_EDEVICE, "stream");
+    for (auto& e : c->ev) if (hipEventCreate(&e) != hipSuccess) return fail(SFMX_EDEVICE, "event");
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->hs), sizeof(double) * sfmx_ba_ctx::HS_N,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return fail(SFMX_ENOMEM, "pinned scalar buffer");
+    std::memset(c->hs, 0, sizeof(double) * sfmx_ba_ctx::HS_N);
+    return SFMX_OK;
+}
+
+int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ctx** out) {
+    RC(validate(caller));
+    auto* c = new (std::nothrow) sfmx_ba_ctx();
+    if (!c) return fail(SFMX_ENOMEM, "host allocation");
+    int rc = init_ctx(c, opt);
+    if (!rc) rc = load_problem(c, caller);
+    if (rc) { delete c; return rc; }
     *out = c;
     return SFMX_OK;
 }
@@ -1250,8 +1491,10 @@ int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
     if (!c || !pb) return fail(SFMX_EINVAL, "null context/problem");
     DeviceGuard dg(c->device);
     const double* x = c->x.as<double>();
-    std::vector<double> pts(3 * (size_t)c->P);
-    if (c->P) HIPCHK(hipMemcpyAsync(pts.data(), x, sizeof(double) * 3 * c->P, hipMemcpyDeviceToHost, c->st));
+    c->stage_off = 0;   // nothing staged is in flight: every upload was synchronised
+    double* pts = c->P ? static_cast<double*>(stage_bytes(c, sizeof(double) * 3 * (size_t)c->P)) : nullptr;
+    if (c->P && !pts) return fail(SFMX_ENOMEM, "pinned staging buffer");
+    if (c->P) HIPCHK(hipMemcpyAsync(pts, x, sizeof(double) * 3 * c->P, hipMemcpyDeviceToHost, c->st));
     if (c->C) HIPCHK(hipMemcpyAsync(pb->poses, x + c->ne, sizeof(double) * 6 * c->C, hipMemcpyDeviceToHost, c->st));
     std::vector<double> iv(c->K);
     HIPCHK(hipMemcpyAsync(iv.data(), x + c->ne + 6 * (size_t)c->C, sizeof(double) * c->K, hipMemcpyDeviceToHost, c->st));
@@ -1288,15 +1531,56 @@ int sfmx_ba_destroy(sfmx_ba_ctx* c) {
     return SFMX_OK;
 }
 
+int sfmx_ba_update(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
+    if (!c) return fail(SFMX_EINVAL, "null context");
+    RC(validate(pb));
+    return load_problem(c, pb);
+}
+
+int sfmx_ba_setup_ms(sfmx_ba_ctx* c, double* ms, int32_t n) {
+    if (!c || !ms) return fail(SFMX_EINVAL, "null");
+    const int m = std::min<int>(n, 5);
+    for (int i = 0; i < m; ++i) ms[i] = c->setup_ms[i];
+    return m;
+}
+
+// sfmx_ba_solve keeps one context per device between calls (the reference solves a growing scene
+// after every registered camera, SfM.cpp:235 / :371): stream, events, pinned memory and device
+// buffers are reused, the plan too while the co-visibility holds.  Plain pointers, no static
+// destructor (the HIP runtime may be gone at process exit); sfmx_ba_release_cache frees them.
+namespace {
+std::mutex g_solve_mu;
+sfmx_ba_ctx* g_solve_ctx[64] = {};
+}
+
+int sfmx_ba_release_cache(void) {
+    std::lock_guard<std::mutex> lk(g_solve_mu);
+    for (auto& c : g_solve_ctx) { delete c; c = nullptr; }
+    return SFMX_OK;
+}
+
 int sfmx_ba_solve(sfmx_ba_problem* pb, const sfmx_ba_options* opt, sfmx_ba_summary* summary, double* trace,
                   int32_t trace_cap) {
     if (!summary) return fail(SFMX_EINVAL, "null summary");
-    sfmx_ba_ctx* c = nullptr;
-    RC(create(pb, opt, &c));
+    RC(validate(pb));
+    sfmx_ba_options o;
+    sfmx_ba_default_options(&o);
+    if (opt) o = *opt;
+    if (o.device < 0 || o.device >= 64) return fail(SFMX_EINVAL, "device index out of range");
+    std::lock_guard<std::mutex> lk(g_solve_mu);
+    sfmx_ba_ctx*& c = g_solve_ctx[o.device];
+    int rc = SFMX_OK;
+    if (!c) {
+        rc = create(pb, &o, &c);
+        if (rc) { c = nullptr; return rc; }
+    } else {
+        c->opt = o;
+        rc = load_problem(c, pb);
+    }
     int nt = 0;
-    int rc = run_lm(c, 0, summary, trace, trace_cap, &nt);
+    if (!rc) rc = run_lm(c, 0, summary, trace, trace_cap, &nt);
     if (!rc) rc = sfmx_ba_get(c, pb);   // write-back (BundleAdjustment.cpp:97-138)
-    delete c;
+    if (rc) { delete c; c = nullptr; }  // a failed call leaves no half-loaded context behind
     return rc ? rc : nt;
 }
 
@@ -1334,6 +1618,26 @@ int sfmx_ba_jacobian(const sfmx_ba_problem* pb, int32_t device, double* r, doubl
     delete c;
     return rc;
 }
+
+#ifdef SFMX_DIAG
+// diagnostic build only: the host part of load_problem without a device (ordering, permutation,
+// point groups / chunks / batches / assembly tasks), ms = [order, permute, topology]
+int sfmx_ba_debug_host_setup(const sfmx_ba_problem* pb, double* ms) {
+    RC(validate(pb));
+    using clk = std::chrono::steady_clock;
+    auto t0 = clk::now();
+    Ordered od;
+    order_problem(pb, od);
+    auto t1 = clk::now();
+    auto t2 = clk::now();
+    Topology tp;
+    build_topology(pb->n_points, pb->n_cams, pb->n_obs, pb->n_intr ? 7 : pb->cam_model, od.pt_start, od.roc.data(), tp);
+    auto t3 = clk::now();
+    auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    ms[0] = d(t0, t1); ms[1] = d(t1, t2); ms[2] = d(t2, t3);
+    return (int)tp.grp.size();
+}
+#endif
 
 #ifdef SFMX_BA_STAMPS
 // diagnostic build only: read and clear the phase cycle totals (ba_group.hpp BA_STAMP)

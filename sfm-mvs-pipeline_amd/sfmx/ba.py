@@ -118,6 +118,11 @@ def solve(problem: BAProblem, options: Optional[sfmx_ba_options] = None, trace_c
     return summary_dict(sm), tr[:n]
 
 
+def release_cache():
+    """Free the solver contexts sfmx_ba_solve keeps per device between calls."""
+    check(lib.sfmx_ba_release_cache(), "sfmx_ba_release_cache")
+
+
 def jacobian(problem: BAProblem, device: int = 0):
     """Device residuals + Jacobian blocks -> (r[O,2], Je[O,2,3], Jc[O,2,6], Ji[O,2,k])."""
     O, k = len(problem.obs_point), len(problem.intr)
@@ -158,6 +163,19 @@ class BAContext:
         n = check(lib.sfmx_ba_run(self._h, max_iterations, C.byref(sm), tr.ctypes.data if trace_cap else None,
                                   trace_cap), "sfmx_ba_run")
         return summary_dict(sm), tr[:n]
+
+    def update(self, problem: BAProblem):
+        """Replace the problem (any topology, e.g. a grown scene), reusing the context's device
+        buffers and, when the co-visibility is unchanged, its factorization plan."""
+        st = problem.struct()
+        check(lib.sfmx_ba_update(self._h, C.byref(st)), "sfmx_ba_update")
+        self.problem = problem
+
+    def setup_ms(self) -> dict:
+        """Host-side setup of the last create / update (ms)."""
+        v = (C.c_double * 5)()
+        n = check(lib.sfmx_ba_setup_ms(self._h, v, 5), "sfmx_ba_setup_ms")
+        return {k: v[i] for i, k in enumerate(["order_groups", "alloc", "upload", "plan", "total"][:n])}
 
     def reset(self, problem: Optional[BAProblem] = None):
         st = (problem or self.problem).struct()

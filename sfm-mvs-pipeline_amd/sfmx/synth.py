@@ -177,6 +177,24 @@ def ba_problem(n_cams: int = 200, n_points: int = 200_000, obs_per_point: int = 
     return (prob, tr) if truth else prob
 
 
+def ba_registered(p: dict, n_cams: int) -> dict:
+    """The BA problem of a scene after its first `n_cams` cameras are registered (SfM.cpp:235 / :371
+    run BundleAdjustment after every registration): their observations of the points seen by at
+    least two of them (a point exists once triangulated), in the original point order."""
+    obs_point, obs_cam = np.asarray(p["obs_point"]), np.asarray(p["obs_cam"])
+    keep_o = obs_cam < n_cams
+    cnt = np.bincount(obs_point[keep_o], minlength=len(p["points"]))
+    keep_p = cnt >= 2
+    keep_o &= keep_p[obs_point]
+    remap = np.cumsum(keep_p) - 1
+    out = dict(p, points=np.asarray(p["points"])[keep_p], poses=np.asarray(p["poses"])[:n_cams],
+               obs_point=remap[obs_point[keep_o]].astype(np.int32), obs_cam=obs_cam[keep_o].astype(np.int32),
+               obs_xy=np.asarray(p["obs_xy"])[keep_o])
+    if p.get("pose_intr") is not None:
+        out["pose_intr"] = np.asarray(p["pose_intr"])[:n_cams]
+    return out
+
+
 def ba_problem_multi(n_cams: int = 24, n_points: int = 3000, cameras=((3, 1.0), (3, 1.1)), obs_per_point: int = 6,
                      noise_px: float = 0.5, seed: int = BA_SEED + 7, width: int = 720, height: int = 405,
                      perturb: bool = True, pose_intr=None):

@@ -267,3 +267,49 @@ def test_dag_wait_timeout_falls_back_to_per_level_launches():
     assert ph["dag_fallbacks"] >= 1
     assert s1["final_cost"] == s0["final_cost"] and np.array_equal(t1, t0)
     assert np.array_equal(P1.points, P0.points) and np.array_equal(P1.poses, P0.poses)
+
+
+# ---- the reference's call pattern: BA after every registered camera (SfM.cpp:235 / :371) ------
+
+grown = synth.ba_registered
+
+
+def test_cached_solve_context_is_bit_identical_to_a_fresh_one():
+    """sfmx_ba_solve reuses one context per device: a growing, shrinking and changing sequence of
+    problems (sizes, camera models, several cameras) gives the bits of fresh contexts."""
+    base = synth.ba_problem(40, 4000, seed=61)
+    seq = [grown(base, 12), grown(base, 20), synth.ba_problem(8, 500, seed=62, cam_model=7), grown(base, 40),
+           synth.ba_problem_multi(12, 800, cameras=((1, 1.0), (3, 1.1)), seed=63), grown(base, 20)]
+    cached = [gpu_solve(p) for p in seq]
+    for p, (P, sm, tr) in zip(seq, cached):
+        ba.release_cache()
+        P1, sm1, tr1 = gpu_solve(p)
+        assert sm1["final_cost"] == sm["final_cost"] and np.array_equal(tr1, tr)
+        assert np.array_equal(P1.points, P.points) and np.array_equal(P1.poses, P.poses) and np.array_equal(P1.intr, P.intr)
+
+
+def test_update_grown_scene_equals_fresh_context_and_reuses_plan():
+    base = synth.ba_problem(60, 6000, seed=64)
+    a, b = ba.BAProblem(**grown(base, 30)), ba.BAProblem(**grown(base, 60))
+    ctx = ba.BAContext(a)
+    try:
+        s_a, t_a = ctx.run(trace_cap=256)
+        first = ctx.setup_ms()
+        ctx.update(b)
+        s_b, t_b = ctx.run(trace_cap=256)
+        grow = ctx.setup_ms()
+        Pb = ctx.get()
+        ctx.update(ba.BAProblem(**grown(base, 60)))   # same graph: the plan is kept
+        ctx.run()
+        same = ctx.setup_ms()
+    finally:
+        ctx.close()
+    ref = ba.BAContext(ba.BAProblem(**grown(base, 60)))
+    try:
+        s_r, t_r = ref.run(trace_cap=256)
+        Pr = ref.get()
+    finally:
+        ref.close()
+    assert s_b["final_cost"] == s_r["final_cost"] and np.array_equal(t_b, t_r) and np.array_equal(Pb.points, Pr.points)
+    assert first["plan"] > 0 and grow["plan"] > 0 and same["plan"] == 0
+    assert all(v >= 0 for v in grow.values()) and grow["total"] >= grow["order_groups"]
