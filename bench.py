@@ -496,14 +496,26 @@ def bench_ba(args, rank, world, local):
     import torch
     import torch.distributed as dist
     from sfmx import ba, synth
-    from sfmx.dist import shard_ba_problem, torch_allreduce
+    from sfmx.dist import shard_ba_problem, torch_allreduce, rccl_comm
     prob = synth.ba_problem(args.ba_cams, args.ba_points)
     local_prob = shard_ba_problem(prob, rank, world) if world > 1 else dict(prob, point_range=(0, args.ba_points))
     local_prob.pop("point_range")
     opts = ba.default_options(device=local)
+    rehearse = os.environ.get("SFMX_BENCH_REHEARSE") == "1"
     use_ar = world > 1 or os.environ.get("SFMX_BENCH_BA_AR1") == "1"
-    ctx = ba.BAContext(ba.BAProblem(**local_prob), opts, allreduce=torch_allreduce(cpu_staging=os.environ.get("SFMX_BENCH_REHEARSE") == "1")
-                         if use_ar else None)
+    # ranks on their own GPUs: native RCCL inside libsfmx (sfmx_ba_set_comm, no Python in the LM
+    # loop); the one-GPU rehearsal (every rank on cuda:0, gloo) keeps the host-staged callback
+    ctx = ba.BAContext(ba.BAProblem(**local_prob), opts,
+                       allreduce=torch_allreduce(cpu_staging=True) if (use_ar and rehearse) else None)
+    collectives = "none (one rank)"
+    if use_ar and not rehearse:
+        if world > 1:
+            rccl_comm(ctx)
+        else:
+            ctx.set_comm(ba.comm_unique_id(), 1, 0)
+        collectives = "RCCL in libsfmx (ncclAllReduce on the solver stream)"
+    elif use_ar:
+        collectives = "gloo callback, host-staged (one-GPU rehearsal)"
     ctx.run(max_iterations=1)                 # warm-up (code objects, allocations)
     ctx.reset()
     if world > 1:
@@ -528,7 +540,7 @@ def bench_ba(args, rank, world, local):
                                   "SimpleRadial, LM + DENSE_SCHUR (Ceres 1.14 defaults)", "parallelism": f"point-sharded x{world}"},
            "iterations": iters, "successful": sm["num_successful_steps"], "initial_cost": sm["initial_cost"],
            "final_cost": sm["final_cost"], "termination": ba.TERMINATION_NAMES[sm["termination_type"]],
-           "total_ms": total_ms, "phase_ms_rank0": phases}
+           "total_ms": total_ms, "phase_ms_rank0": phases, "collectives": collectives}
     res["roofline"] = ba_roofline(args, res["value"], world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

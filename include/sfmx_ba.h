@@ -120,6 +120,14 @@ typedef int (*sfmx_allreduce_fn)(double* device_buf, int64_t count, int32_t op, 
 
 int sfmx_ba_create(const sfmx_ba_problem* problem, const sfmx_ba_options* opt, sfmx_ba_ctx** out);
 int sfmx_ba_set_allreduce(sfmx_ba_ctx* ctx, sfmx_allreduce_fn fn, void* user);
+/* Native collectives (RCCL over xGMI, one process per GPU): rank 0 calls
+ * sfmx_ba_comm_unique_id (128 bytes, ncclUniqueId) and hands it to every rank (any
+ * transport), then every rank calls sfmx_ba_set_comm with it.  The solver's all-reduces
+ * are then ncclAllReduce on its own HIP stream, with no host callback in the LM loop; a
+ * communicator takes precedence over a callback.  RCCL is loaded at run time
+ * (librccl.so.1: the copy the process already has, e.g. PyTorch's). */
+int sfmx_ba_comm_unique_id(void* unique_id_out);
+int sfmx_ba_set_comm(sfmx_ba_ctx* ctx, const void* unique_id, int32_t nranks, int32_t rank);
 /* Run the LM minimizer from the context's current parameters for at most
  * max_iterations iterations (<= 0: options.max_num_iterations). */
 int sfmx_ba_run(sfmx_ba_ctx* ctx, int32_t max_iterations, sfmx_ba_summary* summary,

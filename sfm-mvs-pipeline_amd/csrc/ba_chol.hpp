@@ -53,75 +53,75 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const double* base) {
 __device__ __forceinline__ double2 ld_wt2(__amdgpu_buffer_rsrc_t rs, size_t elem) {
     return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(elem * 8), 0, 16));
 }
-// 64x64 fp64 tiles on the matrix cores (layout: f64x4 / trow / tcol in ba_kernels.hpp).  Wave w of a
-// 256-thread block owns the row strip 16w..16w+15 and four 16x16 column tiles.
+// NB x NB fp64 tiles on the matrix cores (layout: f64x4 / trow / tcol in ba_kernels.hpp).  Wave w of an
+// NTH = 4 NB thread block owns the row strip 16w..16w+15 and NW = NB / 16 16x16 column tiles.
 
 __device__ __forceinline__ void tile_load(double (*dst)[LDT], const double* __restrict__ src, int ld) {
 #pragma unroll
-    for (int q = 0; q < NB * NB / 512; ++q) {
-        const int e = q * 512 + 2 * threadIdx.x;
+    for (int q = 0; q < NB * NB / (2 * NTH); ++q) {
+        const int e = q * (2 * NTH) + 2 * threadIdx.x;
         *reinterpret_cast<double2*>(&dst[e / NB][e % NB]) = *reinterpret_cast<const double2*>(src + (size_t)(e / NB) * ld + e % NB);
     }
 }
 // the same from bytes another workgroup of this launch stored write-through (sc1 loads; elements of rs)
 __device__ __forceinline__ void tile_load_wt(double (*dst)[LDT], __amdgpu_buffer_rsrc_t rs, size_t src, int ld) {
 #pragma unroll
-    for (int q = 0; q < NB * NB / 512; ++q) {
-        const int e = q * 512 + 2 * threadIdx.x;
+    for (int q = 0; q < NB * NB / (2 * NTH); ++q) {
+        const int e = q * (2 * NTH) + 2 * threadIdx.x;
         *reinterpret_cast<double2*>(&dst[e / NB][e % NB]) = ld_wt2(rs, src + (size_t)(e / NB) * ld + e % NB);
     }
 }
-__device__ __forceinline__ void tile_regs_wt(f64x4 (&t)[4], const double* __restrict__ src, int ld) {
+__device__ __forceinline__ void tile_regs_wt(f64x4 (&t)[NW], const double* __restrict__ src, int ld) {
     const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < NW; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r) t[c][r] = ld_wt(&src[(size_t)(16 * w + trow(r)) * ld + 16 * c + tcol()]);
 }
-__device__ __forceinline__ void tile_store_wt(const f64x4 (&t)[4], double* __restrict__ dst, int ld) {
+__device__ __forceinline__ void tile_store_wt(const f64x4 (&t)[NW], double* __restrict__ dst, int ld) {
     const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < NW; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r) st_wt(&dst[(size_t)(16 * w + trow(r)) * ld + 16 * c + tcol()], t[c][r]);
 }
-__device__ __forceinline__ void tile_regs(f64x4 (&t)[4], const double* __restrict__ src, int ld) {
+__device__ __forceinline__ void tile_regs(f64x4 (&t)[NW], const double* __restrict__ src, int ld) {
     const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < NW; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r) t[c][r] = src[(size_t)(16 * w + trow(r)) * ld + 16 * c + tcol()];
 }
-__device__ __forceinline__ void tile_store(const f64x4 (&t)[4], double* __restrict__ dst, int ld) {
+__device__ __forceinline__ void tile_store(const f64x4 (&t)[NW], double* __restrict__ dst, int ld) {
     const int w = threadIdx.x >> 6;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < NW; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r) dst[(size_t)(16 * w + trow(r)) * ld + 16 * c + tcol()] = t[c][r];
 }
 
 // acc[c] = A[strip] * B          (A, B row-major 64x64 in LDS)
-__device__ __forceinline__ void mfma_nn(const double (*A)[LDT], const double (*B)[LDT], f64x4 acc[4]) {
+__device__ __forceinline__ void mfma_nn(const double (*A)[LDT], const double (*B)[LDT], f64x4 acc[NW]) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, m = l & 15, kq = l >> 4;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int c = 0; c < NW; ++c) acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
     for (int st = 0; st < NB / 4; ++st) {
         const double av = A[16 * w + m][4 * st + kq];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, B[4 * st + kq][16 * c + m], acc[c], 0, 0, 0);
+        for (int c = 0; c < NW; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, B[4 * st + kq][16 * c + m], acc[c], 0, 0, 0);
     }
 }
 // acc[c] = A[strip] * X^T        (A, X row-major 64x64 in LDS)
-__device__ __forceinline__ void mfma_nt(const double (*A)[LDT], const double (*X)[LDT], f64x4 acc[4]) {
+__device__ __forceinline__ void mfma_nt(const double (*A)[LDT], const double (*X)[LDT], f64x4 acc[NW]) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, m = l & 15, kq = l >> 4;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int c = 0; c < NW; ++c) acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
     for (int st = 0; st < NB / 4; ++st) {
         const double av = A[16 * w + m][4 * st + kq];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, X[16 * c + m][4 * st + kq], acc[c], 0, 0, 0);
+        for (int c = 0; c < NW; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, X[16 * c + m][4 * st + kq], acc[c], 0, 0, 0);
     }
 }
 
@@ -146,6 +146,10 @@ __device__ __forceinline__ double rcp_nr(double d) {
 //          inverse is closed-form and its two scalar pivots (a, det/a) are the
 //          scalar Cholesky pivots, i.e. exactly where LLT would fail.
 constexpr int LDP = 18;   // LDS row stride of the 16-wide panels (16-B aligned rows)
+// chol_diag_tile's workspace: column panel [NB][LDP] | -A_BB^-1 [16][LDP] | inner panel [32] | one
+// -M strip [16][LDP] per wave; it fits a tile buffer at NB = 64, not at NB = 32
+constexpr int DIAG_WS = NB * LDP + 16 * LDP + 32 + NW * 16 * LDP;
+constexpr bool DIAG_WS_IN_BUF = DIAG_WS <= NB * LDT;
 #ifdef SFMX_CHOL_STAMPS   // tools/micro/chol_tile.hip: phase timestamps of block 0 (never in the product build)
 __device__ long long g_chol_stamps[64];
 #define CHOL_STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_chol_stamps[i] = wall_clock64(); } while (0)
@@ -221,12 +225,13 @@ __device__ __forceinline__ void inner_inverse16(const double* __restrict__ Pc, i
 // buf: 64 x LDT doubles of LDS workspace; wv: NB x RW doubles of LDS.  WT: W_k and the R rows are
 // stored write-through (sc1), for readers in the same launch (chol_factor).
 template <int RW, bool WT = false>
-__device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __restrict__ Wk,
+__device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[NW], int k, double* __restrict__ Wk,
                                                double* __restrict__ R, const double* __restrict__ y,
                                                double* __restrict__ wv, double* __restrict__ contrib,
-                                               int* __restrict__ fail, double (*buf)[LDT], int* wver = nullptr) {
+                                               int* __restrict__ fail, double (*buf)[LDT], double* dws,
+                                               int* wver = nullptr) {
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, m = l & 15, kq = l >> 4, k0 = k * NB;
-    double* ws = &buf[0][0];
+    double* ws = DIAG_WS_IN_BUF ? &buf[0][0] : dws;   // the sweeps' workspace (dead once W is written)
     double* Pc = ws;                       // [64][LDP]  column panel A_:B
     double* Qn = ws + NB * LDP;            // [16][LDP]  -A_BB^-1
     double* ipan = Qn + 16 * LDP;          // [16][2]    inner column panel
@@ -259,7 +264,7 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __r
         CHOL_STAMP(4 + 4 * s);
         // a_il -= M[i][:] A_l,B for the other column tiles (rows in B start from 0)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < NW; ++c) {
             if (c == s) continue;
             f64x4 acc = rowB ? f64x4{0.0, 0.0, 0.0, 0.0} : t[c];
 #pragma unroll
@@ -272,7 +277,7 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __r
     }
     if (bad) atomicOr(fail, 1);
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < NW; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = 16 * w + trow(r), j = 16 * c + tcol();
@@ -292,8 +297,8 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __r
 #pragma unroll
         for (int q = 0; q < RW; ++q) acc[q] = 0.0;
 #pragma unroll
-        for (int cc = 0; cc < 16; cc += 2) {
-            const int c = cp * 16 + cc;
+        for (int cc = 0; cc < NB / 4; cc += 2) {
+            const int c = cp * (NB / 4) + cc;
             const double2 wi = *reinterpret_cast<const double2*>(&buf[i][c]);
 #pragma unroll
             for (int q = 0; q < RW; q += 2) {
@@ -323,7 +328,7 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[4], int k, double* __r
     __syncthreads();
     CHOL_STAMP(23);
     // contrib_k[i][j] = sum_r y[r][i] w[r][j]: 16 lanes per output, 4 rows each, then 4 shuffles
-    for (int o = tid >> 4; o < (RW - 1) * RW; o += 16) {
+    for (int o = tid >> 4; o < (RW - 1) * RW; o += NTH / 16) {
         const int i = o / RW, j = o % RW, rp = tid & 15;
         double sacc = 0.0;
 #pragma unroll
@@ -341,21 +346,22 @@ template <int RW>
 struct alignas(16) CholLds {
     double a[NB][LDT], m[NB][LDT], n[NB][LDT];
     double rk[NB * RW], ra[NB * RW], wv[NB * RW];   // w_k of a source panel; y_a; w_a
+    double dws[DIAG_WS_IN_BUF ? 2 : DIAG_WS];        // chol_diag_tile's workspace when a tile buffer is too small
 };
 
 // launch 0: the diagonal tiles of the level-0 panels (untouched by any update) -> W_k, w_k, contrib_k
 template <int RW>
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(NTH)
 void chol_leaves(double* __restrict__ S, int npad, double* __restrict__ R, const int* __restrict__ leaves,
                  double* __restrict__ W, double* __restrict__ contrib, int* __restrict__ fail) {
     if (step_gated(fail + 1)) return;
     __shared__ CholLds<RW> sm;
     const int k = leaves[blockIdx.x], k0 = k * NB;
-    f64x4 t[4];
+    f64x4 t[NW];
     tile_regs(t, S + (size_t)k0 * npad + k0, npad);
-    for (int e = threadIdx.x; e < NB * RW; e += 256) sm.ra[e] = R[(size_t)k0 * RW + e];
+    for (int e = threadIdx.x; e < NB * RW; e += NTH) sm.ra[e] = R[(size_t)k0 * RW + e];
     __syncthreads();
-    chol_diag_tile<RW>(t, k, W + (size_t)k * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a);
+    chol_diag_tile<RW>(t, k, W + (size_t)k * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a, sm.dws);
 }
 
 // launch l + 1: one workgroup per destination tile (a, b) of level l's updates, its source panels
@@ -363,7 +369,7 @@ void chol_leaves(double* __restrict__ S, int npad, double* __restrict__ R, const
 //   G = A_ak W_k;  A_ab -= G A_bk^T  (b == a: A_aa -= G A_ak^T, G^T -> upper tile (k, a), y_a -= A_ak w_k)
 // The first ninv workgroups hold diagonal tiles whose last update this is: they invert it.
 template <int RW>
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(NTH)
 void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
                 const int* __restrict__ src, int ninv, double* __restrict__ W, double* __restrict__ contrib,
                 int* __restrict__ fail) {
@@ -374,42 +380,42 @@ void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const 
     const int a = task.x, b = task.y, a0 = a * NB, b0 = b * NB;
     const bool diag = (a == b);
     CHOL_STAMP(30);
-    f64x4 t[4];
+    f64x4 t[NW];
     double* dst = S + (size_t)a0 * npad + b0;
     tile_regs(t, dst, npad);                                                   // A_ab (prefetch)
     if (diag)
-        for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = R[(size_t)a0 * RW + e];
+        for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = R[(size_t)a0 * RW + e];
     for (int s = task.z; s < task.w; ++s) {
         const int k = src[s], k0 = k * NB;
         tile_load(sm.a, S + (size_t)a0 * npad + k0, npad);                     // A_ak
         tile_load(sm.m, W + (size_t)k * NB * NB, NB);                          // W_k
         if (!diag) tile_load(sm.n, S + (size_t)b0 * npad + k0, npad);          // A_bk
         else
-            for (int e = tid; e < NB * RW; e += 256) sm.rk[e] = R[(size_t)k0 * RW + e];   // w_k
+            for (int e = tid; e < NB * RW; e += NTH) sm.rk[e] = R[(size_t)k0 * RW + e];   // w_k
         __syncthreads();
         CHOL_STAMP(31);
-        f64x4 g[4];
+        f64x4 g[NW];
         mfma_nn(sm.a, sm.m, g);   // G = A_ak W_k
         __syncthreads();
         CHOL_STAMP(32);
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < NW; ++c)
 #pragma unroll
             for (int r = 0; r < 4; ++r) sm.m[16 * w + trow(r)][16 * c + tcol()] = g[c][r];
         __syncthreads();
-        f64x4 upd[4];
+        f64x4 upd[NW];
         mfma_nt(sm.m, diag ? sm.a : sm.n, upd);   // G X^T
 #pragma unroll
-        for (int c = 0; c < 4; ++c) t[c] -= upd[c];
+        for (int c = 0; c < NW; ++c) t[c] -= upd[c];
         CHOL_STAMP(33);
         if (diag) {
             // y_a -= A_ak w_k: NB x RW outputs, 256 / RW ... threads; 4 lanes per output for RW <= 4
-            constexpr int TPO = (256 / (NB * RW)) > 0 ? 256 / (NB * RW) : 1;
-            constexpr int OPT = (NB * RW) / (256 / TPO);
+            constexpr int TPO = (NTH / (NB * RW)) > 0 ? NTH / (NB * RW) : 1;
+            constexpr int OPT = (NB * RW) / (NTH / TPO);
             const int part = tid % TPO;
 #pragma unroll
             for (int u = 0; u < OPT; ++u) {
-                const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+                const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
                 double sum = 0.0;
                 for (int c = part; c < NB; c += TPO) sum = fma(sm.a[i][c], sm.rk[c * RW + q], sum);
                 if (TPO >= 2) sum += __shfl_xor(sum, 1);
@@ -418,18 +424,18 @@ void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const 
             }
             // upper tile (k, a): row k0 + j, column a0 + i holds G[i][j]
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
+            for (int c = 0; c < NW; ++c)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) S[(size_t)(k0 + 16 * c + tcol()) * npad + a0 + 16 * w + trow(r)] = g[c][r];
         }
         __syncthreads();   // the next source panel overwrites sm
     }
     if (diag && (int)blockIdx.x < ninv) {
-        chol_diag_tile<RW>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n);
+        chol_diag_tile<RW>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n, sm.dws);
     } else {
         tile_store(t, dst, npad);
         if (diag)
-            for (int e = tid; e < NB * RW; e += 256) R[(size_t)a0 * RW + e] = sm.ra[e];
+            for (int e = tid; e < NB * RW; e += NTH) R[(size_t)a0 * RW + e] = sm.ra[e];
     }
     CHOL_STAMP(34);
 }
@@ -447,30 +453,30 @@ void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const 
 // hand-off + inverse.  part = {task (global index), source index, slot, n | inverting << 16};
 // ctr[task] is zero at launch and the last part zeroes it again.
 template <int RW>
-__device__ __forceinline__ void part_store(double* __restrict__ slot, const f64x4 (&u)[4], const double* ys, int nys) {
+__device__ __forceinline__ void part_store(double* __restrict__ slot, const f64x4 (&u)[NW], const double* ys, int nys) {
     const int tid = threadIdx.x;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < NW; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            __hip_atomic_store((g_u64*)&slot[(4 * c + r) * 256 + tid], (unsigned long long)__double_as_longlong(u[c][r]),
+            __hip_atomic_store((g_u64*)&slot[(4 * c + r) * NTH + tid], (unsigned long long)__double_as_longlong(u[c][r]),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int u2 = 0; u2 < nys; ++u2)
-        __hip_atomic_store((g_u64*)&slot[(16 + u2) * 256 + tid], (unsigned long long)__double_as_longlong(ys[u2]),
+        __hip_atomic_store((g_u64*)&slot[(4 * NW + u2) * NTH + tid], (unsigned long long)__double_as_longlong(ys[u2]),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int RW>
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(NTH)
 void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
                       const int4* __restrict__ parts, const int* __restrict__ src, double* __restrict__ W,
                       double* __restrict__ contrib, int* __restrict__ fail, double* pbuf, int* ctr) {
     if (step_gated(fail + 1)) return;
     __shared__ CholLds<RW> sm;
     __shared__ int last_sh;
-    constexpr int TPO = (256 / (NB * RW)) > 0 ? 256 / (NB * RW) : 1;
-    constexpr int OPT = (NB * RW) / (256 / TPO);
-    constexpr int SLOT = (16 + OPT) * 256;   // doubles per part slot
+    constexpr int TPO = (NTH / (NB * RW)) > 0 ? NTH / (NB * RW) : 1;
+    constexpr int OPT = (NB * RW) / (NTH / TPO);
+    constexpr int SLOT = (4 * NW + OPT) * NTH;   // doubles per part slot
     const int tid = threadIdx.x, w = tid >> 6;
     const int4 part = parts[blockIdx.x];
     const int4 task = tasks[part.x];
@@ -478,34 +484,34 @@ void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, 
     const bool diag = (a == b), inv = (part.w >> 16) != 0;
     const int k = src[part.y], k0 = k * NB;
     double* dst = S + (size_t)a0 * npad + b0;
-    f64x4 t[4];
+    f64x4 t[NW];
     if (n == 1) {
         tile_regs(t, dst, npad);                                                   // A_ab (prefetch)
         if (diag)
-            for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = R[(size_t)a0 * RW + e];
+            for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = R[(size_t)a0 * RW + e];
     }
     tile_load(sm.a, S + (size_t)a0 * npad + k0, npad);                         // A_ak
     tile_load(sm.m, W + (size_t)k * NB * NB, NB);                              // W_k
     if (!diag) tile_load(sm.n, S + (size_t)b0 * npad + k0, npad);              // A_bk
     else
-        for (int e = tid; e < NB * RW; e += 256) sm.rk[e] = R[(size_t)k0 * RW + e];   // w_k
+        for (int e = tid; e < NB * RW; e += NTH) sm.rk[e] = R[(size_t)k0 * RW + e];   // w_k
     __syncthreads();
-    f64x4 g[4];
+    f64x4 g[NW];
     mfma_nn(sm.a, sm.m, g);   // G = A_ak W_k
     __syncthreads();
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < NW; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r) sm.m[16 * w + trow(r)][16 * c + tcol()] = g[c][r];
     __syncthreads();
-    f64x4 upd[4];
+    f64x4 upd[NW];
     mfma_nt(sm.m, diag ? sm.a : sm.n, upd);   // G X^T
     double ys[OPT];
     if (diag) {
         const int pp = tid % TPO;
 #pragma unroll
         for (int u = 0; u < OPT; ++u) {
-            const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+            const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
             double sum = 0.0;
             for (int c = pp; c < NB; c += TPO) sum = fma(sm.a[i][c], sm.rk[c * RW + q], sum);
             if (TPO >= 2) sum += __shfl_xor(sum, 1);
@@ -513,7 +519,7 @@ void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, 
             ys[u] = sum;
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < NW; ++c)
 #pragma unroll
             for (int r = 0; r < 4; ++r) S[(size_t)(k0 + 16 * c + tcol()) * npad + a0 + 16 * w + trow(r)] = g[c][r];
     }
@@ -529,42 +535,42 @@ void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, 
         if (tid == 0) ctr[part.x] = 0;                              // nobody else touches it in this launch
         tile_regs(t, dst, npad);
         if (diag)
-            for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = R[(size_t)a0 * RW + e];
+            for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = R[(size_t)a0 * RW + e];
         __syncthreads();
         const double* base = pbuf + (size_t)(part.z - j) * SLOT;   // slot of source 0 of this task
         for (int jj = 0; jj < n; ++jj) {
             const double* sl = base + (size_t)jj * SLOT;
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
+            for (int c = 0; c < NW; ++c)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) t[c][r] -= (jj == j) ? upd[c][r] : ld_wt(&sl[(4 * c + r) * 256 + tid]);
+                for (int r = 0; r < 4; ++r) t[c][r] -= (jj == j) ? upd[c][r] : ld_wt(&sl[(4 * c + r) * NTH + tid]);
             if (diag) {
 #pragma unroll
                 for (int u = 0; u < OPT; ++u) {
-                    const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
-                    const double y = (jj == j) ? ys[u] : ld_wt(&sl[(16 + u) * 256 + tid]);
+                    const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
+                    const double y = (jj == j) ? ys[u] : ld_wt(&sl[(4 * NW + u) * NTH + tid]);
                     if (tid % TPO == 0) sm.ra[i * RW + q] -= y;
                 }
             }
         }
     } else {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) t[c] -= upd[c];
+        for (int c = 0; c < NW; ++c) t[c] -= upd[c];
         if (diag) {
 #pragma unroll
             for (int u = 0; u < OPT; ++u) {
-                const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+                const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
                 if (tid % TPO == 0) sm.ra[i * RW + q] -= ys[u];
             }
         }
     }
     __syncthreads();
     if (diag && inv) {
-        chol_diag_tile<RW>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n);
+        chol_diag_tile<RW>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n, sm.dws);
     } else {
         tile_store(t, dst, npad);
         if (diag)
-            for (int e = tid; e < NB * RW; e += 256) R[(size_t)a0 * RW + e] = sm.ra[e];
+            for (int e = tid; e < NB * RW; e += NTH) R[(size_t)a0 * RW + e] = sm.ra[e];
     }
 }
 
@@ -591,7 +597,7 @@ void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, 
 __device__ __forceinline__ int tver_id(int a, int b) { return a * (a + 1) / 2 + b; }
 
 template <int RW>
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(NTH)
 void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
                  const int4* __restrict__ items, const int4* __restrict__ need, const int* __restrict__ src,
                  double* __restrict__ W, double* __restrict__ contrib, int* __restrict__ fail, double* pbuf,
@@ -599,9 +605,9 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
     if (step_gated(fail + 1)) return;
     __shared__ CholLds<RW> sm;
     __shared__ int sh[2];
-    constexpr int TPO = (256 / (NB * RW)) > 0 ? 256 / (NB * RW) : 1;
-    constexpr int OPT = (NB * RW) / (256 / TPO);
-    constexpr int SLOT = (16 + OPT) * 256;
+    constexpr int TPO = (NTH / (NB * RW)) > 0 ? NTH / (NB * RW) : 1;
+    constexpr int OPT = (NB * RW) / (NTH / TPO);
+    constexpr int SLOT = (4 * NW + OPT) * NTH;
     const int tid = threadIdx.x, w = tid >> 6;
     int* tver = ctr + 2;
     if (tid == 0) sh[0] = __hip_atomic_fetch_add((g_i32*)ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -625,11 +631,11 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
     int done_id = -1;   // the tile whose version this item advances (-1: none)
     if (it.y < 0) {     // leaf: diagonal tile k, untouched by any update
         const int k = it.x, k0 = k * NB;
-        f64x4 t[4];
+        f64x4 t[NW];
         tile_regs(t, S + (size_t)k0 * npad + k0, npad);
-        for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = R[(size_t)k0 * RW + e];
+        for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = R[(size_t)k0 * RW + e];
         __syncthreads();
-        chol_diag_tile<RW, true>(t, k, W + (size_t)k * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a, &tver[tver_id(k, k)]);
+        chol_diag_tile<RW, true>(t, k, W + (size_t)k * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a, sm.dws, &tver[tver_id(k, k)]);
         done_id = tver_id(k, k);
     } else {
         const int4 task = tasks[it.x];
@@ -645,11 +651,11 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
             if (n == 1) wait_ver(tver_id(a, b), nd.w);
         }
         __syncthreads();
-        f64x4 t[4];
+        f64x4 t[NW];
         if (n == 1) {
             tile_regs_wt(t, dst, npad);
             if (diag)
-                for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = ld_wt(&R[(size_t)a0 * RW + e]);
+                for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = ld_wt(&R[(size_t)a0 * RW + e]);
         }
         tile_load_wt(sm.a, rS, (size_t)a0 * npad + k0, npad);                   // A_ak
         if (!diag) tile_load_wt(sm.n, rS, (size_t)b0 * npad + k0, npad);        // A_bk
@@ -657,26 +663,26 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
         __syncthreads();
         tile_load_wt(sm.m, rW, (size_t)k * NB * NB, NB);                        // W_k
         __syncthreads();
-        f64x4 g[4];
+        f64x4 g[NW];
         mfma_nn(sm.a, sm.m, g);   // G = A_ak W_k
         __syncthreads();
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int c = 0; c < NW; ++c)
 #pragma unroll
             for (int r = 0; r < 4; ++r) sm.m[16 * w + trow(r)][16 * c + tcol()] = g[c][r];
         __syncthreads();
-        f64x4 upd[4];
+        f64x4 upd[NW];
         mfma_nt(sm.m, diag ? sm.a : sm.n, upd);   // G X^T
         double ys[OPT];
         if (diag) {
             if (tid == 0) wait_ver(tver_id(k, k), nd.z);   // w_k (the R rows of k) stored
             __syncthreads();
-            for (int e = tid; e < NB * RW; e += 256) sm.rk[e] = ld_wt(&R[(size_t)k0 * RW + e]);   // w_k
+            for (int e = tid; e < NB * RW; e += NTH) sm.rk[e] = ld_wt(&R[(size_t)k0 * RW + e]);   // w_k
             __syncthreads();
             const int pp = tid % TPO;
 #pragma unroll
             for (int u = 0; u < OPT; ++u) {
-                const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+                const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
                 double sum = 0.0;
                 for (int c = pp; c < NB; c += TPO) sum = fma(sm.a[i][c], sm.rk[c * RW + q], sum);
                 if (TPO >= 2) sum += __shfl_xor(sum, 1);
@@ -684,7 +690,7 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
                 ys[u] = sum;
             }
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
+            for (int c = 0; c < NW; ++c)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) S[(size_t)(k0 + 16 * c + tcol()) * npad + a0 + 16 * w + trow(r)] = g[c][r];
         }
@@ -707,20 +713,20 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below
                 tile_regs_wt(t, dst, npad);
                 if (diag)
-                    for (int e = tid; e < NB * RW; e += 256) sm.ra[e] = ld_wt(&R[(size_t)a0 * RW + e]);
+                    for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = ld_wt(&R[(size_t)a0 * RW + e]);
                 __syncthreads();
                 const double* base = pbuf + (size_t)(it.z - j) * SLOT;   // slot of source 0 of this task
                 for (int jj = 0; jj < n; ++jj) {
                     const double* sl = base + (size_t)jj * SLOT;
 #pragma unroll
-                    for (int c = 0; c < 4; ++c)
+                    for (int c = 0; c < NW; ++c)
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) t[c][r] -= (jj == j) ? upd[c][r] : ld_wt(&sl[(4 * c + r) * 256 + tid]);
+                        for (int r = 0; r < 4; ++r) t[c][r] -= (jj == j) ? upd[c][r] : ld_wt(&sl[(4 * c + r) * NTH + tid]);
                     if (diag) {
 #pragma unroll
                         for (int u = 0; u < OPT; ++u) {
-                            const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
-                            const double y = (jj == j) ? ys[u] : ld_wt(&sl[(16 + u) * 256 + tid]);
+                            const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
+                            const double y = (jj == j) ? ys[u] : ld_wt(&sl[(4 * NW + u) * NTH + tid]);
                             if (tid % TPO == 0) sm.ra[i * RW + q] -= y;
                         }
                     }
@@ -728,11 +734,11 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
             }
         } else {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) t[c] -= upd[c];
+            for (int c = 0; c < NW; ++c) t[c] -= upd[c];
             if (diag) {
 #pragma unroll
                 for (int u = 0; u < OPT; ++u) {
-                    const int o = tid / TPO + u * (256 / TPO), i = o / RW, q = o % RW;
+                    const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
                     if (tid % TPO == 0) sm.ra[i * RW + q] -= ys[u];
                 }
             }
@@ -740,12 +746,12 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
         if (fin) {
             __syncthreads();
             if (diag && inv) {
-                chol_diag_tile<RW, true>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n,
+                chol_diag_tile<RW, true>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n, sm.dws,
                                          &tver[tver_id(a, a)]);
             } else {
                 tile_store_wt(t, dst, npad);
                 if (diag)
-                    for (int e = tid; e < NB * RW; e += 256) st_wt(&R[(size_t)a0 * RW + e], sm.ra[e]);
+                    for (int e = tid; e < NB * RW; e += NTH) st_wt(&R[(size_t)a0 * RW + e], sm.ra[e]);
             }
             done_id = tver_id(a, b);
         }
@@ -845,7 +851,7 @@ __device__ __forceinline__ void intr_solve(const double* __restrict__ Dm, const 
 constexpr int BS_PF = 4;                   // ancestor tiles prefetched into LDS per workgroup
 
 template <int RW>
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(NTH)
 void chol_backsolve(const double* __restrict__ S, int npad, const double* __restrict__ R,
                     const double* __restrict__ Dm, const double* __restrict__ ri, const double* __restrict__ contrib,
                     int T, const int* __restrict__ border, const int* __restrict__ bs_start,
@@ -854,7 +860,7 @@ void chol_backsolve(const double* __restrict__ S, int npad, const double* __rest
                     long long tmo) {
     if (step_gated(fail + 1)) return;
     constexpr int K = RW - 1;
-    __shared__ double Ut[BS_PF][NB / 4][256];   // thread-private: its 16 U values per prefetched tile
+    __shared__ double Ut[BS_PF][NB / 4][NTH];   // thread-private: its 16 U values per prefetched tile
     __shared__ double Dp[K * RW], xs[K];
     __shared__ int sh[2];
     const int tid = threadIdx.x;

@@ -21,7 +21,14 @@ namespace ba {
 
 // LM scalars of one step (ba_finalize -> host / ba_decide)
 enum { SC_COST = 0, SC_MODEL = 1, SC_STEPN = 2, SC_XN = 3, SC_GMAX = 4, SC_FAIL = 5, SC_STEPN_F = 6, SC_XN_F = 7, SC_N = 8 };
-constexpr int NB = 64;   // tile of the reduced camera system (ba_chol.hpp, ba_plan.hpp PLAN_NB)
+// Tile of the reduced camera system (ba_chol.hpp, ba_plan.hpp PLAN_NB): NB x NB, factored by
+// workgroups of NW = NB / 16 waves (NTH threads), wave w owning the 16-row strip 16w.
+#ifndef SFMX_BA_NB
+#define SFMX_BA_NB 64
+#endif
+constexpr int NB = SFMX_BA_NB;
+constexpr int NW = NB / 16, NTH = 64 * NW;
+static_assert(NB == 32 || NB == 64, "tile size 32 or 64");
 __host__ __device__ constexpr int jst(int K) { return 20 + 2 * K; }   // Jacobian record stride
 
 // fp64 matrix-core tiles: v_mfma_f64_16x16x4f64 (operands: lane m + 16k holds A[m][k] and

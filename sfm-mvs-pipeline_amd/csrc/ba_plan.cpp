@@ -177,7 +177,9 @@ void pattern(const std::vector<char>& adj, FactorPlan& P) {
 // latency model of one launch sequence (us): per launch its slowest task
 // latency model of one level launch (us, r02q kernels): a task's sources run in parallel parts
 // (chol_level_split), so a task costs one source update, plus the hand-off when it has several
-constexpr double LAT_LAUNCH = 6.0, LAT_LOAD = 2.5, LAT_UPD = 6.5, LAT_INV = 12.0, LAT_HANDOFF = 3.0;
+// (64-row tiles measured; 32-row tiles: a quarter of the tile GEMM work, two of the four sweeps)
+constexpr double LAT_LAUNCH = 6.0, LAT_LOAD = NBP == 64 ? 2.5 : 1.5, LAT_UPD = NBP == 64 ? 6.5 : 2.5,
+                 LAT_INV = NBP == 64 ? 12.0 : 6.0, LAT_HANDOFF = 3.0;
 
 void schedule(FactorPlan& P) {
     const int T = P.T;

@@ -26,7 +26,10 @@
 namespace sfmx {
 namespace ba {
 
-constexpr int PLAN_NB = 64;   // tile size (== NB of the kernels)
+#ifndef SFMX_BA_NB
+#define SFMX_BA_NB 64
+#endif
+constexpr int PLAN_NB = SFMX_BA_NB;   // tile size (== NB of the kernels, ba_kernels.hpp)
 
 struct PlanTask { int a, b, s0, s1; };   // destination tile (a, b), a >= b; source panels src[s0 .. s1)
 

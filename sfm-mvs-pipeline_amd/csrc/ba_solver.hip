@@ -21,6 +21,7 @@
 #include "ba_plan.hpp"
 #include "diag.hpp"
 #include "host_par.hpp"
+#include "rccl_dl.hpp"
 
 #include <algorithm>
 #include <chrono>
@@ -99,6 +100,7 @@ struct sfmx_ba_ctx {
     int nf = 0, npad = 0, T = 0, RW = 0;
     sfmx_allreduce_fn ar = nullptr;
     void* ar_user = nullptr;
+    ncclComm_t comm = nullptr;   // native RCCL (sfmx_ba_set_comm): the collectives go on the solver stream
     // topology: groups, chunks, group cameras, local camera per observation, assembly tasks
     int ngroups = 0, ntasks = 0, nslots = 0, gs_nt = 4;   // gs_nt: ba_gschur specialisation, dp_max / 16
     size_t lds_schur = 0, lds_lin = 0;
@@ -162,6 +164,7 @@ struct sfmx_ba_ctx {
         (void)hipSetDevice(device);
         for (Buf* b : all) b->release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+        if (comm) (void)sfmx::rccl_api().CommDestroy(comm);
         if (st) (void)hipStreamDestroy(st);
         if (hs) (void)hipHostFree(hs);
         if (stage) (void)hipHostFree(stage);
@@ -178,8 +181,18 @@ struct DeviceGuard {
     ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
+// The solve's collectives: native RCCL on the solver's stream when a communicator is set
+// (sfmx_ba_set_comm), else the caller's callback (sfmx_ba_set_allreduce, e.g. gloo in tests).
 int allreduce(sfmx_ba_ctx* c, double* buf, int64_t count, int op) {
-    if (!c->ar || count <= 0) return SFMX_OK;
+    if (count <= 0) return SFMX_OK;
+    if (c->comm) {
+        const sfmx::RcclApi& r = sfmx::rccl_api();
+        const ncclResult_t e = r.AllReduce(buf, buf, (size_t)count, ncclFloat64, op == SFMX_REDUCE_SUM ? ncclSum : ncclMax,
+                                           c->comm, c->st);
+        if (e != ncclSuccess) return fail(SFMX_EDEVICE, std::string("ncclAllReduce: ") + r.GetErrorString(e));
+        return SFMX_OK;
+    }
+    if (!c->ar) return SFMX_OK;
     if (c->ar(buf, count, op, c->ar_user, (void*)c->st) != 0) return fail(SFMX_EDEVICE, "all-reduce callback failed");
     return SFMX_OK;
 }
@@ -223,6 +236,7 @@ int upload(sfmx_ba_ctx* c, Buf& b, const std::vector<T>& v) {
     return SFMX_OK;
 }
 
+bool multirank(const sfmx_ba_ctx* c) { return c->ar != nullptr || c->comm != nullptr; }
 double* scal(sfmx_ba_ctx* c, int i) { return c->scal.as<double>() + i; }
 int* gate(sfmx_ba_ctx* c) { return c->failf.as<int>() + 1; }   // the step gate word (ba_kernels.hpp step_gated)
 
@@ -312,18 +326,18 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double
     // multi-rank speculative steps all-reduce a scratch copy of the camera sums: a skipped step's
     // all-reduce then touches no state (ba_finalize copies them behind the step gate)
     const int ncs = c->C * ncp(K) + K * (K + 1) / 2 + K;
-    double* cs_red = (c->ar && c->spec) ? c->camscr.as<double>() : camsum_o;
+    double* cs_red = (multirank(c) && c->spec) ? c->camscr.as<double>() : camsum_o;
     hipLaunchKernelGGL(ba_camred<K>, dim3(c->C + K * (K + 1) / 2 + K), dim3(128), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
                        c->cref.as<int>(), c->gpart.as<double>(), cs_red, gate(c));
     HIPCHK(hipGetLastError());
     // multi-rank: the group sums ride in the camera-sum all-reduce (cs_red[ncs .. ncs + 4), the
     // rank's point max |grad| at cs_red[ncs + 4] outside it): 3 collectives per LM step, not 4
-    double* pre = c->ar ? cs_red + ncs : nullptr;
+    double* pre = multirank(c) ? cs_red + ncs : nullptr;
     if (pre)
         hipLaunchKernelGGL(ba_group_sums, dim3(1), dim3(256), 0, c->st, c->ngroups, c->gpl.as<double>(), pre, gate(c));
     RC(allreduce(c, cs_red, ncs + (pre ? 4 : 0), SFMX_REDUCE_SUM));
     // one rank, host-judged, no phase mark: ba_finalize publishes the scalars itself (one launch fewer)
-    const bool fold = out && !c->ar && !(c->phases && cand_mode);
+    const bool fold = out && !multirank(c) && !(c->phases && cand_mode);
     const unsigned fold_seq = fold ? ++c->seq : 0;
     hipLaunchKernelGGL(ba_finalize<K>, dim3(1), dim3(256), 0, c->st, c->ngroups, c->P, c->C, cs_red,
                        c->gpl.as<double>(), xp + c->ne, c->x.as<double>() + c->ne, cand_mode ? 1 : 0, c->failf.as<int>(),
@@ -349,28 +363,28 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
     double* ri = Dm + (RW - 1) * (RW - 1);
     int* fl = c->failf.as<int>();
     if (c->dag && c->split) {
-        hipLaunchKernelGGL(chol_factor<RW>, dim3((unsigned)c->n_ditems), dim3(256), 0, c->st, S, npad, R,
+        hipLaunchKernelGGL(chol_factor<RW>, dim3((unsigned)c->n_ditems), dim3(NTH), 0, c->st, S, npad, R,
                            c->ptasks.as<int4>(), c->ditems.as<int4>(), c->dneed.as<int4>(), c->psrc.as<int>(),
                            c->Wt.as<double>(), c->contrib.as<double>(), fl, c->pbuf.as<double>(), c->lctr.as<int>(),
                            c->dctr.as<int>(), c->n_ditems, c->n_ver, c->dag_timeout);
     } else {
-    hipLaunchKernelGGL(chol_leaves<RW>, dim3((unsigned)pl.leaves.size()), dim3(256), 0, c->st, S, npad, R,
+    hipLaunchKernelGGL(chol_leaves<RW>, dim3((unsigned)pl.leaves.size()), dim3(NTH), 0, c->st, S, npad, R,
                        c->leaves.as<int>(), c->Wt.as<double>(), c->contrib.as<double>(), fl);
     for (int l = 0; l < pl.height; ++l) {
         const int t0 = pl.task_start[l], nt = pl.task_start[l + 1] - t0;
         if (c->split) {
             const int p0 = c->part_start[l], np = c->part_start[l + 1] - p0;
-            hipLaunchKernelGGL(chol_level_split<RW>, dim3(np), dim3(256), 0, c->st, S, npad, R, c->ptasks.as<int4>(),
+            hipLaunchKernelGGL(chol_level_split<RW>, dim3(np), dim3(NTH), 0, c->st, S, npad, R, c->ptasks.as<int4>(),
                                c->parts.as<int4>() + p0, c->psrc.as<int>(), c->Wt.as<double>(), c->contrib.as<double>(),
                                fl, c->pbuf.as<double>(), c->lctr.as<int>());
         } else {
-            hipLaunchKernelGGL(chol_level<RW>, dim3(nt), dim3(256), 0, c->st, S, npad, R, c->ptasks.as<int4>() + t0,
+            hipLaunchKernelGGL(chol_level<RW>, dim3(nt), dim3(NTH), 0, c->st, S, npad, R, c->ptasks.as<int4>() + t0,
                                c->psrc.as<int>(), pl.ninv[l], c->Wt.as<double>(), c->contrib.as<double>(), fl);
         }
     }
     }
     if (c->back_dag) {
-        hipLaunchKernelGGL(chol_backsolve<RW>, dim3(c->T), dim3(256), 0, c->st, S, npad, R, Dm, ri,
+        hipLaunchKernelGGL(chol_backsolve<RW>, dim3(c->T), dim3(NTH), 0, c->st, S, npad, R, Dm, ri,
                            c->contrib.as<double>(), c->T, c->border.as<int>(), c->bs_start.as<int>(), c->bs_k.as<int>(),
                            c->rowmap.as<int>(), c->zbuf.as<double>(), sol_f, sol_f + 6 * (size_t)c->C,
                            c->dagctr.as<int>(), fl, c->dag_timeout);
@@ -424,7 +438,7 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     if (c->phases) HIPCHK(hipEventRecord(c->ev[1], c->st));
     // point-sharded ranks: the group part of the reduced camera system and its rhs are sums over
     // ranks; only the structurally nonzero lower tiles (+ R, D, r_i) travel
-    if (c->ar) {
+    if (multirank(c)) {
         const int tail = (int)(c->sr_count - (size_t)npad * npad);
         hipLaunchKernelGGL(chol_pack, dim3(c->n_nztiles + 1), dim3(256), 0, c->st, S, npad, c->nztiles.as<int2>(),
                            c->n_nztiles, tail, c->packbuf.as<double>(), 0, gate(c));
@@ -507,7 +521,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
     const auto t_plan = std::chrono::steady_clock::now();
     const int C = c->C;
     std::vector<char> adj = c->adj;
-    if (c->ar && C > 1) {   // global co-visibility: sum of the ranks' upper triangles
+    if (multirank(c) && C > 1) {   // global co-visibility: sum of the ranks' upper triangles
         std::vector<double> h((size_t)C * (C - 1) / 2);
         for (int a = 0, e = 0; a < C; ++a)
             for (int b = a + 1; b < C; ++b, ++e) h[e] = adj[(size_t)a * C + b] ? 1.0 : 0.0;
@@ -631,8 +645,8 @@ int ensure_plan(sfmx_ba_ctx* c) {
         c->dag = dag_ok && !(ed && ed[0] == '0');
         if (const char* et = SFMX_DIAG_ENV("SFMX_BA_DAG_TIMEOUT")) c->dag_timeout = std::atoll(et);   // recovery test
         max_slots = std::max(max_slots, dslots);
-        const int tpo = std::max(1, 256 / (NB * RW)), opt = NB * RW / (256 / tpo);
-        RC(c->pbuf.alloc(sizeof(double) * (size_t)max_slots * (16 + opt) * 256));
+        const int tpo = std::max(1, NTH / (NB * RW)), opt = NB * RW / (NTH / tpo);
+        RC(c->pbuf.alloc(sizeof(double) * (size_t)max_slots * (4 * NW + opt) * NTH));
         RC(c->lctr.alloc(sizeof(int) * (size_t)((pl.tasks.size() + 4) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->lctr.p, 0, c->lctr.bytes, st));
         const char* e = SFMX_DIAG_ENV("SFMX_BA_SPLIT");
@@ -1277,7 +1291,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
         if (t.type == 0 && t.a != t.b) c->adj[(size_t)t.a * C + t.b] = c->adj[(size_t)t.b * C + t.a] = 1;
     // a plan is reused only when this graph is the one it was built from; ranks of a sharded solve
     // rebuild on every update (the plan needs the co-visibility all-reduced over all of them)
-    if (c->adj != c->plan_adj || c->ar) c->planned = false;
+    if (c->adj != c->plan_adj || multirank(c)) c->planned = false;
     c->setup_ms[0] = ms_since(t_start);
     c->ngroups = (int)tp.grp.size();
     c->ntasks = (int)tp.tasks.size();
@@ -1471,6 +1485,31 @@ int sfmx_ba_create(const sfmx_ba_problem* problem, const sfmx_ba_options* opt, s
     if (!out) return fail(SFMX_EINVAL, "null out");
     *out = nullptr;
     return create(problem, opt, out);
+}
+
+int sfmx_ba_comm_unique_id(void* id) {
+    if (!id) return fail(SFMX_EINVAL, "null id");
+    const sfmx::RcclApi& r = sfmx::rccl_api();
+    if (!r.ok) return fail(SFMX_EDEVICE, "RCCL (librccl.so.1) not loadable");
+    const ncclResult_t e = r.GetUniqueId(static_cast<ncclUniqueId*>(id));
+    if (e != ncclSuccess) return fail(SFMX_EDEVICE, std::string("ncclGetUniqueId: ") + r.GetErrorString(e));
+    return SFMX_OK;
+}
+
+int sfmx_ba_set_comm(sfmx_ba_ctx* c, const void* id, int32_t nranks, int32_t rank) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(SFMX_EINVAL, "bad communicator arguments");
+    const sfmx::RcclApi& r = sfmx::rccl_api();
+    if (!r.ok) return fail(SFMX_EDEVICE, "RCCL (librccl.so.1) not loadable");
+    DeviceGuard dg(c->device);
+    if (c->comm) { (void)r.CommDestroy(c->comm); c->comm = nullptr; }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    ncclComm_t comm = nullptr;
+    const ncclResult_t e = r.CommInitRank(&comm, nranks, uid, rank);
+    if (e != ncclSuccess) return fail(SFMX_EDEVICE, std::string("ncclCommInitRank: ") + r.GetErrorString(e));
+    c->comm = comm;
+    c->planned = false;   // the plan needs the co-visibility of every rank
+    return SFMX_OK;
 }
 
 int sfmx_ba_set_allreduce(sfmx_ba_ctx* c, sfmx_allreduce_fn fn, void* user) {

@@ -117,6 +117,8 @@ PROTOTYPES = {
     "sfmx_ba_solve": (C.c_int, [_P(sfmx_ba_problem), _P(sfmx_ba_options), _P(sfmx_ba_summary), _vp, C.c_int32]),
     "sfmx_ba_create": (C.c_int, [_P(sfmx_ba_problem), _P(sfmx_ba_options), _P(_vp)]),
     "sfmx_ba_set_allreduce": (C.c_int, [_vp, ALLREDUCE_FN, _vp]),
+    "sfmx_ba_comm_unique_id": (C.c_int, [_vp]),
+    "sfmx_ba_set_comm": (C.c_int, [_vp, _vp, C.c_int32, C.c_int32]),
     "sfmx_ba_run": (C.c_int, [_vp, C.c_int32, _P(sfmx_ba_summary), _vp, C.c_int32]),
     "sfmx_ba_get": (C.c_int, [_vp, _P(sfmx_ba_problem)]),
     "sfmx_ba_set": (C.c_int, [_vp, _P(sfmx_ba_problem)]),

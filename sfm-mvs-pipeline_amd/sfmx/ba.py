@@ -118,6 +118,13 @@ def solve(problem: BAProblem, options: Optional[sfmx_ba_options] = None, trace_c
     return summary_dict(sm), tr[:n]
 
 
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (ncclGetUniqueId) for sfmx_ba_set_comm."""
+    buf = C.create_string_buffer(128)
+    check(lib.sfmx_ba_comm_unique_id(buf), "sfmx_ba_comm_unique_id")
+    return buf.raw
+
+
 def release_cache():
     """Free the solver contexts sfmx_ba_solve keeps per device between calls."""
     check(lib.sfmx_ba_release_cache(), "sfmx_ba_release_cache")
@@ -156,6 +163,12 @@ class BAContext:
                     return 1
             self._cb = ALLREDUCE_FN(_cb)
             check(lib.sfmx_ba_set_allreduce(self._h, self._cb, None), "sfmx_ba_set_allreduce")
+
+    def set_comm(self, unique_id: bytes, nranks: int, rank: int):
+        """Native RCCL collectives for the point-sharded solve (sfmx_ba_set_comm): every rank
+        passes the same 128-byte id (from comm_unique_id() on rank 0)."""
+        buf = C.create_string_buffer(bytes(unique_id), 128)
+        check(lib.sfmx_ba_set_comm(self._h, buf, nranks, rank), "sfmx_ba_set_comm")
 
     def run(self, max_iterations: int = 0, trace_cap: int = 0):
         sm = sfmx_ba_summary()

@@ -16,11 +16,15 @@ REDUCE_SUM, REDUCE_MAX = 0, 1
 
 
 def shard_ba_problem(prob: dict, rank: int, world: int) -> dict:
-    """Contiguous point range [P*r/W, P*(r+1)/W) with its observations; cameras and
-    intrinsics replicated.  Observation order (point-major) is preserved."""
+    """A contiguous point range with its observations, cut so that every rank holds about
+    the same number of OBSERVATIONS (the per-step work of ba_glin / ba_gschur / ba_gupdate
+    is per observation; real tracks have 2 to hundreds of them); cameras and intrinsics
+    replicated.  Observation order (point-major) is preserved."""
+    from .shard import shard_bounds
     P = len(prob["points"])
-    lo, hi = P * rank // world, P * (rank + 1) // world
     op = np.asarray(prob["obs_point"])
+    b = shard_bounds(np.bincount(op, minlength=P), world)
+    lo, hi = int(b[rank]), int(b[rank + 1])
     sel = (op >= lo) & (op < hi)
     out = dict(prob)
     out["points"] = np.asarray(prob["points"])[lo:hi]
@@ -29,6 +33,17 @@ def shard_ba_problem(prob: dict, rank: int, world: int) -> dict:
     out["obs_xy"] = np.asarray(prob["obs_xy"])[sel]
     out["point_range"] = (lo, hi)
     return out
+
+
+def rccl_comm(ctx, group=None) -> None:
+    """Give a BAContext native RCCL collectives (sfmx_ba_set_comm): rank 0 creates the id,
+    torch.distributed broadcasts it (any backend), every rank initialises its communicator."""
+    import torch.distributed as dist
+    from .ba import comm_unique_id
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    obj = [comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    ctx.set_comm(obj[0], world, rank)
 
 
 class _DevView:

@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_ba_${1:-r02}
 mkdir -p $OUT
-B="python3 bench.py --only-ba --no-cpu-baseline"
+B="python3 bench.py --only-ba --no-cpu-baseline --no-ba-calls"
 run() { name=$1; shift; timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "ba_|chol_" --output-format csv -d $OUT -o $name -- $B > $OUT/$name.log 2>&1; }
 run p1 FETCH_SIZE && \
 run p2 WRITE_SIZE && \
