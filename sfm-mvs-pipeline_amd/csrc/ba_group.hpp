@@ -138,39 +138,43 @@ __device__ __forceinline__ double dsq(double colsq, double s, double dmin, doubl
     return d * d;
 }
 
-// J records are stored Jacobi-scaled (J_s = J diag(scale): ba_glin writes them scaled once the
-// scale of the solve is known; the first step's ba_gschur<SCALEJ> scales the iteration-0
-// linearization in place), so the step kernels read them without gathering the scales.
+// The linearization is kept as what the step kernels consume, not as Jacobian rows (r03):
+//   per observation  W_o = Je_o^T Jc_o          (3 x 6, row-major [a][d], WST = 18 doubles)
+//   per point        PR_p = E_p 6 | g_p 3 | V_p 3K  with E_p = sum_o Je^T Je (upper: 00 01 02 11 12 22),
+//                    g_p = sum_o Je^T r, V_p = sum_o Je^T Ji ([a][i]), sums in observation order
+// ba_gschur forms M_p, t_p, H_p from them, ba_gupdate back-substitutes with W_o and V_p, and the
+// model cost change is sum_p (s_p.g_p + s_p^T E_p s_p / 2 - s_p.y_p) + the camera part (ba_finalize),
+// i.e. s^T J^T r + |J s|^2 / 2 by blocks: no step kernel reads a Jacobian row.  144 B per observation
+// instead of the 208 B record (K = 3), and ba_gschur no longer sums per-observation partials.
+// Both are stored Jacobi-scaled (ba_glin scales them once the solve's scale is known; the first
+// step's ba_gschur<SCALEJ> scales the iteration-0 linearization in place, with the same products).
+constexpr int WST = 18;
+__host__ __device__ constexpr int npr(int K) { return 9 + 3 * K; }
+// W_o <- diag(sp) W_o diag(sc)
+__device__ __forceinline__ void scale_w(double* w, const double* sp, const double* sc) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int d = 0; d < 6; ++d) w[6 * a + d] = w[6 * a + d] * (sp[a] * sc[d]);
+}
+// element e of a point record -> its scale factor (sp: the point's 3, si: the intrinsics' K)
+// (e may be lane-dependent: selects, no indexed register arrays)
+__device__ __forceinline__ double pick3(const double* s, int u) { return u == 0 ? s[0] : (u == 1 ? s[1] : s[2]); }
 template <int K>
-struct JRec {            // one observation's Jacobian record, scaled
-    double r[2], je[2][3], jc[2][6], ji[2][K];
-};
+__device__ __forceinline__ double pick_k(const double* s, int i) {
+    double v = s[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) v = i == j ? s[j] : v;
+    return v;
+}
 template <int K>
-__device__ __forceinline__ void load_rec(const double* __restrict__ jr, JRec<K>& R) {
-    R.r[0] = jr[0]; R.r[1] = jr[1];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) R.je[j][i] = jr[2 + 3 * j + i];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) R.jc[j][i] = jr[8 + 6 * j + i];
-#pragma unroll
-        for (int i = 0; i < K; ++i) R.ji[j][i] = jr[20 + K * j + i];
+__device__ __forceinline__ double pr_scale(int e, const double* sp, const double* si) {
+    if (e < 6) {
+        const int u = e < 3 ? 0 : (e < 5 ? 1 : 2), v = e < 3 ? e : (e < 5 ? e - 2 : 2);
+        return pick3(sp, u) * pick3(sp, v);
     }
-}
-template <int K>
-__device__ __forceinline__ void load_jrec(const double* __restrict__ J, int o, JRec<K>& R) {
-    load_rec<K>(J + (size_t)o * jst(K), R);
-}
-// the record as 13 (or 10 + K) independent 16-B loads
-template <int K>
-__device__ __forceinline__ void load_jrec_v(const double* __restrict__ J, int o, JRec<K>& R) {
-    constexpr int JS = jst(K);
-    const double2* s2 = reinterpret_cast<const double2*>(J + (size_t)o * JS);
-    double v[JS];
-#pragma unroll
-    for (int i = 0; i < JS / 2; ++i) { const double2 t = s2[i]; v[2 * i] = t.x; v[2 * i + 1] = t.y; }
-    load_rec<K>(v, R);
+    if (e < 9) return pick3(sp, e - 6);
+    return pick3(sp, (e - 9) / K) * pick_k<K>(si, (e - 9) % K);
 }
 
 // Copy n2 16-B pieces global -> LDS with every load issued before the first store (a plain
@@ -193,10 +197,9 @@ __device__ __forceinline__ void stage_copy(double2* __restrict__ dst, const doub
 // (into rg); per point M_p and t_p (plt, 9 doubles) for the back substitution.
 // Normal groups: no workgroup barrier until the end.  Each wave takes every 4th batch of the
 // group (<= 64 observations, <= 16 whole points, host-built) and keeps its own accumulators:
-//   lane = observation: its J record straight into registers (13 x 16-B loads), the scaled
-//     blocks, W_o = Je_s^T Jc_s (registers) and the point partials E (6), g (3), V (3K) -> wave LDS;
-//   lane = point: sums its observations' partials in observation order, + D_p^2, M = chol(E)^-1,
-//     t = M g, Hi = M V -> wave LDS + plt;
+//   lane = observation: its W_o = Je_s^T Jc_s straight into registers (9 x 16-B loads);
+//   4 lanes = point: its record (E, g, V; a quarter each) -> the point's wave LDS slot; lane 0 of
+//     the 4: + D_p^2, M = chol(E)^-1, t = M g, Hi = M V -> wave LDS + plt;
 //   rounds of 4 points: H_p columns (camera rows Z_o = (M W_o)^T, intrinsics rows Hi) -> a zeroed
 //     4 x dp x 3 wave buffer; the SYRK on v_mfma_f64_16x16x4f64 takes the 4 points as its k
 //     slots: lane m + 16kk holds H_{p_kk}[16I + m][c], so tile (I, J) += 3 MFMAs (c = 0..2), the
@@ -207,16 +210,13 @@ __device__ __forceinline__ void stage_copy(double2* __restrict__ dst, const doub
 // NT = dp_max / 16 (NT (NT + 1) / 2 upper 16x16 tiles per wave).
 // Big groups (one point with > 64 observations, too many cameras or two observations in one
 // camera): the serial path, one thread per point / camera.
-// SCALEJ (the first step of a solve, J still unscaled from iteration 0): every record is scaled
-// by the solve's Jacobi scale as it is read, and written back scaled (J_s, load_rec).
-// Dynamic LDS: per wave max(64 x NPF partials, 4 x HS H columns) + WB_PTS x PD point data;
-// the final combine reuses it as [dp][dp + 1] + rhs.
-__host__ __device__ constexpr int gs_npf(int K) { return 9 + 3 * K; }                 // E 6 | g 3 | V 3K
-__host__ __device__ constexpr int gs_pd(int K) { return 9 + 3 * K; }                  // M 6 | t 3 | Hi 3K
+// SCALEJ (the first step of a solve, the records still unscaled from iteration 0): every W_o and
+// point record is scaled by the solve's Jacobi scale as it is read, and written back scaled.
+// Dynamic LDS: per wave 4 x HS H columns + WB_PTS x PD point data; the final combine reuses it
+// as [dp][dp + 1] + rhs.
+__host__ __device__ constexpr int gs_pd(int K) { return 9 + 3 * K; }                  // E | g | V, then M 6 | t 3 | Hi 3K
 __host__ __device__ constexpr int gs_hs(int dp) { return 3 * dp + 2; }                // per-point H column block
-__host__ __device__ constexpr int gs_wreg(int K, int dp) {                            // doubles per wave
-    return (WB_OBS * gs_npf(K) > 4 * gs_hs(dp) ? WB_OBS * gs_npf(K) : 4 * gs_hs(dp)) + WB_PTS * gs_pd(K);
-}
+__host__ __device__ constexpr int gs_wreg(int K, int dp) { return 4 * gs_hs(dp) + WB_PTS * gs_pd(K); }   // doubles per wave
 #ifndef GSCHUR_WAVES
 #define GSCHUR_WAVES 2   // waves per SIMD the register budget targets (A/B: -DGSCHUR_WAVES=3)
 #endif
@@ -224,59 +224,44 @@ template <int K, int NT, bool SCALEJ>
 __global__ __launch_bounds__(256, GSCHUR_WAVES)
 void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const int* __restrict__ gcam,
                const short* __restrict__ obs_lc, const int* __restrict__ obs_point, const int* __restrict__ obs_cam,
-               const int* __restrict__ pt_start, const double* __restrict__ J, const double* __restrict__ scale,
-               const double* __restrict__ colsq, double dmin, double dmax, double radius, int P, int C,
-               double* __restrict__ plt, double* __restrict__ sg, double* __restrict__ rg, double* __restrict__ hbig,
-               int* __restrict__ fail, const double* __restrict__ lm) {
+               const int* __restrict__ pt_start, const double* __restrict__ Wr, const double* __restrict__ PRr,
+               const double* __restrict__ scale, const double* __restrict__ colsq, double dmin, double dmax,
+               double radius, int P, int C, double* __restrict__ plt, double* __restrict__ sg, double* __restrict__ rg,
+               double* __restrict__ hbig, int* __restrict__ fail, const double* __restrict__ lm) {
     if (step_gated(fail + 1)) return;
     if (lm) radius = lm[LM_RADIUS];
     extern __shared__ __attribute__((aligned(16))) double gl[];
-    constexpr int NPF = gs_npf(K), PD = gs_pd(K);
+    constexpr int PD = gs_pd(K), NPR = npr(K);
     const Grp G = grp[blockIdx.x];
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, m16 = l & 15, kk = l >> 4;
     const int dim = gdim(G, K);
+    const size_t ne = 3 * (size_t)P;
+    const double* si = scale + ne + 6 * (size_t)C;
     double* pd = gl;   // big groups: the point's M, t
 
     if (G.big) {   // one point, any number of observations / cameras: serial per point, per camera
         const int p = G.p0;
+        const double* sp = scale + 3 * (size_t)p;
         if (SCALEJ) {   // scale the point's records in place first (one thread per observation)
-            constexpr int JS = jst(K);
-            const size_t ne = 3 * (size_t)P;
             for (int o = G.o0 + tid; o < G.o1; o += blockDim.x) {
-                double* v = const_cast<double*>(J) + (size_t)o * JS;
-                const double* sp = scale + 3 * (size_t)p;
+                double* v = const_cast<double*>(Wr) + (size_t)o * WST;
                 const double* sc = scale + ne + 6 * (size_t)obs_cam[o];
-                const double* si = scale + ne + 6 * (size_t)C;
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) v[2 + 3 * j + i] *= sp[i];
-#pragma unroll
-                    for (int i = 0; i < 6; ++i) v[8 + 6 * j + i] *= sc[i];
-#pragma unroll
-                    for (int i = 0; i < K; ++i) v[20 + K * j + i] *= si[i];
-                }
+                scale_w(v, sp, sc);
+            }
+            if (tid < NPR) {
+                double* v = const_cast<double*>(PRr) + (size_t)p * NPR + tid;
+                *v = *v * pr_scale<K>(tid, sp, si);
             }
             __threadfence_block();
             __syncthreads();
         }
         if (tid == 0) {
-            const double sp[3] = {scale[3 * (size_t)p], scale[3 * (size_t)p + 1], scale[3 * (size_t)p + 2]};
-            double E[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0}, Wi[3 * K];
+            const double* pr = PRr + (size_t)p * NPR;
+            double E[9] = {pr[0], pr[1], pr[2], pr[1], pr[3], pr[4], pr[2], pr[4], pr[5]}, g[3], Wi[3 * K];
 #pragma unroll
-            for (int i = 0; i < 3 * K; ++i) Wi[i] = 0.0;
-            for (int o = G.o0; o < G.o1; ++o) {
-                JRec<K> R;
-                load_jrec<K>(J, o, R);
+            for (int i = 0; i < 3; ++i) g[i] = pr[6 + i];
 #pragma unroll
-                for (int a = 0; a < 3; ++a) {
-#pragma unroll
-                    for (int b = 0; b < 3; ++b) E[a * 3 + b] += R.je[0][a] * R.je[0][b] + R.je[1][a] * R.je[1][b];
-                    g[a] += R.je[0][a] * R.r[0] + R.je[1][a] * R.r[1];
-#pragma unroll
-                    for (int i = 0; i < K; ++i) Wi[a * K + i] += R.je[0][a] * R.ji[0][i] + R.je[1][a] * R.ji[1][i];
-                }
-            }
+            for (int i = 0; i < 3 * K; ++i) Wi[i] = pr[9 + i];
 #pragma unroll
             for (int i = 0; i < 3; ++i) E[4 * i] += dsq(colsq[3 * (size_t)p + i], sp[i], dmin, dmax, radius);
             double M[6];
@@ -320,12 +305,11 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
                 for (int d = 0; d < 6; ++d) W[a][d] = 0.0;
             for (int o = G.o0; o < G.o1; ++o) {
                 if (obs_lc[o] != lc) continue;
-                JRec<K> R;
-                load_jrec<K>(J, o, R);
+                const double* wo = Wr + (size_t)o * WST;
 #pragma unroll
                 for (int a = 0; a < 3; ++a)
 #pragma unroll
-                    for (int d = 0; d < 6; ++d) W[a][d] += R.je[0][a] * R.jc[0][d] + R.je[1][a] * R.jc[1][d];
+                    for (int d = 0; d < 6; ++d) W[a][d] += wo[6 * a + d];
             }
 #pragma unroll
             for (int d = 0; d < 6; ++d)
@@ -345,25 +329,26 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
     BA_T0();
     const int dp = (dim + 15) & ~15, nt = dp >> 4, HS = gs_hs(dp);
     const int wreg = gs_wreg(K, dp);
-    double* part = gl + (size_t)w * wreg;            // [64][NPF] partials, then the H columns [4][HS]
-    double* Hb = part;
-    double* pw = part + wreg - WB_PTS * PD;           // [WB_PTS][PD] point data
+    double* Hb = gl + (size_t)w * wreg;               // [4][HS] the H columns of a round
+    double* pw = Hb + 4 * HS;                         // [WB_PTS][PD] point data
     constexpr int NTT = NT * (NT + 1) / 2;            // upper tiles (NT = dp_max / 16 of the launch)
     f64x4 acc[NTT];
 #pragma unroll
     for (int t = 0; t < NTT; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
     double racc[NT] = {};
     // The group's batch descriptors go to LDS once, so the batch loop issues no dependent loads.
-    // Software pipeline: every global load of batch bi + 4 (this lane's observation: its J record,
-    // point and camera slot; this lane's point: its observation range, colsq and scale) is issued
-    // right after batch bi has consumed its own, before the plt stores; the SYRK rounds in between
-    // touch only LDS and registers, so nothing waits for those loads until the next batch.
+    // Software pipeline: every global load of batch bi + 4 (this lane's observation: its W_o, point
+    // and camera slot; this lane's point: a quarter of its record, colsq and scale) is issued right
+    // after batch bi has consumed its own, before the plt stores; the SYRK rounds in between touch
+    // only LDS and registers, so nothing waits for those loads until the next batch.
     Batch* bl = reinterpret_cast<Batch*>(gl + 4 * (size_t)wreg);
     for (int i = tid; i < G.nb; i += 256) bl[i] = bat[G.b0 + i];
     __syncthreads();
-    constexpr int JS = jst(K);
-    double2 pre[JS / 2];
-    int pre_q = 0, pre_lc = 0, pre_a0 = 0, pre_a1 = 0, pre_p = 0, pre_c = 0;
+    constexpr int QS = (NPR + 3) / 4;                 // record elements per lane of a point
+    const int qp = l >> 2, qk = l & 3;
+    double2 pre[WST / 2];
+    double pre_pr[QS];
+    int pre_q = 0, pre_lc = 0, pre_p = 0, pre_c = 0;
     double pre_cs[3] = {0, 0, 0}, pre_sp[3] = {0, 0, 0};
     auto prefetch = [&](int bi) {
         if (bi >= G.nb) return;
@@ -374,17 +359,22 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
             pre_q = pre_p - Bn.p0;
             pre_lc = obs_lc[on];
             if (SCALEJ) pre_c = obs_cam[on];
-            const double2* s2 = reinterpret_cast<const double2*>(J + (size_t)on * JS);
+            const double2* s2 = reinterpret_cast<const double2*>(Wr + (size_t)on * WST);
 #pragma unroll
-            for (int i = 0; i < JS / 2; ++i) pre[i] = s2[i];
+            for (int i = 0; i < WST / 2; ++i) pre[i] = s2[i];
         }
-        if ((l >> 2) < Bn.p1 - Bn.p0) {   // 4 lanes per point (the point phase)
-            const int p = Bn.p0 + (l >> 2);
-            pre_a0 = pt_start[p] - Bn.o0;
-            pre_a1 = pt_start[p + 1] - Bn.o0;
-            if ((l & 3) == 0)
+        if (qp < Bn.p1 - Bn.p0) {
+            const int p = Bn.p0 + qp;
+            const double* pr = PRr + (size_t)p * NPR + qk * QS;
 #pragma unroll
-                for (int i = 0; i < 3; ++i) { pre_cs[i] = colsq[3 * (size_t)p + i]; pre_sp[i] = scale[3 * (size_t)p + i]; }
+            for (int j = 0; j < QS; ++j)
+                if (qk * QS + j < NPR) pre_pr[j] = pr[j];
+            if (SCALEJ || qk == 0)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) pre_sp[i] = scale[3 * (size_t)p + i];
+            if (qk == 0)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) pre_cs[i] = colsq[3 * (size_t)p + i];
         }
     };
     prefetch(w);
@@ -395,76 +385,40 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
         double W[3][6];
         const int lc = pre_lc, q = pre_q;
         if (ov) {
-            JRec<K> R;
-            {
-                double v[JS];
+            double v[WST];
 #pragma unroll
-                for (int i = 0; i < JS / 2; ++i) { v[2 * i] = pre[i].x; v[2 * i + 1] = pre[i].y; }
-                if (SCALEJ) {   // J_s = J diag(scale), stored back once
-                    const size_t ne = 3 * (size_t)P;
-                    const double* sp = scale + 3 * (size_t)pre_p;
-                    const double* sc = scale + ne + 6 * (size_t)pre_c;
-                    const double* si = scale + ne + 6 * (size_t)C;
+            for (int i = 0; i < WST / 2; ++i) { v[2 * i] = pre[i].x; v[2 * i + 1] = pre[i].y; }
+            if (SCALEJ) {   // W_s = diag(sp) W diag(sc), stored back once
+                scale_w(v, scale + 3 * (size_t)pre_p, scale + ne + 6 * (size_t)pre_c);
+                double2* d2 = reinterpret_cast<double2*>(const_cast<double*>(Wr) + (size_t)o * WST);
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-#pragma unroll
-                        for (int i = 0; i < 3; ++i) v[2 + 3 * j + i] *= sp[i];
-#pragma unroll
-                        for (int i = 0; i < 6; ++i) v[8 + 6 * j + i] *= sc[i];
-#pragma unroll
-                        for (int i = 0; i < K; ++i) v[20 + K * j + i] *= si[i];
-                    }
-                    double2* d2 = reinterpret_cast<double2*>(const_cast<double*>(J) + (size_t)o * JS);
-#pragma unroll
-                    for (int i = 0; i < JS / 2; ++i) d2[i] = make_double2(v[2 * i], v[2 * i + 1]);
-                }
-                load_rec<K>(v, R);
+                for (int i = 0; i < WST / 2; ++i) d2[i] = make_double2(v[2 * i], v[2 * i + 1]);
             }
-            double* pt = part + l * NPF;
-            int e = 0;
-#pragma unroll
-            for (int u = 0; u < 3; ++u)
-#pragma unroll
-                for (int v = u; v < 3; ++v) pt[e++] = R.je[0][u] * R.je[0][v] + R.je[1][u] * R.je[1][v];
-#pragma unroll
-            for (int u = 0; u < 3; ++u) pt[6 + u] = R.je[0][u] * R.r[0] + R.je[1][u] * R.r[1];
-#pragma unroll
-            for (int u = 0; u < 3; ++u)
-#pragma unroll
-                for (int i = 0; i < K; ++i) pt[9 + u * K + i] = R.je[0][u] * R.ji[0][i] + R.je[1][u] * R.ji[1][i];
 #pragma unroll
             for (int a = 0; a < 3; ++a)
 #pragma unroll
-                for (int d = 0; d < 6; ++d) W[a][d] = R.je[0][a] * R.jc[0][d] + R.je[1][a] * R.jc[1][d];
+                for (int d = 0; d < 6; ++d) W[a][d] = v[6 * a + d];
+        }
+        // point phase: the 4 lanes of a point put its record into the point's pw slot; after a wave
+        // barrier lane k = 0 reads it back and does the rest
+        if (qp < np) {
+            double* ps = pw + qp * PD + qk * QS;
+#pragma unroll
+            for (int j = 0; j < QS; ++j)
+                if (qk * QS + j < NPR) {
+                    double vv = pre_pr[j];
+                    if (SCALEJ) {
+                        vv = vv * pr_scale<K>(qk * QS + j, pre_sp, si);
+                        const_cast<double*>(PRr)[(size_t)(B.p0 + qp) * NPR + qk * QS + j] = vv;
+                    }
+                    ps[j] = vv;
+                }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         BA_STAMP(3);
         double Mq[6] = {0, 0, 0, 0, 0, 0}, tq[3] = {0, 0, 0};
-        // point phase, 4 lanes per point (lane = 4 q + k): lane k sums quantities [k QS, (k + 1) QS) of
-        // the point's observation partials (each sum in observation order, as one lane summed them all),
-        // into the point's pw slot; after a wave barrier lane k = 0 reads them back and does the rest
-        constexpr int NQ = 9 + 3 * K, QS = (NQ + 3) / 4;
-        const int qp = l >> 2, qk = l & 3;
-        if (qp < np) {
-            double sq[QS];
-#pragma unroll
-            for (int j = 0; j < QS; ++j) sq[j] = 0.0;
-            for (int b = pre_a0; b < pre_a1; ++b) {
-                const double* pt = part + b * NPF + qk * QS;
-#pragma unroll
-                for (int j = 0; j < QS; ++j)
-                    if (qk * QS + j < NQ) sq[j] += pt[j];
-            }
-            double* ps = pw + qp * PD + qk * QS;
-#pragma unroll
-            for (int j = 0; j < QS; ++j)
-                if (qk * QS + j < NQ) ps[j] = sq[j];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (qp < np && qk == 0) {
             double* pq = pw + qp * PD;
             double E6[6], g[3], V[3 * K];
@@ -515,7 +469,7 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         BA_STAMP(4);
         for (int r0 = 0; r0 < np; r0 += 4) {
-            for (int e = l; e < 4 * HS; e += 64) Hb[e] = 0.0;   // partials are dead: overlay
+            for (int e = l; e < 4 * HS; e += 64) Hb[e] = 0.0;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -765,14 +719,191 @@ __device__ __forceinline__ int field_of(int r, int c) {   // Gram entry (r <= c)
     return -1;   // r^T r (not a partial field)
 }
 
+// The same sums of a normal chunk's point in two halves on different waves (threads 0..127: E | g,
+// colsq, grad; threads 128..255: V), each half in observation order as point_sums, with the scale
+// products of pr_scale.
+template <int K>
+__device__ __forceinline__ void point_eg(const double* __restrict__ jer, int a0, int a1, int p,
+                                         const double* __restrict__ jscale, double* __restrict__ colsq,
+                                         double* __restrict__ grad, double* __restrict__ PRo, double& gmax) {
+    constexpr int NPR = npr(K);
+    double pr[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) pr[i] = 0.0;
+    for (int b = a0; b < a1; ++b) {
+        const double* r = jer + b * 8;
+        int e = 0;
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int v = u; v < 3; ++v) pr[e++] += r[u] * r[v] + r[3 + u] * r[3 + v];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) pr[6 + u] += r[u] * r[6] + r[3 + u] * r[7];
+    }
+    constexpr int dg[3] = {0, 3, 5};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        colsq[3 * (size_t)p + i] = pr[dg[i]];
+        grad[3 * (size_t)p + i] = pr[6 + i];
+        gmax = fmax(gmax, fabs(pr[6 + i]));
+    }
+    if (jscale) {
+        const double* sp = jscale + 3 * (size_t)p;
+        const double sv[3] = {sp[0], sp[1], sp[2]};
+#pragma unroll
+        for (int e = 0; e < 9; ++e) pr[e] = pr[e] * pr_scale<K>(e, sv, sv);
+    }
+#pragma unroll
+    for (int e = 0; e < 9; ++e) PRo[(size_t)p * NPR + e] = pr[e];
+}
+template <int K>
+__device__ __forceinline__ void point_v(const double* __restrict__ jer, const double* __restrict__ G,
+                                        const short* __restrict__ orw, int a0, int a1, int p, int P, int C,
+                                        const double* __restrict__ jscale, double* __restrict__ PRo) {
+    constexpr int NPR = npr(K), NF = nfeat(K);
+    double v[3 * K];
+#pragma unroll
+    for (int i = 0; i < 3 * K; ++i) v[i] = 0.0;
+    for (int b = a0; b < a1; ++b) {
+        const double* r = jer + b * 8;
+        const double* g0 = G + orw[b] * NF;
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int i = 0; i < K; ++i) v[u * K + i] += r[u] * g0[6 + i] + r[3 + u] * g0[NF + 6 + i];
+    }
+    if (jscale) {
+        const double* sp = jscale + 3 * (size_t)p;
+        const double* si = jscale + 3 * (size_t)P + 6 * (size_t)C;
+        const double sv[3] = {sp[0], sp[1], sp[2]};
+        double sk[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) sk[i] = si[i];
+#pragma unroll
+        for (int e = 0; e < 3 * K; ++e) v[e] = v[e] * pr_scale<K>(9 + e, sv, sk);
+    }
+#pragma unroll
+    for (int e = 0; e < 3 * K; ++e) PRo[(size_t)p * NPR + 9 + e] = v[e];
+}
+// The LM step's point update (ba_gupdate): from sol_f (scaled
+// camera/intrinsics solution), the stored M, t and the records: y_p = sum_o W_o sol_c(o) + V_p
+// sol_i (= W_p sol_f), sol_e = M^T (t - M y), step = -sol; candidate points cand = x + step * scale;
+// ||x - cand||^2; and the points' part of the model cost change, s.g + s^T E s / 2 - s.y with s the
+// point's step: the sum of m (r + m / 2), m = J_s step, over the point's residuals, by blocks
+// (s^T J^T r + |J s|^2 / 2 with J^T J's point rows E_p and W_p; the camera rows' part, s_f.g_f +
+// s_f^T C s_f / 2, is ba_finalize's).
+// y_o = W_o sol_c of the observation's camera (the back substitution's per-observation term)
+__device__ __forceinline__ void obs_y(const double* __restrict__ Wr, int o, const double* __restrict__ solc, double* __restrict__ y3) {
+    const double2* s2 = reinterpret_cast<const double2*>(Wr + (size_t)o * WST);
+    double wv[WST], sc[6];
+#pragma unroll
+    for (int i = 0; i < WST / 2; ++i) { const double2 t = s2[i]; wv[2 * i] = t.x; wv[2 * i + 1] = t.y; }
+#pragma unroll
+    for (int d = 0; d < 6; ++d) sc[d] = solc[d];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        double yk = 0.0;
+#pragma unroll
+        for (int d = 0; d < 6; ++d) yk += wv[6 * k + d] * sc[d];
+        y3[k] = yk;
+    }
+}
+template <int K>
+__device__ __forceinline__ void point_step(int p, double (&y)[3], const double* __restrict__ PRr,
+                                           const double* __restrict__ plt, const double (&soli)[K],
+                                           const double* __restrict__ x, const double* __restrict__ scale,
+                                           double* __restrict__ cand, double& model, double& sn, double (&cvo)[3]) {
+    constexpr int NPR = npr(K);
+    const double* pr = PRr + (size_t)p * NPR;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int i = 0; i < K; ++i) y[k] += pr[9 + k * K + i] * soli[i];
+    const double* Mt = plt + 9 * (size_t)p;
+    double v[3], st[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        double my = 0.0;
+#pragma unroll
+        for (int j = 0; j <= k; ++j) my += mlo(Mt, k, j) * y[j];
+        v[k] = Mt[6 + k] - my;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = j; k < 3; ++k) s += mlo(Mt, k, j) * v[k];
+        st[j] = -s;                                 // step_s = -sol
+        const double xv = x[3 * (size_t)p + j], cv = xv + st[j] * scale[3 * (size_t)p + j];
+        cand[3 * (size_t)p + j] = cv;
+        cvo[j] = cv;
+        const double dd = xv - cv;
+        sn += isfinite(dd) ? dd * dd : INFINITY;
+    }
+    const double q = pr[0] * st[0] * st[0] + pr[3] * st[1] * st[1] + pr[5] * st[2] * st[2] +
+                     2.0 * (pr[1] * st[0] * st[1] + pr[2] * st[0] * st[2] + pr[4] * st[1] * st[2]);
+    model += (st[0] * pr[6] + st[1] * pr[7] + st[2] * pr[8]) + 0.5 * q - (st[0] * y[0] + st[1] * y[1] + st[2] * y[2]);
+}
 // ba_glin: residuals + Jacobian at xp (x or the candidate) for the group's observations.
-// Writes the J records (scaled by jscale when given: the solve's Jacobi scale), per point colsq / grad (unscaled), per (group, camera) partials (gpart:
-// the per-camera Gram matrices of the feature rows on the fp64 matrix cores, rows of one camera
-// contiguous and zero-padded by the host-built layout), and the group's cost, sum xp^2 (its
-// points) and max |grad| partials.  Big groups: feature rows in observation order and a scalar
-// per-(camera, field) loop.
-// Dynamic LDS: G[max rows][NF] | jer[GCH][8] (je | r) | olc[GCH] (short).
+// Writes the step kernels' records (scaled by jscale when given: the solve's Jacobi scale): W_o per
+// observation and E | g | V per point (see WST / npr); per point colsq / grad (unscaled: the diagonal
+// of E and g before scaling); per (group, camera) partials (gpart: the per-camera Gram matrices of
+// the feature rows on the fp64 matrix cores, rows of one camera contiguous and zero-padded by the
+// host-built layout); and the group's cost, sum xp^2 (its points) and max |grad| partials.  Big
+// groups: feature rows in observation order, a scalar per-(camera, field) loop, the point sums by
+// thread 0 across the chunks.
+// Dynamic LDS: G[max rows][NF] | jer[GCH][8] (je | r) | olc[GCH] | orw[GCH] (short: camera slot,
+// feature row of the observation).
 constexpr int GROWS = 2 * GCH + 3 * UMAX;   // feature rows of a chunk incl. per-camera padding
+// the point sums of E | g | V over observations b in [a0, a1) of a chunk: Je and r from jer, Ji from
+// the observation's feature rows (unscaled)
+template <int K>
+__device__ __forceinline__ void point_sums(const double* __restrict__ jer, const double* __restrict__ G,
+                                           const short* __restrict__ orw, int a0, int a1, double (&pr)[npr(K)]) {
+    constexpr int NF = nfeat(K);
+    for (int b = a0; b < a1; ++b) {
+        const double* r = jer + b * 8;
+        const double* g0 = G + orw[b] * NF;
+        int e = 0;
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int v = u; v < 3; ++v) pr[e++] += r[u] * r[v] + r[3 + u] * r[3 + v];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) pr[6 + u] += r[u] * r[6] + r[3 + u] * r[7];
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int i = 0; i < K; ++i) pr[9 + u * K + i] += r[u] * g0[6 + i] + r[3 + u] * g0[NF + 6 + i];
+    }
+}
+// colsq / grad of the point (unscaled), then its record (scaled) -> PRo
+template <int K>
+__device__ __forceinline__ void point_store(int p, int P, int C, double (&pr)[npr(K)], const double* __restrict__ jscale,
+                                            double* __restrict__ colsq, double* __restrict__ grad,
+                                            double* __restrict__ PRo, double& gmax) {
+    constexpr int NPR = npr(K);
+    constexpr int dg[3] = {0, 3, 5};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        colsq[3 * (size_t)p + i] = pr[dg[i]];
+        grad[3 * (size_t)p + i] = pr[6 + i];
+        gmax = fmax(gmax, fabs(pr[6 + i]));
+    }
+    if (jscale) {
+        const double* sp = jscale + 3 * (size_t)p;
+        const double* si = jscale + 3 * (size_t)P + 6 * (size_t)C;
+        const double sv[3] = {sp[0], sp[1], sp[2]};
+        double sk[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) sk[i] = si[i];
+#pragma unroll
+        for (int e = 0; e < NPR; ++e) pr[e] = pr[e] * pr_scale<K>(e, sv, sk);
+    }
+    double2* d2 = reinterpret_cast<double2*>(PRo + (size_t)p * NPR);
+#pragma unroll
+    for (int i = 0; i < NPR / 2; ++i) d2[i] = make_double2(pr[2 * i], pr[2 * i + 1]);
+}
 // MULTI: several cameras, each pose's block and principal point from (pim, pcc) (project_blk).
 template <int K, bool MULTI = false>
 __global__ __launch_bounds__(256, 2)
@@ -780,16 +911,17 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
              const short* __restrict__ obs_lc, const short* __restrict__ obs_row, const int* __restrict__ obs_point,
              const int* __restrict__ obs_cam, const double* __restrict__ obs_xy, const int* __restrict__ pt_start,
              double cx, double cy, int P, int C, const double* __restrict__ xp, const double* __restrict__ jscale,
-             double* __restrict__ J, double* __restrict__ colsq, double* __restrict__ grad,
+             double* __restrict__ Wo, double* __restrict__ PRo, double* __restrict__ colsq, double* __restrict__ grad,
              double* __restrict__ gpart, double* __restrict__ gpl, const int* __restrict__ gate,
              const int* __restrict__ pim, const double2* __restrict__ pcc) {
     if (step_gated(gate)) return;
     extern __shared__ __attribute__((aligned(16))) double gl[];
-    constexpr int JS = jst(K), NCP = ncp(K), N = 9 + K, NF = nfeat(K);
+    constexpr int JS = jst(K), NCP = ncp(K), N = 9 + K, NF = nfeat(K), NPR = npr(K);
     __shared__ double sh[8];
     double* G = gl;                                    // [GROWS][NF]
     double* jer = G + GROWS * NF;                      // [GCH][8]
     short* olc = reinterpret_cast<short*>(jer + GCH * 8);
+    short* orw = olc + GCH;
     const Grp Gp = grp[blockIdx.x];
     // w through readfirstlane: the per-camera row ranges (lcrow of camera w + 4i) become scalar, so
     // the Gram loop's bounds and its tail conditions are scalar branches, not exec-masked lanes
@@ -802,7 +934,8 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
 #pragma unroll
     for (int i = 0; i < UMAX / 4; ++i) acc[i] = f64x4{0.0, 0.0, 0.0, 0.0};
     const int npart = Gp.u * NCP;
-    double pcs[3] = {0, 0, 0}, pgr[3] = {0, 0, 0};   // big groups: the point's sums (thread 0)
+    __shared__ double bpr[npr(7)];   // big groups: the point's sums across the chunks (thread 0)
+    if (tid < NPR) bpr[tid] = 0.0;
     if (Gp.big)
         for (int i = tid; i < npart; i += blockDim.x) gpart[(size_t)Gp.cam_off * NCP + i] = 0.0;
     const int nchunks = Gp.big ? (Gp.o1 - Gp.o0 + GCH - 1) / GCH : Gp.nch;
@@ -812,17 +945,22 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
         if (Gp.big) { ch.o0 = Gp.o0 + c * GCH; ch.o1 = min(Gp.o1, ch.o0 + GCH); ch.q0 = 0; ch.q1 = 0; ch.lc0 = 0; ch.nrows = 2 * (ch.o1 - ch.o0); }
         else ch = chk[Gp.ch0 + c];
         for (int e = tid; e < ch.nrows * NF; e += blockDim.x) G[e] = 0.0;   // padding rows stay zero
-        // every global load of the chunk goes out before its J stores: a wait for a load issued
-        // after 13 stores per lane would wait for the stores too (vmcnt counts both, in order)
+        // every global load of the chunk goes out before its record stores: a wait for a load issued
+        // after the stores would wait for the stores too (vmcnt counts both, in order)
         const int a = tid, o = ch.o0 + a;
-        const bool ptl = !Gp.big && tid >= ch.q0 && tid < ch.q1;
+        // point threads: tid and tid + 128 hold point q0 + (tid & 127) (its E | g and V halves); the
+        // point's norm is the first half's
+        const int qv = tid & 127;
+        const bool pth = !Gp.big && qv >= ch.q0 && qv < ch.q1;
+        const bool ptl = pth && tid < 128;
         int pa0 = 0, pa1 = 0, orow = 0, olcv = 0;
-        if (ptl) {
-            const int p = Gp.p0 + tid;
+        if (pth) {
+            const int p = Gp.p0 + qv;
             pa0 = pt_start[p] - ch.o0;
             pa1 = pt_start[p + 1] - ch.o0;
+            if (ptl)
 #pragma unroll
-            for (int i = 0; i < 3; ++i) xn += pts[3 * (size_t)p + i] * pts[3 * (size_t)p + i];
+                for (int i = 0; i < 3; ++i) xn += pts[3 * (size_t)p + i] * pts[3 * (size_t)p + i];
         }
         int cr0[UMAX / 4], cr1[UMAX / 4];
 #pragma unroll
@@ -863,27 +1001,22 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
 #pragma unroll
                 for (int i = 0; i < K; ++i) rec[20 + K * j + i] = res[j].v[9 + i];
             }
-            {   // the stored record is Jacobi-scaled (load_rec); the partials below use the unscaled one
-                double sj[JS];
+            {   // W_o = Je^T Jc (unscaled products, then the scale: the same values ba_gschur<SCALEJ>
+                // makes), one row of 6 at a time straight to its stores
+                double2* dst = reinterpret_cast<double2*>(Wo + (size_t)o * WST);
+                const double* sp = jscale + 3 * (size_t)p;
+                const double* sc = jscale + 3 * (size_t)P + 6 * (size_t)cm;
 #pragma unroll
-                for (int i = 0; i < JS; ++i) sj[i] = rec[i];
-                if (jscale) {
-                    const double* sp = jscale + 3 * (size_t)p;
-                    const double* sc = jscale + 3 * (size_t)P + 6 * (size_t)cm;
-                    const double* si = jscale + 3 * (size_t)P + 6 * (size_t)C;
+                for (int u = 0; u < 3; ++u) {
+                    double wv[6];
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-#pragma unroll
-                        for (int i = 0; i < 3; ++i) sj[2 + 3 * j + i] *= sp[i];
-#pragma unroll
-                        for (int i = 0; i < 6; ++i) sj[8 + 6 * j + i] *= sc[i];
-#pragma unroll
-                        for (int i = 0; i < K; ++i) sj[20 + K * j + i] *= si[i];
+                    for (int d = 0; d < 6; ++d) {
+                        wv[d] = rec[2 + u] * rec[8 + d] + rec[5 + u] * rec[14 + d];
+                        if (jscale) wv[d] = wv[d] * (sp[u] * sc[d]);
                     }
-                }
-                double2* dst = reinterpret_cast<double2*>(J + (size_t)o * JS);
 #pragma unroll
-                for (int i = 0; i < JS / 2; ++i) dst[i] = make_double2(sj[2 * i], sj[2 * i + 1]);
+                    for (int i = 0; i < 3; ++i) dst[3 * u + i] = make_double2(wv[2 * i], wv[2 * i + 1]);
+                }
             }
 #pragma unroll
             for (int i = 0; i < 6; ++i) jer[a * 8 + i] = rec[2 + i];
@@ -900,33 +1033,18 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
                 gr[6 + K] = rec[j];
             }
             olc[a] = (short)olcv;
+            orw[a] = (short)row;
             cost += res[0].a * res[0].a + res[1].a * res[1].a;
         }
         BA_STAMP(1);
         __syncthreads();
         BA_STAMP(2);
         const int no = ch.o1 - ch.o0;
-        // per point: column norms and gradient of its 3 columns (whole points in a normal chunk)
+        // per point: E | g | V of its observations (whole points in a normal chunk)
         if (!Gp.big) {
-            if (ptl) {
-                const int p = Gp.p0 + tid;
-                const int a0 = pa0, a1 = pa1;
-                double cs[3] = {0, 0, 0}, gr[3] = {0, 0, 0};
-                for (int b = a0; b < a1; ++b) {
-                    const double* r = jer + b * 8;
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) {
-                        const double j0 = r[i], j1 = r[3 + i];
-                        cs[i] += j0 * j0 + j1 * j1;
-                        gr[i] += j0 * r[6] + j1 * r[7];
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    colsq[3 * (size_t)p + i] = cs[i];
-                    grad[3 * (size_t)p + i] = gr[i];
-                    gmax = fmax(gmax, fabs(gr[i]));
-                }
+            if (pth) {   // wave-uniform halves
+                if (tid < 128) point_eg<K>(jer, pa0, pa1, Gp.p0 + qv, jscale, colsq, grad, PRo, gmax);
+                else point_v<K>(jer, G, orw, pa0, pa1, Gp.p0 + qv, P, C, jscale, PRo);
             }
             // per camera: Gram of its feature rows, accumulated over the group's chunks; the
             // operand reads go out 8 MFMA steps at a time, ahead of their MFMAs
@@ -948,16 +1066,14 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
                 }
             }
         } else {
-            if (tid == 0)
-                for (int b = 0; b < no; ++b) {
-                    const double* r = jer + b * 8;
+            if (tid == 0) {
+                double pr[NPR];
 #pragma unroll
-                    for (int i = 0; i < 3; ++i) {
-                        const double j0 = r[i], j1 = r[3 + i];
-                        pcs[i] += j0 * j0 + j1 * j1;
-                        pgr[i] += j0 * r[6] + j1 * r[7];
-                    }
-                }
+                for (int i = 0; i < NPR; ++i) pr[i] = bpr[i];
+                point_sums<K>(jer, G, orw, 0, no, pr);
+#pragma unroll
+                for (int i = 0; i < NPR; ++i) bpr[i] = pr[i];
+            }
             for (int x = tid; x < npart; x += blockDim.x) {   // per (camera, field), in observation order
                 const int lc = x / NCP, f = x % NCP;
                 int fr = -1, fc = -1;
@@ -992,13 +1108,12 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
         }
     } else if (tid == 0) {
         const int p = Gp.p0;
+        double pr[NPR];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            colsq[3 * (size_t)p + i] = pcs[i];
-            grad[3 * (size_t)p + i] = pgr[i];
-            gmax = fmax(gmax, fabs(pgr[i]));
-            xn += pts[3 * (size_t)p + i] * pts[3 * (size_t)p + i];
-        }
+        for (int i = 0; i < NPR; ++i) pr[i] = bpr[i];
+        point_store<K>(p, P, C, pr, jscale, colsq, grad, PRo, gmax);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xn += pts[3 * (size_t)p + i] * pts[3 * (size_t)p + i];
     }
     const double sc = block_sum(cost, sh);
     const double sx = block_sum(xn, sh);
@@ -1018,6 +1133,7 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
     BA_FLUSH(8);
 }
 
+// ---------------------------------------------------------------------------------------------
 // ba_camred: per camera (one workgroup) the partials of its (group, camera) slots in group
 // order -> camsum[c]; one more workgroup: the intrinsics fields of every slot, in slot order.
 template <int K>
@@ -1070,7 +1186,8 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
                  int* __restrict__ fail, double* __restrict__ colsq, double* __restrict__ grad,
                  double* __restrict__ scal, double* __restrict__ camsum_out, int ncs,
                  const double* __restrict__ pre, double* __restrict__ pub_dst, unsigned* __restrict__ pub_seq,
-                 unsigned pub_v) {
+                 unsigned pub_v, const double* __restrict__ camsum_cur, const double* __restrict__ sol_f,
+                 const double* __restrict__ scale_f) {
     if (step_gated(fail + 1)) return;
     constexpr int NCP = ncp(K);
     __shared__ double sh[8];
@@ -1122,6 +1239,54 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
         s2 = block_sum(g[2], sh);
         s3 = block_sum(g[3], sh);
     }
+    // candidate mode: the camera rows' part of the model cost change, d.g_f + d^T C d / 2 with the
+    // step d = -sol_f * scale_f and C, g_f the current linearization's (all-reduced, unscaled) camera
+    // sums: per camera its 6 x 6 block, its coupling to the intrinsics and its gradient, then the
+    // intrinsics block (one more slot); fixed order (thread stride, then the block sum)
+    double mf = 0.0;
+    if (cand_mode) {
+        const double* sif = scale_f + 6 * (size_t)C;
+        double di[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) di[i] = -sol_f[6 * (size_t)C + i] * sif[i];
+        for (int c = t; c <= C; c += blockDim.x) {
+            double q = 0.0;
+            if (c < C) {
+                const double* cs = camsum_cur + (size_t)c * NCP;
+                double dc[6];
+#pragma unroll
+                for (int u = 0; u < 6; ++u) dc[u] = -sol_f[6 * (size_t)c + u] * scale_f[6 * (size_t)c + u];
+                int e = 0;
+#pragma unroll
+                for (int u = 0; u < 6; ++u)
+#pragma unroll
+                    for (int v = u; v < 6; ++v, ++e) {
+                        const double m = dc[u] * cs[e] * dc[v];
+                        q += u == v ? 0.5 * m : m;
+                    }
+#pragma unroll
+                for (int u = 0; u < 6; ++u)
+#pragma unroll
+                    for (int i = 0; i < K; ++i) q += dc[u] * cs[cp_ci(K) + u * K + i] * di[i];
+#pragma unroll
+                for (int u = 0; u < 6; ++u) q += dc[u] * cs[cp_gc(K) + u];
+            } else {
+                const double* ii = camsum_cur + (size_t)C * NCP;
+                int e = 0;
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+#pragma unroll
+                    for (int j = i; j < K; ++j, ++e) {
+                        const double m = di[i] * ii[e] * di[j];
+                        q += i == j ? 0.5 * m : m;
+                    }
+#pragma unroll
+                for (int i = 0; i < K; ++i) q += di[i] * ii[K * (K + 1) / 2 + i];
+            }
+            mf += q;
+        }
+    }
+    const double smf = block_sum(mf, sh);
     const double sxn = block_sum(xn, sh);
     const double ssn = block_sum(sn, sh);
     double gm = fmax(gmax, g[4]);
@@ -1133,7 +1298,7 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
         double m = 0.0;
         for (int i = 0; i < 4; ++i) m = fmax(m, sh[i]);
         scal[SC_COST] = s0;
-        scal[SC_MODEL] = s1;
+        scal[SC_MODEL] = cand_mode ? s1 + smf : s1;
         scal[SC_STEPN] = s2;
         scal[SC_XN] = s3;
         scal[SC_GMAX] = m;
@@ -1176,131 +1341,58 @@ void ba_group_sums(int ngroups, const double* __restrict__ gpl, double* __restri
     }
 }
 
-// ba_gupdate: per group, from sol_f (scaled camera/intrinsics solution) and the stored M, t:
-// sol_e = M^T (t - M y), y = sum_o Je_o^T ([Jc_o | Ji_o] sol_f); step = -sol; candidate points
-// cand = x + step * scale; ||x - cand||^2 and the model cost change sum m (r + m / 2), m = J_s step_s.
-// One thread per observation of a chunk: its J record is loaded straight into registers (13
-// independent 16-B loads, kept across the two barriers of the chunk), so a chunk costs one memory
-// latency, not a staging round trip; LDS holds only the per-observation y terms and point steps.
-
+// ba_gupdate: the LM step's point update (above).  One thread per observation of a chunk (its W_o:
+// 9 independent 16-B loads) and one per point.  (Fusing it into the candidate's ba_glin, per chunk
+// before the linearization, was measured slower: DESIGN.md §5.)
 template <int K>
 __global__ __launch_bounds__(256)
-void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const int* __restrict__ obs_point,
-                const int* __restrict__ obs_cam, const int* __restrict__ pt_start, const double* __restrict__ J,
+void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const int* __restrict__ obs_cam,
+                const int* __restrict__ pt_start, const double* __restrict__ Wr, const double* __restrict__ PRr,
                 const double* __restrict__ scale, const double* __restrict__ plt, const double* __restrict__ sol_f,
                 int P, int C, const double* __restrict__ x, double* __restrict__ cand, double* __restrict__ gpl,
                 const int* __restrict__ gate) {
     if (step_gated(gate)) return;
     __shared__ double yv[GCH * 3];
-    __shared__ double pst[GPTS * 3];
     __shared__ double sh[8];
     const Grp G = grp[blockIdx.x];
     const int tid = threadIdx.x;
-        double soli[K];
+    double soli[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) soli[i] = sol_f[6 * (size_t)C + i];
     double model = 0.0, sn = 0.0;
     double ybig[3] = {0, 0, 0};
     const int nchunks = G.big ? (G.o1 - G.o0 + GCH - 1) / GCH : G.nch;
-    // big groups: pass 0 accumulates y over all chunks, pass 1 evaluates the model terms
-    for (int pass = G.big ? 0 : 1; pass < 2; ++pass) {
-        for (int c = 0; c < nchunks; ++c) {
-            Chunk ch;
-            if (G.big) { ch.o0 = G.o0 + c * GCH; ch.o1 = min(G.o1, ch.o0 + GCH); ch.q0 = 0; ch.q1 = 1; }
-            else ch = chk[G.ch0 + c];
-            const int a = tid, o = ch.o0 + a;
-            const bool ov = o < ch.o1;
-            JRec<K> R;
-            int q = 0, cm = 0;
-            double f[2] = {0, 0};
-            if (ov) {
-                const int p = obs_point[o];
-                cm = obs_cam[o];
-                q = p - G.p0;
-                load_jrec_v<K>(J, o, R);
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-#pragma unroll
-                    for (int d = 0; d < 6; ++d) f[j] += R.jc[j][d] * sol_f[6 * (size_t)cm + d];
-#pragma unroll
-                    for (int i = 0; i < K; ++i) f[j] += R.ji[j][i] * soli[i];
-                }
-#pragma unroll
-                for (int k = 0; k < 3; ++k) yv[a * 3 + k] = R.je[0][k] * f[0] + R.je[1][k] * f[1];
-            }
-            __syncthreads();
-            if (G.big) {
-                if (pass == 0 && tid == 0)
-                    for (int b = 0; b < ch.o1 - ch.o0; ++b)
-#pragma unroll
-                        for (int k = 0; k < 3; ++k) ybig[k] += yv[b * 3 + k];
-            } else if (tid >= ch.q0 && tid < ch.q1) {
-                const int p = G.p0 + tid;
-                const int a0 = pt_start[p] - ch.o0, a1 = pt_start[p + 1] - ch.o0;
-                double y[3] = {0, 0, 0};
-                for (int b = a0; b < a1; ++b)
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) y[k] += yv[b * 3 + k];
-                const double* Mt = plt + 9 * (size_t)p;
-                double v[3];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    double my = 0.0;
-#pragma unroll
-                    for (int j = 0; j <= k; ++j) my += mlo(Mt, k, j) * y[j];
-                    v[k] = Mt[6 + k] - my;
-                }
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    double s = 0.0;
-#pragma unroll
-                    for (int k = j; k < 3; ++k) s += mlo(Mt, k, j) * v[k];
-                    const double st = -s;                       // step_s = -sol
-                    pst[tid * 3 + j] = st;
-                    const double xv = x[3 * (size_t)p + j], cv = xv + st * scale[3 * (size_t)p + j];
-                    cand[3 * (size_t)p + j] = cv;
-                    const double dd = xv - cv;
-                    sn += isfinite(dd) ? dd * dd : INFINITY;
-                }
-            }
-            if (G.big && pass == 1 && c == 0 && tid == 0) {   // the big point's step, once
-                const int p = G.p0;
-                const double* Mt = plt + 9 * (size_t)p;
-                double v[3];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    double my = 0.0;
-#pragma unroll
-                    for (int j = 0; j <= k; ++j) my += mlo(Mt, k, j) * ybig[j];
-                    v[k] = Mt[6 + k] - my;
-                }
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    double s = 0.0;
-#pragma unroll
-                    for (int k = j; k < 3; ++k) s += mlo(Mt, k, j) * v[k];
-                    pst[j] = -s;
-                    const double xv = x[3 * (size_t)p + j], cv = xv - s * scale[3 * (size_t)p + j];
-                    cand[3 * (size_t)p + j] = cv;
-                    const double dd = xv - cv;
-                    sn += isfinite(dd) ? dd * dd : INFINITY;
-                }
-            }
-            __syncthreads();   // yv of the next chunk is written after this chunk's point phase
-            if (pass == 1 && ov) {
-                const double* ps = pst + (G.big ? 0 : q) * 3;
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    double mm = R.je[j][0] * ps[0] + R.je[j][1] * ps[1] + R.je[j][2] * ps[2];
-#pragma unroll
-                    for (int d = 0; d < 6; ++d) mm -= R.jc[j][d] * sol_f[6 * (size_t)cm + d];
-#pragma unroll
-                    for (int i = 0; i < K; ++i) mm -= R.ji[j][i] * soli[i];
-                    model += mm * (R.r[j] + mm / 2.0);
-                }
-            }
-            // no barrier: the next chunk's pst writes come after its first barrier
+    for (int c = 0; c < nchunks; ++c) {
+        Chunk ch;
+        if (G.big) { ch.o0 = G.o0 + c * GCH; ch.o1 = min(G.o1, ch.o0 + GCH); ch.q0 = 0; ch.q1 = 0; }
+        else ch = chk[G.ch0 + c];
+        const int o = ch.o0 + tid;
+        int pa0 = 0, pa1 = 0;
+        const bool ptl = tid >= ch.q0 && tid < ch.q1;
+        if (ptl) {
+            pa0 = pt_start[G.p0 + tid] - ch.o0;
+            pa1 = pt_start[G.p0 + tid + 1] - ch.o0;
         }
+        if (o < ch.o1) obs_y(Wr, o, sol_f + 6 * (size_t)obs_cam[o], yv + tid * 3);
+        __syncthreads();
+        if (G.big) {
+            if (tid == 0)
+                for (int b = 0; b < ch.o1 - ch.o0; ++b)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) ybig[k] += yv[b * 3 + k];
+        } else if (ptl) {
+            double y[3] = {0, 0, 0};
+            for (int b = pa0; b < pa1; ++b)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) y[k] += yv[b * 3 + k];
+            double cv[3];
+            point_step<K>(G.p0 + tid, y, PRr, plt, soli, x, scale, cand, model, sn, cv);
+        }
+        __syncthreads();   // yv is rewritten by the next chunk
+    }
+    if (G.big && tid == 0) {
+        double cv[3];
+        point_step<K>(G.p0, ybig, PRr, plt, soli, x, scale, cand, model, sn, cv);
     }
     const double sm = block_sum(model, sh);
     const double ss = block_sum(sn, sh);

@@ -125,10 +125,12 @@ struct sfmx_ba_ctx {
     int n_nztiles = 0;
     size_t sr_count = 0;         // doubles of SR = S_cc | R | D | r_i
     // state (the *2 buffers hold the candidate's linearization until the step is accepted)
-    Buf x, cand, scale, colsq, colsq2, grad, grad2, J, J2, camsum, camsum2, plt, sg, rg, hbig, gpart, gpl, scal,
-        SR, sol, failf, partA;
+    // Wr / PR: the step kernels' records of a linearization (W_o per observation, E | g | V per
+    // point, ba_group.hpp); J: Jacobian rows, for sfmx_ba_jacobian only (allocated there)
+    Buf x, cand, scale, colsq, colsq2, grad, grad2, Wr, Wr2, PR, PR2, J, camsum, camsum2, plt, sg, rg, hbig, gpart, gpl,
+        scal, SR, sol, failf, partA;
     static constexpr int HS_SLOT = SC_N + LM_N, HS_SEQ = 2 * HS_SLOT, HS_N = HS_SEQ + 3;
-    bool scaled = false, j_scaled = false;   // j_scaled: the records in J are J_s (ba_gschur SCALEJ)
+    bool scaled = false, j_scaled = false;   // j_scaled: the records in Wr / PR are scaled (ba_gschur SCALEJ)
     // locality order: internal point p' is caller point pperm[p']; internal
     // observation o' is caller observation operm[o'] (point-major)
     std::vector<int> pperm, operm;
@@ -157,7 +159,7 @@ struct sfmx_ba_ctx {
         Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
                       &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
-                      &grad2, &J, &J2, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
+                      &grad2, &Wr, &Wr2, &PR, &PR2, &J, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
                       &failf, &partA, &lmst, &camscr, &pim, &pcc, &xyraw, &operm_d};
         int prev = 0;
         (void)hipGetDevice(&prev);
@@ -293,6 +295,7 @@ int wait_slot(sfmx_ba_ctx* c, unsigned q, double* out) {
 // 1/2 sum ||r||^2 at parameters xp with the Jacobian into c->partA-sized J (sfmx_ba_jacobian only).
 int eval_jacobian(sfmx_ba_ctx* c, const double* xp, double* cost_out) {
     const unsigned g = nblk(c->O);
+    RC(c->J.alloc(8 * (size_t)std::max(c->O, 1) * jst(c->K)));
     const double* pts = xp;
     const double* poses = xp + c->ne;
     const double* intr = poses + 6 * (size_t)c->C;
@@ -311,14 +314,14 @@ int eval_jacobian(sfmx_ba_ctx* c, const double* xp, double* cost_out) {
 // Linearization at xp (x or the candidate) into (Jo, colsq_o, grad_o, camsum_o) and the LM scalars
 // into scal (cand_mode: the step's model / step-norm partials are already in gpl): -> out[SC_N].
 template <int K>
-int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double* grad_o, double* camsum_o,
-           bool cand_mode, double* out) {
+int lin_at(sfmx_ba_ctx* c, const double* xp, double* Wo, double* PRo, double* colsq_o, double* grad_o,
+           double* camsum_o, bool cand_mode, double* out) {
     if (c->ngroups > 0) {
 #define GLIN(MULTI) hipLaunchKernelGGL((ba_glin<K, MULTI>), dim3(c->ngroups), dim3(256), c->lds_lin, c->st, c->grp.as<Grp>(), \
                            c->chk.as<Chunk>(), c->lcrow.as<int>(), c->obs_lc.as<short>(), c->obs_row.as<short>(),         \
                            c->obs_point.as<int>(), c->obs_cam.as<int>(),                                                   \
                            c->obs_xy.as<double>(), c->pt_start.as<int>(), c->cx, c->cy, c->P, c->C, xp,                    \
-                           c->scaled ? c->scale.as<double>() : nullptr, Jo, colsq_o, grad_o, c->gpart.as<double>(),        \
+                           c->scaled ? c->scale.as<double>() : nullptr, Wo, PRo, colsq_o, grad_o, c->gpart.as<double>(),   \
                            c->gpl.as<double>(), gate(c), c->pim.as<int>(), c->pcc.as<double2>())
         if (c->multi) GLIN(true); else GLIN(false);
 #undef GLIN
@@ -342,7 +345,8 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Jo, double* colsq_o, double
     hipLaunchKernelGGL(ba_finalize<K>, dim3(1), dim3(256), 0, c->st, c->ngroups, c->P, c->C, cs_red,
                        c->gpl.as<double>(), xp + c->ne, c->x.as<double>() + c->ne, cand_mode ? 1 : 0, c->failf.as<int>(),
                        colsq_o, grad_o, scal(c, 0), camsum_o, cs_red == camsum_o ? 0 : ncs, pre,
-                       fold ? c->hs : nullptr, reinterpret_cast<unsigned*>(c->hs + sfmx_ba_ctx::HS_SEQ + 2), fold_seq);
+                       fold ? c->hs : nullptr, reinterpret_cast<unsigned*>(c->hs + sfmx_ba_ctx::HS_SEQ + 2), fold_seq,
+                       c->camsum.as<double>(), c->sol.as<double>() + c->ne, c->scale.as<double>() + c->ne);
     HIPCHK(hipGetLastError());
     RC(allreduce(c, scal(c, SC_GMAX), 2, SFMX_REDUCE_MAX));
     if (!out) return SFMX_OK;   // speculative step: ba_decide judges and publishes
@@ -421,8 +425,9 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
 #define GSCHUR(NTV) if (sj) GSCHUR2(NTV, true); else GSCHUR2(NTV, false)
 #define GSCHUR2(NTV, SJ) hipLaunchKernelGGL((ba_gschur<K, NTV, SJ>), dim3(c->ngroups), dim3(256), c->lds_schur, c->st,     \
                            c->grp.as<Grp>(), c->bat.as<Batch>(), c->gcam.as<int>(), c->obs_lc.as<short>(),             \
-                           c->obs_point.as<int>(), c->obs_cam.as<int>(), c->pt_start.as<int>(), c->J.as<double>(),      \
-                           c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, \
+                           c->obs_point.as<int>(), c->obs_cam.as<int>(), c->pt_start.as<int>(), c->Wr.as<double>(),     \
+                           c->PR.as<double>(), c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal,         \
+                           o.max_lm_diagonal, radius,                                                                   \
                            c->P, C, c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl, lmr)
         const bool sj = !c->j_scaled;   // the first step of a solve scales J in place
         switch (c->gs_nt) { case 1: GSCHUR(1); break; case 2: GSCHUR(2); break; case 3: GSCHUR(3); break; default: GSCHUR(4); }
@@ -455,14 +460,14 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     if (c->phases) HIPCHK(hipEventRecord(c->ev[2], c->st));
     if (c->ngroups > 0)
         hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups), dim3(256), 0, c->st, c->grp.as<Grp>(),
-                           c->chk.as<Chunk>(), c->obs_point.as<int>(), c->obs_cam.as<int>(), c->pt_start.as<int>(),
-                           c->J.as<double>(), c->scale.as<double>(), c->plt.as<double>(), sol + c->ne, c->P, C,
+                           c->chk.as<Chunk>(), c->obs_cam.as<int>(), c->pt_start.as<int>(), c->Wr.as<double>(),
+                           c->PR.as<double>(), c->scale.as<double>(), c->plt.as<double>(), sol + c->ne, c->P, C,
                            c->x.as<double>(), c->cand.as<double>(), c->gpl.as<double>(), gate(c));
     hipLaunchKernelGGL(ba_fstep, dim3(nblk(c->nf)), dim3(256), 0, c->st, c->nf, sol + c->ne, c->scale.as<double>() + c->ne,
                        c->x.as<double>() + c->ne, c->cand.as<double>() + c->ne, gate(c));
     HIPCHK(hipGetLastError());
     double v[SC_N];
-    RC(lin_at<K>(c, c->cand.as<double>(), c->J2.as<double>(), c->colsq2.as<double>(), c->grad2.as<double>(),
+    RC(lin_at<K>(c, c->cand.as<double>(), c->Wr2.as<double>(), c->PR2.as<double>(), c->colsq2.as<double>(), c->grad2.as<double>(),
                  c->camsum2.as<double>(), true, spec ? nullptr : v));
     if (spec) {
         const sfmx_ba_options& op = c->opt;
@@ -681,7 +686,7 @@ int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace,
     HIPCHK(hipMemsetAsync(c->failf.p, 0, sizeof(int), c->st));
     hipLaunchKernelGGL(ba_open_gate, dim3(1), dim3(64), 0, c->st, c->failf.as<int>());
     double v[SC_N];
-    RC(lin_at<K>(c, c->x.as<double>(), c->J.as<double>(), c->colsq.as<double>(), c->grad.as<double>(),
+    RC(lin_at<K>(c, c->x.as<double>(), c->Wr.as<double>(), c->PR.as<double>(), c->colsq.as<double>(), c->grad.as<double>(),
                  c->camsum.as<double>(), false, v));
     if (o.jacobi_scaling) {
         hipLaunchKernelGGL(ba_scale, dim3(nblk(c->n)), dim3(256), 0, c->st, (int)c->n, c->colsq.as<double>(),
@@ -723,7 +728,8 @@ int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace,
             HIPCHK(hipMemcpyAsync(c->lmst.p, li, sizeof(double) * LM_N, hipMemcpyHostToDevice, c->st));
             auto swap_state = [c]() {
                 std::swap(c->x, c->cand);
-                std::swap(c->J, c->J2);
+                std::swap(c->Wr, c->Wr2);
+                std::swap(c->PR, c->PR2);
                 std::swap(c->colsq, c->colsq2);
                 std::swap(c->grad, c->grad2);
                 std::swap(c->camsum, c->camsum2);
@@ -792,7 +798,8 @@ int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace,
         const double rel = (cost - ccost) / mcc;
         if (rel > o.min_relative_decrease) {   // HandleSuccessfulStep: the candidate's linearization is current
             std::swap(c->x, c->cand);
-            std::swap(c->J, c->J2);
+            std::swap(c->Wr, c->Wr2);
+            std::swap(c->PR, c->PR2);
             std::swap(c->colsq, c->colsq2);
             std::swap(c->grad, c->grad2);
             std::swap(c->camsum, c->camsum2);
@@ -1304,7 +1311,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
                        std::max<size_t>({4 * wreg + 2 * nb_max, (size_t)tp.dp_max * (tp.dp_max + 1) + tp.dp_max, 16});
         c->gs_nt = std::min(4, std::max(1, tp.dp_max / 16));
     }
-    c->lds_lin = sizeof(double) * ((size_t)GROWS * nfeat(K) + GCH * 8) + sizeof(short) * GCH;
+    c->lds_lin = sizeof(double) * ((size_t)GROWS * nfeat(K) + GCH * 8) + sizeof(short) * 2 * GCH;
     {
         hipError_t e = hipSuccess;
 #define LDSATTR(KK)                                                                                                  \
@@ -1313,8 +1320,8 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
                               (const void*)ba_gschur<KK, 1, true>, (const void*)ba_gschur<KK, 2, true>,               \
                               (const void*)ba_gschur<KK, 3, true>, (const void*)ba_gschur<KK, 4, true>})              \
             if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_schur); \
-        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_glin<KK, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_lin); \
-        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)ba_glin<KK, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_lin);
+        for (const void* f : {(const void*)ba_glin<KK, false>, (const void*)ba_glin<KK, true>})                    \
+            if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds_lin);
         if (K == 1) { LDSATTR(1); } else if (K == 3) { LDSATTR(3); } else { LDSATTR(7); }
 #undef LDSATTR
         if (e != hipSuccess) return bail(fail(SFMX_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(e)));
@@ -1346,7 +1353,8 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     struct { Buf* b; size_t bytes; } allocs[] = {
         {&c->x, 8 * n}, {&c->cand, 8 * n}, {&c->scale, 8 * n}, {&c->colsq, 8 * n}, {&c->colsq2, 8 * n},
         {&c->grad, 8 * n}, {&c->grad2, 8 * n}, {&c->sol, 8 * n},
-        {&c->J, 8 * so * jst(K)}, {&c->J2, 8 * so * jst(K)}, {&c->camsum, 8 * (ncams + 5)}, {&c->camsum2, 8 * (ncams + 5)},
+        {&c->Wr, 8 * so * WST}, {&c->Wr2, 8 * so * WST}, {&c->PR, 8 * (size_t)std::max(P, 1) * npr(K)},
+        {&c->PR2, 8 * (size_t)std::max(P, 1) * npr(K)}, {&c->camsum, 8 * (ncams + 5)}, {&c->camsum2, 8 * (ncams + 5)},
         {&c->plt, 72 * (size_t)std::max(P, 1)}, {&c->sg, 8 * (size_t)std::max<long long>(tp.sg_total, 1)},
         {&c->rg, 8 * (size_t)std::max(tp.rg_total, 1)}, {&c->hbig, 8 * (size_t)std::max<long long>(tp.h_total, 1)},
         {&c->gpart, 8 * (size_t)std::max(c->nslots, 1) * ncp(K)}, {&c->gpl, 8 * (size_t)std::max(c->ngroups, 1) * GP_N},
