@@ -53,6 +53,7 @@ FP64_PEAK_TFLOPS = 256 * 128 * 2.4e9 / 1e12
 # BA algorithmic work per LM iteration at C5: S assembly ~2-2.5 + J ~0.4 +
 # Cholesky ~0.58 GFLOP; bytes: obs read twice, points, S written and read
 BA_FLOP_PER_ITER_C5, BA_BYTES_PER_ITER_C5 = 3.0e9, 0.1e9
+FEAT_PMC_FILE = "r03_pmc_features.json"   # tools/pmc_feat.sh -> tools/pmc_feat_json.py
 BA_PMC_FILE = "r03h_pmc_ba.json"   # tools/pmc_ba.sh on the current kernels (W_o / point records)
 
 
@@ -73,6 +74,7 @@ def parse():
     ap.add_argument("--no-features", action="store_true", help="skip the SIFT extraction leg (SURVEY §8 f3)")
     ap.add_argument("--no-orb-features", action="store_true", help="skip the ORB extraction leg (SURVEY §8 f3)")
     ap.add_argument("--only-orb-features", action="store_true", help="run only the ORB extraction leg (tuning)")
+    ap.add_argument("--only-features", action="store_true", help="run only the SIFT extraction leg (PMC passes)")
     ap.add_argument("--only-ba", action="store_true", help="run only the bundle-adjustment leg (tuning)")
     ap.add_argument("--only-c3", action="store_true", help="run only the 200-image SIFT (config 3) leg (profiling)")
     ap.add_argument("--no-ba-calls", action="store_true", help="skip the BA call-pattern replay (SfM.cpp:235/371)")
@@ -128,8 +130,8 @@ def main():
             dist.destroy_process_group()
         return
 
-    if args.only_orb_features:
-        res = bench_features_orb(args, rank, world, local)
+    if args.only_orb_features or args.only_features:
+        res = (bench_features_orb if args.only_orb_features else bench_features)(args, rank, world, local)
         if rank == 0:
             print(json.dumps(res), flush=True)
         if world > 1:
@@ -752,6 +754,15 @@ FEAT_SHOTS, FEAT_H, FEAT_W, FEAT_LIMIT = 50, 1080, 1920, 8192
 FEAT_STREAMS = int(os.environ.get("SFMX_FEAT_STREAMS", "8"))   # extraction workers, one HIP stream each (r01f sweep: 2/4/6/8 -> 1197/1500/1534/1554 images/s)
 
 
+def feat_traffic(leg):
+    """HBM bytes per image of an extraction leg from its committed PMC passes, or None."""
+    path = os.path.join(REPO, "profiles", FEAT_PMC_FILE)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)[leg]["bytes_per_image"]
+
+
 def _sift_pyramid_bytes(h, w, layers=3):
     """Algorithmic HBM bytes of one image's scale space (the dominant traffic):
     u8 -> float 2x (4 B/px written), base blur (8 B/px), per octave `layers + 2`
@@ -824,7 +835,8 @@ def bench_features(args, rank, world, local):
                       "parallelism": f"shot-sharded x{world}"},
            "data": "synthetic photos (sfmx.synth.gray_photo: shaded background + Gaussian blobs + noise)",
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": feat_traffic("sift"),
+                        "traffic_unit": f"HBM bytes per image (2 x FETCH_SIZE + WRITE_SIZE, profiles/{FEAT_PMC_FILE})",
                         "kernel": "SIFT pipeline (blur_tile_n_kernel dominant), wall time of the batch",
                         "algorithmic": f"{pyr / 1e6:.0f} MB scale-space traffic per image (bench._sift_pyramid_bytes)"}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -904,7 +916,8 @@ def bench_features_orb(args, rank, world, local):
                       "parallelism": f"shot-sharded x{world}"},
            "data": "synthetic photos (sfmx.synth.gray_photo), two distinct photos, shifted copies",
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": feat_traffic("orb"),
+                        "traffic_unit": f"HBM bytes per image (2 x FETCH_SIZE + WRITE_SIZE, profiles/{FEAT_PMC_FILE})",
                         "kernel": "ORB pipeline, wall time of the batch (host retainBest steps included)",
                         "algorithmic": f"{pyr / 1e6:.1f} MB pyramid / FAST / NMS / blur traffic per image "
                                        f"(bench._orb_pyramid_bytes)"}}

@@ -139,7 +139,8 @@ int sfmx_ba_run(sfmx_ba_ctx* ctx, int32_t max_iterations, sfmx_ba_summary* summa
 int sfmx_ba_update(sfmx_ba_ctx* ctx, const sfmx_ba_problem* problem);
 /* Host-side setup time of the last create / update (ms): [0] point ordering + groups,
  * [1] device allocation, [2] uploads (pinned staging, incl. the parameters), [3] the
- * factorization plan (built at the next run; 0 when reused), [4] total.  n = entries. */
+ * factorization plan (built at the next run; 0 when reused), [4] total, [5] / [6] the ordering
+ * and the point groups (the two parts of [0]).  n = entries (up to 7). */
 int sfmx_ba_setup_ms(sfmx_ba_ctx* ctx, double* ms, int32_t n);
 /* Copy the current parameters back into problem->points/poses/intr. */
 int sfmx_ba_get(sfmx_ba_ctx* ctx, sfmx_ba_problem* problem);

@@ -30,7 +30,7 @@
 //   ba_add_cam   + scaled C, D_f^2 and g_f (after any cross-rank all-reduce of S)
 //   (the solve of S itself: ba_chol.hpp, planned by ba_plan.hpp)
 //   ba_gupdate   back substitution, step, candidate points, model cost change, step norm
-//   ba_fstep     candidate cameras / intrinsics
+//                (its trailing workgroups: the candidate cameras / intrinsics)
 //   ba_finalize  the LM scalars of one step (one workgroup)
 #pragma once
 #include <hip/hip_runtime.h>
@@ -197,13 +197,16 @@ __device__ __forceinline__ void stage_copy(double2* __restrict__ dst, const doub
 // (into rg); per point M_p and t_p (plt, 9 doubles) for the back substitution.
 // Normal groups: no workgroup barrier until the end.  Each wave takes every 4th batch of the
 // group (<= 64 observations, <= 16 whole points, host-built) and keeps its own accumulators:
-//   lane = observation: its W_o = Je_s^T Jc_s straight into registers (9 x 16-B loads);
+//   lane = observation: its W_o = Je_s^T Jc_s (9 x 16-B loads, prefetched a batch ahead) -> its
+//     row of the wave's LDS W table, its lane -> the (point, local camera) map;
 //   4 lanes = point: its record (E, g, V; a quarter each) -> the point's wave LDS slot; lane 0 of
 //     the 4: + D_p^2, M = chol(E)^-1, t = M g, Hi = M V -> wave LDS + plt;
-//   rounds of 4 points: H_p columns (camera rows Z_o = (M W_o)^T, intrinsics rows Hi) -> a zeroed
-//     4 x dp x 3 wave buffer; the SYRK on v_mfma_f64_16x16x4f64 takes the 4 points as its k
-//     slots: lane m + 16kk holds H_{p_kk}[16I + m][c], so tile (I, J) += 3 MFMAs (c = 0..2), the
-//     same register both as the A operand (H[16I + m][kk]) and, for tile row J, the B operand;
+//   rounds of 4 points: the SYRK on v_mfma_f64_16x16x4f64 takes the 4 points as its k slots:
+//     lane m + 16kk forms H_{p_kk}[16I + m][c] itself from LDS (a camera row (lc, d): Z_o[d][c] =
+//     (M W_o)[c][d] of the point's observation o in camera lc, zero without one; an intrinsics
+//     row: Hi), so tile (I, J) += 3 MFMAs (c = 0..2), the same register both as the A operand
+//     (H[16I + m][kk]) and, for tile row J, the B operand; no LDS round trip of H, no barrier
+//     inside a round;
 //   rhs: lane rows 16I + m accumulate H t of its point.
 // Then the 4 waves' tiles and rhs are summed in wave order (fixed, deterministic) through LDS.
 // Groups are cut on the host so that dp = round16(6u + K) <= GDPMAX; the launch is specialised on
@@ -212,11 +215,12 @@ __device__ __forceinline__ void stage_copy(double2* __restrict__ dst, const doub
 // camera): the serial path, one thread per point / camera.
 // SCALEJ (the first step of a solve, the records still unscaled from iteration 0): every W_o and
 // point record is scaled by the solve's Jacobi scale as it is read, and written back scaled.
-// Dynamic LDS: per wave 4 x HS H columns + WB_PTS x PD point data; the final combine reuses it
-// as [dp][dp + 1] + rhs.
+// Dynamic LDS: per wave the W table, WB_PTS x PD point data and the lane map; the final combine
+// reuses it as [dp][dp + 1] + rhs.
 __host__ __device__ constexpr int gs_pd(int K) { return 9 + 3 * K; }                  // E | g | V, then M 6 | t 3 | Hi 3K
-__host__ __device__ constexpr int gs_hs(int dp) { return 3 * dp + 2; }                // per-point H column block
-__host__ __device__ constexpr int gs_wreg(int K, int dp) { return 4 * gs_hs(dp) + WB_PTS * gs_pd(K); }   // doubles per wave
+__host__ __device__ constexpr int gs_wreg(int K, int) {                               // doubles per wave
+    return WB_OBS * WST + WB_PTS * gs_pd(K) + WB_PTS * UMAX / 8;                      // W rows | point data | lane map
+}
 #ifndef GSCHUR_WAVES
 #define GSCHUR_WAVES 2   // waves per SIMD the register budget targets (A/B: -DGSCHUR_WAVES=3)
 #endif
@@ -327,10 +331,11 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
     }
 
     BA_T0();
-    const int dp = (dim + 15) & ~15, nt = dp >> 4, HS = gs_hs(dp);
+    const int dp = (dim + 15) & ~15, nt = dp >> 4;
     const int wreg = gs_wreg(K, dp);
-    double* Hb = gl + (size_t)w * wreg;               // [4][HS] the H columns of a round
-    double* pw = Hb + 4 * HS;                         // [WB_PTS][PD] point data
+    double* Wl = gl + (size_t)w * wreg;               // [WB_OBS][WST] the batch's W_o, one row per lane
+    double* pw = Wl + WB_OBS * WST;                   // [WB_PTS][PD] point data
+    signed char* omap = reinterpret_cast<signed char*>(pw + WB_PTS * PD);   // [WB_PTS][UMAX] lane of (point, camera)
     constexpr int NTT = NT * (NT + 1) / 2;            // upper tiles (NT = dp_max / 16 of the launch)
     f64x4 acc[NTT];
 #pragma unroll
@@ -381,10 +386,13 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
     for (int bi = w; bi < G.nb; bi += 4) {
         const Batch B = bl[bi];
         const int o = B.o0 + l, np = B.p1 - B.p0;
-        const bool ov = o < B.o1;
-        double W[3][6];
-        const int lc = pre_lc, q = pre_q;
-        if (ov) {
+        // (point, local camera) -> lane map of this batch; cleared first (the wave's LDS operations
+        // run in order, the fences keep the compiler's order)
+        reinterpret_cast<int*>(omap)[l] = -1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (o < B.o1) {   // lane = observation: W_o -> its LDS row, its lane into the map
             double v[WST];
 #pragma unroll
             for (int i = 0; i < WST / 2; ++i) { v[2 * i] = pre[i].x; v[2 * i + 1] = pre[i].y; }
@@ -394,10 +402,10 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
 #pragma unroll
                 for (int i = 0; i < WST / 2; ++i) d2[i] = make_double2(v[2 * i], v[2 * i + 1]);
             }
+            double2* wl = reinterpret_cast<double2*>(Wl + l * WST);
 #pragma unroll
-            for (int a = 0; a < 3; ++a)
-#pragma unroll
-                for (int d = 0; d < 6; ++d) W[a][d] = v[6 * a + d];
+            for (int i = 0; i < WST / 2; ++i) wl[i] = make_double2(v[2 * i], v[2 * i + 1]);
+            omap[pre_q * UMAX + pre_lc] = (signed char)l;
         }
         // point phase: the 4 lanes of a point put its record into the point's pw slot; after a wave
         // barrier lane k = 0 reads it back and does the rest
@@ -468,46 +476,42 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         BA_STAMP(4);
+        // rounds of 4 points: lane (m16, kk) forms its own SYRK operands straight from LDS, rows
+        // 16I + m16 of H of the round's point kk: a camera row (lc, d) is Z_o[d] = (M W_o[:, d])
+        // of the point's observation o in camera lc (zero without one), an intrinsics row Hi
         for (int r0 = 0; r0 < np; r0 += 4) {
-            for (int e = l; e < 4 * HS; e += 64) Hb[e] = 0.0;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (ov && q >= r0 && q < r0 + 4) {   // Z_o = (M_q W_o)^T: the observation's 6 camera rows of H_q
-                const double* pq = pw + q * PD;
-                double Mr[6];   // in registers: the h stores below may alias pw for the compiler
-#pragma unroll
-                for (int i = 0; i < 6; ++i) Mr[i] = pq[i];
-                double* h = Hb + (q - r0) * HS + 3 * (6 * lc);
-#pragma unroll
-                for (int d = 0; d < 6; ++d)
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        double z = 0.0;
-#pragma unroll
-                        for (int j = 0; j <= k; ++j) z += mlo(Mr, k, j) * W[j][d];
-                        h[3 * d + k] = z;
-                    }
-            }
-            if (m16 < K && r0 + kk < np) {   // intrinsics rows of the round's points
-                const double* pq = pw + (r0 + kk) * PD;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) Hb[kk * HS + 3 * (6 * G.u + m16) + k] = pq[9 + 3 * m16 + k];
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            BA_STAMP(5);
             double hv[NT][3];
             double tk[3] = {0, 0, 0};
-            if (r0 + kk < np) {
-                const double* pq = pw + (r0 + kk) * PD;
+            const int q = r0 + kk;
+            if (q < np) {
+                const double* pq = pw + q * PD;
+                double Mr[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) Mr[i] = pq[i];
                 tk[0] = pq[6]; tk[1] = pq[7]; tk[2] = pq[8];
+#pragma unroll
+                for (int I = 0; I < NT; ++I) {
+                    const int r = 16 * I + m16;
+                    hv[I][0] = hv[I][1] = hv[I][2] = 0.0;
+                    if (r < 6 * G.u) {
+                        const int lc = r / 6, d = r - 6 * lc, lo = omap[q * UMAX + lc];
+                        if (lo >= 0) {
+                            const double* wo = Wl + lo * WST + d;
+                            const double w0 = wo[0], w1 = wo[6], w2 = wo[12];
+                            hv[I][0] = Mr[0] * w0;
+                            hv[I][1] = Mr[1] * w0 + Mr[2] * w1;
+                            hv[I][2] = Mr[3] * w0 + Mr[4] * w1 + Mr[5] * w2;
+                        }
+                    } else if (r < dim) {
+                        const double* hi = pq + 9 + 3 * (r - 6 * G.u);
+                        hv[I][0] = hi[0]; hv[I][1] = hi[1]; hv[I][2] = hi[2];
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int I = 0; I < NT; ++I) hv[I][0] = hv[I][1] = hv[I][2] = 0.0;
             }
-#pragma unroll
-            for (int I = 0; I < NT; ++I)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) hv[I][c] = I < nt ? Hb[kk * HS + 3 * (16 * I + m16) + c] : 0.0;
+            BA_STAMP(5);
 #pragma unroll
             for (int I = 0, t = 0; I < NT; ++I)
 #pragma unroll
@@ -518,10 +522,11 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
                 }
 #pragma unroll
             for (int I = 0; I < NT; ++I) racc[I] += hv[I][0] * tk[0] + hv[I][1] * tk[1] + hv[I][2] * tk[2];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
+        // the next batch rewrites Wl / pw / omap only after every lane's reads of this one
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         BA_STAMP(0);
     }
     // rhs: the 4 points of a round sit in the 4 lane groups: sum them (fixed order)
@@ -727,6 +732,10 @@ __device__ __forceinline__ void point_eg(const double* __restrict__ jer, int a0,
                                          const double* __restrict__ jscale, double* __restrict__ colsq,
                                          double* __restrict__ grad, double* __restrict__ PRo, double& gmax) {
     constexpr int NPR = npr(K);
+    double sv[3] = {1.0, 1.0, 1.0};   // loaded before any store of this thread (vmcnt order)
+    if (jscale)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) sv[i] = jscale[3 * (size_t)p + i];
     double pr[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) pr[i] = 0.0;
@@ -747,12 +756,9 @@ __device__ __forceinline__ void point_eg(const double* __restrict__ jer, int a0,
         grad[3 * (size_t)p + i] = pr[6 + i];
         gmax = fmax(gmax, fabs(pr[6 + i]));
     }
-    if (jscale) {
-        const double* sp = jscale + 3 * (size_t)p;
-        const double sv[3] = {sp[0], sp[1], sp[2]};
+    if (jscale)
 #pragma unroll
         for (int e = 0; e < 9; ++e) pr[e] = pr[e] * pr_scale<K>(e, sv, sv);
-    }
 #pragma unroll
     for (int e = 0; e < 9; ++e) PRo[(size_t)p * NPR + e] = pr[e];
 }
@@ -761,6 +767,16 @@ __device__ __forceinline__ void point_v(const double* __restrict__ jer, const do
                                         const short* __restrict__ orw, int a0, int a1, int p, int P, int C,
                                         const double* __restrict__ jscale, double* __restrict__ PRo) {
     constexpr int NPR = npr(K), NF = nfeat(K);
+    double sv[3] = {1.0, 1.0, 1.0}, sk[K];   // loaded before any store of this thread (vmcnt order)
+#pragma unroll
+    for (int i = 0; i < K; ++i) sk[i] = 1.0;
+    if (jscale) {
+        const double* si = jscale + 3 * (size_t)P + 6 * (size_t)C;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) sv[i] = jscale[3 * (size_t)p + i];
+#pragma unroll
+        for (int i = 0; i < K; ++i) sk[i] = si[i];
+    }
     double v[3 * K];
 #pragma unroll
     for (int i = 0; i < 3 * K; ++i) v[i] = 0.0;
@@ -772,16 +788,9 @@ __device__ __forceinline__ void point_v(const double* __restrict__ jer, const do
 #pragma unroll
             for (int i = 0; i < K; ++i) v[u * K + i] += r[u] * g0[6 + i] + r[3 + u] * g0[NF + 6 + i];
     }
-    if (jscale) {
-        const double* sp = jscale + 3 * (size_t)p;
-        const double* si = jscale + 3 * (size_t)P + 6 * (size_t)C;
-        const double sv[3] = {sp[0], sp[1], sp[2]};
-        double sk[K];
-#pragma unroll
-        for (int i = 0; i < K; ++i) sk[i] = si[i];
+    if (jscale)
 #pragma unroll
         for (int e = 0; e < 3 * K; ++e) v[e] = v[e] * pr_scale<K>(9 + e, sv, sk);
-    }
 #pragma unroll
     for (int e = 0; e < 3 * K; ++e) PRo[(size_t)p * NPR + 9 + e] = v[e];
 }
@@ -1001,22 +1010,16 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
 #pragma unroll
                 for (int i = 0; i < K; ++i) rec[20 + K * j + i] = res[j].v[9 + i];
             }
-            {   // W_o = Je^T Jc (unscaled products, then the scale: the same values ba_gschur<SCALEJ>
-                // makes), one row of 6 at a time straight to its stores
-                double2* dst = reinterpret_cast<double2*>(Wo + (size_t)o * WST);
+            // the scales go out before any store (a load issued after a store waits for it: vmcnt
+            // counts both, in order); the LDS stores below cover their latency
+            double sv[9];
+            if (jscale) {
                 const double* sp = jscale + 3 * (size_t)p;
                 const double* sc = jscale + 3 * (size_t)P + 6 * (size_t)cm;
 #pragma unroll
-                for (int u = 0; u < 3; ++u) {
-                    double wv[6];
+                for (int i = 0; i < 3; ++i) sv[i] = sp[i];
 #pragma unroll
-                    for (int d = 0; d < 6; ++d) {
-                        wv[d] = rec[2 + u] * rec[8 + d] + rec[5 + u] * rec[14 + d];
-                        if (jscale) wv[d] = wv[d] * (sp[u] * sc[d]);
-                    }
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) dst[3 * u + i] = make_double2(wv[2 * i], wv[2 * i + 1]);
-                }
+                for (int i = 0; i < 6; ++i) sv[3 + i] = sc[i];
             }
 #pragma unroll
             for (int i = 0; i < 6; ++i) jer[a * 8 + i] = rec[2 + i];
@@ -1035,6 +1038,19 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
             olc[a] = (short)olcv;
             orw[a] = (short)row;
             cost += res[0].a * res[0].a + res[1].a * res[1].a;
+            {   // W_o = Je^T Jc (unscaled products, then the scale: the same values ba_gschur<SCALEJ> makes)
+                double wv[WST];
+#pragma unroll
+                for (int u = 0; u < 3; ++u)
+#pragma unroll
+                    for (int d = 0; d < 6; ++d) {
+                        wv[6 * u + d] = rec[2 + u] * rec[8 + d] + rec[5 + u] * rec[14 + d];
+                        if (jscale) wv[6 * u + d] = wv[6 * u + d] * (sv[u] * sv[3 + d]);
+                    }
+                double2* dst = reinterpret_cast<double2*>(Wo + (size_t)o * WST);
+#pragma unroll
+                for (int i = 0; i < WST / 2; ++i) dst[i] = make_double2(wv[2 * i], wv[2 * i + 1]);
+            }
         }
         BA_STAMP(1);
         __syncthreads();
@@ -1176,11 +1192,41 @@ void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int*
     }
 }
 
-// ba_finalize (one workgroup of 256): camera column norms / gradient from camsum, and the LM
+// NS sums and one maximum over a workgroup of up to 1024 threads in one pass: every value reduced
+// within its wave (xor shuffles), then thread 0 adds the waves in wave order (the order of
+// block_sum, value by value).  sh: 16 (NS + 1) doubles.  Results valid in thread 0.
+template <int NS>
+__device__ __forceinline__ void block_reduce(double (&v)[NS], double& mx, double* sh) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+        for (int o = 32; o > 0; o >>= 1) v[i] += __shfl_xor(v[i], o);
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) sh[wid * (NS + 1) + i] = v[i];
+        sh[wid * (NS + 1) + NS] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            double t = 0.0;
+            for (int w = 0; w < nw; ++w) t += sh[w * (NS + 1) + i];
+            v[i] = t;
+        }
+        double m = 0.0;
+        for (int w = 0; w < nw; ++w) m = fmax(m, sh[w * (NS + 1) + NS]);
+        mx = m;
+    }
+}
+
+// ba_finalize (one workgroup of 1024): camera column norms / gradient from camsum, and the LM
 // scalars: sums over the groups' partials (fixed order), max |grad|, the camera part of the
 // step and parameter norms (candidate mode: cand vs x).
 template <int K>
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(1024)
 void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, const double* __restrict__ gpl,
                  const double* __restrict__ xf_new, const double* __restrict__ xf_old, int cand_mode,
                  int* __restrict__ fail, double* __restrict__ colsq, double* __restrict__ grad,
@@ -1190,7 +1236,7 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
                  const double* __restrict__ scale_f) {
     if (step_gated(fail + 1)) return;
     constexpr int NCP = ncp(K);
-    __shared__ double sh[8];
+    __shared__ double sh[16 * 8];
     const int t = threadIdx.x;
     // the camera sums were all-reduced in a scratch buffer (a skipped speculative step reduces only
     // scratch): the linearization's own copy is written here, behind the gate
@@ -1224,21 +1270,12 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
         }
     }
     double g[5] = {0, 0, 0, 0, 0};
-    double s0, s1, s2, s3;
-    if (pre) {   // the group sums came through the camera-sum all-reduce (ba_group_sums), g[4] local
-        s0 = pre[0]; s1 = pre[1]; s2 = pre[2]; s3 = pre[3];
-        g[4] = pre[4];
-    } else {
+    if (!pre)
         for (int b = t; b < ngroups; b += blockDim.x) {
             const double* q = gpl + (size_t)b * GP_N;
             g[0] += q[GP_COST]; g[1] += q[GP_MODEL]; g[2] += q[GP_STEPN]; g[3] += q[GP_XN];
             g[4] = fmax(g[4], q[GP_GMAX]);
         }
-        s0 = block_sum(g[0], sh);
-        s1 = block_sum(g[1], sh);
-        s2 = block_sum(g[2], sh);
-        s3 = block_sum(g[3], sh);
-    }
     // candidate mode: the camera rows' part of the model cost change, d.g_f + d^T C d / 2 with the
     // step d = -sol_f * scale_f and C, g_f the current linearization's (all-reduced, unscaled) camera
     // sums: per camera its 6 x 6 block, its coupling to the intrinsics and its gradient, then the
@@ -1286,25 +1323,22 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
             mf += q;
         }
     }
-    const double smf = block_sum(mf, sh);
-    const double sxn = block_sum(xn, sh);
-    const double ssn = block_sum(sn, sh);
+    // one pass: the group sums (unless the all-reduced ones are given), the camera model part, the
+    // camera parts of the parameter and step norms, and max |grad|
+    double v[7] = {g[0], g[1], g[2], g[3], mf, xn, sn};
     double gm = fmax(gmax, g[4]);
-    for (int o = 32; o > 0; o >>= 1) gm = fmax(gm, __shfl_xor(gm, o));
-    __syncthreads();
-    if ((t & 63) == 0) sh[t >> 6] = gm;
-    __syncthreads();
+    block_reduce<7>(v, gm, sh);
     if (t == 0) {
-        double m = 0.0;
-        for (int i = 0; i < 4; ++i) m = fmax(m, sh[i]);
+        const double s0 = pre ? pre[0] : v[0], s1 = pre ? pre[1] : v[1], s2 = pre ? pre[2] : v[2], s3 = pre ? pre[3] : v[3];
+        const double m = pre ? fmax(gm, pre[4]) : gm;
         scal[SC_COST] = s0;
-        scal[SC_MODEL] = cand_mode ? s1 + smf : s1;
+        scal[SC_MODEL] = cand_mode ? s1 + v[4] : s1;
         scal[SC_STEPN] = s2;
         scal[SC_XN] = s3;
         scal[SC_GMAX] = m;
         scal[SC_FAIL] = (double)*fail;   // bit 0: non-positive pivot / invalid step, bit 1: solve wait timed out
-        scal[SC_STEPN_F] = ssn;
-        scal[SC_XN_F] = sxn;
+        scal[SC_STEPN_F] = v[6];
+        scal[SC_XN_F] = v[5];
         // one rank: nothing is reduced after this kernel, so it publishes the scalars itself (ba_publish)
         if (pub_dst) publish_body(scal, SC_N, nullptr, 0, pub_dst, pub_seq, pub_v, fail);
     }
@@ -1313,36 +1347,25 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
 // Point-sharded ranks: the rank's group sums (cost, model change, step and parameter norms: the
 // loop of ba_finalize) and its max |grad| of the points, written behind the camera sums so the
 // four sums travel in the camera-sum all-reduce (one collective per linearization fewer);
-// out[4] (the max) stays outside the reduced range.  One workgroup of 256.
-__global__ __launch_bounds__(256)
+// out[4] (the max) stays outside the reduced range.  One workgroup of 1024.
+__global__ __launch_bounds__(1024)
 void ba_group_sums(int ngroups, const double* __restrict__ gpl, double* __restrict__ out, const int* __restrict__ gate) {
     if (step_gated(gate)) return;
-    __shared__ double sh[8];
+    __shared__ double sh[16 * 5];
     const int t = threadIdx.x;
-    double g[5] = {0, 0, 0, 0, 0};
+    double g[4] = {0, 0, 0, 0}, gm = 0.0;
     for (int b = t; b < ngroups; b += blockDim.x) {
         const double* q = gpl + (size_t)b * GP_N;
         g[0] += q[GP_COST]; g[1] += q[GP_MODEL]; g[2] += q[GP_STEPN]; g[3] += q[GP_XN];
-        g[4] = fmax(g[4], q[GP_GMAX]);
+        gm = fmax(gm, q[GP_GMAX]);
     }
-    const double s0 = block_sum(g[0], sh);
-    const double s1 = block_sum(g[1], sh);
-    const double s2 = block_sum(g[2], sh);
-    const double s3 = block_sum(g[3], sh);
-    double gm = g[4];
-    for (int o = 32; o > 0; o >>= 1) gm = fmax(gm, __shfl_xor(gm, o));
-    __syncthreads();
-    if ((t & 63) == 0) sh[t >> 6] = gm;
-    __syncthreads();
-    if (t == 0) {
-        double m = 0.0;
-        for (int i = 0; i < 4; ++i) m = fmax(m, sh[i]);
-        out[0] = s0; out[1] = s1; out[2] = s2; out[3] = s3; out[4] = m;
-    }
+    block_reduce<4>(g, gm, sh);
+    if (t == 0) { out[0] = g[0]; out[1] = g[1]; out[2] = g[2]; out[3] = g[3]; out[4] = gm; }
 }
 
 // ba_gupdate: the LM step's point update (above).  One thread per observation of a chunk (its W_o:
-// 9 independent 16-B loads) and one per point.  (Fusing it into the candidate's ba_glin, per chunk
+// 9 independent 16-B loads) and one per point.  Workgroups past the groups do ba_fstep's work
+// (the candidate cameras / intrinsics), so the step needs no launch of its own for it.  (Fusing it into the candidate's ba_glin, per chunk
 // before the linearization, was measured slower: DESIGN.md §5.)
 template <int K>
 __global__ __launch_bounds__(256)
@@ -1350,8 +1373,14 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
                 const int* __restrict__ pt_start, const double* __restrict__ Wr, const double* __restrict__ PRr,
                 const double* __restrict__ scale, const double* __restrict__ plt, const double* __restrict__ sol_f,
                 int P, int C, const double* __restrict__ x, double* __restrict__ cand, double* __restrict__ gpl,
-                const int* __restrict__ gate) {
+                const int* __restrict__ gate, int ngroups, int nf) {
     if (step_gated(gate)) return;
+    if ((int)blockIdx.x >= ngroups) {   // cand_f = x_f + (-sol_f) * scale_f (as ba_fstep)
+        const int i = ((int)blockIdx.x - ngroups) * blockDim.x + threadIdx.x;
+        const size_t ne = 3 * (size_t)P;
+        if (i < nf) cand[ne + i] = x[ne + i] + (-sol_f[i]) * scale[ne + i];
+        return;
+    }
     __shared__ double yv[GCH * 3];
     __shared__ double sh[8];
     const Grp G = grp[blockIdx.x];
@@ -1401,14 +1430,6 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
         q[GP_MODEL] = sm;
         q[GP_STEPN] = ss;
     }
-}
-
-// candidate cameras / intrinsics: cand_f = x_f + (-sol_f) * scale_f (one or more workgroups)
-__global__ void ba_fstep(int nf, const double* __restrict__ sol_f, const double* __restrict__ scale_f,
-                         const double* __restrict__ x_f, double* __restrict__ cand_f, const int* __restrict__ gate) {
-    if (step_gated(gate)) return;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nf) cand_f[i] = x_f[i] + (-sol_f[i]) * scale_f[i];
 }
 
 }  // namespace ba

@@ -357,17 +357,17 @@ __global__ void ba_decide(const double* __restrict__ scal, double* __restrict__ 
 // Re-opens the step gate (after a rejected step, before the host enqueues the step again).
 __global__ void ba_open_gate(int* __restrict__ fail) { if (threadIdx.x == 0) fail[1] = 1; }
 
-// scale = 1 / (1 + sqrt(colsq)) (iteration 0 only, Ceres jacobi_scaling)
-// problem setup: the observed pixels in the internal (locality) order, xy[k] = raw[operm[k]]
-__global__ void ba_gather_xy(int O, const int* __restrict__ operm, const double2* __restrict__ raw,
-                             double2* __restrict__ xy) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < O) xy[k] = raw[operm[k]];
+// problem setup: every observation's (internal) point from the point-major CSR
+__global__ void ba_obs_point(int P, const int* __restrict__ pt_start, int* __restrict__ obs_point) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < P)
+        for (int o = pt_start[p]; o < pt_start[p + 1]; ++o) obs_point[o] = p;
 }
 __global__ void ba_fill(int64_t n, double v, double* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = v;
 }
+// scale = 1 / (1 + sqrt(colsq)) (iteration 0 only, Ceres jacobi_scaling)
 __global__ void ba_scale(int n, const double* __restrict__ colsq, double* __restrict__ scale) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) scale[i] = 1.0 / (1.0 + sqrt(colsq[i]));

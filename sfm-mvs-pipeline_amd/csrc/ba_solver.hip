@@ -11,11 +11,11 @@
 // The controller mirrors oracle/ba_oracle.cpp (the CPU restatement) step for step.
 //
 // Per LM step (try_step), in stream order:
-//   ba_gschur -> memset S -> ba_assemble -> [all-reduce S, R, D, r_i] -> ba_add_cam -> chol_leaves,
-//   chol_level x height, chol_intr, chol_back (the plan's level schedule, ba_plan.hpp / ba_chol.hpp)
-//   -> ba_gupdate, ba_fstep -> ba_glin (the candidate, speculatively: its Jacobian is the next
-//   linearization if the step is accepted) -> ba_camred -> [all-reduce] -> ba_finalize ->
-//   [all-reduce scalars] -> one D2H of the scalars.
+//   ba_gschur -> memset S -> ba_assemble -> [all-reduce S, R, D, r_i] -> ba_add_cam -> chol_factor
+//   (the plan's elimination-tree schedule in one launch, ba_plan.hpp / ba_chol.hpp) -> chol_backsolve
+//   -> ba_gupdate (+ the candidate cameras) -> ba_glin (the candidate, speculatively: its records are
+//   the next linearization if the step is accepted) -> ba_camred -> [all-reduce] -> ba_finalize
+//   (-> ba_publish: the scalars through pinned host-coherent memory) -> [all-reduce scalars].
 #include "ba_group.hpp"
 #include "ba_chol.hpp"
 #include "ba_plan.hpp"
@@ -95,7 +95,6 @@ struct sfmx_ba_ctx {
     int n_intr = 0, intr_len = 0;   // caller's blocks and the length of its intr array
     std::vector<int> isrc;
     Buf pim, pcc;
-    Buf xyraw, operm_d;   // the caller's obs_xy and the internal -> caller observation map (setup)
     int64_t n = 0, ne = 0;
     int nf = 0, npad = 0, T = 0, RW = 0;
     sfmx_allreduce_fn ar = nullptr;
@@ -151,7 +150,8 @@ struct sfmx_ba_ctx {
     size_t stage_cap = 0, stage_off = 0;
     // host-side setup of the last create / update: [0] ordering + topology, [1] device allocation,
     // [2] uploads, [3] factorization plan, [4] total (ms)
-    double setup_ms[5] = {0, 0, 0, 0, 0};
+    // [5] ordering, [6] point groups / topology (the two parts of [0])
+    double setup_ms[7] = {0, 0, 0, 0, 0, 0, 0};
     std::vector<char> plan_adj;   // the co-visibility the current plan was built from (reused if equal)
     int plan_K = 0;
     HostScratch* hscr = nullptr;
@@ -160,7 +160,7 @@ struct sfmx_ba_ctx {
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
                       &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &Wr, &Wr2, &PR, &PR2, &J, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
-                      &failf, &partA, &lmst, &camscr, &pim, &pcc, &xyraw, &operm_d};
+                      &failf, &partA, &lmst, &camscr, &pim, &pcc};
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
@@ -337,12 +337,12 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Wo, double* PRo, double* co
     // rank's point max |grad| at cs_red[ncs + 4] outside it): 3 collectives per LM step, not 4
     double* pre = multirank(c) ? cs_red + ncs : nullptr;
     if (pre)
-        hipLaunchKernelGGL(ba_group_sums, dim3(1), dim3(256), 0, c->st, c->ngroups, c->gpl.as<double>(), pre, gate(c));
+        hipLaunchKernelGGL(ba_group_sums, dim3(1), dim3(1024), 0, c->st, c->ngroups, c->gpl.as<double>(), pre, gate(c));
     RC(allreduce(c, cs_red, ncs + (pre ? 4 : 0), SFMX_REDUCE_SUM));
     // one rank, host-judged, no phase mark: ba_finalize publishes the scalars itself (one launch fewer)
     const bool fold = out && !multirank(c) && !(c->phases && cand_mode);
     const unsigned fold_seq = fold ? ++c->seq : 0;
-    hipLaunchKernelGGL(ba_finalize<K>, dim3(1), dim3(256), 0, c->st, c->ngroups, c->P, c->C, cs_red,
+    hipLaunchKernelGGL(ba_finalize<K>, dim3(1), dim3(1024), 0, c->st, c->ngroups, c->P, c->C, cs_red,
                        c->gpl.as<double>(), xp + c->ne, c->x.as<double>() + c->ne, cand_mode ? 1 : 0, c->failf.as<int>(),
                        colsq_o, grad_o, scal(c, 0), camsum_o, cs_red == camsum_o ? 0 : ncs, pre,
                        fold ? c->hs : nullptr, reinterpret_cast<unsigned*>(c->hs + sfmx_ba_ctx::HS_SEQ + 2), fold_seq,
@@ -458,13 +458,11 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     double* sol = c->sol.as<double>();
     RC(solve_reduced<RW>(c, sol + c->ne));
     if (c->phases) HIPCHK(hipEventRecord(c->ev[2], c->st));
-    if (c->ngroups > 0)
-        hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups), dim3(256), 0, c->st, c->grp.as<Grp>(),
-                           c->chk.as<Chunk>(), c->obs_cam.as<int>(), c->pt_start.as<int>(), c->Wr.as<double>(),
-                           c->PR.as<double>(), c->scale.as<double>(), c->plt.as<double>(), sol + c->ne, c->P, C,
-                           c->x.as<double>(), c->cand.as<double>(), c->gpl.as<double>(), gate(c));
-    hipLaunchKernelGGL(ba_fstep, dim3(nblk(c->nf)), dim3(256), 0, c->st, c->nf, sol + c->ne, c->scale.as<double>() + c->ne,
-                       c->x.as<double>() + c->ne, c->cand.as<double>() + c->ne, gate(c));
+    // the point update, and in workgroups past the groups the candidate cameras / intrinsics
+    hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups + nblk(c->nf)), dim3(256), 0, c->st, c->grp.as<Grp>(),
+                       c->chk.as<Chunk>(), c->obs_cam.as<int>(), c->pt_start.as<int>(), c->Wr.as<double>(),
+                       c->PR.as<double>(), c->scale.as<double>(), c->plt.as<double>(), sol + c->ne, c->P, C,
+                       c->x.as<double>(), c->cand.as<double>(), c->gpl.as<double>(), gate(c), c->ngroups, (int)c->nf);
     HIPCHK(hipGetLastError());
     double v[SC_N];
     RC(lin_at<K>(c, c->cand.as<double>(), c->Wr2.as<double>(), c->PR2.as<double>(), c->colsq2.as<double>(), c->grad2.as<double>(),
@@ -867,8 +865,10 @@ int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
     if (c->P) {
         double* pts = static_cast<double*>(stage_bytes(c, sizeof(double) * 3 * (size_t)c->P));
         if (!pts) return fail(SFMX_ENOMEM, "pinned staging buffer");
-        for (int q = 0; q < c->P; ++q)
-            for (int i = 0; i < 3; ++i) pts[3 * (size_t)q + i] = pb->points[3 * (size_t)c->pperm[q] + i];
+        sfmx::parallel_ranges(c->P, 16, [&](int64_t q0, int64_t q1) {
+            for (int64_t q = q0; q < q1; ++q)
+                for (int i = 0; i < 3; ++i) pts[3 * (size_t)q + i] = pb->points[3 * (size_t)c->pperm[q] + i];
+        });
         HIPCHK(hipMemcpyAsync(x, pts, sizeof(double) * 3 * c->P, hipMemcpyHostToDevice, c->st));
     }
     if (c->C) HIPCHK(hipMemcpyAsync(x + c->ne, pb->poses, sizeof(double) * 6 * c->C, hipMemcpyHostToDevice, c->st));
@@ -883,10 +883,10 @@ int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
 // their sorted camera lists (points seen by the same cameras become neighbours, so a point group
 // spans few cameras), observations point-major in that order.  The sort key is the list's first
 // cameras, as many as fit 64 bits at ceil(log2(C + 2)) bits each, at most 6 (lexicographic, a
-// shorter list first), ties keep the caller's order (an LSD radix sort is stable).  Fills pperm / operm (internal -> caller), rop /
+// shorter list first), ties keep the caller's order (an LSD radix sort is stable).  Fills pperm / operm (internal -> caller),
 // roc (internal observations) and pt_start.
-struct Ordered {   // rxy is gathered on the device (ba_gather_xy) from the caller's obs_xy
-    std::vector<int> pperm, operm, rop, roc, pt_start;
+struct Ordered {   // the observed pixels are gathered in this order into the upload staging (load_problem)
+    std::vector<int> pperm, operm, roc, pt_start;
     std::vector<int> start, obs, tmp;          // scratch, kept with the context between calls
     std::vector<uint64_t> key, ktmp;
     std::vector<uint32_t> cnt;
@@ -897,15 +897,30 @@ void order_problem(const sfmx_ba_problem* pb, Ordered& od) {
     constexpr int PIECES = 64;   // fixed ranges (host_par.hpp): the same result on every host
     std::vector<int>& start = od.start;
     std::vector<int>& obs = od.obs;
-    start.assign(P + 1, 0);
+    start.resize(P + 1);
     obs.resize(O);
-    for (int i = 0; i < O; ++i) start[pb->obs_point[i] + 1]++;
-    for (int p = 0; p < P; ++p) start[p + 1] += start[p];
-    bool point_major = true;   // the reference adds residuals point by point: obs[a] == a then
-    for (int i = 1; i < O && point_major; ++i) point_major = pb->obs_point[i] >= pb->obs_point[i - 1];
+    // the reference adds residuals point by point (BundleAdjustment.cpp:50-91): obs[a] == a then,
+    // and start[] is where the point index steps (both in parallel ranges)
+    std::atomic<bool> pm{true};
+    sfmx::parallel_ranges(O, PIECES, [&](int64_t i0, int64_t i1) {
+        for (int64_t i = std::max<int64_t>(i0, 1); i < i1; ++i)
+            if (pb->obs_point[i] < pb->obs_point[i - 1]) { pm = false; return; }
+    });
+    const bool point_major = pm;
     if (point_major) {
-        for (int i = 0; i < O; ++i) obs[i] = i;
+        const int* op = pb->obs_point;
+        sfmx::parallel_ranges((int64_t)O + 1, PIECES, [&](int64_t i0, int64_t i1) {
+            for (int64_t i = i0; i < i1; ++i) {   // points (op[i - 1], op[i]] start at i
+                const int lo = i == 0 ? -1 : op[i - 1], hi = i == O ? P - 1 : op[i];
+                for (int p = lo + 1; p <= hi; ++p) start[p] = (int)i;
+                if (i < O) obs[i] = (int)i;
+            }
+        });
+        start[P] = O;
     } else {
+        std::fill(start.begin(), start.end(), 0);
+        for (int i = 0; i < O; ++i) start[pb->obs_point[i] + 1]++;
+        for (int p = 0; p < P; ++p) start[p + 1] += start[p];
         std::vector<int> f(start.begin(), start.end() - 1);
         for (int i = 0; i < O; ++i) obs[f[pb->obs_point[i]]++] = i;
     }
@@ -957,14 +972,13 @@ void order_problem(const sfmx_ba_problem* pb, Ordered& od) {
     }
     od.pt_start.assign(P + 1, 0);
     for (int q = 0; q < P; ++q) od.pt_start[q + 1] = od.pt_start[q] + start[pperm[q] + 1] - start[pperm[q]];
-    od.operm.resize(O); od.rop.resize(O); od.roc.resize(O);
+    od.operm.resize(O); od.roc.resize(O);
     sfmx::parallel_ranges(P, PIECES, [&](int64_t q0, int64_t q1) {
         for (int64_t q = q0; q < q1; ++q) {
             const int p = pperm[q];
             for (int a = start[p], k = od.pt_start[q]; a < start[p + 1]; ++a, ++k) {
                 const int o = obs[a];
                 od.operm[k] = o;
-                od.rop[k] = (int)q;
                 od.roc[k] = pb->obs_cam[o];
             }
         }
@@ -1173,7 +1187,17 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
                     pr.push_back(PairRef{((uint64_t)(uint32_t)tp.gcam[G.cam_off + la] << 32) | (uint32_t)tp.gcam[G.cam_off + lb],
                                          g, la, lb});
         }
-        std::stable_sort(pr.begin(), pr.end(), [](const PairRef& x, const PairRef& y) { return x.key < y.key; });
+        if ((int64_t)C * C <= ((int64_t)1 << 22)) {   // stable counting sort on the pair index a C + b
+            std::vector<int> cnt((size_t)C * C + 1, 0);
+            std::vector<PairRef> out(pr.size());
+            auto idx = [C](const PairRef& x) { return (size_t)(x.key >> 32) * C + (size_t)(x.key & 0xffffffffu); };
+            for (const PairRef& x : pr) cnt[idx(x) + 1]++;
+            for (size_t i = 1; i < cnt.size(); ++i) cnt[i] += cnt[i - 1];
+            for (const PairRef& x : pr) out[cnt[idx(x)]++] = x;
+            pr.swap(out);
+        } else {
+            std::stable_sort(pr.begin(), pr.end(), [](const PairRef& x, const PairRef& y) { return x.key < y.key; });
+        }
         tp.ents.reserve(pr.size() + tp.gcam.size() + tp.grp.size());
         for (size_t i = 0; i < pr.size();) {
             ATask t{0, (int)(pr[i].key >> 32), (int)(pr[i].key & 0xffffffffu), (int)tp.ents.size(), 0, 0, 0, 0};
@@ -1221,7 +1245,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     if (!c->hscr) return fail(SFMX_ENOMEM, "host allocation");
     Ordered& od = c->hscr->od;
     order_problem(caller, od);
-    std::vector<int>& rop = od.rop;
+    c->setup_ms[5] = ms_since(t_start);
     std::vector<int>& roc = od.roc;
     c->pperm.swap(od.pperm);
     c->operm.swap(od.operm);
@@ -1291,7 +1315,9 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     std::vector<int>& pt_start = od.pt_start;
     Topology& tp = c->hscr->tp;
     tp.seg = &c->hscr->seg;
+    const auto t_topo = clk::now();
     build_topology(P, C, O, K, pt_start, roc.data(), tp);
+    c->setup_ms[6] = ms_since(t_topo);
     // local camera co-visibility (the pose blocks this rank's points create)
     c->adj.assign((size_t)C * C, 0);
     for (const ATask& t : tp.tasks)
@@ -1329,19 +1355,27 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     hipStream_t st = c->st;
     int rc;
     const auto t_up = clk::now();
-    // observed pixels: the caller's array as it is (no host shuffle), gathered into the internal
-    // order on the device
-    RC(c->xyraw.alloc(sizeof(double) * 2 * std::max<size_t>(O, 1)));
+    // observed pixels: gathered into the internal order while they are copied into the pinned
+    // staging arena (parallel host ranges, then one DMA; the caller's array is pageable)
     RC(c->obs_xy.alloc(sizeof(double) * 2 * std::max<size_t>(O, 1)));
-    if (O) HIPCHK(hipMemcpyAsync(c->xyraw.p, caller->obs_xy, sizeof(double) * 2 * (size_t)O, hipMemcpyHostToDevice, st));
-    RC(upload(c, c->operm_d, c->operm));
     if (O) {
-        hipLaunchKernelGGL(ba_gather_xy, dim3(nblk(O)), dim3(256), 0, st, O, c->operm_d.as<int>(),
-                           c->xyraw.as<double2>(), c->obs_xy.as<double2>());
+        double2* h = static_cast<double2*>(stage_bytes(c, sizeof(double2) * (size_t)O));
+        if (!h) return bail(fail(SFMX_ENOMEM, "pinned staging buffer"));
+        const double2* xy = reinterpret_cast<const double2*>(caller->obs_xy);
+        const int* om = c->operm.data();
+        sfmx::parallel_ranges(O, 64, [&](int64_t k0, int64_t k1) {
+            for (int64_t k = k0; k < k1; ++k) h[k] = xy[om[k]];
+        });
+        HIPCHK(hipMemcpyAsync(c->obs_xy.p, h, sizeof(double2) * (size_t)O, hipMemcpyHostToDevice, st));
+    }
+    // the observations' points from the point-major CSR on the device (no upload of rop)
+    RC(c->obs_point.alloc(sizeof(int) * std::max<size_t>(O, 1)));
+    if ((rc = upload(c, c->pt_start, pt_start))) return bail(rc);
+    if (P && O) {
+        hipLaunchKernelGGL(ba_obs_point, dim3(nblk(P)), dim3(256), 0, st, P, c->pt_start.as<int>(), c->obs_point.as<int>());
         HIPCHK(hipGetLastError());
     }
-    if ((rc = upload(c, c->obs_point, rop)) || (rc = upload(c, c->obs_cam, roc)) ||
-        (rc = upload(c, c->pt_start, pt_start)) || (rc = upload(c, c->grp, tp.grp)) || (rc = upload(c, c->chk, tp.chk)) || (rc = upload(c, c->bat, tp.bat)) ||
+    if ((rc = upload(c, c->obs_cam, roc)) || (rc = upload(c, c->grp, tp.grp)) || (rc = upload(c, c->chk, tp.chk)) || (rc = upload(c, c->bat, tp.bat)) ||
         (rc = upload(c, c->gcam, tp.gcam)) || (rc = upload(c, c->obs_lc, tp.obs_lc)) ||
         (rc = upload(c, c->obs_row, tp.obs_row)) || (rc = upload(c, c->lcrow, tp.lcrow)) ||
         (rc = upload(c, c->tasks, tp.tasks)) || (rc = upload(c, c->ents, tp.ents)) ||
@@ -1586,7 +1620,7 @@ int sfmx_ba_update(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
 
 int sfmx_ba_setup_ms(sfmx_ba_ctx* c, double* ms, int32_t n) {
     if (!c || !ms) return fail(SFMX_EINVAL, "null");
-    const int m = std::min<int>(n, 5);
+    const int m = std::min<int>(n, 7);
     for (int i = 0; i < m; ++i) ms[i] = c->setup_ms[i];
     return m;
 }

@@ -304,12 +304,14 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
             m->any_nonintegral |= fl[i] != 0;
         }
         if (m->any_nonintegral) {
+            // every image gets its fp32 rows: a pair takes the fp32 path when EITHER side is
+            // non-integral, and then reads both sides from this buffer (an integral partner's rows
+            // were left unwritten before r03: stale memory, caught by test_non_integral_fp32_fallback)
             if ((rc = m->f32.ensure((size_t)row * SIFT_DIM * 4))) return rc;
             for (int i = 0; i < n; ++i) {
                 const ImgDev& d = m->imgs[i];
-                if (!d.integral)
-                    HIPCHK(launch_prep_f32((const float*)src[i], d.rows, imgs[i].cols, d.rows_pad,
-                                           m->f32.as<float>() + d.row0 * SIFT_DIM, st));
+                HIPCHK(launch_prep_f32((const float*)src[i], d.rows, imgs[i].cols, d.rows_pad,
+                                       m->f32.as<float>() + d.row0 * SIFT_DIM, st));
             }
         }
     }

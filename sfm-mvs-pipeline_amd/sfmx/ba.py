@@ -186,9 +186,10 @@ class BAContext:
 
     def setup_ms(self) -> dict:
         """Host-side setup of the last create / update (ms)."""
-        v = (C.c_double * 5)()
-        n = check(lib.sfmx_ba_setup_ms(self._h, v, 5), "sfmx_ba_setup_ms")
-        return {k: v[i] for i, k in enumerate(["order_groups", "alloc", "upload", "plan", "total"][:n])}
+        v = (C.c_double * 7)()
+        n = check(lib.sfmx_ba_setup_ms(self._h, v, 7), "sfmx_ba_setup_ms")
+        return {k: v[i] for i, k in enumerate(["order_groups", "alloc", "upload", "plan", "total", "order",
+                                                "groups"][:n])}
 
     def reset(self, problem: Optional[BAProblem] = None):
         st = (problem or self.problem).struct()

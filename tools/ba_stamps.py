@@ -6,7 +6,7 @@ import ctypes as C
 import os
 import sys
 
-os.environ["SFMX_LIB_NAME"] = "libsfmx_stamps.so"
+os.environ.setdefault("SFMX_LIB_NAME", "libsfmx_stamps.so")
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "sfm-mvs-pipeline_amd")]
 import numpy as np  # noqa: E402
