@@ -580,13 +580,16 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
 }
 
 // ---------------------------------------------------------------------------------------------
-// ba_assemble: one 64-thread workgroup per block of the reduced system, summing the group
-// contributions in group order (normal groups: their dense block; big groups: -H_a H_b^T from the
-// stored H).  Bordered layout (ba_chol.hpp): pose blocks into S_cc at the plan's camera rows (and
-// the transpose), pose-intrinsics blocks and the camera rhs into R = [B | r_c], the intrinsics
-// block and rhs into D / r_i.  Everything is zeroed before; C, D^2
-// and g_f are added by ba_add_cam (after any cross-rank all-reduce).  Entries carry absolute offsets (no dependent loads); the
-// intrinsics block (every group) is a strided, fixed-order wave reduction.
+// ba_assemble: one 256-thread workgroup per block of the reduced system, summing the group
+// contributions (normal groups: their dense block; big groups: -H_a H_b^T from the stored H).
+// Bordered layout (ba_chol.hpp): pose blocks into S_cc at the plan's camera rows (and the
+// transpose), pose-intrinsics blocks and the camera rhs into R = [B | r_c], the intrinsics block and
+// rhs into D / r_i.  Everything is zeroed before; C, D^2 and g_f are added by ba_add_cam (after any
+// cross-rank all-reduce).  A block's entry list (a pose pair of C5 is held by ~80 groups, the
+// intrinsics by every group) is split over the workgroup: thread (part, output) sums the entries
+// part, part + NP, ... (NP = 256 / outputs), the parts are then added in part order (fixed,
+// deterministic); the intrinsics outputs (one per workgroup) reduce their 256 strided partials by
+// waves.  r02 ran one thread per output over the whole list, a chain of dependent loads per entry.
 __device__ __forceinline__ double aval(const AEnt& E, const double* __restrict__ sg, const double* __restrict__ hbig,
                                        int r, int c) {
     if (!E.big) return sg[E.b0 + (long long)r * E.dim + c];
@@ -598,53 +601,68 @@ __device__ __forceinline__ double wave_sum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
-__global__ __launch_bounds__(64)
+constexpr int ASM_THREADS = 256;
+__global__ __launch_bounds__(ASM_THREADS)
 void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents, const double* __restrict__ sg,
                  const double* __restrict__ hbig, const double* __restrict__ rg, int K, const int* __restrict__ camrow,
                  int npad, double* __restrict__ S, double* __restrict__ R, double* __restrict__ Dm,
                  double* __restrict__ ri, const int* __restrict__ gate) {
     if (step_gated(gate)) return;
+    __shared__ double part[ASM_THREADS];
     const ATask T = tasks[blockIdx.x];
     const int t = threadIdx.x, RW = K + 1;
-    if (T.type == 0) {
-        if (t >= 36) return;
-        const int u = t / 6, w = t % 6, ra = camrow[T.a], rb = camrow[T.b];
-        double v = 0.0;
-#pragma unroll 4
-        for (int e = T.l0; e < T.l1; ++e) v += aval(ents[e], sg, hbig, u, w);
-        S[(size_t)(ra + u) * npad + rb + w] = v;
-        if (T.a != T.b) S[(size_t)(rb + w) * npad + ra + u] = v;
-    } else if (T.type == 1) {   // entries: b0 / b1 at the camera rows / the intrinsics rows of the group
-        const int ra = camrow[T.a];
-        if (t < 6 * K) {        // B (camera rows x intrinsics): the first K right-hand sides
-            const int u = t / K, i = t % K;
-            double v = 0.0;
-#pragma unroll 4
-            for (int e = T.l0; e < T.l1; ++e) v += aval(ents[e], sg, hbig, u, i);
-            R[(size_t)(ra + u) * RW + i] = v;
-        } else if (t < 6 * K + 6) {
-            const int d = t - 6 * K;
-            double v = 0.0;
-#pragma unroll 4
-            for (int e = T.l0; e < T.l1; ++e) v += rg[ents[e].rg + d];
-            R[(size_t)(ra + d) * RW + K] = v;
-        }
-    } else {                    // one intrinsics output x = T.b over every group; entries at the intrinsics rows
+    if (T.type == 2) {          // one intrinsics output x = T.b over every group; entries at the intrinsics rows
         const int x = T.b;
         double v0 = 0.0, v1 = 0.0;
         int e = T.l0 + t;
         if (x < K * K) {
             const int i = x / K, j = x % K;
-            for (; e + 64 < T.l1; e += 128) { v0 += aval(ents[e], sg, hbig, i, j); v1 += aval(ents[e + 64], sg, hbig, i, j); }
+            for (; e + ASM_THREADS < T.l1; e += 2 * ASM_THREADS) {
+                v0 += aval(ents[e], sg, hbig, i, j);
+                v1 += aval(ents[e + ASM_THREADS], sg, hbig, i, j);
+            }
             if (e < T.l1) v0 += aval(ents[e], sg, hbig, i, j);
         } else {
-            for (; e + 64 < T.l1; e += 128) { v0 += rg[ents[e].rg + (x - K * K)]; v1 += rg[ents[e + 64].rg + (x - K * K)]; }
+            for (; e + ASM_THREADS < T.l1; e += 2 * ASM_THREADS) {
+                v0 += rg[ents[e].rg + (x - K * K)];
+                v1 += rg[ents[e + ASM_THREADS].rg + (x - K * K)];
+            }
             if (e < T.l1) v0 += rg[ents[e].rg + (x - K * K)];
         }
         const double v = wave_sum(v0 + v1);
+        if ((t & 63) == 0) part[t >> 6] = v;
+        __syncthreads();
         if (t == 0) {
-            if (x < K * K) Dm[x] = v;
-            else ri[x - K * K] = v;
+            const double s = ((part[0] + part[1]) + part[2]) + part[3];
+            if (x < K * K) Dm[x] = s;
+            else ri[x - K * K] = s;
+        }
+        return;
+    }
+    // type 0: the 6 x 6 pose block (a, b); type 1: camera a's 6 x K block of B and its 6 rhs entries
+    const int nout = T.type == 0 ? 36 : 6 * K + 6;
+    const int np = ASM_THREADS / nout, o = t % nout, pt = t / nout;
+    double v = 0.0;
+    if (pt < np) {
+        const bool rhs = T.type == 1 && o >= 6 * K;
+        const int r = T.type == 0 ? o / 6 : (rhs ? o - 6 * K : o / K), c = T.type == 0 ? o % 6 : o % K;
+        int e = T.l0 + pt;
+#pragma unroll 4
+        for (; e < T.l1; e += np) v += rhs ? rg[ents[e].rg + r] : aval(ents[e], sg, hbig, r, c);
+        part[t] = v;
+    }
+    __syncthreads();
+    if (t < nout) {
+        double s = part[t];
+        for (int q = 1; q < np; ++q) s += part[q * nout + t];
+        if (T.type == 0) {
+            const int u = t / 6, w = t % 6, ra = camrow[T.a], rb = camrow[T.b];
+            S[(size_t)(ra + u) * npad + rb + w] = s;
+            if (T.a != T.b) S[(size_t)(rb + w) * npad + ra + u] = s;
+        } else {
+            const int ra = camrow[T.a];
+            if (t < 6 * K) R[(size_t)(ra + t / K) * RW + t % K] = s;
+            else R[(size_t)(ra + t - 6 * K) * RW + K] = s;
         }
     }
 }
@@ -1150,45 +1168,45 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
 }
 
 // ---------------------------------------------------------------------------------------------
-// ba_camred: per camera (one workgroup) the partials of its (group, camera) slots in group
-// order -> camsum[c]; one more workgroup: the intrinsics fields of every slot, in slot order.
+// ba_camred: per camera (one workgroup of 256) the partials of its (group, camera) slots ->
+// camsum[c]: thread (part, field) sums the slots part, part + NP, ... (NP = 256 / fields), the parts
+// are added in part order (fixed); one more workgroup per intrinsics field: that field of every
+// slot, strided per thread (2 chains), then a fixed-order block reduction.
+constexpr int CRED_THREADS = 256;
 template <int K>
-__global__ __launch_bounds__(128)
+__global__ __launch_bounds__(CRED_THREADS)
 void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int* __restrict__ cref,
                const double* __restrict__ gpart, double* __restrict__ camsum, const int* __restrict__ gate) {
     if (step_gated(gate)) return;
-    constexpr int NCP = ncp(K);
+    constexpr int NCP = ncp(K), NFC = cp_ii(K), NP = CRED_THREADS / NFC;
+    __shared__ double part[CRED_THREADS];
     const int t = threadIdx.x;
     if ((int)blockIdx.x < C) {
-        const int c = blockIdx.x, e0 = cref_start[c], e1 = cref_start[c + 1];
-        for (int f = t; f < cp_ii(K); f += blockDim.x) {
-            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;   // 4 interleaved chains, combined in fixed order
-            int e = e0;
-            for (; e + 3 < e1; e += 4) {
-                const int c0 = cref[e], c1 = cref[e + 1], c2 = cref[e + 2], c3 = cref[e + 3];
-                s0 += gpart[(size_t)c0 * NCP + f]; s1 += gpart[(size_t)c1 * NCP + f];
-                s2 += gpart[(size_t)c2 * NCP + f]; s3 += gpart[(size_t)c3 * NCP + f];
-            }
-            for (; e < e1; ++e) s0 += gpart[(size_t)cref[e] * NCP + f];
-            camsum[(size_t)c * NCP + f] = (s0 + s1) + (s2 + s3);
+        const int c = blockIdx.x, e0 = cref_start[c], e1 = cref_start[c + 1], f = t % NFC, pt = t / NFC;
+        if (pt < NP) {
+            double sacc = 0.0;
+            int e = e0 + pt;
+#pragma unroll 4
+            for (; e < e1; e += NP) sacc += gpart[(size_t)cref[e] * NCP + f];
+            part[t] = sacc;
         }
-    } else {   // intrinsics field f = blockIdx.x - C over every slot: strided per thread (4 chains), then a
-               // fixed-order block reduction
-        __shared__ double sh[8];
-        {
-            const int f = blockIdx.x - C;
-            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-            int e = t;
-            for (; e + 3 * (int)blockDim.x < nslots; e += 4 * blockDim.x) {
-                s0 += gpart[(size_t)e * NCP + cp_ii(K) + f];
-                s1 += gpart[(size_t)(e + blockDim.x) * NCP + cp_ii(K) + f];
-                s2 += gpart[(size_t)(e + 2 * blockDim.x) * NCP + cp_ii(K) + f];
-                s3 += gpart[(size_t)(e + 3 * blockDim.x) * NCP + cp_ii(K) + f];
-            }
-            for (; e < nslots; e += blockDim.x) s0 += gpart[(size_t)e * NCP + cp_ii(K) + f];
-            const double tot = block_sum((s0 + s1) + (s2 + s3), sh);
-            if (t == 0) camsum[(size_t)C * NCP + f] = tot;
+        __syncthreads();
+        if (t < NFC) {
+            double sm = part[t];
+            for (int q = 1; q < NP; ++q) sm += part[q * NFC + t];
+            camsum[(size_t)c * NCP + t] = sm;
         }
+    } else {   // intrinsics field f = blockIdx.x - C over every slot
+        const int f = blockIdx.x - C;
+        double s0 = 0.0, s1 = 0.0;
+        int e = t;
+        for (; e + CRED_THREADS < nslots; e += 2 * CRED_THREADS) {
+            s0 += gpart[(size_t)e * NCP + NFC + f];
+            s1 += gpart[(size_t)(e + CRED_THREADS) * NCP + NFC + f];
+        }
+        if (e < nslots) s0 += gpart[(size_t)e * NCP + NFC + f];
+        const double tot = block_sum(s0 + s1, part);
+        if (t == 0) camsum[(size_t)C * NCP + f] = tot;
     }
 }
 

@@ -32,6 +32,7 @@
 #include <mutex>
 #include <string>
 #include <cstdlib>
+#include <cstdio>
 #include <unordered_map>
 #include <vector>
 
@@ -50,7 +51,7 @@ int fail(int code, const std::string& m) { sfmx::set_last_error(m.c_str()); retu
         hipError_t e_ = (expr);                                                                     \
         if (e_ != hipSuccess)                                                                       \
             return fail(e_ == hipErrorOutOfMemory ? SFMX_ENOMEM : SFMX_EDEVICE,                     \
-                        std::string(#expr) + ": " + hipGetErrorString(e_));                         \
+                        std::string(#expr) + " (ba_solver.hip:" + std::to_string(__LINE__) + "): " + hipGetErrorString(e_)); \
     } while (0)
 #define RC(expr) do { int rc_ = (expr); if (rc_) return rc_; } while (0)
 
@@ -63,7 +64,7 @@ struct Buf {
     int alloc(size_t b) {
         b = std::max<size_t>(b, 64);
         if (p && b <= cap) { bytes = b; return SFMX_OK; }
-        const size_t want = p ? std::max(b, cap + cap / 4) : b;   // first allocation exact, regrowth with headroom
+        const size_t want = p ? std::max(b, cap + cap / 2) : b;   // first allocation exact, regrowth with headroom
         if (p) { (void)hipFree(p); p = nullptr; }
         hipError_t e = hipMalloc(&p, want);
         if (e != hipSuccess) { p = nullptr; cap = bytes = 0; return fail(SFMX_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)); }
@@ -220,6 +221,23 @@ void* stage_bytes(sfmx_ba_ctx* c, size_t n) {
     return p;
 }
 
+// the arena sized for a whole call's uploads at once (else a full arena waits for the DMAs in flight)
+int stage_reserve(sfmx_ba_ctx* c, size_t n) {
+    if (c->stage_off + n <= c->stage_cap) return SFMX_OK;
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->stage_off = 0;
+    if (n > c->stage_cap) {
+        if (c->stage) (void)hipHostFree(c->stage);
+        c->stage = nullptr;
+        c->stage_cap = n + n / 4;
+        if (hipHostMalloc(reinterpret_cast<void**>(&c->stage), c->stage_cap, hipHostMallocDefault) != hipSuccess) {
+            c->stage_cap = 0;
+            return fail(SFMX_ENOMEM, "pinned staging buffer");
+        }
+    }
+    return SFMX_OK;
+}
+
 template <class T>
 int upload(sfmx_ba_ctx* c, Buf& b, const std::vector<T>& v) {
     RC(b.alloc(sizeof(T) * std::max<size_t>(v.size(), 1)));
@@ -330,7 +348,7 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Wo, double* PRo, double* co
     // all-reduce then touches no state (ba_finalize copies them behind the step gate)
     const int ncs = c->C * ncp(K) + K * (K + 1) / 2 + K;
     double* cs_red = (multirank(c) && c->spec) ? c->camscr.as<double>() : camsum_o;
-    hipLaunchKernelGGL(ba_camred<K>, dim3(c->C + K * (K + 1) / 2 + K), dim3(128), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
+    hipLaunchKernelGGL(ba_camred<K>, dim3(c->C + K * (K + 1) / 2 + K), dim3(CRED_THREADS), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
                        c->cref.as<int>(), c->gpart.as<double>(), cs_red, gate(c));
     HIPCHK(hipGetLastError());
     // multi-rank: the group sums ride in the camera-sum all-reduce (cs_red[ncs .. ncs + 4), the
@@ -436,7 +454,7 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
         c->j_scaled = true;
     }
     HIPCHK(hipMemsetAsync(S, 0, sizeof(double) * c->sr_count, c->st));
-    hipLaunchKernelGGL(ba_assemble, dim3(c->ntasks), dim3(64), 0, c->st, c->tasks.as<ATask>(), c->ents.as<AEnt>(),
+    hipLaunchKernelGGL(ba_assemble, dim3(c->ntasks), dim3(ASM_THREADS), 0, c->st, c->tasks.as<ATask>(), c->ents.as<AEnt>(),
                        c->sg.as<double>(), c->hbig.as<double>(), c->rg.as<double>(), K, c->camrow.as<int>(), npad, S,
                        R, Dm, ri, gate(c));
     HIPCHK(hipGetLastError());
@@ -942,30 +960,50 @@ void order_problem(const sfmx_ba_problem* pb, Ordered& od) {
             key[p] = k;
         }
     });
-    // LSD radix sort of (key, p) pairs over the key's nk * kb bits, 16 per pass (stable), passes
-    // whose digit is constant skipped
+    // LSD radix sort of (key, p) pairs over the key's nk * kb bits, 8 per pass (stable), passes whose
+    // digit is constant skipped; every pass counts and scatters in PIECES fixed ranges in parallel
+    // (per-range digit offsets, range-major within a digit: the stable order of a serial pass)
     std::vector<int>& pperm = od.pperm;
     pperm.resize(P);
-    for (int p = 0; p < P; ++p) pperm[p] = p;
+    sfmx::parallel_ranges(P, PIECES, [&](int64_t p0, int64_t p1) {
+        for (int64_t p = p0; p < p1; ++p) pperm[p] = (int)p;
+    });
     {
         std::vector<int>& tmp = od.tmp;
         std::vector<uint64_t>& ktmp = od.ktmp;
-        std::vector<uint32_t>& cnt = od.cnt;
+        std::vector<uint32_t>& cnt = od.cnt;   // [PIECES][256]
         tmp.resize(P);
         ktmp.resize(P);
-        cnt.resize(65536 + 1);
-        for (int sh = 0; sh < nk * kb; sh += 16) {
-            std::fill(cnt.begin(), cnt.end(), 0u);
-            for (int i = 0; i < P; ++i) cnt[((key[i] >> sh) & 0xffff) + 1]++;
+        cnt.resize(PIECES * 256);
+        const int np = (int)std::max<int64_t>(1, std::min<int64_t>(PIECES, P));
+        auto lo = [&](int i) { return (int64_t)P * i / np; };
+        for (int sh = 0; sh < nk * kb; sh += 8) {
+            sfmx::parallel_items(np, [&](int i) {
+                uint32_t* c = cnt.data() + 256 * (size_t)i;
+                std::fill(c, c + 256, 0u);
+                for (int64_t q = lo(i); q < lo(i + 1); ++q) c[(key[q] >> sh) & 0xff]++;
+            });
+            uint32_t tot[256] = {};
+            for (int i = 0; i < np; ++i)
+                for (int d = 0; d < 256; ++d) tot[d] += cnt[256 * (size_t)i + d];
             bool one = false;
-            for (size_t d = 1; d < cnt.size(); ++d) one |= cnt[d] == (uint32_t)P;
+            for (int d = 0; d < 256; ++d) one |= tot[d] == (uint32_t)P;
             if (one) continue;
-            for (size_t d = 1; d < cnt.size(); ++d) cnt[d] += cnt[d - 1];
-            for (int i = 0; i < P; ++i) {
-                const uint32_t j = cnt[(key[i] >> sh) & 0xffff]++;
-                tmp[j] = pperm[i];
-                ktmp[j] = key[i];
-            }
+            uint32_t run = 0;   // exclusive offsets, digit-major, range-minor
+            for (int d = 0; d < 256; ++d)
+                for (int i = 0; i < np; ++i) {
+                    const uint32_t v = cnt[256 * (size_t)i + d];
+                    cnt[256 * (size_t)i + d] = run;
+                    run += v;
+                }
+            sfmx::parallel_items(np, [&](int i) {
+                uint32_t* c = cnt.data() + 256 * (size_t)i;
+                for (int64_t q = lo(i); q < lo(i + 1); ++q) {
+                    const uint32_t j = c[(key[q] >> sh) & 0xff]++;
+                    tmp[j] = pperm[q];
+                    ktmp[j] = key[q];
+                }
+            });
             pperm.swap(tmp);
             key.swap(ktmp);
         }
@@ -1017,7 +1055,7 @@ struct TopoSeg {
     void clear() { grp.clear(); chk.clear(); bat.clear(); gcam.clear(); lcrow.clear(); sg_total = h_total = 0; rg_total = 0; dp_max = 16; }
 };
 
-void topo_segment(int s0, int s1, int K, const std::vector<int>& pt_start, const int* obs_cam, short* obs_lc,
+void topo_segment(int s0, int s1, int K, int gpts, const std::vector<int>& pt_start, const int* obs_cam, short* obs_lc,
                   short* obs_row, TopoSeg& tp) {
     std::vector<int> cur, pc, uni, cnt, fill;
     tp.clear();
@@ -1102,7 +1140,7 @@ void topo_segment(int s0, int s1, int K, const std::vector<int>& pt_start, const
         }
         uni.clear();
         std::set_union(cur.begin(), cur.end(), pc.begin(), pc.end(), std::back_inserter(uni));
-        if (p > g_p0 && (g_obs + m > GOBS || p - g_p0 + 1 > GPTS || 6 * (int)uni.size() + K > GDPMAX)) {
+        if (p > g_p0 && (g_obs + m > GOBS || p - g_p0 + 1 > gpts || 6 * (int)uni.size() + K > GDPMAX)) {
             add_group(g_p0, p, cur, false);
             g_p0 = p; g_obs = 0; cur = pc;
         } else {
@@ -1117,7 +1155,29 @@ void topo_segment(int s0, int s1, int K, const std::vector<int>& pt_start, const
 // parallel (host_par.hpp), merged in segment order; then the camera slots and assembly tasks.
 constexpr int SEG_PTS = 8192;
 
-void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start, const int* obs_cam, Topology& tp) {
+// Points per group: the group kernels (ba_glin, ba_gschur, ba_gupdate) run one workgroup per group
+// and their workgroups take about the same time, so a launch costs ceil(groups / slots) rounds
+// (slots = workgroups resident at once, from the device's occupancy of ba_glin).  C5 with 128-point
+// groups is 1564 groups on 512 slots: a fourth round for 28 workgroups.  The cap is the smallest
+// group size that keeps the rounds of full-size groups (in fixed SEG_PTS segments, as built below):
+// there, 99 points -> 2027 groups in 4 full rounds.  Camera limits can still cut groups earlier.
+// Only problems of several rounds are re-sized, and never below GPTS / 2 points: a problem of one
+// round keeps full-size groups (the regime every small-problem parity test was pinned in).
+int group_points(int P, int slots) {
+    if (P <= 0 || slots <= 0) return GPTS;
+    auto groups = [P](int cap) {
+        int64_t g = 0;
+        for (int s0 = 0; s0 < P; s0 += SEG_PTS) g += (std::min(P - s0, SEG_PTS) + cap - 1) / cap;
+        return g;
+    };
+    const int64_t rounds = (groups(GPTS) + slots - 1) / slots;
+    if (rounds < 2) return GPTS;
+    for (int cap = std::max<int64_t>(GPTS / 2, P / (rounds * slots)); cap < GPTS; ++cap)
+        if (groups(cap) <= rounds * slots) return cap;
+    return GPTS;
+}
+
+void build_topology(int P, int C, int O, int K, int gpts, const std::vector<int>& pt_start, const int* obs_cam, Topology& tp) {
     tp.clear();
     tp.obs_lc.assign(O, 0);
     tp.obs_row.assign(O, 0);
@@ -1126,7 +1186,7 @@ void build_topology(int P, int C, int O, int K, const std::vector<int>& pt_start
     std::vector<TopoSeg>& seg = tp.seg ? *tp.seg : own;
     if ((int)seg.size() < nseg) seg.resize(nseg);
     sfmx::parallel_items(nseg, [&](int i) {
-        topo_segment(i * SEG_PTS, std::min(P, (i + 1) * SEG_PTS), K, pt_start, obs_cam, tp.obs_lc.data(),
+        topo_segment(i * SEG_PTS, std::min(P, (i + 1) * SEG_PTS), K, gpts, pt_start, obs_cam, tp.obs_lc.data(),
                      tp.obs_row.data(), seg[i]);
     });
     {   // merge: shift every segment's local offsets
@@ -1236,6 +1296,20 @@ struct HostScratch {
 };
 void destroy_scratch(HostScratch* h) { delete h; }
 
+// ba_glin workgroups resident at once on this device (its occupancy at the launch's LDS size times
+// the CUs); 0 when unknown (then full-size groups)
+int group_slots(sfmx_ba_ctx* c, int K) {
+    if (const char* e = SFMX_DIAG_ENV("SFMX_BA_SLOTS")) return std::atoi(e);   // A/B: 0 = full-size groups
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) return 0;
+    const size_t lds = sizeof(double) * ((size_t)GROWS * nfeat(K) + GCH * 8) + sizeof(short) * 2 * GCH;
+    const void* f = K == 1 ? (const void*)ba_glin<1, false> : K == 3 ? (const void*)ba_glin<3, false> : (const void*)ba_glin<7, false>;
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 256, lds) != hipSuccess || nb <= 0) return 0;
+    return nb * prop.multiProcessorCount;
+}
+
 int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     using clk = std::chrono::steady_clock;
     const auto t_start = clk::now();
@@ -1316,7 +1390,12 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     Topology& tp = c->hscr->tp;
     tp.seg = &c->hscr->seg;
     const auto t_topo = clk::now();
-    build_topology(P, C, O, K, pt_start, roc.data(), tp);
+    const int slots = group_slots(c, K), gpts = group_points(P, slots);
+    build_topology(P, C, O, K, gpts, pt_start, roc.data(), tp);
+#ifdef SFMX_DIAG
+    if (SFMX_DIAG_ENV("SFMX_BA_TRACE"))
+        fprintf(stderr, "sfmx ba: P %d slots %d points/group %d groups %zu dp_max %d\n", P, slots, gpts, tp.grp.size(), tp.dp_max);
+#endif
     c->setup_ms[6] = ms_since(t_topo);
     // local camera co-visibility (the pose blocks this rank's points create)
     c->adj.assign((size_t)C * C, 0);
@@ -1355,6 +1434,16 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     hipStream_t st = c->st;
     int rc;
     const auto t_up = clk::now();
+    {   // every staged upload of this call (256-B rounded parts): one arena, no mid-call waits
+        auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        const size_t total = r(16 * (size_t)O) + r(4 * (size_t)(P + 1)) + r(4 * (size_t)O) + 2 * r(2 * (size_t)O) +
+                             r(sizeof(Grp) * tp.grp.size()) + r(sizeof(Chunk) * tp.chk.size()) +
+                             r(sizeof(Batch) * tp.bat.size()) + r(4 * tp.gcam.size()) + r(4 * tp.lcrow.size()) +
+                             r(sizeof(ATask) * tp.tasks.size()) + r(sizeof(AEnt) * tp.ents.size()) +
+                             r(4 * tp.cref_start.size()) + r(4 * tp.cref.size()) + r(4 * pim_h.size()) +
+                             r(sizeof(double2) * pcc_h.size()) + r(24 * (size_t)P) + 4096;
+        RC(stage_reserve(c, total));
+    }
     // observed pixels: gathered into the internal order while they are copied into the pinned
     // staging arena (parallel host ranges, then one DMA; the caller's array is pageable)
     RC(c->obs_xy.alloc(sizeof(double) * 2 * std::max<size_t>(O, 1)));
@@ -1712,7 +1801,7 @@ int sfmx_ba_debug_host_setup(const sfmx_ba_problem* pb, double* ms) {
     auto t1 = clk::now();
     auto t2 = clk::now();
     Topology tp;
-    build_topology(pb->n_points, pb->n_cams, pb->n_obs, pb->n_intr ? 7 : pb->cam_model, od.pt_start, od.roc.data(), tp);
+    build_topology(pb->n_points, pb->n_cams, pb->n_obs, pb->n_intr ? 7 : pb->cam_model, GPTS, od.pt_start, od.roc.data(), tp);
     auto t3 = clk::now();
     auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     ms[0] = d(t0, t1); ms[1] = d(t1, t2); ms[2] = d(t2, t3);
