@@ -51,7 +51,9 @@ struct Plan {
     std::vector<uint32_t> vtx_view;       // sorted image ids
 };
 
-// OpenMvsUtils.cpp:72-133 (which shots become images, which points vertices)
+// OpenMvsUtils.cpp:72-133 (which shots become images, which points vertices).  A point's image ids
+// are kept sorted and unique as they arrive (insertion into a short run; the reference's std::set),
+// straight into the CSR, which is rolled back when fewer than two remain.
 static int plan(const sfmx_mvs_shot* shots, int32_t n_shots, int32_t n_cameras, int32_t n_points,
                 const int64_t* oo, const int32_t* osh, Plan& pl) {
     pl.image_of_shot.assign(n_shots, -1);
@@ -60,20 +62,28 @@ static int plan(const sfmx_mvs_shot* shots, int32_t n_shots, int32_t n_cameras, 
         pl.image_of_shot[s] = (int32_t)pl.image_shot.size();
         pl.image_shot.push_back(s);
     }
-    std::vector<uint32_t> views;
+    if (n_points > 0) {
+        pl.vtx_point.reserve(n_points);
+        pl.vtx_off.reserve((size_t)n_points + 1);
+        pl.vtx_view.reserve((size_t)std::max<int64_t>(oo[n_points] - oo[0], 0));
+    }
     for (int p = 0; p < n_points; ++p) {
-        views.clear();
         if (oo[p + 1] < oo[p]) { set_last_error("origin offsets not ascending"); return SFMX_EINVAL; }
+        const size_t b = pl.vtx_view.size();
         for (int64_t k = oo[p]; k < oo[p + 1]; ++k) {
             const int s = osh[k];
             if (s < 0 || s >= n_shots) { set_last_error("origin shot out of range"); return SFMX_EINVAL; }
-            if (pl.image_of_shot[s] >= 0) views.push_back((uint32_t)pl.image_of_shot[s]);   // :109-112
+            const int32_t id = pl.image_of_shot[s];
+            if (id < 0) continue;                                                       // :109-112
+            size_t e = pl.vtx_view.size(), i = e;                                       // :127-128
+            while (i > b && pl.vtx_view[i - 1] > (uint32_t)id) --i;
+            if (i > b && pl.vtx_view[i - 1] == (uint32_t)id) continue;                  // getOriginShots: std::set
+            pl.vtx_view.push_back(0);
+            for (; e > i; --e) pl.vtx_view[e] = pl.vtx_view[e - 1];
+            pl.vtx_view[i] = (uint32_t)id;
         }
-        std::sort(views.begin(), views.end());                                          // :127-128
-        views.erase(std::unique(views.begin(), views.end()), views.end());   // getOriginShots: std::set
-        if (views.size() < 2) continue;                                                 // :122-124
+        if (pl.vtx_view.size() - b < 2) { pl.vtx_view.resize(b); continue; }            // :122-124
         pl.vtx_point.push_back(p);
-        pl.vtx_view.insert(pl.vtx_view.end(), views.begin(), views.end());
         pl.vtx_off.push_back((int64_t)pl.vtx_view.size());
     }
     return SFMX_OK;
@@ -134,6 +144,26 @@ static void emit(Sink& o, uint32_t version, const sfmx_mvs_camera* cameras, int3
     }
     // vertices: Vertex{X (Point3f), views: View{imageID, confidence}}
     o.count(pl.vtx_point.size());
+    const int64_t vbytes = 20 * (int64_t)pl.vtx_point.size() + 8 * (int64_t)pl.vtx_view.size();
+    if (o.out && o.n + vbytes <= o.cap) {   // the section fits: written in place, element by element
+        uint8_t* w = o.out + o.n;
+        for (size_t v = 0; v < pl.vtx_point.size(); ++v) {
+            const double* X = points + 3 * pl.vtx_point[v];
+            const float Xf[3] = {(float)X[0], (float)X[1], (float)X[2]};
+            const uint64_t nview = (uint64_t)(pl.vtx_off[v + 1] - pl.vtx_off[v]);
+            std::memcpy(w, Xf, 12);
+            std::memcpy(w + 12, &nview, 8);
+            w += 20;
+            for (int64_t k = pl.vtx_off[v]; k < pl.vtx_off[v + 1]; ++k) {
+                const uint32_t id = pl.vtx_view[k];
+                const float conf = 0.0f;                 // confidence (:115-118)
+                std::memcpy(w, &id, 4);
+                std::memcpy(w + 4, &conf, 4);
+                w += 8;
+            }
+        }
+        o.n += vbytes;
+    } else
     for (size_t v = 0; v < pl.vtx_point.size(); ++v) {
         const double* X = points + 3 * pl.vtx_point[v];
         const float Xf[3] = {(float)X[0], (float)X[1], (float)X[2]};

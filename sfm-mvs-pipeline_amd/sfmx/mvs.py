@@ -97,22 +97,36 @@ def _scene_args(cameras, shots, points, origin_offsets, origin_shot):
                   oo.ctypes.data_as(C.POINTER(C.c_int64)), osh.ctypes.data_as(C.POINTER(C.c_int32)) if len(osh) else None)
 
 
+def _serialize_bound(cameras, shots, n_points: int, n_origins: int) -> int:
+    """An upper bound of the Interface size: every shot an image and a pose, every point a vertex
+    with all its origins as views (the native call reports the exact size)."""
+    names = sum(len(n.encode() if isinstance(n, str) else n) for (_, _, _, n) in shots)
+    return (64 + len(cameras) * (8 + 8 + 8 + 8 + 72 + 72 + 24 + 8) + len(shots) * (96 + 8 + 16) + names +
+            n_points * (12 + 8) + n_origins * 8 + 8 * 5 + 128)
+
+
 def serialize(cameras, shots, points, origin_offsets, origin_shot, version: int = 1):
     """openMVS Interface bytes as OpenMvsUtils::toOpenMVS would write them.
     cameras: [(width, height, K 3x3)]; shots: [(camera index or -1, recovered,
     pose 3x4 [R|t], image name)]; points n x 3; origins: CSR of origin shot
-    indices per point.  -> (bytes, n_images, n_vertices)"""
+    indices per point.  -> (bytes, n_images, n_vertices)
+    One native call into a buffer of the bound above (a second one only if that ever fell short)."""
     keep, args = _scene_args(cameras, shots, points, origin_offsets, origin_shot)
+    oo = keep[4]
     size = C.c_int64(0)
     ni, nv = C.c_int32(0), C.c_int32(0)
-    rc = lib.sfmx_openmvs_serialize(int(version), *args, None, 0, C.byref(size), C.byref(ni), C.byref(nv))
-    if rc not in (0, -4):
-        check(rc, "sfmx_openmvs_serialize")
-    buf = (C.c_uint8 * max(size.value, 1))()
-    check(lib.sfmx_openmvs_serialize(int(version), *args, buf, size.value, C.byref(size), C.byref(ni), C.byref(nv)),
-          "sfmx_openmvs_serialize")
+    cap = _serialize_bound(cameras, shots, len(keep[3]), int(oo[-1]) if len(oo) else 0)
+    for _ in range(2):
+        buf = bytearray(max(cap, 1))
+        cbuf = (C.c_uint8 * len(buf)).from_buffer(buf)
+        rc = lib.sfmx_openmvs_serialize(int(version), *args, cbuf, cap, C.byref(size), C.byref(ni), C.byref(nv))
+        del cbuf
+        if rc != -4:   # SFMX_ECAPACITY: size holds the exact size; go again with it
+            break
+        cap = size.value
+    check(rc, "sfmx_openmvs_serialize")
     del keep
-    return bytes(buf[:size.value]), ni.value, nv.value
+    return bytes(memoryview(buf)[:size.value]), ni.value, nv.value
 
 
 def toOpenMVS(cameras, shots, points, origin_offsets, origin_shot, path: str, filename: str = "mvs.bin",

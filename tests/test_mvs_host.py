@@ -144,3 +144,18 @@ def test_undistort_rejects_bad_input():
         sfmx.mvs.undistort([img], [K], [np.zeros(4)])
     with pytest.raises(ValueError, match="channels"):
         sfmx.mvs.undistort([np.zeros((10, 10, 5), np.uint8)], [np.eye(3)], [np.zeros(4)])
+
+
+def test_serialize_capacity_retry_and_errors(monkeypatch):
+    """The wrapper's one native call into a bound-sized buffer: a bound that falls short takes the
+    exact size from SFMX_ECAPACITY and calls again (same bytes); invalid origins still raise."""
+    import sfmx
+    cams, shots, pts, oo, osh = mvs_cases.interface_scene(seed=0)
+    want, ni, nv = sfmx.mvs.serialize(cams, shots, pts, oo, osh)
+    monkeypatch.setattr(sfmx.mvs, "_serialize_bound", lambda *a: 16)
+    got, ni2, nv2 = sfmx.mvs.serialize(cams, shots, pts, oo, osh)
+    assert got == want and (ni2, nv2) == (ni, nv)
+    bad = np.array(osh, np.int32).copy()
+    bad[0] = len(shots) + 5
+    with pytest.raises(Exception):
+        sfmx.mvs.serialize(cams, shots, pts, oo, bad)
