@@ -971,7 +971,6 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
         Chunk ch;
         if (Gp.big) { ch.o0 = Gp.o0 + c * GCH; ch.o1 = min(Gp.o1, ch.o0 + GCH); ch.q0 = 0; ch.q1 = 0; ch.lc0 = 0; ch.nrows = 2 * (ch.o1 - ch.o0); }
         else ch = chk[Gp.ch0 + c];
-        for (int e = tid; e < ch.nrows * NF; e += blockDim.x) G[e] = 0.0;   // padding rows stay zero
         // every global load of the chunk goes out before its record stores: a wait for a load issued
         // after the stores would wait for the stores too (vmcnt counts both, in order)
         const int a = tid, o = ch.o0 + a;
@@ -996,6 +995,13 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
             cr0[i] = cr1[i] = 0;
             if (!Gp.big && lc < Gp.u) { cr0[i] = lcrow[ch.lc0 + lc]; cr1[i] = lcrow[ch.lc0 + lc + 1]; }
         }
+        // a camera's rows are padded to a multiple of 4: 2 zero rows at its end when it has an odd
+        // number of observations in the chunk.  Its last 2 rows are zeroed before the barrier; real
+        // rows there are written after it.  Every other row the Gram and point sums read is written
+        // by an observation (big groups: 2 rows per observation, no padding).
+#pragma unroll
+        for (int i = 0; i < UMAX / 4; ++i)
+            if (cr1[i] > cr0[i] && l < 2 * NF) G[(cr1[i] - 2) * NF + l] = 0.0;
         if (o < ch.o1) {
             orow = Gp.big ? 2 * a : obs_row[o];
             olcv = obs_lc[o];

@@ -93,6 +93,7 @@ struct sfmx_ba_ctx {
     // caller's intr[isrc[j]] (the referenced blocks back to back, then zero padding up to K, -1);
     // per pose its block (pim = model | first column << 4) and principal point (pcc)
     bool multi = false;
+    bool loaded = false;            // a problem is loaded (false after a failed update: run / get / set refuse)
     int n_intr = 0, intr_len = 0;   // caller's blocks and the length of its intr array
     std::vector<int> isrc;
     Buf pim, pcc;
@@ -1284,6 +1285,124 @@ void build_topology(int P, int C, int O, int K, int gpts, const std::vector<int>
     }
 }
 
+// Every index the group kernels derive from the topology, checked against the limits and buffer
+// sizes they assume (ba_glin: GROWS feature rows, GCH observations, GPTS point threads, UMAX
+// cameras; ba_gschur: WB_OBS / WB_PTS batches, the lane map, dp <= GDPMAX; ba_gupdate: one thread
+// per point of a chunk; ba_assemble / ba_camred: entry and slot ranges inside sg / hbig / rg /
+// gpart).  Run by the diagnostic library on every load and by the CPU tests on random problems
+// (tests/test_ba_host.py); "" when everything holds, else the first violation.
+[[maybe_unused]] std::string check_topology(int P, int C, int O, int K, const std::vector<int>& pt_start, const int* obs_cam,
+                                            const Topology& tp) {
+    auto bad = [](const std::string& m) { return m; };
+    auto S = [](long long v) { return std::to_string(v); };
+    if ((int)pt_start.size() != P + 1 || pt_start[0] != 0 || pt_start[P] != O) return bad("pt_start does not span the observations");
+    if ((int)tp.obs_lc.size() != O || (int)tp.obs_row.size() != O) return bad("obs_lc / obs_row size");
+    int next_p = 0;
+    for (size_t g = 0; g < tp.grp.size(); ++g) {
+        const Grp& G = tp.grp[g];
+        const std::string at = "group " + S((long long)g) + ": ";
+        if (G.p0 != next_p || G.p1 <= G.p0 || G.p1 > P) return bad(at + "points not contiguous");
+        next_p = G.p1;
+        if (G.o0 != pt_start[G.p0] || G.o1 != pt_start[G.p1]) return bad(at + "observation range");
+        if (G.u < 0 || G.cam_off < 0 || G.cam_off + G.u > (int)tp.gcam.size()) return bad(at + "camera slots");
+        for (int lc = 0; lc < G.u; ++lc) {
+            const int cm = tp.gcam[G.cam_off + lc];
+            if (cm < 0 || cm >= C || (lc > 0 && tp.gcam[G.cam_off + lc - 1] >= cm)) return bad(at + "cameras not sorted / out of range");
+        }
+        const long long dim = 6LL * G.u + K;
+        if (G.rg_off < 0 || G.rg_off + dim > tp.rg_total) return bad(at + "rhs block outside rg");
+        for (int o = G.o0; o < G.o1; ++o) {
+            const int lc = tp.obs_lc[o];
+            if (lc < 0 || lc >= G.u || tp.gcam[G.cam_off + lc] != obs_cam[o]) return bad(at + "obs_lc of observation " + S(o));
+        }
+        if (G.big) {
+            if (G.p1 != G.p0 + 1) return bad(at + "big group of several points");
+            if (G.h_off < 0 || G.h_off + 3 * dim > tp.h_total) return bad(at + "H outside hbig");
+            continue;
+        }
+        if (G.p1 - G.p0 > GPTS || G.o1 - G.o0 > GOBS) return bad(at + "more points / observations than a workgroup holds");
+        if (G.u > UMAX || dim > GDPMAX) return bad(at + "camera union too wide for ba_gschur / ba_glin");
+        if (G.sg_off < 0 || G.sg_off + dim * dim > tp.sg_total) return bad(at + "block outside sg");
+        if (((dim + 15) & ~15) > tp.dp_max) return bad(at + "dp above the launch's dp_max");
+        // chunks: whole points in order, <= GCH observations, feature rows per camera
+        int q = G.p0;
+        if (G.nch < 1 || G.ch0 < 0 || G.ch0 + G.nch > (int)tp.chk.size()) return bad(at + "chunk range");
+        for (int c = 0; c < G.nch; ++c) {
+            const Chunk& ch = tp.chk[G.ch0 + c];
+            const std::string cat = at + "chunk " + S(c) + ": ";
+            if (ch.q0 != q - G.p0 || ch.q1 < ch.q0 || G.p0 + ch.q1 > G.p1) return bad(cat + "point slots");
+            if (ch.o0 != pt_start[G.p0 + ch.q0] || ch.o1 != pt_start[G.p0 + ch.q1]) return bad(cat + "observation range");
+            if (ch.o1 - ch.o0 > GCH || ch.q1 > GCH) return bad(cat + "more than GCH observations / point threads");
+            if (ch.lc0 < 0 || ch.lc0 + G.u + 1 > (int)tp.lcrow.size()) return bad(cat + "lcrow range");
+            if (tp.lcrow[ch.lc0] != 0 || tp.lcrow[ch.lc0 + G.u] != ch.nrows || ch.nrows > GROWS) return bad(cat + "feature rows");
+            std::vector<int> used(G.u, 0);
+            for (int lc = 0; lc < G.u; ++lc) {
+                const int r0 = tp.lcrow[ch.lc0 + lc], r1 = tp.lcrow[ch.lc0 + lc + 1];
+                if (r1 < r0 || ((r1 - r0) & 3)) return bad(cat + "camera rows not a multiple of 4");
+            }
+            for (int o = ch.o0; o < ch.o1; ++o) {
+                const int lc = tp.obs_lc[o], row = tp.obs_row[o];
+                const int r0 = tp.lcrow[ch.lc0 + lc], r1 = tp.lcrow[ch.lc0 + lc + 1];
+                if (row < r0 || row + 2 > r1 || ((row - r0) & 1)) return bad(cat + "feature row of observation " + S(o));
+                if (row - r0 != 2 * used[lc]) return bad(cat + "feature rows not in observation order");
+                ++used[lc];
+            }
+            for (int lc = 0; lc < G.u; ++lc) {
+                const int r0 = tp.lcrow[ch.lc0 + lc], r1 = tp.lcrow[ch.lc0 + lc + 1];
+                if (((2 * used[lc] + 3) & ~3) != r1 - r0) return bad(cat + "camera row padding");
+            }
+            q = G.p0 + ch.q1;
+        }
+        if (q != G.p1) return bad(at + "chunks do not cover the points");
+        // ba_gschur wave batches: whole points, <= WB_OBS observations, <= WB_PTS points
+        q = G.p0;
+        if (G.nb < 1 || G.b0 < 0 || G.b0 + G.nb > (int)tp.bat.size()) return bad(at + "batch range");
+        for (int b = 0; b < G.nb; ++b) {
+            const Batch& B = tp.bat[G.b0 + b];
+            if (B.p0 != q || B.p1 < B.p0 || B.p1 > G.p1 || B.p1 - B.p0 > WB_PTS) return bad(at + "batch points");
+            if (B.o0 != pt_start[B.p0] || B.o1 != pt_start[B.p1] || B.o1 - B.o0 > WB_OBS) return bad(at + "batch observations");
+            for (int p = B.p0; p < B.p1; ++p) {   // the lane map holds one lane per (point, camera)
+                char seen[UMAX] = {};
+                for (int o = pt_start[p]; o < pt_start[p + 1]; ++o) {
+                    if (seen[tp.obs_lc[o]]) return bad(at + "two observations of one point in one camera (not big)");
+                    seen[tp.obs_lc[o]] = 1;
+                }
+            }
+            q = B.p1;
+        }
+        if (q != G.p1) return bad(at + "batches do not cover the points");
+    }
+    if (next_p != P) return bad("groups do not cover the points");
+    // camera slot lists
+    if ((int)tp.cref_start.size() != C + 1 || tp.cref_start[C] != (int)tp.gcam.size() || (int)tp.cref.size() != (int)tp.gcam.size())
+        return bad("camera slot lists");
+    for (int cm = 0; cm < C; ++cm)
+        for (int e = tp.cref_start[cm]; e < tp.cref_start[cm + 1]; ++e)
+            if (tp.cref[e] < 0 || tp.cref[e] >= (int)tp.gcam.size() || tp.gcam[tp.cref[e]] != cm) return bad("slot of camera " + S(cm));
+    // assembly: every entry's reads inside its group's block
+    for (size_t t = 0; t < tp.tasks.size(); ++t) {
+        const ATask& T = tp.tasks[t];
+        if (T.l0 < 0 || T.l1 < T.l0 || T.l1 > (int)tp.ents.size()) return bad("task " + S((long long)t) + ": entry range");
+        if (T.type == 0 && (T.a < 0 || T.b < T.a || T.b >= C)) return bad("task " + S((long long)t) + ": pose pair");
+        if (T.type == 1 && (T.a < 0 || T.a >= C)) return bad("task " + S((long long)t) + ": camera");
+        if (T.type == 2 && (T.b < 0 || T.b >= K * K + K)) return bad("task " + S((long long)t) + ": intrinsics output");
+        if (T.type < 0 || T.type > 2) return bad("task type");
+        const int rows = T.type == 2 ? K : 6, cols = T.type == 0 ? 6 : K;
+        for (int e = T.l0; e < T.l1; ++e) {
+            const AEnt& E = tp.ents[e];
+            if (E.dim < K || (E.dim - K) % 6) return bad("entry " + S(e) + ": dim");
+            if (E.rg < 0 || E.rg + rows > tp.rg_total) return bad("entry " + S(e) + ": rhs outside rg");
+            if (E.big) {
+                if (E.b0 < 0 || E.b0 + 3LL * rows > tp.h_total || E.b1 < 0 || E.b1 + 3LL * cols > tp.h_total)
+                    return bad("entry " + S(e) + ": H rows outside hbig");
+            } else if (E.b0 < 0 || E.b0 + (long long)(rows - 1) * E.dim + cols > tp.sg_total) {
+                return bad("entry " + S(e) + ": block outside sg");
+            }
+        }
+    }
+    return "";
+}
+
 // Everything problem-dependent of a context: the locality order, the point groups, the device
 // copies of the topology and the state buffers (reused when they are large enough), the
 // parameters.  The factorization plan is kept when the camera co-visibility and the border are
@@ -1310,13 +1429,80 @@ int group_slots(sfmx_ba_ctx* c, int K) {
     return nb * prop.multiProcessorCount;
 }
 
+// The intrinsics border of a problem (no context state touched): one camera -> its block; several
+// cameras -> the blocks some POSE names (pose_intr), in block order, back to back.  Poses and cameras
+// are replicated on every rank of a point-sharded solve, so every rank derives the same border (K,
+// single / multi kernels, column layout) and the collectives agree in size and meaning (ADVICE r03:
+// a border from the rank's own observations could differ between ranks).  A camera only unobserved
+// poses name gets zero Jacobian columns (its step is 0); the reference's scenes have no such pose.
+struct IntrLayout {
+    int K = 0, intr_len = 0;
+    bool multi = false;
+    double cx = 0, cy = 0;
+    std::vector<int> isrc, pim;
+    std::vector<double2> pcc;
+};
+int intr_layout(const sfmx_ba_problem* pb, IntrLayout& L) {
+    const int C = pb->n_cams;
+    L = IntrLayout{};
+    L.cx = pb->cx; L.cy = pb->cy;
+    if (pb->n_intr == 0) {
+        L.K = L.intr_len = pb->cam_model;
+        for (int j = 0; j < L.K; ++j) L.isrc.push_back(j);
+        return SFMX_OK;
+    }
+    const int M = pb->n_intr;
+    std::vector<int> used(M, 0), first(M, -1), off(M + 1, 0);
+    for (int m = 0; m < M; ++m) off[m + 1] = off[m] + pb->intr_model[m];
+    L.intr_len = off[M];
+    for (int cm = 0; cm < C; ++cm) used[pb->pose_intr[cm]] = 1;
+    int kb = 0, nused = 0;
+    for (int m = 0; m < M; ++m)
+        if (used[m]) {
+            ++nused;
+            first[m] = kb;
+            for (int i = 0; i < pb->intr_model[m]; ++i) L.isrc.push_back(off[m] + i);
+            kb += pb->intr_model[m];
+        }
+    if (nused <= 1) {   // one referenced camera: the single-block kernels with its block and centre
+        const int m = (int)(std::find(used.begin(), used.end(), 1) - used.begin());
+        L.K = m < M ? pb->intr_model[m] : pb->intr_model[0];
+        if (m == M) for (int i = 0; i < L.K; ++i) L.isrc.push_back(i);
+        L.cx = pb->intr_center[2 * (m < M ? m : 0)];
+        L.cy = pb->intr_center[2 * (m < M ? m : 0) + 1];
+        return SFMX_OK;
+    }
+    if (kb > SFMX_BA_MAX_INTR)
+        return fail(SFMX_ECAPACITY, "the referenced cameras hold " + std::to_string(kb) +
+                                        " intrinsics parameters; at most SFMX_BA_MAX_INTR = 7 are supported");
+    L.multi = true;
+    L.K = kb <= 1 ? 1 : kb <= 3 ? 3 : 7;   // the kernels' border widths; padding columns stay 0
+    while ((int)L.isrc.size() < L.K) L.isrc.push_back(-1);
+    L.pim.assign(std::max(C, 1), 1);
+    L.pcc.assign(std::max(C, 1), double2{0.0, 0.0});
+    for (int cm = 0; cm < C; ++cm) {
+        const int m = pb->pose_intr[cm];
+        L.pim[cm] = pb->intr_model[m] | (first[m] << 4);
+        L.pcc[cm] = double2{pb->intr_center[2 * m], pb->intr_center[2 * m + 1]};
+    }
+    return SFMX_OK;
+}
+
+// every check that can refuse a problem runs before any context state changes; a failure
+// after that point (allocation, upload) leaves the context marked unloaded, and run / get / set
+// refuse it (SFMX_ESTATE) until an update succeeds.
 int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     using clk = std::chrono::steady_clock;
     const auto t_start = clk::now();
     auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
     DeviceGuard dg(c->device);
+    if (6 * (int64_t)caller->n_cams > MAX_NPAD)
+        return fail(SFMX_EINVAL, "too many cameras for the reduced camera system (6C > 16384)");
+    IntrLayout L;
+    RC(intr_layout(caller, L));
     if (!c->hscr) c->hscr = new (std::nothrow) HostScratch();
     if (!c->hscr) return fail(SFMX_ENOMEM, "host allocation");
+    c->loaded = false;
     Ordered& od = c->hscr->od;
     order_problem(caller, od);
     c->setup_ms[5] = ms_since(t_start);
@@ -1325,76 +1511,38 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     c->operm.swap(od.operm);
     auto bail = [](int rc) { return rc; };
     // per-problem state starts over
-    c->isrc.clear();
-    c->multi = false;
-    c->n_intr = 0;
     c->scaled = c->j_scaled = false;
     c->stage_off = 0;
     const int P = caller->n_points, C = caller->n_cams, O = caller->n_obs;
-    c->P = P; c->C = C; c->O = O; c->cx = caller->cx; c->cy = caller->cy;
-    std::vector<int> pim_h;
-    std::vector<double2> pcc_h;
-    if (caller->n_intr == 0) {
-        c->K = caller->cam_model;
-        c->intr_len = c->K;
-        for (int j = 0; j < c->K; ++j) c->isrc.push_back(j);
-    } else {
-        // several cameras: the blocks some residual references, in block order, back to back in
-        // the border (a camera no residual names is no parameter of the Ceres problem)
-        const int M = caller->n_intr;
-        c->n_intr = M;
-        std::vector<int> used(M, 0), first(M, -1), off(M + 1, 0), cam_used(C, 0);
-        for (int m = 0; m < M; ++m) off[m + 1] = off[m] + caller->intr_model[m];
-        c->intr_len = off[M];
-        for (int q = 0; q < O; ++q) cam_used[roc[q]] = 1;
-        for (int cm = 0; cm < C; ++cm) if (cam_used[cm]) used[caller->pose_intr[cm]] = 1;
-        int kb = 0, nused = 0;
-        for (int m = 0; m < M; ++m)
-            if (used[m]) {
-                ++nused;
-                first[m] = kb;
-                for (int i = 0; i < caller->intr_model[m]; ++i) c->isrc.push_back(off[m] + i);
-                kb += caller->intr_model[m];
-            }
-        if (nused <= 1) {   // one referenced camera: the single-block kernels with its block and centre
-            const int m = (int)(std::find(used.begin(), used.end(), 1) - used.begin());
-            c->K = m < M ? caller->intr_model[m] : caller->intr_model[0];
-            if (m == M) for (int i = 0; i < c->K; ++i) c->isrc.push_back(i);
-            c->cx = caller->intr_center[2 * (m < M ? m : 0)];
-            c->cy = caller->intr_center[2 * (m < M ? m : 0) + 1];
-        } else {
-            if (kb > SFMX_BA_MAX_INTR)
-                return bail(fail(SFMX_ECAPACITY, "the referenced cameras hold " + std::to_string(kb) +
-                                                     " intrinsics parameters; at most SFMX_BA_MAX_INTR = 7 are supported"));
-            c->multi = true;
-            c->K = kb <= 1 ? 1 : kb <= 3 ? 3 : 7;   // the kernels' border widths; padding columns stay 0
-            while ((int)c->isrc.size() < c->K) c->isrc.push_back(-1);
-            pim_h.assign(std::max(C, 1), 1);
-            pcc_h.assign(std::max(C, 1), double2{0.0, 0.0});
-            for (int cm = 0; cm < C; ++cm) {
-                const int m = caller->pose_intr[cm];
-                if (first[m] < 0) continue;   // a pose without observations: never evaluated
-                pim_h[cm] = caller->intr_model[m] | (first[m] << 4);
-                pcc_h[cm] = double2{caller->intr_center[2 * m], caller->intr_center[2 * m + 1]};
-            }
-        }
-    }
+    c->P = P; c->C = C; c->O = O;
+    c->K = L.K; c->intr_len = L.intr_len; c->multi = L.multi; c->cx = L.cx; c->cy = L.cy;
+    c->n_intr = caller->n_intr;
+    c->isrc.swap(L.isrc);
+    std::vector<int>& pim_h = L.pim;
+    std::vector<double2>& pcc_h = L.pcc;
     const int K = c->K;
     if (c->plan_K != K) c->planned = false;   // the border sizes S, W and the Schur terms
     c->ne = 3 * (int64_t)P;
     c->nf = 6 * C + K;
     c->n = c->ne + c->nf;
     c->RW = K + 1;
-    if (6 * (int64_t)C > MAX_NPAD) return bail(fail(SFMX_EINVAL, "too many cameras for the reduced camera system (6C > 16384)"));
     std::vector<int>& pt_start = od.pt_start;
     Topology& tp = c->hscr->tp;
     tp.seg = &c->hscr->seg;
     const auto t_topo = clk::now();
-    const int slots = group_slots(c, K), gpts = group_points(P, slots);
+    const int slots = group_slots(c, K);
+    int gpts = group_points(P, slots);
+#ifdef SFMX_DIAG
+    if (const char* e = SFMX_DIAG_ENV("SFMX_BA_GPTS")) gpts = std::max(1, std::min(GPTS, std::atoi(e)));   // tiny-group tests
+#endif
     build_topology(P, C, O, K, gpts, pt_start, roc.data(), tp);
 #ifdef SFMX_DIAG
     if (SFMX_DIAG_ENV("SFMX_BA_TRACE"))
         fprintf(stderr, "sfmx ba: P %d slots %d points/group %d groups %zu dp_max %d\n", P, slots, gpts, tp.grp.size(), tp.dp_max);
+    {   // the diagnostic library checks every topology it uploads
+        const std::string why = check_topology(P, C, O, K, pt_start, roc.data(), tp);
+        if (!why.empty()) return bail(fail(SFMX_EINTERNAL, "BA topology check: " + why));
+    }
 #endif
     c->setup_ms[6] = ms_since(t_topo);
     // local camera co-visibility (the pose blocks this rank's points create)
@@ -1496,6 +1644,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     c->setup_ms[2] = up_ms + ms_since(t_up2);
     c->setup_ms[3] = 0.0;
     c->setup_ms[4] = ms_since(t_start);
+    c->loaded = true;
     return SFMX_OK;
 }
 
@@ -1652,6 +1801,7 @@ int sfmx_ba_set_allreduce(sfmx_ba_ctx* c, sfmx_allreduce_fn fn, void* user) {
 
 int sfmx_ba_run(sfmx_ba_ctx* c, int32_t max_iterations, sfmx_ba_summary* summary, double* trace, int32_t trace_cap) {
     if (!c || !summary) return fail(SFMX_EINVAL, "null context/summary");
+    if (!c->loaded) return fail(SFMX_ESTATE, "no problem loaded (the last update failed)");
     int nt = 0;
     RC(run_lm(c, max_iterations, summary, trace, trace_cap, &nt));
     return nt;
@@ -1659,6 +1809,7 @@ int sfmx_ba_run(sfmx_ba_ctx* c, int32_t max_iterations, sfmx_ba_summary* summary
 
 int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
     if (!c || !pb) return fail(SFMX_EINVAL, "null context/problem");
+    if (!c->loaded) return fail(SFMX_ESTATE, "no problem loaded (the last update failed)");
     DeviceGuard dg(c->device);
     const double* x = c->x.as<double>();
     c->stage_off = 0;   // nothing staged is in flight: every upload was synchronised
@@ -1677,7 +1828,8 @@ int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
 
 int sfmx_ba_set(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
     if (!c || !pb) return fail(SFMX_EINVAL, "null context/problem");
-    if (pb->n_points != c->P || pb->n_cams != c->C || pb->n_intr != c->n_intr || (!c->multi && pb->cam_model != c->K))
+    if (!c->loaded) return fail(SFMX_ESTATE, "no problem loaded (the last update failed)");
+    if (pb->n_points != c->P || pb->n_cams != c->C || pb->n_intr != c->n_intr || (c->n_intr == 0 && pb->cam_model != c->K))
         return fail(SFMX_EINVAL, "topology mismatch");
     return set_params(c, pb);
 }
@@ -1790,21 +1942,19 @@ int sfmx_ba_jacobian(const sfmx_ba_problem* pb, int32_t device, double* r, doubl
 }
 
 #ifdef SFMX_DIAG
-// diagnostic build only: the host part of load_problem without a device (ordering, permutation,
-// point groups / chunks / batches / assembly tasks), ms = [order, permute, topology]
-int sfmx_ba_debug_host_setup(const sfmx_ba_problem* pb, double* ms) {
+// diagnostic build only, no device needed: the host part of load_problem (locality order, point
+// groups / chunks / batches / assembly tasks at `gpts` points per group, 0 = GPTS) and
+// check_topology on it.  -> number of groups, or SFMX_EINTERNAL with the violation as last error.
+int sfmx_ba_debug_check_topology(const sfmx_ba_problem* pb, int32_t gpts) {
     RC(validate(pb));
-    using clk = std::chrono::steady_clock;
-    auto t0 = clk::now();
     Ordered od;
     order_problem(pb, od);
-    auto t1 = clk::now();
-    auto t2 = clk::now();
     Topology tp;
-    build_topology(pb->n_points, pb->n_cams, pb->n_obs, pb->n_intr ? 7 : pb->cam_model, GPTS, od.pt_start, od.roc.data(), tp);
-    auto t3 = clk::now();
-    auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    ms[0] = d(t0, t1); ms[1] = d(t1, t2); ms[2] = d(t2, t3);
+    const int K = pb->n_intr ? 7 : pb->cam_model;
+    build_topology(pb->n_points, pb->n_cams, pb->n_obs, K, gpts > 0 ? std::min(gpts, GPTS) : GPTS, od.pt_start,
+                   od.roc.data(), tp);
+    const std::string why = check_topology(pb->n_points, pb->n_cams, pb->n_obs, K, od.pt_start, od.roc.data(), tp);
+    if (!why.empty()) return fail(SFMX_EINTERNAL, "BA topology check: " + why);
     return (int)tp.grp.size();
 }
 #endif

@@ -14,6 +14,8 @@
 #include <cstdint>
 #include <string>
 
+#include <hip/hip_runtime_api.h>
+
 namespace sfmx {
 
 constexpr int ROW_ALIGN = 512;       // = query rows per work item = 2 x key chunk (256)
@@ -50,6 +52,16 @@ struct PrepImg {           // one image of a batched prep launch
     int32_t rows, cols, rows_pad, _pad;
     int64_t row0;
 };
+
+// Overlapped two-pass matching (match_kernels.hip launch_two_pass_overlap): a batch of the work list,
+// and the matcher's extra streams / events.
+struct MatchBatch { int32_t w0, nw, p0, np; };   // work items [w0, w0 + nw), pair-order slots [p0, p0 + np)
+struct OverlapStreams {
+    hipStream_t sx, sp;                          // second screen stream, pass-2 stream
+    hipEvent_t start, sx_done, sp_done;          // after the qcount clear; the two joins
+    hipEvent_t* screen;                          // one per batch
+};
+constexpr int MATCH_BATCHES = 8;                 // product default (SFMX_MATCH_BATCHES in the diagnostic build)
 
 // Thread-local last-error text shared by every C-ABI entry point (sfmx_last_error).
 void set_last_error(const char* msg);

@@ -873,8 +873,8 @@ void sift_settle_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restr
                         const int32_t* __restrict__ qlist, const int32_t* __restrict__ qcount,
                         const unsigned long long* __restrict__ top2, int32_t* __restrict__ out_idx,
                         float* __restrict__ out_dist, int2* __restrict__ slow_list, int32_t* __restrict__ slow_count,
-                        double ratio) {
-    const int pi = blockIdx.x;
+                        double ratio, const int32_t* __restrict__ porder = nullptr) {
+    const int pi = porder ? porder[blockIdx.x] : (int)blockIdx.x;   // porder: one batch's pairs (overlapped pass 2)
     const int cnt = qcount[pi];
     if (cnt == 0) return;
     const PairDev P = pairs[pi];
@@ -1695,8 +1695,8 @@ __global__ __launch_bounds__(256)
 void orb_settle_kernel(const PairDev* __restrict__ pairs, const ImgDev* __restrict__ imgs,
                        const int32_t* __restrict__ qlist, const int32_t* __restrict__ qcount,
                        const unsigned long long* __restrict__ top2, int32_t* __restrict__ out_idx,
-                       float* __restrict__ out_dist, double ratio) {
-    const int pi = blockIdx.x;
+                       float* __restrict__ out_dist, double ratio, const int32_t* __restrict__ porder = nullptr) {
+    const int pi = porder ? porder[blockIdx.x] : (int)blockIdx.x;   // porder: one batch's pairs (overlapped pass 2)
     const int cnt = qcount[pi];
     if (cnt == 0) return;
     const PairDev P = pairs[pi];
@@ -1935,6 +1935,10 @@ int sift_variant() {
     const char* e = SFMX_DIAG_ENV("SFMX_SIFT_VARIANT");
     return e ? atoi(e) : 0;
 }
+int match_batches() {   // overlapped two-pass batches (1: one screen launch, then pass 2)
+    const char* e = SFMX_DIAG_ENV("SFMX_MATCH_BATCHES");
+    return e ? std::max(1, std::min(64, atoi(e))) : MATCH_BATCHES;
+}
 int pass2_variant() {   // 10 = subset pass 2 (default), else the full-row GATHER pass 2
     const char* e = SFMX_DIAG_ENV("SFMX_SIFT_P2");   // with that item size (0 / 2 = 128 queries)
     return e ? atoi(e) : 10;
@@ -2041,6 +2045,60 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
     return hipGetLastError();
 #endif   // SFMX_DIAG
 }
+// Pass 2 overlapped with pass 1 (product SIFT / ORB paths).  One screen launch
+// leaves its last partial round of workgroups idle and pass 2 (subset + settle) waits behind it.
+// Here the work list (pairs in train-image order, each pair's items contiguous) is cut into batches
+// at pair boundaries; the screens of consecutive batches alternate between the caller's stream and a
+// second one, so one batch's tail overlaps the next batch's workgroups, and each batch's pass 2 runs
+// on a third stream behind an event on its screen, beside the later screens (its latency-bound
+// staging fills MFMA idle time).  Batches touch disjoint pairs (dense rows, qlist, qcount, top2); the
+// slow list is appended atomically.  Dependencies are events only: no in-kernel waits.  The caller's
+// stream ends after every batch (ev_screen: after the last screen; the join before returning).
+hipError_t launch_two_pass_overlap(bool sift, const MatchBatch* b, int nb, const WorkItem* work, const PairDev* pairs,
+                                   const ImgDev* imgs, const int8_t* desc, const int32_t* norm, const int32_t* keyc,
+                                   int32_t* qlist, int32_t* qcount, int n_pairs, const int32_t* porder, int32_t* out_idx,
+                                   float* out_dist, int2* slow_list, int32_t* slow_count, double ratio, hipStream_t st,
+                                   hipEvent_t ev_screen, int32_t* qmask, unsigned long long* top2,
+                                   const OverlapStreams& os) {
+    hipError_t e;
+#define OCHK(x) do { if ((e = (x)) != hipSuccess) return e; } while (0)
+    OCHK(hipMemsetAsync(qcount, 0, sizeof(int32_t) * n_pairs, st));
+    OCHK(hipEventRecord(os.start, st));
+    OCHK(hipStreamWaitEvent(os.sx, os.start, 0));
+    OCHK(hipStreamWaitEvent(os.sp, os.start, 0));
+    for (int i = 0; i < nb; ++i) {
+        const MatchBatch& B = b[i];
+        hipStream_t s = (i & 1) ? os.sx : st;
+        if (sift)
+            sift_screen16_kernel<8, 4, 2, 64, true><<<B.nw, 256, 0, s>>>(work + B.w0, pairs, imgs, desc, norm, keyc,
+                                                                         out_idx, out_dist, qlist, qcount, ratio, qmask, top2);
+        else
+            orb_screen16_kernel<8, 4, 2, 64, true><<<B.nw, 256, 0, s>>>(work + B.w0, pairs, imgs, (const uint8_t*)desc, keyc,
+                                                                        out_idx, out_dist, qlist, qcount, ratio, qmask, top2);
+        OCHK(hipGetLastError());
+        OCHK(hipEventRecord(os.screen[i], s));
+        OCHK(hipStreamWaitEvent(os.sp, os.screen[i], 0));
+        if (sift) {
+            sift_subset_kernel<4><<<B.np * 16, 256, 0, os.sp>>>(pairs, imgs, desc, norm, qlist, qmask, qcount, porder + B.p0, top2);
+            sift_settle_kernel<<<B.np, 256, 0, os.sp>>>(pairs, imgs, qlist, qcount, top2, out_idx, out_dist, slow_list,
+                                                        slow_count, ratio, porder + B.p0);
+        } else {
+            orb_subset_kernel<4, 2><<<B.np * 16, 256, 0, os.sp>>>(pairs, imgs, (const uint8_t*)desc, qlist, qmask, qcount,
+                                                                  porder + B.p0, top2);
+            orb_settle_kernel<<<B.np, 256, 0, os.sp>>>(pairs, imgs, qlist, qcount, top2, out_idx, out_dist, ratio,
+                                                       porder + B.p0);
+        }
+        OCHK(hipGetLastError());
+    }
+    OCHK(hipEventRecord(os.sx_done, os.sx));
+    OCHK(hipStreamWaitEvent(st, os.sx_done, 0));
+    if (ev_screen) OCHK(hipEventRecord(ev_screen, st));   // every screen done (pass-1 / pass-2 split, approximate)
+    OCHK(hipEventRecord(os.sp_done, os.sp));
+    OCHK(hipStreamWaitEvent(st, os.sp_done, 0));
+#undef OCHK
+    return hipSuccess;
+}
+
 hipError_t launch_sift_slow(const int2* slow_list, const int32_t* slow_count, const PairDev* pairs,
                             const ImgDev* imgs, const int8_t* desc8, const int32_t* norm, int32_t* out_idx,
                             float* out_dist, double ratio, hipStream_t st) {

@@ -50,6 +50,12 @@ hipError_t launch_orb_mfma(const WorkItem*, int, const PairDev*, const ImgDev*, 
                            int32_t*, int32_t*, int, const int32_t*, WorkItem*, int32_t*, int32_t*, float*, double,
                            hipStream_t, hipEvent_t, int32_t*, unsigned long long*);
 int orb_variant();
+int match_batches();
+int pass2_variant();
+hipError_t launch_two_pass_overlap(bool, const MatchBatch*, int, const WorkItem*, const PairDev*, const ImgDev*,
+                                   const int8_t*, const int32_t*, const int32_t*, int32_t*, int32_t*, int, const int32_t*,
+                                   int32_t*, float*, int2*, int32_t*, double, hipStream_t, hipEvent_t, int32_t*,
+                                   unsigned long long*, const OverlapStreams&);
 hipError_t launch_selftest_sqrt(int64_t, uint32_t*, hipStream_t);
 int sift_variant();
 int sift_block_queries(int variant);
@@ -177,6 +183,12 @@ struct sfmx_matcher {
     bool has_run = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // run start, main kernel end, run end, pass-1 end
     bool ev_recorded = false;
+    // overlapped two-pass matching (launch_two_pass_overlap): the plan's batches, two more streams
+    std::vector<MatchBatch> batches;
+    int plan_nb = 0;
+    hipStream_t sx = nullptr, sp = nullptr;
+    hipEvent_t ov_ev[3] = {nullptr, nullptr, nullptr};
+    std::vector<hipEvent_t> bev;
 };
 
 namespace {
@@ -342,7 +354,8 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     const int variant_key = m->norm == SFMX_NORM_L2 ? sift_variant() : 0;
     std::vector<int64_t> img_key(2 * (size_t)m->n_imgs);
     for (int i = 0; i < m->n_imgs; ++i) { img_key[2 * i] = m->imgs[i].rows; img_key[2 * i + 1] = m->imgs[i].integral; }
-    const bool reuse = m->plan_valid && m->plan_variant == variant_key && m->plan_imgs == img_key &&
+    const int nb_want = match_batches();
+    const bool reuse = m->plan_valid && m->plan_variant == variant_key && m->plan_imgs == img_key && m->plan_nb == nb_want &&
                        m->plan_pairs.size() == 2 * (size_t)n_pairs &&
                        (n_pairs == 0 || std::memcmp(m->plan_pairs.data(), pairs, sizeof(int32_t) * 2 * n_pairs) == 0);
     int rc;
@@ -408,6 +421,28 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
         if (!work.empty()) HIPCHK(hipMemcpyAsync(m->work_d.p, hs + b_pd + b_or, sizeof(WorkItem) * work.size(), hipMemcpyHostToDevice, st));
         if (!work32.empty()) HIPCHK(hipMemcpyAsync(m->work32_d.p, hs + b_pd + b_or + b_w, b_w32, hipMemcpyHostToDevice, st));
         if ((rc = m->stage_run.copied(st))) return rc;
+        {   // batches of the overlapped two-pass path: whole pairs in `order`, about n_work / nb items each
+            m->batches.clear();
+            const int64_t per = ((int64_t)work.size() + nb_want - 1) / std::max(nb_want, 1);
+            MatchBatch cur{0, 0, 0, 0};
+            size_t w = 0;
+            for (int i = 0; i < n_pairs; ++i) {
+                const int p = order[i];
+                const bool f32path = m->norm == SFMX_NORM_L2 && !(m->imgs[pd[p].left].integral && m->imgs[pd[p].right].integral);
+                int items = 0;
+                while (!f32path && w + items < work.size() && work[w + items].pair == p) ++items;
+                cur.nw += items;
+                cur.np += 1;
+                w += items;
+                if (cur.nw >= per && i + 1 < n_pairs) {
+                    m->batches.push_back(cur);
+                    cur = MatchBatch{(int32_t)w, 0, i + 1, 0};
+                }
+            }
+            if (cur.np > 0) m->batches.push_back(cur);
+            if (w != work.size()) return fail(SFMX_EINTERNAL, "match batches do not cover the work list");
+        }
+        m->plan_nb = nb_want;
         m->plan_pairs.assign(pairs, pairs + 2 * (size_t)n_pairs);
         m->plan_imgs = img_key;
         m->plan_variant = variant_key;
@@ -429,7 +464,42 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     // right image are handled in-kernel (every query: no neighbour).
     const PairDev* P = m->pairs_d.as<PairDev>();
     const ImgDev* I = m->imgs_d.as<ImgDev>();
-    if (m->norm == SFMX_NORM_L2) {
+    // overlapped two-pass product path (SIFT: the default screen + subset pass 2; ORB: FP4 screen + subset)
+    const bool overlap = m->batches.size() >= 2 && n_work > 0 &&
+                         ((m->norm == SFMX_NORM_L2 && sift_variant() == 0 && pass2_variant() == 10) ||
+                          (m->norm != SFMX_NORM_L2 && m->orb_fp4 && orb_variant() == 0));
+    OverlapStreams os{};
+    if (overlap) {
+        if (!m->sx) {
+            HIPCHK(hipStreamCreateWithFlags(&m->sx, hipStreamNonBlocking));
+            HIPCHK(hipStreamCreateWithFlags(&m->sp, hipStreamNonBlocking));
+            for (auto& e : m->ov_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        while (m->bev.size() < m->batches.size()) {
+            hipEvent_t e = nullptr;
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            m->bev.push_back(e);
+        }
+        os = OverlapStreams{m->sx, m->sp, m->ov_ev[0], m->ov_ev[1], m->ov_ev[2], m->bev.data()};
+    }
+    if (overlap) {
+        const bool sift = m->norm == SFMX_NORM_L2;
+        HIPCHK(launch_two_pass_overlap(sift, m->batches.data(), (int)m->batches.size(), m->work_d.as<WorkItem>(), P, I,
+                                       m->desc8.as<int8_t>(), sift ? m->normv.as<int32_t>() : nullptr,
+                                       sift ? m->keyc2.as<int32_t>() : m->keyc.as<int32_t>(), m->qlist.as<int32_t>(),
+                                       m->qcount.as<int32_t>(), n_pairs, m->porder.as<int32_t>(),
+                                       m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), m->slow_list.as<int2>(),
+                                       m->slow_count.as<int32_t>(), ratio, st, m->ev[3], m->qmask.as<int32_t>(),
+                                       m->top2.as<unsigned long long>(), os));
+        HIPCHK(hipEventRecord(m->ev[1], st));
+        if (sift) {
+            HIPCHK(launch_sift_slow(m->slow_list.as<int2>(), m->slow_count.as<int32_t>(), P, I, m->desc8.as<int8_t>(),
+                                    m->normv.as<int32_t>(), m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
+            if (n_work32)
+                HIPCHK(launch_sift_f32(m->work32_d.as<WorkItem>(), (int)n_work32, P, I, m->f32.as<float>(),
+                                       m->dense_idx.as<int32_t>(), m->dense_dist.as<float>(), ratio, st));
+        }
+    } else if (m->norm == SFMX_NORM_L2) {
         HIPCHK(launch_sift_knn2(m->work_d.as<WorkItem>(), (int)n_work, P, I, m->desc8.as<int8_t>(),
                                 m->normv.as<int32_t>(), m->keyc.as<int32_t>(), m->keyc2.as<int32_t>(),
                                 m->qlist.as<int32_t>(), m->qcount.as<int32_t>(), n_pairs, m->porder.as<int32_t>(),
@@ -550,6 +620,10 @@ int sfmx_matcher_destroy(sfmx_matcher* m) {
                           &m->unsettled, &m->counts, &m->keep, &m->offsets, &m->out};
         for (DevBuf* b : bufs) b->release();
         for (auto& e : m->ev) if (e) (void)hipEventDestroy(e);
+        for (auto& e : m->ov_ev) if (e) (void)hipEventDestroy(e);
+        for (auto& e : m->bev) if (e) (void)hipEventDestroy(e);
+        if (m->sx) (void)hipStreamDestroy(m->sx);
+        if (m->sp) (void)hipStreamDestroy(m->sp);
     }
     delete m;
     return SFMX_OK;

@@ -13,16 +13,17 @@
 //                         tiles + 3-pixel halo staged in LDS)
 //   orb_nms_kernel        3x3 strict maximum + the 31-pixel border test, ordered
 //                         (raster) compaction per row, two passes around a row scan
-//   host                  retainBest(2 n_l) per level (std::nth_element + partition on
-//                         the FAST scores, exactly the reference's libstdc++ calls)
+//   orb_retain_kernel     retainBest(2 n_l) per level on the FAST scores: the permutation of
+//                         the reference's libstdc++ nth_element + partition, in parallel
 //   orb_harris_kernel     Harris response (7x7 block, k = 0.04) per kept corner
-//   host                  retainBest(n_l) per level on the Harris responses
-//   orb_angle_kernel      intensity-centroid angle, one wavefront per keypoint
-//   host                  compute()'s runByImageBorder(31) at full resolution
+//   orb_retain_kernel     retainBest(n_l) per level on the Harris responses
+//   orb_angle_kernel      intensity-centroid angle, one wavefront per keypoint, and
+//                         compute()'s runByImageBorder(31) test at full resolution
+//   orb_compact_kernel    the in-border keypoints in order, their count
 //   orb_blur_kernel       7x7 integer Gaussian of the levels the keypoints use (LDS tile)
 //   orb_brief_kernel      rBRIEF, 32 lanes per keypoint, one descriptor byte per lane
-// The host steps sort a few bytes per corner; everything that touches pixels runs
-// on the device.  Roofline: HBM-bound byte work.
+// One host wait per image (the keypoint count at the end; r02 waited 4 times and ran both
+// retainBest steps on the host).  Roofline: HBM-bound byte work.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -193,7 +194,7 @@ __device__ __forceinline__ int find_level(const Lvl* lv, int nl, int row) {
 __global__ __launch_bounds__(256)
 void orb_nms_kernel(const uint8_t* __restrict__ score, const Lvl* __restrict__ lv, int nl, int border, int pass,
                     int* __restrict__ row_count, const int* __restrict__ row_off, int32_t* __restrict__ cpos,
-                    uint8_t* __restrict__ cscore) {
+                    uint8_t* __restrict__ cscore, int cap) {
     __shared__ int wsum[4];
     const int row = blockIdx.x;
     const int l = find_level(lv, nl, row);
@@ -228,8 +229,10 @@ void orb_nms_kernel(const uint8_t* __restrict__ score, const Lvl* __restrict__ l
         }
         if (pass && keep) {
             const int k = base + total + before + __popcll(m & ((1ull << lane) - 1));
-            cpos[k] = (y << 16) | x;
-            cscore[k] = sc;
+            if (k < cap) {   // (always: one strict maximum per 2 x 2 cell at most; the host checks the total)
+                cpos[k] = (y << 16) | x;
+                cscore[k] = sc;
+            }
         }
         total += chunk;
         __syncthreads();
@@ -261,34 +264,261 @@ void orb_scan_kernel(const int* __restrict__ cnt, int n, int* __restrict__ off) 
     if (threadIdx.x == 1023) off[n] = part[1023];
 }
 
-// ------------------------------------------------------------------ Harris / angle
-struct Kept { int32_t cand; int32_t level; };
+// ------------------------------------------------------------------ device retainBest
+// KeyPointsFilter::retainBest (std::nth_element + std::partition with libstdc++'s algorithms) on
+// (response, payload) records, one 1024-thread workgroup per pyramid level, giving the permutation
+// the reference's host call gives (tests/cpp/orb_select_sim.cpp checks the formulation against
+// libstdc++ itself, tests/test_gpu_orb.py the kernels against the oracle):
+//  * __introselect's loop, median-of-3 pivot, final insertion sort and __heap_select fallback run as
+//    libstdc++ writes them (the serial pieces on thread 0);
+//  * __unguarded_partition (comp = response greater) in parallel: its left scan stops at the
+//    positions with response <= P (Ls, ascending), its right scan at response >= P (Rs, from the
+//    right); the k-th stops are swapped while Ls[k] < Rs[k] (K pairs: Ls rises, Rs falls), every
+//    stop is at an original position (swapped ones lie behind both scans), and the cut is
+//    min(Ls[K + 1], Rs[K]);
+//  * the bidirectional std::partition (pred = response >= the boundary response) the same way.
+// Positions are found by per-thread contiguous chunks and one block scan; Ls / Rs live in scratch.
+struct Resp { float response; int32_t idx; };
+constexpr int RT = 1024;                      // threads of a selection workgroup
+struct SelCounts { int n[MAX_LEVELS]; };      // the retainBest argument per level
 
+__device__ __forceinline__ void wg_sync() { __threadfence_block(); __syncthreads(); }
+
+// exclusive block scan of (a, b) over RT threads; the totals land in sh[32], sh[33] (sh: 36 ints)
+__device__ __forceinline__ void scan2(int& a, int& b, int* sh) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int ia = a, ib = b;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int xa = __shfl_up(ia, o), xb = __shfl_up(ib, o);
+        if (lane >= o) { ia += xa; ib += xb; }
+    }
+    __syncthreads();   // sh may still be read by a previous step
+    if (lane == 63) { sh[w] = ia; sh[16 + w] = ib; }
+    __syncthreads();
+    if (t == 0) {
+        int sa = 0, sb = 0;
+        for (int i = 0; i < RT / 64; ++i) {
+            const int va = sh[i], vb = sh[16 + i];
+            sh[i] = sa; sh[16 + i] = sb;
+            sa += va; sb += vb;
+        }
+        sh[32] = sa; sh[33] = sb;
+    }
+    __syncthreads();
+    a = sh[w] + ia - a;
+    b = sh[16 + w] + ib - b;
+}
+__device__ __forceinline__ int block_sum_i(int v, int* sh) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    __syncthreads();
+    if ((t & 63) == 0) sh[t >> 6] = v;
+    __syncthreads();
+    int s = 0;
+    for (int i = 0; i < RT / 64; ++i) s += sh[i];
+    return s;
+}
+
+// The pairing of two scans over [f, l): left stops where lstop(response), right stops where
+// rstop(response).  Swaps the K pairs; returns K, with nL / nR and the stop lists in Ls / Rs.
+template <class LS, class RS>
+__device__ int wg_pair_swap(Resp* __restrict__ a, int f, int l, LS lstop, RS rstop, int* __restrict__ Ls,
+                            int* __restrict__ Rs, int* sh, int& nL, int& nR) {
+    const int t = threadIdx.x, n = l - f, chunk = (n + RT - 1) / RT;
+    const int s = min(f + t * chunk, l), e = min(s + chunk, l);
+    int cL = 0, cR = 0;
+    for (int p = s; p < e; ++p) {
+        const float v = a[p].response;
+        cL += lstop(v);
+        cR += rstop(v);
+    }
+    scan2(cL, cR, sh);
+    nL = sh[32];
+    nR = sh[33];
+    for (int p = s; p < e; ++p) {
+        const float v = a[p].response;
+        if (lstop(v)) Ls[cL++] = p;
+        if (rstop(v)) Rs[cR++] = p;
+    }
+    wg_sync();
+    const int kmax = min(nL, nR);
+    int c = 0;
+    for (int k = t; k < kmax; k += RT) c += Ls[k] < Rs[nR - 1 - k];
+    const int K = block_sum_i(c, sh);
+    for (int k = t; k < K; k += RT) {
+        const int pl = Ls[k], pr = Rs[nR - 1 - k];
+        const Resp x = a[pl], y = a[pr];
+        a[pl] = y;
+        a[pr] = x;
+    }
+    wg_sync();
+    return K;
+}
+
+__device__ __forceinline__ bool resp_gt(const Resp& x, const Resp& y) { return x.response > y.response; }
+
+// libstdc++ stl_heap.h, thread 0 only (the depth-limit fallback of __introselect)
+__device__ void heap_adjust(Resp* v, int hole, int len, Resp value) {
+    const int top = hole;
+    int second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (resp_gt(v[second], v[second - 1])) second--;
+        v[hole] = v[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        v[hole] = v[second - 1];
+        hole = second - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && resp_gt(v[parent], value)) {
+        v[hole] = v[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    v[hole] = value;
+}
+__device__ void heap_select(Resp* v, int middle, int last) {   // on [0, last), heap [0, middle)
+    if (middle >= 2)
+        for (int parent = (middle - 2) / 2;; --parent) {
+            heap_adjust(v, parent, middle, v[parent]);
+            if (parent == 0) break;
+        }
+    for (int i = middle; i < last; ++i)
+        if (resp_gt(v[i], v[0])) {
+            const Resp value = v[i];
+            v[i] = v[0];
+            heap_adjust(v, 0, middle, value);
+        }
+}
+__device__ __forceinline__ void swap_r(Resp* v, int i, int j) { const Resp x = v[i]; v[i] = v[j]; v[j] = x; }
+
+// retainBest(n) on a[0, m): the kept count; a[0, count) holds the kept records in the order the
+// reference's KeyPoint vector has them
+__device__ int wg_retain(Resp* __restrict__ a, int m, int n, int* __restrict__ Ls, int* __restrict__ Rs, int* sh,
+                         int* __restrict__ err) {
+    const int t = threadIdx.x;
+    if (m <= n) return m;
+    if (n == 0) return 0;
+    const int nth = n - 1;
+    int first = 0, last = m, depth = 2 * (31 - __clz(m));
+    bool heaped = false;
+    while (last - first > 3) {
+        if (depth == 0) {
+            if (t == 0) {
+                heap_select(a + first, nth + 1 - first, last - first);
+                swap_r(a, first, nth);
+            }
+            wg_sync();
+            heaped = true;
+            break;
+        }
+        --depth;
+        if (t == 0) {   // __move_median_to_first(first, first + 1, mid, last - 1)
+            const int x = first + 1, y = first + (last - first) / 2, z = last - 1;
+            int pick;
+            if (resp_gt(a[x], a[y])) pick = resp_gt(a[y], a[z]) ? y : resp_gt(a[x], a[z]) ? z : x;
+            else pick = resp_gt(a[x], a[z]) ? x : resp_gt(a[y], a[z]) ? z : y;
+            swap_r(a, first, pick);
+        }
+        wg_sync();
+        const float P = a[first].response;
+        int nL, nR;
+        const int K = wg_pair_swap(a, first + 1, last, [P](float v) { return v <= P; }, [P](float v) { return v >= P; },
+                                   Ls, Rs, sh, nL, nR);
+        int cut = INT_MAX;
+        if (K < nL) cut = Ls[K];
+        if (K >= 1) cut = min(cut, Rs[nR - K]);
+        if (cut <= first || cut >= last) {   // impossible for the pairing above; never loop on it
+            if (t == 0) atomicOr(err, 1);
+            heaped = true;
+            break;
+        }
+        if (cut <= nth) first = cut;
+        else last = cut;
+    }
+    if (!heaped) {
+        if (t == 0)   // __insertion_sort(first, last)
+            for (int i = first + 1; i < last; ++i) {
+                const Resp val = a[i];
+                if (resp_gt(val, a[first])) {
+                    for (int j = i; j > first; --j) a[j] = a[j - 1];
+                    a[first] = val;
+                } else {
+                    int j = i;
+                    while (resp_gt(val, a[j - 1])) { a[j] = a[j - 1]; --j; }
+                    a[j] = val;
+                }
+            }
+        wg_sync();
+    }
+    const float amb = a[nth].response;
+    int nL, nR;
+    wg_pair_swap(a, n, m, [amb](float v) { return v < amb; }, [amb](float v) { return v >= amb; }, Ls, Rs, sh, nL, nR);
+    return n + nR;
+}
+
+__device__ __forceinline__ int lvl_first(const int* __restrict__ row_off, const Lvl& L) { return row_off[L.row0]; }
+
+// mode 0: level l's FAST corners (raster order) -> retainBest(2 n_l) -> cnt[l] records in A (payload:
+// the corner index); mode 1: the kept corners' Harris responses in B (payload: the position in the
+// level's kept list) -> retainBest(n_l) -> cnt[l]
+__global__ __launch_bounds__(RT)
+void orb_retain_kernel(int mode, const Lvl* __restrict__ lv, const int* __restrict__ row_off,
+                       const uint8_t* __restrict__ cscore, Resp* __restrict__ A, Resp* __restrict__ B,
+                       int* __restrict__ Ls, int* __restrict__ Rs, const int* __restrict__ cnt_in,
+                       int* __restrict__ cnt_out, SelCounts sel, int cap, int* __restrict__ err) {
+    __shared__ int sh[36];
+    const int l = blockIdx.x, t = threadIdx.x;
+    const Lvl L = lv[l];
+    const int c0 = min(lvl_first(row_off, L), cap);   // (the corner count never exceeds cap: one per 2 x 2 cell)
+    int m;
+    Resp* a;
+    if (mode == 0) {
+        m = min(row_off[L.row0 + L.h], cap) - c0;
+        a = A + c0;
+        for (int j = t; j < m; j += RT) a[j] = Resp{(float)cscore[c0 + j], c0 + j};
+        wg_sync();
+    } else {
+        m = cnt_in[l];
+        a = B + c0;
+    }
+    const int k = wg_retain(a, m, sel.n[l], Ls + c0, Rs + c0, sh, err);
+    if (t == 0) cnt_out[l] = k;
+}
+
+// Harris response (7x7 block, k = 0.04) of every kept corner: grid (x, level)
 __global__ __launch_bounds__(256)
-void orb_harris_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const Kept* __restrict__ kept,
-                       int n, const int32_t* __restrict__ cpos, float* __restrict__ resp) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const Kept k = kept[i];
-    const Lvl L = lv[k.level];
-    const int pos = cpos[k.cand], x0 = pos & 0xFFFF, y0 = pos >> 16;
+void orb_harris_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const int* __restrict__ row_off,
+                       const Resp* __restrict__ A, const int* __restrict__ cnt1, const int32_t* __restrict__ cpos,
+                       Resp* __restrict__ B) {
+    const int l = blockIdx.y;
+    const Lvl L = lv[l];
+    const int c0 = lvl_first(row_off, L), m = cnt1[l];
     const uint8_t* img = pyr + L.off;
     const int step = L.w, r = HARRIS_BLOCK / 2;
-    int a = 0, b = 0, c = 0;
-    for (int ii = 0; ii < HARRIS_BLOCK; ii++) {
-        const uint8_t* p = img + (int64_t)(y0 - r + ii) * step + (x0 - r);
-        for (int j = 0; j < HARRIS_BLOCK; j++) {
-            const uint8_t* q = p + j;
-            const int Ix = (q[1] - q[-1]) * 2 + (q[-step + 1] - q[-step - 1]) + (q[step + 1] - q[step - 1]);
-            const int Iy = (q[step] - q[-step]) * 2 + (q[step - 1] - q[-step - 1]) + (q[step + 1] - q[-step + 1]);
-            a += Ix * Ix;
-            b += Iy * Iy;
-            c += Ix * Iy;
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < m; j += gridDim.x * 256) {
+        const int pos = cpos[A[c0 + j].idx], x0 = pos & 0xFFFF, y0 = pos >> 16;
+        int a = 0, b = 0, c = 0;
+        for (int ii = 0; ii < HARRIS_BLOCK; ii++) {
+            const uint8_t* p = img + (int64_t)(y0 - r + ii) * step + (x0 - r);
+            for (int jj = 0; jj < HARRIS_BLOCK; jj++) {
+                const uint8_t* q = p + jj;
+                const int Ix = (q[1] - q[-1]) * 2 + (q[-step + 1] - q[-step - 1]) + (q[step + 1] - q[step - 1]);
+                const int Iy = (q[step] - q[-step]) * 2 + (q[step - 1] - q[-step - 1]) + (q[step + 1] - q[-step + 1]);
+                a += Ix * Ix;
+                b += Iy * Iy;
+                c += Ix * Iy;
+            }
         }
+        const float scale = 1.f / ((1 << 2) * HARRIS_BLOCK * 255.f);
+        const float scale_sq_sq = scale * scale * scale * scale;
+        B[c0 + j] = Resp{((float)a * b - (float)c * c - HARRIS_K * ((float)a + b) * ((float)a + b)) * scale_sq_sq, j};
     }
-    const float scale = 1.f / ((1 << 2) * HARRIS_BLOCK * 255.f);
-    const float scale_sq_sq = scale * scale * scale * scale;
-    resp[i] = ((float)a * b - (float)c * c - HARRIS_K * ((float)a + b) * ((float)a + b)) * scale_sq_sq;
 }
 
 __device__ float fast_atan2(float y, float x) {   // cv::fastAtan2
@@ -317,46 +547,97 @@ __device__ __forceinline__ int wave_isum(int v) {
     return v;
 }
 
-// final[j] -> cv::KeyPoint with ICAngles' angle; one wavefront per keypoint (the 31 patch
-// rows u = -15..15 across lanes; integer moments, so the lane order is irrelevant)
+// the final keypoints in level order -> cv::KeyPoint with ICAngles' angle (one wavefront per
+// keypoint: the 31 patch rows u = -15..15 across lanes; integer moments, so the lane order is
+// irrelevant), and compute()'s runByImageBorder(31) test at full resolution (Rect::contains(Point(pt)))
 __global__ __launch_bounds__(256)
-void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const Kept* __restrict__ kept,
-                      const float* __restrict__ resp, const int32_t* __restrict__ final_idx, int n,
-                      const int32_t* __restrict__ cpos, const int* __restrict__ umax, Kp* __restrict__ out) {
-    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (j >= n) return;
-    const int ki = final_idx[j];
-    const Kept k = kept[ki];
-    const Lvl L = lv[k.level];
-    const int pos = cpos[k.cand], cx = pos & 0xFFFF, cy = pos >> 16;
-    const uint8_t* img = pyr + L.off;
-    const int step = L.w;
-    int m10 = 0, m01 = 0;
-    if (lane < 2 * HALF_PATCH + 1) {
-        const int u = lane - HALF_PATCH;
-        const uint8_t* col = img + (int64_t)cy * step + cx + u;
-        m10 = u * col[0];
-        const int au = u < 0 ? -u : u;
-        for (int v = 1; v <= HALF_PATCH; ++v) {
-            if (au > umax[v]) continue;
-            const int vp = col[v * step], vm = col[-v * step];
-            m10 += u * (vp + vm);
-            m01 += v * (vp - vm);
+void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int nl,
+                      const int* __restrict__ row_off, const Resp* __restrict__ A, const Resp* __restrict__ B,
+                      const int* __restrict__ cnt2, const int32_t* __restrict__ cpos, const int* __restrict__ umax,
+                      int width, int height, int border, Kp* __restrict__ out, int* __restrict__ keep) {
+    const int lane = threadIdx.x & 63;
+    int total = 0;
+    for (int l = 0; l < nl; ++l) total += cnt2[l];
+    for (int f = blockIdx.x * 4 + (threadIdx.x >> 6); f < total; f += gridDim.x * 4) {
+        int l = 0, j = f;
+        while (j >= cnt2[l]) { j -= cnt2[l]; ++l; }
+        const Lvl L = lv[l];
+        const int c0 = lvl_first(row_off, L);
+        const Resp e = B[c0 + j];
+        const int pos = cpos[A[c0 + e.idx].idx], cx = pos & 0xFFFF, cy = pos >> 16;
+        const uint8_t* img = pyr + L.off;
+        const int step = L.w;
+        int m10 = 0, m01 = 0;
+        if (lane < 2 * HALF_PATCH + 1) {
+            const int u = lane - HALF_PATCH;
+            const uint8_t* col = img + (int64_t)cy * step + cx + u;
+            m10 = u * col[0];
+            const int au = u < 0 ? -u : u;
+            for (int v = 1; v <= HALF_PATCH; ++v) {
+                if (au > umax[v]) continue;
+                const int vp = col[v * step], vm = col[-v * step];
+                m10 += u * (vp + vm);
+                m01 += v * (vp - vm);
+            }
+        }
+        m10 = wave_isum(m10);
+        m01 = wave_isum(m01);
+        if (lane == 0) {
+            Kp q;
+            q.x = (float)cx * L.scale;
+            q.y = (float)cy * L.scale;
+            q.size = PATCH * L.scale;
+            q.angle = fast_atan2((float)m01, (float)m10);
+            q.response = e.response;
+            q.octave = l;
+            q.class_id = -1;
+            out[f] = q;
+            const int x = round_f(q.x), y = round_f(q.y);
+            keep[f] = height > 2 * border && width > 2 * border && border <= x && x < width - border && border <= y &&
+                      y < height - border;
         }
     }
-    m10 = wave_isum(m10);
-    m01 = wave_isum(m01);
-    if (lane == 0) {
-        Kp q;
-        q.x = (float)cx * L.scale;
-        q.y = (float)cy * L.scale;
-        q.size = PATCH * L.scale;
-        q.angle = fast_atan2((float)m01, (float)m10);
-        q.response = resp[ki];
-        q.octave = k.level;
-        q.class_id = -1;
-        out[j] = q;
+}
+
+// order-preserving compaction of the kept keypoints (one workgroup): st[0] = count, st[1] = the
+// levels the descriptors read (max octave + 1), st[2] = the corner total (overflow check)
+__global__ __launch_bounds__(RT)
+void orb_compact_kernel(const Kp* __restrict__ in, const int* __restrict__ keep, const int* __restrict__ cnt2, int nl,
+                        const int* __restrict__ row_off, int rows, Kp* __restrict__ out, int* __restrict__ st) {
+    __shared__ int sh[36];
+    const int t = threadIdx.x;
+    int total = 0;
+    for (int l = 0; l < nl; ++l) total += cnt2[l];
+    const int chunk = (total + RT - 1) / RT, s = min(t * chunk, total), e = min(s + chunk, total);
+    int c = 0, mo = 0;
+    for (int f = s; f < e; ++f) c += keep[f];
+    int dummy = 0;
+    scan2(c, dummy, sh);
+    const int n = sh[32];
+    for (int f = s; f < e; ++f)
+        if (keep[f]) {
+            const Kp q = in[f];
+            out[c++] = q;
+            mo = max(mo, q.octave + 1);
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mo = max(mo, __shfl_xor(mo, o));
+    __syncthreads();
+    if ((t & 63) == 0) sh[t >> 6] = mo;
+    __syncthreads();
+    if (t == 0) {
+        int m = 0;
+        for (int i = 0; i < RT / 64; ++i) m = max(m, sh[i]);
+        st[0] = n;
+        st[1] = m;
+        st[2] = row_off[rows];
     }
+}
+
+__global__ __launch_bounds__(256)
+void orb_copy_kp_kernel(const Kp* __restrict__ src, const int* __restrict__ st, int capacity, Kp* __restrict__ dst) {
+    const int m = min(st[0], capacity);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < m; i += gridDim.x * 256) dst[i] = src[i];
 }
 
 // ------------------------------------------------------------------ compute(): blur + rBRIEF
@@ -372,7 +653,9 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 }
 
 __global__ __launch_bounds__(256)
-void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, uint8_t* __restrict__ blur) {
+void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const int* __restrict__ st,
+                     uint8_t* __restrict__ blur) {
+    if ((int)blockIdx.z >= st[1]) return;   // only the levels the kept keypoints use
     const Lvl L = lv[blockIdx.z];
     const int x0 = blockIdx.x * BT_X, y0 = blockIdx.y * BT_Y;
     if (x0 >= L.w || y0 >= L.h) return;
@@ -428,55 +711,41 @@ __device__ void orb_sincos(double x, double* s, double* c) {
 }
 
 // computeOrbDescriptors (WTA_K 2): 32 lanes per keypoint, lane i builds byte i from
-// pattern pairs 8 i .. 8 i + 7
+// pattern pairs 8 i .. 8 i + 7; min(count, capacity) keypoints
 __global__ __launch_bounds__(256)
-void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ lv, const Kp* __restrict__ kps, int n,
-                      uint8_t* __restrict__ desc) {
-    const int j = blockIdx.x * 8 + (threadIdx.x >> 5), i = threadIdx.x & 31;
-    if (j >= n) return;
-    const Kp k = kps[j];
-    const Lvl L = lv[k.octave];
-    float angle = k.angle;
-    angle *= (float)(3.14159265358979323846 / 180.f);
-    double sd, cd;
-    orb_sincos((double)angle, &sd, &cd);
-    const float a = (float)cd, b = (float)sd;
-    const int cy = round_f(k.y * L.inv_scale), cx = round_f(k.x * L.inv_scale);
-    const uint8_t* img = blur + L.off;
-    auto value = [&](int idx) -> int {
-        const int px = c_pattern[2 * idx], py = c_pattern[2 * idx + 1];
-        const float x = px * a - py * b, y = px * b + py * a;
-        const int yy = min(max(cy + round_f(y), 0), L.h - 1), xx = min(max(cx + round_f(x), 0), L.w - 1);
-        return img[(int64_t)yy * L.w + xx];
-    };
-    int val = 0;
-#pragma unroll
-    for (int bit = 0; bit < 8; bit++) {
-        const int base = 16 * i + 2 * bit;
-        val |= (value(base) < value(base + 1)) << bit;
+void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ lv, const Kp* __restrict__ kps,
+                      const int* __restrict__ st, int capacity, uint8_t* __restrict__ desc) {
+    const int n = min(st[0], capacity), i = threadIdx.x & 31;
+    for (int j = blockIdx.x * 8 + (threadIdx.x >> 5); j < n; j += gridDim.x * 8) {
+        const Kp k = kps[j];
+        const Lvl L = lv[k.octave];
+        float angle = k.angle;
+        angle *= (float)(3.14159265358979323846 / 180.f);
+        double sd, cd;
+        orb_sincos((double)angle, &sd, &cd);
+        const float a = (float)cd, b = (float)sd;
+        const int cy = round_f(k.y * L.inv_scale), cx = round_f(k.x * L.inv_scale);
+        const uint8_t* img = blur + L.off;
+        auto value = [&](int idx) -> int {
+            const int px = c_pattern[2 * idx], py = c_pattern[2 * idx + 1];
+            const float x = px * a - py * b, y = px * b + py * a;
+            const int yy = min(max(cy + round_f(y), 0), L.h - 1), xx = min(max(cx + round_f(x), 0), L.w - 1);
+            return img[(int64_t)yy * L.w + xx];
+        };
+        int val = 0;
+    #pragma unroll
+        for (int bit = 0; bit < 8; bit++) {
+            const int base = 16 * i + 2 * bit;
+            val |= (value(base) < value(base + 1)) << bit;
+        }
+        desc[(int64_t)j * 32 + i] = (uint8_t)val;
     }
-    desc[(int64_t)j * 32 + i] = (uint8_t)val;
 }
 
 // ------------------------------------------------------------------ host
 static int host_round_f(float v) { return (int)std::nearbyint(v); }
 static int host_round_d(double v) { return (int)std::nearbyint(v); }
 static float get_scale(int level, double sf) { return (float)std::pow(sf, (double)level); }
-
-struct Resp { float response; int32_t idx; };
-
-// KeyPointsFilter::retainBest on (response, index) records: the same comparisons and moves
-// as on the reference's KeyPoint vector, so the same permutation
-static void retain_best(std::vector<Resp>& k, int n) {
-    if (n >= 0 && k.size() > (size_t)n) {
-        if (n == 0) { k.clear(); return; }
-        std::nth_element(k.begin(), k.begin() + n - 1, k.end(),
-                         [](const Resp& a, const Resp& b) { return a.response > b.response; });
-        const float amb = k[n - 1].response;
-        auto end = std::partition(k.begin() + n, k.end(), [amb](const Resp& p) { return p.response >= amb; });
-        k.resize(end - k.begin());
-    }
-}
 
 static void linear_axis(int dsize, int ssize, std::vector<AxisEnt>& out, int& dmin, int& dmax) {
     dmin = 0;
@@ -696,9 +965,10 @@ int orb_impl(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
     const hipStream_t st = (hipStream_t)stream;
     int rc = SFMX_OK;
     {
-        const size_t need = (size_t)px * 3 + (size_t)CAND_CAP * 5 + (size_t)(rows + 1) * 8 +
+        // corner records: cpos 4 + cscore 1 + A, B 8 + 8 + Ls, Rs 4 + 4 + raw / kept keypoints 28 + 28 + flag 4
+        const size_t need = (size_t)px * 3 + (size_t)CAND_CAP * 89 + (size_t)(rows + 1) * 8 +
                             tables.size() * sizeof(AxisEnt) + sizeof(Lvl) * nl + sizeof(int) * umax.size() +
-                            (size_t)width * height + 256 * 16;
+                            (size_t)width * height + (size_t)capacity * 32 + 256 * 32;
         if (!scratch.img.reserve(device, need)) { rc = SFMX_ENOMEM; set_last_error("device allocation failed"); goto done; }
         std::call_once(g_const_once[device], [] {
             int taps[7];
@@ -712,13 +982,25 @@ int orb_impl(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
             uint8_t* blur = A.take<uint8_t>(px);
             int32_t* cpos = A.take<int32_t>(CAND_CAP);
             uint8_t* cscore = A.take<uint8_t>(CAND_CAP);
+            Resp* rA = A.take<Resp>(CAND_CAP);
+            Resp* rB = A.take<Resp>(CAND_CAP);
+            int* sLs = A.take<int>(CAND_CAP);
+            int* sRs = A.take<int>(CAND_CAP);
+            Kp* kraw = A.take<Kp>(CAND_CAP);
+            Kp* dfin = A.take<Kp>(CAND_CAP);
+            int* keep = A.take<int>(CAND_CAP);
             int* row_cnt = A.take<int>(rows + 1);
             int* row_off = A.take<int>(rows + 1);
+            int* cnt = A.take<int>(2 * MAX_LEVELS + 4);   // cnt1 | cnt2 | status
             AxisEnt* dtab = A.take<AxisEnt>(std::max<size_t>(tables.size(), 1));
             Lvl* dlv = A.take<Lvl>(nl);
             int* dumax = A.take<int>(umax.size());
             uint8_t* t = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)width * height);
+            uint8_t* ddesc = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)std::max(capacity, 1) * 32);
             if (A.overflow) { set_last_error("internal: ORB scratch arena too small"); rc = SFMX_ECAPACITY; goto done; }
+            int* cnt1 = cnt;
+            int* cnt2 = cnt + MAX_LEVELS;
+            int* dst = cnt + 2 * MAX_LEVELS;
             const uint8_t* dimg = image;
             int64_t dpitch = pitch;
             if (!inputs_on_device) {
@@ -737,100 +1019,50 @@ int orb_impl(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
                 orb_resize_kernel<<<dim3((lv[l].w + 255) / 256, lv[l].h), 256, 0, st>>>(pyr, dlv, l, dtab);
             orb_fast_kernel<<<dim3((maxw + FT_X - 1) / FT_X, (maxh + FT_Y - 1) / FT_Y, nl), 256, 0, st>>>(pyr, dlv, thr,
                                                                                                       score);
-            orb_nms_kernel<<<rows, 256, 0, st>>>(score, dlv, nl, border, 0, row_cnt, nullptr, nullptr, nullptr);
+            orb_nms_kernel<<<rows, 256, 0, st>>>(score, dlv, nl, border, 0, row_cnt, nullptr, nullptr, nullptr, (int)CAND_CAP);
             orb_scan_kernel<<<1, 1024, 0, st>>>(row_cnt, rows, row_off);
-            orb_nms_kernel<<<rows, 256, 0, st>>>(score, dlv, nl, border, 1, nullptr, row_off, cpos, cscore);
+            orb_nms_kernel<<<rows, 256, 0, st>>>(score, dlv, nl, border, 1, nullptr, row_off, cpos, cscore, (int)CAND_CAP);
+            // retainBest(2 n_l) on the FAST scores, Harris responses, retainBest(n_l) on them (device)
+            OCHK(hipMemsetAsync(dst + 3, 0, sizeof(int), st));
+            SelCounts s1{}, s2{};
+            for (int l = 0; l < nl; l++) { s1.n[l] = 2 * per[l]; s2.n[l] = per[l]; }
+            orb_retain_kernel<<<nl, RT, 0, st>>>(0, dlv, row_off, cscore, rA, rB, sLs, sRs, nullptr, cnt1, s1, (int)CAND_CAP,
+                                                 dst + 3);
+            orb_harris_kernel<<<dim3(64, nl), 256, 0, st>>>(pyr, dlv, row_off, rA, cnt1, cpos, rB);
+            orb_retain_kernel<<<nl, RT, 0, st>>>(1, dlv, row_off, cscore, rA, rB, sLs, sRs, cnt1, cnt2, s2, (int)CAND_CAP,
+                                                 dst + 3);
+            orb_angle_kernel<<<1024, 256, 0, st>>>(pyr, dlv, nl, row_off, rA, rB, cnt2, cpos, dumax, width, height, border,
+                                                   kraw, keep);
+            orb_compact_kernel<<<1, RT, 0, st>>>(kraw, keep, cnt2, nl, row_off, rows, dfin, dst);
+            // ---- compute(): blur of the levels used, rBRIEF of min(count, capacity) keypoints
+            if (descriptors && capacity > 0) {
+                orb_blur_kernel<<<dim3((maxw + BT_X - 1) / BT_X, (maxh + BT_Y - 1) / BT_Y, nl), 256, 0, st>>>(pyr, dlv, dst,
+                                                                                                       blur);
+                orb_brief_kernel<<<std::min(4096, (capacity + 7) / 8), 256, 0, st>>>(blur, dlv, dfin, dst, capacity,
+                                                                                     inputs_on_device ? descriptors : ddesc);
+            }
+            if (inputs_on_device && capacity > 0)
+                orb_copy_kp_kernel<<<std::min(1024, (capacity + 255) / 256), 256, 0, st>>>(
+                    dfin, dst, capacity, reinterpret_cast<Kp*>(keypoints));
             OCHK(hipGetLastError());
-            std::vector<int> hoff(rows + 1);
-            OCHK(hipMemcpyAsync(hoff.data(), row_off, sizeof(int) * (rows + 1), hipMemcpyDeviceToHost, st));
+            int hst[4] = {0, 0, 0, 0};
+            OCHK(hipMemcpyAsync(hst, dst, sizeof(hst), hipMemcpyDeviceToHost, st));
+            OCHK(hipEventRecord(A.e1, st));
             OCHK(hipStreamSynchronize(st));
-            const int ncand = hoff[rows];
-            if (ncand > CAND_CAP) { set_last_error("internal: corner buffer overflow"); rc = SFMX_EINTERNAL; goto done; }
-            std::vector<uint8_t> hsc(ncand);
-            if (ncand) OCHK(hipMemcpyAsync(hsc.data(), cscore, ncand, hipMemcpyDeviceToHost, st));
-            OCHK(hipStreamSynchronize(st));
-            // retainBest(2 n_l) per level on the FAST scores
-            std::vector<Kept> kept;
-            std::vector<int> kcount(nl);
-            for (int l = 0; l < nl; l++) {
-                const int c0 = hoff[lv[l].row0], c1 = hoff[lv[l].row0 + lv[l].h];
-                std::vector<Resp> r(c1 - c0);
-                for (int i = c0; i < c1; i++) r[i - c0] = Resp{(float)hsc[i], i};
-                retain_best(r, 2 * per[l]);
-                kcount[l] = (int)r.size();
-                for (const Resp& q : r) kept.push_back(Kept{q.idx, l});
-            }
-            const int nk = (int)kept.size();
-            // buffers sized by the kept-corner count (ties at the retainBest boundary can exceed 2 n)
-            const size_t kneed = (size_t)(nk + 1) * (sizeof(Kept) + 4 + 4 + 2 * sizeof(Kp) + 32) + 256 * 8;
-            if (!scratch.kp.reserve(device, kneed)) { rc = SFMX_ENOMEM; set_last_error("device allocation failed"); goto done; }
-            {
-                Arena& K = scratch.kp;
-                Kept* dkept = K.take<Kept>(nk + 1);
-                float* dresp = K.take<float>(nk + 1);
-                int32_t* dfinal = K.take<int32_t>(nk + 1);
-                Kp* dkp = K.take<Kp>(nk + 1);
-                Kp* dfin = K.take<Kp>(nk + 1);
-                uint8_t* ddesc = K.take<uint8_t>((size_t)(nk + 1) * 32);
-                if (K.overflow) { set_last_error("internal: ORB keypoint arena too small"); rc = SFMX_ECAPACITY; goto done; }
-                std::vector<float> hresp(nk);
-                if (nk) {
-                    OCHK(hipMemcpyAsync(dkept, kept.data(), sizeof(Kept) * nk, hipMemcpyHostToDevice, st));
-                    orb_harris_kernel<<<(nk + 255) / 256, 256, 0, st>>>(pyr, dlv, dkept, nk, cpos, dresp);
-                    OCHK(hipGetLastError());
-                    OCHK(hipMemcpyAsync(hresp.data(), dresp, sizeof(float) * nk, hipMemcpyDeviceToHost, st));
-                    OCHK(hipStreamSynchronize(st));
-                }
-                // retainBest(n_l) per level on the Harris responses
-                std::vector<int32_t> fin;
-                for (int l = 0, k0 = 0; l < nl; k0 += kcount[l], l++) {
-                    std::vector<Resp> r(kcount[l]);
-                    for (int i = 0; i < kcount[l]; i++) r[i] = Resp{hresp[k0 + i], k0 + i};
-                    retain_best(r, per[l]);
-                    for (const Resp& q : r) fin.push_back(q.idx);
-                }
-                const int nf = (int)fin.size();
-                std::vector<Kp> kps(nf);
-                if (nf) {
-                    OCHK(hipMemcpyAsync(dfinal, fin.data(), sizeof(int32_t) * nf, hipMemcpyHostToDevice, st));
-                    orb_angle_kernel<<<(nf + 3) / 4, 256, 0, st>>>(pyr, dlv, dkept, dresp, dfinal, nf, cpos, dumax, dkp);
-                    OCHK(hipGetLastError());
-                    OCHK(hipMemcpyAsync(kps.data(), dkp, sizeof(Kp) * nf, hipMemcpyDeviceToHost, st));
-                    OCHK(hipStreamSynchronize(st));
-                }
-                // ---- compute(): runByImageBorder at full resolution (Rect::contains(Point(pt)))
-                if (height <= 2 * border || width <= 2 * border) kps.clear();
-                else
-                    kps.erase(std::remove_if(kps.begin(), kps.end(), [&](const Kp& q) {
-                                  const int x = host_round_f(q.x), y = host_round_f(q.y);
-                                  return !(border <= x && x < width - border && border <= y && y < height - border);
-                              }), kps.end());
-                const int n = (int)kps.size();
-                *n_keypoints = n;
-                const int m = std::min(n, (int)capacity);
-                if (m > 0) {
-                    OCHK(hipMemcpyAsync(dfin, kps.data(), sizeof(Kp) * m, hipMemcpyHostToDevice, st));
-                    if (descriptors) {
-                        int nlev = 0;
-                        for (int q = 0; q < m; q++) nlev = std::max(nlev, kps[q].octave + 1);
-                        orb_blur_kernel<<<dim3((maxw + BT_X - 1) / BT_X, (maxh + BT_Y - 1) / BT_Y, nlev), 256, 0, st>>>(
-                            pyr, dlv, blur);
-                        uint8_t* dd = inputs_on_device ? descriptors : ddesc;
-                        orb_brief_kernel<<<(m + 7) / 8, 256, 0, st>>>(blur, dlv, dfin, m, dd);
-                        OCHK(hipGetLastError());
-                        if (!inputs_on_device)
-                            OCHK(hipMemcpyAsync(descriptors, dd, (size_t)m * 32, hipMemcpyDeviceToHost, st));
-                    }
-                    if (inputs_on_device) OCHK(hipMemcpyAsync(keypoints, dfin, sizeof(Kp) * m, hipMemcpyDeviceToDevice, st));
-                    else std::memcpy(keypoints, kps.data(), sizeof(Kp) * m);
-                }
-                OCHK(hipEventRecord(A.e1, st));
+            if (hst[2] > CAND_CAP) { set_last_error("internal: corner buffer overflow"); rc = SFMX_EINTERNAL; goto done; }
+            if (hst[3]) { set_last_error("internal: device retainBest made no progress"); rc = SFMX_EINTERNAL; goto done; }
+            const int n = hst[0];
+            *n_keypoints = n;
+            const int m = std::min(n, (int)capacity);
+            if (!inputs_on_device && m > 0) {   // host buffers: the kept keypoints and descriptors back
+                OCHK(hipMemcpyAsync(keypoints, dfin, sizeof(Kp) * m, hipMemcpyDeviceToHost, st));
+                if (descriptors) OCHK(hipMemcpyAsync(descriptors, ddesc, (size_t)m * 32, hipMemcpyDeviceToHost, st));
                 OCHK(hipStreamSynchronize(st));
-                float ms = -1.f;
-                (void)hipEventElapsedTime(&ms, A.e0, A.e1);
-                *last_ms = ms;
-                if (n > capacity) { set_last_error("keypoint capacity too small"); rc = SFMX_ECAPACITY; }
             }
+            float ms = -1.f;
+            (void)hipEventElapsedTime(&ms, A.e0, A.e1);
+            *last_ms = ms;
+            if (n > capacity) { set_last_error("keypoint capacity too small"); rc = SFMX_ECAPACITY; }
         }
     done:;
     }

@@ -35,14 +35,18 @@ def shard_ba_problem(prob: dict, rank: int, world: int) -> dict:
     return out
 
 
-def rccl_comm(ctx, group=None) -> None:
-    """Give a BAContext native RCCL collectives (sfmx_ba_set_comm): rank 0 creates the id,
-    torch.distributed broadcasts it (any backend), every rank initialises its communicator."""
+def rccl_comm(ctx, group=None, unique_id=None) -> None:
+    """Give a BAContext native RCCL collectives (sfmx_ba_set_comm): the group's rank 0 creates the
+    id, torch.distributed broadcasts it (any backend), every rank initialises its communicator.
+    `unique_id` replaces sfmx.ba.comm_unique_id (tests of the hand-off without RCCL)."""
     import torch.distributed as dist
-    from .ba import comm_unique_id
+    from .ba import comm_unique_id as _uid
+    comm_unique_id = unique_id or _uid
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     obj = [comm_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0, group=group)
+    # broadcast_object_list takes a GLOBAL source rank: the group's rank 0 (ADVICE r03)
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.broadcast_object_list(obj, src=src, group=group)
     ctx.set_comm(obj[0], world, rank)
 
 

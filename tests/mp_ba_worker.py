@@ -18,7 +18,10 @@ def main():
     torch.cuda.set_device(0)
     from sfmx import ba, synth
     from sfmx.dist import shard_ba_problem, torch_allreduce
-    p = synth.ba_problem(int(sys.argv[1]), int(sys.argv[2]), seed=int(sys.argv[3]))
+    if len(sys.argv) > 4 and sys.argv[4] == "multi":   # several cameras: every rank must derive the same border
+        p = synth.ba_problem_multi(int(sys.argv[1]), int(sys.argv[2]), cameras=((1, 1.0), (3, 1.1)), seed=int(sys.argv[3]))
+    else:
+        p = synth.ba_problem(int(sys.argv[1]), int(sys.argv[2]), seed=int(sys.argv[3]))
     local = shard_ba_problem(p, rank, world)
     local.pop("point_range")
     ctx = ba.BAContext(ba.BAProblem(**local), allreduce=torch_allreduce(cpu_staging=True))

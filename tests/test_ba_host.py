@@ -39,3 +39,53 @@ def test_c5_shape():
     assert np.all(np.diff(p["obs_point"]) >= 0)   # point-major observations
     cams = p["obs_cam"].reshape(-1, 6)
     assert np.all((cams[:, 1:] - cams[:, :-1]) % 200 == 1)
+
+
+# ---- the point-group topology the group kernels index (ba_solver.hip check_topology) ------------
+
+def _ragged_problem(seed, n_cams, n_points, big_every=0, dup_every=0, empty_every=0, shuffle=False):
+    """Ring-like tracks of 2..9 cameras, plus (optionally) long tracks (> 64 observations: big
+    groups), a repeated camera inside a track (big) and points without observations."""
+    rng = np.random.default_rng(seed)
+    op, oc = [], []
+    for p in range(n_points):
+        if empty_every and p % empty_every == 3:
+            continue
+        if big_every and p % big_every == 1:
+            cams = rng.integers(0, n_cams, 70)
+        else:
+            m = int(rng.integers(2, 10))
+            cams = (int(rng.integers(0, n_cams)) + np.arange(m)) % n_cams
+            if dup_every and p % dup_every == 2:
+                cams = np.append(cams, cams[0])
+        op += [p] * len(cams)
+        oc += list(cams)
+    op, oc = np.array(op, np.int32), np.array(oc, np.int32)
+    if shuffle:                      # not point-major: the ordering's counting path
+        perm = rng.permutation(len(op))
+        op, oc = op[perm], oc[perm]
+    xy = rng.uniform(0, 700, (len(op), 2))
+    return ba.BAProblem(3, rng.normal(size=(n_points, 3)), rng.normal(size=(n_cams, 6)), np.array([800.0, 0.0, 0.0]),
+                        op, oc, xy, 360.0, 200.0)
+
+
+TOPO_CASES = [dict(seed=1, n_cams=10, n_points=1000), dict(seed=2, n_cams=40, n_points=3000, big_every=97),
+              dict(seed=3, n_cams=7, n_points=2500, dup_every=13, empty_every=29),
+              dict(seed=4, n_cams=200, n_points=20000, big_every=501, dup_every=333, shuffle=True),
+              dict(seed=5, n_cams=3, n_points=300)]
+
+
+@pytest.mark.parametrize("case", range(len(TOPO_CASES)))
+@pytest.mark.parametrize("gpts", [1, 2, 3, 17, 99, 0])
+def test_point_group_topology_holds_every_kernel_bound(case, gpts):
+    """every index the group kernels derive from the host-built topology (group /
+    chunk / batch ranges, feature rows, lane-map slots, camera slots, assembly entries inside sg / hbig
+    / rg) is checked against the limits the kernels assume, for group sizes down to 1 point (the
+    regime of the r03 launch failure), big and duplicate-camera points, empty points, and a
+    non-point-major observation order."""
+    from diag import diag_lib
+    from sfmx import _lib
+    P = _ragged_problem(**TOPO_CASES[case])
+    st = P.struct()
+    n = diag_lib().sfmx_ba_debug_check_topology(st, gpts)
+    assert n > 0, _lib.lib.sfmx_last_error() or diag_lib().sfmx_last_error()

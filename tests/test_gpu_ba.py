@@ -88,21 +88,24 @@ def test_do_bundle_adjustment_mirror():
     assert not np.array_equal(before, P.points)                  # written back in place
 
 
-def test_point_sharded_two_ranks_match_single():
+@pytest.mark.parametrize("kind", ["single", "multi"])
+def test_point_sharded_two_ranks_match_single(kind):
     """Point-sharded BA over 2 ranks (both on this GPU, gloo all-reduce of the
-    reduced camera system) reaches the 1-rank final cost within 1e-5."""
+    reduced camera system) reaches the 1-rank final cost within 1e-5.  "multi": two camera
+    models (every rank derives the same intrinsics border from the replicated poses)."""
     import json, os, subprocess, sys
     here = os.path.dirname(os.path.abspath(__file__))
-    args = ["10", "1200", "27"]
+    args = ["10", "1200", "27"] if kind == "single" else ["12", "1400", "46", "multi"]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                          "--master-addr=127.0.0.1", "--master-port=29531", os.path.join(here, "mp_ba_worker.py"), *args],
+                          "--master-addr=127.0.0.1", f"--master-port={29531 + (kind == 'multi')}", os.path.join(here, "mp_ba_worker.py"), *args],
                          capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
     r = json.loads(line)
     assert r["cameras_identical"]
-    p = synth.ba_problem(int(args[0]), int(args[1]), seed=int(args[2]))
+    p = synth.ba_problem(int(args[0]), int(args[1]), seed=int(args[2])) if kind == "single" else \
+        synth.ba_problem_multi(int(args[0]), int(args[1]), cameras=((1, 1.0), (3, 1.1)), seed=int(args[2]))
     P, sm, _ = gpu_solve(p)
     assert abs(r["initial_cost"] - sm["initial_cost"]) <= 1e-12 * sm["initial_cost"]
     assert abs(r["final_cost"] - sm["final_cost"]) <= COST_RTOL * sm["final_cost"]
@@ -300,8 +303,9 @@ def test_update_grown_scene_equals_fresh_context_and_reuses_plan():
         grow = ctx.setup_ms()
         Pb = ctx.get()
         ctx.update(ba.BAProblem(**grown(base, 60)))   # same graph: the plan is kept
-        ctx.run()
+        s_s, t_s = ctx.run(trace_cap=256)
         same = ctx.setup_ms()
+        Ps = ctx.get()
     finally:
         ctx.close()
     ref = ba.BAContext(ba.BAProblem(**grown(base, 60)))
@@ -311,5 +315,76 @@ def test_update_grown_scene_equals_fresh_context_and_reuses_plan():
     finally:
         ref.close()
     assert s_b["final_cost"] == s_r["final_cost"] and np.array_equal(t_b, t_r) and np.array_equal(Pb.points, Pr.points)
+    # the plan-reusing run (device counters and buffers carried over) gives the fresh context's bits
+    assert s_s["final_cost"] == s_r["final_cost"] and np.array_equal(t_s, t_r)
+    assert np.array_equal(Ps.points, Pr.points) and np.array_equal(Ps.poses, Pr.poses) and np.array_equal(Ps.intr, Pr.intr)
     assert first["plan"] > 0 and grow["plan"] > 0 and same["plan"] == 0
     assert all(v >= 0 for v in grow.values()) and grow["total"] >= grow["order_groups"]
+
+
+def test_native_rccl_world_of_one_is_bit_identical():
+    """the native RCCL path (sfmx_ba_set_comm: ncclAllReduce of the packed
+    reduced system, the camera sums and the scalars on the solver stream) on a world of one gives
+    the bits of the solve without a communicator."""
+    p = synth.ba_problem(40, 4000, seed=66)
+    P0, s0, t0 = gpu_solve(p)
+    P1 = ba.BAProblem(**p)
+    ctx = ba.BAContext(P1)
+    try:
+        ctx.set_comm(ba.comm_unique_id(), 1, 0)
+        s1, t1 = ctx.run(trace_cap=512)
+        ctx.get(P1)
+    finally:
+        ctx.close()
+    assert s1["final_cost"] == s0["final_cost"] and np.array_equal(t1, t0)
+    assert np.array_equal(P1.points, P0.points) and np.array_equal(P1.poses, P0.poses) and np.array_equal(P1.intr, P0.intr)
+
+
+def test_refused_update_leaves_the_loaded_problem_intact():
+    """an update refused by a check (here: over the intrinsics capacity) fails before any
+    context state changes, so the loaded problem stays usable (a failure after that point marks the
+    context unloaded: run / get / set then refuse with SFMX_ESTATE until an update succeeds)."""
+    from sfmx import _lib
+    p = synth.ba_problem(10, 800, seed=67)
+    ctx = ba.BAContext(ba.BAProblem(**p))
+    try:
+        s0, _ = ctx.run()
+        bad = synth.ba_problem_multi(12, 300, cameras=((3, 1.0), (3, 1.1), (3, 0.9)), seed=44)
+        with pytest.raises(_lib.SfmxError) as e:
+            ctx.update(ba.BAProblem(**bad))
+        assert e.value.code == _lib.SFMX_ECAPACITY
+        s1, _ = ctx.run()                     # refused before any state changed: still the old problem
+        assert s1["initial_cost"] == s0["final_cost"]   # (from where the first run left it)
+        big = synth.ba_problem(200, 6000, seed=68)
+        ctx.update(ba.BAProblem(**big))
+        s2, _ = ctx.run(max_iterations=2)
+        assert s2["initial_cost"] > 0
+    finally:
+        ctx.close()
+
+
+def test_tiny_point_groups_after_differently_sized_solves():
+    """the regime of the r03 launch failure (point groups of 1-3 points, the
+    first solve of test_solve_matches_oracle[1]) placed after solves of other sizes, models and
+    camera counts in one process, so every cached buffer is reused or regrown first.  The
+    diagnostic library forces the group size (SFMX_BA_GPTS) and checks every topology it uploads
+    (check_topology); each result must match the oracle as test_solve_matches_oracle does, and the
+    product library (its own group sizing) must give the same LM decisions."""
+    from oracle import oracle
+    warm = [synth.ba_problem(200, 20000, seed=70), synth.ba_problem(12, 900, seed=71, cam_model=7),
+            synth.ba_problem_multi(16, 1500, cameras=((1, 1.0), (3, 1.1)), seed=72)]
+    target = synth.ba_problem(10, 1000, seed=22, cam_model=1)
+    _, osm, otr = oracle.ba_solve(target, trace_cap=512)
+    for w in warm:
+        gpu_solve(w)
+    _, sp, tp_ = gpu_solve(target)                # product library after the warm-up
+    for gpts in ("2", "1", "3", "2"):
+        with diagnostic(SFMX_BA_GPTS=gpts):
+            for w in warm[:2]:
+                gpu_solve(w, max_num_iterations=3)
+            P, sm, tr = gpu_solve(target)
+        assert sm["termination_type"] == osm["termination_type"], gpts
+        assert abs(sm["final_cost"] - osm["final_cost"]) <= COST_RTOL * osm["final_cost"], gpts
+        n = min(len(tr), len(otr))
+        assert np.array_equal(tr[:n, 2], otr[:n, 2]), gpts
+        assert np.array_equal(tr[:, 2], tp_[:, 2]) and abs(sm["final_cost"] - sp["final_cost"]) <= 1e-9 * sp["final_cost"]

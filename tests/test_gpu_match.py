@@ -281,3 +281,31 @@ def test_previously_failing_variants(env, variant):
             m, off, _, _ = run(imgs, pairs, ratio)
             em, eoff = oracle.match_pairs(imgs, pairs, ratio)
             assert_same(m, off, em, eoff)
+
+
+@pytest.mark.parametrize("batches", ["1", "2", "3", "64"])
+@pytest.mark.parametrize("kind", ["sift", "orb"])
+def test_overlapped_two_pass_batches_vs_oracle(kind, batches):
+    """the screen launches of consecutive batches alternate between two streams
+    and each batch's pass 2 runs on a third stream behind its screen (launch_two_pass_overlap); any
+    batch count, including one batch per pair (64) and the single-launch form (1), gives the oracle's
+    matches, with mixed-size pairs, empty-ish images and a non-integral image (an fp32 pair inside
+    a batch: no screen items, pass 2 skips it)."""
+    from oracle import oracle
+    if kind == "sift":
+        sizes = [1, 33, 700, 1100, 1100, 513, 900]
+        base = synth.sift_images(len(sizes), 1100, seed=91)
+        imgs = [b[:n] for b, n in zip(base, sizes)]
+        imgs.append(np.random.default_rng(92).random((300, 128), dtype=np.float32) * 40)
+        pairs = sfmx.pairs_unordered(len(imgs))
+    else:
+        base = synth.orb_images(7, 1500, seed=93)
+        imgs = [b[:n] for b, n in zip(base, [1500, 1, 700, 513, 1500, 256, 1200])]
+        pairs = sfmx.pairs_grid(7, 3, 2)
+    with diagnostic(SFMX_MATCH_BATCHES=batches):
+        m, off, _, _ = run(imgs, pairs)
+        m2, off2, _, _ = run(imgs, pairs, ratio=1.5)
+    em, eoff = oracle.match_pairs(imgs, pairs)
+    assert_same(m, off, em, eoff)
+    em2, eoff2 = oracle.match_pairs(imgs, pairs, 1.5)
+    assert_same(m2, off2, em2, eoff2)
