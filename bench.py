@@ -563,17 +563,19 @@ def bench_ba(args, rank, world, local):
 
 def bench_ba_calls(args):
     """The reference's BA call pattern (SfM.cpp:235 / :371): BundleAdjustment after every registered
-    camera, on a growing scene.  Replayed on the C5 ring (synth.ba_registered: the first n cameras,
-    points seen by >= 2 of them) for n = 20, 40, ..., 200 through one solver context, as
-    sfmx_ba_solve's per-device cache does; per call the end-to-end ms (host arrays in, results out)
-    split into the host setup (ordering + groups, device allocation, uploads, plan) and the LM
-    minimiser, plus a cold call (fresh context) at the C5 size.  Rank 0, one GPU."""
+    camera, on a growing scene.  Replayed on the C5 ring with its points in the order an incremental
+    SfM creates them (synth.ba_sfm_order: appended when their second camera registers;
+    synth.ba_registered: the first n cameras, points seen by >= 2 of them) for n = 20, 40, ..., 180
+    and then one camera at a time up to 200, through one solver context (sfmx_ba_update, as
+    sfmx_ba_solve's per-device cache does): per call the end-to-end ms (host arrays in, results out)
+    split into the host setup (ordering + groups of the camera buckets that changed, device
+    allocation, uploads, plan) and the LM minimiser, the buckets redone, plus a cold call (fresh
+    context) at the C5 size.  Rank 0, one GPU."""
     from sfmx import ba, synth
-    base = synth.ba_problem(args.ba_cams, args.ba_points)
+    base = synth.ba_sfm_order(synth.ba_problem(args.ba_cams, args.ba_points))
     calls, ctx = [], None
-    sizes = list(range(20, args.ba_cams + 1, 20))
-    if sizes[-1] != args.ba_cams:
-        sizes.append(args.ba_cams)
+    last = args.ba_cams
+    sizes = [n for n in range(20, last - 4, 20)] + list(range(max(1, last - 4), last + 1))
     try:
         for n in sizes:
             P = ba.BAProblem(**synth.ba_registered(base, n))
@@ -603,9 +605,13 @@ def bench_ba_calls(args):
     finally:
         cold.close()
     last = calls[-1]
-    return {"what": "BundleAdjustment after every registered camera (SfM.cpp:235 / :371), C5 ring grown 20 -> "
-                    f"{args.ba_cams} cameras; one context reused (sfmx_ba_update, = sfmx_ba_solve's cache)",
+    single = [c for c in calls if c["cams"] > args.ba_cams - 4]
+    return {"what": "BundleAdjustment after every registered camera (SfM.cpp:235 / :371), C5 ring in SfM point order, "
+                    f"grown 20 -> {args.ba_cams} cameras (the last steps one camera each); one context reused "
+                    "(sfmx_ba_update: unchanged camera buckets kept, = sfmx_ba_solve's cache)",
             "calls": calls, "c5_call_ms": last["ms"], "c5_setup_frac": last["setup_frac"],
+            "single_camera_steps_setup_frac": [round(c["setup_frac"], 3) for c in single],
+            "single_camera_steps_setup_ms": [round(c["ms"] - c["lm_ms"], 3) for c in single],
             "c5_cold_call": {"ms": cold_ms, "lm_ms": sm["total_ms"], "setup_ms": cold_su,
                              "setup_frac": (cold_ms - sm["total_ms"]) / cold_ms}}
 

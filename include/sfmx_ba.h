@@ -132,15 +132,24 @@ int sfmx_ba_set_comm(sfmx_ba_ctx* ctx, const void* unique_id, int32_t nranks, in
  * max_iterations iterations (<= 0: options.max_num_iterations). */
 int sfmx_ba_run(sfmx_ba_ctx* ctx, int32_t max_iterations, sfmx_ba_summary* summary,
                 double* trace, int32_t trace_cap);
-/* Replace the context's problem by another one of any topology (a grown scene): the
- * context's device buffers are reused when large enough and its factorization plan when
- * the camera co-visibility is unchanged (single rank).  Options and the all-reduce
- * callback stay.  Then sfmx_ba_run / sfmx_ba_get as after sfmx_ba_create. */
+/* Replace the context's problem by another one of any topology (a grown scene,
+ * BundleAdjustment after every registered camera, SfM.cpp:235 / :371): the scene stays
+ * resident.  Points are ordered and grouped in buckets of their smallest camera; for a
+ * point-major problem (the reference's residual order) only the buckets holding points whose
+ * observations (count, cameras, pixels) changed since the last load are redone on the host,
+ * the others keep their order and groups and their observation data moves on the device
+ * (no upload).  The result is bit-identical to a fresh context on the same problem.  Device
+ * buffers are reused when large enough and the factorization plan when the camera
+ * co-visibility is unchanged (single rank).  Options and the all-reduce callback stay.  Then
+ * sfmx_ba_run / sfmx_ba_get as after sfmx_ba_create.  A refused problem (SFMX_EINVAL,
+ * SFMX_ECAPACITY) leaves the loaded one intact; a later failure leaves the context unloaded:
+ * run / get / set return SFMX_ESTATE until an update succeeds. */
 int sfmx_ba_update(sfmx_ba_ctx* ctx, const sfmx_ba_problem* problem);
-/* Host-side setup time of the last create / update (ms): [0] point ordering + groups,
- * [1] device allocation, [2] uploads (pinned staging, incl. the parameters), [3] the
- * factorization plan (built at the next run; 0 when reused), [4] total, [5] / [6] the ordering
- * and the point groups (the two parts of [0]).  n = entries (up to 7). */
+/* Host-side setup of the last create / update: [0] point ordering + groups (ms), [1] device
+ * allocation (ms), [2] uploads (pinned staging, incl. the parameters; ms), [3] the
+ * factorization plan (built at the next run; 0 when reused; ms), [4] total (ms), [5] the host
+ * ordering / grouping pass alone (ms), [6] the number of camera buckets it redid.  n = entries
+ * (up to 7). */
 int sfmx_ba_setup_ms(sfmx_ba_ctx* ctx, double* ms, int32_t n);
 /* Copy the current parameters back into problem->points/poses/intr. */
 int sfmx_ba_get(sfmx_ba_ctx* ctx, sfmx_ba_problem* problem);

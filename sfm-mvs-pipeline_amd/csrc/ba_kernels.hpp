@@ -363,6 +363,22 @@ __global__ void ba_obs_point(int P, const int* __restrict__ pt_start, int* __res
     if (p < P)
         for (int o = pt_start[p]; o < pt_start[p + 1]; ++o) obs_point[o] = p;
 }
+// sfmx_ba_update: an unchanged bucket's observation data moves to its offset in the new layout
+// (pixels, camera, local camera, feature row: 24 B per observation), one workgroup per <= 4096.
+struct ObsMove { long long src, dst; int n, pad; };
+constexpr int RELAYOUT_CHUNK = 4096;
+__global__ __launch_bounds__(256) void ba_relayout(const ObsMove* __restrict__ mv, const double2* __restrict__ xy,
+                                                   const int* __restrict__ cam, const short* __restrict__ lc,
+                                                   const short* __restrict__ row, double2* __restrict__ xy2,
+                                                   int* __restrict__ cam2, short* __restrict__ lc2, short* __restrict__ row2) {
+    const ObsMove m = mv[blockIdx.x];
+    for (int k = threadIdx.x; k < m.n; k += blockDim.x) {
+        xy2[m.dst + k] = xy[m.src + k];
+        cam2[m.dst + k] = cam[m.src + k];
+        lc2[m.dst + k] = lc[m.src + k];
+        row2[m.dst + k] = row[m.src + k];
+    }
+}
 __global__ void ba_fill(int64_t n, double v, double* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = v;

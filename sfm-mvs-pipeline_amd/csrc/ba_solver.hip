@@ -106,6 +106,8 @@ struct sfmx_ba_ctx {
     int ngroups = 0, ntasks = 0, nslots = 0, gs_nt = 4;   // gs_nt: ba_gschur specialisation, dp_max / 16
     size_t lds_schur = 0, lds_lin = 0;
     Buf obs_point, obs_cam, obs_xy, pt_start, grp, chk, bat, gcam, obs_lc, obs_row, lcrow, tasks, ents, cref_start, cref;
+    Buf obs_xy_b, obs_cam_b, obs_lc_b, obs_row_b, moves;   // the next layout's observation arrays; relayout moves
+    int64_t setup_up_obs = 0;    // observations the last load uploaded (the rest moved on the device)
     // factorization plan of the reduced camera system (built at the first run, from the camera
     // co-visibility of every rank: the layout of S must be the same on all of them)
     std::vector<char> adj;       // local camera co-visibility, C x C
@@ -158,7 +160,7 @@ struct sfmx_ba_ctx {
     int plan_K = 0;
     HostScratch* hscr = nullptr;
     ~sfmx_ba_ctx() {
-        Buf* all[] = {&obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
+        Buf* all[] = {&obs_xy_b, &obs_cam_b, &obs_lc_b, &obs_row_b, &moves, &obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
                       &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &Wr, &Wr2, &PR, &PR2, &J, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
@@ -902,127 +904,70 @@ int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
 // their sorted camera lists (points seen by the same cameras become neighbours, so a point group
 // spans few cameras), observations point-major in that order.  The sort key is the list's first
 // cameras, as many as fit 64 bits at ceil(log2(C + 2)) bits each, at most 6 (lexicographic, a
-// shorter list first), ties keep the caller's order (an LSD radix sort is stable).  Fills pperm / operm (internal -> caller),
-// roc (internal observations) and pt_start.
-struct Ordered {   // the observed pixels are gathered in this order into the upload staging (load_problem)
-    std::vector<int> pperm, operm, roc, pt_start;
-    std::vector<int> start, obs, tmp;          // scratch, kept with the context between calls
-    std::vector<uint64_t> key, ktmp;
-    std::vector<uint32_t> cnt;
-};
+// shorter list first), ties keep the caller's order.  Its most significant field is the point's
+// smallest camera, so the order is the concatenation of camera BUCKETS (points whose smallest camera
+// lies in [BUCKET_CAMS b, BUCKET_CAMS (b + 1)); points without observations in bucket 0, first), each
+// sorted on its own: a bucket is ordered and grouped independently and kept between calls, and an
+// update (sfmx_ba_update, the SfM loop's grown scene) redoes only the buckets whose points changed
+// (HostScratch below).
+constexpr int BUCKET_CAMS = 8;
 
-void order_problem(const sfmx_ba_problem* pb, Ordered& od) {
-    const int P = pb->n_points, O = pb->n_obs, C = pb->n_cams;
+// The caller's observations as a point-major view: obs of point p are view positions
+// [start[p], start[p + 1]); position i is caller observation i (point-major input, pm) or vobs[i].
+struct View {
+    std::vector<int> start, vobs;
+    bool pm = true;
+    int obs(int64_t i) const { return pm ? (int)i : vobs[i]; }
+};
+void make_view(const sfmx_ba_problem* pb, View& v) {
+    const int P = pb->n_points, O = pb->n_obs;
     constexpr int PIECES = 64;   // fixed ranges (host_par.hpp): the same result on every host
-    std::vector<int>& start = od.start;
-    std::vector<int>& obs = od.obs;
-    start.resize(P + 1);
-    obs.resize(O);
-    // the reference adds residuals point by point (BundleAdjustment.cpp:50-91): obs[a] == a then,
-    // and start[] is where the point index steps (both in parallel ranges)
+    v.start.resize(P + 1);
     std::atomic<bool> pm{true};
     sfmx::parallel_ranges(O, PIECES, [&](int64_t i0, int64_t i1) {
         for (int64_t i = std::max<int64_t>(i0, 1); i < i1; ++i)
             if (pb->obs_point[i] < pb->obs_point[i - 1]) { pm = false; return; }
     });
-    const bool point_major = pm;
-    if (point_major) {
+    v.pm = pm;
+    if (v.pm) {   // the reference adds residuals point by point (BundleAdjustment.cpp:50-91)
         const int* op = pb->obs_point;
         sfmx::parallel_ranges((int64_t)O + 1, PIECES, [&](int64_t i0, int64_t i1) {
             for (int64_t i = i0; i < i1; ++i) {   // points (op[i - 1], op[i]] start at i
                 const int lo = i == 0 ? -1 : op[i - 1], hi = i == O ? P - 1 : op[i];
-                for (int p = lo + 1; p <= hi; ++p) start[p] = (int)i;
-                if (i < O) obs[i] = (int)i;
+                for (int p = lo + 1; p <= hi; ++p) v.start[p] = (int)i;
             }
         });
-        start[P] = O;
+        v.start[P] = O;
+        v.vobs.clear();
     } else {
-        std::fill(start.begin(), start.end(), 0);
-        for (int i = 0; i < O; ++i) start[pb->obs_point[i] + 1]++;
-        for (int p = 0; p < P; ++p) start[p + 1] += start[p];
-        std::vector<int> f(start.begin(), start.end() - 1);
-        for (int i = 0; i < O; ++i) obs[f[pb->obs_point[i]]++] = i;
+        std::fill(v.start.begin(), v.start.end(), 0);
+        for (int i = 0; i < O; ++i) v.start[pb->obs_point[i] + 1]++;
+        for (int p = 0; p < P; ++p) v.start[p + 1] += v.start[p];
+        std::vector<int> f(v.start.begin(), v.start.end() - 1);
+        v.vobs.resize(O);
+        for (int i = 0; i < O; ++i) v.vobs[f[pb->obs_point[i]]++] = i;
     }
-    int kb = 1;   // bits per camera (c + 1, 0 = none) and cameras per 64-bit key
-    while ((1ll << kb) < (long long)C + 2) ++kb;
-    const int nk = std::min(6, 64 / kb);
-    std::vector<uint64_t>& key = od.key;
-    key.resize(P);
-    sfmx::parallel_ranges(P, PIECES, [&](int64_t p0, int64_t p1) {
-        for (int64_t p = p0; p < p1; ++p) {
-            uint32_t lo[6] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u};   // the nk smallest cameras, sorted
-            for (int a = start[p]; a < start[p + 1]; ++a) {
-                uint32_t v = (uint32_t)pb->obs_cam[obs[a]];
-                for (int j = 0; j < nk; ++j)
-                    if (v < lo[j]) std::swap(v, lo[j]);
-            }
-            uint64_t k = 0;
-            for (int j = 0; j < nk; ++j) k = (k << kb) | (lo[j] == ~0u ? 0u : lo[j] + 1);
-            key[p] = k;
-        }
-    });
-    // LSD radix sort of (key, p) pairs over the key's nk * kb bits, 8 per pass (stable), passes whose
-    // digit is constant skipped; every pass counts and scatters in PIECES fixed ranges in parallel
-    // (per-range digit offsets, range-major within a digit: the stable order of a serial pass)
-    std::vector<int>& pperm = od.pperm;
-    pperm.resize(P);
-    sfmx::parallel_ranges(P, PIECES, [&](int64_t p0, int64_t p1) {
-        for (int64_t p = p0; p < p1; ++p) pperm[p] = (int)p;
-    });
-    {
-        std::vector<int>& tmp = od.tmp;
-        std::vector<uint64_t>& ktmp = od.ktmp;
-        std::vector<uint32_t>& cnt = od.cnt;   // [PIECES][256]
-        tmp.resize(P);
-        ktmp.resize(P);
-        cnt.resize(PIECES * 256);
-        const int np = (int)std::max<int64_t>(1, std::min<int64_t>(PIECES, P));
-        auto lo = [&](int i) { return (int64_t)P * i / np; };
-        for (int sh = 0; sh < nk * kb; sh += 8) {
-            sfmx::parallel_items(np, [&](int i) {
-                uint32_t* c = cnt.data() + 256 * (size_t)i;
-                std::fill(c, c + 256, 0u);
-                for (int64_t q = lo(i); q < lo(i + 1); ++q) c[(key[q] >> sh) & 0xff]++;
-            });
-            uint32_t tot[256] = {};
-            for (int i = 0; i < np; ++i)
-                for (int d = 0; d < 256; ++d) tot[d] += cnt[256 * (size_t)i + d];
-            bool one = false;
-            for (int d = 0; d < 256; ++d) one |= tot[d] == (uint32_t)P;
-            if (one) continue;
-            uint32_t run = 0;   // exclusive offsets, digit-major, range-minor
-            for (int d = 0; d < 256; ++d)
-                for (int i = 0; i < np; ++i) {
-                    const uint32_t v = cnt[256 * (size_t)i + d];
-                    cnt[256 * (size_t)i + d] = run;
-                    run += v;
-                }
-            sfmx::parallel_items(np, [&](int i) {
-                uint32_t* c = cnt.data() + 256 * (size_t)i;
-                for (int64_t q = lo(i); q < lo(i + 1); ++q) {
-                    const uint32_t j = c[(key[q] >> sh) & 0xff]++;
-                    tmp[j] = pperm[q];
-                    ktmp[j] = key[q];
-                }
-            });
-            pperm.swap(tmp);
-            key.swap(ktmp);
-        }
-    }
-    od.pt_start.assign(P + 1, 0);
-    for (int q = 0; q < P; ++q) od.pt_start[q + 1] = od.pt_start[q] + start[pperm[q] + 1] - start[pperm[q]];
-    od.operm.resize(O); od.roc.resize(O);
-    sfmx::parallel_ranges(P, PIECES, [&](int64_t q0, int64_t q1) {
-        for (int64_t q = q0; q < q1; ++q) {
-            const int p = pperm[q];
-            for (int a = start[p], k = od.pt_start[q]; a < start[p + 1]; ++a, ++k) {
-                const int o = obs[a];
-                od.operm[k] = o;
-                od.roc[k] = pb->obs_cam[o];
-            }
-        }
-    });
 }
+struct KeyBits { int kb, nk; };
+KeyBits key_bits(int C) {   // bits per camera (c + 1, 0 = none) and cameras per 64-bit key
+    int kb = 1;
+    while ((1ll << kb) < (long long)C + 2) ++kb;
+    return KeyBits{kb, std::min(6, 64 / kb)};
+}
+// the point's sort key and its smallest camera (-1: no observation)
+uint64_t point_key(const sfmx_ba_problem* pb, const View& v, int p, KeyBits kb, int* minc) {
+    uint32_t lo[6] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u};   // the nk smallest cameras, sorted
+    for (int a = v.start[p]; a < v.start[p + 1]; ++a) {
+        uint32_t c = (uint32_t)pb->obs_cam[v.obs(a)];
+        for (int j = 0; j < kb.nk; ++j)
+            if (c < lo[j]) std::swap(c, lo[j]);
+    }
+    uint64_t k = 0;
+    for (int j = 0; j < kb.nk; ++j) k = (k << kb.kb) | (lo[j] == ~0u ? 0u : lo[j] + 1);
+    *minc = lo[0] == ~0u ? -1 : (int)lo[0];
+    return k;
+}
+int bucket_of(int minc) { return minc < 0 ? 0 : minc / BUCKET_CAMS; }
 
 // Point groups, chunks, local cameras, assembly task lists and camera slot lists (see ba_group.hpp).
 struct TopoSeg;
@@ -1036,7 +981,6 @@ struct Topology {   // kept with the context: its vectors keep their capacity be
     std::vector<AEnt> ents;
     long long sg_total = 0, h_total = 0;
     int rg_total = 0, dp_max = 16;
-    std::vector<TopoSeg>* seg = nullptr;   // per-segment scratch (owned by the caller)
     void clear() {
         grp.clear(); chk.clear(); bat.clear(); gcam.clear(); cref_start.clear(); cref.clear(); lcrow.clear();
         tasks.clear(); ents.clear();
@@ -1160,8 +1104,8 @@ constexpr int SEG_PTS = 8192;
 // and their workgroups take about the same time, so a launch costs ceil(groups / slots) rounds
 // (slots = workgroups resident at once, from the device's occupancy of ba_glin).  C5 with 128-point
 // groups is 1564 groups on 512 slots: a fourth round for 28 workgroups.  The cap is the smallest
-// group size that keeps the rounds of full-size groups (in fixed SEG_PTS segments, as built below):
-// there, 99 points -> 2027 groups in 4 full rounds.  Camera limits can still cut groups earlier.
+// group size (a multiple of 8) that keeps the rounds of full-size groups (estimated on SEG_PTS
+// segments): there, 104 points -> ~1930 groups in 4 rounds.  Camera limits can still cut groups earlier.
 // Only problems of several rounds are re-sized, and never below GPTS / 2 points: a problem of one
 // round keeps full-size groups (the regime every small-problem parity test was pinned in).
 int group_points(int P, int slots) {
@@ -1173,43 +1117,15 @@ int group_points(int P, int slots) {
     };
     const int64_t rounds = (groups(GPTS) + slots - 1) / slots;
     if (rounds < 2) return GPTS;
-    for (int cap = std::max<int64_t>(GPTS / 2, P / (rounds * slots)); cap < GPTS; ++cap)
+    // caps in steps of 8 points: a growing scene (sfmx_ba_update) keeps its cap, so its unchanged
+    // buckets keep their groups, until the step no longer fits the rounds
+    for (int cap = (int)((std::max<int64_t>(GPTS / 2, P / (rounds * slots)) + 7) / 8 * 8); cap < GPTS; cap += 8)
         if (groups(cap) <= rounds * slots) return cap;
     return GPTS;
 }
 
-void build_topology(int P, int C, int O, int K, int gpts, const std::vector<int>& pt_start, const int* obs_cam, Topology& tp) {
-    tp.clear();
-    tp.obs_lc.assign(O, 0);
-    tp.obs_row.assign(O, 0);
-    const int nseg = std::max(1, (P + SEG_PTS - 1) / SEG_PTS);
-    std::vector<TopoSeg> own;
-    std::vector<TopoSeg>& seg = tp.seg ? *tp.seg : own;
-    if ((int)seg.size() < nseg) seg.resize(nseg);
-    sfmx::parallel_items(nseg, [&](int i) {
-        topo_segment(i * SEG_PTS, std::min(P, (i + 1) * SEG_PTS), K, gpts, pt_start, obs_cam, tp.obs_lc.data(),
-                     tp.obs_row.data(), seg[i]);
-    });
-    {   // merge: shift every segment's local offsets
-        size_t ng = 0, nc = 0, nb = 0, ngc = 0, nl = 0;
-        for (int i = 0; i < nseg; ++i) { const TopoSeg& g = seg[i]; ng += g.grp.size(); nc += g.chk.size(); nb += g.bat.size(); ngc += g.gcam.size(); nl += g.lcrow.size(); }
-        tp.grp.reserve(ng); tp.chk.reserve(nc); tp.bat.reserve(nb); tp.gcam.reserve(ngc); tp.lcrow.reserve(nl);
-        for (int i = 0; i < nseg; ++i) {
-            TopoSeg& g = seg[i];
-            const int cam0 = (int)tp.gcam.size(), ch0 = (int)tp.chk.size(), b0 = (int)tp.bat.size(), l0 = (int)tp.lcrow.size();
-            for (Grp G : g.grp) {
-                G.cam_off += cam0; G.ch0 += ch0; G.b0 += b0; G.rg_off += tp.rg_total;
-                if (G.big) G.h_off += tp.h_total; else G.sg_off += tp.sg_total;
-                tp.grp.push_back(G);
-            }
-            for (Chunk ch : g.chk) { ch.lc0 += l0; tp.chk.push_back(ch); }
-            tp.bat.insert(tp.bat.end(), g.bat.begin(), g.bat.end());
-            tp.gcam.insert(tp.gcam.end(), g.gcam.begin(), g.gcam.end());
-            tp.lcrow.insert(tp.lcrow.end(), g.lcrow.begin(), g.lcrow.end());
-            tp.rg_total += g.rg_total; tp.sg_total += g.sg_total; tp.h_total += g.h_total;
-            tp.dp_max = std::max(tp.dp_max, g.dp_max);
-        }
-    }
+// The camera slots and assembly tasks of the merged groups (tp.grp / gcam in internal order).
+void finish_topology(int C, int K, Topology& tp) {
     // camera slots: per camera, its (group, local camera) slots in group order
     std::vector<int> slot_g(tp.gcam.size());
     for (int g = 0; g < (int)tp.grp.size(); ++g)
@@ -1408,12 +1324,232 @@ void build_topology(int P, int C, int O, int K, int gpts, const std::vector<int>
 // parameters.  The factorization plan is kept when the camera co-visibility and the border are
 // unchanged (ensure_plan), else rebuilt at the next run.  Used by create and by sfmx_ba_update
 // (the reference's BundleAdjustment call after every registered camera, SfM.cpp:235 / :371).
+// A camera bucket's ordered points and point groups, kept between calls.  Offsets are local to the
+// bucket (points, observations) and to each sub-segment (groups never span SEG_PTS points).
+struct Bucket {
+    std::vector<int> pts;           // caller points in the internal order
+    std::vector<int> lpt;           // bucket-local pt_start (pts.size() + 1)
+    std::vector<int> roc, oin;      // per internal observation: its camera; its index within its point
+    std::vector<short> lc, row;     // obs_lc / obs_row (ba_group.hpp)
+    std::vector<int> sub;           // sub-segment starts in points (+ the end)
+    std::vector<TopoSeg> topo;      // per sub-segment, offsets local to the bucket / sub-segment
+    int no = 0;                     // observations
+    int64_t io0 = -1;               // its observations' offset in the device arrays of the last load (-1: none)
+    int64_t io0_new = 0;            // and in the layout being built
+    int ip0 = 0;                    // its first internal point
+    bool dirty = true;
+};
+// Caller-order copy of one block of SHB caller points: what an update compares to find changed points.
+constexpr int SHB = 4096;
+struct Shadow {
+    std::vector<int> cnt, oc;       // observations per point; their cameras
+    std::vector<double> xy;         // their pixels
+    bool valid = false;
+};
 struct HostScratch {
-    Ordered od;
-    Topology tp;
-    std::vector<TopoSeg> seg;
+    bool valid = false;             // the caches describe the last successfully loaded problem
+    int P = 0, K = 0, kb = 0, gpts = 0;
+    std::vector<int> pbucket;       // caller point -> bucket
+    std::vector<Bucket> bk;
+    std::vector<Shadow> sh;
+    View view;
+    Topology tp;                    // the merged topology of the last load
+    std::vector<int> pt_start;      // internal pt_start of the last load
+    int n_dirty = 0;                // buckets redone by the last load
+    double tm[8] = {};              // host_setup phases (ms): view, compare, bucket lists, order + groups, layout, merge, tasks, shadows
 };
 void destroy_scratch(HostScratch* h) { delete h; }
+
+// The host half of a load: the locality order and point groups of `pb`, redoing only the buckets
+// whose points changed since the last load described by hs (incremental: an unchanged point-major
+// problem prefix, the same K, key width and group size), then merged: tp (every group kernel's
+// topology), pperm (internal -> caller point), operm (internal -> caller observation), pt_start.  A
+// fresh load (incremental = false) runs every bucket through the same code, so both give the same
+// layout bit for bit (tests/test_ba_host.py).  hs.valid stays false until the caller confirms
+// the device half (load_problem).
+void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, HostScratch& hs, std::vector<int>& pperm,
+                std::vector<int>& operm) {
+    const int P = pb->n_points, C = pb->n_cams, O = pb->n_obs;
+    using clk = std::chrono::steady_clock;
+    auto tick = [t = clk::now()](double& slot) mutable {
+        const auto n = clk::now();
+        slot = std::chrono::duration<double, std::milli>(n - t).count();
+        t = n;
+    };
+    View& v = hs.view;
+    make_view(pb, v);
+    tick(hs.tm[0]);
+    const KeyBits kb = key_bits(C);
+    const int nbk = std::max(1, (C + BUCKET_CAMS - 1) / BUCKET_CAMS);
+    incremental = incremental && hs.valid && v.pm && hs.K == K && hs.kb == kb.kb && hs.gpts == gpts;
+    const int Pold = incremental ? hs.P : 0;
+    hs.valid = false;
+    if ((int)hs.bk.size() < nbk) hs.bk.resize(nbk);
+    for (int b = 0; b < (int)hs.bk.size(); ++b) hs.bk[b].dirty = !incremental || b >= nbk;
+    hs.pbucket.resize(std::max(P, Pold));
+    // changed points: per caller block, compare with the shadow; a changed point dirties its old
+    // and its new bucket
+    const int nblk_old = (Pold + SHB - 1) / SHB, nblk = (P + SHB - 1) / SHB;
+    hs.sh.resize(std::max(nblk, nblk_old));
+    std::vector<char> dirty(hs.bk.size(), incremental ? 0 : 1), bchanged(hs.sh.size(), 1);
+    std::mutex mu;
+    sfmx::parallel_items((int)hs.sh.size(), [&](int k) {
+        const int p0 = k * SHB, p1 = std::min(P, p0 + SHB), q1 = std::min(Pold, p0 + SHB);
+        Shadow& S = hs.sh[k];
+        std::vector<int> mark;   // buckets this block dirties
+        if (incremental && S.valid && p1 == q1) {
+            const int o0 = p0 < P ? v.start[p0] : O, o1 = p1 > p0 ? v.start[p1] : o0;
+            bool same = (int)S.oc.size() == o1 - o0;
+            for (int p = p0; same && p < p1; ++p) same = S.cnt[p - p0] == v.start[p + 1] - v.start[p];
+            same = same && std::memcmp(S.oc.data(), pb->obs_cam + o0, sizeof(int) * (size_t)(o1 - o0)) == 0 &&
+                   std::memcmp(S.xy.data(), pb->obs_xy + 2 * (size_t)o0, 16 * (size_t)(o1 - o0)) == 0;
+            if (same) { bchanged[k] = 0; return; }
+        }
+        // point by point (old contents from the shadow when it is valid)
+        std::vector<int> soff;
+        if (S.valid) {
+            soff.assign(S.cnt.size() + 1, 0);
+            for (size_t i = 0; i < S.cnt.size(); ++i) soff[i + 1] = soff[i] + S.cnt[i];
+        }
+        for (int p = p0; p < std::max(p1, incremental ? q1 : p1); ++p) {
+            const bool now = p < P, before = incremental && S.valid && p < q1;
+            bool same = now && before;
+            if (same) {
+                const int i = p - p0, n = v.start[p + 1] - v.start[p];
+                same = S.cnt[i] == n && std::memcmp(S.oc.data() + soff[i], pb->obs_cam + v.start[p], sizeof(int) * n) == 0 &&
+                       std::memcmp(S.xy.data() + 2 * (size_t)soff[i], pb->obs_xy + 2 * (size_t)v.start[p], 16 * (size_t)n) == 0;
+            }
+            if (same) continue;
+            if (incremental && p < Pold) mark.push_back(hs.pbucket[p]);
+            if (now) {
+                int minc;
+                point_key(pb, v, p, kb, &minc);
+                hs.pbucket[p] = bucket_of(minc);
+                mark.push_back(hs.pbucket[p]);
+            }
+        }
+        if (!mark.empty()) {
+            std::lock_guard<std::mutex> lk(mu);
+            for (int b : mark) dirty[b] = 1;
+        }
+    });
+    for (size_t b = 0; b < hs.bk.size(); ++b) hs.bk[b].dirty = hs.bk[b].dirty || dirty[b];
+    hs.pbucket.resize(P);
+    tick(hs.tm[1]);
+    // the dirty buckets' points, in caller order (ties of the sort keep it)
+    for (int b = 0; b < nbk; ++b) if (hs.bk[b].dirty) hs.bk[b].pts.clear();
+    for (int p = 0; p < P; ++p) {
+        Bucket& B = hs.bk[hs.pbucket[p]];
+        if (B.dirty) B.pts.push_back(p);
+    }
+    tick(hs.tm[2]);
+    // order + groups of every dirty bucket, in parallel
+    std::vector<int> todo;
+    for (int b = 0; b < nbk; ++b) if (hs.bk[b].dirty) todo.push_back(b);
+    hs.n_dirty = (int)todo.size();
+    sfmx::parallel_items((int)todo.size(), [&](int t) {
+        Bucket& B = hs.bk[todo[t]];
+        const int np = (int)B.pts.size();
+        std::vector<std::pair<uint64_t, int>> kp(np);
+        for (int i = 0; i < np; ++i) {
+            int minc;
+            kp[i] = {point_key(pb, v, B.pts[i], kb, &minc), B.pts[i]};
+        }
+        std::sort(kp.begin(), kp.end());   // (key, caller index): the stable order of the key
+        B.lpt.assign(np + 1, 0);
+        for (int i = 0; i < np; ++i) {
+            B.pts[i] = kp[i].second;
+            B.lpt[i + 1] = B.lpt[i] + v.start[B.pts[i] + 1] - v.start[B.pts[i]];
+        }
+        B.no = B.lpt[np];
+        B.roc.resize(B.no);
+        B.oin.resize(B.no);
+        for (int i = 0; i < np; ++i)
+            for (int a = v.start[B.pts[i]], k = B.lpt[i], j = 0; a < v.start[B.pts[i] + 1]; ++a, ++k, ++j) {
+                B.roc[k] = pb->obs_cam[v.obs(a)];
+                B.oin[k] = j;
+            }
+        B.lc.assign(B.no, 0);
+        B.row.assign(B.no, 0);
+        B.sub.clear();
+        for (int q = 0; q < np; q += SEG_PTS) B.sub.push_back(q);
+        B.sub.push_back(np);
+        B.topo.resize(B.sub.size() - 1);
+        for (size_t j = 0; j + 1 < B.sub.size(); ++j)
+            topo_segment(B.sub[j], B.sub[j + 1], K, gpts, B.lpt, B.roc.data(), B.lc.data(), B.row.data(), B.topo[j]);
+    });
+    hs.bk.resize(nbk);
+    tick(hs.tm[3]);
+    // layout: buckets in order
+    int ip = 0;
+    int64_t io = 0;
+    for (Bucket& B : hs.bk) { B.ip0 = ip; B.io0_new = io; ip += (int)B.pts.size(); io += B.no; }
+    // pperm, pt_start, operm: per bucket, in parallel
+    pperm.resize(P);
+    operm.resize(O);
+    std::vector<int>& pts = hs.pt_start;
+    pts.resize(P + 1);
+    pts[P] = O;
+    sfmx::parallel_items(nbk, [&](int b) {
+        const Bucket& B = hs.bk[b];
+        for (size_t i = 0; i < B.pts.size(); ++i) {
+            const int p = B.pts[i];
+            pperm[B.ip0 + i] = p;
+            pts[B.ip0 + i] = (int)(B.io0_new + B.lpt[i]);
+            for (int a = v.start[p], k = (int)B.io0_new + B.lpt[i]; a < v.start[p + 1]; ++a, ++k) operm[k] = v.obs(a);
+        }
+    });
+    tick(hs.tm[4]);
+    // merge the groups: bucket / sub-segment offsets -> internal ones
+    Topology& tp = hs.tp;
+    tp.clear();
+    for (const Bucket& B : hs.bk)
+        for (size_t j = 0; j < B.topo.size(); ++j) {
+            const TopoSeg& g = B.topo[j];
+            const int cam0 = (int)tp.gcam.size(), ch0 = (int)tp.chk.size(), b0 = (int)tp.bat.size(), l0 = (int)tp.lcrow.size();
+            const int dp = B.ip0, dobs = (int)B.io0_new;
+            for (Grp G : g.grp) {
+                G.o0 += dobs; G.o1 += dobs; G.p0 += dp; G.p1 += dp;
+                G.cam_off += cam0; G.ch0 += ch0; G.b0 += b0; G.rg_off += tp.rg_total;
+                if (G.big) G.h_off += tp.h_total; else G.sg_off += tp.sg_total;
+                tp.grp.push_back(G);
+            }
+            for (Chunk ch : g.chk) { ch.o0 += dobs; ch.o1 += dobs; ch.lc0 += l0; tp.chk.push_back(ch); }
+            for (Batch bt : g.bat) { bt.o0 += dobs; bt.o1 += dobs; bt.p0 += dp; bt.p1 += dp; tp.bat.push_back(bt); }
+            tp.gcam.insert(tp.gcam.end(), g.gcam.begin(), g.gcam.end());
+            tp.lcrow.insert(tp.lcrow.end(), g.lcrow.begin(), g.lcrow.end());
+            tp.rg_total += g.rg_total; tp.sg_total += g.sg_total; tp.h_total += g.h_total;
+            tp.dp_max = std::max(tp.dp_max, g.dp_max);
+        }
+    tick(hs.tm[5]);
+    finish_topology(C, K, tp);
+    tick(hs.tm[6]);
+    // shadows of the changed blocks (point-major problems only: the next update compares slices)
+    sfmx::parallel_items(nblk, [&](int k) {
+        Shadow& S = hs.sh[k];
+        if (!bchanged[k] && S.valid) return;
+        S.valid = v.pm;
+        if (!v.pm) return;
+        const int p0 = k * SHB, p1 = std::min(P, p0 + SHB), o0 = v.start[p0], o1 = v.start[p1];
+        S.cnt.resize(p1 - p0);
+        for (int p = p0; p < p1; ++p) S.cnt[p - p0] = v.start[p + 1] - v.start[p];
+        S.oc.assign(pb->obs_cam + o0, pb->obs_cam + o1);
+        S.xy.assign(pb->obs_xy + 2 * (size_t)o0, pb->obs_xy + 2 * (size_t)o1);
+    });
+    hs.sh.resize(nblk);
+    hs.P = P; hs.K = K; hs.kb = kb.kb; hs.gpts = gpts;
+    tick(hs.tm[7]);
+}
+
+// The global observation arrays of the merged layout (diagnostics / checks): obs_cam, obs_lc, obs_row.
+[[maybe_unused]] void gather_obs(const HostScratch& hs, int O, std::vector<int>& roc, std::vector<short>& lc, std::vector<short>& row) {
+    roc.resize(O); lc.resize(O); row.resize(O);
+    for (const Bucket& B : hs.bk) {
+        std::copy(B.roc.begin(), B.roc.end(), roc.begin() + B.io0_new);
+        std::copy(B.lc.begin(), B.lc.end(), lc.begin() + B.io0_new);
+        std::copy(B.row.begin(), B.row.end(), row.begin() + B.io0_new);
+    }
+}
 
 // ba_glin workgroups resident at once on this device (its occupancy at the launch's LDS size times
 // the CUs); 0 when unknown (then full-size groups)
@@ -1502,49 +1638,50 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     RC(intr_layout(caller, L));
     if (!c->hscr) c->hscr = new (std::nothrow) HostScratch();
     if (!c->hscr) return fail(SFMX_ENOMEM, "host allocation");
+    HostScratch& hs = *c->hscr;
+    const int P = caller->n_points, C = caller->n_cams, O = caller->n_obs, K = L.K;
+    // the previous load's device layout is reusable only if it completed
+    const bool incremental = c->loaded && hs.valid;
     c->loaded = false;
-    Ordered& od = c->hscr->od;
-    order_problem(caller, od);
+    const int slots = group_slots(c, K);
+    int gpts = group_points(P, slots);
+#ifdef SFMX_DIAG
+    if (const char* e = SFMX_DIAG_ENV("SFMX_BA_GPTS")) gpts = std::max(1, std::min(GPTS, std::atoi(e)));   // tiny-group tests
+    const bool force_fresh = SFMX_DIAG_ENV("SFMX_BA_FRESH") != nullptr;   // A/B: every load rebuilds every bucket
+#else
+    const bool force_fresh = false;
+#endif
+    host_setup(caller, K, gpts, incremental && !force_fresh, hs, c->pperm, c->operm);
+    Topology& tp = hs.tp;
+    const std::vector<int>& pt_start = hs.pt_start;
     c->setup_ms[5] = ms_since(t_start);
-    std::vector<int>& roc = od.roc;
-    c->pperm.swap(od.pperm);
-    c->operm.swap(od.operm);
     auto bail = [](int rc) { return rc; };
     // per-problem state starts over
     c->scaled = c->j_scaled = false;
     c->stage_off = 0;
-    const int P = caller->n_points, C = caller->n_cams, O = caller->n_obs;
     c->P = P; c->C = C; c->O = O;
-    c->K = L.K; c->intr_len = L.intr_len; c->multi = L.multi; c->cx = L.cx; c->cy = L.cy;
+    c->K = K; c->intr_len = L.intr_len; c->multi = L.multi; c->cx = L.cx; c->cy = L.cy;
     c->n_intr = caller->n_intr;
     c->isrc.swap(L.isrc);
     std::vector<int>& pim_h = L.pim;
     std::vector<double2>& pcc_h = L.pcc;
-    const int K = c->K;
     if (c->plan_K != K) c->planned = false;   // the border sizes S, W and the Schur terms
     c->ne = 3 * (int64_t)P;
     c->nf = 6 * C + K;
     c->n = c->ne + c->nf;
     c->RW = K + 1;
-    std::vector<int>& pt_start = od.pt_start;
-    Topology& tp = c->hscr->tp;
-    tp.seg = &c->hscr->seg;
-    const auto t_topo = clk::now();
-    const int slots = group_slots(c, K);
-    int gpts = group_points(P, slots);
-#ifdef SFMX_DIAG
-    if (const char* e = SFMX_DIAG_ENV("SFMX_BA_GPTS")) gpts = std::max(1, std::min(GPTS, std::atoi(e)));   // tiny-group tests
-#endif
-    build_topology(P, C, O, K, gpts, pt_start, roc.data(), tp);
 #ifdef SFMX_DIAG
     if (SFMX_DIAG_ENV("SFMX_BA_TRACE"))
-        fprintf(stderr, "sfmx ba: P %d slots %d points/group %d groups %zu dp_max %d\n", P, slots, gpts, tp.grp.size(), tp.dp_max);
+        fprintf(stderr, "sfmx ba: P %d slots %d points/group %d groups %zu dp_max %d buckets %zu redone %d\n", P, slots, gpts,
+                tp.grp.size(), tp.dp_max, hs.bk.size(), hs.n_dirty);
     {   // the diagnostic library checks every topology it uploads
+        std::vector<int> roc;
+        gather_obs(hs, O, roc, tp.obs_lc, tp.obs_row);
         const std::string why = check_topology(P, C, O, K, pt_start, roc.data(), tp);
         if (!why.empty()) return bail(fail(SFMX_EINTERNAL, "BA topology check: " + why));
     }
 #endif
-    c->setup_ms[6] = ms_since(t_topo);
+    c->setup_ms[6] = hs.n_dirty;   // buckets redone (the ordering's and the groups' ms are [5] and [0])
     // local camera co-visibility (the pose blocks this rank's points create)
     c->adj.assign((size_t)C * C, 0);
     for (const ATask& t : tp.tasks)
@@ -1582,44 +1719,87 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     hipStream_t st = c->st;
     int rc;
     const auto t_up = clk::now();
+    // Observation arrays (pixels, cameras, local camera, feature row) in the new layout, written into
+    // the second set of buffers and then swapped in: an unchanged bucket moves on the device
+    // (ba_relayout, 24 B per observation), a redone one is uploaded from the host.
+    std::vector<ObsMove> moves;
+    int64_t up_obs = 0;
+    for (const Bucket& B : hs.bk) {
+        if (!B.dirty && B.io0 >= 0) {
+            for (int64_t k = 0; k < B.no; k += RELAYOUT_CHUNK)
+                moves.push_back(ObsMove{B.io0 + k, B.io0_new + k, (int)std::min<int64_t>(RELAYOUT_CHUNK, B.no - k), 0});
+        } else {
+            up_obs += B.no;
+        }
+    }
     {   // every staged upload of this call (256-B rounded parts): one arena, no mid-call waits
         auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
-        const size_t total = r(16 * (size_t)O) + r(4 * (size_t)(P + 1)) + r(4 * (size_t)O) + 2 * r(2 * (size_t)O) +
-                             r(sizeof(Grp) * tp.grp.size()) + r(sizeof(Chunk) * tp.chk.size()) +
-                             r(sizeof(Batch) * tp.bat.size()) + r(4 * tp.gcam.size()) + r(4 * tp.lcrow.size()) +
-                             r(sizeof(ATask) * tp.tasks.size()) + r(sizeof(AEnt) * tp.ents.size()) +
-                             r(4 * tp.cref_start.size()) + r(4 * tp.cref.size()) + r(4 * pim_h.size()) +
-                             r(sizeof(double2) * pcc_h.size()) + r(24 * (size_t)P) + 4096;
+        size_t total = r(sizeof(ObsMove) * moves.size()) + r(4 * (size_t)(P + 1)) + r(sizeof(Grp) * tp.grp.size()) +
+                       r(sizeof(Chunk) * tp.chk.size()) + r(sizeof(Batch) * tp.bat.size()) + r(4 * tp.gcam.size()) +
+                       r(4 * tp.lcrow.size()) + r(sizeof(ATask) * tp.tasks.size()) + r(sizeof(AEnt) * tp.ents.size()) +
+                       r(4 * tp.cref_start.size()) + r(4 * tp.cref.size()) + r(4 * pim_h.size()) +
+                       r(sizeof(double2) * pcc_h.size()) + r(24 * (size_t)P) + 4096;
+        for (const Bucket& B : hs.bk)
+            if (B.dirty || B.io0 < 0) total += r(16 * (size_t)B.no) + r(4 * (size_t)B.no) + 2 * r(2 * (size_t)B.no);
         RC(stage_reserve(c, total));
     }
-    // observed pixels: gathered into the internal order while they are copied into the pinned
-    // staging arena (parallel host ranges, then one DMA; the caller's array is pageable)
-    RC(c->obs_xy.alloc(sizeof(double) * 2 * std::max<size_t>(O, 1)));
-    if (O) {
-        double2* h = static_cast<double2*>(stage_bytes(c, sizeof(double2) * (size_t)O));
+    const size_t so = std::max<size_t>(O, 1);
+    if ((rc = c->obs_xy_b.alloc(16 * so)) || (rc = c->obs_cam_b.alloc(4 * so)) || (rc = c->obs_lc_b.alloc(2 * so)) ||
+        (rc = c->obs_row_b.alloc(2 * so)))
+        return bail(rc);
+    if (!moves.empty()) {
+        ObsMove* h = static_cast<ObsMove*>(stage_bytes(c, sizeof(ObsMove) * moves.size()));
         if (!h) return bail(fail(SFMX_ENOMEM, "pinned staging buffer"));
+        std::memcpy(h, moves.data(), sizeof(ObsMove) * moves.size());
+        RC(c->moves.alloc(sizeof(ObsMove) * moves.size()));
+        HIPCHK(hipMemcpyAsync(c->moves.p, h, sizeof(ObsMove) * moves.size(), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(ba_relayout, dim3((unsigned)moves.size()), dim3(256), 0, st, c->moves.as<ObsMove>(),
+                           c->obs_xy.as<double2>(), c->obs_cam.as<int>(), c->obs_lc.as<short>(), c->obs_row.as<short>(),
+                           c->obs_xy_b.as<double2>(), c->obs_cam_b.as<int>(), c->obs_lc_b.as<short>(), c->obs_row_b.as<short>());
+        HIPCHK(hipGetLastError());
+    }
+    {   // the redone buckets: pixels gathered from the caller's array while copied into pinned staging
         const double2* xy = reinterpret_cast<const double2*>(caller->obs_xy);
         const int* om = c->operm.data();
-        sfmx::parallel_ranges(O, 64, [&](int64_t k0, int64_t k1) {
-            for (int64_t k = k0; k < k1; ++k) h[k] = xy[om[k]];
-        });
-        HIPCHK(hipMemcpyAsync(c->obs_xy.p, h, sizeof(double2) * (size_t)O, hipMemcpyHostToDevice, st));
+        for (const Bucket& B : hs.bk) {
+            if ((!B.dirty && B.io0 >= 0) || B.no == 0) continue;
+            double2* h = static_cast<double2*>(stage_bytes(c, 16 * (size_t)B.no));
+            int* hc = static_cast<int*>(stage_bytes(c, 4 * (size_t)B.no));
+            short* hl = static_cast<short*>(stage_bytes(c, 2 * (size_t)B.no));
+            short* hr = static_cast<short*>(stage_bytes(c, 2 * (size_t)B.no));
+            if (!h || !hc || !hl || !hr) return bail(fail(SFMX_ENOMEM, "pinned staging buffer"));
+            const int64_t o0 = B.io0_new;
+            sfmx::parallel_ranges(B.no, B.no >= 65536 ? 16 : 1, [&](int64_t k0, int64_t k1) {
+                for (int64_t k = k0; k < k1; ++k) h[k] = xy[om[o0 + k]];
+            });
+            std::memcpy(hc, B.roc.data(), 4 * (size_t)B.no);
+            std::memcpy(hl, B.lc.data(), 2 * (size_t)B.no);
+            std::memcpy(hr, B.row.data(), 2 * (size_t)B.no);
+            HIPCHK(hipMemcpyAsync(c->obs_xy_b.as<double2>() + o0, h, 16 * (size_t)B.no, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(c->obs_cam_b.as<int>() + o0, hc, 4 * (size_t)B.no, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(c->obs_lc_b.as<short>() + o0, hl, 2 * (size_t)B.no, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(c->obs_row_b.as<short>() + o0, hr, 2 * (size_t)B.no, hipMemcpyHostToDevice, st));
+        }
     }
+    std::swap(c->obs_xy, c->obs_xy_b);
+    std::swap(c->obs_cam, c->obs_cam_b);
+    std::swap(c->obs_lc, c->obs_lc_b);
+    std::swap(c->obs_row, c->obs_row_b);
+    c->setup_up_obs = up_obs;
     // the observations' points from the point-major CSR on the device (no upload of rop)
-    RC(c->obs_point.alloc(sizeof(int) * std::max<size_t>(O, 1)));
+    RC(c->obs_point.alloc(4 * so));
     if ((rc = upload(c, c->pt_start, pt_start))) return bail(rc);
     if (P && O) {
         hipLaunchKernelGGL(ba_obs_point, dim3(nblk(P)), dim3(256), 0, st, P, c->pt_start.as<int>(), c->obs_point.as<int>());
         HIPCHK(hipGetLastError());
     }
-    if ((rc = upload(c, c->obs_cam, roc)) || (rc = upload(c, c->grp, tp.grp)) || (rc = upload(c, c->chk, tp.chk)) || (rc = upload(c, c->bat, tp.bat)) ||
-        (rc = upload(c, c->gcam, tp.gcam)) || (rc = upload(c, c->obs_lc, tp.obs_lc)) ||
-        (rc = upload(c, c->obs_row, tp.obs_row)) || (rc = upload(c, c->lcrow, tp.lcrow)) ||
+    if ((rc = upload(c, c->grp, tp.grp)) || (rc = upload(c, c->chk, tp.chk)) || (rc = upload(c, c->bat, tp.bat)) ||
+        (rc = upload(c, c->gcam, tp.gcam)) || (rc = upload(c, c->lcrow, tp.lcrow)) ||
         (rc = upload(c, c->tasks, tp.tasks)) || (rc = upload(c, c->ents, tp.ents)) ||
         (rc = upload(c, c->cref_start, tp.cref_start)) || (rc = upload(c, c->cref, tp.cref)) ||
         (rc = upload(c, c->pim, pim_h)) || (rc = upload(c, c->pcc, pcc_h)))
         return bail(rc);
-    const size_t n = c->n, so = std::max(O, 1);
+    const size_t n = c->n;
     const size_t ncams = (size_t)C * ncp(K) + K * (K + 1) / 2 + K;
     struct { Buf* b; size_t bytes; } allocs[] = {
         {&c->x, 8 * n}, {&c->cand, 8 * n}, {&c->scale, 8 * n}, {&c->colsq, 8 * n}, {&c->colsq2, 8 * n},
@@ -1640,10 +1820,12 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     // scale = 1 until (and unless) Jacobi scaling sets it
     hipLaunchKernelGGL(ba_fill, dim3(nblk((int64_t)n)), dim3(256), 0, st, (int64_t)n, 1.0, c->scale.as<double>());
     HIPCHK(hipGetLastError());
-    if ((rc = set_params(c, caller))) return bail(rc);
+    if ((rc = set_params(c, caller))) return bail(rc);   // ends with a stream synchronisation
     c->setup_ms[2] = up_ms + ms_since(t_up2);
     c->setup_ms[3] = 0.0;
     c->setup_ms[4] = ms_since(t_start);
+    for (Bucket& B : hs.bk) { B.io0 = B.io0_new; B.dirty = false; }
+    hs.valid = true;
     c->loaded = true;
     return SFMX_OK;
 }
@@ -1945,17 +2127,69 @@ int sfmx_ba_jacobian(const sfmx_ba_problem* pb, int32_t device, double* r, doubl
 // diagnostic build only, no device needed: the host part of load_problem (locality order, point
 // groups / chunks / batches / assembly tasks at `gpts` points per group, 0 = GPTS) and
 // check_topology on it.  -> number of groups, or SFMX_EINTERNAL with the violation as last error.
-int sfmx_ba_debug_check_topology(const sfmx_ba_problem* pb, int32_t gpts) {
+// ms (optional, 3 entries): host time of the ordering + groups (host_setup), 0, and the check.
+int sfmx_ba_debug_check_topology(const sfmx_ba_problem* pb, int32_t gpts, double* ms) {
     RC(validate(pb));
-    Ordered od;
-    order_problem(pb, od);
-    Topology tp;
-    const int K = pb->n_intr ? 7 : pb->cam_model;
-    build_topology(pb->n_points, pb->n_cams, pb->n_obs, K, gpts > 0 ? std::min(gpts, GPTS) : GPTS, od.pt_start,
-                   od.roc.data(), tp);
-    const std::string why = check_topology(pb->n_points, pb->n_cams, pb->n_obs, K, od.pt_start, od.roc.data(), tp);
+    IntrLayout L;
+    RC(intr_layout(pb, L));
+    using clk = std::chrono::steady_clock;
+    auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto t0 = clk::now();
+    HostScratch hs;
+    std::vector<int> pperm, operm, roc;
+    host_setup(pb, L.K, gpts > 0 ? std::min(gpts, GPTS) : GPTS, false, hs, pperm, operm);
+    const auto t1 = clk::now();
+    gather_obs(hs, pb->n_obs, roc, hs.tp.obs_lc, hs.tp.obs_row);
+    const std::string why = check_topology(pb->n_points, pb->n_cams, pb->n_obs, L.K, hs.pt_start, roc.data(), hs.tp);
+    if (ms) { ms[0] = d(t0, t1); ms[1] = 0.0; ms[2] = d(t1, clk::now()); }
     if (!why.empty()) return fail(SFMX_EINTERNAL, "BA topology check: " + why);
-    return (int)tp.grp.size();
+    return (int)hs.tp.grp.size();
+}
+
+// The host half of an update against a fresh load: problem a, then b on the same host caches (the
+// incremental path), must give b's fresh layout exactly (orders, observation permutation, every
+// topology array); -> buckets the update redid (out[0]) and all buckets (out[1]), or SFMX_EINTERNAL
+// naming the first difference.  ms (optional, 10): the update's and the fresh load's host time, then
+// the update's phases (HostScratch::tm).
+int sfmx_ba_debug_incremental_check(const sfmx_ba_problem* a, const sfmx_ba_problem* b, int32_t gpts, int32_t* out,
+                                    double* ms) {
+    RC(validate(a));
+    RC(validate(b));
+    IntrLayout La, Lb;
+    RC(intr_layout(a, La));
+    RC(intr_layout(b, Lb));
+    const int g = gpts > 0 ? std::min(gpts, GPTS) : GPTS;
+    using clk = std::chrono::steady_clock;
+    auto d = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    HostScratch inc, fr;
+    std::vector<int> pp, op, pp2, op2;
+    host_setup(a, La.K, g, false, inc, pp, op);
+    for (Bucket& B : inc.bk) { B.io0 = B.io0_new; B.dirty = false; }
+    inc.valid = true;
+    const auto t0 = clk::now();
+    host_setup(b, Lb.K, g, true, inc, pp, op);
+    const auto t1 = clk::now();
+    host_setup(b, Lb.K, g, false, fr, pp2, op2);
+    const auto t2 = clk::now();
+    if (ms) { ms[0] = d(t0, t1); ms[1] = d(t1, t2); for (int i = 0; i < 8; ++i) ms[2 + i] = inc.tm[i]; }
+    if (out) { out[0] = inc.n_dirty; out[1] = (int)inc.bk.size(); }
+    auto bytes = [](const auto& x, const auto& y) {
+        return x.size() == y.size() && (x.empty() || std::memcmp(x.data(), y.data(), sizeof(x[0]) * x.size()) == 0);
+    };
+    const Topology &ti = inc.tp, &tf = fr.tp;
+    std::vector<int> ri, rf;
+    std::vector<short> li, lf, wi, wf;
+    gather_obs(inc, b->n_obs, ri, li, wi);
+    gather_obs(fr, b->n_obs, rf, lf, wf);
+    const char* diff = !bytes(pp, pp2) ? "pperm" : !bytes(op, op2) ? "operm" : !bytes(inc.pt_start, fr.pt_start) ? "pt_start"
+                     : !bytes(ri, rf) ? "obs_cam" : !bytes(li, lf) ? "obs_lc" : !bytes(wi, wf) ? "obs_row"
+                     : !bytes(ti.grp, tf.grp) ? "groups" : !bytes(ti.chk, tf.chk) ? "chunks" : !bytes(ti.bat, tf.bat) ? "batches"
+                     : !bytes(ti.gcam, tf.gcam) ? "gcam" : !bytes(ti.lcrow, tf.lcrow) ? "lcrow" : !bytes(ti.tasks, tf.tasks) ? "tasks"
+                     : !bytes(ti.ents, tf.ents) ? "ents" : !bytes(ti.cref, tf.cref) ? "cref" : !bytes(ti.cref_start, tf.cref_start) ? "cref_start"
+                     : (ti.sg_total != tf.sg_total || ti.h_total != tf.h_total || ti.rg_total != tf.rg_total || ti.dp_max != tf.dp_max) ? "totals"
+                     : nullptr;
+    if (diff) return fail(SFMX_EINTERNAL, std::string("incremental layout differs from the fresh one: ") + diff);
+    return SFMX_OK;
 }
 #endif
 

@@ -185,11 +185,13 @@ class BAContext:
         self.problem = problem
 
     def setup_ms(self) -> dict:
-        """Host-side setup of the last create / update (ms)."""
+        """Host-side setup of the last create / update (ms): ordering + groups (of the camera buckets
+        that changed), device allocation, uploads, factorization plan, total; plus ``buckets_redone``
+        (a count: the buckets an update re-ordered, include/sfmx_ba.h sfmx_ba_setup_ms)."""
         v = (C.c_double * 7)()
         n = check(lib.sfmx_ba_setup_ms(self._h, v, 7), "sfmx_ba_setup_ms")
-        return {k: v[i] for i, k in enumerate(["order_groups", "alloc", "upload", "plan", "total", "order",
-                                                "groups"][:n])}
+        return {k: v[i] for i, k in enumerate(["order_groups", "alloc", "upload", "plan", "total", "host_setup",
+                                                "buckets_redone"][:n])}
 
     def reset(self, problem: Optional[BAProblem] = None):
         st = (problem or self.problem).struct()

@@ -195,6 +195,27 @@ def ba_registered(p: dict, n_cams: int) -> dict:
     return out
 
 
+def ba_sfm_order(p: dict) -> dict:
+    """The same problem with its points in the order an incremental SfM creates them (SfM.cpp:235 /
+    :371, cameras registered in index order): a point is triangulated when its second camera is
+    registered, and the scene appends it then (ties: the original order); each point's observations
+    in registration order.  ba_registered(ba_sfm_order(p), n) is the scene after n registrations."""
+    obs_point, obs_cam = np.asarray(p["obs_point"]), np.asarray(p["obs_cam"])
+    P = len(p["points"])
+    o = np.lexsort((obs_cam, obs_point))                  # per point, cameras ascending
+    op, oc = obs_point[o], obs_cam[o]
+    start = np.searchsorted(op, np.arange(P + 1))
+    cnt = np.diff(start)
+    second = np.where(cnt >= 2, oc[np.minimum(start[:-1] + 1, len(oc) - 1)], np.iinfo(np.int32).max)
+    pord = np.lexsort((np.arange(P), second))             # new point i = old point pord[i]
+    rank = np.empty(P, np.int64)
+    rank[pord] = np.arange(P)
+    o2 = np.lexsort((oc, rank[op]))
+    out = dict(p, points=np.asarray(p["points"])[pord], obs_point=rank[op][o2].astype(np.int32),
+               obs_cam=oc[o2].astype(np.int32), obs_xy=np.asarray(p["obs_xy"])[o][o2])
+    return out
+
+
 def ba_problem_multi(n_cams: int = 24, n_points: int = 3000, cameras=((3, 1.0), (3, 1.1)), obs_per_point: int = 6,
                      noise_px: float = 0.5, seed: int = BA_SEED + 7, width: int = 720, height: int = 405,
                      perturb: bool = True, pose_intr=None):

@@ -87,5 +87,64 @@ def test_point_group_topology_holds_every_kernel_bound(case, gpts):
     from sfmx import _lib
     P = _ragged_problem(**TOPO_CASES[case])
     st = P.struct()
-    n = diag_lib().sfmx_ba_debug_check_topology(st, gpts)
+    n = diag_lib().sfmx_ba_debug_check_topology(st, gpts, None)
     assert n > 0, _lib.lib.sfmx_last_error() or diag_lib().sfmx_last_error()
+
+
+# ---- the incremental update's host half (sfmx_ba_update: unchanged camera buckets are kept) ----
+
+def _inc_check(a, b, gpts=0):
+    import ctypes as C
+    from diag import diag_lib
+    from sfmx import _lib
+    out = (C.c_int32 * 2)()
+    ms = (C.c_double * 10)()
+    Pa, Pb = ba.BAProblem(**a), ba.BAProblem(**b)
+    rc = diag_lib().sfmx_ba_debug_incremental_check(Pa.struct(), Pb.struct(), gpts, out, ms)
+    assert rc == 0, diag_lib().sfmx_last_error()
+    return out[0], out[1]
+
+
+def test_sfm_order_is_a_permutation_of_the_same_problem():
+    p = synth.ba_problem(30, 3000, seed=5)
+    q = synth.ba_sfm_order(p)
+    assert np.all(np.diff(q["obs_point"]) >= 0)
+    key = lambda d: sorted(zip(map(tuple, np.round(np.asarray(d["points"])[d["obs_point"]], 12)), d["obs_cam"],
+                               map(tuple, d["obs_xy"])))
+    assert key(p) == key(q)
+
+
+@pytest.mark.parametrize("steps", [(20, 40), (40, 41), (60, 80), (199, 200), (180, 200)])
+def test_incremental_layout_equals_fresh_on_a_growing_scene(steps):
+    """the grown scene's layout from the kept buckets equals a fresh load's
+    bit for bit (orders, permutations, every topology array), and an SfM-ordered growth by one
+    camera redoes only the buckets near the new camera (plus the ring's closing bucket)."""
+    base = synth.ba_sfm_order(synth.ba_problem(200, 20000, seed=7))
+    n_dirty, n_all = _inc_check(synth.ba_registered(base, steps[0]), synth.ba_registered(base, steps[1]))
+    if steps[1] - steps[0] == 1:
+        assert n_dirty <= 3, (n_dirty, n_all)
+
+
+@pytest.mark.parametrize("case", ["xy", "points_gone", "cams_shrink", "not_point_major", "K_change", "same"])
+def test_incremental_layout_equals_fresh_on_edits(case):
+    rng = np.random.default_rng(11)
+    a = synth.ba_sfm_order(synth.ba_problem(60, 8000, seed=12))
+    b = dict(a)
+    if case == "xy":            # a few pixels re-measured: their buckets redone
+        xy = np.array(a["obs_xy"]); xy[rng.integers(0, len(xy), 5)] += 0.25; b["obs_xy"] = xy
+    elif case == "points_gone":  # the last points dropped
+        keep = a["obs_point"] < 7000
+        b = dict(a, points=a["points"][:7000], obs_point=a["obs_point"][keep], obs_cam=a["obs_cam"][keep],
+                 obs_xy=a["obs_xy"][keep])
+    elif case == "cams_shrink":
+        b = synth.ba_registered(a, 30)
+    elif case == "not_point_major":
+        perm = rng.permutation(len(a["obs_point"]))
+        b = dict(a, obs_point=a["obs_point"][perm], obs_cam=a["obs_cam"][perm], obs_xy=a["obs_xy"][perm])
+    elif case == "K_change":
+        b = dict(a, cam_model=1, intr=a["intr"][:1])
+    n_dirty, n_all = _inc_check(a, b)
+    if case == "same":
+        assert n_dirty == 0
+    if case == "xy":
+        assert 1 <= n_dirty <= 5

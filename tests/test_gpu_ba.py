@@ -388,3 +388,39 @@ def test_tiny_point_groups_after_differently_sized_solves():
         n = min(len(tr), len(otr))
         assert np.array_equal(tr[:n, 2], otr[:n, 2]), gpts
         assert np.array_equal(tr[:, 2], tp_[:, 2]) and abs(sm["final_cost"] - sp["final_cost"]) <= 1e-9 * sp["final_cost"]
+
+
+def test_incremental_updates_keep_buckets_and_equal_fresh_contexts():
+    """the SfM loop's grown scene (points in creation order, one more camera per
+    call, then a re-measured pixel) through one context: each update redoes only the camera buckets
+    that changed, moves the others' observation data on the device, and solves to the bits of a
+    fresh context on the same problem."""
+    base = synth.ba_sfm_order(synth.ba_problem(48, 9000, seed=69))
+    seq = [synth.ba_registered(base, n) for n in (40, 41, 42, 48)]
+    edit = dict(seq[-1])
+    xy = np.array(edit["obs_xy"]); xy[17] += 0.5; edit["obs_xy"] = xy
+    seq.append(edit)
+    ctx = None
+    redone = []
+    try:
+        for p in seq:
+            P = ba.BAProblem(**p)
+            if ctx is None:
+                ctx = ba.BAContext(P)
+            else:
+                ctx.update(P)
+            s1, t1 = ctx.run(trace_cap=256)
+            redone.append(ctx.setup_ms()["buckets_redone"])
+            ctx.get(P)
+            ref = ba.BAContext(ba.BAProblem(**p))
+            try:
+                s2, t2 = ref.run(trace_cap=256)
+                R = ref.get()
+            finally:
+                ref.close()
+            assert s1["final_cost"] == s2["final_cost"] and np.array_equal(t1, t2)
+            assert np.array_equal(P.points, R.points) and np.array_equal(P.poses, R.poses) and np.array_equal(P.intr, R.intr)
+    finally:
+        if ctx is not None:
+            ctx.close()
+    assert redone[1] < 6 and redone[2] < 6 and redone[4] <= 2, redone   # of 6 buckets (48 cameras / 8)
