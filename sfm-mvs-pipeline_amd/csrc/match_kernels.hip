@@ -2069,7 +2069,8 @@ hipError_t launch_two_pass_overlap(bool sift, const MatchBatch* b, int nb, const
     for (int i = 0; i < nb; ++i) {
         const MatchBatch& B = b[i];
         hipStream_t s = (i & 1) ? os.sx : st;
-        if (sift)
+        if (B.nw == 0) {}   // no screen items (fp32 / empty-left pairs only): pass 2 finds qcount 0
+        else if (sift)
             sift_screen16_kernel<8, 4, 2, 64, true><<<B.nw, 256, 0, s>>>(work + B.w0, pairs, imgs, desc, norm, keyc,
                                                                          out_idx, out_dist, qlist, qcount, ratio, qmask, top2);
         else

@@ -434,7 +434,7 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
                 cur.nw += items;
                 cur.np += 1;
                 w += items;
-                if (cur.nw >= per && i + 1 < n_pairs) {
+                if (cur.nw >= per && i + 1 < n_pairs && w < work.size()) {   // (trailing no-work pairs join the last batch)
                     m->batches.push_back(cur);
                     cur = MatchBatch{(int32_t)w, 0, i + 1, 0};
                 }

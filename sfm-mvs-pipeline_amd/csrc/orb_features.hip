@@ -63,6 +63,25 @@ static_assert(sizeof(Kp) == sizeof(sfmx_keypoint), "cv::KeyPoint layout");
 
 struct AxisEnt { int32_t ofs; uint16_t m0, m1; };
 
+// Batched launches (r04): a chunk of G same-size images runs as ONE set of launches, image g's
+// per-image arrays at byte offset g * istride from image 0's (one scratch block per image, the
+// layout of the one-image arena), its counters at stats + g * CS.  r03 issued ~22 launches, 3
+// pageable uploads and one host wait per image from 8 host threads: the leg was host-bound.
+struct ImgIO {             // per image of a chunk
+    const uint8_t* img;    // the 8-bit input (device), pitch bytes per row
+    int64_t pitch;
+    Kp* kp_out;            // device keypoints (inputs_on_device) or nullptr
+    uint8_t* desc_out;     // descriptor rows (the caller's device buffer or the image's staging)
+    int32_t capacity, pad;
+};
+constexpr int CS = 2 * MAX_LEVELS + 4;   // stats ints per image: cnt1[16] | cnt2[16] | count, levels, corners, err
+template <class T>
+__device__ __forceinline__ T* at(T* p, int64_t bo) { return reinterpret_cast<T*>(reinterpret_cast<char*>(p) + bo); }
+template <class T>
+__device__ __forceinline__ const T* at(const T* p, int64_t bo) {
+    return reinterpret_cast<const T*>(reinterpret_cast<const char*>(p) + bo);
+}
+
 __constant__ int c_pattern[256 * 4] = {
 #include "orb_pattern.inc"
 };
@@ -83,7 +102,8 @@ __device__ __forceinline__ uint32_t hval(const uint8_t* __restrict__ r, const Ax
 
 __global__ __launch_bounds__(256)
 void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int l,
-                       const AxisEnt* __restrict__ tables) {
+                       const AxisEnt* __restrict__ tables, int64_t istride) {
+    pyr = at(pyr, (int64_t)blockIdx.z * istride);
     const Lvl D = lv[l], S = lv[l - 1];
     const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x >= D.w || y >= D.h) return;
@@ -104,8 +124,11 @@ void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, in
     pyr[D.off + (int64_t)y * D.w + x] = (uint8_t)min(v, 255u);
 }
 
-__global__ void orb_copy_kernel(const uint8_t* __restrict__ img, int W, int H, int64_t pitch, uint8_t* __restrict__ dst) {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+__global__ void orb_copy_kernel(const ImgIO* __restrict__ io, int W, int H, uint8_t* __restrict__ dst, int64_t istride) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, g = blockIdx.z;
+    const uint8_t* img = io[g].img;
+    const int64_t pitch = io[g].pitch;
+    dst = at(dst, (int64_t)g * istride);
     if (x < W && y < H) dst[(int64_t)y * W + x] = img[(int64_t)y * pitch + x];
 }
 
@@ -116,8 +139,11 @@ __constant__ int8_t c_ring[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3,
 
 __global__ __launch_bounds__(256)
 void orb_fast_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int threshold,
-                     uint8_t* __restrict__ score) {
-    const Lvl L = lv[blockIdx.z];
+                     uint8_t* __restrict__ score, int nl, int64_t istride) {
+    const int64_t bo = (int64_t)(blockIdx.z / nl) * istride;   // z = image * nl + level
+    pyr = at(pyr, bo);
+    score = at(score, bo);
+    const Lvl L = lv[blockIdx.z % nl];
     const int x0 = blockIdx.x * FT_X, y0 = blockIdx.y * FT_Y;
     if (x0 >= L.w || y0 >= L.h) return;
     __shared__ uint8_t t[FT_Y + 2 * FT_H][FT_X + 2 * FT_H + 2];
@@ -194,9 +220,17 @@ __device__ __forceinline__ int find_level(const Lvl* lv, int nl, int row) {
 __global__ __launch_bounds__(256)
 void orb_nms_kernel(const uint8_t* __restrict__ score, const Lvl* __restrict__ lv, int nl, int border, int pass,
                     int* __restrict__ row_count, const int* __restrict__ row_off, int32_t* __restrict__ cpos,
-                    uint8_t* __restrict__ cscore, int cap) {
+                    uint8_t* __restrict__ cscore, int cap, int64_t istride) {
     __shared__ int wsum[4];
     const int row = blockIdx.x;
+    {
+        const int64_t bo = (int64_t)blockIdx.y * istride;
+        score = at(score, bo);
+        if (row_count) row_count = at(row_count, bo);
+        if (row_off) row_off = at(row_off, bo);
+        if (cpos) cpos = at(cpos, bo);
+        if (cscore) cscore = at(cscore, bo);
+    }
     const int l = find_level(lv, nl, row);
     const Lvl L = lv[l];
     const int y = row - L.row0;
@@ -242,8 +276,11 @@ void orb_nms_kernel(const uint8_t* __restrict__ score, const Lvl* __restrict__ l
 
 // exclusive scan of n row counts into off[0..n] (one workgroup)
 __global__ __launch_bounds__(1024)
-void orb_scan_kernel(const int* __restrict__ cnt, int n, int* __restrict__ off) {
+void orb_scan_kernel(const int* __restrict__ cnt, int n, int* __restrict__ off, int64_t istride, int* __restrict__ stats) {
     __shared__ int part[1024];
+    cnt = at(cnt, (int64_t)blockIdx.x * istride);
+    off = at(off, (int64_t)blockIdx.x * istride);
+    if (threadIdx.x == 0) stats[(int64_t)blockIdx.x * CS + 2 * MAX_LEVELS + 3] = 0;   // retainBest's error flag
     const int per = (n + 1023) / 1024;
     const int b = threadIdx.x * per, e = min(b + per, n);
     int s = 0;
@@ -471,9 +508,21 @@ __global__ __launch_bounds__(RT)
 void orb_retain_kernel(int mode, const Lvl* __restrict__ lv, const int* __restrict__ row_off,
                        const uint8_t* __restrict__ cscore, Resp* __restrict__ A, Resp* __restrict__ B,
                        int* __restrict__ Ls, int* __restrict__ Rs, const int* __restrict__ cnt_in,
-                       int* __restrict__ cnt_out, SelCounts sel, int cap, int* __restrict__ err) {
+                       int* __restrict__ cnt_out, SelCounts sel, int cap, int* __restrict__ err, int64_t istride) {
     __shared__ int sh[36];
-    const int l = blockIdx.x, t = threadIdx.x;
+    const int l = blockIdx.x, t = threadIdx.x, g = blockIdx.y;
+    {   // image g: its arrays and its counters (cnt_in / cnt_out / err are offsets into the stats rows)
+        const int64_t bo = (int64_t)g * istride;
+        row_off = at(row_off, bo);
+        cscore = at(cscore, bo);
+        A = at(A, bo);
+        B = at(B, bo);
+        Ls = at(Ls, bo);
+        Rs = at(Rs, bo);
+        if (cnt_in) cnt_in += (int64_t)g * CS;
+        cnt_out += (int64_t)g * CS;
+        err += (int64_t)g * CS;
+    }
     const Lvl L = lv[l];
     const int c0 = min(lvl_first(row_off, L), cap);   // (the corner count never exceeds cap: one per 2 x 2 cell)
     int m;
@@ -495,8 +544,17 @@ void orb_retain_kernel(int mode, const Lvl* __restrict__ lv, const int* __restri
 __global__ __launch_bounds__(256)
 void orb_harris_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const int* __restrict__ row_off,
                        const Resp* __restrict__ A, const int* __restrict__ cnt1, const int32_t* __restrict__ cpos,
-                       Resp* __restrict__ B) {
+                       Resp* __restrict__ B, int64_t istride) {
     const int l = blockIdx.y;
+    {
+        const int64_t bo = (int64_t)blockIdx.z * istride;
+        pyr = at(pyr, bo);
+        row_off = at(row_off, bo);
+        A = at(A, bo);
+        cnt1 += (int64_t)blockIdx.z * CS;
+        cpos = at(cpos, bo);
+        B = at(B, bo);
+    }
     const Lvl L = lv[l];
     const int c0 = lvl_first(row_off, L), m = cnt1[l];
     const uint8_t* img = pyr + L.off;
@@ -554,8 +612,19 @@ __global__ __launch_bounds__(256)
 void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int nl,
                       const int* __restrict__ row_off, const Resp* __restrict__ A, const Resp* __restrict__ B,
                       const int* __restrict__ cnt2, const int32_t* __restrict__ cpos, const int* __restrict__ umax,
-                      int width, int height, int border, Kp* __restrict__ out, int* __restrict__ keep) {
+                      int width, int height, int border, Kp* __restrict__ out, int* __restrict__ keep, int64_t istride) {
     const int lane = threadIdx.x & 63;
+    {
+        const int64_t bo = (int64_t)blockIdx.y * istride;
+        pyr = at(pyr, bo);
+        row_off = at(row_off, bo);
+        A = at(A, bo);
+        B = at(B, bo);
+        cnt2 += (int64_t)blockIdx.y * CS;
+        cpos = at(cpos, bo);
+        out = at(out, bo);
+        keep = at(keep, bo);
+    }
     int total = 0;
     for (int l = 0; l < nl; ++l) total += cnt2[l];
     for (int f = blockIdx.x * 4 + (threadIdx.x >> 6); f < total; f += gridDim.x * 4) {
@@ -603,9 +672,19 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
 // levels the descriptors read (max octave + 1), st[2] = the corner total (overflow check)
 __global__ __launch_bounds__(RT)
 void orb_compact_kernel(const Kp* __restrict__ in, const int* __restrict__ keep, const int* __restrict__ cnt2, int nl,
-                        const int* __restrict__ row_off, int rows, Kp* __restrict__ out, int* __restrict__ st) {
+                        const int* __restrict__ row_off, int rows, Kp* __restrict__ out, int* __restrict__ st,
+                        int64_t istride) {
     __shared__ int sh[36];
     const int t = threadIdx.x;
+    {
+        const int64_t bo = (int64_t)blockIdx.x * istride;
+        in = at(in, bo);
+        keep = at(keep, bo);
+        cnt2 += (int64_t)blockIdx.x * CS;
+        row_off = at(row_off, bo);
+        out = at(out, bo);
+        st += (int64_t)blockIdx.x * CS;
+    }
     int total = 0;
     for (int l = 0; l < nl; ++l) total += cnt2[l];
     const int chunk = (total + RT - 1) / RT, s = min(t * chunk, total), e = min(s + chunk, total);
@@ -635,8 +714,12 @@ void orb_compact_kernel(const Kp* __restrict__ in, const int* __restrict__ keep,
 }
 
 __global__ __launch_bounds__(256)
-void orb_copy_kp_kernel(const Kp* __restrict__ src, const int* __restrict__ st, int capacity, Kp* __restrict__ dst) {
-    const int m = min(st[0], capacity);
+void orb_copy_kp_kernel(const Kp* __restrict__ src, const int* __restrict__ st, const ImgIO* __restrict__ io,
+                        int64_t istride) {
+    const int g = blockIdx.y;
+    src = at(src, (int64_t)g * istride);
+    Kp* dst = io[g].kp_out;
+    const int m = min(st[(int64_t)g * CS], io[g].capacity);
     for (int i = blockIdx.x * 256 + threadIdx.x; i < m; i += gridDim.x * 256) dst[i] = src[i];
 }
 
@@ -654,9 +737,12 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 
 __global__ __launch_bounds__(256)
 void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const int* __restrict__ st,
-                     uint8_t* __restrict__ blur) {
-    if ((int)blockIdx.z >= st[1]) return;   // only the levels the kept keypoints use
-    const Lvl L = lv[blockIdx.z];
+                     uint8_t* __restrict__ blur, int nl, int64_t istride) {
+    const int g = blockIdx.z / nl, l = blockIdx.z % nl;   // z = image * nl + level
+    if (l >= st[(int64_t)g * CS + 1]) return;   // only the levels the kept keypoints use
+    pyr = at(pyr, (int64_t)g * istride);
+    blur = at(blur, (int64_t)g * istride);
+    const Lvl L = lv[l];
     const int x0 = blockIdx.x * BT_X, y0 = blockIdx.y * BT_Y;
     if (x0 >= L.w || y0 >= L.h) return;
     __shared__ uint8_t t[BT_Y + 2 * BR][BT_X + 2 * BR + 2];
@@ -714,8 +800,13 @@ __device__ void orb_sincos(double x, double* s, double* c) {
 // pattern pairs 8 i .. 8 i + 7; min(count, capacity) keypoints
 __global__ __launch_bounds__(256)
 void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ lv, const Kp* __restrict__ kps,
-                      const int* __restrict__ st, int capacity, uint8_t* __restrict__ desc) {
-    const int n = min(st[0], capacity), i = threadIdx.x & 31;
+                      const int* __restrict__ st, const ImgIO* __restrict__ io, int64_t istride) {
+    const int g = blockIdx.y;
+    blur = at(blur, (int64_t)g * istride);
+    kps = at(kps, (int64_t)g * istride);
+    uint8_t* desc = io[g].desc_out;
+    if (!desc) return;   // this image's caller passed no descriptor buffer
+    const int n = min(st[(int64_t)g * CS], io[g].capacity), i = threadIdx.x & 31;
     for (int j = blockIdx.x * 8 + (threadIdx.x >> 5); j < n; j += gridDim.x * 8) {
         const Kp k = kps[j];
         const Lvl L = lv[k.octave];
@@ -890,20 +981,45 @@ float sfmx_orb_last_kernel_ms(void) { return g_last_ms; }
 namespace {
 
 struct Scratch {            // image-size buffers / corner-count buffers, grown on demand
-    Arena img, kp;
+    Arena img;
+    char* pin = nullptr;    // pinned staging: the chunk's tables / levels / umax / ImgIO up, its stats down
+    size_t pin_cap = 0;
+    int pin_dev = -1;
+    bool pin_reserve(int device, size_t bytes) {
+        if (pin && pin_cap >= bytes && pin_dev == device) return true;
+        if (pin) (void)hipHostFree(pin);
+        pin = nullptr;
+        pin_cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&pin), bytes, hipHostMallocDefault) != hipSuccess) return false;
+        pin_cap = bytes;
+        pin_dev = device;
+        return true;
+    }
 };
 thread_local Scratch g_scratch;
 
-int orb_impl(const uint8_t* image, int32_t width, int32_t height, int64_t pitch, const sfmx_orb_params* P,
-             int32_t inputs_on_device, int32_t device, void* stream, sfmx_keypoint* keypoints, uint8_t* descriptors,
-             int32_t capacity, int32_t* n_keypoints, Scratch& scratch, float* last_ms) {
-    if (!image || !P || !n_keypoints || capacity < 0 || (capacity > 0 && !keypoints)) {
+struct OrbImage { const uint8_t* data; int32_t width, height; int64_t pitch; };
+
+// detect() + compute() of a chunk of G images of one size as one set of launches (image g's arrays
+// at g * istride in the arena, its counters at stats + g * CS).  Per image: keypoints[g] /
+// descriptors[g] / capacities[g] as the one-image call, n_keypoints[g], rcs[g] its status.
+// Returns the first failure that is not a per-image capacity report.
+int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inputs_on_device, int32_t device,
+              hipStream_t st, sfmx_keypoint* const* keypoints, uint8_t* const* descriptors, const int32_t* capacities,
+              int32_t* n_keypoints, int* rcs, Scratch& scratch, float* last_ms) {
+    if (!ims || !P || !n_keypoints || G < 1) {
         set_last_error("null argument");
         return SFMX_EINVAL;
     }
-    if (width < 1 || height < 1 || pitch < width || width > 16384 || height > 16384) {
-        set_last_error("image size must be 1..16384 with pitch >= width");
-        return SFMX_EINVAL;
+    const int width = ims[0].width, height = ims[0].height;
+    for (int g = 0; g < G; ++g) {
+        const OrbImage& im = ims[g];
+        if (!im.data || capacities[g] < 0 || (capacities[g] > 0 && !keypoints[g])) { set_last_error("null argument"); return SFMX_EINVAL; }
+        if (im.width < 1 || im.height < 1 || im.pitch < im.width || im.width > 16384 || im.height > 16384) {
+            set_last_error("image size must be 1..16384 with pitch >= width");
+            return SFMX_EINVAL;
+        }
+        if (im.width != width || im.height != height) { set_last_error("internal: a chunk mixes image sizes"); return SFMX_EINTERNAL; }
     }
     if (P->nfeatures < 0 || !(P->scale_factor > 1.f) || P->n_levels < 1 || P->n_levels > MAX_LEVELS ||
         P->edge_threshold < 16 || P->edge_threshold > 256 || P->first_level != 0 || P->wta_k != 2 ||
@@ -959,17 +1075,25 @@ int orb_impl(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
     }
     const std::vector<int> umax = circle_umax();
     const int64_t CAND_CAP = px / 4 + 1024;    // strict 3x3 maxima: at most one per 2 x 2 cell
+    int capmax = 0;
+    for (int g = 0; g < G; ++g) capmax = std::max(capmax, (int)capacities[g]);
     int prev = -1;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(device);
-    const hipStream_t st = (hipStream_t)stream;
     int rc = SFMX_OK;
     {
-        // corner records: cpos 4 + cscore 1 + A, B 8 + 8 + Ls, Rs 4 + 4 + raw / kept keypoints 28 + 28 + flag 4
-        const size_t need = (size_t)px * 3 + (size_t)CAND_CAP * 89 + (size_t)(rows + 1) * 8 +
-                            tables.size() * sizeof(AxisEnt) + sizeof(Lvl) * nl + sizeof(int) * umax.size() +
-                            (size_t)width * height + (size_t)capacity * 32 + 256 * 32;
-        if (!scratch.img.reserve(device, need)) { rc = SFMX_ENOMEM; set_last_error("device allocation failed"); goto done; }
+        // one image's block: pyr / score / blur slabs, corner records (cpos 4 + cscore 1 + A, B 8 + 8 + Ls, Rs
+        // 4 + 4 + raw / kept keypoints 28 + 28 + flag 4), row counts / offsets, the input copy and the
+        // descriptor staging (host buffers) -- every part 256-B aligned, so the offsets are the same in
+        // every block
+        auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        const size_t blk = 3 * r(px) + r(CAND_CAP * 4) + r(CAND_CAP) + 2 * r(CAND_CAP * sizeof(Resp)) + 2 * r(CAND_CAP * 4) +
+                           2 * r(CAND_CAP * sizeof(Kp)) + r(CAND_CAP * 4) + 2 * r((size_t)(rows + 1) * 4) +
+                           (inputs_on_device ? 0 : r((size_t)width * height) + r((size_t)std::max(capmax, 1) * 32));
+        const size_t shared_b = r(std::max<size_t>(tables.size(), 1) * sizeof(AxisEnt)) + r(sizeof(Lvl) * nl) +
+                                r(sizeof(int) * umax.size()) + r(sizeof(ImgIO) * G) + r(sizeof(int) * CS * G);
+        if (!scratch.img.reserve(device, blk * G + shared_b)) { rc = SFMX_ENOMEM; set_last_error("device allocation failed"); goto done; }
+        if (!scratch.pin_reserve(device, shared_b)) { rc = SFMX_ENOMEM; set_last_error("pinned staging allocation failed"); goto done; }
         std::call_once(g_const_once[device], [] {
             int taps[7];
             blur_taps(taps);
@@ -991,83 +1115,128 @@ int orb_impl(const uint8_t* image, int32_t width, int32_t height, int64_t pitch,
             int* keep = A.take<int>(CAND_CAP);
             int* row_cnt = A.take<int>(rows + 1);
             int* row_off = A.take<int>(rows + 1);
-            int* cnt = A.take<int>(2 * MAX_LEVELS + 4);   // cnt1 | cnt2 | status
+            uint8_t* t = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)width * height);
+            uint8_t* ddesc = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)std::max(capmax, 1) * 32);
+            const int64_t istride = (int64_t)A.used;   // == blk (every part 256-B rounded)
+            if ((size_t)istride != blk) { set_last_error("internal: ORB block layout"); rc = SFMX_EINTERNAL; goto done; }
+            A.used = blk * G;
             AxisEnt* dtab = A.take<AxisEnt>(std::max<size_t>(tables.size(), 1));
             Lvl* dlv = A.take<Lvl>(nl);
             int* dumax = A.take<int>(umax.size());
-            uint8_t* t = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)width * height);
-            uint8_t* ddesc = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)std::max(capacity, 1) * 32);
+            ImgIO* dio = A.take<ImgIO>(G);
+            int* stats = A.take<int>((size_t)CS * G);
             if (A.overflow) { set_last_error("internal: ORB scratch arena too small"); rc = SFMX_ECAPACITY; goto done; }
-            int* cnt1 = cnt;
-            int* cnt2 = cnt + MAX_LEVELS;
-            int* dst = cnt + 2 * MAX_LEVELS;
-            const uint8_t* dimg = image;
-            int64_t dpitch = pitch;
-            if (!inputs_on_device) {
-                OCHK(hipMemcpy2DAsync(t, width, image, pitch, width, height, hipMemcpyHostToDevice, st));
-                dimg = t;
-                dpitch = width;
+            int* cnt1 = stats;
+            int* cnt2 = stats + MAX_LEVELS;
+            int* sst = stats + 2 * MAX_LEVELS;   // count, levels, corners, err
+            // the chunk's small inputs through pinned staging (one copy each, no pageable staging)
+            char* hp = scratch.pin;
+            const size_t o_tab = 0, o_lv = o_tab + r(std::max<size_t>(tables.size(), 1) * sizeof(AxisEnt)),
+                         o_um = o_lv + r(sizeof(Lvl) * nl), o_io = o_um + r(sizeof(int) * umax.size()),
+                         o_st = o_io + r(sizeof(ImgIO) * G);
+            if (!tables.empty()) std::memcpy(hp + o_tab, tables.data(), tables.size() * sizeof(AxisEnt));
+            std::memcpy(hp + o_lv, lv.data(), sizeof(Lvl) * nl);
+            std::memcpy(hp + o_um, umax.data(), sizeof(int) * umax.size());
+            ImgIO* hio = reinterpret_cast<ImgIO*>(hp + o_io);
+            for (int g = 0; g < G; ++g) {
+                ImgIO& e = hio[g];
+                e.img = inputs_on_device ? ims[g].data : t + (int64_t)g * istride;
+                e.pitch = inputs_on_device ? ims[g].pitch : width;
+                e.kp_out = inputs_on_device ? reinterpret_cast<Kp*>(keypoints[g]) : nullptr;
+                e.desc_out = !descriptors ? nullptr : inputs_on_device ? descriptors[g] : ddesc + (int64_t)g * istride;
+                e.capacity = capacities[g];
+                e.pad = 0;
             }
-            if (!tables.empty())
-                OCHK(hipMemcpyAsync(dtab, tables.data(), tables.size() * sizeof(AxisEnt), hipMemcpyHostToDevice, st));
-            OCHK(hipMemcpyAsync(dlv, lv.data(), sizeof(Lvl) * nl, hipMemcpyHostToDevice, st));
-            OCHK(hipMemcpyAsync(dumax, umax.data(), sizeof(int) * umax.size(), hipMemcpyHostToDevice, st));
+            if (!inputs_on_device)
+                for (int g = 0; g < G; ++g)
+                    OCHK(hipMemcpy2DAsync(t + (int64_t)g * istride, width, ims[g].data, ims[g].pitch, width, height,
+                                          hipMemcpyHostToDevice, st));
+            OCHK(hipMemcpyAsync(dtab, hp, o_st, hipMemcpyHostToDevice, st));   // tables | levels | umax | ImgIO: contiguous
             OCHK(hipEventRecord(A.e0, st));
+            const unsigned gz = (unsigned)G;
             // ---- detect(): pyramid, FAST, NMS
-            orb_copy_kernel<<<dim3((width + 255) / 256, height), 256, 0, st>>>(dimg, width, height, dpitch, pyr);
+            orb_copy_kernel<<<dim3((width + 255) / 256, height, gz), 256, 0, st>>>(dio, width, height, pyr, istride);
             for (int l = 1; l < nl; l++)
-                orb_resize_kernel<<<dim3((lv[l].w + 255) / 256, lv[l].h), 256, 0, st>>>(pyr, dlv, l, dtab);
-            orb_fast_kernel<<<dim3((maxw + FT_X - 1) / FT_X, (maxh + FT_Y - 1) / FT_Y, nl), 256, 0, st>>>(pyr, dlv, thr,
-                                                                                                      score);
-            orb_nms_kernel<<<rows, 256, 0, st>>>(score, dlv, nl, border, 0, row_cnt, nullptr, nullptr, nullptr, (int)CAND_CAP);
-            orb_scan_kernel<<<1, 1024, 0, st>>>(row_cnt, rows, row_off);
-            orb_nms_kernel<<<rows, 256, 0, st>>>(score, dlv, nl, border, 1, nullptr, row_off, cpos, cscore, (int)CAND_CAP);
+                orb_resize_kernel<<<dim3((lv[l].w + 255) / 256, lv[l].h, gz), 256, 0, st>>>(pyr, dlv, l, dtab, istride);
+            orb_fast_kernel<<<dim3((maxw + FT_X - 1) / FT_X, (maxh + FT_Y - 1) / FT_Y, nl * gz), 256, 0, st>>>(
+                pyr, dlv, thr, score, nl, istride);
+            orb_nms_kernel<<<dim3(rows, gz), 256, 0, st>>>(score, dlv, nl, border, 0, row_cnt, nullptr, nullptr, nullptr,
+                                                           (int)CAND_CAP, istride);
+            orb_scan_kernel<<<gz, 1024, 0, st>>>(row_cnt, rows, row_off, istride, stats);
+            orb_nms_kernel<<<dim3(rows, gz), 256, 0, st>>>(score, dlv, nl, border, 1, nullptr, row_off, cpos, cscore,
+                                                           (int)CAND_CAP, istride);
             // retainBest(2 n_l) on the FAST scores, Harris responses, retainBest(n_l) on them (device)
-            OCHK(hipMemsetAsync(dst + 3, 0, sizeof(int), st));
             SelCounts s1{}, s2{};
             for (int l = 0; l < nl; l++) { s1.n[l] = 2 * per[l]; s2.n[l] = per[l]; }
-            orb_retain_kernel<<<nl, RT, 0, st>>>(0, dlv, row_off, cscore, rA, rB, sLs, sRs, nullptr, cnt1, s1, (int)CAND_CAP,
-                                                 dst + 3);
-            orb_harris_kernel<<<dim3(64, nl), 256, 0, st>>>(pyr, dlv, row_off, rA, cnt1, cpos, rB);
-            orb_retain_kernel<<<nl, RT, 0, st>>>(1, dlv, row_off, cscore, rA, rB, sLs, sRs, cnt1, cnt2, s2, (int)CAND_CAP,
-                                                 dst + 3);
-            orb_angle_kernel<<<1024, 256, 0, st>>>(pyr, dlv, nl, row_off, rA, rB, cnt2, cpos, dumax, width, height, border,
-                                                   kraw, keep);
-            orb_compact_kernel<<<1, RT, 0, st>>>(kraw, keep, cnt2, nl, row_off, rows, dfin, dst);
+            orb_retain_kernel<<<dim3(nl, gz), RT, 0, st>>>(0, dlv, row_off, cscore, rA, rB, sLs, sRs, nullptr, cnt1, s1,
+                                                           (int)CAND_CAP, sst + 3, istride);
+            orb_harris_kernel<<<dim3(64, nl, gz), 256, 0, st>>>(pyr, dlv, row_off, rA, cnt1, cpos, rB, istride);
+            orb_retain_kernel<<<dim3(nl, gz), RT, 0, st>>>(1, dlv, row_off, cscore, rA, rB, sLs, sRs, cnt1, cnt2, s2,
+                                                           (int)CAND_CAP, sst + 3, istride);
+            orb_angle_kernel<<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rA, rB, cnt2, cpos, dumax,
+                                                                          width, height, border, kraw, keep, istride);
+            orb_compact_kernel<<<gz, RT, 0, st>>>(kraw, keep, cnt2, nl, row_off, rows, dfin, sst, istride);
             // ---- compute(): blur of the levels used, rBRIEF of min(count, capacity) keypoints
-            if (descriptors && capacity > 0) {
-                orb_blur_kernel<<<dim3((maxw + BT_X - 1) / BT_X, (maxh + BT_Y - 1) / BT_Y, nl), 256, 0, st>>>(pyr, dlv, dst,
-                                                                                                       blur);
-                orb_brief_kernel<<<std::min(4096, (capacity + 7) / 8), 256, 0, st>>>(blur, dlv, dfin, dst, capacity,
-                                                                                     inputs_on_device ? descriptors : ddesc);
+            if (descriptors && capmax > 0) {
+                orb_blur_kernel<<<dim3((maxw + BT_X - 1) / BT_X, (maxh + BT_Y - 1) / BT_Y, nl * gz), 256, 0, st>>>(
+                    pyr, dlv, sst, blur, nl, istride);
+                orb_brief_kernel<<<dim3(std::min(G > 1 ? 1024 : 4096, (capmax + 7) / 8), gz), 256, 0, st>>>(blur, dlv, dfin,
+                                                                                                          sst, dio, istride);
             }
-            if (inputs_on_device && capacity > 0)
-                orb_copy_kp_kernel<<<std::min(1024, (capacity + 255) / 256), 256, 0, st>>>(
-                    dfin, dst, capacity, reinterpret_cast<Kp*>(keypoints));
+            if (inputs_on_device && capmax > 0)
+                orb_copy_kp_kernel<<<dim3(std::min(1024, (capmax + 255) / 256), gz), 256, 0, st>>>(dfin, sst, dio, istride);
             OCHK(hipGetLastError());
-            int hst[4] = {0, 0, 0, 0};
-            OCHK(hipMemcpyAsync(hst, dst, sizeof(hst), hipMemcpyDeviceToHost, st));
+            int* hst = reinterpret_cast<int*>(hp + o_st);
+            OCHK(hipMemcpyAsync(hst, stats, sizeof(int) * CS * G, hipMemcpyDeviceToHost, st));
             OCHK(hipEventRecord(A.e1, st));
             OCHK(hipStreamSynchronize(st));
-            if (hst[2] > CAND_CAP) { set_last_error("internal: corner buffer overflow"); rc = SFMX_EINTERNAL; goto done; }
-            if (hst[3]) { set_last_error("internal: device retainBest made no progress"); rc = SFMX_EINTERNAL; goto done; }
-            const int n = hst[0];
-            *n_keypoints = n;
-            const int m = std::min(n, (int)capacity);
-            if (!inputs_on_device && m > 0) {   // host buffers: the kept keypoints and descriptors back
-                OCHK(hipMemcpyAsync(keypoints, dfin, sizeof(Kp) * m, hipMemcpyDeviceToHost, st));
-                if (descriptors) OCHK(hipMemcpyAsync(descriptors, ddesc, (size_t)m * 32, hipMemcpyDeviceToHost, st));
-                OCHK(hipStreamSynchronize(st));
+            for (int g = 0; g < G; ++g) {
+                const int* s = hst + (size_t)g * CS + 2 * MAX_LEVELS;
+                if (s[2] > CAND_CAP) { set_last_error("internal: corner buffer overflow"); rc = SFMX_EINTERNAL; goto done; }
+                if (s[3]) { set_last_error("internal: device retainBest made no progress"); rc = SFMX_EINTERNAL; goto done; }
             }
+            bool copies = false;
+            for (int g = 0; g < G; ++g) {
+                const int n = hst[(size_t)g * CS + 2 * MAX_LEVELS];
+                n_keypoints[g] = n;
+                const int m = std::min(n, (int)capacities[g]);
+                if (!inputs_on_device && m > 0) {   // host buffers: the kept keypoints and descriptors back
+                    OCHK(hipMemcpyAsync(keypoints[g], reinterpret_cast<const char*>(dfin) + (int64_t)g * istride,
+                                        sizeof(Kp) * m, hipMemcpyDeviceToHost, st));
+                    if (descriptors && descriptors[g])
+                        OCHK(hipMemcpyAsync(descriptors[g], ddesc + (int64_t)g * istride, (size_t)m * 32,
+                                            hipMemcpyDeviceToHost, st));
+                    copies = true;
+                }
+                rcs[g] = n > capacities[g] ? SFMX_ECAPACITY : SFMX_OK;
+            }
+            if (copies) OCHK(hipStreamSynchronize(st));
             float ms = -1.f;
             (void)hipEventElapsedTime(&ms, A.e0, A.e1);
             *last_ms = ms;
-            if (n > capacity) { set_last_error("keypoint capacity too small"); rc = SFMX_ECAPACITY; }
         }
     done:;
     }
     if (prev >= 0) (void)hipSetDevice(prev);
     return rc;
+}
+
+int orb_impl(const uint8_t* image, int32_t width, int32_t height, int64_t pitch, const sfmx_orb_params* P,
+             int32_t inputs_on_device, int32_t device, void* stream, sfmx_keypoint* keypoints, uint8_t* descriptors,
+             int32_t capacity, int32_t* n_keypoints, Scratch& scratch, float* last_ms) {
+    if (!image || !P || !n_keypoints || capacity < 0 || (capacity > 0 && !keypoints)) {
+        set_last_error("null argument");
+        return SFMX_EINVAL;
+    }
+    const OrbImage im{image, width, height, pitch};
+    sfmx_keypoint* kp[1] = {keypoints};
+    uint8_t* dd[1] = {descriptors};
+    int rcs[1] = {SFMX_OK};
+    const int rc = orb_chunk(&im, 1, P, inputs_on_device, device, (hipStream_t)stream, kp, descriptors ? dd : nullptr,
+                             &capacity, n_keypoints, rcs, scratch, last_ms);
+    if (rc) return rc;
+    if (rcs[0] == SFMX_ECAPACITY) set_last_error("keypoint capacity too small");
+    return rcs[0];
 }
 
 struct BatchSlot {
@@ -1121,21 +1290,65 @@ int sfmx_orb_detect_compute_batch(const sfmx_gray_image* images, int32_t n_image
             sl.device = device;
         }
     }
-    std::atomic<int> next{0};
+    // chunks: runs of consecutive same-size images, G <= 16 per chunk (one launch set each), spread
+    // over the slots' streams; an image that fails the per-image checks is reported alone
     std::vector<int> rcs(n_images, SFMX_OK);
-    std::vector<float> kms(ns, 0.f);
     std::vector<std::string> errs(n_images);
+    std::vector<std::vector<int>> chunks;
+    {
+        const int gmax = std::max(1, std::min(16, (n_images + ns - 1) / ns));
+        for (int i = 0; i < n_images; ++i) {
+            const sfmx_gray_image& im = images[i];
+            if (!im.data || capacities[i] < 0 || (capacities[i] > 0 && !keypoints[i])) {
+                rcs[i] = SFMX_EINVAL;
+                errs[i] = "null argument";
+                continue;
+            }
+            if (im.width < 1 || im.height < 1 || im.pitch < im.width || im.width > 16384 || im.height > 16384) {
+                rcs[i] = SFMX_EINVAL;
+                errs[i] = "image size must be 1..16384 with pitch >= width";
+                continue;
+            }
+            if (chunks.empty() || (int)chunks.back().size() >= gmax || images[chunks.back()[0]].width != im.width ||
+                images[chunks.back()[0]].height != im.height)
+                chunks.emplace_back();
+            chunks.back().push_back(i);
+        }
+    }
+    std::atomic<int> next{0};
+    std::vector<float> kms(ns, 0.f);
     auto work = [&](int slot) {
         (void)hipSetDevice(device);
         BatchSlot& sl = *g_slots[slot];
-        for (int i; (i = next.fetch_add(1)) < n_images;) {
+        std::vector<OrbImage> ims;
+        std::vector<sfmx_keypoint*> kp;
+        std::vector<uint8_t*> dd;
+        std::vector<int32_t> caps, nk;
+        std::vector<int> crc;
+        for (int c; (c = next.fetch_add(1)) < (int)chunks.size();) {
+            const std::vector<int>& ch = chunks[c];
+            const int G = (int)ch.size();
+            ims.clear(); kp.clear(); dd.clear(); caps.clear();
+            for (int i : ch) {
+                ims.push_back(OrbImage{images[i].data, images[i].width, images[i].height, images[i].pitch});
+                kp.push_back(keypoints[i]);
+                dd.push_back(descriptors ? descriptors[i] : nullptr);
+                caps.push_back(capacities[i]);
+            }
+            nk.assign(G, 0);
+            crc.assign(G, SFMX_OK);
             float ms = 0.f;
-            const sfmx_gray_image& im = images[i];
-            rcs[i] = orb_impl(im.data, im.width, im.height, im.pitch, params, inputs_on_device, device, sl.stream,
-                              keypoints[i], descriptors ? descriptors[i] : nullptr, capacities[i], &n_keypoints[i],
-                              sl.arena, &ms);
-            if (rcs[i] != SFMX_OK) errs[i] = sfmx_last_error();
-            kms[slot] += ms;
+            const int rc = orb_chunk(ims.data(), G, params, inputs_on_device, device, sl.stream, kp.data(),
+                                     descriptors ? dd.data() : nullptr, caps.data(), nk.data(), crc.data(), sl.arena, &ms);
+            const std::string err = rc ? sfmx_last_error() : std::string();
+            for (int k = 0; k < G; ++k) {
+                const int i = ch[k];
+                n_keypoints[i] = nk[k];
+                rcs[i] = rc ? rc : crc[k];
+                if (rc) errs[i] = err;
+                else if (crc[k] == SFMX_ECAPACITY) errs[i] = "keypoint capacity too small";
+            }
+            if (!rc) kms[slot] += ms;
         }
     };
     std::vector<std::thread> th;

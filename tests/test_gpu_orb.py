@@ -90,3 +90,33 @@ def test_device_and_batch_modes_match():
     assert n == len(ref[0][0])
     assert kt[:n].cpu().numpy().tobytes() == ref[0][0].tobytes()
     assert np.array_equal(dt[:n].cpu().numpy(), ref[0][1])
+
+
+@pytest.mark.parametrize("n_streams", [1, 2])
+def test_batched_chunks_equal_the_oracle(n_streams):
+    """r04: a batch runs as chunks of up to 16 same-size images, each chunk ONE set of launches
+    (image g's arrays at g x the per-image block, its counters in a stats row).  Mixed sizes split
+    the chunks; every image -- corner-rich, tie-heavy, cornerless, below 2 x edgeThreshold -- must
+    equal the oracle's one-image result, host and device modes."""
+    import torch
+    import sfmx
+    ties = np.full((240, 320), 100, np.uint8)
+    ties[40:200:8, 40:280:8] = 200
+    ties[44:196:16, 44:276:16] = 10
+    imgs = [sift_cases.blob_image(240, 320, n_blobs=120, seed=s, noise=6.0) for s in (31, 32, 33)]
+    imgs += [ties, np.full((240, 320), 7, np.uint8), sift_cases.blob_image(240, 320, n_blobs=60, seed=34)]
+    imgs += [np.zeros((40, 40), np.uint8), sift_cases.blob_image(97, 131, n_blobs=40, seed=35, noise=4.0)]
+    imgs += [sift_cases.blob_image(240, 320, n_blobs=200, seed=36, noise=9.0)]
+    orb = sfmx.features.ORB.create(2000)
+    got = orb.detectAndCompute_batch(imgs, capacity=4096, n_streams=n_streams)
+    for im, (k, d) in zip(imgs, got):
+        ek, ed = oracle.orb(im, nfeatures=2000)
+        assert k.tobytes() == ek.tobytes() and np.array_equal(d, ed)
+    dev = [torch.from_numpy(im).cuda() for im in imgs]
+    kt = [torch.zeros((4096, 7), dtype=torch.int32, device="cuda") for _ in imgs]
+    dt = [torch.zeros((4096, 32), dtype=torch.uint8, device="cuda") for _ in imgs]
+    ns = orb.detectAndCompute_batch_device(dev, kt, dt, n_streams=n_streams)
+    torch.cuda.synchronize()
+    for (k, d), n, a, b in zip(got, ns, kt, dt):
+        assert n == len(k)
+        assert a[:n].cpu().numpy().tobytes() == k.tobytes() and np.array_equal(b[:n].cpu().numpy(), d)
