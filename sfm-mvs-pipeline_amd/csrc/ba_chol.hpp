@@ -785,6 +785,345 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// chol_factor on NW x NW waves (SFMX_BA_WIDE, default on; 1024 threads at NB = 64).  The NW-wave form
+// above gives each wave a 16-row strip of NW column tiles, so a 64^3 tile product is NW x 16 MFMA
+// steps per wave and a 64 x 64 tile load NB^2 / (2 NTH) 16-B loads per thread: on the level chain
+// (r02q stamps: loads 2.7 us, the two products 2.9 + 3.4 us per level) every workgroup of the launch
+// waits on one CU's worth of issue.  Here wave w owns the single 16 x 16 tile (wr, wc) = (w % NW,
+// w / NW): the products are 16 MFMA steps per wave, the loads a quarter as many per thread.  Every
+// output element is accumulated by the same MFMA sequence as in mfma_nn / mfma_nt (k ascending), the
+// diagonal inverse runs the same sweeps (the inner 16 x 16 inverse on wave 0, M per strip, the rank-16
+// update per tile) and the right-hand-side terms (y_a, w = W y, contrib) run on the first NTH threads
+// with NTH's partition: bit-identical to chol_factor and to the per-level launches.
+constexpr int NWW = NW * NW, NTW = 64 * NWW;   // waves / threads of the wide form
+__device__ __forceinline__ int wrow() { return (threadIdx.x >> 6) % NW; }
+__device__ __forceinline__ int wcol() { return (threadIdx.x >> 6) / NW; }
+__device__ __forceinline__ void tile_load_w(double (*dst)[LDT], const double* __restrict__ src, int ld) {
+#pragma unroll
+    for (int q = 0; q < NB * NB / (2 * NTW); ++q) {
+        const int e = q * (2 * NTW) + 2 * threadIdx.x;
+        *reinterpret_cast<double2*>(&dst[e / NB][e % NB]) = *reinterpret_cast<const double2*>(src + (size_t)(e / NB) * ld + e % NB);
+    }
+}
+__device__ __forceinline__ void tile_load_w_wt(double (*dst)[LDT], __amdgpu_buffer_rsrc_t rs, size_t src, int ld) {
+#pragma unroll
+    for (int q = 0; q < NB * NB / (2 * NTW); ++q) {
+        const int e = q * (2 * NTW) + 2 * threadIdx.x;
+        *reinterpret_cast<double2*>(&dst[e / NB][e % NB]) = ld_wt2(rs, src + (size_t)(e / NB) * ld + e % NB);
+    }
+}
+// this wave's tile (wr, wc) of a row-major NB x NB block at src (leading dimension ld)
+__device__ __forceinline__ size_t wtile_at(int r, int ld) {
+    return (size_t)(16 * wrow() + trow(r)) * ld + 16 * wcol() + tcol();
+}
+__device__ __forceinline__ void wtile_regs(f64x4& t, const double* __restrict__ src, int ld) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t[r] = src[wtile_at(r, ld)];
+}
+__device__ __forceinline__ void wtile_regs_wt(f64x4& t, const double* __restrict__ src, int ld) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t[r] = ld_wt(&src[wtile_at(r, ld)]);
+}
+__device__ __forceinline__ void wtile_store_wt(const f64x4& t, double* __restrict__ dst, int ld) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st_wt(&dst[wtile_at(r, ld)], t[r]);
+}
+// acc = A[strip wr] * B[:, tile wc]   (= mfma_nn's acc[wc] of wave wr)
+__device__ __forceinline__ f64x4 wmfma_nn(const double (*A)[LDT], const double (*B)[LDT]) {
+    const int wr = wrow(), wc = wcol(), l = threadIdx.x & 63, m = l & 15, kq = l >> 4;
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int st = 0; st < NB / 4; ++st)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[16 * wr + m][4 * st + kq], B[4 * st + kq][16 * wc + m], acc, 0, 0, 0);
+    return acc;
+}
+// acc = A[strip wr] * X[tile wc rows]^T   (= mfma_nt's acc[wc] of wave wr)
+__device__ __forceinline__ f64x4 wmfma_nt(const double (*A)[LDT], const double (*X)[LDT]) {
+    const int wr = wrow(), wc = wcol(), l = threadIdx.x & 63, m = l & 15, kq = l >> 4;
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int st = 0; st < NB / 4; ++st)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[16 * wr + m][4 * st + kq], X[16 * wc + m][4 * st + kq], acc, 0, 0, 0);
+    return acc;
+}
+// chol_diag_tile on the NW x NW waves: t is this wave's tile (wr, wc) of the final diagonal tile k.
+// ws: the sweeps' workspace, DIAG_WS_W doubles (two tile buffers: sm.m | sm.n, dead by now); buf: a
+// tile buffer for W (the first of them: the sweeps are over when W is written into it).
+constexpr int DIAG_WS_W = NB * LDP + 16 * LDP + NWW * 16 * LDP;
+static_assert(DIAG_WS_W <= 2 * NB * LDT, "the wide sweeps' workspace spans two tile buffers");
+template <int RW>
+__device__ __forceinline__ void chol_diag_tile_w(f64x4& t, int k, double* __restrict__ Wk, double* __restrict__ R,
+                                                 const double* __restrict__ y, double* __restrict__ wv,
+                                                 double* __restrict__ contrib, int* __restrict__ fail,
+                                                 double (*buf)[LDT], double* ws, int* wver) {
+    const int tid = threadIdx.x, w = tid >> 6, wr = wrow(), wc = wcol(), l = tid & 63, m = l & 15, kq = l >> 4, k0 = k * NB;
+    double* Pc = ws;                       // [64][LDP]  column panel A_:B
+    double* Qn = ws + NB * LDP;            // [16][LDP]  -A_BB^-1
+    double* Mw = Qn + 16 * LDP * (1 + w);  // [16][LDP]  this wave's -M strip (strip wr)
+    bool bad = false;
+#pragma unroll
+    for (int s = 0; s < NW; ++s) {
+        const bool rowB = (wr == s);
+        if (wc == s)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Pc[(16 * wr + trow(r)) * LDP + tcol()] = t[r];
+        __syncthreads();
+        if (tid < 64) inner_inverse16(Pc, s, Qn, bad);
+        __syncthreads();
+        f64x4 mm = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+            mm = __builtin_amdgcn_mfma_f64_16x16x4f64(Pc[(16 * wr + m) * LDP + 4 * st + kq], Qn[(4 * st + kq) * LDP + m], mm, 0, 0, 0);
+        f64x4 mv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mv[r] = rowB ? Qn[trow(r) * LDP + tcol()] : -mm[r];
+        if (wc == s) {
+            t = mv;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Mw[trow(r) * LDP + tcol()] = -mv[r];
+            __builtin_amdgcn_wave_barrier();
+            f64x4 acc = rowB ? f64x4{0.0, 0.0, 0.0, 0.0} : t;
+#pragma unroll
+            for (int st = 0; st < 4; ++st)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Mw[m * LDP + 4 * st + kq], Pc[(16 * wc + m) * LDP + 4 * st + kq], acc, 0, 0, 0);
+            t = acc;
+        }
+        __syncthreads();   // Pc is rewritten by the next sweep
+    }
+    if (bad) atomicOr(fail, 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 16 * wr + trow(r), j = 16 * wc + tcol();
+        buf[i][j] = -t[r];
+        st_wt(&Wk[i * NB + j], -t[r]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W_k drained before its version add
+    __syncthreads();
+    if (wver && tid == 0) __hip_atomic_fetch_add((g_i32*)wver, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // W_k ready
+    if (tid < NTH) {   // w = W y: chol_diag_tile's partition and order
+        static_assert(RW % 2 == 0, "RW is k + 1 with k odd");
+        const int i = tid >> 2, cp = tid & 3;
+        double acc[RW];
+#pragma unroll
+        for (int q = 0; q < RW; ++q) acc[q] = 0.0;
+#pragma unroll
+        for (int cc = 0; cc < NB / 4; cc += 2) {
+            const int c = cp * (NB / 4) + cc;
+            const double2 wi = *reinterpret_cast<const double2*>(&buf[i][c]);
+#pragma unroll
+            for (int q = 0; q < RW; q += 2) {
+                const double2 y0 = *reinterpret_cast<const double2*>(&y[c * RW + q]);
+                const double2 y1 = *reinterpret_cast<const double2*>(&y[(c + 1) * RW + q]);
+                acc[q] = fma(wi.x, y0.x, acc[q]);
+                acc[q + 1] = fma(wi.x, y0.y, acc[q + 1]);
+                acc[q] = fma(wi.y, y1.x, acc[q]);
+                acc[q + 1] = fma(wi.y, y1.y, acc[q + 1]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < RW; ++q) {
+            acc[q] += __shfl_xor(acc[q], 1);
+            acc[q] += __shfl_xor(acc[q], 2);
+        }
+        if (cp == 0) {
+#pragma unroll
+            for (int q = 0; q < RW; ++q) {
+                wv[i * RW + q] = acc[q];
+                st_wt(&R[(size_t)(k0 + i) * RW + q], acc[q]);
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < NTH)   // contrib_k[i][j] = sum_r y[r][i] w[r][j]
+        for (int o = tid >> 4; o < (RW - 1) * RW; o += NTH / 16) {
+            const int i = o / RW, j = o % RW, rp = tid & 15;
+            double sacc = 0.0;
+#pragma unroll
+            for (int h = 0; h < NB / 16; ++h) sacc = fma(y[(rp + 16 * h) * RW + i], wv[(rp + 16 * h) * RW + j], sacc);
+            sacc += __shfl_xor(sacc, 1);
+            sacc += __shfl_xor(sacc, 2);
+            sacc += __shfl_xor(sacc, 4);
+            sacc += __shfl_xor(sacc, 8);
+            if (rp == 0) contrib[(size_t)k * (RW - 1) * RW + o] = sacc;
+        }
+}
+
+// pbuf slot of the wide form: the product (4 doubles per thread of NTW) | the y terms (OPT per thread
+// of the first NTH, NTH's partition)
+template <int RW>
+struct WideSlot {
+    static constexpr int TPO = (NTH / (NB * RW)) > 0 ? NTH / (NB * RW) : 1;
+    static constexpr int OPT = (NB * RW) / (NTH / TPO);
+    static constexpr int SIZE = 4 * NTW + OPT * NTH;
+};
+
+template <int RW>
+__global__ __launch_bounds__(NTW)
+void chol_factor_w(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
+                   const int4* __restrict__ items, const int4* __restrict__ need, const int* __restrict__ src,
+                   double* __restrict__ W, double* __restrict__ contrib, int* __restrict__ fail, double* pbuf,
+                   int* tctr, int* ctr, int nitems, int nver, long long tmo) {
+    if (step_gated(fail + 1)) return;
+    __shared__ CholLds<RW> sm;
+    __shared__ int sh[2];
+    constexpr int TPO = WideSlot<RW>::TPO, OPT = WideSlot<RW>::OPT, SLOT = WideSlot<RW>::SIZE;
+    const int tid = threadIdx.x;
+    int* tver = ctr + 2;
+    if (tid == 0) sh[0] = __hip_atomic_fetch_add((g_i32*)ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int tk = sh[0];
+    const int4 it = items[tk], nd = need[tk];
+    auto wait_ver = [&](int id, int v) {   // as chol_factor's
+        long long t0 = wall_clock64();
+        int last = -1;
+        for (;;) {
+            const int cur = __hip_atomic_load((g_i32*)&tver[id], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur >= v) return;
+            if (cur != last) { last = cur; t0 = wall_clock64(); }
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > tmo) { atomicOr(fail, FAIL_FACTOR_WAIT); return; }
+        }
+    };
+    const __amdgpu_buffer_rsrc_t rS = wt_rsrc(S), rW = wt_rsrc(W);
+    double* ws = &sm.m[0][0];   // the inverse's workspace: sm.m | sm.n (contiguous, dead by then)
+    int done_id = -1;
+    if (it.y < 0) {     // leaf
+        const int k = it.x, k0 = k * NB;
+        f64x4 t;
+        wtile_regs(t, S + (size_t)k0 * npad + k0, npad);
+        for (int e = tid; e < NB * RW; e += NTW) sm.ra[e] = R[(size_t)k0 * RW + e];
+        __syncthreads();
+        chol_diag_tile_w<RW>(t, k, W + (size_t)k * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a, ws, &tver[tver_id(k, k)]);
+        done_id = tver_id(k, k);
+    } else {
+        const int4 task = tasks[it.x];
+        const int a = task.x, b = task.y, a0 = a * NB, b0 = b * NB, n = it.w & 0xffff, j = it.y - task.z;
+        const bool diag = (a == b), inv = (it.w >> 16) != 0;
+        const int k = src[it.y], k0 = k * NB;
+        double* dst = S + (size_t)a0 * npad + b0;
+        if (tid == 0) {
+            wait_ver(tver_id(a, k), nd.x);
+            if (!diag) wait_ver(tver_id(b, k), nd.y);
+            if (n == 1) wait_ver(tver_id(a, b), nd.w);
+        }
+        __syncthreads();
+        f64x4 t = {0.0, 0.0, 0.0, 0.0};
+        if (n == 1) {
+            wtile_regs_wt(t, dst, npad);
+            if (diag)
+                for (int e = tid; e < NB * RW; e += NTW) sm.ra[e] = ld_wt(&R[(size_t)a0 * RW + e]);
+        }
+        tile_load_w_wt(sm.a, rS, (size_t)a0 * npad + k0, npad);                 // A_ak
+        if (!diag) tile_load_w_wt(sm.n, rS, (size_t)b0 * npad + k0, npad);      // A_bk
+        if (tid == 0) wait_ver(tver_id(k, k), nd.z - 1);   // W_k stored
+        __syncthreads();
+        tile_load_w_wt(sm.m, rW, (size_t)k * NB * NB, NB);                      // W_k
+        __syncthreads();
+        const f64x4 g = wmfma_nn(sm.a, sm.m);   // G = A_ak W_k (tile (wr, wc))
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sm.m[16 * wrow() + trow(r)][16 * wcol() + tcol()] = g[r];
+        __syncthreads();
+        const f64x4 upd = wmfma_nt(sm.m, diag ? sm.a : sm.n);   // G X^T
+        double ys[OPT];
+#pragma unroll
+        for (int u = 0; u < OPT; ++u) ys[u] = 0.0;
+        if (diag) {
+            if (tid == 0) wait_ver(tver_id(k, k), nd.z);   // w_k (the R rows of k) stored
+            __syncthreads();
+            for (int e = tid; e < NB * RW; e += NTW) sm.rk[e] = ld_wt(&R[(size_t)k0 * RW + e]);
+            __syncthreads();
+            if (tid < NTH) {
+                const int pp = tid % TPO;
+#pragma unroll
+                for (int u = 0; u < OPT; ++u) {
+                    const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
+                    double sum = 0.0;
+                    for (int c = pp; c < NB; c += TPO) sum = fma(sm.a[i][c], sm.rk[c * RW + q], sum);
+                    if (TPO >= 2) sum += __shfl_xor(sum, 1);
+                    if (TPO >= 4) sum += __shfl_xor(sum, 2);
+                    ys[u] = sum;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                S[(size_t)(k0 + 16 * wcol() + tcol()) * npad + a0 + 16 * wrow() + trow(r)] = g[r];
+        }
+        bool fin = true;
+        if (n > 1) {   // publish this part; the last arriver finishes the task
+            double* slot = pbuf + (size_t)it.z * SLOT;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) st_wt(&slot[r * NTW + tid], upd[r]);
+            if (diag && tid < NTH)
+#pragma unroll
+                for (int u = 0; u < OPT; ++u) st_wt(&slot[4 * NTW + u * NTH + tid], ys[u]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                const bool last = __hip_atomic_fetch_add((g_i32*)&tctr[it.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
+                if (last) {
+                    tctr[it.x] = 0;
+                    wait_ver(tver_id(a, b), nd.w);
+                }
+                sh[1] = last;
+            }
+            __syncthreads();
+            fin = sh[1] != 0;
+            if (fin) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                wtile_regs_wt(t, dst, npad);
+                if (diag)
+                    for (int e = tid; e < NB * RW; e += NTW) sm.ra[e] = ld_wt(&R[(size_t)a0 * RW + e]);
+                __syncthreads();
+                const double* base = pbuf + (size_t)(it.z - j) * SLOT;
+                for (int jj = 0; jj < n; ++jj) {
+                    const double* sl = base + (size_t)jj * SLOT;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) t[r] -= (jj == j) ? upd[r] : ld_wt(&sl[r * NTW + tid]);
+                    if (diag && tid < NTH) {
+#pragma unroll
+                        for (int u = 0; u < OPT; ++u) {
+                            const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
+                            const double y = (jj == j) ? ys[u] : ld_wt(&sl[4 * NTW + u * NTH + tid]);
+                            if (tid % TPO == 0) sm.ra[i * RW + q] -= y;
+                        }
+                    }
+                }
+            }
+        } else {
+            t -= upd;
+            if (diag && tid < NTH) {
+#pragma unroll
+                for (int u = 0; u < OPT; ++u) {
+                    const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
+                    if (tid % TPO == 0) sm.ra[i * RW + q] -= ys[u];
+                }
+            }
+        }
+        if (fin) {
+            __syncthreads();
+            if (diag && inv) {
+                chol_diag_tile_w<RW>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a, ws,
+                                     &tver[tver_id(a, a)]);
+            } else {
+                wtile_store_wt(t, dst, npad);
+                if (diag)
+                    for (int e = tid; e < NB * RW; e += NTW) st_wt(&R[(size_t)a0 * RW + e], sm.ra[e]);
+            }
+            done_id = tver_id(a, b);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains before the version add
+    __syncthreads();
+    if (tid == 0) {
+        if (done_id >= 0) __hip_atomic_fetch_add((g_i32*)&tver[done_id], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_fetch_add((g_i32*)&ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nitems - 1)
+            for (int e = 0; e < nver + 2; ++e) __hip_atomic_store((g_i32*)&ctr[e], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // Cross-rank all-reduce of the reduced system, compacted: the structurally nonzero lower tiles of
 // S_cc (incl. the diagonal ones) + R | D | r_i, packed into one contiguous buffer and back.
 // One workgroup per tile; the tail block (blockIdx.x == ntiles) moves the rest.

@@ -122,6 +122,7 @@ struct sfmx_ba_ctx {
     bool split = true;             // SFMX_BA_SPLIT=0: chol_level (a task's sources in one workgroup)
     std::vector<int> part_start;   // per level: parts[part_start[l] .. part_start[l + 1])
     bool dag = true;               // SFMX_BA_DAG=0: one launch per level (chol_leaves + chol_level[_split])
+    bool wide = true;              // SFMX_BA_WIDE=0: chol_factor on NW waves instead of chol_factor_w on NW x NW
     int n_ditems = 0, n_ver = 0;
     long long dag_timeout = DAG_TIMEOUT;   // in-launch wait bound (wall-clock ticks without progress)
     int dag_fallbacks = 0;                 // steps re-run with the per-level launches after a wait timed out
@@ -157,6 +158,7 @@ struct sfmx_ba_ctx {
     // [5] ordering, [6] point groups / topology (the two parts of [0])
     double setup_ms[7] = {0, 0, 0, 0, 0, 0, 0};
     std::vector<char> plan_adj;   // the co-visibility the current plan was built from (reused if equal)
+    std::string plan_form;        // diagnostic library: the form switches the plan was built with
     int plan_K = 0;
     HostScratch* hscr = nullptr;
     ~sfmx_ba_ctx() {
@@ -387,7 +389,15 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
     double* Dm = R + (size_t)npad * RW;
     double* ri = Dm + (RW - 1) * (RW - 1);
     int* fl = c->failf.as<int>();
-    if (c->dag && c->split) {
+    // the wide form within 128 VGPRs: k = 1, 3 (RW = 8 would spill: k = 7 keeps chol_factor)
+    constexpr bool WIDE_OK = RW <= 4;
+    if (WIDE_OK && c->dag && c->split && c->wide) {
+        if constexpr (WIDE_OK)
+            hipLaunchKernelGGL(chol_factor_w<RW>, dim3((unsigned)c->n_ditems), dim3(NTW), 0, c->st, S, npad, R,
+                               c->ptasks.as<int4>(), c->ditems.as<int4>(), c->dneed.as<int4>(), c->psrc.as<int>(),
+                               c->Wt.as<double>(), c->contrib.as<double>(), fl, c->pbuf.as<double>(), c->lctr.as<int>(),
+                               c->dctr.as<int>(), c->n_ditems, c->n_ver, c->dag_timeout);
+    } else if (c->dag && c->split) {
         hipLaunchKernelGGL(chol_factor<RW>, dim3((unsigned)c->n_ditems), dim3(NTH), 0, c->st, S, npad, R,
                            c->ptasks.as<int4>(), c->ditems.as<int4>(), c->dneed.as<int4>(), c->psrc.as<int>(),
                            c->Wt.as<double>(), c->contrib.as<double>(), fl, c->pbuf.as<double>(), c->lctr.as<int>(),
@@ -541,6 +551,19 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
 // ordering and level schedule (SFMX_BA_ORDER: auto | natural | nd | nd1 | nd2 | nd4), the device
 // copies of the schedule, and S / W / the Schur terms sized by it.
 int ensure_plan(sfmx_ba_ctx* c) {
+#ifdef SFMX_DIAG
+    // the diagnostic library's form switches are read when a plan is built: a cached context (the
+    // per-device one of sfmx_ba_solve) re-plans when they change, so a test that switches forms
+    // between solves really runs each form
+    std::string form;
+    for (const char* k : {"SFMX_BA_ORDER", "SFMX_BA_BACK", "SFMX_BA_SPEC", "SFMX_BA_DAG", "SFMX_BA_DAG_TIMEOUT", "SFMX_BA_WIDE",
+                          "SFMX_BA_SPLIT"}) {
+        const char* v = SFMX_DIAG_ENV(k);
+        form += std::string(k) + "=" + (v ? v : "") + ";";
+    }
+    if (c->planned && form != c->plan_form) c->planned = false;
+    c->plan_form = form;
+#endif
     if (c->planned) return SFMX_OK;
     const auto t_plan = std::chrono::steady_clock::now();
     const int C = c->C;
@@ -670,7 +693,10 @@ int ensure_plan(sfmx_ba_ctx* c) {
         if (const char* et = SFMX_DIAG_ENV("SFMX_BA_DAG_TIMEOUT")) c->dag_timeout = std::atoll(et);   // recovery test
         max_slots = std::max(max_slots, dslots);
         const int tpo = std::max(1, NTH / (NB * RW)), opt = NB * RW / (NTH / tpo);
-        RC(c->pbuf.alloc(sizeof(double) * (size_t)max_slots * (4 * NW + opt) * NTH));
+        const size_t slot = std::max<size_t>((size_t)(4 * NW + opt) * NTH, (size_t)4 * NTW + (size_t)opt * NTH);   // chol_factor | _w
+        RC(c->pbuf.alloc(sizeof(double) * (size_t)max_slots * slot));
+        const char* ew = SFMX_DIAG_ENV("SFMX_BA_WIDE");
+        c->wide = !(ew && ew[0] == '0');
         RC(c->lctr.alloc(sizeof(int) * (size_t)((pl.tasks.size() + 4) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->lctr.p, 0, c->lctr.bytes, st));
         const char* e = SFMX_DIAG_ENV("SFMX_BA_SPLIT");

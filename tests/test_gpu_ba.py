@@ -143,14 +143,16 @@ def test_split_level_and_backsolve_bit_identical_to_r02_forms(order):
     hand-offs) give the same bits as the per-level chol_level launches."""
     p = synth.ba_problem(200, 6000, seed=29)
     res = {}
-    for back, split, dag in (("0", "0", "0"), ("1", "0", "0"), ("1", "1", "0"), ("1", "1", "1")):
+    for back, split, dag, wide in (("0", "0", "0", "0"), ("1", "0", "0", "0"), ("1", "1", "0", "0"), ("1", "1", "1", "0"),
+                                   ("1", "1", "1", "1")):
         # diagnostic library: SFMX_BA_SPLIT = chol_level_split (a task's sources over workgroups),
-        # SFMX_BA_DAG = chol_factor (leaves + every level in one launch)
-        with diagnostic(SFMX_BA_ORDER=order, SFMX_BA_BACK=back, SFMX_BA_SPLIT=split, SFMX_BA_DAG=dag):
+        # SFMX_BA_DAG = chol_factor (leaves + every level in one launch), SFMX_BA_WIDE = chol_factor_w
+        # (the same on 16 waves, one 16 x 16 tile each: r04)
+        with diagnostic(SFMX_BA_ORDER=order, SFMX_BA_BACK=back, SFMX_BA_SPLIT=split, SFMX_BA_DAG=dag, SFMX_BA_WIDE=wide):
             P, sm, tr = gpu_solve(p, max_num_iterations=4)
-        res[back + split + dag] = (P.points.copy(), P.poses.copy(), sm["final_cost"], tr.copy())
-    a = res["000"]
-    for key in ("100", "110", "111"):
+        res[back + split + dag + wide] = (P.points.copy(), P.poses.copy(), sm["final_cost"], tr.copy())
+    a = res["0000"]
+    for key in ("1000", "1100", "1110", "1111"):
         b = res[key]
         assert a[2] == b[2], key
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[3], b[3]), key
