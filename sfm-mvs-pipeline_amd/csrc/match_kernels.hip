@@ -1026,6 +1026,10 @@ void sift_f32_kernel(const WorkItem* __restrict__ work, const int32_t* __restric
                      const PairDev* __restrict__ pairs, const ImgDev* __restrict__ imgs,
                      const float* __restrict__ f32, int32_t* __restrict__ out_idx,
                      float* __restrict__ out_dist, double ratio) {
+    // the default -ffp-contract=fast-honor-pragmas fused the d * d + acc below into v_pk_fma_f32 (r03 wrote
+    // them as __fadd_rn / __fmul_rn, which are inlined plain + / * outside this pragma's reach): 1-ulp
+    // distances vs the oracle's -ffp-contract=off sums, found in r04 on an integral x non-integral pair
+#pragma clang fp contract(off)
     constexpr int STAGE = 32;
     __shared__ float tl[STAGE * SIFT_DIM];
     const WorkItem w = work[blockIdx.x];
@@ -1047,8 +1051,8 @@ void sift_f32_kernel(const WorkItem* __restrict__ work, const int32_t* __restric
             for (int k = 0; k < SIFT_DIM; k += 8)
 #pragma unroll
                 for (int l = 0; l < 8; ++l) {
-                    const float d = __fsub_rn(qrow[k + l], tl[jj * SIFT_DIM + k + l]);
-                    acc[l] = __fadd_rn(acc[l], __fmul_rn(d, d));   // no FMA contraction (oracle: -ffp-contract=off)
+                    const float d = qrow[k + l] - tl[jj * SIFT_DIM + k + l];
+                    acc[l] = acc[l] + d * d;   // no FMA contraction (the pragma above; oracle: -ffp-contract=off)
                 }
             float ssum = acc[0];
 #pragma unroll

@@ -12,4 +12,5 @@ timeout -k 10 600 bash tools/pmc_match.sh sift r04 > gpurun_out/r04b_pmc_sift.lo
 timeout -k 10 600 bash tools/pmc_match.sh orb r04 > gpurun_out/r04b_pmc_orb.log 2>&1 || exit 2
 timeout -k 10 800 bash tools/pmc_feat.sh r04 > gpurun_out/r04b_pmc_feat.log 2>&1 || exit 3
 timeout -k 10 600 bash tools/pmc_ba.sh r04 > gpurun_out/r04b_pmc_ba.log 2>&1 || exit 4
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_r04b_orbf -o orbf -- python3 $GRAFT_REPO_ROOT/bench.py --only-orb-features --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/r04b_prof_orbf.log 2>&1 || exit 5
 echo done
