@@ -61,7 +61,11 @@ struct OverlapStreams {
     hipEvent_t start, sx_done, sp_done;          // after the qcount clear; the two joins
     hipEvent_t* screen;                          // one per batch
 };
-constexpr int MATCH_BATCHES = 8;                 // product default (SFMX_MATCH_BATCHES in the diagnostic build)
+// product default (SFMX_MATCH_BATCHES in the diagnostic build): 1 = one screen launch, then pass 2.  The
+// overlapped form (8 batches, screens on two streams, pass 2 on a third) measured slower on C2 in r04a
+// (launch span 6.94 vs 6.20 ms: concurrent screens and subset kernels contend for the CUs; the subset
+// dispatches stretch to 0.67 ms each, profiles/r04a_c2_span.txt); kept selectable and tested.
+constexpr int MATCH_BATCHES = 1;
 
 // Thread-local last-error text shared by every C-ABI entry point (sfmx_last_error).
 void set_last_error(const char* msg);
