@@ -146,9 +146,9 @@ __device__ __forceinline__ double rcp_nr(double d) {
 //          inverse is closed-form and its two scalar pivots (a, det/a) are the
 //          scalar Cholesky pivots, i.e. exactly where LLT would fail.
 constexpr int LDP = 18;   // LDS row stride of the 16-wide panels (16-B aligned rows)
-// chol_diag_tile's workspace: column panel [NB][LDP] | -A_BB^-1 [16][LDP] | one -M strip [16][LDP]
-// per wave; it fits a tile buffer at NB = 64, not at NB = 32
-constexpr int DIAG_WS = NB * LDP + 16 * LDP + NW * 16 * LDP;
+// chol_diag_tile's workspace: column panel [NB][LDP] | -A_BB^-1 [16][LDP] | inner panel [32] | one
+// -M strip [16][LDP] per wave; it fits a tile buffer at NB = 64, not at NB = 32
+constexpr int DIAG_WS = NB * LDP + 16 * LDP + 32 + NW * 16 * LDP;
 constexpr bool DIAG_WS_IN_BUF = DIAG_WS <= NB * LDT;
 #ifdef SFMX_CHOL_STAMPS   // tools/micro/chol_tile.hip: phase timestamps of block 0 (never in the product build)
 __device__ long long g_chol_stamps[64];
@@ -157,83 +157,65 @@ __device__ long long g_chol_stamps[64];
 #define CHOL_STAMP(i) do { } while (0)
 #endif
 
-// Cross-lane moves of a double within wave 0 of the inner sweep (lane = 8 r + c): no LDS access.
-template <int PAT>
-__device__ __forceinline__ double swz(double v) {   // ds_swizzle, bit mode: lane' = ((lane & and) | or) ^ xor in 32
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_ds_swizzle((int)b, PAT), hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), PAT);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double bperm(double v, int src_lane) {   // ds_bpermute: the value of lane src_lane
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_ds_bpermute(4 * src_lane, (int)b), hi = __builtin_amdgcn_ds_bpermute(4 * src_lane, (int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double rdlane(double v, int src_lane) {   // v_readlane: wave-uniform
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)b, src_lane), hi = __builtin_amdgcn_readlane((int)(b >> 32), src_lane);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-// Qn = -(Pc[16s + i][j])^-1, i, j < 16, by wave 0 alone: 8 sweeps of 2x2 pivot blocks, lane (r, c) =
-// 8 r + c holding the 2x2 block (r, c).  Step j takes the pivot block from lane (j, j) (readlane),
-// the row's panel block (r, j) by a swizzle inside the lane's group of 8 and the column's (c, j) by
-// a permute: the values the r02 form passed through an LDS panel, so the same arithmetic and bits,
-// without an LDS write / read round trip on every pivot step.
-template <int J>
-__device__ __forceinline__ void inner_step(double (&p)[2][2], int r, int c, bool& bad) {
-    const int lane = 8 * r + c;
-    (void)lane;
-    // q = -[a b; b d]^-1 = -adj / det.  The row panel's m = -A_iB q = (A_iB adj) / det: the
-    // adjugate products run beside the reciprocal, so only one multiply follows it.
-    const double a = rdlane(p[0][0], 9 * J), bb = rdlane(p[0][1], 9 * J), d = rdlane(p[1][1], 9 * J);
-    constexpr int PAT = 0x18 | (J << 5);   // and 0b11000 (the lane's group of 8), or J
-    const double ai[2][2] = {{swz<PAT>(p[0][0]), swz<PAT>(p[0][1])}, {swz<PAT>(p[1][0]), swz<PAT>(p[1][1])}};
-    const int src = 8 * c + J;             // al[w][b] = A_(2c+w),(2j+b) = A_Bl[b][w]
-    const double al[2][2] = {{bperm(p[0][0], src), bperm(p[0][1], src)}, {bperm(p[1][0], src), bperm(p[1][1], src)}};
-    double det = fma(a, d, -bb * bb);
-    const bool badj = !(a > 0.0) || !isfinite(a) || !(det > 0.0) || !isfinite(det);   // branch-free
-    bad |= badj;
-    det = badj ? 1.0 : det;
-    double pre[2][2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        pre[u][0] = fma(ai[u][0], d, -ai[u][1] * bb);
-        pre[u][1] = fma(ai[u][1], a, -ai[u][0] * bb);
-    }
-    const double rd = rcp_nr(det);
-    const double q00 = -d * rd, q01 = bb * rd, q11 = -a * rd;   // q10 = q01
-    const bool rowB = (r == J), colB = (c == J);
-    double m[2][2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        m[u][0] = rowB ? (u == 0 ? q00 : q01) : pre[u][0] * rd;
-        m[u][1] = rowB ? (u == 0 ? q01 : q11) : pre[u][1] * rd;
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int w = 0; w < 2; ++w) {
-            const double base = rowB ? 0.0 : p[u][w];
-            const double upd = fma(-m[u][1], al[w][1], fma(-m[u][0], al[w][0], base));
-            p[u][w] = colB ? m[u][w] : upd;
-        }
-}
-__device__ __forceinline__ void inner_inverse16(const double* __restrict__ Pc, int s, double* __restrict__ Qn, bool& bad) {
+// (r04: a form passing the pivot, row and column blocks between lanes by v_readlane / ds_swizzle /
+// ds_bpermute instead of this LDS panel -- 16 LDS-path ops per step instead of 1 store + 6 reads --
+// measured slower: chol_factor 144 -> 165 us per LM step, profiles/r04a_ba_kernel_stats.txt; reverted.)
+__device__ __forceinline__ void inner_inverse16(const double* __restrict__ Pc, int s, double* __restrict__ Qn,
+                                                double* __restrict__ ipan, bool& bad) {
+    // wave 0 only: Qn = -(Pc[16s + i][j])^-1, i, j < 16
     const int lane = threadIdx.x & 63, r = lane >> 3, c = lane & 7;
     double p[2][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int w = 0; w < 2; ++w) p[u][w] = Pc[(16 * s + 2 * r + u) * LDP + 2 * c + w];
-    inner_step<0>(p, r, c, bad);
-    inner_step<1>(p, r, c, bad);
-    inner_step<2>(p, r, c, bad);
-    inner_step<3>(p, r, c, bad);
-    inner_step<4>(p, r, c, bad);
-    inner_step<5>(p, r, c, bad);
-    inner_step<6>(p, r, c, bad);
-    inner_step<7>(p, r, c, bad);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (c == j) {   // column panel of the pivot block: rows 2r.., cols 2j..
+            *reinterpret_cast<double2*>(&ipan[(2 * r) * 2]) = make_double2(p[0][0], p[0][1]);
+            *reinterpret_cast<double2*>(&ipan[(2 * r + 1) * 2]) = make_double2(p[1][0], p[1][1]);
+        }
+        __builtin_amdgcn_wave_barrier();
+        const double2 b0 = *reinterpret_cast<const double2*>(&ipan[(2 * j) * 2]);
+        const double2 b1 = *reinterpret_cast<const double2*>(&ipan[(2 * j + 1) * 2]);
+        const double2 i0 = *reinterpret_cast<const double2*>(&ipan[(2 * r) * 2]);
+        const double2 i1 = *reinterpret_cast<const double2*>(&ipan[(2 * r + 1) * 2]);
+        const double2 l0 = *reinterpret_cast<const double2*>(&ipan[(2 * c) * 2]);
+        const double2 l1 = *reinterpret_cast<const double2*>(&ipan[(2 * c + 1) * 2]);
+        __builtin_amdgcn_wave_barrier();
+        // q = -[a b; b d]^-1 = -adj / det.  The row panel's m = -A_iB q = (A_iB adj) / det: the
+        // adjugate products run beside the reciprocal, so only one multiply follows it.
+        const double a = b0.x, bb = b0.y, d = b1.y;
+        double det = fma(a, d, -bb * bb);
+        const bool badj = !(a > 0.0) || !isfinite(a) || !(det > 0.0) || !isfinite(det);   // branch-free
+        bad |= badj;
+        det = badj ? 1.0 : det;
+        const double ai[2][2] = {{i0.x, i0.y}, {i1.x, i1.y}};
+        double pre[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            pre[u][0] = fma(ai[u][0], d, -ai[u][1] * bb);
+            pre[u][1] = fma(ai[u][1], a, -ai[u][0] * bb);
+        }
+        const double rd = rcp_nr(det);
+        const double q00 = -d * rd, q01 = bb * rd, q11 = -a * rd;   // q10 = q01
+        const bool rowB = (r == j), colB = (c == j);
+        double m[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            m[u][0] = rowB ? (u == 0 ? q00 : q01) : pre[u][0] * rd;
+            m[u][1] = rowB ? (u == 0 ? q01 : q11) : pre[u][1] * rd;
+        }
+        const double al[2][2] = {{l0.x, l0.y}, {l1.x, l1.y}};   // al[w][b] = A_(2c+w),(2j+b) = A_Bl[b][w]
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                const double base = rowB ? 0.0 : p[u][w];
+                const double upd = fma(-m[u][1], al[w][1], fma(-m[u][0], al[w][0], base));
+                p[u][w] = colB ? m[u][w] : upd;
+            }
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -255,7 +237,8 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[NW], int k, double* __
     double* ws = DIAG_WS_IN_BUF ? &buf[0][0] : dws;   // the sweeps' workspace (dead once W is written)
     double* Pc = ws;                       // [64][LDP]  column panel A_:B
     double* Qn = ws + NB * LDP;            // [16][LDP]  -A_BB^-1
-    double* Mw = Qn + 16 * LDP * (1 + w);  // [16][LDP]  this wave's -M strip
+    double* ipan = Qn + 16 * LDP;          // [16][2]    inner column panel
+    double* Mw = ipan + 32 + 16 * LDP * w; // [16][LDP]  this wave's -M strip
     CHOL_STAMP(0);
     bool bad = false;
     CHOL_STAMP(1);
@@ -266,7 +249,7 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[NW], int k, double* __
         for (int r = 0; r < 4; ++r) Pc[(16 * w + trow(r)) * LDP + tcol()] = t[s][r];
         __syncthreads();
         CHOL_STAMP(2 + 4 * s);
-        if (tid < 64) inner_inverse16(Pc, s, Qn, bad);
+        if (tid < 64) inner_inverse16(Pc, s, Qn, ipan, bad);
         __syncthreads();
         CHOL_STAMP(3 + 4 * s);
         // M = A_(strip),B Q on the matrix cores; rows in B take Q itself (-Qn)
@@ -850,7 +833,7 @@ __device__ __forceinline__ f64x4 wmfma_nt(const double (*A)[LDT], const double (
 // chol_diag_tile on the NW x NW waves: t is this wave's tile (wr, wc) of the final diagonal tile k.
 // ws: the sweeps' workspace, DIAG_WS_W doubles (two tile buffers: sm.m | sm.n, dead by now); buf: a
 // tile buffer for W (the first of them: the sweeps are over when W is written into it).
-constexpr int DIAG_WS_W = NB * LDP + 16 * LDP + NWW * 16 * LDP;
+constexpr int DIAG_WS_W = NB * LDP + 16 * LDP + 32 + NWW * 16 * LDP;
 static_assert(DIAG_WS_W <= 2 * NB * LDT, "the wide sweeps' workspace spans two tile buffers");
 template <int RW>
 __device__ __forceinline__ void chol_diag_tile_w(f64x4& t, int k, double* __restrict__ Wk, double* __restrict__ R,
@@ -860,7 +843,8 @@ __device__ __forceinline__ void chol_diag_tile_w(f64x4& t, int k, double* __rest
     const int tid = threadIdx.x, w = tid >> 6, wr = wrow(), wc = wcol(), l = tid & 63, m = l & 15, kq = l >> 4, k0 = k * NB;
     double* Pc = ws;                       // [64][LDP]  column panel A_:B
     double* Qn = ws + NB * LDP;            // [16][LDP]  -A_BB^-1
-    double* Mw = Qn + 16 * LDP * (1 + w);  // [16][LDP]  this wave's -M strip (strip wr)
+    double* ipan = Qn + 16 * LDP;          // [16][2]    inner column panel
+    double* Mw = ipan + 32 + 16 * LDP * w; // [16][LDP]  this wave's -M strip (strip wr)
     bool bad = false;
 #pragma unroll
     for (int s = 0; s < NW; ++s) {
@@ -869,7 +853,7 @@ __device__ __forceinline__ void chol_diag_tile_w(f64x4& t, int k, double* __rest
 #pragma unroll
             for (int r = 0; r < 4; ++r) Pc[(16 * wr + trow(r)) * LDP + tcol()] = t[r];
         __syncthreads();
-        if (tid < 64) inner_inverse16(Pc, s, Qn, bad);
+        if (tid < 64) inner_inverse16(Pc, s, Qn, ipan, bad);
         __syncthreads();
         f64x4 mm = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll

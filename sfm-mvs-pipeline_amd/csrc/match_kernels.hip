@@ -591,14 +591,18 @@ void sift_screen_kernel(const WorkItem* __restrict__ work, const PairDev* __rest
 //   4 (l >> 4) + i, i = 0..3, of column l & 15.  Two row blocks per step feed one
 //   v_max3 per accumulator row i: 4 chains per lane x 4 lanes = 16 disjoint row
 //   subsets per query, the same bound as the 32x32 form.
-template <int QT, int WAVES, int MINW, int STAGE, bool SUBSET = false>
+// PERSIST (r04, product default): a grid of the device's resident workgroup slots takes work items
+// from a ticket counter in list order (the last partial round of a one-item-per-workgroup grid --
+// C2: 19 600 items on 512 slots, 38.3 rounds -- becomes a ragged end of single items).
+template <int QT, int WAVES, int MINW, int STAGE, bool SUBSET = false, bool PERSIST = false>
 __global__ __launch_bounds__(WAVES * 64, MINW)
 void sift_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
                           const ImgDev* __restrict__ imgs, const int8_t* __restrict__ desc8,
                           const int32_t* __restrict__ norm, const int32_t* __restrict__ keyc2,
                           int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
                           int32_t* __restrict__ qlist, int32_t* __restrict__ qcount, double ratio,
-                          int32_t* __restrict__ qmask = nullptr, unsigned long long* __restrict__ top2 = nullptr) {
+                          int32_t* __restrict__ qmask = nullptr, unsigned long long* __restrict__ top2 = nullptr,
+                          int32_t* __restrict__ ticket = nullptr, int n_work = 0) {
     constexpr int GLDS = STAGE * SIFT_DIM / (WAVES * 64 * 16);
     static_assert(GLDS * WAVES * 64 * 16 == STAGE * SIFT_DIM, "stage must split into whole 16-B pieces");
     static_assert(QT * WAVES * 16 == 512, "work items are 512 queries");
@@ -607,7 +611,19 @@ void sift_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __re
     __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
 
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
-    const WorkItem w = work[xcd_remap(blockIdx.x, gridDim.x)];
+    __shared__ int item_sh;
+    for (int round = 0;; ++round) {
+    int wi;
+    if constexpr (PERSIST) {
+        if (threadIdx.x == 0) item_sh = atomicAdd(ticket, 1);
+        __syncthreads();
+        wi = item_sh;
+        if (wi >= n_work) break;
+    } else {
+        if (round > 0) break;
+        wi = xcd_remap(blockIdx.x, gridDim.x);
+    }
+    const WorkItem w = work[wi];
     const PairDev P = pairs[w.pair];
     const ImgDev L = imgs[P.left], R = imgs[P.right];
     const int nq = L.rows, nt = R.rows;
@@ -730,6 +746,8 @@ void sift_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __re
             }
             out_idx[o] = UNSETTLED;   // pass 2 must overwrite it (assemble counts survivors)
         }
+    }
+    __syncthreads();   // the next item restages the LDS buffers and rewrites item_sh
     }
 }
 
@@ -1403,14 +1421,15 @@ void orb_mfma16_kernel(const WorkItem* __restrict__ work, const PairDev* __restr
 // true second best; Lowe's test is non-decreasing in d2, so when it fails at
 // (d1, d2') it fails for the true pair and the query is rejected exactly.  Every
 // other query goes to its pair's qlist for orb_mfma16_kernel<GATHER>.
-template <int QT, int WAVES, int MINW, int STAGE, bool SUBSET = false>
+template <int QT, int WAVES, int MINW, int STAGE, bool SUBSET = false, bool PERSIST = false>
 __global__ __launch_bounds__(WAVES * 64, MINW)
 void orb_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __restrict__ pairs,
                          const ImgDev* __restrict__ imgs, const uint8_t* __restrict__ desc4,
                          const int32_t* __restrict__ keyc, int32_t* __restrict__ out_idx,
                          float* __restrict__ out_dist, int32_t* __restrict__ qlist, int32_t* __restrict__ qcount,
                          double ratio, int32_t* __restrict__ qmask = nullptr,
-                         unsigned long long* __restrict__ top2 = nullptr) {
+                         unsigned long long* __restrict__ top2 = nullptr, int32_t* __restrict__ ticket = nullptr,
+                         int n_work = 0) {
     constexpr int ROWB = 128;
     constexpr int GLDS = STAGE * ROWB / (WAVES * 64 * 16);
     static_assert(GLDS * WAVES * 64 * 16 == STAGE * ROWB, "stage must split into whole 16-B pieces");
@@ -1421,7 +1440,19 @@ void orb_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __res
     __shared__ __attribute__((aligned(16))) char lds[2 * BUF_BYTES];
 
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
-    const WorkItem w = work[xcd_remap(blockIdx.x, gridDim.x)];
+    __shared__ int item_sh;
+    for (int round = 0;; ++round) {
+    int wi;
+    if constexpr (PERSIST) {   // as sift_screen16_kernel
+        if (threadIdx.x == 0) item_sh = atomicAdd(ticket, 1);
+        __syncthreads();
+        wi = item_sh;
+        if (wi >= n_work) break;
+    } else {
+        if (round > 0) break;
+        wi = xcd_remap(blockIdx.x, gridDim.x);
+    }
+    const WorkItem w = work[wi];
     const PairDev P = pairs[w.pair];
     const ImgDev L = imgs[P.left], R = imgs[P.right];
     const int nq = L.rows, nt = R.rows;
@@ -1549,6 +1580,8 @@ void orb_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __res
             }
             out_idx[o] = UNSETTLED;   // pass 2 must overwrite it (assemble counts survivors)
         }
+    }
+    __syncthreads();   // the next item restages the LDS buffers and rewrites item_sh
     }
 }
 
@@ -1953,6 +1986,20 @@ int sift_block_queries(int v) { return v == 2 || v == 4 || v == 23 ? 256 : 512; 
     sift_knn2_kernel<QT, W, MINW, ST, MF __VA_OPT__(,) __VA_ARGS__><<<n_work, W * 64, 0, st>>>(work, pairs, imgs, desc8, norm, keyc, \
                                                                      out_idx, out_dist, slow_list, slow_count, ratio)
 
+// Resident workgroups of a kernel on the current device (the persistent screens' grid); 0 = unknown.
+template <class F>
+int resident_slots(F kernel, int threads) {
+    int dev = 0, nb = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, 0) != hipSuccess) return 0;
+    return nb * prop.multiProcessorCount;
+}
+bool persist_screens() {   // SFMX_SCREEN_PERSIST=0 (diagnostic build): one workgroup per item, as r03
+    const char* e = SFMX_DIAG_ENV("SFMX_SCREEN_PERSIST");
+    return !(e && e[0] == '0');
+}
+
 hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,
                             const int8_t* desc8, const int32_t* norm, const int32_t* keyc, const int32_t* keyc2,
                             int32_t* qlist, int32_t* qcount, int n_pairs, const int32_t* porder, WorkItem* work2,
@@ -1962,11 +2009,17 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
     if (n_work == 0) return hipSuccess;
     const int v = sift_variant();
     if (v == 0 || v >= 101) {   // two-pass ratio test: screen every query, exact kernel on the rest
-        hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * n_pairs, st);
+        hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * (n_pairs + 1), st);   // + the screen's ticket
         if (e != hipSuccess) return e;
         if (pass2_variant() == 10 && qmask && top2) {   // subset-restricted pass 2
-            sift_screen16_kernel<8, 4, 2, 64, true><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc8, norm, keyc2, out_idx,
-                                                                           out_dist, qlist, qcount, ratio, qmask, top2);
+            static const int slots = resident_slots(sift_screen16_kernel<8, 4, 2, 64, true, true>, 256);
+            if (slots > 0 && persist_screens())
+                sift_screen16_kernel<8, 4, 2, 64, true, true><<<std::min(n_work, slots), 256, 0, st>>>(
+                    work, pairs, imgs, desc8, norm, keyc2, out_idx, out_dist, qlist, qcount, ratio, qmask, top2,
+                    qcount + n_pairs, n_work);
+            else
+                sift_screen16_kernel<8, 4, 2, 64, true><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc8, norm, keyc2, out_idx,
+                                                                               out_dist, qlist, qcount, ratio, qmask, top2);
             if (ev_screen) {
                 e = hipEventRecord(ev_screen, st);
                 if (e != hipSuccess) return e;
@@ -2143,11 +2196,17 @@ hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pair
                            unsigned long long* top2) {
     if (n_work == 0) return hipSuccess;
     if (orb_variant() == 0 || orb_variant() >= 10) {   // two-pass ratio test (default)
-        hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * n_pairs, st);
+        hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * (n_pairs + 1), st);   // + the screen's ticket
         if (e != hipSuccess) return e;
         if (orb_variant() == 0 && qmask && top2) {   // subset-restricted pass 2 (default)
-            orb_screen16_kernel<8, 4, 2, 64, true><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx,
-                                                                          out_dist, qlist, qcount, ratio, qmask, top2);
+            static const int slots = resident_slots(orb_screen16_kernel<8, 4, 2, 64, true, true>, 256);
+            if (slots > 0 && persist_screens())
+                orb_screen16_kernel<8, 4, 2, 64, true, true><<<std::min(n_work, slots), 256, 0, st>>>(
+                    work, pairs, imgs, desc4, keyc, out_idx, out_dist, qlist, qcount, ratio, qmask, top2,
+                    qcount + n_pairs, n_work);
+            else
+                orb_screen16_kernel<8, 4, 2, 64, true><<<n_work, 256, 0, st>>>(work, pairs, imgs, desc4, keyc, out_idx,
+                                                                              out_dist, qlist, qcount, ratio, qmask, top2);
             if (ev_screen) {
                 e = hipEventRecord(ev_screen, st);
                 if (e != hipSuccess) return e;

@@ -283,6 +283,28 @@ def test_previously_failing_variants(env, variant):
             assert_same(m, off, em, eoff)
 
 
+@pytest.mark.parametrize("persist", ["1", "0"])
+@pytest.mark.parametrize("kind", ["sift", "orb"])
+def test_persistent_screen_vs_oracle(kind, persist):
+    """r04: the product screens run as a grid of resident workgroups fed by a ticket counter
+    (sfmx_screen16 PERSIST); with the per-item grid of r03 (SFMX_SCREEN_PERSIST=0) both give the
+    oracle's matches: mixed sizes, a 1-row image (the full-size C2 / C3 / C4 tests run many more
+    items than resident slots, i.e. several items per workgroup)."""
+    from oracle import oracle
+    if kind == "sift":
+        sizes = [1, 2048, 700, 1100, 1600, 513, 900, 2048]
+        base = synth.sift_images(len(sizes), 2048, seed=94)
+        imgs = [b[:n] for b, n in zip(base, sizes)]
+    else:
+        base = synth.orb_images(8, 2048, seed=95)
+        imgs = [b[:n] for b, n in zip(base, [2048, 1, 700, 513, 1500, 256, 1200, 2048])]
+    pairs = sfmx.pairs_unordered(len(imgs))
+    with diagnostic(SFMX_SCREEN_PERSIST=persist):
+        m, off, _, _ = run(imgs, pairs)
+    em, eoff = oracle.match_pairs(imgs, pairs)
+    assert_same(m, off, em, eoff)
+
+
 @pytest.mark.parametrize("batches", ["1", "2", "3", "64"])
 @pytest.mark.parametrize("kind", ["sift", "orb"])
 def test_overlapped_two_pass_batches_vs_oracle(kind, batches):

@@ -30,12 +30,13 @@ int main() {
             if (a != 1 || b != 1) tasks.push_back(make_int4(a, b, 0, 1));
     int zero = 0;
     double *S, *W, *S0, *contrib; int *fail, *src, *leaves; int4* dt;
-    hipMalloc(&S, h.size() * 8); hipMalloc(&S0, h.size() * 8); hipMalloc(&W, (size_t)T * NB * NB * 8); hipMalloc(&fail, 4);
+    hipMalloc(&S, h.size() * 8); hipMalloc(&S0, h.size() * 8); hipMalloc(&W, (size_t)T * NB * NB * 8); hipMalloc(&fail, 64);
     hipMalloc(&contrib, (size_t)T * 3 * RW * 8); hipMalloc(&src, 4); hipMalloc(&leaves, 4); hipMalloc(&dt, tasks.size() * 16);
     hipMemcpy(src, &zero, 4, hipMemcpyHostToDevice); hipMemcpy(leaves, &zero, 4, hipMemcpyHostToDevice);
     hipMemcpy(dt, tasks.data(), tasks.size() * 16, hipMemcpyHostToDevice);
     hipMemcpy(S0, h.data(), h.size() * 8, hipMemcpyHostToDevice);
-    hipMemset(fail, 0, 4);
+    hipMemset(fail, 0, 64);
+    { const int one = 1; hipMemcpy(fail + 1, &one, 4, hipMemcpyHostToDevice); }   // the step gate open (ba_kernels.hpp step_gated)
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
     long long st[64];
     for (int rep = 0; rep < 3; ++rep) {
@@ -61,6 +62,30 @@ int main() {
         hipMemcpyFromSymbol(st, HIP_SYMBOL(g_chol_stamps), sizeof st);
         printf("chol_level(0) %.2f us: load %lld gemm1 %lld store+gemm2 %lld -> inverse %lld | diag inverse %lld | GT %lld ticks\n", ms * 1e3,
                st[31] - st[30], st[32] - st[31], st[33] - st[32], st[0] - st[33], st[21] - st[0], st[34] - st[21]);
+    }
+    // the leaf inverse of tile 0 through the one-launch kernels: chol_factor (NW waves) vs chol_factor_w
+    // (NW x NW waves), one item each (a leaf), 5 launches each, alternating
+    {
+        const int nver = T * (T + 1) / 2;
+        int4 leaf = make_int4(0, -1, 0, 0), zero4 = make_int4(0, 0, 0, 0);
+        int4 *items, *need; int *ctr, *tctr; double* pbuf;
+        hipMalloc(&items, 16); hipMalloc(&need, 16); hipMalloc(&ctr, 4 * (nver + 4)); hipMalloc(&tctr, 64);
+        hipMalloc(&pbuf, 8 * 8192);
+        hipMemcpy(items, &leaf, 16, hipMemcpyHostToDevice); hipMemcpy(need, &zero4, 16, hipMemcpyHostToDevice);
+        hipMemset(ctr, 0, 4 * (nver + 4)); hipMemset(tctr, 0, 64);
+        double* R = S + (size_t)npad * npad;
+        for (int rep = 0; rep < 5; ++rep)
+            for (int wide = 0; wide < 2; ++wide) {
+                hipMemcpy(S, S0, h.size() * 8, hipMemcpyDeviceToDevice);
+                float ms;
+                hipEventRecord(e0);
+                if (wide) chol_factor_w<RW><<<1, NTW>>>(S, npad, R, dt, items, need, src, W, contrib, fail, pbuf, tctr, ctr, 1, nver, DAG_TIMEOUT);
+                else chol_factor<RW><<<1, NTH>>>(S, npad, R, dt, items, need, src, W, contrib, fail, pbuf, tctr, ctr, 1, nver, DAG_TIMEOUT);
+                hipEventRecord(e1);
+                hipEventSynchronize(e1);
+                hipEventElapsedTime(&ms, e0, e1);
+                printf("leaf inverse via %s: %.2f us\n", wide ? "chol_factor_w (16 waves)" : "chol_factor (4 waves)  ", ms * 1e3);
+            }
     }
     int hf; hipMemcpy(&hf, fail, 4, hipMemcpyDeviceToHost);
     printf("fail flag %d\n", hf);
