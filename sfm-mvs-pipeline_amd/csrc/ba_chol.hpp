@@ -769,7 +769,7 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
 }
 
 // ---------------------------------------------------------------------------------------------
-// chol_factor on NW x NW waves (SFMX_BA_WIDE, default on; 1024 threads at NB = 64).  The NW-wave form
+// chol_factor on NW x NW waves (SFMX_BA_WIDE=1, diagnostic build: measured no faster, ba_solver.hip ensure_plan).  The NW-wave form
 // above gives each wave a 16-row strip of NW column tiles, so a 64^3 tile product is NW x 16 MFMA
 // steps per wave and a 64 x 64 tile load NB^2 / (2 NTH) 16-B loads per thread: on the level chain
 // (r02q stamps: loads 2.7 us, the two products 2.9 + 3.4 us per level) every workgroup of the launch

@@ -122,7 +122,7 @@ struct sfmx_ba_ctx {
     bool split = true;             // SFMX_BA_SPLIT=0: chol_level (a task's sources in one workgroup)
     std::vector<int> part_start;   // per level: parts[part_start[l] .. part_start[l + 1])
     bool dag = true;               // SFMX_BA_DAG=0: one launch per level (chol_leaves + chol_level[_split])
-    bool wide = true;              // SFMX_BA_WIDE=0: chol_factor on NW waves instead of chol_factor_w on NW x NW
+    bool wide = false;             // SFMX_BA_WIDE=1 (diagnostic): chol_factor_w on NW x NW waves instead of chol_factor
     int n_ditems = 0, n_ver = 0;
     long long dag_timeout = DAG_TIMEOUT;   // in-launch wait bound (wall-clock ticks without progress)
     int dag_fallbacks = 0;                 // steps re-run with the per-level launches after a wait timed out
@@ -695,8 +695,11 @@ int ensure_plan(sfmx_ba_ctx* c) {
         const int tpo = std::max(1, NTH / (NB * RW)), opt = NB * RW / (NTH / tpo);
         const size_t slot = std::max<size_t>((size_t)(4 * NW + opt) * NTH, (size_t)4 * NTW + (size_t)opt * NTH);   // chol_factor | _w
         RC(c->pbuf.alloc(sizeof(double) * (size_t)max_slots * slot));
+        // chol_factor_w (SFMX_BA_WIDE=1, diagnostic build only): measured no faster (r04c / r04d: the 16-wave
+        // diagonal inverse's barriers cost what the quarter-length products save; C5 0.627-0.631 vs
+        // 0.613-0.616 ms per iteration for the r03 library, profiles/r04d_ab.txt)
         const char* ew = SFMX_DIAG_ENV("SFMX_BA_WIDE");
-        c->wide = !(ew && ew[0] == '0');
+        c->wide = ew && ew[0] == '1';
         RC(c->lctr.alloc(sizeof(int) * (size_t)((pl.tasks.size() + 4) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->lctr.p, 0, c->lctr.bytes, st));
         const char* e = SFMX_DIAG_ENV("SFMX_BA_SPLIT");

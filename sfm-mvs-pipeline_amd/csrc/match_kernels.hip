@@ -591,7 +591,7 @@ void sift_screen_kernel(const WorkItem* __restrict__ work, const PairDev* __rest
 //   4 (l >> 4) + i, i = 0..3, of column l & 15.  Two row blocks per step feed one
 //   v_max3 per accumulator row i: 4 chains per lane x 4 lanes = 16 disjoint row
 //   subsets per query, the same bound as the 32x32 form.
-// PERSIST (r04, product default): a grid of the device's resident workgroup slots takes work items
+// PERSIST (r04, diagnostic build only, see persist_screens): a grid of resident workgroup slots takes work items
 // from a ticket counter in list order (the last partial round of a one-item-per-workgroup grid --
 // C2: 19 600 items on 512 slots, 38.3 rounds -- becomes a ragged end of single items).
 template <int QT, int WAVES, int MINW, int STAGE, bool SUBSET = false, bool PERSIST = false>
@@ -1995,9 +1995,13 @@ int resident_slots(F kernel, int threads) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, 0) != hipSuccess) return 0;
     return nb * prop.multiProcessorCount;
 }
-bool persist_screens() {   // SFMX_SCREEN_PERSIST=0 (diagnostic build): one workgroup per item, as r03
+// SFMX_SCREEN_PERSIST=1 (diagnostic build only): the ticket-fed persistent screens.  Measured slower in
+// r04d (C2 6.85 vs 6.40 ms, C4 18.96 vs 17.44 ms per launch, profiles/r04d_ab.txt): items taken in list
+// order land on every XCD, so each XCD's L2 streams every active train image, where the
+// one-item-per-workgroup grid's XCD-contiguous mapping keeps a train image on one XCD.
+bool persist_screens() {
     const char* e = SFMX_DIAG_ENV("SFMX_SCREEN_PERSIST");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 
 hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pairs, const ImgDev* imgs,

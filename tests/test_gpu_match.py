@@ -286,8 +286,9 @@ def test_previously_failing_variants(env, variant):
 @pytest.mark.parametrize("persist", ["1", "0"])
 @pytest.mark.parametrize("kind", ["sift", "orb"])
 def test_persistent_screen_vs_oracle(kind, persist):
-    """r04: the product screens run as a grid of resident workgroups fed by a ticket counter
-    (sfmx_screen16 PERSIST); with the per-item grid of r03 (SFMX_SCREEN_PERSIST=0) both give the
+    """r04: the screens as a grid of resident workgroups fed by a ticket counter (PERSIST,
+    SFMX_SCREEN_PERSIST=1, measured slower and kept in the diagnostic build only) and the product's
+    one-workgroup-per-item grid (SFMX_SCREEN_PERSIST=0) both give the
     oracle's matches: mixed sizes, a 1-row image (the full-size C2 / C3 / C4 tests run many more
     items than resident slots, i.e. several items per workgroup)."""
     from oracle import oracle
