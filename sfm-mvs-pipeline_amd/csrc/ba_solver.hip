@@ -939,7 +939,10 @@ int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
 // sorted on its own: a bucket is ordered and grouped independently and kept between calls, and an
 // update (sfmx_ba_update, the SfM loop's grown scene) redoes only the buckets whose points changed
 // (HostScratch below).
-constexpr int BUCKET_CAMS = 8;
+// 4 (r04; 8 before): an SfM step's new camera dirties its own bucket and the ring's closing one, so the
+// points re-ordered and re-grouped per update halve (C5: ~2 x 4000 instead of ~2 x 8000), for a few more
+// partial groups at bucket edges
+constexpr int BUCKET_CAMS = 4;
 
 // The caller's observations as a point-major view: obs of point p are view positions
 // [start[p], start[p + 1]); position i is caller observation i (point-major input, pm) or vobs[i].
@@ -1000,7 +1003,16 @@ int bucket_of(int minc) { return minc < 0 ? 0 : minc / BUCKET_CAMS; }
 
 // Point groups, chunks, local cameras, assembly task lists and camera slot lists (see ba_group.hpp).
 struct TopoSeg;
+struct PairRef { uint64_t key; int g, la, lb; };   // finish_topology: one (camera a, camera b) block of a group
 struct Topology {   // kept with the context: its vectors keep their capacity between calls
+    std::vector<PairRef> pr, pr_out;   // finish_topology's scratch (kept: no per-call allocation)
+    std::vector<int> pr_cnt, slot_g;
+    // the camera co-visibility of the problem's points: bit a C + b set when some point is observed by
+    // cameras a and b (a != b).  S_cc's pattern and the factorization plan come from it, not from the
+    // point groups' camera unions (a group's dense block holds exact zeros for the pairs none of its
+    // points connects: on the C5 ring the unions add ~150 such pairs, the elimination tree gets one level
+    // more and 82 instead of 66 nonzero tiles, r04)
+    std::vector<uint64_t> covis;
     std::vector<Grp> grp;
     std::vector<Chunk> chk;
     std::vector<Batch> bat;
@@ -1156,9 +1168,46 @@ int group_points(int P, int slots) {
 }
 
 // The camera slots and assembly tasks of the merged groups (tp.grp / gcam in internal order).
+bool covisible(const Topology& tp, int C, int a, int b) {
+    const size_t bit = (size_t)a * C + b;
+    return (tp.covis[bit >> 6] >> (bit & 63)) & 1;
+}
+// The co-visibility bitset of the problem's points (parallel ranges of points, OR-merged).
+void build_covis(const sfmx_ba_problem* pb, const View& v, Topology& tp) {
+    const int P = pb->n_points, C = pb->n_cams;
+    const size_t words = ((size_t)C * C + 63) / 64;
+    constexpr int PIECES = 16;
+    std::vector<std::vector<uint64_t>> part(PIECES);
+    sfmx::parallel_items(PIECES, [&](int r) {
+        std::vector<uint64_t>& b = part[r];
+        b.assign(words, 0);
+        std::vector<int> cams;
+        const int p0 = (int)((int64_t)P * r / PIECES), p1 = (int)((int64_t)P * (r + 1) / PIECES);
+        for (int p = p0; p < p1; ++p) {
+            cams.clear();
+            for (int a = v.start[p]; a < v.start[p + 1]; ++a) cams.push_back(pb->obs_cam[v.obs(a)]);
+            for (size_t i = 0; i < cams.size(); ++i)
+                for (size_t j = 0; j < cams.size(); ++j)
+                    if (cams[i] != cams[j]) {
+                        const size_t bit = (size_t)cams[i] * C + cams[j];
+                        b[bit >> 6] |= 1ull << (bit & 63);
+                    }
+        }
+    });
+    tp.covis.assign(words, 0);
+    sfmx::parallel_ranges((int64_t)words, 16, [&](int64_t w0, int64_t w1) {
+        for (int64_t w = w0; w < w1; ++w) {
+            uint64_t x = 0;
+            for (int r = 0; r < PIECES; ++r) x |= part[r][w];
+            tp.covis[w] = x;
+        }
+    });
+}
+
 void finish_topology(int C, int K, Topology& tp) {
     // camera slots: per camera, its (group, local camera) slots in group order
-    std::vector<int> slot_g(tp.gcam.size());
+    std::vector<int>& slot_g = tp.slot_g;
+    slot_g.resize(tp.gcam.size());
     for (int g = 0; g < (int)tp.grp.size(); ++g)
         for (int lc = 0; lc < tp.grp[g].u; ++lc) slot_g[tp.grp[g].cam_off + lc] = g;
     tp.cref_start.assign(C + 1, 0);
@@ -1183,21 +1232,30 @@ void finish_topology(int C, int K, Topology& tp) {
         return e;
     };
     {   // (camera a, camera b) keys in group order, stably sorted: tasks in key order, entries in group order
-        struct PairRef { uint64_t key; int g, la, lb; };
-        std::vector<PairRef> pr;
+        std::vector<PairRef>& pr = tp.pr;
         size_t npr = 0;
         for (const Grp& G : tp.grp) npr += (size_t)G.u * (G.u + 1) / 2;
-        pr.reserve(npr);
-        for (int g = 0; g < (int)tp.grp.size(); ++g) {
-            const Grp& G = tp.grp[g];
-            for (int la = 0; la < G.u; ++la)
-                for (int lb = la; lb < G.u; ++lb)
-                    pr.push_back(PairRef{((uint64_t)(uint32_t)tp.gcam[G.cam_off + la] << 32) | (uint32_t)tp.gcam[G.cam_off + lb],
-                                         g, la, lb});
+        pr.resize(npr);
+        {   // the groups' pairs in parallel ranges of groups (offsets from the per-group counts)
+            const int ng = (int)tp.grp.size();
+            std::vector<size_t> goff(ng + 1, 0);
+            for (int g = 0; g < ng; ++g) goff[g + 1] = goff[g] + (size_t)tp.grp[g].u * (tp.grp[g].u + 1) / 2;
+            sfmx::parallel_ranges(ng, 16, [&](int64_t g0, int64_t g1) {
+                for (int64_t g = g0; g < g1; ++g) {
+                    const Grp& G = tp.grp[g];
+                    size_t e = goff[g];
+                    for (int la = 0; la < G.u; ++la)
+                        for (int lb = la; lb < G.u; ++lb)
+                            pr[e++] = PairRef{((uint64_t)(uint32_t)tp.gcam[G.cam_off + la] << 32) | (uint32_t)tp.gcam[G.cam_off + lb],
+                                              (int)g, la, lb};
+                }
+            });
         }
         if ((int64_t)C * C <= ((int64_t)1 << 22)) {   // stable counting sort on the pair index a C + b
-            std::vector<int> cnt((size_t)C * C + 1, 0);
-            std::vector<PairRef> out(pr.size());
+            std::vector<int>& cnt = tp.pr_cnt;
+            cnt.assign((size_t)C * C + 1, 0);
+            std::vector<PairRef>& out = tp.pr_out;
+            out.resize(pr.size());
             auto idx = [C](const PairRef& x) { return (size_t)(x.key >> 32) * C + (size_t)(x.key & 0xffffffffu); };
             for (const PairRef& x : pr) cnt[idx(x) + 1]++;
             for (size_t i = 1; i < cnt.size(); ++i) cnt[i] += cnt[i - 1];
@@ -1210,9 +1268,12 @@ void finish_topology(int C, int K, Topology& tp) {
         for (size_t i = 0; i < pr.size();) {
             ATask t{0, (int)(pr[i].key >> 32), (int)(pr[i].key & 0xffffffffu), (int)tp.ents.size(), 0, 0, 0, 0};
             size_t j = i;
-            for (; j < pr.size() && pr[j].key == pr[i].key; ++j) tp.ents.push_back(ent(pr[j].g, pr[j].la, pr[j].lb));
-            t.l1 = (int)tp.ents.size();
-            tp.tasks.push_back(t);
+            while (j < pr.size() && pr[j].key == pr[i].key) ++j;
+            if (t.a == t.b || covisible(tp, C, t.a, t.b)) {   // a pair no point connects: exact zeros, no task
+                for (size_t q = i; q < j; ++q) tp.ents.push_back(ent(pr[q].g, pr[q].la, pr[q].lb));
+                t.l1 = (int)tp.ents.size();
+                tp.tasks.push_back(t);
+            }
             i = j;
         }
     }
@@ -1560,6 +1621,7 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
             tp.dp_max = std::max(tp.dp_max, g.dp_max);
         }
     tick(hs.tm[5]);
+    build_covis(pb, v, tp);
     finish_topology(C, K, tp);
     tick(hs.tm[6]);
     // shadows of the changed blocks (point-major problems only: the next update compares slices)
@@ -1722,7 +1784,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     c->setup_ms[6] = hs.n_dirty;   // buckets redone (the ordering's and the groups' ms are [5] and [0])
     // local camera co-visibility (the pose blocks this rank's points create)
     c->adj.assign((size_t)C * C, 0);
-    for (const ATask& t : tp.tasks)
+    for (const ATask& t : tp.tasks)   // (the pose-pair tasks are exactly the co-visible pairs)
         if (t.type == 0 && t.a != t.b) c->adj[(size_t)t.a * C + t.b] = c->adj[(size_t)t.b * C + t.a] = 1;
     // a plan is reused only when this graph is the one it was built from; ranks of a sharded solve
     // rebuild on every update (the plan needs the co-visibility all-reduced over all of them)
@@ -2041,8 +2103,10 @@ int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
     HIPCHK(hipMemcpyAsync(iv.data(), x + c->ne + 6 * (size_t)c->C, sizeof(double) * c->K, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     for (int j = 0; j < c->K; ++j) if (c->isrc[j] >= 0) pb->intr[c->isrc[j]] = iv[j];   // unreferenced cameras: untouched
-    for (int q = 0; q < c->P; ++q)
-        for (int i = 0; i < 3; ++i) pb->points[3 * (size_t)c->pperm[q] + i] = pts[3 * (size_t)q + i];
+    sfmx::parallel_ranges(c->P, c->P >= 65536 ? 16 : 1, [&](int64_t q0, int64_t q1) {   // write-back in caller order
+        for (int64_t q = q0; q < q1; ++q)
+            for (int i = 0; i < 3; ++i) pb->points[3 * (size_t)c->pperm[q] + i] = pts[3 * (size_t)q + i];
+    });
     return SFMX_OK;
 }
 
@@ -2179,8 +2243,26 @@ int sfmx_ba_debug_check_topology(const sfmx_ba_problem* pb, int32_t gpts, double
     const auto t1 = clk::now();
     gather_obs(hs, pb->n_obs, roc, hs.tp.obs_lc, hs.tp.obs_row);
     const std::string why = check_topology(pb->n_points, pb->n_cams, pb->n_obs, L.K, hs.pt_start, roc.data(), hs.tp);
-    if (ms) { ms[0] = d(t0, t1); ms[1] = 0.0; ms[2] = d(t1, clk::now()); }
+    int pose_pairs = 0;   // S_cc's nonzero 6 x 6 pose blocks (a <= b) the groups create: the factorization's pattern
+    for (const ATask& t : hs.tp.tasks) pose_pairs += t.type == 0;
+    if (ms) { ms[0] = d(t0, t1); ms[1] = pose_pairs; ms[2] = d(t1, clk::now()); }
     if (!why.empty()) return fail(SFMX_EINTERNAL, "BA topology check: " + why);
+    return (int)hs.tp.grp.size();
+}
+
+// diagnostic build only: the camera co-visibility S_cc's pattern comes from (the pose pairs of the point
+// groups, C x C bytes into adj) for `gpts` points per group (0 = GPTS), without a device.
+int sfmx_ba_debug_adjacency(const sfmx_ba_problem* pb, int32_t gpts, uint8_t* adj) {
+    RC(validate(pb));
+    IntrLayout L;
+    RC(intr_layout(pb, L));
+    HostScratch hs;
+    std::vector<int> pperm, operm;
+    host_setup(pb, L.K, gpts > 0 ? std::min(gpts, GPTS) : GPTS, false, hs, pperm, operm);
+    const int C = pb->n_cams;
+    std::memset(adj, 0, (size_t)C * C);
+    for (const ATask& t : hs.tp.tasks)
+        if (t.type == 0 && t.a != t.b) adj[(size_t)t.a * C + t.b] = adj[(size_t)t.b * C + t.a] = 1;
     return (int)hs.tp.grp.size();
 }
 

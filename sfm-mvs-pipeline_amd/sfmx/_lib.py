@@ -129,6 +129,7 @@ PROTOTYPES = {
     "sfmx_ba_setup_ms": (C.c_int, [_vp, _P(C.c_double), C.c_int32]),
     "sfmx_ba_release_cache": (C.c_int, []),
     "sfmx_ba_debug_check_topology": (C.c_int, [_P(sfmx_ba_problem), C.c_int32, _P(C.c_double)]),   # diagnostic library only
+    "sfmx_ba_debug_adjacency": (C.c_int, [_P(sfmx_ba_problem), C.c_int32, _vp]),   # diagnostic library only
     "sfmx_ba_debug_incremental_check": (C.c_int, [_P(sfmx_ba_problem), _P(sfmx_ba_problem), C.c_int32, _i32p,
                                                   _P(C.c_double)]),   # diagnostic library only
     "sfmx_ba_jacobian": (C.c_int, [_P(sfmx_ba_problem), C.c_int32, _vp, _vp, _vp, _vp]),
