@@ -53,8 +53,8 @@ FP64_PEAK_TFLOPS = 256 * 128 * 2.4e9 / 1e12
 # BA algorithmic work per LM iteration at C5: S assembly ~2-2.5 + J ~0.4 +
 # Cholesky ~0.58 GFLOP; bytes: obs read twice, points, S written and read
 BA_FLOP_PER_ITER_C5, BA_BYTES_PER_ITER_C5 = 3.0e9, 0.1e9
-FEAT_PMC_FILE = "r03_pmc_features.json"   # tools/pmc_feat.sh -> tools/pmc_feat_json.py
-BA_PMC_FILE = "r03n_pmc_ba.json"   # tools/pmc_ba.sh on the current kernels (r03n: slot-sized point groups)
+FEAT_PMC_FILE = "r04_pmc_features.json"   # tools/pmc_feat.sh -> tools/pmc_feat_json.py
+BA_PMC_FILE = "r04_pmc_ba.json"   # tools/pmc_ba.sh -> tools/pmc_ba_json.py (r04b session)
 
 
 def parse():
@@ -466,8 +466,9 @@ def bench_3d2d(args, imgs, my_pairs, got, off, rank, world, local, stream):
 
 
 SIFT_KERNELS = ("sift_screen16_kernel", "sift_subset_kernel", "sift_settle_kernel")
-PMC_FILES = {"sift": ("r02_pmc_sift_c2.json", SIFT_KERNELS, 50),
-             "orb": ("r02_pmc_orb_c4.json", ("orb_screen16_kernel", "orb_subset_kernel", "orb_settle_kernel"), 200),
+# r04 files: counter totals per matcher launch (tools/pmc_match.sh -> tools/pmc_launch_json.py)
+PMC_FILES = {"sift": ("r04_pmc_sift_c2.json", SIFT_KERNELS, 50),
+             "orb": ("r04_pmc_orb_c4.json", ("orb_screen16_kernel", "orb_subset_kernel", "orb_settle_kernel"), 200),
              "c3": ("r02_pmc_sift_c3.json", SIFT_KERNELS, 200)}
 
 
