@@ -220,7 +220,7 @@ __device__ __forceinline__ int find_level(const Lvl* lv, int nl, int row) {
 __global__ __launch_bounds__(256)
 void orb_nms_kernel(const uint8_t* __restrict__ score, const Lvl* __restrict__ lv, int nl, int border, int pass,
                     int* __restrict__ row_count, const int* __restrict__ row_off, int32_t* __restrict__ cpos,
-                    uint8_t* __restrict__ cscore, int cap, int64_t istride) {
+                    uint8_t* __restrict__ cscore, int cap, int64_t istride, uint64_t* __restrict__ kmask, int mw) {
     __shared__ int wsum[4];
     const int row = blockIdx.x;
     {
@@ -230,6 +230,7 @@ void orb_nms_kernel(const uint8_t* __restrict__ score, const Lvl* __restrict__ l
         if (row_off) row_off = at(row_off, bo);
         if (cpos) cpos = at(cpos, bo);
         if (cscore) cscore = at(cscore, bo);
+        kmask = at(kmask, bo) + (int64_t)row * mw;   // the row's keep bits (pass 0 writes, pass 1 reads: r04)
     }
     const int l = find_level(lv, nl, row);
     const Lvl L = lv[l];
@@ -240,20 +241,32 @@ void orb_nms_kernel(const uint8_t* __restrict__ score, const Lvl* __restrict__ l
     int base = pass ? row_off[row] : 0;
     int total = 0;
     const uint8_t* s = score + L.off;
+    if (!row_ok) {   // no corner in this row (pass 0 counts 0; pass 1 has nothing to write)
+        if (!pass && threadIdx.x == 0) row_count[row] = 0;
+        return;
+    }
     for (int xc = 0; xc < L.w; xc += 256) {
         const int x = xc + threadIdx.x;
         bool keep = false;
         uint8_t sc = 0;
-        if (row_ok && x >= b && x < L.w - b) {
-            const uint8_t* p = s + (int64_t)y * L.w + x;
-            sc = p[0];
-            if (sc) {
-                const int w = L.w;
-                keep = sc > p[-1] && sc > p[1] && sc > p[-w - 1] && sc > p[-w] && sc > p[-w + 1] && sc > p[w - 1] &&
-                       sc > p[w] && sc > p[w + 1];
+        uint64_t m;
+        if (!pass) {
+            if (x >= b && x < L.w - b) {
+                const uint8_t* p = s + (int64_t)y * L.w + x;
+                sc = p[0];
+                if (sc) {
+                    const int w = L.w;
+                    keep = sc > p[-1] && sc > p[1] && sc > p[-w - 1] && sc > p[-w] && sc > p[-w + 1] && sc > p[w - 1] &&
+                           sc > p[w] && sc > p[w + 1];
+                }
             }
+            m = __ballot(keep);
+            if (lane == 0) kmask[xc / 64 + wid] = m;
+        } else {
+            m = kmask[xc / 64 + wid];   // (wave-uniform load)
+            keep = (m >> lane) & 1;
+            if (keep) sc = s[(int64_t)y * L.w + x];
         }
-        const uint64_t m = __ballot(keep);
         if (lane == 0) wsum[wid] = __popcll(m);
         __syncthreads();
         int before = 0, chunk = 0;
@@ -726,7 +739,7 @@ void orb_copy_kp_kernel(const Kp* __restrict__ src, const int* __restrict__ st, 
 // ------------------------------------------------------------------ compute(): blur + rBRIEF
 // GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on the 8U level through OpenCV's
 // integer separable path: taps x 2^8, (sum + 2^15) >> 16, saturated.
-constexpr int BT_X = 64, BT_Y = 16, BR = 3;
+constexpr int BT_X = 64, BT_Y = 32, BR = 3;
 __constant__ int c_taps[7];
 
 __device__ __forceinline__ int reflect101(int p, int n) {
@@ -735,6 +748,9 @@ __device__ __forceinline__ int reflect101(int p, int n) {
     return p;
 }
 
+// r04: 64 x 32 output tiles (halo rows 38 / 32 instead of 22 / 16); interior tiles load without the
+// reflection; the row pass makes 4 neighbouring sums per thread from a 10-byte window, the column pass 8
+// rows of one column from a 14-sum window (the same taps in the same order: the same integers).
 __global__ __launch_bounds__(256)
 void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const int* __restrict__ st,
                      uint8_t* __restrict__ blur, int nl, int64_t istride) {
@@ -745,31 +761,54 @@ void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv
     const Lvl L = lv[l];
     const int x0 = blockIdx.x * BT_X, y0 = blockIdx.y * BT_Y;
     if (x0 >= L.w || y0 >= L.h) return;
-    __shared__ uint8_t t[BT_Y + 2 * BR][BT_X + 2 * BR + 2];
-    __shared__ int r[BT_Y + 2 * BR][BT_X + 1];
+    constexpr int TH = BT_Y + 2 * BR, TW = BT_X + 2 * BR;
+    __shared__ uint8_t t[TH][TW + 2];
+    __shared__ int r[TH][BT_X + 1];
     const uint8_t* src = pyr + L.off;
-    for (int i = threadIdx.x; i < (BT_Y + 2 * BR) * (BT_X + 2 * BR); i += 256) {
-        const int ty = i / (BT_X + 2 * BR), tx = i % (BT_X + 2 * BR);
-        const int gy = reflect101(y0 + ty - BR, L.h), gx = reflect101(x0 + tx - BR, L.w);
-        t[ty][tx] = src[(int64_t)gy * L.w + gx];
+    const bool interior = x0 >= BR && x0 + BT_X + BR <= L.w && y0 >= BR && y0 + BT_Y + BR <= L.h;
+    if (interior) {
+        for (int i = threadIdx.x; i < TH * TW; i += 256) {
+            const int ty = i / TW, tx = i % TW;
+            t[ty][tx] = src[(int64_t)(y0 + ty - BR) * L.w + (x0 + tx - BR)];
+        }
+    } else {
+        for (int i = threadIdx.x; i < TH * TW; i += 256) {
+            const int ty = i / TW, tx = i % TW;
+            const int gy = reflect101(y0 + ty - BR, L.h), gx = reflect101(x0 + tx - BR, L.w);
+            t[ty][tx] = src[(int64_t)gy * L.w + gx];
+        }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < (BT_Y + 2 * BR) * BT_X; i += 256) {
-        const int ty = i / BT_X, tx = i % BT_X;
-        int s = 0;
+    for (int i = threadIdx.x; i < TH * (BT_X / 4); i += 256) {   // 4 sums per thread
+        const int ty = i / (BT_X / 4), tx = 4 * (i % (BT_X / 4));
+        int w[10];
 #pragma unroll
-        for (int j = 0; j < 7; j++) s += c_taps[j] * t[ty][tx + j];
-        r[ty][tx] = s;
+        for (int k = 0; k < 10; ++k) w[k] = t[ty][tx + k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int s = 0;
+#pragma unroll
+            for (int j = 0; j < 7; j++) s += c_taps[j] * w[q + j];
+            r[ty][tx + q] = s;
+        }
     }
     __syncthreads();
-    const int tx = threadIdx.x % BT_X;
-    for (int ty = threadIdx.x / BT_X; ty < BT_Y; ty += 256 / BT_X) {
-        const int x = x0 + tx, y = y0 + ty;
-        if (x >= L.w || y >= L.h) continue;
-        int s = 0;
+    static_assert(BT_Y % 8 == 0 && (BT_X * BT_Y / 8) == 256, "one column strip of 8 rows per thread");
+    const int tx = threadIdx.x % BT_X, ty0 = 8 * (threadIdx.x / BT_X);
+    const int x = x0 + tx;
+    if (x < L.w) {
+        int w[14];
 #pragma unroll
-        for (int j = 0; j < 7; j++) s += c_taps[j] * r[ty + j][tx];
-        blur[L.off + (int64_t)y * L.w + x] = (uint8_t)min(max((s + (1 << 15)) >> 16, 0), 255);
+        for (int k = 0; k < 14; ++k) w[k] = r[ty0 + k][tx];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int y = y0 + ty0 + q;
+            if (y >= L.h) break;
+            int s = 0;
+#pragma unroll
+            for (int j = 0; j < 7; j++) s += c_taps[j] * w[q + j];
+            blur[L.off + (int64_t)y * L.w + x] = (uint8_t)min(max((s + (1 << 15)) >> 16, 0), 255);
+        }
     }
 }
 
@@ -1087,8 +1126,10 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
         // descriptor staging (host buffers) -- every part 256-B aligned, so the offsets are the same in
         // every block
         auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        const int mw = (maxw + 255) / 256 * 4;   // keep-bit words per NMS row
         const size_t blk = 3 * r(px) + r(CAND_CAP * 4) + r(CAND_CAP) + 2 * r(CAND_CAP * sizeof(Resp)) + 2 * r(CAND_CAP * 4) +
                            2 * r(CAND_CAP * sizeof(Kp)) + r(CAND_CAP * 4) + 2 * r((size_t)(rows + 1) * 4) +
+                           r((size_t)rows * mw * 8) +
                            (inputs_on_device ? 0 : r((size_t)width * height) + r((size_t)std::max(capmax, 1) * 32));
         const size_t shared_b = r(std::max<size_t>(tables.size(), 1) * sizeof(AxisEnt)) + r(sizeof(Lvl) * nl) +
                                 r(sizeof(int) * umax.size()) + r(sizeof(ImgIO) * G) + r(sizeof(int) * CS * G);
@@ -1115,6 +1156,7 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             int* keep = A.take<int>(CAND_CAP);
             int* row_cnt = A.take<int>(rows + 1);
             int* row_off = A.take<int>(rows + 1);
+            uint64_t* kmask = A.take<uint64_t>((size_t)rows * mw);
             uint8_t* t = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)width * height);
             uint8_t* ddesc = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)std::max(capmax, 1) * 32);
             const int64_t istride = (int64_t)A.used;   // == blk (every part 256-B rounded)
@@ -1161,10 +1203,10 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             orb_fast_kernel<<<dim3((maxw + FT_X - 1) / FT_X, (maxh + FT_Y - 1) / FT_Y, nl * gz), 256, 0, st>>>(
                 pyr, dlv, thr, score, nl, istride);
             orb_nms_kernel<<<dim3(rows, gz), 256, 0, st>>>(score, dlv, nl, border, 0, row_cnt, nullptr, nullptr, nullptr,
-                                                           (int)CAND_CAP, istride);
+                                                           (int)CAND_CAP, istride, kmask, mw);
             orb_scan_kernel<<<gz, 1024, 0, st>>>(row_cnt, rows, row_off, istride, stats);
             orb_nms_kernel<<<dim3(rows, gz), 256, 0, st>>>(score, dlv, nl, border, 1, nullptr, row_off, cpos, cscore,
-                                                           (int)CAND_CAP, istride);
+                                                           (int)CAND_CAP, istride, kmask, mw);
             // retainBest(2 n_l) on the FAST scores, Harris responses, retainBest(n_l) on them (device)
             SelCounts s1{}, s2{};
             for (int l = 0; l < nl; l++) { s1.n[l] = 2 * per[l]; s2.n[l] = per[l]; }
