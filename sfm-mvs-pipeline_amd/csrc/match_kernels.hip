@@ -591,6 +591,21 @@ void sift_screen_kernel(const WorkItem* __restrict__ work, const PairDev* __rest
 //   4 (l >> 4) + i, i = 0..3, of column l & 15.  Two row blocks per step feed one
 //   v_max3 per accumulator row i: 4 chains per lane x 4 lanes = 16 disjoint row
 //   subsets per query, the same bound as the 32x32 form.
+// The persistent screens' item source: XCD x (HW_REG_XCC_ID) owns the contiguous item range
+// [x n / 8, (x + 1) n / 8) -- the train-image locality of xcd_remap -- and takes from its own ticket
+// counter; an XCD whose range is done steals from the next ones (only the tail leaves its L2).
+// ticket[0..8) is zero at launch.  -> item, or -1 when every range is done.
+__device__ __forceinline__ int xcd_ticket(int32_t* ticket, int n) {
+    const int x0 = (int)(__builtin_amdgcn_s_getreg(0x1814) & 7);   // hwreg(HW_REG_XCC_ID, 0, 4)
+    for (int k = 0; k < 8; ++k) {
+        const int x = (x0 + k) & 7, b0 = (int)((int64_t)n * x / 8), b1 = (int)((int64_t)n * (x + 1) / 8);
+        if (b1 <= b0) continue;
+        if (__hip_atomic_load(&ticket[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= b1 - b0) continue;
+        const int t = atomicAdd(&ticket[x], 1);
+        if (t < b1 - b0) return b0 + t;
+    }
+    return -1;
+}
 // PERSIST (r04, diagnostic build only, see persist_screens): a grid of resident workgroup slots takes work items
 // from a ticket counter in list order (the last partial round of a one-item-per-workgroup grid --
 // C2: 19 600 items on 512 slots, 38.3 rounds -- becomes a ragged end of single items).
@@ -615,10 +630,10 @@ void sift_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __re
     for (int round = 0;; ++round) {
     int wi;
     if constexpr (PERSIST) {
-        if (threadIdx.x == 0) item_sh = atomicAdd(ticket, 1);
+        if (threadIdx.x == 0) item_sh = xcd_ticket(ticket, n_work);
         __syncthreads();
         wi = item_sh;
-        if (wi >= n_work) break;
+        if (wi < 0) break;
     } else {
         if (round > 0) break;
         wi = xcd_remap(blockIdx.x, gridDim.x);
@@ -1443,11 +1458,11 @@ void orb_screen16_kernel(const WorkItem* __restrict__ work, const PairDev* __res
     __shared__ int item_sh;
     for (int round = 0;; ++round) {
     int wi;
-    if constexpr (PERSIST) {   // as sift_screen16_kernel
-        if (threadIdx.x == 0) item_sh = atomicAdd(ticket, 1);
+    if constexpr (PERSIST) {
+        if (threadIdx.x == 0) item_sh = xcd_ticket(ticket, n_work);
         __syncthreads();
         wi = item_sh;
-        if (wi >= n_work) break;
+        if (wi < 0) break;
     } else {
         if (round > 0) break;
         wi = xcd_remap(blockIdx.x, gridDim.x);
@@ -1995,10 +2010,11 @@ int resident_slots(F kernel, int threads) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, 0) != hipSuccess) return 0;
     return nb * prop.multiProcessorCount;
 }
-// SFMX_SCREEN_PERSIST=1 (diagnostic build only): the ticket-fed persistent screens.  Measured slower in
-// r04d (C2 6.85 vs 6.40 ms, C4 18.96 vs 17.44 ms per launch, profiles/r04d_ab.txt): items taken in list
-// order land on every XCD, so each XCD's L2 streams every active train image, where the
-// one-item-per-workgroup grid's XCD-contiguous mapping keeps a train image on one XCD.
+// SFMX_SCREEN_PERSIST=1 (diagnostic build only): the ticket-fed persistent screens.  A single global
+// ticket measured slower in r04d (C2 6.85 vs 6.40 ms, C4 18.96 vs 17.44 ms per launch,
+// profiles/r04d_ab.txt): items taken in list order landed on every XCD, so each XCD's L2 streamed every
+// active train image, where the one-item-per-workgroup grid's XCD-contiguous mapping keeps a train image
+// on one XCD.  Hence the per-XCD ranges and tickets of xcd_ticket (r04e A/B).
 bool persist_screens() {
     const char* e = SFMX_DIAG_ENV("SFMX_SCREEN_PERSIST");
     return e && e[0] == '1';
@@ -2013,7 +2029,7 @@ hipError_t launch_sift_knn2(const WorkItem* work, int n_work, const PairDev* pai
     if (n_work == 0) return hipSuccess;
     const int v = sift_variant();
     if (v == 0 || v >= 101) {   // two-pass ratio test: screen every query, exact kernel on the rest
-        hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * (n_pairs + 1), st);   // + the screen's ticket
+        hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * (n_pairs + 8), st);   // + the screen's XCD tickets
         if (e != hipSuccess) return e;
         if (pass2_variant() == 10 && qmask && top2) {   // subset-restricted pass 2
             static const int slots = resident_slots(sift_screen16_kernel<8, 4, 2, 64, true, true>, 256);
@@ -2200,7 +2216,7 @@ hipError_t launch_orb_mfma(const WorkItem* work, int n_work, const PairDev* pair
                            unsigned long long* top2) {
     if (n_work == 0) return hipSuccess;
     if (orb_variant() == 0 || orb_variant() >= 10) {   // two-pass ratio test (default)
-        hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * (n_pairs + 1), st);   // + the screen's ticket
+        hipError_t e = hipMemsetAsync(qcount, 0, sizeof(int32_t) * (n_pairs + 8), st);   // + the screen's XCD tickets
         if (e != hipSuccess) return e;
         if (orb_variant() == 0 && qmask && top2) {   // subset-restricted pass 2 (default)
             static const int slots = resident_slots(orb_screen16_kernel<8, 4, 2, 64, true, true>, 256);

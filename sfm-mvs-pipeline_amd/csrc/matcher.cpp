@@ -398,7 +398,7 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
             if ((rc = m->qmask.ensure(sizeof(int32_t) * std::max<int64_t>(dense, 1)))) return rc;
             if ((rc = m->top2.ensure(2 * sizeof(uint64_t) * std::max<int64_t>(dense, 1)))) return rc;
         }
-        if ((rc = m->qcount.ensure(sizeof(int32_t) * (n_pairs + 1)))) return rc;   // + the persistent screen's ticket
+        if ((rc = m->qcount.ensure(sizeof(int32_t) * (n_pairs + 8)))) return rc;   // + the persistent screens' XCD tickets
         if ((rc = m->porder.ensure(sizeof(int32_t) * std::max(n_pairs, 1)))) return rc;
         if ((rc = m->work2.ensure(sizeof(WorkItem) * std::max<size_t>(4 * work.size(), 1)))) return rc;   // pass-2 items >= 128 queries
         if ((rc = m->work2_n.ensure(sizeof(int32_t)))) return rc;

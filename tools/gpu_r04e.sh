@@ -20,4 +20,12 @@ for i in 1 2; do
   SFMX_LIB_NAME=libsfmx_r03.so timeout -k 10 300 python -u bench.py --only-orb-features --no-cpu-baseline > gpurun_out/r04e_orbf_r03_$i.log 2>&1 || exit 7
 done
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_r04e_orb1 -o orb1 -- python3 $GRAFT_REPO_ROOT/tools/orb_prof.py 32 > $GRAFT_REPO_ROOT/gpurun_out/r04e_prof_orb1.log 2>&1 || exit 8
+M="--no-cpu-baseline --no-ba --no-orb --no-c3 --no-homography --no-f4 --no-mvs --no-features --no-orb-features"
+for i in 1 2; do
+  timeout -k 10 300 python -u bench.py $M > gpurun_out/r04e_c2_items_$i.log 2>&1 || exit 9
+  SFMX_LIB_NAME=libsfmx_diag.so SFMX_SCREEN_PERSIST=1 timeout -k 10 300 python -u bench.py $M > gpurun_out/r04e_c2_xcd_$i.log 2>&1 || exit 10
+done
+timeout -k 10 300 python -u bench.py --workload orb $M > gpurun_out/r04e_c4_items.log 2>&1 || exit 11
+SFMX_LIB_NAME=libsfmx_diag.so SFMX_SCREEN_PERSIST=1 timeout -k 10 300 python -u bench.py --workload orb $M > gpurun_out/r04e_c4_xcd.log 2>&1 || exit 12
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_match.py -m gpu -k persistent > gpurun_out/r04e_pytest_persist.log 2>&1 || exit 13
 echo done
