@@ -1172,38 +1172,6 @@ bool covisible(const Topology& tp, int C, int a, int b) {
     const size_t bit = (size_t)a * C + b;
     return (tp.covis[bit >> 6] >> (bit & 63)) & 1;
 }
-// The co-visibility bitset of the problem's points (parallel ranges of points, OR-merged).
-void build_covis(const sfmx_ba_problem* pb, const View& v, Topology& tp) {
-    const int P = pb->n_points, C = pb->n_cams;
-    const size_t words = ((size_t)C * C + 63) / 64;
-    constexpr int PIECES = 16;
-    std::vector<std::vector<uint64_t>> part(PIECES);
-    sfmx::parallel_items(PIECES, [&](int r) {
-        std::vector<uint64_t>& b = part[r];
-        b.assign(words, 0);
-        std::vector<int> cams;
-        const int p0 = (int)((int64_t)P * r / PIECES), p1 = (int)((int64_t)P * (r + 1) / PIECES);
-        for (int p = p0; p < p1; ++p) {
-            cams.clear();
-            for (int a = v.start[p]; a < v.start[p + 1]; ++a) cams.push_back(pb->obs_cam[v.obs(a)]);
-            for (size_t i = 0; i < cams.size(); ++i)
-                for (size_t j = 0; j < cams.size(); ++j)
-                    if (cams[i] != cams[j]) {
-                        const size_t bit = (size_t)cams[i] * C + cams[j];
-                        b[bit >> 6] |= 1ull << (bit & 63);
-                    }
-        }
-    });
-    tp.covis.assign(words, 0);
-    sfmx::parallel_ranges((int64_t)words, 16, [&](int64_t w0, int64_t w1) {
-        for (int64_t w = w0; w < w1; ++w) {
-            uint64_t x = 0;
-            for (int r = 0; r < PIECES; ++r) x |= part[r][w];
-            tp.covis[w] = x;
-        }
-    });
-}
-
 void finish_topology(int C, int K, Topology& tp) {
     // camera slots: per camera, its (group, local camera) slots in group order
     std::vector<int>& slot_g = tp.slot_g;
@@ -1423,6 +1391,7 @@ struct Bucket {
     std::vector<int> lpt;           // bucket-local pt_start (pts.size() + 1)
     std::vector<int> roc, oin;      // per internal observation: its camera; its index within its point
     std::vector<short> lc, row;     // obs_lc / obs_row (ba_group.hpp)
+    std::vector<uint32_t> cpairs;   // the camera pairs (a << 16 | b, a < b) some point of the bucket connects
     std::vector<int> sub;           // sub-segment starts in points (+ the end)
     std::vector<TopoSeg> topo;      // per sub-segment, offsets local to the bucket / sub-segment
     int no = 0;                     // observations
@@ -1562,6 +1531,26 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
                 B.roc[k] = pb->obs_cam[v.obs(a)];
                 B.oin[k] = j;
             }
+        {   // the bucket's co-visible camera pairs, deduplicated through a per-thread bit table
+            thread_local std::vector<uint64_t> mark;
+            const size_t words = ((size_t)C * C + 63) / 64;
+            if (mark.size() < words) mark.assign(words, 0);
+            B.cpairs.clear();
+            for (int i = 0; i < np; ++i)
+                for (int x = B.lpt[i]; x < B.lpt[i + 1]; ++x)
+                    for (int y = B.lpt[i]; y < B.lpt[i + 1]; ++y) {
+                        const int a = B.roc[x], b = B.roc[y];
+                        if (a >= b) continue;
+                        const size_t bit = (size_t)a * C + b;
+                        if ((mark[bit >> 6] >> (bit & 63)) & 1) continue;
+                        mark[bit >> 6] |= 1ull << (bit & 63);
+                        B.cpairs.push_back((uint32_t)a << 16 | (uint32_t)b);
+                    }
+            for (uint32_t q : B.cpairs) {   // leave the table clear for the thread's next bucket
+                const size_t bit = (size_t)(q >> 16) * C + (q & 0xffff);
+                mark[bit >> 6] &= ~(1ull << (bit & 63));
+            }
+        }
         B.lc.assign(B.no, 0);
         B.row.assign(B.no, 0);
         B.sub.clear();
@@ -1621,7 +1610,15 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
             tp.dp_max = std::max(tp.dp_max, g.dp_max);
         }
     tick(hs.tm[5]);
-    build_covis(pb, v, tp);
+    {   // the problem's co-visibility: the union of the buckets' pairs (kept ones included)
+        tp.covis.assign(((size_t)C * C + 63) / 64, 0);
+        for (const Bucket& B : hs.bk)
+            for (uint32_t q : B.cpairs) {
+                const size_t a = q >> 16, b = q & 0xffff, b1 = a * C + b, b2 = b * C + a;
+                tp.covis[b1 >> 6] |= 1ull << (b1 & 63);
+                tp.covis[b2 >> 6] |= 1ull << (b2 & 63);
+            }
+    }
     finish_topology(C, K, tp);
     tick(hs.tm[6]);
     // shadows of the changed blocks (point-major problems only: the next update compares slices)
