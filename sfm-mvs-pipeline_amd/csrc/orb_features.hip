@@ -5,14 +5,15 @@
 // i.e. OpenCV 4.5.1's ORB_Impl::detectAndCompute twice.  Bit-identical to the
 // restatement in oracle/orb_oracle.cpp (which lists the OpenCV pieces restated).
 //
-// Device pipeline per image (one HIP stream; every level of the pyramid lives in
-// one packed u8 slab in HBM, level l at lv[l].off, pitch = width):
+// Device pipeline per chunk of same-size images (one HIP stream; every level of the pyramid lives in
+// one packed u8 slab in HBM, level l at lv[l].off, rows lv[l].pitch = width rounded up to 64 bytes):
+//   orb_copy_kernel       level 0 from the caller's image (4 pixels per thread)
 //   orb_resize_kernel     level l = INTER_LINEAR_EXACT resize of level l-1 (8.8 fixed
-//                         point; per-axis offset/coefficient tables from the host)
-//   orb_fast_kernel       FAST 9/16 score map of every level in one launch (64 x 16
-//                         tiles + 3-pixel halo staged in LDS)
-//   orb_nms_kernel        3x3 strict maximum + the 31-pixel border test, ordered
-//                         (raster) compaction per row, two passes around a row scan
+//                         point; per-axis offset/coefficient tables from the host; 4 pixels per thread)
+//   orb_fast_nms_kernel   FAST 9/16 scores + the 3x3 strict maximum + the border test on 64 x 16
+//                         tiles (16-byte tile loads, scores in LDS): keep words and their counts
+//   orb_scan_kernel       the rows' corner counts scanned
+//   orb_rows_kernel       ordered (raster) compaction, one wave per row, from the keep words
 //   orb_retain_kernel     retainBest(2 n_l) per level on the FAST scores: the permutation of
 //                         the reference's libstdc++ nth_element + partition, in parallel
 //   orb_harris_kernel     Harris response (7x7 block, k = 0.04) per kept corner
@@ -22,8 +23,8 @@
 //   orb_compact_kernel    the in-border keypoints in order, their count
 //   orb_blur_kernel       7x7 integer Gaussian of the levels the keypoints use (LDS tile)
 //   orb_brief_kernel      rBRIEF, 32 lanes per keypoint, one descriptor byte per lane
-// One host wait per image (the keypoint count at the end; r02 waited 4 times and ran both
-// retainBest steps on the host).  Roofline: HBM-bound byte work.
+// One host wait per chunk (the keypoint counts at the end).  Roofline: HBM-bound byte work (see
+// DESIGN.md §3).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -52,6 +53,7 @@ constexpr float HARRIS_K = 0.04f;
 struct Lvl {              // one pyramid level in the packed slabs
     int64_t off;          // byte offset of (0, 0) in pyr / score / blur slabs
     int w, h;
+    int pitch;            // bytes per row: w rounded up to 64 (r04: 16-byte tile loads, 4-byte stores)
     int row0;             // first global row index of this level (NMS rows)
     float scale, inv_scale;
     int ax_off, ay_off;   // offsets of this level's axis tables in the coefficient buffer (level >= 1)
@@ -100,204 +102,201 @@ __device__ __forceinline__ uint32_t hval(const uint8_t* __restrict__ r, const Ax
     return min((uint32_t)e.m0 * r[e.ofs] + (uint32_t)e.m1 * r[e.ofs + 1], 0xFFFFu);
 }
 
+// r04: 4 neighbouring outputs per thread, one 4-byte store (the level pitch is a multiple of 64; the
+// outputs past the width land in the row's padding, computed from the replicated edge column)
 __global__ __launch_bounds__(256)
 void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int l,
                        const AxisEnt* __restrict__ tables, int64_t istride) {
     pyr = at(pyr, (int64_t)blockIdx.z * istride);
     const Lvl D = lv[l], S = lv[l - 1];
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    const int x = (blockIdx.x * 256 + threadIdx.x) * 4, y = blockIdx.y;
     if (x >= D.w || y >= D.h) return;
     const AxisEnt* ax = tables + D.ax_off;
     const AxisEnt* ay = tables + D.ay_off;
     const uint8_t* src = pyr + S.off;
     const int last_ofs = ax[D.w - 1].ofs;
-    uint32_t v;
+    uint32_t out = 0;
     if (y < D.ydmin || y >= D.ydmax) {
-        const int sy = y < D.ydmin ? 0 : S.h - 1;
-        v = (hval(src + (int64_t)sy * S.w, ax, x, D.xdmin, D.xdmax, last_ofs) + 128u) >> 8;
+        const uint8_t* r = src + (int64_t)(y < D.ydmin ? 0 : S.h - 1) * S.pitch;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) out |= min((hval(r, ax, x + i, D.xdmin, D.xdmax, last_ofs) + 128u) >> 8, 255u) << (8 * i);
     } else {
         const AxisEnt e = ay[y];
-        const uint32_t h0 = hval(src + (int64_t)e.ofs * S.w, ax, x, D.xdmin, D.xdmax, last_ofs);
-        const uint32_t h1 = hval(src + (int64_t)(e.ofs + 1) * S.w, ax, x, D.xdmin, D.xdmax, last_ofs);
-        v = (h0 * e.m0 + h1 * e.m1 + 32768u) >> 16;
+        const uint8_t* r0 = src + (int64_t)e.ofs * S.pitch;
+        const uint8_t* r1 = r0 + S.pitch;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t h0 = hval(r0, ax, x + i, D.xdmin, D.xdmax, last_ofs);
+            const uint32_t h1 = hval(r1, ax, x + i, D.xdmin, D.xdmax, last_ofs);
+            out |= min((h0 * e.m0 + h1 * e.m1 + 32768u) >> 16, 255u) << (8 * i);
+        }
     }
-    pyr[D.off + (int64_t)y * D.w + x] = (uint8_t)min(v, 255u);
+    *reinterpret_cast<uint32_t*>(pyr + D.off + (int64_t)y * D.pitch + x) = out;
 }
 
-__global__ void orb_copy_kernel(const ImgIO* __restrict__ io, int W, int H, uint8_t* __restrict__ dst, int64_t istride) {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, g = blockIdx.z;
-    const uint8_t* img = io[g].img;
-    const int64_t pitch = io[g].pitch;
-    dst = at(dst, (int64_t)g * istride);
-    if (x < W && y < H) dst[(int64_t)y * W + x] = img[(int64_t)y * pitch + x];
-}
-
-// ------------------------------------------------------------------ FAST 9/16
-constexpr int FT_X = 64, FT_Y = 16, FT_H = 3;
-__constant__ int8_t c_ring[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
-                                     {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
-
+// level 0 from the caller's image: 4 pixels per thread, one 4-byte store into the padded row
 __global__ __launch_bounds__(256)
-void orb_fast_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int threshold,
-                     uint8_t* __restrict__ score, int nl, int64_t istride) {
+void orb_copy_kernel(const ImgIO* __restrict__ io, int W, int H, int P0, uint8_t* __restrict__ dst, int64_t istride) {
+    const int x = (blockIdx.x * 256 + threadIdx.x) * 4, y = blockIdx.y, g = blockIdx.z;
+    if (x >= W || y >= H) return;
+    const uint8_t* p = io[g].img + (int64_t)y * io[g].pitch + x;
+    dst = at(dst, (int64_t)g * istride);
+    uint32_t v = p[0];
+    if (x + 1 < W) v |= (uint32_t)p[1] << 8;
+    if (x + 2 < W) v |= (uint32_t)p[2] << 16;
+    if (x + 3 < W) v |= (uint32_t)p[3] << 24;
+    *reinterpret_cast<uint32_t*>(dst + (int64_t)y * P0 + x) = v;
+}
+
+// ------------------------------------------------------------------ FAST 9/16 + NMS
+// r04: FAST and the 3x3 strict-maximum test in one tile pass.  A workgroup owns 64 x 16 pixels of
+// one level: the image tile (rows y0-4 .. y0+19, columns x0-16 .. x0+79) comes in as 16-byte
+// loads, the FAST scores of the 66 x 18 ring around the tile go to LDS, and every wave tests its
+// rows against LDS: one keep word per (row, 64-pixel word) from the ballot, its popcount, and the
+// tile's scores (read back only at kept pixels).  r03 wrote the score map from one kernel and
+// re-read every 3 x 3 neighbourhood from HBM in a second.
+constexpr int FT_X = 64, FT_Y = 16;
+constexpr int FI_R = FT_Y + 8, FI_C = 96;        // image tile
+constexpr int FS_R = FT_Y + 2, FS_C = FT_X + 2;  // score tile
+
+// cornerScore<16> of the pixel c points at, when it is a FAST 9/16 corner, else 0 (S: LDS row stride)
+template <int S>
+__device__ __forceinline__ int fast_score_lds(const uint8_t* c, int threshold) {
+    const int v = c[0];
+    const int p[16] = {c[3 * S],  c[3 * S + 1],  c[2 * S + 2],  c[S + 3],  c[3],  c[-S + 3], c[-2 * S + 2], c[-3 * S + 1],
+                       c[-3 * S], c[-3 * S - 1], c[-2 * S - 2], c[-S - 3], c[-3], c[S - 3],  c[2 * S - 2],  c[3 * S - 1]};
+    int d[16];
+    uint32_t dark = 0, bright = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        d[k] = v - p[k];
+        dark |= (uint32_t)(p[k] < v - threshold) << k;
+        bright |= (uint32_t)(p[k] > v + threshold) << k;
+    }
+    // a run of >= 9 consecutive ring pixels (cyclic): AND of 9 rotations
+    const uint32_t dd = dark | (dark << 16), bb = bright | (bright << 16);
+    uint32_t rd = dd, rb = bb;
+#pragma unroll
+    for (int s = 1; s < 9; s++) { rd &= dd >> s; rb &= bb >> s; }
+    if (!((rd | rb) & 0xFFFFu)) return 0;
+    int a0 = threshold;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int a = min(min(d[(k + 1) & 15], d[(k + 2) & 15]), d[(k + 3) & 15]);
+        a = min(a, d[(k + 4) & 15]);
+        a = min(a, d[(k + 5) & 15]);
+        a = min(a, d[(k + 6) & 15]);
+        a = min(a, d[(k + 7) & 15]);
+        a = min(a, d[(k + 8) & 15]);
+        a0 = max(a0, min(a, d[k]));
+        a0 = max(a0, min(a, d[(k + 9) & 15]));
+    }
+    int b0 = -a0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int b = max(max(d[(k + 1) & 15], d[(k + 2) & 15]), d[(k + 3) & 15]);
+        b = max(b, d[(k + 4) & 15]);
+        b = max(b, d[(k + 5) & 15]);
+        b = max(b, d[(k + 6) & 15]);
+        b = max(b, d[(k + 7) & 15]);
+        b = max(b, d[(k + 8) & 15]);
+        b0 = min(b0, max(b, d[k]));
+        b0 = min(b0, max(b, d[(k + 9) & 15]));
+    }
+    return (-b0 - 1) & 255;
+}
+
+// grid (mw words, rows / 16, image * nl + level).  kmask / wcnt: (global row) x mw, every word of every
+// row of the level written (0 past the width, outside the border, or without a corner).  Scores are 0
+// in FAST's own 3-pixel frame; a corner needs b <= x < w - b, b <= y < h - b (b = max(border, 3)),
+// a nonzero score and a score above all 8 neighbours'.
+__global__ __launch_bounds__(256)
+void orb_fast_nms_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int threshold, int border,
+                         uint8_t* __restrict__ score, uint64_t* __restrict__ kmask, uint8_t* __restrict__ wcnt, int mw,
+                         int nl, int64_t istride) {
     const int64_t bo = (int64_t)(blockIdx.z / nl) * istride;   // z = image * nl + level
-    pyr = at(pyr, bo);
-    score = at(score, bo);
     const Lvl L = lv[blockIdx.z % nl];
     const int x0 = blockIdx.x * FT_X, y0 = blockIdx.y * FT_Y;
-    if (x0 >= L.w || y0 >= L.h) return;
-    __shared__ uint8_t t[FT_Y + 2 * FT_H][FT_X + 2 * FT_H + 2];
-    const uint8_t* src = pyr + L.off;
-    for (int i = threadIdx.x; i < (FT_Y + 2 * FT_H) * (FT_X + 2 * FT_H); i += 256) {
-        const int ty = i / (FT_X + 2 * FT_H), tx = i % (FT_X + 2 * FT_H);
-        const int gy = min(max(y0 + ty - FT_H, 0), L.h - 1), gx = min(max(x0 + tx - FT_H, 0), L.w - 1);
-        t[ty][tx] = src[(int64_t)gy * L.w + gx];
+    if (y0 >= L.h) return;
+    const int ny = min(FT_Y, L.h - y0), b = max(border, 3);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t w0 = (int64_t)(L.row0 + y0) * mw + blockIdx.x;
+    kmask = at(kmask, bo) + w0;
+    wcnt = at(wcnt, bo) + w0;
+    if (!(x0 + FT_X > b && x0 < L.w - b && y0 + ny > b && y0 < L.h - b)) {   // no pixel of the tile may be a corner
+        if (threadIdx.x < ny) {
+            kmask[(int64_t)threadIdx.x * mw] = 0;
+            wcnt[(int64_t)threadIdx.x * mw] = 0;
+        }
+        return;
+    }
+    __shared__ __align__(16) uint8_t ti[FI_R][FI_C];
+    __shared__ uint8_t ts[FS_R][FS_C + 2];
+    const uint8_t* src = at(pyr, bo) + L.off;
+    if (threadIdx.x < FI_R * (FI_C / 16)) {
+        const int r = threadIdx.x / (FI_C / 16), q = threadIdx.x % (FI_C / 16);
+        const int gy = min(max(y0 - 4 + r, 0), L.h - 1), gx = x0 - 16 + 16 * q;
+        uint4 v = make_uint4(0, 0, 0, 0);   // (columns outside the row: only ever read for frame pixels)
+        if (gx >= 0 && gx < L.pitch) v = *reinterpret_cast<const uint4*>(src + (int64_t)gy * L.pitch + gx);
+        *reinterpret_cast<uint4*>(&ti[r][16 * q]) = v;
     }
     __syncthreads();
-    const int tx = threadIdx.x % FT_X;
-    for (int ty = threadIdx.x / FT_X; ty < FT_Y; ty += 256 / FT_X) {
-        const int x = x0 + tx, y = y0 + ty;
-        if (x >= L.w || y >= L.h) continue;
+    for (int i = threadIdx.x; i < FS_R * FS_C; i += 256) {
+        const int sy = i / FS_C, sx = i - sy * FS_C;
+        const int x = x0 - 1 + sx, y = y0 - 1 + sy;
         int sc = 0;
-        if (x >= 3 && x < L.w - 3 && y >= 3 && y < L.h - 3) {
-            const int v = t[ty + FT_H][tx + FT_H];
-            int d[16];
-            uint32_t dark = 0, bright = 0;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const int p = t[ty + FT_H + c_ring[k][1]][tx + FT_H + c_ring[k][0]];
-                d[k] = v - p;
-                dark |= (uint32_t)(p < v - threshold) << k;
-                bright |= (uint32_t)(p > v + threshold) << k;
-            }
-            // a run of >= 9 consecutive ring pixels (cyclic): AND of 9 rotations
-            const uint32_t dd = dark | (dark << 16), bb = bright | (bright << 16);
-            uint32_t rd = dd, rb = bb;
-#pragma unroll
-            for (int s = 1; s < 9; s++) { rd &= dd >> s; rb &= bb >> s; }
-            if ((rd | rb) & 0xFFFFu) {
-                // cornerScore<16>
-                int a0 = threshold;
-#pragma unroll
-                for (int k = 0; k < 16; k += 2) {
-                    int a = min(min(d[(k + 1) & 15], d[(k + 2) & 15]), d[(k + 3) & 15]);
-                    a = min(a, d[(k + 4) & 15]);
-                    a = min(a, d[(k + 5) & 15]);
-                    a = min(a, d[(k + 6) & 15]);
-                    a = min(a, d[(k + 7) & 15]);
-                    a = min(a, d[(k + 8) & 15]);
-                    a0 = max(a0, min(a, d[k]));
-                    a0 = max(a0, min(a, d[(k + 9) & 15]));
-                }
-                int b0 = -a0;
-#pragma unroll
-                for (int k = 0; k < 16; k += 2) {
-                    int b = max(max(d[(k + 1) & 15], d[(k + 2) & 15]), d[(k + 3) & 15]);
-                    b = max(b, d[(k + 4) & 15]);
-                    b = max(b, d[(k + 5) & 15]);
-                    b = max(b, d[(k + 6) & 15]);
-                    b = max(b, d[(k + 7) & 15]);
-                    b = max(b, d[(k + 8) & 15]);
-                    b0 = min(b0, max(b, d[k]));
-                    b0 = min(b0, max(b, d[(k + 9) & 15]));
-                }
-                sc = (-b0 - 1) & 255;
-            }
+        if (x >= 3 && x < L.w - 3 && y >= 3 && y < L.h - 3) sc = fast_score_lds<FI_C>(&ti[sy + 3][sx + 15], threshold);
+        ts[sy][sx] = (uint8_t)sc;
+    }
+    __syncthreads();
+    score = at(score, bo) + L.off;
+    const int x = x0 + lane;
+    for (int ty = wid; ty < ny; ty += 4) {
+        const int y = y0 + ty;
+        const int s = ts[ty + 1][lane + 1];
+        bool keep = false;
+        if (s && y >= b && y < L.h - b && x >= b && x < L.w - b)
+            keep = s > ts[ty][lane] && s > ts[ty][lane + 1] && s > ts[ty][lane + 2] && s > ts[ty + 1][lane] &&
+                   s > ts[ty + 1][lane + 2] && s > ts[ty + 2][lane] && s > ts[ty + 2][lane + 1] && s > ts[ty + 2][lane + 2];
+        const uint64_t m = __ballot(keep);
+        if (lane == 0) {
+            kmask[(int64_t)ty * mw] = m;
+            wcnt[(int64_t)ty * mw] = (uint8_t)__popcll(m);
         }
-        score[L.off + (int64_t)y * L.w + x] = (uint8_t)sc;
+        score[(int64_t)y * L.pitch + x] = (uint8_t)s;   // (x0 + 64 <= pitch)
     }
 }
 
-// ------------------------------------------------------------------ NMS + ordered compaction
-// One workgroup per (level, row).  pass 0 writes the row's corner count, pass 1 the
-// corners (packed (y << 16) | x and the FAST score) at the scanned row offset.
 __device__ __forceinline__ int find_level(const Lvl* lv, int nl, int row) {
     int l = 0;
     while (l + 1 < nl && row >= lv[l + 1].row0) l++;
     return l;
 }
 
-__global__ __launch_bounds__(256)
-void orb_nms_kernel(const uint8_t* __restrict__ score, const Lvl* __restrict__ lv, int nl, int border, int pass,
-                    int* __restrict__ row_count, const int* __restrict__ row_off, int32_t* __restrict__ cpos,
-                    uint8_t* __restrict__ cscore, int cap, int64_t istride, uint64_t* __restrict__ kmask, int mw) {
-    __shared__ int wsum[4];
-    const int row = blockIdx.x;
-    {
-        const int64_t bo = (int64_t)blockIdx.y * istride;
-        score = at(score, bo);
-        if (row_count) row_count = at(row_count, bo);
-        if (row_off) row_off = at(row_off, bo);
-        if (cpos) cpos = at(cpos, bo);
-        if (cscore) cscore = at(cscore, bo);
-        kmask = at(kmask, bo) + (int64_t)row * mw;   // the row's keep bits (pass 0 writes, pass 1 reads: r04)
-    }
-    const int l = find_level(lv, nl, row);
-    const Lvl L = lv[l];
-    const int y = row - L.row0;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int b = max(border, 3);                        // FAST_t's own 3-pixel frame
-    const bool row_ok = y >= b && y < L.h - b && L.w > 2 * b;
-    int base = pass ? row_off[row] : 0;
-    int total = 0;
-    const uint8_t* s = score + L.off;
-    if (!row_ok) {   // no corner in this row (pass 0 counts 0; pass 1 has nothing to write)
-        if (!pass && threadIdx.x == 0) row_count[row] = 0;
-        return;
-    }
-    for (int xc = 0; xc < L.w; xc += 256) {
-        const int x = xc + threadIdx.x;
-        bool keep = false;
-        uint8_t sc = 0;
-        uint64_t m;
-        if (!pass) {
-            if (x >= b && x < L.w - b) {
-                const uint8_t* p = s + (int64_t)y * L.w + x;
-                sc = p[0];
-                if (sc) {
-                    const int w = L.w;
-                    keep = sc > p[-1] && sc > p[1] && sc > p[-w - 1] && sc > p[-w] && sc > p[-w + 1] && sc > p[w - 1] &&
-                           sc > p[w] && sc > p[w + 1];
-                }
-            }
-            m = __ballot(keep);
-            if (lane == 0) kmask[xc / 64 + wid] = m;
-        } else {
-            m = kmask[xc / 64 + wid];   // (wave-uniform load)
-            keep = (m >> lane) & 1;
-            if (keep) sc = s[(int64_t)y * L.w + x];
-        }
-        if (lane == 0) wsum[wid] = __popcll(m);
-        __syncthreads();
-        int before = 0, chunk = 0;
-        for (int w = 0; w < 4; w++) {
-            before += w < wid ? wsum[w] : 0;
-            chunk += wsum[w];
-        }
-        if (pass && keep) {
-            const int k = base + total + before + __popcll(m & ((1ull << lane) - 1));
-            if (k < cap) {   // (always: one strict maximum per 2 x 2 cell at most; the host checks the total)
-                cpos[k] = (y << 16) | x;
-                cscore[k] = sc;
-            }
-        }
-        total += chunk;
-        __syncthreads();
-    }
-    if (!pass && threadIdx.x == 0) row_count[row] = total;
-}
-
-// exclusive scan of n row counts into off[0..n] (one workgroup)
+// exclusive scan of the n rows' corner counts (the sums of their mw word counts) into off[0..n]
+// (one workgroup per image); also clears retainBest's error flag
 __global__ __launch_bounds__(1024)
-void orb_scan_kernel(const int* __restrict__ cnt, int n, int* __restrict__ off, int64_t istride, int* __restrict__ stats) {
+void orb_scan_kernel(const uint8_t* __restrict__ wcnt, int mw, int n, int* __restrict__ off, int64_t istride,
+                     int* __restrict__ stats) {
     __shared__ int part[1024];
-    cnt = at(cnt, (int64_t)blockIdx.x * istride);
+    wcnt = at(wcnt, (int64_t)blockIdx.x * istride);
     off = at(off, (int64_t)blockIdx.x * istride);
     if (threadIdx.x == 0) stats[(int64_t)blockIdx.x * CS + 2 * MAX_LEVELS + 3] = 0;   // retainBest's error flag
+    auto row_sum = [&](int i) {   // mw is a multiple of 4, rows 4-byte aligned
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(wcnt + (int64_t)i * mw);
+        uint32_t s = 0;
+        for (int k = 0; k < mw / 4; ++k) s = __builtin_amdgcn_sad_u8(w[k], 0u, s);
+        return (int)s;
+    };
     const int per = (n + 1023) / 1024;
     const int b = threadIdx.x * per, e = min(b + per, n);
+    int cnt[8];
     int s = 0;
-    for (int i = b; i < e; i++) s += cnt[i];
+    for (int i = b, j = 0; i < e; i++, j++) {
+        const int c = row_sum(i);
+        if (j < 8) cnt[j] = c;
+        s += c;
+    }
     part[threadIdx.x] = s;
     __syncthreads();
     for (int d = 1; d < 1024; d <<= 1) {
@@ -307,11 +306,48 @@ void orb_scan_kernel(const int* __restrict__ cnt, int n, int* __restrict__ off, 
         __syncthreads();
     }
     int run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (int i = b; i < e; i++) {
+    for (int i = b, j = 0; i < e; i++, j++) {
         off[i] = run;
-        run += cnt[i];
+        run += j < 8 ? cnt[j] : row_sum(i);
     }
     if (threadIdx.x == 1023) off[n] = part[1023];
+}
+
+// the corners of every row in raster order at the row's scanned offset (packed (y << 16) | x and the
+// FAST score): one wave per row, the row's keep words in the lanes, walked word by word
+__global__ __launch_bounds__(256)
+void orb_rows_kernel(const uint8_t* __restrict__ score, const Lvl* __restrict__ lv, int nl, int rows,
+                     const int* __restrict__ row_off, const uint64_t* __restrict__ kmask, int mw, int32_t* __restrict__ cpos,
+                     uint8_t* __restrict__ cscore, int cap, int64_t istride) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const int64_t bo = (int64_t)blockIdx.y * istride;
+    row_off = at(row_off, bo);
+    int base = row_off[row];
+    if (row_off[row + 1] == base) return;
+    score = at(score, bo);
+    kmask = at(kmask, bo) + (int64_t)row * mw;
+    cpos = at(cpos, bo);
+    cscore = at(cscore, bo);
+    const Lvl L = lv[find_level(lv, nl, row)];
+    const int y = row - L.row0, nw = (L.w + 63) >> 6;
+    const uint8_t* s = score + L.off + (int64_t)y * L.pitch;
+    for (int c0 = 0; c0 < nw; c0 += 64) {
+        const uint64_t mine = c0 + lane < nw ? kmask[c0 + lane] : 0;
+        const int nn = min(64, nw - c0);
+        for (int j = 0; j < nn; ++j) {
+            const uint64_t m = __shfl(mine, j);
+            if (!m) continue;
+            if ((m >> lane) & 1) {
+                const int k = base + __popcll(m & ((1ull << lane) - 1)), x = (c0 + j) * 64 + lane;
+                if (k < cap) {   // (always: one strict maximum per 2 x 2 cell at most; the host checks the total)
+                    cpos[k] = (y << 16) | x;
+                    cscore[k] = s[x];
+                }
+            }
+            base += __popcll(m);
+        }
+    }
 }
 
 // ------------------------------------------------------------------ device retainBest
@@ -571,7 +607,7 @@ void orb_harris_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ 
     const Lvl L = lv[l];
     const int c0 = lvl_first(row_off, L), m = cnt1[l];
     const uint8_t* img = pyr + L.off;
-    const int step = L.w, r = HARRIS_BLOCK / 2;
+    const int step = L.pitch, r = HARRIS_BLOCK / 2;
     for (int j = blockIdx.x * 256 + threadIdx.x; j < m; j += gridDim.x * 256) {
         const int pos = cpos[A[c0 + j].idx], x0 = pos & 0xFFFF, y0 = pos >> 16;
         int a = 0, b = 0, c = 0;
@@ -648,7 +684,7 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         const Resp e = B[c0 + j];
         const int pos = cpos[A[c0 + e.idx].idx], cx = pos & 0xFFFF, cy = pos >> 16;
         const uint8_t* img = pyr + L.off;
-        const int step = L.w;
+        const int step = L.pitch;
         int m10 = 0, m01 = 0;
         if (lane < 2 * HALF_PATCH + 1) {
             const int u = lane - HALF_PATCH;
@@ -761,21 +797,23 @@ void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv
     const Lvl L = lv[l];
     const int x0 = blockIdx.x * BT_X, y0 = blockIdx.y * BT_Y;
     if (x0 >= L.w || y0 >= L.h) return;
-    constexpr int TH = BT_Y + 2 * BR, TW = BT_X + 2 * BR;
-    __shared__ uint8_t t[TH][TW + 2];
+    constexpr int TH = BT_Y + 2 * BR, TW = BT_X + 2 * BR, TC = 96, C0 = 16 - BR;   // tile column 0 = x0 - 16
+    __shared__ __align__(16) uint8_t t[TH][TC];
     __shared__ int r[TH][BT_X + 1];
     const uint8_t* src = pyr + L.off;
-    const bool interior = x0 >= BR && x0 + BT_X + BR <= L.w && y0 >= BR && y0 + BT_Y + BR <= L.h;
+    // interior: rows y0-3 .. y0+34 as 16-byte loads of columns x0-16 .. x0+79 (inside the padded row)
+    const bool interior = x0 >= 16 && x0 + BT_X + 16 <= L.pitch && x0 + BT_X + BR <= L.w && y0 >= BR && y0 + BT_Y + BR <= L.h;
     if (interior) {
-        for (int i = threadIdx.x; i < TH * TW; i += 256) {
-            const int ty = i / TW, tx = i % TW;
-            t[ty][tx] = src[(int64_t)(y0 + ty - BR) * L.w + (x0 + tx - BR)];
+        for (int i = threadIdx.x; i < TH * (TC / 16); i += 256) {
+            const int ty = i / (TC / 16), q = i % (TC / 16);
+            *reinterpret_cast<uint4*>(&t[ty][16 * q]) =
+                *reinterpret_cast<const uint4*>(src + (int64_t)(y0 + ty - BR) * L.pitch + (x0 - 16 + 16 * q));
         }
     } else {
         for (int i = threadIdx.x; i < TH * TW; i += 256) {
             const int ty = i / TW, tx = i % TW;
             const int gy = reflect101(y0 + ty - BR, L.h), gx = reflect101(x0 + tx - BR, L.w);
-            t[ty][tx] = src[(int64_t)gy * L.w + gx];
+            t[ty][C0 + tx] = src[(int64_t)gy * L.pitch + gx];
         }
     }
     __syncthreads();
@@ -783,7 +821,7 @@ void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv
         const int ty = i / (BT_X / 4), tx = 4 * (i % (BT_X / 4));
         int w[10];
 #pragma unroll
-        for (int k = 0; k < 10; ++k) w[k] = t[ty][tx + k];
+        for (int k = 0; k < 10; ++k) w[k] = t[ty][C0 + tx + k];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             int s = 0;
@@ -807,7 +845,7 @@ void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv
             int s = 0;
 #pragma unroll
             for (int j = 0; j < 7; j++) s += c_taps[j] * w[q + j];
-            blur[L.off + (int64_t)y * L.w + x] = (uint8_t)min(max((s + (1 << 15)) >> 16, 0), 255);
+            blur[L.off + (int64_t)y * L.pitch + x] = (uint8_t)min(max((s + (1 << 15)) >> 16, 0), 255);
         }
     }
 }
@@ -860,7 +898,7 @@ void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ 
             const int px = c_pattern[2 * idx], py = c_pattern[2 * idx + 1];
             const float x = px * a - py * b, y = px * b + py * a;
             const int yy = min(max(cy + round_f(y), 0), L.h - 1), xx = min(max(cx + round_f(x), 0), L.w - 1);
-            return img[(int64_t)yy * L.w + xx];
+            return img[(int64_t)yy * L.pitch + xx];
         };
         int val = 0;
     #pragma unroll
@@ -1087,9 +1125,10 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
         L.w = host_round_f(width * inv);
         L.h = host_round_f(height * inv);
         if (L.w < 1 || L.h < 1) { set_last_error("pyramid level of zero size (image too small for n_levels)"); return SFMX_EINVAL; }
+        L.pitch = (L.w + 63) & ~63;
         L.off = px;
         L.row0 = rows;
-        px += ((int64_t)L.w * L.h + 255) & ~(int64_t)255;
+        px += ((int64_t)L.pitch * L.h + 255) & ~(int64_t)255;
         rows += L.h;
         maxw = std::max(maxw, L.w);
         maxh = std::max(maxh, L.h);
@@ -1126,10 +1165,10 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
         // descriptor staging (host buffers) -- every part 256-B aligned, so the offsets are the same in
         // every block
         auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
-        const int mw = (maxw + 255) / 256 * 4;   // keep-bit words per NMS row
+        const int mw = (maxw + 255) / 256 * 4;   // keep words per row (64 pixels each; a multiple of 4)
         const size_t blk = 3 * r(px) + r(CAND_CAP * 4) + r(CAND_CAP) + 2 * r(CAND_CAP * sizeof(Resp)) + 2 * r(CAND_CAP * 4) +
-                           2 * r(CAND_CAP * sizeof(Kp)) + r(CAND_CAP * 4) + 2 * r((size_t)(rows + 1) * 4) +
-                           r((size_t)rows * mw * 8) +
+                           2 * r(CAND_CAP * sizeof(Kp)) + r(CAND_CAP * 4) + r((size_t)(rows + 1) * 4) +
+                           r((size_t)rows * mw * 8) + r((size_t)rows * mw) +
                            (inputs_on_device ? 0 : r((size_t)width * height) + r((size_t)std::max(capmax, 1) * 32));
         const size_t shared_b = r(std::max<size_t>(tables.size(), 1) * sizeof(AxisEnt)) + r(sizeof(Lvl) * nl) +
                                 r(sizeof(int) * umax.size()) + r(sizeof(ImgIO) * G) + r(sizeof(int) * CS * G);
@@ -1154,9 +1193,9 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             Kp* kraw = A.take<Kp>(CAND_CAP);
             Kp* dfin = A.take<Kp>(CAND_CAP);
             int* keep = A.take<int>(CAND_CAP);
-            int* row_cnt = A.take<int>(rows + 1);
             int* row_off = A.take<int>(rows + 1);
             uint64_t* kmask = A.take<uint64_t>((size_t)rows * mw);
+            uint8_t* wcnt = A.take<uint8_t>((size_t)rows * mw);
             uint8_t* t = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)width * height);
             uint8_t* ddesc = inputs_on_device ? nullptr : A.take<uint8_t>((size_t)std::max(capmax, 1) * 32);
             const int64_t istride = (int64_t)A.used;   // == blk (every part 256-B rounded)
@@ -1197,16 +1236,15 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             OCHK(hipEventRecord(A.e0, st));
             const unsigned gz = (unsigned)G;
             // ---- detect(): pyramid, FAST, NMS
-            orb_copy_kernel<<<dim3((width + 255) / 256, height, gz), 256, 0, st>>>(dio, width, height, pyr, istride);
+            orb_copy_kernel<<<dim3((width + 1023) / 1024, height, gz), 256, 0, st>>>(dio, width, height, lv[0].pitch, pyr,
+                                                                                    istride);
             for (int l = 1; l < nl; l++)
-                orb_resize_kernel<<<dim3((lv[l].w + 255) / 256, lv[l].h, gz), 256, 0, st>>>(pyr, dlv, l, dtab, istride);
-            orb_fast_kernel<<<dim3((maxw + FT_X - 1) / FT_X, (maxh + FT_Y - 1) / FT_Y, nl * gz), 256, 0, st>>>(
-                pyr, dlv, thr, score, nl, istride);
-            orb_nms_kernel<<<dim3(rows, gz), 256, 0, st>>>(score, dlv, nl, border, 0, row_cnt, nullptr, nullptr, nullptr,
-                                                           (int)CAND_CAP, istride, kmask, mw);
-            orb_scan_kernel<<<gz, 1024, 0, st>>>(row_cnt, rows, row_off, istride, stats);
-            orb_nms_kernel<<<dim3(rows, gz), 256, 0, st>>>(score, dlv, nl, border, 1, nullptr, row_off, cpos, cscore,
-                                                           (int)CAND_CAP, istride, kmask, mw);
+                orb_resize_kernel<<<dim3((lv[l].w + 1023) / 1024, lv[l].h, gz), 256, 0, st>>>(pyr, dlv, l, dtab, istride);
+            orb_fast_nms_kernel<<<dim3(mw, (maxh + FT_Y - 1) / FT_Y, nl * gz), 256, 0, st>>>(pyr, dlv, thr, border, score,
+                                                                                           kmask, wcnt, mw, nl, istride);
+            orb_scan_kernel<<<gz, 1024, 0, st>>>(wcnt, mw, rows, row_off, istride, stats);
+            orb_rows_kernel<<<dim3((rows + 3) / 4, gz), 256, 0, st>>>(score, dlv, nl, rows, row_off, kmask, mw, cpos, cscore,
+                                                                      (int)CAND_CAP, istride);
             // retainBest(2 n_l) on the FAST scores, Harris responses, retainBest(n_l) on them (device)
             SelCounts s1{}, s2{};
             for (int l = 0; l < nl; l++) { s1.n[l] = 2 * per[l]; s2.n[l] = per[l]; }
