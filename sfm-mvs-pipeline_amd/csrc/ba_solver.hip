@@ -909,7 +909,7 @@ int validate(const sfmx_ba_problem* pb) {
     return SFMX_OK;
 }
 
-int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
+int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb, bool sync = true) {
     DeviceGuard dg(c->device);
     double* x = c->x.as<double>();
     if (c->P) {
@@ -922,10 +922,11 @@ int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
         HIPCHK(hipMemcpyAsync(x, pts, sizeof(double) * 3 * c->P, hipMemcpyHostToDevice, c->st));
     }
     if (c->C) HIPCHK(hipMemcpyAsync(x + c->ne, pb->poses, sizeof(double) * 6 * c->C, hipMemcpyHostToDevice, c->st));
-    std::vector<double> iv(c->K, 0.0);   // the border: referenced blocks, zero padding
-    for (int j = 0; j < c->K; ++j) if (c->isrc[j] >= 0) iv[j] = pb->intr[c->isrc[j]];
-    HIPCHK(hipMemcpyAsync(x + c->ne + 6 * (size_t)c->C, iv.data(), sizeof(double) * c->K, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    double* iv = static_cast<double*>(stage_bytes(c, sizeof(double) * std::max(c->K, 1)));   // the border: referenced
+    if (!iv) return fail(SFMX_ENOMEM, "pinned staging buffer");                             // blocks, zero padding
+    for (int j = 0; j < c->K; ++j) iv[j] = c->isrc[j] >= 0 ? pb->intr[c->isrc[j]] : 0.0;
+    HIPCHK(hipMemcpyAsync(x + c->ne + 6 * (size_t)c->C, iv, sizeof(double) * c->K, hipMemcpyHostToDevice, c->st));
+    if (sync) HIPCHK(hipStreamSynchronize(c->st));
     return SFMX_OK;
 }
 
@@ -1000,6 +1001,26 @@ uint64_t point_key(const sfmx_ba_problem* pb, const View& v, int p, KeyBits kb, 
     return k;
 }
 int bucket_of(int minc) { return minc < 0 ? 0 : minc / BUCKET_CAMS; }
+
+// Stable LSD radix sort of (key, index) records on the key's low `bits` bits, 8 bits a pass, passes
+// whose digit is the same for every record skipped: the order std::sort gives (key, index) records
+// whose indices ascend on entry (r04: std::sort took ~80 ns per point of the ring-closing bucket).
+void radix_sort_keys(std::vector<std::pair<uint64_t, int>>& kp, int bits) {
+    const size_t n = kp.size();
+    if (n < 2) return;
+    thread_local std::vector<std::pair<uint64_t, int>> tmp;
+    tmp.resize(n);
+    for (int sh = 0; sh < bits; sh += 8) {
+        size_t cnt[257] = {};
+        for (const auto& e : kp) cnt[((e.first >> sh) & 255) + 1]++;
+        bool one = false;
+        for (int d = 1; d <= 256; ++d) if (cnt[d] == n) one = true;
+        if (one) continue;
+        for (int d = 0; d < 256; ++d) cnt[d + 1] += cnt[d];
+        for (const auto& e : kp) tmp[cnt[(e.first >> sh) & 255]++] = e;
+        kp.swap(tmp);
+    }
+}
 
 // Point groups, chunks, local cameras, assembly task lists and camera slot lists (see ba_group.hpp).
 struct TopoSeg;
@@ -1388,8 +1409,9 @@ void finish_topology(int C, int K, Topology& tp) {
 // bucket (points, observations) and to each sub-segment (groups never span SEG_PTS points).
 struct Bucket {
     std::vector<int> pts;           // caller points in the internal order
+    std::vector<int> cpts, rank;    // the same points in caller order; rank[j] = internal position of cpts[j]
     std::vector<int> lpt;           // bucket-local pt_start (pts.size() + 1)
-    std::vector<int> roc, oin;      // per internal observation: its camera; its index within its point
+    std::vector<int> roc;           // per internal observation: its camera
     std::vector<short> lc, row;     // obs_lc / obs_row (ba_group.hpp)
     std::vector<uint32_t> cpairs;   // the camera pairs (a << 16 | b, a < b) some point of the bucket connects
     std::vector<int> sub;           // sub-segment starts in points (+ the end)
@@ -1512,25 +1534,33 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
     sfmx::parallel_items((int)todo.size(), [&](int t) {
         Bucket& B = hs.bk[todo[t]];
         const int np = (int)B.pts.size();
+        // the caller's arrays are read in caller order only (ascending addresses; r03 read them in the
+        // sorted order, a cache miss per point on a bucket spread over the whole problem)
+        B.cpts.swap(B.pts);
+        B.pts.resize(np);
         std::vector<std::pair<uint64_t, int>> kp(np);
-        for (int i = 0; i < np; ++i) {
+        std::vector<int> m(np);
+        for (int j = 0; j < np; ++j) {
             int minc;
-            kp[i] = {point_key(pb, v, B.pts[i], kb, &minc), B.pts[i]};
+            const int p = B.cpts[j];
+            kp[j] = {point_key(pb, v, p, kb, &minc), j};
+            m[j] = v.start[p + 1] - v.start[p];
         }
-        std::sort(kp.begin(), kp.end());   // (key, caller index): the stable order of the key
+        radix_sort_keys(kp, kb.kb * kb.nk);   // (key, caller order): the stable order of the key
         B.lpt.assign(np + 1, 0);
+        B.rank.resize(np);
         for (int i = 0; i < np; ++i) {
-            B.pts[i] = kp[i].second;
-            B.lpt[i + 1] = B.lpt[i] + v.start[B.pts[i] + 1] - v.start[B.pts[i]];
+            const int j = kp[i].second;
+            B.pts[i] = B.cpts[j];
+            B.rank[j] = i;
+            B.lpt[i + 1] = B.lpt[i] + m[j];
         }
         B.no = B.lpt[np];
         B.roc.resize(B.no);
-        B.oin.resize(B.no);
-        for (int i = 0; i < np; ++i)
-            for (int a = v.start[B.pts[i]], k = B.lpt[i], j = 0; a < v.start[B.pts[i] + 1]; ++a, ++k, ++j) {
-                B.roc[k] = pb->obs_cam[v.obs(a)];
-                B.oin[k] = j;
-            }
+        for (int j = 0; j < np; ++j) {
+            const int p = B.cpts[j];
+            for (int a = v.start[p], k = B.lpt[B.rank[j]]; a < v.start[p + 1]; ++a, ++k) B.roc[k] = pb->obs_cam[v.obs(a)];
+        }
         {   // the bucket's co-visible camera pairs, deduplicated through a per-thread bit table
             thread_local std::vector<uint64_t> mark;
             const size_t words = ((size_t)C * C + 63) / 64;
@@ -1538,9 +1568,9 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
             B.cpairs.clear();
             for (int i = 0; i < np; ++i)
                 for (int x = B.lpt[i]; x < B.lpt[i + 1]; ++x)
-                    for (int y = B.lpt[i]; y < B.lpt[i + 1]; ++y) {
-                        const int a = B.roc[x], b = B.roc[y];
-                        if (a >= b) continue;
+                    for (int y = x + 1; y < B.lpt[i + 1]; ++y) {
+                        const int a = std::min(B.roc[x], B.roc[y]), b = std::max(B.roc[x], B.roc[y]);
+                        if (a == b) continue;
                         const size_t bit = (size_t)a * C + b;
                         if ((mark[bit >> 6] >> (bit & 63)) & 1) continue;
                         mark[bit >> 6] |= 1ull << (bit & 63);
@@ -1578,10 +1608,10 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
     std::vector<int>& pts = hs.pt_start;
     pts.resize(P + 1);
     pts[P] = O;
-    sfmx::parallel_items(nbk, [&](int b) {
+    sfmx::parallel_items(nbk, [&](int b) {   // in caller order (see phase 1)
         const Bucket& B = hs.bk[b];
-        for (size_t i = 0; i < B.pts.size(); ++i) {
-            const int p = B.pts[i];
+        for (size_t j = 0; j < B.cpts.size(); ++j) {
+            const int p = B.cpts[j], i = B.rank[j];
             pperm[B.ip0 + i] = p;
             pts[B.ip0 + i] = (int)(B.io0_new + B.lpt[i]);
             for (int a = v.start[p], k = (int)B.io0_new + B.lpt[i]; a < v.start[p + 1]; ++a, ++k) operm[k] = v.obs(a);
@@ -1857,7 +1887,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     }
     {   // the redone buckets: pixels gathered from the caller's array while copied into pinned staging
         const double2* xy = reinterpret_cast<const double2*>(caller->obs_xy);
-        const int* om = c->operm.data();
+        const View& v = hs.view;
         for (const Bucket& B : hs.bk) {
             if ((!B.dirty && B.io0 >= 0) || B.no == 0) continue;
             double2* h = static_cast<double2*>(stage_bytes(c, 16 * (size_t)B.no));
@@ -1866,8 +1896,12 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
             short* hr = static_cast<short*>(stage_bytes(c, 2 * (size_t)B.no));
             if (!h || !hc || !hl || !hr) return bail(fail(SFMX_ENOMEM, "pinned staging buffer"));
             const int64_t o0 = B.io0_new;
-            sfmx::parallel_ranges(B.no, B.no >= 65536 ? 16 : 1, [&](int64_t k0, int64_t k1) {
-                for (int64_t k = k0; k < k1; ++k) h[k] = xy[om[o0 + k]];
+            const int np = (int)B.cpts.size();
+            sfmx::parallel_ranges(np, B.no >= 65536 ? 16 : 1, [&](int64_t j0, int64_t j1) {   // caller order
+                for (int64_t j = j0; j < j1; ++j) {
+                    const int p = B.cpts[j];
+                    for (int a = v.start[p], k = B.lpt[B.rank[j]]; a < v.start[p + 1]; ++a, ++k) h[k] = xy[v.obs(a)];
+                }
             });
             std::memcpy(hc, B.roc.data(), 4 * (size_t)B.no);
             std::memcpy(hl, B.lc.data(), 2 * (size_t)B.no);
@@ -1917,10 +1951,16 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     // scale = 1 until (and unless) Jacobi scaling sets it
     hipLaunchKernelGGL(ba_fill, dim3(nblk((int64_t)n)), dim3(256), 0, st, (int64_t)n, 1.0, c->scale.as<double>());
     HIPCHK(hipGetLastError());
-    if ((rc = set_params(c, caller))) return bail(rc);   // ends with a stream synchronisation
+    // one rank: the factorization plan of the new co-visibility is built (host) while this call's copies
+    // and relayout run, and its own uploads end with the stream synchronisation; ranks of a sharded
+    // solve plan at run (the plan's co-visibility all-reduce needs every rank)
+    const bool plan_now = !multirank(c);
+    if ((rc = set_params(c, caller, !plan_now))) return bail(rc);
     c->setup_ms[2] = up_ms + ms_since(t_up2);
     c->setup_ms[3] = 0.0;
     c->setup_ms[4] = ms_since(t_start);
+    if (plan_now && (rc = ensure_plan(c))) return bail(rc);   // (adds its time to setup_ms[3] / [4])
+    HIPCHK(hipStreamSynchronize(st));   // (an unchanged plan returns at once: the copies end here)
     for (Bucket& B : hs.bk) { B.io0 = B.io0_new; B.dirty = false; }
     hs.valid = true;
     c->loaded = true;
