@@ -607,16 +607,34 @@ void orb_harris_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ 
     const Lvl L = lv[l];
     const int c0 = lvl_first(row_off, L), m = cnt1[l];
     const uint8_t* img = pyr + L.off;
-    const int step = L.pitch, r = HARRIS_BLOCK / 2;
+    const int step = L.pitch;
+    static_assert(HARRIS_BLOCK == 7, "9 x 9 pixel window");
     for (int j = blockIdx.x * 256 + threadIdx.x; j < m; j += gridDim.x * 256) {
         const int pos = cpos[A[c0 + j].idx], x0 = pos & 0xFFFF, y0 = pos >> 16;
+        // r04: the 9 x 9 window (rows y0-4 .. y0+4, columns x0-4 .. x0+4) as 27 aligned 4-byte loads
+        // (rows are 64-byte aligned; a corner lies >= 31 pixels inside its level), realigned with
+        // v_alignbyte; r03 made 392 byte loads per corner.  The sums are integers: the same values.
+        const int xa = (x0 - 4) & ~3, sh = (x0 - 4) & 3;
+        const uint8_t* base = img + (int64_t)(y0 - 4) * step + xa;
+        uint32_t win[9][3];
+#pragma unroll
+        for (int rr = 0; rr < 9; ++rr) {
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(base + (int64_t)rr * step);
+            const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+            win[rr][0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            win[rr][1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            win[rr][2] = __builtin_amdgcn_alignbyte(0u, w2, sh);
+        }
+        auto px = [&](int rr, int cc) -> int { return (int)((win[rr][cc >> 2] >> (8 * (cc & 3))) & 255u); };
         int a = 0, b = 0, c = 0;
-        for (int ii = 0; ii < HARRIS_BLOCK; ii++) {
-            const uint8_t* p = img + (int64_t)(y0 - r + ii) * step + (x0 - r);
-            for (int jj = 0; jj < HARRIS_BLOCK; jj++) {
-                const uint8_t* q = p + jj;
-                const int Ix = (q[1] - q[-1]) * 2 + (q[-step + 1] - q[-step - 1]) + (q[step + 1] - q[step - 1]);
-                const int Iy = (q[step] - q[-step]) * 2 + (q[step - 1] - q[-step - 1]) + (q[step + 1] - q[-step + 1]);
+#pragma unroll
+        for (int ii = 1; ii <= HARRIS_BLOCK; ii++) {
+#pragma unroll
+            for (int jj = 1; jj <= HARRIS_BLOCK; jj++) {
+                const int Ix = (px(ii, jj + 1) - px(ii, jj - 1)) * 2 + (px(ii - 1, jj + 1) - px(ii - 1, jj - 1)) +
+                               (px(ii + 1, jj + 1) - px(ii + 1, jj - 1));
+                const int Iy = (px(ii + 1, jj) - px(ii - 1, jj)) * 2 + (px(ii + 1, jj - 1) - px(ii - 1, jj - 1)) +
+                               (px(ii + 1, jj + 1) - px(ii - 1, jj + 1));
                 a += Ix * Ix;
                 b += Iy * Iy;
                 c += Ix * Iy;
@@ -674,6 +692,9 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         out = at(out, bo);
         keep = at(keep, bo);
     }
+    __shared__ int sumax[HALF_PATCH + 1];
+    if (threadIdx.x <= HALF_PATCH) sumax[threadIdx.x] = umax[threadIdx.x];
+    __syncthreads();
     int total = 0;
     for (int l = 0; l < nl; ++l) total += cnt2[l];
     for (int f = blockIdx.x * 4 + (threadIdx.x >> 6); f < total; f += gridDim.x * 4) {
@@ -685,17 +706,25 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         const int pos = cpos[A[c0 + e.idx].idx], cx = pos & 0xFFFF, cy = pos >> 16;
         const uint8_t* img = pyr + L.off;
         const int step = L.pitch;
+        // r04: the 31 patch rows as aligned 4-byte loads, 9 per row (columns (cx-15) & ~3 ..), 5 per
+        // lane; a pixel counts where |u| <= umax[|v|] (integer moments: any order, the same sums).
+        // r03 made 31 byte loads per lane, one row at a time.
+        const int xa = (cx - HALF_PATCH) & ~3;
         int m10 = 0, m01 = 0;
-        if (lane < 2 * HALF_PATCH + 1) {
-            const int u = lane - HALF_PATCH;
-            const uint8_t* col = img + (int64_t)cy * step + cx + u;
-            m10 = u * col[0];
-            const int au = u < 0 ? -u : u;
-            for (int v = 1; v <= HALF_PATCH; ++v) {
-                if (au > umax[v]) continue;
-                const int vp = col[v * step], vm = col[-v * step];
-                m10 += u * (vp + vm);
-                m01 += v * (vp - vm);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const int idx = lane + 64 * k;
+            if (idx >= (2 * HALF_PATCH + 1) * 9) break;
+            const int r = idx / 9, d = idx - 9 * r, v = r - HALF_PATCH;
+            const int um = sumax[v < 0 ? -v : v];
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(img + (int64_t)(cy + v) * step + xa + 4 * d);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int u = xa + 4 * d + i - cx, val = (int)((w >> (8 * i)) & 255u);
+                if (u >= -um && u <= um) {
+                    m10 += u * val;
+                    m01 += v * val;
+                }
             }
         }
         m10 = wave_isum(m10);
