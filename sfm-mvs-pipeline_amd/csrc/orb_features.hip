@@ -148,6 +148,29 @@ void orb_copy_kernel(const ImgIO* __restrict__ io, int W, int H, int P0, uint8_t
     *reinterpret_cast<uint32_t*>(dst + (int64_t)y * P0 + x) = v;
 }
 
+// Flat tile grids (r04): blockIdx.x counts the tiles of level 0, then level 1, ... (tw x th pixels each);
+// -> the level and the tile's pixel origin, or -1 past the last level.  A grid sized by the largest level
+// for every level left ~2/3 of the workgroups with nothing to do.
+template <int TW, int TH>
+__device__ __forceinline__ int flat_tile(const Lvl* __restrict__ lv, int nl, int t, int& x0, int& y0) {
+    for (int l = 0; l < nl; ++l) {
+        const int w = lv[l].w, h = lv[l].h, ntx = (w + TW - 1) / TW, n = ntx * ((h + TH - 1) / TH);
+        if (t < n) {
+            y0 = (t / ntx) * TH;
+            x0 = (t - (t / ntx) * ntx) * TW;
+            return l;
+        }
+        t -= n;
+    }
+    return -1;
+}
+template <int TW, int TH>
+int flat_tiles(const std::vector<Lvl>& lv) {
+    int n = 0;
+    for (const Lvl& L : lv) n += ((L.w + TW - 1) / TW) * ((L.h + TH - 1) / TH);
+    return n;
+}
+
 // ------------------------------------------------------------------ FAST 9/16 + NMS
 // r04: FAST and the 3x3 strict-maximum test in one tile pass.  A workgroup owns 64 x 16 pixels of
 // one level: the image tile (rows y0-4 .. y0+19, columns x0-16 .. x0+79) comes in as 16-byte
@@ -206,21 +229,22 @@ __device__ __forceinline__ int fast_score_lds(const uint8_t* c, int threshold) {
     return (-b0 - 1) & 255;
 }
 
-// grid (mw words, rows / 16, image * nl + level).  kmask / wcnt: (global row) x mw, every word of every
-// row of the level written (0 past the width, outside the border, or without a corner).  Scores are 0
+// grid (flat 64 x 16 tiles of all levels, images).  kmask / wcnt: (global row) x mw, the words
+// [0, ceil(w / 64)) of every row of the level written (0 outside the border or without a corner).  Scores are 0
 // in FAST's own 3-pixel frame; a corner needs b <= x < w - b, b <= y < h - b (b = max(border, 3)),
 // a nonzero score and a score above all 8 neighbours'.
 __global__ __launch_bounds__(256)
 void orb_fast_nms_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int threshold, int border,
                          uint8_t* __restrict__ score, uint64_t* __restrict__ kmask, uint8_t* __restrict__ wcnt, int mw,
                          int nl, int64_t istride) {
-    const int64_t bo = (int64_t)(blockIdx.z / nl) * istride;   // z = image * nl + level
-    const Lvl L = lv[blockIdx.z % nl];
-    const int x0 = blockIdx.x * FT_X, y0 = blockIdx.y * FT_Y;
-    if (y0 >= L.h) return;
+    const int64_t bo = (int64_t)blockIdx.y * istride;   // y = image
+    int x0, y0;
+    const int lvl = flat_tile<FT_X, FT_Y>(lv, nl, blockIdx.x, x0, y0);
+    if (lvl < 0) return;
+    const Lvl L = lv[lvl];
     const int ny = min(FT_Y, L.h - y0), b = max(border, 3);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t w0 = (int64_t)(L.row0 + y0) * mw + blockIdx.x;
+    const int64_t w0 = (int64_t)(L.row0 + y0) * mw + x0 / FT_X;
     kmask = at(kmask, bo) + w0;
     wcnt = at(wcnt, bo) + w0;
     if (!(x0 + FT_X > b && x0 < L.w - b && y0 + ny > b && y0 < L.h - b)) {   // no pixel of the tile may be a corner
@@ -277,15 +301,17 @@ __device__ __forceinline__ int find_level(const Lvl* lv, int nl, int row) {
 // (one workgroup per image); also clears retainBest's error flag
 __global__ __launch_bounds__(1024)
 void orb_scan_kernel(const uint8_t* __restrict__ wcnt, int mw, int n, int* __restrict__ off, int64_t istride,
-                     int* __restrict__ stats) {
+                     int* __restrict__ stats, const Lvl* __restrict__ lv, int nl) {
     __shared__ int part[1024];
     wcnt = at(wcnt, (int64_t)blockIdx.x * istride);
     off = at(off, (int64_t)blockIdx.x * istride);
     if (threadIdx.x == 0) stats[(int64_t)blockIdx.x * CS + 2 * MAX_LEVELS + 3] = 0;   // retainBest's error flag
-    auto row_sum = [&](int i) {   // mw is a multiple of 4, rows 4-byte aligned
+    auto row_sum = [&](int i) {   // the row's level's ceil(w / 64) words; rows 4-byte aligned (mw % 4 == 0)
         const uint32_t* w = reinterpret_cast<const uint32_t*>(wcnt + (int64_t)i * mw);
+        const int nw = (lv[find_level(lv, nl, i)].w + 63) >> 6;
         uint32_t s = 0;
-        for (int k = 0; k < mw / 4; ++k) s = __builtin_amdgcn_sad_u8(w[k], 0u, s);
+        for (int k = 0; k < nw / 4; ++k) s = __builtin_amdgcn_sad_u8(w[k], 0u, s);
+        if (nw & 3) s = __builtin_amdgcn_sad_u8(w[nw / 4] & ((1u << (8 * (nw & 3))) - 1u), 0u, s);
         return (int)s;
     };
     const int per = (n + 1023) / 1024;
@@ -819,13 +845,13 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 __global__ __launch_bounds__(256)
 void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const int* __restrict__ st,
                      uint8_t* __restrict__ blur, int nl, int64_t istride) {
-    const int g = blockIdx.z / nl, l = blockIdx.z % nl;   // z = image * nl + level
-    if (l >= st[(int64_t)g * CS + 1]) return;   // only the levels the kept keypoints use
+    const int g = blockIdx.y;   // grid (flat 64 x 32 tiles of all levels, images)
+    int x0, y0;
+    const int l = flat_tile<BT_X, BT_Y>(lv, nl, blockIdx.x, x0, y0);
+    if (l < 0 || l >= st[(int64_t)g * CS + 1]) return;   // only the levels the kept keypoints use
     pyr = at(pyr, (int64_t)g * istride);
     blur = at(blur, (int64_t)g * istride);
     const Lvl L = lv[l];
-    const int x0 = blockIdx.x * BT_X, y0 = blockIdx.y * BT_Y;
-    if (x0 >= L.w || y0 >= L.h) return;
     constexpr int TH = BT_Y + 2 * BR, TW = BT_X + 2 * BR, TC = 96, C0 = 16 - BR;   // tile column 0 = x0 - 16
     __shared__ __align__(16) uint8_t t[TH][TC];
     __shared__ int r[TH][BT_X + 1];
@@ -1269,9 +1295,9 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
                                                                                     istride);
             for (int l = 1; l < nl; l++)
                 orb_resize_kernel<<<dim3((lv[l].w + 1023) / 1024, lv[l].h, gz), 256, 0, st>>>(pyr, dlv, l, dtab, istride);
-            orb_fast_nms_kernel<<<dim3(mw, (maxh + FT_Y - 1) / FT_Y, nl * gz), 256, 0, st>>>(pyr, dlv, thr, border, score,
-                                                                                           kmask, wcnt, mw, nl, istride);
-            orb_scan_kernel<<<gz, 1024, 0, st>>>(wcnt, mw, rows, row_off, istride, stats);
+            orb_fast_nms_kernel<<<dim3(flat_tiles<FT_X, FT_Y>(lv), gz), 256, 0, st>>>(pyr, dlv, thr, border, score, kmask,
+                                                                                   wcnt, mw, nl, istride);
+            orb_scan_kernel<<<gz, 1024, 0, st>>>(wcnt, mw, rows, row_off, istride, stats, dlv, nl);
             orb_rows_kernel<<<dim3((rows + 3) / 4, gz), 256, 0, st>>>(score, dlv, nl, rows, row_off, kmask, mw, cpos, cscore,
                                                                       (int)CAND_CAP, istride);
             // retainBest(2 n_l) on the FAST scores, Harris responses, retainBest(n_l) on them (device)
@@ -1287,7 +1313,7 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             orb_compact_kernel<<<gz, RT, 0, st>>>(kraw, keep, cnt2, nl, row_off, rows, dfin, sst, istride);
             // ---- compute(): blur of the levels used, rBRIEF of min(count, capacity) keypoints
             if (descriptors && capmax > 0) {
-                orb_blur_kernel<<<dim3((maxw + BT_X - 1) / BT_X, (maxh + BT_Y - 1) / BT_Y, nl * gz), 256, 0, st>>>(
+                orb_blur_kernel<<<dim3(flat_tiles<BT_X, BT_Y>(lv), gz), 256, 0, st>>>(
                     pyr, dlv, sst, blur, nl, istride);
                 orb_brief_kernel<<<dim3(std::min(G > 1 ? 1024 : 4096, (capmax + 7) / 8), gz), 256, 0, st>>>(blur, dlv, dfin,
                                                                                                           sst, dio, istride);
