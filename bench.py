@@ -869,7 +869,9 @@ def _orb_pyramid_bytes(h, w, nlevels=8, sf=1.2):
     """Algorithmic HBM bytes of one image's ORB pass: per level of the 1.2 pyramid the
     level written (1 B/px) and read by the next resize (1), the FAST pass (read 1 +
     score written 1), the two NMS passes over the score map (2), and compute()'s blur
-    (read 1 + write 1) -- 8 B per level pixel; corner / keypoint records are noise."""
+    (read 1 + write 1) -- 8 B per level pixel; corner / keypoint records are noise.
+    (Kept as defined in r02: since r04 FAST and NMS run as one tile pass that never reads
+    the score map back, so the product moves less than this per image.)"""
     px = 0.0
     for l in range(nlevels):
         s = float(np.float32(float(np.float32(sf)) ** l))
@@ -925,7 +927,7 @@ def bench_features_orb(args, rank, world, local):
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": feat_traffic("orb"),
                         "traffic_unit": f"HBM bytes per image (2 x FETCH_SIZE + WRITE_SIZE, profiles/{FEAT_PMC_FILE})",
-                        "kernel": "ORB pipeline, wall time of the batch (host retainBest steps included)",
+                        "kernel": "ORB pipeline, wall time of the batch (every kernel of detect + compute, one host wait per chunk)",
                         "algorithmic": f"{pyr / 1e6:.1f} MB pyramid / FAST / NMS / blur traffic per image "
                                        f"(bench._orb_pyramid_bytes)"}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

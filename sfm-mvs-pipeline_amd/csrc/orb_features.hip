@@ -10,7 +10,7 @@
 //   orb_copy_kernel       level 0 from the caller's image (4 pixels per thread)
 //   orb_resize_kernel     level l = INTER_LINEAR_EXACT resize of level l-1 (8.8 fixed
 //                         point; per-axis offset/coefficient tables from the host; 4 pixels per thread)
-//   orb_fast_nms_kernel   FAST 9/16 scores + the 3x3 strict maximum + the border test on 64 x 16
+//   orb_fast_nms_kernel   FAST 9/16 scores + the 3x3 strict maximum + the border test on 64 x 32
 //                         tiles (16-byte tile loads, scores in LDS): keep words and their counts
 //   orb_scan_kernel       the rows' corner counts scanned
 //   orb_rows_kernel       ordered (raster) compaction, one wave per row, from the keep words
@@ -172,64 +172,48 @@ int flat_tiles(const std::vector<Lvl>& lv) {
 }
 
 // ------------------------------------------------------------------ FAST 9/16 + NMS
-// r04: FAST and the 3x3 strict-maximum test in one tile pass.  A workgroup owns 64 x 16 pixels of
-// one level: the image tile (rows y0-4 .. y0+19, columns x0-16 .. x0+79) comes in as 16-byte
-// loads, the FAST scores of the 66 x 18 ring around the tile go to LDS, and every wave tests its
+// r04: FAST and the 3x3 strict-maximum test in one tile pass.  A workgroup owns 64 x 32 pixels of
+// one level: the image tile (rows y0-4 .. y0+35, columns x0-16 .. x0+79) comes in as 16-byte
+// loads, the FAST scores of the 66 x 34 ring around the tile go to LDS, and every wave tests its
 // rows against LDS: one keep word per (row, 64-pixel word) from the ballot, its popcount, and the
 // tile's scores (read back only at kept pixels).  r03 wrote the score map from one kernel and
 // re-read every 3 x 3 neighbourhood from HBM in a second.
-constexpr int FT_X = 64, FT_Y = 16;
+constexpr int FT_X = 64, FT_Y = 32;
 constexpr int FI_R = FT_Y + 8, FI_C = 96;        // image tile
 constexpr int FS_R = FT_Y + 2, FS_C = FT_X + 2;  // score tile
 
-// cornerScore<16> of the pixel c points at, when it is a FAST 9/16 corner, else 0 (S: LDS row stride)
+// cornerScore<16> of the pixel c points at, when it is a FAST 9/16 corner, else 0 (S: LDS row stride).
+// With d_k = v - p_k on the ring, M = the largest minimum of d over the 16 arcs of 9 pixels and N = the
+// smallest maximum: FAST_t<16> calls the pixel a corner iff some arc is all darker (min d > t) or all
+// brighter (max d < -t), i.e. iff max(M, -N) > t; cornerScore<16> (its a0 / b0 loops over the arcs
+// split as min(d[k+1..k+8]) with d[k] or d[k+9]) returns max(t, M, -N) - 1.  So the score is
+// max(M, -N) - 1 for a corner, and both follow from sliding minima / maxima of width 3 and 9 (v_min3 /
+// v_max3) without the dark / bright bit masks: r04, ~half the VALU work of the bit-mask test followed
+// by cornerScore's loops (the tile pass measured VALU-bound: 372 M VALU instructions per 16 images).
 template <int S>
 __device__ __forceinline__ int fast_score_lds(const uint8_t* c, int threshold) {
     const int v = c[0];
     const int p[16] = {c[3 * S],  c[3 * S + 1],  c[2 * S + 2],  c[S + 3],  c[3],  c[-S + 3], c[-2 * S + 2], c[-3 * S + 1],
                        c[-3 * S], c[-3 * S - 1], c[-2 * S - 2], c[-S - 3], c[-3], c[S - 3],  c[2 * S - 2],  c[3 * S - 1]};
-    int d[16];
-    uint32_t dark = 0, bright = 0;
+    int d[16], m3[16], x3[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = v - p[k];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        d[k] = v - p[k];
-        dark |= (uint32_t)(p[k] < v - threshold) << k;
-        bright |= (uint32_t)(p[k] > v + threshold) << k;
+        m3[k] = min(min(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+        x3[k] = max(max(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
     }
-    // a run of >= 9 consecutive ring pixels (cyclic): AND of 9 rotations
-    const uint32_t dd = dark | (dark << 16), bb = bright | (bright << 16);
-    uint32_t rd = dd, rb = bb;
+    int M = INT_MIN, N = INT_MAX;
 #pragma unroll
-    for (int s = 1; s < 9; s++) { rd &= dd >> s; rb &= bb >> s; }
-    if (!((rd | rb) & 0xFFFFu)) return 0;
-    int a0 = threshold;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        int a = min(min(d[(k + 1) & 15], d[(k + 2) & 15]), d[(k + 3) & 15]);
-        a = min(a, d[(k + 4) & 15]);
-        a = min(a, d[(k + 5) & 15]);
-        a = min(a, d[(k + 6) & 15]);
-        a = min(a, d[(k + 7) & 15]);
-        a = min(a, d[(k + 8) & 15]);
-        a0 = max(a0, min(a, d[k]));
-        a0 = max(a0, min(a, d[(k + 9) & 15]));
+    for (int k = 0; k < 16; k++) {   // arc k .. k+8 = three runs of 3
+        M = max(M, min(min(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]));
+        N = min(N, max(max(x3[k], x3[(k + 3) & 15]), x3[(k + 6) & 15]));
     }
-    int b0 = -a0;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        int b = max(max(d[(k + 1) & 15], d[(k + 2) & 15]), d[(k + 3) & 15]);
-        b = max(b, d[(k + 4) & 15]);
-        b = max(b, d[(k + 5) & 15]);
-        b = max(b, d[(k + 6) & 15]);
-        b = max(b, d[(k + 7) & 15]);
-        b = max(b, d[(k + 8) & 15]);
-        b0 = min(b0, max(b, d[k]));
-        b0 = min(b0, max(b, d[(k + 9) & 15]));
-    }
-    return (-b0 - 1) & 255;
+    const int e = max(M, -N);
+    return e > threshold ? e - 1 : 0;
 }
 
-// grid (flat 64 x 16 tiles of all levels, images).  kmask / wcnt: (global row) x mw, the words
+// grid (flat 64 x 32 tiles of all levels, images).  kmask / wcnt: (global row) x mw, the words
 // [0, ceil(w / 64)) of every row of the level written (0 outside the border or without a corner).  Scores are 0
 // in FAST's own 3-pixel frame; a corner needs b <= x < w - b, b <= y < h - b (b = max(border, 3)),
 // a nonzero score and a score above all 8 neighbours'.
@@ -852,37 +836,47 @@ void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv
     pyr = at(pyr, (int64_t)g * istride);
     blur = at(blur, (int64_t)g * istride);
     const Lvl L = lv[l];
-    constexpr int TH = BT_Y + 2 * BR, TW = BT_X + 2 * BR, TC = 96, C0 = 16 - BR;   // tile column 0 = x0 - 16
-    __shared__ __align__(16) uint8_t t[TH][TC];
+    constexpr int TH = BT_Y + 2 * BR;
     __shared__ int r[TH][BT_X + 1];
     const uint8_t* src = pyr + L.off;
-    // interior: rows y0-3 .. y0+34 as 16-byte loads of columns x0-16 .. x0+79 (inside the padded row)
-    const bool interior = x0 >= 16 && x0 + BT_X + 16 <= L.pitch && x0 + BT_X + BR <= L.w && y0 >= BR && y0 + BT_Y + BR <= L.h;
-    if (interior) {
-        for (int i = threadIdx.x; i < TH * (TC / 16); i += 256) {
-            const int ty = i / (TC / 16), q = i % (TC / 16);
-            *reinterpret_cast<uint4*>(&t[ty][16 * q]) =
-                *reinterpret_cast<const uint4*>(src + (int64_t)(y0 + ty - BR) * L.pitch + (x0 - 16 + 16 * q));
-        }
-    } else {
-        for (int i = threadIdx.x; i < TH * TW; i += 256) {
-            const int ty = i / TW, tx = i % TW;
-            const int gy = reflect101(y0 + ty - BR, L.h), gx = reflect101(x0 + tx - BR, L.w);
-            t[ty][C0 + tx] = src[(int64_t)gy * L.pitch + gx];
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < TH * (BT_X / 4); i += 256) {   // 4 sums per thread
-        const int ty = i / (BT_X / 4), tx = 4 * (i % (BT_X / 4));
-        int w[10];
+    // Row pass (r04): each thread makes 4 neighbouring row sums from the 12 bytes x-4 .. x+7 of its
+    // row, read as 3 aligned 4-byte words (interior tiles) or gathered with the reflection (border
+    // tiles); per output the 7-byte window is two realigned words (v_alignbyte) dotted with the taps
+    // (v_dot4_u32_u8, the 8th tap 0).  Integer sums: the same values as the tap-by-tap form.  The
+    // byte tile in LDS it replaces cost bank conflicts and ~2x the VALU work (PMC r04h).
+    const bool interior = x0 >= 64 && x0 + BT_X + 4 <= L.pitch && x0 + BT_X + BR <= L.w && y0 >= BR && y0 + BT_Y + BR <= L.h;
+    const uint32_t T0 = (uint32_t)c_taps[0] | (uint32_t)c_taps[1] << 8 | (uint32_t)c_taps[2] << 16 | (uint32_t)c_taps[3] << 24;
+    const uint32_t T1 = (uint32_t)c_taps[4] | (uint32_t)c_taps[5] << 8 | (uint32_t)c_taps[6] << 16;
+    constexpr int ITEMS = TH * (BT_X / 4);
 #pragma unroll
-        for (int k = 0; k < 10; ++k) w[k] = t[ty][C0 + tx + k];
+    for (int it = 0; it < (ITEMS + 255) / 256; ++it) {
+        const int i = threadIdx.x + 256 * it;
+        if (i < ITEMS) {
+            const int ty = i / (BT_X / 4), tx = 4 * (i % (BT_X / 4));
+            uint32_t wa, wb, wc;   // bytes x-4 .. x-1 | x .. x+3 | x+4 .. x+7 of the row, x = x0 + tx
+            if (interior) {
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(src + (int64_t)(y0 + ty - BR) * L.pitch + x0 + tx - 4);
+                wa = q[0];
+                wb = q[1];
+                wc = q[2];
+            } else {
+                const uint8_t* row = src + (int64_t)reflect101(y0 + ty - BR, L.h) * L.pitch;
+                uint32_t wv[3] = {0u, 0u, 0u};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            int s = 0;
-#pragma unroll
-            for (int j = 0; j < 7; j++) s += c_taps[j] * w[q + j];
-            r[ty][tx + q] = s;
+                for (int k = 1; k <= 10; ++k)   // (bytes 0 and 11 are never used)
+                    wv[k >> 2] |= (uint32_t)row[reflect101(x0 + tx - 4 + k, L.w)] << (8 * (k & 3));
+                wa = wv[0];
+                wb = wv[1];
+                wc = wv[2];
+            }
+            // output q: bytes 1+q .. 7+q
+            r[ty][tx + 0] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wc, wb, 1), T1,
+                                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wb, wa, 1), T0, 0u, false), false);
+            r[ty][tx + 1] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wc, wb, 2), T1,
+                                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wb, wa, 2), T0, 0u, false), false);
+            r[ty][tx + 2] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wc, wb, 3), T1,
+                                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wb, wa, 3), T0, 0u, false), false);
+            r[ty][tx + 3] = (int)__builtin_amdgcn_udot4(wc, T1, __builtin_amdgcn_udot4(wb, T0, 0u, false), false);
         }
     }
     __syncthreads();
