@@ -705,6 +705,17 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
     __shared__ int sumax[HALF_PATCH + 1];
     if (threadIdx.x <= HALF_PATCH) sumax[threadIdx.x] = umax[threadIdx.x];
     __syncthreads();
+    // this lane's words of the 31 patch rows (9 aligned words a row, 5 per lane), the same for every keypoint
+    bool wok[5];
+    int wd[5], wrow[5], wum[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const int idx = lane + 64 * k, r = idx / 9;
+        wok[k] = idx < (2 * HALF_PATCH + 1) * 9;
+        wd[k] = idx - 9 * r;
+        wrow[k] = r - HALF_PATCH;
+        wum[k] = wok[k] ? sumax[wrow[k] < 0 ? -wrow[k] : wrow[k]] : 0;
+    }
     int total = 0;
     for (int l = 0; l < nl; ++l) total += cnt2[l];
     for (int f = blockIdx.x * 4 + (threadIdx.x >> 6); f < total; f += gridDim.x * 4) {
@@ -723,19 +734,17 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         int m10 = 0, m01 = 0;
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
-            const int idx = lane + 64 * k;
-            if (idx >= (2 * HALF_PATCH + 1) * 9) break;
-            const int r = idx / 9, d = idx - 9 * r, v = r - HALF_PATCH;
-            const int um = sumax[v < 0 ? -v : v];
-            const uint32_t w = *reinterpret_cast<const uint32_t*>(img + (int64_t)(cy + v) * step + xa + 4 * d);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int u = xa + 4 * d + i - cx, val = (int)((w >> (8 * i)) & 255u);
-                if (u >= -um && u <= um) {
-                    m10 += u * val;
-                    m01 += v * val;
-                }
-            }
+            if (!wok[k]) continue;
+            // the word's pixels inside the circle (|u| <= umax[|v|]) are one byte run [lo, hi]; with
+            // the others masked off, sum I and sum i I come from two v_dot4_u32_u8:
+            // sum u I = (X - cx) sum I + sum i I, X the word's first column
+            const int X = xa + 4 * wd[k], lo = max(0, cx - wum[k] - X), hi = min(3, cx + wum[k] - X);
+            const uint32_t mask = lo <= hi ? (0xFFFFFFFFu >> (8 * (3 - hi + lo))) << (8 * lo) : 0u;
+            const uint32_t w = *reinterpret_cast<const uint32_t*>(img + (int64_t)(cy + wrow[k]) * step + X) & mask;
+            const int s1 = (int)__builtin_amdgcn_udot4(w, 0x01010101u, 0u, false);
+            const int si = (int)__builtin_amdgcn_udot4(w, 0x03020100u, 0u, false);
+            m10 += (X - cx) * s1 + si;
+            m01 += wrow[k] * s1;
         }
         m10 = wave_isum(m10);
         m01 = wave_isum(m01);
@@ -923,17 +932,31 @@ __device__ void orb_sincos(double x, double* s, double* c) {
 }
 
 // computeOrbDescriptors (WTA_K 2): 32 lanes per keypoint, lane i builds byte i from
-// pattern pairs 8 i .. 8 i + 7; min(count, capacity) keypoints
+// pattern pairs 8 i .. 8 i + 7; min(count, capacity) keypoints.
+// r04: the lane's 16 pattern points are loaded once (they were 32 loads per keypoint, half the
+// kernel's memory instructions, PMC r04h), and the keypoint's 37 x 37 sample window (|round(rotated
+// pattern point)| <= 18: the pattern lies in [-13, 12]^2) is staged in LDS by 16-byte loads, one
+// window per keypoint slot; keypoints whose window needs the edge clamp read the level directly.
+constexpr int BW = 18;                 // window half-size
+constexpr int BWR = 2 * BW + 1, BWC = 64;
 __global__ __launch_bounds__(256)
 void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ lv, const Kp* __restrict__ kps,
                       const int* __restrict__ st, const ImgIO* __restrict__ io, int64_t istride) {
+    __shared__ __align__(16) uint8_t win[8][BWR * BWC];
     const int g = blockIdx.y;
     blur = at(blur, (int64_t)g * istride);
     kps = at(kps, (int64_t)g * istride);
     uint8_t* desc = io[g].desc_out;
     if (!desc) return;   // this image's caller passed no descriptor buffer
-    const int n = min(st[(int64_t)g * CS], io[g].capacity), i = threadIdx.x & 31;
-    for (int j = blockIdx.x * 8 + (threadIdx.x >> 5); j < n; j += gridDim.x * 8) {
+    const int n = min(st[(int64_t)g * CS], io[g].capacity), i = threadIdx.x & 31, slot = threadIdx.x >> 5;
+    uint8_t* wn = win[slot];
+    float pxf[16], pyf[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        pxf[e] = (float)c_pattern[2 * (16 * i + e)];
+        pyf[e] = (float)c_pattern[2 * (16 * i + e) + 1];
+    }
+    for (int j = blockIdx.x * 8 + slot; j < n; j += gridDim.x * 8) {
         const Kp k = kps[j];
         const Lvl L = lv[k.octave];
         float angle = k.angle;
@@ -943,18 +966,30 @@ void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ 
         const float a = (float)cd, b = (float)sd;
         const int cy = round_f(k.y * L.inv_scale), cx = round_f(k.x * L.inv_scale);
         const uint8_t* img = blur + L.off;
-        auto value = [&](int idx) -> int {
-            const int px = c_pattern[2 * idx], py = c_pattern[2 * idx + 1];
-            const float x = px * a - py * b, y = px * b + py * a;
+        const int xs = (cx - BW) & ~15;
+        const bool staged = cy >= BW && cy + BW < L.h && cx >= BW && cx + BW < L.w;
+        __builtin_amdgcn_wave_barrier();   // (the slot's previous window fully read)
+        if (staged) {
+            const int nq = (cx + BW - xs) / 16 + 1;   // 16-byte words a row (the last one ends inside the pitch)
+            for (int e = i; e < BWR * 4; e += 32) {
+                const int rr = e >> 2, q = e & 3;
+                if (q < nq)
+                    *reinterpret_cast<uint4*>(&wn[rr * BWC + 16 * q]) =
+                        *reinterpret_cast<const uint4*>(img + (int64_t)(cy - BW + rr) * L.pitch + xs + 16 * q);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        auto value = [&](int e) -> int {
+            const float x = pxf[e] * a - pyf[e] * b, y = pxf[e] * b + pyf[e] * a;
+            if (staged) return wn[(round_f(y) + BW) * BWC + cx + round_f(x) - xs];
             const int yy = min(max(cy + round_f(y), 0), L.h - 1), xx = min(max(cx + round_f(x), 0), L.w - 1);
             return img[(int64_t)yy * L.pitch + xx];
         };
         int val = 0;
-    #pragma unroll
-        for (int bit = 0; bit < 8; bit++) {
-            const int base = 16 * i + 2 * bit;
-            val |= (value(base) < value(base + 1)) << bit;
-        }
+#pragma unroll
+        for (int bit = 0; bit < 8; bit++) val |= (value(2 * bit) < value(2 * bit + 1)) << bit;
         desc[(int64_t)j * 32 + i] = (uint8_t)val;
     }
 }
