@@ -102,33 +102,71 @@ __device__ __forceinline__ uint32_t hval(const uint8_t* __restrict__ r, const Ax
     return min((uint32_t)e.m0 * r[e.ofs] + (uint32_t)e.m1 * r[e.ofs + 1], 0xFFFFu);
 }
 
-// r04: 4 neighbouring outputs per thread, one 4-byte store (the level pitch is a multiple of 64; the
-// outputs past the width land in the row's padding, computed from the replicated edge column)
+// r04: one workgroup per 64 x 16 output tile, 4 neighbouring outputs per thread, one 4-byte store (the
+// level pitch is a multiple of 64).  A tile whose outputs all take the interpolating branch on both
+// axes (and whose source span fits, i.e. scale factors up to ~2) stages its source rectangle in LDS by
+// 16-byte loads and reads the taps' bytes from there; the tiles at the edges (replicated rows /
+// columns, the padding past the width) keep the per-pixel form.  The same integer expressions either
+// way.  r03 made 4 byte loads and a table load per output pixel, the level chain measured load-bound.
+constexpr int RZ_X = 64, RZ_Y = 16, RZ_R = 32, RZ_C = 144;   // tile; the largest staged source span
 __global__ __launch_bounds__(256)
 void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int l,
                        const AxisEnt* __restrict__ tables, int64_t istride) {
+    __shared__ __align__(16) uint8_t T[RZ_R][RZ_C];
     pyr = at(pyr, (int64_t)blockIdx.z * istride);
     const Lvl D = lv[l], S = lv[l - 1];
-    const int x = (blockIdx.x * 256 + threadIdx.x) * 4, y = blockIdx.y;
-    if (x >= D.w || y >= D.h) return;
+    const int x0 = blockIdx.x * RZ_X, y0 = blockIdx.y * RZ_Y;
+    const int x = x0 + 4 * (threadIdx.x & 15), y = y0 + (threadIdx.x >> 4);
     const AxisEnt* ax = tables + D.ax_off;
     const AxisEnt* ay = tables + D.ay_off;
     const uint8_t* src = pyr + S.off;
-    const int last_ofs = ax[D.w - 1].ofs;
+    bool staged = x0 >= D.xdmin && x0 + RZ_X <= D.xdmax && y0 >= D.ydmin && y0 + RZ_Y <= D.ydmax;
+    int bx = 0, sy0 = 0;
+    if (staged) {
+        bx = ax[x0].ofs & ~15;
+        sy0 = ay[y0].ofs;
+        const int ncols = ax[x0 + RZ_X - 1].ofs + 2 - bx, nrows = ay[y0 + RZ_Y - 1].ofs + 2 - sy0;
+        staged = ncols <= RZ_C && nrows <= RZ_R;   // (block-uniform)
+        if (staged) {
+            const int nq = (ncols + 15) >> 4;   // (the last word ends inside the padded row)
+            for (int e = threadIdx.x; e < nrows * nq; e += 256) {
+                const int rr = e / nq, q = e - rr * nq;
+                *reinterpret_cast<uint4*>(&T[rr][16 * q]) =
+                    *reinterpret_cast<const uint4*>(src + (int64_t)(sy0 + rr) * S.pitch + bx + 16 * q);
+            }
+        }
+        __syncthreads();
+    }
+    if (x >= D.w || y >= D.h) return;
     uint32_t out = 0;
-    if (y < D.ydmin || y >= D.ydmax) {
-        const uint8_t* r = src + (int64_t)(y < D.ydmin ? 0 : S.h - 1) * S.pitch;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) out |= min((hval(r, ax, x + i, D.xdmin, D.xdmax, last_ofs) + 128u) >> 8, 255u) << (8 * i);
-    } else {
+    if (staged) {
         const AxisEnt e = ay[y];
-        const uint8_t* r0 = src + (int64_t)e.ofs * S.pitch;
-        const uint8_t* r1 = r0 + S.pitch;
+        const uint8_t* t0 = T[e.ofs - sy0];
+        const uint8_t* t1 = T[e.ofs + 1 - sy0];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const uint32_t h0 = hval(r0, ax, x + i, D.xdmin, D.xdmax, last_ofs);
-            const uint32_t h1 = hval(r1, ax, x + i, D.xdmin, D.xdmax, last_ofs);
+            const AxisEnt h = ax[x + i];
+            const int o = h.ofs - bx;
+            const uint32_t h0 = min((uint32_t)h.m0 * t0[o] + (uint32_t)h.m1 * t0[o + 1], 0xFFFFu);
+            const uint32_t h1 = min((uint32_t)h.m0 * t1[o] + (uint32_t)h.m1 * t1[o + 1], 0xFFFFu);
             out |= min((h0 * e.m0 + h1 * e.m1 + 32768u) >> 16, 255u) << (8 * i);
+        }
+    } else {
+        const int last_ofs = ax[D.w - 1].ofs;
+        if (y < D.ydmin || y >= D.ydmax) {
+            const uint8_t* r = src + (int64_t)(y < D.ydmin ? 0 : S.h - 1) * S.pitch;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) out |= min((hval(r, ax, x + i, D.xdmin, D.xdmax, last_ofs) + 128u) >> 8, 255u) << (8 * i);
+        } else {
+            const AxisEnt e = ay[y];
+            const uint8_t* r0 = src + (int64_t)e.ofs * S.pitch;
+            const uint8_t* r1 = r0 + S.pitch;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t h0 = hval(r0, ax, x + i, D.xdmin, D.xdmax, last_ofs);
+                const uint32_t h1 = hval(r1, ax, x + i, D.xdmin, D.xdmax, last_ofs);
+                out |= min((h0 * e.m0 + h1 * e.m1 + 32768u) >> 16, 255u) << (8 * i);
+            }
         }
     }
     *reinterpret_cast<uint32_t*>(pyr + D.off + (int64_t)y * D.pitch + x) = out;
@@ -1323,7 +1361,8 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             orb_copy_kernel<<<dim3((width + 1023) / 1024, height, gz), 256, 0, st>>>(dio, width, height, lv[0].pitch, pyr,
                                                                                     istride);
             for (int l = 1; l < nl; l++)
-                orb_resize_kernel<<<dim3((lv[l].w + 1023) / 1024, lv[l].h, gz), 256, 0, st>>>(pyr, dlv, l, dtab, istride);
+                orb_resize_kernel<<<dim3((lv[l].w + RZ_X - 1) / RZ_X, (lv[l].h + RZ_Y - 1) / RZ_Y, gz), 256, 0, st>>>(pyr, dlv, l,
+                                                                                                        dtab, istride);
             orb_fast_nms_kernel<<<dim3(flat_tiles<FT_X, FT_Y>(lv), gz), 256, 0, st>>>(pyr, dlv, thr, border, score, kmask,
                                                                                    wcnt, mw, nl, istride);
             orb_scan_kernel<<<gz, 1024, 0, st>>>(wcnt, mw, rows, row_off, istride, stats, dlv, nl);
