@@ -18,14 +18,30 @@ namespace {
 constexpr int NBP = PLAN_NB;
 
 // ---- nested dissection of the camera graph ----------------------------------------------
+// The recursion is recorded as a tree of calls (r04): its splits do not depend on the leaf size, only
+// where it stops does, so the plans of the larger leaf sizes are read off the tree of the smallest
+// (derive) instead of dissecting the graph once per candidate.
 struct Nd {
     const std::vector<std::vector<int>>& g;
     int leaf;                       // cameras per leaf node
     std::vector<int> in, seen, lvl, taken;
     int epoch = 0, stamp = 0;
-    std::vector<std::vector<int>> nodes;   // children before their separator
+    struct Call {
+        std::vector<int> verts;     // sorted
+        int kind = 0;               // 0 one node (verts), 1 connected components (kids), 2 split (kids = left, right; then sep)
+        std::vector<int> kids, sep;
+    };
+    std::vector<Call> calls;
     Nd(const std::vector<std::vector<int>>& g_, int leaf_)
         : g(g_), leaf(leaf_), in(g_.size(), 0), seen(g_.size(), 0), lvl(g_.size(), 0), taken(g_.size(), 0) {}
+
+    // the nodes (children before their separator) of the dissection stopping at `lf` >= leaf cameras
+    void derive(int c, int lf, std::vector<std::vector<int>>& nodes) const {
+        const Call& k = calls[c];
+        if ((int)k.verts.size() <= lf || k.kind == 0) { nodes.push_back(k.verts); return; }
+        for (int kid : k.kids) derive(kid, lf, nodes);
+        if (k.kind == 2 && !k.sep.empty()) nodes.push_back(k.sep);
+    }
 
     // BFS from root inside the current set (in == ep): level sets
     void levels(int root, int ep, std::vector<std::vector<int>>& L) {
@@ -56,9 +72,12 @@ struct Nd {
         return best;
     }
 
-    void rec(std::vector<int> verts) {
+    int rec(std::vector<int> verts) {
         std::sort(verts.begin(), verts.end());
-        if ((int)verts.size() <= leaf) { nodes.push_back(verts); return; }
+        const int me = (int)calls.size();
+        calls.emplace_back();
+        calls[me].verts = verts;
+        if ((int)verts.size() <= leaf) return me;
         const int ep = ++epoch;
         for (int v : verts) in[v] = ep;
         {   // connected components (each dissected on its own, no separator between them)
@@ -72,8 +91,12 @@ struct Nd {
                 comps.push_back(std::move(comp));
             }
             if (comps.size() > 1) {
-                for (auto& c : comps) rec(std::move(c));
-                return;
+                calls[me].kind = 1;
+                for (auto& c : comps) {
+                    const int kid = rec(std::move(c));
+                    calls[me].kids.push_back(kid);
+                }
+                return me;
             }
         }
         // pseudo-peripheral root: repeated BFS from the farthest minimum-degree vertex
@@ -90,7 +113,7 @@ struct Nd {
         }
         levels(root, ep, L);   // leaves lvl[] of this BFS
         const int h = (int)L.size(), n = (int)verts.size();
-        if (h < 3) { nodes.push_back(verts); return; }
+        if (h < 3) return me;
         // separator level: smallest level set among the balanced ones (each side >= n/4), ties to
         // the most balanced; none balanced: the most balanced
         int m = -1;
@@ -117,10 +140,14 @@ struct Nd {
             for (int w : g[v]) if (in[w] == ep && lvl[w] == m + 1) { touches = true; break; }
             (touches ? sep : left).push_back(v);
         }
-        rec(std::move(left));
-        rec(std::move(right));
+        calls[me].kind = 2;
+        const int kl = rec(std::move(left));
+        calls[me].kids.push_back(kl);
+        const int kr = rec(std::move(right));
+        calls[me].kids.push_back(kr);
         std::sort(sep.begin(), sep.end());
-        if (!sep.empty()) nodes.push_back(std::move(sep));
+        calls[me].sep = std::move(sep);
+        return me;
     }
 };
 
@@ -150,7 +177,7 @@ void layout(int C, const std::vector<std::vector<int>>& nodes, FactorPlan& P) {
     P.T = row / NBP;
 }
 
-void pattern(const std::vector<char>& adj, FactorPlan& P) {
+void pattern(const std::vector<std::vector<int>>& g, FactorPlan& P) {
     const int T = P.T, C = P.C;
     std::vector<char>& nz = P.nz;
     nz.assign((size_t)T * T, 0);
@@ -161,8 +188,8 @@ void pattern(const std::vector<char>& adj, FactorPlan& P) {
     for (int I = 0; I < T; ++I) nz[(size_t)I * T + I] = 1;
     for (int a = 0; a < C; ++a) {
         mark(P.camrow[a], P.camrow[a] + 6, P.camrow[a], P.camrow[a] + 6);
-        for (int b = a + 1; b < C; ++b)
-            if (adj[(size_t)a * C + b] || adj[(size_t)b * C + a]) mark(P.camrow[a], P.camrow[a] + 6, P.camrow[b], P.camrow[b] + 6);
+        for (int b : g[a])   // (the symmetric co-visibility lists; each pair marks the same lower tile twice)
+            if (b > a) mark(P.camrow[a], P.camrow[a] + 6, P.camrow[b], P.camrow[b] + 6);
     }
     // symbolic fill of the block factorization in tile order
     for (int k = 0; k < T; ++k)
@@ -244,43 +271,47 @@ void schedule(FactorPlan& P) {
     P.lvl_start[P.height + 1] = (int)P.lvl_panels.size();
 }
 
-void build(int C, const std::vector<char>& adj, const std::vector<std::vector<int>>& nodes, int order,
+void build(int C, const std::vector<std::vector<int>>& g, const std::vector<std::vector<int>>& nodes, int order,
            int leaf_tiles, FactorPlan& P) {
     P = FactorPlan{};
     P.C = C;
     P.order = order;
     P.leaf_tiles = leaf_tiles;
     layout(C, nodes, P);
-    pattern(adj, P);
+    pattern(g, P);
     schedule(P);
 }
 
 }  // namespace
 
 void make_plan(int C, const std::vector<char>& adj, int order_mode, FactorPlan& out) {
+    std::vector<std::vector<int>> g(C);   // co-visibility lists (either triangle of adj)
+    for (int a = 0; a < C; ++a)
+        for (int b = 0; b < C; ++b)
+            if (a != b && (adj[(size_t)a * C + b] || adj[(size_t)b * C + a])) g[a].push_back(b);
     std::vector<std::vector<int>> natural;
     if (C > 0) {
         natural.emplace_back(C);
         for (int c = 0; c < C; ++c) natural[0][c] = c;
     }
     FactorPlan best;
-    build(C, adj, natural, 0, 0, best);
+    build(C, g, natural, 0, 0, best);
     if (order_mode == 0 || C == 0) { out = std::move(best); return; }
-    std::vector<std::vector<int>> g(C);
-    for (int a = 0; a < C; ++a)
-        for (int b = 0; b < C; ++b)
-            if (a != b && (adj[(size_t)a * C + b] || adj[(size_t)b * C + a])) g[a].push_back(b);
     const int leaves_all[3] = {1, 2, 4};
+    Nd nd(g, std::max(1, leaves_all[0] * NBP / 6));   // one dissection, the smallest leaf
+    {
+        std::vector<int> all(C);
+        for (int c = 0; c < C; ++c) all[c] = c;
+        nd.rec(all);
+    }
     bool have_nd = false;
     for (int li = 0; li < 3; ++li) {
         const int lt = leaves_all[li];
         if (order_mode >= 2 && order_mode - 1 != li + 1) continue;
-        Nd nd(g, std::max(1, lt * NBP / 6));
-        std::vector<int> all(C);
-        for (int c = 0; c < C; ++c) all[c] = c;
-        nd.rec(all);
+        std::vector<std::vector<int>> nodes;
+        nd.derive(0, std::max(1, lt * NBP / 6), nodes);
         FactorPlan p;
-        build(C, adj, nd.nodes, 1, lt, p);
+        build(C, g, nodes, 1, lt, p);
         const bool forced = order_mode >= 1;
         if ((forced && !have_nd) || p.predicted_us < best.predicted_us ||
             (p.predicted_us == best.predicted_us && p.T < best.T)) {
