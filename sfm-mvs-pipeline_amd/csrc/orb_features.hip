@@ -172,18 +172,25 @@ void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, in
     *reinterpret_cast<uint32_t*>(pyr + D.off + (int64_t)y * D.pitch + x) = out;
 }
 
-// level 0 from the caller's image: 4 pixels per thread, one 4-byte store into the padded row
+// level 0 from the caller's image: 16 pixels per thread (64 x 4 threads: 1024 columns of 4 rows), one
+// 16-byte store into the padded row; 16-byte loads when the caller's rows are 16-byte aligned
 __global__ __launch_bounds__(256)
 void orb_copy_kernel(const ImgIO* __restrict__ io, int W, int H, int P0, uint8_t* __restrict__ dst, int64_t istride) {
-    const int x = (blockIdx.x * 256 + threadIdx.x) * 4, y = blockIdx.y, g = blockIdx.z;
+    const int x = (blockIdx.x * 64 + (threadIdx.x & 63)) * 16, y = blockIdx.y * 4 + (threadIdx.x >> 6), g = blockIdx.z;
     if (x >= W || y >= H) return;
     const uint8_t* p = io[g].img + (int64_t)y * io[g].pitch + x;
     dst = at(dst, (int64_t)g * istride);
-    uint32_t v = p[0];
-    if (x + 1 < W) v |= (uint32_t)p[1] << 8;
-    if (x + 2 < W) v |= (uint32_t)p[2] << 16;
-    if (x + 3 < W) v |= (uint32_t)p[3] << 24;
-    *reinterpret_cast<uint32_t*>(dst + (int64_t)y * P0 + x) = v;
+    uint4 v;
+    if (((reinterpret_cast<uintptr_t>(io[g].img) | (uintptr_t)io[g].pitch) & 15) == 0 && x + 16 <= W) {
+        v = *reinterpret_cast<const uint4*>(p);
+    } else {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (x + i < W) w[i >> 2] |= (uint32_t)p[i] << (8 * (i & 3));
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    *reinterpret_cast<uint4*>(dst + (int64_t)y * P0 + x) = v;   // (x + 16 <= P0: P0 is a multiple of 64)
 }
 
 // Flat tile grids (r04): blockIdx.x counts the tiles of level 0, then level 1, ... (tw x th pixels each);
@@ -1358,8 +1365,8 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             OCHK(hipEventRecord(A.e0, st));
             const unsigned gz = (unsigned)G;
             // ---- detect(): pyramid, FAST, NMS
-            orb_copy_kernel<<<dim3((width + 1023) / 1024, height, gz), 256, 0, st>>>(dio, width, height, lv[0].pitch, pyr,
-                                                                                    istride);
+            orb_copy_kernel<<<dim3((width + 1023) / 1024, (height + 3) / 4, gz), 256, 0, st>>>(dio, width, height, lv[0].pitch,
+                                                                                          pyr, istride);
             for (int l = 1; l < nl; l++)
                 orb_resize_kernel<<<dim3((lv[l].w + RZ_X - 1) / RZ_X, (lv[l].h + RZ_Y - 1) / RZ_Y, gz), 256, 0, st>>>(pyr, dlv, l,
                                                                                                         dtab, istride);
