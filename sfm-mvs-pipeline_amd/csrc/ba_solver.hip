@@ -1229,7 +1229,8 @@ void finish_topology(int C, int K, Topology& tp) {
             const int ng = (int)tp.grp.size();
             std::vector<size_t> goff(ng + 1, 0);
             for (int g = 0; g < ng; ++g) goff[g + 1] = goff[g] + (size_t)tp.grp[g].u * (tp.grp[g].u + 1) / 2;
-            sfmx::parallel_ranges(ng, 16, [&](int64_t g0, int64_t g1) {
+            // (in parallel only when large: a pool dispatch costs more than ~100k pair records)
+            sfmx::parallel_ranges(ng, npr >= ((size_t)1 << 18) ? 16 : 1, [&](int64_t g0, int64_t g1) {
                 for (int64_t g = g0; g < g1; ++g) {
                     const Grp& G = tp.grp[g];
                     size_t e = goff[g];

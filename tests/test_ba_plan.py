@@ -144,3 +144,46 @@ def test_plan_deterministic_and_capacity():
     rc = lib.sfmx_ba_plan(60, np.ascontiguousarray(adj).ctypes.data, -1, C.byref(info), None, None, 0,
                           tasks.ctypes.data_as(C.POINTER(C.c_int32)), 1, None, 0)
     assert rc == -4 and info.tasks == a["tasks"].shape[0]
+
+
+def test_plans_equal_the_r03_library_on_random_graphs():
+    """r04 records one nested dissection as a call tree and reads the leaf-size candidates off it
+    (ba_plan.cpp Nd::derive) instead of dissecting once per candidate: the plans must be the ones the
+    r03 library (lib/libsfmx_r03.so, built from the r03 tree) makes, field for field, every order mode."""
+    import ctypes as C
+    import os
+    from sfmx import _lib
+    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libsfmx_r03.so")
+    if not os.path.exists(path):
+        pytest.skip("lib/libsfmx_r03.so not built here")
+    old = C.CDLL(path)
+    for name, (res, args) in _lib.PROTOTYPES.items():
+        if hasattr(old, name):
+            f = getattr(old, name)
+            f.restype, f.argtypes = res, args
+    rng = np.random.default_rng(3)
+    cur = ba.lib
+    try:
+        for it in range(60):
+            n = int(rng.integers(1, 120))
+            if it % 3 == 0:
+                adj = (rng.random((n, n)) < rng.uniform(0.01, 0.3)).astype(np.uint8)
+            elif it % 3 == 1:   # rings of bandwidth 1..5 (C5's shape)
+                adj = np.zeros((n, n), np.uint8)
+                for d in range(1, int(rng.integers(1, 6)) + 1):
+                    adj[np.arange(n), (np.arange(n) + d) % n] = 1
+            else:   # disconnected blocks
+                adj = np.zeros((n, n), np.uint8)
+                for s in range(0, n, 7):
+                    e = min(n, s + 7)
+                    adj[s:e, s:e] = rng.random((e - s, e - s)) < 0.5
+            np.fill_diagonal(adj, 0)
+            for order in (ba.ORDER_AUTO, 0, 1, 2, 3, 4):
+                ba.lib = old
+                a = ba.factor_plan(adj, order)
+                ba.lib = cur
+                b = ba.factor_plan(adj, order)
+                for k in a:
+                    assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), (it, order, k)
+    finally:
+        ba.lib = cur
