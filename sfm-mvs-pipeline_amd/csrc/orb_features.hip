@@ -18,9 +18,10 @@
 //                         the reference's libstdc++ nth_element + partition, in parallel
 //   orb_harris_kernel     Harris response (7x7 block, k = 0.04) per kept corner
 //   orb_retain_kernel     retainBest(n_l) per level on the Harris responses
-//   orb_angle_kernel      intensity-centroid angle, one wavefront per keypoint, and
-//                         compute()'s runByImageBorder(31) test at full resolution
-//   orb_compact_kernel    the in-border keypoints in order, their count
+//   orb_keep_kernel       compute()'s runByImageBorder(31) test at full resolution, the kept
+//                         keypoints' places in order (one workgroup per level)
+//   orb_angle_kernel      intensity-centroid angle of the kept keypoints, one wavefront per
+//                         keypoint, written in place
 //   orb_blur_kernel       7x7 integer Gaussian of the levels the keypoints use (LDS tile)
 //   orb_brief_kernel      rBRIEF, 32 lanes per keypoint, one descriptor byte per lane
 // One host wait per chunk (the keypoint counts at the end).  Roofline: HBM-bound byte work (see
@@ -76,7 +77,8 @@ struct ImgIO {             // per image of a chunk
     uint8_t* desc_out;     // descriptor rows (the caller's device buffer or the image's staging)
     int32_t capacity, pad;
 };
-constexpr int CS = 2 * MAX_LEVELS + 4;   // stats ints per image: cnt1[16] | cnt2[16] | count, levels, corners, err
+// stats ints per image: cnt1[16] | cnt2[16] | kcnt[16] (kept by compute()'s border test) | count, levels, corners, err
+constexpr int ST_CNT2 = MAX_LEVELS, ST_KCNT = 2 * MAX_LEVELS, ST_TAIL = 3 * MAX_LEVELS, CS = ST_TAIL + 4;
 template <class T>
 __device__ __forceinline__ T* at(T* p, int64_t bo) { return reinterpret_cast<T*>(reinterpret_cast<char*>(p) + bo); }
 template <class T>
@@ -334,7 +336,7 @@ void orb_scan_kernel(const uint8_t* __restrict__ wcnt, int mw, int n, int* __res
     __shared__ int part[1024];
     wcnt = at(wcnt, (int64_t)blockIdx.x * istride);
     off = at(off, (int64_t)blockIdx.x * istride);
-    if (threadIdx.x == 0) stats[(int64_t)blockIdx.x * CS + 2 * MAX_LEVELS + 3] = 0;   // retainBest's error flag
+    if (threadIdx.x == 0) stats[(int64_t)blockIdx.x * CS + ST_TAIL + 3] = 0;   // retainBest's error flag
     auto row_sum = [&](int i) {   // the row's level's ceil(w / 64) words; rows 4-byte aligned (mw % 4 == 0)
         const uint32_t* w = reinterpret_cast<const uint32_t*>(wcnt + (int64_t)i * mw);
         const int nw = (lv[find_level(lv, nl, i)].w + 63) >> 6;
@@ -732,9 +734,9 @@ __device__ __forceinline__ int wave_isum(int v) {
 // irrelevant), and compute()'s runByImageBorder(31) test at full resolution (Rect::contains(Point(pt)))
 __global__ __launch_bounds__(256)
 void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int nl,
-                      const int* __restrict__ row_off, const Resp* __restrict__ A, const Resp* __restrict__ B,
-                      const int* __restrict__ cnt2, const int32_t* __restrict__ cpos, const int* __restrict__ umax,
-                      int width, int height, int border, Kp* __restrict__ out, int* __restrict__ keep, int64_t istride) {
+                      const int* __restrict__ row_off, int rows, const Resp* __restrict__ A, const Resp* __restrict__ B,
+                      int* __restrict__ stats, const int32_t* __restrict__ cpos, const int* __restrict__ umax,
+                      const int* __restrict__ kpos, Kp* __restrict__ out, int64_t istride) {
     const int lane = threadIdx.x & 63;
     {
         const int64_t bo = (int64_t)blockIdx.y * istride;
@@ -742,13 +744,28 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         row_off = at(row_off, bo);
         A = at(A, bo);
         B = at(B, bo);
-        cnt2 += (int64_t)blockIdx.y * CS;
+        stats += (int64_t)blockIdx.y * CS;
         cpos = at(cpos, bo);
+        kpos = at(kpos, bo);
         out = at(out, bo);
-        keep = at(keep, bo);
     }
-    __shared__ int sumax[HALF_PATCH + 1];
+    const int* cnt2 = stats + ST_CNT2;
+    __shared__ int sumax[HALF_PATCH + 1], lbase[MAX_LEVELS + 1];
     if (threadIdx.x <= HALF_PATCH) sumax[threadIdx.x] = umax[threadIdx.x];
+    if (threadIdx.x == 0) {   // the kept keypoints' level offsets; block 0 publishes count, levels, corners
+        int b = 0, used = 0;
+        for (int l = 0; l < nl; ++l) {
+            lbase[l] = b;
+            b += stats[ST_KCNT + l];
+            if (stats[ST_KCNT + l] > 0) used = l + 1;
+        }
+        lbase[nl] = b;
+        if (blockIdx.x == 0) {
+            stats[ST_TAIL + 0] = b;
+            stats[ST_TAIL + 1] = used;
+            stats[ST_TAIL + 2] = row_off[rows];
+        }
+    }
     __syncthreads();
     // this lane's words of the 31 patch rows (9 aligned words a row, 5 per lane), the same for every keypoint
     bool wok[5];
@@ -768,6 +785,8 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         while (j >= cnt2[l]) { j -= cnt2[l]; ++l; }
         const Lvl L = lv[l];
         const int c0 = lvl_first(row_off, L);
+        const int kp = kpos[c0 + j];
+        if (kp < 0) continue;   // dropped by compute()'s border test (orb_keep_kernel)
         const Resp e = B[c0 + j];
         const int pos = cpos[A[c0 + e.idx].idx], cx = pos & 0xFFFF, cy = pos >> 16;
         const uint8_t* img = pyr + L.off;
@@ -802,57 +821,50 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
             q.response = e.response;
             q.octave = l;
             q.class_id = -1;
-            out[f] = q;
-            const int x = round_f(q.x), y = round_f(q.y);
-            keep[f] = height > 2 * border && width > 2 * border && border <= x && x < width - border && border <= y &&
-                      y < height - border;
+            out[lbase[l] + kp] = q;
         }
     }
 }
 
-// order-preserving compaction of the kept keypoints (one workgroup): st[0] = count, st[1] = the
-// levels the descriptors read (max octave + 1), st[2] = the corner total (overflow check)
+// compute()'s runByImageBorder(31) on the full-resolution positions (Rect::contains(Point(pt)), pt =
+// the level position x scale) of every level's retained keypoints, and their places in the kept list,
+// before the angles (r04: the angle kernel writes the kept keypoints in place; r03 wrote them all and
+// compacted them in one workgroup per image).  One workgroup per (level, image), rounds of RT records
+// scanned in order: kpos[c0 + j] = position among the level's kept keypoints or -1, kcnt[l] = their count.
 __global__ __launch_bounds__(RT)
-void orb_compact_kernel(const Kp* __restrict__ in, const int* __restrict__ keep, const int* __restrict__ cnt2, int nl,
-                        const int* __restrict__ row_off, int rows, Kp* __restrict__ out, int* __restrict__ st,
-                        int64_t istride) {
+void orb_keep_kernel(const Lvl* __restrict__ lv, const int* __restrict__ row_off, const Resp* __restrict__ A,
+                     const Resp* __restrict__ B, int* __restrict__ stats, const int32_t* __restrict__ cpos, int width,
+                     int height, int border, int* __restrict__ kpos, int64_t istride) {
     __shared__ int sh[36];
-    const int t = threadIdx.x;
+    const int l = blockIdx.x, t = threadIdx.x;
     {
-        const int64_t bo = (int64_t)blockIdx.x * istride;
-        in = at(in, bo);
-        keep = at(keep, bo);
-        cnt2 += (int64_t)blockIdx.x * CS;
+        const int64_t bo = (int64_t)blockIdx.y * istride;
         row_off = at(row_off, bo);
-        out = at(out, bo);
-        st += (int64_t)blockIdx.x * CS;
+        A = at(A, bo);
+        B = at(B, bo);
+        stats += (int64_t)blockIdx.y * CS;
+        cpos = at(cpos, bo);
+        kpos = at(kpos, bo);
     }
-    int total = 0;
-    for (int l = 0; l < nl; ++l) total += cnt2[l];
-    const int chunk = (total + RT - 1) / RT, s = min(t * chunk, total), e = min(s + chunk, total);
-    int c = 0, mo = 0;
-    for (int f = s; f < e; ++f) c += keep[f];
-    int dummy = 0;
-    scan2(c, dummy, sh);
-    const int n = sh[32];
-    for (int f = s; f < e; ++f)
-        if (keep[f]) {
-            const Kp q = in[f];
-            out[c++] = q;
-            mo = max(mo, q.octave + 1);
+    const Lvl L = lv[l];
+    const int c0 = lvl_first(row_off, L), m = stats[ST_CNT2 + l];
+    const bool fits = height > 2 * border && width > 2 * border;
+    int base = 0;
+    for (int r0 = 0; r0 < m; r0 += RT) {   // (block-uniform)
+        const int j = r0 + t;
+        int k = 0;
+        if (j < m) {
+            const Resp e = B[c0 + j];
+            const int pos = cpos[A[c0 + e.idx].idx];
+            const int x = round_f((float)(pos & 0xFFFF) * L.scale), y = round_f((float)(pos >> 16) * L.scale);
+            k = fits && border <= x && x < width - border && border <= y && y < height - border;
         }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mo = max(mo, __shfl_xor(mo, o));
-    __syncthreads();
-    if ((t & 63) == 0) sh[t >> 6] = mo;
-    __syncthreads();
-    if (t == 0) {
-        int m = 0;
-        for (int i = 0; i < RT / 64; ++i) m = max(m, sh[i]);
-        st[0] = n;
-        st[1] = m;
-        st[2] = row_off[rows];
+        int pre = k, dummy = 0;
+        scan2(pre, dummy, sh);   // exclusive prefix over the round; its total in sh[32]
+        if (j < m) kpos[c0 + j] = k ? base + pre : -1;
+        base += sh[32];
     }
+    if (t == 0) stats[ST_KCNT + l] = base;
 }
 
 __global__ __launch_bounds__(256)
@@ -1290,13 +1302,13 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
     int rc = SFMX_OK;
     {
         // one image's block: pyr / score / blur slabs, corner records (cpos 4 + cscore 1 + A, B 8 + 8 + Ls, Rs
-        // 4 + 4 + raw / kept keypoints 28 + 28 + flag 4), row counts / offsets, the input copy and the
+        // 4 + 4 + kept keypoints 28 + kept position 4), row offsets, keep words / counts, the input copy and the
         // descriptor staging (host buffers) -- every part 256-B aligned, so the offsets are the same in
         // every block
         auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
         const int mw = (maxw + 255) / 256 * 4;   // keep words per row (64 pixels each; a multiple of 4)
         const size_t blk = 3 * r(px) + r(CAND_CAP * 4) + r(CAND_CAP) + 2 * r(CAND_CAP * sizeof(Resp)) + 2 * r(CAND_CAP * 4) +
-                           2 * r(CAND_CAP * sizeof(Kp)) + r(CAND_CAP * 4) + r((size_t)(rows + 1) * 4) +
+                           r(CAND_CAP * sizeof(Kp)) + r(CAND_CAP * 4) + r((size_t)(rows + 1) * 4) +
                            r((size_t)rows * mw * 8) + r((size_t)rows * mw) +
                            (inputs_on_device ? 0 : r((size_t)width * height) + r((size_t)std::max(capmax, 1) * 32));
         const size_t shared_b = r(std::max<size_t>(tables.size(), 1) * sizeof(AxisEnt)) + r(sizeof(Lvl) * nl) +
@@ -1319,9 +1331,8 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             Resp* rB = A.take<Resp>(CAND_CAP);
             int* sLs = A.take<int>(CAND_CAP);
             int* sRs = A.take<int>(CAND_CAP);
-            Kp* kraw = A.take<Kp>(CAND_CAP);
             Kp* dfin = A.take<Kp>(CAND_CAP);
-            int* keep = A.take<int>(CAND_CAP);
+            int* kpos = A.take<int>(CAND_CAP);
             int* row_off = A.take<int>(rows + 1);
             uint64_t* kmask = A.take<uint64_t>((size_t)rows * mw);
             uint8_t* wcnt = A.take<uint8_t>((size_t)rows * mw);
@@ -1337,8 +1348,8 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             int* stats = A.take<int>((size_t)CS * G);
             if (A.overflow) { set_last_error("internal: ORB scratch arena too small"); rc = SFMX_ECAPACITY; goto done; }
             int* cnt1 = stats;
-            int* cnt2 = stats + MAX_LEVELS;
-            int* sst = stats + 2 * MAX_LEVELS;   // count, levels, corners, err
+            int* cnt2 = stats + ST_CNT2;
+            int* sst = stats + ST_TAIL;   // count, levels, corners, err
             // the chunk's small inputs through pinned staging (one copy each, no pageable staging)
             char* hp = scratch.pin;
             const size_t o_tab = 0, o_lv = o_tab + r(std::max<size_t>(tables.size(), 1) * sizeof(AxisEnt)),
@@ -1383,9 +1394,10 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             orb_harris_kernel<<<dim3(64, nl, gz), 256, 0, st>>>(pyr, dlv, row_off, rA, cnt1, cpos, rB, istride);
             orb_retain_kernel<<<dim3(nl, gz), RT, 0, st>>>(1, dlv, row_off, cscore, rA, rB, sLs, sRs, cnt1, cnt2, s2,
                                                            (int)CAND_CAP, sst + 3, istride);
-            orb_angle_kernel<<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rA, rB, cnt2, cpos, dumax,
-                                                                          width, height, border, kraw, keep, istride);
-            orb_compact_kernel<<<gz, RT, 0, st>>>(kraw, keep, cnt2, nl, row_off, rows, dfin, sst, istride);
+            orb_keep_kernel<<<dim3(nl, gz), RT, 0, st>>>(dlv, row_off, rA, rB, stats, cpos, width, height, border, kpos,
+                                                         istride);
+            orb_angle_kernel<<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rows, rA, rB, stats, cpos,
+                                                                          dumax, kpos, dfin, istride);
             // ---- compute(): blur of the levels used, rBRIEF of min(count, capacity) keypoints
             if (descriptors && capmax > 0) {
                 orb_blur_kernel<<<dim3(flat_tiles<BT_X, BT_Y>(lv), gz), 256, 0, st>>>(
@@ -1401,13 +1413,13 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             OCHK(hipEventRecord(A.e1, st));
             OCHK(hipStreamSynchronize(st));
             for (int g = 0; g < G; ++g) {
-                const int* s = hst + (size_t)g * CS + 2 * MAX_LEVELS;
+                const int* s = hst + (size_t)g * CS + ST_TAIL;
                 if (s[2] > CAND_CAP) { set_last_error("internal: corner buffer overflow"); rc = SFMX_EINTERNAL; goto done; }
                 if (s[3]) { set_last_error("internal: device retainBest made no progress"); rc = SFMX_EINTERNAL; goto done; }
             }
             bool copies = false;
             for (int g = 0; g < G; ++g) {
-                const int n = hst[(size_t)g * CS + 2 * MAX_LEVELS];
+                const int n = hst[(size_t)g * CS + ST_TAIL];
                 n_keypoints[g] = n;
                 const int m = std::min(n, (int)capacities[g]);
                 if (!inputs_on_device && m > 0) {   // host buffers: the kept keypoints and descriptors back
