@@ -1518,7 +1518,10 @@ int sfmx_orb_detect_compute_batch(const sfmx_gray_image* images, int32_t n_image
     std::vector<std::string> errs(n_images);
     std::vector<std::vector<int>> chunks;
     {
-        const int gmax = std::max(1, std::min(16, (n_images + ns - 1) / ns));
+        // chunk size: at most 16, and the chunks a whole number of rounds over the streams (200 images on
+        // 8 streams: 16 chunks of 13 rather than 13 chunks of 16, whose second round left 3 streams idle)
+        const int rounds = std::max(1, (n_images + ns * 16 - 1) / (ns * 16));
+        const int gmax = std::max(1, std::min(16, (n_images + ns * rounds - 1) / (ns * rounds)));
         for (int i = 0; i < n_images; ++i) {
             const sfmx_gray_image& im = images[i];
             if (!im.data || capacities[i] < 0 || (capacities[i] > 0 && !keypoints[i])) {
