@@ -287,6 +287,9 @@ void orb_fast_nms_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict_
     }
     __shared__ __align__(16) uint8_t ti[FI_R][FI_C];
     __shared__ uint8_t ts[FS_R][FS_C + 2];
+    __shared__ uint16_t cand[FS_R * FS_C];
+    __shared__ int ncand;
+    if (threadIdx.x == 0) ncand = 0;
     const uint8_t* src = at(pyr, bo) + L.off;
     if (threadIdx.x < FI_R * (FI_C / 16)) {
         const int r = threadIdx.x / (FI_C / 16), q = threadIdx.x % (FI_C / 16);
@@ -296,12 +299,36 @@ void orb_fast_nms_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict_
         *reinterpret_cast<uint4*>(&ti[r][16 * q]) = v;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < FS_R * FS_C; i += 256) {
-        const int sy = i / FS_C, sx = i - sy * FS_C;
-        const int x = x0 - 1 + sx, y = y0 - 1 + sy;
-        int sc = 0;
-        if (x >= 3 && x < L.w - 3 && y >= 3 && y < L.h - 3) sc = fast_score_lds<FI_C>(&ti[sy + 3][sx + 15], threshold);
-        ts[sy][sx] = (uint8_t)sc;
+    // r04: a quick necessary test first -- an arc of 9 holds two ring pixels 4 apart among 0, 4, 8, 12
+    // (any 8 consecutive positions hold two such, 4 apart), so a corner has some k in {0, 4, 8, 12} with
+    // d_k, d_k+4 both > t or both < -t; the positions passing it are compacted in LDS and only they get
+    // the full score (the tile pass was VALU-bound on the full score of every position, PMC r04h / r04i)
+    for (int i0 = 0; i0 < FS_R * FS_C; i0 += 256) {
+        const int i = i0 + threadIdx.x;
+        bool pass = false;
+        if (i < FS_R * FS_C) {
+            const int sy = i / FS_C, sx = i - sy * FS_C;
+            const int x = x0 - 1 + sx, y = y0 - 1 + sy;
+            if (x >= 3 && x < L.w - 3 && y >= 3 && y < L.h - 3) {
+                const uint8_t* c = &ti[sy + 3][sx + 15];
+                const int v = c[0], d0 = v - c[3 * FI_C], d4 = v - c[3], d8 = v - c[-3 * FI_C], d12 = v - c[-3];
+                const int M = max(max(min(d0, d4), min(d4, d8)), max(min(d8, d12), min(d12, d0)));
+                const int N = min(min(max(d0, d4), max(d4, d8)), min(max(d8, d12), max(d12, d0)));
+                pass = M > threshold || N < -threshold;
+            }
+            ts[sy][sx] = 0;
+        }
+        const uint64_t m = __ballot(pass);
+        int wb = 0;
+        if (lane == 0 && m) wb = atomicAdd(&ncand, __popcll(m));
+        wb = __shfl(wb, 0);
+        if (pass) cand[wb + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)i;
+    }
+    __syncthreads();
+    const int nc = ncand;
+    for (int c = threadIdx.x; c < nc; c += 256) {
+        const int i = cand[c], sy = i / FS_C, sx = i - sy * FS_C;
+        ts[sy][sx] = (uint8_t)fast_score_lds<FI_C>(&ti[sy + 3][sx + 15], threshold);
     }
     __syncthreads();
     score = at(score, bo) + L.off;

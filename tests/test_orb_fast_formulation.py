@@ -1,7 +1,7 @@
 """The FAST score formulation of the device kernel (orb_features.hip fast_score_lds, r04) against the
 bit-mask test + cornerScore<16> loops it replaced, which restate OpenCV 4.5.1's FAST_t<16> and
 cornerScore<16> (oracle/orb_oracle.cpp): on random, near-threshold and arc-shaped rings the corner
-decision and the score agree for every threshold.  CPU only (test infrastructure)."""
+decision and the score agree for every threshold, and the kernel's quick pre-test passes every corner.  CPU only (test infrastructure)."""
 import numpy as np
 
 
@@ -37,6 +37,13 @@ def _arc_form(v, p, t):   # the kernel's: sliding minima / maxima of width 3, ar
     return e - 1 if e > t else 0
 
 
+def _quick_pass(v, p, t):   # the kernel's pre-test: ring pixels 0, 4, 8, 12 pairwise 4 apart
+    d = [v - p[k] for k in (0, 4, 8, 12)]
+    M = max(min(d[k], d[(k + 1) % 4]) for k in range(4))
+    N = min(max(d[k], d[(k + 1) % 4]) for k in range(4))
+    return M > t or N < -t
+
+
 def test_arc_form_equals_mask_test_and_corner_score():
     rng = np.random.default_rng(7)
     corners = 0
@@ -58,5 +65,6 @@ def test_arc_form_equals_mask_test_and_corner_score():
         p = [int(x) for x in p]
         a = _mask_form(v, p, t)
         assert a == _arc_form(v, p, t), (v, p, t)
+        assert a == 0 or _quick_pass(v, p, t), (v, p, t)   # the pre-test never rejects a corner
         corners += a > 0
     assert corners > 3000
