@@ -124,7 +124,11 @@ void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, in
     const uint8_t* src = pyr + S.off;
     bool staged = x0 >= D.xdmin && x0 + RZ_X <= D.xdmax && y0 >= D.ydmin && y0 + RZ_Y <= D.ydmax;
     int bx = 0, sy0 = 0;
+    AxisEnt hx[4], ey{0, 0, 0};   // this thread's table entries, loaded ahead of the tile
     if (staged) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hx[i] = ax[x + i];
+        ey = ay[y];
         bx = ax[x0].ofs & ~15;
         sy0 = ay[y0].ofs;
         const int ncols = ax[x0 + RZ_X - 1].ofs + 2 - bx, nrows = ay[y0 + RZ_Y - 1].ofs + 2 - sy0;
@@ -142,12 +146,12 @@ void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, in
     if (x >= D.w || y >= D.h) return;
     uint32_t out = 0;
     if (staged) {
-        const AxisEnt e = ay[y];
+        const AxisEnt e = ey;
         const uint8_t* t0 = T[e.ofs - sy0];
         const uint8_t* t1 = T[e.ofs + 1 - sy0];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const AxisEnt h = ax[x + i];
+            const AxisEnt h = hx[i];
             const int o = h.ofs - bx;
             const uint32_t h0 = min((uint32_t)h.m0 * t0[o] + (uint32_t)h.m1 * t0[o + 1], 0xFFFFu);
             const uint32_t h1 = min((uint32_t)h.m0 * t1[o] + (uint32_t)h.m1 * t1[o + 1], 0xFFFFu);
@@ -750,39 +754,29 @@ __device__ float fast_atan2(float y, float x) {   // cv::fastAtan2
     return a;
 }
 
-__device__ __forceinline__ int wave_isum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
 // the final keypoints in level order -> cv::KeyPoint with ICAngles' angle (one wavefront per
 // keypoint: the 31 patch rows u = -15..15 across lanes; integer moments, so the lane order is
 // irrelevant), and compute()'s runByImageBorder(31) test at full resolution (Rect::contains(Point(pt)))
 __global__ __launch_bounds__(256)
 void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int nl,
-                      const int* __restrict__ row_off, int rows, const Resp* __restrict__ A, const Resp* __restrict__ B,
-                      int* __restrict__ stats, const int32_t* __restrict__ cpos, const int* __restrict__ umax,
-                      const int* __restrict__ kpos, Kp* __restrict__ out, int64_t istride) {
+                      const int* __restrict__ row_off, int rows, int* __restrict__ stats, const int* __restrict__ umax,
+                      const Resp* __restrict__ kin, Kp* __restrict__ out, int64_t istride) {
     const int lane = threadIdx.x & 63;
     {
         const int64_t bo = (int64_t)blockIdx.y * istride;
         pyr = at(pyr, bo);
         row_off = at(row_off, bo);
-        A = at(A, bo);
-        B = at(B, bo);
         stats += (int64_t)blockIdx.y * CS;
-        cpos = at(cpos, bo);
-        kpos = at(kpos, bo);
+        kin = at(kin, bo);
         out = at(out, bo);
     }
-    const int* cnt2 = stats + ST_CNT2;
-    __shared__ int sumax[HALF_PATCH + 1], lbase[MAX_LEVELS + 1];
+    __shared__ int sumax[HALF_PATCH + 1], lbase[MAX_LEVELS + 1], lfirst[MAX_LEVELS];
     if (threadIdx.x <= HALF_PATCH) sumax[threadIdx.x] = umax[threadIdx.x];
     if (threadIdx.x == 0) {   // the kept keypoints' level offsets; block 0 publishes count, levels, corners
         int b = 0, used = 0;
         for (int l = 0; l < nl; ++l) {
             lbase[l] = b;
+            lfirst[l] = lvl_first(row_off, lv[l]);
             b += stats[ST_KCNT + l];
             if (stats[ST_KCNT + l] > 0) used = l + 1;
         }
@@ -794,37 +788,36 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         }
     }
     __syncthreads();
-    // this lane's words of the 31 patch rows (9 aligned words a row, 5 per lane), the same for every keypoint
-    bool wok[5];
-    int wd[5], wrow[5], wum[5];
+    // two keypoints per wave (r04), 32 lanes each: this lane's words of the 31 patch rows (9 aligned words a
+    // row, 279 in all, 9 per lane), the same for every keypoint
+    const int hl = lane & 31;
+    constexpr int NWD = (2 * HALF_PATCH + 1) * 9, NK = (NWD + 31) / 32;
+    bool wok[NK];
+    int wd[NK], wrow[NK], wum[NK];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const int idx = lane + 64 * k, r = idx / 9;
-        wok[k] = idx < (2 * HALF_PATCH + 1) * 9;
+    for (int k = 0; k < NK; ++k) {
+        const int idx = hl + 32 * k, r = idx / 9;
+        wok[k] = idx < NWD;
         wd[k] = idx - 9 * r;
         wrow[k] = r - HALF_PATCH;
         wum[k] = wok[k] ? sumax[wrow[k] < 0 ? -wrow[k] : wrow[k]] : 0;
     }
-    int total = 0;
-    for (int l = 0; l < nl; ++l) total += cnt2[l];
-    for (int f = blockIdx.x * 4 + (threadIdx.x >> 6); f < total; f += gridDim.x * 4) {
-        int l = 0, j = f;
-        while (j >= cnt2[l]) { j -= cnt2[l]; ++l; }
+    const int total = lbase[nl];   // the kept keypoints (orb_keep_kernel), in output order
+    for (int f = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5); f < total; f += gridDim.x * 8) {
+        int l = 0;
+        while (f >= lbase[l + 1]) ++l;
         const Lvl L = lv[l];
-        const int c0 = lvl_first(row_off, L);
-        const int kp = kpos[c0 + j];
-        if (kp < 0) continue;   // dropped by compute()'s border test (orb_keep_kernel)
-        const Resp e = B[c0 + j];
-        const int pos = cpos[A[c0 + e.idx].idx], cx = pos & 0xFFFF, cy = pos >> 16;
+        const Resp e = kin[lfirst[l] + f - lbase[l]];   // (response, packed position)
+        const int pos = e.idx, cx = pos & 0xFFFF, cy = pos >> 16;
         const uint8_t* img = pyr + L.off;
         const int step = L.pitch;
-        // r04: the 31 patch rows as aligned 4-byte loads, 9 per row (columns (cx-15) & ~3 ..), 5 per
-        // lane; a pixel counts where |u| <= umax[|v|] (integer moments: any order, the same sums).
-        // r03 made 31 byte loads per lane, one row at a time.
+        // the 31 patch rows as aligned 4-byte words (columns (cx-15) & ~3 ..); a pixel counts where
+        // |u| <= umax[|v|] (integer moments: any order, the same sums).  r03 made 31 byte loads per
+        // lane, one row at a time.
         const int xa = (cx - HALF_PATCH) & ~3;
         int m10 = 0, m01 = 0;
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
+        for (int k = 0; k < NK; ++k) {
             if (!wok[k]) continue;
             // the word's pixels inside the circle (|u| <= umax[|v|]) are one byte run [lo, hi]; with
             // the others masked off, sum I and sum i I come from two v_dot4_u32_u8:
@@ -837,9 +830,12 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
             m10 += (X - cx) * s1 + si;
             m01 += wrow[k] * s1;
         }
-        m10 = wave_isum(m10);
-        m01 = wave_isum(m01);
-        if (lane == 0) {
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) {   // the half-wave's sums (xor partners stay in the half)
+            m10 += __shfl_xor(m10, o);
+            m01 += __shfl_xor(m01, o);
+        }
+        if (hl == 0) {
             Kp q;
             q.x = (float)cx * L.scale;
             q.y = (float)cy * L.scale;
@@ -848,7 +844,7 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
             q.response = e.response;
             q.octave = l;
             q.class_id = -1;
-            out[lbase[l] + kp] = q;
+            out[f] = q;
         }
     }
 }
@@ -857,11 +853,12 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
 // the level position x scale) of every level's retained keypoints, and their places in the kept list,
 // before the angles (r04: the angle kernel writes the kept keypoints in place; r03 wrote them all and
 // compacted them in one workgroup per image).  One workgroup per (level, image), rounds of RT records
-// scanned in order: kpos[c0 + j] = position among the level's kept keypoints or -1, kcnt[l] = their count.
+// scanned in order: kin[c0 + i] = (response, packed position) of the level's i-th kept keypoint,
+// kcnt[l] = their count.
 __global__ __launch_bounds__(RT)
 void orb_keep_kernel(const Lvl* __restrict__ lv, const int* __restrict__ row_off, const Resp* __restrict__ A,
                      const Resp* __restrict__ B, int* __restrict__ stats, const int32_t* __restrict__ cpos, int width,
-                     int height, int border, int* __restrict__ kpos, int64_t istride) {
+                     int height, int border, Resp* __restrict__ kin, int64_t istride) {
     __shared__ int sh[36];
     const int l = blockIdx.x, t = threadIdx.x;
     {
@@ -871,7 +868,7 @@ void orb_keep_kernel(const Lvl* __restrict__ lv, const int* __restrict__ row_off
         B = at(B, bo);
         stats += (int64_t)blockIdx.y * CS;
         cpos = at(cpos, bo);
-        kpos = at(kpos, bo);
+        kin = at(kin, bo);
     }
     const Lvl L = lv[l];
     const int c0 = lvl_first(row_off, L), m = stats[ST_CNT2 + l];
@@ -879,16 +876,18 @@ void orb_keep_kernel(const Lvl* __restrict__ lv, const int* __restrict__ row_off
     int base = 0;
     for (int r0 = 0; r0 < m; r0 += RT) {   // (block-uniform)
         const int j = r0 + t;
-        int k = 0;
+        int k = 0, pos = 0;
+        float resp = 0.f;
         if (j < m) {
             const Resp e = B[c0 + j];
-            const int pos = cpos[A[c0 + e.idx].idx];
+            pos = cpos[A[c0 + e.idx].idx];
+            resp = e.response;
             const int x = round_f((float)(pos & 0xFFFF) * L.scale), y = round_f((float)(pos >> 16) * L.scale);
             k = fits && border <= x && x < width - border && border <= y && y < height - border;
         }
         int pre = k, dummy = 0;
         scan2(pre, dummy, sh);   // exclusive prefix over the round; its total in sh[32]
-        if (j < m) kpos[c0 + j] = k ? base + pre : -1;
+        if (k) kin[c0 + base + pre] = Resp{resp, pos};   // the level's kept keypoints, dense, in order
         base += sh[32];
     }
     if (t == 0) stats[ST_KCNT + l] = base;
@@ -1022,7 +1021,7 @@ __device__ void orb_sincos(double x, double* s, double* c) {
 // pattern point)| <= 18: the pattern lies in [-13, 12]^2) is staged in LDS by 16-byte loads, one
 // window per keypoint slot; keypoints whose window needs the edge clamp read the level directly.
 constexpr int BW = 18;                 // window half-size
-constexpr int BWR = 2 * BW + 1, BWC = 64;
+constexpr int BWR = 2 * BW + 1, BWC = 80;   // (80-byte rows: 20 banks apart, not 16 -- fewer conflicts)
 __global__ __launch_bounds__(256)
 void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ lv, const Kp* __restrict__ kps,
                       const int* __restrict__ st, const ImgIO* __restrict__ io, int64_t istride) {
@@ -1329,13 +1328,13 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
     int rc = SFMX_OK;
     {
         // one image's block: pyr / score / blur slabs, corner records (cpos 4 + cscore 1 + A, B 8 + 8 + Ls, Rs
-        // 4 + 4 + kept keypoints 28 + kept position 4), row offsets, keep words / counts, the input copy and the
+        // 4 + 4 + kept keypoints 28 + kept records 8), row offsets, keep words / counts, the input copy and the
         // descriptor staging (host buffers) -- every part 256-B aligned, so the offsets are the same in
         // every block
         auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
         const int mw = (maxw + 255) / 256 * 4;   // keep words per row (64 pixels each; a multiple of 4)
         const size_t blk = 3 * r(px) + r(CAND_CAP * 4) + r(CAND_CAP) + 2 * r(CAND_CAP * sizeof(Resp)) + 2 * r(CAND_CAP * 4) +
-                           r(CAND_CAP * sizeof(Kp)) + r(CAND_CAP * 4) + r((size_t)(rows + 1) * 4) +
+                           r(CAND_CAP * sizeof(Kp)) + r(CAND_CAP * sizeof(Resp)) + r((size_t)(rows + 1) * 4) +
                            r((size_t)rows * mw * 8) + r((size_t)rows * mw) +
                            (inputs_on_device ? 0 : r((size_t)width * height) + r((size_t)std::max(capmax, 1) * 32));
         const size_t shared_b = r(std::max<size_t>(tables.size(), 1) * sizeof(AxisEnt)) + r(sizeof(Lvl) * nl) +
@@ -1359,7 +1358,7 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             int* sLs = A.take<int>(CAND_CAP);
             int* sRs = A.take<int>(CAND_CAP);
             Kp* dfin = A.take<Kp>(CAND_CAP);
-            int* kpos = A.take<int>(CAND_CAP);
+            Resp* kin = A.take<Resp>(CAND_CAP);
             int* row_off = A.take<int>(rows + 1);
             uint64_t* kmask = A.take<uint64_t>((size_t)rows * mw);
             uint8_t* wcnt = A.take<uint8_t>((size_t)rows * mw);
@@ -1421,10 +1420,10 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             orb_harris_kernel<<<dim3(64, nl, gz), 256, 0, st>>>(pyr, dlv, row_off, rA, cnt1, cpos, rB, istride);
             orb_retain_kernel<<<dim3(nl, gz), RT, 0, st>>>(1, dlv, row_off, cscore, rA, rB, sLs, sRs, cnt1, cnt2, s2,
                                                            (int)CAND_CAP, sst + 3, istride);
-            orb_keep_kernel<<<dim3(nl, gz), RT, 0, st>>>(dlv, row_off, rA, rB, stats, cpos, width, height, border, kpos,
+            orb_keep_kernel<<<dim3(nl, gz), RT, 0, st>>>(dlv, row_off, rA, rB, stats, cpos, width, height, border, kin,
                                                          istride);
-            orb_angle_kernel<<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rows, rA, rB, stats, cpos,
-                                                                          dumax, kpos, dfin, istride);
+            orb_angle_kernel<<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rows, stats, dumax, kin,
+                                                                          dfin, istride);
             // ---- compute(): blur of the levels used, rBRIEF of min(count, capacity) keypoints
             if (descriptors && capmax > 0) {
                 orb_blur_kernel<<<dim3(flat_tiles<BT_X, BT_Y>(lv), gz), 256, 0, st>>>(
