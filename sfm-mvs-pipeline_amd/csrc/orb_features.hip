@@ -104,13 +104,13 @@ __device__ __forceinline__ uint32_t hval(const uint8_t* __restrict__ r, const Ax
     return min((uint32_t)e.m0 * r[e.ofs] + (uint32_t)e.m1 * r[e.ofs + 1], 0xFFFFu);
 }
 
-// r04: one workgroup per 64 x 16 output tile, 4 neighbouring outputs per thread, one 4-byte store (the
+// r04: one workgroup per 128 x 16 output tile, 8 neighbouring outputs per thread, one 8-byte store (the
 // level pitch is a multiple of 64).  A tile whose outputs all take the interpolating branch on both
 // axes (and whose source span fits, i.e. scale factors up to ~2) stages its source rectangle in LDS by
 // 16-byte loads and reads the taps' bytes from there; the tiles at the edges (replicated rows /
 // columns, the padding past the width) keep the per-pixel form.  The same integer expressions either
 // way.  r03 made 4 byte loads and a table load per output pixel, the level chain measured load-bound.
-constexpr int RZ_X = 64, RZ_Y = 16, RZ_R = 32, RZ_C = 144;   // tile; the largest staged source span
+constexpr int RZ_PX = 8, RZ_X = 16 * RZ_PX, RZ_Y = 16, RZ_R = 32, RZ_C = 272;   // tile; the largest staged source span
 __global__ __launch_bounds__(256)
 void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int l,
                        const AxisEnt* __restrict__ tables, int64_t istride) {
@@ -118,16 +118,16 @@ void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, in
     pyr = at(pyr, (int64_t)blockIdx.z * istride);
     const Lvl D = lv[l], S = lv[l - 1];
     const int x0 = blockIdx.x * RZ_X, y0 = blockIdx.y * RZ_Y;
-    const int x = x0 + 4 * (threadIdx.x & 15), y = y0 + (threadIdx.x >> 4);
+    const int x = x0 + RZ_PX * (threadIdx.x & 15), y = y0 + (threadIdx.x >> 4);
     const AxisEnt* ax = tables + D.ax_off;
     const AxisEnt* ay = tables + D.ay_off;
     const uint8_t* src = pyr + S.off;
     bool staged = x0 >= D.xdmin && x0 + RZ_X <= D.xdmax && y0 >= D.ydmin && y0 + RZ_Y <= D.ydmax;
     int bx = 0, sy0 = 0;
-    AxisEnt hx[4], ey{0, 0, 0};   // this thread's table entries, loaded ahead of the tile
+    AxisEnt hx[RZ_PX], ey{0, 0, 0};   // this thread's table entries, loaded ahead of the tile
     if (staged) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) hx[i] = ax[x + i];
+        for (int i = 0; i < RZ_PX; ++i) hx[i] = ax[x + i];
         ey = ay[y];
         bx = ax[x0].ofs & ~15;
         sy0 = ay[y0].ofs;
@@ -144,38 +144,39 @@ void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, in
         __syncthreads();
     }
     if (x >= D.w || y >= D.h) return;
-    uint32_t out = 0;
+    uint32_t out[RZ_PX / 4] = {};
     if (staged) {
         const AxisEnt e = ey;
         const uint8_t* t0 = T[e.ofs - sy0];
         const uint8_t* t1 = T[e.ofs + 1 - sy0];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < RZ_PX; ++i) {
             const AxisEnt h = hx[i];
             const int o = h.ofs - bx;
             const uint32_t h0 = min((uint32_t)h.m0 * t0[o] + (uint32_t)h.m1 * t0[o + 1], 0xFFFFu);
             const uint32_t h1 = min((uint32_t)h.m0 * t1[o] + (uint32_t)h.m1 * t1[o + 1], 0xFFFFu);
-            out |= min((h0 * e.m0 + h1 * e.m1 + 32768u) >> 16, 255u) << (8 * i);
+            out[i >> 2] |= min((h0 * e.m0 + h1 * e.m1 + 32768u) >> 16, 255u) << (8 * (i & 3));
         }
     } else {
         const int last_ofs = ax[D.w - 1].ofs;
         if (y < D.ydmin || y >= D.ydmax) {
             const uint8_t* r = src + (int64_t)(y < D.ydmin ? 0 : S.h - 1) * S.pitch;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) out |= min((hval(r, ax, x + i, D.xdmin, D.xdmax, last_ofs) + 128u) >> 8, 255u) << (8 * i);
+            for (int i = 0; i < RZ_PX; ++i)
+                out[i >> 2] |= min((hval(r, ax, x + i, D.xdmin, D.xdmax, last_ofs) + 128u) >> 8, 255u) << (8 * (i & 3));
         } else {
             const AxisEnt e = ay[y];
             const uint8_t* r0 = src + (int64_t)e.ofs * S.pitch;
             const uint8_t* r1 = r0 + S.pitch;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < RZ_PX; ++i) {
                 const uint32_t h0 = hval(r0, ax, x + i, D.xdmin, D.xdmax, last_ofs);
                 const uint32_t h1 = hval(r1, ax, x + i, D.xdmin, D.xdmax, last_ofs);
-                out |= min((h0 * e.m0 + h1 * e.m1 + 32768u) >> 16, 255u) << (8 * i);
+                out[i >> 2] |= min((h0 * e.m0 + h1 * e.m1 + 32768u) >> 16, 255u) << (8 * (i & 3));
             }
         }
     }
-    *reinterpret_cast<uint32_t*>(pyr + D.off + (int64_t)y * D.pitch + x) = out;
+    *reinterpret_cast<uint2*>(pyr + D.off + (int64_t)y * D.pitch + x) = make_uint2(out[0], out[1]);   // (x + 8 <= pitch)
 }
 
 // level 0 from the caller's image: 16 pixels per thread (64 x 4 threads: 1024 columns of 4 rows), one
