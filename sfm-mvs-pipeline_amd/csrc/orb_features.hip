@@ -110,13 +110,17 @@ __device__ __forceinline__ uint32_t hval(const uint8_t* __restrict__ r, const Ax
 // 16-byte loads and reads the taps' bytes from there; the tiles at the edges (replicated rows /
 // columns, the padding past the width) keep the per-pixel form.  The same integer expressions either
 // way.  r03 made 4 byte loads and a table load per output pixel, the level chain measured load-bound.
-constexpr int RZ_PX = 8, RZ_X = 16 * RZ_PX, RZ_Y = 16, RZ_R = 32, RZ_C = 272;   // tile; the largest staged source span
+constexpr int RZ_PX = 8, RZ_X = 16 * RZ_PX, RZ_Y = 16, RZ_R = 40, RZ_C = 272;   // tile; the largest staged source span
+// the source offset linear_axis gives destination v (the same double expression, so the same value;
+// the staged rectangle keeps a one-pixel margin either way)
+__device__ __forceinline__ int src_ofs(double scale, int v) { return (int)floor(scale * ((double)v + 0.5) - 0.5); }
+// D / S (this level and the one it is resized from) come as kernel arguments and the staged source
+// rectangle from the axis scales, so the tile's loads do not wait on the level table or the axis tables
 __global__ __launch_bounds__(256)
-void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int l,
+void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl D, const Lvl S, double sx, double sy,
                        const AxisEnt* __restrict__ tables, int64_t istride) {
     __shared__ __align__(16) uint8_t T[RZ_R][RZ_C];
     pyr = at(pyr, (int64_t)blockIdx.z * istride);
-    const Lvl D = lv[l], S = lv[l - 1];
     const int x0 = blockIdx.x * RZ_X, y0 = blockIdx.y * RZ_Y;
     const int x = x0 + RZ_PX * (threadIdx.x & 15), y = y0 + (threadIdx.x >> 4);
     const AxisEnt* ax = tables + D.ax_off;
@@ -124,14 +128,15 @@ void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, in
     const uint8_t* src = pyr + S.off;
     bool staged = x0 >= D.xdmin && x0 + RZ_X <= D.xdmax && y0 >= D.ydmin && y0 + RZ_Y <= D.ydmax;
     int bx = 0, sy0 = 0;
-    AxisEnt hx[RZ_PX], ey{0, 0, 0};   // this thread's table entries, loaded ahead of the tile
+    AxisEnt hx[RZ_PX], ey{0, 0, 0};   // this thread's table entries, loaded beside the tile
     if (staged) {
 #pragma unroll
         for (int i = 0; i < RZ_PX; ++i) hx[i] = ax[x + i];
         ey = ay[y];
-        bx = ax[x0].ofs & ~15;
-        sy0 = ay[y0].ofs;
-        const int ncols = ax[x0 + RZ_X - 1].ofs + 2 - bx, nrows = ay[y0 + RZ_Y - 1].ofs + 2 - sy0;
+        bx = max(0, src_ofs(sx, x0) - 1) & ~15;
+        sy0 = max(0, src_ofs(sy, y0) - 1);
+        const int ncols = min(S.w - 1, src_ofs(sx, x0 + RZ_X - 1) + 2) + 1 - bx;
+        const int nrows = min(S.h - 1, src_ofs(sy, y0 + RZ_Y - 1) + 2) + 1 - sy0;
         staged = ncols <= RZ_C && nrows <= RZ_R;   // (block-uniform)
         if (staged) {
             const int nq = (ncols + 15) >> 4;   // (the last word ends inside the padded row)
@@ -1065,8 +1070,12 @@ void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const float2 ab = make_float2(a, b), nba = make_float2(-b, a);
         auto value = [&](int e) -> int {
-            const float x = pxf[e] * a - pyf[e] * b, y = pxf[e] * b + pyf[e] * a;
+            // (x, y) = (px a - py b, px b + py a): the same products and sums (exact negation, no
+            // contraction), two packed fp32 multiplies and one packed add (v_pk_*_f32)
+            const float2 r = make_float2(pxf[e], pxf[e]) * ab + make_float2(pyf[e], pyf[e]) * nba;
+            const float x = r.x, y = r.y;
             if (staged) return wn[(round_f(y) + BW) * BWC + cx + round_f(x) - xs];
             const int yy = min(max(cy + round_f(y), 0), L.h - 1), xx = min(max(cx + round_f(x), 0), L.w - 1);
             return img[(int64_t)yy * L.pitch + xx];
@@ -1405,9 +1414,10 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             // ---- detect(): pyramid, FAST, NMS
             orb_copy_kernel<<<dim3((width + 1023) / 1024, (height + 3) / 4, gz), 256, 0, st>>>(dio, width, height, lv[0].pitch,
                                                                                           pyr, istride);
-            for (int l = 1; l < nl; l++)
-                orb_resize_kernel<<<dim3((lv[l].w + RZ_X - 1) / RZ_X, (lv[l].h + RZ_Y - 1) / RZ_Y, gz), 256, 0, st>>>(pyr, dlv, l,
-                                                                                                        dtab, istride);
+            for (int l = 1; l < nl; l++)   // (the axis scales as linear_axis computes them)
+                orb_resize_kernel<<<dim3((lv[l].w + RZ_X - 1) / RZ_X, (lv[l].h + RZ_Y - 1) / RZ_Y, gz), 256, 0, st>>>(
+                    pyr, lv[l], lv[l - 1], 1.0 / ((double)lv[l].w / lv[l - 1].w), 1.0 / ((double)lv[l].h / lv[l - 1].h), dtab,
+                    istride);
             orb_fast_nms_kernel<<<dim3(flat_tiles<FT_X, FT_Y>(lv), gz), 256, 0, st>>>(pyr, dlv, thr, border, score, kmask,
                                                                                    wcnt, mw, nl, istride);
             orb_scan_kernel<<<gz, 1024, 0, st>>>(wcnt, mw, rows, row_off, istride, stats, dlv, nl);
