@@ -104,13 +104,14 @@ __device__ __forceinline__ uint32_t hval(const uint8_t* __restrict__ r, const Ax
     return min((uint32_t)e.m0 * r[e.ofs] + (uint32_t)e.m1 * r[e.ofs + 1], 0xFFFFu);
 }
 
-// r04: one workgroup per 128 x 16 output tile, 8 neighbouring outputs per thread, one 8-byte store (the
+// r04: one workgroup per 128 x 32 output tile, 8 neighbouring outputs x 2 rows per thread, 8-byte stores (the
 // level pitch is a multiple of 64).  A tile whose outputs all take the interpolating branch on both
 // axes (and whose source span fits, i.e. scale factors up to ~2) stages its source rectangle in LDS by
 // 16-byte loads and reads the taps' bytes from there; the tiles at the edges (replicated rows /
 // columns, the padding past the width) keep the per-pixel form.  The same integer expressions either
 // way.  r03 made 4 byte loads and a table load per output pixel, the level chain measured load-bound.
-constexpr int RZ_PX = 8, RZ_X = 16 * RZ_PX, RZ_Y = 16, RZ_R = 40, RZ_C = 272;   // tile; the largest staged source span
+constexpr int RZ_PX = 8, RZ_RT = 2, RZ_X = 16 * RZ_PX, RZ_Y = 16 * RZ_RT;   // 8 columns x 2 rows per thread
+constexpr int RZ_R = 2 * RZ_Y + 8, RZ_C = 2 * RZ_X + 16;                     // the largest staged source span
 // the source offset linear_axis gives destination v (the same double expression, so the same value;
 // the staged rectangle keeps a one-pixel margin either way)
 __device__ __forceinline__ int src_ofs(double scale, int v) { return (int)floor(scale * ((double)v + 0.5) - 0.5); }
@@ -122,17 +123,18 @@ void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl D, const Lvl S, doub
     __shared__ __align__(16) uint8_t T[RZ_R][RZ_C];
     pyr = at(pyr, (int64_t)blockIdx.z * istride);
     const int x0 = blockIdx.x * RZ_X, y0 = blockIdx.y * RZ_Y;
-    const int x = x0 + RZ_PX * (threadIdx.x & 15), y = y0 + (threadIdx.x >> 4);
+    const int x = x0 + RZ_PX * (threadIdx.x & 15), yb = y0 + (threadIdx.x >> 4);   // rows yb + 16 r
     const AxisEnt* ax = tables + D.ax_off;
     const AxisEnt* ay = tables + D.ay_off;
     const uint8_t* src = pyr + S.off;
     bool staged = x0 >= D.xdmin && x0 + RZ_X <= D.xdmax && y0 >= D.ydmin && y0 + RZ_Y <= D.ydmax;
     int bx = 0, sy0 = 0;
-    AxisEnt hx[RZ_PX], ey{0, 0, 0};   // this thread's table entries, loaded beside the tile
+    AxisEnt hx[RZ_PX], ey[RZ_RT];   // this thread's table entries, loaded beside the tile
     if (staged) {
 #pragma unroll
         for (int i = 0; i < RZ_PX; ++i) hx[i] = ax[x + i];
-        ey = ay[y];
+#pragma unroll
+        for (int r = 0; r < RZ_RT; ++r) ey[r] = ay[yb + 16 * r];
         bx = max(0, src_ofs(sx, x0) - 1) & ~15;
         sy0 = max(0, src_ofs(sy, y0) - 1);
         const int ncols = min(S.w - 1, src_ofs(sx, x0 + RZ_X - 1) + 2) + 1 - bx;
@@ -148,40 +150,45 @@ void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl D, const Lvl S, doub
         }
         __syncthreads();
     }
-    if (x >= D.w || y >= D.h) return;
-    uint32_t out[RZ_PX / 4] = {};
-    if (staged) {
-        const AxisEnt e = ey;
-        const uint8_t* t0 = T[e.ofs - sy0];
-        const uint8_t* t1 = T[e.ofs + 1 - sy0];
+    if (x >= D.w) return;
 #pragma unroll
-        for (int i = 0; i < RZ_PX; ++i) {
-            const AxisEnt h = hx[i];
-            const int o = h.ofs - bx;
-            const uint32_t h0 = min((uint32_t)h.m0 * t0[o] + (uint32_t)h.m1 * t0[o + 1], 0xFFFFu);
-            const uint32_t h1 = min((uint32_t)h.m0 * t1[o] + (uint32_t)h.m1 * t1[o + 1], 0xFFFFu);
-            out[i >> 2] |= min((h0 * e.m0 + h1 * e.m1 + 32768u) >> 16, 255u) << (8 * (i & 3));
-        }
-    } else {
-        const int last_ofs = ax[D.w - 1].ofs;
-        if (y < D.ydmin || y >= D.ydmax) {
-            const uint8_t* r = src + (int64_t)(y < D.ydmin ? 0 : S.h - 1) * S.pitch;
-#pragma unroll
-            for (int i = 0; i < RZ_PX; ++i)
-                out[i >> 2] |= min((hval(r, ax, x + i, D.xdmin, D.xdmax, last_ofs) + 128u) >> 8, 255u) << (8 * (i & 3));
-        } else {
-            const AxisEnt e = ay[y];
-            const uint8_t* r0 = src + (int64_t)e.ofs * S.pitch;
-            const uint8_t* r1 = r0 + S.pitch;
+    for (int r = 0; r < RZ_RT; ++r) {
+        const int y = yb + 16 * r;
+        if (y >= D.h) break;
+        uint32_t out[RZ_PX / 4] = {};
+        if (staged) {
+            const AxisEnt e = ey[r];
+            const uint8_t* t0 = T[e.ofs - sy0];
+            const uint8_t* t1 = T[e.ofs + 1 - sy0];
 #pragma unroll
             for (int i = 0; i < RZ_PX; ++i) {
-                const uint32_t h0 = hval(r0, ax, x + i, D.xdmin, D.xdmax, last_ofs);
-                const uint32_t h1 = hval(r1, ax, x + i, D.xdmin, D.xdmax, last_ofs);
+                const AxisEnt h = hx[i];
+                const int o = h.ofs - bx;
+                const uint32_t h0 = min((uint32_t)h.m0 * t0[o] + (uint32_t)h.m1 * t0[o + 1], 0xFFFFu);
+                const uint32_t h1 = min((uint32_t)h.m0 * t1[o] + (uint32_t)h.m1 * t1[o + 1], 0xFFFFu);
                 out[i >> 2] |= min((h0 * e.m0 + h1 * e.m1 + 32768u) >> 16, 255u) << (8 * (i & 3));
             }
+        } else {
+            const int last_ofs = ax[D.w - 1].ofs;
+            if (y < D.ydmin || y >= D.ydmax) {
+                const uint8_t* rw = src + (int64_t)(y < D.ydmin ? 0 : S.h - 1) * S.pitch;
+#pragma unroll
+                for (int i = 0; i < RZ_PX; ++i)
+                    out[i >> 2] |= min((hval(rw, ax, x + i, D.xdmin, D.xdmax, last_ofs) + 128u) >> 8, 255u) << (8 * (i & 3));
+            } else {
+                const AxisEnt e = ay[y];
+                const uint8_t* r0 = src + (int64_t)e.ofs * S.pitch;
+                const uint8_t* r1 = r0 + S.pitch;
+#pragma unroll
+                for (int i = 0; i < RZ_PX; ++i) {
+                    const uint32_t h0 = hval(r0, ax, x + i, D.xdmin, D.xdmax, last_ofs);
+                    const uint32_t h1 = hval(r1, ax, x + i, D.xdmin, D.xdmax, last_ofs);
+                    out[i >> 2] |= min((h0 * e.m0 + h1 * e.m1 + 32768u) >> 16, 255u) << (8 * (i & 3));
+                }
+            }
         }
+        *reinterpret_cast<uint2*>(pyr + D.off + (int64_t)y * D.pitch + x) = make_uint2(out[0], out[1]);   // (x + 8 <= pitch)
     }
-    *reinterpret_cast<uint2*>(pyr + D.off + (int64_t)y * D.pitch + x) = make_uint2(out[0], out[1]);   // (x + 8 <= pitch)
 }
 
 // level 0 from the caller's image: 16 pixels per thread (64 x 4 threads: 1024 columns of 4 rows), one
