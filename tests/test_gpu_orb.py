@@ -62,6 +62,10 @@ def test_large_photo_and_parameters():
     k, _ = _check(img, nfeatures=30000)
     assert len(k) > 1000
     _check(img, nfeatures=3000, scaleFactor=1.5, nlevels=5, fastThreshold=12, edgeThreshold=40)
+    # r04 kernels' edge regimes: the resize's staged source span at its limit (scale 2) and past it
+    # (2.6: the per-pixel form), the smallest edge threshold (rBRIEF windows that need the edge clamp)
+    _check(img, nfeatures=2000, scaleFactor=2.0, nlevels=4, edgeThreshold=16)
+    _check(img, nfeatures=1000, scaleFactor=2.6, nlevels=3, edgeThreshold=16, fastThreshold=8)
 
 
 def test_degenerate_inputs():
