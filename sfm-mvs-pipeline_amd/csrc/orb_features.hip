@@ -1290,9 +1290,12 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
         if (im.width != width || im.height != height) { set_last_error("internal: a chunk mixes image sizes"); return SFMX_EINTERNAL; }
     }
     if (P->nfeatures < 0 || !(P->scale_factor > 1.f) || P->n_levels < 1 || P->n_levels > MAX_LEVELS ||
-        P->edge_threshold < 16 || P->edge_threshold > 256 || P->first_level != 0 || P->wta_k != 2 ||
+        P->edge_threshold < 19 || P->edge_threshold > 256 || P->first_level != 0 || P->wta_k != 2 ||
         P->score_type != 0 || P->patch_size != 31 || P->fast_threshold < 0) {
-        set_last_error("unsupported ORB parameters (edgeThreshold 16..256, firstLevel 0, WTA_K 2, HARRIS_SCORE, patchSize 31)");
+        // edgeThreshold >= 19: rBRIEF's rotated samples reach 18 pixels from a keypoint, so from 19 on they stay
+        // inside the level, where the blurred level is defined the same way in OpenCV (its bordered pyramid)
+        // and here; below, OpenCV reads the blurred reflected border, which this pipeline does not build
+        set_last_error("unsupported ORB parameters (edgeThreshold 19..256, firstLevel 0, WTA_K 2, HARRIS_SCORE, patchSize 31)");
         return SFMX_EINVAL;
     }
     int ndev = 0;

@@ -63,9 +63,9 @@ def test_large_photo_and_parameters():
     assert len(k) > 1000
     _check(img, nfeatures=3000, scaleFactor=1.5, nlevels=5, fastThreshold=12, edgeThreshold=40)
     # r04 kernels' edge regimes: the resize's staged source span at its limit (scale 2) and past it
-    # (2.6: the per-pixel form), the smallest edge threshold (rBRIEF windows that need the edge clamp)
-    _check(img, nfeatures=2000, scaleFactor=2.0, nlevels=4, edgeThreshold=16)
-    _check(img, nfeatures=1000, scaleFactor=2.6, nlevels=3, edgeThreshold=16, fastThreshold=8)
+    # (2.6: the per-pixel form), the smallest edge threshold (rBRIEF windows touching the level's edge)
+    _check(img, nfeatures=2000, scaleFactor=2.0, nlevels=4, edgeThreshold=19)
+    _check(img, nfeatures=1000, scaleFactor=2.6, nlevels=3, edgeThreshold=19, fastThreshold=8)
 
 
 def test_degenerate_inputs():
@@ -75,6 +75,8 @@ def test_degenerate_inputs():
     assert len(_check(np.full((100, 100), 7, np.uint8))[0]) == 0     # no corners
     with pytest.raises(ValueError):                                  # SFMX_EINVAL
         sfmx.features.ORB.create(100, WTA_K=3).detectAndCompute(np.zeros((64, 64), np.uint8))
+    with pytest.raises(ValueError):   # rBRIEF samples would leave the level (OpenCV reads its bordered pyramid)
+        sfmx.features.ORB.create(100, edgeThreshold=18).detectAndCompute(np.zeros((64, 64), np.uint8))
 
 
 def test_device_and_batch_modes_match():
