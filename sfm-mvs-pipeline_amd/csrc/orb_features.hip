@@ -476,7 +476,6 @@ void orb_rows_kernel(const uint8_t* __restrict__ score, const Lvl* __restrict__ 
 //  * the bidirectional std::partition (pred = response >= the boundary response) the same way.
 // Positions are found by per-thread contiguous chunks and one block scan; Ls / Rs live in scratch.
 struct Resp { float response; int32_t idx; };
-struct KRec { float response; int32_t pos, out, pad; };   // a kept keypoint: response, packed position, output index
 constexpr int RT = 1024;                      // threads of a selection workgroup
 struct SelCounts { int n[MAX_LEVELS]; };      // the retainBest argument per level
 
@@ -784,14 +783,14 @@ __device__ float fast_atan2(float y, float x) {   // cv::fastAtan2
 __global__ __launch_bounds__(256)
 void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int nl,
                       const int* __restrict__ row_off, int rows, int* __restrict__ stats, const int* __restrict__ umax,
-                      const KRec* __restrict__ kord, Kp* __restrict__ out, int64_t istride) {
+                      const Resp* __restrict__ kin, Kp* __restrict__ out, int64_t istride) {
     const int lane = threadIdx.x & 63;
     {
         const int64_t bo = (int64_t)blockIdx.y * istride;
         pyr = at(pyr, bo);
         row_off = at(row_off, bo);
         stats += (int64_t)blockIdx.y * CS;
-        kord = at(kord, bo);
+        kin = at(kin, bo);
         out = at(out, bo);
     }
     __shared__ int sumax[HALF_PATCH + 1], lbase[MAX_LEVELS + 1], lfirst[MAX_LEVELS];
@@ -831,8 +830,8 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         int l = 0;
         while (f >= lbase[l + 1]) ++l;
         const Lvl L = lv[l];
-        const KRec e = kord[lfirst[l] + f - lbase[l]];   // (response, packed position, output index), band order
-        const int pos = e.pos, cx = pos & 0xFFFF, cy = pos >> 16;
+        const Resp e = kin[lfirst[l] + f - lbase[l]];   // (response, packed position)
+        const int pos = e.idx, cx = pos & 0xFFFF, cy = pos >> 16;
         const uint8_t* img = pyr + L.off;
         const int step = L.pitch;
         // the 31 patch rows as aligned 4-byte words (columns (cx-15) & ~3 ..); a pixel counts where
@@ -868,7 +867,7 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
             q.response = e.response;
             q.octave = l;
             q.class_id = -1;
-            out[lbase[l] + e.out] = q;
+            out[f] = q;
         }
     }
 }
@@ -882,8 +881,8 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
 __global__ __launch_bounds__(RT)
 void orb_keep_kernel(const Lvl* __restrict__ lv, const int* __restrict__ row_off, const Resp* __restrict__ A,
                      const Resp* __restrict__ B, int* __restrict__ stats, const int32_t* __restrict__ cpos, int width,
-                     int height, int border, Resp* __restrict__ kin, KRec* __restrict__ kord, int64_t istride) {
-    __shared__ int sh[36], band[RT];
+                     int height, int border, Resp* __restrict__ kin, int64_t istride) {
+    __shared__ int sh[36];
     const int l = blockIdx.x, t = threadIdx.x;
     {
         const int64_t bo = (int64_t)blockIdx.y * istride;
@@ -893,12 +892,10 @@ void orb_keep_kernel(const Lvl* __restrict__ lv, const int* __restrict__ row_off
         stats += (int64_t)blockIdx.y * CS;
         cpos = at(cpos, bo);
         kin = at(kin, bo);
-        kord = at(kord, bo);
     }
     const Lvl L = lv[l];
     const int c0 = lvl_first(row_off, L), m = stats[ST_CNT2 + l];
     const bool fits = height > 2 * border && width > 2 * border;
-    band[t] = 0;
     int base = 0;
     for (int r0 = 0; r0 < m; r0 += RT) {   // (block-uniform)
         const int j = r0 + t;
@@ -913,26 +910,10 @@ void orb_keep_kernel(const Lvl* __restrict__ lv, const int* __restrict__ row_off
         }
         int pre = k, dummy = 0;
         scan2(pre, dummy, sh);   // exclusive prefix over the round; its total in sh[32]
-        if (k) {
-            kin[c0 + base + pre] = Resp{resp, pos};   // the level's kept keypoints, dense, in order
-            atomicAdd(&band[min((pos >> 16) >> 4, RT - 1)], 1);
-        }
+        if (k) kin[c0 + base + pre] = Resp{resp, pos};   // the level's kept keypoints, dense, in order
         base += sh[32];
     }
     if (t == 0) stats[ST_KCNT + l] = base;
-    // r04: the same keypoints in 16-row bands (kord: counting sort on y / 16, any order inside a band)
-    // for the angle and rBRIEF kernels' walks, whose patch reads then stay in the L2s; each record keeps
-    // its output index, so the outputs are the retain order's.  (A walk in retain order -- nth_element's
-    // permutation -- read its patches from all over the level: 3.5x the algorithmic bytes, PMC r04j.)
-    int cnt = band[t], dummy = 0;
-    scan2(cnt, dummy, sh);   // exclusive prefix over the bands (syncs first: every count is in)
-    band[t] = cnt;
-    __syncthreads();
-    for (int i = t; i < base; i += RT) {
-        const Resp e = kin[c0 + i];
-        const int slot = atomicAdd(&band[min((e.idx >> 16) >> 4, RT - 1)], 1);
-        kord[c0 + slot] = KRec{e.response, e.idx, i, 0};
-    }
 }
 
 __global__ __launch_bounds__(256)
@@ -1065,30 +1046,15 @@ __device__ void orb_sincos(double x, double* s, double* c) {
 constexpr int BW = 18;                 // window half-size
 constexpr int BWR = 2 * BW + 1, BWC = 80;   // (80-byte rows: 20 banks apart, not 16 -- fewer conflicts)
 __global__ __launch_bounds__(256)
-void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ lv, int nl, const int* __restrict__ row_off,
-                      const Kp* __restrict__ kps, const int* __restrict__ stats, const KRec* __restrict__ kord,
-                      const ImgIO* __restrict__ io, int64_t istride) {
+void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ lv, const Kp* __restrict__ kps,
+                      const int* __restrict__ st, const ImgIO* __restrict__ io, int64_t istride) {
     __shared__ __align__(16) uint8_t win[8][BWR * BWC];
-    __shared__ int lbase[MAX_LEVELS + 1], lfirst[MAX_LEVELS];
     const int g = blockIdx.y;
     blur = at(blur, (int64_t)g * istride);
     kps = at(kps, (int64_t)g * istride);
-    row_off = at(row_off, (int64_t)g * istride);
-    kord = at(kord, (int64_t)g * istride);
-    stats += (int64_t)g * CS;
     uint8_t* desc = io[g].desc_out;
     if (!desc) return;   // this image's caller passed no descriptor buffer
-    if (threadIdx.x == 0) {   // the kept keypoints' level offsets (orb_keep_kernel's band-ordered records)
-        int b = 0;
-        for (int l = 0; l < nl; ++l) {
-            lbase[l] = b;
-            lfirst[l] = lvl_first(row_off, lv[l]);
-            b += stats[ST_KCNT + l];
-        }
-        lbase[nl] = b;
-    }
-    __syncthreads();
-    const int n = min(stats[ST_TAIL], io[g].capacity), total = lbase[nl], i = threadIdx.x & 31, slot = threadIdx.x >> 5;
+    const int n = min(st[(int64_t)g * CS], io[g].capacity), i = threadIdx.x & 31, slot = threadIdx.x >> 5;
     uint8_t* wn = win[slot];
     float pxf[16], pyf[16];
 #pragma unroll
@@ -1096,11 +1062,7 @@ void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ 
         pxf[e] = (float)c_pattern[2 * (16 * i + e)];
         pyf[e] = (float)c_pattern[2 * (16 * i + e) + 1];
     }
-    for (int f = blockIdx.x * 8 + slot; f < total; f += gridDim.x * 8) {   // band order: nearby windows together
-        int l = 0;
-        while (f >= lbase[l + 1]) ++l;
-        const int j = lbase[l] + kord[lfirst[l] + f - lbase[l]].out;
-        if (j >= n) continue;   // (past the caller's capacity)
+    for (int j = blockIdx.x * 8 + slot; j < n; j += gridDim.x * 8) {
         const Kp k = kps[j];
         const Lvl L = lv[k.octave];
         float angle = k.angle;
@@ -1399,8 +1361,7 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
         auto r = [](size_t b) { return (b + 255) & ~(size_t)255; };
         const int mw = (maxw + 255) / 256 * 4;   // keep words per row (64 pixels each; a multiple of 4)
         const size_t blk = 3 * r(px) + r(CAND_CAP * 4) + r(CAND_CAP) + 2 * r(CAND_CAP * sizeof(Resp)) + 2 * r(CAND_CAP * 4) +
-                           r(CAND_CAP * sizeof(Kp)) + r(CAND_CAP * sizeof(Resp)) + r(CAND_CAP * sizeof(KRec)) +
-                           r((size_t)(rows + 1) * 4) +
+                           r(CAND_CAP * sizeof(Kp)) + r(CAND_CAP * sizeof(Resp)) + r((size_t)(rows + 1) * 4) +
                            r((size_t)rows * mw * 8) + r((size_t)rows * mw) +
                            (inputs_on_device ? 0 : r((size_t)width * height) + r((size_t)std::max(capmax, 1) * 32));
         const size_t shared_b = r(std::max<size_t>(tables.size(), 1) * sizeof(AxisEnt)) + r(sizeof(Lvl) * nl) +
@@ -1425,7 +1386,6 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             int* sRs = A.take<int>(CAND_CAP);
             Kp* dfin = A.take<Kp>(CAND_CAP);
             Resp* kin = A.take<Resp>(CAND_CAP);
-            KRec* kord = A.take<KRec>(CAND_CAP);
             int* row_off = A.take<int>(rows + 1);
             uint64_t* kmask = A.take<uint64_t>((size_t)rows * mw);
             uint8_t* wcnt = A.take<uint8_t>((size_t)rows * mw);
@@ -1489,15 +1449,15 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             orb_retain_kernel<<<dim3(nl, gz), RT, 0, st>>>(1, dlv, row_off, cscore, rA, rB, sLs, sRs, cnt1, cnt2, s2,
                                                            (int)CAND_CAP, sst + 3, istride);
             orb_keep_kernel<<<dim3(nl, gz), RT, 0, st>>>(dlv, row_off, rA, rB, stats, cpos, width, height, border, kin,
-                                                         kord, istride);
-            orb_angle_kernel<<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rows, stats, dumax, kord,
+                                                         istride);
+            orb_angle_kernel<<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rows, stats, dumax, kin,
                                                                           dfin, istride);
             // ---- compute(): blur of the levels used, rBRIEF of min(count, capacity) keypoints
             if (descriptors && capmax > 0) {
                 orb_blur_kernel<<<dim3(flat_tiles<BT_X, BT_Y>(lv), gz), 256, 0, st>>>(
                     pyr, dlv, sst, blur, nl, istride);
-                orb_brief_kernel<<<dim3(std::min(G > 1 ? 1024 : 4096, (capmax + 7) / 8), gz), 256, 0, st>>>(
-                    blur, dlv, nl, row_off, dfin, stats, kord, dio, istride);
+                orb_brief_kernel<<<dim3(std::min(G > 1 ? 1024 : 4096, (capmax + 7) / 8), gz), 256, 0, st>>>(blur, dlv, dfin,
+                                                                                                          sst, dio, istride);
             }
             if (inputs_on_device && capmax > 0)
                 orb_copy_kp_kernel<<<dim3(std::min(1024, (capmax + 255) / 256), gz), 256, 0, st>>>(dfin, sst, dio, istride);
