@@ -2116,6 +2116,7 @@ int sfmx_ba_set_allreduce(sfmx_ba_ctx* c, sfmx_allreduce_fn fn, void* user) {
     if (!c) return fail(SFMX_EINVAL, "null context");
     c->ar = fn;
     c->ar_user = user;
+    c->planned = false;   // the plan needs the co-visibility of every rank (a one-rank load planned on its own)
     return SFMX_OK;
 }
 

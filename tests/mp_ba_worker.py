@@ -20,6 +20,8 @@ def main():
     from sfmx.dist import shard_ba_problem, torch_allreduce
     if len(sys.argv) > 4 and sys.argv[4] == "multi":   # several cameras: every rank must derive the same border
         p = synth.ba_problem_multi(int(sys.argv[1]), int(sys.argv[2]), cameras=((1, 1.0), (3, 1.1)), seed=int(sys.argv[3]))
+    elif len(sys.argv) > 4 and sys.argv[4] == "ring":   # SfM point order: the shards see different camera pairs
+        p = synth.ba_sfm_order(synth.ba_problem(int(sys.argv[1]), int(sys.argv[2]), seed=int(sys.argv[3])))
     else:
         p = synth.ba_problem(int(sys.argv[1]), int(sys.argv[2]), seed=int(sys.argv[3]))
     local = shard_ba_problem(p, rank, world)

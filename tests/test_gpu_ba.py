@@ -88,24 +88,32 @@ def test_do_bundle_adjustment_mirror():
     assert not np.array_equal(before, P.points)                  # written back in place
 
 
-@pytest.mark.parametrize("kind", ["single", "multi"])
+@pytest.mark.parametrize("kind", ["single", "multi", "ring"])
 def test_point_sharded_two_ranks_match_single(kind):
     """Point-sharded BA over 2 ranks (both on this GPU, gloo all-reduce of the
     reduced camera system) reaches the 1-rank final cost within 1e-5.  "multi": two camera
-    models (every rank derives the same intrinsics border from the replicated poses)."""
+    models (every rank derives the same intrinsics border from the replicated poses).
+    "ring": a 40-camera ring in SfM point order, so the two shards see different camera pairs -- the
+    plan must come from the all-reduced co-visibility (r04: a one-rank load plans on its own, and
+    setting the all-reduce callback afterwards must drop that plan)."""
     import json, os, subprocess, sys
     here = os.path.dirname(os.path.abspath(__file__))
-    args = ["10", "1200", "27"] if kind == "single" else ["12", "1400", "46", "multi"]
+    args = {"single": ["10", "1200", "27"], "multi": ["12", "1400", "46", "multi"], "ring": ["40", "4000", "7", "ring"]}[kind]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    port = 29531 + ["single", "multi", "ring"].index(kind)
     out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                          "--master-addr=127.0.0.1", f"--master-port={29531 + (kind == 'multi')}", os.path.join(here, "mp_ba_worker.py"), *args],
+                          "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(here, "mp_ba_worker.py"), *args],
                          capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
     r = json.loads(line)
     assert r["cameras_identical"]
-    p = synth.ba_problem(int(args[0]), int(args[1]), seed=int(args[2])) if kind == "single" else \
-        synth.ba_problem_multi(int(args[0]), int(args[1]), cameras=((1, 1.0), (3, 1.1)), seed=int(args[2]))
+    if kind == "single":
+        p = synth.ba_problem(int(args[0]), int(args[1]), seed=int(args[2]))
+    elif kind == "multi":
+        p = synth.ba_problem_multi(int(args[0]), int(args[1]), cameras=((1, 1.0), (3, 1.1)), seed=int(args[2]))
+    else:
+        p = synth.ba_sfm_order(synth.ba_problem(int(args[0]), int(args[1]), seed=int(args[2])))
     P, sm, _ = gpu_solve(p)
     assert abs(r["initial_cost"] - sm["initial_cost"]) <= 1e-12 * sm["initial_cost"]
     assert abs(r["final_cost"] - sm["final_cost"]) <= COST_RTOL * sm["final_cost"]
