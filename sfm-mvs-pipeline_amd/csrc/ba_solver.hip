@@ -1786,6 +1786,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     auto bail = [](int rc) { return rc; };
     // per-problem state starts over
     c->scaled = c->j_scaled = false;
+    HIPCHK(hipStreamSynchronize(c->st));   // (a failed earlier load may have left copies from the arena in flight)
     c->stage_off = 0;
     c->P = P; c->C = C; c->O = O;
     c->K = K; c->intr_len = L.intr_len; c->multi = L.multi; c->cx = L.cx; c->cy = L.cy;
@@ -1960,7 +1961,10 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     c->setup_ms[2] = up_ms + ms_since(t_up2);
     c->setup_ms[3] = 0.0;
     c->setup_ms[4] = ms_since(t_start);
-    if (plan_now && (rc = ensure_plan(c))) return bail(rc);   // (adds its time to setup_ms[3] / [4])
+    if (plan_now && (rc = ensure_plan(c))) {   // (adds its time to setup_ms[3] / [4])
+        (void)hipStreamSynchronize(st);         // the copies from the staging arena end before it is reused
+        return bail(rc);
+    }
     HIPCHK(hipStreamSynchronize(st));   // (an unchanged plan returns at once: the copies end here)
     for (Bucket& B : hs.bk) { B.io0 = B.io0_new; B.dirty = false; }
     hs.valid = true;
