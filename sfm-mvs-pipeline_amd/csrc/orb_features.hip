@@ -1492,6 +1492,7 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             *last_ms = ms;
         }
     done:;
+        if (rc != SFMX_OK) (void)hipStreamSynchronize(st);   // nothing of this chunk in flight from the pinned staging
     }
     if (prev >= 0) (void)hipSetDevice(prev);
     return rc;
