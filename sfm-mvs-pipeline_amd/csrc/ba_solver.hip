@@ -108,8 +108,8 @@ struct sfmx_ba_ctx {
     Buf obs_point, obs_cam, obs_xy, pt_start, grp, chk, bat, gcam, obs_lc, obs_row, lcrow, tasks, ents, cref_start, cref;
     Buf obs_xy_b, obs_cam_b, obs_lc_b, obs_row_b, moves;   // the next layout's observation arrays; relayout moves
     int64_t setup_up_obs = 0;    // observations the last load uploaded (the rest moved on the device)
-    // factorization plan of the reduced camera system (built at the first run, from the camera
-    // co-visibility of every rank: the layout of S must be the same on all of them)
+    // factorization plan of the reduced camera system (one rank: built during the load; sharded: at the
+    // first run, from the camera co-visibility of every rank -- the layout of S must be the same on all)
     std::vector<char> adj;       // local camera co-visibility, C x C
     bool planned = false;
     sfmx::ba::FactorPlan plan;
@@ -546,8 +546,9 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     return SFMX_OK;
 }
 
-// The factorization plan, once per context (at the first run, when the all-reduce callback is
-// known): the camera co-visibility summed over ranks (every rank builds the same plan), the
+// The factorization plan, rebuilt when the co-visibility changes (one rank: during the load, beside its
+// copies; sharded: at the first run, when the collectives are known -- setting them drops a plan): the
+// camera co-visibility summed over ranks (every rank builds the same plan), the
 // ordering and level schedule (SFMX_BA_ORDER: auto | natural | nd | nd1 | nd2 | nd4), the device
 // copies of the schedule, and S / W / the Schur terms sized by it.
 int ensure_plan(sfmx_ba_ctx* c) {
