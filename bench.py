@@ -54,7 +54,7 @@ FP64_PEAK_TFLOPS = 256 * 128 * 2.4e9 / 1e12
 # Cholesky ~0.58 GFLOP; bytes: obs read twice, points, S written and read
 BA_FLOP_PER_ITER_C5, BA_BYTES_PER_ITER_C5 = 3.0e9, 0.1e9
 FEAT_PMC_FILE = "r04n_pmc_features.json"   # tools/pmc_feat.sh -> tools/pmc_feat_json.py (r04n session)
-BA_PMC_FILE = "r04j_pmc_ba.json"   # tools/pmc_ba.sh -> tools/pmc_ba_json.py (r04j session)
+BA_PMC_FILE = "r04r_pmc_ba.json"   # tools/pmc_ba.sh -> tools/pmc_ba_json.py (r04r session)
 
 
 def parse():

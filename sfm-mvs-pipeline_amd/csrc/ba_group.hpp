@@ -727,6 +727,10 @@ void ba_add_cam(int P, int C, int npad, const int* __restrict__ camrow, const in
 // holds every partial field (see ncp): D[u][w] = Jc^T Jc, D[u][6 + i] = Jc^T Ji, D[u][6 + K] =
 // Jc^T r, D[6 + i][6 + l] = Ji^T Ji, D[6 + i][6 + K] = Ji^T r.
 __host__ __device__ constexpr int nfeat(int K) { return 7 + K; }
+// jer's row stride: 80 B keeps the 16-B alignment of the b128 reads and writes and moves a row 20
+// banks on (64 B put every lane of a 16-lane read group on 4 bank sets: 12M conflict cycles, r04 PMC);
+// K = 7 keeps 64 B: its 14 feature columns leave no room for two padded workgroups in 160 KiB
+__host__ __device__ constexpr int jers(int K) { return K < 7 ? 10 : 8; }
 template <int K>
 __device__ __forceinline__ int field_of(int r, int c) {   // Gram entry (r <= c) -> partial field, -1: none
     if (r < 6) {
@@ -758,7 +762,7 @@ __device__ __forceinline__ void point_eg(const double* __restrict__ jer, int a0,
 #pragma unroll
     for (int i = 0; i < 9; ++i) pr[i] = 0.0;
     for (int b = a0; b < a1; ++b) {
-        const double* r = jer + b * 8;
+        const double* r = jer + b * jers(K);
         int e = 0;
 #pragma unroll
         for (int u = 0; u < 3; ++u)
@@ -799,7 +803,7 @@ __device__ __forceinline__ void point_v(const double* __restrict__ jer, const do
 #pragma unroll
     for (int i = 0; i < 3 * K; ++i) v[i] = 0.0;
     for (int b = a0; b < a1; ++b) {
-        const double* r = jer + b * 8;
+        const double* r = jer + b * jers(K);
         const double* g0 = G + orw[b] * NF;
 #pragma unroll
         for (int u = 0; u < 3; ++u)
@@ -879,8 +883,8 @@ __device__ __forceinline__ void point_step(int p, double (&y)[3], const double* 
 // host-built layout); and the group's cost, sum xp^2 (its points) and max |grad| partials.  Big
 // groups: feature rows in observation order, a scalar per-(camera, field) loop, the point sums by
 // thread 0 across the chunks.
-// Dynamic LDS: G[max rows][NF] | jer[GCH][8] (je | r) | olc[GCH] | orw[GCH] (short: camera slot,
-// feature row of the observation).
+// Dynamic LDS: G[max rows][NF] | jer[GCH][jers(K)] (je | r, padded) | olc[GCH] | orw[GCH]
+// (short: camera slot, feature row of the observation).
 constexpr int GROWS = 2 * GCH + 3 * UMAX;   // feature rows of a chunk incl. per-camera padding
 // the point sums of E | g | V over observations b in [a0, a1) of a chunk: Je and r from jer, Ji from
 // the observation's feature rows (unscaled)
@@ -889,7 +893,7 @@ __device__ __forceinline__ void point_sums(const double* __restrict__ jer, const
                                            const short* __restrict__ orw, int a0, int a1, double (&pr)[npr(K)]) {
     constexpr int NF = nfeat(K);
     for (int b = a0; b < a1; ++b) {
-        const double* r = jer + b * 8;
+        const double* r = jer + b * jers(K);
         const double* g0 = G + orw[b] * NF;
         int e = 0;
 #pragma unroll
@@ -946,8 +950,8 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
     constexpr int JS = jst(K), NCP = ncp(K), N = 9 + K, NF = nfeat(K), NPR = npr(K);
     __shared__ double sh[8];
     double* G = gl;                                    // [GROWS][NF]
-    double* jer = G + GROWS * NF;                      // [GCH][8]
-    short* olc = reinterpret_cast<short*>(jer + GCH * 8);
+    double* jer = G + GROWS * NF;                      // [GCH][jers(K)]
+    short* olc = reinterpret_cast<short*>(jer + GCH * jers(K));
     short* orw = olc + GCH;
     const Grp Gp = grp[blockIdx.x];
     // w through readfirstlane: the per-camera row ranges (lcrow of camera w + 4i) become scalar, so
@@ -1046,9 +1050,9 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
                 for (int i = 0; i < 6; ++i) sv[3 + i] = sc[i];
             }
 #pragma unroll
-            for (int i = 0; i < 6; ++i) jer[a * 8 + i] = rec[2 + i];
-            jer[a * 8 + 6] = rec[0];
-            jer[a * 8 + 7] = rec[1];
+            for (int i = 0; i < 6; ++i) jer[a * jers(K) + i] = rec[2 + i];
+            jer[a * jers(K) + 6] = rec[0];
+            jer[a * jers(K) + 7] = rec[1];
             const int row = orow;
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
