@@ -886,6 +886,12 @@ __device__ __forceinline__ void point_step(int p, double (&y)[3], const double* 
 // Dynamic LDS: G[max rows][NF] | jer[GCH][jers(K)] (je | r, padded) | olc[GCH] | orw[GCH]
 // (short: camera slot, feature row of the observation).
 constexpr int GROWS = 2 * GCH + 3 * UMAX;   // feature rows of a chunk incl. per-camera padding
+// ba_glin's dynamic LDS (bytes) and the two workgroups per CU its launch bounds and group sizing assume
+__host__ __device__ constexpr size_t glin_lds(int K) {
+    return sizeof(double) * ((size_t)GROWS * nfeat(K) + (size_t)GCH * jers(K)) + sizeof(short) * 2 * GCH;
+}
+static_assert(2 * glin_lds(1) <= 160 * 1024 && 2 * glin_lds(3) <= 160 * 1024 && 2 * glin_lds(7) <= 160 * 1024,
+              "two ba_glin workgroups per CU");
 // the point sums of E | g | V over observations b in [a0, a1) of a chunk: Je and r from jer, Ji from
 // the observation's feature rows (unscaled)
 template <int K>

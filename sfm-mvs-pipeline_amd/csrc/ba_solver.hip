@@ -1686,7 +1686,7 @@ int group_slots(sfmx_ba_ctx* c, int K) {
     if (const char* e = SFMX_DIAG_ENV("SFMX_BA_SLOTS")) return std::atoi(e);   // A/B: 0 = full-size groups
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) return 0;
-    const size_t lds = sizeof(double) * ((size_t)GROWS * nfeat(K) + GCH * jers(K)) + sizeof(short) * 2 * GCH;
+    const size_t lds = glin_lds(K);
     const void* f = K == 1 ? (const void*)ba_glin<1, false> : K == 3 ? (const void*)ba_glin<3, false> : (const void*)ba_glin<7, false>;
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     int nb = 0;
@@ -1831,7 +1831,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
                        std::max<size_t>({4 * wreg + 2 * nb_max, (size_t)tp.dp_max * (tp.dp_max + 1) + tp.dp_max, 16});
         c->gs_nt = std::min(4, std::max(1, tp.dp_max / 16));
     }
-    c->lds_lin = sizeof(double) * ((size_t)GROWS * nfeat(K) + GCH * jers(K)) + sizeof(short) * 2 * GCH;
+    c->lds_lin = glin_lds(K);
     {
         hipError_t e = hipSuccess;
 #define LDSATTR(KK)                                                                                                  \
