@@ -434,6 +434,8 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
     return SFMX_OK;
 }
 
+constexpr unsigned GUPDATE_LDS = 33 * 1024;   // + 6.1 KB static: 4 x 39 KB fit 160 KiB, 5 do not
+
 // One LM step at `radius`: Schur solve of (J_s^T J_s + D^2) sol = J_s^T r, step_s = -sol,
 // candidate = x + step_s * scale, its cost, Jacobian and scalars (speculative linearization).
 // spec: speculative mode (the device LM state supplies the radius; ba_decide judges the step and
@@ -490,7 +492,9 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     RC(solve_reduced<RW>(c, sol + c->ne));
     if (c->phases) HIPCHK(hipEventRecord(c->ev[2], c->st));
     // the point update, and in workgroups past the groups the candidate cameras / intrinsics
-    hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups + nblk(c->nf)), dim3(256), 0, c->st, c->grp.as<Grp>(),
+    // An unused dynamic LDS request of GUPDATE_LDS holds it at 4 workgroups (4 waves per SIMD) per CU:
+    // 52.8 us against 57-58 at the 5 its VGPRs allow, 64 at 6 and 61 at 3 (r04u..y)
+    hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups + nblk(c->nf)), dim3(256), GUPDATE_LDS, c->st, c->grp.as<Grp>(),
                        c->chk.as<Chunk>(), c->obs_cam.as<int>(), c->pt_start.as<int>(), c->Wr.as<double>(),
                        c->PR.as<double>(), c->scale.as<double>(), c->plt.as<double>(), sol + c->ne, c->P, C,
                        c->x.as<double>(), c->cand.as<double>(), c->gpl.as<double>(), gate(c), c->ngroups, (int)c->nf);
