@@ -75,6 +75,11 @@ typedef struct sfmx_ba_options {     /* defaults = CeresUtils::defaultOptions + 
     double min_lm_diagonal;                  /* 1e-6  */
     double max_lm_diagonal;                  /* 1e32  */
     double min_relative_decrease;            /* 1e-3  */
+    /* sfmx only (no Ceres counterpart; 0 = automatic): at most this many points per point group of
+     * the Schur kernels (1 .. 128).  Automatic sizing fills the device's workgroup slots; a small cap
+     * gives many tiny groups (tests of that regime run on the product library). */
+    int32_t max_group_points;
+    int32_t _reserved_opt;
 } sfmx_ba_options;
 
 typedef struct sfmx_ba_summary {

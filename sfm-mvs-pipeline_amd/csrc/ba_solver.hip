@@ -1778,6 +1778,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
     c->loaded = false;
     const int slots = group_slots(c, K);
     int gpts = group_points(P, slots);
+    if (c->opt.max_group_points > 0) gpts = std::min(gpts, std::min(GPTS, (int)c->opt.max_group_points));
 #ifdef SFMX_DIAG
     if (const char* e = SFMX_DIAG_ENV("SFMX_BA_GPTS")) gpts = std::max(1, std::min(GPTS, std::atoi(e)));   // tiny-group tests
     const bool force_fresh = SFMX_DIAG_ENV("SFMX_BA_FRESH") != nullptr;   // A/B: every load rebuilds every bucket
@@ -2087,6 +2088,8 @@ int sfmx_ba_default_options(sfmx_ba_options* o) {
     o->min_lm_diagonal = 1e-6;
     o->max_lm_diagonal = 1e32;
     o->min_relative_decrease = 1e-3;
+    o->max_group_points = 0;
+    o->_reserved_opt = 0;
     return SFMX_OK;
 }
 

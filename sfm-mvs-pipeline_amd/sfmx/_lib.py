@@ -53,7 +53,7 @@ class sfmx_ba_options(C.Structure):
                 ("parameter_tolerance", C.c_double), ("initial_trust_region_radius", C.c_double),
                 ("max_trust_region_radius", C.c_double), ("min_trust_region_radius", C.c_double),
                 ("min_lm_diagonal", C.c_double), ("max_lm_diagonal", C.c_double),
-                ("min_relative_decrease", C.c_double)]
+                ("min_relative_decrease", C.c_double), ("max_group_points", C.c_int32), ("_reserved_opt", C.c_int32)]
 
 
 class sfmx_ba_plan_info(C.Structure):

@@ -5,6 +5,7 @@ libm) within 1e-9 relative."""
 import numpy as np
 import pytest
 
+import sfmx
 from sfmx import ba, synth
 from diag import diagnostic
 
@@ -374,30 +375,41 @@ def test_refused_update_leaves_the_loaded_problem_intact():
 
 
 def test_tiny_point_groups_after_differently_sized_solves():
-    """the regime of the r03 launch failure (point groups of 1-3 points, the
-    first solve of test_solve_matches_oracle[1]) placed after solves of other sizes, models and
-    camera counts in one process, so every cached buffer is reused or regrown first.  The
-    diagnostic library forces the group size (SFMX_BA_GPTS) and checks every topology it uploads
-    (check_topology); each result must match the oracle as test_solve_matches_oracle does, and the
-    product library (its own group sizing) must give the same LM decisions."""
+    """the regime of the r03 launch failure (point groups of 1-3
+    points, the first solve of test_solve_matches_oracle[1]) placed after solves of other sizes,
+    models and camera counts in one process, so every cached buffer is reused or regrown first.
+    The PRODUCT library (libsfmx.so) forms the tiny groups through sfmx_ba_options.max_group_points
+    (the build that faulted in r03 was a product build); the diagnostic library then repeats the
+    regime with check_topology on every upload.  Each result must match the oracle as
+    test_solve_matches_oracle does, with the automatic sizing's LM decisions."""
     from oracle import oracle
+    assert ba.lib is sfmx._lib.lib and "libsfmx.so" in ba.lib._name
     warm = [synth.ba_problem(200, 20000, seed=70), synth.ba_problem(12, 900, seed=71, cam_model=7),
             synth.ba_problem_multi(16, 1500, cameras=((1, 1.0), (3, 1.1)), seed=72)]
     target = synth.ba_problem(10, 1000, seed=22, cam_model=1)
     _, osm, otr = oracle.ba_solve(target, trace_cap=512)
     for w in warm:
         gpu_solve(w)
-    _, sp, tp_ = gpu_solve(target)                # product library after the warm-up
-    for gpts in ("2", "1", "3", "2"):
+    _, sp, tp_ = gpu_solve(target)                # automatic group sizing after the warm-up
+
+    def check(sm, tr, what):
+        assert sm["termination_type"] == osm["termination_type"], what
+        assert abs(sm["final_cost"] - osm["final_cost"]) <= COST_RTOL * osm["final_cost"], what
+        n = min(len(tr), len(otr))
+        assert np.array_equal(tr[:n, 2], otr[:n, 2]), what
+        assert np.array_equal(tr[:, 2], tp_[:, 2]) and abs(sm["final_cost"] - sp["final_cost"]) <= 1e-9 * sp["final_cost"]
+
+    for cap in (2, 1, 3, 2):                      # product library, tiny groups
+        for w in warm[:2]:
+            gpu_solve(w, max_num_iterations=3, max_group_points=cap + 5)
+        P, sm, tr = gpu_solve(target, max_group_points=cap)
+        check(sm, tr, f"product, {cap} points per group")
+    for gpts in ("2", "1", "3", "2"):             # diagnostic library: topology checked on every upload
         with diagnostic(SFMX_BA_GPTS=gpts):
             for w in warm[:2]:
                 gpu_solve(w, max_num_iterations=3)
             P, sm, tr = gpu_solve(target)
-        assert sm["termination_type"] == osm["termination_type"], gpts
-        assert abs(sm["final_cost"] - osm["final_cost"]) <= COST_RTOL * osm["final_cost"], gpts
-        n = min(len(tr), len(otr))
-        assert np.array_equal(tr[:n, 2], otr[:n, 2]), gpts
-        assert np.array_equal(tr[:, 2], tp_[:, 2]) and abs(sm["final_cost"] - sp["final_cost"]) <= 1e-9 * sp["final_cost"]
+        check(sm, tr, f"diagnostic, {gpts} points per group")
 
 
 def test_incremental_updates_keep_buckets_and_equal_fresh_contexts():
@@ -433,4 +445,6 @@ def test_incremental_updates_keep_buckets_and_equal_fresh_contexts():
     finally:
         if ctx is not None:
             ctx.close()
-    assert redone[1] < 6 and redone[2] < 6 and redone[4] <= 2, redone   # of 6 buckets (48 cameras / 8)
+    # 48 cameras in buckets of 4 (BUCKET_CAMS): 11-12 buckets; one new camera dirties the two buckets
+    # holding the points it adds observations to (sfmx_ba_debug_incremental_check on CPU: 2, 2)
+    assert redone[1] <= 2 and redone[2] <= 2 and redone[4] <= 2, redone
