@@ -729,10 +729,15 @@ def bench_ba_calls(args):
                 ctx = ba.BAContext(P)
             else:
                 ctx.update(P)
+            t1 = time.perf_counter()
             sm, _ = ctx.run()
+            t2 = time.perf_counter()
             ctx.get(P)
             wall = (time.perf_counter() - t0) * 1e3
             su = ctx.setup_ms()
+            su["update_call"] = (t1 - t0) * 1e3
+            su["run_call_minus_lm"] = (t2 - t1) * 1e3 - sm["total_ms"]
+            su["get"] = (time.perf_counter() - t2) * 1e3
             it = sm["num_successful_steps"] + sm["num_unsuccessful_steps"]
             calls.append({"cams": n, "points": len(P.points), "obs": len(P.obs_point), "ms": wall, "lm_ms": sm["total_ms"],
                           "setup_ms": su, "iterations": it, "setup_frac": (wall - sm["total_ms"]) / wall})

@@ -153,8 +153,11 @@ int sfmx_ba_update(sfmx_ba_ctx* ctx, const sfmx_ba_problem* problem);
 /* Host-side setup of the last create / update: [0] point ordering + groups (ms), [1] device
  * allocation (ms), [2] uploads (pinned staging, incl. the parameters; ms), [3] the
  * factorization plan (built at the next run; 0 when reused; ms), [4] total (ms), [5] the host
- * ordering / grouping pass alone (ms), [6] the number of camera buckets it redid.  n = entries
- * (up to 7). */
+ * ordering / grouping pass alone (ms), [6] the number of camera buckets it redid, [7] the problem's
+ * validation (ms), [8 .. 15] the phases of [5] (ms: point-major view, change detection, bucket
+ * lists, ordering + groups of the redone buckets, layout arrays, merge, assembly tasks, shadows),
+ * [16] the plan's host computation and [17] the load's final stream wait (ms).  n = entries
+ * (up to 18). */
 int sfmx_ba_setup_ms(sfmx_ba_ctx* ctx, double* ms, int32_t n);
 /* Copy the current parameters back into problem->points/poses/intr. */
 int sfmx_ba_get(sfmx_ba_ctx* ctx, sfmx_ba_problem* problem);

@@ -153,10 +153,13 @@ struct sfmx_ba_ctx {
     // it is reused), not pageable memory
     char* stage = nullptr;
     size_t stage_cap = 0, stage_off = 0;
-    // host-side setup of the last create / update: [0] ordering + topology, [1] device allocation,
-    // [2] uploads, [3] factorization plan, [4] total (ms)
-    // [5] ordering, [6] point groups / topology (the two parts of [0])
-    double setup_ms[7] = {0, 0, 0, 0, 0, 0, 0};
+    // host-side setup of the last create / update (include/sfmx_ba.h sfmx_ba_setup_ms): [0] ordering +
+    // topology, [1] device allocation, [2] uploads, [3] factorization plan, [4] total (ms), [5] the host
+    // ordering / grouping pass alone (ms), [6] buckets redone (a count), [7] validation (ms), [8 .. 15]
+    // host_setup's phases (HostScratch::tm), [16] the plan's host computation, [17] the load's final
+    // stream wait (ms)
+    static constexpr int SETUP_N = 18;
+    double setup_ms[SETUP_N] = {};
     std::vector<char> plan_adj;   // the co-visibility the current plan was built from (reused if equal)
     std::string plan_form;        // diagnostic library: the form switches the plan was built with
     int plan_K = 0;
@@ -592,6 +595,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
         mode = m == "natural" ? 0 : m == "nd" ? 1 : m == "nd1" ? 2 : m == "nd2" ? 3 : m == "nd4" ? 4 : -1;
     }
     sfmx::ba::FactorPlan& pl = c->plan;
+    const auto t_make = std::chrono::steady_clock::now();
     sfmx::ba::make_plan(C, adj, mode, pl);
     if (pl.npad > MAX_NPAD) sfmx::ba::make_plan(C, adj, 0, pl);   // padding past the back solve's LDS
     c->npad = pl.npad;
@@ -716,7 +720,10 @@ int ensure_plan(sfmx_ba_ctx* c) {
     if (RW == 2) BACKATTR(2); else if (RW == 4) BACKATTR(4); else BACKATTR(8);
 #undef BACKATTR
     if (e != hipSuccess) return fail(SFMX_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(e));
+    const auto t_wait = std::chrono::steady_clock::now();
+    c->setup_ms[16] = std::chrono::duration<double, std::milli>(t_wait - t_make).count();
     HIPCHK(hipStreamSynchronize(st));
+    c->setup_ms[17] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_wait).count();
     c->planned = true;
     c->plan_adj = c->adj;
     c->plan_K = c->K;
@@ -908,9 +915,15 @@ int validate(const sfmx_ba_problem* pb) {
     if ((pb->n_points && !pb->points) || (pb->n_cams && !pb->poses) || !pb->intr ||
         (pb->n_obs && (!pb->obs_point || !pb->obs_cam || !pb->obs_xy)))
         return fail(SFMX_EINVAL, "null problem array");
-    for (int o = 0; o < pb->n_obs; ++o)
-        if (pb->obs_point[o] < 0 || pb->obs_point[o] >= pb->n_points || pb->obs_cam[o] < 0 || pb->obs_cam[o] >= pb->n_cams)
-            return fail(SFMX_EINVAL, "observation index out of range");
+    std::atomic<bool> bad{false};   // O(observations) on every call: on the worker pool
+    sfmx::parallel_ranges(pb->n_obs, pb->n_obs >= 65536 ? 16 : 1, [&](int64_t o0, int64_t o1) {
+        const int P = pb->n_points, C = pb->n_cams;
+        bool b = false;
+        for (int64_t o = o0; o < o1; ++o)
+            b |= (unsigned)pb->obs_point[o] >= (unsigned)P || (unsigned)pb->obs_cam[o] >= (unsigned)C;
+        if (b) bad = true;
+    });
+    if (bad) return fail(SFMX_EINVAL, "observation index out of range");
     return SFMX_OK;
 }
 
@@ -1010,21 +1023,22 @@ int bucket_of(int minc) { return minc < 0 ? 0 : minc / BUCKET_CAMS; }
 // Stable LSD radix sort of (key, index) records on the key's low `bits` bits, 8 bits a pass, passes
 // whose digit is the same for every record skipped: the order std::sort gives (key, index) records
 // whose indices ascend on entry (r04: std::sort took ~80 ns per point of the ring-closing bucket).
-void radix_sort_keys(std::vector<std::pair<uint64_t, int>>& kp, int bits) {
-    const size_t n = kp.size();
+void radix_sort_keys(std::pair<uint64_t, int>* kp, size_t n, int bits) {
     if (n < 2) return;
     thread_local std::vector<std::pair<uint64_t, int>> tmp;
     tmp.resize(n);
+    std::pair<uint64_t, int>*src = kp, *dst = tmp.data();
     for (int sh = 0; sh < bits; sh += 8) {
-        size_t cnt[257] = {};
-        for (const auto& e : kp) cnt[((e.first >> sh) & 255) + 1]++;
+        uint32_t cnt[257] = {};
+        for (size_t i = 0; i < n; ++i) cnt[((src[i].first >> sh) & 255) + 1]++;
         bool one = false;
         for (int d = 1; d <= 256; ++d) if (cnt[d] == n) one = true;
         if (one) continue;
         for (int d = 0; d < 256; ++d) cnt[d + 1] += cnt[d];
-        for (const auto& e : kp) tmp[cnt[(e.first >> sh) & 255]++] = e;
-        kp.swap(tmp);
+        for (size_t i = 0; i < n; ++i) dst[cnt[(src[i].first >> sh) & 255]++] = src[i];
+        std::swap(src, dst);
     }
+    if (src != kp) std::copy(src, src + n, kp);
 }
 
 // Point groups, chunks, local cameras, assembly task lists and camera slot lists (see ba_group.hpp).
@@ -1067,18 +1081,22 @@ struct TopoSeg {
     void clear() { grp.clear(); chk.clear(); bat.clear(); gcam.clear(); lcrow.clear(); sg_total = h_total = 0; rg_total = 0; dp_max = 16; }
 };
 
-void topo_segment(int s0, int s1, int K, int gpts, const std::vector<int>& pt_start, const int* obs_cam, short* obs_lc,
-                  short* obs_row, TopoSeg& tp) {
-    std::vector<int> cur, pc, uni, cnt, fill;
+// (r05: the per-point sort / union on small stack arrays and the local-camera lookups through a
+// per-thread camera -> slot table instead of binary searches: the same groups, ~3x less host time)
+void topo_segment(int s0, int s1, int K, int gpts, int C, const std::vector<int>& pt_start, const int* obs_cam,
+                  short* obs_lc, short* obs_row, TopoSeg& tp) {
+    thread_local std::vector<int> lcm;   // camera -> its slot in the group being added (set before every use)
+    if ((int)lcm.size() < C) lcm.resize(C);
+    std::vector<int> bigc;               // a big point's cameras (any count)
+    int cur[UMAX + WB_OBS], uni[UMAX + WB_OBS], pc[WB_OBS];
+    int ncur = 0;
+    int cnt[UMAX], fill[UMAX];
     tp.clear();
     int g_p0 = s0, g_obs = 0;
-    auto lc_of = [](const std::vector<int>& cams, int cm) {
-        return (int)(std::lower_bound(cams.begin(), cams.end(), cm) - cams.begin());
-    };
-    auto add_group = [&](int p0, int p1, const std::vector<int>& cams, bool big) {
+    auto add_group = [&](int p0, int p1, const int* cams, int u, bool big) {
         Grp G{};
         G.o0 = pt_start[p0]; G.o1 = pt_start[p1]; G.p0 = p0; G.p1 = p1;
-        G.u = (int)cams.size();
+        G.u = u;
         G.cam_off = (int)tp.gcam.size();
         G.big = big ? 1 : 0;
         const int dim = 6 * G.u + K;
@@ -1088,6 +1106,7 @@ void topo_segment(int s0, int s1, int K, int gpts, const std::vector<int>& pt_st
         G.nch = 0;
         G.b0 = (int)tp.bat.size();
         G.nb = 0;
+        for (int i = 0; i < u; ++i) lcm[cams[i]] = i;
         if (big) {
             G.h_off = tp.h_total;
             tp.h_total += (long long)dim * 3;
@@ -1113,11 +1132,10 @@ void topo_segment(int s0, int s1, int K, int gpts, const std::vector<int>& pt_st
                 Chunk ch{pt_start[q], pt_start[q], q - p0, q - p0, (int)tp.lcrow.size(), 0, 0, 0};
                 while (q < p1 && pt_start[q + 1] - ch.o0 <= GCH) { ++q; }
                 ch.o1 = pt_start[q]; ch.q1 = q - p0;
-                cnt.assign(cams.size(), 0);
-                for (int o = ch.o0; o < ch.o1; ++o) cnt[lc_of(cams, obs_cam[o])]++;
-                fill.resize(cams.size());
+                for (int lc = 0; lc < u; ++lc) cnt[lc] = 0;
+                for (int o = ch.o0; o < ch.o1; ++o) cnt[lcm[obs_cam[o]]]++;
                 int row = 0;
-                for (size_t lc = 0; lc < cams.size(); ++lc) {
+                for (int lc = 0; lc < u; ++lc) {
                     tp.lcrow.push_back(row);
                     fill[lc] = row;
                     row += (2 * cnt[lc] + 3) & ~3;
@@ -1125,7 +1143,7 @@ void topo_segment(int s0, int s1, int K, int gpts, const std::vector<int>& pt_st
                 tp.lcrow.push_back(row);
                 ch.nrows = row;
                 for (int o = ch.o0; o < ch.o1; ++o) {
-                    const int lc = lc_of(cams, obs_cam[o]);
+                    const int lc = lcm[obs_cam[o]];
                     obs_row[o] = (short)fill[lc];
                     fill[lc] += 2;
                 }
@@ -1133,34 +1151,54 @@ void topo_segment(int s0, int s1, int K, int gpts, const std::vector<int>& pt_st
                 ++G.nch;
             }
         }
-        for (int cm : cams) tp.gcam.push_back(cm);
-        for (int o = G.o0; o < G.o1; ++o) obs_lc[o] = (short)lc_of(cams, obs_cam[o]);
+        tp.gcam.insert(tp.gcam.end(), cams, cams + u);
+        for (int o = G.o0; o < G.o1; ++o) obs_lc[o] = (short)lcm[obs_cam[o]];
         tp.grp.push_back(G);
     };
     for (int p = s0; p < s1; ++p) {
         const int m = pt_start[p + 1] - pt_start[p];
-        pc.assign(obs_cam + pt_start[p], obs_cam + pt_start[p + 1]);
-        std::sort(pc.begin(), pc.end());
-        const bool dup = std::adjacent_find(pc.begin(), pc.end()) != pc.end();
-        pc.erase(std::unique(pc.begin(), pc.end()), pc.end());
-        const bool big = m > WB_OBS || 6 * (int)pc.size() + K > GDPMAX || dup;
+        const int* oc = obs_cam + pt_start[p];
+        bool big = m > WB_OBS, dup = false;
+        int npc = 0;
+        if (!big) {   // insertion sort of the point's cameras, duplicates dropped (and noted)
+            for (int i = 0; i < m; ++i) {
+                const int c = oc[i];
+                int j = npc;
+                while (j > 0 && pc[j - 1] > c) --j;
+                if (j > 0 && pc[j - 1] == c) { dup = true; continue; }
+                for (int k = npc; k > j; --k) pc[k] = pc[k - 1];
+                pc[j] = c;
+                ++npc;
+            }
+            big = dup || 6 * npc + K > GDPMAX;
+        }
         if (big) {
-            if (p > g_p0) add_group(g_p0, p, cur, false);
-            add_group(p, p + 1, pc, true);
-            g_p0 = p + 1; g_obs = 0; cur.clear();
+            bigc.assign(oc, oc + m);
+            std::sort(bigc.begin(), bigc.end());
+            bigc.erase(std::unique(bigc.begin(), bigc.end()), bigc.end());
+            if (p > g_p0) add_group(g_p0, p, cur, ncur, false);
+            add_group(p, p + 1, bigc.data(), (int)bigc.size(), true);
+            g_p0 = p + 1; g_obs = 0; ncur = 0;
             continue;
         }
-        uni.clear();
-        std::set_union(cur.begin(), cur.end(), pc.begin(), pc.end(), std::back_inserter(uni));
-        if (p > g_p0 && (g_obs + m > GOBS || p - g_p0 + 1 > gpts || 6 * (int)uni.size() + K > GDPMAX)) {
-            add_group(g_p0, p, cur, false);
-            g_p0 = p; g_obs = 0; cur = pc;
+        int nu = 0;   // cur U pc (both sorted, unique)
+        for (int a = 0, b = 0; a < ncur || b < npc;) {
+            if (b == npc || (a < ncur && cur[a] < pc[b])) uni[nu++] = cur[a++];
+            else if (a == ncur || pc[b] < cur[a]) uni[nu++] = pc[b++];
+            else { uni[nu++] = cur[a++]; ++b; }
+        }
+        if (p > g_p0 && (g_obs + m > GOBS || p - g_p0 + 1 > gpts || 6 * nu + K > GDPMAX)) {
+            add_group(g_p0, p, cur, ncur, false);
+            g_p0 = p; g_obs = 0;
+            std::copy(pc, pc + npc, cur);
+            ncur = npc;
         } else {
-            cur.swap(uni);
+            std::copy(uni, uni + nu, cur);
+            ncur = nu;
         }
         g_obs += m;
     }
-    if (s1 > g_p0) add_group(g_p0, s1, cur, false);
+    if (s1 > g_p0) add_group(g_p0, s1, cur, ncur, false);
 }
 
 // Points in segments of SEG_PTS (a fixed size: the same groups on every host), scanned in
@@ -1198,13 +1236,28 @@ bool covisible(const Topology& tp, int C, int a, int b) {
     const size_t bit = (size_t)a * C + b;
     return (tp.covis[bit >> 6] >> (bit & 63)) & 1;
 }
+// (r05: in parallel.  The pose-pair tasks are cut by camera ranges: piece t owns the pairs whose first
+// camera lies in [C t / TP, C (t + 1) / TP), scans every group in order for them (a group's cameras are
+// sorted, so they are one run of its local cameras), sorts them stably by pair and builds its tasks and
+// entries; the pieces are concatenated in camera order.  The same tasks and entries as one serial pass.)
+constexpr int TOPO_PIECES = 16;
+struct TaskPiece {
+    std::vector<PairRef> pr, out;
+    std::vector<int> cnt;
+    std::vector<ATask> tasks;
+    std::vector<AEnt> ents;
+};
 void finish_topology(int C, int K, Topology& tp) {
+    thread_local std::vector<TaskPiece> pcs_tl;   // the caller thread's pieces, kept between calls (the
+    std::vector<TaskPiece>& pcs = pcs_tl;          // workers below reach them through this reference)
+    pcs.resize(TOPO_PIECES);
+    const int ng = (int)tp.grp.size();
     // camera slots: per camera, its (group, local camera) slots in group order
     std::vector<int>& slot_g = tp.slot_g;
     slot_g.resize(tp.gcam.size());
-    for (int g = 0; g < (int)tp.grp.size(); ++g)
-        for (int lc = 0; lc < tp.grp[g].u; ++lc) slot_g[tp.grp[g].cam_off + lc] = g;
     tp.cref_start.assign(C + 1, 0);
+    for (int g = 0; g < ng; ++g)
+        for (int lc = 0; lc < tp.grp[g].u; ++lc) slot_g[tp.grp[g].cam_off + lc] = g;
     for (int cm : tp.gcam) tp.cref_start[cm + 1]++;
     for (int c = 0; c < C; ++c) tp.cref_start[c + 1] += tp.cref_start[c];
     tp.cref.assign(tp.cref_start[C], 0);
@@ -1212,8 +1265,6 @@ void finish_topology(int C, int K, Topology& tp) {
         std::vector<int> f(tp.cref_start.begin(), tp.cref_start.end() - 1);
         for (int sl = 0; sl < (int)tp.gcam.size(); ++sl) tp.cref[f[tp.gcam[sl]]++] = sl;
     }
-    // assembly tasks: pose blocks (a <= b) with their (group, la, lb) lists in group order, then
-    // pose-intrinsics blocks per camera, then the intrinsics block
     auto ent = [&](int g, int la, int lb) {   // contribution of group g at local rows 6la / 6lb
         const Grp& G = tp.grp[g];
         const int dim = 6 * G.u + K;
@@ -1225,67 +1276,82 @@ void finish_topology(int C, int K, Topology& tp) {
         else { e.b0 = G.sg_off + (long long)(6 * la) * dim + 6 * lb; e.b1 = 0; }
         return e;
     };
-    {   // (camera a, camera b) keys in group order, stably sorted: tasks in key order, entries in group order
-        std::vector<PairRef>& pr = tp.pr;
-        size_t npr = 0;
-        for (const Grp& G : tp.grp) npr += (size_t)G.u * (G.u + 1) / 2;
-        pr.resize(npr);
-        {   // the groups' pairs in parallel ranges of groups (offsets from the per-group counts)
-            const int ng = (int)tp.grp.size();
-            std::vector<size_t> goff(ng + 1, 0);
-            for (int g = 0; g < ng; ++g) goff[g + 1] = goff[g] + (size_t)tp.grp[g].u * (tp.grp[g].u + 1) / 2;
-            // (in parallel only when large: a pool dispatch costs more than ~100k pair records)
-            sfmx::parallel_ranges(ng, npr >= ((size_t)1 << 18) ? 16 : 1, [&](int64_t g0, int64_t g1) {
-                for (int64_t g = g0; g < g1; ++g) {
-                    const Grp& G = tp.grp[g];
-                    size_t e = goff[g];
-                    for (int la = 0; la < G.u; ++la)
-                        for (int lb = la; lb < G.u; ++lb)
-                            pr[e++] = PairRef{((uint64_t)(uint32_t)tp.gcam[G.cam_off + la] << 32) | (uint32_t)tp.gcam[G.cam_off + lb],
-                                              (int)g, la, lb};
-                }
-            });
+    // assembly tasks: pose blocks (a <= b) with their (group, la, lb) lists in group order, then
+    // pose-intrinsics blocks per camera, then the intrinsics block
+    sfmx::parallel_items(TOPO_PIECES, [&](int t) {
+        TaskPiece& P = pcs[t];
+        const int a0 = (int)((int64_t)C * t / TOPO_PIECES), a1 = (int)((int64_t)C * (t + 1) / TOPO_PIECES);
+        P.pr.clear(); P.tasks.clear(); P.ents.clear();
+        if (a1 <= a0) return;
+        for (int g = 0; g < ng; ++g) {   // (key (a, b), group order)
+            const Grp& G = tp.grp[g];
+            const int* cams = tp.gcam.data() + G.cam_off;
+            for (int la = 0; la < G.u; ++la) {
+                if (cams[la] < a0) continue;
+                if (cams[la] >= a1) break;
+                for (int lb = la; lb < G.u; ++lb)
+                    P.pr.push_back(PairRef{((uint64_t)(uint32_t)cams[la] << 32) | (uint32_t)cams[lb], g, la, lb});
+            }
         }
-        if ((int64_t)C * C <= ((int64_t)1 << 22)) {   // stable counting sort on the pair index a C + b
-            std::vector<int>& cnt = tp.pr_cnt;
-            cnt.assign((size_t)C * C + 1, 0);
-            std::vector<PairRef>& out = tp.pr_out;
-            out.resize(pr.size());
-            auto idx = [C](const PairRef& x) { return (size_t)(x.key >> 32) * C + (size_t)(x.key & 0xffffffffu); };
-            for (const PairRef& x : pr) cnt[idx(x) + 1]++;
-            for (size_t i = 1; i < cnt.size(); ++i) cnt[i] += cnt[i - 1];
-            for (const PairRef& x : pr) out[cnt[idx(x)]++] = x;
-            pr.swap(out);
-        } else {
-            std::stable_sort(pr.begin(), pr.end(), [](const PairRef& x, const PairRef& y) { return x.key < y.key; });
-        }
-        tp.ents.reserve(pr.size() + tp.gcam.size() + tp.grp.size());
+        // stable counting sort on the pair index (a - a0) C + b
+        auto idx = [C, a0](const PairRef& x) { return (size_t)((int)(x.key >> 32) - a0) * C + (size_t)(x.key & 0xffffffffu); };
+        P.cnt.assign((size_t)(a1 - a0) * C + 1, 0);
+        for (const PairRef& x : P.pr) P.cnt[idx(x) + 1]++;
+        for (size_t i = 1; i < P.cnt.size(); ++i) P.cnt[i] += P.cnt[i - 1];
+        P.out.resize(P.pr.size());
+        for (const PairRef& x : P.pr) P.out[P.cnt[idx(x)]++] = x;
+        const std::vector<PairRef>& pr = P.out;
         for (size_t i = 0; i < pr.size();) {
-            ATask t{0, (int)(pr[i].key >> 32), (int)(pr[i].key & 0xffffffffu), (int)tp.ents.size(), 0, 0, 0, 0};
+            ATask tk{0, (int)(pr[i].key >> 32), (int)(pr[i].key & 0xffffffffu), (int)P.ents.size(), 0, 0, 0, 0};
             size_t j = i;
             while (j < pr.size() && pr[j].key == pr[i].key) ++j;
-            if (t.a == t.b || covisible(tp, C, t.a, t.b)) {   // a pair no point connects: exact zeros, no task
-                for (size_t q = i; q < j; ++q) tp.ents.push_back(ent(pr[q].g, pr[q].la, pr[q].lb));
-                t.l1 = (int)tp.ents.size();
-                tp.tasks.push_back(t);
+            if (tk.a == tk.b || covisible(tp, C, tk.a, tk.b)) {   // a pair no point connects: exact zeros, no task
+                for (size_t q = i; q < j; ++q) P.ents.push_back(ent(pr[q].g, pr[q].la, pr[q].lb));
+                tk.l1 = (int)P.ents.size();
+                P.tasks.push_back(tk);
             }
             i = j;
         }
+    });
+    // concatenated in camera order; then the per-camera and intrinsics tasks
+    std::vector<size_t> eoff(TOPO_PIECES + 1, 0), toff(TOPO_PIECES + 1, 0);
+    for (int t = 0; t < TOPO_PIECES; ++t) {
+        eoff[t + 1] = eoff[t] + pcs[t].ents.size();
+        toff[t + 1] = toff[t] + pcs[t].tasks.size();
     }
-    for (int cm = 0; cm < C; ++cm) {
-        ATask t{1, cm, 0, (int)tp.ents.size(), 0, 0, 0, 0};
-        for (int e = tp.cref_start[cm]; e < tp.cref_start[cm + 1]; ++e) {
-            const int sl = tp.cref[e], g = slot_g[sl];
-            tp.ents.push_back(ent(g, sl - tp.grp[g].cam_off, tp.grp[g].u));   // column block: the intrinsics rows
+    const size_t ne_pose = eoff[TOPO_PIECES], nt_pose = toff[TOPO_PIECES];
+    const size_t ne_cam = tp.cref.size(), ne = ne_pose + ne_cam + (size_t)ng;
+    size_t nt_cam = 0;
+    for (int cm = 0; cm < C; ++cm) nt_cam += tp.cref_start[cm + 1] > tp.cref_start[cm];
+    tp.ents.resize(ne);
+    tp.tasks.resize(nt_pose + nt_cam + (size_t)(K * K + K));
+    sfmx::parallel_items(TOPO_PIECES + 2, [&](int t) {
+        if (t < TOPO_PIECES) {
+            const TaskPiece& P = pcs[t];
+            std::copy(P.ents.begin(), P.ents.end(), tp.ents.begin() + eoff[t]);
+            for (size_t i = 0; i < P.tasks.size(); ++i) {
+                ATask tk = P.tasks[i];
+                tk.l0 += (int)eoff[t];
+                tk.l1 += (int)eoff[t];
+                tp.tasks[toff[t] + i] = tk;
+            }
+        } else if (t == TOPO_PIECES) {   // pose-intrinsics blocks per camera (column block: the intrinsics rows)
+            size_t e = ne_pose, k = nt_pose;
+            for (int cm = 0; cm < C; ++cm) {
+                ATask tk{1, cm, 0, (int)e, 0, 0, 0, 0};
+                for (int q = tp.cref_start[cm]; q < tp.cref_start[cm + 1]; ++q) {
+                    const int sl = tp.cref[q], g = slot_g[sl];
+                    tp.ents[e++] = ent(g, sl - tp.grp[g].cam_off, tp.grp[g].u);
+                }
+                tk.l1 = (int)e;
+                if (tk.l1 > tk.l0) tp.tasks[k++] = tk;
+            }
+        } else {   // the intrinsics block and rhs: one task per output, every group
+            const int l0 = (int)(ne_pose + ne_cam);
+            for (int g = 0; g < ng; ++g) tp.ents[l0 + g] = ent(g, tp.grp[g].u, tp.grp[g].u);
+            for (int x = 0; x < K * K + K; ++x) tp.tasks[nt_pose + nt_cam + x] = ATask{2, 0, x, l0, (int)ne, 0, 0, 0};
         }
-        t.l1 = (int)tp.ents.size();
-        if (t.l1 > t.l0) tp.tasks.push_back(t);
-    }
-    {   // the intrinsics block and rhs: one task per output, every group
-        const int l0 = (int)tp.ents.size();
-        for (int g = 0; g < (int)tp.grp.size(); ++g) tp.ents.push_back(ent(g, tp.grp[g].u, tp.grp[g].u));
-        for (int x = 0; x < K * K + K; ++x) tp.tasks.push_back(ATask{2, 0, x, l0, (int)tp.ents.size(), 0, 0, 0});
-    }
+    });
 }
 
 // Every index the group kernels derive from the topology, checked against the limits and buffer
@@ -1420,6 +1486,10 @@ struct Bucket {
     std::vector<int> roc;           // per internal observation: its camera
     std::vector<short> lc, row;     // obs_lc / obs_row (ba_group.hpp)
     std::vector<uint32_t> cpairs;   // the camera pairs (a << 16 | b, a < b) some point of the bucket connects
+    std::vector<std::pair<uint64_t, int>> kp, kp2;   // ordering scratch: (key, caller position) per piece
+                                                     // sorted, then merged
+    std::vector<int> m;                         // observations per point (caller order)
+    std::vector<std::vector<uint32_t>> pcp;     // co-visible pairs per piece of OPIECE internal points
     std::vector<int> sub;           // sub-segment starts in points (+ the end)
     std::vector<TopoSeg> topo;      // per sub-segment, offsets local to the bucket / sub-segment
     int no = 0;                     // observations
@@ -1445,7 +1515,8 @@ struct HostScratch {
     Topology tp;                    // the merged topology of the last load
     std::vector<int> pt_start;      // internal pt_start of the last load
     int n_dirty = 0;                // buckets redone by the last load
-    double tm[8] = {};              // host_setup phases (ms): view, compare, bucket lists, order + groups, layout, merge, tasks, shadows
+    double tm[9] = {};              // host_setup phases (ms): view, compare, bucket lists, order + groups, layout, merge, tasks,
+                                    // shadows; [8] the ordering part of [3] (keys, sort, co-visible pairs)
 };
 void destroy_scratch(HostScratch* h) { delete h; }
 
@@ -1456,8 +1527,9 @@ void destroy_scratch(HostScratch* h) { delete h; }
 // fresh load (incremental = false) runs every bucket through the same code, so both give the same
 // layout bit for bit (tests/test_ba_host.py).  hs.valid stays false until the caller confirms
 // the device half (load_problem).
+void build_operm(const HostScratch& hs, int O, std::vector<int>& operm);
 void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, HostScratch& hs, std::vector<int>& pperm,
-                std::vector<int>& operm) {
+                std::vector<int>* operm) {
     const int P = pb->n_points, C = pb->n_cams, O = pb->n_obs;
     using clk = std::chrono::steady_clock;
     auto tick = [t = clk::now()](double& slot) mutable {
@@ -1526,81 +1598,160 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
     hs.pbucket.resize(P);
     tick(hs.tm[1]);
     // the dirty buckets' points, in caller order (ties of the sort keep it)
-    for (int b = 0; b < nbk; ++b) if (hs.bk[b].dirty) hs.bk[b].pts.clear();
-    for (int p = 0; p < P; ++p) {
-        Bucket& B = hs.bk[hs.pbucket[p]];
-        if (B.dirty) B.pts.push_back(p);
+    {   // (fixed caller ranges on the worker pool, concatenated in range order)
+        constexpr int LP = 32;
+        std::vector<int> slot(hs.bk.size(), -1), dl;
+        for (int b = 0; b < nbk; ++b)
+            if (hs.bk[b].dirty) { slot[b] = (int)dl.size(); dl.push_back(b); hs.bk[b].pts.clear(); }
+        const int nd = (int)dl.size();
+        std::vector<std::vector<int>> part((size_t)LP * nd);
+        if (nd > 0) {
+            sfmx::parallel_items(LP, [&](int r) {
+                const int p0 = (int)((int64_t)P * r / LP), p1 = (int)((int64_t)P * (r + 1) / LP);
+                for (int p = p0; p < p1; ++p) {
+                    const int sl = slot[hs.pbucket[p]];
+                    if (sl >= 0) part[(size_t)r * nd + sl].push_back(p);
+                }
+            });
+            sfmx::parallel_items(nd, [&](int k) {
+                Bucket& B = hs.bk[dl[k]];
+                size_t n = 0;
+                for (int r = 0; r < LP; ++r) n += part[(size_t)r * nd + k].size();
+                B.pts.reserve(n);
+                for (int r = 0; r < LP; ++r) B.pts.insert(B.pts.end(), part[(size_t)r * nd + k].begin(), part[(size_t)r * nd + k].end());
+            });
+        }
     }
     tick(hs.tm[2]);
     // order + groups of every dirty bucket, in parallel
     std::vector<int> todo;
     for (int b = 0; b < nbk; ++b) if (hs.bk[b].dirty) todo.push_back(b);
     hs.n_dirty = (int)todo.size();
-    // (1) per dirty bucket: keys, order, observation lists, sub-segments; (2) every sub-segment's groups
-    sfmx::parallel_items((int)todo.size(), [&](int t) {
-        Bucket& B = hs.bk[todo[t]];
+    // (1) per dirty bucket: keys, order, observation lists, co-visible pairs, sub-segments, in pieces of
+    // OPIECE points on the worker pool (r05: the ring-closing bucket holds ~9000 points, one thread per
+    // bucket made it the critical path); (2) every sub-segment's groups
+    constexpr int OPIECE = 1024;
+    std::vector<std::pair<int, int>> pieces;   // (bucket, first point)
+    for (int b : todo) {
+        Bucket& B = hs.bk[b];
         const int np = (int)B.pts.size();
         // the caller's arrays are read in caller order only (ascending addresses; r03 read them in the
         // sorted order, a cache miss per point on a bucket spread over the whole problem)
         B.cpts.swap(B.pts);
         B.pts.resize(np);
-        std::vector<std::pair<uint64_t, int>> kp(np);
-        std::vector<int> m(np);
-        for (int j = 0; j < np; ++j) {
+        B.kp.resize(np);
+        B.m.resize(np);
+        for (int q = 0; q < np; q += OPIECE) pieces.emplace_back(b, q);
+    }
+    sfmx::parallel_items((int)pieces.size(), [&](int t) {   // keys and observation counts
+        Bucket& B = hs.bk[pieces[t].first];
+        const int j0 = pieces[t].second, j1 = std::min((int)B.cpts.size(), j0 + OPIECE);
+        for (int j = j0; j < j1; ++j) {
             int minc;
             const int p = B.cpts[j];
-            kp[j] = {point_key(pb, v, p, kb, &minc), j};
-            m[j] = v.start[p + 1] - v.start[p];
+            B.kp[j] = {point_key(pb, v, p, kb, &minc), j};
+            B.m[j] = v.start[p + 1] - v.start[p];
         }
-        radix_sort_keys(kp, kb.kb * kb.nk);   // (key, caller order): the stable order of the key
+        radix_sort_keys(B.kp.data() + j0, (size_t)(j1 - j0), kb.kb * kb.nk);   // the piece, stably
+    });
+    sfmx::parallel_items((int)todo.size(), [&](int t) {   // the order (stable radix sort of the keys)
+        Bucket& B = hs.bk[todo[t]];
+        const int np = (int)B.pts.size();
+        {   // (key, caller order): the pieces' sorted runs merged pairwise, bottom-up (std::merge takes the
+            // first run's element on ties, so the result is the stable order of the key)
+            B.kp2.resize(np);
+            auto by_key = [](const std::pair<uint64_t, int>& x, const std::pair<uint64_t, int>& y) { return x.first < y.first; };
+            std::vector<std::pair<uint64_t, int>>*src = &B.kp, *dst = &B.kp2;
+            for (int w = OPIECE; w < np; w *= 2) {
+                for (int i = 0; i < np; i += 2 * w) {
+                    const int m = std::min(np, i + w), e = std::min(np, i + 2 * w);
+                    std::merge(src->begin() + i, src->begin() + m, src->begin() + m, src->begin() + e, dst->begin() + i, by_key);
+                }
+                std::swap(src, dst);
+            }
+            if (src != &B.kp2) std::copy(src->begin(), src->end(), B.kp2.begin());
+        }
+        const std::vector<std::pair<uint64_t, int>>& kps = B.kp2;
         B.lpt.assign(np + 1, 0);
         B.rank.resize(np);
         for (int i = 0; i < np; ++i) {
-            const int j = kp[i].second;
+            const int j = kps[i].second;
             B.pts[i] = B.cpts[j];
             B.rank[j] = i;
-            B.lpt[i + 1] = B.lpt[i] + m[j];
+            B.lpt[i + 1] = B.lpt[i] + B.m[j];
         }
         B.no = B.lpt[np];
         B.roc.resize(B.no);
-        for (int j = 0; j < np; ++j) {
-            const int p = B.cpts[j];
-            for (int a = v.start[p], k = B.lpt[B.rank[j]]; a < v.start[p + 1]; ++a, ++k) B.roc[k] = pb->obs_cam[v.obs(a)];
-        }
-        {   // the bucket's co-visible camera pairs, deduplicated through a per-thread bit table
-            thread_local std::vector<uint64_t> mark;
-            const size_t words = ((size_t)C * C + 63) / 64;
-            if (mark.size() < words) mark.assign(words, 0);
-            B.cpairs.clear();
-            for (int i = 0; i < np; ++i)
-                for (int x = B.lpt[i]; x < B.lpt[i + 1]; ++x)
-                    for (int y = x + 1; y < B.lpt[i + 1]; ++y) {
-                        const int a = std::min(B.roc[x], B.roc[y]), b = std::max(B.roc[x], B.roc[y]);
-                        if (a == b) continue;
-                        const size_t bit = (size_t)a * C + b;
-                        if ((mark[bit >> 6] >> (bit & 63)) & 1) continue;
-                        mark[bit >> 6] |= 1ull << (bit & 63);
-                        B.cpairs.push_back((uint32_t)a << 16 | (uint32_t)b);
-                    }
-            for (uint32_t q : B.cpairs) {   // leave the table clear for the thread's next bucket
-                const size_t bit = (size_t)(q >> 16) * C + (q & 0xffff);
-                mark[bit >> 6] &= ~(1ull << (bit & 63));
-            }
-        }
         B.lc.assign(B.no, 0);
         B.row.assign(B.no, 0);
         B.sub.clear();
         for (int q = 0; q < np; q += SEG_PTS) B.sub.push_back(q);
         B.sub.push_back(np);
         B.topo.resize(B.sub.size() - 1);
+        B.pcp.resize((np + OPIECE - 1) / OPIECE);
     });
+    const size_t cwords = ((size_t)C * C + 63) / 64;
+    sfmx::parallel_items((int)pieces.size(), [&](int t) {   // observation cameras (then the pieces' co-visible pairs)
+        Bucket& B = hs.bk[pieces[t].first];
+        const int j0 = pieces[t].second, j1 = std::min((int)B.cpts.size(), j0 + OPIECE);
+        for (int j = j0; j < j1; ++j) {   // (caller order: ascending addresses)
+            const int p = B.cpts[j];
+            for (int a = v.start[p], k = B.lpt[B.rank[j]]; a < v.start[p + 1]; ++a, ++k) B.roc[k] = pb->obs_cam[v.obs(a)];
+        }
+    });
+    sfmx::parallel_items((int)pieces.size(), [&](int t) {
+        Bucket& B = hs.bk[pieces[t].first];
+        const int j0 = pieces[t].second, j1 = std::min((int)B.cpts.size(), j0 + OPIECE);
+        // the piece's internal points [j0, j1): pairs deduplicated through a per-thread bit table
+        thread_local std::vector<uint64_t> mark;
+        if (mark.size() < cwords) mark.assign(cwords, 0);
+        std::vector<uint32_t>& out = B.pcp[j0 / OPIECE];
+        out.clear();
+        for (int i = j0; i < j1; ++i)
+            for (int x = B.lpt[i]; x < B.lpt[i + 1]; ++x)
+                for (int y = x + 1; y < B.lpt[i + 1]; ++y) {
+                    const int a = std::min(B.roc[x], B.roc[y]), b = std::max(B.roc[x], B.roc[y]);
+                    if (a == b) continue;
+                    const size_t bit = (size_t)a * C + b;
+                    if ((mark[bit >> 6] >> (bit & 63)) & 1) continue;
+                    mark[bit >> 6] |= 1ull << (bit & 63);
+                    out.push_back((uint32_t)a << 16 | (uint32_t)b);
+                }
+        for (uint32_t q : out) {   // leave the table clear for the thread's next piece
+            const size_t bit = (size_t)(q >> 16) * C + (q & 0xffff);
+            mark[bit >> 6] &= ~(1ull << (bit & 63));
+        }
+    });
+    sfmx::parallel_items((int)todo.size(), [&](int t) {   // the bucket's pairs: the pieces' lists, deduplicated
+        Bucket& B = hs.bk[todo[t]];
+        thread_local std::vector<uint64_t> mark;
+        if (mark.size() < cwords) mark.assign(cwords, 0);
+        B.cpairs.clear();
+        for (const auto& pc : B.pcp)
+            for (uint32_t q : pc) {
+                const size_t bit = (size_t)(q >> 16) * C + (q & 0xffff);
+                if ((mark[bit >> 6] >> (bit & 63)) & 1) continue;
+                mark[bit >> 6] |= 1ull << (bit & 63);
+                B.cpairs.push_back(q);
+            }
+        for (uint32_t q : B.cpairs) {
+            const size_t bit = (size_t)(q >> 16) * C + (q & 0xffff);
+            mark[bit >> 6] &= ~(1ull << (bit & 63));
+        }
+    });
+    {
+        double t1;
+        auto t = tick;
+        t(t1);
+        hs.tm[8] = t1;
+    }
     std::vector<std::pair<int, int>> segs;   // (bucket, sub-segment)
     for (int b : todo)
         for (int j = 0; j + 1 < (int)hs.bk[b].sub.size(); ++j) segs.emplace_back(b, j);
     sfmx::parallel_items((int)segs.size(), [&](int t) {   // disjoint observation ranges of lc / row
         Bucket& B = hs.bk[segs[t].first];
         const int j = segs[t].second;
-        topo_segment(B.sub[j], B.sub[j + 1], K, gpts, B.lpt, B.roc.data(), B.lc.data(), B.row.data(), B.topo[j]);
+        topo_segment(B.sub[j], B.sub[j + 1], K, gpts, C, B.lpt, B.roc.data(), B.lc.data(), B.row.data(), B.topo[j]);
     });
     hs.bk.resize(nbk);
     tick(hs.tm[3]);
@@ -1608,43 +1759,65 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
     int ip = 0;
     int64_t io = 0;
     for (Bucket& B : hs.bk) { B.ip0 = ip; B.io0_new = io; ip += (int)B.pts.size(); io += B.no; }
-    // pperm, pt_start, operm: per bucket, in parallel
+    // pperm, pt_start: per bucket, in parallel (operm only when asked: the solve never reads it)
     pperm.resize(P);
-    operm.resize(O);
     std::vector<int>& pts = hs.pt_start;
     pts.resize(P + 1);
     pts[P] = O;
-    sfmx::parallel_items(nbk, [&](int b) {   // in caller order (see phase 1)
+    sfmx::parallel_items(nbk, [&](int b) {
         const Bucket& B = hs.bk[b];
-        for (size_t j = 0; j < B.cpts.size(); ++j) {
-            const int p = B.cpts[j], i = B.rank[j];
-            pperm[B.ip0 + i] = p;
+        const int np = (int)B.pts.size();
+        for (int i = 0; i < np; ++i) {
+            pperm[B.ip0 + i] = B.pts[i];
             pts[B.ip0 + i] = (int)(B.io0_new + B.lpt[i]);
-            for (int a = v.start[p], k = (int)B.io0_new + B.lpt[i]; a < v.start[p + 1]; ++a, ++k) operm[k] = v.obs(a);
         }
     });
+    if (operm) build_operm(hs, O, *operm);
     tick(hs.tm[4]);
     // merge the groups: bucket / sub-segment offsets -> internal ones
     Topology& tp = hs.tp;
     tp.clear();
-    for (const Bucket& B : hs.bk)
-        for (size_t j = 0; j < B.topo.size(); ++j) {
-            const TopoSeg& g = B.topo[j];
-            const int cam0 = (int)tp.gcam.size(), ch0 = (int)tp.chk.size(), b0 = (int)tp.bat.size(), l0 = (int)tp.lcrow.size();
-            const int dp = B.ip0, dobs = (int)B.io0_new;
-            for (Grp G : g.grp) {
-                G.o0 += dobs; G.o1 += dobs; G.p0 += dp; G.p1 += dp;
-                G.cam_off += cam0; G.ch0 += ch0; G.b0 += b0; G.rg_off += tp.rg_total;
-                if (G.big) G.h_off += tp.h_total; else G.sg_off += tp.sg_total;
-                tp.grp.push_back(G);
+    {   // every segment's offsets first (serial, one entry per segment), then the copies on the worker pool
+        struct SegOff { const Bucket* B; const TopoSeg* g; size_t grp, chk, bat, gcam, lcrow; long long sg, h; int rg; };
+        std::vector<SegOff> so;
+        SegOff o{nullptr, nullptr, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (const Bucket& B : hs.bk)
+            for (size_t j = 0; j < B.topo.size(); ++j) {
+                const TopoSeg& g = B.topo[j];
+                o.B = &B; o.g = &g;
+                so.push_back(o);
+                o.grp += g.grp.size(); o.chk += g.chk.size(); o.bat += g.bat.size(); o.gcam += g.gcam.size();
+                o.lcrow += g.lcrow.size(); o.sg += g.sg_total; o.h += g.h_total; o.rg += g.rg_total;
+                tp.dp_max = std::max(tp.dp_max, g.dp_max);
             }
-            for (Chunk ch : g.chk) { ch.o0 += dobs; ch.o1 += dobs; ch.lc0 += l0; tp.chk.push_back(ch); }
-            for (Batch bt : g.bat) { bt.o0 += dobs; bt.o1 += dobs; bt.p0 += dp; bt.p1 += dp; tp.bat.push_back(bt); }
-            tp.gcam.insert(tp.gcam.end(), g.gcam.begin(), g.gcam.end());
-            tp.lcrow.insert(tp.lcrow.end(), g.lcrow.begin(), g.lcrow.end());
-            tp.rg_total += g.rg_total; tp.sg_total += g.sg_total; tp.h_total += g.h_total;
-            tp.dp_max = std::max(tp.dp_max, g.dp_max);
-        }
+        tp.grp.resize(o.grp); tp.chk.resize(o.chk); tp.bat.resize(o.bat); tp.gcam.resize(o.gcam); tp.lcrow.resize(o.lcrow);
+        tp.sg_total = o.sg; tp.h_total = o.h; tp.rg_total = o.rg;
+        sfmx::parallel_items((int)so.size(), [&](int k) {
+            const SegOff& s0 = so[k];
+            const TopoSeg& g = *s0.g;
+            const int dp = s0.B->ip0, dobs = (int)s0.B->io0_new;
+            const int cam0 = (int)s0.gcam, ch0 = (int)s0.chk, b0 = (int)s0.bat, l0 = (int)s0.lcrow;
+            for (size_t i = 0; i < g.grp.size(); ++i) {
+                Grp G = g.grp[i];
+                G.o0 += dobs; G.o1 += dobs; G.p0 += dp; G.p1 += dp;
+                G.cam_off += cam0; G.ch0 += ch0; G.b0 += b0; G.rg_off += s0.rg;
+                if (G.big) G.h_off += s0.h; else G.sg_off += s0.sg;
+                tp.grp[s0.grp + i] = G;
+            }
+            for (size_t i = 0; i < g.chk.size(); ++i) {
+                Chunk ch = g.chk[i];
+                ch.o0 += dobs; ch.o1 += dobs; ch.lc0 += l0;
+                tp.chk[s0.chk + i] = ch;
+            }
+            for (size_t i = 0; i < g.bat.size(); ++i) {
+                Batch bt = g.bat[i];
+                bt.o0 += dobs; bt.o1 += dobs; bt.p0 += dp; bt.p1 += dp;
+                tp.bat[s0.bat + i] = bt;
+            }
+            std::copy(g.gcam.begin(), g.gcam.end(), tp.gcam.begin() + s0.gcam);
+            std::copy(g.lcrow.begin(), g.lcrow.end(), tp.lcrow.begin() + s0.lcrow);
+        });
+    }
     tick(hs.tm[5]);
     {   // the problem's co-visibility: the union of the buckets' pairs (kept ones included)
         tp.covis.assign(((size_t)C * C + 63) / 64, 0);
@@ -1672,6 +1845,20 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
     hs.sh.resize(nblk);
     hs.P = P; hs.K = K; hs.kb = kb.kb; hs.gpts = gpts;
     tick(hs.tm[7]);
+}
+
+// internal -> caller observation of the layout hs describes (the buckets' io0_new offsets and the view
+// of the problem it was built from): sfmx_ba_jacobian and the layout checks only
+void build_operm(const HostScratch& hs, int O, std::vector<int>& operm) {
+    operm.resize(O);
+    const View& v = hs.view;
+    sfmx::parallel_items((int)hs.bk.size(), [&](int b) {   // in caller order (see phase 1)
+        const Bucket& B = hs.bk[b];
+        for (size_t j = 0; j < B.cpts.size(); ++j) {
+            const int p = B.cpts[j], i = B.rank[j];
+            for (int a = v.start[p], k = (int)B.io0_new + B.lpt[i]; a < v.start[p + 1]; ++a, ++k) operm[k] = v.obs(a);
+        }
+    });
 }
 
 // The global observation arrays of the merged layout (diagnostics / checks): obs_cam, obs_lc, obs_row.
@@ -1760,7 +1947,7 @@ int intr_layout(const sfmx_ba_problem* pb, IntrLayout& L) {
 // every check that can refuse a problem runs before any context state changes; a failure
 // after that point (allocation, upload) leaves the context marked unloaded, and run / get / set
 // refuse it (SFMX_ESTATE) until an update succeeds.
-int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
+int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_ms = 0.0) {
     using clk = std::chrono::steady_clock;
     const auto t_start = clk::now();
     auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
@@ -1785,10 +1972,14 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
 #else
     const bool force_fresh = false;
 #endif
-    host_setup(caller, K, gpts, incremental && !force_fresh, hs, c->pperm, c->operm);
+    host_setup(caller, K, gpts, incremental && !force_fresh, hs, c->pperm, nullptr);
+    c->operm.clear();
     Topology& tp = hs.tp;
     const std::vector<int>& pt_start = hs.pt_start;
     c->setup_ms[5] = ms_since(t_start);
+    c->setup_ms[7] = validate_ms;
+    for (int i = 0; i < 8; ++i) c->setup_ms[8 + i] = hs.tm[i];
+    c->setup_ms[16] = c->setup_ms[17] = 0.0;
     auto bail = [](int rc) { return rc; };
     // per-problem state starts over
     c->scaled = c->j_scaled = false;
@@ -1971,7 +2162,11 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller) {
         (void)hipStreamSynchronize(st);         // the copies from the staging arena end before it is reused
         return bail(rc);
     }
-    HIPCHK(hipStreamSynchronize(st));   // (an unchanged plan returns at once: the copies end here)
+    {
+        const auto t_wait = clk::now();
+        HIPCHK(hipStreamSynchronize(st));   // (an unchanged plan returns at once: the copies end here)
+        c->setup_ms[17] += ms_since(t_wait);
+    }
     for (Bucket& B : hs.bk) { B.io0 = B.io0_new; B.dirty = false; }
     hs.valid = true;
     c->loaded = true;
@@ -2001,11 +2196,13 @@ int init_ctx(sfmx_ba_ctx* c, const sfmx_ba_options* opt) {
 }
 
 int create(const sfmx_ba_problem* caller, const sfmx_ba_options* opt, sfmx_ba_ctx** out) {
+    const auto t0 = std::chrono::steady_clock::now();
     RC(validate(caller));
+    const double vms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     auto* c = new (std::nothrow) sfmx_ba_ctx();
     if (!c) return fail(SFMX_ENOMEM, "host allocation");
     int rc = init_ctx(c, opt);
-    if (!rc) rc = load_problem(c, caller);
+    if (!rc) rc = load_problem(c, caller, vms);
     if (rc) { delete c; return rc; }
     *out = c;
     return SFMX_OK;
@@ -2190,13 +2387,14 @@ int sfmx_ba_destroy(sfmx_ba_ctx* c) {
 
 int sfmx_ba_update(sfmx_ba_ctx* c, const sfmx_ba_problem* pb) {
     if (!c) return fail(SFMX_EINVAL, "null context");
+    const auto t0 = std::chrono::steady_clock::now();
     RC(validate(pb));
-    return load_problem(c, pb);
+    return load_problem(c, pb, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
 int sfmx_ba_setup_ms(sfmx_ba_ctx* c, double* ms, int32_t n) {
     if (!c || !ms) return fail(SFMX_EINVAL, "null");
-    const int m = std::min<int>(n, 7);
+    const int m = std::min<int>(n, sfmx_ba_ctx::SETUP_N);
     for (int i = 0; i < m; ++i) ms[i] = c->setup_ms[i];
     return m;
 }
@@ -2247,6 +2445,7 @@ int sfmx_ba_jacobian(const sfmx_ba_problem* pb, int32_t device, double* r, doubl
     o.device = device;
     sfmx_ba_ctx* c = nullptr;
     RC(create(pb, &o, &c));
+    build_operm(*c->hscr, c->O, c->operm);
     int rc = SFMX_OK;
     {
         DeviceGuard dg(c->device);
@@ -2290,7 +2489,7 @@ int sfmx_ba_debug_check_topology(const sfmx_ba_problem* pb, int32_t gpts, double
     const auto t0 = clk::now();
     HostScratch hs;
     std::vector<int> pperm, operm, roc;
-    host_setup(pb, L.K, gpts > 0 ? std::min(gpts, GPTS) : GPTS, false, hs, pperm, operm);
+    host_setup(pb, L.K, gpts > 0 ? std::min(gpts, GPTS) : GPTS, false, hs, pperm, &operm);
     const auto t1 = clk::now();
     gather_obs(hs, pb->n_obs, roc, hs.tp.obs_lc, hs.tp.obs_row);
     const std::string why = check_topology(pb->n_points, pb->n_cams, pb->n_obs, L.K, hs.pt_start, roc.data(), hs.tp);
@@ -2309,7 +2508,7 @@ int sfmx_ba_debug_adjacency(const sfmx_ba_problem* pb, int32_t gpts, uint8_t* ad
     RC(intr_layout(pb, L));
     HostScratch hs;
     std::vector<int> pperm, operm;
-    host_setup(pb, L.K, gpts > 0 ? std::min(gpts, GPTS) : GPTS, false, hs, pperm, operm);
+    host_setup(pb, L.K, gpts > 0 ? std::min(gpts, GPTS) : GPTS, false, hs, pperm, &operm);
     const int C = pb->n_cams;
     std::memset(adj, 0, (size_t)C * C);
     for (const ATask& t : hs.tp.tasks)
@@ -2320,7 +2519,7 @@ int sfmx_ba_debug_adjacency(const sfmx_ba_problem* pb, int32_t gpts, uint8_t* ad
 // The host half of an update against a fresh load: problem a, then b on the same host caches (the
 // incremental path), must give b's fresh layout exactly (orders, observation permutation, every
 // topology array); -> buckets the update redid (out[0]) and all buckets (out[1]), or SFMX_EINTERNAL
-// naming the first difference.  ms (optional, 10): the update's and the fresh load's host time, then
+// naming the first difference.  ms (optional, 11): the update's and the fresh load's host time, then
 // the update's phases (HostScratch::tm).
 int sfmx_ba_debug_incremental_check(const sfmx_ba_problem* a, const sfmx_ba_problem* b, int32_t gpts, int32_t* out,
                                     double* ms) {
@@ -2334,15 +2533,17 @@ int sfmx_ba_debug_incremental_check(const sfmx_ba_problem* a, const sfmx_ba_prob
     auto d = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
     HostScratch inc, fr;
     std::vector<int> pp, op, pp2, op2;
-    host_setup(a, La.K, g, false, inc, pp, op);
+    host_setup(a, La.K, g, false, inc, pp, &op);
     for (Bucket& B : inc.bk) { B.io0 = B.io0_new; B.dirty = false; }
     inc.valid = true;
     const auto t0 = clk::now();
-    host_setup(b, Lb.K, g, true, inc, pp, op);
+    host_setup(b, Lb.K, g, true, inc, pp, nullptr);   // (timed as the product runs it: no operm)
     const auto t1 = clk::now();
-    host_setup(b, Lb.K, g, false, fr, pp2, op2);
+    host_setup(b, Lb.K, g, false, fr, pp2, nullptr);
     const auto t2 = clk::now();
-    if (ms) { ms[0] = d(t0, t1); ms[1] = d(t1, t2); for (int i = 0; i < 8; ++i) ms[2 + i] = inc.tm[i]; }
+    build_operm(inc, b->n_obs, op);
+    build_operm(fr, b->n_obs, op2);
+    if (ms) { ms[0] = d(t0, t1); ms[1] = d(t1, t2); for (int i = 0; i < 9; ++i) ms[2 + i] = inc.tm[i]; }
     if (out) { out[0] = inc.n_dirty; out[1] = (int)inc.bk.size(); }
     auto bytes = [](const auto& x, const auto& y) {
         return x.size() == y.size() && (x.empty() || std::memcmp(x.data(), y.data(), sizeof(x[0]) * x.size()) == 0);

@@ -6,6 +6,7 @@
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -20,17 +21,23 @@ inline int host_threads() {
 }
 
 // A persistent worker pool (host_threads() - 1 threads, started on first use): spawning and joining
-// 15 std::threads per parallel loop cost ~0.1-0.2 ms each, and a BA call makes ~10 such loops.  One
+// 15 std::threads per parallel loop cost ~0.1-0.2 ms each, and a BA call makes ~15 such loops.  One
 // job at a time; a caller that finds the pool busy (another thread's loop) runs its loop serially.
+// r05: a worker spins on the job generation for SPIN_US after its last job before it blocks on the
+// condition variable, and the caller spins on the completion count: a load's parallel loops come in
+// bursts a few hundred us apart, and a condition-variable wake-up of every worker per loop (each loop
+// waits for its slowest worker) cost 50-400 us per loop on a loaded host.
 class HostPool {
 public:
+    static constexpr int SPIN_US = 3000;
     explicit HostPool(int workers) {
         for (int t = 0; t < workers; ++t) th_.emplace_back([this] { loop(); });
     }
     ~HostPool() {
         {
             std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
+            stop_.store(true);
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         for (auto& t : th_) t.join();
@@ -41,44 +48,56 @@ public:
         std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
         if (!busy.owns_lock()) return false;
         std::function<void()> job = [&work] { work(); };
+        job_.store(&job, std::memory_order_relaxed);
+        pending_.store((int)th_.size(), std::memory_order_relaxed);
         {
-            std::lock_guard<std::mutex> lk(mu_);
-            job_ = &job;
-            pending_ = (int)th_.size();
-            ++gen_;
+            std::lock_guard<std::mutex> lk(mu_);   // (a worker about to block re-checks the generation under it)
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         work();
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [this] { return pending_ == 0; });
-        job_ = nullptr;
+        while (pending_.load(std::memory_order_acquire) != 0) cpu_relax();
+        job_.store(nullptr, std::memory_order_relaxed);
         return true;
     }
 
 private:
+    static void cpu_relax() {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
     void loop() {
         unsigned seen = 0;
         for (;;) {
-            std::function<void()>* job;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-                job = job_;
+            unsigned g = gen_.load(std::memory_order_acquire);
+            if (g == seen) {   // spin a while, then block
+                const auto t0 = std::chrono::steady_clock::now();
+                for (int i = 0; g == seen; ++i) {
+                    cpu_relax();
+                    g = gen_.load(std::memory_order_acquire);
+                    if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(SPIN_US)) break;
+                }
+                if (g == seen) {
+                    std::unique_lock<std::mutex> lk(mu_);
+                    cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+                    g = gen_.load(std::memory_order_acquire);
+                }
             }
+            seen = g;
+            if (stop_.load()) return;
+            std::function<void()>* job = job_.load(std::memory_order_relaxed);
             (*job)();
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--pending_ == 0) done_.notify_one();
+            pending_.fetch_sub(1, std::memory_order_acq_rel);
         }
     }
     std::vector<std::thread> th_;
     std::mutex mu_, run_mu_;
-    std::condition_variable cv_, done_;
-    std::function<void()>* job_ = nullptr;
-    unsigned gen_ = 0;
-    int pending_ = 0;
-    bool stop_ = false;
+    std::condition_variable cv_;
+    std::atomic<std::function<void()>*> job_{nullptr};
+    std::atomic<unsigned> gen_{0};
+    std::atomic<int> pending_{0};
+    std::atomic<bool> stop_{false};
 };
 
 inline HostPool& host_pool() {

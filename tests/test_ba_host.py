@@ -98,7 +98,7 @@ def _inc_check(a, b, gpts=0):
     from diag import diag_lib
     from sfmx import _lib
     out = (C.c_int32 * 2)()
-    ms = (C.c_double * 10)()
+    ms = (C.c_double * 11)()   # sfmx_ba_debug_incremental_check writes 11
     Pa, Pb = ba.BAProblem(**a), ba.BAProblem(**b)
     rc = diag_lib().sfmx_ba_debug_incremental_check(Pa.struct(), Pb.struct(), gpts, out, ms)
     assert rc == 0, diag_lib().sfmx_last_error()

@@ -14,10 +14,10 @@ from sfmx import ba, synth  # noqa: E402
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 base = synth.ba_sfm_order(synth.ba_problem(200, 200000))
 a, b = ba.BAProblem(**synth.ba_registered(base, 199)), ba.BAProblem(**synth.ba_registered(base, 200))
-names = ["view", "compare", "bucket_lists", "order_groups", "layout", "merge", "tasks", "shadows"]
+names = ["view", "compare", "bucket_lists", "order_groups", "layout", "merge", "tasks", "shadows", "(ordering part)"]
 best = None
 for _ in range(reps):
-    out, ms = (C.c_int32 * 2)(), (C.c_double * 10)()
+    out, ms = (C.c_int32 * 2)(), (C.c_double * 11)()
     rc = diag_lib().sfmx_ba_debug_incremental_check(a.struct(), b.struct(), 0, out, ms)
     assert rc == 0, diag_lib().sfmx_last_error()
     best = list(ms) if best is None else [min(x, y) for x, y in zip(best, ms)]
