@@ -1193,7 +1193,11 @@ struct Arena {                 // per-thread device scratch, grown on demand
             if (p) (void)hipFree(p);
             p = nullptr;
             cap = 0;
-            if (hipMalloc(&p, bytes) != hipSuccess) return false;
+            if (hipMalloc(&p, bytes) != hipSuccess) {
+                p = nullptr;
+                (void)hipGetLastError();   // clear it: a later launch check must not report this
+                return false;
+            }
             cap = bytes;
         }
         if (!e0 && (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)) return false;
@@ -1576,7 +1580,20 @@ int sfmx_orb_detect_compute_batch(const sfmx_gray_image* images, int32_t n_image
         // chunk size: at most 16, and the chunks a whole number of rounds over the streams (200 images on
         // 8 streams: 16 chunks of 13 rather than 13 chunks of 16, whose second round left 3 streams idle)
         const int rounds = std::max(1, (n_images + ns * 16 - 1) / (ns * 16));
-        const int gmax = std::max(1, std::min(16, (n_images + ns * rounds - 1) / (ns * rounds)));
+        int gmax = std::max(1, std::min(16, (n_images + ns * rounds - 1) / (ns * rounds)));
+        {   // a chunk reserves its per-image scratch (~19 B per pyramid pixel, ~60 B per image
+            // pixel) for each of its G images on each stream: G is also cut to what 80 % of the free device
+            // memory holds over the ns streams (a chunk that still fails is re-run image by image below)
+            int64_t maxpx = 1;
+            for (int i = 0; i < n_images; ++i)
+                if (images[i].data) maxpx = std::max<int64_t>(maxpx, (int64_t)images[i].width * images[i].height);
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0) {
+                const double per_image = 64.0 * (double)maxpx + (1 << 20);
+                const double budget = 0.8 * (double)fr / ns;
+                gmax = std::max(1, std::min<int>(gmax, (int)std::min(16.0, budget / per_image)));
+            }
+        }
         for (int i = 0; i < n_images; ++i) {
             const sfmx_gray_image& im = images[i];
             if (!im.data || capacities[i] < 0 || (capacities[i] > 0 && !keypoints[i])) {
@@ -1620,12 +1637,28 @@ int sfmx_orb_detect_compute_batch(const sfmx_gray_image* images, int32_t n_image
             float ms = 0.f;
             const int rc = orb_chunk(ims.data(), G, params, inputs_on_device, device, sl.stream, kp.data(),
                                      descriptors ? dd.data() : nullptr, caps.data(), nk.data(), crc.data(), sl.arena, &ms);
-            const std::string err = rc ? sfmx_last_error() : std::string();
+            if (rc != SFMX_OK && G > 1) {
+                // a chunk-level failure (device memory, a launch, an internal check): the chunk's images
+                // again one at a time, so each gets its own status (r03's per-image semantics)
+                for (int k = 0; k < G; ++k) {
+                    const int i = ch[k];
+                    int32_t nk1 = 0, crc1 = SFMX_OK;
+                    float ms1 = 0.f;
+                    const int r1 = orb_chunk(&ims[k], 1, params, inputs_on_device, device, sl.stream, &kp[k],
+                                             descriptors ? &dd[k] : nullptr, &caps[k], &nk1, &crc1, sl.arena, &ms1);
+                    n_keypoints[i] = nk1;
+                    rcs[i] = r1 ? r1 : crc1;
+                    if (r1) errs[i] = sfmx_last_error();
+                    else if (crc1 == SFMX_ECAPACITY) errs[i] = "keypoint capacity too small";
+                    if (!r1) kms[slot] += ms1;
+                }
+                continue;
+            }
             for (int k = 0; k < G; ++k) {
                 const int i = ch[k];
                 n_keypoints[i] = nk[k];
                 rcs[i] = rc ? rc : crc[k];
-                if (rc) errs[i] = err;
+                if (rc) errs[i] = sfmx_last_error();
                 else if (crc[k] == SFMX_ECAPACITY) errs[i] = "keypoint capacity too small";
             }
             if (!rc) kms[slot] += ms;

@@ -126,3 +126,31 @@ def test_batched_chunks_equal_the_oracle(n_streams):
     for (k, d), n, a, b in zip(got, ns, kt, dt):
         assert n == len(k)
         assert a[:n].cpu().numpy().tobytes() == k.tobytes() and np.array_equal(b[:n].cpu().numpy(), d)
+
+
+def test_large_images_through_several_streams():
+    """every chunk reserves its per-image scratch (~15 GB for a 16384^2 photo) for
+    each of its images on each stream, so 24 such images on 8 streams (chunks of 3) asked for ~375 GB.
+    The batch now cuts the chunk size to the free device memory (and re-runs a failing chunk image by
+    image): every image comes back OK and equal to its one-image call."""
+    import torch
+    import sfmx
+    tile = torch.from_numpy(sift_cases.blob_image(2048, 2048, n_blobs=900, seed=41, noise=6.0)).cuda()
+    base = tile.repeat(8, 8).contiguous()                     # 16384 x 16384
+    imgs = [torch.roll(base, shifts=37 * i, dims=1).contiguous() for i in range(24)]
+    orb = sfmx.features.ORB.create(30000)
+    cap = 1 << 15
+    kt = [torch.zeros((cap, 7), dtype=torch.int32, device="cuda") for _ in imgs]
+    dt = [torch.zeros((cap, 32), dtype=torch.uint8, device="cuda") for _ in imgs]
+    counts = orb.detectAndCompute_batch_device(imgs, kt, dt, n_streams=8)
+    torch.cuda.synchronize()
+    assert all(c > 0 for c in counts)
+    for i in (0, 13, 23):
+        k1 = torch.zeros((cap, 7), dtype=torch.int32, device="cuda")
+        d1 = torch.zeros((cap, 32), dtype=torch.uint8, device="cuda")
+        n = orb.detectAndCompute_device(imgs[i], k1, d1)
+        torch.cuda.synchronize()
+        assert n == counts[i]
+        assert torch.equal(k1[:n], kt[i][:n]) and torch.equal(d1[:n], dt[i][:n])
+    del imgs, kt, dt
+    torch.cuda.empty_cache()
