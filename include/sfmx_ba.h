@@ -156,8 +156,8 @@ int sfmx_ba_update(sfmx_ba_ctx* ctx, const sfmx_ba_problem* problem);
  * ordering / grouping pass alone (ms), [6] the number of camera buckets it redid, [7] the problem's
  * validation (ms), [8 .. 15] the phases of [5] (ms: point-major view, change detection, bucket
  * lists, ordering + groups of the redone buckets, layout arrays, merge, assembly tasks, shadows),
- * [16] the plan's host computation and [17] the load's final stream wait (ms).  n = entries
- * (up to 18). */
+ * [16] the plan's host computation, [17] the load's final stream wait, [18] the parameters'
+ * staging and copies, [19] the topology arrays' (ms).  n = entries (up to 20). */
 int sfmx_ba_setup_ms(sfmx_ba_ctx* ctx, double* ms, int32_t n);
 /* Copy the current parameters back into problem->points/poses/intr. */
 int sfmx_ba_get(sfmx_ba_ctx* ctx, sfmx_ba_problem* problem);

@@ -27,6 +27,8 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <functional>
+#include <future>
 #include <limits>
 #include <map>
 #include <mutex>
@@ -141,6 +143,7 @@ struct sfmx_ba_ctx {
     double phase_ms[4] = {0, 0, 0, 0};
     bool phases = false;         // per-phase events (sfmx_ba_set_phase_timing): ~6 us of GPU time each
     hipEvent_t ev[6] = {};
+    hipEvent_t gev[4] = {};      // sfmx_ba_get: the points' D2H in pieces, each scattered as it lands
     double* hs = nullptr;        // pinned host-coherent: 2 slots of [scalars SC_N | LM state LM_N], their
                                  // sequence words (HS_SEQ + slot) and ba_publish's sequence word (HS_SEQ + 2)
     Buf lmst;                    // device LM state (speculative mode, ba_decide)
@@ -158,9 +161,15 @@ struct sfmx_ba_ctx {
     // ordering / grouping pass alone (ms), [6] buckets redone (a count), [7] validation (ms), [8 .. 15]
     // host_setup's phases (HostScratch::tm), [16] the plan's host computation, [17] the load's final
     // stream wait (ms)
-    static constexpr int SETUP_N = 18;
+    static constexpr int SETUP_N = 20;   // [18] the parameters' staging + copies, [19] the topology arrays' (ms)
     double setup_ms[SETUP_N] = {};
     std::vector<char> plan_adj;   // the co-visibility the current plan was built from (reused if equal)
+    // r05: one rank's plan of a new co-visibility is computed on its own thread while the rest of the
+    // load (topology, uploads) runs; ensure_plan takes it when the graph and the mode match
+    std::future<void> plan_fut;
+    sfmx::ba::FactorPlan plan_pre;
+    std::vector<char> plan_pre_adj;
+    int plan_pre_mode = -2;
     std::string plan_form;        // diagnostic library: the form switches the plan was built with
     int plan_K = 0;
     HostScratch* hscr = nullptr;
@@ -170,11 +179,13 @@ struct sfmx_ba_ctx {
                       &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &Wr, &Wr2, &PR, &PR2, &J, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
                       &failf, &partA, &lmst, &camscr, &pim, &pcc};
+        if (plan_fut.valid()) plan_fut.wait();
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
         for (Buf* b : all) b->release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+        for (auto& e : gev) if (e) (void)hipEventDestroy(e);
         if (comm) (void)sfmx::rccl_api().CommDestroy(comm);
         if (st) (void)hipStreamDestroy(st);
         if (hs) (void)hipHostFree(hs);
@@ -555,6 +566,15 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
 
 // The factorization plan, rebuilt when the co-visibility changes (one rank: during the load, beside its
 // copies; sharded: at the first run, when the collectives are known -- setting them drops a plan): the
+int plan_mode() {   // SFMX_BA_ORDER (diagnostic library): auto | natural | nd | nd1 | nd2 | nd4
+    int mode = -1;
+    if (const char* e = SFMX_DIAG_ENV("SFMX_BA_ORDER")) {
+        const std::string m(e);
+        mode = m == "natural" ? 0 : m == "nd" ? 1 : m == "nd1" ? 2 : m == "nd2" ? 3 : m == "nd4" ? 4 : -1;
+    }
+    return mode;
+}
+
 // camera co-visibility summed over ranks (every rank builds the same plan), the
 // ordering and level schedule (SFMX_BA_ORDER: auto | natural | nd | nd1 | nd2 | nd4), the device
 // copies of the schedule, and S / W / the Schur terms sized by it.
@@ -589,14 +609,19 @@ int ensure_plan(sfmx_ba_ctx* c) {
         for (int a = 0, e = 0; a < C; ++a)
             for (int b = a + 1; b < C; ++b, ++e) adj[(size_t)a * C + b] = adj[(size_t)b * C + a] = h[e] > 0.0;
     }
-    int mode = -1;
-    if (const char* e = SFMX_DIAG_ENV("SFMX_BA_ORDER")) {
-        const std::string m(e);
-        mode = m == "natural" ? 0 : m == "nd" ? 1 : m == "nd1" ? 2 : m == "nd2" ? 3 : m == "nd4" ? 4 : -1;
-    }
+    const int mode = plan_mode();
     sfmx::ba::FactorPlan& pl = c->plan;
     const auto t_make = std::chrono::steady_clock::now();
-    sfmx::ba::make_plan(C, adj, mode, pl);
+    bool pre = false;
+    if (c->plan_fut.valid()) {   // the load's plan, computed beside it (same graph and mode: the same plan)
+        c->plan_fut.get();
+        if (!multirank(c) && c->plan_pre_mode == mode && c->plan_pre_adj == adj) {
+            std::swap(pl, c->plan_pre);
+            pre = true;
+        }
+        c->plan_pre_mode = -2;
+    }
+    if (!pre) sfmx::ba::make_plan(C, adj, mode, pl);
     if (pl.npad > MAX_NPAD) sfmx::ba::make_plan(C, adj, 0, pl);   // padding past the back solve's LDS
     c->npad = pl.npad;
     c->T = pl.T;
@@ -1529,7 +1554,7 @@ void destroy_scratch(HostScratch* h) { delete h; }
 // the device half (load_problem).
 void build_operm(const HostScratch& hs, int O, std::vector<int>& operm);
 void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, HostScratch& hs, std::vector<int>& pperm,
-                std::vector<int>* operm) {
+                std::vector<int>* operm, const std::function<void(const std::vector<uint64_t>&)>& on_covis = nullptr) {
     const int P = pb->n_points, C = pb->n_cams, O = pb->n_obs;
     using clk = std::chrono::steady_clock;
     auto tick = [t = clk::now()](double& slot) mutable {
@@ -1828,6 +1853,7 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
                 tp.covis[b2 >> 6] |= 1ull << (b2 & 63);
             }
     }
+    if (on_covis) on_covis(tp.covis);   // (load_problem: the plan of this graph starts here, on its own thread)
     finish_topology(C, K, tp);
     tick(hs.tm[6]);
     // shadows of the changed blocks (point-major problems only: the next update compares slices)
@@ -1972,7 +1998,24 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
 #else
     const bool force_fresh = false;
 #endif
-    host_setup(caller, K, gpts, incremental && !force_fresh, hs, c->pperm, nullptr);
+    if (c->plan_fut.valid()) c->plan_fut.wait();   // (a failed earlier load may have left one running)
+    // the co-visibility as soon as the ordering has it: S_cc's pattern (the pose-pair tasks are exactly
+    // its edges) and, on one rank, the plan of a new graph computed beside the rest of the load
+    auto on_covis = [c, C](const std::vector<uint64_t>& covis) {
+        c->adj.assign((size_t)C * C, 0);
+        for (int a = 0; a < C; ++a)
+            for (int b = 0; b < C; ++b) {
+                const size_t bit = (size_t)a * C + b;
+                if (a != b && ((covis[bit >> 6] >> (bit & 63)) & 1)) c->adj[bit] = 1;
+            }
+        if (multirank(c) || (c->planned && c->adj == c->plan_adj)) return;
+        c->plan_pre_adj = c->adj;
+        c->plan_pre_mode = plan_mode();
+        c->plan_fut = std::async(std::launch::async, [c, C] {
+            sfmx::ba::make_plan(C, c->plan_pre_adj, c->plan_pre_mode, c->plan_pre);
+        });
+    };
+    host_setup(caller, K, gpts, incremental && !force_fresh, hs, c->pperm, nullptr, on_covis);
     c->operm.clear();
     Topology& tp = hs.tp;
     const std::vector<int>& pt_start = hs.pt_start;
@@ -2008,10 +2051,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
     }
 #endif
     c->setup_ms[6] = hs.n_dirty;   // buckets redone (the ordering's and the groups' ms are [5] and [0])
-    // local camera co-visibility (the pose blocks this rank's points create)
-    c->adj.assign((size_t)C * C, 0);
-    for (const ATask& t : tp.tasks)   // (the pose-pair tasks are exactly the co-visible pairs)
-        if (t.type == 0 && t.a != t.b) c->adj[(size_t)t.a * C + t.b] = c->adj[(size_t)t.b * C + t.a] = 1;
+    // local camera co-visibility (the pose blocks this rank's points create): c->adj, from on_covis
     // a plan is reused only when this graph is the one it was built from; ranks of a sharded solve
     // rebuild on every update (the plan needs the co-visibility all-reduced over all of them)
     if (c->adj != c->plan_adj || multirank(c)) c->planned = false;
@@ -2123,12 +2163,14 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
         hipLaunchKernelGGL(ba_obs_point, dim3(nblk(P)), dim3(256), 0, st, P, c->pt_start.as<int>(), c->obs_point.as<int>());
         HIPCHK(hipGetLastError());
     }
+    const auto t_topo = clk::now();
     if ((rc = upload(c, c->grp, tp.grp)) || (rc = upload(c, c->chk, tp.chk)) || (rc = upload(c, c->bat, tp.bat)) ||
         (rc = upload(c, c->gcam, tp.gcam)) || (rc = upload(c, c->lcrow, tp.lcrow)) ||
         (rc = upload(c, c->tasks, tp.tasks)) || (rc = upload(c, c->ents, tp.ents)) ||
         (rc = upload(c, c->cref_start, tp.cref_start)) || (rc = upload(c, c->cref, tp.cref)) ||
         (rc = upload(c, c->pim, pim_h)) || (rc = upload(c, c->pcc, pcc_h)))
         return bail(rc);
+    c->setup_ms[19] = ms_since(t_topo);
     const size_t n = c->n;
     const size_t ncams = (size_t)C * ncp(K) + K * (K + 1) / 2 + K;
     struct { Buf* b; size_t bytes; } allocs[] = {
@@ -2154,7 +2196,9 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
     // and relayout run, and its own uploads end with the stream synchronisation; ranks of a sharded
     // solve plan at run (the plan's co-visibility all-reduce needs every rank)
     const bool plan_now = !multirank(c);
+    const auto t_par = clk::now();
     if ((rc = set_params(c, caller, !plan_now))) return bail(rc);
+    c->setup_ms[18] = ms_since(t_par);
     c->setup_ms[2] = up_ms + ms_since(t_up2);
     c->setup_ms[3] = 0.0;
     c->setup_ms[4] = ms_since(t_start);
@@ -2188,6 +2232,7 @@ int init_ctx(sfmx_ba_ctx* c, const sfmx_ba_options* opt) {
     DeviceGuard dg(c->device);
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) return fail(SFMX_EDEVICE, "stream");
     for (auto& e : c->ev) if (hipEventCreate(&e) != hipSuccess) return fail(SFMX_EDEVICE, "event");
+    for (auto& e : c->gev) if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(SFMX_EDEVICE, "event");
     if (hipHostMalloc(reinterpret_cast<void**>(&c->hs), sizeof(double) * sfmx_ba_ctx::HS_N,
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
         return fail(SFMX_ENOMEM, "pinned scalar buffer");
@@ -2345,16 +2390,28 @@ int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
     c->stage_off = 0;   // nothing staged is in flight: every upload was synchronised
     double* pts = c->P ? static_cast<double*>(stage_bytes(c, sizeof(double) * 3 * (size_t)c->P)) : nullptr;
     if (c->P && !pts) return fail(SFMX_ENOMEM, "pinned staging buffer");
-    if (c->P) HIPCHK(hipMemcpyAsync(pts, x, sizeof(double) * 3 * c->P, hipMemcpyDeviceToHost, c->st));
+    // the points in pieces: piece k is scattered into the caller's order while piece k + 1 is copied
+    const int P = c->P, npc = P >= 65536 ? 4 : 1;
+    for (int k = 0; k < npc && P; ++k) {
+        const int64_t q0 = (int64_t)P * k / npc, q1 = (int64_t)P * (k + 1) / npc;
+        HIPCHK(hipMemcpyAsync(pts + 3 * q0, x + 3 * q0, sizeof(double) * 3 * (q1 - q0), hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipEventRecord(c->gev[k], c->st));
+    }
     if (c->C) HIPCHK(hipMemcpyAsync(pb->poses, x + c->ne, sizeof(double) * 6 * c->C, hipMemcpyDeviceToHost, c->st));
     std::vector<double> iv(c->K);
     HIPCHK(hipMemcpyAsync(iv.data(), x + c->ne + 6 * (size_t)c->C, sizeof(double) * c->K, hipMemcpyDeviceToHost, c->st));
+    for (int k = 0; k < npc && P; ++k) {
+        hipError_t e;
+        while ((e = hipEventQuery(c->gev[k])) == hipErrorNotReady) {}
+        if (e != hipSuccess) return fail(SFMX_EDEVICE, std::string("D2H: ") + hipGetErrorString(e));
+        const int64_t q0 = (int64_t)P * k / npc, q1 = (int64_t)P * (k + 1) / npc;
+        sfmx::parallel_ranges(q1 - q0, q1 - q0 >= 16384 ? 16 : 1, [&](int64_t a0, int64_t a1) {   // write-back in caller order
+            for (int64_t q = q0 + a0; q < q0 + a1; ++q)
+                for (int i = 0; i < 3; ++i) pb->points[3 * (size_t)c->pperm[q] + i] = pts[3 * (size_t)q + i];
+        });
+    }
     HIPCHK(hipStreamSynchronize(c->st));
     for (int j = 0; j < c->K; ++j) if (c->isrc[j] >= 0) pb->intr[c->isrc[j]] = iv[j];   // unreferenced cameras: untouched
-    sfmx::parallel_ranges(c->P, c->P >= 65536 ? 16 : 1, [&](int64_t q0, int64_t q1) {   // write-back in caller order
-        for (int64_t q = q0; q < q1; ++q)
-            for (int i = 0; i < 3; ++i) pb->points[3 * (size_t)c->pperm[q] + i] = pts[3 * (size_t)q + i];
-    });
     return SFMX_OK;
 }
 

@@ -188,8 +188,8 @@ class BAContext:
         """Host-side setup of the last create / update (ms): ordering + groups (of the camera buckets
         that changed), device allocation, uploads, factorization plan, total; plus ``buckets_redone``
         (a count: the buckets an update re-ordered, include/sfmx_ba.h sfmx_ba_setup_ms)."""
-        v = (C.c_double * 18)()
-        n = check(lib.sfmx_ba_setup_ms(self._h, v, 18), "sfmx_ba_setup_ms")
+        v = (C.c_double * len(SETUP_NAMES))()
+        n = check(lib.sfmx_ba_setup_ms(self._h, v, len(SETUP_NAMES)), "sfmx_ba_setup_ms")
         return {k: v[i] for i, k in enumerate(SETUP_NAMES[:n])}
 
     def reset(self, problem: Optional[BAProblem] = None):
@@ -229,7 +229,7 @@ ORDER_AUTO, ORDER_NATURAL, ORDER_ND = -1, 0, 1
 # include/sfmx_ba.h sfmx_ba_setup_ms: ms unless noted
 SETUP_NAMES = ["order_groups", "alloc", "upload", "plan", "total", "host_setup", "buckets_redone", "validate",
                "h_view", "h_compare", "h_bucket_lists", "h_order_groups", "h_layout", "h_merge", "h_tasks", "h_shadows",
-               "plan_host", "stream_wait"]
+               "plan_host", "stream_wait", "params_upload", "topology_upload"]
 
 
 def factor_plan(adj: np.ndarray, order: int = ORDER_AUTO) -> dict:
