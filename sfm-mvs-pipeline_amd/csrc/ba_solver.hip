@@ -2391,7 +2391,8 @@ int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
     double* pts = c->P ? static_cast<double*>(stage_bytes(c, sizeof(double) * 3 * (size_t)c->P)) : nullptr;
     if (c->P && !pts) return fail(SFMX_ENOMEM, "pinned staging buffer");
     // the points in pieces: piece k is scattered into the caller's order while piece k + 1 is copied
-    const int P = c->P, npc = P >= 65536 ? 4 : 1;
+    static const int get_pieces = sfmx::env_int("SFMX_BA_GET_PIECES", 4, 1, 4);   // (A/B knob)
+    const int P = c->P, npc = P >= 65536 ? get_pieces : 1;
     for (int k = 0; k < npc && P; ++k) {
         const int64_t q0 = (int64_t)P * k / npc, q1 = (int64_t)P * (k + 1) / npc;
         HIPCHK(hipMemcpyAsync(pts + 3 * q0, x + 3 * q0, sizeof(double) * 3 * (q1 - q0), hipMemcpyDeviceToHost, c->st));

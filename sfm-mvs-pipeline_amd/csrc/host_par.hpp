@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -15,9 +16,17 @@
 
 namespace sfmx {
 
+// SFMX_HOST_THREADS (1 .. 64, default 16) and SFMX_HOST_SPIN_US (0 .. 100000, default below): read once
+inline int env_int(const char* k, int def, int lo, int hi) {
+    const char* e = std::getenv(k);
+    return e ? std::max(lo, std::min(hi, std::atoi(e))) : def;
+}
 inline int host_threads() {
-    const unsigned h = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(16u, h ? h : 1u));
+    static const int n = [] {
+        const unsigned h = std::thread::hardware_concurrency();
+        return std::min(env_int("SFMX_HOST_THREADS", 16, 1, 64), (int)std::max(1u, h ? h : 1u));
+    }();
+    return n;
 }
 
 // A persistent worker pool (host_threads() - 1 threads, started on first use): spawning and joining
@@ -30,6 +39,7 @@ inline int host_threads() {
 class HostPool {
 public:
     static constexpr int SPIN_US = 3000;
+    const int spin_us = env_int("SFMX_HOST_SPIN_US", SPIN_US, 0, 100000);
     explicit HostPool(int workers) {
         for (int t = 0; t < workers; ++t) th_.emplace_back([this] { loop(); });
     }
@@ -76,7 +86,7 @@ private:
                 for (int i = 0; g == seen; ++i) {
                     cpu_relax();
                     g = gen_.load(std::memory_order_acquire);
-                    if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(SPIN_US)) break;
+                    if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) break;
                 }
                 if (g == seen) {
                     std::unique_lock<std::mutex> lk(mu_);
