@@ -28,7 +28,6 @@
 #include <cmath>
 #include <cstring>
 #include <functional>
-#include <future>
 #include <limits>
 #include <map>
 #include <mutex>
@@ -166,7 +165,8 @@ struct sfmx_ba_ctx {
     std::vector<char> plan_adj;   // the co-visibility the current plan was built from (reused if equal)
     // r05: one rank's plan of a new co-visibility is computed on its own thread while the rest of the
     // load (topology, uploads) runs; ensure_plan takes it when the graph and the mode match
-    std::future<void> plan_fut;
+    sfmx::SideThread* plan_th = nullptr;   // (created on first use)
+    bool plan_pending = false;
     sfmx::ba::FactorPlan plan_pre;
     std::vector<char> plan_pre_adj;
     int plan_pre_mode = -2;
@@ -179,7 +179,7 @@ struct sfmx_ba_ctx {
                       &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &Wr, &Wr2, &PR, &PR2, &J, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
                       &failf, &partA, &lmst, &camscr, &pim, &pcc};
-        if (plan_fut.valid()) plan_fut.wait();
+        if (plan_th) { plan_th->wait(); delete plan_th; }
         int prev = 0;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
@@ -264,7 +264,7 @@ int upload(sfmx_ba_ctx* c, Buf& b, const std::vector<T>& v) {
     void* h = stage_bytes(c, sizeof(T) * v.size());
     if (!h) return fail(SFMX_ENOMEM, "pinned staging buffer");
     const size_t nb = sizeof(T) * v.size();
-    if (nb < ((size_t)1 << 20)) {
+    if (nb < ((size_t)1 << 18)) {
         std::memcpy(h, v.data(), nb);
     } else {   // large arrays: the copy into pinned memory on several host threads
         sfmx::parallel_ranges((int64_t)nb, 16, [&](int64_t b0, int64_t b1) {
@@ -613,8 +613,9 @@ int ensure_plan(sfmx_ba_ctx* c) {
     sfmx::ba::FactorPlan& pl = c->plan;
     const auto t_make = std::chrono::steady_clock::now();
     bool pre = false;
-    if (c->plan_fut.valid()) {   // the load's plan, computed beside it (same graph and mode: the same plan)
-        c->plan_fut.get();
+    if (c->plan_pending) {   // the load's plan, computed beside it (same graph and mode: the same plan)
+        c->plan_th->wait();
+        c->plan_pending = false;
         if (!multirank(c) && c->plan_pre_mode == mode && c->plan_pre_adj == adj) {
             std::swap(pl, c->plan_pre);
             pre = true;
@@ -1998,7 +1999,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
 #else
     const bool force_fresh = false;
 #endif
-    if (c->plan_fut.valid()) c->plan_fut.wait();   // (a failed earlier load may have left one running)
+    if (c->plan_pending) { c->plan_th->wait(); c->plan_pending = false; }   // (a failed earlier load's)
     // the co-visibility as soon as the ordering has it: S_cc's pattern (the pose-pair tasks are exactly
     // its edges) and, on one rank, the plan of a new graph computed beside the rest of the load
     auto on_covis = [c, C](const std::vector<uint64_t>& covis) {
@@ -2011,9 +2012,9 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
         if (multirank(c) || (c->planned && c->adj == c->plan_adj)) return;
         c->plan_pre_adj = c->adj;
         c->plan_pre_mode = plan_mode();
-        c->plan_fut = std::async(std::launch::async, [c, C] {
-            sfmx::ba::make_plan(C, c->plan_pre_adj, c->plan_pre_mode, c->plan_pre);
-        });
+        if (!c->plan_th) c->plan_th = new sfmx::SideThread();
+        c->plan_pending = true;
+        c->plan_th->submit([c, C] { sfmx::ba::make_plan(C, c->plan_pre_adj, c->plan_pre_mode, c->plan_pre); });
     };
     host_setup(caller, K, gpts, incremental && !force_fresh, hs, c->pperm, nullptr, on_covis);
     c->operm.clear();
@@ -2136,7 +2137,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
             if (!h || !hc || !hl || !hr) return bail(fail(SFMX_ENOMEM, "pinned staging buffer"));
             const int64_t o0 = B.io0_new;
             const int np = (int)B.cpts.size();
-            sfmx::parallel_ranges(np, B.no >= 65536 ? 16 : 1, [&](int64_t j0, int64_t j1) {   // caller order
+            sfmx::parallel_ranges(np, B.no >= 8192 ? 16 : 1, [&](int64_t j0, int64_t j1) {   // caller order
                 for (int64_t j = j0; j < j1; ++j) {
                     const int p = B.cpts[j];
                     for (int a = v.start[p], k = B.lpt[B.rank[j]]; a < v.start[p + 1]; ++a, ++k) h[k] = xy[v.obs(a)];
@@ -2391,7 +2392,8 @@ int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
     double* pts = c->P ? static_cast<double*>(stage_bytes(c, sizeof(double) * 3 * (size_t)c->P)) : nullptr;
     if (c->P && !pts) return fail(SFMX_ENOMEM, "pinned staging buffer");
     // the points in pieces: piece k is scattered into the caller's order while piece k + 1 is copied
-    static const int get_pieces = sfmx::env_int("SFMX_BA_GET_PIECES", 4, 1, 4);   // (A/B knob)
+    // (r05d A/B: one piece 0.31 ms, four 0.40 ms at C5: the per-piece waits cost more than the overlap)
+    static const int get_pieces = sfmx::env_int(SFMX_DIAG_ENV("SFMX_BA_GET_PIECES"), 1, 1, 4);
     const int P = c->P, npc = P >= 65536 ? get_pieces : 1;
     for (int k = 0; k < npc && P; ++k) {
         const int64_t q0 = (int64_t)P * k / npc, q1 = (int64_t)P * (k + 1) / npc;

@@ -4,6 +4,7 @@
 // number of ranges (independent of the machine's thread count), so every result is the same on
 // every host; the ranges run on up to 16 threads (a persistent pool).
 #pragma once
+#include "diag.hpp"
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -16,15 +17,15 @@
 
 namespace sfmx {
 
-// SFMX_HOST_THREADS (1 .. 64, default 16) and SFMX_HOST_SPIN_US (0 .. 100000, default below): read once
-inline int env_int(const char* k, int def, int lo, int hi) {
-    const char* e = std::getenv(k);
-    return e ? std::max(lo, std::min(hi, std::atoi(e))) : def;
+// diagnostic library only (diag.hpp): SFMX_HOST_THREADS (1 .. 64, default 16), SFMX_HOST_SPIN_US (0 .. 100000,
+// default below); read once
+inline int env_int(const char* v, int def, int lo, int hi) {
+    return v ? std::max(lo, std::min(hi, std::atoi(v))) : def;
 }
 inline int host_threads() {
     static const int n = [] {
         const unsigned h = std::thread::hardware_concurrency();
-        return std::min(env_int("SFMX_HOST_THREADS", 16, 1, 64), (int)std::max(1u, h ? h : 1u));
+        return std::min(env_int(SFMX_DIAG_ENV("SFMX_HOST_THREADS"), 16, 1, 64), (int)std::max(1u, h ? h : 1u));
     }();
     return n;
 }
@@ -39,7 +40,7 @@ inline int host_threads() {
 class HostPool {
 public:
     static constexpr int SPIN_US = 3000;
-    const int spin_us = env_int("SFMX_HOST_SPIN_US", SPIN_US, 0, 100000);
+    const int spin_us = env_int(SFMX_DIAG_ENV("SFMX_HOST_SPIN_US"), SPIN_US, 0, 100000);
     explicit HostPool(int workers) {
         for (int t = 0; t < workers; ++t) th_.emplace_back([this] { loop(); });
     }
@@ -114,6 +115,59 @@ inline HostPool& host_pool() {
     static HostPool p(host_threads() - 1);
     return p;
 }
+
+// One persistent side thread for a job that runs beside the caller's parallel loops (the BA load's
+// factorization plan): std::async spawned a thread per call (~30-50 us on the critical path).
+class SideThread {
+public:
+    SideThread() : th_([this] { loop(); }) {}
+    ~SideThread() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    void submit(std::function<void()> f) {
+        wait();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = std::move(f);
+            busy_ = true;
+        }
+        cv_.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return !busy_; });
+    }
+
+private:
+    void loop() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return stop_ || (busy_ && job_); });
+                if (stop_) return;
+                f = std::move(job_);
+                job_ = nullptr;
+            }
+            f();
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                busy_ = false;
+            }
+            done_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    std::function<void()> job_;
+    bool busy_ = false, stop_ = false;
+    std::thread th_;
+};
 
 // f(i) for i in [0, n): items taken from a shared counter by the pool's threads and the caller
 template <class F>
