@@ -59,21 +59,24 @@ int fail(int code, const std::string& m) { sfmx::set_last_error(m.c_str()); retu
 // Device buffer that keeps its allocation across problems (sfmx_ba_update, the cached context of
 // sfmx_ba_solve): alloc(b) reuses the block when it holds b bytes, else reallocates with 25 %
 // headroom (a scene grows by a few cameras per BundleAdjustment call, SfM.cpp:235 / :371).
+// A Buf with cap == 0 and p set is a view into another Buf's block (UploadSet below): never freed here.
 struct Buf {
     void* p = nullptr;
     size_t bytes = 0, cap = 0;
     int alloc(size_t b) {
         b = std::max<size_t>(b, 64);
         if (p && b <= cap) { bytes = b; return SFMX_OK; }
-        const size_t want = p ? std::max(b, cap + cap / 2) : b;   // first allocation exact, regrowth with headroom
-        if (p) { (void)hipFree(p); p = nullptr; }
+        const size_t want = p && cap ? std::max(b, cap + cap / 2) : b;   // first allocation exact, regrowth with headroom
+        if (p && cap) (void)hipFree(p);
+        p = nullptr;
         hipError_t e = hipMalloc(&p, want);
         if (e != hipSuccess) { p = nullptr; cap = bytes = 0; return fail(SFMX_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)); }
         cap = want;
         bytes = b;
         return SFMX_OK;
     }
-    void release() { if (p) (void)hipFree(p); p = nullptr; cap = bytes = 0; }
+    void release() { if (p && cap) (void)hipFree(p); p = nullptr; cap = bytes = 0; }
+    void set_view(void* q, size_t b) { release(); p = q; bytes = b; }
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
@@ -108,6 +111,7 @@ struct sfmx_ba_ctx {
     size_t lds_schur = 0, lds_lin = 0;
     Buf obs_point, obs_cam, obs_xy, pt_start, grp, chk, bat, gcam, obs_lc, obs_row, lcrow, tasks, ents, cref_start, cref;
     Buf obs_xy_b, obs_cam_b, obs_lc_b, obs_row_b, moves;   // the next layout's observation arrays; relayout moves
+    Buf topo_arena, plan_arena;   // one block each for the load's topology arrays and the plan's (UploadSet)
     int64_t setup_up_obs = 0;    // observations the last load uploaded (the rest moved on the device)
     // factorization plan of the reduced camera system (one rank: built during the load; sharded: at the
     // first run, from the camera co-visibility of every rank -- the layout of S must be the same on all)
@@ -142,7 +146,6 @@ struct sfmx_ba_ctx {
     double phase_ms[4] = {0, 0, 0, 0};
     bool phases = false;         // per-phase events (sfmx_ba_set_phase_timing): ~6 us of GPU time each
     hipEvent_t ev[6] = {};
-    hipEvent_t gev[4] = {};      // sfmx_ba_get: the points' D2H in pieces, each scattered as it lands
     double* hs = nullptr;        // pinned host-coherent: 2 slots of [scalars SC_N | LM state LM_N], their
                                  // sequence words (HS_SEQ + slot) and ba_publish's sequence word (HS_SEQ + 2)
     Buf lmst;                    // device LM state (speculative mode, ba_decide)
@@ -174,7 +177,7 @@ struct sfmx_ba_ctx {
     int plan_K = 0;
     HostScratch* hscr = nullptr;
     ~sfmx_ba_ctx() {
-        Buf* all[] = {&obs_xy_b, &obs_cam_b, &obs_lc_b, &obs_row_b, &moves, &obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
+        Buf* all[] = {&topo_arena, &plan_arena, &obs_xy_b, &obs_cam_b, &obs_lc_b, &obs_row_b, &moves, &obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
                       &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &Wr, &Wr2, &PR, &PR2, &J, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
@@ -185,7 +188,6 @@ struct sfmx_ba_ctx {
         (void)hipSetDevice(device);
         for (Buf* b : all) b->release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
-        for (auto& e : gev) if (e) (void)hipEventDestroy(e);
         if (comm) (void)sfmx::rccl_api().CommDestroy(comm);
         if (st) (void)hipStreamDestroy(st);
         if (hs) (void)hipHostFree(hs);
@@ -257,23 +259,45 @@ int stage_reserve(sfmx_ba_ctx* c, size_t n) {
     return SFMX_OK;
 }
 
-template <class T>
-int upload(sfmx_ba_ctx* c, Buf& b, const std::vector<T>& v) {
-    RC(b.alloc(sizeof(T) * std::max<size_t>(v.size(), 1)));
-    if (v.empty()) return SFMX_OK;
-    void* h = stage_bytes(c, sizeof(T) * v.size());
-    if (!h) return fail(SFMX_ENOMEM, "pinned staging buffer");
-    const size_t nb = sizeof(T) * v.size();
-    if (nb < ((size_t)1 << 18)) {
-        std::memcpy(h, v.data(), nb);
-    } else {   // large arrays: the copy into pinned memory on several host threads
-        sfmx::parallel_ranges((int64_t)nb, 16, [&](int64_t b0, int64_t b1) {
-            std::memcpy(static_cast<char*>(h) + b0, reinterpret_cast<const char*>(v.data()) + b0, (size_t)(b1 - b0));
-        });
+// Several host arrays to the device in ONE copy (r05: every hipMemcpyAsync costs ~5-10 us of host
+// time, and a load made ~25 of them): each array at a 256-B aligned offset of one device block
+// (`arena`, regrown like any Buf), its Buf a view of that range.  add() keeps a pointer (the array
+// must live until flush) or, with copy = true, a copy.
+struct UploadSet {
+    struct Part { Buf* dst; const void* src; size_t bytes; std::vector<char> own; };
+    std::vector<Part> parts;
+    template <class T>
+    void add(Buf& dst, const std::vector<T>& v, bool copy = false) {
+        Part pt{&dst, v.data(), sizeof(T) * v.size(), {}};
+        if (copy) {
+            pt.own.assign(reinterpret_cast<const char*>(v.data()), reinterpret_cast<const char*>(v.data()) + pt.bytes);
+            pt.src = pt.own.data();
+        }
+        parts.push_back(std::move(pt));
     }
-    HIPCHK(hipMemcpyAsync(b.p, h, sizeof(T) * v.size(), hipMemcpyHostToDevice, c->st));
-    return SFMX_OK;
-}
+    int flush(sfmx_ba_ctx* c, Buf& arena) {
+        if (parts.empty()) return SFMX_OK;
+        auto r = [](size_t b) { return (std::max<size_t>(b, 1) + 255) & ~(size_t)255; };
+        std::vector<size_t> off(parts.size() + 1, 0);
+        for (size_t i = 0; i < parts.size(); ++i) off[i + 1] = off[i] + r(parts[i].bytes);
+        RC(arena.alloc(off.back()));
+        char* h = static_cast<char*>(stage_bytes(c, off.back()));
+        if (!h) return fail(SFMX_ENOMEM, "pinned staging buffer");
+        // the copies into pinned memory in 256 KiB pieces on the worker pool
+        std::vector<std::pair<int, size_t>> pieces;
+        for (size_t i = 0; i < parts.size(); ++i)
+            for (size_t b = 0; b < parts[i].bytes; b += (size_t)1 << 18) pieces.emplace_back((int)i, b);
+        sfmx::parallel_items((int)pieces.size(), [&](int k) {
+            const Part& pt = parts[pieces[k].first];
+            const size_t b0 = pieces[k].second, n = std::min(pt.bytes - b0, (size_t)1 << 18);
+            std::memcpy(h + off[pieces[k].first] + b0, static_cast<const char*>(pt.src) + b0, n);
+        });
+        HIPCHK(hipMemcpyAsync(arena.p, h, off.back(), hipMemcpyHostToDevice, c->st));
+        for (size_t i = 0; i < parts.size(); ++i) parts[i].dst->set_view(arena.as<char>() + off[i], std::max<size_t>(parts[i].bytes, 64));
+        parts.clear();
+        return SFMX_OK;
+    }
+};
 
 bool multirank(const sfmx_ba_ctx* c) { return c->ar != nullptr || c->comm != nullptr; }
 double* scal(sfmx_ba_ctx* c, int i) { return c->scal.as<double>() + i; }
@@ -631,13 +655,10 @@ int ensure_plan(sfmx_ba_ctx* c) {
     std::vector<int4> tk(pl.tasks.size());
     for (size_t i = 0; i < tk.size(); ++i) tk[i] = make_int4(pl.tasks[i].a, pl.tasks[i].b, pl.tasks[i].s0, pl.tasks[i].s1);
     hipStream_t st = c->st;
-    int rc;
-    if ((rc = upload(c, c->camrow, pl.camrow)) || (rc = upload(c, c->padrows, pl.padrows)) ||
-        (rc = upload(c, c->rowmap, pl.rowmap)) || (rc = upload(c, c->leaves, pl.leaves)) ||
-        (rc = upload(c, c->ptasks, tk)) || (rc = upload(c, c->psrc, pl.src)) ||
-        (rc = upload(c, c->lvl_start, pl.lvl_start)) || (rc = upload(c, c->lvl_panels, pl.lvl_panels)) ||
-        (rc = upload(c, c->bs_start, pl.bs_start)) || (rc = upload(c, c->bs_k, pl.bs_k)))
-        return rc;
+    UploadSet up;   // every schedule array in one copy at the end (no launch reads them before)
+    up.add(c->camrow, pl.camrow); up.add(c->padrows, pl.padrows); up.add(c->rowmap, pl.rowmap);
+    up.add(c->leaves, pl.leaves); up.add(c->ptasks, tk); up.add(c->psrc, pl.src); up.add(c->lvl_start, pl.lvl_start);
+    up.add(c->lvl_panels, pl.lvl_panels); up.add(c->bs_start, pl.bs_start); up.add(c->bs_k, pl.bs_k);
     RC(c->SR.alloc(sizeof(double) * c->sr_count));
     {   // nonzero lower tiles (diagonal included): the compact all-reduce payload
         std::vector<int2> nzt;
@@ -645,7 +666,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
             for (int b = 0; b <= a; ++b)
                 if (pl.nz[(size_t)a * pl.T + b]) nzt.push_back(make_int2(a, b));
         c->n_nztiles = (int)nzt.size();
-        RC(upload(c, c->nztiles, nzt));
+        up.add(c->nztiles, nzt, true);
         RC(c->packbuf.alloc(sizeof(double) * ((size_t)c->n_nztiles * NB * NB + (c->sr_count - (size_t)pl.npad * pl.npad))));
     }
     RC(c->Wt.alloc(sizeof(double) * (size_t)pl.T * NB * NB));
@@ -655,7 +676,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
         std::vector<int> order;
         for (int l = pl.height; l >= 0; --l)
             for (int t = pl.lvl_start[l]; t < pl.lvl_start[l + 1]; ++t) order.push_back(pl.lvl_panels[t]);
-        RC(upload(c, c->border, order));
+        up.add(c->border, order, true);
         RC(c->zbuf.alloc(sizeof(double) * (size_t)pl.npad));
         RC(c->dagctr.alloc(sizeof(int) * (size_t)((pl.T + 2 + 3) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->dagctr.p, 0, c->dagctr.bytes, st));
@@ -679,7 +700,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
             max_slots = std::max(max_slots, slot);
             c->part_start.push_back((int)parts.size());
         }
-        RC(upload(c, c->parts, parts));
+        up.add(c->parts, parts, true);
         // chol_factor: the leaves, then every level's parts in the same order, product slots unique over
         // the launch; need = the versions (finished tasks, leaf inverse included) of A_ak, A_bk, (k, k)
         // and of A_ab before the task.  A plan whose source tile is not final at its use (never built
@@ -719,8 +740,8 @@ int ensure_plan(sfmx_ba_ctx* c) {
         }
         c->n_ditems = (int)items.size();
         c->n_ver = nver;
-        RC(upload(c, c->ditems, items));
-        RC(upload(c, c->dneed, need));
+        up.add(c->ditems, items, true);
+        up.add(c->dneed, need, true);
         RC(c->dctr.alloc(sizeof(int) * (size_t)((nver + 2 + 3) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->dctr.p, 0, c->dctr.bytes, st));
         const char* ed = SFMX_DIAG_ENV("SFMX_BA_DAG");
@@ -746,6 +767,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
     if (RW == 2) BACKATTR(2); else if (RW == 4) BACKATTR(4); else BACKATTR(8);
 #undef BACKATTR
     if (e != hipSuccess) return fail(SFMX_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(e));
+    RC(up.flush(c, c->plan_arena));
     const auto t_wait = std::chrono::steady_clock::now();
     c->setup_ms[16] = std::chrono::duration<double, std::milli>(t_wait - t_make).count();
     HIPCHK(hipStreamSynchronize(st));
@@ -956,20 +978,18 @@ int validate(const sfmx_ba_problem* pb) {
 int set_params(sfmx_ba_ctx* c, const sfmx_ba_problem* pb, bool sync = true) {
     DeviceGuard dg(c->device);
     double* x = c->x.as<double>();
-    if (c->P) {
-        double* pts = static_cast<double*>(stage_bytes(c, sizeof(double) * 3 * (size_t)c->P));
-        if (!pts) return fail(SFMX_ENOMEM, "pinned staging buffer");
-        sfmx::parallel_ranges(c->P, 16, [&](int64_t q0, int64_t q1) {
-            for (int64_t q = q0; q < q1; ++q)
-                for (int i = 0; i < 3; ++i) pts[3 * (size_t)q + i] = pb->points[3 * (size_t)c->pperm[q] + i];
-        });
-        HIPCHK(hipMemcpyAsync(x, pts, sizeof(double) * 3 * c->P, hipMemcpyHostToDevice, c->st));
-    }
-    if (c->C) HIPCHK(hipMemcpyAsync(x + c->ne, pb->poses, sizeof(double) * 6 * c->C, hipMemcpyHostToDevice, c->st));
-    double* iv = static_cast<double*>(stage_bytes(c, sizeof(double) * std::max(c->K, 1)));   // the border: referenced
-    if (!iv) return fail(SFMX_ENOMEM, "pinned staging buffer");                             // blocks, zero padding
+    // x = [points 3P | poses 6C | intrinsics border K]: staged back to back, one copy (r05)
+    const size_t n = 3 * (size_t)c->P + 6 * (size_t)c->C + (size_t)c->K;
+    double* h = static_cast<double*>(stage_bytes(c, sizeof(double) * std::max<size_t>(n, 1)));
+    if (!h) return fail(SFMX_ENOMEM, "pinned staging buffer");
+    sfmx::parallel_ranges(c->P, c->P >= 16384 ? 16 : 1, [&](int64_t q0, int64_t q1) {
+        for (int64_t q = q0; q < q1; ++q)
+            for (int i = 0; i < 3; ++i) h[3 * (size_t)q + i] = pb->points[3 * (size_t)c->pperm[q] + i];
+    });
+    if (c->C) std::memcpy(h + 3 * (size_t)c->P, pb->poses, sizeof(double) * 6 * c->C);
+    double* iv = h + 3 * (size_t)c->P + 6 * (size_t)c->C;   // the border: referenced blocks, zero padding
     for (int j = 0; j < c->K; ++j) iv[j] = c->isrc[j] >= 0 ? pb->intr[c->isrc[j]] : 0.0;
-    HIPCHK(hipMemcpyAsync(x + c->ne + 6 * (size_t)c->C, iv, sizeof(double) * c->K, hipMemcpyHostToDevice, c->st));
+    if (n) HIPCHK(hipMemcpyAsync(x, h, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
     if (sync) HIPCHK(hipStreamSynchronize(c->st));
     return SFMX_OK;
 }
@@ -2105,7 +2125,7 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
                        r(sizeof(Chunk) * tp.chk.size()) + r(sizeof(Batch) * tp.bat.size()) + r(4 * tp.gcam.size()) +
                        r(4 * tp.lcrow.size()) + r(sizeof(ATask) * tp.tasks.size()) + r(sizeof(AEnt) * tp.ents.size()) +
                        r(4 * tp.cref_start.size()) + r(4 * tp.cref.size()) + r(4 * pim_h.size()) +
-                       r(sizeof(double2) * pcc_h.size()) + r(24 * (size_t)P) + 4096;
+                       r(sizeof(double2) * pcc_h.size()) + r(24 * (size_t)P + 48 * (size_t)C + 8 * (size_t)K) + 4096;
         for (const Bucket& B : hs.bk)
             if (B.dirty || B.io0 < 0) total += r(16 * (size_t)B.no) + r(4 * (size_t)B.no) + 2 * r(2 * (size_t)B.no);
         RC(stage_reserve(c, total));
@@ -2159,19 +2179,19 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
     c->setup_up_obs = up_obs;
     // the observations' points from the point-major CSR on the device (no upload of rop)
     RC(c->obs_point.alloc(4 * so));
-    if ((rc = upload(c, c->pt_start, pt_start))) return bail(rc);
+    UploadSet up;   // the layout's CSR and topology arrays in one copy
+    up.add(c->pt_start, pt_start);
+    up.add(c->grp, tp.grp); up.add(c->chk, tp.chk); up.add(c->bat, tp.bat); up.add(c->gcam, tp.gcam);
+    up.add(c->lcrow, tp.lcrow); up.add(c->tasks, tp.tasks); up.add(c->ents, tp.ents); up.add(c->cref_start, tp.cref_start);
+    up.add(c->cref, tp.cref); up.add(c->pim, pim_h); up.add(c->pcc, pcc_h);
+    const auto t_topo = clk::now();
+    if ((rc = up.flush(c, c->topo_arena))) return bail(rc);
+    c->setup_ms[19] = ms_since(t_topo);
     if (P && O) {
         hipLaunchKernelGGL(ba_obs_point, dim3(nblk(P)), dim3(256), 0, st, P, c->pt_start.as<int>(), c->obs_point.as<int>());
         HIPCHK(hipGetLastError());
     }
-    const auto t_topo = clk::now();
-    if ((rc = upload(c, c->grp, tp.grp)) || (rc = upload(c, c->chk, tp.chk)) || (rc = upload(c, c->bat, tp.bat)) ||
-        (rc = upload(c, c->gcam, tp.gcam)) || (rc = upload(c, c->lcrow, tp.lcrow)) ||
-        (rc = upload(c, c->tasks, tp.tasks)) || (rc = upload(c, c->ents, tp.ents)) ||
-        (rc = upload(c, c->cref_start, tp.cref_start)) || (rc = upload(c, c->cref, tp.cref)) ||
-        (rc = upload(c, c->pim, pim_h)) || (rc = upload(c, c->pcc, pcc_h)))
-        return bail(rc);
-    c->setup_ms[19] = ms_since(t_topo);
+
     const size_t n = c->n;
     const size_t ncams = (size_t)C * ncp(K) + K * (K + 1) / 2 + K;
     struct { Buf* b; size_t bytes; } allocs[] = {
@@ -2233,7 +2253,6 @@ int init_ctx(sfmx_ba_ctx* c, const sfmx_ba_options* opt) {
     DeviceGuard dg(c->device);
     if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) return fail(SFMX_EDEVICE, "stream");
     for (auto& e : c->ev) if (hipEventCreate(&e) != hipSuccess) return fail(SFMX_EDEVICE, "event");
-    for (auto& e : c->gev) if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(SFMX_EDEVICE, "event");
     if (hipHostMalloc(reinterpret_cast<void**>(&c->hs), sizeof(double) * sfmx_ba_ctx::HS_N,
                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
         return fail(SFMX_ENOMEM, "pinned scalar buffer");
@@ -2389,31 +2408,19 @@ int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
     DeviceGuard dg(c->device);
     const double* x = c->x.as<double>();
     c->stage_off = 0;   // nothing staged is in flight: every upload was synchronised
-    double* pts = c->P ? static_cast<double*>(stage_bytes(c, sizeof(double) * 3 * (size_t)c->P)) : nullptr;
-    if (c->P && !pts) return fail(SFMX_ENOMEM, "pinned staging buffer");
-    // the points in pieces: piece k is scattered into the caller's order while piece k + 1 is copied
-    // (r05d A/B: one piece 0.31 ms, four 0.40 ms at C5: the per-piece waits cost more than the overlap)
-    static const int get_pieces = sfmx::env_int(SFMX_DIAG_ENV("SFMX_BA_GET_PIECES"), 1, 1, 4);
-    const int P = c->P, npc = P >= 65536 ? get_pieces : 1;
-    for (int k = 0; k < npc && P; ++k) {
-        const int64_t q0 = (int64_t)P * k / npc, q1 = (int64_t)P * (k + 1) / npc;
-        HIPCHK(hipMemcpyAsync(pts + 3 * q0, x + 3 * q0, sizeof(double) * 3 * (q1 - q0), hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipEventRecord(c->gev[k], c->st));
-    }
-    if (c->C) HIPCHK(hipMemcpyAsync(pb->poses, x + c->ne, sizeof(double) * 6 * c->C, hipMemcpyDeviceToHost, c->st));
-    std::vector<double> iv(c->K);
-    HIPCHK(hipMemcpyAsync(iv.data(), x + c->ne + 6 * (size_t)c->C, sizeof(double) * c->K, hipMemcpyDeviceToHost, c->st));
-    for (int k = 0; k < npc && P; ++k) {
-        hipError_t e;
-        while ((e = hipEventQuery(c->gev[k])) == hipErrorNotReady) {}
-        if (e != hipSuccess) return fail(SFMX_EDEVICE, std::string("D2H: ") + hipGetErrorString(e));
-        const int64_t q0 = (int64_t)P * k / npc, q1 = (int64_t)P * (k + 1) / npc;
-        sfmx::parallel_ranges(q1 - q0, q1 - q0 >= 16384 ? 16 : 1, [&](int64_t a0, int64_t a1) {   // write-back in caller order
-            for (int64_t q = q0 + a0; q < q0 + a1; ++q)
-                for (int i = 0; i < 3; ++i) pb->points[3 * (size_t)c->pperm[q] + i] = pts[3 * (size_t)q + i];
-        });
-    }
+    // x = [points | poses | border] in one copy; the points scattered into the caller's order (r05d:
+    // one copy and one wait beat four pieces scattered as they land: 0.31 vs 0.40 ms at C5)
+    const size_t n = 3 * (size_t)c->P + 6 * (size_t)c->C + (size_t)c->K;
+    double* h = static_cast<double*>(stage_bytes(c, sizeof(double) * std::max<size_t>(n, 1)));
+    if (!h) return fail(SFMX_ENOMEM, "pinned staging buffer");
+    if (n) HIPCHK(hipMemcpyAsync(h, x, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    sfmx::parallel_ranges(c->P, c->P >= 16384 ? 16 : 1, [&](int64_t q0, int64_t q1) {   // write-back in caller order
+        for (int64_t q = q0; q < q1; ++q)
+            for (int i = 0; i < 3; ++i) pb->points[3 * (size_t)c->pperm[q] + i] = h[3 * (size_t)q + i];
+    });
+    if (c->C) std::memcpy(pb->poses, h + c->ne, sizeof(double) * 6 * c->C);
+    const double* iv = h + c->ne + 6 * (size_t)c->C;
     for (int j = 0; j < c->K; ++j) if (c->isrc[j] >= 0) pb->intr[c->isrc[j]] = iv[j];   // unreferenced cameras: untouched
     return SFMX_OK;
 }
