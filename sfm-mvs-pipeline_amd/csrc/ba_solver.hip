@@ -1021,19 +1021,21 @@ void make_view(const sfmx_ba_problem* pb, View& v) {
     constexpr int PIECES = 64;   // fixed ranges (host_par.hpp): the same result on every host
     v.start.resize(P + 1);
     std::atomic<bool> pm{true};
-    sfmx::parallel_ranges(O, PIECES, [&](int64_t i0, int64_t i1) {
-        for (int64_t i = std::max<int64_t>(i0, 1); i < i1; ++i)
-            if (pb->obs_point[i] < pb->obs_point[i - 1]) { pm = false; return; }
-    });
-    v.pm = pm;
-    if (v.pm) {   // the reference adds residuals point by point (BundleAdjustment.cpp:50-91)
+    {   // the reference adds residuals point by point (BundleAdjustment.cpp:50-91): one pass both checks
+        // the order and, for a point-major problem, fills the starts (r05: two passes before)
         const int* op = pb->obs_point;
         sfmx::parallel_ranges((int64_t)O + 1, PIECES, [&](int64_t i0, int64_t i1) {
+            bool ok = true;
             for (int64_t i = i0; i < i1; ++i) {   // points (op[i - 1], op[i]] start at i
                 const int lo = i == 0 ? -1 : op[i - 1], hi = i == O ? P - 1 : op[i];
+                ok &= lo <= hi;   // (a decrease: not point-major)
                 for (int p = lo + 1; p <= hi; ++p) v.start[p] = (int)i;
             }
+            if (!ok) pm = false;
         });
+    }
+    v.pm = pm;
+    if (v.pm) {
         v.start[P] = O;
         v.vobs.clear();
     } else {
@@ -1560,6 +1562,7 @@ struct HostScratch {
     View view;
     Topology tp;                    // the merged topology of the last load
     std::vector<int> pt_start;      // internal pt_start of the last load
+    std::vector<int> iperm;         // caller point -> internal point (the inverse of pperm)
     int n_dirty = 0;                // buckets redone by the last load
     double tm[9] = {};              // host_setup phases (ms): view, compare, bucket lists, order + groups, layout, merge, tasks,
                                     // shadows; [8] the ordering part of [3] (keys, sort, co-visible pairs)
@@ -1807,6 +1810,7 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
     for (Bucket& B : hs.bk) { B.ip0 = ip; B.io0_new = io; ip += (int)B.pts.size(); io += B.no; }
     // pperm, pt_start: per bucket, in parallel (operm only when asked: the solve never reads it)
     pperm.resize(P);
+    hs.iperm.resize(P);
     std::vector<int>& pts = hs.pt_start;
     pts.resize(P + 1);
     pts[P] = O;
@@ -1815,6 +1819,7 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
         const int np = (int)B.pts.size();
         for (int i = 0; i < np; ++i) {
             pperm[B.ip0 + i] = B.pts[i];
+            hs.iperm[B.pts[i]] = B.ip0 + i;
             pts[B.ip0 + i] = (int)(B.io0_new + B.lpt[i]);
         }
     });
@@ -2415,9 +2420,11 @@ int sfmx_ba_get(sfmx_ba_ctx* c, sfmx_ba_problem* pb) {
     if (!h) return fail(SFMX_ENOMEM, "pinned staging buffer");
     if (n) HIPCHK(hipMemcpyAsync(h, x, sizeof(double) * n, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
-    sfmx::parallel_ranges(c->P, c->P >= 16384 ? 16 : 1, [&](int64_t q0, int64_t q1) {   // write-back in caller order
-        for (int64_t q = q0; q < q1; ++q)
-            for (int i = 0; i < 3; ++i) pb->points[3 * (size_t)c->pperm[q] + i] = h[3 * (size_t)q + i];
+    if (!c->hscr || (int)c->hscr->iperm.size() != c->P) return fail(SFMX_EINTERNAL, "BA get: no layout of the loaded problem");
+    const int* ip = c->hscr->iperm.data();   // caller -> internal: the caller's array written in order
+    sfmx::parallel_ranges(c->P, c->P >= 16384 ? 16 : 1, [&](int64_t p0, int64_t p1) {   // write-back in caller order
+        for (int64_t p = p0; p < p1; ++p)
+            for (int i = 0; i < 3; ++i) pb->points[3 * (size_t)p + i] = h[3 * (size_t)ip[p] + i];
     });
     if (c->C) std::memcpy(pb->poses, h + c->ne, sizeof(double) * 6 * c->C);
     const double* iv = h + c->ne + 6 * (size_t)c->C;
