@@ -141,10 +141,9 @@ int sfmx_ba_run(sfmx_ba_ctx* ctx, int32_t max_iterations, sfmx_ba_summary* summa
  * BundleAdjustment after every registered camera, SfM.cpp:235 / :371): the scene stays
  * resident.  Points are ordered and grouped in buckets of their smallest camera; for a
  * point-major problem (the reference's residual order) only the buckets holding points whose
- * observations (count, cameras) changed since the last load are redone on the host, the others
- * keep their order and groups and their observation records move on the device (no upload); the
- * pixels go up whole every call and are put in the internal order on the device.  The result
- * is bit-identical to a fresh context on the same problem.  Device
+ * observations (count, cameras, pixels) changed since the last load are redone on the host,
+ * the others keep their order and groups and their observation data moves on the device
+ * (no upload).  The result is bit-identical to a fresh context on the same problem.  Device
  * buffers are reused when large enough and the factorization plan when the camera
  * co-visibility is unchanged (single rank).  Options and the all-reduce callback stay.  Then
  * sfmx_ba_run / sfmx_ba_get as after sfmx_ba_create.  A refused problem (SFMX_EINVAL,
@@ -158,7 +157,7 @@ int sfmx_ba_update(sfmx_ba_ctx* ctx, const sfmx_ba_problem* problem);
  * validation (ms), [8 .. 15] the phases of [5] (ms: point-major view, change detection, bucket
  * lists, ordering + groups of the redone buckets, layout arrays, merge, assembly tasks, shadows),
  * [16] the plan's host computation, [17] the load's final stream wait, [18] the parameters'
- * staging and copies, [19] the topology arrays', [20] the pixels' (ms).  n = entries (up to 21). */
+ * staging and copies, [19] the topology arrays' (ms).  n = entries (up to 20). */
 int sfmx_ba_setup_ms(sfmx_ba_ctx* ctx, double* ms, int32_t n);
 /* Copy the current parameters back into problem->points/poses/intr. */
 int sfmx_ba_get(sfmx_ba_ctx* ctx, sfmx_ba_problem* problem);

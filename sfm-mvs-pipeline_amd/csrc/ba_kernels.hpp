@@ -358,33 +358,22 @@ __global__ void ba_decide(const double* __restrict__ scal, double* __restrict__ 
 __global__ void ba_open_gate(int* __restrict__ fail) { if (threadIdx.x == 0) fail[1] = 1; }
 
 // problem setup: every observation's (internal) point from the point-major CSR
-// Per internal point q (one thread): its observations' point index, and their pixels gathered from
-// the caller's array as it was copied up (r05: every load copies the pixels up whole and the device
-// puts them in the internal order, so the host neither compares nor gathers them).  Point-major
-// caller arrays: caller point pperm[q]'s observations start at vstart[pperm[q]]; otherwise omap[k] is
-// the caller observation of internal observation k.
-__global__ void ba_obs_gather(int P, const int* __restrict__ pt_start, const int* __restrict__ pperm,
-                              const int* __restrict__ vstart, const int* __restrict__ omap, const double2* __restrict__ raw,
-                              int* __restrict__ obs_point, double2* __restrict__ obs_xy) {
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= P) return;
-    const int k0 = pt_start[q], k1 = pt_start[q + 1];
-    const int c0 = omap ? 0 : vstart[pperm[q]];
-    for (int k = k0; k < k1; ++k) {
-        obs_point[k] = q;
-        obs_xy[k] = raw[omap ? omap[k] : c0 + (k - k0)];
-    }
+__global__ void ba_obs_point(int P, const int* __restrict__ pt_start, int* __restrict__ obs_point) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < P)
+        for (int o = pt_start[p]; o < pt_start[p + 1]; ++o) obs_point[o] = p;
 }
 // sfmx_ba_update: an unchanged bucket's observation data moves to its offset in the new layout
-// (camera, local camera, feature row: 8 B per observation; the pixels come from ba_obs_gather), one
-// workgroup per <= 4096.
+// (pixels, camera, local camera, feature row: 24 B per observation), one workgroup per <= 4096.
 struct ObsMove { long long src, dst; int n, pad; };
 constexpr int RELAYOUT_CHUNK = 4096;
-__global__ __launch_bounds__(256) void ba_relayout(const ObsMove* __restrict__ mv, const int* __restrict__ cam,
-                                                   const short* __restrict__ lc, const short* __restrict__ row,
+__global__ __launch_bounds__(256) void ba_relayout(const ObsMove* __restrict__ mv, const double2* __restrict__ xy,
+                                                   const int* __restrict__ cam, const short* __restrict__ lc,
+                                                   const short* __restrict__ row, double2* __restrict__ xy2,
                                                    int* __restrict__ cam2, short* __restrict__ lc2, short* __restrict__ row2) {
     const ObsMove m = mv[blockIdx.x];
     for (int k = threadIdx.x; k < m.n; k += blockDim.x) {
+        xy2[m.dst + k] = xy[m.src + k];
         cam2[m.dst + k] = cam[m.src + k];
         lc2[m.dst + k] = lc[m.src + k];
         row2[m.dst + k] = row[m.src + k];

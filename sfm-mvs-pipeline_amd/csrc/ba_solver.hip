@@ -110,10 +110,7 @@ struct sfmx_ba_ctx {
     int ngroups = 0, ntasks = 0, nslots = 0, gs_nt = 4;   // gs_nt: ba_gschur specialisation, dp_max / 16
     size_t lds_schur = 0, lds_lin = 0;
     Buf obs_point, obs_cam, obs_xy, pt_start, grp, chk, bat, gcam, obs_lc, obs_row, lcrow, tasks, ents, cref_start, cref;
-    Buf obs_cam_b, obs_lc_b, obs_row_b, moves;   // the next layout's observation arrays; relayout moves
-    Buf raw_xy, dperm, dvstart, domap;           // the caller's pixels as copied up; ba_obs_gather's maps
-    char* xy_stage = nullptr;                    // pinned staging of the caller's pixels (its own block)
-    size_t xy_stage_cap = 0;
+    Buf obs_xy_b, obs_cam_b, obs_lc_b, obs_row_b, moves;   // the next layout's observation arrays; relayout moves
     Buf topo_arena, plan_arena;   // one block each for the load's topology arrays and the plan's (UploadSet)
     int64_t setup_up_obs = 0;    // observations the last load uploaded (the rest moved on the device)
     // factorization plan of the reduced camera system (one rank: built during the load; sharded: at the
@@ -166,8 +163,7 @@ struct sfmx_ba_ctx {
     // ordering / grouping pass alone (ms), [6] buckets redone (a count), [7] validation (ms), [8 .. 15]
     // host_setup's phases (HostScratch::tm), [16] the plan's host computation, [17] the load's final
     // stream wait (ms)
-    static constexpr int SETUP_N = 21;   // [18] the parameters' staging + copies, [19] the topology arrays',
-                                         // [20] the pixels' staging + copy (ms)
+    static constexpr int SETUP_N = 20;   // [18] the parameters' staging + copies, [19] the topology arrays' (ms)
     double setup_ms[SETUP_N] = {};
     std::vector<char> plan_adj;   // the co-visibility the current plan was built from (reused if equal)
     // r05: one rank's plan of a new co-visibility is computed on its own thread while the rest of the
@@ -181,7 +177,7 @@ struct sfmx_ba_ctx {
     int plan_K = 0;
     HostScratch* hscr = nullptr;
     ~sfmx_ba_ctx() {
-        Buf* all[] = {&topo_arena, &plan_arena, &raw_xy, &dperm, &dvstart, &domap, &obs_cam_b, &obs_lc_b, &obs_row_b, &moves, &obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
+        Buf* all[] = {&topo_arena, &plan_arena, &obs_xy_b, &obs_cam_b, &obs_lc_b, &obs_row_b, &moves, &obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
                       &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &Wr, &Wr2, &PR, &PR2, &J, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
@@ -196,7 +192,6 @@ struct sfmx_ba_ctx {
         if (st) (void)hipStreamDestroy(st);
         if (hs) (void)hipHostFree(hs);
         if (stage) (void)hipHostFree(stage);
-        if (xy_stage) (void)hipHostFree(xy_stage);
         destroy_scratch(hscr);
         (void)hipSetDevice(prev);
     }
@@ -1553,10 +1548,9 @@ struct Bucket {
 };
 // Caller-order copy of one block of SHB caller points: what an update compares to find changed points.
 constexpr int SHB = 4096;
-// (r05: the pixels are not compared: they go to the device whole every load, ba_obs_gather; a changed
-// pixel changes no order or group, so only the observation counts and cameras can dirty a bucket)
 struct Shadow {
     std::vector<int> cnt, oc;       // observations per point; their cameras
+    std::vector<double> xy;         // their pixels
     bool valid = false;
 };
 struct HostScratch {
@@ -1617,7 +1611,8 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
             const int o0 = p0 < P ? v.start[p0] : O, o1 = p1 > p0 ? v.start[p1] : o0;
             bool same = (int)S.oc.size() == o1 - o0;
             for (int p = p0; same && p < p1; ++p) same = S.cnt[p - p0] == v.start[p + 1] - v.start[p];
-            same = same && std::memcmp(S.oc.data(), pb->obs_cam + o0, sizeof(int) * (size_t)(o1 - o0)) == 0;
+            same = same && std::memcmp(S.oc.data(), pb->obs_cam + o0, sizeof(int) * (size_t)(o1 - o0)) == 0 &&
+                   std::memcmp(S.xy.data(), pb->obs_xy + 2 * (size_t)o0, 16 * (size_t)(o1 - o0)) == 0;
             if (same) { bchanged[k] = 0; return; }
         }
         // point by point (old contents from the shadow when it is valid)
@@ -1631,7 +1626,8 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
             bool same = now && before;
             if (same) {
                 const int i = p - p0, n = v.start[p + 1] - v.start[p];
-                same = S.cnt[i] == n && std::memcmp(S.oc.data() + soff[i], pb->obs_cam + v.start[p], sizeof(int) * n) == 0;
+                same = S.cnt[i] == n && std::memcmp(S.oc.data() + soff[i], pb->obs_cam + v.start[p], sizeof(int) * n) == 0 &&
+                       std::memcmp(S.xy.data() + 2 * (size_t)soff[i], pb->obs_xy + 2 * (size_t)v.start[p], 16 * (size_t)n) == 0;
             }
             if (same) continue;
             if (incremental && p < Pold) mark.push_back(hs.pbucket[p]);
@@ -1896,6 +1892,7 @@ void host_setup(const sfmx_ba_problem* pb, int K, int gpts, bool incremental, Ho
         S.cnt.resize(p1 - p0);
         for (int p = p0; p < p1; ++p) S.cnt[p - p0] = v.start[p + 1] - v.start[p];
         S.oc.assign(pb->obs_cam + o0, pb->obs_cam + o1);
+        S.xy.assign(pb->obs_xy + 2 * (size_t)o0, pb->obs_xy + 2 * (size_t)o1);
     });
     hs.sh.resize(nblk);
     hs.P = P; hs.K = K; hs.kb = kb.kb; hs.gpts = gpts;
@@ -2044,36 +2041,11 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
         c->plan_pending = true;
         c->plan_th->submit([c, C] { sfmx::ba::make_plan(C, c->plan_pre_adj, c->plan_pre_mode, c->plan_pre); });
     };
-    // the caller's pixels go up whole, in the caller's order, while the host orders the points (r05):
-    // ba_obs_gather puts them in the internal order on the device, so the host neither compares nor
-    // gathers pixels (r04: 24 MB compared against a shadow copy per call, the redone buckets gathered)
-    HIPCHK(hipStreamSynchronize(c->st));   // (nothing may still read the pixel staging)
-    if (O) {
-        const size_t nb = 16 * (size_t)O;
-        if (c->xy_stage_cap < nb) {
-            if (c->xy_stage) (void)hipHostFree(c->xy_stage);
-            c->xy_stage = nullptr;
-            c->xy_stage_cap = 0;
-            if (hipHostMalloc(reinterpret_cast<void**>(&c->xy_stage), nb + nb / 4, hipHostMallocDefault) != hipSuccess) {
-                c->xy_stage = nullptr;
-                return fail(SFMX_ENOMEM, "pinned staging buffer");
-            }
-            c->xy_stage_cap = nb + nb / 4;
-        }
-        const char* src = reinterpret_cast<const char*>(caller->obs_xy);
-        sfmx::parallel_ranges((int64_t)nb, nb >= ((size_t)1 << 18) ? 16 : 1, [&](int64_t b0, int64_t b1) {
-            std::memcpy(c->xy_stage + b0, src + b0, (size_t)(b1 - b0));
-        });
-        RC(c->raw_xy.alloc(nb));
-        HIPCHK(hipMemcpyAsync(c->raw_xy.p, c->xy_stage, nb, hipMemcpyHostToDevice, c->st));
-    }
-    const double t_pix = ms_since(t_start);
     host_setup(caller, K, gpts, incremental && !force_fresh, hs, c->pperm, nullptr, on_covis);
     c->operm.clear();
     Topology& tp = hs.tp;
     const std::vector<int>& pt_start = hs.pt_start;
-    c->setup_ms[5] = ms_since(t_start) - t_pix;
-    c->setup_ms[20] = t_pix;
+    c->setup_ms[5] = ms_since(t_start);
     c->setup_ms[7] = validate_ms;
     for (int i = 0; i < 8; ++i) c->setup_ms[8 + i] = hs.tm[i];
     c->setup_ms[16] = c->setup_ms[17] = 0.0;
@@ -2160,12 +2132,11 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
                        r(4 * tp.cref_start.size()) + r(4 * tp.cref.size()) + r(4 * pim_h.size()) +
                        r(sizeof(double2) * pcc_h.size()) + r(24 * (size_t)P + 48 * (size_t)C + 8 * (size_t)K) + 4096;
         for (const Bucket& B : hs.bk)
-            if (B.dirty || B.io0 < 0) total += r(4 * (size_t)B.no) + 2 * r(2 * (size_t)B.no);
-        total += r(4 * (size_t)P) + r(4 * (size_t)(P + 1)) + (hs.view.pm ? 0 : r(4 * (size_t)O));   // gather maps
+            if (B.dirty || B.io0 < 0) total += r(16 * (size_t)B.no) + r(4 * (size_t)B.no) + 2 * r(2 * (size_t)B.no);
         RC(stage_reserve(c, total));
     }
     const size_t so = std::max<size_t>(O, 1);
-    if ((rc = c->obs_xy.alloc(16 * so)) || (rc = c->obs_cam_b.alloc(4 * so)) || (rc = c->obs_lc_b.alloc(2 * so)) ||
+    if ((rc = c->obs_xy_b.alloc(16 * so)) || (rc = c->obs_cam_b.alloc(4 * so)) || (rc = c->obs_lc_b.alloc(2 * so)) ||
         (rc = c->obs_row_b.alloc(2 * so)))
         return bail(rc);
     if (!moves.empty()) {
@@ -2175,26 +2146,38 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
         RC(c->moves.alloc(sizeof(ObsMove) * moves.size()));
         HIPCHK(hipMemcpyAsync(c->moves.p, h, sizeof(ObsMove) * moves.size(), hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(ba_relayout, dim3((unsigned)moves.size()), dim3(256), 0, st, c->moves.as<ObsMove>(),
-                           c->obs_cam.as<int>(), c->obs_lc.as<short>(), c->obs_row.as<short>(),
-                           c->obs_cam_b.as<int>(), c->obs_lc_b.as<short>(), c->obs_row_b.as<short>());
+                           c->obs_xy.as<double2>(), c->obs_cam.as<int>(), c->obs_lc.as<short>(), c->obs_row.as<short>(),
+                           c->obs_xy_b.as<double2>(), c->obs_cam_b.as<int>(), c->obs_lc_b.as<short>(), c->obs_row_b.as<short>());
         HIPCHK(hipGetLastError());
     }
-    {   // the redone buckets' observation records (cameras, local cameras, feature rows)
+    {   // the redone buckets: pixels gathered from the caller's array while copied into pinned staging
+        const double2* xy = reinterpret_cast<const double2*>(caller->obs_xy);
+        const View& v = hs.view;
         for (const Bucket& B : hs.bk) {
             if ((!B.dirty && B.io0 >= 0) || B.no == 0) continue;
+            double2* h = static_cast<double2*>(stage_bytes(c, 16 * (size_t)B.no));
             int* hc = static_cast<int*>(stage_bytes(c, 4 * (size_t)B.no));
             short* hl = static_cast<short*>(stage_bytes(c, 2 * (size_t)B.no));
             short* hr = static_cast<short*>(stage_bytes(c, 2 * (size_t)B.no));
-            if (!hc || !hl || !hr) return bail(fail(SFMX_ENOMEM, "pinned staging buffer"));
+            if (!h || !hc || !hl || !hr) return bail(fail(SFMX_ENOMEM, "pinned staging buffer"));
             const int64_t o0 = B.io0_new;
+            const int np = (int)B.cpts.size();
+            sfmx::parallel_ranges(np, B.no >= 8192 ? 16 : 1, [&](int64_t j0, int64_t j1) {   // caller order
+                for (int64_t j = j0; j < j1; ++j) {
+                    const int p = B.cpts[j];
+                    for (int a = v.start[p], k = B.lpt[B.rank[j]]; a < v.start[p + 1]; ++a, ++k) h[k] = xy[v.obs(a)];
+                }
+            });
             std::memcpy(hc, B.roc.data(), 4 * (size_t)B.no);
             std::memcpy(hl, B.lc.data(), 2 * (size_t)B.no);
             std::memcpy(hr, B.row.data(), 2 * (size_t)B.no);
+            HIPCHK(hipMemcpyAsync(c->obs_xy_b.as<double2>() + o0, h, 16 * (size_t)B.no, hipMemcpyHostToDevice, st));
             HIPCHK(hipMemcpyAsync(c->obs_cam_b.as<int>() + o0, hc, 4 * (size_t)B.no, hipMemcpyHostToDevice, st));
             HIPCHK(hipMemcpyAsync(c->obs_lc_b.as<short>() + o0, hl, 2 * (size_t)B.no, hipMemcpyHostToDevice, st));
             HIPCHK(hipMemcpyAsync(c->obs_row_b.as<short>() + o0, hr, 2 * (size_t)B.no, hipMemcpyHostToDevice, st));
         }
     }
+    std::swap(c->obs_xy, c->obs_xy_b);
     std::swap(c->obs_cam, c->obs_cam_b);
     std::swap(c->obs_lc, c->obs_lc_b);
     std::swap(c->obs_row, c->obs_row_b);
@@ -2206,20 +2189,11 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
     up.add(c->grp, tp.grp); up.add(c->chk, tp.chk); up.add(c->bat, tp.bat); up.add(c->gcam, tp.gcam);
     up.add(c->lcrow, tp.lcrow); up.add(c->tasks, tp.tasks); up.add(c->ents, tp.ents); up.add(c->cref_start, tp.cref_start);
     up.add(c->cref, tp.cref); up.add(c->pim, pim_h); up.add(c->pcc, pcc_h);
-    if (hs.view.pm) {   // ba_obs_gather's maps: internal -> caller point and the caller's point starts
-        up.add(c->dperm, c->pperm);
-        up.add(c->dvstart, hs.view.start);
-    } else {            // (not point-major: the caller observation of every internal one)
-        build_operm(hs, O, c->operm);
-        up.add(c->domap, c->operm);
-    }
     const auto t_topo = clk::now();
     if ((rc = up.flush(c, c->topo_arena))) return bail(rc);
     c->setup_ms[19] = ms_since(t_topo);
-    if (P && O) {   // the observations' points (from the CSR) and pixels (from the caller's copy)
-        hipLaunchKernelGGL(ba_obs_gather, dim3(nblk(P)), dim3(256), 0, st, P, c->pt_start.as<int>(), c->dperm.as<int>(),
-                           c->dvstart.as<int>(), hs.view.pm ? nullptr : c->domap.as<int>(), c->raw_xy.as<double2>(),
-                           c->obs_point.as<int>(), c->obs_xy.as<double2>());
+    if (P && O) {
+        hipLaunchKernelGGL(ba_obs_point, dim3(nblk(P)), dim3(256), 0, st, P, c->pt_start.as<int>(), c->obs_point.as<int>());
         HIPCHK(hipGetLastError());
     }
 

@@ -229,7 +229,7 @@ ORDER_AUTO, ORDER_NATURAL, ORDER_ND = -1, 0, 1
 # include/sfmx_ba.h sfmx_ba_setup_ms: ms unless noted
 SETUP_NAMES = ["order_groups", "alloc", "upload", "plan", "total", "host_setup", "buckets_redone", "validate",
                "h_view", "h_compare", "h_bucket_lists", "h_order_groups", "h_layout", "h_merge", "h_tasks", "h_shadows",
-               "plan_host", "stream_wait", "params_upload", "topology_upload", "pixels_upload"]
+               "plan_host", "stream_wait", "params_upload", "topology_upload"]
 
 
 def factor_plan(adj: np.ndarray, order: int = ORDER_AUTO) -> dict:

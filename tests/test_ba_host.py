@@ -130,7 +130,7 @@ def test_incremental_layout_equals_fresh_on_edits(case):
     rng = np.random.default_rng(11)
     a = synth.ba_sfm_order(synth.ba_problem(60, 8000, seed=12))
     b = dict(a)
-    if case == "xy":            # a few pixels re-measured: the layout is unchanged (pixels are gathered on the device)
+    if case == "xy":            # a few pixels re-measured: their buckets redone
         xy = np.array(a["obs_xy"]); xy[rng.integers(0, len(xy), 5)] += 0.25; b["obs_xy"] = xy
     elif case == "points_gone":  # the last points dropped
         keep = a["obs_point"] < 7000
@@ -146,5 +146,5 @@ def test_incremental_layout_equals_fresh_on_edits(case):
     n_dirty, n_all = _inc_check(a, b)
     if case == "same":
         assert n_dirty == 0
-    if case == "xy":   # r05: pixels go to the device whole every load (ba_obs_gather); they dirty no bucket
-        assert n_dirty == 0
+    if case == "xy":
+        assert 1 <= n_dirty <= 5
