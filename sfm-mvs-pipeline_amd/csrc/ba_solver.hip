@@ -266,9 +266,9 @@ int stage_reserve(sfmx_ba_ctx* c, size_t n) {
 struct UploadSet {
     struct Part { Buf* dst; const void* src; size_t bytes; std::vector<char> own; };
     std::vector<Part> parts;
-    template <class T>
-    void add(Buf& dst, const std::vector<T>& v, bool copy = false) {
-        Part pt{&dst, v.data(), sizeof(T) * v.size(), {}};
+    template <class V>
+    void add(Buf& dst, const V& v, bool copy = false) {
+        Part pt{&dst, v.data(), sizeof(v[0]) * v.size(), {}};
         if (copy) {
             pt.own.assign(reinterpret_cast<const char*>(v.data()), reinterpret_cast<const char*>(v.data()) + pt.bytes);
             pt.src = pt.own.data();
@@ -1092,6 +1092,20 @@ void radix_sort_keys(std::pair<uint64_t, int>* kp, size_t n, int bits) {
 // Point groups, chunks, local cameras, assembly task lists and camera slot lists (see ba_group.hpp).
 struct TopoSeg;
 struct PairRef { uint64_t key; int g, la, lb; };   // finish_topology: one (camera a, camera b) block of a group
+// A vector whose resize() leaves new elements of trivial types uninitialised (r05: the merged topology
+// is resized and then filled in parallel; value-initialising ~3 MB of assembly entries first was a
+// serial memset on every load)
+template <class T, class A = std::allocator<T>>
+struct uninit_alloc : A {
+    template <class U> struct rebind { using other = uninit_alloc<U, typename std::allocator_traits<A>::template rebind_alloc<U>>; };
+    using A::A;
+    template <class U> void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) { ::new (static_cast<void*>(p)) U; }
+    template <class U, class... Args> void construct(U* p, Args&&... args) {
+        std::allocator_traits<A>::construct(static_cast<A&>(*this), p, std::forward<Args>(args)...);
+    }
+};
+template <class T> using uvec = std::vector<T, uninit_alloc<T>>;
+
 struct Topology {   // kept with the context: its vectors keep their capacity between calls
     std::vector<PairRef> pr, pr_out;   // finish_topology's scratch (kept: no per-call allocation)
     std::vector<int> pr_cnt, slot_g;
@@ -1101,13 +1115,14 @@ struct Topology {   // kept with the context: its vectors keep their capacity be
     // points connects: on the C5 ring the unions add ~150 such pairs, the elimination tree gets one level
     // more and 82 instead of 66 nonzero tiles, r04)
     std::vector<uint64_t> covis;
-    std::vector<Grp> grp;
-    std::vector<Chunk> chk;
-    std::vector<Batch> bat;
-    std::vector<int> gcam, cref_start, cref, lcrow;
+    uvec<Grp> grp;
+    uvec<Chunk> chk;
+    uvec<Batch> bat;
+    uvec<int> gcam, lcrow;
+    std::vector<int> cref_start, cref;
     std::vector<short> obs_lc, obs_row;
-    std::vector<ATask> tasks;
-    std::vector<AEnt> ents;
+    uvec<ATask> tasks;
+    uvec<AEnt> ents;
     long long sg_total = 0, h_total = 0;
     int rg_total = 0, dp_max = 16;
     void clear() {
@@ -1290,7 +1305,8 @@ bool covisible(const Topology& tp, int C, int a, int b) {
 // entries; the pieces are concatenated in camera order.  The same tasks and entries as one serial pass.)
 constexpr int TOPO_PIECES = 16;
 struct TaskPiece {
-    std::vector<PairRef> pr, out;
+    std::vector<PairRef> pr;
+    uvec<PairRef> out;
     std::vector<int> cnt;
     std::vector<ATask> tasks;
     std::vector<AEnt> ents;
@@ -1348,7 +1364,7 @@ void finish_topology(int C, int K, Topology& tp) {
         for (size_t i = 1; i < P.cnt.size(); ++i) P.cnt[i] += P.cnt[i - 1];
         P.out.resize(P.pr.size());
         for (const PairRef& x : P.pr) P.out[P.cnt[idx(x)]++] = x;
-        const std::vector<PairRef>& pr = P.out;
+        const uvec<PairRef>& pr = P.out;
         for (size_t i = 0; i < pr.size();) {
             ATask tk{0, (int)(pr[i].key >> 32), (int)(pr[i].key & 0xffffffffu), (int)P.ents.size(), 0, 0, 0, 0};
             size_t j = i;
