@@ -1563,7 +1563,7 @@ struct Bucket {
     bool dirty = true;
 };
 // Caller-order copy of one block of SHB caller points: what an update compares to find changed points.
-constexpr int SHB = 4096;
+constexpr int SHB = 1024;   // (r05: 4096 before; finer work items for the compare and the shadow copies)
 struct Shadow {
     std::vector<int> cnt, oc;       // observations per point; their cameras
     std::vector<double> xy;         // their pixels
