@@ -2655,6 +2655,25 @@ int sfmx_ba_debug_incremental_check(const sfmx_ba_problem* a, const sfmx_ba_prob
 }
 #endif
 
+#ifdef SFMX_DIAG
+// diagnostic build only: the workgroups per CU the two launches whose occupancy is held by
+// design actually get on this device: out[0] ba_gupdate<K> with its GUPDATE_LDS request (4: its static
+// LDS + 33 KiB must keep 5 from fitting 160 KiB), out[1] ba_glin<K> at glin_lds(K) (2).
+int sfmx_ba_debug_occupancy(int32_t K, int32_t* out) {
+    if (!out || (K != 1 && K != 3 && K != 7)) return fail(SFMX_EINVAL, "K must be 1, 3 or 7");
+    const void* gu = K == 1 ? (const void*)ba_gupdate<1> : K == 3 ? (const void*)ba_gupdate<3> : (const void*)ba_gupdate<7>;
+    const void* gl = K == 1 ? (const void*)ba_glin<1, false> : K == 3 ? (const void*)ba_glin<3, false> : (const void*)ba_glin<7, false>;
+    int a = 0, b = 0;
+    const size_t lds = glin_lds(K);
+    (void)hipFuncSetAttribute(gl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, gu, 256, GUPDATE_LDS));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gl, 256, lds));
+    out[0] = a;
+    out[1] = b;
+    return SFMX_OK;
+}
+#endif
+
 #ifdef SFMX_BA_STAMPS
 // diagnostic build only: read and clear the phase cycle totals (ba_group.hpp BA_STAMP)
 int sfmx_ba_debug_stamps(unsigned long long* out, int32_t n) {

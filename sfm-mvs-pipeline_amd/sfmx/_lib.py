@@ -132,6 +132,7 @@ PROTOTYPES = {
     "sfmx_ba_debug_adjacency": (C.c_int, [_P(sfmx_ba_problem), C.c_int32, _vp]),   # diagnostic library only
     "sfmx_ba_debug_incremental_check": (C.c_int, [_P(sfmx_ba_problem), _P(sfmx_ba_problem), C.c_int32, _i32p,
                                                   _P(C.c_double)]),   # diagnostic library only
+    "sfmx_ba_debug_occupancy": (C.c_int, [C.c_int32, _i32p]),   # diagnostic library only
     "sfmx_ba_jacobian": (C.c_int, [_P(sfmx_ba_problem), C.c_int32, _vp, _vp, _vp, _vp]),
     "sfmx_ba_plan": (C.c_int, [C.c_int32, _vp, C.c_int32, _P(sfmx_ba_plan_info), _i32p, _i32p, C.c_int32, _i32p,
                                C.c_int32, _i32p, C.c_int32]),

@@ -448,3 +448,16 @@ def test_incremental_updates_keep_buckets_and_equal_fresh_contexts():
     # 48 cameras in buckets of 4 (BUCKET_CAMS): 11-12 buckets; one new camera dirties the two buckets
     # holding the points it adds observations to (sfmx_ba_debug_incremental_check on CPU: 2, 2)
     assert redone[1] <= 2 and redone[2] <= 2 and redone[4] <= 2, redone
+
+
+def test_held_occupancies_on_this_device():
+    """ba_gupdate is held at 4 workgroups per CU by an unused dynamic LDS request
+    (GUPDATE_LDS; 5 measured slower) and the group sizing assumes 2 ba_glin workgroups per CU.
+    Nothing at compile time ties the request to ba_gupdate's static LDS: a grown static part would
+    drop it to 3 (measured slower) silently.  The device's own occupancy query, per border width."""
+    import ctypes as C
+    from diag import diag_lib
+    for K in (1, 3, 7):
+        out = (C.c_int32 * 2)()
+        assert diag_lib().sfmx_ba_debug_occupancy(K, out) == 0, diag_lib().sfmx_last_error()
+        assert list(out) == [4, 2], (K, list(out))
