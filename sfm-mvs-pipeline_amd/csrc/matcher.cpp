@@ -189,6 +189,19 @@ struct sfmx_matcher {
     hipStream_t sx = nullptr, sp = nullptr;
     hipEvent_t ov_ev[3] = {nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> bev;
+    // r05: device-resident descriptors (set_images_device) are not waited on for their integrality:
+    // the run assumes every image integral (SIFT descriptors always are) and the assumption is checked
+    // when results are read (fetch / stats / device_results); a non-integral image then gets its fp32
+    // rows and the last run is re-run on the exact paths.  The host no longer waits mid-step.
+    bool flags_pending = false;
+    unsigned flags_want = 0;
+    hipStream_t flags_stream = nullptr;
+    std::vector<const void*> last_src;     // the device descriptors of the last set_images_device
+    std::vector<int> last_cols;
+    bool run_spec = false;                 // the last run assumed integrality not yet confirmed
+    std::vector<int32_t> last_pairs;
+    double last_ratio = 0.0;
+    int last_distinct = 0, last_min_count = 0;
 };
 
 namespace {
@@ -205,6 +218,7 @@ int check_device(int dev) {
 }
 
 int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hipStream_t st, bool device_src) {
+    if (m) m->flags_pending = m->run_spec = false;   // (a pending check of earlier images is moot now)
     if (!m || (n > 0 && !imgs) || n < 0) return fail(SFMX_EINVAL, "null matcher/images");
     if (norm != SFMX_NORM_L2 && norm != SFMX_NORM_HAMMING) return fail(SFMX_EINVAL, "norm must be SFMX_NORM_L2 or SFMX_NORM_HAMMING");
     const int want_type = norm == SFMX_NORM_L2 ? SFMX_32F : SFMX_8U;
@@ -300,7 +314,15 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
         unsigned* hseq = reinterpret_cast<unsigned*>(m->hflags + m->hflags_cap);
         const unsigned want = ++m->flag_seq;
         HIPCHK(launch_publish_flags(m->flags.as<int32_t>(), n, m->hflags, hseq, want, st));
-        for (unsigned spins = 1;; ++spins) {   // the host needs the flags to plan the run
+        if (device_src) {   // (see flags_pending) every image integral until the flags say otherwise
+            m->flags_pending = true;
+            m->flags_want = want;
+            m->flags_stream = st;
+            m->last_src = src;
+            m->last_cols.resize(n);
+            for (int i = 0; i < n; ++i) m->last_cols[i] = imgs[i].cols;
+        }
+        for (unsigned spins = 1; !device_src; ++spins) {   // host buffers: the flags before the run is planned
             if (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == want) break;
             if ((spins & 255) == 0) {
                 const hipError_t e = hipStreamQuery(st);
@@ -311,7 +333,7 @@ int set_images_impl(sfmx_matcher* m, const sfmx_desc* imgs, int n, int norm, hip
             __builtin_ia32_pause();
         }
         const int32_t* fl = m->hflags;
-        for (int i = 0; i < n; ++i) {
+        for (int i = 0; i < n && !device_src; ++i) {
             m->imgs[i].integral = fl[i] ? 0 : 1;
             m->any_nonintegral |= fl[i] != 0;
         }
@@ -533,7 +555,57 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     m->n_pairs = n_pairs;
     m->dense_total = dense;
     m->has_run = true;
+    m->run_spec = m->flags_pending;
+    if (m->run_spec) {   // what a re-run on the exact paths needs (resolve_flags)
+        m->last_pairs.assign(pairs, pairs + 2 * (size_t)n_pairs);
+        m->last_ratio = ratio;
+        m->last_distinct = distinct;
+        m->last_min_count = min_count;
+    }
     return SFMX_OK;
+}
+
+// The integrality check of set_images_device, deferred to the first read of results (flags_pending):
+// wait for the published flags (long since written); if an image is not integral, give every image
+// its fp32 rows, mark the images, and re-run the last run, whose int8 results assumed integrality.
+int resolve_flags(sfmx_matcher* m) {
+    if (!m->flags_pending) return SFMX_OK;
+    const hipStream_t st = m->flags_stream;
+    const int n = m->n_imgs;
+    unsigned* hseq = reinterpret_cast<unsigned*>(m->hflags + m->hflags_cap);
+    for (unsigned spins = 1;; ++spins) {
+        if (__atomic_load_n(hseq, __ATOMIC_ACQUIRE) == m->flags_want) break;
+        if ((spins & 255) == 0) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e != hipSuccess && e != hipErrorNotReady) return fail(SFMX_EDEVICE, std::string("integrality flags: ") + hipGetErrorString(e));
+            if (e == hipSuccess && __atomic_load_n(hseq, __ATOMIC_ACQUIRE) != m->flags_want)
+                return fail(SFMX_EINTERNAL, "integrality flags: stream drained without the flag handoff");
+        }
+        __builtin_ia32_pause();
+    }
+    m->flags_pending = false;
+    const int32_t* fl = m->hflags;
+    bool any = false;
+    for (int i = 0; i < n; ++i) any |= fl[i] != 0;
+    if (!any) { m->run_spec = false; return SFMX_OK; }   // the assumption held
+    m->any_nonintegral = true;
+    for (int i = 0; i < n; ++i) m->imgs[i].integral = fl[i] ? 0 : 1;
+    int rc;
+    if ((rc = m->f32.ensure((size_t)m->total_rows * SIFT_DIM * 4))) return rc;
+    for (int i = 0; i < n; ++i) {
+        const ImgDev& d = m->imgs[i];
+        HIPCHK(launch_prep_f32((const float*)m->last_src[i], d.rows, m->last_cols[i], d.rows_pad,
+                               m->f32.as<float>() + d.row0 * SIFT_DIM, st));
+    }
+    if ((rc = m->stage_imgs.ensure(sizeof(ImgDev) * n))) return rc;
+    std::memcpy(m->stage_imgs.p, m->imgs.data(), sizeof(ImgDev) * n);
+    HIPCHK(hipMemcpyAsync(m->imgs_d.p, m->stage_imgs.p, sizeof(ImgDev) * n, hipMemcpyHostToDevice, st));
+    if ((rc = m->stage_imgs.copied(st))) return rc;
+    m->plan_valid = false;
+    if (!m->run_spec) return SFMX_OK;
+    m->run_spec = false;
+    const std::vector<int32_t> pairs = m->last_pairs;
+    return run_impl(m, pairs.data(), (int)(pairs.size() / 2), m->last_ratio, m->last_distinct, m->last_min_count, st);
 }
 
 int fetch_impl(sfmx_matcher* m, sfmx_dmatch* out, int64_t cap, int64_t* required, int64_t* pair_offsets,
@@ -541,6 +613,7 @@ int fetch_impl(sfmx_matcher* m, sfmx_dmatch* out, int64_t cap, int64_t* required
     if (!m) return fail(SFMX_EINVAL, "null matcher");
     if (!m->has_run) return fail(SFMX_ESTATE, "fetch before run");
     DeviceGuard g(m->device);
+    { const int rc_ = resolve_flags(m); if (rc_) return rc_; }
     std::vector<int64_t> off(m->n_pairs + 1);
     int32_t unsettled = 0;
     HIPCHK(hipMemcpyAsync(off.data(), m->offsets.p, sizeof(int64_t) * (m->n_pairs + 1), hipMemcpyDeviceToHost, st));
@@ -651,6 +724,10 @@ int sfmx_matcher_device_results(sfmx_matcher* m, const sfmx_dmatch** matches, co
                                 const int32_t** keep) {
     if (!m) return fail(SFMX_EINVAL, "null matcher");
     if (!m->has_run) return fail(SFMX_ESTATE, "no results before run");
+    {
+        DeviceGuard g(m->device);
+        { const int rc_ = resolve_flags(m); if (rc_) return rc_; }
+    }
     if (matches) *matches = m->out.as<const sfmx_dmatch>();
     if (pair_offsets) *pair_offsets = m->offsets.as<const int64_t>();
     if (keep) *keep = m->keep.as<const int32_t>();
@@ -661,6 +738,7 @@ int sfmx_matcher_stats(sfmx_matcher* m, int64_t* slow_queries, int64_t* fp32_pai
     if (!m) return fail(SFMX_EINVAL, "null matcher");
     if (!m->has_run) return fail(SFMX_ESTATE, "no stats before run");
     DeviceGuard g(m->device);
+    { const int rc_ = resolve_flags(m); if (rc_) return rc_; }
     int32_t sc = 0, unsettled = 0;
     HIPCHK(hipMemcpyAsync(&sc, m->slow_count.p, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
     HIPCHK(hipMemcpyAsync(&unsettled, m->unsettled.p, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));

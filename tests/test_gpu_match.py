@@ -234,6 +234,54 @@ def test_device_resident_inputs():
     assert_same(got, off, d["matches"], d["offsets"])
 
 
+def test_device_inputs_non_integral_rerun_on_read():
+    """r05: set_images_device no longer waits for the integrality flags (the run assumes integral SIFT
+    rows, the check happens when results are read).  A non-integral image there must still give the
+    oracle's exact result: fetch, stats and device_results each re-run the last run on the fp32 path
+    (every pair touching the image); a later integral batch in the same matcher runs on int8 again;
+    two runs before one fetch: the last one's results."""
+    import torch
+    from oracle import oracle
+    rng = np.random.default_rng(19)
+    imgs = [synth.sift_images(1, 400, seed=5)[0], rng.random((300, 128), dtype=np.float32) * 50,
+            synth.sift_images(1, 350, seed=6)[0]]
+    pairs = sfmx.pairs_unordered(3)
+    em, eoff = oracle.match_pairs(imgs, pairs)
+    em2, eoff2 = oracle.match_pairs(imgs, pairs, 0.9)
+    s = torch.cuda.current_stream().cuda_stream
+    ts = [torch.from_numpy(x).cuda() for x in imgs]
+    m = sfmx.BFMatcher(sfmx.NORM_L2)
+    try:
+        for first in ("fetch", "stats", "device"):
+            m.set_images_device(ts, stream=s)
+            m.run(pairs, 0.9, stream=s)          # superseded by the next run
+            m.run(pairs, stream=s)
+            if first == "stats":
+                assert m.stats(stream=s)[1] == 2  # the two pairs with image 1 on the fp32 path
+            elif first == "device":
+                mp, op, _ = m.device_results()   # resolves (re-runs) before it hands out the pointers
+
+                class _View:
+                    def __init__(self, ptr, n):
+                        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 3}
+                torch.cuda.synchronize()
+                dev = torch.as_tensor(_View(mp, 16 * int(eoff[-1])), device="cuda").cpu().numpy()
+                assert dev.tobytes() == em.tobytes()
+            got, off, _ = m.fetch(stream=s)
+            assert_same(got, off, em, eoff)
+            assert m.stats(stream=s)[1] == 2
+        # an integral batch after it: the int8 path again, exact
+        ok = [torch.from_numpy(x).cuda() for x in (imgs[0], imgs[2])]
+        m.set_images_device(ok, stream=s)
+        m.run(np.array([[0, 1]], np.int32), 0.9, stream=s)
+        got, off, _ = m.fetch(stream=s)
+        e3, eo3 = oracle.match_pairs([imgs[0], imgs[2]], np.array([[0, 1]], np.int32), 0.9)
+        assert_same(got, off, e3, eo3)
+        assert m.stats(stream=s)[1] == 0
+    finally:
+        m.close()
+
+
 def test_errors():
     m = sfmx.BFMatcher(sfmx.NORM_L2)
     with pytest.raises(ValueError):
