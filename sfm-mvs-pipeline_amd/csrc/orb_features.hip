@@ -92,6 +92,16 @@ __constant__ int c_pattern[256 * 4] = {
 
 __device__ __forceinline__ int round_f(float v) { return __float2int_rn(v); }   // cvRound(float)
 
+// [t0, t1) of n items for this workgroup: contiguous ranges, the workgroups that share an XCD (blocks
+// b, b + 8, ... under round-robin dispatch) given adjacent ranges (speed only, never correctness)
+__device__ __forceinline__ void xcd_range(int n, int& t0, int& t1) {
+    const int nwg = gridDim.x, b = blockIdx.x, q = nwg >> 3, r = nwg & 7, x = b & 7;
+    const int rb = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+    const int per = (n + nwg - 1) / nwg;
+    t0 = min(n, rb * per);
+    t1 = min(n, t0 + per);
+}
+
 // ------------------------------------------------------------------ pyramid
 // resize(prev, level, INTER_LINEAR_EXACT): horizontal 8.8 taps, then vertical taps,
 // (sum + 2^15) >> 16; rows/columns outside [dmin, dmax) replicate the edge source
@@ -783,7 +793,7 @@ __device__ float fast_atan2(float y, float x) {   // cv::fastAtan2
 __global__ __launch_bounds__(256)
 void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int nl,
                       const int* __restrict__ row_off, int rows, int* __restrict__ stats, const int* __restrict__ umax,
-                      const Resp* __restrict__ kin, Kp* __restrict__ out, int64_t istride) {
+                      const Resp* __restrict__ kin, const int* __restrict__ sidx, Kp* __restrict__ out, int64_t istride) {
     const int lane = threadIdx.x & 63;
     {
         const int64_t bo = (int64_t)blockIdx.y * istride;
@@ -791,6 +801,7 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         row_off = at(row_off, bo);
         stats += (int64_t)blockIdx.y * CS;
         kin = at(kin, bo);
+        sidx = at(sidx, bo);
         out = at(out, bo);
     }
     __shared__ int sumax[HALF_PATCH + 1], lbase[MAX_LEVELS + 1], lfirst[MAX_LEVELS];
@@ -825,8 +836,11 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         wrow[k] = r - HALF_PATCH;
         wum[k] = wok[k] ? sumax[wrow[k] < 0 ? -wrow[k] : wrow[k]] : 0;
     }
-    const int total = lbase[nl];   // the kept keypoints (orb_keep_kernel), in output order
-    for (int f = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5); f < total; f += gridDim.x * 8) {
+    const int total = lbase[nl];   // the kept keypoints (orb_keep_kernel), walked in sidx's row order
+    int t0, t1;
+    xcd_range(total, t0, t1);
+    for (int ts = t0 + (threadIdx.x >> 6) * 2 + (lane >> 5); ts < t1; ts += 8) {
+        const int f = sidx[ts];
         int l = 0;
         while (f >= lbase[l + 1]) ++l;
         const Lvl L = lv[l];
@@ -915,6 +929,49 @@ void orb_keep_kernel(const Lvl* __restrict__ lv, const int* __restrict__ row_off
     }
     if (t == 0) stats[ST_KCNT + l] = base;
 }
+
+// r05: the kept keypoints' processing order for the angle and rBRIEF passes.  Both
+// read a patch around every keypoint; in the kept (retainBest) order the patches of consecutive
+// keypoints are scattered over the level, so every patch row came from the MALL / HBM again (the
+// angle pass fetched ~2 KB per keypoint).  sidx lists the kept keypoints (their output indices f)
+// bucketed by level row (SB buckets of whole rows per level, one workgroup per (level, image)); the
+// two passes walk it in contiguous ranges per workgroup, the ranges of one XCD adjacent (xcd_range), so
+// neighbouring patches share L2 lines.  Only the order of the work changes: every output is written
+// to its keypoint's own slot, bit-identical.
+constexpr int SB = 2048;
+__global__ __launch_bounds__(RT)
+void orb_sort_kernel(const Lvl* __restrict__ lv, const int* __restrict__ row_off, const int* __restrict__ stats,
+                     const Resp* __restrict__ kin, int* __restrict__ sidx, int64_t istride) {
+    __shared__ int cnt[SB];
+    __shared__ int sh[36];
+    const int l = blockIdx.x, t = threadIdx.x;
+    {
+        const int64_t bo = (int64_t)blockIdx.y * istride;
+        row_off = at(row_off, bo);
+        stats += (int64_t)blockIdx.y * CS;
+        kin = at(kin, bo);
+        sidx = at(sidx, bo);
+    }
+    const Lvl L = lv[l];
+    const int m = stats[ST_KCNT + l], c0 = lvl_first(row_off, L);
+    int base = 0;
+    for (int q = 0; q < l; ++q) base += stats[ST_KCNT + q];
+    const int rb = (L.h + SB - 1) / SB;   // rows per bucket
+    for (int b = t; b < SB; b += RT) cnt[b] = 0;
+    __syncthreads();
+    for (int i = t; i < m; i += RT) atomicAdd(&cnt[(kin[c0 + i].idx >> 16) / rb], 1);
+    __syncthreads();
+    int a = cnt[2 * t], b2 = cnt[2 * t + 1];   // (SB = 2 RT) exclusive scan of the bucket counts
+    const int s0 = a + b2;
+    int pre = s0, dummy = 0;
+    scan2(pre, dummy, sh);
+    __syncthreads();
+    cnt[2 * t] = base + pre;
+    cnt[2 * t + 1] = base + pre + a;
+    __syncthreads();
+    for (int i = t; i < m; i += RT) sidx[atomicAdd(&cnt[(kin[c0 + i].idx >> 16) / rb], 1)] = base + i;
+}
+static_assert(SB == 2 * RT, "two buckets per thread in the scan");
 
 __global__ __launch_bounds__(256)
 void orb_copy_kp_kernel(const Kp* __restrict__ src, const int* __restrict__ st, const ImgIO* __restrict__ io,
@@ -1047,11 +1104,13 @@ constexpr int BW = 18;                 // window half-size
 constexpr int BWR = 2 * BW + 1, BWC = 80;   // (80-byte rows: 20 banks apart, not 16 -- fewer conflicts)
 __global__ __launch_bounds__(256)
 void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ lv, const Kp* __restrict__ kps,
-                      const int* __restrict__ st, const ImgIO* __restrict__ io, int64_t istride) {
+                      const int* __restrict__ sidx, const int* __restrict__ st, const ImgIO* __restrict__ io,
+                      int64_t istride) {
     __shared__ __align__(16) uint8_t win[8][BWR * BWC];
     const int g = blockIdx.y;
     blur = at(blur, (int64_t)g * istride);
     kps = at(kps, (int64_t)g * istride);
+    sidx = at(sidx, (int64_t)g * istride);
     uint8_t* desc = io[g].desc_out;
     if (!desc) return;   // this image's caller passed no descriptor buffer
     const int n = min(st[(int64_t)g * CS], io[g].capacity), i = threadIdx.x & 31, slot = threadIdx.x >> 5;
@@ -1062,7 +1121,13 @@ void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ 
         pxf[e] = (float)c_pattern[2 * (16 * i + e)];
         pyf[e] = (float)c_pattern[2 * (16 * i + e) + 1];
     }
-    for (int j = blockIdx.x * 8 + slot; j < n; j += gridDim.x * 8) {
+    // the kept keypoints in sidx's row order (orb_sort_kernel), contiguous per workgroup; the first
+    // min(count, capacity) of the output order are described
+    int t0, t1;
+    xcd_range(st[(int64_t)g * CS], t0, t1);
+    for (int ts = t0 + slot; ts < t1; ts += 8) {
+        const int j = sidx[ts];
+        if (j >= n) continue;
         const Kp k = kps[j];
         const Lvl L = lv[k.octave];
         float angle = k.angle;
@@ -1454,14 +1519,16 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
                                                            (int)CAND_CAP, sst + 3, istride);
             orb_keep_kernel<<<dim3(nl, gz), RT, 0, st>>>(dlv, row_off, rA, rB, stats, cpos, width, height, border, kin,
                                                          istride);
+            int* sidx = sLs;   // (the retain kernels' scratch is free from here: the processing order)
+            orb_sort_kernel<<<dim3(nl, gz), RT, 0, st>>>(dlv, row_off, stats, kin, sidx, istride);
             orb_angle_kernel<<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rows, stats, dumax, kin,
-                                                                          dfin, istride);
+                                                                          sidx, dfin, istride);
             // ---- compute(): blur of the levels used, rBRIEF of min(count, capacity) keypoints
             if (descriptors && capmax > 0) {
                 orb_blur_kernel<<<dim3(flat_tiles<BT_X, BT_Y>(lv), gz), 256, 0, st>>>(
                     pyr, dlv, sst, blur, nl, istride);
                 orb_brief_kernel<<<dim3(std::min(G > 1 ? 1024 : 4096, (capmax + 7) / 8), gz), 256, 0, st>>>(blur, dlv, dfin,
-                                                                                                          sst, dio, istride);
+                                                                                                          sidx, sst, dio, istride);
             }
             if (inputs_on_device && capmax > 0)
                 orb_copy_kp_kernel<<<dim3(std::min(1024, (capmax + 255) / 256), gz), 256, 0, st>>>(dfin, sst, dio, istride);
