@@ -43,6 +43,7 @@
 
 #include "../../include/sfmx.h"
 #include "../../include/sfmx_features.h"
+#include "diag.hpp"
 #include "match_common.hpp"
 
 namespace sfmx {
@@ -801,7 +802,7 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         row_off = at(row_off, bo);
         stats += (int64_t)blockIdx.y * CS;
         kin = at(kin, bo);
-        sidx = at(sidx, bo);
+        if (sidx) sidx = at(sidx, bo);
         out = at(out, bo);
     }
     __shared__ int sumax[HALF_PATCH + 1], lbase[MAX_LEVELS + 1], lfirst[MAX_LEVELS];
@@ -837,10 +838,17 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         wum[k] = wok[k] ? sumax[wrow[k] < 0 ? -wrow[k] : wrow[k]] : 0;
     }
     const int total = lbase[nl];   // the kept keypoints (orb_keep_kernel), walked in sidx's row order
-    int t0, t1;
-    xcd_range(total, t0, t1);
-    for (int ts = t0 + (threadIdx.x >> 6) * 2 + (lane >> 5); ts < t1; ts += 8) {
-        const int f = sidx[ts];
+    int t0, t1, tstep = 8;
+    if (sidx) {
+        xcd_range(total, t0, t1);
+        t0 += (threadIdx.x >> 6) * 2 + (lane >> 5);
+    } else {   // (diagnostic A/B: the kept order, strided over the grid, as r04)
+        t0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+        t1 = total;
+        tstep = gridDim.x * 8;
+    }
+    for (int ts = t0; ts < t1; ts += tstep) {
+        const int f = sidx ? sidx[ts] : ts;
         int l = 0;
         while (f >= lbase[l + 1]) ++l;
         const Lvl L = lv[l];
@@ -1110,7 +1118,7 @@ void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ 
     const int g = blockIdx.y;
     blur = at(blur, (int64_t)g * istride);
     kps = at(kps, (int64_t)g * istride);
-    sidx = at(sidx, (int64_t)g * istride);
+    if (sidx) sidx = at(sidx, (int64_t)g * istride);
     uint8_t* desc = io[g].desc_out;
     if (!desc) return;   // this image's caller passed no descriptor buffer
     const int n = min(st[(int64_t)g * CS], io[g].capacity), i = threadIdx.x & 31, slot = threadIdx.x >> 5;
@@ -1123,10 +1131,17 @@ void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ 
     }
     // the kept keypoints in sidx's row order (orb_sort_kernel), contiguous per workgroup; the first
     // min(count, capacity) of the output order are described
-    int t0, t1;
-    xcd_range(st[(int64_t)g * CS], t0, t1);
-    for (int ts = t0 + slot; ts < t1; ts += 8) {
-        const int j = sidx[ts];
+    int t0, t1, tstep = 8;
+    if (sidx) {
+        xcd_range(st[(int64_t)g * CS], t0, t1);
+        t0 += slot;
+    } else {   // (diagnostic A/B: the output order, strided over the grid, as r04)
+        t0 = blockIdx.x * 8 + slot;
+        t1 = n;
+        tstep = gridDim.x * 8;
+    }
+    for (int ts = t0; ts < t1; ts += tstep) {
+        const int j = sidx ? sidx[ts] : ts;
         if (j >= n) continue;
         const Kp k = kps[j];
         const Lvl L = lv[k.octave];
@@ -1520,7 +1535,8 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             orb_keep_kernel<<<dim3(nl, gz), RT, 0, st>>>(dlv, row_off, rA, rB, stats, cpos, width, height, border, kin,
                                                          istride);
             int* sidx = sLs;   // (the retain kernels' scratch is free from here: the processing order)
-            orb_sort_kernel<<<dim3(nl, gz), RT, 0, st>>>(dlv, row_off, stats, kin, sidx, istride);
+            if (SFMX_DIAG_ENV("SFMX_ORB_KEPT_ORDER")) sidx = nullptr;   // A/B: the r04 order
+            if (sidx) orb_sort_kernel<<<dim3(nl, gz), RT, 0, st>>>(dlv, row_off, stats, kin, sidx, istride);
             orb_angle_kernel<<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rows, stats, dumax, kin,
                                                                           sidx, dfin, istride);
             // ---- compute(): blur of the levels used, rBRIEF of min(count, capacity) keypoints
