@@ -139,17 +139,27 @@ def main():
         return
 
     primary = bench_match(args.workload, args, rank, world, local)
+
+    def leg(fn, *a):
+        # a secondary leg that fails leaves an error in its place, never the headline line unprinted
+        # (the N-rank paths of the secondary legs have run only in the gloo rehearsal)
+        try:
+            return fn(*a)
+        except Exception as e:   # pragma: no cover
+            import traceback
+            traceback.print_exc()
+            return {"error": f"{type(e).__name__}: {e}"[:300]}
     orb = c3 = None
     if args.workload == "sift" and not args.no_orb:
-        orb = bench_match("orb", args, rank, world, local)
+        orb = leg(bench_match, "orb", args, rank, world, local)
     if args.workload == "sift" and not args.no_c3:
-        c3 = bench_match("c3", args, rank, world, local)
-    ba_res = None if args.no_ba else bench_ba(args, rank, world, local)
-    if ba_res is not None and world == 1 and not args.no_ba_calls:
-        ba_res["calls"] = bench_ba_calls(args)
-    mvs_res = None if args.no_mvs else bench_mvs(args, rank, world, local)
-    feat_res = None if args.no_features else bench_features(args, rank, world, local)
-    orbf_res = None if args.no_orb_features else bench_features_orb(args, rank, world, local)
+        c3 = leg(bench_match, "c3", args, rank, world, local)
+    ba_res = None if args.no_ba else leg(bench_ba, args, rank, world, local)
+    if ba_res is not None and "error" not in ba_res and world == 1 and not args.no_ba_calls:
+        ba_res["calls"] = leg(bench_ba_calls, args)
+    mvs_res = None if args.no_mvs else leg(bench_mvs, args, rank, world, local)
+    feat_res = None if args.no_features else leg(bench_features, args, rank, world, local)
+    orbf_res = None if args.no_orb_features else leg(bench_features_orb, args, rank, world, local)
     if rank == 0:
         full = {k: v for k, v in primary.items() if not k.startswith("_")}
         if orb is not None:
@@ -218,6 +228,8 @@ def leg_summary(leg):
     """<= LEG_MAX_BYTES: value, frac, cpu_baseline value, parity bool."""
     if leg is None:
         return None
+    if "error" in leg:
+        return {"error": str(leg["error"])[:300]}
     rf = leg.get("roofline") or {}
     s = {"value": leg.get("value"), "unit": leg.get("unit")}
     for k in ("ms_per_step", "ms_per_image", "ms_per_shot"):
@@ -280,13 +292,16 @@ def compact_line(full, detail=None):
         if full.get(name) is not None:
             legs[name] = leg_summary(full[name])
     ba = full.get("ba")
-    if ba is not None:
+    if ba is not None and "error" in ba:
+        legs["ba"] = leg_summary(ba)
+    elif ba is not None:
         s = leg_summary(ba)
         s.update(_r({"iterations": ba.get("iterations"), "final_cost": ba.get("final_cost"),
                      "termination": ba.get("termination")}, 7))
         legs["ba"] = s
         if ba.get("calls"):
-            legs["ba_calls"] = ba_calls_summary(ba["calls"])
+            legs["ba_calls"] = ({"error": str(ba["calls"]["error"])[:300]} if "error" in ba["calls"]
+                                else ba_calls_summary(ba["calls"]))
     for name in ("homography", "find_3d2d"):
         if full.get(name) is not None:
             legs[name] = leg_summary(full[name])

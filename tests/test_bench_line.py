@@ -74,3 +74,14 @@ def test_write_detail_side_file(tmp_path, monkeypatch):
     full = _full()
     rel = bench.write_detail(full)
     assert rel is not None and json.loads(p.read_text())["ba"]["calls"]["calls"] == full["ba"]["calls"]["calls"]
+
+
+def test_failed_legs_leave_an_error_not_a_missing_line():
+    full = _full()
+    full["ba"] = {"error": "SfmxError: ncclCommInitRank: unhandled system error"}
+    full["mvs"] = {"error": "RuntimeError: x" * 100}
+    line = bench.compact_line(full)
+    assert line["legs"]["ba"]["error"].startswith("SfmxError")
+    assert len(line["legs"]["mvs"]["error"]) <= 300
+    assert "ba_calls" not in line["legs"]
+    assert len(json.dumps(line)) <= bench.LINE_MAX_BYTES and line["roofline"]["frac"] is not None
