@@ -1543,8 +1543,12 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             if (descriptors && capmax > 0) {
                 orb_blur_kernel<<<dim3(flat_tiles<BT_X, BT_Y>(lv), gz), 256, 0, st>>>(
                     pyr, dlv, sst, blur, nl, istride);
+                // rBRIEF keeps the output order strided over the grid: in the row order its counter traffic
+                // fell 37 -> 7.6 MB per image but the kernel took 181 instead of 159 us per 16 images (r05j
+                // A/B, profiles/r05j_ab_orb_order.txt: it is not bandwidth-bound); the angle pass keeps it
+                int* bsidx = SFMX_DIAG_ENV("SFMX_ORB_BRIEF_SORTED") ? sidx : nullptr;
                 orb_brief_kernel<<<dim3(std::min(G > 1 ? 1024 : 4096, (capmax + 7) / 8), gz), 256, 0, st>>>(blur, dlv, dfin,
-                                                                                                          sidx, sst, dio, istride);
+                                                                                                          bsidx, sst, dio, istride);
             }
             if (inputs_on_device && capmax > 0)
                 orb_copy_kp_kernel<<<dim3(std::min(1024, (capmax + 255) / 256), gz), 256, 0, st>>>(dfin, sst, dio, istride);
