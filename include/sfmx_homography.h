@@ -53,7 +53,10 @@ typedef struct sfmx_point2f {
  * (n_keypoints, image_size, pairs) stay host.  out_ratio is always host memory.
  * A queryIdx / trainIdx outside its image's keypoints returns SFMX_EINVAL
  * (host inputs) or yields ratio NaN for that pair (device inputs, checked in
- * the kernel).
+ * the kernel).  Device inputs are not read back: a pair list of more than 2048
+ * matches must lie inside [0, sum over pairs of n_keypoints[left]) of the
+ * offsets (at most one match per query keypoint, as the matcher writes them),
+ * else its ratio is NaN.
  * Replaces: SfM::calculateHomography, SfM.cpp:599-637. */
 int sfmx_homography_ratios(const sfmx_point2f* const* keypoints, const int32_t* n_keypoints, int32_t n_imgs,
                            const int32_t* image_size, const int32_t* pairs, int32_t n_pairs,

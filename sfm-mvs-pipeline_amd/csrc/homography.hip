@@ -25,6 +25,7 @@
 #include <cfloat>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -205,8 +206,8 @@ constexpr int BATCH = 64;   // hypotheses per round (the first round draws 16)
 __global__ __launch_bounds__(256)
 void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_t* __restrict__ nkp,
                               const PairH* __restrict__ pairs, const DMatchDev* __restrict__ matches,
-                              const int64_t* __restrict__ off, float4* __restrict__ scratch, int max_iters,
-                              double confidence, double* __restrict__ out) {
+                              const int64_t* __restrict__ off, float4* __restrict__ scratch, int64_t scratch_cap,
+                              int max_iters, double confidence, double* __restrict__ out) {
     __shared__ float4 pts[CAP];
     __shared__ int sub[BATCH][4];
     __shared__ float hf[BATCH][8];
@@ -217,6 +218,10 @@ void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_
     const int n = (int)(off[p + 1] - o0);
     if (n < 4) {
         if (tid == 0) out[p] = -1.0;
+        return;
+    }
+    if (n > CAP && (o0 < 0 || o0 + n > scratch_cap)) {   // (device inputs: a list past the scratch bound)
+        if (tid == 0) out[p] = __builtin_nan("");
         return;
     }
     const PairH P = pairs[p];
@@ -341,16 +346,21 @@ void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_
 
 thread_local float g_last_ms = -1.f;
 
-struct Bufs {
-    std::vector<void*> ptrs;
-    ~Bufs() { for (void* q : ptrs) (void)hipFree(q); }
-    void* alloc(size_t bytes) {
-        void* q = nullptr;
-        if (hipMalloc(&q, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
-        ptrs.push_back(q);
-        return q;
-    }
+// Per device, kept between calls (r05): the device check's result, one device block for the call's
+// tables / outputs / scratch (regrown with headroom), pinned staging for the small uploads and the
+// ratios, two timing events.  r04 made ~7 hipMalloc / hipFree pairs, a device-properties query, a D2H
+// of the pair offsets and pageable copies per call: twice the kernel's time around a 0.3 ms kernel.
+struct Slot {
+    bool checked = false;
+    char* dev = nullptr;
+    size_t dev_cap = 0;
+    char* pin = nullptr;
+    size_t pin_cap = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
 };
+Slot g_slot[64];
+std::mutex g_mu;
+size_t r256(size_t b) { return (std::max<size_t>(b, 1) + 255) & ~(size_t)255; }
 
 }  // namespace homog
 }  // namespace sfmx
@@ -377,12 +387,19 @@ int sfmx_homography_ratios(const sfmx_point2f* const* keypoints, const int32_t* 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { set_last_error("no HIP device visible"); return SFMX_EDEVICE; }
     if (device < 0 || device >= ndev) { set_last_error("device index out of range"); return SFMX_EINVAL; }
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-        set_last_error("sfmx kernels are built for gfx950 only");
-        return SFMX_EDEVICE;
+    if (device >= 64) { set_last_error("device index out of range"); return SFMX_EINVAL; }
+    std::lock_guard<std::mutex> lock(g_mu);
+    Slot& S = g_slot[device];
+    if (!S.checked) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            set_last_error("sfmx kernels are built for gfx950 only");
+            return SFMX_EDEVICE;
+        }
+        S.checked = true;
     }
     std::vector<PairH> ph(n_pairs);
+    int64_t bound = 0;   // device inputs: the scratch bound (at most one match per query keypoint)
     for (int p = 0; p < n_pairs; ++p) {
         const int L = pairs[2 * p], R = pairs[2 * p + 1];
         if (L < 0 || L >= n_imgs || R < 0 || R >= n_imgs) { set_last_error("pair image index out of range"); return SFMX_EINVAL; }
@@ -390,6 +407,7 @@ int sfmx_homography_ratios(const sfmx_point2f* const* keypoints, const int32_t* 
                                          : std::max({image_size[2 * L], image_size[2 * L + 1], image_size[2 * R + 1],
                                                      image_size[2 * R + 1]}) * threshold;   // SfM.cpp:615-619
         ph[p] = PairH{L, R, thr};
+        bound += std::max(n_keypoints[L], 0);
     }
     int prev = -1;
     (void)hipGetDevice(&prev);
@@ -397,16 +415,8 @@ int sfmx_homography_ratios(const sfmx_point2f* const* keypoints, const int32_t* 
     const hipStream_t st = (hipStream_t)stream;
     int rc = SFMX_OK;
     {
-        Bufs b;
-        std::vector<int64_t> hoff;
-        const int64_t* doff = pair_offsets;
-        int64_t total = 0;
-        if (inputs_on_device) {
-            hoff.resize(n_pairs + 1);
-            if (hipMemcpyAsync(hoff.data(), pair_offsets, sizeof(int64_t) * (n_pairs + 1), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess) { rc = SFMX_EDEVICE; goto done; }
-            total = hoff[n_pairs];
-        } else {
+        int64_t total = bound, nk = 0;
+        if (!inputs_on_device) {
             total = pair_offsets[n_pairs];
             for (int p = 0; p < n_pairs; ++p) {
                 if (pair_offsets[p + 1] < pair_offsets[p]) { set_last_error("pair offsets not ascending"); rc = SFMX_EINVAL; goto done; }
@@ -419,28 +429,67 @@ int sfmx_homography_ratios(const sfmx_point2f* const* keypoints, const int32_t* 
                         goto done;
                     }
             }
+            for (int i = 0; i < n_imgs; ++i) nk += n_keypoints[i];
         }
         {
-            std::vector<const float2*> kptr(std::max(n_imgs, 1));
+            // device block: [keypoint table | counts | pairs | ratios | scratch | (host inputs: keypoints,
+            // matches, offsets)]; the first three parts staged back to back and copied up at once
+            const size_t b_kp = r256(sizeof(float2*) * std::max(n_imgs, 1)), b_nk = r256(sizeof(int32_t) * std::max(n_imgs, 1)),
+                         b_ph = r256(sizeof(PairH) * n_pairs), b_out = r256(sizeof(double) * n_pairs),
+                         b_scr = r256(sizeof(float4) * std::max<int64_t>(total, 1));
+            const size_t b_kd = inputs_on_device ? 0 : r256(sizeof(float2) * nk),
+                         b_md = inputs_on_device ? 0 : r256(sizeof(sfmx_dmatch) * total),
+                         b_od = inputs_on_device ? 0 : r256(sizeof(int64_t) * (n_pairs + 1));
+            const size_t need = b_kp + b_nk + b_ph + b_out + b_scr + b_kd + b_md + b_od;
+            if (S.dev_cap < need) {
+                if (S.dev) (void)hipFree(S.dev);
+                S.dev = nullptr;
+                S.dev_cap = 0;
+                if (hipMalloc(reinterpret_cast<void**>(&S.dev), need + need / 4) != hipSuccess) {
+                    S.dev = nullptr;
+                    (void)hipGetLastError();
+                    rc = SFMX_ENOMEM;
+                    goto done;
+                }
+                S.dev_cap = need + need / 4;
+            }
+            const size_t need_pin = b_kp + b_nk + b_ph + b_out;
+            if (S.pin_cap < need_pin) {
+                if (S.pin) (void)hipHostFree(S.pin);
+                S.pin = nullptr;
+                S.pin_cap = 0;
+                if (hipHostMalloc(reinterpret_cast<void**>(&S.pin), need_pin + need_pin / 4, hipHostMallocDefault) != hipSuccess) {
+                    S.pin = nullptr;
+                    rc = SFMX_ENOMEM;
+                    goto done;
+                }
+                S.pin_cap = need_pin + need_pin / 4;
+            }
+            if (!S.e0 && (hipEventCreate(&S.e0) != hipSuccess || hipEventCreate(&S.e1) != hipSuccess)) { rc = SFMX_EDEVICE; goto done; }
+            char* d = S.dev;
+            const float2** kpd = reinterpret_cast<const float2**>(d);
+            int32_t* nkd = reinterpret_cast<int32_t*>(d + b_kp);
+            PairH* phd = reinterpret_cast<PairH*>(d + b_kp + b_nk);
+            double* outd = reinterpret_cast<double*>(d + b_kp + b_nk + b_ph);
+            float4* scr = reinterpret_cast<float4*>(d + b_kp + b_nk + b_ph + b_out);
+            char* hx = d + b_kp + b_nk + b_ph + b_out + b_scr;
+            const float2** hk = reinterpret_cast<const float2**>(S.pin);
+            const int64_t* doff = pair_offsets;
             if (inputs_on_device) {
-                for (int i = 0; i < n_imgs; ++i) kptr[i] = reinterpret_cast<const float2*>(keypoints[i]);
-            } else {
-                int64_t nk = 0;
-                for (int i = 0; i < n_imgs; ++i) nk += n_keypoints[i];
-                auto* kd = static_cast<float2*>(b.alloc(sizeof(float2) * nk));
-                if (!kd) { rc = SFMX_ENOMEM; goto done; }
+                for (int i = 0; i < n_imgs; ++i) hk[i] = reinterpret_cast<const float2*>(keypoints[i]);
+            } else {   // host inputs: keypoints, matches and offsets go up (pageable copies)
+                float2* kd = reinterpret_cast<float2*>(hx);
+                auto* md = reinterpret_cast<sfmx_dmatch*>(hx + b_kd);
+                auto* od = reinterpret_cast<int64_t*>(hx + b_kd + b_md);
                 int64_t o = 0;
                 for (int i = 0; i < n_imgs; ++i) {
                     if (n_keypoints[i] &&
                         hipMemcpyAsync(kd + o, keypoints[i], sizeof(float2) * n_keypoints[i], hipMemcpyHostToDevice, st) != hipSuccess) {
                         rc = SFMX_EDEVICE; goto done;
                     }
-                    kptr[i] = kd + o;
+                    hk[i] = kd + o;
                     o += n_keypoints[i];
                 }
-                auto* md = static_cast<sfmx_dmatch*>(b.alloc(sizeof(sfmx_dmatch) * total));
-                auto* od = static_cast<int64_t*>(b.alloc(sizeof(int64_t) * (n_pairs + 1)));
-                if (!md || !od) { rc = SFMX_ENOMEM; goto done; }
                 if ((total && hipMemcpyAsync(md, matches, sizeof(sfmx_dmatch) * total, hipMemcpyHostToDevice, st) != hipSuccess) ||
                     hipMemcpyAsync(od, pair_offsets, sizeof(int64_t) * (n_pairs + 1), hipMemcpyHostToDevice, st) != hipSuccess) {
                     rc = SFMX_EDEVICE; goto done;
@@ -448,36 +497,27 @@ int sfmx_homography_ratios(const sfmx_point2f* const* keypoints, const int32_t* 
                 matches = md;
                 doff = od;
             }
-            auto* kpd = static_cast<const float2**>(b.alloc(sizeof(float2*) * kptr.size()));
-            auto* nkd = static_cast<int32_t*>(b.alloc(sizeof(int32_t) * std::max(n_imgs, 1)));
-            auto* phd = static_cast<PairH*>(b.alloc(sizeof(PairH) * n_pairs));
-            auto* scr = static_cast<float4*>(b.alloc(sizeof(float4) * std::max<int64_t>(total, 1)));
-            auto* outd = static_cast<double*>(b.alloc(sizeof(double) * n_pairs));
-            if (!kpd || !nkd || !phd || !scr || !outd) { rc = SFMX_ENOMEM; goto done; }
-            hipEvent_t e0 = nullptr, e1 = nullptr;
-            if (hipMemcpyAsync(kpd, kptr.data(), sizeof(float2*) * kptr.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
-                hipMemcpyAsync(nkd, n_keypoints, sizeof(int32_t) * n_imgs, hipMemcpyHostToDevice, st) != hipSuccess ||
-                hipMemcpyAsync(phd, ph.data(), sizeof(PairH) * n_pairs, hipMemcpyHostToDevice, st) != hipSuccess ||
-                hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
-                rc = SFMX_EDEVICE; goto done;
-            }
-            (void)hipEventRecord(e0, st);
+            std::memcpy(S.pin + b_kp, n_keypoints, sizeof(int32_t) * n_imgs);
+            std::memcpy(S.pin + b_kp + b_nk, ph.data(), sizeof(PairH) * n_pairs);
+            double* hout = reinterpret_cast<double*>(S.pin + b_kp + b_nk + b_ph);
+            if (hipMemcpyAsync(d, S.pin, b_kp + b_nk + b_ph, hipMemcpyHostToDevice, st) != hipSuccess) { rc = SFMX_EDEVICE; goto done; }
+            (void)hipEventRecord(S.e0, st);
             homography_ransac_kernel<<<n_pairs, 256, 0, st>>>(kpd, nkd, phd, reinterpret_cast<const DMatchDev*>(matches),
-                                                              doff, scr, max_iters, confidence, outd);
-            (void)hipEventRecord(e1, st);
+                                                              doff, scr, std::max<int64_t>(total, 1), max_iters, confidence, outd);
+            (void)hipEventRecord(S.e1, st);
             if (hipGetLastError() != hipSuccess ||
-                hipMemcpyAsync(out_ratio, outd, sizeof(double) * n_pairs, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(hout, outd, sizeof(double) * n_pairs, hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess) {
                 rc = SFMX_EDEVICE;
             } else {
+                std::memcpy(out_ratio, hout, sizeof(double) * n_pairs);
                 float ms = -1.f;
-                (void)hipEventElapsedTime(&ms, e0, e1);
+                (void)hipEventElapsedTime(&ms, S.e0, S.e1);
                 g_last_ms = ms;
             }
-            (void)hipEventDestroy(e0);
-            (void)hipEventDestroy(e1);
         }
     done:;
+        if (rc != SFMX_OK) (void)hipStreamSynchronize(st);   // nothing in flight from the pinned staging
     }
     if (rc == SFMX_EDEVICE) set_last_error("HIP error in sfmx_homography_ratios");
     if (rc == SFMX_ENOMEM) set_last_error("device allocation failed");

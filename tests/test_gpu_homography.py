@@ -52,3 +52,23 @@ def test_invalid_index_rejected():
     m["trainIdx"][5] = 10 ** 6
     with pytest.raises(ValueError):
         homography.homography_ratios(kps, sizes, pairs, m, off)
+
+
+def test_device_list_past_the_scratch_bound_is_nan():
+    # device inputs are not read back: the scratch for lists over 2048 matches is sized from the
+    # host-known keypoint counts (one match per query keypoint); a list past that bound is NaN, the
+    # same list from the host is solved (sfmx_homography.h)
+    kps, sizes, pairs, m, off = homog_cases.scene_case(5, 1500, seed=6)
+    l = int(pairs[0][0])
+    n = max(len(kps[l]) + 600, 2100)
+    mm = np.resize(m[off[0]:off[1]], n)
+    one = np.asarray(pairs[:1])
+    o = np.array([0, n], np.int64)
+    host = homography.homography_ratios(kps, sizes, one, mm, o)
+    assert np.isfinite(host[0])
+    dk = [torch.from_numpy(k).cuda() for k in kps]
+    dm = torch.from_numpy(mm.view(np.uint8)).cuda()
+    do = torch.from_numpy(o).cuda()
+    dev = homography.homography_ratios_device([t.data_ptr() for t in dk], [len(k) for k in kps], sizes, one,
+                                              dm.data_ptr(), do.data_ptr())
+    assert np.isnan(dev[0])
