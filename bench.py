@@ -53,7 +53,7 @@ FP64_PEAK_TFLOPS = 256 * 128 * 2.4e9 / 1e12
 # BA algorithmic work per LM iteration at C5: S assembly ~2-2.5 + J ~0.4 +
 # Cholesky ~0.58 GFLOP; bytes: obs read twice, points, S written and read
 BA_FLOP_PER_ITER_C5, BA_BYTES_PER_ITER_C5 = 3.0e9, 0.1e9
-FEAT_PMC_FILE = "r04n_pmc_features.json"   # tools/pmc_feat.sh -> tools/pmc_feat_json.py (r04n session)
+FEAT_PMC_FILE = "r05u_pmc_features.json"   # tools/pmc_feat.sh -> tools/pmc_feat_json.py (SIFT r05i, ORB r05u sessions)
 BA_PMC_FILE = "r04r_pmc_ba.json"   # tools/pmc_ba.sh -> tools/pmc_ba_json.py (r04r session)
 
 
@@ -1038,15 +1038,16 @@ def _orb_level_px(h, w, nlevels=8, sf=1.2):
 
 
 def _orb_pyramid_bytes(h, w, nlevels=8, sf=1.2):
-    """Algorithmic HBM bytes of one image's ORB pass as the product runs it since r04 (fused FAST + NMS
-    tile pass): the caller's image read once (1 B per level-0 pixel); every level
-    written once (1 B/px) and read by the next level's resize (1), the FAST + NMS tile pass (1), the
-    angle pass (1) and the blur (1); the blurred level written (1) and read by rBRIEF (1) -- 7 B per
-    level pixel + the input.  Keep bits, corner / keypoint records and descriptors are < 1 %.  (The
-    angle and rBRIEF reads touch only the patches around keypoints; counting every level pixel once
-    makes this an upper bound of the algorithmic bytes, so the fraction is not flattered.)"""
+    """Algorithmic HBM bytes of one image's ORB pass as the product runs it since r05 (one tile pass for
+    FAST + NMS + compute()'s blur, DESIGN.md §8d): the caller's image read once (1 B per level-0 pixel);
+    every level written once (1 B/px) and read by the next level's resize (1), the FAST + NMS + blur
+    tile pass (1) and the angle pass (1); the blurred level written (1) and read by rBRIEF (1) -- 6 B
+    per level pixel + the input (r04's separate blur pass read every level once more: 7 B, kept as
+    `frac_r04`).  Keep bits, corner / keypoint records and descriptors are < 1 %.  (The angle and rBRIEF
+    reads touch only the patches around keypoints; counting every level pixel once makes this an
+    upper bound of the algorithmic bytes, so the fraction is not flattered.)"""
     px = _orb_level_px(h, w, nlevels, sf)
-    return 7.0 * sum(px) + 1.0 * px[0]
+    return 6.0 * sum(px) + 1.0 * px[0]
 
 
 def _orb_pyramid_bytes_r02(h, w, nlevels=8, sf=1.2):
@@ -1094,6 +1095,7 @@ def bench_features_orb(args, rank, world, local):
     pyr = _orb_pyramid_bytes(FEAT_H, FEAT_W)
     achieved = pyr * len(imgs) * steps / el_rank / 1e9
     achieved_r02 = _orb_pyramid_bytes_r02(FEAT_H, FEAT_W) * len(imgs) * steps / el_rank / 1e9
+    achieved_r04 = (pyr + sum(_orb_level_px(FEAT_H, FEAT_W))) * len(imgs) * steps / el_rank / 1e9
     res = {"metric": "images/s featurised (ORB detect + compute, SfM::extractFeatures)",
            "value": ORB_SHOTS * steps / el, "unit": "images/s", "ms_per_image": el_rank / (steps * len(imgs)) * 1e3,
            "kernel_ms_per_image": float(np.mean(kms)), "streams": FEAT_STREAMS,
@@ -1102,12 +1104,13 @@ def bench_features_orb(args, rank, world, local):
                       "parallelism": f"shot-sharded x{world}"},
            "data": "synthetic photos (sfmx.synth.gray_photo), two distinct photos, shifted copies",
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "frac_r02": achieved_r02 / HBM_PEAK_GBS,
+                        "frac": achieved / HBM_PEAK_GBS, "frac_r04": achieved_r04 / HBM_PEAK_GBS,
+                        "frac_r02": achieved_r02 / HBM_PEAK_GBS,
                         "traffic": feat_traffic("orb"),
                         "traffic_unit": f"HBM bytes per image (2 x FETCH_SIZE + WRITE_SIZE, profiles/{FEAT_PMC_FILE})",
                         "kernel": "ORB pipeline, wall time of the batch (every kernel of detect + compute, one host wait per chunk)",
-                        "algorithmic": f"{pyr / 1e6:.1f} MB per image: input + 7 B per level pixel of the fused "
-                                       f"pipeline (bench._orb_pyramid_bytes; r02's 8 B/px in frac_r02)"}}
+                        "algorithmic": f"{pyr / 1e6:.1f} MB per image: input + 6 B per level pixel of the fused "
+                                       f"pipeline (bench._orb_pyramid_bytes; r04's 7 B/px in frac_r04, r02's 8 in frac_r02)"}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()

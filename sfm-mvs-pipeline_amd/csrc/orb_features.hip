@@ -34,6 +34,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -103,6 +104,35 @@ __device__ __forceinline__ void xcd_range(int n, int& t0, int& t1) {
     t1 = min(n, t0 + per);
 }
 
+// The tile passes (resize, FAST + NMS, blur) read a halo around every tile: under round-robin
+// dispatch the tiles either side of a tile run on other XCDs, whose L2s each fetch the shared lines
+// again (from MALL or HBM; FETCH_SIZE counts both).  r05: xcd_grid remaps the grid's linear (x, y, z)
+// block order so that one XCD's workgroups take neighbouring blocks: run < 0, a contiguous 1/8 of the
+// grid per XCD (whole images); run > 0, runs of `run` consecutive blocks dealt to the XCDs in turn (the
+// remainder past the last full round of 8 runs keeps its place).  Speed only: every block still runs
+// exactly once.  Measured (r05m, one-stream traces, 16-image chunks): the halo passes' counter bytes
+// fall 2-4x either way, but the FAST + NMS pass took 312 (plain grid) / 319 (run < 0) / 331 us (runs of
+// 8 .. 128) and the separate blur 121 / 134 / 147 us: neither is bandwidth-bound and both keep the plain
+// grid (run = 0); the resize chain is unchanged (26.4 / 26.8 us a level) and rBRIEF, which reads
+// patches in the output order, gains (whole images per XCD: 159 -> 152 us, 37 -> 7 MB per image).
+__device__ __forceinline__ void xcd_grid(int run, int& bx, int& by, int& bz) {
+    bx = blockIdx.x; by = blockIdx.y; bz = blockIdx.z;
+    if (!run) return;
+    const int gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
+    const int b = bx + gx * (by + gy * bz), x = b & 7, k = b >> 3;
+    int lin = b;
+    if (run < 0) {
+        const int q = n >> 3, r = n & 7;
+        lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+    } else if (b < n / (8 * run) * (8 * run)) {
+        lin = ((k / run) * 8 + x) * run + k % run;
+    }
+    bx = lin % gx;
+    const int t = lin / gx;
+    by = t % gy;
+    bz = t / gy;
+}
+
 // ------------------------------------------------------------------ pyramid
 // resize(prev, level, INTER_LINEAR_EXACT): horizontal 8.8 taps, then vertical taps,
 // (sum + 2^15) >> 16; rows/columns outside [dmin, dmax) replicate the edge source
@@ -130,10 +160,12 @@ __device__ __forceinline__ int src_ofs(double scale, int v) { return (int)floor(
 // rectangle from the axis scales, so the tile's loads do not wait on the level table or the axis tables
 __global__ __launch_bounds__(256)
 void orb_resize_kernel(uint8_t* __restrict__ pyr, const Lvl D, const Lvl S, double sx, double sy,
-                       const AxisEnt* __restrict__ tables, int64_t istride) {
+                       const AxisEnt* __restrict__ tables, int64_t istride, int xcd) {
     __shared__ __align__(16) uint8_t T[RZ_R][RZ_C];
-    pyr = at(pyr, (int64_t)blockIdx.z * istride);
-    const int x0 = blockIdx.x * RZ_X, y0 = blockIdx.y * RZ_Y;
+    int tx, ty, tz;
+    xcd_grid(xcd, tx, ty, tz);
+    pyr = at(pyr, (int64_t)tz * istride);
+    const int x0 = tx * RZ_X, y0 = ty * RZ_Y;
     const int x = x0 + RZ_PX * (threadIdx.x & 15), yb = y0 + (threadIdx.x >> 4);   // rows yb + 16 r
     const AxisEnt* ax = tables + D.ax_off;
     const AxisEnt* ay = tables + D.ay_off;
@@ -246,6 +278,112 @@ int flat_tiles(const std::vector<Lvl>& lv) {
     return n;
 }
 
+// ------------------------------------------------------------------ compute()'s blur
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on the 8U level through OpenCV's
+// integer separable path: taps x 2^8, (sum + 2^15) >> 16, saturated.
+constexpr int BT_X = 64, BT_Y = 32, BR = 3, BT_H = BT_Y + 2 * BR;
+__constant__ int c_taps[7];
+
+__device__ __forceinline__ int reflect101(int p, int n) {
+    if (n == 1) return 0;
+    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+    return p;
+}
+
+// The blurred 64 x 32 tile (x0, y0) of level L (src / dst: the level's (0, 0) in the pyramid / blur slabs).
+// r04: 64 x 32 output tiles (halo rows 38 / 32 instead of 22 / 16); interior tiles load without the
+// reflection; the row pass makes 4 neighbouring sums per thread from a 10-byte window, the column pass 8
+// rows of one column from a 14-sum window (the same taps in the same order: the same integers).
+// r05: ti (optional) is the FAST pass's LDS image tile (rows y0 - 4 .., columns x0 - 16 .., row stride
+// TIC): an interior tile's rows come from there instead of a second read of the level.  r: BT_H x
+// (BT_X + 1) ints of LDS.  Two halves, a workgroup barrier between them (the caller's: a barrier waits
+// for the wave's outstanding global stores too, so the caller keeps its own stores after it).
+template <int TIC>
+__device__ __forceinline__ void blur_rows(const uint8_t* __restrict__ src, const Lvl& L, int x0, int y0,
+                                          const uint8_t* ti, int (*r)[BT_X + 1]) {
+    // Row pass (r04): each thread makes 4 neighbouring row sums from the 12 bytes x-4 .. x+7 of its
+    // row, read as 3 aligned 4-byte words (interior tiles) or gathered with the reflection (border
+    // tiles); per output the 7-byte window is two realigned words (v_alignbyte) dotted with the taps
+    // (v_dot4_u32_u8, the 8th tap 0).  Integer sums: the same values as the tap-by-tap form.  The
+    // byte tile in LDS it replaces cost bank conflicts and ~2x the VALU work (PMC r04h).
+    const bool interior = x0 >= 64 && x0 + BT_X + 4 <= L.pitch && x0 + BT_X + BR <= L.w && y0 >= BR && y0 + BT_Y + BR <= L.h;
+    const uint32_t T0 = (uint32_t)c_taps[0] | (uint32_t)c_taps[1] << 8 | (uint32_t)c_taps[2] << 16 | (uint32_t)c_taps[3] << 24;
+    const uint32_t T1 = (uint32_t)c_taps[4] | (uint32_t)c_taps[5] << 8 | (uint32_t)c_taps[6] << 16;
+    constexpr int ITEMS = BT_H * (BT_X / 4);
+#pragma unroll
+    for (int it = 0; it < (ITEMS + 255) / 256; ++it) {
+        const int i = threadIdx.x + 256 * it;
+        if (i < ITEMS) {
+            const int ty = i / (BT_X / 4), tx = 4 * (i % (BT_X / 4));
+            uint32_t wa, wb, wc;   // bytes x-4 .. x-1 | x .. x+3 | x+4 .. x+7 of the row, x = x0 + tx
+            if (interior && ti) {   // (a branch of its own: the loads stay LDS loads, not flat ones)
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(ti + (ty + 4 - BR) * TIC + tx + 12);
+                wa = q[0];
+                wb = q[1];
+                wc = q[2];
+            } else if (interior) {
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(src + (int64_t)(y0 + ty - BR) * L.pitch + x0 + tx - 4);
+                wa = q[0];
+                wb = q[1];
+                wc = q[2];
+            } else {
+                const uint8_t* row = src + (int64_t)reflect101(y0 + ty - BR, L.h) * L.pitch;
+                uint32_t wv[3] = {0u, 0u, 0u};
+#pragma unroll
+                for (int k = 1; k <= 10; ++k)   // (bytes 0 and 11 are never used)
+                    wv[k >> 2] |= (uint32_t)row[reflect101(x0 + tx - 4 + k, L.w)] << (8 * (k & 3));
+                wa = wv[0];
+                wb = wv[1];
+                wc = wv[2];
+            }
+            // output q: bytes 1+q .. 7+q
+            r[ty][tx + 0] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wc, wb, 1), T1,
+                                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wb, wa, 1), T0, 0u, false), false);
+            r[ty][tx + 1] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wc, wb, 2), T1,
+                                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wb, wa, 2), T0, 0u, false), false);
+            r[ty][tx + 2] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wc, wb, 3), T1,
+                                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wb, wa, 3), T0, 0u, false), false);
+            r[ty][tx + 3] = (int)__builtin_amdgcn_udot4(wc, T1, __builtin_amdgcn_udot4(wb, T0, 0u, false), false);
+        }
+    }
+}
+__device__ __forceinline__ void blur_cols(const Lvl& L, int x0, int y0, const int (*r)[BT_X + 1], uint8_t* __restrict__ dst) {
+    static_assert(BT_Y % 8 == 0 && (BT_X * BT_Y / 8) == 256, "one column strip of 8 rows per thread");
+    const int tx = threadIdx.x % BT_X, ty0 = 8 * (threadIdx.x / BT_X);
+    const int x = x0 + tx;
+    if (x < L.w) {
+        int w[14];
+#pragma unroll
+        for (int k = 0; k < 14; ++k) w[k] = r[ty0 + k][tx];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int y = y0 + ty0 + q;
+            if (y >= L.h) break;
+            int s = 0;
+#pragma unroll
+            for (int j = 0; j < 7; j++) s += c_taps[j] * w[q + j];
+            dst[(int64_t)y * L.pitch + x] = (uint8_t)min(max((s + (1 << 15)) >> 16, 0), 255);
+        }
+    }
+}
+
+// the separate blur pass (diagnostic A/B of the fused one: SFMX_ORB_BLUR_SEPARATE) -- only the levels the
+// kept keypoints use
+__global__ __launch_bounds__(256)
+void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const int* __restrict__ st,
+                     uint8_t* __restrict__ blur, int nl, int64_t istride, int xcd) {
+    int bx, g, bz;   // grid (flat 64 x 32 tiles of all levels, images)
+    xcd_grid(xcd, bx, g, bz);
+    int x0, y0;
+    const int l = flat_tile<BT_X, BT_Y>(lv, nl, bx, x0, y0);
+    if (l < 0 || l >= st[(int64_t)g * CS + 1]) return;
+    __shared__ int r[BT_H][BT_X + 1];
+    const Lvl L = lv[l];
+    blur_rows<0>(at(pyr, (int64_t)g * istride) + L.off, L, x0, y0, nullptr, r);
+    __syncthreads();
+    blur_cols(L, x0, y0, r, at(blur, (int64_t)g * istride) + L.off);
+}
+
 // ------------------------------------------------------------------ FAST 9/16 + NMS
 // r04: FAST and the 3x3 strict-maximum test in one tile pass.  A workgroup owns 64 x 32 pixels of
 // one level: the image tile (rows y0-4 .. y0+35, columns x0-16 .. x0+79) comes in as 16-byte
@@ -288,102 +426,137 @@ __device__ __forceinline__ int fast_score_lds(const uint8_t* c, int threshold) {
     return e > threshold ? e - 1 : 0;
 }
 
-// grid (flat 64 x 32 tiles of all levels, images).  kmask / wcnt: (global row) x mw, the words
-// [0, ceil(w / 64)) of every row of the level written (0 outside the border or without a corner).  Scores are 0
-// in FAST's own 3-pixel frame; a corner needs b <= x < w - b, b <= y < h - b (b = max(border, 3)),
-// a nonzero score and a score above all 8 neighbours'.
+// grid (flat 64 x 32 tiles of all levels in runs of `strip`, images).  kmask / wcnt: (global row) x mw,
+// the words [0, ceil(w / 64)) of every row of the level written (0 outside the border or without a
+// corner); score: the FAST score of every kept pixel (other pixels are not written).  Scores are 0 in
+// FAST's own 3-pixel frame; a corner needs b <= x < w - b, b <= y < h - b (b = max(border, 3)), a
+// nonzero score and a score above all 8 neighbours'.
+// r05: blur (optional: compute()'s blurred slab) -- the tile's 7x7 Gaussian from the same LDS image tile
+// (blur_rows / blur_cols), so the blur no longer reads the level a second time or launches a pass of its
+// own (r05s, 16-image chunks: FAST + NMS 259 us and blur 121 us -> 342 us together); only the kept
+// pixels' scores are stored.  The grid is dealt to the XCDs in contiguous ranges (xcd = -1: whole
+// images per XCD), so the lines a tile's halo shares with its neighbours come from the XCD's own L2:
+// the pass's counter fetch 14.3 -> 3.2 MB per image for ~2 % of its time (r05m, r05r).  (Also measured:
+// the kept scores packed per tile instead of the score map, 41 us per 16 images slower for 6 MB per
+// image less written, r05s; 2 or 4 tiles per workgroup in turn, 94 VGPRs and 30 % slower, r05t.)
+static_assert(BT_X == FT_X && BT_Y == FT_Y && BR < 4, "the blur tile is the FAST tile, its halo inside the image tile");
 __global__ __launch_bounds__(256)
 void orb_fast_nms_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int threshold, int border,
                          uint8_t* __restrict__ score, uint64_t* __restrict__ kmask, uint8_t* __restrict__ wcnt, int mw,
-                         int nl, int64_t istride) {
-    const int64_t bo = (int64_t)blockIdx.y * istride;   // y = image
-    int x0, y0;
-    const int lvl = flat_tile<FT_X, FT_Y>(lv, nl, blockIdx.x, x0, y0);
-    if (lvl < 0) return;
-    const Lvl L = lv[lvl];
-    const int ny = min(FT_Y, L.h - y0), b = max(border, 3);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t w0 = (int64_t)(L.row0 + y0) * mw + x0 / FT_X;
-    kmask = at(kmask, bo) + w0;
-    wcnt = at(wcnt, bo) + w0;
-    if (!(x0 + FT_X > b && x0 < L.w - b && y0 + ny > b && y0 < L.h - b)) {   // no pixel of the tile may be a corner
-        if (threadIdx.x < ny) {
-            kmask[(int64_t)threadIdx.x * mw] = 0;
-            wcnt[(int64_t)threadIdx.x * mw] = 0;
-        }
-        return;
-    }
+                         int nl, int64_t istride, int xcd, uint8_t* __restrict__ blur) {
+    // LDS: the image tile; the score tile + candidate list, later (aliased) the blur's row sums
+    constexpr int TS_B = FS_R * (FS_C + 2), U_B = TS_B + FS_R * FS_C * 2, R_B = BT_H * (BT_X + 1) * 4;
     __shared__ __align__(16) uint8_t ti[FI_R][FI_C];
-    __shared__ uint8_t ts[FS_R][FS_C + 2];
-    __shared__ uint16_t cand[FS_R * FS_C];
+    __shared__ __align__(16) uint8_t u[U_B > R_B ? U_B : R_B];
     __shared__ int ncand;
-    if (threadIdx.x == 0) ncand = 0;
-    const uint8_t* src = at(pyr, bo) + L.off;
-    if (threadIdx.x < FI_R * (FI_C / 16)) {
-        const int r = threadIdx.x / (FI_C / 16), q = threadIdx.x % (FI_C / 16);
-        const int gy = min(max(y0 - 4 + r, 0), L.h - 1), gx = x0 - 16 + 16 * q;
-        uint4 v = make_uint4(0, 0, 0, 0);   // (columns outside the row: only ever read for frame pixels)
-        if (gx >= 0 && gx < L.pitch) v = *reinterpret_cast<const uint4*>(src + (int64_t)gy * L.pitch + gx);
-        *reinterpret_cast<uint4*>(&ti[r][16 * q]) = v;
-    }
-    __syncthreads();
-    // r04: a quick necessary test first -- an arc of 9 holds two ring pixels 4 apart among 0, 4, 8, 12
-    // (any 8 consecutive positions hold two such, 4 apart), so a corner has some k in {0, 4, 8, 12} with
-    // d_k, d_k+4 both > t or both < -t; the positions passing it are compacted in LDS and only they get
-    // the full score (the tile pass was VALU-bound on the full score of every position, PMC r04h / r04i)
-    // rows across the waves, columns across the lanes (no index division), then the last two columns
-    auto pretest = [&](int sy, int sx, bool ok) {
-        bool pass = false;
-        if (ok) {
-            const uint8_t* c = &ti[sy + 3][sx + 15];
-            const int v = c[0], d0 = v - c[3 * FI_C], d4 = v - c[3], d8 = v - c[-3 * FI_C], d12 = v - c[-3];
-            const int M = max(max(min(d0, d4), min(d4, d8)), max(min(d8, d12), min(d12, d0)));
-            const int N = min(min(max(d0, d4), max(d4, d8)), min(max(d8, d12), max(d12, d0)));
-            pass = M > threshold || N < -threshold;
-        }
-        ts[sy][sx] = 0;
-        const uint64_t m = __ballot(pass);
-        int wb = 0;
-        if (lane == 0 && m) wb = atomicAdd(&ncand, __popcll(m));
-        wb = __shfl(wb, 0);
-        if (pass) cand[wb + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)(sy * FS_C + sx);
-    };
+    auto ts = reinterpret_cast<uint8_t (*)[FS_C + 2]>(u);
+    auto cand = reinterpret_cast<uint16_t*>(u + TS_B);
+    auto rs = reinterpret_cast<int (*)[BT_X + 1]>(u);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int bx, by, bz;
+    xcd_grid(xcd, bx, by, bz);
+    const int64_t bo = (int64_t)by * istride;   // y = image
+    int x0, y0;
+    const int lvl = flat_tile<FT_X, FT_Y>(lv, nl, bx, x0, y0);
+    if (lvl < 0) return;
+    const uint8_t* pyr_g = at(pyr, bo);
+    uint8_t* score_g = at(score, bo);
+    uint8_t* blur_g = blur ? at(blur, bo) : nullptr;
+    kmask = at(kmask, bo);
+    wcnt = at(wcnt, bo);
     {
-        const int xl = x0 - 1 + lane;
-        const bool colok = xl >= 3 && xl < L.w - 3;
-        for (int sy = wid; sy < FS_R; sy += 4) {
-            const int y = y0 - 1 + sy;
-            pretest(sy, lane, colok && y >= 3 && y < L.h - 3);
+        const Lvl L = lv[lvl];
+        const int ny = min(FT_Y, L.h - y0), b = max(border, 3);
+        const int64_t w0 = (int64_t)(L.row0 + y0) * mw + x0 / FT_X;
+        uint64_t* km = kmask + w0;
+        uint8_t* wc = wcnt + w0;
+        const uint8_t* src = pyr_g + L.off;
+        uint8_t* bl = blur_g ? blur_g + L.off : nullptr;
+        if (!(x0 + FT_X > b && x0 < L.w - b && y0 + ny > b && y0 < L.h - b)) {   // no pixel of the tile may be a corner
+            if (bl) {
+                blur_rows<FI_C>(src, L, x0, y0, nullptr, rs);
+                __syncthreads();
+                blur_cols(L, x0, y0, rs, bl);
+            }
+            if ((int)threadIdx.x < ny) {
+                km[(int64_t)threadIdx.x * mw] = 0;
+                wc[(int64_t)threadIdx.x * mw] = 0;
+            }
+            return;
         }
-        static_assert(FS_C - 64 == 2 && 2 * FS_R <= 128, "two trailing columns on waves 0 and 1");
-        if (wid < 2) {
-            const int e = threadIdx.x, sy = e >> 1, sx = 64 + (e & 1);
-            const int xe = x0 - 1 + sx, y = y0 - 1 + sy;
-            if (sy < FS_R) pretest(sy, sx, xe >= 3 && xe < L.w - 3 && y >= 3 && y < L.h - 3);
+        if (threadIdx.x == 0) ncand = 0;
+        if (threadIdx.x < FI_R * (FI_C / 16)) {
+            const int r = threadIdx.x / (FI_C / 16), q = threadIdx.x % (FI_C / 16);
+            const int gy = min(max(y0 - 4 + r, 0), L.h - 1), gx = x0 - 16 + 16 * q;
+            uint4 v = make_uint4(0, 0, 0, 0);   // (columns outside the row: only ever read for frame pixels)
+            if (gx >= 0 && gx < L.pitch) v = *reinterpret_cast<const uint4*>(src + (int64_t)gy * L.pitch + gx);
+            *reinterpret_cast<uint4*>(&ti[r][16 * q]) = v;
         }
-    }
-    __syncthreads();
-    const int nc = ncand;
-    for (int c = threadIdx.x; c < nc; c += 256) {
-        const int i = cand[c], sy = i / FS_C, sx = i - sy * FS_C;
-        ts[sy][sx] = (uint8_t)fast_score_lds<FI_C>(&ti[sy + 3][sx + 15], threshold);
-    }
-    __syncthreads();
-    score = at(score, bo) + L.off;
-    const int x = x0 + lane;
-    for (int ty = wid; ty < ny; ty += 4) {
-        const int y = y0 + ty;
-        const int s = ts[ty + 1][lane + 1];
-        bool keep = false;
-        if (s && y >= b && y < L.h - b && x >= b && x < L.w - b)
-            keep = s > ts[ty][lane] && s > ts[ty][lane + 1] && s > ts[ty][lane + 2] && s > ts[ty + 1][lane] &&
-                   s > ts[ty + 1][lane + 2] && s > ts[ty + 2][lane] && s > ts[ty + 2][lane + 1] && s > ts[ty + 2][lane + 2];
-        const uint64_t m = __ballot(keep);
-        if (lane == 0) {
-            kmask[(int64_t)ty * mw] = m;
-            wcnt[(int64_t)ty * mw] = (uint8_t)__popcll(m);
+        __syncthreads();
+        // r04: a quick necessary test first -- an arc of 9 holds two ring pixels 4 apart among 0, 4, 8, 12
+        // (any 8 consecutive positions hold two such, 4 apart), so a corner has some k in {0, 4, 8, 12} with
+        // d_k, d_k+4 both > t or both < -t; the positions passing it are compacted in LDS and only they get
+        // the full score (the tile pass was VALU-bound on the full score of every position, PMC r04h / r04i)
+        // rows across the waves, columns across the lanes (no index division), then the last two columns
+        auto pretest = [&](int sy, int sx, bool ok) {
+            bool pass = false;
+            if (ok) {
+                const uint8_t* c = &ti[sy + 3][sx + 15];
+                const int v = c[0], d0 = v - c[3 * FI_C], d4 = v - c[3], d8 = v - c[-3 * FI_C], d12 = v - c[-3];
+                const int M = max(max(min(d0, d4), min(d4, d8)), max(min(d8, d12), min(d12, d0)));
+                const int N = min(min(max(d0, d4), max(d4, d8)), min(max(d8, d12), max(d12, d0)));
+                pass = M > threshold || N < -threshold;
+            }
+            ts[sy][sx] = 0;
+            const uint64_t m = __ballot(pass);
+            int wb = 0;
+            if (lane == 0 && m) wb = atomicAdd(&ncand, __popcll(m));
+            wb = __shfl(wb, 0);
+            if (pass) cand[wb + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)(sy * FS_C + sx);
+        };
+        {
+            const int xl = x0 - 1 + lane;
+            const bool colok = xl >= 3 && xl < L.w - 3;
+            for (int sy = wid; sy < FS_R; sy += 4) {
+                const int y = y0 - 1 + sy;
+                pretest(sy, lane, colok && y >= 3 && y < L.h - 3);
+            }
+            static_assert(FS_C - 64 == 2 && 2 * FS_R <= 128, "two trailing columns on waves 0 and 1");
+            if (wid < 2) {
+                const int e = threadIdx.x, sy = e >> 1, sx = 64 + (e & 1);
+                const int xe = x0 - 1 + sx, y = y0 - 1 + sy;
+                if (sy < FS_R) pretest(sy, sx, xe >= 3 && xe < L.w - 3 && y >= 3 && y < L.h - 3);
+            }
         }
-        score[(int64_t)y * L.pitch + x] = (uint8_t)s;   // (x0 + 64 <= pitch)
+        __syncthreads();
+        const int nc = ncand;
+        for (int c = threadIdx.x; c < nc; c += 256) {
+            const int i = cand[c], sy = i / FS_C, sx = i - sy * FS_C;
+            ts[sy][sx] = (uint8_t)fast_score_lds<FI_C>(&ti[sy + 3][sx + 15], threshold);
+        }
+        __syncthreads();
+        uint8_t* sc = score_g + L.off;
+        const int x = x0 + lane;
+        for (int ty = wid; ty < ny; ty += 4) {
+            const int y = y0 + ty;
+            const int s = ts[ty + 1][lane + 1];
+            bool keep = false;
+            if (s && y >= b && y < L.h - b && x >= b && x < L.w - b)
+                keep = s > ts[ty][lane] && s > ts[ty][lane + 1] && s > ts[ty][lane + 2] && s > ts[ty + 1][lane] &&
+                       s > ts[ty + 1][lane + 2] && s > ts[ty + 2][lane] && s > ts[ty + 2][lane + 1] && s > ts[ty + 2][lane + 2];
+            const uint64_t m = __ballot(keep);
+            if (lane == 0) {
+                km[(int64_t)ty * mw] = m;
+                wc[(int64_t)ty * mw] = (uint8_t)__popcll(m);
+            }
+            if (keep) sc[(int64_t)y * L.pitch + x] = (uint8_t)s;
+        }
+        if (bl) {
+            __syncthreads();   // (the score tile and the candidate list are dead: rs aliases them)
+            blur_rows<FI_C>(src, L, x0, y0, &ti[0][0], rs);
+            __syncthreads();
+            blur_cols(L, x0, y0, rs, bl);
+        }
     }
 }
 
@@ -991,94 +1164,6 @@ void orb_copy_kp_kernel(const Kp* __restrict__ src, const int* __restrict__ st, 
     for (int i = blockIdx.x * 256 + threadIdx.x; i < m; i += gridDim.x * 256) dst[i] = src[i];
 }
 
-// ------------------------------------------------------------------ compute(): blur + rBRIEF
-// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on the 8U level through OpenCV's
-// integer separable path: taps x 2^8, (sum + 2^15) >> 16, saturated.
-constexpr int BT_X = 64, BT_Y = 32, BR = 3;
-__constant__ int c_taps[7];
-
-__device__ __forceinline__ int reflect101(int p, int n) {
-    if (n == 1) return 0;
-    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
-    return p;
-}
-
-// r04: 64 x 32 output tiles (halo rows 38 / 32 instead of 22 / 16); interior tiles load without the
-// reflection; the row pass makes 4 neighbouring sums per thread from a 10-byte window, the column pass 8
-// rows of one column from a 14-sum window (the same taps in the same order: the same integers).
-__global__ __launch_bounds__(256)
-void orb_blur_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const int* __restrict__ st,
-                     uint8_t* __restrict__ blur, int nl, int64_t istride) {
-    const int g = blockIdx.y;   // grid (flat 64 x 32 tiles of all levels, images)
-    int x0, y0;
-    const int l = flat_tile<BT_X, BT_Y>(lv, nl, blockIdx.x, x0, y0);
-    if (l < 0 || l >= st[(int64_t)g * CS + 1]) return;   // only the levels the kept keypoints use
-    pyr = at(pyr, (int64_t)g * istride);
-    blur = at(blur, (int64_t)g * istride);
-    const Lvl L = lv[l];
-    constexpr int TH = BT_Y + 2 * BR;
-    __shared__ int r[TH][BT_X + 1];
-    const uint8_t* src = pyr + L.off;
-    // Row pass (r04): each thread makes 4 neighbouring row sums from the 12 bytes x-4 .. x+7 of its
-    // row, read as 3 aligned 4-byte words (interior tiles) or gathered with the reflection (border
-    // tiles); per output the 7-byte window is two realigned words (v_alignbyte) dotted with the taps
-    // (v_dot4_u32_u8, the 8th tap 0).  Integer sums: the same values as the tap-by-tap form.  The
-    // byte tile in LDS it replaces cost bank conflicts and ~2x the VALU work (PMC r04h).
-    const bool interior = x0 >= 64 && x0 + BT_X + 4 <= L.pitch && x0 + BT_X + BR <= L.w && y0 >= BR && y0 + BT_Y + BR <= L.h;
-    const uint32_t T0 = (uint32_t)c_taps[0] | (uint32_t)c_taps[1] << 8 | (uint32_t)c_taps[2] << 16 | (uint32_t)c_taps[3] << 24;
-    const uint32_t T1 = (uint32_t)c_taps[4] | (uint32_t)c_taps[5] << 8 | (uint32_t)c_taps[6] << 16;
-    constexpr int ITEMS = TH * (BT_X / 4);
-#pragma unroll
-    for (int it = 0; it < (ITEMS + 255) / 256; ++it) {
-        const int i = threadIdx.x + 256 * it;
-        if (i < ITEMS) {
-            const int ty = i / (BT_X / 4), tx = 4 * (i % (BT_X / 4));
-            uint32_t wa, wb, wc;   // bytes x-4 .. x-1 | x .. x+3 | x+4 .. x+7 of the row, x = x0 + tx
-            if (interior) {
-                const uint32_t* q = reinterpret_cast<const uint32_t*>(src + (int64_t)(y0 + ty - BR) * L.pitch + x0 + tx - 4);
-                wa = q[0];
-                wb = q[1];
-                wc = q[2];
-            } else {
-                const uint8_t* row = src + (int64_t)reflect101(y0 + ty - BR, L.h) * L.pitch;
-                uint32_t wv[3] = {0u, 0u, 0u};
-#pragma unroll
-                for (int k = 1; k <= 10; ++k)   // (bytes 0 and 11 are never used)
-                    wv[k >> 2] |= (uint32_t)row[reflect101(x0 + tx - 4 + k, L.w)] << (8 * (k & 3));
-                wa = wv[0];
-                wb = wv[1];
-                wc = wv[2];
-            }
-            // output q: bytes 1+q .. 7+q
-            r[ty][tx + 0] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wc, wb, 1), T1,
-                                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wb, wa, 1), T0, 0u, false), false);
-            r[ty][tx + 1] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wc, wb, 2), T1,
-                                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wb, wa, 2), T0, 0u, false), false);
-            r[ty][tx + 2] = (int)__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wc, wb, 3), T1,
-                                                        __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(wb, wa, 3), T0, 0u, false), false);
-            r[ty][tx + 3] = (int)__builtin_amdgcn_udot4(wc, T1, __builtin_amdgcn_udot4(wb, T0, 0u, false), false);
-        }
-    }
-    __syncthreads();
-    static_assert(BT_Y % 8 == 0 && (BT_X * BT_Y / 8) == 256, "one column strip of 8 rows per thread");
-    const int tx = threadIdx.x % BT_X, ty0 = 8 * (threadIdx.x / BT_X);
-    const int x = x0 + tx;
-    if (x < L.w) {
-        int w[14];
-#pragma unroll
-        for (int k = 0; k < 14; ++k) w[k] = r[ty0 + k][tx];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int y = y0 + ty0 + q;
-            if (y >= L.h) break;
-            int s = 0;
-#pragma unroll
-            for (int j = 0; j < 7; j++) s += c_taps[j] * w[q + j];
-            blur[L.off + (int64_t)y * L.pitch + x] = (uint8_t)min(max((s + (1 << 15)) >> 16, 0), 255);
-        }
-    }
-}
-
 // fdlibm-style double sin/cos for the descriptor angle (|x| < 8), the same operation
 // sequence as oracle/orb_oracle.cpp:orb_sincos (this file is built with -ffp-contract=off)
 __device__ void orb_sincos(double x, double* s, double* c) {
@@ -1113,9 +1198,10 @@ constexpr int BWR = 2 * BW + 1, BWC = 80;   // (80-byte rows: 20 banks apart, no
 __global__ __launch_bounds__(256)
 void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ lv, const Kp* __restrict__ kps,
                       const int* __restrict__ sidx, const int* __restrict__ st, const ImgIO* __restrict__ io,
-                      int64_t istride) {
+                      int64_t istride, int xcd) {
     __shared__ __align__(16) uint8_t win[8][BWR * BWC];
-    const int g = blockIdx.y;
+    int bx, g, bz;   // (the output order: one XCD's workgroups take whole images, xcd_grid)
+    xcd_grid(sidx ? 0 : xcd, bx, g, bz);
     blur = at(blur, (int64_t)g * istride);
     kps = at(kps, (int64_t)g * istride);
     if (sidx) sidx = at(sidx, (int64_t)g * istride);
@@ -1135,8 +1221,8 @@ void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ 
     if (sidx) {
         xcd_range(st[(int64_t)g * CS], t0, t1);
         t0 += slot;
-    } else {   // (diagnostic A/B: the output order, strided over the grid, as r04)
-        t0 = blockIdx.x * 8 + slot;
+    } else {   // the output order, strided over the image's workgroups
+        t0 = bx * 8 + slot;
         t1 = n;
         tstep = gridDim.x * 8;
     }
@@ -1512,15 +1598,21 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             OCHK(hipMemcpyAsync(dtab, hp, o_st, hipMemcpyHostToDevice, st));   // tables | levels | umax | ImgIO: contiguous
             OCHK(hipEventRecord(A.e0, st));
             const unsigned gz = (unsigned)G;
+            // XCD runs of the tile passes (A/B: SFMX_ORB_XCD_RUN / _FAST, 0 = the plain grids of r04)
+            int xcd = -1, xcd_blur = 0;
+            if (const char* v = SFMX_DIAG_ENV("SFMX_ORB_XCD_RUN")) xcd = xcd_blur = std::atoi(v);
+            // compute()'s blur inside the FAST + NMS tile pass (A/B: SFMX_ORB_BLUR_SEPARATE, r04's own pass)
+            const bool fuse_blur = descriptors && capmax > 0 && !SFMX_DIAG_ENV("SFMX_ORB_BLUR_SEPARATE");
+            const int xcd_brief = -1;   // rBRIEF: whole images per XCD (the working set is one image's blurred levels)
             // ---- detect(): pyramid, FAST, NMS
             orb_copy_kernel<<<dim3((width + 1023) / 1024, (height + 3) / 4, gz), 256, 0, st>>>(dio, width, height, lv[0].pitch,
                                                                                           pyr, istride);
             for (int l = 1; l < nl; l++)   // (the axis scales as linear_axis computes them)
                 orb_resize_kernel<<<dim3((lv[l].w + RZ_X - 1) / RZ_X, (lv[l].h + RZ_Y - 1) / RZ_Y, gz), 256, 0, st>>>(
                     pyr, lv[l], lv[l - 1], 1.0 / ((double)lv[l].w / lv[l - 1].w), 1.0 / ((double)lv[l].h / lv[l - 1].h), dtab,
-                    istride);
-            orb_fast_nms_kernel<<<dim3(flat_tiles<FT_X, FT_Y>(lv), gz), 256, 0, st>>>(pyr, dlv, thr, border, score, kmask,
-                                                                                   wcnt, mw, nl, istride);
+                    istride, xcd);
+            orb_fast_nms_kernel<<<dim3(flat_tiles<FT_X, FT_Y>(lv), gz), 256, 0, st>>>(pyr, dlv, thr, border, score, kmask, wcnt,
+                                                                                   mw, nl, istride, xcd, fuse_blur ? blur : nullptr);
             orb_scan_kernel<<<gz, 1024, 0, st>>>(wcnt, mw, rows, row_off, istride, stats, dlv, nl);
             orb_rows_kernel<<<dim3((rows + 3) / 4, gz), 256, 0, st>>>(score, dlv, nl, rows, row_off, kmask, mw, cpos, cscore,
                                                                       (int)CAND_CAP, istride);
@@ -1541,14 +1633,14 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
                                                                           sidx, dfin, istride);
             // ---- compute(): blur of the levels used, rBRIEF of min(count, capacity) keypoints
             if (descriptors && capmax > 0) {
-                orb_blur_kernel<<<dim3(flat_tiles<BT_X, BT_Y>(lv), gz), 256, 0, st>>>(
-                    pyr, dlv, sst, blur, nl, istride);
+                if (!fuse_blur) orb_blur_kernel<<<dim3(flat_tiles<BT_X, BT_Y>(lv), gz), 256, 0, st>>>(
+                    pyr, dlv, sst, blur, nl, istride, xcd_blur);
                 // rBRIEF keeps the output order strided over the grid: in the row order its counter traffic
                 // fell 37 -> 7.6 MB per image but the kernel took 181 instead of 159 us per 16 images (r05j
                 // A/B, profiles/r05j_ab_orb_order.txt: it is not bandwidth-bound); the angle pass keeps it
                 int* bsidx = SFMX_DIAG_ENV("SFMX_ORB_BRIEF_SORTED") ? sidx : nullptr;
                 orb_brief_kernel<<<dim3(std::min(G > 1 ? 1024 : 4096, (capmax + 7) / 8), gz), 256, 0, st>>>(blur, dlv, dfin,
-                                                                                                          bsidx, sst, dio, istride);
+                                                                                                          bsidx, sst, dio, istride, xcd_brief);
             }
             if (inputs_on_device && capmax > 0)
                 orb_copy_kp_kernel<<<dim3(std::min(1024, (capmax + 255) / 256), gz), 256, 0, st>>>(dfin, sst, dio, istride);
