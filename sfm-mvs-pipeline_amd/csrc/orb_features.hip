@@ -11,7 +11,9 @@
 //   orb_resize_kernel     level l = INTER_LINEAR_EXACT resize of level l-1 (8.8 fixed
 //                         point; per-axis offset/coefficient tables from the host; 4 pixels per thread)
 //   orb_fast_nms_kernel   FAST 9/16 scores + the 3x3 strict maximum + the border test on 64 x 32
-//                         tiles (16-byte tile loads, scores in LDS): keep words and their counts
+//                         tiles (16-byte tile loads, scores in LDS): keep words and their counts;
+//                         with descriptors, compute()'s 7x7 integer Gaussian of the same tile from
+//                         its LDS image tile (r05)
 //   orb_scan_kernel       the rows' corner counts scanned
 //   orb_rows_kernel       ordered (raster) compaction, one wave per row, from the keep words
 //   orb_retain_kernel     retainBest(2 n_l) per level on the FAST scores: the permutation of
@@ -22,7 +24,7 @@
 //                         keypoints' places in order (one workgroup per level)
 //   orb_angle_kernel      intensity-centroid angle of the kept keypoints, one wavefront per
 //                         keypoint, written in place
-//   orb_blur_kernel       7x7 integer Gaussian of the levels the keypoints use (LDS tile)
+//   (orb_blur_kernel      the blur as a pass of its own: diagnostic A/B only)
 //   orb_brief_kernel      rBRIEF, 32 lanes per keypoint, one descriptor byte per lane
 // One host wait per chunk (the keypoint counts at the end).  Roofline: HBM-bound byte work (see
 // DESIGN.md §3).
@@ -1635,9 +1637,9 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             if (descriptors && capmax > 0) {
                 if (!fuse_blur) orb_blur_kernel<<<dim3(flat_tiles<BT_X, BT_Y>(lv), gz), 256, 0, st>>>(
                     pyr, dlv, sst, blur, nl, istride, xcd_blur);
-                // rBRIEF keeps the output order strided over the grid: in the row order its counter traffic
-                // fell 37 -> 7.6 MB per image but the kernel took 181 instead of 159 us per 16 images (r05j
-                // A/B, profiles/r05j_ab_orb_order.txt: it is not bandwidth-bound); the angle pass keeps it
+                // rBRIEF keeps the output order, whole images per XCD (37 -> 7 MB per image, 159 -> 152 us per
+                // 16 images, r05m); in the row order it read 7.6 MB but took 181 us (r05j A/B,
+                // profiles/r05j_ab_orb_order.txt: it is not bandwidth-bound); the angle pass keeps the row order
                 int* bsidx = SFMX_DIAG_ENV("SFMX_ORB_BRIEF_SORTED") ? sidx : nullptr;
                 orb_brief_kernel<<<dim3(std::min(G > 1 ? 1024 : 4096, (capmax + 7) / 8), gz), 256, 0, st>>>(blur, dlv, dfin,
                                                                                                           bsidx, sst, dio, istride, xcd_brief);
