@@ -10,13 +10,14 @@
 // is compiled with -ffp-contract=off): the ratios agree bit for bit.
 //
 // One 256-thread workgroup per pair.  RANSAC iterations are processed in
-// batches of B = 64 (16 in the first round) in iteration order:
-//   1. lane 0 draws the next B minimal subsets (the RNG stream and the
-//      checkSubset rejections are sequential by definition);
+// batches of B = 64 (32 in the first round) in iteration order:
+//   1. wave 0 draws the next B minimal subsets: getSubset's attempts speculated
+//      64 at a time (the RNG stream cut into attempts as the redraw loop reads
+//      it, checkSubset on one lane each, the passing ones taken in order; r05);
 //   2. lanes 0..B-1 fit one homography each (normalised DLT of the minimal
 //      sample: its 8x8 system solved in registers, fp64);
-//   3. all 256 threads count the inliers of every hypothesis over the pair's
-//      correspondences (fp32 reprojection error, ballot + popcount);
+//   3. each wave counts the inliers of a quarter of the hypotheses over the
+//      pair's correspondences (fp32 reprojection error, ballot + popcount);
 //   4. lane 0 replays the batch in order: best-so-far (strict >, at least 4
 //      inliers) and the adaptive iteration count RANSACUpdateNumIters.
 // Hypotheses past the (shrinking) iteration count are discarded.
@@ -27,9 +28,11 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/sfmx_homography.h"
+#include "diag.hpp"
 #include "match_common.hpp"
 
 namespace sfmx {
@@ -44,6 +47,27 @@ struct PairH {
 __device__ __forceinline__ uint32_t rng_next(unsigned long long& st) {
     st = (unsigned long long)(uint32_t)st * 4164903690ull + (uint32_t)(st >> 32);
     return (uint32_t)st;
+}
+
+// old with lane j set to the (uniform) v
+__device__ __forceinline__ uint32_t wlane(uint32_t v, int j, uint32_t old) { return (threadIdx.x & 63) == (unsigned)j ? v : old; }
+__device__ __forceinline__ int wlane(int v, int j, int old) { return (threadIdx.x & 63) == (unsigned)j ? v : old; }
+
+// cv::RNG::next on the state's two halves in scalar registers (uniform)
+__device__ __forceinline__ void rng_step_s(uint32_t& lo, uint32_t& hi) {
+    const uint32_t m0 = lo * 4164903690u, m1 = __umulhi(lo, 4164903690u);
+    lo = m0 + hi;
+    hi = m1 + (lo < m0 ? 1u : 0u);
+}
+// the next 64 values of the stream, value j into lane j of x (v_writelane with an immediate lane: the
+// value's SGPR is the instruction's one constant-bus read)
+template <int J>
+__device__ __forceinline__ void wlane_imm(uint32_t& x, uint32_t v) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(v), "n"(J));
+}
+template <int... J>
+__device__ __forceinline__ void rng64(uint32_t& x, uint32_t& y, uint32_t& lo, uint32_t& hi, std::integer_sequence<int, J...>) {
+    ((rng_step_s(lo, hi), wlane_imm<J>(x, lo), wlane_imm<J>(y, hi)), ...);
 }
 
 // Minimal-sample solve (the oracle's solve8): [Lx; Ly] h = 0 of 4 normalised
@@ -207,13 +231,18 @@ __global__ __launch_bounds__(256)
 void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_t* __restrict__ nkp,
                               const PairH* __restrict__ pairs, const DMatchDev* __restrict__ matches,
                               const int64_t* __restrict__ off, float4* __restrict__ scratch, int64_t scratch_cap,
-                              int max_iters, double confidence, double* __restrict__ out) {
+                              int max_iters, double confidence, double* __restrict__ out, int serial) {
     __shared__ float4 pts[CAP];
     __shared__ int sub[BATCH][4];
     __shared__ float hf[BATCH][8];
     __shared__ int okb[BATCH], good[BATCH];
     __shared__ int s_nb, s_fail_at, s_done, s_niters, s_maxgood, s_it;
-    const int p = blockIdx.x, tid = threadIdx.x;
+    constexpr int NV = 320;   // RNG values per speculation round (> 64 attempts unless n is tiny)
+    __shared__ int s_idx[NV];
+    __shared__ uint32_t s_stl[NV], s_sth[NV];
+    __shared__ int4 s_att[64];
+    __shared__ int s_aend[64];
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int64_t o0 = off[p];
     const int n = (int)(off[p + 1] - o0);
     if (n < 4) {
@@ -255,11 +284,130 @@ void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_
         return;
     }
     const float thr2 = (float)(P.thr * P.thr);
-    unsigned long long rng = ~0ull;   // cv::RNG((uint64)-1), lane 0 only
+    unsigned long long rng = ~0ull;   // cv::RNG((uint64)-1): wave 0, the same value in every lane
     if (tid == 0) { s_niters = max(max_iters, 1); s_maxgood = 0; s_it = 0; s_done = 0; }
     __syncthreads();
     for (;;) {
-        if (tid == 0) {   // 1. the next minimal subsets, in iteration order
+        if (wid == 0 && !serial) {   // 1. the next minimal subsets, in iteration order (r05, wave 0)
+            // getSubset's attempts are speculated 64 at a time: the RNG stream (uniform, scalar) is cut
+            // into attempts of 4 distinct indices exactly as the redraw loop consumes it (a value equal
+            // to one already drawn in the attempt is skipped), lane a checks attempt a (checkSubset),
+            // and the attempts are then taken in order: every passing one is the next subset until the
+            // batch is full, and getSubset fails after 10000 consecutive rejected attempts.  The RNG
+            // resumes after the last attempt taken.  The same subsets as the serial draw, 64 checks at a
+            // time instead of one (the serial lane-0 draw was most of the kernel: ~3 us per subset).
+            const int want = min(s_it == 0 ? BATCH / 2 : BATCH, s_niters - s_it);
+            int b = 0, fail_at = -1, natt = 0;
+            // the stream in scalar registers (uniform): cv::RNG::next on two 32-bit halves
+            uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rng), hi = __builtin_amdgcn_readfirstlane((uint32_t)(rng >> 32));
+            while (b < want) {
+                // (a) nv values (enough for the attempts still wanted, ~4.1 values each, with margin):
+                // value k's index (value % n) to LDS; the stream itself in scalar registers, each value
+                // written into lane k % 64 by v_writelane (one VALU instruction per value)
+                const int nr = min(NV / 64, (9 * (want - b) + 16 + 63) / 64), nv = 64 * nr;   // (checkSubset passes ~2/3)
+                {
+                    uint32_t vl[NV / 64], vh[NV / 64];   // (the state after each value: where the stream resumes)
+#pragma unroll
+                    for (int r = 0; r < NV / 64; ++r) {
+                        vl[r] = vh[r] = 0u;
+                        if (r < nr) rng64(vl[r], vh[r], lo, hi, std::make_integer_sequence<int, 64>{});
+                    }
+#pragma unroll
+                    for (int r = 0; r < NV / 64; ++r)
+                        if (r < nr) {
+                            s_idx[64 * r + lane] = (int)(vl[r] % (uint32_t)n);
+                            s_stl[64 * r + lane] = vl[r];
+                            s_sth[64 * r + lane] = vh[r];
+                        }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                H_STAMP(5);
+                // (b) the attempts: runs without a repeated index are consecutive groups of 4 (lane a takes
+                // the group at pos + 4a); the first group with a repeat is resolved as the redraw loop reads it
+                int na = 0, pos = 0;
+                while (na < 64 && pos + 4 <= nv) {
+                    const int s0 = pos + 4 * lane;
+                    bool ok = false;
+                    int v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+                    if (na + lane < 64 && s0 + 4 <= nv) {
+                        v0 = s_idx[s0]; v1 = s_idx[s0 + 1]; v2 = s_idx[s0 + 2]; v3 = s_idx[s0 + 3];
+                        ok = v0 != v1 && v0 != v2 && v0 != v3 && v1 != v2 && v1 != v3 && v2 != v3;
+                    }
+                    const uint64_t okm = __ballot(ok);
+                    const int f = ~okm ? (int)__builtin_ctzll(~okm) : 64;   // groups 0 .. f-1 are attempts as they stand
+                    if (lane < f) { s_att[na + lane] = make_int4(v0, v1, v2, v3); s_aend[na + lane] = s0 + 3; }
+                    na += f;
+                    pos += 4 * f;
+                    if (na >= 64 || pos + 4 > nv) break;
+                    // group f: the redraw loop's own reading of the values from pos (uniform, scalar)
+                    int c0 = 0, c1 = 0, c2 = 0, c3 = 0, ci = 0, k = pos;
+                    for (; k < nv && ci < 4; ++k) {
+                        const int v = __builtin_amdgcn_readfirstlane(s_idx[k]);
+                        if (ci > 0 && (v == c0 || (ci > 1 && v == c1) || (ci > 2 && v == c2))) continue;   // redraw
+                        if (ci == 0) c0 = v;
+                        else if (ci == 1) c1 = v;
+                        else if (ci == 2) c2 = v;
+                        else c3 = v;
+                        ++ci;
+                    }
+                    if (ci < 4) break;   // (the values ran out inside this attempt)
+                    if (lane == 0) { s_att[na] = make_int4(c0, c1, c2, c3); s_aend[na] = k - 1; }
+                    ++na;
+                    pos = k;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                H_STAMP(6);
+                // (c) checkSubset of every attempt, one per lane
+                bool pass = false;
+                int4 ai = make_int4(0, 0, 0, 0);
+                if (lane < na) {
+                    ai = s_att[lane];
+                    float q[4][4];
+                    const int id[4] = {ai.x, ai.y, ai.z, ai.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float4 v = C[id[i]];
+                        q[i][0] = v.x; q[i][1] = v.y; q[i][2] = v.z; q[i][3] = v.w;
+                    }
+                    pass = check_subset(q);
+                }
+                const uint64_t pm = __ballot(pass);
+                H_STAMP(7);
+                // (d) in order: the passing attempts are the next subsets until the batch is full; getSubset
+                // fails after 10000 rejected attempts in a row
+                const int need = want - b;
+                const int npass = __popcll(pm);
+                const int first = pm ? (int)__builtin_ctzll(pm) : na;
+                if (natt + first >= 10000) { fail_at = s_it + b; break; }
+                int last;   // the last attempt consumed
+                if (npass >= need) {
+                    uint64_t mm = pm;   // the need-th passing attempt
+                    for (int i = 1; i < need; ++i) mm &= mm - 1;
+                    last = (int)__builtin_ctzll(mm);
+                } else {
+                    last = na - 1;
+                }
+                const int rank = __popcll(pm & ((1ull << lane) - 1));
+                if (pass && lane <= last) { sub[b + rank][0] = ai.x; sub[b + rank][1] = ai.y; sub[b + rank][2] = ai.z; sub[b + rank][3] = ai.w; }
+                b += min(npass, need);
+                if (b < want) {   // every attempt consumed: the rejections after the last pass carry over
+                    const int lastpass = pm ? 63 - (int)__builtin_clzll(pm) : -1;
+                    natt = pm ? na - 1 - lastpass : natt + na;
+                    if (natt >= 10000) { fail_at = s_it + b; break; }
+                }
+                // the stream resumes after the last attempt taken
+                const int kend = __builtin_amdgcn_readfirstlane(s_aend[last]);
+                lo = __builtin_amdgcn_readfirstlane(s_stl[kend]);
+                hi = __builtin_amdgcn_readfirstlane(s_sth[kend]);
+            }
+            rng = ((unsigned long long)hi << 32) | lo;
+            if (lane == 0) { s_nb = b; s_fail_at = fail_at; }
+        }
+        if (tid == 0 && serial) {   // 1. (diagnostic A/B: r04's serial draw on lane 0, SFMX_HOMOG_SERIAL)
             int b = 0;
             s_fail_at = -1;
             const int want = s_it == 0 ? BATCH / 2 : BATCH;
@@ -304,20 +452,30 @@ void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_
         }
         __syncthreads();
         H_STAMP(3);
-        for (int b = 0; b < nb; ++b) {   // 3. inlier counts (computeError + findInliers)
+        // 3. inlier counts (computeError + findInliers).  r05: wave w takes hypotheses w, w + 4, ... whole,
+        // its lanes walk the correspondences and a ballot + popcount per 64 of them sums the count (r04: all
+        // 256 threads per hypothesis, a shuffle reduction and an LDS atomic each: ~0.7 us per hypothesis)
+        for (int b = wid; b < nb; b += 4) {
             if (!okb[b]) continue;
             const float h0 = hf[b][0], h1 = hf[b][1], h2 = hf[b][2], h3 = hf[b][3], h4 = hf[b][4], h5 = hf[b][5],
                         h6 = hf[b][6], h7 = hf[b][7];
             int cnt = 0;
-            for (int i = tid; i < n; i += 256) {
-                const float4 v = C[i];
-                const float ww = 1.f / (h6 * v.x + h7 * v.y + 1.f);
-                const float dx = (h0 * v.x + h1 * v.y + h2) * ww - v.z;
-                const float dy = (h3 * v.x + h4 * v.y + h5) * ww - v.w;
-                cnt += (dx * dx + dy * dy) <= thr2;
+            for (int i0 = 0; i0 < n; i0 += 4 * 64) {   // (4 loads in flight per lane)
+                float4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = i0 + 64 * u + lane;
+                    v[u] = C[min(i, n - 1)];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float ww = 1.f / (h6 * v[u].x + h7 * v[u].y + 1.f);
+                    const float dx = (h0 * v[u].x + h1 * v[u].y + h2) * ww - v[u].z;
+                    const float dy = (h3 * v[u].x + h4 * v[u].y + h5) * ww - v[u].w;
+                    cnt += __popcll(__ballot(i0 + 64 * u + lane < n && (dx * dx + dy * dy) <= thr2));
+                }
             }
-            for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-            if ((tid & 63) == 0 && cnt) atomicAdd(&good[b], cnt);
+            if (lane == 0) good[b] = cnt;
         }
         __syncthreads();
         H_STAMP(4);
@@ -503,7 +661,8 @@ int sfmx_homography_ratios(const sfmx_point2f* const* keypoints, const int32_t* 
             if (hipMemcpyAsync(d, S.pin, b_kp + b_nk + b_ph, hipMemcpyHostToDevice, st) != hipSuccess) { rc = SFMX_EDEVICE; goto done; }
             (void)hipEventRecord(S.e0, st);
             homography_ransac_kernel<<<n_pairs, 256, 0, st>>>(kpd, nkd, phd, reinterpret_cast<const DMatchDev*>(matches),
-                                                              doff, scr, std::max<int64_t>(total, 1), max_iters, confidence, outd);
+                                                              doff, scr, std::max<int64_t>(total, 1), max_iters, confidence, outd,
+                                                              SFMX_DIAG_ENV("SFMX_HOMOG_SERIAL") ? 1 : 0);
             (void)hipEventRecord(S.e1, st);
             if (hipGetLastError() != hipSuccess ||
                 hipMemcpyAsync(hout, outd, sizeof(double) * n_pairs, hipMemcpyDeviceToHost, st) != hipSuccess ||
