@@ -47,6 +47,7 @@
 #include "../../include/sfmx.h"
 #include "../../include/sfmx_features.h"
 #include "diag.hpp"
+#include "xcd.hpp"
 #include "match_common.hpp"
 
 namespace sfmx {
@@ -104,35 +105,6 @@ __device__ __forceinline__ void xcd_range(int n, int& t0, int& t1) {
     const int per = (n + nwg - 1) / nwg;
     t0 = min(n, rb * per);
     t1 = min(n, t0 + per);
-}
-
-// The tile passes (resize, FAST + NMS, blur) read a halo around every tile: under round-robin
-// dispatch the tiles either side of a tile run on other XCDs, whose L2s each fetch the shared lines
-// again (from MALL or HBM; FETCH_SIZE counts both).  r05: xcd_grid remaps the grid's linear (x, y, z)
-// block order so that one XCD's workgroups take neighbouring blocks: run < 0, a contiguous 1/8 of the
-// grid per XCD (whole images); run > 0, runs of `run` consecutive blocks dealt to the XCDs in turn (the
-// remainder past the last full round of 8 runs keeps its place).  Speed only: every block still runs
-// exactly once.  Measured (r05m, one-stream traces, 16-image chunks): the halo passes' counter bytes
-// fall 2-4x either way, but the FAST + NMS pass took 312 (plain grid) / 319 (run < 0) / 331 us (runs of
-// 8 .. 128) and the separate blur 121 / 134 / 147 us: neither is bandwidth-bound and both keep the plain
-// grid (run = 0); the resize chain is unchanged (26.4 / 26.8 us a level) and rBRIEF, which reads
-// patches in the output order, gains (whole images per XCD: 159 -> 152 us, 37 -> 7 MB per image).
-__device__ __forceinline__ void xcd_grid(int run, int& bx, int& by, int& bz) {
-    bx = blockIdx.x; by = blockIdx.y; bz = blockIdx.z;
-    if (!run) return;
-    const int gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
-    const int b = bx + gx * (by + gy * bz), x = b & 7, k = b >> 3;
-    int lin = b;
-    if (run < 0) {
-        const int q = n >> 3, r = n & 7;
-        lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-    } else if (b < n / (8 * run) * (8 * run)) {
-        lin = ((k / run) * 8 + x) * run + k % run;
-    }
-    bx = lin % gx;
-    const int t = lin / gx;
-    by = t % gy;
-    bz = t / gy;
 }
 
 // ------------------------------------------------------------------ pyramid
@@ -1600,7 +1572,11 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             OCHK(hipMemcpyAsync(dtab, hp, o_st, hipMemcpyHostToDevice, st));   // tables | levels | umax | ImgIO: contiguous
             OCHK(hipEventRecord(A.e0, st));
             const unsigned gz = (unsigned)G;
-            // XCD runs of the tile passes (A/B: SFMX_ORB_XCD_RUN / _FAST, 0 = the plain grids of r04)
+            // XCD order of the tile passes (xcd.hpp; A/B: SFMX_ORB_XCD_RUN, 0 = the plain grids of r04).  r05m
+            // (one-stream traces, 16-image chunks): contiguous ranges per XCD cut the halo passes' counter
+            // bytes 2-4x; the resize chain is unchanged (26.4 vs 26.8 us a level), the separate blur slower
+            // (121 plain / 134 contiguous / 147 us runs of 8-128), FAST + NMS with the fused blur +2.5 %
+            // (r05u) for 14.3 -> 3.3 MB fetched per image, rBRIEF faster (159 -> 152 us)
             int xcd = -1, xcd_blur = 0;
             if (const char* v = SFMX_DIAG_ENV("SFMX_ORB_XCD_RUN")) xcd = xcd_blur = std::atoi(v);
             // compute()'s blur inside the FAST + NMS tile pass (A/B: SFMX_ORB_BLUR_SEPARATE, r04's own pass)

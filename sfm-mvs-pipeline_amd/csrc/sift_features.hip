@@ -29,6 +29,7 @@
 // bit-identical to the oracle.
 #include <hip/hip_runtime.h>
 #include "diag.hpp"
+#include <cstdlib>
 #include <algorithm>
 #include <atomic>
 #include <cfloat>
@@ -44,6 +45,7 @@
 
 #include "../../include/sfmx_features.h"
 #include "match_common.hpp"
+#include "xcd.hpp"
 
 namespace sfmx {
 namespace sift {
@@ -189,12 +191,14 @@ __global__ void blur_col_kernel(const float* __restrict__ src, float* __restrict
 constexpr int TX = 64, TY = 32, RMAX = 16;
 __global__ __launch_bounds__(256)
 void blur_tile_kernel(const float* __restrict__ src, float* __restrict__ dst, float* __restrict__ dog, int w, int h,
-                      const float* __restrict__ fk, int n) {
+                      const float* __restrict__ fk, int n, int xcd) {
     __shared__ float in[(TY + 2 * RMAX) * (TX + 2 * RMAX)];
     __shared__ float rowf[(TY + 2 * RMAX) * TX];
     __shared__ float f[2 * RMAX + 1];
     const int r = n / 2;
-    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    int bx, by, bz;
+    xcd_grid(xcd, bx, by, bz);
+    const int x0 = bx * TX, y0 = by * TY;
     const int IW = TX + 2 * r, IH = TY + 2 * r;
     if (threadIdx.x < n) f[threadIdx.x] = fk[threadIdx.x];
     for (int q = threadIdx.x; q < IW * IH; q += 256) {
@@ -231,11 +235,13 @@ void blur_tile_kernel(const float* __restrict__ src, float* __restrict__ dst, fl
 template <int N>
 __global__ __launch_bounds__(256)
 void blur_tile_n_kernel(const float* __restrict__ src, float* __restrict__ dst, float* __restrict__ dog, int w, int h,
-                        const float* __restrict__ fk) {
+                        const float* __restrict__ fk, int xcd) {
     constexpr int R = N / 2, IW = TX + 2 * R, IH = TY + 2 * R;
     __shared__ float in[IH * IW];
     __shared__ float rowf[IH * TX];
-    const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+    int bx, by, bz;
+    xcd_grid(xcd, bx, by, bz);
+    const int x0 = bx * TX, y0 = by * TY;
     float f[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) f[k] = fk[k];
@@ -389,10 +395,12 @@ __global__ void dog_kernel(const float* __restrict__ a, const float* __restrict_
 // so a small octave's three scans fill the chip together.  Candidate slots come from
 // one atomic counter in any order; the host filter sorts them (as before).
 __global__ void extrema_kernel(const Layer* __restrict__ dog, int L, int w, int h, int threshold, int o,
-                               Cand* __restrict__ out, int* __restrict__ count, int cap) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x + IMG_BORDER, r = blockIdx.y + IMG_BORDER;
+                               Cand* __restrict__ out, int* __restrict__ count, int cap, int xcd) {
+    int bx, by, bz;
+    xcd_grid(xcd, bx, by, bz);
+    const int c = bx * blockDim.x + threadIdx.x + IMG_BORDER, r = by + IMG_BORDER;
     if (c >= w - IMG_BORDER || r >= h - IMG_BORDER) return;
-    const int layer = 1 + (int)blockIdx.z;
+    const int layer = 1 + bz;
     const float* __restrict__ prev = dog[o * (L + 2) + layer - 1].p;
     const float* __restrict__ img = dog[o * (L + 2) + layer].p;
     const float* __restrict__ next = dog[o * (L + 2) + layer + 1].p;
@@ -905,17 +913,25 @@ int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int
             FCHK(hipMemcpyAsync(ddog, hdog.data(), sizeof(Layer) * hdog.size(), hipMemcpyHostToDevice, st));
             FCHK(hipMemsetAsync(counters, 0, 16, st));
             FCHK(hipEventRecord(A.e0, st));
+            // the tile blurs on XCD-contiguous block ranges (xcd.hpp: a tile's halo lines from the XCD's own
+            // L2).  r05zd/ze (features leg, 150 images): the leg's counter traffic 1565 -> 1051 MB per image
+            // (blurs 1.22 GB -> 0.69), one-stream blur 17.9 -> 17.4 us a launch; the extrema scan took
+            // 18.2 -> 23.3 us on the same order for 115 -> 92 MB, so it keeps the plain grid.  A/B:
+            // SFMX_SIFT_XCD (blurs), SFMX_SIFT_XCD_EXTREMA.
+            int xcd = -1, xcd_ext = 0;
+            if (const char* v = SFMX_DIAG_ENV("SFMX_SIFT_XCD")) xcd = std::atoi(v);
+            if (const char* v = SFMX_DIAG_ENV("SFMX_SIFT_XCD_EXTREMA")) xcd_ext = std::atoi(v);
             // blur (+ the DoG of the new layer against its source layer when `dg` is set)
             auto blur = [&](const float* src, float* dst, float* dg, int w, int h, int ki) {
                 const int n = (int)kern[ki].size();
                 const dim3 tg((w + TX - 1) / TX, (h + TY - 1) / TY);
-                if (n == 11) blur_tile_n_kernel<11><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki]);
-                else if (n == 13) blur_tile_n_kernel<13><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki]);
-                else if (n == 17) blur_tile_n_kernel<17><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki]);
-                else if (n == 21) blur_tile_n_kernel<21><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki]);
-                else if (n == 27) blur_tile_n_kernel<27><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki]);
+                if (n == 11) blur_tile_n_kernel<11><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki], xcd);
+                else if (n == 13) blur_tile_n_kernel<13><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki], xcd);
+                else if (n == 17) blur_tile_n_kernel<17><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki], xcd);
+                else if (n == 21) blur_tile_n_kernel<21><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki], xcd);
+                else if (n == 27) blur_tile_n_kernel<27><<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki], xcd);
                 else if (n / 2 <= RMAX) {
-                    blur_tile_kernel<<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki], n);
+                    blur_tile_kernel<<<tg, 256, 0, st>>>(src, dst, dg, w, h, dk[ki], n, xcd);
                 } else {
                     const dim3 g((w + 255) / 256, h);
                     blur_row_kernel<<<g, 256, 0, st>>>(src, tmp, w, h, dk[ki], n);
@@ -955,7 +971,7 @@ int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int
                 const int w = ow[o], h = oh[o];
                 if (w <= 2 * IMG_BORDER || h <= 2 * IMG_BORDER || L < 1) continue;
                 extrema_kernel<<<dim3((w - 2 * IMG_BORDER + 255) / 256, h - 2 * IMG_BORDER, L), 256, 0, st>>>(
-                    ddog, L, w, h, threshold, o, cands, counters + 0, CAND_CAP);
+                    ddog, L, w, h, threshold, o, cands, counters + 0, CAND_CAP, xcd_ext);
             }
             refine_kernel<<<CAND_CAP / 256, 256, 0, st>>>(cands, counters + 0, CAND_CAP, ddog, L,
                                                           (float)params->contrast_threshold, (float)params->edge_threshold,
