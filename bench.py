@@ -54,7 +54,7 @@ FP64_PEAK_TFLOPS = 256 * 128 * 2.4e9 / 1e12
 # Cholesky ~0.58 GFLOP; bytes: obs read twice, points, S written and read
 BA_FLOP_PER_ITER_C5, BA_BYTES_PER_ITER_C5 = 3.0e9, 0.1e9
 FEAT_PMC_FILE = "r05zf_pmc_features.json"   # tools/pmc_feat.sh -> tools/pmc_feat_json.py (SIFT r05zf, ORB r05u sessions)
-BA_PMC_FILE = "r04r_pmc_ba.json"   # tools/pmc_ba.sh -> tools/pmc_ba_json.py (r04r session)
+BA_PMC_FILE = "r05zg_pmc_ba.json"   # tools/pmc_ba.sh -> tools/pmc_ba_json.py (r05zg session)
 
 
 def parse():

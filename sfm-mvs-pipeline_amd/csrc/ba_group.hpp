@@ -146,8 +146,10 @@ __device__ __forceinline__ double dsq(double colsq, double s, double dmin, doubl
 // model cost change is sum_p (s_p.g_p + s_p^T E_p s_p / 2 - s_p.y_p) + the camera part (ba_finalize),
 // i.e. s^T J^T r + |J s|^2 / 2 by blocks: no step kernel reads a Jacobian row.  144 B per observation
 // instead of the 208 B record (K = 3), and ba_gschur no longer sums per-observation partials.
-// Both are stored Jacobi-scaled (ba_glin scales them once the solve's scale is known; the first
-// step's ba_gschur<SCALEJ> scales the iteration-0 linearization in place, with the same products).
+// Both are stored Jacobi-scaled once the solve's scale is known (ba_glin at every candidate); the
+// iteration-0 linearization, written before the scale exists, stays unscaled and the steps on it
+// (ba_gschur / ba_gupdate <SCALEJ>) scale what they read, with the products rounded as stored (r05;
+// r02-r04 scaled it in place in the first step: 144 B/obs + the records written once more per solve).
 constexpr int WST = 18;
 __host__ __device__ constexpr int npr(int K) { return 9 + 3 * K; }
 // W_o <- diag(sp) W_o diag(sc)
@@ -213,8 +215,9 @@ __device__ __forceinline__ void stage_copy(double2* __restrict__ dst, const doub
 // NT = dp_max / 16 (NT (NT + 1) / 2 upper 16x16 tiles per wave).
 // Big groups (one point with > 64 observations, too many cameras or two observations in one
 // camera): the serial path, one thread per point / camera.
-// SCALEJ (the first step of a solve, the records still unscaled from iteration 0): every W_o and
-// point record is scaled by the solve's Jacobi scale as it is read, and written back scaled.
+// SCALEJ (a step on the iteration-0 linearization, whose records are unscaled): every W_o and point
+// record is scaled by the solve's Jacobi scale as it is read (r05: no longer written back -- that was a
+// 144 B/obs + record write per solve; ba_gupdate<SCALEJ> scales its reads the same way).
 // Dynamic LDS: per wave the W table, WB_PTS x PD point data and the lane map; the final combine
 // reuses it as [dp][dp + 1] + rhs.
 __host__ __device__ constexpr int gs_pd(int K) { return 9 + 3 * K; }                  // E | g | V, then M 6 | t 3 | Hi 3K
@@ -246,21 +249,13 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
     if (G.big) {   // one point, any number of observations / cameras: serial per point, per camera
         const int p = G.p0;
         const double* sp = scale + 3 * (size_t)p;
-        if (SCALEJ) {   // scale the point's records in place first (one thread per observation)
-            for (int o = G.o0 + tid; o < G.o1; o += blockDim.x) {
-                double* v = const_cast<double*>(Wr) + (size_t)o * WST;
-                const double* sc = scale + ne + 6 * (size_t)obs_cam[o];
-                scale_w(v, sp, sc);
-            }
-            if (tid < NPR) {
-                double* v = const_cast<double*>(PRr) + (size_t)p * NPR + tid;
-                *v = *v * pr_scale<K>(tid, sp, si);
-            }
-            __threadfence_block();
-            __syncthreads();
-        }
         if (tid == 0) {
-            const double* pr = PRr + (size_t)p * NPR;
+            double pr[NPR];   // the point's record (SCALEJ: scaled as it is read, the products rounded as stored)
+#pragma unroll
+            for (int e = 0; e < NPR; ++e) {
+                const double v = PRr[(size_t)p * NPR + e];
+                pr[e] = SCALEJ ? __dmul_rn(v, pr_scale<K>(e, sp, si)) : v;
+            }
             double E[9] = {pr[0], pr[1], pr[2], pr[1], pr[3], pr[4], pr[2], pr[4], pr[5]}, g[3], Wi[3 * K];
 #pragma unroll
             for (int i = 0; i < 3; ++i) g[i] = pr[6 + i];
@@ -310,10 +305,12 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
             for (int o = G.o0; o < G.o1; ++o) {
                 if (obs_lc[o] != lc) continue;
                 const double* wo = Wr + (size_t)o * WST;
+                const double* sc = scale + ne + 6 * (size_t)obs_cam[o];
 #pragma unroll
                 for (int a = 0; a < 3; ++a)
 #pragma unroll
-                    for (int d = 0; d < 6; ++d) W[a][d] += wo[6 * a + d];
+                    for (int d = 0; d < 6; ++d)
+                        W[a][d] += SCALEJ ? __dmul_rn(wo[6 * a + d], __dmul_rn(sp[a], sc[d])) : wo[6 * a + d];
             }
 #pragma unroll
             for (int d = 0; d < 6; ++d)
@@ -396,12 +393,7 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
             double v[WST];
 #pragma unroll
             for (int i = 0; i < WST / 2; ++i) { v[2 * i] = pre[i].x; v[2 * i + 1] = pre[i].y; }
-            if (SCALEJ) {   // W_s = diag(sp) W diag(sc), stored back once
-                scale_w(v, scale + 3 * (size_t)pre_p, scale + ne + 6 * (size_t)pre_c);
-                double2* d2 = reinterpret_cast<double2*>(const_cast<double*>(Wr) + (size_t)o * WST);
-#pragma unroll
-                for (int i = 0; i < WST / 2; ++i) d2[i] = make_double2(v[2 * i], v[2 * i + 1]);
-            }
+            if (SCALEJ) scale_w(v, scale + 3 * (size_t)pre_p, scale + ne + 6 * (size_t)pre_c);   // W_s = diag(sp) W diag(sc)
             double2* wl = reinterpret_cast<double2*>(Wl + l * WST);
 #pragma unroll
             for (int i = 0; i < WST / 2; ++i) wl[i] = make_double2(v[2 * i], v[2 * i + 1]);
@@ -415,10 +407,7 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
             for (int j = 0; j < QS; ++j)
                 if (qk * QS + j < NPR) {
                     double vv = pre_pr[j];
-                    if (SCALEJ) {
-                        vv = vv * pr_scale<K>(qk * QS + j, pre_sp, si);
-                        const_cast<double*>(PRr)[(size_t)(B.p0 + qp) * NPR + qk * QS + j] = vv;
-                    }
+                    if (SCALEJ) vv = vv * pr_scale<K>(qk * QS + j, pre_sp, si);
                     ps[j] = vv;
                 }
         }
@@ -824,11 +813,19 @@ __device__ __forceinline__ void point_v(const double* __restrict__ jer, const do
 // (s^T J^T r + |J s|^2 / 2 with J^T J's point rows E_p and W_p; the camera rows' part, s_f.g_f +
 // s_f^T C s_f / 2, is ba_finalize's).
 // y_o = W_o sol_c of the observation's camera (the back substitution's per-observation term)
-__device__ __forceinline__ void obs_y(const double* __restrict__ Wr, int o, const double* __restrict__ solc, double* __restrict__ y3) {
+// (jsp / jsc: the point's and the camera's Jacobi scales when the records are unscaled, else null:
+// W_o scaled as it is read, each product rounded as scale_w stores it)
+__device__ __forceinline__ void obs_y(const double* __restrict__ Wr, int o, const double* __restrict__ solc, double* __restrict__ y3,
+                                      const double* __restrict__ jsp = nullptr, const double* __restrict__ jsc = nullptr) {
     const double2* s2 = reinterpret_cast<const double2*>(Wr + (size_t)o * WST);
     double wv[WST], sc[6];
 #pragma unroll
     for (int i = 0; i < WST / 2; ++i) { const double2 t = s2[i]; wv[2 * i] = t.x; wv[2 * i + 1] = t.y; }
+    if (jsp)
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int d = 0; d < 6; ++d) wv[6 * a + d] = __dmul_rn(wv[6 * a + d], __dmul_rn(jsp[a], jsc[d]));
 #pragma unroll
     for (int d = 0; d < 6; ++d) sc[d] = solc[d];
 #pragma unroll
@@ -839,13 +836,19 @@ __device__ __forceinline__ void obs_y(const double* __restrict__ Wr, int o, cons
         y3[k] = yk;
     }
 }
-template <int K>
+template <int K, bool SCALEJ = false>
 __device__ __forceinline__ void point_step(int p, double (&y)[3], const double* __restrict__ PRr,
                                            const double* __restrict__ plt, const double (&soli)[K],
                                            const double* __restrict__ x, const double* __restrict__ scale,
-                                           double* __restrict__ cand, double& model, double& sn, double (&cvo)[3]) {
+                                           double* __restrict__ cand, double& model, double& sn, double (&cvo)[3],
+                                           const double* __restrict__ si = nullptr) {
     constexpr int NPR = npr(K);
-    const double* pr = PRr + (size_t)p * NPR;
+    double pr[NPR];   // (SCALEJ: the unscaled record scaled as it is read, the products rounded as stored)
+#pragma unroll
+    for (int e = 0; e < NPR; ++e) {
+        const double v = PRr[(size_t)p * NPR + e];
+        pr[e] = SCALEJ ? __dmul_rn(v, pr_scale<K>(e, scale + 3 * (size_t)p, si)) : v;
+    }
 #pragma unroll
     for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -1401,9 +1404,10 @@ void ba_group_sums(int ngroups, const double* __restrict__ gpl, double* __restri
 // 9 independent 16-B loads) and one per point.  Workgroups past the groups do ba_fstep's work
 // (the candidate cameras / intrinsics), so the step needs no launch of its own for it.  (Fusing it into the candidate's ba_glin, per chunk
 // before the linearization, was measured slower: DESIGN.md §5.)
-template <int K>
+template <int K, bool SCALEJ>
 __global__ __launch_bounds__(256)
 void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const int* __restrict__ obs_cam,
+                const int* __restrict__ obs_point,
                 const int* __restrict__ pt_start, const double* __restrict__ Wr, const double* __restrict__ PRr,
                 const double* __restrict__ scale, const double* __restrict__ plt, const double* __restrict__ sol_f,
                 int P, int C, const double* __restrict__ x, double* __restrict__ cand, double* __restrict__ gpl,
@@ -1436,7 +1440,12 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
             pa0 = pt_start[G.p0 + tid] - ch.o0;
             pa1 = pt_start[G.p0 + tid + 1] - ch.o0;
         }
-        if (o < ch.o1) obs_y(Wr, o, sol_f + 6 * (size_t)obs_cam[o], yv + tid * 3);
+        if (o < ch.o1) {
+            const int cam = obs_cam[o];
+            if (SCALEJ) obs_y(Wr, o, sol_f + 6 * (size_t)cam, yv + tid * 3, scale + 3 * (size_t)obs_point[o],
+                              scale + 3 * (size_t)P + 6 * (size_t)cam);
+            else obs_y(Wr, o, sol_f + 6 * (size_t)cam, yv + tid * 3);
+        }
         __syncthreads();
         if (G.big) {
             if (tid == 0)
@@ -1449,13 +1458,13 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
 #pragma unroll
                 for (int k = 0; k < 3; ++k) y[k] += yv[b * 3 + k];
             double cv[3];
-            point_step<K>(G.p0 + tid, y, PRr, plt, soli, x, scale, cand, model, sn, cv);
+            point_step<K, SCALEJ>(G.p0 + tid, y, PRr, plt, soli, x, scale, cand, model, sn, cv, scale + 3 * (size_t)P + 6 * (size_t)C);
         }
         __syncthreads();   // yv is rewritten by the next chunk
     }
     if (G.big && tid == 0) {
         double cv[3];
-        point_step<K>(G.p0, ybig, PRr, plt, soli, x, scale, cand, model, sn, cv);
+        point_step<K, SCALEJ>(G.p0, ybig, PRr, plt, soli, x, scale, cand, model, sn, cv, scale + 3 * (size_t)P + 6 * (size_t)C);
     }
     const double sm = block_sum(model, sh);
     const double ss = block_sum(sn, sh);

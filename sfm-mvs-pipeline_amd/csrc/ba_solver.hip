@@ -139,7 +139,10 @@ struct sfmx_ba_ctx {
     Buf x, cand, scale, colsq, colsq2, grad, grad2, Wr, Wr2, PR, PR2, J, camsum, camsum2, plt, sg, rg, hbig, gpart, gpl,
         scal, SR, sol, failf, partA;
     static constexpr int HS_SLOT = SC_N + LM_N, HS_SEQ = 2 * HS_SLOT, HS_N = HS_SEQ + 3;
-    bool scaled = false, j_scaled = false;   // j_scaled: the records in Wr / PR are scaled (ba_gschur SCALEJ)
+    bool scaled = false;
+    // the Wr buffer that holds the iteration-0 records, still unscaled (Jacobi scaling on) until the
+    // solve's first accepted step: steps on it read them through ba_gschur / ba_gupdate <SCALEJ>
+    void* unscaled_wr = nullptr;
     // locality order: internal point p' is caller point pperm[p']; internal
     // observation o' is caller observation operm[o'] (point-major)
     std::vector<int> pperm, operm;
@@ -492,6 +495,7 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     const sfmx_ba_options& o = c->opt;
     // the failure flag is zero here: cleared by the run's start and by every scalar handoff (ba_publish)
     if (c->phases) HIPCHK(hipEventRecord(c->ev[0], c->st));
+    const bool sj = c->unscaled_wr && c->Wr.p == c->unscaled_wr;   // a step on the unscaled iteration-0 records
     if (c->ngroups > 0) {
 #define GSCHUR(NTV) if (sj) GSCHUR2(NTV, true); else GSCHUR2(NTV, false)
 #define GSCHUR2(NTV, SJ) hipLaunchKernelGGL((ba_gschur<K, NTV, SJ>), dim3(c->ngroups), dim3(256), c->lds_schur, c->st,     \
@@ -500,11 +504,9 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
                            c->PR.as<double>(), c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal,         \
                            o.max_lm_diagonal, radius,                                                                   \
                            c->P, C, c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl, lmr)
-        const bool sj = !c->j_scaled;   // the first step of a solve scales J in place
         switch (c->gs_nt) { case 1: GSCHUR(1); break; case 2: GSCHUR(2); break; case 3: GSCHUR(3); break; default: GSCHUR(4); }
 #undef GSCHUR2
 #undef GSCHUR
-        c->j_scaled = true;
     }
     HIPCHK(hipMemsetAsync(S, 0, sizeof(double) * c->sr_count, c->st));
     hipLaunchKernelGGL(ba_assemble, dim3(c->ntasks), dim3(ASM_THREADS), 0, c->st, c->tasks.as<ATask>(), c->ents.as<AEnt>(),
@@ -532,10 +534,13 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     // the point update, and in workgroups past the groups the candidate cameras / intrinsics
     // An unused dynamic LDS request of GUPDATE_LDS holds it at 4 workgroups (4 waves per SIMD) per CU:
     // 52.8 us against 57-58 at the 5 its VGPRs allow, 64 at 6 and 61 at 3 (r04u..y)
-    hipLaunchKernelGGL(ba_gupdate<K>, dim3(c->ngroups + nblk(c->nf)), dim3(256), GUPDATE_LDS, c->st, c->grp.as<Grp>(),
-                       c->chk.as<Chunk>(), c->obs_cam.as<int>(), c->pt_start.as<int>(), c->Wr.as<double>(),
-                       c->PR.as<double>(), c->scale.as<double>(), c->plt.as<double>(), sol + c->ne, c->P, C,
-                       c->x.as<double>(), c->cand.as<double>(), c->gpl.as<double>(), gate(c), c->ngroups, (int)c->nf);
+#define GUPD(SJ) hipLaunchKernelGGL((ba_gupdate<K, SJ>), dim3(c->ngroups + nblk(c->nf)), dim3(256), GUPDATE_LDS, c->st, \
+                       c->grp.as<Grp>(), c->chk.as<Chunk>(), c->obs_cam.as<int>(), c->obs_point.as<int>(),             \
+                       c->pt_start.as<int>(), c->Wr.as<double>(), c->PR.as<double>(), c->scale.as<double>(),           \
+                       c->plt.as<double>(), sol + c->ne, c->P, C, c->x.as<double>(), c->cand.as<double>(),               \
+                       c->gpl.as<double>(), gate(c), c->ngroups, (int)c->nf)
+    if (sj) GUPD(true); else GUPD(false);
+#undef GUPD
     HIPCHK(hipGetLastError());
     double v[SC_N];
     RC(lin_at<K>(c, c->cand.as<double>(), c->Wr2.as<double>(), c->PR2.as<double>(), c->colsq2.as<double>(), c->grad2.as<double>(),
@@ -800,8 +805,8 @@ int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace,
         hipLaunchKernelGGL(ba_scale, dim3(nblk(c->n)), dim3(256), 0, c->st, (int)c->n, c->colsq.as<double>(),
                            c->scale.as<double>());
     }
-    // the iteration-0 records were written unscaled: the first step's ba_gschur scales them in place
-    c->j_scaled = !o.jacobi_scaling;
+    // the iteration-0 records were written unscaled: the steps on them scale what they read
+    c->unscaled_wr = o.jacobi_scaling ? c->Wr.p : nullptr;
     c->scaled = true;
     HIPCHK(hipEventRecord(c->ev[5], c->st));
     HIPCHK(hipEventSynchronize(c->ev[5]));
@@ -859,6 +864,7 @@ int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace,
                 }
                 const bool acc = lm[LM_ACCEPTED] != 0.0;
                 if (!acc) swap_state();
+                else c->unscaled_wr = nullptr;   // (the iteration-0 buffer is candidate storage from here)
                 if (lm[LM_TRACE] != 0.0 && trace && ntrace < trace_cap) {
                     trace[3 * ntrace] = lm[LM_COST]; trace[3 * ntrace + 1] = lm[LM_RADIUS];
                     trace[3 * ntrace + 2] = lm[LM_SUCCESSFUL]; ++ntrace;
@@ -905,6 +911,7 @@ int run_lm_k(sfmx_ba_ctx* c, int max_iters, sfmx_ba_summary* sum, double* trace,
         if (std::fabs(cost - ccost) <= o.function_tolerance * cost) { term = SFMX_BA_CONVERGENCE; break; }
         const double rel = (cost - ccost) / mcc;
         if (rel > o.min_relative_decrease) {   // HandleSuccessfulStep: the candidate's linearization is current
+            c->unscaled_wr = nullptr;   // (the iteration-0 buffer is candidate storage from here)
             std::swap(c->x, c->cand);
             std::swap(c->Wr, c->Wr2);
             std::swap(c->PR, c->PR2);
@@ -2067,7 +2074,8 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
     c->setup_ms[16] = c->setup_ms[17] = 0.0;
     auto bail = [](int rc) { return rc; };
     // per-problem state starts over
-    c->scaled = c->j_scaled = false;
+    c->scaled = false;
+    c->unscaled_wr = nullptr;
     HIPCHK(hipStreamSynchronize(c->st));   // (a failed earlier load may have left copies from the arena in flight)
     c->stage_off = 0;
     c->P = P; c->C = C; c->O = O;
@@ -2661,7 +2669,7 @@ int sfmx_ba_debug_incremental_check(const sfmx_ba_problem* a, const sfmx_ba_prob
 // LDS + 33 KiB must keep 5 from fitting 160 KiB), out[1] ba_glin<K> at glin_lds(K) (2).
 int sfmx_ba_debug_occupancy(int32_t K, int32_t* out) {
     if (!out || (K != 1 && K != 3 && K != 7)) return fail(SFMX_EINVAL, "K must be 1, 3 or 7");
-    const void* gu = K == 1 ? (const void*)ba_gupdate<1> : K == 3 ? (const void*)ba_gupdate<3> : (const void*)ba_gupdate<7>;
+    const void* gu = K == 1 ? (const void*)ba_gupdate<1, false> : K == 3 ? (const void*)ba_gupdate<3, false> : (const void*)ba_gupdate<7, false>;
     const void* gl = K == 1 ? (const void*)ba_glin<1, false> : K == 3 ? (const void*)ba_glin<3, false> : (const void*)ba_glin<7, false>;
     int a = 0, b = 0;
     const size_t lds = glin_lds(K);
