@@ -58,3 +58,26 @@ def edge_case(seed=11):
     pairs = np.zeros((len(lists), 2), np.int32)
     pairs[:, 1] = 1
     return [k0, k1], [(1280, 720), (1280, 720)], pairs, m, off
+
+
+def speculation_case(seed=21):
+    """Pairs that stress the subset draw's speculation (homography.hip step 1): tiny lists (5 .. 12
+    matches: repeated indices within an attempt are frequent), a list whose points are mostly on one line
+    (most attempts fail checkSubset, so the rejections run on across speculation rounds), and a duplicated
+    list (the same correspondence many times: every attempt repeats indices)."""
+    rng = np.random.default_rng(seed)
+    n = 400
+    k0 = rng.uniform([0, 0], [1280, 720], (n, 2)).astype(np.float32)
+    H = np.array([[1.05, 0.03, -12.0], [0.02, 0.97, 8.0], [5e-5, 1e-5, 1.0]])
+    ph = np.concatenate([k0, np.ones((n, 1), np.float32)], 1) @ H.T
+    k1 = (ph[:, :2] / ph[:, 2:3] + rng.normal(0, 0.5, (n, 2))).astype(np.float32)
+    t = rng.uniform(0, 1, 120).astype(np.float32)   # points 200..319 on one line in both images
+    k0[200:320] = np.stack([100 + 900 * t, 80 + 500 * t], 1)
+    k1[200:320] = np.stack([130 + 880 * t, 60 + 520 * t], 1)
+    lists = [[(int(i), int(i)) for i in rng.choice(200, m, replace=False)] for m in range(5, 13)]
+    lists.append([(i, i) for i in range(200, 316)] + [(i, i) for i in range(4)])
+    lists.append([(i % 7, i % 7) for i in range(60)])
+    m, off = _pack(lists)
+    pairs = np.zeros((len(lists), 2), np.int32)
+    pairs[:, 1] = 1
+    return [k0, k1], [(1280, 720), (1280, 720)], pairs, m, off

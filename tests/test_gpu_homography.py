@@ -72,3 +72,14 @@ def test_device_list_past_the_scratch_bound_is_nan():
     dev = homography.homography_ratios_device([t.data_ptr() for t in dk], [len(k) for k in kps], sizes, one,
                                               dm.data_ptr(), do.data_ptr())
     assert np.isnan(dev[0])
+
+
+def test_speculated_subset_draw_edge_cases_bit_exact():
+    # tiny lists, a mostly collinear list (rejections across speculation rounds) and repeated matches,
+    # each through several iteration budgets: the speculated draw takes the serial draw's subsets
+    from oracle import oracle
+    kps, sizes, pairs, m, off = homog_cases.speculation_case()
+    for thr, iters, conf in ((-3.0, 2000, 0.995), (2.0, 37, 0.9), (-1.0, 2000, 0.999999)):
+        exp = oracle.homography_ratios(kps, sizes, pairs, m, off, thr, iters, conf)
+        got = homography.homography_ratios(kps, sizes, pairs, m, off, thr, iters, conf)
+        assert np.array_equal(got, exp), (thr, iters, got, exp)
