@@ -394,31 +394,44 @@ __global__ void dog_kernel(const float* __restrict__ a, const float* __restrict_
 // One launch per octave: blockIdx.z picks the inner DoG layer 1 + z of dog[o * (L + 2) ..],
 // so a small octave's three scans fill the chip together.  Candidate slots come from
 // one atomic counter in any order; the host filter sorts them (as before).
+// r05: each thread scans `rows` (<= EX_ROWS) rows of its column, their values loaded together: one row
+// per workgroup (r01-r04) made the octave-0 launch ~97k short workgroups (51.7 us per 1080p image on
+// one stream; 8 rows: 40.9 us, r05zh), while the smaller octaves run faster with one row (their launches
+// have few workgroups, r05zh: 8 rows made octave 1 24.3 -> 27.4 us).
+constexpr int EX_ROWS = 8;
 __global__ void extrema_kernel(const Layer* __restrict__ dog, int L, int w, int h, int threshold, int o,
-                               Cand* __restrict__ out, int* __restrict__ count, int cap, int xcd) {
+                               Cand* __restrict__ out, int* __restrict__ count, int cap, int xcd, int rows) {
     int bx, by, bz;
     xcd_grid(xcd, bx, by, bz);
-    const int c = bx * blockDim.x + threadIdx.x + IMG_BORDER, r = by + IMG_BORDER;
-    if (c >= w - IMG_BORDER || r >= h - IMG_BORDER) return;
+    const int c = bx * blockDim.x + threadIdx.x + IMG_BORDER, r0 = by * rows + IMG_BORDER;
+    if (c >= w - IMG_BORDER || r0 >= h - IMG_BORDER) return;
     const int layer = 1 + bz;
     const float* __restrict__ prev = dog[o * (L + 2) + layer - 1].p;
     const float* __restrict__ img = dog[o * (L + 2) + layer].p;
     const float* __restrict__ next = dog[o * (L + 2) + layer + 1].p;
-    const float val = img[(int64_t)r * w + c];
-    if (!(fabsf(val) > threshold)) return;
-    bool mx = val > 0, mn = val < 0;
+    const int nr = min(rows, h - IMG_BORDER - r0);
+    float vals[EX_ROWS];
 #pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
+    for (int k = 0; k < EX_ROWS; ++k) vals[k] = k < nr ? img[(int64_t)(r0 + k) * w + c] : 0.f;
 #pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-            const int64_t q = (int64_t)(r + dy) * w + c + dx;
-            const float a = img[q], b = prev[q], e = next[q];
-            mx = mx && val >= a && val >= b && val >= e;
-            mn = mn && val <= a && val <= b && val <= e;
-        }
-    if (!mx && !mn) return;
-    const int slot = atomicAdd(count, 1);
-    if (slot < cap) out[slot] = Cand{o, layer, r, c};
+    for (int k = 0; k < EX_ROWS; ++k) {
+        const float val = vals[k];
+        if (k >= nr || !(fabsf(val) > threshold)) continue;
+        const int r = r0 + k;
+        bool mx = val > 0, mn = val < 0;
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int64_t q = (int64_t)(r + dy) * w + c + dx;
+                const float a = img[q], b = prev[q], e = next[q];
+                mx = mx && val >= a && val >= b && val >= e;
+                mn = mn && val <= a && val <= b && val <= e;
+            }
+        if (!mx && !mn) continue;
+        const int slot = atomicAdd(count, 1);
+        if (slot < cap) out[slot] = Cand{o, layer, r, c};
+    }
 }
 
 __device__ __forceinline__ float at(const Layer& L, int r, int c) { return L.p[(int64_t)r * L.w + c]; }
@@ -970,8 +983,11 @@ int detect_compute_impl(const uint8_t* image, int32_t width, int32_t height, int
             for (int o = 0; o < o_small; ++o) {
                 const int w = ow[o], h = oh[o];
                 if (w <= 2 * IMG_BORDER || h <= 2 * IMG_BORDER || L < 1) continue;
-                extrema_kernel<<<dim3((w - 2 * IMG_BORDER + 255) / 256, h - 2 * IMG_BORDER, L), 256, 0, st>>>(
-                    ddog, L, w, h, threshold, o, cands, counters + 0, CAND_CAP, xcd_ext);
+                const int nbx = (w - 2 * IMG_BORDER + 255) / 256, hr = h - 2 * IMG_BORDER;
+                int rows = (int64_t)nbx * hr * L >= 65536 ? EX_ROWS : 1;   // (rows per thread, above)
+                if (const char* v = SFMX_DIAG_ENV("SFMX_SIFT_EX_ROWS")) if (rows > 1) rows = std::max(1, std::min(EX_ROWS, std::atoi(v)));
+                extrema_kernel<<<dim3(nbx, (hr + rows - 1) / rows, L), 256, 0, st>>>(ddog, L, w, h, threshold, o, cands,
+                                                                                    counters + 0, CAND_CAP, xcd_ext, rows);
             }
             refine_kernel<<<CAND_CAP / 256, 256, 0, st>>>(cands, counters + 0, CAND_CAP, ddog, L,
                                                           (float)params->contrast_threshold, (float)params->edge_threshold,
