@@ -300,11 +300,13 @@ void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_
             int b = 0, fail_at = -1, natt = 0;
             // the stream in scalar registers (uniform): cv::RNG::next on two 32-bit halves
             uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)rng), hi = __builtin_amdgcn_readfirstlane((uint32_t)(rng >> 32));
+            int full = 0;   // (1: a round that formed no attempt is redone with every value slot)
             while (b < want) {
+                const uint32_t lo0 = lo, hi0 = hi;
                 // (a) nv values (enough for the attempts still wanted, ~4.1 values each, with margin):
                 // value k's index (value % n) to LDS; the stream itself in scalar registers, each value
                 // written into lane k % 64 by v_writelane (one VALU instruction per value)
-                const int nr = min(NV / 64, (9 * (want - b) + 16 + 63) / 64), nv = 64 * nr;   // (checkSubset passes ~2/3)
+                const int nr = full ? NV / 64 : min(NV / 64, (9 * (want - b) + 16 + 63) / 64), nv = 64 * nr;   // (checkSubset passes ~2/3)
                 {
                     uint32_t vl[NV / 64], vh[NV / 64];   // (the state after each value: where the stream resumes)
 #pragma unroll
@@ -361,6 +363,13 @@ void homography_ransac_kernel(const float2* const* __restrict__ kp, const int32_
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 H_STAMP(6);
+                if (na == 0) {   // fewer than 4 distinct indices in nv values (n tiny): never in practice
+                    lo = lo0;
+                    hi = hi0;
+                    if (!full) { full = 1; continue; }
+                    fail_at = s_it + b;   // (320 values without 4 distinct indices: a bound, not OpenCV's)
+                    break;
+                }
                 // (c) checkSubset of every attempt, one per lane
                 bool pass = false;
                 int4 ai = make_int4(0, 0, 0, 0);
