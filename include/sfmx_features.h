@@ -87,7 +87,7 @@ typedef struct {
     int32_t nfeatures;            /* featureLimit (OpenCV default 500)               */
     float scale_factor;           /* 1.2                                             */
     int32_t n_levels;             /* 8 (1..16)                                       */
-    int32_t edge_threshold;       /* 31 (19..256: rBRIEF samples stay in the level)  */
+    int32_t edge_threshold;       /* 31 (0..256; reads outside a level: OpenCV's bordered pyramid) */
     int32_t first_level;          /* 0 (only 0)                                      */
     int32_t wta_k;                /* 2 (only 2)                                      */
     int32_t score_type;           /* 0 = HARRIS_SCORE (only)                         */

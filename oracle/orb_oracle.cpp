@@ -17,6 +17,8 @@
 //   computeKeyPoints nfeaturesPerLevel, runByImageBorder(31), retainBest(2 n),
 //                    HarrisResponses(blockSize 7, k 0.04), retainBest(n) per level,
 //                    ICAngles (intensity centroid, umax circle), pt *= scale
+//   bordered pyramid reads outside a level (edgeThreshold < 19: Harris, ICAngles, rBRIEF near
+//                    the edge) see copyMakeBorder(BORDER_REFLECT_101) pixels, unblurred
 //   compute          runByImageBorder(31) at full resolution, each level blurred
 //                    with GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) through the
 //                    8U sepFilter2D path (kernel from getGaussianKernel, x256 integer
@@ -49,10 +51,20 @@ const int PATTERN[256 * 4] = {
 int round_f(float v) { return (int)std::nearbyint(v); }   // cvRound(float)
 int round_d(double v) { return (int)std::nearbyint(v); }  // cvRound(double / softdouble)
 
+int reflect101(int p, int n) {   // cv::borderInterpolate(BORDER_REFLECT_101)
+    if (n == 1) return 0;
+    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+    return p;
+}
+
 struct Level {
     int w = 0, h = 0;
     std::vector<uint8_t> p;
     uint8_t at(int y, int x) const { return p[(size_t)y * w + x]; }
+    // OpenCV's bordered pyramid (ORB_Impl::detectAndCompute: every level is copyMakeBorder'ed with
+    // BORDER_REFLECT_101 by border = max(edgeThreshold, 22) + 1 pixels, more than any read below
+    // reaches): a read outside the level is the level's pixel at the reflected position
+    uint8_t at_r(int y, int x) const { return at(reflect101(y, h), reflect101(x, w)); }
 };
 
 // ---- resize(INTER_LINEAR_EXACT), 8U, one channel ------------------------------------
@@ -235,10 +247,10 @@ float harris(const Level& L, int x0, int y0) {
     for (int i = 0; i < HARRIS_BLOCK; i++)
         for (int j = 0; j < HARRIS_BLOCK; j++) {
             const int y = y0 - r + i, x = x0 - r + j;
-            const int Ix = (L.at(y, x + 1) - L.at(y, x - 1)) * 2 + (L.at(y - 1, x + 1) - L.at(y - 1, x - 1)) +
-                           (L.at(y + 1, x + 1) - L.at(y + 1, x - 1));
-            const int Iy = (L.at(y + 1, x) - L.at(y - 1, x)) * 2 + (L.at(y + 1, x - 1) - L.at(y - 1, x - 1)) +
-                           (L.at(y + 1, x + 1) - L.at(y - 1, x + 1));
+            const int Ix = (L.at_r(y, x + 1) - L.at_r(y, x - 1)) * 2 + (L.at_r(y - 1, x + 1) - L.at_r(y - 1, x - 1)) +
+                           (L.at_r(y + 1, x + 1) - L.at_r(y + 1, x - 1));
+            const int Iy = (L.at_r(y + 1, x) - L.at_r(y - 1, x)) * 2 + (L.at_r(y + 1, x - 1) - L.at_r(y - 1, x - 1)) +
+                           (L.at_r(y + 1, x + 1) - L.at_r(y - 1, x + 1));
             a += Ix * Ix;
             b += Iy * Iy;
             c += Ix * Iy;
@@ -281,12 +293,12 @@ float fast_atan2(float y, float x) {   // cv::fastAtan2
 
 float ic_angle(const Level& L, int cx, int cy, const std::vector<int>& umax) {
     int m_01 = 0, m_10 = 0;
-    for (int u = -HALF_PATCH; u <= HALF_PATCH; ++u) m_10 += u * L.at(cy, cx + u);
+    for (int u = -HALF_PATCH; u <= HALF_PATCH; ++u) m_10 += u * L.at_r(cy, cx + u);
     for (int v = 1; v <= HALF_PATCH; ++v) {
         int v_sum = 0;
         const int d = umax[v];
         for (int u = -d; u <= d; ++u) {
-            const int vp = L.at(cy + v, cx + u), vm = L.at(cy - v, cx + u);
+            const int vp = L.at_r(cy + v, cx + u), vm = L.at_r(cy - v, cx + u);
             v_sum += vp - vm;
             m_10 += u * (vp + vm);
         }
@@ -296,11 +308,6 @@ float ic_angle(const Level& L, int cx, int cy, const std::vector<int>& umax) {
 }
 
 // ---- compute(): blur + rBRIEF ----------------------------------------------------------
-int reflect101(int p, int n) {
-    if (n == 1) return 0;
-    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
-    return p;
-}
 
 // getGaussianKernel(7, 2, CV_32F) (bit-exact form: t_i = exp(x_i^2 * (-0.125 / sigma^2)),
 // x_i = 1 - n + 2 i, k_i = t_i / (2 sum_{i<n/2} t_i + 1)), then x 2^8 integer taps
@@ -365,7 +372,10 @@ void orb_sincos(double x, double* s, double* c) {
     }
 }
 
-void brief(const Level& B, const Kp& k, float inv_scale, uint8_t* desc) {
+// B: the blurred level.  compute() blurs each level in place inside its bordered pyramid
+// (GaussianBlur on the level's sub-matrix): the border keeps the unblurred reflected pixels, so a
+// sample outside the level (edgeThreshold < 19) reads the unblurred level L at the reflected position.
+void brief(const Level& B, const Level& L, const Kp& k, float inv_scale, uint8_t* desc) {
     float angle = k.angle;
     angle *= (float)(3.14159265358979323846 / 180.f);
     double sd, cd;
@@ -375,7 +385,8 @@ void brief(const Level& B, const Kp& k, float inv_scale, uint8_t* desc) {
     auto value = [&](int idx) {
         const int px = PATTERN[2 * idx], py = PATTERN[2 * idx + 1];
         const float x = px * a - py * b, y = px * b + py * a;
-        return (int)B.at(cy + round_f(y), cx + round_f(x));
+        const int yy = cy + round_f(y), xx = cx + round_f(x);
+        return (int)(yy >= 0 && yy < B.h && xx >= 0 && xx < B.w ? B.at(yy, xx) : L.at_r(yy, xx));
     };
     for (int i = 0; i < 32; i++) {
         int val = 0;
@@ -461,7 +472,8 @@ int orc_orb(const uint8_t* image, int W, int H, int64_t pitch, int nfeatures, fl
     const int n = (int)all.size();
     for (int j = 0; j < n && j < cap; j++) {
         std::memcpy((char*)kps_out + (size_t)j * sizeof(Kp), &all[j], sizeof(Kp));
-        if (desc_out) brief(B[all[j].octave], all[j], 1.f / get_scale(all[j].octave, sf), desc_out + (size_t)j * 32);
+        if (desc_out)
+            brief(B[all[j].octave], L[all[j].octave], all[j], 1.f / get_scale(all[j].octave, sf), desc_out + (size_t)j * 32);
     }
     return n;
 }

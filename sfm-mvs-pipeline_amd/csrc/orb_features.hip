@@ -859,6 +859,9 @@ void orb_retain_kernel(int mode, const Lvl* __restrict__ lv, const int* __restri
 }
 
 // Harris response (7x7 block, k = 0.04) of every kept corner: grid (x, level)
+// EDGE (edgeThreshold < 4): windows may leave the level (the reflected reads); the default instantiation
+// keeps r04's register budget
+template <bool EDGE>
 __global__ __launch_bounds__(256)
 void orb_harris_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, const int* __restrict__ row_off,
                        const Resp* __restrict__ A, const int* __restrict__ cnt1, const int32_t* __restrict__ cpos,
@@ -883,16 +886,29 @@ void orb_harris_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ 
         // r04: the 9 x 9 window (rows y0-4 .. y0+4, columns x0-4 .. x0+4) as 27 aligned 4-byte loads
         // (rows are 64-byte aligned; a corner lies >= 31 pixels inside its level), realigned with
         // v_alignbyte; r03 made 392 byte loads per corner.  The sums are integers: the same values.
-        const int xa = (x0 - 4) & ~3, sh = (x0 - 4) & 3;
-        const uint8_t* base = img + (int64_t)(y0 - 4) * step + xa;
         uint32_t win[9][3];
+        if (!EDGE || (x0 >= 4 && x0 + 4 < L.w && y0 >= 4 && y0 + 4 < L.h)) {
+            const int xa = (x0 - 4) & ~3, sh = (x0 - 4) & 3;
+            const uint8_t* base = img + (int64_t)(y0 - 4) * step + xa;
 #pragma unroll
-        for (int rr = 0; rr < 9; ++rr) {
-            const uint32_t* q = reinterpret_cast<const uint32_t*>(base + (int64_t)rr * step);
-            const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
-            win[rr][0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            win[rr][1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-            win[rr][2] = __builtin_amdgcn_alignbyte(0u, w2, sh);
+            for (int rr = 0; rr < 9; ++rr) {
+                const uint32_t* q = reinterpret_cast<const uint32_t*>(base + (int64_t)rr * step);
+                const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+                win[rr][0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                win[rr][1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                win[rr][2] = __builtin_amdgcn_alignbyte(0u, w2, sh);
+            }
+        } else {   // (r05: edgeThreshold < 4) the window leaves the level: OpenCV's bordered pyramid, reflected
+#pragma unroll
+            for (int rr = 0; rr < 9; ++rr) {
+                const uint8_t* row = img + (int64_t)reflect101(y0 - 4 + rr, L.h) * step;
+                uint32_t w[3] = {0u, 0u, 0u};
+#pragma unroll
+                for (int cc = 0; cc < 9; ++cc) w[cc >> 2] |= (uint32_t)row[reflect101(x0 - 4 + cc, L.w)] << (8 * (cc & 3));
+                win[rr][0] = w[0];
+                win[rr][1] = w[1];
+                win[rr][2] = w[2];
+            }
         }
         auto px = [&](int rr, int cc) -> int { return (int)((win[rr][cc >> 2] >> (8 * (cc & 3))) & 255u); };
         int a = 0, b = 0, c = 0;
@@ -938,6 +954,8 @@ __device__ float fast_atan2(float y, float x) {   // cv::fastAtan2
 // the final keypoints in level order -> cv::KeyPoint with ICAngles' angle (one wavefront per
 // keypoint: the 31 patch rows u = -15..15 across lanes; integer moments, so the lane order is
 // irrelevant), and compute()'s runByImageBorder(31) test at full resolution (Rect::contains(Point(pt)))
+// EDGE (edgeThreshold < 15): patches may leave the level (the reflected reads)
+template <bool EDGE>
 __global__ __launch_bounds__(256)
 void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv, int nl,
                       const int* __restrict__ row_off, int rows, int* __restrict__ stats, const int* __restrict__ umax,
@@ -1008,6 +1026,19 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
         // lane, one row at a time.
         const int xa = (cx - HALF_PATCH) & ~3;
         int m10 = 0, m01 = 0;
+        if (EDGE && !(cx >= HALF_PATCH && cx + HALF_PATCH < L.w && cy >= HALF_PATCH && cy + HALF_PATCH < L.h)) {
+            // (r05: edgeThreshold < 15) the patch leaves the level: OpenCV's bordered pyramid, reflected;
+            // lane hl takes patch row v = hl - 15 pixel by pixel
+            if (hl < 2 * HALF_PATCH + 1) {
+                const int v = hl - HALF_PATCH, d = sumax[v < 0 ? -v : v];
+                const uint8_t* row = img + (int64_t)reflect101(cy + v, L.h) * step;
+                for (int u = -d; u <= d; ++u) {
+                    const int I = row[reflect101(cx + u, L.w)];
+                    m10 += u * I;
+                    m01 += v * I;
+                }
+            }
+        } else {
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
             if (!wok[k]) continue;
@@ -1021,6 +1052,7 @@ void orb_angle_kernel(const uint8_t* __restrict__ pyr, const Lvl* __restrict__ l
             const int si = (int)__builtin_amdgcn_udot4(w, 0x03020100u, 0u, false);
             m10 += (X - cx) * s1 + si;
             m01 += wrow[k] * s1;
+        }
         }
 #pragma unroll
         for (int o = 16; o > 0; o >>= 1) {   // the half-wave's sums (xor partners stay in the half)
@@ -1169,14 +1201,18 @@ __device__ void orb_sincos(double x, double* s, double* c) {
 // window per keypoint slot; keypoints whose window needs the edge clamp read the level directly.
 constexpr int BW = 18;                 // window half-size
 constexpr int BWR = 2 * BW + 1, BWC = 80;   // (80-byte rows: 20 banks apart, not 16 -- fewer conflicts)
+// EDGE (edgeThreshold < 19): samples may leave the level (the bordered pyramid's unblurred reflected pixels);
+// otherwise a window touching the edge stays inside it and reads the blurred level directly
+template <bool EDGE>
 __global__ __launch_bounds__(256)
-void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ lv, const Kp* __restrict__ kps,
-                      const int* __restrict__ sidx, const int* __restrict__ st, const ImgIO* __restrict__ io,
-                      int64_t istride, int xcd) {
+void orb_brief_kernel(const uint8_t* __restrict__ blur, const uint8_t* __restrict__ pyr, const Lvl* __restrict__ lv,
+                      const Kp* __restrict__ kps, const int* __restrict__ sidx, const int* __restrict__ st,
+                      const ImgIO* __restrict__ io, int64_t istride, int xcd) {
     __shared__ __align__(16) uint8_t win[8][BWR * BWC];
     int bx, g, bz;   // (the output order: one XCD's workgroups take whole images, xcd_grid)
     xcd_grid(sidx ? 0 : xcd, bx, g, bz);
     blur = at(blur, (int64_t)g * istride);
+    pyr = at(pyr, (int64_t)g * istride);
     kps = at(kps, (int64_t)g * istride);
     if (sidx) sidx = at(sidx, (int64_t)g * istride);
     uint8_t* desc = io[g].desc_out;
@@ -1212,6 +1248,7 @@ void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ 
         const float a = (float)cd, b = (float)sd;
         const int cy = round_f(k.y * L.inv_scale), cx = round_f(k.x * L.inv_scale);
         const uint8_t* img = blur + L.off;
+        const uint8_t* raw = pyr + L.off;
         const int xs = (cx - BW) & ~15;
         const bool staged = cy >= BW && cy + BW < L.h && cx >= BW && cx + BW < L.w;
         __builtin_amdgcn_wave_barrier();   // (the slot's previous window fully read)
@@ -1231,8 +1268,15 @@ void orb_brief_kernel(const uint8_t* __restrict__ blur, const Lvl* __restrict__ 
             // (r04: packed fp32 rotations measured slower, 155 -> 186 us per 16 images; kept scalar)
             const float x = pxf[e] * a - pyf[e] * b, y = pxf[e] * b + pyf[e] * a;
             if (staged) return wn[(round_f(y) + BW) * BWC + cx + round_f(x) - xs];
-            const int yy = min(max(cy + round_f(y), 0), L.h - 1), xx = min(max(cx + round_f(x), 0), L.w - 1);
-            return img[(int64_t)yy * L.pitch + xx];
+            if (!EDGE) {   // (edgeThreshold >= 19: every sample inside the level; r04's form, its codegen)
+                const int yy = min(max(cy + round_f(y), 0), L.h - 1), xx = min(max(cx + round_f(x), 0), L.w - 1);
+                return img[(int64_t)yy * L.pitch + xx];
+            }
+            // (r05: edgeThreshold < 19) a sample outside the level: compute() blurs each level in place
+            // inside OpenCV's bordered pyramid, whose border keeps the unblurred reflected pixels
+            const int yy = cy + round_f(y), xx = cx + round_f(x);
+            if (yy >= 0 && yy < L.h && xx >= 0 && xx < L.w) return img[(int64_t)yy * L.pitch + xx];
+            return raw[(int64_t)reflect101(yy, L.h) * L.pitch + reflect101(xx, L.w)];
         };
         int val = 0;
 #pragma unroll
@@ -1434,12 +1478,11 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
         if (im.width != width || im.height != height) { set_last_error("internal: a chunk mixes image sizes"); return SFMX_EINTERNAL; }
     }
     if (P->nfeatures < 0 || !(P->scale_factor > 1.f) || P->n_levels < 1 || P->n_levels > MAX_LEVELS ||
-        P->edge_threshold < 19 || P->edge_threshold > 256 || P->first_level != 0 || P->wta_k != 2 ||
+        P->edge_threshold < 0 || P->edge_threshold > 256 || P->first_level != 0 || P->wta_k != 2 ||
         P->score_type != 0 || P->patch_size != 31 || P->fast_threshold < 0) {
-        // edgeThreshold >= 19: rBRIEF's rotated samples reach 18 pixels from a keypoint, so from 19 on they stay
-        // inside the level, where the blurred level is defined the same way in OpenCV (its bordered pyramid)
-        // and here; below, OpenCV reads the blurred reflected border, which this pipeline does not build
-        set_last_error("unsupported ORB parameters (edgeThreshold 19..256, firstLevel 0, WTA_K 2, HARRIS_SCORE, patchSize 31)");
+        // (r05: every edgeThreshold from 0: the Harris window, the angle patch and rBRIEF's samples that leave
+        // a level read OpenCV's bordered pyramid -- its BORDER_REFLECT_101 copy of the level, unblurred)
+        set_last_error("unsupported ORB parameters (edgeThreshold 0..256, firstLevel 0, WTA_K 2, HARRIS_SCORE, patchSize 31)");
         return SFMX_EINVAL;
     }
     int ndev = 0;
@@ -1599,7 +1642,10 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             for (int l = 0; l < nl; l++) { s1.n[l] = 2 * per[l]; s2.n[l] = per[l]; }
             orb_retain_kernel<<<dim3(nl, gz), RT, 0, st>>>(0, dlv, row_off, cscore, rA, rB, sLs, sRs, nullptr, cnt1, s1,
                                                            (int)CAND_CAP, sst + 3, istride);
-            orb_harris_kernel<<<dim3(64, nl, gz), 256, 0, st>>>(pyr, dlv, row_off, rA, cnt1, cpos, rB, istride);
+            // reads that may leave a level (small edgeThreshold: the bordered-pyramid instantiations)
+            const bool e_h = border < 4, e_a = border < HALF_PATCH, e_b = border < BW + 1;
+            if (e_h) orb_harris_kernel<true><<<dim3(64, nl, gz), 256, 0, st>>>(pyr, dlv, row_off, rA, cnt1, cpos, rB, istride);
+            else orb_harris_kernel<false><<<dim3(64, nl, gz), 256, 0, st>>>(pyr, dlv, row_off, rA, cnt1, cpos, rB, istride);
             orb_retain_kernel<<<dim3(nl, gz), RT, 0, st>>>(1, dlv, row_off, cscore, rA, rB, sLs, sRs, cnt1, cnt2, s2,
                                                            (int)CAND_CAP, sst + 3, istride);
             orb_keep_kernel<<<dim3(nl, gz), RT, 0, st>>>(dlv, row_off, rA, rB, stats, cpos, width, height, border, kin,
@@ -1607,8 +1653,12 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
             int* sidx = sLs;   // (the retain kernels' scratch is free from here: the processing order)
             if (SFMX_DIAG_ENV("SFMX_ORB_KEPT_ORDER")) sidx = nullptr;   // A/B: the r04 order
             if (sidx) orb_sort_kernel<<<dim3(nl, gz), RT, 0, st>>>(dlv, row_off, stats, kin, sidx, istride);
-            orb_angle_kernel<<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rows, stats, dumax, kin,
-                                                                          sidx, dfin, istride);
+            if (e_a)
+                orb_angle_kernel<true><<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rows, stats, dumax,
+                                                                                    kin, sidx, dfin, istride);
+            else
+                orb_angle_kernel<false><<<dim3(G > 1 ? 256 : 1024, gz), 256, 0, st>>>(pyr, dlv, nl, row_off, rows, stats, dumax,
+                                                                                     kin, sidx, dfin, istride);
             // ---- compute(): blur of the levels used, rBRIEF of min(count, capacity) keypoints
             if (descriptors && capmax > 0) {
                 if (!fuse_blur) orb_blur_kernel<<<dim3(flat_tiles<BT_X, BT_Y>(lv), gz), 256, 0, st>>>(
@@ -1617,8 +1667,9 @@ int orb_chunk(const OrbImage* ims, int G, const sfmx_orb_params* P, int32_t inpu
                 // 16 images, r05m); in the row order it read 7.6 MB but took 181 us (r05j A/B,
                 // profiles/r05j_ab_orb_order.txt: it is not bandwidth-bound); the angle pass keeps the row order
                 int* bsidx = SFMX_DIAG_ENV("SFMX_ORB_BRIEF_SORTED") ? sidx : nullptr;
-                orb_brief_kernel<<<dim3(std::min(G > 1 ? 1024 : 4096, (capmax + 7) / 8), gz), 256, 0, st>>>(blur, dlv, dfin,
-                                                                                                          bsidx, sst, dio, istride, xcd_brief);
+                const dim3 bg(std::min(G > 1 ? 1024 : 4096, (capmax + 7) / 8), gz);
+                if (e_b) orb_brief_kernel<true><<<bg, 256, 0, st>>>(blur, pyr, dlv, dfin, bsidx, sst, dio, istride, xcd_brief);
+                else orb_brief_kernel<false><<<bg, 256, 0, st>>>(blur, pyr, dlv, dfin, bsidx, sst, dio, istride, xcd_brief);
             }
             if (inputs_on_device && capmax > 0)
                 orb_copy_kp_kernel<<<dim3(std::min(1024, (capmax + 255) / 256), gz), 256, 0, st>>>(dfin, sst, dio, istride);

@@ -63,7 +63,7 @@ def test_large_photo_and_parameters():
     assert len(k) > 1000
     _check(img, nfeatures=3000, scaleFactor=1.5, nlevels=5, fastThreshold=12, edgeThreshold=40)
     # r04 kernels' edge regimes: the resize's staged source span at its limit (scale 2) and past it
-    # (2.6: the per-pixel form), the smallest edge threshold (rBRIEF windows touching the level's edge)
+    # (2.6: the per-pixel form), edge threshold 19 (rBRIEF windows touching the level's edge)
     _check(img, nfeatures=2000, scaleFactor=2.0, nlevels=4, edgeThreshold=19)
     _check(img, nfeatures=1000, scaleFactor=2.6, nlevels=3, edgeThreshold=19, fastThreshold=8)
 
@@ -75,8 +75,24 @@ def test_degenerate_inputs():
     assert len(_check(np.full((100, 100), 7, np.uint8))[0]) == 0     # no corners
     with pytest.raises(ValueError):                                  # SFMX_EINVAL
         sfmx.features.ORB.create(100, WTA_K=3).detectAndCompute(np.zeros((64, 64), np.uint8))
-    with pytest.raises(ValueError):   # rBRIEF samples would leave the level (OpenCV reads its bordered pyramid)
-        sfmx.features.ORB.create(100, edgeThreshold=18).detectAndCompute(np.zeros((64, 64), np.uint8))
+    with pytest.raises(ValueError):
+        sfmx.features.ORB.create(100, edgeThreshold=-1).detectAndCompute(np.zeros((64, 64), np.uint8))
+
+
+@pytest.mark.parametrize("edge", [18, 16, 10, 5, 3, 0])
+def test_small_edge_thresholds_read_the_bordered_pyramid(edge):
+    # below 19 rBRIEF's samples (below 15 the angle patch, below 4 the Harris window) leave their level and
+    # read OpenCV's bordered pyramid: the level's BORDER_REFLECT_101 copy, unblurred (compute() blurs each
+    # level in place inside it); r04 refused these parameters
+    img = sift_cases.blob_image(300, 420, n_blobs=160, seed=13, noise=6.0)
+    k, _ = _check(img, nfeatures=1500, edgeThreshold=edge, nlevels=5)
+    assert len(k) > 100
+    if edge <= 10:   # some keypoints close enough to their level's edge for rBRIEF's border reads
+        s = np.float32(1.2) ** k["octave"].astype(np.float64)
+        x, y = k["x"] / s, k["y"] / s
+        w, h = np.round(420 / s), np.round(300 / s)
+        assert (np.minimum(np.minimum(x, y), np.minimum(w - 1 - x, h - 1 - y)) < 18).any()
+    _check(img, nfeatures=800, edgeThreshold=edge, scaleFactor=1.6, nlevels=4, fastThreshold=10)
 
 
 def test_device_and_batch_modes_match():
