@@ -57,9 +57,14 @@ FEAT_PMC_FILE = "r05zf_pmc_features.json"   # tools/pmc_feat.sh -> tools/pmc_fea
 BA_PMC_FILE = "r05zg_pmc_ba.json"   # tools/pmc_ba.sh -> tools/pmc_ba_json.py (r05zg session)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment and N > 1 this process "
+                         "starts the N ranks itself (launch_ranks) before anything touches the GPU")
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="launcher test only: each rank joins a gloo group, all-reduces its rank and exits "
+                         "(no GPU, no torch.cuda call)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=["sift", "orb"], default="sift")
@@ -81,14 +86,115 @@ def parse():
     ap.add_argument("--ba-cams", type=int, default=200)
     ap.add_argument("--ba-points", type=int, default=200_000)
     ap.add_argument("--ba-cpu-iters", type=int, default=2, help="LM iterations of the CPU BA baseline sample")
-    return ap.parse_args()
+    ap.add_argument("--no-ba-weak", action="store_true",
+                    help="N > 1: skip the BA weak-scaling problem (200 cams x 200k*N points)")
+    return ap.parse_args(argv)
+
+
+def resolve_world(args, env=None):
+    """(world, launch): the rank count this run measures and whether this process must start
+    the ranks itself.  WORLD_SIZE set (torch.distributed.run, or launch_ranks' children): this
+    process is one rank, and an explicit --gpus that disagrees is an error (exit 2), never a
+    silent world-of-one line.  WORLD_SIZE unset: --gpus N > 1 means start N ranks here."""
+    env = os.environ if env is None else env
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        world = int(ws)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to measure "
+                             f"a different rank count than asked for")
+        return world, False
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n} < 1")
+    return n, n > 1
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, timeout=None):
+    """Start N fresh rank processes of this script (one per GPU, LOCAL_RANK = rank) with the
+    torch.distributed env rendezvous on 127.0.0.1, wait for all of them, forward rank 0's JSON
+    line to stdout, and return the exit status: non-zero if any rank failed.  This process has
+    imported neither torch nor the HIP runtime (the children are started, never exec'ed), so the
+    GPU is first touched in the ranks.  Other ranks' stdout goes to stderr.  A failing rank
+    ends the others (their exact PIDs), so a rank stuck in a collective cannot hang the run."""
+    import subprocess
+    import threading
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE, text=True))
+    lines = [[] for _ in range(n)]
+
+    def pump(r):
+        for ln in procs[r].stdout:
+            lines[r].append(ln)
+            if r != 0 or not ln.lstrip().startswith("{"):
+                sys.stderr.write(f"[rank {r}] {ln}")
+                sys.stderr.flush()
+    pumps = [threading.Thread(target=pump, args=(r,), daemon=True) for r in range(n)]
+    for t in pumps:
+        t.start()
+    t_end = None if timeout is None else time.monotonic() + timeout
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+        failed = [r for r, rc in enumerate(rcs) if rc not in (None, 0)]
+        if failed or (t_end is not None and time.monotonic() > t_end):
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    p.kill()
+                    rcs[r] = p.wait()
+            break
+        time.sleep(0.05)
+    for t in pumps:
+        t.join(timeout=5)
+    json_lines = [ln for ln in lines[0] if ln.lstrip().startswith("{")]
+    if json_lines:
+        sys.stdout.write(json_lines[-1])
+        sys.stdout.flush()
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        sys.stderr.write(f"bench.py: rank(s) failed: {bad}\n")
+        return 1
+    return 0 if json_lines else 1
+
+
+def launch_probe(rank, world):
+    """--launch-probe: prove the N ranks rendezvous (gloo, CPU) and agree on the world."""
+    if os.environ.get("SFMX_BENCH_PROBE_FAIL_RANK") == str(rank):
+        sys.exit(3)     # the launcher test of a failing rank: the others block in the rendezvous
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group(backend="gloo")
+    t = torch.tensor([float(rank)])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": "launch-probe", "n_gpus": world, "rank_sum": float(t.item()),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "-1"))}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    world, launch = resolve_world(args)
+    if launch:
+        sys.exit(launch_ranks(world, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_probe:
+        return launch_probe(rank, world)
     # Rehearsal of the N-rank path on a one-GPU box (tests only, never a bench
     # result): every rank on cuda:0, collectives over gloo instead of RCCL.
     rehearse = os.environ.get("SFMX_BENCH_REHEARSE") == "1"
@@ -299,6 +405,11 @@ def compact_line(full, detail=None):
         s.update(_r({"iterations": ba.get("iterations"), "final_cost": ba.get("final_cost"),
                      "termination": ba.get("termination")}, 7))
         legs["ba"] = s
+        w = ba.get("weak")
+        if isinstance(w, dict):
+            legs["ba_weak"] = ({"error": str(w["error"])[:300]} if "error" in w else
+                               _r({k: w.get(k) for k in ("value", "unit", "scaling", "n_gpus", "points_per_s",
+                                                         "iterations", "final_cost", "termination")}, 7))
         if ba.get("calls"):
             legs["ba_calls"] = ({"error": str(ba["calls"]["error"])[:300]} if "error" in ba["calls"]
                                 else ba_calls_summary(ba["calls"]))
@@ -695,6 +806,11 @@ def bench_ba(args, rank, world, local):
            "final_cost": sm["final_cost"], "termination": ba.TERMINATION_NAMES[sm["termination_type"]],
            "total_ms": total_ms, "phase_ms_rank0": phases, "collectives": collectives}
     res["roofline"] = ba_roofline(args, res["value"], world)
+    if world > 1 and not args.no_ba_weak:
+        try:
+            res["weak"] = bench_ba_weak(args, rank, world, local, rehearse)
+        except Exception as e:   # pragma: no cover
+            res["weak"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             from oracle import oracle
@@ -719,6 +835,46 @@ def bench_ba(args, rank, world, local):
         except Exception as e:   # pragma: no cover
             res["cpu_baseline"] = {"error": str(e)}
     return res
+
+
+def bench_ba_weak(args, rank, world, local, rehearse):
+    """BA weak scaling beside the strong-scaling C5 line: at N ranks the
+    problem is 200 cameras x (200k * N) points, still point-sharded, so every rank holds a C5-sized
+    point shard and the replicated camera chain (S factorisation, back solve) is the same as at
+    N = 1.  Collectives: native RCCL inside libsfmx on real ranks (never the gloo callback); the
+    one-GPU rehearsal keeps the host-staged gloo callback."""
+    import torch
+    import torch.distributed as dist
+    from sfmx import ba, synth
+    from sfmx.dist import shard_ba_problem, torch_allreduce, rccl_comm
+    n_pts = args.ba_points * world
+    prob = synth.ba_problem(args.ba_cams, n_pts)
+    local_prob = shard_ba_problem(prob, rank, world)
+    local_prob.pop("point_range")
+    ctx = ba.BAContext(ba.BAProblem(**local_prob), ba.default_options(device=local),
+                       allreduce=torch_allreduce(cpu_staging=True) if rehearse else None)
+    if not rehearse:
+        rccl_comm(ctx)
+    ctx.run(max_iterations=1)
+    ctx.reset()
+    dist.barrier()
+    torch.cuda.synchronize()
+    sm, _ = ctx.run(trace_cap=0)
+    ctx.close()
+    iters = sm["num_successful_steps"] + sm["num_unsuccessful_steps"]
+    ms = torch.tensor([sm["total_ms"]], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+    total_ms = float(ms.item())
+    per_iter = total_ms / max(iters, 1)
+    return {"metric": "ms per LM iteration", "value": per_iter, "unit": "ms", "higher_is_better": False,
+            "scaling": "weak", "n_gpus": world,
+            "points_per_s": n_pts / (per_iter * 1e-3),
+            "config": {"workload": f"BA {args.ba_cams} cams / {n_pts} points / {len(prob['obs_point'])} obs "
+                                   f"(C5 points x {world}), SimpleRadial", "parallelism": f"point-sharded x{world}"},
+            "iterations": iters, "final_cost": sm["final_cost"],
+            "termination": ba.TERMINATION_NAMES[sm["termination_type"]],
+            "collectives": "gloo callback, host-staged (one-GPU rehearsal)" if rehearse
+                           else "RCCL in libsfmx (ncclAllReduce on the solver stream)"}
 
 
 def bench_ba_calls(args):
