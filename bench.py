@@ -566,7 +566,7 @@ def bench_match(kind, args, rank, world, local):
                    "logical_descriptor_pairs": logical_total, "parallelism": f"pair-sharded x{world}",
                    "ratio": sfmx.LOWE_RATIO},
         "roofline": {"bound": bound, "achieved": achieved, "peak": peak, "unit": unit,
-                     "frac": achieved / peak, "traffic": pmc_traffic(kind, n_img),
+                     "frac": achieved / peak, "traffic": pmc_traffic(kind, n_img) if world == 1 else None,
                      "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE from the committed PMC pass)",
                      "kernel": kernel, "kernel_ms_per_launch": kern_ms, "run_ms_per_step": float(np.median(run_ms)),
                      "kernel_ms_samples": [float(x) for x in main_ms],

@@ -97,7 +97,12 @@ int sfmx_matcher_set_images(sfmx_matcher* m, const sfmx_desc* imgs, int32_t n_im
                             int32_t norm, void* stream);
 
 /* Same, from descriptor matrices already resident in device memory on this
- * matcher's device (imgs[i].data are device pointers). */
+ * matcher's device (imgs[i].data are device pointers).  The host does not wait
+ * for the SIFT integrality check here: the next run assumes integral rows and
+ * the check is resolved when its results are first read (fetch, stats,
+ * device_results), re-running on the fp32 path if an image is not integral.
+ * The device buffers must therefore stay valid and unchanged until the
+ * results of the following run have been read. */
 int sfmx_matcher_set_images_device(sfmx_matcher* m, const sfmx_desc* imgs, int32_t n_imgs,
                                    int32_t norm, void* stream);
 

@@ -1028,19 +1028,23 @@ void make_view(const sfmx_ba_problem* pb, View& v) {
     constexpr int PIECES = 64;   // fixed ranges (host_par.hpp): the same result on every host
     v.start.resize(P + 1);
     std::atomic<bool> pm{true};
-    {   // the reference adds residuals point by point (BundleAdjustment.cpp:50-91): one pass both checks
-        // the order and, for a point-major problem, fills the starts (r05: two passes before)
-        const int* op = pb->obs_point;
+    // the reference adds residuals point by point (BundleAdjustment.cpp:50-91).  Two passes: the
+    // order check over every range (each range compares across its left boundary, so all ranges
+    // monotone = the whole array monotone), then, only for a point-major problem, the start fill, where
+    // every start is written by exactly one range.  (r05 fused them: on shuffled input the fill then
+    // wrote overlapping start ranges from several threads, O(O * P) work and a data race)
+    const int* op = pb->obs_point;
+    sfmx::parallel_ranges((int64_t)O + 1, PIECES, [&](int64_t i0, int64_t i1) {
+        for (int64_t i = std::max<int64_t>(i0, 1); i < std::min<int64_t>(i1, O); ++i)
+            if (op[i - 1] > op[i]) { pm = false; return; }
+    });
+    if (pm)
         sfmx::parallel_ranges((int64_t)O + 1, PIECES, [&](int64_t i0, int64_t i1) {
-            bool ok = true;
             for (int64_t i = i0; i < i1; ++i) {   // points (op[i - 1], op[i]] start at i
                 const int lo = i == 0 ? -1 : op[i - 1], hi = i == O ? P - 1 : op[i];
-                ok &= lo <= hi;   // (a decrease: not point-major)
                 for (int p = lo + 1; p <= hi; ++p) v.start[p] = (int)i;
             }
-            if (!ok) pm = false;
         });
-    }
     v.pm = pm;
     if (v.pm) {
         v.start[P] = O;
@@ -1366,11 +1370,17 @@ void finish_topology(int C, int K, Topology& tp) {
         }
         // stable counting sort on the pair index (a - a0) C + b
         auto idx = [C, a0](const PairRef& x) { return (size_t)((int)(x.key >> 32) - a0) * C + (size_t)(x.key & 0xffffffffu); };
-        P.cnt.assign((size_t)(a1 - a0) * C + 1, 0);
-        for (const PairRef& x : P.pr) P.cnt[idx(x) + 1]++;
-        for (size_t i = 1; i < P.cnt.size(); ++i) P.cnt[i] += P.cnt[i - 1];
-        P.out.resize(P.pr.size());
-        for (const PairRef& x : P.pr) P.out[P.cnt[idx(x)]++] = x;
+        const size_t span = (size_t)(a1 - a0) * C;
+        if (span <= ((size_t)1 << 20) || span <= 4 * P.pr.size()) {   // dense counting sort (C5: 13 x 200 slots)
+            P.cnt.assign(span + 1, 0);
+            for (const PairRef& x : P.pr) P.cnt[idx(x) + 1]++;
+            for (size_t i = 1; i < P.cnt.size(); ++i) P.cnt[i] += P.cnt[i - 1];
+            P.out.resize(P.pr.size());
+            for (const PairRef& x : P.pr) P.out[P.cnt[idx(x)]++] = x;
+        } else {   // large C with few pairs per slot: the same stable order without C^2 counters
+            P.out.assign(P.pr.begin(), P.pr.end());
+            std::stable_sort(P.out.begin(), P.out.end(), [](const PairRef& x, const PairRef& y) { return x.key < y.key; });
+        }
         const uvec<PairRef>& pr = P.out;
         for (size_t i = 0; i < pr.size();) {
             ATask tk{0, (int)(pr[i].key >> 32), (int)(pr[i].key & 0xffffffffu), (int)P.ents.size(), 0, 0, 0, 0};

@@ -524,9 +524,9 @@ struct Slot {
     char* pin = nullptr;
     size_t pin_cap = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    std::mutex mu;   // one call per device at a time; calls on different devices run concurrently
 };
 Slot g_slot[64];
-std::mutex g_mu;
 size_t r256(size_t b) { return (std::max<size_t>(b, 1) + 255) & ~(size_t)255; }
 
 }  // namespace homog
@@ -555,8 +555,8 @@ int sfmx_homography_ratios(const sfmx_point2f* const* keypoints, const int32_t* 
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { set_last_error("no HIP device visible"); return SFMX_EDEVICE; }
     if (device < 0 || device >= ndev) { set_last_error("device index out of range"); return SFMX_EINVAL; }
     if (device >= 64) { set_last_error("device index out of range"); return SFMX_EINVAL; }
-    std::lock_guard<std::mutex> lock(g_mu);
     Slot& S = g_slot[device];
+    std::lock_guard<std::mutex> lock(S.mu);
     if (!S.checked) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {

@@ -39,7 +39,7 @@ inline int host_threads() {
 // waits for its slowest worker) cost 50-400 us per loop on a loaded host.
 class HostPool {
 public:
-    static constexpr int SPIN_US = 3000;
+    static constexpr int SPIN_US = 1000;   // r06: 3000 before; CPU burn between calls
     const int spin_us = env_int(SFMX_DIAG_ENV("SFMX_HOST_SPIN_US"), SPIN_US, 0, 100000);
     explicit HostPool(int workers) {
         for (int t = 0; t < workers; ++t) th_.emplace_back([this] { loop(); });

@@ -197,6 +197,8 @@ struct sfmx_matcher {
     unsigned flags_want = 0;
     hipStream_t flags_stream = nullptr;
     std::vector<const void*> last_src;     // the device descriptors of the last set_images_device
+    hipStream_t run_stream = nullptr;      // the stream of the last run (the re-run is ordered behind it)
+    hipEvent_t fix_ev[2] = {nullptr, nullptr};   // set-stream point / re-run end (resolve_flags)
     std::vector<int> last_cols;
     bool run_spec = false;                 // the last run assumed integrality not yet confirmed
     std::vector<int32_t> last_pairs;
@@ -555,6 +557,7 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     m->n_pairs = n_pairs;
     m->dense_total = dense;
     m->has_run = true;
+    m->run_stream = st;
     m->run_spec = m->flags_pending;
     if (m->run_spec) {   // what a re-run on the exact paths needs (resolve_flags)
         m->last_pairs.assign(pairs, pairs + 2 * (size_t)n_pairs);
@@ -568,7 +571,12 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
 // The integrality check of set_images_device, deferred to the first read of results (flags_pending):
 // wait for the published flags (long since written); if an image is not integral, give every image
 // its fp32 rows, mark the images, and re-run the last run, whose int8 results assumed integrality.
-int resolve_flags(sfmx_matcher* m) {
+// Ordering: the fp32 prep and the re-run go on the last run's stream, after an event of
+// the set stream (the images' prep), so they can neither overlap the original run nor the set; the
+// reader's stream then waits on the re-run's end (fetch / stats), or the host does (device_results,
+// whose pointers may be used on any stream).  The caller's device descriptors are re-read here:
+// sfmx.h requires them to stay valid and unchanged until the run's results are read.
+int resolve_flags(sfmx_matcher* m, hipStream_t reader, bool host_wait) {
     if (!m->flags_pending) return SFMX_OK;
     const hipStream_t st = m->flags_stream;
     const int n = m->n_imgs;
@@ -590,22 +598,37 @@ int resolve_flags(sfmx_matcher* m) {
     if (!any) { m->run_spec = false; return SFMX_OK; }   // the assumption held
     m->any_nonintegral = true;
     for (int i = 0; i < n; ++i) m->imgs[i].integral = fl[i] ? 0 : 1;
+    if (!m->fix_ev[0])
+        for (auto& e : m->fix_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const hipStream_t rs = m->has_run ? m->run_stream : st;
+    if (rs != st) {
+        HIPCHK(hipEventRecord(m->fix_ev[0], st));
+        HIPCHK(hipStreamWaitEvent(rs, m->fix_ev[0], 0));
+    }
     int rc;
     if ((rc = m->f32.ensure((size_t)m->total_rows * SIFT_DIM * 4))) return rc;
     for (int i = 0; i < n; ++i) {
         const ImgDev& d = m->imgs[i];
         HIPCHK(launch_prep_f32((const float*)m->last_src[i], d.rows, m->last_cols[i], d.rows_pad,
-                               m->f32.as<float>() + d.row0 * SIFT_DIM, st));
+                               m->f32.as<float>() + d.row0 * SIFT_DIM, rs));
     }
     if ((rc = m->stage_imgs.ensure(sizeof(ImgDev) * n))) return rc;
     std::memcpy(m->stage_imgs.p, m->imgs.data(), sizeof(ImgDev) * n);
-    HIPCHK(hipMemcpyAsync(m->imgs_d.p, m->stage_imgs.p, sizeof(ImgDev) * n, hipMemcpyHostToDevice, st));
-    if ((rc = m->stage_imgs.copied(st))) return rc;
+    HIPCHK(hipMemcpyAsync(m->imgs_d.p, m->stage_imgs.p, sizeof(ImgDev) * n, hipMemcpyHostToDevice, rs));
+    if ((rc = m->stage_imgs.copied(rs))) return rc;
     m->plan_valid = false;
-    if (!m->run_spec) return SFMX_OK;
-    m->run_spec = false;
-    const std::vector<int32_t> pairs = m->last_pairs;
-    return run_impl(m, pairs.data(), (int)(pairs.size() / 2), m->last_ratio, m->last_distinct, m->last_min_count, st);
+    if (m->run_spec) {
+        m->run_spec = false;
+        const std::vector<int32_t> pairs = m->last_pairs;
+        if ((rc = run_impl(m, pairs.data(), (int)(pairs.size() / 2), m->last_ratio, m->last_distinct,
+                           m->last_min_count, rs))) return rc;
+    }
+    if (host_wait) HIPCHK(hipStreamSynchronize(rs));
+    else if (reader != rs) {
+        HIPCHK(hipEventRecord(m->fix_ev[1], rs));
+        HIPCHK(hipStreamWaitEvent(reader, m->fix_ev[1], 0));
+    }
+    return SFMX_OK;
 }
 
 int fetch_impl(sfmx_matcher* m, sfmx_dmatch* out, int64_t cap, int64_t* required, int64_t* pair_offsets,
@@ -613,7 +636,7 @@ int fetch_impl(sfmx_matcher* m, sfmx_dmatch* out, int64_t cap, int64_t* required
     if (!m) return fail(SFMX_EINVAL, "null matcher");
     if (!m->has_run) return fail(SFMX_ESTATE, "fetch before run");
     DeviceGuard g(m->device);
-    { const int rc_ = resolve_flags(m); if (rc_) return rc_; }
+    { const int rc_ = resolve_flags(m, st, false); if (rc_) return rc_; }
     std::vector<int64_t> off(m->n_pairs + 1);
     int32_t unsettled = 0;
     HIPCHK(hipMemcpyAsync(off.data(), m->offsets.p, sizeof(int64_t) * (m->n_pairs + 1), hipMemcpyDeviceToHost, st));
@@ -694,6 +717,7 @@ int sfmx_matcher_destroy(sfmx_matcher* m) {
         for (DevBuf* b : bufs) b->release();
         for (auto& e : m->ev) if (e) (void)hipEventDestroy(e);
         for (auto& e : m->ov_ev) if (e) (void)hipEventDestroy(e);
+        for (auto& e : m->fix_ev) if (e) (void)hipEventDestroy(e);
         for (auto& e : m->bev) if (e) (void)hipEventDestroy(e);
         if (m->sx) (void)hipStreamDestroy(m->sx);
         if (m->sp) (void)hipStreamDestroy(m->sp);
@@ -726,7 +750,7 @@ int sfmx_matcher_device_results(sfmx_matcher* m, const sfmx_dmatch** matches, co
     if (!m->has_run) return fail(SFMX_ESTATE, "no results before run");
     {
         DeviceGuard g(m->device);
-        { const int rc_ = resolve_flags(m); if (rc_) return rc_; }
+        { const int rc_ = resolve_flags(m, nullptr, true); if (rc_) return rc_; }
     }
     if (matches) *matches = m->out.as<const sfmx_dmatch>();
     if (pair_offsets) *pair_offsets = m->offsets.as<const int64_t>();
@@ -738,7 +762,7 @@ int sfmx_matcher_stats(sfmx_matcher* m, int64_t* slow_queries, int64_t* fp32_pai
     if (!m) return fail(SFMX_EINVAL, "null matcher");
     if (!m->has_run) return fail(SFMX_ESTATE, "no stats before run");
     DeviceGuard g(m->device);
-    { const int rc_ = resolve_flags(m); if (rc_) return rc_; }
+    { const int rc_ = resolve_flags(m, (hipStream_t)stream, false); if (rc_) return rc_; }
     int32_t sc = 0, unsettled = 0;
     HIPCHK(hipMemcpyAsync(&sc, m->slow_count.p, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
     HIPCHK(hipMemcpyAsync(&unsettled, m->unsettled.p, sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
