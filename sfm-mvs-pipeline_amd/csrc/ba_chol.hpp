@@ -71,6 +71,15 @@ __device__ __forceinline__ void tile_load_wt(double (*dst)[LDT], __amdgpu_buffer
         *reinterpret_cast<double2*>(&dst[e / NB][e % NB]) = ld_wt2(rs, src + (size_t)(e / NB) * ld + e % NB);
     }
 }
+// tile_load_wt of the rows in 4-row chunks `chunks` only (the other rows of dst are not written)
+__device__ __forceinline__ void tile_load_wt_rows(double (*dst)[LDT], __amdgpu_buffer_rsrc_t rs, size_t src, int ld, int chunks) {
+#pragma unroll
+    for (int q = 0; q < NB * NB / (2 * NTH); ++q) {
+        const int e = q * (2 * NTH) + 2 * threadIdx.x;
+        if ((chunks >> ((e / NB) >> 2)) & 1)
+            *reinterpret_cast<double2*>(&dst[e / NB][e % NB]) = ld_wt2(rs, src + (size_t)(e / NB) * ld + e % NB);
+    }
+}
 __device__ __forceinline__ void tile_regs_wt(f64x4 (&t)[NW], const double* __restrict__ src, int ld) {
     const int w = threadIdx.x >> 6;
 #pragma unroll
@@ -125,6 +134,55 @@ __device__ __forceinline__ void mfma_nt(const double (*A)[LDT], const double (*X
     }
 }
 
+// The same products restricted to the structurally nonzero operands (r06, ba_plan.cpp row_masks):
+// only the waves whose row strip is in `rows`, the output column tiles in `cols` and the 4-wide
+// k-steps of the hull of `ks`; the skipped steps would add exact zeros, so every computed tile has
+// the bits of the full product (up to the sign of a zero).  Masks are wave-uniform; the column set
+// is a template argument (a switch over the 15 sets) so the k loop keeps the branch-free form whose
+// LDS operand loads the compiler pipelines (a per-MFMA mask test made the r06 first form slower
+// than the full product: 4.1 us for 36 MFMA steps per wave against 2.9 us for 64).
+template <int CM, bool NT>
+__device__ __forceinline__ void mfma_cm(const double (*A)[LDT], const double (*B)[LDT], f64x4 acc[NW], int w, int klo,
+                                        int khi) {
+    const int l = threadIdx.x & 63, m = l & 15, kq = l >> 4;
+#pragma unroll 4
+    for (int st = klo; st < khi; ++st) {
+        const double av = A[16 * w + m][4 * st + kq];
+#pragma unroll
+        for (int c = 0; c < NW; ++c)
+            if ((CM >> c) & 1)
+                acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, NT ? B[16 * c + m][4 * st + kq] : B[4 * st + kq][16 * c + m],
+                                                              acc[c], 0, 0, 0);
+    }
+}
+template <bool NT>
+__device__ __forceinline__ void mfma_masked(const double (*A)[LDT], const double (*B)[LDT], f64x4 acc[NW], int rows,
+                                            int cols, int ks) {
+    static_assert(NW == 4, "column-set dispatch over 4 column tiles");
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int c = 0; c < NW; ++c) acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+    if (!((rows >> w) & 1) || !ks || !cols) return;
+    const int klo = __builtin_ctz((unsigned)ks), khi = 32 - __builtin_clz((unsigned)ks);
+    switch (cols & 15) {
+#define SFMX_CM(v) case v: mfma_cm<v, NT>(A, B, acc, w, klo, khi); break;
+        SFMX_CM(1) SFMX_CM(2) SFMX_CM(3) SFMX_CM(4) SFMX_CM(5) SFMX_CM(6) SFMX_CM(7) SFMX_CM(8) SFMX_CM(9)
+        SFMX_CM(10) SFMX_CM(11) SFMX_CM(12) SFMX_CM(13) SFMX_CM(14) SFMX_CM(15)
+#undef SFMX_CM
+        default: break;
+    }
+}
+// acc[c] = A[strip] * B restricted (A, B row-major 64x64 in LDS)
+__device__ __forceinline__ void mfma_nn_m(const double (*A)[LDT], const double (*B)[LDT], f64x4 acc[NW], int rows,
+                                          int cols, int ks) {
+    mfma_masked<false>(A, B, acc, rows, cols, ks);
+}
+// acc[c] = A[strip] * X^T restricted
+__device__ __forceinline__ void mfma_nt_m(const double (*A)[LDT], const double (*X)[LDT], f64x4 acc[NW], int rows,
+                                          int cols, int ks) {
+    mfma_masked<true>(A, X, acc, rows, cols, ks);
+}
+
 // 1/d: hardware estimate + two Newton steps (within an ulp or so of the divide).
 __device__ __forceinline__ double rcp_nr(double d) {
     double r = __builtin_amdgcn_rcp(d);
@@ -145,6 +203,17 @@ __device__ __forceinline__ double rcp_nr(double d) {
 //          of 2x2 pivot blocks, each lane holding a 2x2 block; the 2x2 pivot
 //          inverse is closed-form and its two scalar pivots (a, det/a) are the
 //          scalar Cholesky pivots, i.e. exactly where LLT would fail.
+// diagnostic build only (r06): a timeline of the last chol_factor launch, per ticket 16 wall-clock stamps
+// (0 start, 1 operands ready, 2 W_k ready, 3 W_k loaded, 4 G done, 5 update done, 6 task finisher known,
+// 7 inverse start, 8-11 its sweeps, 12 W_k published, 13 end, 15 hw id),
+// read by sfmx_ba_debug_chol_trace (tools/chol_trace.py)
+constexpr int CHOL_TRACE_MAX = 512;
+#ifdef SFMX_DIAG
+__device__ long long g_chol_trace[CHOL_TRACE_MAX][16];
+#define CHOL_TRACE(tk, i) do { if (threadIdx.x == 0 && (tk) < CHOL_TRACE_MAX) g_chol_trace[tk][i] = wall_clock64(); } while (0)
+#else
+#define CHOL_TRACE(tk, i) do { } while (0)
+#endif
 constexpr int LDP = 18;   // LDS row stride of the 16-wide panels (16-B aligned rows)
 // chol_diag_tile's workspace: column panel [NB][LDP] | -A_BB^-1 [16][LDP] | inner panel [32] | one
 // -M strip [16][LDP] per wave; it fits a tile buffer at NB = 64, not at NB = 32
@@ -227,24 +296,30 @@ __device__ __forceinline__ void inner_inverse16(const double* __restrict__ Pc, i
 // tile k) and the panel's intrinsics Schur terms contrib_k[i][j] = sum_r y[r][i] w[r][j] (i < RW-1).
 // buf: 64 x LDT doubles of LDS workspace; wv: NB x RW doubles of LDS.  WT: W_k and the R rows are
 // stored write-through (sc1), for readers in the same launch (chol_factor).
-template <int RW, bool WT = false>
-__device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[NW], int k, double* __restrict__ Wk,
-                                               double* __restrict__ R, const double* __restrict__ y,
-                                               double* __restrict__ wv, double* __restrict__ contrib,
-                                               int* __restrict__ fail, double (*buf)[LDT], double* dws,
-                                               int* wver = nullptr) {
-    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, m = l & 15, kq = l >> 4, k0 = k * NB;
-    double* ws = DIAG_WS_IN_BUF ? &buf[0][0] : dws;   // the sweeps' workspace (dead once W is written)
+// The symmetric sweeps of chol_diag_tile over the 16-row panels in `sweep` (ascending); the panels in
+// `pad` are identity padding (r06: not swept, set to their result directly); the others are left
+// alone (already swept: r06's pre-sweep of the panels an update does not touch, see chol_factor).
+// A non-positive pivot sets fail bit 1.
+__device__ __forceinline__ void diag_sweeps(f64x4 (&t)[NW], int sweep, int skip_panels, int* __restrict__ fail,
+                                            double (*buf)[LDT], double* dws, int trk = CHOL_TRACE_MAX) {
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, m = l & 15, kq = l >> 4;
+    double* ws = DIAG_WS_IN_BUF ? &buf[0][0] : dws;   // the sweeps' workspace
     double* Pc = ws;                       // [64][LDP]  column panel A_:B
     double* Qn = ws + NB * LDP;            // [16][LDP]  -A_BB^-1
     double* ipan = Qn + 16 * LDP;          // [16][2]    inner column panel
     double* Mw = ipan + 32 + 16 * LDP * w; // [16][LDP]  this wave's -M strip
-    CHOL_STAMP(0);
     bool bad = false;
-    CHOL_STAMP(1);
 #pragma unroll
     for (int s = 0; s < NB / 16; ++s) {
         const bool rowB = (w == s);
+        if (!(((sweep | skip_panels) >> s) & 1)) continue;   // swept before (pre-sweep)
+        if ((skip_panels >> s) & 1) {
+            // r06: a panel of identity padding rows (no coupling, diagonal exactly 1: ba_add_cam) sweeps
+            // to A_BB <- -1 on its diagonal and M = 0; the other column tiles are unchanged
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t[s][r] = (rowB && trow(r) == tcol()) ? -1.0 : 0.0;
+            continue;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) Pc[(16 * w + trow(r)) * LDP + tcol()] = t[s][r];
         __syncthreads();
@@ -277,8 +352,24 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[NW], int k, double* __
         }
         __syncthreads();   // Pc is rewritten by the next sweep
         CHOL_STAMP(5 + 4 * s);
+        CHOL_TRACE(trk, 8 + s);
     }
     if (bad) atomicOr(fail, 1);
+}
+
+struct NoDefer { __device__ void operator()() const {} };
+
+template <int RW, bool WT = false, class Defer = NoDefer>
+__device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[NW], int k, double* __restrict__ Wk,
+                                               double* __restrict__ R, const double* __restrict__ y,
+                                               double* __restrict__ wv, double* __restrict__ contrib,
+                                               int* __restrict__ fail, double (*buf)[LDT], double* dws,
+                                               int* wver = nullptr, int skip_panels = 0, int trk = CHOL_TRACE_MAX,
+                                               int done_panels = 0, Defer defer = Defer{}) {
+    const int tid = threadIdx.x, w = tid >> 6, k0 = k * NB;
+    CHOL_STAMP(0);
+    CHOL_STAMP(1);
+    diag_sweeps(t, ((1 << (NB / 16)) - 1) & ~skip_panels & ~done_panels, skip_panels, fail, buf, dws, trk);
 #pragma unroll
     for (int c = 0; c < NW; ++c)
 #pragma unroll
@@ -291,7 +382,9 @@ __device__ __forceinline__ void chol_diag_tile(f64x4 (&t)[NW], int k, double* __
     if (WT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // W_k drained before its version add
     __syncthreads();
     if (wver && tid == 0) __hip_atomic_fetch_add((g_i32*)wver, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // W_k ready
+    CHOL_TRACE(trk, 12);
     CHOL_STAMP(20);
+    defer();   // (r06: an inverting one-source task's y terms, once W_k is out; they only feed y below)
     {   // w = W y: 4 threads per row i, each over 16 columns c for all RW right-hand sides (16-B LDS
         // reads), the 4 partial sums combined by two shuffles in a fixed order
         static_assert(RW % 2 == 0, "RW is k + 1 with k odd");
@@ -375,7 +468,7 @@ template <int RW>
 __global__ __launch_bounds__(NTH)
 void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
                 const int* __restrict__ src, int ninv, double* __restrict__ W, double* __restrict__ contrib,
-                int* __restrict__ fail) {
+                int* __restrict__ fail, const int* __restrict__ tpre) {
     if (step_gated(fail + 1)) return;
     __shared__ CholLds<RW> sm;
     const int tid = threadIdx.x, w = tid >> 6;
@@ -388,6 +481,10 @@ void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const 
     tile_regs(t, dst, npad);                                                   // A_ab (prefetch)
     if (diag)
         for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = R[(size_t)a0 * RW + e];
+    // r06: an inverting one-source task sweeps the panels its update does not touch first (tpre,
+    // ba_plan.cpp row_masks), as chol_factor does while it waits for W_k: the same bits in every form
+    const int pre = (diag && (int)blockIdx.x < ninv && task.w - task.z == 1) ? tpre[blockIdx.x] : 0;
+    if (pre) diag_sweeps(t, pre, 0, fail, sm.n, sm.dws);
     for (int s = task.z; s < task.w; ++s) {
         const int k = src[s], k0 = k * NB;
         tile_load(sm.a, S + (size_t)a0 * npad + k0, npad);                     // A_ak
@@ -434,7 +531,8 @@ void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const 
         __syncthreads();   // the next source panel overwrites sm
     }
     if (diag && (int)blockIdx.x < ninv) {
-        chol_diag_tile<RW>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n, sm.dws);
+        chol_diag_tile<RW>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n, sm.dws, nullptr, 0,
+                           CHOL_TRACE_MAX, pre);
     } else {
         tile_store(t, dst, npad);
         if (diag)
@@ -455,6 +553,24 @@ void chol_level(double* __restrict__ S, int npad, double* __restrict__ R, const 
 // The critical path of a level falls from n source steps + inverse to one source step + the
 // hand-off + inverse.  part = {task (global index), source index, slot, n | inverting << 16};
 // ctr[task] is zero at launch and the last part zeroes it again.
+// r06: only the product tiles a part's row masks allow (strip w in ra, column tile c in rb; the rest
+// are exact zeros): a quarter of the stores on the C5 ring, and the finisher loads the same subset
+template <int RW>
+__device__ __forceinline__ void part_store_m(double* __restrict__ slot, const f64x4 (&u)[NW], const double* ys, int nys,
+                                             int ra, int rb) {
+    const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if ((ra >> w) & 1)
+#pragma unroll
+        for (int c = 0; c < NW; ++c)
+            if ((rb >> c) & 1)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    __hip_atomic_store((g_u64*)&slot[(4 * c + r) * NTH + tid], (unsigned long long)__double_as_longlong(u[c][r]),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int u2 = 0; u2 < nys; ++u2)
+        __hip_atomic_store((g_u64*)&slot[(4 * NW + u2) * NTH + tid], (unsigned long long)__double_as_longlong(ys[u2]),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <int RW>
 __device__ __forceinline__ void part_store(double* __restrict__ slot, const f64x4 (&u)[NW], const double* ys, int nys) {
     const int tid = threadIdx.x;
@@ -473,7 +589,8 @@ template <int RW>
 __global__ __launch_bounds__(NTH)
 void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
                       const int4* __restrict__ parts, const int* __restrict__ src, double* __restrict__ W,
-                      double* __restrict__ contrib, int* __restrict__ fail, double* pbuf, int* ctr) {
+                      double* __restrict__ contrib, int* __restrict__ fail, double* pbuf, int* ctr,
+                      const int* __restrict__ tpre) {
     if (step_gated(fail + 1)) return;
     __shared__ CholLds<RW> sm;
     __shared__ int last_sh;
@@ -488,10 +605,12 @@ void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, 
     const int k = src[part.y], k0 = k * NB;
     double* dst = S + (size_t)a0 * npad + b0;
     f64x4 t[NW];
+    const int pre = (n == 1 && diag && inv) ? tpre[part.x] : 0;   // (r06, as chol_level)
     if (n == 1) {
         tile_regs(t, dst, npad);                                                   // A_ab (prefetch)
         if (diag)
             for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = R[(size_t)a0 * RW + e];
+        if (pre) diag_sweeps(t, pre, 0, fail, sm.n, sm.dws);
     }
     tile_load(sm.a, S + (size_t)a0 * npad + k0, npad);                         // A_ak
     tile_load(sm.m, W + (size_t)k * NB * NB, NB);                              // W_k
@@ -569,7 +688,8 @@ void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, 
     }
     __syncthreads();
     if (diag && inv) {
-        chol_diag_tile<RW>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n, sm.dws);
+        chol_diag_tile<RW>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n, sm.dws, nullptr, 0,
+                           CHOL_TRACE_MAX, pre);
     } else {
         tile_store(t, dst, npad);
         if (diag)
@@ -599,12 +719,14 @@ void chol_level_split(double* __restrict__ S, int npad, double* __restrict__ R, 
 // Same operations in the same order as the level launches: bit-identical.
 __device__ __forceinline__ int tver_id(int a, int b) { return a * (a + 1) / 2 + b; }
 
+
+
 template <int RW>
 __global__ __launch_bounds__(NTH)
 void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const int4* __restrict__ tasks,
                  const int4* __restrict__ items, const int4* __restrict__ need, const int* __restrict__ src,
                  double* __restrict__ W, double* __restrict__ contrib, int* __restrict__ fail, double* pbuf,
-                 int* tctr, int* ctr, int nitems, int nver, long long tmo) {
+                 int* tctr, int* ctr, int nitems, int nver, long long tmo, const int4* __restrict__ imask) {
     if (step_gated(fail + 1)) return;
     __shared__ CholLds<RW> sm;
     __shared__ int sh[2];
@@ -617,28 +739,50 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
     __syncthreads();
     const int tk = sh[0];
     const int4 it = items[tk], nd = need[tk];
+    // r06 row masks (ba_plan.cpp row_masks): x = ra | rb << 4 | G's column tiles << 8 | the inverted
+    // tile's padding panels << 12, y = ka, z = kb (wave-uniform)
+    const int4 mk0 = imask[tk];
+    const int mx = __builtin_amdgcn_readfirstlane(mk0.x), mka = __builtin_amdgcn_readfirstlane(mk0.y),
+              mkb = __builtin_amdgcn_readfirstlane(mk0.z);
+    const int m_ra = mx & 15, m_rb = (mx >> 4) & 15, m_gc = (mx >> 8) & 15, m_pad = (mx >> 12) & 15,
+              m_pre = (mx >> 16) & 15;   // pre: an inverting one-source task's panels its update leaves alone
+    CHOL_TRACE(tk, 0);
+#ifdef SFMX_DIAG
+    if (tid == 0 && tk < CHOL_TRACE_MAX) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_chol_trace[tk][15] = ((long long)xcc << 32) | hw;
+        for (int q = 1; q < 15; ++q) g_chol_trace[tk][q] = 0;
+    }
+#endif
     // one lane waits until tile `id` carries version `v` (bounded: `tmo` ticks without the version
     // moving set fail bit 2 and the item runs on, so every counter still advances and the launch drains)
-    auto wait_ver = [&](int id, int v) {
+    auto wait_at = [&](int* word, int v) {
         long long t0 = wall_clock64();
         int last = -1;
         for (;;) {
-            const int cur = __hip_atomic_load((g_i32*)&tver[id], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int cur = __hip_atomic_load((g_i32*)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (cur >= v) return;
             if (cur != last) { last = cur; t0 = wall_clock64(); }   // progress restarts the clock
             __builtin_amdgcn_s_sleep(1);
             if (wall_clock64() - t0 > tmo) { atomicOr(fail, FAIL_FACTOR_WAIT); return; }
         }
     };
+    auto wait_ver = [&](int id, int v) { wait_at(&tver[id], v); };
     const __amdgpu_buffer_rsrc_t rS = wt_rsrc(S), rW = wt_rsrc(W);
     int done_id = -1;   // the tile whose version this item advances (-1: none)
+    int upper_k0 = -1, upper_a0 = 0;   // a diagonal part's upper tile G^T, stored after the version add
     if (it.y < 0) {     // leaf: diagonal tile k, untouched by any update
         const int k = it.x, k0 = k * NB;
         f64x4 t[NW];
         tile_regs(t, S + (size_t)k0 * npad + k0, npad);
         for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = R[(size_t)k0 * RW + e];
         __syncthreads();
-        chol_diag_tile<RW, true>(t, k, W + (size_t)k * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a, sm.dws, &tver[tver_id(k, k)]);
+        CHOL_TRACE(tk, 7);
+        chol_diag_tile<RW, true>(t, k, W + (size_t)k * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.a, sm.dws, &tver[tver_id(k, k)],
+                                 m_pad, tk);
         done_id = tver_id(k, k);
     } else {
         const int4 task = tasks[it.x];
@@ -654,30 +798,45 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
             if (n == 1) wait_ver(tver_id(a, b), nd.w);
         }
         __syncthreads();
+        CHOL_TRACE(tk, 1);
         f64x4 t[NW];
-        if (n == 1) {
+        // the destination (final but for this task) loads now in a one-source task and, r06, in every
+        // part of an inverting multi-source task (the finisher then starts its subtraction at once)
+        const bool early_dst = n == 1 || (diag && inv);
+        if (n > 1 && early_dst && tid == 0) wait_ver(tver_id(a, b), nd.w);
+        if (n > 1 && early_dst) __syncthreads();
+        if (early_dst) {
             tile_regs_wt(t, dst, npad);
             if (diag)
                 for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = ld_wt(&R[(size_t)a0 * RW + e]);
         }
         tile_load_wt(sm.a, rS, (size_t)a0 * npad + k0, npad);                   // A_ak
         if (!diag) tile_load_wt(sm.n, rS, (size_t)b0 * npad + k0, npad);        // A_bk
+        // r06: the update A_aa -= G A_ak^T touches only A_ak's row strips; the other panels of the
+        // (final-but-this-update) diagonal tile are swept now, while W_k is still being computed
+        // (sweeping commutes with adding to the unswept block: the same inverse, other rounding)
+        if (m_pre) diag_sweeps(t, m_pre, 0, fail, sm.n, sm.dws, tk);
         if (tid == 0) wait_ver(tver_id(k, k), nd.z - 1);   // W_k stored (its R rows may still be in flight)
         __syncthreads();
-        tile_load_wt(sm.m, rW, (size_t)k * NB * NB, NB);                        // W_k
+        CHOL_TRACE(tk, 2);
+        tile_load_wt_rows(sm.m, rW, (size_t)k * NB * NB, NB, mka);             // W_k (the rows G reads)
         __syncthreads();
+        CHOL_TRACE(tk, 3);
         f64x4 g[NW];
-        mfma_nn(sm.a, sm.m, g);   // G = A_ak W_k
+        mfma_nn_m(sm.a, sm.m, g, m_ra, m_gc, mka);   // G = A_ak W_k (its structurally nonzero part)
         __syncthreads();
+        CHOL_TRACE(tk, 4);
 #pragma unroll
         for (int c = 0; c < NW; ++c)
 #pragma unroll
             for (int r = 0; r < 4; ++r) sm.m[16 * w + trow(r)][16 * c + tcol()] = g[c][r];
         __syncthreads();
         f64x4 upd[NW];
-        mfma_nt(sm.m, diag ? sm.a : sm.n, upd);   // G X^T
+        mfma_nt_m(sm.m, diag ? sm.a : sm.n, upd, m_ra, m_rb, mkb);   // G X^T
+        CHOL_TRACE(tk, 5);
         double ys[OPT];
-        if (diag) {
+        // y_a terms of a diagonal part: ys = A_ak w_k (w_k = the R rows of k, stored after W_k)
+        auto y_terms = [&]() {
             if (tid == 0) wait_ver(tver_id(k, k), nd.z);   // w_k (the R rows of k) stored
             __syncthreads();
             for (int e = tid; e < NB * RW; e += NTH) sm.rk[e] = ld_wt(&R[(size_t)k0 * RW + e]);   // w_k
@@ -692,40 +851,67 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
                 if (TPO >= 4) sum += __shfl_xor(sum, 2);
                 ys[u] = sum;
             }
-#pragma unroll
-            for (int c = 0; c < NW; ++c)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) S[(size_t)(k0 + 16 * c + tcol()) * npad + a0 + 16 * w + trow(r)] = g[c][r];
-        }
+        };
+        // r06: an inverting diagonal task takes its y terms after W_a is out (they feed only the inverse's
+        // right-hand-side phase), its parts publish their products first and their y terms second, and
+        // every diagonal part stores the upper tile G^T (read by the next launch only) after its version
+        // add: none of it is on the level chain any more
+        const bool defer_y = diag && inv;
+        if (diag && !defer_y) y_terms();
         bool fin = true;
-        if (n > 1) {   // publish this part; the last arriver finishes the task
-            part_store<RW>(pbuf + (size_t)it.z * SLOT, upd, ys, diag ? OPT : 0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) {
-                const bool last = __hip_atomic_fetch_add((g_i32*)&tctr[it.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
-                if (last) {
-                    tctr[it.x] = 0;   // nobody else touches it in this launch
-                    wait_ver(tver_id(a, b), nd.w);
-                }
-                sh[1] = last;
-            }
+        int* const stored1 = tctr + nitems;       // per task: non-finishing parts whose product is stored
+        int* const stored2 = tctr + 2 * nitems;   // ... and whose y terms are (inverting diagonal tasks)
+        if (n > 1) {
+            // arrive first, publish only if not last: the arrival add picks the finisher, whose own
+            // product never leaves its registers (r05 stored and drained it before knowing)
+            if (tid == 0)
+                sh[1] = __hip_atomic_fetch_add((g_i32*)&tctr[it.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
             __syncthreads();
             fin = sh[1] != 0;
-            if (fin) {
+            double* const slot = pbuf + (size_t)it.z * SLOT;
+            if (!fin) {
+                part_store_m<RW>(slot, upd, ys, diag && !defer_y ? OPT : 0, m_ra, m_rb);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) __hip_atomic_fetch_add((g_i32*)&stored1[it.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (defer_y) {   // the y terms, then their count
+                    y_terms();
+                    for (int u2 = 0; u2 < OPT; ++u2)
+                        __hip_atomic_store((g_u64*)&slot[(4 * NW + u2) * NTH + tid], (unsigned long long)__double_as_longlong(ys[u2]),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    if (tid == 0) __hip_atomic_fetch_add((g_i32*)&stored2[it.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else {
+                if (tid == 0) {
+                    wait_at(&stored1[it.x], n - 1);   // every other part's product stored
+                    tctr[it.x] = 0;                   // nobody else touches them in this launch
+                    stored1[it.x] = 0;
+                    if (!early_dst) wait_ver(tver_id(a, b), nd.w);
+                }
+                __syncthreads();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below
-                tile_regs_wt(t, dst, npad);
-                if (diag)
-                    for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = ld_wt(&R[(size_t)a0 * RW + e]);
+                if (!early_dst) {
+                    tile_regs_wt(t, dst, npad);
+                    if (diag)
+                        for (int e = tid; e < NB * RW; e += NTH) sm.ra[e] = ld_wt(&R[(size_t)a0 * RW + e]);
+                }
                 __syncthreads();
                 const double* base = pbuf + (size_t)(it.z - j) * SLOT;   // slot of source 0 of this task
+                const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
                 for (int jj = 0; jj < n; ++jj) {
                     const double* sl = base + (size_t)jj * SLOT;
+                    // the part's row masks (its item is tk - j + jj): the tiles it stored; the rest are zeros
+                    const int pm = jj == j ? mx : __builtin_amdgcn_readfirstlane(imask[tk - j + jj].x);
+                    const int pra = pm & 15, prb = (pm >> 4) & 15;
+                    if ((pra >> wv) & 1)
 #pragma unroll
-                    for (int c = 0; c < NW; ++c)
+                        for (int c = 0; c < NW; ++c)
+                            if ((prb >> c) & 1)
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) t[c][r] -= (jj == j) ? upd[c][r] : ld_wt(&sl[(4 * c + r) * NTH + tid]);
-                    if (diag) {
+                                for (int r = 0; r < 4; ++r) t[c][r] -= (jj == j) ? upd[c][r] : ld_wt(&sl[(4 * c + r) * NTH + tid]);
+                    if (diag && !defer_y) {
 #pragma unroll
                         for (int u = 0; u < OPT; ++u) {
                             const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
@@ -738,7 +924,7 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
         } else {
 #pragma unroll
             for (int c = 0; c < NW; ++c) t[c] -= upd[c];
-            if (diag) {
+            if (diag && !defer_y) {
 #pragma unroll
                 for (int u = 0; u < OPT; ++u) {
                     const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
@@ -746,11 +932,33 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
                 }
             }
         }
+        CHOL_TRACE(tk, 6);
         if (fin) {
             __syncthreads();
-            if (diag && inv) {
+            if (defer_y) {
+                CHOL_TRACE(tk, 7);
+                // the y terms in source order (the immediate path's arithmetic and order), once W_a is out
+                auto later = [&]() {
+                    y_terms();
+                    if (n > 1 && tid == 0) {
+                        wait_at(&stored2[it.x], n - 1);   // every other part's y terms stored
+                        stored2[it.x] = 0;
+                    }
+                    __syncthreads();
+                    const double* base = pbuf + (size_t)(it.z - j) * SLOT;
+                    for (int jj = 0; jj < n; ++jj) {
+                        const double* sl = base + (size_t)jj * SLOT;
+#pragma unroll
+                        for (int u = 0; u < OPT; ++u) {
+                            const int o = tid / TPO + u * (NTH / TPO), i = o / RW, q = o % RW;
+                            const double y = (jj == j) ? ys[u] : ld_wt(&sl[(4 * NW + u) * NTH + tid]);
+                            if (tid % TPO == 0) sm.ra[i * RW + q] -= y;
+                        }
+                    }
+                    __syncthreads();
+                };
                 chol_diag_tile<RW, true>(t, a, W + (size_t)a * NB * NB, R, sm.ra, sm.wv, contrib, fail, sm.n, sm.dws,
-                                         &tver[tver_id(a, a)]);
+                                         &tver[tver_id(a, a)], m_pad, tk, m_pre, later);
             } else {
                 tile_store_wt(t, dst, npad);
                 if (diag)
@@ -758,14 +966,23 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
             }
             done_id = tver_id(a, b);
         }
+        upper_k0 = diag ? k0 : -1;
+        upper_a0 = a0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains before the version add
     __syncthreads();
+    CHOL_TRACE(tk, 13);
     if (tid == 0) {
         if (done_id >= 0) __hip_atomic_fetch_add((g_i32*)&tver[done_id], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (__hip_atomic_fetch_add((g_i32*)&ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nitems - 1)
             for (int e = 0; e < nver + 2; ++e) __hip_atomic_store((g_i32*)&ctr[e], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (upper_k0 >= 0)   // a diagonal part: upper tile (k, a) = G^T (row k0 + j, column a0 + i holds G[i][j]), from sm.m
+#pragma unroll
+        for (int c = 0; c < NW; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                S[(size_t)(upper_k0 + 16 * c + tcol()) * npad + upper_a0 + 16 * w + trow(r)] = sm.m[16 * w + trow(r)][16 * c + tcol()];
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1219,6 +1219,23 @@ void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int*
         const int f = blockIdx.x - C;
         double s0 = 0.0, s1 = 0.0;
         int e = t;
+        // r06: 8 iterations' loads in flight before their adds (same chains, same order): these few
+        // workgroups stream every slot of the launch (C5: ~20k strided loads each) and with 2 loads in
+        // flight per thread they set ba_camred's length
+        constexpr int BT = 8;
+        for (; e + (2 * BT - 1) * CRED_THREADS < nslots; e += 2 * BT * CRED_THREADS) {
+            double va[BT], vb[BT];
+#pragma unroll
+            for (int j = 0; j < BT; ++j) {
+                va[j] = gpart[(size_t)(e + 2 * j * CRED_THREADS) * NCP + NFC + f];
+                vb[j] = gpart[(size_t)(e + (2 * j + 1) * CRED_THREADS) * NCP + NFC + f];
+            }
+#pragma unroll
+            for (int j = 0; j < BT; ++j) {
+                s0 += va[j];
+                s1 += vb[j];
+            }
+        }
         for (; e + CRED_THREADS < nslots; e += 2 * CRED_THREADS) {
             s0 += gpart[(size_t)e * NCP + NFC + f];
             s1 += gpart[(size_t)(e + CRED_THREADS) * NCP + NFC + f];

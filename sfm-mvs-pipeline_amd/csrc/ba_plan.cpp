@@ -322,6 +322,68 @@ void make_plan(int C, const std::vector<char>& adj, int order_mode, FactorPlan& 
     out = std::move(best);
 }
 
+
+// Row-level symbolic structure of the block LDL^T (r06).  Each lower tile's 64 x 64
+// pattern starts from the camera co-visibility (6 x 6 camera blocks; identity padding rows: their
+// diagonal only) and is filled by the plan's tasks in schedule order: an update of (a, b) from panel k
+// touches the rows of a that A_ak has nonzeros in times the rows of b that A_bk has.  The masks name,
+// per (task, source), the 16-row strips and 4-column chunks where A_ak / A_bk are structurally nonzero,
+// and per tile the 16-row panels that are pure padding; chol_factor skips the matrix-core steps and the
+// sweeps whose operands are exact zeros (identity), so the values are unchanged (up to signed zeros).
+void row_masks(const FactorPlan& P, const std::vector<char>& adj, std::vector<RowMask>& src_mask,
+               std::vector<int>& pad_panels) {
+    const int T = P.T, C = P.C;
+    static_assert(NBP == 64, "row masks are 64-bit rows of 64-row tiles");
+    std::vector<int> tid((size_t)T * T, -1);
+    int ntiles = 0;
+    for (int a = 0; a < T; ++a)
+        for (int b = 0; b <= a; ++b)
+            if (P.nz[(size_t)a * T + b] || a == b) tid[(size_t)a * T + b] = ntiles++;
+    std::vector<uint64_t> pat((size_t)ntiles * NBP, 0);
+    auto rowcam = [&](int r) { const int m = P.rowmap[r]; return m < 0 ? -1 : m / 6; };
+    for (int a = 0; a < T; ++a)
+        for (int b = 0; b <= a; ++b) {
+            const int id = tid[(size_t)a * T + b];
+            if (id < 0) continue;
+            for (int i = 0; i < NBP; ++i) {
+                const int ci = rowcam(a * NBP + i);
+                uint64_t m = 0;
+                for (int j = 0; j < NBP; ++j) {
+                    const int cj = rowcam(b * NBP + j);
+                    const bool nzv = ci < 0 || cj < 0 ? (a == b && i == j) : (ci == cj || adj[(size_t)ci * C + cj]);
+                    m |= (uint64_t)nzv << j;
+                }
+                pat[(size_t)id * NBP + i] = m;
+            }
+        }
+    auto rows_of = [&](int id) { uint64_t r = 0; for (int i = 0; i < NBP; ++i) r |= (uint64_t)(pat[(size_t)id * NBP + i] != 0) << i; return r; };
+    auto cols_of = [&](int id) { uint64_t c = 0; for (int i = 0; i < NBP; ++i) c |= pat[(size_t)id * NBP + i]; return c; };
+    auto strips = [](uint64_t m) { int s = 0; for (int q = 0; q < NBP / 16; ++q) s |= ((m >> (16 * q)) & 0xffffu ? 1 : 0) << q; return s; };
+    auto chunks = [](uint64_t m) { int s = 0; for (int q = 0; q < NBP / 4; ++q) s |= ((m >> (4 * q)) & 0xfu ? 1 : 0) << q; return s; };
+    src_mask.assign(P.src.size(), RowMask{0xf, 0xf, 0xffff, 0xffff});
+    for (int l = 0; l < P.height; ++l)
+        for (int t = P.task_start[l]; t < P.task_start[l + 1]; ++t) {
+            const PlanTask& tk = P.tasks[t];
+            const int dst = tid[(size_t)tk.a * T + tk.b];
+            for (int s = tk.s0; s < tk.s1; ++s) {
+                const int k = P.src[s];
+                const int ia = tid[(size_t)tk.a * T + k], ib = tid[(size_t)tk.b * T + k];
+                if (ia < 0 || ib < 0 || dst < 0) continue;   // (never: a source tile of a task is nonzero)
+                const uint64_t ra = rows_of(ia), rb = rows_of(ib);
+                src_mask[s] = RowMask{strips(ra), strips(rb), chunks(cols_of(ia)), chunks(cols_of(ib))};
+                for (int i = 0; i < NBP; ++i)
+                    if ((ra >> i) & 1) pat[(size_t)dst * NBP + i] |= rb;
+            }
+        }
+    pad_panels.assign(T, 0);
+    for (int a = 0; a < T; ++a)
+        for (int q = 0; q < NBP / 16; ++q) {
+            bool pad = true;
+            for (int i = 0; i < 16; ++i) pad = pad && P.rowmap[a * NBP + 16 * q + i] < 0;
+            pad_panels[a] |= (pad ? 1 : 0) << q;
+        }
+}
+
 }  // namespace ba
 }  // namespace sfmx
 

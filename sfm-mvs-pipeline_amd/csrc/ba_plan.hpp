@@ -60,5 +60,12 @@ struct FactorPlan {
 // the model), 2/3/4 nested dissection with leaves of 1/2/4 tiles.
 void make_plan(int C, const std::vector<char>& adj, int order_mode, FactorPlan& out);
 
+// Row-level zero structure of the factorization (ba_plan.cpp): per src entry (task, source k) the
+// 16-row strips of A_ak (ra) and A_bk (rb) and the 4-column chunks of their columns (ka, kb) that
+// can be nonzero; per tile the 16-row panels that are identity padding (bit q = rows 16q .. 16q + 15).
+struct RowMask { int ra, rb, ka, kb; };
+void row_masks(const FactorPlan& P, const std::vector<char>& adj, std::vector<RowMask>& src_mask,
+               std::vector<int>& pad_panels);
+
 }  // namespace ba
 }  // namespace sfmx

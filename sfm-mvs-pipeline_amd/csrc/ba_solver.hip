@@ -122,7 +122,9 @@ struct sfmx_ba_ctx {
         nztiles, packbuf,          // all-reduce of the nonzero lower tiles only (multi-rank)
         border, zbuf, dagctr,      // chol_backsolve: panels root first, z, [ticket, finished, zdone[T]]
         parts, pbuf, lctr,         // chol_level_split: (task, source) parts per level, product slots, arrivals
-        ditems, dneed, dctr;       // chol_factor: leaves + every level's parts, their version needs, [ticket, finished, tver]
+        ditems, dneed, dctr,       // chol_factor: leaves + every level's parts, their version needs, [ticket, finished, tver]
+        dmask,                     // chol_factor: per item, the row masks of its operands (ba_plan.cpp row_masks)
+        tpre;                      // per task: the panels swept before its update (r06 pre-sweep, every form)
     bool back_dag = true;          // SFMX_BA_BACK=0: the r02 chol_intr + one-workgroup chol_back
     bool split = true;             // SFMX_BA_SPLIT=0: chol_level (a task's sources in one workgroup)
     std::vector<int> part_start;   // per level: parts[part_start[l] .. part_start[l + 1])
@@ -182,7 +184,7 @@ struct sfmx_ba_ctx {
     ~sfmx_ba_ctx() {
         Buf* all[] = {&topo_arena, &plan_arena, &obs_xy_b, &obs_cam_b, &obs_lc_b, &obs_row_b, &moves, &obs_point, &obs_cam, &obs_xy, &pt_start, &grp, &chk, &bat, &gcam, &obs_lc, &obs_row, &lcrow, &tasks,
                       &ents, &cref_start, &cref, &camrow, &padrows, &rowmap, &leaves, &ptasks, &psrc, &lvl_start,
-                      &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &x, &cand, &scale, &colsq, &colsq2, &grad,
+                      &lvl_panels, &bs_start, &bs_k, &Wt, &contrib, &xi, &nztiles, &packbuf, &border, &zbuf, &dagctr, &parts, &pbuf, &lctr, &ditems, &dneed, &dctr, &dmask, &tpre, &x, &cand, &scale, &colsq, &colsq2, &grad,
                       &grad2, &Wr, &Wr2, &PR, &PR2, &J, &camsum, &camsum2, &plt, &sg, &rg, &hbig, &gpart, &gpl, &scal, &SR, &sol,
                       &failf, &partA, &lmst, &camscr, &pim, &pcc};
         if (plan_th) { plan_th->wait(); delete plan_th; }
@@ -442,7 +444,7 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
         hipLaunchKernelGGL(chol_factor<RW>, dim3((unsigned)c->n_ditems), dim3(NTH), 0, c->st, S, npad, R,
                            c->ptasks.as<int4>(), c->ditems.as<int4>(), c->dneed.as<int4>(), c->psrc.as<int>(),
                            c->Wt.as<double>(), c->contrib.as<double>(), fl, c->pbuf.as<double>(), c->lctr.as<int>(),
-                           c->dctr.as<int>(), c->n_ditems, c->n_ver, c->dag_timeout);
+                           c->dctr.as<int>(), c->n_ditems, c->n_ver, c->dag_timeout, c->dmask.as<int4>());
     } else {
     hipLaunchKernelGGL(chol_leaves<RW>, dim3((unsigned)pl.leaves.size()), dim3(NTH), 0, c->st, S, npad, R,
                        c->leaves.as<int>(), c->Wt.as<double>(), c->contrib.as<double>(), fl);
@@ -452,10 +454,11 @@ int solve_reduced(sfmx_ba_ctx* c, double* sol_f) {
             const int p0 = c->part_start[l], np = c->part_start[l + 1] - p0;
             hipLaunchKernelGGL(chol_level_split<RW>, dim3(np), dim3(NTH), 0, c->st, S, npad, R, c->ptasks.as<int4>(),
                                c->parts.as<int4>() + p0, c->psrc.as<int>(), c->Wt.as<double>(), c->contrib.as<double>(),
-                               fl, c->pbuf.as<double>(), c->lctr.as<int>());
+                               fl, c->pbuf.as<double>(), c->lctr.as<int>(), c->tpre.as<int>());
         } else {
             hipLaunchKernelGGL(chol_level<RW>, dim3(nt), dim3(NTH), 0, c->st, S, npad, R, c->ptasks.as<int4>() + t0,
-                               c->psrc.as<int>(), pl.ninv[l], c->Wt.as<double>(), c->contrib.as<double>(), fl);
+                               c->psrc.as<int>(), pl.ninv[l], c->Wt.as<double>(), c->contrib.as<double>(), fl,
+                               c->tpre.as<int>() + t0);
         }
     }
     }
@@ -718,10 +721,25 @@ int ensure_plan(sfmx_ba_ctx* c) {
         for (int l = 0; l < pl.height; ++l)
             for (int t = pl.task_start[l]; t < pl.task_start[l + 1]; ++t)
                 vfin[vid(pl.tasks[t].a, pl.tasks[t].b)] += 1 + ((t - pl.task_start[l]) < pl.ninv[l] ? 1 : 0);
-        std::vector<int4> items, need;
+        std::vector<int4> items, need, imask;
+        std::vector<sfmx::ba::RowMask> smask;
+        std::vector<int> padp;
+        sfmx::ba::row_masks(pl, adj, smask, padp);
+        // r06: per task, the panels an inverting one-source task sweeps before its update (the ones
+        // outside A_ak's row strips and not padding); every factorization form uses the same order
+        std::vector<int> tpre(std::max<size_t>(pl.tasks.size(), 1), 0);
+        for (int l = 0; l < pl.height; ++l)
+            for (int t = pl.task_start[l]; t < pl.task_start[l + 1]; ++t) {
+                const auto& tk = pl.tasks[t];
+                const bool inv = (t - pl.task_start[l]) < pl.ninv[l];
+                if (inv && tk.a == tk.b && tk.s1 - tk.s0 == 1)
+                    tpre[t] = ~smask[tk.s0].ra & ((1 << NW) - 1) & ~padp[tk.a];
+            }
+        up.add(c->tpre, tpre, true);
         for (int k : pl.leaves) {
             items.push_back(make_int4(k, -1, 0, 0));
             need.push_back(make_int4(0, 0, 0, 0));
+            imask.push_back(make_int4(padp[k] << 12, 0, 0, 0));
             vcnt[vid(k, k)] = 2;
         }
         int dslots = 0;
@@ -735,6 +753,16 @@ int ensure_plan(sfmx_ba_ctx* c) {
                     dag_ok = dag_ok && k < tk.b && vcnt[vid(tk.a, k)] == vfin[vid(tk.a, k)] &&
                              vcnt[vid(tk.b, k)] == vfin[vid(tk.b, k)] && vcnt[vid(k, k)] == vfin[vid(k, k)];
                     items.push_back(make_int4(t, tk.s0 + j, n == 1 ? 0 : dslots + j, n | inv << 16));
+                    {   // G's column tiles: all for a diagonal task (G^T is stored for the back solve), else
+                        // the tiles holding A_bk's nonzero columns (the only ones G A_bk^T reads)
+                        const sfmx::ba::RowMask& rm = smask[tk.s0 + j];
+                        int gc = 0;
+                        for (int c = 0; c < NW; ++c) gc |= ((rm.kb >> (4 * c)) & 15 ? 1 : 0) << c;
+                        if (tk.a == tk.b) gc = (1 << NW) - 1;
+                        const int pre = tpre[t];
+                        imask.push_back(make_int4(rm.ra | rm.rb << 4 | gc << 8 | (inv ? padp[tk.a] << 12 : 0) | pre << 16,
+                                                  rm.ka, rm.kb, 0));
+                    }
                     need.push_back(make_int4(vfin[vid(tk.a, k)], tk.a == tk.b ? 0 : vfin[vid(tk.b, k)], vfin[vid(k, k)],
                                              vcnt[vid(tk.a, tk.b)]));
                 }
@@ -747,6 +775,7 @@ int ensure_plan(sfmx_ba_ctx* c) {
         c->n_ver = nver;
         up.add(c->ditems, items, true);
         up.add(c->dneed, need, true);
+        up.add(c->dmask, imask, true);
         RC(c->dctr.alloc(sizeof(int) * (size_t)((nver + 2 + 3) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->dctr.p, 0, c->dctr.bytes, st));
         const char* ed = SFMX_DIAG_ENV("SFMX_BA_DAG");
@@ -761,7 +790,9 @@ int ensure_plan(sfmx_ba_ctx* c) {
         // 0.613-0.616 ms per iteration for the r03 library, profiles/r04d_ab.txt)
         const char* ew = SFMX_DIAG_ENV("SFMX_BA_WIDE");
         c->wide = ew && ew[0] == '1';
-        RC(c->lctr.alloc(sizeof(int) * (size_t)((pl.tasks.size() + 4) / 4 * 4)));
+        // [arrivals per task | chol_factor: per task, parts whose product / y terms are stored, at nitems +
+        // task / 2 nitems + task]
+        RC(c->lctr.alloc(sizeof(int) * (size_t)((pl.tasks.size() + 2 * (size_t)c->n_ditems + 4) / 4 * 4)));
         HIPCHK(hipMemsetAsync(c->lctr.p, 0, c->lctr.bytes, st));
         const char* e = SFMX_DIAG_ENV("SFMX_BA_SPLIT");
         c->split = !(e && e[0] == '0');
@@ -2689,6 +2720,28 @@ int sfmx_ba_debug_occupancy(int32_t K, int32_t* out) {
     out[0] = a;
     out[1] = b;
     return SFMX_OK;
+}
+#endif
+
+#ifdef SFMX_DIAG
+// diagnostic build only: the per-ticket timeline of the last chol_factor launch (ba_chol.hpp CHOL_TRACE),
+// n_items x 16 int64 (stamps 0-13 in 100 MHz wall-clock ticks, [15] = XCC id << 32 | HW_ID)
+int sfmx_ba_debug_chol_trace(long long* out, int32_t n_items) {
+    if (n_items > sfmx::ba::CHOL_TRACE_MAX) n_items = sfmx::ba::CHOL_TRACE_MAX;
+    if (n_items <= 0 || !out) return 0;
+    if (hipDeviceSynchronize() != hipSuccess) return SFMX_EDEVICE;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sfmx::ba::g_chol_trace), sizeof(long long) * 16 * n_items) != hipSuccess)
+        return SFMX_EDEVICE;
+    return n_items;
+}
+int sfmx_ba_debug_chol_items(sfmx_ba_ctx* c, int32_t* out, int32_t cap) {   // items (int4) of the current plan
+    if (!c) return SFMX_EINVAL;
+    const int n = c->n_ditems;
+    if (out && cap >= 8 * n) {
+        if (hipMemcpy(out, c->ditems.p, sizeof(int4) * n, hipMemcpyDeviceToHost) != hipSuccess) return SFMX_EDEVICE;
+        if (hipMemcpy(out + 4 * n, c->dmask.p, sizeof(int4) * n, hipMemcpyDeviceToHost) != hipSuccess) return SFMX_EDEVICE;
+    }
+    return n;
 }
 #endif
 

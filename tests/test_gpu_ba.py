@@ -161,10 +161,17 @@ def test_split_level_and_backsolve_bit_identical_to_r02_forms(order):
             P, sm, tr = gpu_solve(p, max_num_iterations=4)
         res[back + split + dag + wide] = (P.points.copy(), P.poses.copy(), sm["final_cost"], tr.copy())
     a = res["0000"]
-    for key in ("1000", "1100", "1110", "1111"):
+    for key in ("1000", "1100", "1110"):
         b = res[key]
         assert a[2] == b[2], key
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[3], b[3]), key
+    # chol_factor_w (diagnostic, measured slower in r04) keeps the r05 sweep order: since r06 the other
+    # forms sweep an inverting one-source task's untouched panels before its update (another rounding
+    # of the same factorization), so it agrees to rounding, with the same LM decisions
+    b = res["1111"]
+    assert abs(a[2] - b[2]) <= 1e-10 * abs(a[2]), (a[2], b[2])
+    assert np.array_equal(a[3][:, 2] != 0, b[3][:, 2] != 0)
+    assert np.allclose(a[0], b[0], rtol=1e-8, atol=1e-10) and np.allclose(a[1], b[1], rtol=1e-8, atol=1e-10)
 
 
 def _hard_problem(seed):

@@ -38,6 +38,7 @@ int main() {
     hipMemset(fail, 0, 64);
     { const int one = 1; hipMemcpy(fail + 1, &one, 4, hipMemcpyHostToDevice); }   // the step gate open (ba_kernels.hpp step_gated)
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+    int* zpre; hipMalloc(&zpre, 4 * 64); hipMemset(zpre, 0, 4 * 64);   // no pre-swept panels
     long long st[64];
     for (int rep = 0; rep < 3; ++rep) {
         hipMemcpy(S, S0, h.size() * 8, hipMemcpyDeviceToDevice);
@@ -55,7 +56,7 @@ int main() {
         printf(" | store %lld rhs %lld (w %lld sync %lld contrib %lld)  (ticks of 100 MHz wall clock)\n", st[20] - st[17], st[21] - st[20],
                st[22] - st[20], st[23] - st[22], st[21] - st[23]);
         hipEventRecord(e0);
-        chol_level<RW><<<(unsigned)tasks.size(), 256>>>(S, npad, R, dt, src, 1, W, contrib, fail);
+        chol_level<RW><<<(unsigned)tasks.size(), 256>>>(S, npad, R, dt, src, 1, W, contrib, fail, zpre);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         hipEventElapsedTime(&ms, e0, e1);
@@ -80,7 +81,8 @@ int main() {
                 float ms;
                 hipEventRecord(e0);
                 if (wide) chol_factor_w<RW><<<1, NTW>>>(S, npad, R, dt, items, need, src, W, contrib, fail, pbuf, tctr, ctr, 1, nver, DAG_TIMEOUT);
-                else chol_factor<RW><<<1, NTH>>>(S, npad, R, dt, items, need, src, W, contrib, fail, pbuf, tctr, ctr, 1, nver, DAG_TIMEOUT);
+                else chol_factor<RW><<<1, NTH>>>(S, npad, R, dt, items, need, src, W, contrib, fail, pbuf, tctr, ctr, 1, nver, DAG_TIMEOUT,
+                                                 need /* all-zero row masks: a leaf with no padding panel */);
                 hipEventRecord(e1);
                 hipEventSynchronize(e1);
                 hipEventElapsedTime(&ms, e0, e1);
