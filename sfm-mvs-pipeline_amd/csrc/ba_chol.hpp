@@ -183,6 +183,72 @@ __device__ __forceinline__ void mfma_nt_m(const double (*A)[LDT], const double (
     mfma_masked<true>(A, X, acc, rows, cols, ks);
 }
 
+// r06: the masked products with their output tiles spread over the waves.  The tiles (strip of
+// `rows`) x (column tile of `cols`) are listed row by row; tile q goes to wave q % NW, which keeps up
+// to 4 of them (acc[i]: strip ts[i], column tile tc[i]).  Each tile is accumulated over the same
+// k-steps in the same order as in mfma_masked, so its bits are those of the full product; only the
+// waves share the work (mfma_masked leaves the waves of zero strips idle: 2 of 4 on the C5 chain).
+__device__ __forceinline__ int nth_bit(int m, int i) {   // the i-th set bit of m (scalar)
+    for (int b = 0; b < 4; ++b)
+        if ((m >> b) & 1) { if (i == 0) return b; --i; }
+    return 0;
+}
+template <int NTI, bool NT>
+__device__ __forceinline__ void mfma_tiles(const double (*A)[LDT], const double (*B)[LDT], f64x4 acc[4], const int (&ts)[4],
+                                           const int (&tc)[4], int klo, int khi) {
+    const int l = threadIdx.x & 63, m = l & 15, kq = l >> 4;
+#pragma unroll 4
+    for (int st = klo; st < khi; ++st) {
+#pragma unroll
+        for (int i = 0; i < NTI; ++i)
+            acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[16 * ts[i] + m][4 * st + kq],
+                                                          NT ? B[16 * tc[i] + m][4 * st + kq] : B[4 * st + kq][16 * tc[i] + m],
+                                                          acc[i], 0, 0, 0);
+    }
+}
+template <bool NT>
+__device__ __forceinline__ int mfma_spread(const double (*A)[LDT], const double (*B)[LDT], f64x4 acc[4], int rows, int cols,
+                                           int ks, int (&ts)[4], int (&tc)[4]) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nr = __builtin_popcount(rows & 15), nc = __builtin_popcount(cols & 15);
+    int nt = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        acc[i] = f64x4{0.0, 0.0, 0.0, 0.0};
+        const int q = w + NW * i;
+        ts[i] = tc[i] = 0;
+        if (q < nr * nc) {
+            ts[i] = nth_bit(rows, q / nc);
+            tc[i] = nth_bit(cols, q % nc);
+            nt = i + 1;
+        }
+    }
+    if (!ks || !nt) return nt;
+    const int klo = __builtin_ctz((unsigned)ks), khi = 32 - __builtin_clz((unsigned)ks);
+    switch (nt) {
+        case 1: mfma_tiles<1, NT>(A, B, acc, ts, tc, klo, khi); break;
+        case 2: mfma_tiles<2, NT>(A, B, acc, ts, tc, klo, khi); break;
+        case 3: mfma_tiles<3, NT>(A, B, acc, ts, tc, klo, khi); break;
+        default: mfma_tiles<4, NT>(A, B, acc, ts, tc, klo, khi); break;
+    }
+    return nt;
+}
+// the spread tiles into an LDS tile buffer (row-major 64 x 64); the tiles outside rows x cols as zeros
+__device__ __forceinline__ void spread_store(double (*dst)[LDT], const f64x4 (&acc)[4], const int (&ts)[4], const int (&tc)[4],
+                                             int nt, int rows, int cols) {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (i < nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dst[16 * ts[i] + trow(r)][16 * tc[i] + tcol()] = acc[i][r];
+#pragma unroll
+    for (int c = 0; c < NW; ++c)   // wave w: the zero tiles of strip w
+        if (!((rows >> w) & 1) || !((cols >> c) & 1))
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dst[16 * w + trow(r)][16 * c + tcol()] = 0.0;
+}
+
 // 1/d: hardware estimate + two Newton steps (within an ulp or so of the divide).
 __device__ __forceinline__ double rcp_nr(double d) {
     double r = __builtin_amdgcn_rcp(d);
@@ -822,17 +888,24 @@ void chol_factor(double* __restrict__ S, int npad, double* __restrict__ R, const
         tile_load_wt_rows(sm.m, rW, (size_t)k * NB * NB, NB, mka);             // W_k (the rows G reads)
         __syncthreads();
         CHOL_TRACE(tk, 3);
-        f64x4 g[NW];
-        mfma_nn_m(sm.a, sm.m, g, m_ra, m_gc, mka);   // G = A_ak W_k (its structurally nonzero part)
-        __syncthreads();
-        CHOL_TRACE(tk, 4);
-#pragma unroll
-        for (int c = 0; c < NW; ++c)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sm.m[16 * w + trow(r)][16 * c + tcol()] = g[c][r];
-        __syncthreads();
         f64x4 upd[NW];
-        mfma_nt_m(sm.m, diag ? sm.a : sm.n, upd, m_ra, m_rb, mkb);   // G X^T
+        {   // r06: G = A_ak W_k and U = G X^T on their structurally nonzero tiles, spread over the waves
+            f64x4 sp[4];
+            int ts[4], tc[4];
+            const int n1 = mfma_spread<false>(sm.a, sm.m, sp, m_ra, m_gc, mka, ts, tc);   // G
+            __syncthreads();
+            CHOL_TRACE(tk, 4);
+            spread_store(sm.m, sp, ts, tc, n1, m_ra, m_gc);   // G (zero strips included: G^T is stored whole)
+            __syncthreads();
+            const int n2 = mfma_spread<true>(sm.m, diag ? sm.a : sm.n, sp, m_ra, m_rb, mkb, ts, tc);   // G X^T
+            __syncthreads();   // (X = A_bk in sm.n is read; sm.n takes U)
+            spread_store(sm.n, sp, ts, tc, n2, m_ra, m_rb);
+            __syncthreads();
+#pragma unroll
+            for (int c = 0; c < NW; ++c)   // back to the strip-owned layout of t
+#pragma unroll
+                for (int r = 0; r < 4; ++r) upd[c][r] = sm.n[16 * w + trow(r)][16 * c + tcol()];
+        }
         CHOL_TRACE(tk, 5);
         double ys[OPT];
         // y_a terms of a diagonal part: ys = A_ak w_k (w_k = the R rows of k, stored after W_k)

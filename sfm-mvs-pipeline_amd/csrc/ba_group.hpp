@@ -234,8 +234,27 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
                const int* __restrict__ pt_start, const double* __restrict__ Wr, const double* __restrict__ PRr,
                const double* __restrict__ scale, const double* __restrict__ colsq, double dmin, double dmax,
                double radius, int P, int C, double* __restrict__ plt, double* __restrict__ sg, double* __restrict__ rg,
-               double* __restrict__ hbig, int* __restrict__ fail, const double* __restrict__ lm) {
+               double* __restrict__ hbig, int* __restrict__ fail, const double* __restrict__ lm, int ngroups,
+               double* __restrict__ zS, int npad, const int2* __restrict__ nzt, int nnz, long long tail) {
     if (step_gated(fail + 1)) return;
+    if ((int)blockIdx.x >= ngroups) {
+        // r06: the workgroups past the groups zero what ba_assemble accumulates into (instead of a 17 MB
+        // memset of the dense S at C5): the structurally nonzero lower tiles of S_cc (the diagonal ones
+        // whole) and the tail R | D | r_i.  Nothing reads another part of S_cc before the factorization
+        // has written it (its upper tiles G^T; ba_plan.cpp row_masks).
+        const int b = (int)blockIdx.x - ngroups;
+        const double2 z = make_double2(0.0, 0.0);
+        if (b < nnz) {
+            const int2 tl = nzt[b];
+            double* t0 = zS + (size_t)tl.x * 64 * npad + (size_t)tl.y * 64;
+            for (int e = threadIdx.x; e < 64 * 32; e += blockDim.x)
+                reinterpret_cast<double2*>(t0 + (size_t)(e >> 5) * npad)[e & 31] = z;
+        } else {
+            double* t0 = zS + (size_t)npad * npad;
+            for (long long e = threadIdx.x; e < tail; e += blockDim.x) t0[e] = 0.0;
+        }
+        return;
+    }
     if (lm) radius = lm[LM_RADIUS];
     extern __shared__ __attribute__((aligned(16))) double gl[];
     constexpr int PD = gs_pd(K), NPR = npr(K);

@@ -499,19 +499,20 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
     // the failure flag is zero here: cleared by the run's start and by every scalar handoff (ba_publish)
     if (c->phases) HIPCHK(hipEventRecord(c->ev[0], c->st));
     const bool sj = c->unscaled_wr && c->Wr.p == c->unscaled_wr;   // a step on the unscaled iteration-0 records
-    if (c->ngroups > 0) {
+    const long long sr_tail = (long long)(c->sr_count - (size_t)npad * npad);
+    {   // (r06: ba_gschur's workgroups past the groups zero S's nonzero tiles and its tail; no S memset)
 #define GSCHUR(NTV) if (sj) GSCHUR2(NTV, true); else GSCHUR2(NTV, false)
-#define GSCHUR2(NTV, SJ) hipLaunchKernelGGL((ba_gschur<K, NTV, SJ>), dim3(c->ngroups), dim3(256), c->lds_schur, c->st,     \
+#define GSCHUR2(NTV, SJ) hipLaunchKernelGGL((ba_gschur<K, NTV, SJ>), dim3(c->ngroups + c->n_nztiles + 1), dim3(256), c->lds_schur, c->st, \
                            c->grp.as<Grp>(), c->bat.as<Batch>(), c->gcam.as<int>(), c->obs_lc.as<short>(),             \
                            c->obs_point.as<int>(), c->obs_cam.as<int>(), c->pt_start.as<int>(), c->Wr.as<double>(),     \
                            c->PR.as<double>(), c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal,         \
                            o.max_lm_diagonal, radius,                                                                   \
-                           c->P, C, c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl, lmr)
+                           c->P, C, c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl, lmr, \
+                           c->ngroups, S, npad, c->nztiles.as<int2>(), c->n_nztiles, sr_tail)
         switch (c->gs_nt) { case 1: GSCHUR(1); break; case 2: GSCHUR(2); break; case 3: GSCHUR(3); break; default: GSCHUR(4); }
 #undef GSCHUR2
 #undef GSCHUR
     }
-    HIPCHK(hipMemsetAsync(S, 0, sizeof(double) * c->sr_count, c->st));
     hipLaunchKernelGGL(ba_assemble, dim3(c->ntasks), dim3(ASM_THREADS), 0, c->st, c->tasks.as<ATask>(), c->ents.as<AEnt>(),
                        c->sg.as<double>(), c->hbig.as<double>(), c->rg.as<double>(), K, c->camrow.as<int>(), npad, S,
                        R, Dm, ri, gate(c));
