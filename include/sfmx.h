@@ -144,6 +144,11 @@ int sfmx_matcher_timing(sfmx_matcher* m, float* main_kernel_ms, float* total_ms)
  * the forwarded queries).  Single-pass variants report screen_ms = 0. */
 int sfmx_matcher_pass_timing(sfmx_matcher* m, float* screen_ms, float* pass2_ms);
 
+/* The main-kernel and pass-1 times (ms, HIP events on the run's stream) of the last min(n, runs, 32)
+ * runs, oldest first, so a loop of runs can be timed per run without a host sync inside it.
+ * Synchronises on the last run.  Returns the count written (>= 0) or a negative code. */
+int sfmx_matcher_timing_history(sfmx_matcher* m, float* main_kernel_ms, float* screen_ms, int32_t n);
+
 /* One-shot convenience wrapper = the whole strategy call
  * (IFeatureMatchingStrategy::calculateShotMatches, IFeatureMatchingStrategy.h:45-46, as SfM.cpp:545
  * calls it): uses n_gpus devices (pairs split by Σ Nq·Nt, one host thread per device; each device

@@ -235,7 +235,8 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
                const double* __restrict__ scale, const double* __restrict__ colsq, double dmin, double dmax,
                double radius, int P, int C, double* __restrict__ plt, double* __restrict__ sg, double* __restrict__ rg,
                double* __restrict__ hbig, int* __restrict__ fail, const double* __restrict__ lm, int ngroups,
-               double* __restrict__ zS, int npad, const int2* __restrict__ nzt, int nnz, long long tail) {
+               double* __restrict__ zS, int npad, const int2* __restrict__ nzt, int nnz, long long tail,
+               const int* __restrict__ rowmap) {
     if (step_gated(fail + 1)) return;
     if ((int)blockIdx.x >= ngroups) {
         // r06: the workgroups past the groups zero what ba_assemble accumulates into (instead of a 17 MB
@@ -249,6 +250,11 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
             double* t0 = zS + (size_t)tl.x * 64 * npad + (size_t)tl.y * 64;
             for (int e = threadIdx.x; e < 64 * 32; e += blockDim.x)
                 reinterpret_cast<double2*>(t0 + (size_t)(e >> 5) * npad)[e & 31] = z;
+            if (tl.x == tl.y) {   // the identity padding rows of a diagonal tile (ba_add_cam's, r05)
+                __syncthreads();
+                if (threadIdx.x < 64 && rowmap[tl.x * 64 + threadIdx.x] < 0)
+                    t0[(size_t)threadIdx.x * npad + threadIdx.x] = 1.0;
+            }
         } else {
             double* t0 = zS + (size_t)npad * npad;
             for (long long e = threadIdx.x; e < tail; e += blockDim.x) t0[e] = 0.0;
@@ -605,6 +611,47 @@ __device__ __forceinline__ double aval(const AEnt& E, const double* __restrict__
     const double* Hb = hbig + E.b1 + 3 * c;
     return -(Ha[0] * Hb[0] + Ha[1] * Hb[1] + Ha[2] * Hb[2]);
 }
+// ba_add_cam's terms, one rounding per operation (no contraction), shared by ba_add_cam (point-sharded
+// ranks: added after the all-reduce) and ba_assemble's fused form (one rank, r06), so both give the
+// same bits: the camera-camera block entry (u, w) (+ D^2 on the diagonal), camera-intrinsics B entry,
+// camera gradient, intrinsics block entry, intrinsics gradient
+// (HIP's __dadd_rn / __dmul_rn are plain + / * here, which the compiler may contract into an FMA with
+// a neighbouring multiply depending on the surrounding code: these two never contract, so a term gives
+// the same bits whichever kernel forms it)
+__device__ __forceinline__ double add_nc(double a, double b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
+__device__ __forceinline__ double mul_nc(double a, double b) {
+#pragma clang fp contract(off)
+    return a * b;
+}
+__device__ __forceinline__ int sym_idx(int a, int b, int n) {   // packed upper-triangle index of (a, b), a <= b
+    int e = 0;
+    for (int x = 0; x < a; ++x) e += n - x;
+    return e + b - a;
+}
+__device__ __forceinline__ double cam_cc_term(const double* cs, const double* sc, const double* colsq_c, int u, int w,
+                                              double dmin, double dmax, double radius) {
+    double v = mul_nc(mul_nc(sc[u], sc[w]), cs[sym_idx(u < w ? u : w, u < w ? w : u, 6)]);
+    if (u == w) v = add_nc(v, dsq(colsq_c[u], sc[u], dmin, dmax, radius));
+    return v;
+}
+__device__ __forceinline__ double cam_ci_term(const double* cs, const double* sc, const double* si, int K, int u, int i) {
+    return mul_nc(mul_nc(sc[u], si[i]), cs[cp_ci(K) + u * K + i]);
+}
+__device__ __forceinline__ double cam_g_term(const double* cs, const double* sc, int K, int u) {
+    return mul_nc(sc[u], cs[cp_gc(K) + u]);
+}
+__device__ __forceinline__ double intr_ii_term(const double* ii, const double* si, const double* colsq_i, int K, int i, int j,
+                                               double dmin, double dmax, double radius) {
+    double v = mul_nc(mul_nc(si[i], si[j]), ii[sym_idx(i < j ? i : j, i < j ? j : i, K)]);
+    if (i == j) v = add_nc(v, dsq(colsq_i[i], si[i], dmin, dmax, radius));
+    return v;
+}
+__device__ __forceinline__ double intr_g_term(const double* ii, const double* si, int K, int i) {
+    return mul_nc(si[i], ii[K * (K + 1) / 2 + i]);
+}
 __device__ __forceinline__ double wave_sum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
@@ -614,11 +661,20 @@ __global__ __launch_bounds__(ASM_THREADS)
 void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents, const double* __restrict__ sg,
                  const double* __restrict__ hbig, const double* __restrict__ rg, int K, const int* __restrict__ camrow,
                  int npad, double* __restrict__ S, double* __restrict__ R, double* __restrict__ Dm,
-                 double* __restrict__ ri, const int* __restrict__ gate) {
+                 double* __restrict__ ri, const int* __restrict__ gate, int fuse, int P, int C,
+                 const double* __restrict__ camsum, const double* __restrict__ scale, const double* __restrict__ colsq,
+                 double dmin, double dmax, double radius, const double* __restrict__ lm) {
     if (step_gated(gate)) return;
+    if (fuse && lm) radius = lm[LM_RADIUS];
     __shared__ double part[ASM_THREADS];
     const ATask T = tasks[blockIdx.x];
     const int t = threadIdx.x, RW = K + 1;
+    // fuse (one rank, r06): each output takes ba_add_cam's term as it is written, s + v in that order
+    // (ba_add_cam added v to the stored s): the camera-camera C block + D^2, the camera-intrinsics part of
+    // B and the camera gradient, the intrinsics block + D^2 and gradient (camsum unscaled, all-reduced)
+    const int NCP = ncp(K);
+    const size_t ne = 3 * (size_t)P, nfc = 6 * (size_t)C;
+    const double* si = scale + ne + nfc;
     if (T.type == 2) {          // one intrinsics output x = T.b over every group; entries at the intrinsics rows
         const int x = T.b;
         double v0 = 0.0, v1 = 0.0;
@@ -641,7 +697,12 @@ void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents,
         if ((t & 63) == 0) part[t >> 6] = v;
         __syncthreads();
         if (t == 0) {
-            const double s = ((part[0] + part[1]) + part[2]) + part[3];
+            double s = ((part[0] + part[1]) + part[2]) + part[3];
+            if (fuse & 4) {
+                const double* ii = camsum + (size_t)C * NCP;
+                s = add_nc(s, x < K * K ? intr_ii_term(ii, si, colsq + ne + nfc, K, x / K, x % K, dmin, dmax, radius)
+                                           : intr_g_term(ii, si, K, x - K * K));
+            }
             if (x < K * K) Dm[x] = s;
             else ri[x - K * K] = s;
         }
@@ -665,10 +726,18 @@ void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents,
         for (int q = 1; q < np; ++q) s += part[q * nout + t];
         if (T.type == 0) {
             const int u = t / 6, w = t % 6, ra = camrow[T.a], rb = camrow[T.b];
+            if ((fuse & 1) && T.a == T.b)   // camera T.a's diagonal block
+                s = add_nc(s, cam_cc_term(camsum + (size_t)T.a * NCP, scale + ne + 6 * (size_t)T.a,
+                                             colsq + ne + 6 * (size_t)T.a, u, w, dmin, dmax, radius));
             S[(size_t)(ra + u) * npad + rb + w] = s;
             if (T.a != T.b) S[(size_t)(rb + w) * npad + ra + u] = s;
         } else {
             const int ra = camrow[T.a];
+            if (fuse & 2) {
+                const double* cs = camsum + (size_t)T.a * NCP;
+                const double* sc = scale + ne + 6 * (size_t)T.a;
+                s = add_nc(s, t < 6 * K ? cam_ci_term(cs, sc, si, K, t / K, t % K) : cam_g_term(cs, sc, K, t - 6 * K));
+            }
             if (t < 6 * K) R[(size_t)(ra + t / K) * RW + t % K] = s;
             else R[(size_t)(ra + t - 6 * K) * RW + K] = s;
         }
@@ -684,7 +753,7 @@ void ba_add_cam(int P, int C, int npad, const int* __restrict__ camrow, const in
                 int npadrows, const double* __restrict__ camsum,
                 const double* __restrict__ scale, const double* __restrict__ colsq, double dmin, double dmax,
                 double radius, double* __restrict__ S, double* __restrict__ R, double* __restrict__ Dm,
-                double* __restrict__ ri, const int* __restrict__ gate, const double* __restrict__ lm) {
+                double* __restrict__ ri, const int* __restrict__ gate, const double* __restrict__ lm, int fused = 0) {
     if (step_gated(gate)) return;
     if (lm) radius = lm[LM_RADIUS];
     constexpr int NCP = ncp(K), RW = K + 1;
@@ -695,36 +764,26 @@ void ba_add_cam(int P, int C, int npad, const int* __restrict__ camrow, const in
         const double* cs = camsum + (size_t)c * NCP;
         const double* sc = scale + ne + 6 * (size_t)c;
         for (int t = threadIdx.x; t < 42 + 6 * K; t += 64)
-        if (t < 36) {
-            const int u = t / 6, w = t % 6, a = u < w ? u : w, b = u < w ? w : u;
-            int e = 0;
-            for (int x = 0; x < a; ++x) e += 6 - x;
-            e += b - a;
-            double v = sc[u] * sc[w] * cs[e];
-            if (u == w) v += dsq(colsq[ne + 6 * (size_t)c + u], sc[u], dmin, dmax, radius);
-            S[(size_t)(rc + u) * npad + rc + w] += v;
+        if (t < 36 ? (fused & 1) : (fused & 2)) {
+            continue;   // (ba_assemble added this term)
+        } else if (t < 36) {
+            const int u = t / 6, w = t % 6;
+            double* d = &S[(size_t)(rc + u) * npad + rc + w];
+            *d = add_nc(*d, cam_cc_term(cs, sc, colsq + ne + 6 * (size_t)c, u, w, dmin, dmax, radius));
         } else if (t < 36 + 6 * K) {
             const int x = t - 36, u = x / K, i = x % K;
-            R[(size_t)(rc + u) * RW + i] += sc[u] * si[i] * cs[cp_ci(K) + u * K + i];
+            double* d = &R[(size_t)(rc + u) * RW + i];
+            *d = add_nc(*d, cam_ci_term(cs, sc, si, K, u, i));
         } else if (t < 42 + 6 * K) {
             const int u = t - 36 - 6 * K;
-            R[(size_t)(rc + u) * RW + K] += sc[u] * cs[cp_gc(K) + u];
+            double* d = &R[(size_t)(rc + u) * RW + K];
+            *d = add_nc(*d, cam_g_term(cs, sc, K, u));
         }
     } else {
         const double* ii = camsum + (size_t)C * NCP;
-        for (int x = threadIdx.x; x < K * K + K; x += 64) {
-            if (x < K * K) {
-                const int i = x / K, j = x % K, a = i < j ? i : j, b = i < j ? j : i;
-                int e = 0;
-                for (int y = 0; y < a; ++y) e += K - y;
-                e += b - a;
-                double v = si[i] * si[j] * ii[e];
-                if (i == j) v += dsq(colsq[ne + nfc + i], si[i], dmin, dmax, radius);
-                Dm[x] += v;
-            } else {
-                const int i = x - K * K;
-                ri[i] += si[i] * ii[K * (K + 1) / 2 + i];
-            }
+        for (int x = threadIdx.x; x < K * K + K && !(fused & 4); x += 64) {
+            if (x < K * K) Dm[x] = add_nc(Dm[x], intr_ii_term(ii, si, colsq + ne + nfc, K, x / K, x % K, dmin, dmax, radius));
+            else ri[x - K * K] = add_nc(ri[x - K * K], intr_g_term(ii, si, K, x - K * K));
         }
         for (int i = threadIdx.x; i < npadrows; i += 64) S[(size_t)padrows[i] * npad + padrows[i]] = 1.0;
     }
@@ -1224,7 +1283,19 @@ void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int*
         if (pt < NP) {
             double sacc = 0.0;
             int e = e0 + pt;
-#pragma unroll 4
+            // r06: a C5 camera has ~100 slots, ~20 per thread, each a dependent cref -> gpart load pair:
+            // 8 slot indices, then their 8 partials, in flight before the adds (same order, same bits)
+            constexpr int BT = 8;
+            for (; e + (BT - 1) * NP < e1; e += BT * NP) {
+                int ix[BT];
+                double va[BT];
+#pragma unroll
+                for (int j = 0; j < BT; ++j) ix[j] = cref[e + j * NP];
+#pragma unroll
+                for (int j = 0; j < BT; ++j) va[j] = gpart[(size_t)ix[j] * NCP + f];
+#pragma unroll
+                for (int j = 0; j < BT; ++j) sacc += va[j];
+            }
             for (; e < e1; e += NP) sacc += gpart[(size_t)cref[e] * NCP + f];
             part[t] = sacc;
         }

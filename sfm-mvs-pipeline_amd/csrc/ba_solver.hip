@@ -508,14 +508,22 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
                            c->PR.as<double>(), c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal,         \
                            o.max_lm_diagonal, radius,                                                                   \
                            c->P, C, c->plt.as<double>(), c->sg.as<double>(), c->rg.as<double>(), c->hbig.as<double>(), fl, lmr, \
-                           c->ngroups, S, npad, c->nztiles.as<int2>(), c->n_nztiles, sr_tail)
+                           c->ngroups, S, npad, c->nztiles.as<int2>(), c->n_nztiles, sr_tail, c->rowmap.as<int>())
         switch (c->gs_nt) { case 1: GSCHUR(1); break; case 2: GSCHUR(2); break; case 3: GSCHUR(3); break; default: GSCHUR(4); }
 #undef GSCHUR2
 #undef GSCHUR
     }
+    // one rank: ba_assemble adds ba_add_cam's camera terms to its outputs itself (r06: one launch fewer);
+    // point-sharded ranks add them after the all-reduce (they are replicated, not sharded)
+    // diagnostic library: SFMX_BA_FUSE = the terms ba_assemble adds (bit 0 camera blocks, 1 camera B rows
+    // and gradient, 2 intrinsics); the rest stay with ba_add_cam
+    const char* nf_env = SFMX_DIAG_ENV("SFMX_BA_FUSE");
+    const int fuse_mask = multirank(c) ? 0 : nf_env ? (std::atoi(nf_env) & 7) : 7;
+    const bool fuse_cam = fuse_mask == 7;
     hipLaunchKernelGGL(ba_assemble, dim3(c->ntasks), dim3(ASM_THREADS), 0, c->st, c->tasks.as<ATask>(), c->ents.as<AEnt>(),
                        c->sg.as<double>(), c->hbig.as<double>(), c->rg.as<double>(), K, c->camrow.as<int>(), npad, S,
-                       R, Dm, ri, gate(c));
+                       R, Dm, ri, gate(c), fuse_mask, c->P, C, c->camsum.as<double>(), c->scale.as<double>(),
+                       c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, lmr);
     HIPCHK(hipGetLastError());
     if (c->phases) HIPCHK(hipEventRecord(c->ev[1], c->st));
     // point-sharded ranks: the group part of the reduced camera system and its rhs are sums over
@@ -528,10 +536,11 @@ int try_step(sfmx_ba_ctx* c, double radius, bool* valid, double* mcc, double* st
         hipLaunchKernelGGL(chol_pack, dim3(c->n_nztiles + 1), dim3(256), 0, c->st, S, npad, c->nztiles.as<int2>(),
                            c->n_nztiles, tail, c->packbuf.as<double>(), 1, gate(c));
     }
+    if (!fuse_cam)
     hipLaunchKernelGGL(ba_add_cam<K>, dim3(C + 1), dim3(64), 0, c->st, c->P, C, npad, c->camrow.as<int>(),
                        c->padrows.as<int>(), (int)c->plan.padrows.size(), c->camsum.as<double>(),
                        c->scale.as<double>(), c->colsq.as<double>(), o.min_lm_diagonal, o.max_lm_diagonal, radius, S,
-                       R, Dm, ri, gate(c), lmr);
+                       R, Dm, ri, gate(c), lmr, fuse_mask);
     double* sol = c->sol.as<double>();
     RC(solve_reduced<RW>(c, sol + c->ne));
     if (c->phases) HIPCHK(hipEventRecord(c->ev[2], c->st));
@@ -1434,10 +1443,14 @@ void finish_topology(int C, int K, Topology& tp) {
     }
     const size_t ne_pose = eoff[TOPO_PIECES], nt_pose = toff[TOPO_PIECES];
     const size_t ne_cam = tp.cref.size(), ne = ne_pose + ne_cam + (size_t)ng;
-    size_t nt_cam = 0;
-    for (int cm = 0; cm < C; ++cm) nt_cam += tp.cref_start[cm + 1] > tp.cref_start[cm];
+    // r06: a type-1 task for every camera and an (empty) diagonal pose task for every camera no group
+    // holds: ba_assemble adds the camera terms of ba_add_cam to its outputs (one rank), so every camera
+    // row block needs a task (its D^2 damping even without observations)
+    const size_t nt_cam = (size_t)C;
+    size_t n_orph = 0;
+    for (int cm = 0; cm < C; ++cm) n_orph += tp.cref_start[cm + 1] == tp.cref_start[cm];
     tp.ents.resize(ne);
-    tp.tasks.resize(nt_pose + nt_cam + (size_t)(K * K + K));
+    tp.tasks.resize(nt_pose + nt_cam + n_orph + (size_t)(K * K + K));
     sfmx::parallel_items(TOPO_PIECES + 2, [&](int t) {
         if (t < TOPO_PIECES) {
             const TaskPiece& P = pcs[t];
@@ -1457,12 +1470,14 @@ void finish_topology(int C, int K, Topology& tp) {
                     tp.ents[e++] = ent(g, sl - tp.grp[g].cam_off, tp.grp[g].u);
                 }
                 tk.l1 = (int)e;
-                if (tk.l1 > tk.l0) tp.tasks[k++] = tk;
+                tp.tasks[k++] = tk;
             }
+            for (int cm = 0; cm < C; ++cm)   // cameras without observations: their diagonal block
+                if (tp.cref_start[cm + 1] == tp.cref_start[cm]) tp.tasks[k++] = ATask{0, cm, cm, 0, 0, 0, 0, 0};
         } else {   // the intrinsics block and rhs: one task per output, every group
             const int l0 = (int)(ne_pose + ne_cam);
             for (int g = 0; g < ng; ++g) tp.ents[l0 + g] = ent(g, tp.grp[g].u, tp.grp[g].u);
-            for (int x = 0; x < K * K + K; ++x) tp.tasks[nt_pose + nt_cam + x] = ATask{2, 0, x, l0, (int)ne, 0, 0, 0};
+            for (int x = 0; x < K * K + K; ++x) tp.tasks[nt_pose + nt_cam + n_orph + x] = ATask{2, 0, x, l0, (int)ne, 0, 0, 0};
         }
     });
 }

@@ -181,7 +181,13 @@ struct sfmx_matcher {
     size_t plan_nwork = 0, plan_nwork32 = 0;
     int plan_max_nt = 0;
     bool has_run = false;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // run start, main kernel end, run end, pass-1 end
+    // per run: start, main kernel end, run end, pass-1 end; a ring of EV_RING sets (r06) so the timing
+    // of every run of a loop is readable afterwards (sfmx_matcher_timing_history) without a host sync
+    // inside it; ev points at the current run's set
+    static constexpr int EV_RING = 32;
+    hipEvent_t evr[EV_RING][4] = {};
+    hipEvent_t* ev = evr[0];
+    long long runs = 0;
     bool ev_recorded = false;
     // overlapped two-pass matching (launch_two_pass_overlap): the plan's batches, two more streams
     std::vector<MatchBatch> batches;
@@ -478,8 +484,11 @@ int run_impl(sfmx_matcher* m, const int32_t* pairs, int n_pairs, double ratio, i
     }
     const int64_t dense = m->plan_dense;
     const size_t n_work = m->plan_nwork, n_work32 = m->plan_nwork32;
-    if (!m->ev[0])
-        for (auto& e : m->ev) HIPCHK(hipEventCreate(&e));
+    if (!m->evr[0][0])
+        for (auto& set : m->evr)
+            for (auto& e : set) HIPCHK(hipEventCreate(&e));
+    m->ev = m->evr[m->runs % sfmx_matcher::EV_RING];
+    ++m->runs;
     HIPCHK(hipMemsetAsync(m->slow_count.p, 0, sizeof(int32_t), st));
     HIPCHK(hipMemsetAsync(m->unsettled.p, 0, sizeof(int32_t), st));
     HIPCHK(hipEventRecord(m->ev[0], st));
@@ -715,7 +724,8 @@ int sfmx_matcher_destroy(sfmx_matcher* m) {
                           &m->work_d, &m->work32_d, &m->dense_idx, &m->dense_dist, &m->slow_list, &m->slow_count,
                           &m->unsettled, &m->counts, &m->keep, &m->offsets, &m->out};
         for (DevBuf* b : bufs) b->release();
-        for (auto& e : m->ev) if (e) (void)hipEventDestroy(e);
+        for (auto& set : m->evr)
+            for (auto& e : set) if (e) (void)hipEventDestroy(e);
         for (auto& e : m->ov_ev) if (e) (void)hipEventDestroy(e);
         for (auto& e : m->fix_ev) if (e) (void)hipEventDestroy(e);
         for (auto& e : m->bev) if (e) (void)hipEventDestroy(e);
@@ -784,6 +794,24 @@ int sfmx_matcher_timing(sfmx_matcher* m, float* main_kernel_ms, float* total_ms)
     if (main_kernel_ms) *main_kernel_ms = a;
     if (total_ms) *total_ms = b;
     return SFMX_OK;
+}
+
+int sfmx_matcher_timing_history(sfmx_matcher* m, float* main_kernel_ms, float* screen_ms, int32_t n) {
+    if (!m) return fail(SFMX_EINVAL, "null matcher");
+    if (!m->ev_recorded) return fail(SFMX_ESTATE, "no timing before run");
+    if (n < 0) return fail(SFMX_EINVAL, "negative count");
+    DeviceGuard g(m->device);
+    HIPCHK(hipEventSynchronize(m->ev[2]));
+    const long long k = std::min<long long>({(long long)n, m->runs, (long long)sfmx_matcher::EV_RING});
+    for (long long i = 0; i < k; ++i) {   // oldest first: runs (runs - k) .. (runs - 1)
+        hipEvent_t* e = m->evr[(m->runs - k + i) % sfmx_matcher::EV_RING];
+        float a = 0.f, b = 0.f;
+        HIPCHK(hipEventElapsedTime(&a, e[0], e[1]));
+        HIPCHK(hipEventElapsedTime(&b, e[0], e[3]));
+        if (main_kernel_ms) main_kernel_ms[i] = a;
+        if (screen_ms) screen_ms[i] = b;
+    }
+    return (int)k;
 }
 
 int sfmx_matcher_pass_timing(sfmx_matcher* m, float* screen_ms, float* pass2_ms) {

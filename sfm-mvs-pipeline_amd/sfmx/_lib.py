@@ -107,6 +107,7 @@ PROTOTYPES = {
     "sfmx_matcher_stats": (C.c_int, [_vp, _i64p, _i64p, _vp]),
     "sfmx_matcher_timing": (C.c_int, [_vp, _P(C.c_float), _P(C.c_float)]),
     "sfmx_matcher_pass_timing": (C.c_int, [_vp, _P(C.c_float), _P(C.c_float)]),
+    "sfmx_matcher_timing_history": (C.c_int, [_vp, _P(C.c_float), _P(C.c_float), C.c_int32]),
     "sfmx_match_pairs": (C.c_int, [_P(sfmx_desc), C.c_int32, _i32p, C.c_int32, C.c_int32, C.c_double,
                                    C.c_int32, C.c_int32, C.c_int32, _vp, C.c_int64, _i64p, _i64p, _i32p]),
     "sfmx_device_count": (C.c_int, []),

@@ -163,6 +163,16 @@ class BFMatcher:
         check(lib.sfmx_matcher_timing(self._h, C.byref(a), C.byref(b)), "sfmx_matcher_timing")
         return a.value, b.value
 
+    def timing_history(self, n):
+        """-> (main 2-NN kernel ms, screen ms) arrays of the last min(n, runs, 32) runs, oldest first
+        (HIP events of each run; read without a host sync inside the loop that made them)."""
+        a = np.zeros(max(n, 1), np.float32)
+        b = np.zeros(max(n, 1), np.float32)
+        k = check(lib.sfmx_matcher_timing_history(self._h, a.ctypes.data_as(C.POINTER(C.c_float)),
+                                                  b.ctypes.data_as(C.POINTER(C.c_float)), int(n)),
+                  "sfmx_matcher_timing_history")
+        return a[:k].astype(float), b[:k].astype(float)
+
     def pass_timing(self):
         """-> (screen ms, pass-2 ms) of the last run's two-pass 2-NN launch (screen 0 when single pass)."""
         a, b = C.c_float(), C.c_float()
