@@ -1283,19 +1283,7 @@ void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int*
         if (pt < NP) {
             double sacc = 0.0;
             int e = e0 + pt;
-            // r06: a C5 camera has ~100 slots, ~20 per thread, each a dependent cref -> gpart load pair:
-            // 8 slot indices, then their 8 partials, in flight before the adds (same order, same bits)
-            constexpr int BT = 8;
-            for (; e + (BT - 1) * NP < e1; e += BT * NP) {
-                int ix[BT];
-                double va[BT];
-#pragma unroll
-                for (int j = 0; j < BT; ++j) ix[j] = cref[e + j * NP];
-#pragma unroll
-                for (int j = 0; j < BT; ++j) va[j] = gpart[(size_t)ix[j] * NCP + f];
-#pragma unroll
-                for (int j = 0; j < BT; ++j) sacc += va[j];
-            }
+#pragma unroll 4
             for (; e < e1; e += NP) sacc += gpart[(size_t)cref[e] * NCP + f];
             part[t] = sacc;
         }
@@ -1309,23 +1297,6 @@ void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int*
         const int f = blockIdx.x - C;
         double s0 = 0.0, s1 = 0.0;
         int e = t;
-        // r06: 8 iterations' loads in flight before their adds (same chains, same order): these few
-        // workgroups stream every slot of the launch (C5: ~20k strided loads each) and with 2 loads in
-        // flight per thread they set ba_camred's length
-        constexpr int BT = 8;
-        for (; e + (2 * BT - 1) * CRED_THREADS < nslots; e += 2 * BT * CRED_THREADS) {
-            double va[BT], vb[BT];
-#pragma unroll
-            for (int j = 0; j < BT; ++j) {
-                va[j] = gpart[(size_t)(e + 2 * j * CRED_THREADS) * NCP + NFC + f];
-                vb[j] = gpart[(size_t)(e + (2 * j + 1) * CRED_THREADS) * NCP + NFC + f];
-            }
-#pragma unroll
-            for (int j = 0; j < BT; ++j) {
-                s0 += va[j];
-                s1 += vb[j];
-            }
-        }
         for (; e + CRED_THREADS < nslots; e += 2 * CRED_THREADS) {
             s0 += gpart[(size_t)e * NCP + NFC + f];
             s1 += gpart[(size_t)(e + CRED_THREADS) * NCP + NFC + f];
@@ -1384,35 +1355,12 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
     const int t = threadIdx.x;
     // the camera sums were all-reduced in a scratch buffer (a skipped speculative step reduces only
     // scratch): the linearization's own copy is written here, behind the gate
-    for (int i = t; i < ncs; i += blockDim.x) camsum_out[i] = camsum[i];
+    // r06: every load-only loop first (group partials, the camera model part), the loops with stores
+    // last: a load issued after a store waits for it (vmcnt counts both, in order), which serialised
+    // the loops' memory round trips.  Each quantity keeps its per-thread order and the block reduction.
     const size_t ne = 3 * (size_t)P;
     const int nf = 6 * C + K;
     double gmax = 0.0, xn = 0.0, sn = 0.0;
-    for (int i = t; i < nf; i += blockDim.x) {
-        double cs, gr;
-        if (i < 6 * C) {
-            const int c = i / 6, u = i % 6;
-            int e = 0;
-            for (int x = 0; x < u; ++x) e += 6 - x;
-            cs = camsum[(size_t)c * NCP + e];
-            gr = camsum[(size_t)c * NCP + cp_gc(K) + u];
-        } else {
-            const int ii = i - 6 * C;
-            int e = 0;
-            for (int x = 0; x < ii; ++x) e += K - x;
-            cs = camsum[(size_t)C * NCP + e];
-            gr = camsum[(size_t)C * NCP + K * (K + 1) / 2 + ii];
-        }
-        colsq[ne + i] = cs;
-        grad[ne + i] = gr;
-        gmax = fmax(gmax, fabs(gr));
-        const double v = xf_new[i];
-        xn += v * v;
-        if (cand_mode) {
-            const double d = xf_old[i] - v;
-            sn += isfinite(d) ? d * d : INFINITY;
-        }
-    }
     double g[5] = {0, 0, 0, 0, 0};
     if (!pre)
         for (int b = t; b < ngroups; b += blockDim.x) {
@@ -1467,6 +1415,32 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
             mf += q;
         }
     }
+    for (int i = t; i < nf; i += blockDim.x) {
+        double cs, gr;
+        if (i < 6 * C) {
+            const int c = i / 6, u = i % 6;
+            int e = 0;
+            for (int x = 0; x < u; ++x) e += 6 - x;
+            cs = camsum[(size_t)c * NCP + e];
+            gr = camsum[(size_t)c * NCP + cp_gc(K) + u];
+        } else {
+            const int ii = i - 6 * C;
+            int e = 0;
+            for (int x = 0; x < ii; ++x) e += K - x;
+            cs = camsum[(size_t)C * NCP + e];
+            gr = camsum[(size_t)C * NCP + K * (K + 1) / 2 + ii];
+        }
+        colsq[ne + i] = cs;
+        grad[ne + i] = gr;
+        gmax = fmax(gmax, fabs(gr));
+        const double v = xf_new[i];
+        xn += v * v;
+        if (cand_mode) {
+            const double d = xf_old[i] - v;
+            sn += isfinite(d) ? d * d : INFINITY;
+        }
+    }
+    for (int i = t; i < ncs; i += blockDim.x) camsum_out[i] = camsum[i];
     // one pass: the group sums (unless the all-reduced ones are given), the camera model part, the
     // camera parts of the parameter and step norms, and max |grad|
     double v[7] = {g[0], g[1], g[2], g[3], mf, xn, sn};
