@@ -85,3 +85,15 @@ def test_failed_legs_leave_an_error_not_a_missing_line():
     assert len(line["legs"]["mvs"]["error"]) <= 300
     assert "ba_calls" not in line["legs"]
     assert len(json.dumps(line)) <= bench.LINE_MAX_BYTES and line["roofline"]["frac"] is not None
+
+
+def test_recorded_r06_line_kernel_time_within_the_step():
+    """the line's kernel time comes from the timed steps' own events (the
+    matcher's per-run event ring), so it cannot exceed the step it is part of."""
+    with open(os.path.join(REPO, "profiles", "r06n_bench_line.json")) as f:
+        line = json.loads(f.read())
+    assert list(line)[:len(HEAD)] == HEAD
+    rf = line["roofline"]
+    assert 0 < rf["kernel_ms_per_launch"] <= line["ms_per_step"]
+    assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], rel=1e-4)
+    assert line["n_gpus"] == 1 and line["config"]["workload"].startswith("50 images")
