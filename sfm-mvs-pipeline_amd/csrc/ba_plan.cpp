@@ -296,7 +296,11 @@ void make_plan(int C, const std::vector<char>& adj, int order_mode, FactorPlan& 
     }
     FactorPlan best;
     build(C, g, natural, 0, 0, best);
-    if (order_mode == 0 || C == 0) { out = std::move(best); return; }
+    if (order_mode == 0 || C == 0) {
+        out = std::move(best);
+        row_masks(out, adj, out.src_mask, out.pad_panels);
+        return;
+    }
     const int leaves_all[3] = {1, 2, 4};
     Nd nd(g, std::max(1, leaves_all[0] * NBP / 6));   // one dissection, the smallest leaf
     {
@@ -320,6 +324,7 @@ void make_plan(int C, const std::vector<char>& adj, int order_mode, FactorPlan& 
         }
     }
     out = std::move(best);
+    row_masks(out, adj, out.src_mask, out.pad_panels);   // (r06: beside the plan, e.g. on the load's plan thread)
 }
 
 
@@ -340,21 +345,34 @@ void row_masks(const FactorPlan& P, const std::vector<char>& adj, std::vector<Ro
         for (int b = 0; b <= a; ++b)
             if (P.nz[(size_t)a * T + b] || a == b) tid[(size_t)a * T + b] = ntiles++;
     std::vector<uint64_t> pat((size_t)ntiles * NBP, 0);
-    auto rowcam = [&](int r) { const int m = P.rowmap[r]; return m < 0 ? -1 : m / 6; };
+    // per tile: its cameras and the row mask of each (a camera's 6 rows are contiguous, padding rows
+    // are -1 in rowmap): the patterns are built camera by camera (C5: 66 tiles x ~11 x ~11 camera pairs
+    // instead of 66 x 64 x 64 row pairs: this runs on every plan, i.e. every SfM call whose co-visibility
+    // changed)
+    std::vector<std::vector<std::pair<int, uint64_t>>> tcams(T);
+    for (int a = 0; a < T; ++a)
+        for (int i = 0; i < NBP; ++i) {
+            const int m = P.rowmap[a * NBP + i];
+            if (m < 0) continue;
+            const int ci = m / 6;
+            if (tcams[a].empty() || tcams[a].back().first != ci) tcams[a].push_back({ci, 0});
+            tcams[a].back().second |= (uint64_t)1 << i;
+        }
     for (int a = 0; a < T; ++a)
         for (int b = 0; b <= a; ++b) {
             const int id = tid[(size_t)a * T + b];
             if (id < 0) continue;
-            for (int i = 0; i < NBP; ++i) {
-                const int ci = rowcam(a * NBP + i);
+            uint64_t* pt = &pat[(size_t)id * NBP];
+            for (const auto& ca : tcams[a]) {
                 uint64_t m = 0;
-                for (int j = 0; j < NBP; ++j) {
-                    const int cj = rowcam(b * NBP + j);
-                    const bool nzv = ci < 0 || cj < 0 ? (a == b && i == j) : (ci == cj || adj[(size_t)ci * C + cj]);
-                    m |= (uint64_t)nzv << j;
-                }
-                pat[(size_t)id * NBP + i] = m;
+                for (const auto& cb : tcams[b])
+                    if (ca.first == cb.first || adj[(size_t)ca.first * C + cb.first]) m |= cb.second;
+                for (int i = 0; i < NBP; ++i)
+                    if ((ca.second >> i) & 1) pt[i] = m;
             }
+            if (a == b)   // identity padding rows: their diagonal only
+                for (int i = 0; i < NBP; ++i)
+                    if (P.rowmap[a * NBP + i] < 0) pt[i] = (uint64_t)1 << i;
         }
     auto rows_of = [&](int id) { uint64_t r = 0; for (int i = 0; i < NBP; ++i) r |= (uint64_t)(pat[(size_t)id * NBP + i] != 0) << i; return r; };
     auto cols_of = [&](int id) { uint64_t c = 0; for (int i = 0; i < NBP; ++i) c |= pat[(size_t)id * NBP + i]; return c; };

@@ -32,6 +32,10 @@ namespace ba {
 constexpr int PLAN_NB = SFMX_BA_NB;   // tile size (== NB of the kernels, ba_kernels.hpp)
 
 struct PlanTask { int a, b, s0, s1; };   // destination tile (a, b), a >= b; source panels src[s0 .. s1)
+// Row-level zero structure of the factorization (ba_plan.cpp row_masks): per src entry (task, source k) the
+// 16-row strips of A_ak (ra) and A_bk (rb) and the 4-column chunks of their columns (ka, kb) that
+// can be nonzero; per tile the 16-row panels that are identity padding (bit q = rows 16q .. 16q + 15).
+struct RowMask { int ra, rb, ka, kb; };
 
 struct FactorPlan {
     int C = 0, npad = 0, T = 0, order = 0;          // order: 0 natural, 1 nested dissection
@@ -53,6 +57,8 @@ struct FactorPlan {
     std::vector<int> bs_start, bs_k, lvl_start, lvl_panels;
     int tiles_nz = 0;
     double predicted_us = 0.0;
+    std::vector<RowMask> src_mask;                  // per src entry (r06, row_masks; made with the plan)
+    std::vector<int> pad_panels;                    // per tile
 };
 
 // adj: C x C row-major 0/1, the global camera co-visibility (symmetric; the diagonal is ignored).
@@ -60,10 +66,7 @@ struct FactorPlan {
 // the model), 2/3/4 nested dissection with leaves of 1/2/4 tiles.
 void make_plan(int C, const std::vector<char>& adj, int order_mode, FactorPlan& out);
 
-// Row-level zero structure of the factorization (ba_plan.cpp): per src entry (task, source k) the
-// 16-row strips of A_ak (ra) and A_bk (rb) and the 4-column chunks of their columns (ka, kb) that
-// can be nonzero; per tile the 16-row panels that are identity padding (bit q = rows 16q .. 16q + 15).
-struct RowMask { int ra, rb, ka, kb; };
+// (computed at the end of make_plan into P.src_mask / P.pad_panels)
 void row_masks(const FactorPlan& P, const std::vector<char>& adj, std::vector<RowMask>& src_mask,
                std::vector<int>& pad_panels);
 

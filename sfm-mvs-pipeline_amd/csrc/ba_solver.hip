@@ -732,9 +732,8 @@ int ensure_plan(sfmx_ba_ctx* c) {
             for (int t = pl.task_start[l]; t < pl.task_start[l + 1]; ++t)
                 vfin[vid(pl.tasks[t].a, pl.tasks[t].b)] += 1 + ((t - pl.task_start[l]) < pl.ninv[l] ? 1 : 0);
         std::vector<int4> items, need, imask;
-        std::vector<sfmx::ba::RowMask> smask;
-        std::vector<int> padp;
-        sfmx::ba::row_masks(pl, adj, smask, padp);
+        const std::vector<sfmx::ba::RowMask>& smask = pl.src_mask;   // (made with the plan)
+        const std::vector<int>& padp = pl.pad_panels;
         // r06: per task, the panels an inverting one-source task sweeps before its update (the ones
         // outside A_ak's row strips and not padding); every factorization form uses the same order
         std::vector<int> tpre(std::max<size_t>(pl.tasks.size(), 1), 0);
