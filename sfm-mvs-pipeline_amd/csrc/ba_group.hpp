@@ -24,7 +24,8 @@
 //   ba_glin      residuals + Jacobian (dual numbers, = ceres::AutoDiffCostFunction on the reference
 //                functors) at x or at the candidate; J records; cost; per-point column norms and
 //                gradient; per-(group, camera) partials of J^T J and J^T r of the camera columns
-//   ba_camred    per camera (one workgroup each, + one for the intrinsics): those partials in group order
+//   ba_camred    per camera (one workgroup each): those partials in group order (the intrinsics fields
+//                per camera, folded over the cameras by ba_finalize)
 //   ba_gschur    per-point E, M, t, H; the group's -sum H H^T block and -sum H t
 //   ba_assemble  one workgroup per block of S: sum over the groups that hold it, in group order
 //   ba_add_cam   + scaled C, D_f^2 and g_f (after any cross-rank all-reduce of S)
@@ -1265,46 +1266,72 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
 }
 
 // ---------------------------------------------------------------------------------------------
-// ba_camred: per camera (one workgroup of 256) the partials of its (group, camera) slots ->
-// camsum[c]: thread (part, field) sums the slots part, part + NP, ... (NP = 256 / fields), the parts
-// are added in part order (fixed); one more workgroup per intrinsics field: that field of every
-// slot, strided per thread (2 chains), then a fixed-order block reduction.
-constexpr int CRED_THREADS = 256;
+// stamps of ba_camred (slots 24..31): phase totals, then per kind (camera / intrinsics workgroups) the
+// workgroup count and the longest workgroup
+#ifdef SFMX_BA_STAMPS
+#define CAMRED_FLUSH(kind)                                                                         \
+    do {                                                                                           \
+        BA_FLUSH(24);                                                                              \
+        if (threadIdx.x == 0) {                                                                    \
+            const long long d_ = ba_acc_[0] + ba_acc_[1] + ba_acc_[2] + ba_acc_[3];                 \
+            atomicAdd(&g_ba_stamps[28 + 2 * (kind)], 1ull);                                        \
+            atomicMax(&g_ba_stamps[29 + 2 * (kind)], (unsigned long long)d_);                      \
+        }                                                                                          \
+    } while (0)
+#else
+#define CAMRED_FLUSH(kind) do { } while (0)
+#endif
+// ba_camred: per camera (one workgroup of 512) the partials of its (group, camera) slots ->
+// camsum[c]: thread (part, field) sums the slots part, part + NP, ... (NP = 512 / NCP), the parts are
+// added in part order (fixed).  Every field of the slot record is summed, the intrinsics ones too:
+// camsum[c]'s intrinsics fields hold camera c's share of the intrinsics block and gradient, which
+// ba_finalize folds over the cameras (fixed order) after the all-reduce.  (r06: until then one
+// workgroup per intrinsics field gathered that field from every slot, 113 dependent rounds per
+// thread at C5: 40-47 k cycles per workgroup against 7.6 k for a camera, profiles/r06o_ba_stamps.txt.)
+constexpr int CRED_THREADS = 512;
 template <int K>
 __global__ __launch_bounds__(CRED_THREADS)
 void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int* __restrict__ cref,
                const double* __restrict__ gpart, double* __restrict__ camsum, const int* __restrict__ gate) {
     if (step_gated(gate)) return;
-    constexpr int NCP = ncp(K), NFC = cp_ii(K), NP = CRED_THREADS / NFC;
+    BA_T0();
+    constexpr int NCP = ncp(K), NP = CRED_THREADS / NCP;
     __shared__ double part[CRED_THREADS];
     const int t = threadIdx.x;
-    if ((int)blockIdx.x < C) {
-        const int c = blockIdx.x, e0 = cref_start[c], e1 = cref_start[c + 1], f = t % NFC, pt = t / NFC;
-        if (pt < NP) {
-            double sacc = 0.0;
-            int e = e0 + pt;
+    const int c = blockIdx.x, e0 = cref_start[c], e1 = cref_start[c + 1], f = t % NCP, pt = t / NCP;
+    if (pt < NP) {
+        double sacc = 0.0;
+        int e = e0 + pt;
 #pragma unroll 4
-            for (; e < e1; e += NP) sacc += gpart[(size_t)cref[e] * NCP + f];
-            part[t] = sacc;
-        }
-        __syncthreads();
-        if (t < NFC) {
-            double sm = part[t];
-            for (int q = 1; q < NP; ++q) sm += part[q * NFC + t];
-            camsum[(size_t)c * NCP + t] = sm;
-        }
-    } else {   // intrinsics field f = blockIdx.x - C over every slot
-        const int f = blockIdx.x - C;
-        double s0 = 0.0, s1 = 0.0;
-        int e = t;
-        for (; e + CRED_THREADS < nslots; e += 2 * CRED_THREADS) {
-            s0 += gpart[(size_t)e * NCP + NFC + f];
-            s1 += gpart[(size_t)(e + CRED_THREADS) * NCP + NFC + f];
-        }
-        if (e < nslots) s0 += gpart[(size_t)e * NCP + NFC + f];
-        const double tot = block_sum(s0 + s1, part);
-        if (t == 0) camsum[(size_t)C * NCP + f] = tot;
+        for (; e < e1; e += NP) sacc += gpart[(size_t)cref[e] * NCP + f];
+        part[t] = sacc;
     }
+    __syncthreads();
+    BA_STAMP(0);
+    if (t < NCP) {
+        double sm = part[t];
+        for (int q = 1; q < NP; ++q) sm += part[q * NCP + t];
+        camsum[(size_t)c * NCP + t] = sm;
+    }
+    BA_STAMP(1);
+    CAMRED_FLUSH(0);
+    (void)nslots;
+}
+
+// The intrinsics block and gradient: camsum[c]'s intrinsics fields summed over the cameras, one wave
+// per field (lane l adds cameras l, l + 64, ... in order, then the wave's xor tree: a fixed order).
+// Every thread of the workgroup calls it; tot[NI] in LDS, valid after the call.
+template <int K>
+__device__ __forceinline__ void fold_intrinsics(int C, const double* __restrict__ camsum, double* tot) {
+    constexpr int NCP = ncp(K), NFC = cp_ii(K), NI = NCP - NFC;
+    const int lane = threadIdx.x & 63, nw = (int)(blockDim.x >> 6);
+    for (int f = (int)(threadIdx.x >> 6); f < NI; f += nw) {
+        double s = 0.0;
+        for (int c = lane; c < C; c += 64) s += camsum[(size_t)c * NCP + NFC + f];
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        if (lane == 0) tot[f] = s;
+    }
+    __syncthreads();
 }
 
 // NS sums and one maximum over a workgroup of up to 1024 threads in one pass: every value reduced
@@ -1350,9 +1377,11 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
                  unsigned pub_v, const double* __restrict__ camsum_cur, const double* __restrict__ sol_f,
                  const double* __restrict__ scale_f) {
     if (step_gated(fail + 1)) return;
-    constexpr int NCP = ncp(K);
+    constexpr int NCP = ncp(K), NI = K * (K + 1) / 2 + K;
     __shared__ double sh[16 * 8];
+    __shared__ double itot[NI];
     const int t = threadIdx.x;
+    fold_intrinsics<K>(C, camsum, itot);   // (ba_camred leaves the intrinsics per camera)
     // the camera sums were all-reduced in a scratch buffer (a skipped speculative step reduces only
     // scratch): the linearization's own copy is written here, behind the gate
     // r06: every load-only loop first (group partials, the camera model part), the loops with stores
@@ -1427,8 +1456,8 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
             const int ii = i - 6 * C;
             int e = 0;
             for (int x = 0; x < ii; ++x) e += K - x;
-            cs = camsum[(size_t)C * NCP + e];
-            gr = camsum[(size_t)C * NCP + K * (K + 1) / 2 + ii];
+            cs = itot[e];
+            gr = itot[K * (K + 1) / 2 + ii];
         }
         colsq[ne + i] = cs;
         grad[ne + i] = gr;
@@ -1440,7 +1469,9 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
             sn += isfinite(d) ? d * d : INFINITY;
         }
     }
-    for (int i = t; i < ncs; i += blockDim.x) camsum_out[i] = camsum[i];
+    for (int i = t; i < ncs; i += blockDim.x)
+        if ((unsigned)(i - C * NCP) >= (unsigned)NI) camsum_out[i] = camsum[i];
+    if (t < NI) camsum_out[(size_t)C * NCP + t] = itot[t];   // (camsum_out may be camsum: other bytes)
     // one pass: the group sums (unless the all-reduced ones are given), the camera model part, the
     // camera parts of the parameter and step norms, and max |grad|
     double v[7] = {g[0], g[1], g[2], g[3], mf, xn, sn};

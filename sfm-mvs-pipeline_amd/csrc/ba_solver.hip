@@ -396,7 +396,7 @@ int lin_at(sfmx_ba_ctx* c, const double* xp, double* Wo, double* PRo, double* co
     // all-reduce then touches no state (ba_finalize copies them behind the step gate)
     const int ncs = c->C * ncp(K) + K * (K + 1) / 2 + K;
     double* cs_red = (multirank(c) && c->spec) ? c->camscr.as<double>() : camsum_o;
-    hipLaunchKernelGGL(ba_camred<K>, dim3(c->C + K * (K + 1) / 2 + K), dim3(CRED_THREADS), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
+    if (c->C) hipLaunchKernelGGL(ba_camred<K>, dim3(c->C), dim3(CRED_THREADS), 0, c->st, c->C, c->nslots, c->cref_start.as<int>(),
                        c->cref.as<int>(), c->gpart.as<double>(), cs_red, gate(c));
     HIPCHK(hipGetLastError());
     // multi-rank: the group sums ride in the camera-sum all-reduce (cs_red[ncs .. ncs + 4), the

@@ -18,7 +18,10 @@ NAMES = {0: "gschur round MFMA", 1: "gschur wave combine", 2: "gschur store", 3:
          4: "gschur point phase", 5: "gschur round H fill", 8: "glin zero G + sync",
          9: "glin dual numbers + stores", 10: "glin barrier wait", 11: "glin point sums + gram + sync",
          12: "glin epilogue",
-         16: "gupdate obs", 17: "gupdate point", 18: "gupdate model", 19: "gupdate epilogue"}
+         16: "gupdate obs", 17: "gupdate point", 18: "gupdate model", 19: "gupdate epilogue",
+         24: "camred cam loads", 25: "camred cam combine", 26: "camred intr loads", 27: "camred intr sum",
+         28: "camred cam WGs (count)", 29: "camred cam WG max", 30: "camred intr WGs (count)",
+         31: "camred intr WG max"}
 prob = synth.ba_problem(200, 200_000)
 ctx = ba.BAContext(ba.BAProblem(**prob), ba.default_options())
 ctx.run(max_iterations=1)
@@ -33,4 +36,9 @@ steps = sm["num_successful_steps"] + sm["num_unsuccessful_steps"] - 1
 print(f"LM steps {steps}; cycles per step (thread 0 of each workgroup, summed over workgroups):")
 for i, v in enumerate(buf):
     if v:
-        print(f"  [{i:2d}] {NAMES.get(i, '?'):22s} {v / max(steps, 1) / 1e6:10.2f} Mcyc")
+        if i in (29, 31):   # the longest single workgroup (s_memtime cycles), not a total
+            print(f"  [{i:2d}] {NAMES.get(i, '?'):22s} {v:10d} cyc")
+        elif i in (28, 30):
+            print(f"  [{i:2d}] {NAMES.get(i, '?'):22s} {v / max(steps, 1):10.1f} per step")
+        else:
+            print(f"  [{i:2d}] {NAMES.get(i, '?'):22s} {v / max(steps, 1) / 1e6:10.2f} Mcyc")
