@@ -657,7 +657,38 @@ __device__ __forceinline__ double wave_sum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
-constexpr int ASM_THREADS = 256;
+constexpr int ASM_THREADS = 256, ASM_BATCH = 8;
+// ASM_BATCH entries e0, e0 + step, ... (< l1) of a block's list: every entry record loaded, then every
+// value (the normal groups' sg element, a big group's H rows, or the rhs rg element), so one batch costs
+// two memory round trips instead of two per entry (r06: the lists are 80-2000 entries long, and a
+// thread walked its share one dependent pair of loads at a time)
+template <int NB_>
+__device__ __forceinline__ void asm_batch(const AEnt* __restrict__ ents, const double* __restrict__ sg,
+                                          const double* __restrict__ hbig, const double* __restrict__ rg, int e0,
+                                          int step, int l1, bool rhs, int r, int c, double (&xv)[NB_]) {
+    AEnt E[NB_];
+#pragma unroll
+    for (int k = 0; k < NB_; ++k)
+        if (e0 + k * step < l1) E[k] = ents[e0 + k * step];
+#pragma unroll
+    for (int k = 0; k < NB_; ++k) {
+        xv[k] = 0.0;
+        if (e0 + k * step < l1) xv[k] = rhs ? rg[E[k].rg + r] : aval(E[k], sg, hbig, r, c);
+    }
+}
+// stamps (diagnostic stamp build): per task type the longest workgroup's load phase, slots 32 + 2 type
+#ifdef SFMX_BA_STAMPS
+#define ASM_STAMP_END(type)                                                                        \
+    do {                                                                                           \
+        if (threadIdx.x == 0) {                                                                    \
+            const long long d_ = (long long)__builtin_amdgcn_s_memtime() - ba_t_;                  \
+            atomicAdd(&g_ba_stamps[32 + 2 * (type)], 1ull);                                        \
+            atomicMax(&g_ba_stamps[33 + 2 * (type)], (unsigned long long)d_);                      \
+        }                                                                                          \
+    } while (0)
+#else
+#define ASM_STAMP_END(type) do { } while (0)
+#endif
 __global__ __launch_bounds__(ASM_THREADS)
 void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents, const double* __restrict__ sg,
                  const double* __restrict__ hbig, const double* __restrict__ rg, int K, const int* __restrict__ camrow,
@@ -666,6 +697,7 @@ void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents,
                  const double* __restrict__ camsum, const double* __restrict__ scale, const double* __restrict__ colsq,
                  double dmin, double dmax, double radius, const double* __restrict__ lm) {
     if (step_gated(gate)) return;
+    BA_T0();
     if (fuse && lm) radius = lm[LM_RADIUS];
     __shared__ double part[ASM_THREADS];
     const ATask T = tasks[blockIdx.x];
@@ -678,22 +710,19 @@ void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents,
     const double* si = scale + ne + nfc;
     if (T.type == 2) {          // one intrinsics output x = T.b over every group; entries at the intrinsics rows
         const int x = T.b;
-        double v0 = 0.0, v1 = 0.0;
-        int e = T.l0 + t;
-        if (x < K * K) {
-            const int i = x / K, j = x % K;
-            for (; e + ASM_THREADS < T.l1; e += 2 * ASM_THREADS) {
-                v0 += aval(ents[e], sg, hbig, i, j);
-                v1 += aval(ents[e + ASM_THREADS], sg, hbig, i, j);
+        double v0 = 0.0, v1 = 0.0;   // the thread's entries k = 0, 1, 2, ... alternate between two chains
+        const bool blk = x < K * K;
+        const int i = blk ? x / K : x - K * K, j = blk ? x % K : 0;   // (rhs: rg row i)
+        for (int e0 = T.l0 + t; e0 < T.l1; e0 += ASM_BATCH * ASM_THREADS) {
+            double xv[ASM_BATCH];
+            asm_batch<ASM_BATCH>(ents, sg, hbig, rg, e0, ASM_THREADS, T.l1, !blk, i, j, xv);
+#pragma unroll
+            for (int k = 0; k < ASM_BATCH; k += 2) {   // (ASM_BATCH even: k keeps its parity across batches)
+                if (e0 + k * ASM_THREADS < T.l1) v0 += xv[k];
+                if (e0 + (k + 1) * ASM_THREADS < T.l1) v1 += xv[k + 1];
             }
-            if (e < T.l1) v0 += aval(ents[e], sg, hbig, i, j);
-        } else {
-            for (; e + ASM_THREADS < T.l1; e += 2 * ASM_THREADS) {
-                v0 += rg[ents[e].rg + (x - K * K)];
-                v1 += rg[ents[e + ASM_THREADS].rg + (x - K * K)];
-            }
-            if (e < T.l1) v0 += rg[ents[e].rg + (x - K * K)];
         }
+        ASM_STAMP_END(2);
         const double v = wave_sum(v0 + v1);
         if ((t & 63) == 0) part[t >> 6] = v;
         __syncthreads();
@@ -716,11 +745,16 @@ void ba_assemble(const ATask* __restrict__ tasks, const AEnt* __restrict__ ents,
     if (pt < np) {
         const bool rhs = T.type == 1 && o >= 6 * K;
         const int r = T.type == 0 ? o / 6 : (rhs ? o - 6 * K : o / K), c = T.type == 0 ? o % 6 : o % K;
-        int e = T.l0 + pt;
-#pragma unroll 4
-        for (; e < T.l1; e += np) v += rhs ? rg[ents[e].rg + r] : aval(ents[e], sg, hbig, r, c);
+        for (int e0 = T.l0 + pt; e0 < T.l1; e0 += ASM_BATCH * np) {
+            double xv[ASM_BATCH];
+            asm_batch<ASM_BATCH>(ents, sg, hbig, rg, e0, np, T.l1, rhs, r, c, xv);
+#pragma unroll
+            for (int k = 0; k < ASM_BATCH; ++k)
+                if (e0 + k * np < T.l1) v += xv[k];
+        }
         part[t] = v;
     }
+    ASM_STAMP_END(T.type);
     __syncthreads();
     if (t < nout) {
         double s = part[t];
@@ -1320,18 +1354,28 @@ void ba_camred(int C, int nslots, const int* __restrict__ cref_start, const int*
 
 // The intrinsics block and gradient: camsum[c]'s intrinsics fields summed over the cameras, one wave
 // per field (lane l adds cameras l, l + 64, ... in order, then the wave's xor tree: a fixed order).
-// Every thread of the workgroup calls it; tot[NI] in LDS, valid after the call.
+// Every thread of the workgroup calls it; tot[NI] in LDS, valid after the caller's next barrier.
+// The loads go out 4 cameras at a time (one memory round trip per 256 cameras, not per 64).
 template <int K>
 __device__ __forceinline__ void fold_intrinsics(int C, const double* __restrict__ camsum, double* tot) {
     constexpr int NCP = ncp(K), NFC = cp_ii(K), NI = NCP - NFC;
     const int lane = threadIdx.x & 63, nw = (int)(blockDim.x >> 6);
     for (int f = (int)(threadIdx.x >> 6); f < NI; f += nw) {
         double s = 0.0;
-        for (int c = lane; c < C; c += 64) s += camsum[(size_t)c * NCP + NFC + f];
+        for (int c0 = lane; c0 < C; c0 += 256) {
+            double v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int c = c0 + 64 * k;
+                v[k] = c < C ? camsum[(size_t)c * NCP + NFC + f] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (c0 + 64 * k < C) s += v[k];
+        }
         for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
         if (lane == 0) tot[f] = s;
     }
-    __syncthreads();
 }
 
 // NS sums and one maximum over a workgroup of up to 1024 threads in one pass: every value reduced
@@ -1381,7 +1425,7 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
     __shared__ double sh[16 * 8];
     __shared__ double itot[NI];
     const int t = threadIdx.x;
-    fold_intrinsics<K>(C, camsum, itot);   // (ba_camred leaves the intrinsics per camera)
+    fold_intrinsics<K>(C, camsum, itot);   // (ba_camred leaves the intrinsics per camera; barrier below)
     // the camera sums were all-reduced in a scratch buffer (a skipped speculative step reduces only
     // scratch): the linearization's own copy is written here, behind the gate
     // r06: every load-only loop first (group partials, the camera model part), the loops with stores
@@ -1392,6 +1436,7 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
     double gmax = 0.0, xn = 0.0, sn = 0.0;
     double g[5] = {0, 0, 0, 0, 0};
     if (!pre)
+#pragma unroll 2
         for (int b = t; b < ngroups; b += blockDim.x) {
             const double* q = gpl + (size_t)b * GP_N;
             g[0] += q[GP_COST]; g[1] += q[GP_MODEL]; g[2] += q[GP_STEPN]; g[3] += q[GP_XN];
@@ -1444,29 +1489,45 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
             mf += q;
         }
     }
-    for (int i = t; i < nf; i += blockDim.x) {
-        double cs, gr;
-        if (i < 6 * C) {
-            const int c = i / 6, u = i % 6;
-            int e = 0;
-            for (int x = 0; x < u; ++x) e += 6 - x;
-            cs = camsum[(size_t)c * NCP + e];
-            gr = camsum[(size_t)c * NCP + cp_gc(K) + u];
-        } else {
-            const int ii = i - 6 * C;
-            int e = 0;
-            for (int x = 0; x < ii; ++x) e += K - x;
-            cs = itot[e];
-            gr = itot[K * (K + 1) / 2 + ii];
+    __syncthreads();   // itot
+    // two rows per thread per pass, both rows' loads ahead of both rows' stores
+    const int bd = (int)blockDim.x;
+    for (int i0 = t; i0 < nf; i0 += 2 * bd) {
+        double cs[2], gr[2], xv[2], xo[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int i = i0 + r * bd;
+            cs[r] = gr[r] = xv[r] = xo[r] = 0.0;
+            if (i >= nf) continue;
+            if (i < 6 * C) {
+                const int c = i / 6, u = i % 6;
+                int e = 0;
+                for (int x = 0; x < u; ++x) e += 6 - x;
+                cs[r] = camsum[(size_t)c * NCP + e];
+                gr[r] = camsum[(size_t)c * NCP + cp_gc(K) + u];
+            } else {
+                const int ii = i - 6 * C;
+                int e = 0;
+                for (int x = 0; x < ii; ++x) e += K - x;
+                cs[r] = itot[e];
+                gr[r] = itot[K * (K + 1) / 2 + ii];
+            }
+            xv[r] = xf_new[i];
+            if (cand_mode) xo[r] = xf_old[i];
         }
-        colsq[ne + i] = cs;
-        grad[ne + i] = gr;
-        gmax = fmax(gmax, fabs(gr));
-        const double v = xf_new[i];
-        xn += v * v;
-        if (cand_mode) {
-            const double d = xf_old[i] - v;
-            sn += isfinite(d) ? d * d : INFINITY;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int i = i0 + r * bd;
+            if (i >= nf) continue;
+            colsq[ne + i] = cs[r];
+            grad[ne + i] = gr[r];
+            gmax = fmax(gmax, fabs(gr[r]));
+            const double v = xv[r];
+            xn += v * v;
+            if (cand_mode) {
+                const double d = xo[r] - v;
+                sn += isfinite(d) ? d * d : INFINITY;
+            }
         }
     }
     for (int i = t; i < ncs; i += blockDim.x)

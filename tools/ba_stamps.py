@@ -21,7 +21,9 @@ NAMES = {0: "gschur round MFMA", 1: "gschur wave combine", 2: "gschur store", 3:
          16: "gupdate obs", 17: "gupdate point", 18: "gupdate model", 19: "gupdate epilogue",
          24: "camred cam loads", 25: "camred cam combine", 26: "camred intr loads", 27: "camred intr sum",
          28: "camred cam WGs (count)", 29: "camred cam WG max", 30: "camred intr WGs (count)",
-         31: "camred intr WG max"}
+         31: "camred intr WG max", 32: "assemble pose WGs", 33: "assemble pose WG max",
+         34: "assemble cam-intr WGs", 35: "assemble cam-intr WG max", 36: "assemble intr WGs",
+         37: "assemble intr WG max"}
 prob = synth.ba_problem(200, 200_000)
 ctx = ba.BAContext(ba.BAProblem(**prob), ba.default_options())
 ctx.run(max_iterations=1)
@@ -36,9 +38,9 @@ steps = sm["num_successful_steps"] + sm["num_unsuccessful_steps"] - 1
 print(f"LM steps {steps}; cycles per step (thread 0 of each workgroup, summed over workgroups):")
 for i, v in enumerate(buf):
     if v:
-        if i in (29, 31):   # the longest single workgroup (s_memtime cycles), not a total
+        if i in (29, 31, 33, 35, 37):   # the longest single workgroup (s_memtime cycles), not a total
             print(f"  [{i:2d}] {NAMES.get(i, '?'):22s} {v:10d} cyc")
-        elif i in (28, 30):
+        elif i in (28, 30, 32, 34, 36):
             print(f"  [{i:2d}] {NAMES.get(i, '?'):22s} {v / max(steps, 1):10.1f} per step")
         else:
             print(f"  [{i:2d}] {NAMES.get(i, '?'):22s} {v / max(steps, 1) / 1e6:10.2f} Mcyc")
