@@ -1425,7 +1425,9 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
     __shared__ double sh[16 * 8];
     __shared__ double itot[NI];
     const int t = threadIdx.x;
+    BA_T0();
     fold_intrinsics<K>(C, camsum, itot);   // (ba_camred leaves the intrinsics per camera; barrier below)
+    BA_STAMP(0);
     // the camera sums were all-reduced in a scratch buffer (a skipped speculative step reduces only
     // scratch): the linearization's own copy is written here, behind the gate
     // r06: every load-only loop first (group partials, the camera model part), the loops with stores
@@ -1447,6 +1449,7 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
     // sums: per camera its 6 x 6 block, its coupling to the intrinsics and its gradient, then the
     // intrinsics block (one more slot); fixed order (thread stride, then the block sum)
     double mf = 0.0;
+    BA_STAMP(1);
     if (cand_mode) {
         const double* sif = scale_f + 6 * (size_t)C;
         double di[K];
@@ -1489,7 +1492,9 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
             mf += q;
         }
     }
+    BA_STAMP(2);
     __syncthreads();   // itot
+    BA_STAMP(3);
     // two rows per thread per pass, both rows' loads ahead of both rows' stores
     const int bd = (int)blockDim.x;
     for (int i0 = t; i0 < nf; i0 += 2 * bd) {
@@ -1530,6 +1535,7 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
             }
         }
     }
+    BA_STAMP(4);
     for (int i = t; i < ncs; i += blockDim.x)
         if ((unsigned)(i - C * NCP) >= (unsigned)NI) camsum_out[i] = camsum[i];
     if (t < NI) camsum_out[(size_t)C * NCP + t] = itot[t];   // (camsum_out may be camsum: other bytes)
@@ -1538,6 +1544,7 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
     double v[7] = {g[0], g[1], g[2], g[3], mf, xn, sn};
     double gm = fmax(gmax, g[4]);
     block_reduce<7>(v, gm, sh);
+    BA_STAMP(5);
     if (t == 0) {
         const double s0 = pre ? pre[0] : v[0], s1 = pre ? pre[1] : v[1], s2 = pre ? pre[2] : v[2], s3 = pre ? pre[3] : v[3];
         const double m = pre ? fmax(gm, pre[4]) : gm;
@@ -1552,6 +1559,11 @@ void ba_finalize(int ngroups, int P, int C, const double* __restrict__ camsum, c
         // one rank: nothing is reduced after this kernel, so it publishes the scalars itself (ba_publish)
         if (pub_dst) publish_body(scal, SC_N, nullptr, 0, pub_dst, pub_seq, pub_v, fail);
     }
+    BA_STAMP(6);
+#ifdef SFMX_BA_STAMPS
+    ba_acc_[7] = 1;   // calls
+#endif
+    BA_FLUSH(cand_mode ? 48 : 40);
 }
 
 // Point-sharded ranks: the rank's group sums (cost, model change, step and parameter norms: the
