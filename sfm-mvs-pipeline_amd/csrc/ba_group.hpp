@@ -225,6 +225,9 @@ __host__ __device__ constexpr int gs_pd(int K) { return 9 + 3 * K; }            
 __host__ __device__ constexpr int gs_wreg(int K, int) {                               // doubles per wave
     return WB_OBS * WST + WB_PTS * gs_pd(K) + WB_PTS * UMAX / 8;                      // W rows | point data | lane map
 }
+__host__ __device__ constexpr int gs_comb(int NT) {   // doubles of the NT <= 3 combine's wave partials (tiles | rhs)
+    return NT <= 3 ? 4 * (NT * (NT + 1) / 2 * 256 + 16 * NT) : 0;
+}
 #ifndef GSCHUR_WAVES
 #define GSCHUR_WAVES 2   // waves per SIMD the register budget targets (A/B: -DGSCHUR_WAVES=3)
 #endif
@@ -550,8 +553,43 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
         const double a = racc[I] + __shfl_xor(racc[I], 16);   // lanes m, m+16 | m+32, m+48
         racc[I] = a + __shfl_xor(a, 32);
     }
-    // combine the 4 waves' tiles and rhs in wave order: [dp][dp + 1] | rhs[dp]
     __syncthreads();
+    if constexpr (NT <= 3) {
+        // r06: every wave stores its tiles and rhs into its own LDS partial at once, one barrier, then all
+        // 256 threads form each output element as ((p0 + p1) + p2) + p3 -- the association of the
+        // wave-by-wave combine below, so the same bits -- with no chain of four store / barrier rounds
+        // (the combine was ≈ 12 k cycles of a workgroup's ≈ 83 k, profiles/r06o_ba_stamps.txt).
+        // gs_comb(NT) doubles: 4 x [NTT][256] | 4 x [16 NT]; NT = 4 would not fit two workgroups per CU.
+        double* Pt = gl;                               // [4][NTT][256]
+        double* Pr = gl + 4 * NTT * 256;               // [4][16 NT]
+#pragma unroll
+        for (int I = 0, t = 0; I < NT; ++I)
+#pragma unroll
+            for (int Jt = I; Jt < NT; ++Jt, ++t) {
+                if (Jt >= nt) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Pt[(w * NTT + t) * 256 + (kk + 4 * r) * 16 + m16] = acc[t][r];
+            }
+        if (l < 16)
+#pragma unroll
+            for (int I = 0; I < NT; ++I)
+                if (I < nt) Pr[w * 16 * NT + 16 * I + l] = racc[I];
+        __syncthreads();
+        BA_STAMP(1);
+        double* Sg = sg + G.sg_off;
+        for (int e = tid; e < dim * dim; e += 256) {
+            const int r0 = e / dim, c0 = e % dim, r = r0 <= c0 ? r0 : c0, c = r0 <= c0 ? c0 : r0;
+            const int I = r >> 4, Jt = c >> 4, t = I * NT - I * (I - 1) / 2 + (Jt - I);
+            const int at = t * 256 + (r & 15) * 16 + (c & 15);
+            Sg[e] = -(((Pt[at] + Pt[NTT * 256 + at]) + Pt[2 * NTT * 256 + at]) + Pt[3 * NTT * 256 + at]);
+        }
+        if (tid < dim)
+            rg[G.rg_off + tid] = -(((Pr[tid] + Pr[16 * NT + tid]) + Pr[32 * NT + tid]) + Pr[48 * NT + tid]);
+        BA_STAMP(2);
+        BA_FLUSH(0);
+        return;
+    }
+    // NT = 4: combine the 4 waves' tiles and rhs in wave order: [dp][dp + 1] | rhs[dp]
     double* Sb = gl;
     double* Rb = gl + dp * (dp + 1);
     for (int ww = 0; ww < 4; ++ww) {
@@ -1057,6 +1095,14 @@ __device__ __forceinline__ void point_store(int p, int P, int C, double (&pr)[np
 #pragma unroll
     for (int i = 0; i < NPR / 2; ++i) d2[i] = make_double2(pr[2 * i], pr[2 * i + 1]);
 }
+// A workgroup barrier for LDS only: s_waitcnt lgkmcnt(0) + s_barrier.  __syncthreads' workgroup
+// release also waits vmcnt(0), i.e. for every outstanding global load AND store of the wave (gfx9
+// counts both); a barrier whose other side reads only LDS does not need that.  Global data the waves
+// exchange inside a launch still needs __syncthreads.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // MULTI: several cameras, each pose's block and principal point from (pim, pcc) (project_blk).
 template <int K, bool MULTI = false>
 __global__ __launch_bounds__(256, 2)
@@ -1132,7 +1178,9 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
             orow = Gp.big ? 2 * a : obs_row[o];
             olcv = obs_lc[o];
         }
-        __syncthreads();
+        // r06: LDS-only barriers in the chunk loop of a normal group (the W_o / point record stores and
+        // the next loads stay in flight); a big group exchanges its gpart sums through global memory
+        if (Gp.big) __syncthreads(); else lds_barrier();
         BA_STAMP(0);
         if (o < ch.o1) {
             const int p = obs_point[o], cm = obs_cam[o];
@@ -1203,7 +1251,7 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
             }
         }
         BA_STAMP(1);
-        __syncthreads();
+        if (Gp.big) __syncthreads(); else lds_barrier();
         BA_STAMP(2);
         const int no = ch.o1 - ch.o0;
         // per point: E | g | V of its observations (whole points in a normal chunk)
@@ -1255,7 +1303,7 @@ void ba_glin(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, const i
                 gpart[(size_t)Gp.cam_off * NCP + x] += sum;
             }
         }
-        __syncthreads();
+        if (Gp.big) __syncthreads(); else lds_barrier();
         BA_STAMP(3);
     }
     if (!Gp.big) {
@@ -1631,7 +1679,7 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
                               scale + 3 * (size_t)P + 6 * (size_t)cam);
             else obs_y(Wr, o, sol_f + 6 * (size_t)cam, yv + tid * 3);
         }
-        __syncthreads();
+        if (G.big) __syncthreads(); else lds_barrier();   // (r06: the point stores of the last chunk stay in flight)
         if (G.big) {
             if (tid == 0)
                 for (int b = 0; b < ch.o1 - ch.o0; ++b)
@@ -1645,7 +1693,7 @@ void ba_gupdate(const Grp* __restrict__ grp, const Chunk* __restrict__ chk, cons
             double cv[3];
             point_step<K, SCALEJ>(G.p0 + tid, y, PRr, plt, soli, x, scale, cand, model, sn, cv, scale + 3 * (size_t)P + 6 * (size_t)C);
         }
-        __syncthreads();   // yv is rewritten by the next chunk
+        if (G.big) __syncthreads(); else lds_barrier();   // yv is rewritten by the next chunk
     }
     if (G.big && tid == 0) {
         double cv[3];

@@ -2169,9 +2169,9 @@ int load_problem(sfmx_ba_ctx* c, const sfmx_ba_problem* caller, double validate_
         const size_t wreg = K == 1 ? gs_wreg(1, tp.dp_max) : K == 3 ? gs_wreg(3, tp.dp_max) : gs_wreg(7, tp.dp_max);
         size_t nb_max = 0;   // batch descriptors of one group in LDS (2 doubles each)
         for (const Grp& G : tp.grp) nb_max = std::max<size_t>(nb_max, G.nb);
-        c->lds_schur = sizeof(double) *
-                       std::max<size_t>({4 * wreg + 2 * nb_max, (size_t)tp.dp_max * (tp.dp_max + 1) + tp.dp_max, 16});
         c->gs_nt = std::min(4, std::max(1, tp.dp_max / 16));
+        c->lds_schur = sizeof(double) * std::max<size_t>({4 * wreg + 2 * nb_max, (size_t)tp.dp_max * (tp.dp_max + 1) + tp.dp_max,
+                                                          (size_t)gs_comb(c->gs_nt), 16});
     }
     c->lds_lin = glin_lds(K);
     {
