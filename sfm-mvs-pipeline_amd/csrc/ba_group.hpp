@@ -83,6 +83,14 @@ struct AEnt { long long b0, b1; int dim, big, rg, pad; };
 
 __device__ __forceinline__ int gdim(const Grp& G, int K) { return 6 * G.u + K; }
 
+// A workgroup barrier for LDS only: s_waitcnt lgkmcnt(0) + s_barrier.  __syncthreads' workgroup
+// release also waits vmcnt(0), i.e. for every outstanding global load AND store of the wave (gfx9
+// counts both); a barrier whose other side reads only LDS does not need that.  Global data the waves
+// exchange inside a launch still needs __syncthreads.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Diagnostic build only (make stamps -> lib/libsfmx_stamps.so, tools/ba_stamps.py): per-phase
 // s_memtime cycle totals of thread 0 of every workgroup.  Compiled out of the product library.
 #ifdef SFMX_BA_STAMPS
@@ -553,8 +561,8 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
         const double a = racc[I] + __shfl_xor(racc[I], 16);   // lanes m, m+16 | m+32, m+48
         racc[I] = a + __shfl_xor(a, 32);
     }
-    __syncthreads();
     if constexpr (NT <= 3) {
+        lds_barrier();   // (the last batch's plt stores stay in flight: nothing here reads them)
         // r06: every wave stores its tiles and rhs into its own LDS partial at once, one barrier, then all
         // 256 threads form each output element as ((p0 + p1) + p2) + p3 -- the association of the
         // wave-by-wave combine below, so the same bits -- with no chain of four store / barrier rounds
@@ -574,7 +582,7 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
 #pragma unroll
             for (int I = 0; I < NT; ++I)
                 if (I < nt) Pr[w * 16 * NT + 16 * I + l] = racc[I];
-        __syncthreads();
+        lds_barrier();
         BA_STAMP(1);
         double* Sg = sg + G.sg_off;
         for (int e = tid; e < dim * dim; e += 256) {
@@ -590,6 +598,7 @@ void ba_gschur(const Grp* __restrict__ grp, const Batch* __restrict__ bat, const
         return;
     }
     // NT = 4: combine the 4 waves' tiles and rhs in wave order: [dp][dp + 1] | rhs[dp]
+    __syncthreads();
     double* Sb = gl;
     double* Rb = gl + dp * (dp + 1);
     for (int ww = 0; ww < 4; ++ww) {
@@ -1095,14 +1104,6 @@ __device__ __forceinline__ void point_store(int p, int P, int C, double (&pr)[np
 #pragma unroll
     for (int i = 0; i < NPR / 2; ++i) d2[i] = make_double2(pr[2 * i], pr[2 * i + 1]);
 }
-// A workgroup barrier for LDS only: s_waitcnt lgkmcnt(0) + s_barrier.  __syncthreads' workgroup
-// release also waits vmcnt(0), i.e. for every outstanding global load AND store of the wave (gfx9
-// counts both); a barrier whose other side reads only LDS does not need that.  Global data the waves
-// exchange inside a launch still needs __syncthreads.
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
 // MULTI: several cameras, each pose's block and principal point from (pim, pcc) (project_blk).
 template <int K, bool MULTI = false>
 __global__ __launch_bounds__(256, 2)
